@@ -1,0 +1,117 @@
+"""ctypes binding of libafgpu.so (include/afgpu.h).
+
+The library is built in-tree (``csrc/Makefile`` -> ``anchored-fusion_amd/libafgpu.so``) and
+loaded from there, so the GPU box sees exactly the code object that ``build()`` produced.
+There is no CPU fallback: if the library is missing or no GPU is present, calls raise.
+
+torch is imported first when available so that a process using both torch and this library
+shares one HIP runtime (both link ``libamdhip64.so.7``).
+"""
+import ctypes
+import os
+import subprocess
+
+try:  # one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the host-buffer API
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libafgpu.so")
+CSRC = os.path.join(HERE, "csrc")
+
+AF_OK = 0
+AF_MAX_CIGAR = 32
+AF_MAX_READ = 320
+AF_K = 16
+AF_FLAG_MEM_OVERFLOW = 0x10000
+AF_FLAG_CIGAR_OVERFLOW = 0x20000
+
+# every symbol include/afgpu.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
+    "af_index_free", "af_index_anchor_len", "af_index_filter_buckets", "af_index_filter_table",
+    "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
+    "af_last_candidates",
+)
+
+
+class AFError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop",
+        "min_seed_len", "max_occ", "T", "max_ext", "max_mems")]
+
+
+class AlnOut(ctypes.Structure):
+    _fields_ = [("flag", ctypes.c_void_p), ("pos", ctypes.c_void_p), ("score", ctypes.c_void_p),
+                ("n_cigar", ctypes.c_void_p), ("hits", ctypes.c_void_p), ("cigar", ctypes.c_void_p)]
+
+
+def build(force=False):
+    """Compiles libafgpu.so for gfx950 (hipcc cross-compiles without a GPU)."""
+    if force and os.path.exists(LIB_PATH):
+        os.remove(LIB_PATH)
+    subprocess.run(["make", "-s", "-C", CSRC], check=True)
+
+
+_L = None
+
+_vp, _i32, _i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+
+
+def lib():
+    """Loads libafgpu.so (raises if it has not been built -- no silent fallback)."""
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(LIB_PATH):
+        raise AFError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C {CSRC})")
+    L = ctypes.CDLL(LIB_PATH)
+    L.af_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(_vp)]
+    L.af_ctx_create.restype = ctypes.c_int
+    L.af_ctx_destroy.argtypes = [_vp]
+    L.af_ctx_destroy.restype = None
+    L.af_last_error.argtypes = [_vp]
+    L.af_last_error.restype = ctypes.c_char_p
+    L.af_params_default.argtypes = [ctypes.POINTER(Params)]
+    L.af_params_default.restype = None
+    L.af_index_build.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
+    L.af_index_build.restype = ctypes.c_int
+    L.af_index_free.argtypes = [_vp]
+    L.af_index_free.restype = None
+    L.af_index_anchor_len.argtypes = [_vp]
+    L.af_index_anchor_len.restype = _i64
+    L.af_index_filter_buckets.argtypes = [_vp]
+    L.af_index_filter_buckets.restype = _i32
+    L.af_index_filter_table.argtypes = [_vp, _vp, _i64]
+    L.af_index_filter_table.restype = ctypes.c_int
+    L.af_align_pairs.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), ctypes.POINTER(AlnOut)]
+    L.af_align_pairs.restype = ctypes.c_int
+    L.af_align_pairs_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params),
+                                        ctypes.POINTER(AlnOut), _vp]
+    L.af_align_pairs_device.restype = ctypes.c_int
+    L.af_align_candidates_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params),
+                                             ctypes.POINTER(AlnOut), _vp]
+    L.af_align_candidates_device.restype = ctypes.c_int
+    L.af_seed_filter_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]
+    L.af_seed_filter_device.restype = ctypes.c_int
+    L.af_last_candidates.argtypes = [_vp]
+    L.af_last_candidates.restype = _i64
+    _L = L
+    return L
+
+
+def default_params():
+    p = Params()
+    lib().af_params_default(ctypes.byref(p))
+    return p
+
+
+def check(ctx, rc, what):
+    if rc != AF_OK:
+        msg = lib().af_last_error(ctx) if ctx else b""
+        raise AFError(f"{what} failed (rc={rc}): {(msg or b'').decode(errors='replace')}")

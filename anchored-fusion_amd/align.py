@@ -1,0 +1,167 @@
+"""Anchor alignment of read pairs on the GPU: the drop-in for ``bwa index`` + ``bwa mem -M``
+against the anchored transcript (Anchored_Fusion.py:167-172, 181-182).
+
+``AnchorAligner(anchor).align_pairs(reads, lens)`` returns per-read primary records (the SAM
+fields Anchored-Fusion consumes: FLAG, POS, CIGAR) computed by the HIP kernels in csrc/.
+``partition`` then applies the samtools flag filters and coordinate sort of
+Anchored_Fusion.py:183-194 (S3) to those records.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+CIGAR_OPS = "MIDNSHP=X"
+
+
+class AlignResult:
+    """Per-read arrays (pair-major rows: 2p = mate 1, 2p+1 = mate 2)."""
+
+    def __init__(self, flag, pos, score, n_cigar, cigar, hits):
+        self.flag, self.pos, self.score = flag, pos, score
+        self.n_cigar, self.cigar, self.hits = n_cigar, cigar, hits
+
+    def __len__(self):
+        return len(self.flag)
+
+    def as_dict(self):
+        return dict(flag=self.flag, pos=self.pos, score=self.score, n_cigar=self.n_cigar,
+                    cigar=self.cigar, hits=self.hits)
+
+    def cigar_ops(self, r):
+        return [(int(c >> 4), CIGAR_OPS[c & 0xF]) for c in self.cigar[r][: self.n_cigar[r]]]
+
+    def cigar_str(self, r):
+        if self.flag[r] & 0x4:
+            return "*"
+        return "".join(f"{n}{op}" for n, op in self.cigar_ops(r))
+
+    def mapped(self):
+        return (self.flag & 0x4) == 0
+
+
+class AnchorAligner:
+    """One GPU context + one anchor index.  Not thread-safe (one host thread per GPU)."""
+
+    def __init__(self, anchor: bytes, device: int = 0, params=None):
+        L = _lib.lib()
+        self._ctx = ctypes.c_void_p()
+        rc = L.af_ctx_create(int(device), ctypes.byref(self._ctx))
+        if rc != _lib.AF_OK:
+            raise _lib.AFError(f"af_ctx_create(device={device}) failed (rc={rc}): no usable GPU?")
+        self._idx = ctypes.c_void_p()
+        self.anchor = bytes(anchor)
+        _lib.check(self._ctx, L.af_index_build(self._ctx, self.anchor, len(self.anchor), ctypes.byref(self._idx)),
+                   "af_index_build")
+        self.params = params or _lib.default_params()
+        self.device = device
+
+    def close(self):
+        L = _lib._L
+        if L is None:
+            return
+        if getattr(self, "_idx", None):
+            L.af_index_free(self._idx)
+            self._idx = None
+        if getattr(self, "_ctx", None):
+            L.af_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def filter_table(self):
+        L = _lib.lib()
+        nb = L.af_index_filter_buckets(self._idx)
+        out = np.zeros(nb * 8, dtype=np.uint16)
+        _lib.check(self._ctx, L.af_index_filter_table(self._idx, out.ctypes.data, out.size), "af_index_filter_table")
+        return out
+
+    def align_pairs(self, reads, lens=None) -> AlignResult:
+        """reads: uint8 [2N, stride] pair-major ASCII; lens: optional int32 [2N]."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        nr, stride = reads.shape
+        if nr % 2:
+            raise ValueError("reads must hold an even number of rows (pair-major mates)")
+        out = {k: np.zeros(nr, dtype=np.int32) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+        out["cigar"] = np.zeros((nr, _lib.AF_MAX_CIGAR), dtype=np.uint32)
+        o = _lib.AlnOut(*(out[k].ctypes.data for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        _lib.check(self._ctx, _lib.lib().af_align_pairs(self._ctx, self._idx, reads.ctypes.data, nr // 2, stride,
+                                                        None if lp is None else lp.ctypes.data,
+                                                        ctypes.byref(self.params), ctypes.byref(o)),
+                   "af_align_pairs")
+        return AlignResult(**out)
+
+    # ---- device-resident entry points (torch tensors as HBM buffers) ----------------------
+    def align_pairs_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None):
+        """Enqueues S2 on ``stream`` (torch.cuda.Stream or raw handle); all tensors on-device.
+        out_t: dict flag/pos/score/n_cigar/hits (int32 [2N]) and cigar (int32/uint32 [2N, 32])."""
+        o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        sh = _stream_handle(stream)
+        _lib.check(self._ctx, _lib.lib().af_align_pairs_device(
+            self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o), sh),
+            "af_align_pairs_device")
+
+    def align_candidates_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None):
+        """Second half of align_pairs_device; seed_filter_device(hits_t=out_t['hits']) must have
+        run on the same stream for this batch."""
+        o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        _lib.check(self._ctx, _lib.lib().af_align_candidates_device(
+            self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o),
+            _stream_handle(stream)), "af_align_candidates_device")
+
+    def seed_filter_device(self, reads_t, n_reads, stride, hits_t, lens_t=None, stream=None):
+        sh = _stream_handle(stream)
+        _lib.check(self._ctx, _lib.lib().af_seed_filter_device(
+            self._ctx, self._idx, reads_t.data_ptr(), int(n_reads), int(stride),
+            None if lens_t is None else lens_t.data_ptr(), hits_t.data_ptr(), sh), "af_seed_filter_device")
+
+    def last_candidates(self):
+        return int(_lib.lib().af_last_candidates(self._ctx))
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def partition(res: AlignResult):
+    """S3 of Anchored_Fusion.py:183-194 on the records of ``res``.
+
+    ``realign.bam`` is coordinate-sorted (``samtools sort``, AF:182): key (ref, pos, strand),
+    unmapped-with-unmapped-mate last, ties in input order (pair, mate).  Returns read indices:
+      tmp1      ``samtools view -f 8 -F 260``  mapped primary reads whose mate is unmapped (AF:186)
+      tmp2      ``samtools view -f 4 -F 264``  unmapped reads whose mate is mapped (AF:187)
+      anchored  ``samtools view -F 772``       mapped primary reads (AF:194)
+    each in realign.bam order.
+    """
+    flag = res.flag
+    n = len(flag)
+    pos = res.pos.astype(np.int64)
+    rev = ((flag & 0x10) != 0).astype(np.int64)
+    placed = pos >= 0
+    # samtools coordinate order: placed records by (pos, is_rev), then unplaced; stable
+    key = np.where(placed, pos * 2 + rev, np.int64(1) << 62)
+    order = np.argsort(key, kind="stable")
+    f = flag[order]
+    tmp1 = order[((f & 0x8) != 0) & ((f & 260) == 0)]
+    tmp2 = order[((f & 0x4) != 0) & ((f & 264) == 0)]
+    anchored = order[(f & 772) == 0]
+    del n
+    return tmp1, tmp2, anchored

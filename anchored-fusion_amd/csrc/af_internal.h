@@ -1,0 +1,51 @@
+// af_internal.h -- shared definitions for the libafgpu HIP kernels and host code.
+// gfx950 (CDNA4) only; wave64 is assumed everywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/afgpu.h"
+
+#define AF_NEG_INF (-0x40000000)
+#define AF_SEED_TILE 256        // reads per wave tile in the seed filter
+#define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
+#define AF_ALN_WAVES 4          // waves per alignment workgroup
+#define AF_CPL 6                // DP columns per lane: 6*64 = 384 >= AF_MAX_READ+1
+#define AF_ZCAP 12288           // LDS traceback bytes per wave; larger DPs use global scratch
+#define AF_TMAX (AF_MAX_READ + 2 * 100 * 4 + 64)  // max target window held in LDS
+
+// Device view of an anchor index (all pointers are device memory).
+struct DevIndex {
+    const uint8_t *D;       // doubled reference codes (anchor ++ revcomp), N = 4, length 2n
+    const uint32_t *D2;     // 2-bit packed D, 16 bases per word (base i at bits 2i), padded
+    const uint32_t *Dn;     // N bitmap of D, 32 bases per word, padded
+    const uint32_t *hkey;   // 16-mer position hash: key
+    const int32_t *hstart;  //   first index into kpos
+    const int32_t *hcnt;    //   occurrences (0 = empty slot)
+    const int32_t *kpos;    // positions grouped by 16-mer, ascending
+    const uint4 *ftab;      // filter buckets: 8 x u16 (slots 0..6 fingerprints, slot 7 overflow)
+    int64_t n;              // anchor length
+    int32_t hbits;          // log2 position-hash slots
+    int32_t nb_bits;        // log2 filter buckets
+};
+
+__host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
+__host__ __device__ static inline uint32_t af_ffp(uint32_t h) { return ((h >> 4) & 0x7FFFu) | 0x8000u; }
+
+// Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
+struct ReadRec {
+    int32_t flag;    // 0x4 unmapped, 0x10 reverse, AF_FLAG_* overflow bits
+    int32_t pos;
+    int32_t score;
+    int32_t n_cigar;
+};
+
+// launch helpers (defined in the .hip files)
+hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
+                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *n_cand,
+                                 hipStream_t s);
+hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
+                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
+                           int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch,
+                           int32_t n_slots, hipStream_t s);
+hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
+                           hipStream_t s);

@@ -1,0 +1,723 @@
+// align.hip -- K2 (candidate alignment) and K3 (pair flags) of the anchor alignment path
+// (`bwa mem -M` at Anchored_Fusion.py:182; a3 record fields).
+//
+// K2 is a persistent kernel: one 64-thread workgroup (= one wave, one LDS slot) per
+// resident slot pulls candidate reads from a device-side work counter.  Per read the wave
+//   1. finds every MEM >= min_seed_len against the doubled anchor (16-mer position hash in
+//      L2, right extension by 2-bit word compares),
+//   2. sorts MEMs (len desc, qb, rb) with a wave rank sort in LDS,
+//   3. extends seeds in order (skipping seeds contained in an earlier region) with a
+//      row-parallel banded DP: lanes own contiguous query columns, the horizontal gap chain
+//      is a wave prefix-max scan, row max / band trimming are wave reductions and ballots,
+//   4. runs band inference + the global DP with traceback bits in LDS (global scratch for
+//      oversize matrices) to produce the CIGAR of the best region.
+// The recurrences, tie-breaks and band bookkeeping are exactly those of oracle/af_oracle.c.
+#include "af_internal.h"
+
+namespace {
+
+struct __attribute__((aligned(16))) AlnLds {
+    uint64_t mem[256];
+    uint64_t smem[256];
+    int32_t regs[16][8];   // score, truesc, qb, qe, rb, re, seedlen0, w
+    uint32_t ring[64];     // traceback CIGAR ring
+    int32_t misc[8];       // [0] nmem (total found), [1] work item, [2] n traceback ops
+    uint8_t q[AF_MAX_READ + 16];
+    uint8_t qs[AF_MAX_READ + 16];
+    uint8_t t[1024];
+    uint8_t z[AF_ZCAP];
+};
+
+__device__ __forceinline__ int scd(const af_params &p, int x, int y) {
+    return (x > 3 || y > 3) ? -1 : (x == y ? p.a : -p.b);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+// inclusive prefix max over lanes
+__device__ __forceinline__ int wave_scan_max(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(v, d);
+        if (lane >= d) v = max(v, o);
+    }
+    return v;
+}
+
+__device__ __forceinline__ int cal_max_gap(const af_params &p, int qlen) {
+    int l_del = (int)((double)(qlen * p.a - p.o_del) / p.e_del + 1.);
+    int l_ins = (int)((double)(qlen * p.a - p.o_ins) / p.e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < p.w << 1 ? l : p.w << 1;
+}
+
+__device__ __forceinline__ int infer_bw(int l1, int l2, int score, int a, int q, int r) {
+    if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
+    int w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
+    int d = l1 - l2 < 0 ? l2 - l1 : l1 - l2;
+    return w < d ? d : w;
+}
+
+struct ExtRes { int max, qle, tle, gtle, gscore, max_off; };
+
+// ksw_extend2 semantics (see oracle ext_dp), row-parallel over query columns.
+__device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
+                              int end_bonus, int zdrop, int h0, int lane) {
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int cpl = (qlen + 1 + 63) >> 6;
+    const int j0 = lane * cpl;
+    int eh_h[AF_CPL], eh_e[AF_CPL], qc[AF_CPL];
+    {
+        const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            int v = 0;
+            if (c < cpl && j <= qlen) {
+                if (j == 0) v = h0;
+                else {
+                    const int vj = v1 - (j - 1) * p.e_ins;
+                    v = j == 1 ? v1 : (vj > 0 ? vj : 0);
+                }
+            }
+            eh_h[c] = v;
+            eh_e[c] = 0;
+            qc[c] = (c < cpl && j < qlen) ? q[j] : 4;
+        }
+    }
+    {
+        const int mx = p.a;
+        int max_ins = (int)((double)(qlen * mx + end_bonus - p.o_ins) / p.e_ins + 1.);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = (int)((double)(qlen * mx + end_bonus - p.o_del) / p.e_del + 1.);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    int beg = 0, end = qlen;
+    const int NEGB = -(1 << 28);
+    for (int i = 0; i < tlen; ++i) {
+        if (beg < i - w) beg = i - w;
+        if (end > i + w + 1) end = i + w + 1;
+        if (end > qlen) end = qlen;
+        int h1s = 0;
+        if (beg == 0) {
+            h1s = h0 - (p.o_del + p.e_del * (i + 1));
+            if (h1s < 0) h1s = 0;
+        }
+        if (beg >= end) {  // empty row: bwa's loop body never runs, m == 0
+            if (beg == qlen) {
+                max_ie = gscore > h1s ? max_ie : i;
+                gscore = gscore > h1s ? gscore : h1s;
+            }
+            break;
+        }
+        const int ti = t[i];
+        int Mv[AF_CPL], bx[AF_CPL], hv[AF_CPL];
+        int run = NEGB;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j >= beg && j < end;
+            int M = 0;
+            if (in) {
+                const int d = eh_h[c];
+                M = d ? d + scd(p, ti, qc[c]) : 0;
+            }
+            Mv[c] = M;
+            bx[c] = run;  // exclusive within lane
+            const int tk = M - oe_ins > 0 ? M - oe_ins : 0;
+            if (in) run = max(run, tk + j * p.e_ins);
+        }
+        const int inc = wave_scan_max(run, lane);
+        int lex = __shfl_up(inc, 1);
+        if (lane == 0) lex = NEGB;
+        int key = -1;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j >= beg && j < end;
+            const int P = max(lex, bx[c]);
+            const int f = j > beg ? P - (j - 1) * p.e_ins : 0;
+            const int e = eh_e[c], M = Mv[c];
+            int h = M > e ? M : e;
+            h = h > f ? h : f;
+            hv[c] = h;
+            if (in) {
+                int tt = M - oe_del;
+                tt = tt > 0 ? tt : 0;
+                int en = e - p.e_del;
+                eh_e[c] = en > tt ? en : tt;
+                key = max(key, (h << 10) | j);
+            }
+        }
+        key = wave_max(key);
+        const int m = key < 0 ? 0 : key >> 10;
+        const int mj = key < 0 ? -1 : (key & 1023);
+        // H(i, j-1) shift into eh_h; eh_h[beg] = h1s; eh_e[end] = 0
+        int lastv = hv[0];
+#pragma unroll
+        for (int c = 1; c < AF_CPL; ++c)
+            if (c == cpl - 1) lastv = hv[c];
+        const int from_left = __shfl_up(lastv, 1);
+        // value of H(i, qlen-1) for gscore
+        int hq = 0;
+        {
+            const int jq = qlen - 1;
+            const int ln = jq / cpl, cc = jq - ln * cpl;
+            int sel = hv[0];
+#pragma unroll
+            for (int c = 1; c < AF_CPL; ++c)
+                if (c == cc) sel = hv[c];
+            hq = __shfl(sel, ln);
+        }
+#pragma unroll
+        for (int c = AF_CPL - 1; c >= 0; --c) {
+            const int j = j0 + c;
+            if (c < cpl) {
+                const int prevH = c == 0 ? from_left : hv[c > 0 ? c - 1 : 0];
+                if (j == beg) eh_h[c] = h1s;
+                else if (j > beg && j <= end) eh_h[c] = prevH;
+                if (j == end) eh_e[c] = 0;
+            }
+        }
+        if (end == qlen) {
+            max_ie = gscore > hq ? max_ie : i;
+            gscore = gscore > hq ? gscore : hq;
+        }
+        if (m == 0) break;
+        if (m > mx) {
+            mx = m; max_i = i; max_j = mj;
+            const int off = mj - i < 0 ? i - mj : mj - i;
+            max_off = max_off > off ? max_off : off;
+        } else if (zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (mx - m - ((i - max_i) - (mj - max_j)) * p.e_del > zdrop) break;
+            } else {
+                if (mx - m - ((mj - max_j) - (i - max_i)) * p.e_ins > zdrop) break;
+            }
+        }
+        // band trimming on the updated eh over [beg, end]
+        int fnz = 1 << 30, lnz = -1;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            if (c < cpl && (eh_h[c] != 0 || eh_e[c] != 0)) {
+                if (j >= beg && j < end) fnz = min(fnz, j);
+                if (j >= beg && j <= end) lnz = max(lnz, j);
+            }
+        }
+        const uint64_t bf = __ballot(fnz < (1 << 30));
+        const uint64_t bl = __ballot(lnz >= 0);
+        const int FNZ = bf ? __shfl(fnz, __ffsll((long long)bf) - 1) : (1 << 30);
+        const int LNZ = bl ? __shfl(lnz, 63 - __clzll((long long)bl)) : -1;
+        const int beg_new = FNZ == (1 << 30) ? end : FNZ;
+        const int jstar = LNZ >= beg_new ? LNZ : beg_new - 1;
+        beg = beg_new;
+        end = jstar + 2 < qlen ? jstar + 2 : qlen;
+    }
+    ExtRes r;
+    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off;
+    return r;
+}
+
+// ksw_global2 semantics with traceback (see oracle global_dp).  z: n_col*tlen bytes.
+// Returns the score; the CIGAR (forward order) is left in lds.ring / lds.misc[2] (count).
+__device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
+                              uint8_t *z, AlnLds &L, int lane) {
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    const int cpl = (qlen + 1 + 63) >> 6;
+    const int j0 = lane * cpl;
+    int eh_h[AF_CPL], eh_e[AF_CPL], qc[AF_CPL];
+#pragma unroll
+    for (int c = 0; c < AF_CPL; ++c) {
+        const int j = j0 + c;
+        eh_h[c] = AF_NEG_INF;
+        eh_e[c] = AF_NEG_INF;
+        if (c < cpl && j <= qlen) {
+            if (j == 0) eh_h[c] = 0;
+            else if (j <= w) eh_h[c] = -(p.o_ins + p.e_ins * j);
+        }
+        qc[c] = (c < cpl && j < qlen) ? q[j] : 4;
+    }
+    for (int i = 0; i < tlen; ++i) {
+        const int beg = i > w ? i - w : 0;
+        const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        const int h1s = beg == 0 ? -(p.o_del + p.e_del * (i + 1)) : AF_NEG_INF;
+        const int ti = t[i];
+        int Mv[AF_CPL], bx[AF_CPL], hv[AF_CPL];
+        int run = AF_NEG_INF + (beg - 1) * p.e_ins;  // the f = -inf chain entering at beg
+        int lane_seed = run;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j >= beg && j < end;
+            const int m = eh_h[c] + scd(p, ti, qc[c]);
+            Mv[c] = m;
+            bx[c] = run;
+            if (in) run = max(run, m - oe_ins + j * p.e_ins);
+        }
+        const int inc = wave_scan_max(run, lane);
+        int lex = __shfl_up(inc, 1);
+        if (lane == 0) lex = lane_seed;
+        uint8_t *zi = z + (size_t)i * n_col;
+#pragma unroll
+        for (int c = 0; c < AF_CPL; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j >= beg && j < end;
+            const int P = max(lex, bx[c]);
+            const int f = P - (j - 1) * p.e_ins;
+            const int m = Mv[c];
+            int e = eh_e[c];
+            int d = m >= e ? 0 : 1;
+            int h = m >= e ? m : e;
+            d = h >= f ? d : 2;
+            h = h >= f ? h : f;
+            hv[c] = h;
+            if (in) {
+                const int tt = m - oe_del;
+                const int ee = e - p.e_del;
+                d |= ee > tt ? 1 << 2 : 0;
+                eh_e[c] = ee > tt ? ee : tt;
+                const int tf = m - oe_ins;
+                const int ff = f - p.e_ins;
+                d |= ff > tf ? 2 << 4 : 0;
+                zi[j - beg] = (uint8_t)d;
+            }
+        }
+        int lastv = hv[0];
+#pragma unroll
+        for (int c = 1; c < AF_CPL; ++c)
+            if (c == cpl - 1) lastv = hv[c];
+        const int from_left = __shfl_up(lastv, 1);
+#pragma unroll
+        for (int c = AF_CPL - 1; c >= 0; --c) {
+            const int j = j0 + c;
+            if (c < cpl) {
+                const int prevH = c == 0 ? from_left : hv[c > 0 ? c - 1 : 0];
+                if (j == beg) eh_h[c] = h1s;
+                else if (j > beg && j <= end) eh_h[c] = prevH;
+                if (j == end) eh_e[c] = AF_NEG_INF;
+            }
+        }
+    }
+    // score = eh[qlen].h
+    int score;
+    {
+        const int ln = qlen / cpl, cc = qlen - ln * cpl;
+        int sel = eh_h[0];
+#pragma unroll
+        for (int c = 1; c < AF_CPL; ++c)
+            if (c == cc) sel = eh_h[c];
+        score = __shfl(sel, ln);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        int nc = 0, which = 0;
+        int i = tlen - 1;
+        int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+        auto push = [&](int op, int len) {
+            if (nc > 0 && (int)(L.ring[(nc - 1) & 63] & 0xf) == op) L.ring[(nc - 1) & 63] += (uint32_t)len << 4;
+            else { L.ring[nc & 63] = (uint32_t)len << 4 | (uint32_t)op; ++nc; }
+        };
+        while (i >= 0 && k >= 0) {
+            which = z[(size_t)i * n_col + (k - (i > w ? i - w : 0))] >> (which << 1) & 3;
+            if (which == 0) { push(0, 1); --i; --k; }
+            else if (which == 1) { push(2, 1); --i; }
+            else { push(1, 1); --k; }
+        }
+        if (i >= 0) push(2, i + 1);
+        if (k >= 0) push(1, k + 1);
+        L.misc[2] = nc;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return score;
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 16 bases of the packed doubled reference starting at pos, plus its N mask (bit per base)
+__device__ __forceinline__ void getD16(const DevIndex &ix, int64_t pos, uint32_t &bits, uint32_t &nmask) {
+    const int64_t wi = pos >> 4;
+    const int sh = (int)(pos & 15) * 2;
+    const uint32_t lo = ix.D2[wi], hi = ix.D2[wi + 1];
+    bits = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+    const int64_t ni = pos >> 5;
+    const int nsh = (int)(pos & 31);
+    const uint32_t nlo = ix.Dn[ni], nhi = ix.Dn[ni + 1];
+    nmask = (nsh ? (nlo >> nsh) | (nhi << (32 - nsh)) : nlo) & 0xFFFFu;
+}
+
+// gen_cigar restated (bwa_gen_cigar2): returns score, cigar in L.ring/L.misc[2]
+__device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, int lq, int qb, int64_t rb, int64_t re,
+                              AlnLds &L, uint8_t *zg, int lane) {
+    const int rlen = (int)(re - rb);
+    const bool rev = rb >= ix.n;
+    // stage (possibly reversed) query segment into qs and reference segment into t
+    for (int x = lane; x < lq; x += 64) L.qs[x] = rev ? L.q[qb + lq - 1 - x] : L.q[qb + x];
+    for (int x = lane; x < rlen; x += 64) L.t[x] = rev ? ix.D[re - 1 - x] : ix.D[rb + x];
+    wave_sync();
+    int score;
+    if (lq == rlen && w_ == 0) {
+        int s = 0;
+        for (int x = lane; x < lq; x += 64) s += scd(p, L.t[x], L.qs[x]);
+        score = wave_sum(s);
+        if (lane == 0) { L.ring[0] = (uint32_t)lq << 4; L.misc[2] = 1; }
+        wave_sync();
+    } else {
+        int max_ins = (int)((double)(((lq + 1) >> 1) * p.a - p.o_ins) / p.e_ins + 1.);
+        int max_del = (int)((double)(((lq + 1) >> 1) * p.a - p.o_del) / p.e_del + 1.);
+        int max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        const int d = rlen - lq < 0 ? lq - rlen : rlen - lq;
+        int w = (max_gap + d + 1) >> 1;
+        w = w < w_ ? w : w_;
+        const int min_w = d + 3;
+        w = w > min_w ? w : min_w;
+        const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
+        uint8_t *z = ((size_t)n_col * rlen <= AF_ZCAP) ? L.z : zg;
+        score = global_dp_wave(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+    }
+    return score;
+}
+
+__global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
+                                              const int32_t *__restrict__ lens, af_params p,
+                                              const int32_t *__restrict__ cand, const int32_t *__restrict__ n_cand,
+                                              int32_t *__restrict__ work, ReadRec *__restrict__ recs,
+                                              uint32_t *__restrict__ cigar, uint8_t *__restrict__ zscratch,
+                                              size_t zstride) {
+    __shared__ AlnLds L;
+    const int lane = threadIdx.x;
+    const int ncand = *n_cand;
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    const int64_t n = ix.n, n2 = 2 * ix.n;
+    const int max_ext = p.max_ext < 16 ? p.max_ext : 16;
+    const int max_mems = p.max_mems < 256 ? p.max_mems : 256;
+    for (;;) {
+        int item = 0;
+        if (lane == 0) item = atomicAdd(work, 1);
+        item = __shfl(item, 0);
+        if (item >= ncand) break;
+        const int64_t r = cand[item];
+        int l = lens ? lens[r] : stride;
+        if (l > AF_MAX_READ) l = AF_MAX_READ;
+        const uint8_t *rd = reads + r * (int64_t)stride;
+        for (int x = lane; x < l; x += 64) {
+            const uint8_t c = rd[x];
+            uint8_t v = 4;
+            switch (c) {
+            case 'A': case 'a': v = 0; break;
+            case 'C': case 'c': v = 1; break;
+            case 'G': case 'g': v = 2; break;
+            case 'T': case 't': v = 3; break;
+            default: v = 4;
+            }
+            L.q[x] = v;
+        }
+        if (lane == 0) L.misc[0] = 0;
+        wave_sync();
+        // ---- 1. MEMs ------------------------------------------------------------------
+        for (int qb = lane; qb + AF_K <= l; qb += 64) {
+            uint32_t k = 0;
+            bool ok = true;
+            for (int u = 0; u < AF_K; ++u) {
+                const int c = L.q[qb + u];
+                ok &= c < 4;
+                k |= (uint32_t)(c & 3) << (2 * u);
+            }
+            if (!ok) continue;
+            const uint32_t hm = (1u << ix.hbits) - 1u;
+            uint32_t s = af_fmix(k) & hm;
+            int cnt = 0, st = 0;
+            for (;;) {
+                const int cc = ix.hcnt[s];
+                if (cc == 0) break;
+                if (ix.hkey[s] == k) { cnt = cc; st = ix.hstart[s]; break; }
+                s = (s + 1) & hm;
+            }
+            if (cnt == 0 || cnt > p.max_occ) continue;
+            for (int o = 0; o < cnt; ++o) {
+                const int64_t rb = ix.kpos[st + o];
+                if (qb > 0 && rb != 0 && rb != n) {
+                    const int qc = L.q[qb - 1];
+                    if (qc < 4 && qc == ix.D[rb - 1]) continue;
+                }
+                const int64_t lim = rb < n ? n : n2;
+                int len = AF_K;
+                for (;;) {
+                    const int qp = qb + len;
+                    const int64_t rp = rb + len;
+                    const int64_t room64 = min((int64_t)(l - qp), lim - rp);
+                    if (room64 <= 0) break;
+                    const int room = (int)min(room64, (int64_t)16);
+                    uint32_t qk = 0;
+                    int qn = 16;
+                    for (int u = 0; u < 16; ++u) {
+                        const int c = qp + u < l ? L.q[qp + u] : 4;
+                        if (c > 3 && qn == 16) qn = u;
+                        qk |= (uint32_t)(c & 3) << (2 * u);
+                    }
+                    uint32_t dk, dn;
+                    getD16(ix, rp, dk, dn);
+                    const uint32_t x = qk ^ dk;
+                    const int eq = x ? (__builtin_ctz(x) >> 1) : 16;
+                    const int dnf = dn ? __builtin_ctz(dn) : 16;
+                    int step = min(min(eq, room), min(qn, dnf));
+                    len += step;
+                    if (step < 16) break;
+                }
+                if (len < p.min_seed_len) continue;
+                const int slot = atomicAdd(&L.misc[0], 1);
+                if (slot < 256)
+                    L.mem[slot] = ((uint64_t)(1023 - len) << 50) | ((uint64_t)qb << 40) | (uint64_t)rb;
+            }
+        }
+        wave_sync();
+        const int nm_total = L.misc[0];
+        int flag = 0x4;
+        int out_pos = 0, out_score = 0, out_nc = 0;
+        if (nm_total > max_mems) {
+            flag = 0x4 | AF_FLAG_MEM_OVERFLOW;
+        } else {
+            const int nm = nm_total;
+            // ---- 2. rank sort --------------------------------------------------------
+            for (int a = lane; a < nm; a += 64) {
+                const uint64_t ka = L.mem[a];
+                int rank = 0;
+                for (int b = 0; b < nm; ++b) rank += L.mem[b] < ka;
+                L.smem[rank] = ka;
+            }
+            wave_sync();
+            // ---- 3. seed extension ---------------------------------------------------
+            int n_reg = 0;
+            for (int si = 0; si < nm; ++si) {
+                const uint64_t key = L.smem[si];
+                const int slen = 1023 - (int)(key >> 50);
+                const int sqb = (int)((key >> 40) & 1023);
+                const int64_t srb = (int64_t)(key & 0xFFFFFFFFFFull);
+                bool skip = false;
+                for (int rr = 0; rr < n_reg; ++rr) {
+                    const int *a = L.regs[rr];
+                    const int aqb = a[2], aqe = a[3], arb = a[4], are = a[5], asl = a[6], aw = a[7];
+                    if (srb < arb || srb + slen > are || sqb < aqb || sqb + slen > aqe) continue;
+                    if (10 * (slen - asl) > l) continue;
+                    int qd = sqb - aqb, rd = (int)(srb - arb);
+                    int mg = cal_max_gap(p, qd < rd ? qd : rd);
+                    int ww = mg < aw ? mg : aw;
+                    if (qd - rd < ww && rd - qd < ww) { skip = true; break; }
+                    qd = aqe - (sqb + slen); rd = (int)(are - (srb + slen));
+                    mg = cal_max_gap(p, qd < rd ? qd : rd);
+                    ww = mg < aw ? mg : aw;
+                    if (qd - rd < ww && rd - qd < ww) { skip = true; break; }
+                }
+                if (skip) continue;
+                if (n_reg >= max_ext) break;
+                // extend_seed
+                const int64_t bq = srb - (sqb + cal_max_gap(p, sqb));
+                const int rem = l - sqb - slen;
+                const int64_t eq = srb + slen + (rem + cal_max_gap(p, rem));
+                int64_t rmax0 = bq > 0 ? bq : 0, rmax1 = eq < n2 ? eq : n2;
+                if (rmax0 < n && n < rmax1) {
+                    if (srb < n) rmax1 = n; else rmax0 = n;
+                }
+                int a_score = 0, a_truesc = 0, a_qb = 0, a_qe = 0;
+                int64_t a_rb = 0, a_re = 0;
+                int aw0 = p.w, aw1 = p.w;
+                if (sqb) {
+                    const int tmp = (int)(srb - rmax0);
+                    for (int x = lane; x < sqb; x += 64) L.qs[x] = L.q[sqb - 1 - x];
+                    for (int x = lane; x < tmp; x += 64) L.t[x] = ix.D[rmax0 + tmp - 1 - x];
+                    wave_sync();
+                    ExtRes er;
+                    for (int it = 0; it < 2; ++it) {
+                        const int prev = a_score;
+                        aw0 = p.w << it;
+                        er = ext_dp_wave(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
+                        a_score = er.max;
+                        if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+                    }
+                    if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip5) {
+                        a_qb = sqb - er.qle; a_rb = srb - er.tle; a_truesc = a_score;
+                    } else {
+                        a_qb = 0; a_rb = srb - er.gtle; a_truesc = er.gscore;
+                    }
+                    wave_sync();
+                } else {
+                    a_score = a_truesc = slen * p.a; a_qb = 0; a_rb = srb;
+                }
+                if (sqb + slen != l) {
+                    const int qe = sqb + slen;
+                    const int re = (int)(srb + slen - rmax0);
+                    const int sc0 = a_score;
+                    const int tl = (int)(rmax1 - rmax0 - re);
+                    for (int x = lane; x < tl; x += 64) L.t[x] = ix.D[rmax0 + re + x];
+                    wave_sync();
+                    ExtRes er;
+                    for (int it = 0; it < 2; ++it) {
+                        const int prev = a_score;
+                        aw1 = p.w << it;
+                        er = ext_dp_wave(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                        a_score = er.max;
+                        if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+                    }
+                    if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip3) {
+                        a_qe = qe + er.qle; a_re = rmax0 + re + er.tle; a_truesc += a_score - sc0;
+                    } else {
+                        a_qe = l; a_re = rmax0 + re + er.gtle; a_truesc += er.gscore - sc0;
+                    }
+                    wave_sync();
+                } else {
+                    a_qe = l; a_re = srb + slen;
+                }
+                if (lane == 0) {
+                    int *a = L.regs[n_reg];
+                    a[0] = a_score; a[1] = a_truesc; a[2] = a_qb; a[3] = a_qe;
+                    a[4] = (int)a_rb; a[5] = (int)a_re; a[6] = slen; a[7] = aw0 > aw1 ? aw0 : aw1;
+                }
+                wave_sync();
+                ++n_reg;
+            }
+            int best = -1;
+            for (int rr = 0; rr < n_reg; ++rr)
+                if (best < 0 || L.regs[rr][0] > L.regs[best][0]) best = rr;
+            if (best >= 0 && L.regs[best][0] >= p.T) {
+                // ---- 4. CIGAR --------------------------------------------------------
+                const int *a = L.regs[best];
+                const int a_score = a[0], a_truesc = a[1], aqb = a[2], aqe = a[3], awb = a[7];
+                const int64_t arb = a[4], are = a[5];
+                const bool is_rev = arb >= n;
+                const int lq = aqe - aqb;
+                const int tmpw = infer_bw(lq, (int)(are - arb), a_truesc, p.a, p.o_del, p.e_del);
+                int w2 = infer_bw(lq, (int)(are - arb), a_truesc, p.a, p.o_ins, p.e_ins);
+                w2 = w2 > tmpw ? w2 : tmpw;
+                if (w2 > p.w) w2 = w2 < awb ? w2 : awb;
+                int score = 0, last_sc = -(1 << 30), it = 0;
+                do {
+                    w2 = w2 < p.w << 2 ? w2 : p.w << 2;
+                    score = gen_cigar_wave(ix, p, w2, lq, aqb, arb, are, L, zg, lane);
+                    if (score == last_sc || w2 == p.w << 2) break;
+                    last_sc = score;
+                    w2 <<= 1;
+                } while (++it < 3 && score < a_truesc - p.a);
+                // assemble: ring holds the traceback in reverse order (count misc[2])
+                if (lane == 0) {
+                    const int nc = L.misc[2];
+                    const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
+                    bool of = nc > AF_MAX_CIGAR;
+                    uint32_t cg[AF_MAX_CIGAR + 2];
+                    const bool ungapped = (nc == 1 && L.ring[0] == ((uint32_t)lq << 4));
+                    for (int x = 0; x < ncap; ++x) cg[x] = ungapped ? L.ring[0] : L.ring[(nc - 1 - x) & 63];
+                    int nn = ncap;
+                    int64_t pos = is_rev ? n2 - are : arb;
+                    if (nn > 0) {
+                        if ((cg[0] & 0xf) == 2) {
+                            pos += cg[0] >> 4;
+                            for (int x = 0; x + 1 < nn; ++x) cg[x] = cg[x + 1];
+                            --nn;
+                        } else if ((cg[nn - 1] & 0xf) == 2) {
+                            --nn;
+                        }
+                    }
+                    const int clip5 = is_rev ? l - aqe : aqb;
+                    const int clip3 = is_rev ? aqb : l - aqe;
+                    uint32_t *co = cigar + r * AF_MAX_CIGAR;
+                    int nf = 0;
+                    auto put = [&](uint32_t v) {
+                        if (nf < AF_MAX_CIGAR) co[nf] = v;
+                        ++nf;
+                    };
+                    if (clip5) put((uint32_t)clip5 << 4 | 4);
+                    for (int x = 0; x < nn; ++x) put(cg[x]);
+                    if (clip3) put((uint32_t)clip3 << 4 | 4);
+                    if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
+                    flag = (is_rev ? 0x10 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
+                    out_pos = (int)pos;
+                    out_score = a_score;
+                    out_nc = nf;
+                }
+            }
+        }
+        if (lane == 0) {
+            ReadRec rec;
+            rec.flag = flag; rec.pos = out_pos; rec.score = out_score; rec.n_cigar = out_nc;
+            recs[r] = rec;
+        }
+        wave_sync();
+    }
+}
+
+__global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const ReadRec *__restrict__ recs,
+                        af_aln_out out) {
+    const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pp >= n_pairs) return;
+    ReadRec R[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const int64_t r = 2 * pp + m;
+        if (hits[r] > 0) R[m] = recs[r];
+        else { R[m].flag = 0x4; R[m].pos = 0; R[m].score = 0; R[m].n_cigar = 0; }
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+        const ReadRec &x = R[m], &y = R[m ^ 1];
+        const int64_t r = 2 * pp + m;
+        const int xf = x.flag, yf = y.flag;
+        int f = 0x1 | (m ? 0x80 : 0x40) | (xf & ~0x4 & 0x30000);
+        int pos = x.pos;
+        if (!(xf & 0x4)) f |= xf & 0x10;
+        else f |= 0x4;
+        if (yf & 0x4) f |= 0x8;
+        else f |= (yf & 0x10) ? 0x20 : 0;
+        if ((xf & 0x4) && !(yf & 0x4)) { pos = y.pos; f |= (yf & 0x10); }
+        if ((xf & 0x4) && (yf & 0x4)) pos = -1;
+        out.flag[r] = f;
+        out.pos[r] = pos;
+        out.score[r] = x.score;
+        out.n_cigar[r] = (xf & 0x4) ? 0 : x.n_cigar;
+    }
+}
+
+}  // namespace
+
+hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
+                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
+                           int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
+                           hipStream_t s) {
+    (void)n_reads; (void)cand_cap;
+    // work counter lives right after n_cand (see api.hip scratch layout)
+    int32_t *work = const_cast<int32_t *>(n_cand) + 1;
+    hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    hipLaunchKernelGGL(k_align, dim3(n_slots), dim3(64), 0, s, ix, reads, stride, lens, p, cand, n_cand, work, recs,
+                       cigar, zscratch, zstride);
+    return hipGetLastError();
+}
+
+hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
+                           hipStream_t s) {
+    if (n_pairs <= 0) return hipSuccess;
+    const int bs = 256;
+    hipLaunchKernelGGL(k_pairs, dim3((unsigned)((n_pairs + bs - 1) / bs)), dim3(bs), 0, s, n_pairs, hits, recs, out);
+    return hipGetLastError();
+}

@@ -1,0 +1,370 @@
+// api.hip -- C-ABI of libafgpu.so (include/afgpu.h): contexts, anchor index build and the
+// align entry points that replace `bwa index` / `bwa mem -M` (Anchored_Fusion.py:172, 182).
+#include "af_internal.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+struct af_ctx {
+    int device = 0;
+    int n_slots = 0;
+    std::string err;
+    // scratch (device)
+    int32_t *ctrl = nullptr;   // [0] n_cand, [1] work counter
+    int32_t *cand = nullptr;
+    ReadRec *recs = nullptr;
+    int64_t cap_reads = 0;
+    uint8_t *zscratch = nullptr;
+    // host-API staging (device)
+    uint8_t *d_reads = nullptr;
+    int64_t cap_bytes = 0;
+    int32_t *d_lens = nullptr;
+    int32_t *d_flag = nullptr, *d_pos = nullptr, *d_score = nullptr, *d_ncig = nullptr, *d_hits = nullptr;
+    uint32_t *d_cigar = nullptr;
+    int64_t cap_out = 0;
+    hipStream_t stream = nullptr;
+};
+
+struct af_index {
+    af_ctx *ctx = nullptr;
+    DevIndex dev{};
+    std::vector<uint16_t> ftab_host;
+    void *allocs[8] = {};
+    int n_allocs = 0;
+};
+
+namespace {
+
+inline void af_free(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+int fail(af_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                       \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess) return fail(ctx, AF_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+inline uint8_t nt4(uint8_t c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+template <class T>
+int dev_upload(af_ctx *ctx, af_index *ix, const std::vector<T> &v, const T **out) {
+    void *p = nullptr;
+    const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    HIPCHK(ctx, hipMalloc(&p, bytes));
+    ix->allocs[ix->n_allocs++] = p;
+    if (!v.empty()) HIPCHK(ctx, hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    *out = static_cast<const T *>(p);
+    return AF_OK;
+}
+
+int ensure_reads_cap(af_ctx *c, int64_t n_reads) {
+    if (n_reads <= c->cap_reads) return AF_OK;
+    af_free(c->cand); af_free(c->recs);
+    c->cand = nullptr; c->recs = nullptr; c->cap_reads = 0;
+    const int64_t cap = std::max<int64_t>(n_reads, 1 << 16);
+    HIPCHK(c, hipMalloc(&c->cand, sizeof(int32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->recs, sizeof(ReadRec) * cap));
+    c->cap_reads = cap;
+    return AF_OK;
+}
+
+int ensure_zscratch(af_ctx *c) {
+    if (c->zscratch) return AF_OK;
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    HIPCHK(c, hipMalloc(&c->zscratch, zstride * c->n_slots));
+    return AF_OK;
+}
+
+int check_params(af_ctx *c, const af_params *p) {
+    if (!p) return fail(c, AF_E_INVALID, "params is NULL");
+    if (p->a <= 0 || p->b < 0 || p->o_del < 0 || p->e_del <= 0 || p->o_ins < 0 || p->e_ins <= 0 || p->w < 0 ||
+        p->min_seed_len < AF_K || p->max_ext < 1 || p->max_ext > 16 || p->max_mems < 1 || p->max_mems > 256 ||
+        p->max_occ < 1)
+        return fail(c, AF_E_INVALID, "invalid af_params (min_seed_len>=%d, 1<=max_ext<=16, 1<=max_mems<=256)", AF_K);
+    return AF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void af_params_default(af_params *p) {
+    // bwa mem defaults (bwa 0.7.17 usage text): -A1 -B4 -O6 -E1 -L5 -w100 -d100 -k19 -T30
+    p->a = 1; p->b = 4; p->o_del = 6; p->e_del = 1; p->o_ins = 6; p->e_ins = 1;
+    p->pen_clip5 = 5; p->pen_clip3 = 5; p->w = 100; p->zdrop = 100;
+    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 256;
+}
+
+int af_ctx_create(int device, af_ctx **out) {
+    if (!out) return AF_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return AF_E_HIP;
+    if (device < 0 || device >= ndev) return AF_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return AF_E_HIP;
+    af_ctx *c = new (std::nothrow) af_ctx;
+    if (!c) return AF_E_NOMEM;
+    c->device = device;
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    c->n_slots = std::max(1, cus) * 8;
+    if (hipMalloc(&c->ctrl, 64) != hipSuccess) { delete c; return AF_E_HIP; }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        af_free(c->ctrl);
+        delete c;
+        return AF_E_HIP;
+    }
+    *out = c;
+    return AF_OK;
+}
+
+void af_ctx_destroy(af_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch);
+    af_free(c->d_reads); af_free(c->d_lens);
+    af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
+    af_free(c->d_cigar);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *af_last_error(const af_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
+    if (!c || !anchor || !out) return fail(c, AF_E_INVALID, "null argument");
+    *out = nullptr;
+    if (len <= 0) return fail(c, AF_E_INVALID, "empty anchor");
+    if (len > (1LL << 30)) return fail(c, AF_E_UNSUPPORTED, "anchor longer than 2^30");
+    (void)hipSetDevice(c->device);
+    const int64_t n = len, n2 = 2 * len;
+    std::vector<uint8_t> D(n2);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t v = nt4((uint8_t)anchor[i]);
+        D[i] = v;
+        D[n2 - 1 - i] = v < 4 ? 3 - v : 4;
+    }
+    std::vector<uint32_t> D2((n2 + 15) / 16 + 2, 0), Dn((n2 + 31) / 32 + 2, 0);
+    for (int64_t i = 0; i < n2; ++i) {
+        D2[i >> 4] |= (uint32_t)(D[i] & 3) << (2 * (i & 15));
+        if (D[i] > 3) Dn[i >> 5] |= 1u << (i & 31);
+    }
+    // 16-mer occurrences that do not cross the strand boundary, sorted by (kmer, pos)
+    std::vector<uint64_t> occ;
+    occ.reserve(n2);
+    for (int64_t p = 0; p + AF_K <= n2; ++p) {
+        if (p < n && p + AF_K > n) continue;
+        uint32_t k = 0;
+        bool ok = true;
+        for (int u = 0; u < AF_K && ok; ++u) {
+            ok = D[p + u] < 4;
+            k |= (uint32_t)(D[p + u] & 3) << (2 * u);
+        }
+        if (ok) occ.push_back((uint64_t)k << 32 | (uint64_t)p);
+    }
+    std::sort(occ.begin(), occ.end());
+    std::vector<uint32_t> keys;
+    std::vector<int32_t> starts, cnts, kpos(occ.size());
+    for (size_t i = 0; i < occ.size(); ++i) {
+        const uint32_t k = (uint32_t)(occ[i] >> 32);
+        kpos[i] = (int32_t)(occ[i] & 0xffffffffu);
+        if (i == 0 || k != keys.back()) { keys.push_back(k); starts.push_back((int32_t)i); cnts.push_back(0); }
+        ++cnts.back();
+    }
+    const int64_t nd = (int64_t)keys.size();
+    int hbits = 10;
+    while ((1LL << hbits) < 2 * nd) ++hbits;
+    const uint32_t hm = (1u << hbits) - 1u;
+    std::vector<uint32_t> hkey(1u << hbits, 0);
+    std::vector<int32_t> hstart(1u << hbits, 0), hcnt(1u << hbits, 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        uint32_t s = af_fmix(keys[i]) & hm;
+        while (hcnt[s]) s = (s + 1) & hm;
+        hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
+    }
+    // LDS filter table: avg load <= 4 per 8-slot bucket, min 256 buckets
+    int nb_bits = 8;
+    while ((1LL << nb_bits) * 4 < nd) ++nb_bits;
+    if (nb_bits > 13)
+        return fail(c, AF_E_UNSUPPORTED, "anchor has %lld distinct 16-mers; the LDS filter holds <= 32768",
+                    (long long)nd);
+    const uint32_t nb = 1u << nb_bits;
+    std::vector<uint16_t> ft((size_t)nb * 8, 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        const uint32_t h = af_fmix(keys[i]);
+        uint32_t b = h >> (32 - nb_bits);
+        const uint16_t f = (uint16_t)af_ffp(h);
+        for (;;) {
+            uint16_t *bk = &ft[(size_t)b * 8];
+            int s = 0;
+            while (s < 7 && bk[s]) ++s;
+            if (s < 7) { bk[s] = f; break; }
+            bk[7] = 1;
+            b = (b + 1) & (nb - 1);
+        }
+    }
+    af_index *ix = new (std::nothrow) af_index;
+    if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
+    ix->ctx = c;
+    ix->ftab_host = ft;
+    int rc = AF_OK;
+    const uint16_t *ftd = nullptr;
+    if ((rc = dev_upload(c, ix, D, &ix->dev.D)) || (rc = dev_upload(c, ix, D2, &ix->dev.D2)) ||
+        (rc = dev_upload(c, ix, Dn, &ix->dev.Dn)) || (rc = dev_upload(c, ix, hkey, &ix->dev.hkey)) ||
+        (rc = dev_upload(c, ix, hstart, &ix->dev.hstart)) || (rc = dev_upload(c, ix, hcnt, &ix->dev.hcnt)) ||
+        (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, ft, &ftd))) {
+        af_index_free(ix);
+        return rc;
+    }
+    ix->dev.ftab = reinterpret_cast<const uint4 *>(ftd);
+    ix->dev.n = n;
+    ix->dev.hbits = hbits;
+    ix->dev.nb_bits = nb_bits;
+    *out = ix;
+    return AF_OK;
+}
+
+void af_index_free(af_index *ix) {
+    if (!ix) return;
+    if (ix->ctx) (void)hipSetDevice(ix->ctx->device);
+    for (int i = 0; i < ix->n_allocs; ++i) af_free(ix->allocs[i]);
+    delete ix;
+}
+
+int64_t af_index_anchor_len(const af_index *ix) { return ix ? ix->dev.n : -1; }
+int32_t af_index_filter_buckets(const af_index *ix) { return ix ? (1 << ix->dev.nb_bits) : -1; }
+
+int af_index_filter_table(const af_index *ix, uint16_t *out, int64_t cap) {
+    if (!ix || !out) return AF_E_INVALID;
+    if (cap < (int64_t)ix->ftab_host.size()) return AF_E_CAPACITY;
+    memcpy(out, ix->ftab_host.data(), ix->ftab_host.size() * sizeof(uint16_t));
+    return AF_OK;
+}
+
+int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
+                          const int32_t *d_lens, int32_t *d_hits, void *stream) {
+    if (!c || !ix || (!d_reads && n_reads) || !d_hits) return fail(c, AF_E_INVALID, "null argument");
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    if (((uintptr_t)d_reads & 15) != 0) return fail(c, AF_E_INVALID, "reads buffer must be 16-byte aligned");
+    (void)hipSetDevice(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = ensure_reads_cap(c, n_reads);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(c->ctrl, 0, 64, s));
+    HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand, c->ctrl, s));
+    return AF_OK;
+}
+
+int64_t af_last_candidates(af_ctx *c) {
+    if (!c) return -1;
+    int32_t v = -1;
+    (void)hipSetDevice(c->device);
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpy(&v, c->ctrl, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return v;
+}
+
+int af_align_pairs_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
+                          const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream) {
+    if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    if (n_pairs < 0) return fail(c, AF_E_INVALID, "n_pairs < 0");
+    if (n_pairs == 0) return AF_OK;
+    if (!o->flag || !o->pos || !o->score || !o->n_cigar || !o->hits || !o->cigar)
+        return fail(c, AF_E_INVALID, "output arrays must all be non-NULL");
+    if ((rc = af_seed_filter_device(c, ix, d_reads, 2 * n_pairs, stride, d_lens, o->hits, stream))) return rc;
+    return af_align_candidates_device(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream);
+}
+
+int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
+                               int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
+                               void *stream) {
+    if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    if (n_pairs <= 0) return n_pairs == 0 ? AF_OK : fail(c, AF_E_INVALID, "n_pairs < 0");
+    if (!o->flag || !o->pos || !o->score || !o->n_cigar || !o->hits || !o->cigar)
+        return fail(c, AF_E_INVALID, "output arrays must all be non-NULL");
+    if (2 * n_pairs > c->cap_reads) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
+    const int64_t nr = 2 * n_pairs;
+    if ((rc = ensure_zscratch(c))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, c->ctrl, c->cap_reads, c->recs,
+                              o->cigar, c->zscratch, c->n_slots, s));
+    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, s));
+    return AF_OK;
+}
+
+int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                   const int32_t *lens, const af_params *p, af_aln_out *out) {
+    if (!c || !ix || !out || (!reads && n_pairs)) return fail(c, AF_E_INVALID, "null argument");
+    if (n_pairs == 0) return AF_OK;
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    (void)hipSetDevice(c->device);
+    const int64_t nr = 2 * n_pairs;
+    const int64_t bytes = nr * (int64_t)stride;
+    if (bytes > c->cap_bytes) {
+        af_free(c->d_reads); af_free(c->d_lens);
+        c->d_reads = nullptr; c->d_lens = nullptr; c->cap_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_reads, bytes + 64));
+        HIPCHK(c, hipMalloc(&c->d_lens, sizeof(int32_t) * nr + 64));
+        c->cap_bytes = bytes;
+    }
+    if (nr > c->cap_out) {
+        af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
+        af_free(c->d_cigar);
+        c->cap_out = 0;
+        HIPCHK(c, hipMalloc(&c->d_flag, 4 * nr)); HIPCHK(c, hipMalloc(&c->d_pos, 4 * nr));
+        HIPCHK(c, hipMalloc(&c->d_score, 4 * nr)); HIPCHK(c, hipMalloc(&c->d_ncig, 4 * nr));
+        HIPCHK(c, hipMalloc(&c->d_hits, 4 * nr));
+        HIPCHK(c, hipMalloc(&c->d_cigar, sizeof(uint32_t) * AF_MAX_CIGAR * nr));
+        c->cap_out = nr;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_reads, reads, bytes, hipMemcpyHostToDevice, s));
+    if (lens) {
+        for (int64_t i = 0; i < nr; ++i)
+            if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
+        HIPCHK(c, hipMemcpyAsync(c->d_lens, lens, 4 * nr, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_cigar, 0, sizeof(uint32_t) * AF_MAX_CIGAR * nr, s));
+    af_aln_out d{c->d_flag, c->d_pos, c->d_score, c->d_ncig, c->d_hits, c->d_cigar};
+    int rc = af_align_pairs_device(c, ix, c->d_reads, n_pairs, stride, lens ? c->d_lens : nullptr, p, &d, s);
+    if (rc) return rc;
+    if (out->flag) HIPCHK(c, hipMemcpyAsync(out->flag, c->d_flag, 4 * nr, hipMemcpyDeviceToHost, s));
+    if (out->pos) HIPCHK(c, hipMemcpyAsync(out->pos, c->d_pos, 4 * nr, hipMemcpyDeviceToHost, s));
+    if (out->score) HIPCHK(c, hipMemcpyAsync(out->score, c->d_score, 4 * nr, hipMemcpyDeviceToHost, s));
+    if (out->n_cigar) HIPCHK(c, hipMemcpyAsync(out->n_cigar, c->d_ncig, 4 * nr, hipMemcpyDeviceToHost, s));
+    if (out->hits) HIPCHK(c, hipMemcpyAsync(out->hits, c->d_hits, 4 * nr, hipMemcpyDeviceToHost, s));
+    if (out->cigar)
+        HIPCHK(c, hipMemcpyAsync(out->cigar, c->d_cigar, sizeof(uint32_t) * AF_MAX_CIGAR * nr, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return AF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Benchmark of the anchored split-read alignment hot path (BASELINE.json metric:
+paired reads/sec through anchored split-read align on 1/2/4/8 MI355X).
+
+Workload (BASELINE.json configs[1]): 1 M synthetic 2x100 bp pairs per GPU against one
+anchor transcript (the bundled BCR NM_004327.4, 6,783 nt), 5 % of pairs from anchor
+fusions, the rest from a random background transcriptome (wgsim-style simulator, seeded).
+A step = one pass of the GPU path over the resident batch: seed filter (K1), candidate
+seed/extend/CIGAR (K2) and pair flags (K3), i.e. the records `bwa mem -M` hands to samtools
+at Anchored_Fusion.py:182.  Inputs are resident in HBM before timing starts.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
+torch.distributed.run; each rank aligns its own shard (no data-path collective: pairs are
+independent), and the time is the max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU")
+    ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--fusion-frac", type=float, default=0.05)
+    ap.add_argument("--cpu-sample", type=int, default=100_000, help="pairs timed on the CPU oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import afpkg  # noqa: F401
+    from anchored_fusion_amd import io as afio
+    from anchored_fusion_amd import simulate as sim
+    from anchored_fusion_amd.align import AnchorAligner
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
+    L = args.read_len
+    _, reads, _, _ = sim.fusion_reads(anchor, args.pairs, read_len=L, fusion_frac=args.fusion_frac,
+                                      seed=20251015 + 7919 * rank)
+    nr = reads.shape[0]
+    reads_t = torch.from_numpy(reads).to(dev)
+    out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+    out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
+    al = AnchorAligner(anchor, device=local)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        al.seed_filter_device(reads_t, nr, L, out["hits"], stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        al.align_candidates_device(reads_t, args.pairs, L, out, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    n_cand = al.last_candidates()
+    mapped = int(((out["flag"] & 4) == 0).sum().item())
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    k1_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    k23_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+
+    bytes_per_launch = nr * L + 4 * nr  # 2L bases + 2 x int32 per pair (SURVEY.md §8 d)
+    achieved = bytes_per_launch / (k1_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_seed_filter.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("pairs") == args.pairs and pm.get("read_len") == L:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    total_pairs = args.pairs * world * args.steps
+    value = total_pairs / elapsed
+    res = {
+        "metric": "paired reads/sec through anchored split-read align",
+        "value": round(value, 1),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (wgsim-style simulator, seed 20251015 + rank)",
+        "config": {
+            "workload": f"configs[1]: {args.pairs} synthetic 2x{L} bp pairs per GPU, one anchor "
+                        f"(BCR NM_004327.4, {len(anchor)} nt), {args.fusion_frac:.0%} fusion pairs",
+            "pairs_per_gpu": args.pairs, "read_len": L, "anchor_len": len(anchor),
+            "parallelism": f"dp{world}", "candidates_per_step": n_cand, "mapped_reads_per_step": mapped,
+        },
+        "kernels_ms": {"seed_filter": round(k1_ms, 5), "align_candidates_and_pairs": round(k23_ms, 5)},
+        "roofline": {
+            "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(anchor, args, L)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    al.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(anchor, args, L):
+    """The CPU oracle (a port of the same algorithm; bwa itself is absent) on a bounded sample."""
+    import oracle
+    from anchored_fusion_amd import simulate as sim
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n = args.cpu_sample
+    _, reads, _, _ = sim.fusion_reads(anchor, n, read_len=L, fusion_frac=args.fusion_frac, seed=20251015)
+    ix = oracle.OracleIndex(anchor)
+    t0 = time.perf_counter()
+    ix.align_pairs(reads, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} pairs of the same workload (first {n} of rank 0's generator), oracle/af_oracle.c, "
+                      f"OpenMP {threads} threads, {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+/*
+ * afgpu.h -- C-ABI of libafgpu.so, the MI355X-native anchored split-read aligner.
+ *
+ * Drop-in boundary (SURVEY.md §8 b).  The reference has no plugin API: the hot path is a
+ * shell string plus files.  Each entry point below replaces one of those tool calls:
+ *
+ *   af_index_build        <- `bwa index <G>_fusion_anchored_gene_sequence.fa`
+ *                            (Anchored_Fusion.py:167-172; FASTA written at AF:154-163)
+ *   af_align_pairs        <- `bwa mem -M -t T anchor fq1 fq2 | samtools view -bSu -`
+ *                            (Anchored_Fusion.py:182); per-read primary records carrying the
+ *                            SAM fields the callers read (FLAG/POS/CIGAR, functions.py:380-385,
+ *                            515-516, 712-714, 917-918; AF:186-194 flag filters)
+ *   af_align_pairs_device <- same, device-resident buffers, enqueued on a HIP stream
+ *   af_seed_filter_device <- the seeding pass of the same call (the HBM-bound kernel)
+ *   af_align_candidates_device <- the extension/CIGAR/pairing pass of the same call
+ *
+ * Conventions: plain pointers and sizes only; every function returns AF_OK (0) or a
+ * negative AF_E_* code and sets a message readable with af_last_error().  No C++
+ * exception crosses this boundary.  One context per GPU; calls on a context are not
+ * re-entrant (one host thread per GPU is the supported model).
+ *
+ * Reads are pair-major, one byte per base (ASCII): row 2p = mate 1, row 2p+1 = mate 2,
+ * `stride` bytes per row; `lens` may be NULL when every read has length `stride`.
+ * Output arrays are caller-owned, 2*n_pairs entries each (cigar: 2*n_pairs*AF_MAX_CIGAR,
+ * BAM op encoding len<<4|op, M=0 I=1 D=2 S=4).  pos is the 0-based leftmost position of
+ * the primary alignment (or of the mate, for an unmapped read with a mapped mate, as bwa
+ * prints it); flag carries the SAM bits 0x1 0x4 0x8 0x10 0x20 0x40 0x80 plus
+ * AF_FLAG_MEM_OVERFLOW / AF_FLAG_CIGAR_OVERFLOW.
+ */
+#ifndef AFGPU_H
+#define AFGPU_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AF_OK 0
+#define AF_E_INVALID (-1)
+#define AF_E_HIP (-2)
+#define AF_E_CAPACITY (-3)
+#define AF_E_NOMEM (-4)
+#define AF_E_UNSUPPORTED (-5)
+
+#define AF_K 16
+#define AF_MAX_CIGAR 32
+#define AF_MAX_READ 320
+#define AF_FLAG_MEM_OVERFLOW 0x10000
+#define AF_FLAG_CIGAR_OVERFLOW 0x20000
+
+typedef struct af_ctx af_ctx;
+typedef struct af_index af_index;
+
+/* bwa mem scoring/seeding parameters (defaults = bwa mem defaults, see af_params_default) */
+typedef struct {
+    int32_t a, b;                       /* -A -B */
+    int32_t o_del, e_del, o_ins, e_ins; /* -O -E */
+    int32_t pen_clip5, pen_clip3;       /* -L    */
+    int32_t w;                          /* -w    */
+    int32_t zdrop;                      /* -d    */
+    int32_t min_seed_len;               /* -k    */
+    int32_t max_occ;                    /* k-mer occurrence cap */
+    int32_t T;                          /* -T    */
+    int32_t max_ext;                    /* seeds extended per read (<= 64) */
+    int32_t max_mems;                   /* MEM cap per read (<= 256) */
+} af_params;
+
+typedef struct {
+    int32_t *flag, *pos, *score, *n_cigar, *hits;
+    uint32_t *cigar;
+} af_aln_out;
+
+int af_ctx_create(int device, af_ctx **out);
+void af_ctx_destroy(af_ctx *ctx);
+const char *af_last_error(const af_ctx *ctx);
+void af_params_default(af_params *p);
+
+/* anchor index (doubled reference anchor ++ revcomp, 16-mer position map, LDS filter table) */
+int af_index_build(af_ctx *ctx, const char *anchor, int64_t len, af_index **out);
+void af_index_free(af_index *idx);
+int64_t af_index_anchor_len(const af_index *idx);
+int32_t af_index_filter_buckets(const af_index *idx);
+/* copies the filter table (nbuckets*8 uint16) to host memory */
+int af_index_filter_table(const af_index *idx, uint16_t *out, int64_t cap);
+
+/* host buffers in, host buffers out; synchronous */
+int af_align_pairs(af_ctx *ctx, const af_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                   const int32_t *lens, const af_params *p, af_aln_out *out);
+/* device buffers in/out, asynchronous on `stream` (hipStream_t; NULL = default stream) */
+int af_align_pairs_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
+                          int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
+                          void *stream);
+int af_seed_filter_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_reads,
+                          int32_t stride, const int32_t *d_lens, int32_t *d_hits, void *stream);
+/* the rest of af_align_pairs_device after af_seed_filter_device ran on the same context and
+ * stream with d_hits = d_out->hits for these reads: candidate alignment + pair flags */
+int af_align_candidates_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
+                               int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
+                               void *stream);
+/* number of candidate reads found by the last seed-filter pass on this context (synchronises) */
+int64_t af_last_candidates(af_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,108 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU oracle (oracle/af_oracle.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  The product path (anchored-fusion_amd/) never loads it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libafo.so")
+MAX_CIGAR = 32
+FLAG_MEM_OVERFLOW = 0x10000
+FLAG_CIGAR_OVERFLOW = 0x20000
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop",
+        "min_seed_len", "max_occ", "T", "max_ext", "max_mems")]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("flag", ctypes.c_void_p), ("pos", ctypes.c_void_p), ("score", ctypes.c_void_p),
+                ("n_cigar", ctypes.c_void_p), ("hits", ctypes.c_void_p), ("cigar", ctypes.c_void_p)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.afo_index_build.restype = ctypes.c_void_p
+        L.afo_index_build.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+        L.afo_index_free.argtypes = [ctypes.c_void_p]
+        L.afo_filter_nbuckets.restype = ctypes.c_int32
+        L.afo_filter_nbuckets.argtypes = [ctypes.c_void_p]
+        L.afo_filter_table.restype = ctypes.c_void_p
+        L.afo_filter_table.argtypes = [ctypes.c_void_p]
+        L.afo_params_default.argtypes = [ctypes.POINTER(Params)]
+        L.afo_seed_filter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.afo_align_pairs.restype = ctypes.c_int
+        L.afo_align_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                      ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int,
+                                      ctypes.POINTER(_Out)]
+        _lib = L
+    return _lib
+
+
+def default_params():
+    p = Params()
+    lib().afo_params_default(ctypes.byref(p))
+    return p
+
+
+class OracleIndex:
+    def __init__(self, anchor: bytes):
+        self.anchor = bytes(anchor)
+        self.h = lib().afo_index_build(self.anchor, len(self.anchor))
+        if not self.h:
+            raise ValueError("empty anchor")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.afo_index_free(self.h)
+            self.h = None
+
+    def filter_table(self):
+        nb = lib().afo_filter_nbuckets(self.h)
+        ptr = lib().afo_filter_table(self.h)
+        return np.ctypeslib.as_array((ctypes.c_uint16 * (nb * 8)).from_address(ptr)).copy()
+
+    def seed_filter(self, reads, lens=None):
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        hits = np.zeros(n, dtype=np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        lib().afo_seed_filter(self.h, reads.ctypes.data, n, reads.shape[1],
+                              None if lp is None else lp.ctypes.data, hits.ctypes.data)
+        return hits
+
+    def align_pairs(self, reads, lens=None, params=None, threads=0):
+        """reads: [2N, stride] uint8 pair-major.  Returns dict of per-read arrays."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        nr = reads.shape[0]
+        assert nr % 2 == 0
+        out = {k: np.zeros(nr, dtype=np.int32) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+        out["cigar"] = np.zeros((nr, MAX_CIGAR), dtype=np.uint32)
+        o = _Out(*(out[k].ctypes.data for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        p = params or default_params()
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = lib().afo_align_pairs(self.h, reads.ctypes.data, nr // 2, reads.shape[1],
+                                   None if lp is None else lp.ctypes.data, ctypes.byref(p), int(threads),
+                                   ctypes.byref(o))
+        if rc != 0:
+            raise RuntimeError(f"afo_align_pairs failed: {rc}")
+        return out

@@ -1,0 +1,591 @@
+/*
+ * af_oracle.c -- TEST INFRASTRUCTURE ONLY (see af_oracle.h).
+ *
+ * Plain-C restatement of the S2 path of the reference (Anchored_Fusion.py:181-182:
+ * `bwa mem -M -t T anchor fq1 fq2`), written as the bit-exact contract for the HIP
+ * kernels in anchored-fusion_amd/csrc.  Every stage cites the published bwa-mem
+ * algorithm it restates; nothing here is called by the product path.
+ */
+#include "af_oracle.h"
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NEG_INF (-0x40000000)
+
+struct afo_index {
+    int64_t n;          /* anchor length                                    */
+    uint8_t *D;         /* 2n codes: anchor ++ revcomp(anchor), N = 4       */
+    int64_t nk;         /* number of indexed 16-mer positions              */
+    uint32_t *kmer;     /* sorted by (kmer, pos)                            */
+    int32_t *kpos;
+    int32_t nb;         /* filter buckets (power of two)                    */
+    int32_t nb_bits;
+    uint16_t *ftab;     /* nb * 8 halfwords; slot 7 = overflow flag         */
+};
+
+/* ---- encoding ---------------------------------------------------------------------- */
+static inline uint8_t nt4(uint8_t c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+void afo_params_default(afo_params *p) {
+    /* bwa mem defaults (bwa 0.7.17 `bwa mem` usage text) */
+    p->a = 1; p->b = 4; p->o_del = 6; p->e_del = 1; p->o_ins = 6; p->e_ins = 1;
+    p->pen_clip5 = 5; p->pen_clip3 = 5; p->w = 100; p->zdrop = 100;
+    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 256;
+}
+
+/* filter hash: bijective 32-bit mix; bucket = top bits, fingerprint = bits 4..18 | 0x8000 */
+static inline uint32_t fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
+static inline uint16_t ffp(uint32_t h) { return (uint16_t)(((h >> 4) & 0x7FFFu) | 0x8000u); }
+
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* 16-mer packing: base i at bits [2i, 2i+1] */
+static inline int pack16(const uint8_t *c, uint32_t *k) {
+    uint32_t v = 0;
+    for (int i = 0; i < AFO_K; ++i) {
+        if (c[i] > 3) return 0;
+        v |= (uint32_t)c[i] << (2 * i);
+    }
+    *k = v;
+    return 1;
+}
+
+afo_index *afo_index_build(const char *anchor, int64_t n) {
+    if (n <= 0) return NULL;
+    afo_index *I = (afo_index *)calloc(1, sizeof(afo_index));
+    I->n = n;
+    I->D = (uint8_t *)malloc(2 * n);
+    for (int64_t i = 0; i < n; ++i) {
+        uint8_t c = nt4((uint8_t)anchor[i]);
+        I->D[i] = c;
+        I->D[2 * n - 1 - i] = c < 4 ? 3 - c : 4;
+    }
+    /* every valid 16-mer position of D that does not cross the strand boundary at n */
+    uint64_t *tmp = (uint64_t *)malloc(sizeof(uint64_t) * (2 * n + 1));
+    int64_t m = 0;
+    for (int64_t p = 0; p + AFO_K <= 2 * n; ++p) {
+        if (p < n && p + AFO_K > n) continue;
+        uint32_t k;
+        if (!pack16(I->D + p, &k)) continue;
+        tmp[m++] = ((uint64_t)k << 32) | (uint64_t)p;
+    }
+    qsort(tmp, m, sizeof(uint64_t), cmp_u64);
+    I->nk = m;
+    I->kmer = (uint32_t *)malloc(sizeof(uint32_t) * (m + 1));
+    I->kpos = (int32_t *)malloc(sizeof(int32_t) * (m + 1));
+    int64_t nd = 0;
+    for (int64_t i = 0; i < m; ++i) {
+        I->kmer[i] = (uint32_t)(tmp[i] >> 32);
+        I->kpos[i] = (int32_t)(tmp[i] & 0xffffffffu);
+        if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
+    }
+    /* filter table: smallest power of two with average load <= 4 (min 256 buckets) */
+    int bits = 8;
+    while ((1LL << bits) * 4 < nd) ++bits;
+    I->nb_bits = bits;
+    I->nb = 1 << bits;
+    I->ftab = (uint16_t *)calloc((size_t)I->nb * 8, sizeof(uint16_t));
+    for (int64_t i = 0; i < m; ++i) {
+        if (i > 0 && I->kmer[i] == I->kmer[i - 1]) continue; /* distinct keys, ascending */
+        uint32_t h = fmix(I->kmer[i]);
+        uint32_t b = h >> (32 - bits);
+        uint16_t f = ffp(h);
+        for (;;) {
+            uint16_t *bk = I->ftab + (size_t)b * 8;
+            int s = 0;
+            while (s < 7 && bk[s]) ++s;
+            if (s < 7) { bk[s] = f; break; }
+            bk[7] = 1; /* overflow: continue in the next bucket */
+            b = (b + 1) & (uint32_t)(I->nb - 1);
+        }
+    }
+    free(tmp);
+    return I;
+}
+
+void afo_index_free(afo_index *I) {
+    if (!I) return;
+    free(I->D); free(I->kmer); free(I->kpos); free(I->ftab); free(I);
+}
+int64_t afo_index_len(const afo_index *I) { return I->n; }
+int32_t afo_filter_nbuckets(const afo_index *I) { return I->nb; }
+const uint16_t *afo_filter_table(const afo_index *I) { return I->ftab; }
+
+static int filter_query(const afo_index *I, uint32_t k) {
+    uint32_t h = fmix(k);
+    uint32_t b = h >> (32 - I->nb_bits);
+    uint16_t f = ffp(h);
+    for (;;) {
+        const uint16_t *bk = I->ftab + (size_t)b * 8;
+        for (int s = 0; s < 7; ++s)
+            if (bk[s] == f) return 1;
+        if (bk[7] != 1) return 0;
+        b = (b + 1) & (uint32_t)(I->nb - 1);
+    }
+}
+
+/* K1 semantics: sampled positions are those whose byte offset in the read buffer is a
+ * multiple of 4; any MEM >= 19 nt contains such a 16-mer, so hits==0 => no seed. */
+void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, int32_t stride,
+                     const int32_t *lens, int32_t *hits) {
+    for (int64_t r = 0; r < n_reads; ++r) {
+        int32_t l = lens ? lens[r] : stride;
+        int64_t base = r * (int64_t)stride;
+        int32_t h = 0;
+        int32_t i0 = (int32_t)((4 - (base & 3)) & 3);
+        for (int32_t i = i0; i + AFO_K <= l; i += 4) {
+            uint8_t c[AFO_K];
+            for (int j = 0; j < AFO_K; ++j) c[j] = nt4(reads[base + i + j]);
+            uint32_t k;
+            if (!pack16(c, &k)) continue;
+            h += filter_query(I, k);
+        }
+        hits[r] = h;
+    }
+}
+
+/* ---- score matrix (bwa_fill_scmat): a / -b for ACGT, -1 for anything with N -------- */
+static inline int sc(const afo_params *p, uint8_t x, uint8_t y) {
+    if (x > 3 || y > 3) return -1;
+    return x == y ? p->a : -p->b;
+}
+
+/* ---- ksw_extend restated (bwa ksw.c ksw_extend2): target rows, query columns ------- */
+typedef struct { int32_t h, e; } eh_t;
+
+static int ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
+                  int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
+                  int *_gscore, int *_max_off) {
+    eh_t eh[AFO_MAX_READ + 2];
+    int oe_del = p->o_del + p->e_del, oe_ins = p->o_ins + p->e_ins;
+    int i, j, max, max_i, max_j, max_ie, gscore, max_off, beg, end;
+    memset(eh, 0, sizeof(eh_t) * (qlen + 2));
+    /* first row */
+    eh[0].h = h0;
+    eh[1].h = h0 > oe_ins ? h0 - oe_ins : 0;
+    for (j = 2; j <= qlen && eh[j - 1].h > p->e_ins; ++j) eh[j].h = eh[j - 1].h - p->e_ins;
+    /* band adjustment: the longest gap that can still score */
+    {
+        int mx = p->a;
+        int max_ins = (int)((double)(qlen * mx + end_bonus - p->o_ins) / p->e_ins + 1.);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = (int)((double)(qlen * mx + end_bonus - p->o_del) / p->e_del + 1.);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    max = h0; max_i = max_j = -1; max_ie = -1; gscore = -1; max_off = 0;
+    beg = 0; end = qlen;
+    for (i = 0; i < tlen; ++i) {
+        int t, f = 0, h1, m = 0, mj = -1;
+        uint8_t ti = target[i];
+        if (beg < i - w) beg = i - w;
+        if (end > i + w + 1) end = i + w + 1;
+        if (end > qlen) end = qlen;
+        if (beg == 0) {
+            h1 = h0 - (p->o_del + p->e_del * (i + 1));
+            if (h1 < 0) h1 = 0;
+        } else h1 = 0;
+        for (j = beg; j < end; ++j) {
+            eh_t *q = &eh[j];
+            int h, M = q->h, e = q->e;
+            q->h = h1;
+            M = M ? M + sc(p, ti, query[j]) : 0;
+            h = M > e ? M : e;
+            h = h > f ? h : f;
+            h1 = h;
+            mj = m > h ? mj : j;
+            m = m > h ? m : h;
+            t = M - oe_del; t = t > 0 ? t : 0;
+            e -= p->e_del; e = e > t ? e : t;
+            q->e = e;
+            t = M - oe_ins; t = t > 0 ? t : 0;
+            f -= p->e_ins; f = f > t ? f : t;
+        }
+        eh[end].h = h1; eh[end].e = 0;
+        if (j == qlen) {
+            max_ie = gscore > h1 ? max_ie : i;
+            gscore = gscore > h1 ? gscore : h1;
+        }
+        if (m == 0) break;
+        if (m > max) {
+            max = m; max_i = i; max_j = mj;
+            int off = mj - i < 0 ? i - mj : mj - i;
+            max_off = max_off > off ? max_off : off;
+        } else if (zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (max - m - ((i - max_i) - (mj - max_j)) * p->e_del > zdrop) break;
+            } else {
+                if (max - m - ((mj - max_j) - (i - max_i)) * p->e_ins > zdrop) break;
+            }
+        }
+        for (j = beg; j < end && eh[j].h == 0 && eh[j].e == 0; ++j) ;
+        beg = j;
+        for (j = end; j >= beg && eh[j].h == 0 && eh[j].e == 0; --j) ;
+        end = j + 2 < qlen ? j + 2 : qlen;
+    }
+    *_qle = max_j + 1; *_tle = max_i + 1; *_gtle = max_ie + 1; *_gscore = gscore;
+    *_max_off = max_off;
+    return max;
+}
+
+/* ---- ksw_global restated (bwa ksw.c ksw_global2) with traceback -------------------- */
+static inline int push_cigar(uint32_t *cig, int n, int cap, int op, int len) {
+    if (n > 0 && (int)(cig[n - 1] & 0xf) == op) { cig[n - 1] += (uint32_t)len << 4; return n; }
+    if (n < cap) cig[n] = (uint32_t)len << 4 | (uint32_t)op;
+    return n + 1;
+}
+
+/* returns score; writes cigar (ops M=0 I=1 D=2), *n_cig may exceed cap (overflow) */
+static int global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
+                     int w, uint32_t *cig, int cap, int *n_cig) {
+    int oe_del = p->o_del + p->e_del, oe_ins = p->o_ins + p->e_ins;
+    int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    eh_t *eh = (eh_t *)malloc(sizeof(eh_t) * (qlen + 1));
+    uint8_t *z = (uint8_t *)malloc((size_t)n_col * (tlen > 0 ? tlen : 1));
+    int i, j, k;
+    eh[0].h = 0; eh[0].e = NEG_INF;
+    for (j = 1; j <= qlen && j <= w; ++j) { eh[j].h = -(p->o_ins + p->e_ins * j); eh[j].e = NEG_INF; }
+    for (; j <= qlen; ++j) eh[j].h = eh[j].e = NEG_INF;
+    for (i = 0; i < tlen; ++i) {
+        int32_t f = NEG_INF, h1, beg, end, t;
+        uint8_t *zi = z + (size_t)i * n_col;
+        beg = i > w ? i - w : 0;
+        end = i + w + 1 < qlen ? i + w + 1 : qlen;
+        h1 = beg == 0 ? -(p->o_del + p->e_del * (i + 1)) : NEG_INF;
+        for (j = beg; j < end; ++j) {
+            eh_t *q = &eh[j];
+            int32_t h, m = q->h, e = q->e;
+            uint8_t d;
+            q->h = h1;
+            m += sc(p, target[i], query[j]);
+            d = m >= e ? 0 : 1;
+            h = m >= e ? m : e;
+            d = h >= f ? d : 2;
+            h = h >= f ? h : f;
+            h1 = h;
+            t = m - oe_del;
+            e -= p->e_del;
+            d |= e > t ? 1 << 2 : 0;
+            e = e > t ? e : t;
+            q->e = e;
+            t = m - oe_ins;
+            f -= p->e_ins;
+            d |= f > t ? 2 << 4 : 0;
+            f = f > t ? f : t;
+            zi[j - beg] = d;
+        }
+        eh[end].h = h1; eh[end].e = NEG_INF;
+    }
+    int score = eh[qlen].h;
+    /* backtrack from the last cell, then reverse */
+    int nc = 0, which = 0;
+    uint32_t tmp[2 * AFO_MAX_READ + 8];
+    int tcap = 2 * AFO_MAX_READ + 8;
+    i = tlen - 1;
+    k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+    while (i >= 0 && k >= 0) {
+        which = z[(size_t)i * n_col + (k - (i > w ? i - w : 0))] >> (which << 1) & 3;
+        if (which == 0) { nc = push_cigar(tmp, nc, tcap, 0, 1); --i; --k; }
+        else if (which == 1) { nc = push_cigar(tmp, nc, tcap, 2, 1); --i; }
+        else { nc = push_cigar(tmp, nc, tcap, 1, 1); --k; }
+    }
+    if (i >= 0) nc = push_cigar(tmp, nc, tcap, 2, i + 1);
+    if (k >= 0) nc = push_cigar(tmp, nc, tcap, 1, k + 1);
+    for (int x = 0; x < nc && x < cap; ++x) cig[x] = tmp[nc - 1 - x];
+    *n_cig = nc;
+    free(eh); free(z);
+    return score;
+}
+
+/* ---- bwa helpers restated (bwamem.c cal_max_gap / infer_bw) ------------------------ */
+static inline int cal_max_gap(const afo_params *p, int qlen) {
+    int l_del = (int)((double)(qlen * p->a - p->o_del) / p->e_del + 1.);
+    int l_ins = (int)((double)(qlen * p->a - p->o_ins) / p->e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < p->w << 1 ? l : p->w << 1;
+}
+
+static inline int infer_bw(int l1, int l2, int score, int a, int q, int r) {
+    int w;
+    if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
+    w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
+    int d = l1 - l2 < 0 ? l2 - l1 : l1 - l2;
+    if (w < d) w = d;
+    return w;
+}
+
+typedef struct { int32_t qb, rb, len; } mem_t;
+typedef struct { int32_t score, truesc, qb, qe, rb, re, seedlen0, w; } reg_t;
+
+static int cmp_mem(const void *a, const void *b) {
+    const mem_t *x = (const mem_t *)a, *y = (const mem_t *)b;
+    if (x->len != y->len) return y->len - x->len;
+    if (x->qb != y->qb) return x->qb - y->qb;
+    return x->rb - y->rb;
+}
+
+typedef struct { int32_t flag, pos, score, n_cigar; uint32_t cigar[AFO_MAX_CIGAR]; } rec_t;
+
+#define FLAG_MEM_OVERFLOW 0x10000
+#define FLAG_CIGAR_OVERFLOW 0x20000
+
+/* MEM search on the doubled reference (SMEM seeding of bwa mem, restated as all MEMs
+ * >= min_seed_len whose first 16-mer occurs <= max_occ times) */
+static int find_mems(const afo_index *I, const uint8_t *q, int l, const afo_params *p, mem_t *mems, int *overflow) {
+    int nm = 0;
+    int64_t n = I->n;
+    *overflow = 0;
+    for (int qb = 0; qb + AFO_K <= l; ++qb) {
+        uint32_t k;
+        if (!pack16(q + qb, &k)) continue;
+        /* equal range of k in sorted kmer[] */
+        int64_t lo = 0, hi = I->nk;
+        while (lo < hi) { int64_t mid = (lo + hi) >> 1; if (I->kmer[mid] < k) lo = mid + 1; else hi = mid; }
+        int64_t e = lo;
+        while (e < I->nk && I->kmer[e] == k) ++e;
+        int64_t cnt = e - lo;
+        if (cnt == 0 || cnt > p->max_occ) continue;
+        for (int64_t x = lo; x < e; ++x) {
+            int64_t rb = I->kpos[x];
+            if (qb > 0 && rb != 0 && rb != n && q[qb - 1] < 4 && q[qb - 1] == I->D[rb - 1]) continue;
+            int64_t lim = rb < n ? n : 2 * n;
+            int len = AFO_K;
+            while (qb + len < l && rb + len < lim && q[qb + len] < 4 && q[qb + len] == I->D[rb + len]) ++len;
+            if (len < p->min_seed_len) continue;
+            if (nm >= p->max_mems) { *overflow = 1; return nm; }
+            mems[nm].qb = qb; mems[nm].rb = (int32_t)rb; mems[nm].len = len;
+            ++nm;
+        }
+    }
+    return nm;
+}
+
+/* mem_chain2aln restated for a single-seed chain */
+static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t *s, const afo_params *p, reg_t *a) {
+    int64_t n2 = 2 * I->n;
+    int64_t b = s->rb - (s->qb + cal_max_gap(p, s->qb));
+    int rem = l - s->qb - s->len;
+    int64_t e = s->rb + s->len + (rem + cal_max_gap(p, rem));
+    int64_t rmax0 = b > 0 ? b : 0, rmax1 = e < n2 ? e : n2;
+    if (rmax0 < I->n && I->n < rmax1) {
+        if (s->rb < I->n) rmax1 = I->n; else rmax0 = I->n;
+    }
+    const uint8_t *rseq = I->D + rmax0;
+    int aw0 = p->w, aw1 = p->w;
+    int qle, tle, gtle, gscore, max_off;
+    memset(a, 0, sizeof(*a));
+    if (s->qb) {
+        uint8_t qs[AFO_MAX_READ], rs[2 * AFO_MAX_READ + 512];
+        int tmp = (int)(s->rb - rmax0);
+        for (int i = 0; i < s->qb; ++i) qs[i] = q[s->qb - 1 - i];
+        for (int i = 0; i < tmp; ++i) rs[i] = rseq[tmp - 1 - i];
+        for (int it = 0; it < 2; ++it) {
+            int prev = a->score;
+            aw0 = p->w << it;
+            a->score = ext_dp(s->qb, qs, tmp, rs, p, aw0, p->pen_clip5, p->zdrop, s->len * p->a, &qle, &tle,
+                              &gtle, &gscore, &max_off);
+            if (a->score == prev || max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+        }
+        if (gscore <= 0 || gscore <= a->score - p->pen_clip5) {
+            a->qb = s->qb - qle; a->rb = s->rb - tle; a->truesc = a->score;
+        } else {
+            a->qb = 0; a->rb = s->rb - gtle; a->truesc = gscore;
+        }
+    } else {
+        a->score = a->truesc = s->len * p->a; a->qb = 0; a->rb = s->rb;
+    }
+    if (s->qb + s->len != l) {
+        int qe = s->qb + s->len;
+        int re = (int)(s->rb + s->len - rmax0);
+        int sc0 = a->score;
+        for (int it = 0; it < 2; ++it) {
+            int prev = a->score;
+            aw1 = p->w << it;
+            a->score = ext_dp(l - qe, q + qe, (int)(rmax1 - rmax0 - re), rseq + re, p, aw1, p->pen_clip3, p->zdrop,
+                              sc0, &qle, &tle, &gtle, &gscore, &max_off);
+            if (a->score == prev || max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+        }
+        if (gscore <= 0 || gscore <= a->score - p->pen_clip3) {
+            a->qe = qe + qle; a->re = (int32_t)(rmax0 + re + tle); a->truesc += a->score - sc0;
+        } else {
+            a->qe = l; a->re = (int32_t)(rmax0 + re + gtle); a->truesc += gscore - sc0;
+        }
+    } else {
+        a->qe = l; a->re = s->rb + s->len;
+    }
+    a->seedlen0 = s->len;
+    a->w = aw0 > aw1 ? aw0 : aw1;
+}
+
+/* bwa_gen_cigar2 restated; query/ref segments in forward-reference orientation */
+static int gen_cigar(const afo_index *I, const afo_params *p, int w_, int lq, const uint8_t *qseg, int64_t rb,
+                     int64_t re, uint32_t *cig, int *n_cig) {
+    uint8_t qq[AFO_MAX_READ], rr[2 * AFO_MAX_READ + 512];
+    int rlen = (int)(re - rb);
+    int score = 0;
+    for (int i = 0; i < lq; ++i) qq[i] = qseg[i];
+    for (int i = 0; i < rlen; ++i) rr[i] = I->D[rb + i];
+    if (rb >= I->n) { /* reverse both so indels land leftmost in forward coordinates */
+        for (int i = 0; i < lq >> 1; ++i) { uint8_t t = qq[i]; qq[i] = qq[lq - 1 - i]; qq[lq - 1 - i] = t; }
+        for (int i = 0; i < rlen >> 1; ++i) { uint8_t t = rr[i]; rr[i] = rr[rlen - 1 - i]; rr[rlen - 1 - i] = t; }
+    }
+    if (lq == rlen && w_ == 0) {
+        cig[0] = (uint32_t)lq << 4;
+        *n_cig = 1;
+        for (int i = 0; i < lq; ++i) score += sc(p, rr[i], qq[i]);
+    } else {
+        int max_ins = (int)((double)(((lq + 1) >> 1) * p->a - p->o_ins) / p->e_ins + 1.);
+        int max_del = (int)((double)(((lq + 1) >> 1) * p->a - p->o_del) / p->e_del + 1.);
+        int max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        int d = rlen - lq < 0 ? lq - rlen : rlen - lq;
+        int w = (max_gap + d + 1) >> 1;
+        w = w < w_ ? w : w_;
+        int min_w = d + 3;
+        w = w > min_w ? w : min_w;
+        score = global_dp(lq, qq, rlen, rr, p, w, cig, AFO_MAX_CIGAR, n_cig);
+    }
+    return score;
+}
+
+static void align_read(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, rec_t *out) {
+    uint8_t q[AFO_MAX_READ];
+    mem_t *mems = (mem_t *)malloc(sizeof(mem_t) * (p->max_mems > 0 ? p->max_mems : 1));
+    reg_t regs[64];
+    int n_reg = 0, overflow = 0;
+    memset(out, 0, sizeof(*out));
+    out->flag = 0x4;
+    if (l > AFO_MAX_READ) l = AFO_MAX_READ;
+    for (int i = 0; i < l; ++i) q[i] = nt4(ascii[i]);
+    int nm = find_mems(I, q, l, p, mems, &overflow);
+    if (overflow) { out->flag |= FLAG_MEM_OVERFLOW; free(mems); return; }
+    qsort(mems, nm, sizeof(mem_t), cmp_mem);
+    int max_ext = p->max_ext < 64 ? p->max_ext : 64;
+    for (int si = 0; si < nm; ++si) {
+        const mem_t *s = &mems[si];
+        int skip = 0;
+        for (int r = 0; r < n_reg; ++r) {
+            const reg_t *a = &regs[r];
+            if (s->rb < a->rb || s->rb + s->len > a->re || s->qb < a->qb || s->qb + s->len > a->qe) continue;
+            if (10 * (s->len - a->seedlen0) > l) continue;
+            int qd = s->qb - a->qb, rd = s->rb - a->rb;
+            int mg = cal_max_gap(p, qd < rd ? qd : rd);
+            int ww = mg < a->w ? mg : a->w;
+            if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
+            qd = a->qe - (s->qb + s->len); rd = a->re - (s->rb + s->len);
+            mg = cal_max_gap(p, qd < rd ? qd : rd);
+            ww = mg < a->w ? mg : a->w;
+            if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
+        }
+        if (skip) continue;
+        if (n_reg >= max_ext) break;
+        extend_seed(I, q, l, s, p, &regs[n_reg++]);
+    }
+    free(mems);
+    int best = -1;
+    for (int r = 0; r < n_reg; ++r)
+        if (best < 0 || regs[r].score > regs[best].score) best = r;
+    if (best < 0 || regs[best].score < p->T) return;
+    const reg_t *a = &regs[best];
+    int is_rev = a->rb >= I->n;
+    /* forward-read segment; gen_cigar reverses it together with the revcomp-reference
+     * segment for reverse hits (bwa_gen_cigar2), i.e. aligns in forward-ref order */
+    const uint8_t *qseg = q + a->qb;
+    int lq = a->qe - a->qb;
+    int tmp_w = infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_del, p->e_del);
+    int w2 = infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_ins, p->e_ins);
+    w2 = w2 > tmp_w ? w2 : tmp_w;
+    if (w2 > p->w) w2 = w2 < a->w ? w2 : a->w;
+    uint32_t cig[AFO_MAX_CIGAR];
+    int nc = 0, score = 0, last_sc = -(1 << 30), it = 0;
+    do {
+        w2 = w2 < p->w << 2 ? w2 : p->w << 2;
+        score = gen_cigar(I, p, w2, lq, qseg, a->rb, a->re, cig, &nc);
+        if (score == last_sc || w2 == p->w << 2) break;
+        last_sc = score;
+        w2 <<= 1;
+    } while (++it < 3 && score < a->truesc - p->a);
+    int64_t pos = is_rev ? 2 * I->n - a->re : a->rb;
+    int ncap = nc < AFO_MAX_CIGAR ? nc : AFO_MAX_CIGAR;
+    int of = nc > AFO_MAX_CIGAR;
+    /* squeeze out a leading or trailing deletion */
+    if (ncap > 0) {
+        if ((cig[0] & 0xf) == 2) {
+            pos += cig[0] >> 4;
+            memmove(cig, cig + 1, sizeof(uint32_t) * (ncap - 1));
+            --ncap;
+        } else if ((cig[ncap - 1] & 0xf) == 2) {
+            --ncap;
+        }
+    }
+    int clip5 = is_rev ? l - a->qe : a->qb;
+    int clip3 = is_rev ? a->qb : l - a->qe;
+    uint32_t fin[AFO_MAX_CIGAR + 2];
+    int nf = 0;
+    if (clip5) fin[nf++] = (uint32_t)clip5 << 4 | 4;
+    for (int x = 0; x < ncap; ++x) fin[nf++] = cig[x];
+    if (clip3) fin[nf++] = (uint32_t)clip3 << 4 | 4;
+    if (nf > AFO_MAX_CIGAR) { of = 1; nf = AFO_MAX_CIGAR; }
+    memcpy(out->cigar, fin, sizeof(uint32_t) * nf);
+    out->n_cigar = nf;
+    out->flag = (is_rev ? 0x10 : 0) | (of ? FLAG_CIGAR_OVERFLOW : 0);
+    out->pos = (int32_t)pos;
+    out->score = a->score;
+}
+
+int afo_align_pairs(const afo_index *I, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                    const int32_t *lens, const afo_params *p, int n_threads, afo_out *out) {
+    int64_t nr = 2 * n_pairs;
+    rec_t *recs = (rec_t *)malloc(sizeof(rec_t) * (nr > 0 ? nr : 1));
+    if (out->hits) afo_seed_filter(I, reads, nr, stride, lens, out->hits);
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+    for (int64_t r = 0; r < nr; ++r) {
+        int l = lens ? lens[r] : stride;
+        align_read(I, reads + r * (int64_t)stride, l, p, &recs[r]);
+    }
+    /* pair flags (mem_aln2sam conventions): 0x1 paired, 0x40/0x80 mate order, 0x8/0x20 mate
+     * state; an unmapped read with a mapped mate takes the mate's position and strand */
+    for (int64_t pp = 0; pp < n_pairs; ++pp) {
+        for (int m = 0; m < 2; ++m) {
+            rec_t *x = &recs[2 * pp + m], *y = &recs[2 * pp + (m ^ 1)];
+            int64_t r = 2 * pp + m;
+            int xf = x->flag, yf = y->flag;
+            int f = 0x1 | (m ? 0x80 : 0x40) | (xf & ~0x4 & 0x30000);
+            int32_t pos = x->pos;
+            if (!(xf & 0x4)) f |= xf & 0x10;
+            else f |= 0x4;
+            if (yf & 0x4) f |= 0x8;
+            else f |= (yf & 0x10) ? 0x20 : 0;
+            if ((xf & 0x4) && !(yf & 0x4)) { pos = y->pos; f |= (yf & 0x10); }
+            if ((xf & 0x4) && (yf & 0x4)) pos = -1;
+            out->flag[r] = f;
+            out->pos[r] = pos;
+            out->score[r] = x->score;
+            out->n_cigar[r] = (xf & 0x4) ? 0 : x->n_cigar;
+            for (int c = 0; c < AFO_MAX_CIGAR; ++c)
+                out->cigar[r * AFO_MAX_CIGAR + c] = (!(xf & 0x4) && c < x->n_cigar) ? x->cigar[c] : 0;
+        }
+    }
+    free(recs);
+    return 0;
+}

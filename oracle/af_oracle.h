@@ -1,0 +1,64 @@
+/*
+ * af_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the anchored split-read alignment path used
+ * as the parity oracle for the HIP product path in anchored-fusion_amd/csrc.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * What it restates: the reference drives `bwa mem -M` (bwa >= 0.7.17, README.md:18;
+ * third-party, NOT vendored under /root/reference) at Anchored_Fusion.py:182.  bwa is
+ * absent from this image, so this file restates bwa-mem's published algorithm
+ * (Li 2013, arXiv:1303.3997; ksw extension/global DP as published in bwa 0.7.17):
+ * MEM seeds >= 19 nt on the doubled reference (anchor ++ revcomp), per-seed banded
+ * extension with z-drop and clipping penalty, band inference + global DP for CIGAR.
+ * Parity with the bwa binary itself is UNPINNED; the oracle is
+ * pinned by the wgsim truth in the bundled test FASTQ names and the junction known-answers.
+ */
+#ifndef AF_ORACLE_H
+#define AF_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AFO_K 16
+#define AFO_MAX_CIGAR 32
+#define AFO_MAX_READ 512
+
+typedef struct {
+    int32_t a, b;                       /* match score / mismatch penalty (bwa -A -B)      */
+    int32_t o_del, e_del, o_ins, e_ins; /* affine gaps (bwa -O -E)                          */
+    int32_t pen_clip5, pen_clip3;       /* clipping penalty (bwa -L)                        */
+    int32_t w;                          /* band width (bwa -w)                              */
+    int32_t zdrop;                      /* z-drop (bwa -d)                                  */
+    int32_t min_seed_len;               /* bwa -k                                           */
+    int32_t max_occ;                    /* k-mer occurrence cap                             */
+    int32_t T;                          /* min output score (bwa -T)                        */
+    int32_t max_ext;                    /* max seeds extended per read                      */
+    int32_t max_mems;                   /* MEM cap per read (overflow -> unmapped + flag)   */
+} afo_params;
+
+typedef struct {
+    int32_t *flag, *pos, *score, *n_cigar, *hits;
+    uint32_t *cigar; /* [n_reads * AFO_MAX_CIGAR], BAM op encoding len<<4|op */
+} afo_out;
+
+typedef struct afo_index afo_index;
+
+void afo_params_default(afo_params *p);
+afo_index *afo_index_build(const char *anchor, int64_t n);
+void afo_index_free(afo_index *idx);
+int64_t afo_index_len(const afo_index *idx);
+int32_t afo_filter_nbuckets(const afo_index *idx);
+const uint16_t *afo_filter_table(const afo_index *idx);
+/* K1 restatement: per read, number of sampled 16-mers passing the anchor filter */
+void afo_seed_filter(const afo_index *idx, const uint8_t *reads, int64_t n_reads, int32_t stride,
+                     const int32_t *lens, int32_t *hits);
+/* S2 restatement: SE alignment of every read + pair flags (reads pair-major: 2p, 2p+1) */
+int afo_align_pairs(const afo_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                    const int32_t *lens, const afo_params *p, int n_threads, afo_out *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,71 @@
+"""Deterministic read sets shared by the CPU oracle tests and the GPU parity tests."""
+import numpy as np
+
+from anchored_fusion_amd import simulate as sim
+
+
+def _pad(seqs, stride):
+    out = np.full((len(seqs), stride), ord("N"), dtype=np.uint8)
+    lens = np.zeros(len(seqs), dtype=np.int32)
+    for i, s in enumerate(seqs):
+        s = s[:stride]
+        out[i, : len(s)] = np.frombuffer(s, dtype=np.uint8)
+        lens[i] = len(s)
+    return out, lens
+
+
+def edge_pairs(anchor: bytes, read_len=100, seed=7):
+    """Hand-made pairs covering the edge cases of the aligner (returned pair-major)."""
+    rng = np.random.default_rng(seed)
+    n = len(anchor)
+    L = read_len
+    rc = sim.revcomp
+    seqs = []
+    # exact full-length matches at both anchor ends, both strands
+    seqs += [anchor[:L], rc(anchor[n - L:])]
+    seqs += [rc(anchor[:L]), anchor[n - L:]]
+    # split reads: anchor part + random tail (MS) and random head + anchor part (SM)
+    for cut in (20, 31, 45, 60, 75, 85):
+        a = int(rng.integers(200, n - 300))
+        seqs += [anchor[a:a + cut] + sim.random_seq(rng, L - cut), sim.random_seq(rng, L - cut) + anchor[a:a + cut]]
+    # exon-skip-like read (two anchor segments), and its reverse complement
+    a = 1500
+    seqs += [anchor[a:a + 50] + anchor[a + 150:a + 200], rc(anchor[a:a + 55] + anchor[a + 400:a + 445])]
+    # insertions / deletions inside a read
+    a = 3000
+    seqs += [anchor[a:a + 40] + b"GT" + anchor[a + 40:a + L - 2], anchor[a:a + 50] + anchor[a + 53:a + L + 3]]
+    seqs += [rc(anchor[a:a + 30] + b"TTTA" + anchor[a + 30:a + L - 4]), rc(anchor[a:a + 60] + anchor[a + 66:a + L + 6])]
+    # N handling: all-N, single N, N-dense
+    s = bytearray(anchor[4000:4000 + L]); s[50] = ord("N")
+    seqs += [b"N" * L, bytes(s)]
+    s2 = bytearray(anchor[4200:4200 + L])
+    for k in range(0, L, 9):
+        s2[k] = ord("N")
+    seqs += [bytes(s2), anchor[4300:4300 + L].lower()]
+    # low complexity and random
+    seqs += [b"AC" * (L // 2), sim.random_seq(rng, L)]
+    # many mismatches (forces the global DP path)
+    s3 = bytearray(anchor[5000:5000 + L])
+    for k in range(5, L, 11):
+        s3[k] = ord("A") if s3[k] != ord("A") else ord("C")
+    seqs += [bytes(s3), rc(bytes(s3))]
+    if len(seqs) % 2:
+        seqs.append(sim.random_seq(rng, L))
+    return _pad(seqs, L)
+
+
+def synthetic_pairs(anchor: bytes, n_pairs, read_len, seed, err=0.02, indel_frac=0.03, n_rate=0.001, fusion_frac=0.6):
+    _, reads, truth, world = sim.fusion_reads(anchor, n_pairs, read_len=read_len, fusion_frac=fusion_frac, seed=seed,
+                                              err=err, indel_frac=indel_frac, n_rate=n_rate)
+    return reads, truth, world
+
+
+def ragged(reads, seed):
+    """Random per-read lengths in [12, stride] with N padding (exercises the lens path)."""
+    rng = np.random.default_rng(seed)
+    n, stride = reads.shape
+    lens = rng.integers(12, stride + 1, size=n).astype(np.int32)
+    out = reads.copy()
+    for i in range(n):
+        out[i, lens[i]:] = ord("N")
+    return out, lens
