@@ -23,9 +23,11 @@ struct DevIndex {
     const int32_t *hcnt;    //   occurrences (0 = empty slot)
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
     const uint4 *ftab;      // filter buckets: 8 x u16 (slots 0..6 fingerprints, slot 7 overflow)
+    const uint32_t *bitmap; // stage-1 filter: bit (fmix(k) >> (32 - bm_bits)) set for anchor 16-mers
     int64_t n;              // anchor length
     int32_t hbits;          // log2 position-hash slots
     int32_t nb_bits;        // log2 filter buckets
+    int32_t bm_bits;        // log2 bitmap bits
 };
 
 __host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
@@ -40,8 +42,10 @@ struct ReadRec {
 };
 
 // launch helpers (defined in the .hip files)
+// ctrl: [0] candidate count, [1] K2 work counter, [2] K1 tile counter (zeroed per call)
+size_t af_seed_filter_lds(int nb_bits, int bm_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *n_cand,
+                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,
                                  hipStream_t s);
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                            const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,

@@ -7,8 +7,9 @@
 //      L2, right extension by 2-bit word compares),
 //   2. sorts MEMs (len desc, qb, rb) with a wave rank sort in LDS,
 //   3. extends seeds in order (skipping seeds contained in an earlier region) with a
-//      row-parallel banded DP: lanes own contiguous query columns, the horizontal gap chain
-//      is a wave prefix-max scan, row max / band trimming are wave reductions and ballots,
+//      row-parallel banded DP: lanes own contiguous query columns; the horizontal gap chain
+//      is a DPP prefix-max scan, row max / band trimming are DPP scans, ballots and
+//      readlanes (no LDS round trips on the per-row critical path),
 //   4. runs band inference + the global DP with traceback bits in LDS (global scratch for
 //      oversize matrices) to produce the CIGAR of the best region.
 // The recurrences, tie-breaks and band bookkeeping are exactly those of oracle/af_oracle.c.
@@ -16,40 +17,56 @@
 
 namespace {
 
+constexpr int MEMCAP = 64;   // == max allowed af_params.max_mems
+constexpr int ZLDS = 6144;   // traceback bytes per wave kept in LDS
+
 struct __attribute__((aligned(16))) AlnLds {
-    uint64_t mem[256];
-    uint64_t smem[256];
+    uint64_t mem[MEMCAP];
+    uint64_t smem[MEMCAP];
     int32_t regs[16][8];   // score, truesc, qb, qe, rb, re, seedlen0, w
     uint32_t ring[64];     // traceback CIGAR ring
-    int32_t misc[8];       // [0] nmem (total found), [1] work item, [2] n traceback ops
+    int32_t misc[8];       // [0] nmem (total found), [2] n traceback ops
     uint8_t q[AF_MAX_READ + 16];
     uint8_t qs[AF_MAX_READ + 16];
     uint8_t t[1024];
-    uint8_t z[AF_ZCAP];
+    uint8_t z[ZLDS];
 };
 
-__device__ __forceinline__ int scd(const af_params &p, int x, int y) {
-    return (x > 3 || y > 3) ? -1 : (x == y ? p.a : -p.b);
+// ---- wave primitives (DPP; gfx9-family controls) ---------------------------------------
+template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
+__device__ __forceinline__ int dpp(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, BANKM, false);
 }
+constexpr int kNeg = -(1 << 30) - (1 << 29);  // identity for max (below every DP value used)
 
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+// inclusive prefix max over lanes 0..63
+__device__ __forceinline__ int wave_incl_max(int v) {
+    v = max(v, dpp<0x111>(kNeg, v));        // row_shr:1
+    v = max(v, dpp<0x112>(kNeg, v));        // row_shr:2
+    v = max(v, dpp<0x114>(kNeg, v));        // row_shr:4
+    v = max(v, dpp<0x118>(kNeg, v));        // row_shr:8
+    v = max(v, dpp<0x142, 0xa>(kNeg, v));   // row_bcast:15 -> rows 1, 3
+    v = max(v, dpp<0x143, 0xc>(kNeg, v));   // row_bcast:31 -> rows 2, 3
     return v;
 }
+// lane l receives lane l-1's value; lane 0 receives `old`
+__device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }
+__device__ __forceinline__ int bcast(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ int wave_max(int v) { return bcast(wave_incl_max(v), 63); }
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     return v;
 }
-// inclusive prefix max over lanes
-__device__ __forceinline__ int wave_scan_max(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int o = __shfl_up(v, d);
-        if (lane >= d) v = max(v, o);
-    }
-    return v;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int scd(const af_params &p, int x, int y) {
+    return (x > 3 || y > 3) ? -1 : (x == y ? p.a : -p.b);
 }
 
 __device__ __forceinline__ int cal_max_gap(const af_params &p, int qlen) {
@@ -69,17 +86,28 @@ __device__ __forceinline__ int infer_bw(int l1, int l2, int score, int a, int q,
 
 struct ExtRes { int max, qle, tle, gtle, gscore, max_off; };
 
+// select element c (runtime, < CPL) of a register array without scratch
+template <int CPL>
+__device__ __forceinline__ int pick(const int (&a)[CPL], int c) {
+    int v = a[0];
+#pragma unroll
+    for (int x = 1; x < CPL; ++x)
+        if (x == c) v = a[x];
+    return v;
+}
+
 // ksw_extend2 semantics (see oracle ext_dp), row-parallel over query columns.
+template <int CPL>
 __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
                               int end_bonus, int zdrop, int h0, int lane) {
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
     const int cpl = (qlen + 1 + 63) >> 6;
     const int j0 = lane * cpl;
-    int eh_h[AF_CPL], eh_e[AF_CPL], qc[AF_CPL];
+    int eh_h[CPL], eh_e[CPL], qc[CPL];
     {
         const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             int v = 0;
             if (c < cpl && j <= qlen) {
@@ -105,8 +133,11 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     }
     int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
     int beg = 0, end = qlen;
-    const int NEGB = -(1 << 28);
+    const int jq = qlen - 1, lq_lane = jq / cpl, lq_c = jq - lq_lane * cpl;
+    int ti_next = tlen > 0 ? t[0] : 4;
     for (int i = 0; i < tlen; ++i) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
         if (beg < i - w) beg = i - w;
         if (end > i + w + 1) end = i + w + 1;
         if (end > qlen) end = qlen;
@@ -122,29 +153,23 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
             }
             break;
         }
-        const int ti = t[i];
-        int Mv[AF_CPL], bx[AF_CPL], hv[AF_CPL];
-        int run = NEGB;
+        int Mv[CPL], bx[CPL], hv[CPL];
+        int run = kNeg;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             const bool in = c < cpl && j >= beg && j < end;
-            int M = 0;
-            if (in) {
-                const int d = eh_h[c];
-                M = d ? d + scd(p, ti, qc[c]) : 0;
-            }
+            const int d = eh_h[c];
+            const int M = (in && d) ? d + scd(p, ti, qc[c]) : 0;
             Mv[c] = M;
-            bx[c] = run;  // exclusive within lane
+            bx[c] = run;
             const int tk = M - oe_ins > 0 ? M - oe_ins : 0;
             if (in) run = max(run, tk + j * p.e_ins);
         }
-        const int inc = wave_scan_max(run, lane);
-        int lex = __shfl_up(inc, 1);
-        if (lane == 0) lex = NEGB;
+        const int lex = wave_shr1(kNeg, wave_incl_max(run));
         int key = -1;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             const bool in = c < cpl && j >= beg && j < end;
             const int P = max(lex, bx[c]);
@@ -156,7 +181,7 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
             if (in) {
                 int tt = M - oe_del;
                 tt = tt > 0 ? tt : 0;
-                int en = e - p.e_del;
+                const int en = e - p.e_del;
                 eh_e[c] = en > tt ? en : tt;
                 key = max(key, (h << 10) | j);
             }
@@ -164,25 +189,10 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         key = wave_max(key);
         const int m = key < 0 ? 0 : key >> 10;
         const int mj = key < 0 ? -1 : (key & 1023);
-        // H(i, j-1) shift into eh_h; eh_h[beg] = h1s; eh_e[end] = 0
-        int lastv = hv[0];
+        const int hq = bcast(pick<CPL>(hv, lq_c), lq_lane);
+        const int from_left = wave_shr1(0, pick<CPL>(hv, cpl - 1));
 #pragma unroll
-        for (int c = 1; c < AF_CPL; ++c)
-            if (c == cpl - 1) lastv = hv[c];
-        const int from_left = __shfl_up(lastv, 1);
-        // value of H(i, qlen-1) for gscore
-        int hq = 0;
-        {
-            const int jq = qlen - 1;
-            const int ln = jq / cpl, cc = jq - ln * cpl;
-            int sel = hv[0];
-#pragma unroll
-            for (int c = 1; c < AF_CPL; ++c)
-                if (c == cc) sel = hv[c];
-            hq = __shfl(sel, ln);
-        }
-#pragma unroll
-        for (int c = AF_CPL - 1; c >= 0; --c) {
+        for (int c = CPL - 1; c >= 0; --c) {
             const int j = j0 + c;
             if (c < cpl) {
                 const int prevH = c == 0 ? from_left : hv[c > 0 ? c - 1 : 0];
@@ -210,7 +220,7 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         // band trimming on the updated eh over [beg, end]
         int fnz = 1 << 30, lnz = -1;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             if (c < cpl && (eh_h[c] != 0 || eh_e[c] != 0)) {
                 if (j >= beg && j < end) fnz = min(fnz, j);
@@ -219,8 +229,8 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         }
         const uint64_t bf = __ballot(fnz < (1 << 30));
         const uint64_t bl = __ballot(lnz >= 0);
-        const int FNZ = bf ? __shfl(fnz, __ffsll((long long)bf) - 1) : (1 << 30);
-        const int LNZ = bl ? __shfl(lnz, 63 - __clzll((long long)bl)) : -1;
+        const int FNZ = bf ? bcast(fnz, __ffsll((unsigned long long)bf) - 1) : (1 << 30);
+        const int LNZ = bl ? bcast(lnz, 63 - __clzll((unsigned long long)bl)) : -1;
         const int beg_new = FNZ == (1 << 30) ? end : FNZ;
         const int jstar = LNZ >= beg_new ? LNZ : beg_new - 1;
         beg = beg_new;
@@ -232,16 +242,17 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
 }
 
 // ksw_global2 semantics with traceback (see oracle global_dp).  z: n_col*tlen bytes.
-// Returns the score; the CIGAR (forward order) is left in lds.ring / lds.misc[2] (count).
+// Returns the score; the CIGAR (reverse order) is left in L.ring with L.misc[2] ops.
+template <int CPL>
 __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
                               uint8_t *z, AlnLds &L, int lane) {
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
     const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
     const int cpl = (qlen + 1 + 63) >> 6;
     const int j0 = lane * cpl;
-    int eh_h[AF_CPL], eh_e[AF_CPL], qc[AF_CPL];
+    int eh_h[CPL], eh_e[CPL], qc[CPL];
 #pragma unroll
-    for (int c = 0; c < AF_CPL; ++c) {
+    for (int c = 0; c < CPL; ++c) {
         const int j = j0 + c;
         eh_h[c] = AF_NEG_INF;
         eh_e[c] = AF_NEG_INF;
@@ -251,16 +262,18 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         }
         qc[c] = (c < cpl && j < qlen) ? q[j] : 4;
     }
+    int ti_next = tlen > 0 ? t[0] : 4;
     for (int i = 0; i < tlen; ++i) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
         const int beg = i > w ? i - w : 0;
         const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
         const int h1s = beg == 0 ? -(p.o_del + p.e_del * (i + 1)) : AF_NEG_INF;
-        const int ti = t[i];
-        int Mv[AF_CPL], bx[AF_CPL], hv[AF_CPL];
-        int run = AF_NEG_INF + (beg - 1) * p.e_ins;  // the f = -inf chain entering at beg
-        int lane_seed = run;
+        int Mv[CPL], bx[CPL], hv[CPL];
+        const int seed = AF_NEG_INF + (beg - 1) * p.e_ins;  // the f = -inf chain entering at beg
+        int run = seed;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             const bool in = c < cpl && j >= beg && j < end;
             const int m = eh_h[c] + scd(p, ti, qc[c]);
@@ -268,18 +281,16 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
             bx[c] = run;
             if (in) run = max(run, m - oe_ins + j * p.e_ins);
         }
-        const int inc = wave_scan_max(run, lane);
-        int lex = __shfl_up(inc, 1);
-        if (lane == 0) lex = lane_seed;
+        const int lex = wave_shr1(seed, wave_incl_max(run));
         uint8_t *zi = z + (size_t)i * n_col;
 #pragma unroll
-        for (int c = 0; c < AF_CPL; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const int j = j0 + c;
             const bool in = c < cpl && j >= beg && j < end;
             const int P = max(lex, bx[c]);
             const int f = P - (j - 1) * p.e_ins;
             const int m = Mv[c];
-            int e = eh_e[c];
+            const int e = eh_e[c];
             int d = m >= e ? 0 : 1;
             int h = m >= e ? m : e;
             d = h >= f ? d : 2;
@@ -296,13 +307,9 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
                 zi[j - beg] = (uint8_t)d;
             }
         }
-        int lastv = hv[0];
+        const int from_left = wave_shr1(0, pick<CPL>(hv, cpl - 1));
 #pragma unroll
-        for (int c = 1; c < AF_CPL; ++c)
-            if (c == cpl - 1) lastv = hv[c];
-        const int from_left = __shfl_up(lastv, 1);
-#pragma unroll
-        for (int c = AF_CPL - 1; c >= 0; --c) {
+        for (int c = CPL - 1; c >= 0; --c) {
             const int j = j0 + c;
             if (c < cpl) {
                 const int prevH = c == 0 ? from_left : hv[c > 0 ? c - 1 : 0];
@@ -312,19 +319,8 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
             }
         }
     }
-    // score = eh[qlen].h
-    int score;
-    {
-        const int ln = qlen / cpl, cc = qlen - ln * cpl;
-        int sel = eh_h[0];
-#pragma unroll
-        for (int c = 1; c < AF_CPL; ++c)
-            if (c == cc) sel = eh_h[c];
-        score = __shfl(sel, ln);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int score = bcast(pick<CPL>(eh_h, qlen - (qlen / cpl) * cpl), qlen / cpl);
+    wave_sync();
     if (lane == 0) {
         int nc = 0, which = 0;
         int i = tlen - 1;
@@ -343,16 +339,8 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         if (k >= 0) push(1, k + 1);
         L.misc[2] = nc;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
     return score;
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // 16 bases of the packed doubled reference starting at pos, plus its N mask (bit per base)
@@ -368,11 +356,11 @@ __device__ __forceinline__ void getD16(const DevIndex &ix, int64_t pos, uint32_t
 }
 
 // gen_cigar restated (bwa_gen_cigar2): returns score, cigar in L.ring/L.misc[2]
+template <int CPL>
 __device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, int lq, int qb, int64_t rb, int64_t re,
                               AlnLds &L, uint8_t *zg, int lane) {
     const int rlen = (int)(re - rb);
     const bool rev = rb >= ix.n;
-    // stage (possibly reversed) query segment into qs and reference segment into t
     for (int x = lane; x < lq; x += 64) L.qs[x] = rev ? L.q[qb + lq - 1 - x] : L.q[qb + x];
     for (int x = lane; x < rlen; x += 64) L.t[x] = rev ? ix.D[re - 1 - x] : ix.D[rb + x];
     wave_sync();
@@ -394,29 +382,31 @@ __device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, in
         const int min_w = d + 3;
         w = w > min_w ? w : min_w;
         const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
-        uint8_t *z = ((size_t)n_col * rlen <= AF_ZCAP) ? L.z : zg;
-        score = global_dp_wave(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        uint8_t *z = ((size_t)n_col * rlen <= ZLDS) ? L.z : zg;
+        score = global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
     }
     return score;
 }
 
+template <int CPL>
 __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
                                               const int32_t *__restrict__ lens, af_params p,
-                                              const int32_t *__restrict__ cand, const int32_t *__restrict__ n_cand,
+                                              const int32_t *__restrict__ cand, const int32_t *__restrict__ ctrl,
                                               int32_t *__restrict__ work, ReadRec *__restrict__ recs,
                                               uint32_t *__restrict__ cigar, uint8_t *__restrict__ zscratch,
                                               size_t zstride) {
     __shared__ AlnLds L;
     const int lane = threadIdx.x;
-    const int ncand = *n_cand;
+    const int ncand = ctrl[0];
     uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
     const int64_t n = ix.n, n2 = 2 * ix.n;
     const int max_ext = p.max_ext < 16 ? p.max_ext : 16;
-    const int max_mems = p.max_mems < 256 ? p.max_mems : 256;
+    const int max_mems = p.max_mems < MEMCAP ? p.max_mems : MEMCAP;
+    const uint32_t hm = (1u << ix.hbits) - 1u;
     for (;;) {
         int item = 0;
         if (lane == 0) item = atomicAdd(work, 1);
-        item = __shfl(item, 0);
+        item = bcast(item, 0);
         if (item >= ncand) break;
         const int64_t r = cand[item];
         int l = lens ? lens[r] : stride;
@@ -440,13 +430,13 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
         for (int qb = lane; qb + AF_K <= l; qb += 64) {
             uint32_t k = 0;
             bool ok = true;
+#pragma unroll
             for (int u = 0; u < AF_K; ++u) {
                 const int c = L.q[qb + u];
                 ok &= c < 4;
                 k |= (uint32_t)(c & 3) << (2 * u);
             }
             if (!ok) continue;
-            const uint32_t hm = (1u << ix.hbits) - 1u;
             uint32_t s = af_fmix(k) & hm;
             int cnt = 0, st = 0;
             for (;;) {
@@ -482,13 +472,13 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     const uint32_t x = qk ^ dk;
                     const int eq = x ? (__builtin_ctz(x) >> 1) : 16;
                     const int dnf = dn ? __builtin_ctz(dn) : 16;
-                    int step = min(min(eq, room), min(qn, dnf));
+                    const int step = min(min(eq, room), min(qn, dnf));
                     len += step;
                     if (step < 16) break;
                 }
                 if (len < p.min_seed_len) continue;
                 const int slot = atomicAdd(&L.misc[0], 1);
-                if (slot < 256)
+                if (slot < MEMCAP)
                     L.mem[slot] = ((uint64_t)(1023 - len) << 50) | ((uint64_t)qb << 40) | (uint64_t)rb;
             }
         }
@@ -501,8 +491,8 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
         } else {
             const int nm = nm_total;
             // ---- 2. rank sort --------------------------------------------------------
-            for (int a = lane; a < nm; a += 64) {
-                const uint64_t ka = L.mem[a];
+            if (lane < nm) {
+                const uint64_t ka = L.mem[lane];
                 int rank = 0;
                 for (int b = 0; b < nm; ++b) rank += L.mem[b] < ka;
                 L.smem[rank] = ka;
@@ -552,7 +542,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw0 = p.w << it;
-                        er = ext_dp_wave(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
+                        er = ext_dp_wave<CPL>(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
                     }
@@ -576,7 +566,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw1 = p.w << it;
-                        er = ext_dp_wave(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                        er = ext_dp_wave<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
                     }
@@ -614,7 +604,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                 int score = 0, last_sc = -(1 << 30), it = 0;
                 do {
                     w2 = w2 < p.w << 2 ? w2 : p.w << 2;
-                    score = gen_cigar_wave(ix, p, w2, lq, aqb, arb, are, L, zg, lane);
+                    score = gen_cigar_wave<CPL>(ix, p, w2, lq, aqb, arb, are, L, zg, lane);
                     if (score == last_sc || w2 == p.w << 2) break;
                     last_sc = score;
                     w2 <<= 1;
@@ -624,31 +614,27 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     const int nc = L.misc[2];
                     const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
                     bool of = nc > AF_MAX_CIGAR;
-                    uint32_t cg[AF_MAX_CIGAR + 2];
-                    const bool ungapped = (nc == 1 && L.ring[0] == ((uint32_t)lq << 4));
-                    for (int x = 0; x < ncap; ++x) cg[x] = ungapped ? L.ring[0] : L.ring[(nc - 1 - x) & 63];
-                    int nn = ncap;
+                    uint32_t *co = cigar + r * AF_MAX_CIGAR;
                     int64_t pos = is_rev ? n2 - are : arb;
-                    if (nn > 0) {
-                        if ((cg[0] & 0xf) == 2) {
-                            pos += cg[0] >> 4;
-                            for (int x = 0; x + 1 < nn; ++x) cg[x] = cg[x + 1];
-                            --nn;
-                        } else if ((cg[nn - 1] & 0xf) == 2) {
-                            --nn;
-                        }
+                    int xs = 0, xe = ncap;  // window of ring entries (forward order)
+                    const uint32_t first = L.ring[(nc - 1) & 63];
+                    const uint32_t last = L.ring[(nc - ncap) & 63];
+                    if (ncap > 0) {
+                        if ((first & 0xf) == 2) { pos += first >> 4; xs = 1; }
+                        else if ((last & 0xf) == 2) xe = ncap - 1;
                     }
                     const int clip5 = is_rev ? l - aqe : aqb;
                     const int clip3 = is_rev ? aqb : l - aqe;
-                    uint32_t *co = cigar + r * AF_MAX_CIGAR;
                     int nf = 0;
-                    auto put = [&](uint32_t v) {
-                        if (nf < AF_MAX_CIGAR) co[nf] = v;
+                    if (clip5) { co[nf++] = (uint32_t)clip5 << 4 | 4; }
+                    for (int x = xs; x < xe; ++x) {
+                        if (nf < AF_MAX_CIGAR) co[nf] = L.ring[(nc - 1 - x) & 63];
                         ++nf;
-                    };
-                    if (clip5) put((uint32_t)clip5 << 4 | 4);
-                    for (int x = 0; x < nn; ++x) put(cg[x]);
-                    if (clip3) put((uint32_t)clip3 << 4 | 4);
+                    }
+                    if (clip3) {
+                        if (nf < AF_MAX_CIGAR) co[nf] = (uint32_t)clip3 << 4 | 4;
+                        ++nf;
+                    }
                     if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
                     flag = (is_rev ? 0x10 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
                     out_pos = (int)pos;
@@ -700,17 +686,24 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
 }  // namespace
 
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
+                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *ctrl,
                            int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
                            hipStream_t s) {
     (void)n_reads; (void)cand_cap;
-    // work counter lives right after n_cand (see api.hip scratch layout)
-    int32_t *work = const_cast<int32_t *>(n_cand) + 1;
+    int32_t *work = const_cast<int32_t *>(ctrl) + 1;
     hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
-    hipLaunchKernelGGL(k_align, dim3(n_slots), dim3(64), 0, s, ix, reads, stride, lens, p, cand, n_cand, work, recs,
-                       cigar, zscratch, zstride);
+    const int cpl = (stride + 1 + 63) / 64;
+    dim3 g(n_slots), b(64);
+    if (cpl <= 2)
+        hipLaunchKernelGGL(k_align<2>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+    else if (cpl <= 3)
+        hipLaunchKernelGGL(k_align<3>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+    else if (cpl <= 4)
+        hipLaunchKernelGGL(k_align<4>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+    else
+        hipLaunchKernelGGL(k_align<AF_CPL>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
     return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 
 struct af_ctx {
     int device = 0;
+    int n_cu = 0;
     int n_slots = 0;
     std::string err;
     // scratch (device)
@@ -34,7 +35,7 @@ struct af_index {
     af_ctx *ctx = nullptr;
     DevIndex dev{};
     std::vector<uint16_t> ftab_host;
-    void *allocs[8] = {};
+    void *allocs[16] = {};
     int n_allocs = 0;
 };
 
@@ -102,9 +103,9 @@ int ensure_zscratch(af_ctx *c) {
 int check_params(af_ctx *c, const af_params *p) {
     if (!p) return fail(c, AF_E_INVALID, "params is NULL");
     if (p->a <= 0 || p->b < 0 || p->o_del < 0 || p->e_del <= 0 || p->o_ins < 0 || p->e_ins <= 0 || p->w < 0 ||
-        p->min_seed_len < AF_K || p->max_ext < 1 || p->max_ext > 16 || p->max_mems < 1 || p->max_mems > 256 ||
+        p->min_seed_len < AF_K || p->max_ext < 1 || p->max_ext > 16 || p->max_mems < 1 || p->max_mems > 64 ||
         p->max_occ < 1)
-        return fail(c, AF_E_INVALID, "invalid af_params (min_seed_len>=%d, 1<=max_ext<=16, 1<=max_mems<=256)", AF_K);
+        return fail(c, AF_E_INVALID, "invalid af_params (min_seed_len>=%d, 1<=max_ext<=16, 1<=max_mems<=64)", AF_K);
     return AF_OK;
 }
 
@@ -116,7 +117,7 @@ void af_params_default(af_params *p) {
     // bwa mem defaults (bwa 0.7.17 usage text): -A1 -B4 -O6 -E1 -L5 -w100 -d100 -k19 -T30
     p->a = 1; p->b = 4; p->o_del = 6; p->e_del = 1; p->o_ins = 6; p->e_ins = 1;
     p->pen_clip5 = 5; p->pen_clip3 = 5; p->w = 100; p->zdrop = 100;
-    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 256;
+    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 64;
 }
 
 int af_ctx_create(int device, af_ctx **out) {
@@ -131,7 +132,8 @@ int af_ctx_create(int device, af_ctx **out) {
     c->device = device;
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    c->n_slots = std::max(1, cus) * 8;
+    c->n_cu = std::max(1, cus);
+    c->n_slots = c->n_cu * 16;  // k_align: 4 waves per SIMD (VGPR and LDS budget)
     if (hipMalloc(&c->ctrl, 64) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         af_free(c->ctrl);
@@ -227,6 +229,14 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
             b = (b + 1) & (nb - 1);
         }
     }
+    // stage-1 bitmap: as many bits as fit beside the table in 160 KiB of LDS (<= 2^19)
+    int bm_bits = 19;
+    while (bm_bits > 10 && af_seed_filter_lds(nb_bits, bm_bits) > 160 * 1024) --bm_bits;
+    std::vector<uint32_t> bitmap((size_t)1 << (bm_bits - 5), 0);
+    for (int64_t i = 0; i < nd; ++i) {
+        const uint32_t bi = af_fmix(keys[i]) >> (32 - bm_bits);
+        bitmap[bi >> 5] |= 1u << (bi & 31);
+    }
     af_index *ix = new (std::nothrow) af_index;
     if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
     ix->ctx = c;
@@ -236,7 +246,8 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     if ((rc = dev_upload(c, ix, D, &ix->dev.D)) || (rc = dev_upload(c, ix, D2, &ix->dev.D2)) ||
         (rc = dev_upload(c, ix, Dn, &ix->dev.Dn)) || (rc = dev_upload(c, ix, hkey, &ix->dev.hkey)) ||
         (rc = dev_upload(c, ix, hstart, &ix->dev.hstart)) || (rc = dev_upload(c, ix, hcnt, &ix->dev.hcnt)) ||
-        (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, ft, &ftd))) {
+        (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, ft, &ftd)) ||
+        (rc = dev_upload(c, ix, bitmap, &ix->dev.bitmap))) {
         af_index_free(ix);
         return rc;
     }
@@ -244,6 +255,7 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     ix->dev.n = n;
     ix->dev.hbits = hbits;
     ix->dev.nb_bits = nb_bits;
+    ix->dev.bm_bits = bm_bits;
     *out = ix;
     return AF_OK;
 }
@@ -275,7 +287,7 @@ int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
     int rc = ensure_reads_cap(c, n_reads);
     if (rc) return rc;
     HIPCHK(c, hipMemsetAsync(c->ctrl, 0, 64, s));
-    HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand, c->ctrl, s));
+    HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand, c->ctrl, c->n_cu, s));
     return AF_OK;
 }
 

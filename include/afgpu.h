@@ -60,8 +60,8 @@ typedef struct {
     int32_t min_seed_len;               /* -k    */
     int32_t max_occ;                    /* k-mer occurrence cap */
     int32_t T;                          /* -T    */
-    int32_t max_ext;                    /* seeds extended per read (<= 64) */
-    int32_t max_mems;                   /* MEM cap per read (<= 256) */
+    int32_t max_ext;                    /* seeds extended per read (<= 16) */
+    int32_t max_mems;                   /* MEM cap per read (<= 64; more -> unmapped + AF_FLAG_MEM_OVERFLOW) */
 } af_params;
 
 typedef struct {

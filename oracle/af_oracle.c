@@ -42,7 +42,7 @@ void afo_params_default(afo_params *p) {
     /* bwa mem defaults (bwa 0.7.17 `bwa mem` usage text) */
     p->a = 1; p->b = 4; p->o_del = 6; p->e_del = 1; p->o_ins = 6; p->e_ins = 1;
     p->pen_clip5 = 5; p->pen_clip3 = 5; p->w = 100; p->zdrop = 100;
-    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 256;
+    p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 64;
 }
 
 /* filter hash: bijective 32-bit mix; bucket = top bits, fingerprint = bits 4..18 | 0x8000 */
@@ -140,7 +140,9 @@ static int filter_query(const afo_index *I, uint32_t k) {
 }
 
 /* K1 semantics: sampled positions are those whose byte offset in the read buffer is a
- * multiple of 4; any MEM >= 19 nt contains such a 16-mer, so hits==0 => no seed. */
+ * multiple of 4; any MEM >= 19 nt contains such a 16-mer, so hits==0 => no seed.  Bytes are
+ * projected to 2 bits by ((c >> 1) ^ (c >> 2)) & 3 (exact for ACGT/acgt; other bytes land on
+ * some code, which can only add hits -- MEMs never contain N, so the superset property holds). */
 void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, int32_t stride,
                      const int32_t *lens, int32_t *hits) {
     for (int64_t r = 0; r < n_reads; ++r) {
@@ -149,10 +151,11 @@ void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, 
         int32_t h = 0;
         int32_t i0 = (int32_t)((4 - (base & 3)) & 3);
         for (int32_t i = i0; i + AFO_K <= l; i += 4) {
-            uint8_t c[AFO_K];
-            for (int j = 0; j < AFO_K; ++j) c[j] = nt4(reads[base + i + j]);
-            uint32_t k;
-            if (!pack16(c, &k)) continue;
+            uint32_t k = 0;
+            for (int j = 0; j < AFO_K; ++j) {
+                const uint8_t c = reads[base + i + j];
+                k |= (uint32_t)(((c >> 1) ^ (c >> 2)) & 3) << (2 * j);
+            }
             h += filter_query(I, k);
         }
         hits[r] = h;
