@@ -229,9 +229,11 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
             b = (b + 1) & (nb - 1);
         }
     }
-    // stage-1 bitmap: as many bits as fit beside the table in 160 KiB of LDS (<= 2^19)
-    int bm_bits = 19;
-    while (bm_bits > 10 && af_seed_filter_lds(nb_bits, bm_bits) > 160 * 1024) --bm_bits;
+    // stage-1 bitmap: 2^19 bits beside a <= 4096-bucket table, 2^16 beside 8192 buckets
+    // (what fits in 160 KiB of LDS; the oracle restates the same rule)
+    const int bm_bits = nb_bits <= 12 ? 19 : 16;
+    if (af_seed_filter_lds(nb_bits, bm_bits) > 160 * 1024)
+        return fail(c, AF_E_UNSUPPORTED, "seed-filter LDS image exceeds 160 KiB");
     std::vector<uint32_t> bitmap((size_t)1 << (bm_bits - 5), 0);
     for (int64_t i = 0; i < nd; ++i) {
         const uint32_t bi = af_fmix(keys[i]) >> (32 - bm_bits);

@@ -25,6 +25,8 @@ struct afo_index {
     int32_t nb;         /* filter buckets (power of two)                    */
     int32_t nb_bits;
     uint16_t *ftab;     /* nb * 8 halfwords; slot 7 = overflow flag         */
+    int32_t bm_bits;    /* stage-1 bitmap: 19 bits (<= 4096 buckets) else 16 */
+    uint32_t *bitmap;
 };
 
 /* ---- encoding ---------------------------------------------------------------------- */
@@ -114,20 +116,30 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
             b = (b + 1) & (uint32_t)(I->nb - 1);
         }
     }
+    /* stage-1 bitmap of the same keys, indexed by the top bm_bits of fmix(k) */
+    I->bm_bits = I->nb_bits <= 12 ? 19 : 16;
+    I->bitmap = (uint32_t *)calloc((size_t)1 << (I->bm_bits - 5), sizeof(uint32_t));
+    for (int64_t i = 0; i < m; ++i) {
+        uint32_t bi = fmix(I->kmer[i]) >> (32 - I->bm_bits);
+        I->bitmap[bi >> 5] |= 1u << (bi & 31);
+    }
     free(tmp);
     return I;
 }
 
 void afo_index_free(afo_index *I) {
     if (!I) return;
-    free(I->D); free(I->kmer); free(I->kpos); free(I->ftab); free(I);
+    free(I->D); free(I->kmer); free(I->kpos); free(I->ftab); free(I->bitmap); free(I);
 }
 int64_t afo_index_len(const afo_index *I) { return I->n; }
 int32_t afo_filter_nbuckets(const afo_index *I) { return I->nb; }
 const uint16_t *afo_filter_table(const afo_index *I) { return I->ftab; }
 
+/* a sampled 16-mer is a hit when it passes the stage-1 bitmap AND the fingerprint table */
 static int filter_query(const afo_index *I, uint32_t k) {
     uint32_t h = fmix(k);
+    uint32_t bi = h >> (32 - I->bm_bits);
+    if (!((I->bitmap[bi >> 5] >> (bi & 31)) & 1u)) return 0;
     uint32_t b = h >> (32 - I->nb_bits);
     uint16_t f = ffp(h);
     for (;;) {
