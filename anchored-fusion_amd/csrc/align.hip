@@ -406,7 +406,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
     for (;;) {
         int item = 0;
         if (lane == 0) item = atomicAdd(work, 1);
-        item = bcast(item, 0);
+        item = __builtin_amdgcn_readfirstlane(item);
         if (item >= ncand) break;
         const int64_t r = cand[item];
         int l = lens ? lens[r] : stride;

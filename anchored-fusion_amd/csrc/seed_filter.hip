@@ -2,10 +2,10 @@
 // pass of `bwa mem` at Anchored_Fusion.py:182).
 //
 // Layout and schedule:
-//  * persistent grid, one 1024-thread workgroup per CU; each of its 16 waves pulls tiles of
-//    AF_SEED_TILE whole reads from a device work counter;
+//  * persistent grid, one 1024-thread workgroup per CU; its 16 waves take tiles of
+//    AF_SEED_TILE whole reads round-robin;
 //  * a tile is streamed as rounds of 64 x 16-byte chunks (lane l loads chunk l: one fully
-//    coalesced 1-KiB global_load_dwordx4 per round) with two rounds of loads in flight;
+//    coalesced 1-KiB global_load_dwordx4 per round), unrolled x3 with two rounds in flight;
 //  * ASCII -> 2-bit codes by SWAR ((c>>1)^(c>>2))&3, 4 bases per byte; each lane forms the
 //    four 16-mers starting at its 4-byte-aligned offsets, borrowing the next lane's packed
 //    chunk through a shuffle (lane 63 uses the first chunk of the next round);
@@ -111,6 +111,36 @@ __device__ __forceinline__ void drain(const uint4 *tab, int nb_bits, const uint3
     }
 }
 
+// One round: chunk c = r*64 + lane (packed P), lane 63's right neighbour packed Px.
+template <bool HAS_LENS>
+__device__ __forceinline__ void scan_round(uint32_t P, uint32_t Px, int c, bool in, int lane, int bsh,
+                                           const uint32_t *bm, const uint4 *tab, int nb_bits, uint32_t *qk,
+                                           uint32_t *qo, int &qn, int32_t stride, const int32_t *lens, int64_t r0,
+                                           uint32_t *cnt) {
+    uint32_t Pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x130, 0xf, 0xf, false);  // wave_shl:1
+    if (lane == 63) Pn = Px;
+    const uint64_t PP = ((uint64_t)Pn << 32) | P;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t k = (uint32_t)(PP >> (8 * j));
+        const uint32_t bi = af_fmix(k) >> bsh;
+        const bool pass = in && ((bm[bi >> 5] >> (bi & 31)) & 1u);
+        const uint64_t m = __ballot(pass);
+        if (m) {
+            if (pass) {
+                const int pos = qn + (int)__popcll(m & ((1ull << lane) - 1ull));
+                qk[pos] = k;
+                qo[pos] = (uint32_t)(c * 16 + 4 * j);
+            }
+            qn += (int)__popcll(m);
+            if (qn >= 64) {
+                drain<HAS_LENS>(tab, nb_bits, qk, qo, qn - 64, qn, lane, stride, lens, r0, cnt);
+                qn -= 64;
+            }
+        }
+    }
+}
+
 template <bool HAS_LENS>
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const int32_t *__restrict__ lens,
@@ -122,7 +152,8 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     uint4 *tab = reinterpret_cast<uint4 *>(smem);
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem + (size_t)nb * 16);
     unsigned char *wbase = smem + (size_t)nb * 16 + (size_t)bmw * 4;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
     uint32_t *cnt = reinterpret_cast<uint32_t *>(wbase + (size_t)wv * (AF_SEED_TILE + QCAP * 8));
     uint32_t *qk = cnt + AF_SEED_TILE / 4;
     uint32_t *qo = qk + QCAP;
@@ -132,52 +163,57 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
 
     const int64_t ntiles = (n_reads + AF_SEED_TILE - 1) / AF_SEED_TILE;
     const int bsh = 32 - bm_bits;
-    for (;;) {
-        int tile = 0;
-        if (lane == 0) tile = atomicAdd(&ctrl[2], 1);
-        tile = __shfl(tile, 0);
-        if (tile >= ntiles) break;
-        const int64_t r0 = (int64_t)tile * AF_SEED_TILE;
-        const int nr = (int)min((int64_t)AF_SEED_TILE, n_reads - r0);
+    const int64_t nwaves = (int64_t)gridDim.x * AF_SEED_WAVES;
+    // static round-robin tiles (uniform work per tile; no contended dequeue word)
+    for (int64_t tile = (int64_t)blockIdx.x * AF_SEED_WAVES + wv; tile < ntiles; tile += nwaves) {
+        const int64_t r0 = tile * AF_SEED_TILE;
+        const int nr = __builtin_amdgcn_readfirstlane((int)min((int64_t)AF_SEED_TILE, n_reads - r0));
         cnt[lane] = 0;  // AF_SEED_TILE / 4 == 64 counter words
         TileGeo g;
         g.base = reads + r0 * (int64_t)stride;
         g.bytes = (int64_t)nr * stride;
-        g.nfull = (int)(g.bytes >> 4);
-        g.nchunks = (int)((g.bytes + 15) >> 4);
+        // readfirstlane: make the tile geometry provably uniform (scalar loop control)
+        g.nfull = __builtin_amdgcn_readfirstlane((int)(g.bytes >> 4));
+        g.nchunks = __builtin_amdgcn_readfirstlane((int)((g.bytes + 15) >> 4));
         g.nround = (g.nchunks + 63) >> 6;
         int qn = 0;
-        uint4 va = load_round(g, 0, lane), xa = load_next(g, 0);
-        uint4 vb = load_round(g, 1, lane), xb = load_next(g, 1);
-        for (int r = 0; r < g.nround; ++r) {
-            const uint4 vc = load_round(g, r + 2, lane), xc = load_next(g, r + 2);
-            const uint32_t P = pack_chunk(va);
-            const uint32_t Px = pack_chunk(xa);
-            uint32_t Pn = __shfl_down(P, 1);
-            if (lane == 63) Pn = Px;
-            const int c = r * 64 + lane;
-            const bool in = c < g.nchunks;
-            const uint64_t PP = ((uint64_t)Pn << 32) | P;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = (uint32_t)(PP >> (8 * j));
-                const uint32_t bi = af_fmix(k) >> bsh;
-                const bool pass = in && ((bm[bi >> 5] >> (bi & 31)) & 1u);
-                const uint64_t m = __ballot(pass);
-                if (m) {
-                    if (pass) {
-                        const int pos = qn + (int)__popcll(m & ((1ull << lane) - 1ull));
-                        qk[pos] = k;
-                        qo[pos] = (uint32_t)(c * 16 + 4 * j);
-                    }
-                    qn += (int)__popcll(m);
-                    if (qn >= 64) {
-                        drain<HAS_LENS>(tab, nb_bits, qk, qo, qn - 64, qn, lane, stride, lens, r0, cnt);
-                        qn -= 64;
-                    }
-                }
+        if (g.nfull == g.nchunks) {
+            // every chunk is whole: branch-free loads, addresses clamped into the tile
+            // (clamped lanes are masked by `in`; a clamped neighbour only feeds 16-mers that
+            // cross the tile end, which drain() rejects)
+            const uint4 *cb = reinterpret_cast<const uint4 *>(g.base);
+            const int last = g.nfull - 1;
+            // three named round buffers, unrolled by 3: each load lands directly in the
+            // registers consumed two rounds later (no register moves of in-flight loads)
+            uint4 vA = cb[min(lane, last)], xA = cb[min(64, last)];
+            uint4 vB = cb[min(64 + lane, last)], xB = cb[min(128, last)];
+            uint4 vC = cb[min(128 + lane, last)], xC = cb[min(192, last)];
+            for (int r = 0; r < g.nround; r += 3) {
+                // refill loads are unconditional (clamped) so every path leaves the same
+                // number of loads in flight and the waits stay counted (vmcnt(4), not 0)
+                scan_round<HAS_LENS>(pack_chunk(vA), pack_chunk(xA), r * 64 + lane, r * 64 + lane < g.nchunks, lane,
+                                     bsh, bm, tab, nb_bits, qk, qo, qn, stride, lens, r0, cnt);
+                vA = cb[min((r + 3) * 64 + lane, last)];
+                xA = cb[min((r + 4) * 64, last)];
+                if (r + 1 < g.nround)
+                    scan_round<HAS_LENS>(pack_chunk(vB), pack_chunk(xB), (r + 1) * 64 + lane,
+                                         (r + 1) * 64 + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
+                                         stride, lens, r0, cnt);
+                vB = cb[min((r + 4) * 64 + lane, last)];
+                xB = cb[min((r + 5) * 64, last)];
+                if (r + 2 < g.nround)
+                    scan_round<HAS_LENS>(pack_chunk(vC), pack_chunk(xC), (r + 2) * 64 + lane,
+                                         (r + 2) * 64 + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
+                                         stride, lens, r0, cnt);
+                vC = cb[min((r + 5) * 64 + lane, last)];
+                xC = cb[min((r + 6) * 64, last)];
             }
-            va = vb; xa = xb; vb = vc; xb = xc;
+        } else {
+            for (int r = 0; r < g.nround; ++r) {
+                const int c = r * 64 + lane;
+                scan_round<HAS_LENS>(pack_chunk(load_round(g, r, lane)), pack_chunk(load_next(g, r)), c,
+                                     c < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn, stride, lens, r0, cnt);
+            }
         }
         if (qn > 0) drain<HAS_LENS>(tab, nb_bits, qk, qo, 0, qn, lane, stride, lens, r0, cnt);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
