@@ -2,10 +2,10 @@
 // pass of `bwa mem` at Anchored_Fusion.py:182).
 //
 // Layout and schedule:
-//  * persistent grid, one 1024-thread workgroup per CU; its 16 waves take tiles of
-//    AF_SEED_TILE whole reads round-robin;
-//  * a tile is streamed as rounds of 64 x 16-byte chunks (lane l loads chunk l: one fully
-//    coalesced 1-KiB global_load_dwordx4 per round), unrolled x3 with two rounds in flight;
+//  * persistent grid, one 1024-thread workgroup per CU, block tiles of AF_SEED_BTILE whole
+//    reads taken round-robin; the 16 waves sweep a tile together, 16 KiB contiguous per
+//    round (lane l of wave w loads one 16-byte chunk: a coalesced 1-KiB dwordx4 per wave),
+//    unrolled x3 with two rounds of loads in flight;
 //  * ASCII -> 2-bit codes by SWAR ((c>>1)^(c>>2))&3, 4 bases per byte; each lane forms the
 //    four 16-mers starting at its 4-byte-aligned offsets, borrowing the next lane's packed
 //    chunk through a shuffle (lane 63 uses the first chunk of the next round);
@@ -75,26 +75,6 @@ struct TileGeo {
     int nfull, nchunks, nround;
 };
 
-// round r: chunk r*64 + lane
-__device__ __forceinline__ uint4 load_round(const TileGeo &g, int r, int lane) {
-    const uint4 nf = make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu);
-    if (r >= g.nround) return nf;
-    const int c = r * 64 + lane;
-    if (r * 64 + 64 <= g.nfull) return *reinterpret_cast<const uint4 *>(g.base + 16 * (int64_t)c);
-    if (c < g.nfull) return *reinterpret_cast<const uint4 *>(g.base + 16 * (int64_t)c);
-    if (c < g.nchunks) return load_tail(g.base, c, g.bytes);
-    return nf;
-}
-
-// the chunk after round r (lane 63's right neighbour); wave-uniform address
-__device__ __forceinline__ uint4 load_next(const TileGeo &g, int r) {
-    const uint4 nf = make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu);
-    const int c = (r + 1) * 64;
-    if (r >= g.nround || c >= g.nchunks) return nf;
-    if (c < g.nfull) return *reinterpret_cast<const uint4 *>(g.base + 16 * (int64_t)c);
-    return load_tail(g.base, c, g.bytes);
-}
-
 template <bool HAS_LENS>
 __device__ __forceinline__ void drain(const uint4 *tab, int nb_bits, const uint32_t *qk, const uint32_t *qo, int lo,
                                       int hi, int lane, int32_t stride, const int32_t *lens, int64_t r0,
@@ -111,7 +91,20 @@ __device__ __forceinline__ void drain(const uint4 *tab, int nb_bits, const uint3
     }
 }
 
-// One round: chunk c = r*64 + lane (packed P), lane 63's right neighbour packed Px.
+// copies n uint4 from global to LDS with the whole workgroup, 8 loads in flight per thread
+__device__ __forceinline__ void fill_lds(uint4 *dst, const uint4 *__restrict__ src, int n) {
+    int i0 = 0;
+    for (; i0 + 8 * 1024 <= n; i0 += 8 * 1024) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[i0 + u * 1024 + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dst[i0 + u * 1024 + threadIdx.x] = v[u];
+    }
+    for (int i = i0 + (int)threadIdx.x; i < n; i += 1024) dst[i] = src[i];
+}
+
+// One round of a wave: chunk c (packed P), the chunk right after lane 63's (packed Px).
 template <bool HAS_LENS>
 __device__ __forceinline__ void scan_round(uint32_t P, uint32_t Px, int c, bool in, int lane, int bsh,
                                            const uint32_t *bm, const uint4 *tab, int nb_bits, uint32_t *qk,
@@ -141,6 +134,9 @@ __device__ __forceinline__ void scan_round(uint32_t P, uint32_t Px, int c, bool 
     }
 }
 
+// Block tile = AF_SEED_BTILE whole reads, swept by the 16 waves together: in round r wave w
+// loads chunk block (r * 16 + w), i.e. the workgroup streams 16 KiB of contiguous bytes per
+// round (DRAM row locality), while each wave still owns 64 consecutive chunks.
 template <bool HAS_LENS>
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const int32_t *__restrict__ lens,
@@ -151,73 +147,84 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const int bmw = 1 << (bm_bits - 5);
     uint4 *tab = reinterpret_cast<uint4 *>(smem);
     uint32_t *bm = reinterpret_cast<uint32_t *>(smem + (size_t)nb * 16);
-    unsigned char *wbase = smem + (size_t)nb * 16 + (size_t)bmw * 4;
+    uint32_t *cnt = bm + bmw;                       // AF_SEED_BTILE 8-bit counters
+    uint32_t *qbase = cnt + AF_SEED_BTILE / 4;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(wbase + (size_t)wv * (AF_SEED_TILE + QCAP * 8));
-    uint32_t *qk = cnt + AF_SEED_TILE / 4;
+    uint32_t *qk = qbase + wv * 2 * QCAP;
     uint32_t *qo = qk + QCAP;
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) tab[i] = ftab[i];
-    for (int i = threadIdx.x; i < bmw; i += blockDim.x) bm[i] = bitmap[i];
-    __syncthreads();
-
-    const int64_t ntiles = (n_reads + AF_SEED_TILE - 1) / AF_SEED_TILE;
+    {   // table + bitmap fill (uint4), loads batched ahead of the LDS stores
+        const uint4 *bm4 = reinterpret_cast<const uint4 *>(bitmap);
+        uint4 *bml = reinterpret_cast<uint4 *>(bm);
+        const int n4 = bmw / 4;
+        fill_lds(tab, ftab, nb);
+        fill_lds(bml, bm4, n4);
+    }
+    const int64_t ntiles = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     const int bsh = 32 - bm_bits;
-    const int64_t nwaves = (int64_t)gridDim.x * AF_SEED_WAVES;
-    // static round-robin tiles (uniform work per tile; no contended dequeue word)
-    for (int64_t tile = (int64_t)blockIdx.x * AF_SEED_WAVES + wv; tile < ntiles; tile += nwaves) {
-        const int64_t r0 = tile * AF_SEED_TILE;
-        const int nr = __builtin_amdgcn_readfirstlane((int)min((int64_t)AF_SEED_TILE, n_reads - r0));
-        cnt[lane] = 0;  // AF_SEED_TILE / 4 == 64 counter words
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * AF_SEED_BTILE;
+        const int nr = __builtin_amdgcn_readfirstlane((int)min((int64_t)AF_SEED_BTILE, n_reads - r0));
+        for (int i = threadIdx.x; i < AF_SEED_BTILE / 4; i += blockDim.x) cnt[i] = 0;
+        __syncthreads();
         TileGeo g;
         g.base = reads + r0 * (int64_t)stride;
         g.bytes = (int64_t)nr * stride;
-        // readfirstlane: make the tile geometry provably uniform (scalar loop control)
         g.nfull = __builtin_amdgcn_readfirstlane((int)(g.bytes >> 4));
         g.nchunks = __builtin_amdgcn_readfirstlane((int)((g.bytes + 15) >> 4));
-        g.nround = (g.nchunks + 63) >> 6;
+        const int nblk = (g.nchunks + 63) >> 6;                      // 64-chunk blocks in the tile
+        const int nround = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of this wave
         int qn = 0;
         if (g.nfull == g.nchunks) {
-            // every chunk is whole: branch-free loads, addresses clamped into the tile
-            // (clamped lanes are masked by `in`; a clamped neighbour only feeds 16-mers that
-            // cross the tile end, which drain() rejects)
+            // every chunk is whole: branch-free loads, addresses clamped into the tile (clamped
+            // lanes are masked by `in`; a clamped neighbour only feeds 16-mers that cross the
+            // tile end, which drain() rejects).  Three named round buffers, unrolled by 3, so
+            // each load lands in the registers consumed two rounds later.
             const uint4 *cb = reinterpret_cast<const uint4 *>(g.base);
             const int last = g.nfull - 1;
-            // three named round buffers, unrolled by 3: each load lands directly in the
-            // registers consumed two rounds later (no register moves of in-flight loads)
-            uint4 vA = cb[min(lane, last)], xA = cb[min(64, last)];
-            uint4 vB = cb[min(64 + lane, last)], xB = cb[min(128, last)];
-            uint4 vC = cb[min(128 + lane, last)], xC = cb[min(192, last)];
-            for (int r = 0; r < g.nround; r += 3) {
-                // refill loads are unconditional (clamped) so every path leaves the same
-                // number of loads in flight and the waits stay counted (vmcnt(4), not 0)
-                scan_round<HAS_LENS>(pack_chunk(vA), pack_chunk(xA), r * 64 + lane, r * 64 + lane < g.nchunks, lane,
-                                     bsh, bm, tab, nb_bits, qk, qo, qn, stride, lens, r0, cnt);
-                vA = cb[min((r + 3) * 64 + lane, last)];
-                xA = cb[min((r + 4) * 64, last)];
-                if (r + 1 < g.nround)
-                    scan_round<HAS_LENS>(pack_chunk(vB), pack_chunk(xB), (r + 1) * 64 + lane,
-                                         (r + 1) * 64 + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
+#define AF_CH(rr) ((((rr) * AF_SEED_WAVES + wv) << 6))
+            uint4 vA = cb[min(AF_CH(0) + lane, last)], xA = cb[min(AF_CH(0) + 64, last)];
+            uint4 vB = cb[min(AF_CH(1) + lane, last)], xB = cb[min(AF_CH(1) + 64, last)];
+            uint4 vC = cb[min(AF_CH(2) + lane, last)], xC = cb[min(AF_CH(2) + 64, last)];
+            for (int r = 0; r < nround; r += 3) {
+                scan_round<HAS_LENS>(pack_chunk(vA), pack_chunk(xA), AF_CH(r) + lane, AF_CH(r) + lane < g.nchunks,
+                                     lane, bsh, bm, tab, nb_bits, qk, qo, qn, stride, lens, r0, cnt);
+                vA = cb[min(AF_CH(r + 3) + lane, last)];
+                xA = cb[min(AF_CH(r + 3) + 64, last)];
+                if (r + 1 < nround)
+                    scan_round<HAS_LENS>(pack_chunk(vB), pack_chunk(xB), AF_CH(r + 1) + lane,
+                                         AF_CH(r + 1) + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
                                          stride, lens, r0, cnt);
-                vB = cb[min((r + 4) * 64 + lane, last)];
-                xB = cb[min((r + 5) * 64, last)];
-                if (r + 2 < g.nround)
-                    scan_round<HAS_LENS>(pack_chunk(vC), pack_chunk(xC), (r + 2) * 64 + lane,
-                                         (r + 2) * 64 + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
+                vB = cb[min(AF_CH(r + 4) + lane, last)];
+                xB = cb[min(AF_CH(r + 4) + 64, last)];
+                if (r + 2 < nround)
+                    scan_round<HAS_LENS>(pack_chunk(vC), pack_chunk(xC), AF_CH(r + 2) + lane,
+                                         AF_CH(r + 2) + lane < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn,
                                          stride, lens, r0, cnt);
-                vC = cb[min((r + 5) * 64 + lane, last)];
-                xC = cb[min((r + 6) * 64, last)];
+                vC = cb[min(AF_CH(r + 5) + lane, last)];
+                xC = cb[min(AF_CH(r + 5) + 64, last)];
             }
         } else {
-            for (int r = 0; r < g.nround; ++r) {
-                const int c = r * 64 + lane;
-                scan_round<HAS_LENS>(pack_chunk(load_round(g, r, lane)), pack_chunk(load_next(g, r)), c,
-                                     c < g.nchunks, lane, bsh, bm, tab, nb_bits, qk, qo, qn, stride, lens, r0, cnt);
+            for (int r = 0; r < nround; ++r) {
+                const int b = r * AF_SEED_WAVES + wv;
+                const int c = (b << 6) + lane;
+                const uint4 v = c < g.nfull ? *reinterpret_cast<const uint4 *>(g.base + 16 * (int64_t)c)
+                                            : (c < g.nchunks ? load_tail(g.base, c, g.bytes)
+                                                             : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu,
+                                                                          0x4E4E4E4Eu));
+                const int cx = (b + 1) << 6;
+                const uint4 x = cx < g.nfull ? *reinterpret_cast<const uint4 *>(g.base + 16 * (int64_t)cx)
+                                             : (cx < g.nchunks ? load_tail(g.base, cx, g.bytes)
+                                                               : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu,
+                                                                            0x4E4E4E4Eu));
+                scan_round<HAS_LENS>(pack_chunk(v), pack_chunk(x), c, c < g.nchunks, lane, bsh, bm, tab, nb_bits,
+                                     qk, qo, qn, stride, lens, r0, cnt);
             }
         }
+#undef AF_CH
         if (qn > 0) drain<HAS_LENS>(tab, nb_bits, qk, qo, 0, qn, lane, stride, lens, r0, cnt);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int i0 = 0; i0 < nr; i0 += 64) {
+        __syncthreads();
+        for (int i0 = wv * 64; i0 < nr; i0 += 64 * AF_SEED_WAVES) {
             const int i = i0 + lane;
             uint32_t h = 0;
             if (i < nr) {
@@ -232,24 +239,22 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
                 if (h) cand[basei + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(r0 + i);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __syncthreads();
     }
 }
 
 }  // namespace
 
 size_t af_seed_filter_lds(int nb_bits, int bm_bits) {
-    return ((size_t)1 << nb_bits) * 16 + ((size_t)1 << (bm_bits - 3)) +
-           (size_t)AF_SEED_WAVES * (AF_SEED_TILE + QCAP * 8);
+    return ((size_t)1 << nb_bits) * 16 + ((size_t)1 << (bm_bits - 3)) + AF_SEED_BTILE +
+           (size_t)AF_SEED_WAVES * QCAP * 8;
 }
 
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,
                                  hipStream_t s) {
     if (n_reads <= 0) return hipSuccess;
-    static_assert(AF_SEED_TILE == 256, "counter layout assumes 64 words per wave");
-    const int64_t tiles = (n_reads + AF_SEED_TILE - 1) / AF_SEED_TILE;
-    const int64_t want = (tiles + AF_SEED_WAVES - 1) / AF_SEED_WAVES;
+    const int64_t want = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     const size_t lds = af_seed_filter_lds(ix.nb_bits, ix.bm_bits);
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
     const int64_t blocks = std::min<int64_t>(want, (int64_t)n_cu * per_cu);
