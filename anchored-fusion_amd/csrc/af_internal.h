@@ -22,16 +22,18 @@ struct DevIndex {
     const int32_t *hstart;  //   first index into kpos
     const int32_t *hcnt;    //   occurrences (0 = empty slot)
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
-    const uint4 *ftab;      // filter buckets: 8 x u16 (slots 0..6 fingerprints, slot 7 overflow)
-    const uint32_t *bitmap; // stage-1 filter: bit (fmix(k) >> (32 - bm_bits)) set for anchor 16-mers
+    const uint2 *bloom;     // blocked Bloom filter of the anchor 16-mers (2 x 32-bit words per block)
     int64_t n;              // anchor length
     int32_t hbits;          // log2 position-hash slots
-    int32_t nb_bits;        // log2 filter buckets
-    int32_t bm_bits;        // log2 bitmap bits
+    int32_t bl_bits;        // log2 Bloom blocks
 };
 
 __host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
-__host__ __device__ static inline uint32_t af_ffp(uint32_t h) { return ((h >> 4) & 0x7FFFu) | 0x8000u; }
+__host__ __device__ static inline uint32_t af_fmix2(uint32_t h) { return (h ^ (h >> 15)) * 0x2C1B3C6Du; }
+// three bits of a 32-bit Bloom word, chosen by bits 0..14 of a hash (block index uses the top bits)
+__host__ __device__ static inline uint32_t af_bloom_mask(uint32_t h) {
+    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
+}
 
 // Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
 struct ReadRec {
@@ -43,7 +45,7 @@ struct ReadRec {
 
 // launch helpers (defined in the .hip files)
 // ctrl: [0] candidate count, [1] K2 work counter, [2] K1 tile counter (zeroed per call)
-size_t af_seed_filter_lds(int nb_bits, int bm_bits);
+size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,
                                  hipStream_t s);

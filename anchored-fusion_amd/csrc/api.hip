@@ -34,7 +34,7 @@ struct af_ctx {
 struct af_index {
     af_ctx *ctx = nullptr;
     DevIndex dev{};
-    std::vector<uint16_t> ftab_host;
+    std::vector<uint32_t> bloom_host;
     void *allocs[16] = {};
     int n_allocs = 0;
 };
@@ -208,56 +208,34 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         while (hcnt[s]) s = (s + 1) & hm;
         hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
     }
-    // LDS filter table: avg load <= 4 per 8-slot bucket, min 256 buckets
-    int nb_bits = 8;
-    while ((1LL << nb_bits) * 4 < nd) ++nb_bits;
-    if (nb_bits > 13)
-        return fail(c, AF_E_UNSUPPORTED, "anchor has %lld distinct 16-mers; the LDS filter holds <= 32768",
-                    (long long)nd);
-    const uint32_t nb = 1u << nb_bits;
-    std::vector<uint16_t> ft((size_t)nb * 8, 0);
+    // blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
+    // ~0.6 blocks per key (64 KiB for a 6.8 kb anchor), 3 bits per word (see af_bloom_mask)
+    int bl_bits = 8;
+    while ((double)(1LL << bl_bits) < 0.6 * (double)nd && bl_bits < 14) ++bl_bits;
+    std::vector<uint32_t> bloom((size_t)2 << bl_bits, 0);
     for (int64_t i = 0; i < nd; ++i) {
-        const uint32_t h = af_fmix(keys[i]);
-        uint32_t b = h >> (32 - nb_bits);
-        const uint16_t f = (uint16_t)af_ffp(h);
-        for (;;) {
-            uint16_t *bk = &ft[(size_t)b * 8];
-            int s = 0;
-            while (s < 7 && bk[s]) ++s;
-            if (s < 7) { bk[s] = f; break; }
-            bk[7] = 1;
-            b = (b + 1) & (nb - 1);
-        }
-    }
-    // stage-1 bitmap: 2^19 bits beside a <= 4096-bucket table, 2^16 beside 8192 buckets
-    // (what fits in 160 KiB of LDS; the oracle restates the same rule)
-    const int bm_bits = nb_bits <= 12 ? 19 : 16;
-    if (af_seed_filter_lds(nb_bits, bm_bits) > 160 * 1024)
-        return fail(c, AF_E_UNSUPPORTED, "seed-filter LDS image exceeds 160 KiB");
-    std::vector<uint32_t> bitmap((size_t)1 << (bm_bits - 5), 0);
-    for (int64_t i = 0; i < nd; ++i) {
-        const uint32_t bi = af_fmix(keys[i]) >> (32 - bm_bits);
-        bitmap[bi >> 5] |= 1u << (bi & 31);
+        const uint32_t h1 = af_fmix(keys[i]), h2 = af_fmix2(h1);
+        const size_t blk = h1 >> (32 - bl_bits);
+        bloom[2 * blk] |= af_bloom_mask(h1);
+        bloom[2 * blk + 1] |= af_bloom_mask(h2);
     }
     af_index *ix = new (std::nothrow) af_index;
     if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
     ix->ctx = c;
-    ix->ftab_host = ft;
+    ix->bloom_host = bloom;
     int rc = AF_OK;
-    const uint16_t *ftd = nullptr;
+    const uint32_t *bld = nullptr;
     if ((rc = dev_upload(c, ix, D, &ix->dev.D)) || (rc = dev_upload(c, ix, D2, &ix->dev.D2)) ||
         (rc = dev_upload(c, ix, Dn, &ix->dev.Dn)) || (rc = dev_upload(c, ix, hkey, &ix->dev.hkey)) ||
         (rc = dev_upload(c, ix, hstart, &ix->dev.hstart)) || (rc = dev_upload(c, ix, hcnt, &ix->dev.hcnt)) ||
-        (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, ft, &ftd)) ||
-        (rc = dev_upload(c, ix, bitmap, &ix->dev.bitmap))) {
+        (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, bloom, &bld))) {
         af_index_free(ix);
         return rc;
     }
-    ix->dev.ftab = reinterpret_cast<const uint4 *>(ftd);
+    ix->dev.bloom = reinterpret_cast<const uint2 *>(bld);
     ix->dev.n = n;
     ix->dev.hbits = hbits;
-    ix->dev.nb_bits = nb_bits;
-    ix->dev.bm_bits = bm_bits;
+    ix->dev.bl_bits = bl_bits;
     *out = ix;
     return AF_OK;
 }
@@ -270,12 +248,12 @@ void af_index_free(af_index *ix) {
 }
 
 int64_t af_index_anchor_len(const af_index *ix) { return ix ? ix->dev.n : -1; }
-int32_t af_index_filter_buckets(const af_index *ix) { return ix ? (1 << ix->dev.nb_bits) : -1; }
+int32_t af_index_filter_blocks(const af_index *ix) { return ix ? (1 << ix->dev.bl_bits) : -1; }
 
-int af_index_filter_table(const af_index *ix, uint16_t *out, int64_t cap) {
+int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
     if (!ix || !out) return AF_E_INVALID;
-    if (cap < (int64_t)ix->ftab_host.size()) return AF_E_CAPACITY;
-    memcpy(out, ix->ftab_host.data(), ix->ftab_host.size() * sizeof(uint16_t));
+    if (cap < (int64_t)ix->bloom_host.size()) return AF_E_CAPACITY;
+    memcpy(out, ix->bloom_host.data(), ix->bloom_host.size() * sizeof(uint32_t));
     return AF_OK;
 }
 

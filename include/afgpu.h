@@ -74,13 +74,13 @@ void af_ctx_destroy(af_ctx *ctx);
 const char *af_last_error(const af_ctx *ctx);
 void af_params_default(af_params *p);
 
-/* anchor index (doubled reference anchor ++ revcomp, 16-mer position map, LDS filter table) */
+/* anchor index (doubled reference anchor ++ revcomp, 16-mer position map, Bloom seed filter) */
 int af_index_build(af_ctx *ctx, const char *anchor, int64_t len, af_index **out);
 void af_index_free(af_index *idx);
 int64_t af_index_anchor_len(const af_index *idx);
-int32_t af_index_filter_buckets(const af_index *idx);
-/* copies the filter table (nbuckets*8 uint16) to host memory */
-int af_index_filter_table(const af_index *idx, uint16_t *out, int64_t cap);
+int32_t af_index_filter_blocks(const af_index *idx);
+/* copies the seed-filter Bloom words (2 x uint32 per block) to host memory */
+int af_index_filter_table(const af_index *idx, uint32_t *out, int64_t cap);
 
 /* host buffers in, host buffers out; synchronous */
 int af_align_pairs(af_ctx *ctx, const af_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,

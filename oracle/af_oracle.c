@@ -22,11 +22,8 @@ struct afo_index {
     int64_t nk;         /* number of indexed 16-mer positions              */
     uint32_t *kmer;     /* sorted by (kmer, pos)                            */
     int32_t *kpos;
-    int32_t nb;         /* filter buckets (power of two)                    */
-    int32_t nb_bits;
-    uint16_t *ftab;     /* nb * 8 halfwords; slot 7 = overflow flag         */
-    int32_t bm_bits;    /* stage-1 bitmap: 19 bits (<= 4096 buckets) else 16 */
-    uint32_t *bitmap;
+    int32_t bl_bits;    /* log2 Bloom blocks                               */
+    uint32_t *bloom;    /* 2 words per block                               */
 };
 
 /* ---- encoding ---------------------------------------------------------------------- */
@@ -47,9 +44,13 @@ void afo_params_default(afo_params *p) {
     p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 64;
 }
 
-/* filter hash: bijective 32-bit mix; bucket = top bits, fingerprint = bits 4..18 | 0x8000 */
+/* seed-filter hashes: block = top bits of fmix(k); bits 0..14 of fmix(k) and of fmix2(fmix(k))
+ * pick three bits in each of the block's two words */
 static inline uint32_t fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
-static inline uint16_t ffp(uint32_t h) { return (uint16_t)(((h >> 4) & 0x7FFFu) | 0x8000u); }
+static inline uint32_t fmix2(uint32_t h) { return (h ^ (h >> 15)) * 0x2C1B3C6Du; }
+static inline uint32_t bloom_mask(uint32_t h) {
+    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
+}
 
 static int cmp_u64(const void *a, const void *b) {
     uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
@@ -96,32 +97,18 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
         I->kpos[i] = (int32_t)(tmp[i] & 0xffffffffu);
         if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
     }
-    /* filter table: smallest power of two with average load <= 4 (min 256 buckets) */
+    /* blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
+     * ~0.6 blocks per key (at most 2^14), three bits set per word */
     int bits = 8;
-    while ((1LL << bits) * 4 < nd) ++bits;
-    I->nb_bits = bits;
-    I->nb = 1 << bits;
-    I->ftab = (uint16_t *)calloc((size_t)I->nb * 8, sizeof(uint16_t));
+    while ((double)(1LL << bits) < 0.6 * (double)nd && bits < 14) ++bits;
+    I->bl_bits = bits;
+    I->bloom = (uint32_t *)calloc((size_t)2 << bits, sizeof(uint32_t));
     for (int64_t i = 0; i < m; ++i) {
-        if (i > 0 && I->kmer[i] == I->kmer[i - 1]) continue; /* distinct keys, ascending */
-        uint32_t h = fmix(I->kmer[i]);
-        uint32_t b = h >> (32 - bits);
-        uint16_t f = ffp(h);
-        for (;;) {
-            uint16_t *bk = I->ftab + (size_t)b * 8;
-            int s = 0;
-            while (s < 7 && bk[s]) ++s;
-            if (s < 7) { bk[s] = f; break; }
-            bk[7] = 1; /* overflow: continue in the next bucket */
-            b = (b + 1) & (uint32_t)(I->nb - 1);
-        }
-    }
-    /* stage-1 bitmap of the same keys, indexed by the top bm_bits of fmix(k) */
-    I->bm_bits = I->nb_bits <= 12 ? 19 : 16;
-    I->bitmap = (uint32_t *)calloc((size_t)1 << (I->bm_bits - 5), sizeof(uint32_t));
-    for (int64_t i = 0; i < m; ++i) {
-        uint32_t bi = fmix(I->kmer[i]) >> (32 - I->bm_bits);
-        I->bitmap[bi >> 5] |= 1u << (bi & 31);
+        if (i > 0 && I->kmer[i] == I->kmer[i - 1]) continue;
+        uint32_t h1 = fmix(I->kmer[i]), h2 = fmix2(h1);
+        size_t blk = h1 >> (32 - bits);
+        I->bloom[2 * blk] |= bloom_mask(h1);
+        I->bloom[2 * blk + 1] |= bloom_mask(h2);
     }
     free(tmp);
     return I;
@@ -129,30 +116,23 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
 
 void afo_index_free(afo_index *I) {
     if (!I) return;
-    free(I->D); free(I->kmer); free(I->kpos); free(I->ftab); free(I->bitmap); free(I);
+    free(I->D); free(I->kmer); free(I->kpos); free(I->bloom); free(I);
 }
 int64_t afo_index_len(const afo_index *I) { return I->n; }
-int32_t afo_filter_nbuckets(const afo_index *I) { return I->nb; }
-const uint16_t *afo_filter_table(const afo_index *I) { return I->ftab; }
+int32_t afo_filter_blocks(const afo_index *I) { return 1 << I->bl_bits; }
+const uint32_t *afo_filter_table(const afo_index *I) { return I->bloom; }
 
-/* a sampled 16-mer is a hit when it passes the stage-1 bitmap AND the fingerprint table */
+/* a sampled 16-mer is a hit when all six Bloom bits of its block are set */
 static int filter_query(const afo_index *I, uint32_t k) {
-    uint32_t h = fmix(k);
-    uint32_t bi = h >> (32 - I->bm_bits);
-    if (!((I->bitmap[bi >> 5] >> (bi & 31)) & 1u)) return 0;
-    uint32_t b = h >> (32 - I->nb_bits);
-    uint16_t f = ffp(h);
-    for (;;) {
-        const uint16_t *bk = I->ftab + (size_t)b * 8;
-        for (int s = 0; s < 7; ++s)
-            if (bk[s] == f) return 1;
-        if (bk[7] != 1) return 0;
-        b = (b + 1) & (uint32_t)(I->nb - 1);
-    }
+    uint32_t h1 = fmix(k), h2 = fmix2(h1);
+    size_t blk = h1 >> (32 - I->bl_bits);
+    uint32_t m0 = bloom_mask(h1), m1 = bloom_mask(h2);
+    return (I->bloom[2 * blk] & m0) == m0 && (I->bloom[2 * blk + 1] & m1) == m1;
 }
 
 /* K1 semantics: sampled positions are those whose byte offset in the read buffer is a
- * multiple of 4; any MEM >= 19 nt contains such a 16-mer, so hits==0 => no seed.  Bytes are
+ * multiple of 4; any MEM >= 19 nt contains such a 16-mer and a Bloom filter has no false
+ * negatives, so hits==0 => no seed.  Bytes are
  * projected to 2 bits by ((c >> 1) ^ (c >> 2)) & 3 (exact for ACGT/acgt; other bytes land on
  * some code, which can only add hits -- MEMs never contain N, so the superset property holds). */
 void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, int32_t stride,
