@@ -209,9 +209,9 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
     }
     // blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
-    // ~0.6 blocks per key (64 KiB for a 6.8 kb anchor), 3 bits per word (see af_bloom_mask)
+    // ~1.2 blocks per key (128 KiB for a 6.8 kb anchor), 3 bits per word (see af_bloom_mask)
     int bl_bits = 8;
-    while ((double)(1LL << bl_bits) < 0.6 * (double)nd && bl_bits < 14) ++bl_bits;
+    while ((double)(1LL << bl_bits) < 1.2 * (double)nd && bl_bits < 14) ++bl_bits;
     std::vector<uint32_t> bloom((size_t)2 << bl_bits, 0);
     for (int64_t i = 0; i < nd; ++i) {
         const uint32_t h1 = af_fmix(keys[i]), h2 = af_fmix2(h1);

@@ -98,9 +98,9 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
         if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
     }
     /* blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
-     * ~0.6 blocks per key (at most 2^14), three bits set per word */
+     * ~1.2 blocks per key (at most 2^14), three bits set per word */
     int bits = 8;
-    while ((double)(1LL << bits) < 0.6 * (double)nd && bits < 14) ++bits;
+    while ((double)(1LL << bits) < 1.2 * (double)nd && bits < 14) ++bits;
     I->bl_bits = bits;
     I->bloom = (uint32_t *)calloc((size_t)2 << bits, sizeof(uint32_t));
     for (int64_t i = 0; i < m; ++i) {
