@@ -8,6 +8,7 @@
 #define AF_NEG_INF (-0x40000000)
 #define AF_SEED_BTILE 2048      // reads per workgroup tile in the seed filter
 #define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
+#define AF_SEED_GROUPS (AF_SEED_BTILE / 64)  // 64-read ballot groups per tile
 #define AF_ALN_WAVES 4          // waves per alignment workgroup
 #define AF_CPL 6                // DP columns per lane: 6*64 = 384 >= AF_MAX_READ+1
 #define AF_ZCAP 12288           // LDS traceback bytes per wave; larger DPs use global scratch

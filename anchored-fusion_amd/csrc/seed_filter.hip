@@ -2,7 +2,7 @@
 // pass of `bwa mem` at Anchored_Fusion.py:182).
 //
 // Layout and schedule:
-//  * persistent grid, two 1024-thread workgroups per CU; block tiles of AF_SEED_BTILE whole
+//  * persistent grid, one or two 1024-thread workgroups per CU (LDS-bound); block tiles of AF_SEED_BTILE whole
 //    reads taken round-robin; the 16 waves of a workgroup sweep a tile together, so every
 //    round moves ~16 KiB of contiguous bytes (lane l of wave w loads one 16-byte chunk: one
 //    coalesced 1-KiB global_load_dwordx4 per wave), unrolled x3 with two rounds in flight;
@@ -16,8 +16,8 @@
 //    each (~1e-7 false positives per probe for a 6.8 kb anchor), no data-dependent control
 //    flow on the hot path;
 //  * Bloom-positive 16-mers add to 8-bit per-read counters in LDS; after the tile each wave
-//    writes one int32 per read and appends reads with hits to the candidate list (one global
-//    atomic per 64 reads).
+//    writes one int32 per read; the tile's reads with hits are appended to the candidate
+//    list with ONE global atomic per tile (LDS prefix over the tile's 64-read ballots).
 //
 // Exactness: any MEM >= 19 nt (bwa -k 19) contains a 16-mer starting at an offset that is a
 // multiple of 4 and a Bloom filter has no false negatives, so hits == 0 implies no seed; the
@@ -96,6 +96,8 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const uint2 *__restrict__ bloom_g, int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand,
     int32_t *__restrict__ ctrl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint64_t gbal[AF_SEED_GROUPS];  // per 64-read group: ballot of reads with hits
+    __shared__ int gbase[AF_SEED_GROUPS];      // per group: first cand slot
     const int nbl = 1 << bl_bits;
     uint2 *bloom = reinterpret_cast<uint2 *>(smem);
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nbl * 8);  // AF_SEED_BTILE 8-bit counters
@@ -178,20 +180,38 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
             }
             __syncthreads();
         }
-        for (int i0 = wv * 64; i0 < nr; i0 += 64 * AF_SEED_WAVES) {
-            const int i = i0 + lane;
+        // candidate append: ONE device atomic per tile.  A device-scope atomic on a single
+        // address is serialised across all 8 XCDs; one per 64-read group (~30k per launch)
+        // cost more than the whole scan.
+        for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
+            const int i = g * 64 + lane;
             uint32_t h = 0;
             if (i < nr) {
                 h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
                 hits[r0 + i] = (int32_t)h;
             }
             const uint64_t bal = __ballot(h != 0);
-            if (bal) {
-                int basei = 0;
-                if (lane == 0) basei = atomicAdd(&ctrl[0], (int)__popcll(bal));
-                basei = __shfl(basei, 0);
-                if (h) cand[basei + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(r0 + i);
+            if (lane == 0) gbal[g] = bal;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            const int c = lane < AF_SEED_GROUPS ? (int)__popcll(gbal[lane]) : 0;
+            int incl = c;  // inclusive prefix over the tile's groups
+            for (int d = 1; d < AF_SEED_GROUPS; d <<= 1) {
+                const int t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
             }
+            const int total = __shfl(incl, AF_SEED_GROUPS - 1);
+            int basei = 0;
+            if (lane == 0 && total) basei = atomicAdd(&ctrl[0], total);
+            basei = __shfl(basei, 0);
+            if (lane < AF_SEED_GROUPS) gbase[lane] = basei + incl - c;
+        }
+        __syncthreads();
+        for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
+            const uint64_t bal = gbal[g];
+            if ((bal >> lane) & 1ull)
+                cand[gbase[g] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(r0 + g * 64 + lane);
         }
         __syncthreads();
     }
@@ -207,14 +227,17 @@ hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64
     if (n_reads <= 0) return hipSuccess;
     const int64_t want = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     const size_t lds = af_seed_filter_lds(ix.bl_bits);
-    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / (lds + 1024)));
     const int64_t blocks = std::min<int64_t>(want, (int64_t)n_cu * per_cu);
     static bool attr_done = false;
     if (!attr_done) {  // dynamic LDS above 64 KiB needs the opt-in on both instantiations
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        // (static + dynamic must stay within the CU's 160 KiB: leave 1 KiB for the static arrays)
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<true>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+        if (e != hipSuccess) return e;
         attr_done = true;
     }
     dim3 grid((unsigned)blocks), block(64 * AF_SEED_WAVES);
