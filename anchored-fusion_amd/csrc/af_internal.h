@@ -45,7 +45,10 @@ struct ReadRec {
 };
 
 // launch helpers (defined in the .hip files)
-// ctrl: [0] candidate count, [1] K2 work counter, [2] K1 tile counter (zeroed per call)
+// ctrl (AF_CTRL_BYTES): [0] candidate count (zeroed per K1 call); K2 dequeue head x at
+// [AF_HEAD_STRIDE * (1 + x)], x = 0..7, one 128-B line each (zeroed per K2 call)
+#define AF_HEAD_STRIDE 32
+#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 9)
 size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,

@@ -17,6 +17,18 @@
 
 namespace {
 
+#ifdef AF_K2_PROF
+// profiling build only (make prof -> libafgpu_prof.so): per-candidate phase timings
+__device__ int32_t *g_k2prof = nullptr;
+constexpr int PROF_W = 12;
+#define PROF(...) __VA_ARGS__
+#else
+#define PROF(...)
+#endif
+
+#ifndef AF_K2_STATIC_PCT
+#define AF_K2_STATIC_PCT 0  // share of candidates assigned round-robin (rest: per-XCD dequeue)
+#endif
 constexpr int MEMCAP = 64;   // == max allowed af_params.max_mems
 constexpr int ZLDS = 6144;   // traceback bytes per wave kept in LDS
 
@@ -39,14 +51,16 @@ __device__ __forceinline__ int dpp(int old, int v) {
 }
 constexpr int kNeg = -(1 << 30) - (1 << 29);  // identity for max (below every DP value used)
 
-// inclusive prefix max over lanes 0..63
+// inclusive prefix max over lanes 0..63.  The DPP `old` operand is INT_MIN, the identity of
+// max, so the compiler folds each step into one v_max_i32_dpp.
+constexpr int kMaxId = (int)0x80000000;
 __device__ __forceinline__ int wave_incl_max(int v) {
-    v = max(v, dpp<0x111>(kNeg, v));        // row_shr:1
-    v = max(v, dpp<0x112>(kNeg, v));        // row_shr:2
-    v = max(v, dpp<0x114>(kNeg, v));        // row_shr:4
-    v = max(v, dpp<0x118>(kNeg, v));        // row_shr:8
-    v = max(v, dpp<0x142, 0xa>(kNeg, v));   // row_bcast:15 -> rows 1, 3
-    v = max(v, dpp<0x143, 0xc>(kNeg, v));   // row_bcast:31 -> rows 2, 3
+    v = max(v, dpp<0x111>(kMaxId, v));        // row_shr:1
+    v = max(v, dpp<0x112>(kMaxId, v));        // row_shr:2
+    v = max(v, dpp<0x114>(kMaxId, v));        // row_shr:4
+    v = max(v, dpp<0x118>(kMaxId, v));        // row_shr:8
+    v = max(v, dpp<0x142, 0xa>(kMaxId, v));   // row_bcast:15 -> rows 1, 3
+    v = max(v, dpp<0x143, 0xc>(kMaxId, v));   // row_bcast:31 -> rows 2, 3
     return v;
 }
 // lane l receives lane l-1's value; lane 0 receives `old`
@@ -84,7 +98,7 @@ __device__ __forceinline__ int infer_bw(int l1, int l2, int score, int a, int q,
     return w < d ? d : w;
 }
 
-struct ExtRes { int max, qle, tle, gtle, gscore, max_off; };
+struct ExtRes { int max, qle, tle, gtle, gscore, max_off, rows; };
 
 // select element c (runtime, < CPL) of a register array without scratch
 template <int CPL>
@@ -135,9 +149,11 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     int beg = 0, end = qlen;
     const int jq = qlen - 1, lq_lane = jq / cpl, lq_c = jq - lq_lane * cpl;
     int ti_next = tlen > 0 ? t[0] : 4;
+    int rows = 0;
     for (int i = 0; i < tlen; ++i) {
         const int ti = ti_next;
         if (i + 1 < tlen) ti_next = t[i + 1];
+        ++rows;
         if (beg < i - w) beg = i - w;
         if (end > i + w + 1) end = i + w + 1;
         if (end > qlen) end = qlen;
@@ -235,10 +251,34 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         const int jstar = LNZ >= beg_new ? LNZ : beg_new - 1;
         beg = beg_new;
         end = jstar + 2 < qlen ? jstar + 2 : qlen;
+        // Early exit (exact): no later row can raise any cell above
+        // U = max_j (max(eh[j].h, eh[j].e) + (qlen - j) * a) -- cells only grow along the
+        // diagonal and a zero cell never restarts -- so once U <= max and U < gscore no later
+        // row can change max/max_i/max_j/max_off (need m > max) or gscore/max_ie (need
+        // H(i, qlen-1) >= gscore).  Checked on odd rows; the oracle runs every row.
+        if ((i & 1) && gscore > 0) {
+            int u = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = j0 + c;
+                if (c < cpl && j >= beg && j <= qlen) u = max(u, max(eh_h[c], eh_e[c]) + (qlen - j) * p.a);
+            }
+            const int U = wave_max(u);
+            if (U <= mx && U < gscore) break;
+        }
     }
     ExtRes r;
-    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off;
+    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off; r.rows = rows;
     return r;
+}
+
+// one column per lane when the query fits a wave (the common case: a 100-bp read's flanks),
+// otherwise CPL columns per lane; the per-row VALU cost scales with the columns per lane
+template <int CPL>
+__device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p,
+                                         int w, int end_bonus, int zdrop, int h0, int lane) {
+    if (CPL == 1 || qlen + 1 <= 64) return ext_dp_wave<1>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
+    return ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
 }
 
 // ksw_global2 semantics with traceback (see oracle global_dp).  z: n_col*tlen bytes.
@@ -321,6 +361,7 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     }
     const int score = bcast(pick<CPL>(eh_h, qlen - (qlen / cpl) * cpl), qlen / cpl);
     wave_sync();
+    PROF(const int64_t tb0 = clock64();)
     if (lane == 0) {
         int nc = 0, which = 0;
         int i = tlen - 1;
@@ -340,6 +381,7 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         L.misc[2] = nc;
     }
     wave_sync();
+    PROF(L.misc[3] += (int)(clock64() - tb0);)
     return score;
 }
 
@@ -383,7 +425,8 @@ __device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, in
         w = w > min_w ? w : min_w;
         const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
         uint8_t *z = ((size_t)n_col * rlen <= ZLDS) ? L.z : zg;
-        score = global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        score = lq + 1 <= 64 ? global_dp_wave<1>(lq, L.qs, rlen, L.t, p, w, z, L, lane)
+                             : global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
     }
     return score;
 }
@@ -403,12 +446,34 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
     const int max_ext = p.max_ext < 16 ? p.max_ext : 16;
     const int max_mems = p.max_mems < MEMCAP ? p.max_mems : MEMCAP;
     const uint32_t hm = (1u << ix.hbits) - 1u;
+    // Work split: the first AF_K2_STATIC_PCT % of the candidates go round-robin to slots (no atomics); the
+    // tail is dequeued from 8 per-XCD heads (one 128-B line each) so that no single word
+    // takes every dequeue (one device-scope word saturates near 88 dequeues/us).
+    const int S = (int)gridDim.x;
+    const int nstat = (int)(((int64_t)ncand * AF_K2_STATIC_PCT / 100) / S * S);
+    int next_static = (int)blockIdx.x;
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
-        int item = 0;
-        if (lane == 0) item = atomicAdd(work, 1);
-        item = __builtin_amdgcn_readfirstlane(item);
-        if (item >= ncand) break;
+        int item;
+        if (next_static < nstat) {
+            item = next_static;
+            next_static += S;
+        } else {
+            item = ncand;
+            while (heads_left > 0) {
+                int v = 0;
+                if (lane == 0) v = atomicAdd(&work[AF_HEAD_STRIDE * head], 1);
+                v = __builtin_amdgcn_readfirstlane(v);
+                const int64_t it = (int64_t)nstat + head + 8 * (int64_t)v;
+                if (it < ncand) { item = (int)it; break; }
+                head = (head + 1) & 7;
+                --heads_left;
+            }
+            if (item >= ncand) break;
+        }
         const int64_t r = cand[item];
+        PROF(const int64_t pt0 = clock64(); int64_t pt1 = pt0, pt2 = pt0; int p_ext_rows = 0, p_cig_rows = 0,
+             p_ext_calls = 0, p_nreg = 0;)
         int l = lens ? lens[r] : stride;
         if (l > AF_MAX_READ) l = AF_MAX_READ;
         const uint8_t *rd = reads + r * (int64_t)stride;
@@ -425,6 +490,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             L.q[x] = v;
         }
         if (lane == 0) L.misc[0] = 0;
+        PROF(if (lane == 0) L.misc[3] = 0;)
         wave_sync();
         // ---- 1. MEMs ------------------------------------------------------------------
         for (int qb = lane; qb + AF_K <= l; qb += 64) {
@@ -483,6 +549,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             }
         }
         wave_sync();
+        PROF(pt1 = clock64();)
         const int nm_total = L.misc[0];
         int flag = 0x4;
         int out_pos = 0, out_score = 0, out_nc = 0;
@@ -542,7 +609,8 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw0 = p.w << it;
-                        er = ext_dp_wave<CPL>(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
+                        er = ext_dp<CPL>(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
+                        PROF(p_ext_rows += er.rows; ++p_ext_calls;)
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
                     }
@@ -566,7 +634,8 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw1 = p.w << it;
-                        er = ext_dp_wave<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                        er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                        PROF(p_ext_rows += er.rows; ++p_ext_calls;)
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
                     }
@@ -587,6 +656,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                 wave_sync();
                 ++n_reg;
             }
+            PROF(pt2 = clock64(); p_nreg = n_reg;)
             int best = -1;
             for (int rr = 0; rr < n_reg; ++rr)
                 if (best < 0 || L.regs[rr][0] > L.regs[best][0]) best = rr;
@@ -605,6 +675,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                 do {
                     w2 = w2 < p.w << 2 ? w2 : p.w << 2;
                     score = gen_cigar_wave<CPL>(ix, p, w2, lq, aqb, arb, are, L, zg, lane);
+                    PROF(p_cig_rows += (int)(are - arb);)
                     if (score == last_sc || w2 == p.w << 2) break;
                     last_sc = score;
                     w2 <<= 1;
@@ -648,6 +719,16 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             rec.flag = flag; rec.pos = out_pos; rec.score = out_score; rec.n_cigar = out_nc;
             recs[r] = rec;
         }
+#ifdef AF_K2_PROF
+        if (lane == 0 && g_k2prof) {
+            const int64_t pt3 = clock64();
+            int32_t *o = g_k2prof + (int64_t)item * PROF_W;
+            o[0] = (int32_t)r; o[1] = (int32_t)(pt3 - pt0); o[2] = (int32_t)(pt1 - pt0);
+            o[3] = (int32_t)(pt2 - pt1); o[4] = (int32_t)(pt3 - pt2); o[5] = nm_total; o[6] = p_nreg;
+            o[7] = p_ext_rows; o[8] = p_cig_rows; o[9] = (int32_t)blockIdx.x; o[10] = p_ext_calls;
+            o[11] = L.misc[3];
+        }
+#endif
         wave_sync();
     }
 }
@@ -685,13 +766,27 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
 
 }  // namespace
 
+#ifdef AF_K2_PROF
+extern "C" int af_debug_k2_prof_enable(int64_t max_items) {
+    int32_t *d = nullptr;
+    if (hipMalloc(&d, sizeof(int32_t) * PROF_W * max_items) != hipSuccess) return -1;
+    (void)hipMemset(d, 0, sizeof(int32_t) * PROF_W * max_items);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_k2prof), &d, sizeof d) == hipSuccess ? PROF_W : -1;
+}
+extern "C" int af_debug_k2_prof_read(int32_t *host, int64_t n_items) {
+    int32_t *d = nullptr;
+    if (hipMemcpyFromSymbol(&d, HIP_SYMBOL(g_k2prof), sizeof d) != hipSuccess || !d) return -1;
+    return hipMemcpy(host, d, sizeof(int32_t) * PROF_W * n_items, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                            const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *ctrl,
                            int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
                            hipStream_t s) {
     (void)n_reads; (void)cand_cap;
-    int32_t *work = const_cast<int32_t *>(ctrl) + 1;
-    hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t), s);
+    int32_t *work = const_cast<int32_t *>(ctrl) + AF_HEAD_STRIDE;  // 8 dequeue heads
+    hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t) * AF_HEAD_STRIDE * 8, s);
     if (e != hipSuccess) return e;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;

@@ -16,7 +16,7 @@ struct af_ctx {
     int n_slots = 0;
     std::string err;
     // scratch (device)
-    int32_t *ctrl = nullptr;   // [0] n_cand, [1] work counter
+    int32_t *ctrl = nullptr;   // af_internal.h: candidate count + K2 dequeue heads
     int32_t *cand = nullptr;
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
@@ -134,7 +134,7 @@ int af_ctx_create(int device, af_ctx **out) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 16;  // k_align: 4 waves per SIMD (VGPR and LDS budget)
-    if (hipMalloc(&c->ctrl, 64) != hipSuccess) { delete c; return AF_E_HIP; }
+    if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         af_free(c->ctrl);
         delete c;
