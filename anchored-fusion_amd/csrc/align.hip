@@ -362,23 +362,52 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     const int score = bcast(pick<CPL>(eh_h, qlen - (qlen / cpl) * cpl), qlen / cpl);
     wave_sync();
     PROF(const int64_t tb0 = clock64();)
-    if (lane == 0) {
-        int nc = 0, which = 0;
+    // Traceback, wave-parallel.  The serial walk (bwa ksw_global2) is
+    //   which = z[i][k] >> (2 * which) & 3;  0: M (--i, --k)  1: D (--i)  2: I (--k)
+    // While `which` keeps its value the walk moves in a straight line, so lane t reads the
+    // cell t steps ahead on that line; the first lane whose code differs (or that leaves the
+    // matrix) ends the run.  One LDS read per lane and a ballot per run instead of one
+    // dependent read per step.
+    {
+        const int zsize = n_col * tlen;
         int i = tlen - 1;
         int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+        int state = 0, nc = 0, cur_op = -1, cur_len = 0;
         auto push = [&](int op, int len) {
-            if (nc > 0 && (int)(L.ring[(nc - 1) & 63] & 0xf) == op) L.ring[(nc - 1) & 63] += (uint32_t)len << 4;
-            else { L.ring[nc & 63] = (uint32_t)len << 4 | (uint32_t)op; ++nc; }
+            if (len <= 0) return;
+            if (op == cur_op) { cur_len += len; return; }
+            if (cur_op >= 0) {
+                if (lane == 0) L.ring[nc & 63] = (uint32_t)cur_len << 4 | (uint32_t)cur_op;
+                ++nc;
+            }
+            cur_op = op; cur_len = len;
         };
         while (i >= 0 && k >= 0) {
-            which = z[(size_t)i * n_col + (k - (i > w ? i - w : 0))] >> (which << 1) & 3;
+            const int it = i - (state != 2 ? lane : 0), kt = k - (state != 1 ? lane : 0);
+            int wt = -1;
+            if (it >= 0 && kt >= 0) {
+                const int idx = it * n_col + (kt - (it > w ? it - w : 0));
+                if (idx >= 0 && idx < zsize) wt = z[idx] >> (state << 1) & 3;
+            }
+            const uint64_t stop = __ballot(wt != state);
+            const int r = stop ? __ffsll((unsigned long long)stop) - 1 : 64;
+            const int op_state = state == 0 ? 0 : (state == 1 ? 2 : 1);
+            push(op_state, r);
+            if (state != 2) i -= r;
+            if (state != 1) k -= r;
+            if (r == 64) continue;
+            if (i < 0 || k < 0) break;
+            const int which = bcast(wt, r);
+            if (which < 0) break;  // walked off the stored matrix (not reachable from a valid score)
             if (which == 0) { push(0, 1); --i; --k; }
             else if (which == 1) { push(2, 1); --i; }
             else { push(1, 1); --k; }
+            state = which;
         }
         if (i >= 0) push(2, i + 1);
         if (k >= 0) push(1, k + 1);
-        L.misc[2] = nc;
+        push(-2, 1);  // flush
+        if (lane == 0) L.misc[2] = nc;
     }
     wave_sync();
     PROF(L.misc[3] += (int)(clock64() - tb0);)
