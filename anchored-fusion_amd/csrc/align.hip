@@ -20,7 +20,7 @@ namespace {
 #ifdef AF_K2_PROF
 // profiling build only (make prof -> libafgpu_prof.so): per-candidate phase timings
 __device__ int32_t *g_k2prof = nullptr;
-constexpr int PROF_W = 12;
+constexpr int PROF_W = 16;
 #define PROF(...) __VA_ARGS__
 #else
 #define PROF(...)
@@ -43,6 +43,10 @@ struct __attribute__((aligned(16))) AlnLds {
     uint8_t t[1024];
     uint8_t z[ZLDS];
 };
+
+// One wave per workgroup: the per-wave LDS slot lives at namespace scope so that out-of-line
+// helpers address it as LDS (ds_* instructions) rather than through generic pointers.
+__shared__ AlnLds g_aln;
 
 // ---- wave primitives (DPP; gfx9-family controls) ---------------------------------------
 template <int CTRL, int ROWM = 0xf, int BANKM = 0xf>
@@ -272,12 +276,139 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     return r;
 }
 
+// ksw_extend2 for qlen <= 63: lane j owns query column j (and lane qlen the eh[qlen] slot).
+// Same recurrences and tie-breaks as ext_dp_wave; the band bookkeeping is done on 64-bit lane
+// masks (ballots + s_ff1/s_flbit) so that a row costs ~40 VALU and no readlane of an index.
+// Kept out of line: inlined into k_align its loop ran out of SGPRs and spilled to VGPR lanes
+// on every row; as a call it gets its own register allocation (one save/restore per call).
+struct Sc { int a, b, o_del, e_del, o_ins, e_ins; };
+__device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tlen_, Sc p_, int w_, int end_bonus_,
+                                         int zdrop_, int h0_) {
+    // arguments of an out-of-line call arrive in VGPRs: re-assert wave uniformity
+#define AF_U(x) __builtin_amdgcn_readfirstlane(x)
+    const int qlen = AF_U(qlen_), tlen = AF_U(tlen_), end_bonus = AF_U(end_bonus_), zdrop = AF_U(zdrop_),
+              h0 = AF_U(h0_), qoff = AF_U(qoff_);
+    int w = AF_U(w_);
+    const Sc p{AF_U(p_.a), AF_U(p_.b), AF_U(p_.o_del), AF_U(p_.e_del), AF_U(p_.o_ins), AF_U(p_.e_ins)};
+    const uint8_t *q = (AF_U(qsel_) ? g_aln.q : g_aln.qs) + qoff;
+    const uint8_t *t = g_aln.t;
+#undef AF_U
+    const int lane = threadIdx.x;
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int j = lane;
+    int H, E = 0;
+    {
+        const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+        const int vj = v1 - (j - 1) * p.e_ins;
+        H = j > qlen ? 0 : (j == 0 ? h0 : (j == 1 ? v1 : (vj > 0 ? vj : 0)));
+    }
+    const int qc = j < qlen ? q[j] : 4;
+    const bool qn = qc > 3;
+    const int jE = j * p.e_ins, jE1 = (j - 1) * p.e_ins, tailA = (qlen - j) * p.a;
+    {
+        int max_ins = (int)((double)(qlen * p.a + end_bonus - p.o_ins) / p.e_ins + 1.);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = (int)((double)(qlen * p.a + end_bonus - p.o_del) / p.e_del + 1.);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    int beg = 0, end = qlen, rows = 0;
+    int ti_next = tlen > 0 ? t[0] : 4;
+    for (int i = 0; i < tlen; ++i) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
+        ++rows;
+        beg = max(beg, i - w);
+        end = min(min(end, i + w + 1), qlen);
+        int h1s = 0;
+        if (beg == 0) h1s = max(h0 - (p.o_del + p.e_del * (i + 1)), 0);
+        if (beg >= end) {
+            if (beg == qlen) {
+                max_ie = gscore > h1s ? max_ie : i;
+                gscore = gscore > h1s ? gscore : h1s;
+            }
+            break;
+        }
+        const bool in = j >= beg && j < end;
+        // score: a / -b, -1 when either base is N (ti is wave-uniform)
+        const int sa = ti > 3 ? -1 : p.a, sb = ti > 3 ? -1 : -p.b;
+        const int sc = qn ? -1 : (qc == ti ? sa : sb);
+        const int M = (in && H != 0) ? H + sc : 0;
+        const int run = in ? max(M - oe_ins, 0) + jE : kMaxId;
+        const int P = wave_shr1(kNeg, wave_incl_max(run));
+        const int f = j > beg ? P - jE1 : 0;
+        const int h = max(max(M, E), f);
+        const int En = in ? max(E - p.e_del, max(M - oe_del, 0)) : E;
+        const int key = in ? ((h << 10) | j) : -1;
+        const int kmax = wave_max(key);
+        const int m = kmax < 0 ? 0 : kmax >> 10;
+        const int mj = kmax < 0 ? -1 : (kmax & 1023);
+        const int hq = bcast(h, qlen - 1);
+        const int from_left = wave_shr1(0, h);
+        H = j == beg ? h1s : ((j > beg && j <= end) ? from_left : H);
+        E = j == end ? 0 : En;
+        if (end == qlen) {
+            max_ie = gscore > hq ? max_ie : i;
+            gscore = gscore > hq ? gscore : hq;
+        }
+        if (m == 0) break;
+        if (m > mx) {
+            mx = m; max_i = i; max_j = mj;
+            const int off = mj - i < 0 ? i - mj : mj - i;
+            max_off = max_off > off ? max_off : off;
+        } else if (zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (mx - m - ((i - max_i) - (mj - max_j)) * p.e_del > zdrop) break;
+            } else {
+                if (mx - m - ((mj - max_j) - (i - max_i)) * p.e_ins > zdrop) break;
+            }
+        }
+        // band trimming: first non-zero eh in [beg, end), last in [beg, end]
+        const uint64_t nz = __ballot((H | E) != 0);
+        const uint64_t lo = ~0ull << beg;
+        const uint64_t f_m = nz & lo & ((1ull << end) - 1ull);  // end <= 63
+        const uint64_t l_m = nz & lo & (end >= 63 ? ~0ull : ((2ull << end) - 1ull));
+        const int beg_new = f_m ? (int)__builtin_ctzll(f_m) : end;
+        const int lnz = l_m ? 63 - (int)__builtin_clzll(l_m) : -1;
+        const int jstar = lnz >= beg_new ? lnz : beg_new - 1;
+        beg = beg_new;
+        end = jstar + 2 < qlen ? jstar + 2 : qlen;
+        // exact early exit (see ext_dp_wave)
+        if ((i & 1) && gscore > 0) {
+            const int u = (j >= beg && j <= qlen) ? max(H, E) + tailA : 0;
+            const int U = wave_max(u);
+            if (U <= mx && U < gscore) break;
+        }
+    }
+    ExtRes r;
+    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off;
+    r.rows = rows;
+    return r;
+}
+
 // one column per lane when the query fits a wave (the common case: a 100-bp read's flanks),
 // otherwise CPL columns per lane; the per-row VALU cost scales with the columns per lane
 template <int CPL>
 __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p,
                                          int w, int end_bonus, int zdrop, int h0, int lane) {
-    if (CPL == 1 || qlen + 1 <= 64) return ext_dp_wave<1>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
+#ifdef AF_K2_PROF
+    const int64_t c0 = clock64();
+    ExtRes r;
+    const bool one = CPL == 1 || qlen + 1 <= 64;
+    if (one)
+        r = ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
+                      Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
+    else
+        r = ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
+    const int dc = (int)(clock64() - c0);
+    if (lane == 0) { g_aln.misc[one ? 4 : 6] += dc; g_aln.misc[one ? 5 : 7] += r.rows; }
+    return r;
+#endif
+    if (CPL == 1 || qlen + 1 <= 64)
+        return ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
+                         Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
     return ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
 }
 
@@ -467,7 +598,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                                               int32_t *__restrict__ work, ReadRec *__restrict__ recs,
                                               uint32_t *__restrict__ cigar, uint8_t *__restrict__ zscratch,
                                               size_t zstride) {
-    __shared__ AlnLds L;
+    AlnLds &L = g_aln;
     const int lane = threadIdx.x;
     const int ncand = ctrl[0];
     uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
@@ -502,7 +633,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
         }
         const int64_t r = cand[item];
         PROF(const int64_t pt0 = clock64(); int64_t pt1 = pt0, pt2 = pt0; int p_ext_rows = 0, p_cig_rows = 0,
-             p_ext_calls = 0, p_nreg = 0;)
+             p_ext_calls = 0, p_nreg = 0, p_ext_dp = 0;)
         int l = lens ? lens[r] : stride;
         if (l > AF_MAX_READ) l = AF_MAX_READ;
         const uint8_t *rd = reads + r * (int64_t)stride;
@@ -519,7 +650,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             L.q[x] = v;
         }
         if (lane == 0) L.misc[0] = 0;
-        PROF(if (lane == 0) L.misc[3] = 0;)
+        PROF(if (lane < 8 && lane >= 3) L.misc[lane] = 0;)
         wave_sync();
         // ---- 1. MEMs ------------------------------------------------------------------
         for (int qb = lane; qb + AF_K <= l; qb += 64) {
@@ -638,7 +769,9 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw0 = p.w << it;
+                        PROF(const int64_t te0 = clock64();)
                         er = ext_dp<CPL>(sqb, L.qs, tmp, L.t, p, aw0, p.pen_clip5, p.zdrop, slen * p.a, lane);
+                        PROF(p_ext_dp += (int)(clock64() - te0);)
                         PROF(p_ext_rows += er.rows; ++p_ext_calls;)
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
@@ -663,7 +796,9 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     for (int it = 0; it < 2; ++it) {
                         const int prev = a_score;
                         aw1 = p.w << it;
+                        PROF(const int64_t te0 = clock64();)
                         er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                        PROF(p_ext_dp += (int)(clock64() - te0);)
                         PROF(p_ext_rows += er.rows; ++p_ext_calls;)
                         a_score = er.max;
                         if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
@@ -753,9 +888,9 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             const int64_t pt3 = clock64();
             int32_t *o = g_k2prof + (int64_t)item * PROF_W;
             o[0] = (int32_t)r; o[1] = (int32_t)(pt3 - pt0); o[2] = (int32_t)(pt1 - pt0);
-            o[3] = (int32_t)(pt2 - pt1); o[4] = (int32_t)(pt3 - pt2); o[5] = nm_total; o[6] = p_nreg;
-            o[7] = p_ext_rows; o[8] = p_cig_rows; o[9] = (int32_t)blockIdx.x; o[10] = p_ext_calls;
-            o[11] = L.misc[3];
+            o[3] = (int32_t)(pt2 - pt1); o[4] = (int32_t)(pt3 - pt2); o[5] = nm_total; o[6] = p_nreg; o[9] = p_ext_dp;
+            o[7] = p_ext_rows; o[8] = p_cig_rows; o[10] = p_ext_calls;
+            o[11] = L.misc[3]; o[12] = L.misc[4]; o[13] = L.misc[5]; o[14] = L.misc[6]; o[15] = L.misc[7];
         }
 #endif
         wave_sync();

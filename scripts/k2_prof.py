@@ -49,11 +49,11 @@ buf = np.zeros((nc, W), dtype=np.int32)
 assert lib.af_debug_k2_prof_read(buf.ctypes.data, nc) == 0
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 np.save(os.path.join(ROOT, "gpurun_out", "k2prof.npy"), buf)
-names = ["read", "total", "mem", "ext", "cigar", "nmem", "nreg", "ext_rows", "cig_rows", "slot", "ext_calls", "traceback"]
+names = ["read", "total", "mem", "ext", "cigar", "nmem", "nreg", "ext_rows", "cig_rows", "ext_dp", "ext_calls", "traceback"]
 T = buf[:, 1].astype(np.int64)
 print(f"candidates {nc}; cycles/read mean {T.mean():.0f} p50 {np.median(T):.0f} p90 {np.percentile(T, 90):.0f} "
       f"p99 {np.percentile(T, 99):.0f} max {T.max()}")
-for k, nm in ((2, "mem"), (3, "ext"), (4, "cigar"), (11, "trace")):
+for k, nm in ((2, "mem"), (3, "ext"), (9, "ext_dp"), (4, "cigar"), (11, "trace")):
     v = buf[:, k].astype(np.int64)
     print(f"  {nm:6s} share {v.sum() / T.sum():.3f}  mean {v.mean():.0f}  p99 {np.percentile(v, 99):.0f}")
 for k in (5, 6, 7, 8, 10):
@@ -62,10 +62,11 @@ for k in (5, 6, 7, 8, 10):
 mapped = buf[:, 6] > 0
 print(f"  reads with regions {mapped.sum()}  cycles/read with regions {T[mapped].mean():.0f}, "
       f"without {T[~mapped].mean() if (~mapped).any() else 0:.0f}")
+for nm, (cc, rr) in (("ext w1", (12, 13)), ("ext gen", (14, 15))):
+    c, r = buf[:, cc].astype(np.int64).sum(), buf[:, rr].astype(np.int64).sum()
+    print(f"  {nm}: rows {r} cycles/row {c / max(r, 1):.0f} share of ext_dp {c / max(buf[:, 9].astype(np.int64).sum(), 1):.3f}")
 # cycles per extension row and per cigar row (least squares over reads with work)
 A = np.stack([buf[:, 7], buf[:, 8], np.ones(nc)], 1).astype(np.float64)
 coef, *_ = np.linalg.lstsq(A, (buf[:, 3] + buf[:, 4]).astype(np.float64), rcond=None)
 print(f"  fit ext+cigar cycles ~ {coef[0]:.0f}*ext_rows + {coef[1]:.0f}*cig_rows + {coef[2]:.0f}")
-slot_busy = np.bincount(buf[:, 9], weights=T)
-print(f"  slots {len(slot_busy)} busy cycles mean {slot_busy.mean():.0f} max {slot_busy.max():.0f} "
-      f"(max/mean {slot_busy.max() / slot_busy.mean():.2f}); items/slot max {np.bincount(buf[:, 9]).max()}")
+
