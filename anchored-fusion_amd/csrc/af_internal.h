@@ -45,17 +45,20 @@ struct ReadRec {
 };
 
 // launch helpers (defined in the .hip files)
-// ctrl (AF_CTRL_BYTES): [0] candidate count (zeroed per K1 call); K2 dequeue head x at
-// [AF_HEAD_STRIDE * (1 + x)], x = 0..7, one 128-B line each (zeroed per K2 call)
+// ctrl (AF_CTRL_BYTES, one 128-B line per word, no memsets on the hot path):
+//  [AF_HEAD_STRIDE * e], e = 0, 1: candidate count of K1 epoch e (K1 of epoch e zeroes the
+//                                  other epoch's count for the next call);
+//  [AF_HEAD_STRIDE * (2 + x)], x = 0..7: K2 dequeue heads (k_pairs zeroes them after K2).
 #define AF_HEAD_STRIDE 32
-#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 9)
+#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 10)
+#define AF_CTRL_HEADS (2 * AF_HEAD_STRIDE)
 size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,
+                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next, int n_cu,
                                  hipStream_t s);
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                            const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
-                           int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch,
-                           int32_t n_slots, hipStream_t s);
-hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
+                           int32_t *heads, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
                            hipStream_t s);
+hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
+                           int32_t *heads, hipStream_t s);

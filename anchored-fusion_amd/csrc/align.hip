@@ -594,13 +594,13 @@ __device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, in
 template <int CPL>
 __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
                                               const int32_t *__restrict__ lens, af_params p,
-                                              const int32_t *__restrict__ cand, const int32_t *__restrict__ ctrl,
+                                              const int32_t *__restrict__ cand, const int32_t *__restrict__ n_cand,
                                               int32_t *__restrict__ work, ReadRec *__restrict__ recs,
                                               uint32_t *__restrict__ cigar, uint8_t *__restrict__ zscratch,
                                               size_t zstride) {
     AlnLds &L = g_aln;
     const int lane = threadIdx.x;
-    const int ncand = ctrl[0];
+    const int ncand = *n_cand;
     uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
     const int64_t n = ix.n, n2 = 2 * ix.n;
     const int max_ext = p.max_ext < 16 ? p.max_ext : 16;
@@ -898,8 +898,9 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
 }
 
 __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const ReadRec *__restrict__ recs,
-                        af_aln_out out) {
+                        af_aln_out out, int32_t *__restrict__ heads) {
     const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 8) heads[AF_HEAD_STRIDE * threadIdx.x] = 0;  // K2 ran: reset its heads
     if (pp >= n_pairs) return;
     ReadRec R[2];
 #pragma unroll
@@ -945,31 +946,28 @@ extern "C" int af_debug_k2_prof_read(int32_t *host, int64_t n_items) {
 #endif
 
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *ctrl,
-                           int64_t cand_cap, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
+                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
+                           int32_t *heads, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
                            hipStream_t s) {
-    (void)n_reads; (void)cand_cap;
-    int32_t *work = const_cast<int32_t *>(ctrl) + AF_HEAD_STRIDE;  // 8 dequeue heads
-    hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t) * AF_HEAD_STRIDE * 8, s);
-    if (e != hipSuccess) return e;
+    (void)n_reads;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
     dim3 g(n_slots), b(64);
     if (cpl <= 2)
-        hipLaunchKernelGGL(k_align<2>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+        hipLaunchKernelGGL(k_align<2>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
     else if (cpl <= 3)
-        hipLaunchKernelGGL(k_align<3>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+        hipLaunchKernelGGL(k_align<3>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
     else if (cpl <= 4)
-        hipLaunchKernelGGL(k_align<4>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+        hipLaunchKernelGGL(k_align<4>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
     else
-        hipLaunchKernelGGL(k_align<AF_CPL>, g, b, 0, s, ix, reads, stride, lens, p, cand, ctrl, work, recs, cigar, zscratch, zstride);
+        hipLaunchKernelGGL(k_align<AF_CPL>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
     return hipGetLastError();
 }
 
 hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
-                           hipStream_t s) {
-    if (n_pairs <= 0) return hipSuccess;
+                           int32_t *heads, hipStream_t s) {
     const int bs = 256;
-    hipLaunchKernelGGL(k_pairs, dim3((unsigned)((n_pairs + bs - 1) / bs)), dim3(bs), 0, s, n_pairs, hits, recs, out);
+    const int64_t nb = n_pairs > 0 ? (n_pairs + bs - 1) / bs : 1;
+    hipLaunchKernelGGL(k_pairs, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, heads);
     return hipGetLastError();
 }

@@ -16,7 +16,8 @@ struct af_ctx {
     int n_slots = 0;
     std::string err;
     // scratch (device)
-    int32_t *ctrl = nullptr;   // af_internal.h: candidate count + K2 dequeue heads
+    int32_t *ctrl = nullptr;   // af_internal.h: candidate counts (2 epochs) + K2 dequeue heads
+    int64_t epoch = 0;         // seed-filter calls so far; the last call used count slot (epoch - 1) & 1
     int32_t *cand = nullptr;
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
@@ -135,6 +136,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 16;  // k_align: 4 waves per SIMD (VGPR and LDS budget)
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
+    if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         af_free(c->ctrl);
         delete c;
@@ -266,8 +268,10 @@ int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
     hipStream_t s = (hipStream_t)stream;
     int rc = ensure_reads_cap(c, n_reads);
     if (rc) return rc;
-    HIPCHK(c, hipMemsetAsync(c->ctrl, 0, 64, s));
-    HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand, c->ctrl, c->n_cu, s));
+    const int slot = (int)(c->epoch & 1);
+    HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand,
+                                    c->ctrl + AF_HEAD_STRIDE * slot, c->ctrl + AF_HEAD_STRIDE * (slot ^ 1), c->n_cu, s));
+    ++c->epoch;
     return AF_OK;
 }
 
@@ -276,7 +280,9 @@ int64_t af_last_candidates(af_ctx *c) {
     int32_t v = -1;
     (void)hipSetDevice(c->device);
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpy(&v, c->ctrl, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (c->epoch == 0) return 0;
+    const int slot = (int)((c->epoch - 1) & 1);
+    if (hipMemcpy(&v, c->ctrl + AF_HEAD_STRIDE * slot, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return v;
 }
 
@@ -306,9 +312,11 @@ int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_r
     const int64_t nr = 2 * n_pairs;
     if ((rc = ensure_zscratch(c))) return rc;
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, c->ctrl, c->cap_reads, c->recs,
-                              o->cigar, c->zscratch, c->n_slots, s));
-    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, s));
+    if (c->epoch == 0) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
+    const int slot = (int)((c->epoch - 1) & 1);
+    HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, c->ctrl + AF_HEAD_STRIDE * slot,
+                              c->ctrl + AF_CTRL_HEADS, c->recs, o->cigar, c->zscratch, c->n_slots, s));
+    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, c->ctrl + AF_CTRL_HEADS, s));
     return AF_OK;
 }
 

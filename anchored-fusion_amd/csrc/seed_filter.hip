@@ -94,7 +94,7 @@ template <bool HAS_LENS>
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const int32_t *__restrict__ lens,
     const uint2 *__restrict__ bloom_g, int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand,
-    int32_t *__restrict__ ctrl) {
+    int32_t *__restrict__ cnt_g, int32_t *__restrict__ cnt_next) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ uint64_t gbal[AF_SEED_GROUPS];  // per 64-read group: ballot of reads with hits
     __shared__ int gbase[AF_SEED_GROUPS];      // per group: first cand slot
@@ -104,6 +104,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
     const int bshift = 32 - bl_bits;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;  // next epoch's count (see af_internal.h)
     fill_lds(bloom, bloom_g, nbl);
 
     const int64_t ntiles = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
             }
             const int total = __shfl(incl, AF_SEED_GROUPS - 1);
             int basei = 0;
-            if (lane == 0 && total) basei = atomicAdd(&ctrl[0], total);
+            if (lane == 0 && total) basei = atomicAdd(cnt_g, total);
             basei = __shfl(basei, 0);
             if (lane < AF_SEED_GROUPS) gbase[lane] = basei + incl - c;
         }
@@ -222,9 +223,12 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
 size_t af_seed_filter_lds(int bl_bits) { return ((size_t)1 << bl_bits) * 8 + AF_SEED_BTILE; }
 
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *ctrl, int n_cu,
-                                 hipStream_t s) {
-    if (n_reads <= 0) return hipSuccess;
+                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next,
+                                 int n_cu, hipStream_t s) {
+    if (n_reads <= 0) {
+        hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int32_t), s);
+        return e == hipSuccess ? hipMemsetAsync(cnt_next, 0, sizeof(int32_t), s) : e;
+    }
     const int64_t want = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     const size_t lds = af_seed_filter_lds(ix.bl_bits);
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / (lds + 1024)));
@@ -243,9 +247,9 @@ hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64
     dim3 grid((unsigned)blocks), block(64 * AF_SEED_WAVES);
     if (lens)
         hipLaunchKernelGGL((k_seed_filter<true>), grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom,
-                           ix.bl_bits, hits, cand, ctrl);
+                           ix.bl_bits, hits, cand, cnt, cnt_next);
     else
         hipLaunchKernelGGL((k_seed_filter<false>), grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom,
-                           ix.bl_bits, hits, cand, ctrl);
+                           ix.bl_bits, hits, cand, cnt, cnt_next);
     return hipGetLastError();
 }
