@@ -898,9 +898,10 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
 }
 
 __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const ReadRec *__restrict__ recs,
-                        af_aln_out out, int32_t *__restrict__ heads) {
+                        af_aln_out out, int32_t *__restrict__ ctrl) {
     const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < 8) heads[AF_HEAD_STRIDE * threadIdx.x] = 0;  // K2 ran: reset its heads
+    if (blockIdx.x == 0 && threadIdx.x < 17)  // K2 ran: reset both head sets and the deferred count
+        ctrl[AF_CTRL_HEADS + AF_HEAD_STRIDE * threadIdx.x] = 0;
     if (pp >= n_pairs) return;
     ReadRec R[2];
 #pragma unroll
@@ -965,9 +966,9 @@ hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_r
 }
 
 hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
-                           int32_t *heads, hipStream_t s) {
+                           int32_t *ctrl, hipStream_t s) {
     const int bs = 256;
     const int64_t nb = n_pairs > 0 ? (n_pairs + bs - 1) / bs : 1;
-    hipLaunchKernelGGL(k_pairs, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, heads);
+    hipLaunchKernelGGL(k_pairs, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, ctrl);
     return hipGetLastError();
 }
