@@ -1,0 +1,127 @@
+"""CPU tests of the host restatements of the split-read consumer stages (SURVEY.md §8 a4-a8,
+a11, a12, a14) against golden fixtures produced by the reference's own functions.py
+(tests/golden/make_fixtures.py, canned tool outputs; see its docstring).
+"""
+import json
+import os
+
+import pytest
+
+import afpkg  # noqa: F401
+from anchored_fusion_amd import annotation, blocks, cigar, genome_check, report, splitreads
+
+FX_PATH = os.path.join(os.path.dirname(__file__), "golden", "consumers.json")
+
+
+@pytest.fixture(scope="module")
+def fx():
+    with open(FX_PATH) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def index(fx):
+    return annotation.ExonIndex.from_lines(fx["gtf"])
+
+
+def _plain(x):
+    """tuples -> lists, recursively (JSON has no tuples)."""
+    if isinstance(x, (list, tuple)):
+        return [_plain(v) for v in x]
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    return x
+
+
+def test_annotation_table(fx, index):
+    assert _plain(index.dic) == fx["gene_co"]
+
+
+def test_find_exon(fx, index):
+    for chrom, s, e, gene, k in fx["find_exon"]:
+        assert _plain(index.find_exon(chrom, s, e)) == [gene, k], (chrom, s, e)
+
+
+def test_find_positions(fx, index):
+    for chrom, p, ln, want, err in fx["find_positions"]:
+        assert err is None
+        assert _plain(index.walk(chrom, p, ln)) == want, (chrom, p, ln)
+
+
+def test_deal_cigar(fx):
+    for cig, seq, ops, seq2 in fx["deal_cigar"]:
+        got_ops, got_seq = cigar.normalize(cig, seq)
+        assert (got_ops, got_seq) == (ops, seq2), cig
+
+
+def test_reverse(fx):
+    for s, r in fx["reverse"]:
+        assert cigar.revcomp(s) == r
+
+
+def test_contact_reads(fx):
+    for lines, want in fx["contact_reads"]:
+        got = [list(r.as_tuple()) for r in splitreads.cluster_split_reads(lines)]
+        assert got == want
+
+
+def _dump(bc):
+    return {c: [list(b.as_tuple()) for b in bl] for c, bl in bc.items()}
+
+
+def test_find_blocks(fx, index):
+    homo = fx["homo_genes"]
+    for recs, want, err in fx["find_blocks"]:
+        assert err is None
+        assert _plain(_dump(blocks.spanning_blocks(recs, index, homo))) == want
+
+
+def test_find_fine_block(fx, index):
+    homo = fx["homo_genes"]
+    for lines, psl, base_recs, want, err in fx["find_fine_block"]:
+        assert err is None
+        base = blocks.spanning_blocks(base_recs, index, homo) if base_recs else {}
+        tails, fasta = blocks.split_read_queries(lines)
+        got = blocks.add_fine_blocks(base, tails, psl, index, homo)
+        assert _plain(_dump(got)) == want
+
+
+def test_del_too_many_reads(fx):
+    for anch, gsam, want in fx["del_too_many_reads"]:
+        fasta = genome_check.split_read_fasta(anch)
+        names = [n for n, _ in fasta]
+        # the genome SAM's queries are exactly the FASTA the function sends to bwa
+        assert {ln.split("\t")[0] for ln in gsam if not ln.startswith("@")} <= set(names)
+        assert genome_check.filter_genome_hits(gsam) == want
+
+
+def _split_row(row, n_fixed):
+    f = row.rstrip("\n").split("\t")
+    head, rest = f[:n_fixed], f[n_fixed:]
+    return head, [set(x.split(";")) - {""} for x in rest]
+
+
+def test_final_fusion(fx, index, tmp_path):
+    for case in fx["final_fusion"]:
+        cands = []
+        for c in case["spec"]:
+            obj = report.Candidate(c["type"])
+            for a in c["adds"]:
+                obj.add_reads(a["target"], list(a["other"]), a["left"], a["right"], a["mid"], a["cnt"],
+                              list(a["spanning"]), list(a["split"]))
+            obj.score = c["score"]
+            cands.append(obj)
+        for obj, want in zip(cands, case["maxpos"]):
+            pos, best = obj.find_max_pos()
+            assert list(pos) + [best] == want
+        scores = [c["score"] for c in case["spec"]]
+        prefix = str(tmp_path / "pred")
+        report.write_predictions(prefix, cands, "BCR", index, scores, case["cnt_max"], case["no_filter"])
+        with open(prefix + "_predictions_abridged.txt") as fa:
+            assert fa.readlines() == case["abridged"]
+        n_fixed = 7 if case["no_filter"] else 8   # read-name columns follow; order = set order
+        with open(prefix + "_predictions.txt") as fo:
+            got = fo.readlines()
+        assert len(got) == len(case["full"]) and got[0] == case["full"][0]
+        for g, w in zip(got[1:], case["full"][1:]):
+            assert _split_row(g, n_fixed) == _split_row(w, n_fixed)
