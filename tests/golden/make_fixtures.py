@@ -26,6 +26,11 @@ import types
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference"
+sys.path.insert(0, os.path.dirname(HERE))          # tests/ (fake_tools)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))  # repo root (afpkg)
+import fake_tools  # noqa: E402
+import afpkg  # noqa: E402,F401
+from anchored_fusion_amd.partner import PRESETS  # noqa: E402
 
 
 def load_reference():
@@ -82,6 +87,61 @@ class Canned:
         self.fn.os.popen, self.fn.os.system = self.orig_popen, self.orig_system
 
 
+class ToolSim:
+    """Runs the fake tools (tests/fake_tools.py) in place of blat / bedtools / bwa index, reading
+    the files functions.py wrote and writing where the tool would have written."""
+
+    def __init__(self, fn, genome_path, genome_targets):
+        self.fn, self.genome_path, self.genome = fn, genome_path, genome_targets
+        self.orig = fn.os.system
+        self.calls = []  # (preset, queries) of every blat call, in order
+
+    def __enter__(self):
+        self.fn.os.system = self.system
+        return self
+
+    def __exit__(self, *a):
+        self.fn.os.system = self.orig
+
+    def _fasta(self, path):
+        if path == self.genome_path:
+            return self.genome
+        with open(path) as fh:
+            return fake_tools.read_fasta_text(fh.read())
+
+    def system(self, cmd):
+        head, _, redirect = cmd.partition(">")
+        toks = head.split()
+        if toks[0] == "blat":
+            opts = " ".join(t for t in toks[1:] if t.startswith("-"))
+            files = [t for t in toks[1:] if not t.startswith("-")]
+            preset = next(k for k, v in PRESETS.items() if v == opts)
+            queries = self._fasta(files[1])
+            self.calls.append([preset, [list(q) for q in queries]])
+            out = fake_tools.blat(self._fasta(files[0]), queries, preset)
+            with open(files[2], "w") as fh:
+                fh.writelines(out)
+        elif toks[:2] == ["bedtools", "getfasta"]:
+            with open(toks[toks.index("-bed") + 1]) as fh:
+                rows = [ln.rstrip("\n").split("\t") for ln in fh if ln.strip()]
+            recs = [(f"{r[3]}::{r[0]}:{r[1]}-{r[2]}", fake_tools.genome_seq(r[0], int(r[1]), int(r[2]))) for r in rows]
+            with open(redirect.strip(), "w") as fh:
+                fh.write(fake_tools.fasta_text(recs))
+        elif toks[:2] == ["bedtools", "intersect"]:
+            a, b = toks[toks.index("-a") + 1], toks[toks.index("-b") + 1]
+            rows = []
+            for path in (a, b):
+                with open(path) as fh:
+                    rows.append([ln.rstrip("\n").split("\t") for ln in fh if ln.strip()])
+            with open(redirect.strip(), "w") as fh:
+                fh.writelines("\t".join(r) + "\n" for r in fake_tools.intersect_wa(rows[0], rows[1]))
+        elif toks[:2] == ["bwa", "index"]:
+            pass
+        else:
+            raise RuntimeError("unexpected tool call: " + cmd)
+        return 0
+
+
 # ---------------------------------------------------------------------------------------------
 # synthetic world
 # ---------------------------------------------------------------------------------------------
@@ -103,6 +163,9 @@ def make_gtf(rng):
                 exons.append((p, p + ln))
                 p += ln + rng.randint(150, 3000)
             genes.append((chrom, gene_id, name, exons))
+            lines.append("\t".join([chrom, "SYN", "gene", str(exons[0][0]), str(exons[-1][1]), ".",
+                                    rng.choice("+-"), ".", f'gene_id "{gene_id}"; gene_type "{tt_gene}"; '
+                                    f'gene_name "{name}"; level 2;']) + "\n")
             for t in range(rng.randint(1, 3)):
                 tt = tt_gene if t == 0 else rng.choice(["protein_coding", "artifact", "retained_intron",
                                                          "protein_coding_LoF", "unprocessed_pseudogene"])
@@ -286,6 +349,84 @@ def candidates_spec(rng, genes, n):
     return spec
 
 
+def dump_breakpoints(bps):
+    return [[b.chrom, b.breakpoint, b.type_, b.seq_left, b.seq_right, b.cnt, list(b.reads),
+             [list(o) for o in b.other_breakpoints]] for b in bps]
+
+
+def dump_candidate(c):
+    return dict(type=c.type_, pos=[list(p) for p in c.pos], left=c.return_seq_left(), right=c.return_seq_right(),
+                mid=c.return_seq_mid(), l=[c.l_left, c.l_mid, c.l_right], spanning=list(c.spanning_reads),
+                split=list(c.split_reads))
+
+
+def partner_trials(fn, rng, genes, gc, gtf_path, homo_ids, work):
+    """a9-a11, a13 and a14 chained on one synthetic sample per trial."""
+    chroms = sorted({g[0] for g in genes})
+    genome_targets = [(c, 400000) for c in chroms]
+    genome_path = os.path.join(work, "genome.fa")
+    anchor = ("BCR", rand_seq(rng, 3000))
+    anchor_path = os.path.join(work, "anchor.fa")
+    with open(anchor_path, "w") as fh:
+        fh.write(fake_tools.fasta_text([anchor]))
+    trials = []
+    homo = []
+    small_genome = [(c, 90000) for c in chroms]
+    with ToolSim(fn, genome_path, small_genome):
+        for k in range(12):
+            anc = (f"A{k}", rand_seq(rng, rng.randint(200, 3000)))
+            with open(anchor_path, "w") as fh:
+                fh.write(fake_tools.fasta_text([anc]))
+            bad = os.path.join(work, "homo.bed")
+            fn.Find_homo_genes(genome_path, anchor_path, gtf_path, os.path.join(work, "hg"), bad)
+            with open(bad) as fh:
+                homo.append([list(anc), fh.readlines()])
+    with open(anchor_path, "w") as fh:
+        fh.write(fake_tools.fasta_text([anchor]))
+    for trial in range(14):
+        if True:
+            spans = spanning_records(rng, genes, homo_ids, rng.randint(60, 200))
+            split = split_sam_lines(rng, "BCR", rng.randint(6, 16), rng.randint(2, 10))
+            with Canned(fn) as cn:
+                cn.popen_text = "".join(spans)
+                blocks_chr = fn.Find_blocks("spanning.bam", gc, homo_ids)
+            # the reference's widening can leave '' as a block end (find_positions found no
+            # downstream interval); Build_candidate_fasta would then raise TypeError.  The chain
+            # drops such blocks (the tests do the same: test_consumers.sanitize_blocks).
+            for c in list(blocks_chr):
+                blocks_chr[c] = [b for b in blocks_chr[c] if isinstance(b.start, int) and isinstance(b.end, int)]
+            cand_fa = os.path.join(work, f"cand{trial}.fa")
+            with ToolSim(fn, genome_path, genome_targets) as sim:
+                fn.Build_candidate_fasta(cand_fa, os.path.join(work, f"bc{trial}"), genome_path, anchor_path,
+                                         blocks_chr)
+                with open(cand_fa) as fh:
+                    cand_recs = fake_tools.read_fasta_text(fh.read())
+                split_path = os.path.join(work, f"psplit{trial}.sam")
+                with open(split_path, "w") as fh:
+                    fh.writelines(split)
+                bps = fn.contact_reads(split_path, work, genome_path, "1")
+                good = fn.Find_Anchored_split(os.path.join(work, f"fa{trial}"), cand_fa, blocks_chr, bps, gc,
+                                              anchor_path)
+                after_a9 = dict(good=sorted(good), breakpoints=dump_breakpoints(bps),
+                                anchored={c: [sorted(b.anchored_split_breakpoints) for b in bl]
+                                          for c, bl in blocks_chr.items()})
+                try:
+                    cands, cnt_max = fn.Find_candidate_genes(os.path.join(work, f"cg{trial}"), genome_path, good,
+                                                             bps, blocks_chr, gc, "1")
+                    a11 = dict(candidates=[dump_candidate(c) for c in cands], cnt_max=cnt_max, error=None)
+                except Exception as e:  # noqa: BLE001
+                    cands, a11 = [], dict(candidates=None, cnt_max=None, error=type(e).__name__)
+            prefix = os.path.join(work, f"final{trial}")
+            fn.Final_fusion(prefix, cands, "BCR", gc, [], a11["cnt_max"] or 0, True)
+            with open(prefix + "_predictions_abridged.txt") as fa, open(prefix + "_predictions.txt") as fo:
+                final = dict(abridged=fa.readlines(), full=fo.readlines())
+            trials.append(dict(spanning=spans, split=split, blocks_after_a10={
+                c: [[b.chrom, b.start, b.end, b.count] for b in bl] for c, bl in blocks_chr.items()},
+                candidate_records=cand_recs, a9=after_a9, a11=a11, final=final, blat_calls=sim.calls))
+    return dict(genome=genome_targets, small_genome=small_genome, anchor=list(anchor), homologs=homo,
+                trials=trials)
+
+
 def main():
     fn = load_reference()
     rng = random.Random(20251015)
@@ -429,6 +570,7 @@ def main():
             fin.append(dict(spec=spec, no_filter=no_filter, cnt_max=cnt_max, maxpos=maxpos,
                             abridged=fa.readlines(), full=fo.readlines()))
     fx["final_fusion"] = fin
+    fx["partner"] = partner_trials(fn, rng, genes, gc, gtf_path, homo_ids, work)
     with open(os.path.join(HERE, "consumers.json"), "w") as fh:
         json.dump(fx, fh, separators=(",", ":"))
     print("wrote", os.path.join(HERE, "consumers.json"), {k: len(v) for k, v in fx.items() if isinstance(v, list)})

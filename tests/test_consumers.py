@@ -125,3 +125,14 @@ def test_final_fusion(fx, index, tmp_path):
         assert len(got) == len(case["full"]) and got[0] == case["full"][0]
         for g, w in zip(got[1:], case["full"][1:]):
             assert _split_row(g, n_fixed) == _split_row(w, n_fixed)
+
+
+def test_partner_chain():
+    """a9 -> a10 -> a11 -> a13 -> a14 replayed against the reference's outputs (and the
+    exact sequence of tool queries it issued), in a PYTHONHASHSEED=0 subprocess."""
+    import subprocess
+    import sys
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "partner_chain.py")],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
