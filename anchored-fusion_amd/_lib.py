@@ -33,7 +33,7 @@ EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_blocks", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates",
+    "af_last_candidates", "af_place",
 )
 
 
@@ -102,6 +102,8 @@ def lib():
     L.af_seed_filter_device.restype = ctypes.c_int
     L.af_last_candidates.argtypes = [_vp]
     L.af_last_candidates.restype = _i64
+    L.af_place.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _i32, _vp, _vp]
+    L.af_place.restype = ctypes.c_int
     _L = L
     return L
 

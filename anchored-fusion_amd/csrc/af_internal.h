@@ -52,10 +52,13 @@ struct ReadRec {
 //  [AF_HEAD_STRIDE * (10 + x)]: dequeue heads of the wave-per-read K2 (deferred reads);
 //  [AF_HEAD_STRIDE * 18]: deferred-read count.  k_pairs zeroes heads and count after K2.
 #define AF_HEAD_STRIDE 32
-#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 19)
+#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 29)
 #define AF_CTRL_HEADS (2 * AF_HEAD_STRIDE)
 #define AF_CTRL_HEADS2 (10 * AF_HEAD_STRIDE)
 #define AF_CTRL_NDEFER (18 * AF_HEAD_STRIDE)
+//  [AF_HEAD_STRIDE * (19 + x)]: dequeue heads of af_place; [AF_HEAD_STRIDE * 27]: its query count.
+#define AF_CTRL_PLACE_HEADS (19 * AF_HEAD_STRIDE)
+#define AF_CTRL_PLACE_N (27 * AF_HEAD_STRIDE)
 #define AF_LANE_Z 8192                          // traceback bytes per lane (larger: deferred)
 #define AF_LANE_SCRATCH (1024 + AF_LANE_Z + 256)  // per-lane global scratch of the lane K2
 size_t af_seed_filter_lds(int bl_bits);
@@ -68,6 +71,9 @@ hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_r
                            hipStream_t s);
 hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
                            int32_t *ctrl, hipStream_t s);
+hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
+                           const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
+                           int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
 size_t af_align_lane_lds(int32_t stride);
 bool af_lane_params_ok(const af_params &p, int32_t stride);
 hipError_t af_launch_align_lane(const DevIndex &ix, const uint8_t *reads, int32_t stride, const int32_t *lens,

@@ -591,13 +591,16 @@ __device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, in
     return score;
 }
 
-template <int CPL>
+// MULTI = placement mode (af_place): every region scoring >= T becomes an af_hit (best first,
+// at most max_hits per query); cand == nullptr means "all reads".
+template <int CPL, bool MULTI>
 __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
                                               const int32_t *__restrict__ lens, af_params p,
                                               const int32_t *__restrict__ cand, const int32_t *__restrict__ n_cand,
                                               int32_t *__restrict__ work, ReadRec *__restrict__ recs,
                                               uint32_t *__restrict__ cigar, uint8_t *__restrict__ zscratch,
-                                              size_t zstride) {
+                                              size_t zstride, af_hit *__restrict__ hits, int32_t *__restrict__ n_hits,
+                                              int32_t max_hits) {
     AlnLds &L = g_aln;
     const int lane = threadIdx.x;
     const int ncand = *n_cand;
@@ -631,7 +634,7 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
             }
             if (item >= ncand) break;
         }
-        const int64_t r = cand[item];
+        const int64_t r = cand ? cand[item] : item;
         PROF(const int64_t pt0 = clock64(); int64_t pt1 = pt0, pt2 = pt0; int p_ext_rows = 0, p_cig_rows = 0,
              p_ext_calls = 0, p_nreg = 0, p_ext_dp = 0;)
         int l = lens ? lens[r] : stride;
@@ -821,12 +824,12 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                 ++n_reg;
             }
             PROF(pt2 = clock64(); p_nreg = n_reg;)
-            int best = -1;
-            for (int rr = 0; rr < n_reg; ++rr)
-                if (best < 0 || L.regs[rr][0] > L.regs[best][0]) best = rr;
-            if (best >= 0 && L.regs[best][0] >= p.T) {
-                // ---- 4. CIGAR --------------------------------------------------------
-                const int *a = L.regs[best];
+            // ---- 4. CIGAR of a region (bwa_gen_cigar2 + the band retry loop) -------------
+            // Lane 0 writes the assembled ops to `co` and the record fields; with `want_mt`
+            // every lane also gets the identical-base count and reference span of the
+            // alignment (the oracle's emit_region, over its first AF_MAX_CIGAR ops).
+            auto emit = [&](const int *a, uint32_t *co, int &o_flag, int &o_pos, int &o_score, int &o_nc,
+                            bool want_mt, int &o_mt, int &o_span) {
                 const int a_score = a[0], a_truesc = a[1], aqb = a[2], aqe = a[3], awb = a[7];
                 const int64_t arb = a[4], are = a[5];
                 const bool is_rev = arb >= n;
@@ -844,12 +847,33 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                     last_sc = score;
                     w2 <<= 1;
                 } while (++it < 3 && score < a_truesc - p.a);
+                const int nc = L.misc[2];
+                const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
+                if (want_mt) {
+                    int mt = 0, span = 0, x = 0, y = 0;
+                    for (int k = 0; k < ncap; ++k) {
+                        const uint32_t op = L.ring[(nc - 1 - k) & 63];
+                        const int len = (int)(op >> 4), o = (int)(op & 0xf);
+                        if (o == 0) {
+                            for (int u = lane; u < len; u += 64) mt += (L.qs[x + u] < 4 && L.qs[x + u] == L.t[y + u]);
+                            x += len; y += len; span += len;
+                        } else if (o == 1) {
+                            x += len;
+                        } else {
+                            y += len; span += len;
+                        }
+                    }
+                    if (ncap > 0) {
+                        const uint32_t f0 = L.ring[(nc - 1) & 63], fl = L.ring[(nc - ncap) & 63];
+                        if ((f0 & 0xf) == 2) span -= (int)(f0 >> 4);
+                        else if ((fl & 0xf) == 2) span -= (int)(fl >> 4);
+                    }
+                    o_mt = wave_sum(mt);
+                    o_span = span;
+                }
                 // assemble: ring holds the traceback in reverse order (count misc[2])
                 if (lane == 0) {
-                    const int nc = L.misc[2];
-                    const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
                     bool of = nc > AF_MAX_CIGAR;
-                    uint32_t *co = cigar + r * AF_MAX_CIGAR;
                     int64_t pos = is_rev ? n2 - are : arb;
                     int xs = 0, xe = ncap;  // window of ring entries (forward order)
                     const uint32_t first = L.ring[(nc - 1) & 63];
@@ -871,14 +895,55 @@ __global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__rest
                         ++nf;
                     }
                     if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
-                    flag = (is_rev ? 0x10 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
-                    out_pos = (int)pos;
-                    out_score = a_score;
-                    out_nc = nf;
+                    o_flag = (is_rev ? 0x10 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
+                    o_pos = (int)pos;
+                    o_score = a_score;
+                    o_nc = nf;
                 }
+                wave_sync();
+            };
+            if (!MULTI) {
+                int best = -1;
+                for (int rr = 0; rr < n_reg; ++rr)
+                    if (best < 0 || L.regs[rr][0] > L.regs[best][0]) best = rr;
+                if (best >= 0 && L.regs[best][0] >= p.T) {
+                    int mt_unused = 0, span_unused = 0;
+                    emit(L.regs[best], cigar + r * AF_MAX_CIGAR, flag, out_pos, out_score, out_nc, false, mt_unused,
+                         span_unused);
+                }
+            } else {
+                // every region scoring >= T, best first (ties: region order), at most max_hits
+                int32_t *order = reinterpret_cast<int32_t *>(L.mem);
+                if (lane < n_reg) {
+                    const int me = L.regs[lane][0];
+                    int rank = 0;
+                    for (int u = 0; u < n_reg; ++u) {
+                        const int su = L.regs[u][0];
+                        rank += su > me || (su == me && u < lane);
+                    }
+                    order[rank] = lane;
+                }
+                wave_sync();
+                int nh = 0;
+                for (int k = 0; k < n_reg && nh < max_hits; ++k) {
+                    const int *a = L.regs[order[k]];
+                    if (a[0] < p.T) break;
+                    af_hit *h = hits + r * max_hits + nh;
+                    int hf = 0, hp = 0, hs = 0, hn = 0, mt = 0, span = 0;
+                    emit(a, h->cigar, hf, hp, hs, hn, true, mt, span);
+                    if (lane == 0) {
+                        h->query = (int32_t)r; h->flag = hf; h->score = hs;
+                        h->q_start = a[2]; h->q_end = a[3]; h->q_size = l; h->matches = mt;
+                        h->n_cigar = hn; h->t_start = hp; h->t_end = (int64_t)hp + span;
+                        for (int c = hn; c < AF_MAX_CIGAR; ++c) h->cigar[c] = 0;
+                    }
+                    ++nh;
+                }
+                if (lane == 0) n_hits[r] = nh;
             }
         }
-        if (lane == 0) {
+        if (MULTI && nm_total > max_mems && lane == 0) n_hits[r] = -1;
+        if (!MULTI && lane == 0) {
             ReadRec rec;
             rec.flag = flag; rec.pos = out_pos; rec.score = out_score; rec.n_cigar = out_nc;
             recs[r] = rec;
@@ -954,14 +1019,29 @@ hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_r
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
     dim3 g(n_slots), b(64);
-    if (cpl <= 2)
-        hipLaunchKernelGGL(k_align<2>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
-    else if (cpl <= 3)
-        hipLaunchKernelGGL(k_align<3>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
-    else if (cpl <= 4)
-        hipLaunchKernelGGL(k_align<4>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
-    else
-        hipLaunchKernelGGL(k_align<AF_CPL>, g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, recs, cigar, zscratch, zstride);
+#define AF_GO(C) hipLaunchKernelGGL((k_align<C, false>), g, b, 0, s, ix, reads, stride, lens, p, cand, n_cand, heads, \
+                                    recs, cigar, zscratch, zstride, nullptr, nullptr, 0)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}
+
+hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
+                           const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
+                           int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s) {
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    const int cpl = (stride + 1 + 63) / 64;
+    dim3 g(n_slots), b(64);
+#define AF_GO(C) hipLaunchKernelGGL((k_align<C, true>), g, b, 0, s, ix, reads, stride, lens, p, nullptr, n_queries, \
+                                    heads, nullptr, nullptr, zscratch, zstride, hits, n_hits, max_hits)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
     return hipGetLastError();
 }
 

@@ -27,6 +27,11 @@ struct af_ctx {
     uint8_t *lane_scratch = nullptr;  // lane-per-read K2: AF_LANE_SCRATCH bytes per lane
     int32_t *defer = nullptr;         // reads the lane K2 hands to the wave K2
     int lane_waves = 0;
+    // af_place staging (host-buffer API)
+    uint8_t *p_q = nullptr;
+    int32_t *p_lens = nullptr, *p_nhits = nullptr;
+    af_hit *p_hits = nullptr;
+    int64_t p_cap_bytes = 0, p_cap_q = 0, p_cap_hits = 0;
     int lane_stride = 0;
     // host-API staging (device)
     uint8_t *d_reads = nullptr;
@@ -174,6 +179,7 @@ void af_ctx_destroy(af_ctx *c) {
     (void)hipSetDevice(c->device);
     af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch);
     af_free(c->lane_scratch); af_free(c->defer);
+    af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
     af_free(c->d_cigar);
@@ -403,6 +409,53 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
     if (out->hits) HIPCHK(c, hipMemcpyAsync(out->hits, c->d_hits, 4 * nr, hipMemcpyDeviceToHost, s));
     if (out->cigar)
         HIPCHK(c, hipMemcpyAsync(out->cigar, c->d_cigar, sizeof(uint32_t) * AF_MAX_CIGAR * nr, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return AF_OK;
+}
+
+int af_place(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_queries, int32_t stride,
+             const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits) {
+    static_assert(sizeof(af_hit) == 176, "af_hit layout is part of the C-ABI");
+    if (!c || !ix || !hits || !n_hits || (!queries && n_queries)) return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
+    if (n_queries == 0) return AF_OK;
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    if (max_hits < 1 || max_hits > 16) return fail(c, AF_E_INVALID, "max_hits must be in [1, 16]");
+    if (lens)
+        for (int64_t i = 0; i < n_queries; ++i)
+            if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_zscratch(c))) return rc;
+    const int64_t bytes = n_queries * (int64_t)stride, nh = n_queries * (int64_t)max_hits;
+    if (bytes > c->p_cap_bytes) {
+        af_free(c->p_q); c->p_q = nullptr; c->p_cap_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->p_q, bytes + 64));
+        c->p_cap_bytes = bytes;
+    }
+    if (n_queries > c->p_cap_q) {
+        af_free(c->p_lens); af_free(c->p_nhits); c->p_lens = c->p_nhits = nullptr; c->p_cap_q = 0;
+        HIPCHK(c, hipMalloc(&c->p_lens, 4 * n_queries + 64));
+        HIPCHK(c, hipMalloc(&c->p_nhits, 4 * n_queries + 64));
+        c->p_cap_q = n_queries;
+    }
+    if (nh > c->p_cap_hits) {
+        af_free(c->p_hits); c->p_hits = nullptr; c->p_cap_hits = 0;
+        HIPCHK(c, hipMalloc(&c->p_hits, sizeof(af_hit) * nh));
+        c->p_cap_hits = nh;
+    }
+    hipStream_t s = c->stream;
+    const int32_t nq = (int32_t)n_queries;
+    HIPCHK(c, hipMemcpyAsync(c->p_q, queries, bytes, hipMemcpyHostToDevice, s));
+    if (lens) HIPCHK(c, hipMemcpyAsync(c->p_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
+    HIPCHK(c, hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, af_launch_place(ix->dev, c->p_q, c->ctrl + AF_CTRL_PLACE_N, stride, lens ? c->p_lens : nullptr, *p,
+                              c->ctrl + AF_CTRL_PLACE_HEADS, c->zscratch, c->n_slots, c->p_hits, c->p_nhits, max_hits,
+                              s));
+    HIPCHK(c, hipMemcpyAsync(hits, c->p_hits, sizeof(af_hit) * nh, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(n_hits, c->p_nhits, 4 * n_queries, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     return AF_OK;
 }

@@ -1,0 +1,255 @@
+"""GPU tail placement: the searches behind the partner stages (SURVEY.md §8 a4, a5, a7, a9,
+a10, a11, a13).
+
+The reference shells out for each of these searches:
+
+- `bwa mem` of the one-end-anchored pairs vs the genome (Anchored_Fusion.py:188);
+- `bwa mem` of the anchored split reads vs the genome (functions.py:716);
+- BLAT of tails and candidates vs the genome, the candidate blocks and the anchor
+  (functions.py:341, 530, 966, 1007, 1071, 1122, 1244).
+
+Here one GPU multi-hit placement kernel (`af_place`, the K2 seed-and-extend in placement
+mode) serves all of them:
+
+- `Reference` joins contigs with runs of 512 N and indexes them once. Seeds cannot cross an
+  N run, and extension cannot score across one.
+- Every query gets up to 16 local alignments scoring at least T, best first. Each has a CIGAR,
+  forward query coordinates and the identical-base count.
+- `Placer` is the `place(targets, queries, preset)` callback the partner stages take
+  (partner.py). It renders hits as PSL rows, and `sam_records` renders them as SAM records for
+  the genome-alignment consumers.
+
+Placement parity with BLAT / bwa themselves is unpinned: neither is available (SURVEY.md §8 c).
+The kernel is bit-exact against oracle/af_oracle.c `afo_place` (tests/test_gpu_place.py).
+BLAT presets map onto the local aligner as follows:
+
+- minScore -> T;
+- minIdentity -> matches / max(query span, target span);
+- stepSize / minMatch / repMatch have no counterpart.
+
+Seeds are 16-mers, the smallest the index supports.
+"""
+import bisect
+import ctypes
+import re
+
+import numpy as np
+
+from . import _lib
+
+SEP = 512  # N run between contigs
+HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_start", "<i4"), ("q_end", "<i4"),
+                      ("q_size", "<i4"), ("matches", "<i4"), ("n_cigar", "<i4"), ("t_start", "<i8"),
+                      ("t_end", "<i8"), ("cigar", "<u4", (32,))])
+assert HIT_DTYPE.itemsize == 176
+
+# BLAT option sets used by the reference -> (T, min identity %)
+PRESET_PARAMS = {
+    "homologs": (50, 80),            # fn:341
+    "split_tail": (20, 0),           # fn:530
+    "candidate_homolog": (20, 0),    # fn:966
+    "anchored_split": (12, 90),      # fn:1007, 1071, 1122
+    "genome_validate": (20, 90),     # fn:1244
+    "genome_bwa": (30, 0),           # AF:188, fn:716 (bwa mem -T 30)
+}
+
+_OPS = "MIDNSHP=X"
+
+
+def cigar_string(ops):
+    return "".join(f"{int(c) >> 4}{_OPS[int(c) & 15]}" for c in ops)
+
+
+def pack_queries(seqs):
+    stride = max(1, max((len(s) for s in seqs), default=1))
+    if stride > _lib.AF_MAX_READ:
+        raise ValueError(f"query longer than {_lib.AF_MAX_READ}")
+    buf = np.full((len(seqs), stride), ord("N"), dtype=np.uint8)
+    lens = np.zeros(len(seqs), dtype=np.int32)
+    for i, s in enumerate(seqs):
+        b = s.encode() if isinstance(s, str) else bytes(s)
+        buf[i, :len(b)] = np.frombuffer(b, dtype=np.uint8)
+        lens[i] = len(b)
+    return buf, lens
+
+
+def concat_contigs(contigs):
+    """Contigs [(name, seq)] -> (joined bytes, contig offsets); SEP N's between contigs."""
+    parts, offsets, off = [], [], 0
+    for k, (_, seq) in enumerate(contigs):
+        if k:
+            parts.append("N" * SEP)
+            off += SEP
+        offsets.append(off)
+        parts.append(seq)
+        off += len(seq)
+    blob = "".join(parts).encode()
+    return (blob if blob else b"N"), offsets
+
+
+class Reference:
+    """Contigs [(name, seq)] indexed on the GPU for af_place."""
+
+    def __init__(self, contigs, device=0, ctx=None):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob, self.offsets = concat_contigs(contigs)
+        self.total = len(blob)
+        L = _lib.lib()
+        self._own_ctx = ctx is None
+        if ctx is None:
+            ctx = ctypes.c_void_p()
+            _lib.check(None, L.af_ctx_create(int(device), ctypes.byref(ctx)), "af_ctx_create")
+        self.ctx = ctx
+        self.idx = ctypes.c_void_p()
+        _lib.check(self.ctx, L.af_index_build(self.ctx, blob, len(blob), ctypes.byref(self.idx)), "af_index_build")
+
+    def close(self):
+        L = _lib.lib()
+        if getattr(self, "idx", None):
+            L.af_index_free(self.idx)
+            self.idx = None
+        if getattr(self, "_own_ctx", False) and getattr(self, "ctx", None):
+            L.af_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def raw_hits(self, seqs, params=None, max_hits=16):
+        """af_place on packed queries -> (hits structured array [n, max_hits], n_hits [n])."""
+        buf, lens = pack_queries(seqs)
+        n = len(seqs)
+        hits = np.zeros((n, max_hits), dtype=HIT_DTYPE)
+        nh = np.zeros(n, dtype=np.int32)
+        if n == 0:
+            return hits, nh
+        p = params or _lib.default_params()
+        rc = _lib.lib().af_place(self.ctx, self.idx, buf.ctypes.data, n, buf.shape[1], lens.ctypes.data,
+                                 ctypes.byref(p), max_hits, hits.ctypes.data, nh.ctypes.data)
+        _lib.check(self.ctx, rc, "af_place")
+        return hits, nh
+
+    def locate(self, t_start, t_end):
+        """Concatenated forward coordinates -> (contig index, local start, local end) or None."""
+        k = bisect.bisect_right(self.offsets, int(t_start)) - 1
+        if k < 0:
+            return None
+        s, e = int(t_start) - self.offsets[k], int(t_end) - self.offsets[k]
+        if s < 0 or e > self.lens[k] or e <= s:
+            return None
+        return k, s, e
+
+
+def _cigar_counts(ops):
+    """(q inserts, q inserted bases, t inserts, t inserted bases, block sizes, q starts, t starts)."""
+    qi = qb = ti = tb = 0
+    sizes, qs, ts = [], [], []
+    x = y = 0
+    for c in ops:
+        n, o = int(c) >> 4, int(c) & 15
+        if o == 0:
+            sizes.append(n); qs.append(x); ts.append(y)
+            x += n; y += n
+        elif o == 1:
+            qi += 1; qb += n; x += n
+        elif o == 2:
+            ti += 1; tb += n; y += n
+        elif o == 4:
+            x += n
+    return qi, qb, ti, tb, sizes, qs, ts
+
+
+def psl_rows(ref, queries, hits, nh, min_identity=0):
+    """PSL lines (BLAT column layout) for the hits of queries [(name, seq)]."""
+    out = []
+    for qi, (qname, qseq) in enumerate(queries):
+        for k in range(max(int(nh[qi]), 0)):
+            h = hits[qi, k]
+            loc = ref.locate(h["t_start"], h["t_end"])
+            if loc is None:
+                continue
+            tk, ts, te = loc
+            qsp, tsp = int(h["q_end"] - h["q_start"]), te - ts
+            if min_identity and 100 * int(h["matches"]) < min_identity * max(qsp, tsp, 1):
+                continue
+            ops = h["cigar"][:int(h["n_cigar"])]
+            q_ins, q_ins_b, t_ins, t_ins_b, sizes, qst, tst = _cigar_counts(ops)
+            strand = "-" if h["flag"] & 0x10 else "+"
+            aligned = sum(sizes)
+            mism = aligned - int(h["matches"])
+            lead = int(ops[0]) >> 4 if len(ops) and (int(ops[0]) & 15) == 4 else 0
+            qs_list = ",".join(str(lead + v) for v in qst) + ","
+            ts_list = ",".join(str(ts + v) for v in tst) + ","
+            f = [int(h["matches"]), mism, 0, 0, q_ins, q_ins_b, t_ins, t_ins_b, strand, qname, len(qseq),
+                 int(h["q_start"]), int(h["q_end"]), ref.names[tk], ref.lens[tk], ts, te, len(sizes),
+                 ",".join(map(str, sizes)) + ",", qs_list, ts_list]
+            out.append("\t".join(map(str, f)) + "\n")
+    return out
+
+
+def sam_records(ref, queries, hits, nh, flag_extra=0):
+    """SAM lines (primary first, the rest 0x100) of the hits of queries [(name, seq)]."""
+    comp = str.maketrans("ACGTNacgtn", "TGCANtgcan")
+    out = []
+    for qi, (qname, qseq) in enumerate(queries):
+        n = max(int(nh[qi]), 0)
+        if n == 0:
+            out.append(f"{qname}\t{4 | flag_extra}\t*\t0\t0\t*\t*\t0\t0\t{qseq}\t*\n")
+            continue
+        for k in range(n):
+            h = hits[qi, k]
+            loc = ref.locate(h["t_start"], h["t_end"])
+            if loc is None:
+                continue
+            tk, ts, _ = loc
+            rev = bool(h["flag"] & 0x10)
+            seq = qseq.translate(comp)[::-1] if rev else qseq
+            flag = (0x10 if rev else 0) | (0x100 if k else 0) | flag_extra
+            out.append(f"{qname}\t{flag}\t{ref.names[tk]}\t{ts + 1}\t60\t{cigar_string(h['cigar'][:int(h['n_cigar'])])}"
+                       f"\t*\t0\t0\t{seq}\t*\n")
+    return out
+
+
+class Placer:
+    """The `place(targets, queries, preset)` callback of partner.py on the GPU.
+
+    Targets are indexed once per distinct target set (by identity of the list or its content)."""
+
+    def __init__(self, device=0, max_hits=16):
+        self.device, self.max_hits = device, max_hits
+        self._refs = {}
+
+    def reference(self, targets):
+        key = tuple((n, len(s) if isinstance(s, str) else s) for n, s in targets)
+        ref = self._refs.get(key)
+        if ref is None:
+            ref = Reference([(n, s) for n, s in targets], device=self.device)
+            self._refs[key] = ref
+        return ref
+
+    def params(self, preset):
+        T, _ = PRESET_PARAMS[preset]
+        p = _lib.default_params()
+        p.T = T
+        p.min_seed_len = _lib.AF_K
+        return p
+
+    def __call__(self, targets, queries, preset):
+        header = ["psLayout version 3\n", "\n"]
+        if not targets or not queries:
+            return header
+        ref = self.reference(targets)
+        hits, nh = ref.raw_hits([s for _, s in queries], self.params(preset), self.max_hits)
+        return header + psl_rows(ref, queries, hits, nh, PRESET_PARAMS[preset][1])
+
+    def close(self):
+        for r in self._refs.values():
+            r.close()
+        self._refs.clear()
+
+
+_FASTA_NAME = re.compile(r"^>(\S+)")

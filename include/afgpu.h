@@ -69,6 +69,20 @@ typedef struct {
     uint32_t *cigar;
 } af_aln_out;
 
+/* One placement of a query on a reference (af_place).  Replaces one PSL row of the
+ * reference's BLAT searches (functions.py:341, 530, 1007, 1071, 1122, 1244) and one SAM record
+ * of its genome `bwa mem` calls (Anchored_Fusion.py:188, functions.py:716). */
+typedef struct {
+    int32_t query;                  /* query index                                               */
+    int32_t flag;                   /* 0x10 reverse strand | AF_FLAG_CIGAR_OVERFLOW              */
+    int32_t score;                  /* local alignment score (bwa extension score)               */
+    int32_t q_start, q_end, q_size; /* forward query coordinates (PSL qStart, qEnd, qSize)       */
+    int32_t matches;                /* identical aligned bases (PSL matches)                     */
+    int32_t n_cigar;
+    int64_t t_start, t_end;         /* reference span, 0-based forward coordinates of the index  */
+    uint32_t cigar[AF_MAX_CIGAR];   /* SAM CIGAR with soft clips (reverse hits: revcomp query)   */
+} af_hit;
+
 int af_ctx_create(int device, af_ctx **out);
 void af_ctx_destroy(af_ctx *ctx);
 const char *af_last_error(const af_ctx *ctx);
@@ -98,6 +112,16 @@ int af_align_candidates_device(af_ctx *ctx, const af_index *idx, const uint8_t *
                                void *stream);
 /* number of candidate reads found by the last seed-filter pass on this context (synchronises) */
 int64_t af_last_candidates(af_ctx *ctx);
+
+/* Multi-hit placement of queries (ASCII, `stride` bytes per row, optional lens) on an index
+ * built with af_index_build over any reference (anchor, candidate blocks, or contigs joined by
+ * N runs).  Every seed-extended region scoring >= p->T is reported, best score first, at most
+ * max_hits (1..16) per query: hits[q * max_hits + k] for k < n_hits[q]; n_hits[q] = -1 marks a
+ * query with more than p->max_mems MEMs.  Host buffers; synchronous.
+ * Replaces: functions.py BLAT calls (fn:341, 530, 1007, 1071, 1122, 1244) and the genome
+ * `bwa mem` calls (AF:188, fn:716). */
+int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,
+             const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits);
 
 #ifdef __cplusplus
 }

@@ -51,6 +51,9 @@ def lib():
         L.afo_seed_filter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p]
         L.afo_align_pairs.restype = ctypes.c_int
+        L.afo_place.restype = ctypes.c_int
+        L.afo_place.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.afo_align_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int,
                                       ctypes.POINTER(_Out)]
@@ -106,3 +109,22 @@ class OracleIndex:
         if rc != 0:
             raise RuntimeError(f"afo_align_pairs failed: {rc}")
         return out
+
+    def place(self, reads, lens=None, params=None, max_hits=16, threads=0):
+        """Multi-hit placement (afo_place): (hits [n, max_hits] structured, n_hits [n])."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        hits = np.zeros((n, max_hits), dtype=HIT_DTYPE)
+        nh = np.zeros(n, dtype=np.int32)
+        p = params or default_params()
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = lib().afo_place(self.h, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
+                             ctypes.byref(p), max_hits, int(threads), hits.ctypes.data, nh.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"afo_place failed: {rc}")
+        return hits, nh
+
+
+HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_start", "<i4"), ("q_end", "<i4"),
+                      ("q_size", "<i4"), ("matches", "<i4"), ("n_cigar", "<i4"), ("t_start", "<i8"),
+                      ("t_end", "<i8"), ("cigar", "<u4", (32,))])

@@ -341,6 +341,9 @@ typedef struct { int32_t flag, pos, score, n_cigar; uint32_t cigar[AFO_MAX_CIGAR
 #define FLAG_MEM_OVERFLOW 0x10000
 #define FLAG_CIGAR_OVERFLOW 0x20000
 
+static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_params *p, const reg_t *a,
+                        rec_t *out, int *matches, int *ref_span);
+
 /* MEM search on the doubled reference (SMEM seeding of bwa mem, restated as all MEMs
  * >= min_seed_len whose first 16-mer occurs <= max_occ times) */
 static int find_mems(const afo_index *I, const uint8_t *q, int l, const afo_params *p, mem_t *mems, int *overflow) {
@@ -460,17 +463,15 @@ static int gen_cigar(const afo_index *I, const afo_params *p, int w_, int lq, co
     return score;
 }
 
-static void align_read(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, rec_t *out) {
-    uint8_t q[AFO_MAX_READ];
+/* seeds -> extended regions for one read (the body of mem_align1_core restated for one
+ * anchor-like reference); returns n_reg, -1 on MEM overflow.  q: the read's codes. */
+static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, uint8_t *q,
+                        reg_t *regs) {
     mem_t *mems = (mem_t *)malloc(sizeof(mem_t) * (p->max_mems > 0 ? p->max_mems : 1));
-    reg_t regs[64];
     int n_reg = 0, overflow = 0;
-    memset(out, 0, sizeof(*out));
-    out->flag = 0x4;
-    if (l > AFO_MAX_READ) l = AFO_MAX_READ;
     for (int i = 0; i < l; ++i) q[i] = nt4(ascii[i]);
     int nm = find_mems(I, q, l, p, mems, &overflow);
-    if (overflow) { out->flag |= FLAG_MEM_OVERFLOW; free(mems); return; }
+    if (overflow) { free(mems); return -1; }
     qsort(mems, nm, sizeof(mem_t), cmp_mem);
     int max_ext = p->max_ext < 64 ? p->max_ext : 64;
     for (int si = 0; si < nm; ++si) {
@@ -494,11 +495,28 @@ static void align_read(const afo_index *I, const uint8_t *ascii, int l, const af
         extend_seed(I, q, l, s, p, &regs[n_reg++]);
     }
     free(mems);
+    return n_reg;
+}
+
+static void align_read(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, rec_t *out) {
+    uint8_t q[AFO_MAX_READ];
+    reg_t regs[64];
+    memset(out, 0, sizeof(*out));
+    out->flag = 0x4;
+    if (l > AFO_MAX_READ) l = AFO_MAX_READ;
+    int n_reg = read_regions(I, ascii, l, p, q, regs);
+    if (n_reg < 0) { out->flag |= FLAG_MEM_OVERFLOW; return; }
     int best = -1;
     for (int r = 0; r < n_reg; ++r)
         if (best < 0 || regs[r].score > regs[best].score) best = r;
     if (best < 0 || regs[best].score < p->T) return;
-    const reg_t *a = &regs[best];
+    emit_region(I, q, l, p, &regs[best], out, NULL, NULL);
+}
+
+/* CIGAR and record of one region (the tail of align_read, shared with afo_place).  *matches
+ * (optional) = identical aligned bases; *ref_span (optional) = reference bases covered. */
+static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_params *p, const reg_t *a,
+                        rec_t *out, int *matches, int *ref_span) {
     int is_rev = a->rb >= I->n;
     /* forward-read segment; gen_cigar reverses it together with the revcomp-reference
      * segment for reverse hits (bwa_gen_cigar2), i.e. aligns in forward-ref order */
@@ -517,6 +535,30 @@ static void align_read(const afo_index *I, const uint8_t *ascii, int l, const af
         last_sc = score;
         w2 <<= 1;
     } while (++it < 3 && score < a->truesc - p->a);
+    if (matches || ref_span) {
+        /* walk the alignment in forward-reference orientation (as gen_cigar aligned it) */
+        int mt = 0, x = 0, y = 0, rs = 0;
+        int ncap0 = nc < AFO_MAX_CIGAR ? nc : AFO_MAX_CIGAR;
+        for (int k = 0; k < ncap0; ++k) {
+            int len = (int)(cig[k] >> 4), op = (int)(cig[k] & 0xf);
+            if (op == 0) {
+                for (int u = 0; u < len; ++u) {
+                    int qx = is_rev ? qseg[lq - 1 - (x + u)] : qseg[x + u];
+                    int64_t ty = is_rev ? a->re - 1 - (y + u) : a->rb + y + u;
+                    if (qx < 4 && qx == I->D[ty]) ++mt;
+                }
+                x += len; y += len; rs += len;
+            } else if (op == 1) {
+                x += len;
+            } else {
+                y += len; rs += len;
+            }
+        }
+        if (ncap0 > 0 && (cig[0] & 0xf) == 2) rs -= (int)(cig[0] >> 4);
+        else if (ncap0 > 0 && (cig[ncap0 - 1] & 0xf) == 2) rs -= (int)(cig[ncap0 - 1] >> 4);
+        if (matches) *matches = mt;
+        if (ref_span) *ref_span = rs;
+    }
     int64_t pos = is_rev ? 2 * I->n - a->re : a->rb;
     int ncap = nc < AFO_MAX_CIGAR ? nc : AFO_MAX_CIGAR;
     int of = nc > AFO_MAX_CIGAR;
@@ -582,5 +624,47 @@ int afo_align_pairs(const afo_index *I, const uint8_t *reads, int64_t n_pairs, i
         }
     }
     free(recs);
+    return 0;
+}
+
+/* Multi-hit placement (the searches behind S4-S8: every region of a query scoring >= T, best
+ * score first, ties in region order, at most max_hits; each with its CIGAR as for a primary). */
+int afo_place(const afo_index *I, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,
+              const afo_params *p, int32_t max_hits, int n_threads, afo_hit *hits, int32_t *n_hits) {
+    if (max_hits < 1 || max_hits > 16) return -1;
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+    for (int64_t r = 0; r < n_queries; ++r) {
+        uint8_t q[AFO_MAX_READ];
+        reg_t regs[64];
+        int l = lens ? lens[r] : stride;
+        if (l > AFO_MAX_READ) l = AFO_MAX_READ;
+        int n_reg = read_regions(I, reads + r * (int64_t)stride, l, p, q, regs);
+        int nh = 0;
+        if (n_reg < 0) { n_hits[r] = -1; continue; }
+        int order[64];
+        for (int k = 0; k < n_reg; ++k) {   /* rank: score desc, then region order */
+            int rank = 0;
+            for (int u = 0; u < n_reg; ++u)
+                rank += regs[u].score > regs[k].score || (regs[u].score == regs[k].score && u < k);
+            order[rank] = k;
+        }
+        for (int k = 0; k < n_reg && nh < max_hits; ++k) {
+            const reg_t *a = &regs[order[k]];
+            if (a->score < p->T) break;
+            rec_t rec;
+            int mt = 0, rs = 0;
+            emit_region(I, q, l, p, a, &rec, &mt, &rs);
+            afo_hit *h = &hits[r * max_hits + nh];
+            h->query = (int32_t)r; h->flag = rec.flag; h->score = rec.score;
+            h->q_start = a->qb; h->q_end = a->qe; h->q_size = l; h->matches = mt;
+            h->t_start = rec.pos; h->t_end = rec.pos + rs; h->n_cigar = rec.n_cigar;
+            for (int c = 0; c < AFO_MAX_CIGAR; ++c) h->cigar[c] = c < rec.n_cigar ? rec.cigar[c] : 0;
+            ++nh;
+        }
+        n_hits[r] = nh;
+    }
     return 0;
 }

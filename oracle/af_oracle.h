@@ -43,6 +43,15 @@ typedef struct {
     uint32_t *cigar; /* [n_reads * AFO_MAX_CIGAR], BAM op encoding len<<4|op */
 } afo_out;
 
+typedef struct {
+    int32_t query, flag, score;
+    int32_t q_start, q_end, q_size;   /* forward query coordinates (PSL qStart/qEnd/qSize)      */
+    int32_t matches;                  /* identical aligned bases                                 */
+    int32_t n_cigar;
+    int64_t t_start, t_end;           /* forward reference coordinates of the aligned span       */
+    uint32_t cigar[AFO_MAX_CIGAR];    /* SAM-orientation CIGAR with soft clips (as for a primary) */
+} afo_hit;
+
 typedef struct afo_index afo_index;
 
 void afo_params_default(afo_params *p);
@@ -57,6 +66,10 @@ void afo_seed_filter(const afo_index *idx, const uint8_t *reads, int64_t n_reads
 /* S2 restatement: SE alignment of every read + pair flags (reads pair-major: 2p, 2p+1) */
 int afo_align_pairs(const afo_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
                     const int32_t *lens, const afo_params *p, int n_threads, afo_out *out);
+
+/* multi-hit placement: hits[r * max_hits + k], n_hits[r] (-1 = MEM overflow) */
+int afo_place(const afo_index *idx, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,
+              const afo_params *p, int32_t max_hits, int n_threads, afo_hit *hits, int32_t *n_hits);
 
 #ifdef __cplusplus
 }
