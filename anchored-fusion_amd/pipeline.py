@@ -1,0 +1,172 @@
+"""End-to-end anchored fusion detection on the GPU path (the per-gene loop of
+Anchored_Fusion.py:121-227 with its shell calls replaced).
+
+| reference step | here |
+|---|---|
+| AF:58-80 gene names | `gene_names_from_fasta` / `gene_names_from_file` |
+| AF:144-172 anchor FASTA + `bwa index` | `AnchorAligner(anchor)` (GPU index) |
+| AF:182 `bwa mem -M anchor fq1 fq2 \\| samtools sort` | `AnchorAligner.align_pairs` (K1+K2+K3) |
+| AF:186-194 samtools flag partitions | `align.partition` |
+| AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam` (af_place on the genome) |
+| AF:198 `Find_homo_genes` | `partner.homolog_genes` |
+| AF:204 `del_too_many_reads` | `genome_check` + `Searches.genome_sam` |
+| AF:205-206 `Find_blocks`, `Find_fine_block` | `blocks.spanning_blocks`, `blocks.add_fine_blocks` |
+| AF:207 `Build_candidate_fasta` | `partner.candidate_targets` |
+| AF:208 `contact_reads` | `splitreads.cluster_split_reads` |
+| AF:209-210 `Find_Anchored_split`, `Find_candidate_genes` | `partner.*` |
+| AF:227 `Final_fusion` | `report.write_predictions` |
+
+Searches are injectable (`Searches`):
+- the default runs everything on the GPU;
+- tests may pass the CPU oracle. It is test infrastructure and is never a fallback here.
+
+The filter model (Model.py, `--not_filter_false_positive` off) is outside SURVEY.md §8 and not
+built, so runs behave as `--not_filter_false_positive`.
+"""
+import os
+import re
+
+from . import blocks as blk
+from . import genome_check, partner, report, splitreads
+from .align import partition
+from .annotation import ExonIndex
+from .io import read_fasta, read_pairs
+
+_COMP = str.maketrans("ACGTNacgtn", "TGCANtgcan")
+
+
+def revcomp(s):
+    return s.translate(_COMP)[::-1]
+
+
+def gene_names_from_fasta(path):
+    """AF:58-73: the first header token that is neither an accession (`NM_004327.4`) nor a
+    descriptive word (gene/specie/trans/for/homo/sapiens, any case)."""
+    names = []
+    with open(path) as fh:
+        for line in fh:
+            if not line.startswith(">"):
+                continue
+            toks = line.rstrip()[1:].split(" ")
+            keep = [t for t in toks if not re.match(r"[a-zA-Z]+_\d+\.\d+", t)
+                    and not re.search(r"gene|specie|trans|for|homo|sapiens", t, re.IGNORECASE)]
+            names.append(keep[0])
+    return names
+
+
+def gene_names_from_file(path):
+    with open(path) as fh:
+        return [ln.rstrip() for ln in fh if ln.rstrip() != ""]
+
+
+def sam_line(name, flag, rname, pos1, cigar, seq):
+    return f"{name}\t{flag}\t{rname}\t{pos1}\t60\t{cigar}\t*\t0\t0\t{seq}\t*\n"
+
+
+class Searches:
+    """The two search services the partner stages need, on the GPU by default.
+
+    `place(targets, queries, preset)` -> PSL lines (partner.py callback);
+    `genome_sam(queries)` -> one list of SAM lines per query (primary first)."""
+
+    def __init__(self, genome_contigs, device=0, placer=None):
+        from .place import Placer, sam_records
+        self.genome = genome_contigs
+        self.place = placer or Placer(device=device)
+
+        def genome_sam(queries):
+            ref = self.place.reference(self.genome)   # shared with the genome PSL searches
+            hits, nh = ref.raw_hits([s for _, s in queries], self.place.params("genome_bwa"), 16)
+            return [sam_records(ref, [q], hits[i:i + 1], nh[i:i + 1]) for i, q in enumerate(queries)]
+
+        self.genome_sam = genome_sam
+
+    def getfasta(self, rows):
+        """bedtools getfasta -name: rows (chrom, start, end, name) -> [(name::chrom:start-end, seq)];
+        intervals outside the contig are skipped, as bedtools does."""
+        contigs = dict(self.genome)
+        out = []
+        for chrom, s, e, name in rows:
+            seq = contigs.get(chrom)
+            if seq is None or s < 0 or e > len(seq) or s >= e:
+                continue
+            out.append((f"{name}::{chrom}:{s}-{e}", seq[s:e]))
+        return out
+
+
+def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory, out_prefix, log=print):
+    """One anchored gene (the body of AF:121-227).  Returns the candidate list."""
+    anchor_rec = [(gene, anchor)]
+    aligner = aligner_factory(anchor.encode())
+    try:
+        res = aligner.align_pairs(reads, lens)
+    finally:
+        close = getattr(aligner, "close", None)
+        if close:
+            close()
+    flag, pos = res.flag, res.pos
+    seqs = [bytes(reads[r, : (lens[r] if lens is not None else reads.shape[1])]).decode() for r in range(len(reads))]
+    tmp1, tmp2, anchored = partition(res)
+    log(f"[{gene}] S2: {int(((flag & 4) == 0).sum())} of {len(flag)} reads on the anchor; "
+        f"{len(tmp1)} one-end-anchored pairs; {len(anchored)} anchored records")
+    # S4: one-end-anchored pairs on the genome (samtools fastq restores the sequenced orientation)
+    q4 = []
+    for a, b in zip(tmp1, tmp2):
+        q4 += [(names[a // 2], seqs[a]), (names[b // 2], seqs[b])]
+    s4 = [ln for recs in (searches.genome_sam(q4) if q4 else []) for ln in recs]
+    homo = [row[3] for row in homo_rows]
+    # anchored.bam as `samtools view` prints it (SEQ reverse-complemented for 0x10)
+    anch_lines = []
+    for r in anchored:
+        cig = res.cigar_str(r)
+        seq = revcomp(seqs[r]) if flag[r] & 0x10 else seqs[r]
+        anch_lines.append(sam_line(names[r // 2], int(flag[r]) & 0xFFFF, gene, int(pos[r]) + 1, cig, seq))
+    # S5: split reads vs the genome
+    fasta = genome_check.split_read_fasta(anch_lines)
+    gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam(fasta) if fasta else []) for ln in recs]
+    split_sam = genome_check.filter_genome_hits(gsam)
+    log(f"[{gene}] S5: {len(fasta)} split reads, {len(split_sam)} kept")
+    blocks_chr = blk.spanning_blocks(s4, index, homo)
+    tails, tail_fa = blk.split_read_queries(split_sam)
+    if tail_fa:
+        blk.add_fine_blocks(blocks_chr, tails, searches.place(searches.genome, tail_fa, "split_tail"), index, homo)
+    # the reference's widening can leave a non-integer end; its next step would raise
+    for c in list(blocks_chr):
+        blocks_chr[c] = [b for b in blocks_chr[c] if isinstance(b.start, int) and isinstance(b.end, int)]
+    cand_recs = partner.candidate_targets(blocks_chr, searches.getfasta, searches.place, anchor_rec)
+    bps = splitreads.cluster_split_reads(split_sam)
+    good = partner.anchored_split_placement(cand_recs, blocks_chr, bps, index, searches.place, anchor_rec)
+    cands, cnt_max = partner.candidate_genes(good, bps, blocks_chr, searches.place, searches.genome)
+    log(f"[{gene}] blocks {sum(len(v) for v in blocks_chr.values())}, breakpoints {len(bps)}, "
+        f"placed {len(good)}, candidates {len(cands)}")
+    report.write_predictions(out_prefix, cands, gene, index, [], cnt_max, True)
+    return cands
+
+
+def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
+        aligner_factory=None, log=print):
+    """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt."""
+    genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
+        else gene_names_from_fasta(anchored_cds)
+    anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
+    genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
+    with open(ref_ann) as fh:
+        gtf = fh.readlines()
+    index = ExonIndex.from_lines(gtf)
+    names, reads, lens = read_pairs(fastq1, fastq2)
+    if searches is None:
+        searches = Searches(genome, device=device)
+    if aligner_factory is None:
+        from .align import AnchorAligner
+
+        def aligner_factory(anchor):
+            return AnchorAligner(anchor, device=device)
+    results = {}
+    for gene, anchor in zip(genes, anchors):
+        folder = os.path.join(out_folder, gene + "_fusion")
+        os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
+        homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+        results[gene] = run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory,
+                                 os.path.join(folder, gene + "_fusion"), log=log)
+    return results
+

@@ -38,6 +38,7 @@ import numpy as np
 from . import _lib
 
 SEP = 512  # N run between contigs
+WINDOW = 300  # long-query window (step WINDOW // 2)
 HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_start", "<i4"), ("q_end", "<i4"),
                       ("q_size", "<i4"), ("matches", "<i4"), ("n_cigar", "<i4"), ("t_start", "<i8"),
                       ("t_end", "<i8"), ("cigar", "<u4", (32,))])
@@ -219,15 +220,16 @@ class Placer:
 
     Targets are indexed once per distinct target set (by identity of the list or its content)."""
 
-    def __init__(self, device=0, max_hits=16):
+    def __init__(self, device=0, max_hits=16, reference_factory=None):
         self.device, self.max_hits = device, max_hits
+        self.factory = reference_factory or (lambda contigs: Reference(contigs, device=device))
         self._refs = {}
 
     def reference(self, targets):
-        key = tuple((n, len(s) if isinstance(s, str) else s) for n, s in targets)
+        key = tuple((n, hash(s)) for n, s in targets)
         ref = self._refs.get(key)
         if ref is None:
-            ref = Reference([(n, s) for n, s in targets], device=self.device)
+            ref = self.factory([(n, s) for n, s in targets])
             self._refs[key] = ref
         return ref
 
@@ -243,8 +245,29 @@ class Placer:
         if not targets or not queries:
             return header
         ref = self.reference(targets)
-        hits, nh = ref.raw_hits([s for _, s in queries], self.params(preset), self.max_hits)
-        return header + psl_rows(ref, queries, hits, nh, PRESET_PARAMS[preset][1])
+        # queries longer than the kernel's read limit (the anchor transcript itself, fn:341/966)
+        # are searched as overlapping windows; rows keep the full query's name and size
+        pieces = []  # (name, window seq, offset, full length)
+        for name, seq in queries:
+            if len(seq) <= _lib.AF_MAX_READ:
+                pieces.append((name, seq, 0, len(seq)))
+            else:
+                for off in range(0, max(1, len(seq) - WINDOW // 2), WINDOW // 2):
+                    pieces.append((name, seq[off:off + WINDOW], off, len(seq)))
+        hits, nh = ref.raw_hits([w for _, w, _, _ in pieces], self.params(preset), self.max_hits)
+        min_id = PRESET_PARAMS[preset][1]
+        out = list(header)
+        for i, (name, w, off, full) in enumerate(pieces):
+            rows = psl_rows(ref, [(name, w)], hits[i:i + 1], nh[i:i + 1], min_id)
+            if off == 0 and full == len(w):
+                out += rows
+                continue
+            for r in rows:
+                f = r.rstrip("\n").split("\t")
+                f[10], f[11], f[12] = str(full), str(int(f[11]) + off), str(int(f[12]) + off)
+                f[19] = "".join(f"{int(v) + off}," for v in f[19].split(",") if v)
+                out.append("\t".join(f) + "\n")
+        return out
 
     def close(self):
         for r in self._refs.values():

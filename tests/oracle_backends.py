@@ -1,0 +1,51 @@
+"""CPU oracle stand-ins for the GPU search services -- TEST INFRASTRUCTURE ONLY.
+
+They let the end-to-end pipeline (anchored_fusion_amd.pipeline) run on CPU in the
+`-m "not gpu"` suite. The product never imports this module.
+"""
+import bisect
+
+import afpkg  # noqa: F401
+import oracle
+from anchored_fusion_amd.align import AlignResult
+from anchored_fusion_amd.place import concat_contigs, pack_queries
+
+
+class OracleReference:
+    def __init__(self, contigs):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob, self.offsets = concat_contigs(contigs)
+        self.ix = oracle.OracleIndex(blob)
+
+    def raw_hits(self, seqs, params=None, max_hits=16):
+        buf, lens = pack_queries(seqs)
+        p = oracle.default_params()
+        if params is not None:
+            for f, _ in p._fields_:
+                setattr(p, f, getattr(params, f))
+        return self.ix.place(buf, lens, p, max_hits, threads=8)
+
+    def locate(self, t_start, t_end):
+        k = bisect.bisect_right(self.offsets, int(t_start)) - 1
+        if k < 0:
+            return None
+        s, e = int(t_start) - self.offsets[k], int(t_end) - self.offsets[k]
+        if s < 0 or e > self.lens[k] or e <= s:
+            return None
+        return k, s, e
+
+    def close(self):
+        pass
+
+
+class OracleAligner:
+    def __init__(self, anchor):
+        self.ix = oracle.OracleIndex(anchor)
+
+    def align_pairs(self, reads, lens=None):
+        o = self.ix.align_pairs(reads, lens, threads=8)
+        return AlignResult(o["flag"], o["pos"], o["score"], o["n_cigar"], o["cigar"], o["hits"])
+
+    def close(self):
+        pass

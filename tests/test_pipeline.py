@@ -1,0 +1,48 @@
+"""End-to-end runs of the fusion pipeline (anchored_fusion_amd.pipeline) on a synthetic
+fusion sample.
+
+The CPU test swaps the GPU search services for the oracle (tests/oracle_backends.py). The
+GPU test runs the product path. Both must report the planted BCRX-ABLX fusion, with its anchor
+breakpoint within a few bases of the junction.
+"""
+import os
+
+import pytest
+
+import afpkg  # noqa: F401
+from anchored_fusion_amd import pipeline
+from fusion_world import make_world
+
+
+def _check(out_folder, truth):
+    pred = os.path.join(out_folder, "BCRX_fusion", "BCRX_fusion_predictions_abridged.txt")
+    full = os.path.join(out_folder, "BCRX_fusion", "BCRX_fusion_predictions.txt")
+    assert os.path.exists(pred) and os.path.exists(full)
+    rows = [ln.rstrip("\n").split("\t") for ln in open(pred)][1:]
+    assert rows, "no fusion predicted"
+    hit = [r for r in rows if "ABLX" in r[0]]
+    assert hit, rows
+    bp = int(hit[0][2].split(":")[1])
+    assert abs(bp - truth["anchor_junction"]) <= 3, (bp, truth)
+    assert hit[0][4].startswith("chr2:")
+    return hit
+
+
+def test_pipeline_cpu_backends(tmp_path):
+    from oracle_backends import OracleAligner, OracleReference
+    from anchored_fusion_amd.place import Placer
+    paths, truth = make_world(str(tmp_path / "world"))
+    genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
+    searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference))
+    out = str(tmp_path / "out")
+    pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out,
+                 searches=searches, aligner_factory=OracleAligner, log=lambda *_: None)
+    _check(out, truth)
+
+
+@pytest.mark.gpu
+def test_pipeline_gpu(tmp_path):
+    paths, truth = make_world(str(tmp_path / "world"))
+    out = str(tmp_path / "out")
+    pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out)
+    _check(out, truth)
