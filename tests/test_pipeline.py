@@ -46,3 +46,18 @@ def test_pipeline_gpu(tmp_path):
     out = str(tmp_path / "out")
     pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out)
     _check(out, truth)
+
+
+@pytest.mark.gpu
+def test_cli_gpu(tmp_path):
+    import subprocess
+    import sys
+    paths, truth = make_world(str(tmp_path / "world"), seed=7)
+    out = str(tmp_path / "cli_out")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "run_anchored_fusion.py"), "--file_anchored_cds",
+                        paths["anchor"], "--fastq1", paths["fq1"], "--fastq2", paths["fq2"], "--file_ref_seq",
+                        paths["genome"], "--file_ref_ann", paths["gtf"], "--out_folder", out,
+                        "--not_filter_false_positive", "--thread", "4"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check(out, truth)
