@@ -31,7 +31,7 @@ AF_FLAG_CIGAR_OVERFLOW = 0x20000
 # every symbol include/afgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
-    "af_index_free", "af_index_anchor_len", "af_index_filter_blocks", "af_index_filter_table",
+    "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
     "af_last_candidates", "af_place",
 )
@@ -86,8 +86,8 @@ def lib():
     L.af_index_free.restype = None
     L.af_index_anchor_len.argtypes = [_vp]
     L.af_index_anchor_len.restype = _i64
-    L.af_index_filter_blocks.argtypes = [_vp]
-    L.af_index_filter_blocks.restype = _i32
+    L.af_index_filter_words.argtypes = [_vp]
+    L.af_index_filter_words.restype = _i32
     L.af_index_filter_table.argtypes = [_vp, _vp, _i64]
     L.af_index_filter_table.restype = ctypes.c_int
     L.af_align_pairs.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), ctypes.POINTER(AlnOut)]

@@ -82,8 +82,8 @@ class AnchorAligner:
 
     def filter_table(self):
         L = _lib.lib()
-        nb = L.af_index_filter_blocks(self._idx)
-        out = np.zeros(nb * 2, dtype=np.uint32)
+        nw = L.af_index_filter_words(self._idx)
+        out = np.zeros(nw, dtype=np.uint32)
         _lib.check(self._ctx, L.af_index_filter_table(self._idx, out.ctypes.data, out.size), "af_index_filter_table")
         return out
 

@@ -23,18 +23,38 @@ struct DevIndex {
     const int32_t *hstart;  //   first index into kpos
     const int32_t *hcnt;    //   occurrences (0 = empty slot)
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
-    const uint2 *bloom;     // blocked Bloom filter of the anchor 16-mers (2 x 32-bit words per block)
+    const uint32_t *bloom;  // Bloom filter of the anchor 16-mers (2^bl_bits words, see af_k1_hash)
     int64_t n;              // anchor length
     int32_t hbits;          // log2 position-hash slots
-    int32_t bl_bits;        // log2 Bloom blocks
+    int32_t bl_bits;        // log2 Bloom words
 };
 
 __host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
-__host__ __device__ static inline uint32_t af_fmix2(uint32_t h) { return (h ^ (h >> 15)) * 0x2C1B3C6Du; }
-// three bits of a 32-bit Bloom word, chosen by bits 0..14 of a hash (block index uses the top bits)
-__host__ __device__ static inline uint32_t af_bloom_mask(uint32_t h) {
-    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
+
+// ---- K1 seed-filter keys and Bloom filter --------------------------------
+// Base code of a read byte: a 2-bit table indexed by the byte's low 3 bits (A/a 1 -> 0,
+// C/c 3 -> 1, G/g 7 -> 2, T/t 4 -> 3; N 6 and the unused slots -> 0).  On the device this is
+// one v_and + one v_perm_b32 per four bytes.
+#define AF_K1_CODE_TBL 0x8340u
+__host__ __device__ static inline uint32_t af_k1_code(uint32_t ch) { return (AF_K1_CODE_TBL >> (2 * (ch & 7))) & 3u; }
+// A sampled 16-mer's key is its codes in "word-transposed" order: base 4w+b of the 16-mer at
+// bits 8b+2w, so four byte-wise code words of consecutive 4-base groups combine with three
+// shift-ors.  The map from the 2-bit packing (base i at bits 2i) is a bijection.
+__host__ __device__ static inline uint32_t af_k1_key(uint32_t packed) {
+    uint32_t t = 0;
+    for (int i = 0; i < 16; ++i) t |= ((packed >> (2 * i)) & 3u) << (8 * (i & 3) + 2 * (i >> 2));
+    return t;
 }
+// One 32x32->64 multiply per key (h = key * AF_K1_MUL).  The filter is 2^bits 32-bit words (bits <= 15); a key sets
+// three bits in each of two words: word 1 = hi[31:32-bits], word 2 = hi[bits+1:2], bit
+// positions from bytes 1..3 of lo (word 1) and of lo rotated right by 4 (word 2).
+#define AF_K1_MUL 0x9E3779B1u
+#define AF_K1_MAX_BITS 15
+__host__ __device__ static inline uint64_t af_k1_hash(uint32_t key) { return (uint64_t)key * AF_K1_MUL; }
+__host__ __device__ static inline uint32_t af_k1_mask(uint32_t v) {
+    return (1u << ((v >> 8) & 31)) | (1u << ((v >> 16) & 31)) | (1u << ((v >> 24) & 31));
+}
+__host__ __device__ static inline uint32_t af_k1_rot4(uint32_t v) { return (v >> 4) | (v << 28); }
 
 // Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
 struct ReadRec {

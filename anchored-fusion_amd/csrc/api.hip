@@ -240,16 +240,16 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         while (hcnt[s]) s = (s + 1) & hm;
         hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
     }
-    // blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
-    // ~1.2 blocks per key (128 KiB for a 6.8 kb anchor), 3 bits per word (see af_bloom_mask)
+    // Bloom filter of the distinct 16-mers (seed filter K1): 2^bl_bits 32-bit words, ~2.4 words
+    // per key (at most 2^15 words = 128 KiB, a 6.8 kb anchor), three bits in each of two words
     int bl_bits = 8;
-    while ((double)(1LL << bl_bits) < 1.2 * (double)nd && bl_bits < 14) ++bl_bits;
-    std::vector<uint32_t> bloom((size_t)2 << bl_bits, 0);
+    while ((double)(1LL << bl_bits) < 2.4 * (double)nd && bl_bits < AF_K1_MAX_BITS) ++bl_bits;
+    std::vector<uint32_t> bloom((size_t)1 << bl_bits, 0);
     for (int64_t i = 0; i < nd; ++i) {
-        const uint32_t h1 = af_fmix(keys[i]), h2 = af_fmix2(h1);
-        const size_t blk = h1 >> (32 - bl_bits);
-        bloom[2 * blk] |= af_bloom_mask(h1);
-        bloom[2 * blk + 1] |= af_bloom_mask(h2);
+        const uint64_t h = af_k1_hash(af_k1_key(keys[i]));
+        const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+        bloom[hi >> (32 - bl_bits)] |= af_k1_mask(lo);
+        bloom[(hi >> 2) & ((1u << bl_bits) - 1u)] |= af_k1_mask(af_k1_rot4(lo));
     }
     af_index *ix = new (std::nothrow) af_index;
     if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
@@ -264,7 +264,7 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         af_index_free(ix);
         return rc;
     }
-    ix->dev.bloom = reinterpret_cast<const uint2 *>(bld);
+    ix->dev.bloom = bld;
     ix->dev.n = n;
     ix->dev.hbits = hbits;
     ix->dev.bl_bits = bl_bits;
@@ -280,7 +280,7 @@ void af_index_free(af_index *ix) {
 }
 
 int64_t af_index_anchor_len(const af_index *ix) { return ix ? ix->dev.n : -1; }
-int32_t af_index_filter_blocks(const af_index *ix) { return ix ? (1 << ix->dev.bl_bits) : -1; }
+int32_t af_index_filter_words(const af_index *ix) { return ix ? (1 << ix->dev.bl_bits) : -1; }
 
 int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
     if (!ix || !out) return AF_E_INVALID;

@@ -26,19 +26,22 @@
 
 #include <algorithm>
 
+#ifndef AF_K1_ABL
+#define AF_K1_ABL 0    // 1 = stream-only ablation build (scripts/k1_ablate.sh); 0 = the product kernel
+#endif
+#ifndef AF_K1_PASS
+#define AF_K1_PASS 8   // full tiles per streaming pass of k_seed_stream (8-bit counters in LDS)
+#endif
+
 namespace {
 
-__device__ __forceinline__ uint32_t codes4(uint32_t x) { return ((x >> 1) ^ (x >> 2)) & 0x03030303u; }
-
-// bytes y0..y3 (2-bit codes) -> y0 | y1<<2 | y2<<4 | y3<<6
-__device__ __forceinline__ uint32_t pack4(uint32_t y) {
-    const uint32_t t = y | (y >> 6);
-    return (t & 0xFu) | ((t >> 12) & 0xF0u);
+// four read bytes -> four 2-bit codes, one per byte (af_k1_code: v_and + v_perm_b32)
+__device__ __forceinline__ uint32_t codes_w(uint32_t x) {
+    return __builtin_amdgcn_perm(0x02000003u, 0x01000000u, x & 0x07070707u);
 }
 
-__device__ __forceinline__ uint32_t pack_chunk(const uint4 v) {
-    return pack4(codes4(v.x)) | (pack4(codes4(v.y)) << 8) | (pack4(codes4(v.z)) << 16) |
-           (pack4(codes4(v.w)) << 24);
+__device__ __forceinline__ uint32_t next_lane(uint32_t x) {  // lane l <- lane l+1 (DPP wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
 }
 
 // chunk c of the tile when it is only partly inside the tile (bytes past the end read 'N')
@@ -66,161 +69,274 @@ __device__ __forceinline__ void fill_lds(uint2 *dst, const uint2 *__restrict__ s
     for (int i = i0 + (int)threadIdx.x; i < n; i += 1024) dst[i] = src[i];
 }
 
-// One round of a wave: lane l holds chunk c (packed P); lanes >= 63 or past the tile are off.
-__device__ __forceinline__ void scan_round(uint32_t P, int c, bool in, const uint2 *bloom, int bshift,
-                                           int32_t stride, uint32_t *cnt) {
-    const uint32_t Pn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x130, 0xf, 0xf, false);  // wave_shl:1
-    const uint64_t PP = ((uint64_t)Pn << 32) | P;
-    bool pass[4];
+// One Bloom probe of a key (af_k1_hash): both words are read from LDS, no branches.
+__device__ __forceinline__ bool probe(uint32_t key, const unsigned char *bloom, int bshift, uint32_t wmask4) {
+    const uint64_t h = af_k1_hash(key);
+    const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(bloom + ((hi >> bshift) << 2));
+    const uint32_t w2 = *reinterpret_cast<const uint32_t *>(bloom + (hi & wmask4));
+    const uint32_t m1 = af_k1_mask(lo), m2 = af_k1_mask(af_k1_rot4(lo));
+    return ((m1 & ~w1) | (m2 & ~w2)) == 0u;
+}
+
+// One round of a wave: lane l holds chunk c (16 read bytes = 4 code words); lanes >= 63 or
+// past the tile are off.  The four 16-mers starting in the chunk take the next lane's first
+// three code words through DPP.  Positives (rare) add to 8-bit per-read counters in LDS.
+__device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const unsigned char *bloom, int bshift,
+                                           uint32_t wmask4, int32_t stride, uint32_t *cnt) {
+    const uint32_t c0 = codes_w(v.x), c1 = codes_w(v.y), c2 = codes_w(v.z), c3 = codes_w(v.w);
+    const uint32_t a0 = c0 | (c1 << 2), a1 = c1 | (c2 << 2), a2 = c2 | (c3 << 2);
+    const uint32_t a3 = c3 | (next_lane(c0) << 2);
+    const uint32_t a4 = next_lane(a0), a5 = next_lane(a1);
+    const bool p0 = probe(a0 | (a2 << 4), bloom, bshift, wmask4);
+    const bool p1 = probe(a1 | (a3 << 4), bloom, bshift, wmask4);
+    const bool p2 = probe(a2 | (a4 << 4), bloom, bshift, wmask4);
+    const bool p3 = probe(a3 | (a5 << 4), bloom, bshift, wmask4);
+    if (in && (p0 | p1 | p2 | p3)) {
+        const int off = c * 16;
+        const int r = off / stride;
+        const int o = off - r * stride;
+        const bool pj[4] = {p0, p1, p2, p3};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t k = (uint32_t)(PP >> (8 * j));
-        const uint32_t h1 = af_fmix(k), h2 = af_fmix2(h1);
-        const uint2 w = bloom[h1 >> bshift];
-        const uint32_t m0 = af_bloom_mask(h1), m1 = af_bloom_mask(h2);
-        pass[j] = in && ((w.x & m0) == m0) && ((w.y & m1) == m1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (pass[j]) {
-            const int off = c * 16 + 4 * j;
-            const int r = off / stride;
-            if (off - r * stride + AF_K <= stride) atomicAdd(&cnt[r >> 2], 1u << (8 * (r & 3)));
+        for (int j = 0; j < 4; ++j) {
+            int oo = o + 4 * j, rr = r;
+            if (oo >= stride) { oo -= stride; ++rr; }
+            if (pj[j] && oo + AF_K <= stride) atomicAdd(&cnt[rr >> 2], 1u << (8 * (rr & 3)));
         }
     }
 }
 
+// All tiles a block processes share this state (LDS pointers and wave coordinates).
+struct K1 {
+    const unsigned char *bloom;
+    int bshift;
+    uint32_t wmask4;
+    int32_t stride;
+    int lane, wv;
+};
+
+#define AF_CH(rr) ((((rr) * AF_SEED_WAVES + k.wv) * 63))
+
+// One tile, unpipelined: rounds, optional ragged recount, and an epilogue with its own
+// atomic.  Used for ragged batches and for the partial last tile of k_seed_stream.
 template <bool HAS_LENS>
-__global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_filter(
+__device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t n_reads, int64_t tile,
+                         const int32_t *__restrict__ lens, uint32_t *cnt, uint64_t *gbal, int *gbase,
+                         int32_t *__restrict__ hits, int32_t *__restrict__ cand, int32_t *__restrict__ cnt_g) {
+    const int32_t stride = k.stride;
+    const int lane = k.lane, wv = k.wv;
+    const int64_t r0 = tile * AF_SEED_BTILE;
+    const int nr = __builtin_amdgcn_readfirstlane((int)min((int64_t)AF_SEED_BTILE, n_reads - r0));
+    for (int i = threadIdx.x; i < AF_SEED_BTILE / 4; i += blockDim.x) cnt[i] = 0;
+    __syncthreads();
+    const uint8_t *base = reads + r0 * (int64_t)stride;
+    const int64_t bytes = (int64_t)nr * stride;
+    const int nfull = __builtin_amdgcn_readfirstlane((int)(bytes >> 4));
+    const int nchunks = __builtin_amdgcn_readfirstlane((int)((bytes + 15) >> 4));
+    const int nblk = (nchunks + 62) / 63;                            // 63-chunk wave blocks
+    const int nround = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of this wave
+    const bool l63 = lane < 63;
+    for (int r = 0; r < nround; ++r) {
+        const int c = AF_CH(r) + lane;
+        const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
+                                  : (c < nchunks ? load_tail(base, c, bytes)
+                                                 : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu));
+        scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, cnt);
+    }
+    __syncthreads();
+    if (HAS_LENS) {
+        // ragged batch: recount reads shorter than stride exactly (rare path; the streamed
+        // count above used the stride bound)
+        for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+            const int l = lens[r0 + i];
+            if (l >= stride) continue;
+            uint32_t h = 0;
+            const int64_t rb = (r0 + i) * (int64_t)stride;
+            for (int o = (int)((4 - (rb & 3)) & 3); o + AF_K <= l; o += 4) {
+                uint32_t key = 0;
+                for (int u = 0; u < AF_K; ++u)
+                    key |= af_k1_code(reads[rb + o + u]) << (8 * (u & 3) + 2 * (u >> 2));
+                h += probe(key, k.bloom, k.bshift, k.wmask4);
+            }
+            const uint32_t sh = 8 * (i & 3);
+            const uint32_t old = (cnt[i >> 2] >> sh) & 0xFFu;
+            atomicAdd(&cnt[i >> 2], (h - old) << sh);  // per-byte replace, no carry (h, old < 256)
+        }
+        __syncthreads();
+    }
+    for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
+        const int i = g * 64 + lane;
+        uint32_t h = 0;
+        if (i < nr) {
+            h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            hits[r0 + i] = (int32_t)h;
+        }
+        const uint64_t bal = __ballot(h != 0);
+        if (lane == 0) gbal[g] = bal;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const int c = lane < AF_SEED_GROUPS ? (int)__popcll(gbal[lane]) : 0;
+        int incl = c;  // inclusive prefix over the tile's groups
+        for (int d = 1; d < AF_SEED_GROUPS; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int total = __shfl(incl, AF_SEED_GROUPS - 1);
+        int basei = 0;
+        if (lane == 0 && total) basei = atomicAdd(cnt_g, total);
+        basei = __shfl(basei, 0);
+        if (lane < AF_SEED_GROUPS) gbase[lane] = basei + incl - c;
+    }
+    __syncthreads();
+    for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
+        const uint64_t bal = gbal[g];
+        if ((bal >> lane) & 1ull)
+            cand[gbase[g] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(r0 + g * 64 + lane);
+    }
+    __syncthreads();
+}
+
+// Ragged batches (lens != nullptr): one unpipelined tile at a time.
+__global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const int32_t *__restrict__ lens,
-    const uint2 *__restrict__ bloom_g, int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand,
+    const uint32_t *__restrict__ bloom_g, int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand,
     int32_t *__restrict__ cnt_g, int32_t *__restrict__ cnt_next) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint64_t gbal[AF_SEED_GROUPS];  // per 64-read group: ballot of reads with hits
-    __shared__ int gbase[AF_SEED_GROUPS];      // per group: first cand slot
-    const int nbl = 1 << bl_bits;
-    uint2 *bloom = reinterpret_cast<uint2 *>(smem);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nbl * 8);  // AF_SEED_BTILE 8-bit counters
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
-    const int bshift = 32 - bl_bits;
+    const int nw = 1 << bl_bits;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);
+    uint64_t *gbal = reinterpret_cast<uint64_t *>(cnt + AF_K1_PASS * (AF_SEED_BTILE / 4));
+    int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
+    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, stride, (int)(threadIdx.x & 63),
+               __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;  // next epoch's count (see af_internal.h)
-    fill_lds(bloom, bloom_g, nbl);
-
+    fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
     const int64_t ntiles = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t r0 = tile * AF_SEED_BTILE;
-        const int nr = __builtin_amdgcn_readfirstlane((int)min((int64_t)AF_SEED_BTILE, n_reads - r0));
-        for (int i = threadIdx.x; i < AF_SEED_BTILE / 4; i += blockDim.x) cnt[i] = 0;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+        one_tile<true>(k, reads, n_reads, tile, lens, cnt, gbal, gbase, hits, cand, cnt_g);
+}
+
+// Uniform-length batches.  A block's FULL tiles are streamed in passes of up to
+// AF_K1_PASS tiles: each wave keeps AF_K1_DEPTH chunk loads in flight straight through the
+// pass (tile boundaries included), counting into per-tile 8-bit counters in LDS.  The loop
+// body has no global stores, no atomics that return and no barriers, so every wait is a
+// counted `vmcnt(DEPTH-1)`.  One epilogue per pass writes the hits, and one device atomic per
+// pass reserves the candidate slots.  A partial last tile is finished unpipelined (one_tile).
+__global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
+    const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const uint32_t *__restrict__ bloom_g,
+    int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand, int32_t *__restrict__ cnt_g,
+    int32_t *__restrict__ cnt_next) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nw = 1 << bl_bits;
+    uint32_t *cntp = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);  // [AF_K1_PASS][AF_SEED_BTILE / 4]
+    uint64_t *gbal = reinterpret_cast<uint64_t *>(cntp + AF_K1_PASS * (AF_SEED_BTILE / 4));
+    int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
+    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, stride, (int)(threadIdx.x & 63),
+               __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
+    const int lane = k.lane, wv = k.wv;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
+    fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
+    const int64_t full_tiles = n_reads / AF_SEED_BTILE;
+    const int G = (int)gridDim.x, B = (int)blockIdx.x;
+    const int KF = full_tiles > B ? (int)((full_tiles - B + G - 1) / G) : 0;  // this block's full tiles
+    const int NCH = (AF_SEED_BTILE * stride) >> 4;  // chunks per full tile (2048 * stride is 16-aligned)
+    const int NR = ((NCH + 62) / 63 + AF_SEED_WAVES - 1) / AF_SEED_WAVES;   // rounds per wave per tile
+    const bool l63 = lane < 63;
+    const int64_t tile_bytes = (int64_t)AF_SEED_BTILE * stride;
+    for (int p0 = 0; p0 < KF; p0 += AF_K1_PASS) {
+        const int nt = min(AF_K1_PASS, KF - p0);
+        for (int i = threadIdx.x; i < nt * (AF_SEED_BTILE / 4); i += blockDim.x) cntp[i] = 0;
         __syncthreads();
-        const uint8_t *base = reads + r0 * (int64_t)stride;
-        const int64_t bytes = (int64_t)nr * stride;
-        const int nfull = __builtin_amdgcn_readfirstlane((int)(bytes >> 4));
-        const int nchunks = __builtin_amdgcn_readfirstlane((int)((bytes + 15) >> 4));
-        const int nblk = (nchunks + 62) / 63;                            // 63-chunk wave blocks
-        const int nround = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of this wave
-        const bool l63 = lane < 63;
-#define AF_CH(rr) ((((rr) * AF_SEED_WAVES + wv) * 63))
-        if (nfull == nchunks) {
-            // every chunk is whole: branch-free loads, addresses clamped into the tile (clamped
-            // lanes are masked by `in`; a clamped neighbour only feeds 16-mers that cross the
-            // tile end, which the per-read bound rejects).  Three named round buffers,
-            // unrolled by 3: each load lands in the registers consumed two rounds later.
-            const uint4 *cb = reinterpret_cast<const uint4 *>(base);
-            const int last = nfull - 1;
-            uint4 vA = cb[min(AF_CH(0) + lane, last)];
-            uint4 vB = cb[min(AF_CH(1) + lane, last)];
-            uint4 vC = cb[min(AF_CH(2) + lane, last)];
-            for (int r = 0; r < nround; r += 3) {
-                scan_round(pack_chunk(vA), AF_CH(r) + lane, l63 && AF_CH(r) + lane < nchunks, bloom, bshift, stride,
-                           cnt);
-                vA = cb[min(AF_CH(r + 3) + lane, last)];
-                if (r + 1 < nround)
-                    scan_round(pack_chunk(vB), AF_CH(r + 1) + lane, l63 && AF_CH(r + 1) + lane < nchunks, bloom,
-                               bshift, stride, cnt);
-                vB = cb[min(AF_CH(r + 4) + lane, last)];
-                if (r + 2 < nround)
-                    scan_round(pack_chunk(vC), AF_CH(r + 2) + lane, l63 && AF_CH(r + 2) + lane < nchunks, bloom,
-                               bshift, stride, cnt);
-                vC = cb[min(AF_CH(r + 5) + lane, last)];
-            }
-        } else {
-            for (int r = 0; r < nround; ++r) {
-                const int c = AF_CH(r) + lane;
-                const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
-                                          : (c < nchunks ? load_tail(base, c, bytes)
-                                                         : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu,
-                                                                      0x4E4E4E4Eu));
-                scan_round(pack_chunk(v), c, l63 && c < nchunks, bloom, bshift, stride, cnt);
-            }
+        const int total = nt * NR;
+        // load position (lt, lr) runs AF_K1_DEPTH rounds ahead of the scan position (st, sr)
+        int lt = 0, lr = 0;
+        auto next_load = [&]() -> uint4 {
+            const int t = lt < nt ? lt : nt - 1, r = lt < nt ? lr : NR - 1;  // past the pass: re-read
+            const uint4 *cb = reinterpret_cast<const uint4 *>(reads + (B + (int64_t)(p0 + t) * G) * tile_bytes);
+            const uint4 v = cb[min(AF_CH(r) + lane, NCH - 1)];
+            if (++lr == NR) { lr = 0; ++lt; }
+            return v;
+        };
+        uint4 b0 = next_load(), b1 = next_load(), b2 = next_load(), b3 = next_load();
+        int st = 0, sr = 0;
+#if AF_K1_ABL
+        uint32_t abl = 0;
+#endif
+        auto scan = [&](const uint4 &v) {
+#if AF_K1_ABL == 1
+            abl ^= v.x ^ v.y ^ v.z ^ v.w;
+#else
+            scan_round(v, AF_CH(sr) + lane, l63 && AF_CH(sr) + lane < NCH, k.bloom, k.bshift, k.wmask4, stride,
+                       cntp + st * (AF_SEED_BTILE / 4));
+#endif
+            if (++sr == NR) { sr = 0; ++st; }
+        };
+        int g = 0;
+        for (; g + 4 <= total; g += 4) {
+            scan(b0); b0 = next_load();
+            scan(b1); b1 = next_load();
+            scan(b2); b2 = next_load();
+            scan(b3); b3 = next_load();
         }
-#undef AF_CH
-        __syncthreads();
-        if (HAS_LENS) {
-            // ragged batch: recount reads shorter than stride exactly (rare path; the streamed
-            // count above used the stride bound)
-            for (int i = threadIdx.x; i < nr; i += blockDim.x) {
-                const int l = lens[r0 + i];
-                if (l >= stride) continue;
-                uint32_t h = 0;
-                const int64_t rb = (r0 + i) * (int64_t)stride;
-                for (int o = (int)((4 - (rb & 3)) & 3); o + AF_K <= l; o += 4) {
-                    uint32_t k = 0;
-                    for (int u = 0; u < AF_K; ++u) {
-                        const uint32_t ch = reads[rb + o + u];
-                        k |= (((ch >> 1) ^ (ch >> 2)) & 3u) << (2 * u);
-                    }
-                    const uint32_t h1 = af_fmix(k), h2 = af_fmix2(h1);
-                    const uint2 w = bloom[h1 >> bshift];
-                    const uint32_t m0 = af_bloom_mask(h1), m1 = af_bloom_mask(h2);
-                    h += ((w.x & m0) == m0) && ((w.y & m1) == m1);
-                }
-                const uint32_t sh = 8 * (i & 3);
-                const uint32_t old = (cnt[i >> 2] >> sh) & 0xFFu;
-                atomicAdd(&cnt[i >> 2], (h - old) << sh);  // per-byte replace, no carry (h, old < 256)
-            }
-            __syncthreads();
-        }
-        // candidate append: ONE device atomic per tile.  A device-scope atomic on a single
-        // address is serialised across all 8 XCDs; one per 64-read group (~30k per launch)
-        // cost more than the whole scan.
-        for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
-            const int i = g * 64 + lane;
-            uint32_t h = 0;
-            if (i < nr) {
-                h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                hits[r0 + i] = (int32_t)h;
-            }
+        if (g < total) scan(b0);
+        if (g + 1 < total) scan(b1);
+        if (g + 2 < total) scan(b2);
+#if AF_K1_ABL
+        if (abl == 0x12345679u) cntp[0] = abl;  // keep the ablated work live
+#endif
+        __syncthreads();  // the pass is counted
+        // epilogue: hits and ballots of every tile, one atomic for the pass
+        for (int q = wv; q < nt * AF_SEED_GROUPS; q += AF_SEED_WAVES) {
+            const int t = q / AF_SEED_GROUPS, gq = q - t * AF_SEED_GROUPS;
+            const int i = gq * 64 + lane;
+            const uint32_t *cnt = cntp + t * (AF_SEED_BTILE / 4);
+            const uint32_t h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            hits[(B + (int64_t)(p0 + t) * G) * AF_SEED_BTILE + i] = (int32_t)h;
             const uint64_t bal = __ballot(h != 0);
-            if (lane == 0) gbal[g] = bal;
+            if (lane == 0) gbal[q] = bal;
         }
         __syncthreads();
         if (wv == 0) {
-            const int c = lane < AF_SEED_GROUPS ? (int)__popcll(gbal[lane]) : 0;
-            int incl = c;  // inclusive prefix over the tile's groups
-            for (int d = 1; d < AF_SEED_GROUPS; d <<= 1) {
-                const int t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
+            // exclusive prefix over the pass's nt*32 groups, 64 per step
+            int carry = 0;
+            for (int q0 = 0; q0 < nt * AF_SEED_GROUPS; q0 += 64) {
+                const int q = q0 + lane;
+                const int c = q < nt * AF_SEED_GROUPS ? (int)__popcll(gbal[q]) : 0;
+                int incl = c;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int u = __shfl_up(incl, d);
+                    if (lane >= d) incl += u;
+                }
+                if (q < nt * AF_SEED_GROUPS) gbase[q] = carry + incl - c;
+                carry += __shfl(incl, 63);
             }
-            const int total = __shfl(incl, AF_SEED_GROUPS - 1);
-            int basei = 0;
-            if (lane == 0 && total) basei = atomicAdd(cnt_g, total);
-            basei = __shfl(basei, 0);
-            if (lane < AF_SEED_GROUPS) gbase[lane] = basei + incl - c;
+            int bse = 0;
+            if (lane == 0 && carry) bse = atomicAdd(cnt_g, carry);
+            bse = __shfl(bse, 0);
+            for (int q = lane; q < nt * AF_SEED_GROUPS; q += 64) gbase[q] += bse;
         }
         __syncthreads();
-        for (int g = wv; g < AF_SEED_GROUPS; g += AF_SEED_WAVES) {
-            const uint64_t bal = gbal[g];
+        for (int q = wv; q < nt * AF_SEED_GROUPS; q += AF_SEED_WAVES) {
+            const int t = q / AF_SEED_GROUPS, gq = q - t * AF_SEED_GROUPS;
+            const uint64_t bal = gbal[q];
             if ((bal >> lane) & 1ull)
-                cand[gbase[g] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(r0 + g * 64 + lane);
+                cand[gbase[q] + __popcll(bal & ((1ull << lane) - 1ull))] =
+                    (int32_t)((B + (int64_t)(p0 + t) * G) * AF_SEED_BTILE + gq * 64 + lane);
         }
         __syncthreads();
     }
+    // partial last tile (n_reads not a multiple of the tile), on the block that owns it
+    if (n_reads % AF_SEED_BTILE != 0 && full_tiles % G == B)
+        one_tile<false>(k, reads, n_reads, full_tiles, nullptr, cntp, gbal, gbase, hits, cand, cnt_g);
 }
+#undef AF_CH
 
 }  // namespace
 
-size_t af_seed_filter_lds(int bl_bits) { return ((size_t)1 << bl_bits) * 8 + AF_SEED_BTILE; }
+// dynamic LDS: Bloom words, then per-pass 8-bit read counters, then ballots and bases
+size_t af_seed_filter_lds(int bl_bits) {
+    return ((size_t)1 << bl_bits) * 4 + AF_K1_PASS * AF_SEED_BTILE + AF_K1_PASS * AF_SEED_GROUPS * 12;
+}
 
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next,
@@ -234,22 +350,25 @@ hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / (lds + 1024)));
     const int64_t blocks = std::min<int64_t>(want, (int64_t)n_cu * per_cu);
     static bool attr_done = false;
-    if (!attr_done) {  // dynamic LDS above 64 KiB needs the opt-in on both instantiations
-        // (static + dynamic must stay within the CU's 160 KiB: leave 1 KiB for the static arrays)
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<true>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_seed_filter<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-        if (e != hipSuccess) return e;
+    if (!attr_done) {  // dynamic LDS above 64 KiB needs the opt-in; static + dynamic stays within 160 KiB
+        const void *fns[2] = {reinterpret_cast<const void *>(&k_seed_ragged),
+                              reinterpret_cast<const void *>(&k_seed_stream)};
+        for (const void *fn : fns) {
+            hipFuncAttributes fa;
+            hipError_t e = hipFuncGetAttributes(&fa, fn);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(160 * 1024 - fa.sharedSizeBytes));
+            if (e != hipSuccess) return e;
+        }
         attr_done = true;
     }
     dim3 grid((unsigned)blocks), block(64 * AF_SEED_WAVES);
     if (lens)
-        hipLaunchKernelGGL((k_seed_filter<true>), grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom,
-                           ix.bl_bits, hits, cand, cnt, cnt_next);
+        hipLaunchKernelGGL(k_seed_ragged, grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom, ix.bl_bits,
+                           hits, cand, cnt, cnt_next);
     else
-        hipLaunchKernelGGL((k_seed_filter<false>), grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom,
-                           ix.bl_bits, hits, cand, cnt, cnt_next);
+        hipLaunchKernelGGL(k_seed_stream, grid, block, lds, s, reads, n_reads, stride, ix.bloom, ix.bl_bits, hits,
+                           cand, cnt, cnt_next);
     return hipGetLastError();
 }

@@ -92,8 +92,8 @@ void af_params_default(af_params *p);
 int af_index_build(af_ctx *ctx, const char *anchor, int64_t len, af_index **out);
 void af_index_free(af_index *idx);
 int64_t af_index_anchor_len(const af_index *idx);
-int32_t af_index_filter_blocks(const af_index *idx);
-/* copies the seed-filter Bloom words (2 x uint32 per block) to host memory */
+int32_t af_index_filter_words(const af_index *idx);
+/* copies the seed-filter Bloom words (af_index_filter_words uint32) to host memory */
 int af_index_filter_table(const af_index *idx, uint32_t *out, int64_t cap);
 
 /* host buffers in, host buffers out; synchronous */

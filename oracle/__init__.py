@@ -43,8 +43,8 @@ def lib():
         L.afo_index_build.restype = ctypes.c_void_p
         L.afo_index_build.argtypes = [ctypes.c_char_p, ctypes.c_int64]
         L.afo_index_free.argtypes = [ctypes.c_void_p]
-        L.afo_filter_blocks.restype = ctypes.c_int32
-        L.afo_filter_blocks.argtypes = [ctypes.c_void_p]
+        L.afo_filter_words.restype = ctypes.c_int32
+        L.afo_filter_words.argtypes = [ctypes.c_void_p]
         L.afo_filter_table.restype = ctypes.c_void_p
         L.afo_filter_table.argtypes = [ctypes.c_void_p]
         L.afo_params_default.argtypes = [ctypes.POINTER(Params)]
@@ -80,9 +80,9 @@ class OracleIndex:
             self.h = None
 
     def filter_table(self):
-        nb = lib().afo_filter_blocks(self.h)
+        nw = lib().afo_filter_words(self.h)
         ptr = lib().afo_filter_table(self.h)
-        return np.ctypeslib.as_array((ctypes.c_uint32 * (nb * 2)).from_address(ptr)).copy()
+        return np.ctypeslib.as_array((ctypes.c_uint32 * nw).from_address(ptr)).copy()
 
     def seed_filter(self, reads, lens=None):
         reads = np.ascontiguousarray(reads, dtype=np.uint8)

@@ -22,7 +22,7 @@ struct afo_index {
     int64_t nk;         /* number of indexed 16-mer positions              */
     uint32_t *kmer;     /* sorted by (kmer, pos)                            */
     int32_t *kpos;
-    int32_t bl_bits;    /* log2 Bloom blocks                               */
+    int32_t bl_bits;    /* log2 Bloom words                                */
     uint32_t *bloom;    /* 2 words per block                               */
 };
 
@@ -44,13 +44,21 @@ void afo_params_default(afo_params *p) {
     p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 64;
 }
 
-/* seed-filter hashes: block = top bits of fmix(k); bits 0..14 of fmix(k) and of fmix2(fmix(k))
- * pick three bits in each of the block's two words */
-static inline uint32_t fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
-static inline uint32_t fmix2(uint32_t h) { return (h ^ (h >> 15)) * 0x2C1B3C6Du; }
-static inline uint32_t bloom_mask(uint32_t h) {
-    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
+/* ---- seed-filter (K1) keys and Bloom filter, restated from the kernel's definition
+ * (anchored-fusion_amd/csrc/af_internal.h; not a reference algorithm: the filter
+ * only has to keep every read that can hold a bwa seed).
+ * code(byte) = 2-bit table 0x8340 indexed by the byte's low 3 bits (A C G T -> 0 1 2 3, N -> 0);
+ * key = the 16 codes with base 4w+b at bits 8b+2w; h = key * 0x9E3779B1 (64-bit product);
+ * word 1 = hi >> (32-bits) takes three bits picked by bytes 1..3 of lo, word 2 =
+ * (hi >> 2) & (2^bits-1) three bits picked by bytes 1..3 of lo rotated right by 4. */
+static inline uint32_t k1_code(uint8_t c) { return (0x8340u >> (2 * (c & 7))) & 3u; }
+static inline uint64_t k1_hash(uint32_t key) { return (uint64_t)key * 0x9E3779B1u; }
+static inline uint32_t k1_mask(uint32_t v) {
+    return (1u << ((v >> 8) & 31)) | (1u << ((v >> 16) & 31)) | (1u << ((v >> 24) & 31));
 }
+static inline uint32_t k1_rot4(uint32_t v) { return (v >> 4) | (v << 28); }
+static inline uint32_t k1_w1(uint64_t h, int bits) { return (uint32_t)(h >> 32) >> (32 - bits); }
+static inline uint32_t k1_w2(uint64_t h, int bits) { return ((uint32_t)(h >> 32) >> 2) & ((1u << bits) - 1u); }
 
 static int cmp_u64(const void *a, const void *b) {
     uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
@@ -97,18 +105,19 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
         I->kpos[i] = (int32_t)(tmp[i] & 0xffffffffu);
         if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
     }
-    /* blocked Bloom filter of the distinct 16-mers: 2^bl_bits blocks of two 32-bit words,
-     * ~1.2 blocks per key (at most 2^14), three bits set per word */
+    /* Bloom filter of the distinct 16-mers: 2^bl_bits 32-bit words, ~2.4 words per key (at
+     * most 2^15), three bits set in each of two words */
     int bits = 8;
-    while ((double)(1LL << bits) < 1.2 * (double)nd && bits < 14) ++bits;
+    while ((double)(1LL << bits) < 2.4 * (double)nd && bits < 15) ++bits;
     I->bl_bits = bits;
-    I->bloom = (uint32_t *)calloc((size_t)2 << bits, sizeof(uint32_t));
+    I->bloom = (uint32_t *)calloc((size_t)1 << bits, sizeof(uint32_t));
     for (int64_t i = 0; i < m; ++i) {
         if (i > 0 && I->kmer[i] == I->kmer[i - 1]) continue;
-        uint32_t h1 = fmix(I->kmer[i]), h2 = fmix2(h1);
-        size_t blk = h1 >> (32 - bits);
-        I->bloom[2 * blk] |= bloom_mask(h1);
-        I->bloom[2 * blk + 1] |= bloom_mask(h2);
+        uint32_t key = 0;  /* base j of the 16-mer (bits 2j of kmer) to bits 8(j&3)+2(j>>2) */
+        for (int j = 0; j < AFO_K; ++j) key |= ((I->kmer[i] >> (2 * j)) & 3u) << (8 * (j & 3) + 2 * (j >> 2));
+        uint64_t h = k1_hash(key);
+        I->bloom[k1_w1(h, bits)] |= k1_mask((uint32_t)h);
+        I->bloom[k1_w2(h, bits)] |= k1_mask(k1_rot4((uint32_t)h));
     }
     free(tmp);
     return I;
@@ -119,22 +128,21 @@ void afo_index_free(afo_index *I) {
     free(I->D); free(I->kmer); free(I->kpos); free(I->bloom); free(I);
 }
 int64_t afo_index_len(const afo_index *I) { return I->n; }
-int32_t afo_filter_blocks(const afo_index *I) { return 1 << I->bl_bits; }
+int32_t afo_filter_words(const afo_index *I) { return 1 << I->bl_bits; }
 const uint32_t *afo_filter_table(const afo_index *I) { return I->bloom; }
 
-/* a sampled 16-mer is a hit when all six Bloom bits of its block are set */
-static int filter_query(const afo_index *I, uint32_t k) {
-    uint32_t h1 = fmix(k), h2 = fmix2(h1);
-    size_t blk = h1 >> (32 - I->bl_bits);
-    uint32_t m0 = bloom_mask(h1), m1 = bloom_mask(h2);
-    return (I->bloom[2 * blk] & m0) == m0 && (I->bloom[2 * blk + 1] & m1) == m1;
+/* a sampled 16-mer (key layout above) is a hit when all six of its Bloom bits are set */
+static int filter_query(const afo_index *I, uint32_t key) {
+    uint64_t h = k1_hash(key);
+    uint32_t m1 = k1_mask((uint32_t)h), m2 = k1_mask(k1_rot4((uint32_t)h));
+    return (I->bloom[k1_w1(h, I->bl_bits)] & m1) == m1 && (I->bloom[k1_w2(h, I->bl_bits)] & m2) == m2;
 }
 
 /* K1 semantics: sampled positions are those whose byte offset in the read buffer is a
  * multiple of 4; any MEM >= 19 nt contains such a 16-mer and a Bloom filter has no false
  * negatives, so hits==0 => no seed.  Bytes are
- * projected to 2 bits by ((c >> 1) ^ (c >> 2)) & 3 (exact for ACGT/acgt; other bytes land on
- * some code, which can only add hits -- MEMs never contain N, so the superset property holds). */
+ * projected to 2 bits by k1_code (exact for ACGT/acgt; other bytes land on some code, which
+ * can only add hits -- MEMs never contain N, so the superset property holds). */
 void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, int32_t stride,
                      const int32_t *lens, int32_t *hits) {
     for (int64_t r = 0; r < n_reads; ++r) {
@@ -145,8 +153,7 @@ void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, 
         for (int32_t i = i0; i + AFO_K <= l; i += 4) {
             uint32_t k = 0;
             for (int j = 0; j < AFO_K; ++j) {
-                const uint8_t c = reads[base + i + j];
-                k |= (uint32_t)(((c >> 1) ^ (c >> 2)) & 3) << (2 * j);
+                k |= k1_code(reads[base + i + j]) << (8 * (j & 3) + 2 * (j >> 2));
             }
             h += filter_query(I, k);
         }

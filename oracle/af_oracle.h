@@ -58,7 +58,7 @@ void afo_params_default(afo_params *p);
 afo_index *afo_index_build(const char *anchor, int64_t n);
 void afo_index_free(afo_index *idx);
 int64_t afo_index_len(const afo_index *idx);
-int32_t afo_filter_blocks(const afo_index *idx);
+int32_t afo_filter_words(const afo_index *idx);
 const uint32_t *afo_filter_table(const afo_index *idx);
 /* K1 restatement: per read, number of sampled 16-mers passing the anchor filter */
 void afo_seed_filter(const afo_index *idx, const uint8_t *reads, int64_t n_reads, int32_t stride,
