@@ -45,16 +45,20 @@ __host__ __device__ static inline uint32_t af_k1_key(uint32_t packed) {
     for (int i = 0; i < 16; ++i) t |= ((packed >> (2 * i)) & 3u) << (8 * (i & 3) + 2 * (i >> 2));
     return t;
 }
-// One 32x32->64 multiply per key (h = key * AF_K1_MUL).  The filter is 2^bits 32-bit words (bits <= 15); a key sets
-// three bits in each of two words: word 1 = hi[31:32-bits], word 2 = hi[bits+1:2], bit
-// positions from bytes 1..3 of lo (word 1) and of lo rotated right by 4 (word 2).
+// One 32x32->64 multiply per key (h = key * AF_K1_MUL = hi:lo).  The filter is 2^bits 32-bit
+// words (bits <= 15); a key sets four bits, one per byte, in each of two words:
+//   word 1 = hi[bits+1:2],   bit (byte i) = lo byte i & 7;
+//   word 2 = lo[31:32-bits], bit (byte i) = hi byte i & 7,
+// so neither word's bits come from the half of h that indexes it.  On the device a mask is
+// one v_and + one v_perm_b32 over the one-hot bytes 01 02 .. 80.
 #define AF_K1_MUL 0x9E3779B1u
 #define AF_K1_MAX_BITS 15
 __host__ __device__ static inline uint64_t af_k1_hash(uint32_t key) { return (uint64_t)key * AF_K1_MUL; }
 __host__ __device__ static inline uint32_t af_k1_mask(uint32_t v) {
-    return (1u << ((v >> 8) & 31)) | (1u << ((v >> 16) & 31)) | (1u << ((v >> 24) & 31));
+    uint32_t m = 0;
+    for (int b = 0; b < 4; ++b) m |= 1u << (8 * b + ((v >> (8 * b)) & 7));
+    return m;
 }
-__host__ __device__ static inline uint32_t af_k1_rot4(uint32_t v) { return (v >> 4) | (v << 28); }
 
 // Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
 struct ReadRec {

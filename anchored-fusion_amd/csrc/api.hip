@@ -241,15 +241,15 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
     }
     // Bloom filter of the distinct 16-mers (seed filter K1): 2^bl_bits 32-bit words, ~2.4 words
-    // per key (at most 2^15 words = 128 KiB, a 6.8 kb anchor), three bits in each of two words
+    // per key (at most 2^15 words = 128 KiB, a 6.8 kb anchor), four bits in each of two words
     int bl_bits = 8;
     while ((double)(1LL << bl_bits) < 2.4 * (double)nd && bl_bits < AF_K1_MAX_BITS) ++bl_bits;
     std::vector<uint32_t> bloom((size_t)1 << bl_bits, 0);
     for (int64_t i = 0; i < nd; ++i) {
         const uint64_t h = af_k1_hash(af_k1_key(keys[i]));
         const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-        bloom[hi >> (32 - bl_bits)] |= af_k1_mask(lo);
-        bloom[(hi >> 2) & ((1u << bl_bits) - 1u)] |= af_k1_mask(af_k1_rot4(lo));
+        bloom[(hi >> 2) & ((1u << bl_bits) - 1u)] |= af_k1_mask(lo);
+        bloom[lo >> (32 - bl_bits)] |= af_k1_mask(hi);
     }
     af_index *ix = new (std::nothrow) af_index;
     if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");

@@ -27,7 +27,7 @@
 #include <algorithm>
 
 #ifndef AF_K1_ABL
-#define AF_K1_ABL 0    // 1 = stream-only ablation build (scripts/k1_ablate.sh); 0 = the product kernel
+#define AF_K1_ABL 0    // 1 = stream-only timing build (scripts/k1_ablate.sh); 0 = the product kernel
 #endif
 #ifndef AF_K1_PASS
 #define AF_K1_PASS 8   // full tiles per streaming pass of k_seed_stream (8-bit counters in LDS)
@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t codes_w(uint32_t x) {
 }
 
 __device__ __forceinline__ uint32_t next_lane(uint32_t x) {  // lane l <- lane l+1 (DPP wave_shl:1)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x130, 0xf, 0xf, true);  // lane 63 reads 0
 }
 
 // chunk c of the tile when it is only partly inside the tile (bytes past the end read 'N')
@@ -70,20 +70,27 @@ __device__ __forceinline__ void fill_lds(uint2 *dst, const uint2 *__restrict__ s
 }
 
 // One Bloom probe of a key (af_k1_hash): both words are read from LDS, no branches.
+__device__ __forceinline__ uint32_t onehot_bytes(uint32_t v) {  // af_k1_mask
+    return __builtin_amdgcn_perm(0x80402010u, 0x08040201u, v & 0x07070707u);
+}
 __device__ __forceinline__ bool probe(uint32_t key, const unsigned char *bloom, int bshift, uint32_t wmask4) {
     const uint64_t h = af_k1_hash(key);
     const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(bloom + ((hi >> bshift) << 2));
-    const uint32_t w2 = *reinterpret_cast<const uint32_t *>(bloom + (hi & wmask4));
-    const uint32_t m1 = af_k1_mask(lo), m2 = af_k1_mask(af_k1_rot4(lo));
+    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(bloom + (hi & wmask4));
+    const uint32_t w2 = *reinterpret_cast<const uint32_t *>(bloom + ((lo >> bshift) << 2));
+    const uint32_t m1 = onehot_bytes(lo), m2 = onehot_bytes(hi);
     return ((m1 & ~w1) | (m2 & ~w2)) == 0u;
 }
 
 // One round of a wave: lane l holds chunk c (16 read bytes = 4 code words); lanes >= 63 or
 // past the tile are off.  The four 16-mers starting in the chunk take the next lane's first
 // three code words through DPP.  Positives (rare) add to 8-bit per-read counters in LDS.
+//
+// The positives' read index: r = floor((off + 0.5) / stride) in f32 is exact here (off < 2^23
+// is a tile-relative byte offset, stride <= AF_MAX_READ, so the quotient sits >= 0.5 / stride
+// from an integer, far beyond f32 error); a chunk spans at most two reads, so at most two adds.
 __device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const unsigned char *bloom, int bshift,
-                                           uint32_t wmask4, int32_t stride, uint32_t *cnt) {
+                                           uint32_t wmask4, int32_t stride, float inv_stride, uint32_t *cnt) {
     const uint32_t c0 = codes_w(v.x), c1 = codes_w(v.y), c2 = codes_w(v.z), c3 = codes_w(v.w);
     const uint32_t a0 = c0 | (c1 << 2), a1 = c1 | (c2 << 2), a2 = c2 | (c3 << 2);
     const uint32_t a3 = c3 | (next_lane(c0) << 2);
@@ -93,16 +100,21 @@ __device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const 
     const bool p2 = probe(a2 | (a4 << 4), bloom, bshift, wmask4);
     const bool p3 = probe(a3 | (a5 << 4), bloom, bshift, wmask4);
     if (in && (p0 | p1 | p2 | p3)) {
-        const int off = c * 16;
-        const int r = off / stride;
-        const int o = off - r * stride;
+        const uint32_t off = (uint32_t)c * 16u;
+        const uint32_t r = (uint32_t)(((float)off + 0.5f) * inv_stride);
+        const int o = (int)(off - r * (uint32_t)stride);
         const bool pj[4] = {p0, p1, p2, p3};
+        uint32_t na = 0, nb = 0;  // positives in read r and in read r + 1
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            int oo = o + 4 * j, rr = r;
-            if (oo >= stride) { oo -= stride; ++rr; }
-            if (pj[j] && oo + AF_K <= stride) atomicAdd(&cnt[rr >> 2], 1u << (8 * (rr & 3)));
+            const int oo = o + 4 * j;
+            const bool wrap = oo >= stride;
+            const bool ok = pj[j] && (wrap ? oo + AF_K <= 2 * stride : oo + AF_K <= stride);
+            na += ok && !wrap;
+            nb += ok && wrap;
         }
+        if (na) atomicAdd(&cnt[r >> 2], na << (8 * (r & 3)));
+        if (nb) atomicAdd(&cnt[(r + 1) >> 2], nb << (8 * ((r + 1) & 3)));
     }
 }
 
@@ -111,6 +123,7 @@ struct K1 {
     const unsigned char *bloom;
     int bshift;
     uint32_t wmask4;
+    float inv_stride;
     int32_t stride;
     int lane, wv;
 };
@@ -141,7 +154,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
         const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
                                   : (c < nchunks ? load_tail(base, c, bytes)
                                                  : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu));
-        scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, cnt);
+        scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
     }
     __syncthreads();
     if (HAS_LENS) {
@@ -207,7 +220,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);
     uint64_t *gbal = reinterpret_cast<uint64_t *>(cnt + AF_K1_PASS * (AF_SEED_BTILE / 4));
     int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
-    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, stride, (int)(threadIdx.x & 63),
+    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;  // next epoch's count (see af_internal.h)
     fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
@@ -231,7 +244,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     uint32_t *cntp = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);  // [AF_K1_PASS][AF_SEED_BTILE / 4]
     uint64_t *gbal = reinterpret_cast<uint64_t *>(cntp + AF_K1_PASS * (AF_SEED_BTILE / 4));
     int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
-    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, stride, (int)(threadIdx.x & 63),
+    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int lane = k.lane, wv = k.wv;
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
@@ -257,7 +270,17 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
             if (++lr == NR) { lr = 0; ++lt; }
             return v;
         };
-        uint4 b0 = next_load(), b1 = next_load(), b2 = next_load(), b3 = next_load();
+        // the compiler barriers pin the issue order (b0 oldest), so the waits below count to
+        // vmcnt(3) on the loop's entry edge as on its back edge
+#define AF_PIN asm volatile("" ::: "memory")
+        uint4 b0 = next_load();
+        AF_PIN;
+        uint4 b1 = next_load();
+        AF_PIN;
+        uint4 b2 = next_load();
+        AF_PIN;
+        uint4 b3 = next_load();
+        AF_PIN;
         int st = 0, sr = 0;
 #if AF_K1_ABL
         uint32_t abl = 0;
@@ -267,17 +290,18 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
             abl ^= v.x ^ v.y ^ v.z ^ v.w;
 #else
             scan_round(v, AF_CH(sr) + lane, l63 && AF_CH(sr) + lane < NCH, k.bloom, k.bshift, k.wmask4, stride,
-                       cntp + st * (AF_SEED_BTILE / 4));
+                       k.inv_stride, cntp + st * (AF_SEED_BTILE / 4));
 #endif
             if (++sr == NR) { sr = 0; ++st; }
         };
         int g = 0;
         for (; g + 4 <= total; g += 4) {
-            scan(b0); b0 = next_load();
-            scan(b1); b1 = next_load();
-            scan(b2); b2 = next_load();
-            scan(b3); b3 = next_load();
+            scan(b0); b0 = next_load(); AF_PIN;
+            scan(b1); b1 = next_load(); AF_PIN;
+            scan(b2); b2 = next_load(); AF_PIN;
+            scan(b3); b3 = next_load(); AF_PIN;
         }
+#undef AF_PIN
         if (g < total) scan(b0);
         if (g + 1 < total) scan(b1);
         if (g + 2 < total) scan(b2);

@@ -48,17 +48,18 @@ void afo_params_default(afo_params *p) {
  * (anchored-fusion_amd/csrc/af_internal.h; not a reference algorithm: the filter
  * only has to keep every read that can hold a bwa seed).
  * code(byte) = 2-bit table 0x8340 indexed by the byte's low 3 bits (A C G T -> 0 1 2 3, N -> 0);
- * key = the 16 codes with base 4w+b at bits 8b+2w; h = key * 0x9E3779B1 (64-bit product);
- * word 1 = hi >> (32-bits) takes three bits picked by bytes 1..3 of lo, word 2 =
- * (hi >> 2) & (2^bits-1) three bits picked by bytes 1..3 of lo rotated right by 4. */
+ * key = the 16 codes with base 4w+b at bits 8b+2w; h = key * 0x9E3779B1 (64-bit product hi:lo);
+ * word 1 = (hi >> 2) & (2^bits-1) gets one bit per byte at (lo byte & 7), word 2 =
+ * lo >> (32-bits) one bit per byte at (hi byte & 7). */
 static inline uint32_t k1_code(uint8_t c) { return (0x8340u >> (2 * (c & 7))) & 3u; }
 static inline uint64_t k1_hash(uint32_t key) { return (uint64_t)key * 0x9E3779B1u; }
 static inline uint32_t k1_mask(uint32_t v) {
-    return (1u << ((v >> 8) & 31)) | (1u << ((v >> 16) & 31)) | (1u << ((v >> 24) & 31));
+    uint32_t m = 0;
+    for (int b = 0; b < 4; ++b) m |= 1u << (8 * b + ((v >> (8 * b)) & 7));
+    return m;
 }
-static inline uint32_t k1_rot4(uint32_t v) { return (v >> 4) | (v << 28); }
-static inline uint32_t k1_w1(uint64_t h, int bits) { return (uint32_t)(h >> 32) >> (32 - bits); }
-static inline uint32_t k1_w2(uint64_t h, int bits) { return ((uint32_t)(h >> 32) >> 2) & ((1u << bits) - 1u); }
+static inline uint32_t k1_w1(uint64_t h, int bits) { return ((uint32_t)(h >> 32) >> 2) & ((1u << bits) - 1u); }
+static inline uint32_t k1_w2(uint64_t h, int bits) { return (uint32_t)h >> (32 - bits); }
 
 static int cmp_u64(const void *a, const void *b) {
     uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
@@ -106,7 +107,7 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
         if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
     }
     /* Bloom filter of the distinct 16-mers: 2^bl_bits 32-bit words, ~2.4 words per key (at
-     * most 2^15), three bits set in each of two words */
+     * most 2^15), four bits set in each of two words */
     int bits = 8;
     while ((double)(1LL << bits) < 2.4 * (double)nd && bits < 15) ++bits;
     I->bl_bits = bits;
@@ -117,7 +118,7 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
         for (int j = 0; j < AFO_K; ++j) key |= ((I->kmer[i] >> (2 * j)) & 3u) << (8 * (j & 3) + 2 * (j >> 2));
         uint64_t h = k1_hash(key);
         I->bloom[k1_w1(h, bits)] |= k1_mask((uint32_t)h);
-        I->bloom[k1_w2(h, bits)] |= k1_mask(k1_rot4((uint32_t)h));
+        I->bloom[k1_w2(h, bits)] |= k1_mask((uint32_t)(h >> 32));
     }
     free(tmp);
     return I;
@@ -134,7 +135,7 @@ const uint32_t *afo_filter_table(const afo_index *I) { return I->bloom; }
 /* a sampled 16-mer (key layout above) is a hit when all six of its Bloom bits are set */
 static int filter_query(const afo_index *I, uint32_t key) {
     uint64_t h = k1_hash(key);
-    uint32_t m1 = k1_mask((uint32_t)h), m2 = k1_mask(k1_rot4((uint32_t)h));
+    uint32_t m1 = k1_mask((uint32_t)h), m2 = k1_mask((uint32_t)(h >> 32));
     return (I->bloom[k1_w1(h, I->bl_bits)] & m1) == m1 && (I->bloom[k1_w2(h, I->bl_bits)] & m2) == m2;
 }
 

@@ -78,3 +78,66 @@ def two_word(h):
 
 run("2 words x 3 bits, premix", h_mix, bits, two_word)
 run("2 words x 3 bits, no premix", h_raw, bits, two_word)
+
+
+def fld(v, b):
+    return np.uint32(1) << ((v >> np.uint32(8 * b)) & np.uint32(31))
+
+
+def split_hl(h):
+    return (h & np.uint64(0xFFFFFFFF)).astype(np.uint32), (h >> np.uint64(32)).astype(np.uint32)
+
+
+def w22(h):   # 2 + 2 bits, fields = lo bytes 0..3
+    lo, hi = split_hl(h)
+    return [(hi >> np.uint32(32 - bits), fld(lo, 0) | fld(lo, 1)),
+            ((hi >> np.uint32(2)) & np.uint32((1 << bits) - 1), fld(lo, 2) | fld(lo, 3))]
+
+
+def w33h(h):  # 3 + 3 bits: word 1 from hi bytes 0,1 + lo byte 3; word 2 from lo bytes 0..2
+    lo, hi = split_hl(h)
+    return [(hi >> np.uint32(32 - bits), fld(hi, 0) | fld(hi, 1) | fld(lo, 3)),
+            ((hi >> np.uint32(2)) & np.uint32((1 << bits) - 1), fld(lo, 0) | fld(lo, 1) | fld(lo, 2))]
+
+
+def w32(h):   # 3 + 2 bits
+    lo, hi = split_hl(h)
+    return [(hi >> np.uint32(32 - bits), fld(hi, 0) | fld(hi, 1) | fld(lo, 3)),
+            ((hi >> np.uint32(2)) & np.uint32((1 << bits) - 1), fld(lo, 0) | fld(lo, 1))]
+
+
+run("2 words x 2 bits (lo bytes)", h_raw, bits, w22)
+run("2 words x 3 bits (hi+lo bytes)", h_raw, bits, w33h)
+run("3 + 2 bits (hi+lo bytes)", h_raw, bits, w32)
+
+BYTEBIT = np.array([1 << i for i in range(8)], dtype=np.uint32)
+
+
+def pmask(v):  # v_perm of one-bit bytes: byte i of the mask = 1 << (byte i of v & 7)
+    out = np.zeros_like(v)
+    for b in range(4):
+        out |= BYTEBIT[(v >> np.uint32(8 * b)) & np.uint32(7)] << np.uint32(8 * b)
+    return out
+
+
+def wp_a(h):  # word1 = hi[31:17] mask(lo), word2 = lo[31:17] mask(hi)
+    lo, hi = split_hl(h)
+    return [(hi >> np.uint32(32 - bits), pmask(lo)), (lo >> np.uint32(32 - bits), pmask(hi))]
+
+
+def wp_b(h):  # word1 = hi[16:2] mask(lo), word2 = hi[31:17] mask(lo >> 4)
+    lo, hi = split_hl(h)
+    return [((hi >> np.uint32(2)) & np.uint32((1 << bits) - 1), pmask(lo)),
+            (hi >> np.uint32(32 - bits), pmask(lo >> np.uint32(4)))]
+
+
+run("perm masks A (hi/lo addresses)", h_raw, bits, wp_a)
+run("perm masks B (hi addresses)", h_raw, bits, wp_b)
+
+
+def wp_a2(h):  # word1 = hi[16:2] mask(lo), word2 = lo[31:17] mask(hi)
+    lo, hi = split_hl(h)
+    return [((hi >> np.uint32(2)) & np.uint32((1 << bits) - 1), pmask(lo)), (lo >> np.uint32(32 - bits), pmask(hi))]
+
+
+run("perm masks A' (hi[16:2] / lo[31:17])", h_raw, bits, wp_a2)
