@@ -99,20 +99,22 @@ __device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const 
     const bool p1 = probe(a1 | (a3 << 4), bloom, bshift, wmask4);
     const bool p2 = probe(a2 | (a4 << 4), bloom, bshift, wmask4);
     const bool p3 = probe(a3 | (a5 << 4), bloom, bshift, wmask4);
+#if AF_K1_ABL == 4  // timing only: positives are kept live but not counted
+    if (in && (p0 | p1 | p2 | p3) && c == -12345) {
+#else
     if (in && (p0 | p1 | p2 | p3)) {
+#endif
         const uint32_t off = (uint32_t)c * 16u;
         const uint32_t r = (uint32_t)(((float)off + 0.5f) * inv_stride);
         const int o = (int)(off - r * (uint32_t)stride);
-        const bool pj[4] = {p0, p1, p2, p3};
-        uint32_t na = 0, nb = 0;  // positives in read r and in read r + 1
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int oo = o + 4 * j;
-            const bool wrap = oo >= stride;
-            const bool ok = pj[j] && (wrap ? oo + AF_K <= 2 * stride : oo + AF_K <= stride);
-            na += ok && !wrap;
-            nb += ok && wrap;
-        }
+        // read r holds the chunk's k-mers j < ja (o + 4j + 16 <= stride); read r + 1 those with
+        // jb <= j < jc (o + 4j >= stride, o + 4j - stride + 16 <= stride)
+        const uint32_t pm = (uint32_t)p0 | ((uint32_t)p1 << 1) | ((uint32_t)p2 << 2) | ((uint32_t)p3 << 3);
+        const int ja = min(max((stride - 12 - o) >> 2, 0), 4);
+        const int jb = min((stride - o + 3) >> 2, 4);
+        const int jc = min(max((2 * stride - 12 - o) >> 2, 0), 4);
+        const uint32_t na = __builtin_popcount(pm & ((1u << ja) - 1u));
+        const uint32_t nb = __builtin_popcount((pm >> jb) & ((1u << max(jc - jb, 0)) - 1u));
         if (na) atomicAdd(&cnt[r >> 2], na << (8 * (r & 3)));
         if (nb) atomicAdd(&cnt[(r + 1) >> 2], nb << (8 * ((r + 1) & 3)));
     }

@@ -133,3 +133,29 @@ def test_lane_kernel_parity(anchor, oidx, monkeypatch):
         g = a.align_pairs(reads).as_dict()
     r = oidx.align_pairs(reads, threads=8)
     assert_records_equal(g, r, reads)
+
+
+@pytest.mark.parametrize("stride", [16, 17, 20, 27, 28, 29, 33, 64, 99, 100, 101, 150, 251, 320])
+def test_seed_filter_strides(aligner, oidx, anchor, stride):
+    """K1 alone: per-read Bloom hits equal the oracle's for every stride class (reads that end
+    inside a 16-byte chunk, chunks spanning two reads, strides below 28 where one chunk's
+    k-mers can straddle a read end), on a batch that leaves a partial last tile."""
+    import torch
+    from anchored_fusion_amd import simulate as sim
+    n = 2 * 2048 * 3 + 777
+    L = min(stride, 150)
+    reads = np.full((n, stride), ord("N"), dtype=np.uint8)
+    r, _, _ = synthetic_pairs(anchor, n // 2 + 1, max(L, 40), seed=stride)
+    reads[:, :min(L, stride)] = r[:n, :min(L, stride)]
+    rng = np.random.default_rng(stride)
+    noise = rng.random(reads.shape) < 0.3                    # background-like bytes too
+    reads[noise] = np.frombuffer(sim.random_seq(rng, int(noise.sum())), dtype=np.uint8)
+    dev = torch.device("cuda:0")
+    rt = torch.from_numpy(reads).to(dev)
+    hits = torch.zeros(n, dtype=torch.int32, device=dev)
+    aligner.seed_filter_device(rt, n, stride, hits)
+    torch.cuda.synchronize()
+    want = oidx.seed_filter(reads)
+    got = hits.cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert aligner.last_candidates() == int((want > 0).sum())
