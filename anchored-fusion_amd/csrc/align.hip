@@ -559,7 +559,7 @@ __device__ __forceinline__ void getD16(const DevIndex &ix, int64_t pos, uint32_t
 
 // gen_cigar restated (bwa_gen_cigar2): returns score, cigar in L.ring/L.misc[2]
 template <int CPL>
-__device__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, int lq, int qb, int64_t rb, int64_t re,
+__device__ __forceinline__ int gen_cigar_wave(const DevIndex &ix, const af_params &p, int w_, int lq, int qb, int64_t rb, int64_t re,
                               AlnLds &L, uint8_t *zg, int lane) {
     const int rlen = (int)(re - rb);
     const bool rev = rb >= ix.n;
