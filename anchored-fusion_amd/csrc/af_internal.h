@@ -10,6 +10,9 @@
 #define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
 #define AF_SEED_GROUPS (AF_SEED_BTILE / 64)  // 64-read ballot groups per tile
 #define AF_ALN_WAVES 4          // waves per alignment workgroup
+#ifndef AF_K2_WPS
+#define AF_K2_WPS 6             // k_align waves per SIMD (launch bound; persistent slots = 4 x this per CU)
+#endif
 #define AF_CPL 6                // DP columns per lane: 6*64 = 384 >= AF_MAX_READ+1
 #define AF_ZCAP 12288           // LDS traceback bytes per wave; larger DPs use global scratch
 #define AF_TMAX (AF_MAX_READ + 2 * 100 * 4 + 64)  // max target window held in LDS

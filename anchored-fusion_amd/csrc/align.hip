@@ -30,7 +30,10 @@ constexpr int PROF_W = 16;
 #define AF_K2_STATIC_PCT 0  // share of candidates assigned round-robin (rest: per-XCD dequeue)
 #endif
 constexpr int MEMCAP = 64;   // == max allowed af_params.max_mems
-constexpr int ZLDS = 6144;   // traceback bytes per wave kept in LDS
+#ifndef AF_K2_ZLDS
+#define AF_K2_ZLDS 2048
+#endif
+constexpr int ZLDS = AF_K2_ZLDS;  // traceback bytes per wave kept in LDS (larger DPs: global scratch)
 
 struct __attribute__((aligned(16))) AlnLds {
     uint64_t mem[MEMCAP];
@@ -594,7 +597,7 @@ __device__ __forceinline__ int gen_cigar_wave(const DevIndex &ix, const af_param
 // MULTI = placement mode (af_place): every region scoring >= T becomes an af_hit (best first,
 // at most max_hits per query); cand == nullptr means "all reads".
 template <int CPL, bool MULTI>
-__global__ __launch_bounds__(64) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
+__global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint8_t *__restrict__ reads, int32_t stride,
                                               const int32_t *__restrict__ lens, af_params p,
                                               const int32_t *__restrict__ cand, const int32_t *__restrict__ n_cand,
                                               int32_t *__restrict__ work, ReadRec *__restrict__ recs,

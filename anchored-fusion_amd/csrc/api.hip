@@ -162,7 +162,7 @@ int af_ctx_create(int device, af_ctx **out) {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     c->n_cu = std::max(1, cus);
-    c->n_slots = c->n_cu * 16;  // k_align: 4 waves per SIMD (VGPR and LDS budget)
+    c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
