@@ -415,6 +415,63 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     return ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
 }
 
+// Traceback of a filled ksw_global2 direction matrix z (n_col = min(qlen, 2w+1) bytes per row),
+// leaving the CIGAR (reverse order) in L.ring with L.misc[2] ops.
+__device__ __forceinline__ void global_traceback(int qlen, int tlen, int w, const uint8_t *z, AlnLds &L, int lane) {
+    const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    wave_sync();
+    PROF(const int64_t tb0 = clock64();)
+    // Traceback, wave-parallel.  The serial walk (bwa ksw_global2) is
+    //   which = z[i][k] >> (2 * which) & 3;  0: M (--i, --k)  1: D (--i)  2: I (--k)
+    // While `which` keeps its value the walk moves in a straight line, so lane t reads the
+    // cell t steps ahead on that line; the first lane whose code differs (or that leaves the
+    // matrix) ends the run.  One LDS read per lane and a ballot per run instead of one
+    // dependent read per step.
+    {
+        const int zsize = n_col * tlen;
+        int i = tlen - 1;
+        int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+        int state = 0, nc = 0, cur_op = -1, cur_len = 0;
+        auto push = [&](int op, int len) {
+            if (len <= 0) return;
+            if (op == cur_op) { cur_len += len; return; }
+            if (cur_op >= 0) {
+                if (lane == 0) L.ring[nc & 63] = (uint32_t)cur_len << 4 | (uint32_t)cur_op;
+                ++nc;
+            }
+            cur_op = op; cur_len = len;
+        };
+        while (i >= 0 && k >= 0) {
+            const int it = i - (state != 2 ? lane : 0), kt = k - (state != 1 ? lane : 0);
+            int wt = -1;
+            if (it >= 0 && kt >= 0) {
+                const int idx = it * n_col + (kt - (it > w ? it - w : 0));
+                if (idx >= 0 && idx < zsize) wt = z[idx] >> (state << 1) & 3;
+            }
+            const uint64_t stop = __ballot(wt != state);
+            const int r = stop ? __ffsll((unsigned long long)stop) - 1 : 64;
+            const int op_state = state == 0 ? 0 : (state == 1 ? 2 : 1);
+            push(op_state, r);
+            if (state != 2) i -= r;
+            if (state != 1) k -= r;
+            if (r == 64) continue;
+            if (i < 0 || k < 0) break;
+            const int which = bcast(wt, r);
+            if (which < 0) break;  // walked off the stored matrix (not reachable from a valid score)
+            if (which == 0) { push(0, 1); --i; --k; }
+            else if (which == 1) { push(2, 1); --i; }
+            else { push(1, 1); --k; }
+            state = which;
+        }
+        if (i >= 0) push(2, i + 1);
+        if (k >= 0) push(1, k + 1);
+        push(-2, 1);  // flush
+        if (lane == 0) L.misc[2] = nc;
+    }
+    wave_sync();
+    PROF(L.misc[3] += (int)(clock64() - tb0);)
+}
+
 // ksw_global2 semantics with traceback (see oracle global_dp).  z: n_col*tlen bytes.
 // Returns the score; the CIGAR (reverse order) is left in L.ring with L.misc[2] ops.
 template <int CPL>
@@ -494,57 +551,58 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         }
     }
     const int score = bcast(pick<CPL>(eh_h, qlen - (qlen / cpl) * cpl), qlen / cpl);
-    wave_sync();
-    PROF(const int64_t tb0 = clock64();)
-    // Traceback, wave-parallel.  The serial walk (bwa ksw_global2) is
-    //   which = z[i][k] >> (2 * which) & 3;  0: M (--i, --k)  1: D (--i)  2: I (--k)
-    // While `which` keeps its value the walk moves in a straight line, so lane t reads the
-    // cell t steps ahead on that line; the first lane whose code differs (or that leaves the
-    // matrix) ends the run.  One LDS read per lane and a ballot per run instead of one
-    // dependent read per step.
+    global_traceback(qlen, tlen, w, z, L, lane);
+    return score;
+}
+
+// ksw_global2 (as global_dp_wave) when the band is at most 64 columns wide (w <= 31): lane k
+// holds column j = i - w + k of row i, so one cell per lane whatever qlen is.  H(i-1, j-1) stays
+// in the lane, E(i, j) arrives from lane k + 1 (wave_shl:1) and the query base moves down one
+// lane per row.  Lanes outside [beg, end) carry -inf, except the H(i, -1) boundary of rows with
+// beg == 0.  Same recurrences, tie-breaks and direction codes as global_dp_wave.
+__device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
+                              uint8_t *z, AlnLds &L, int lane) {
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    const int k = lane;
+    const bool band = k <= 2 * w;
+    int Hd;  // H(i-1, j-1) for this lane's cell of row i; row 0 reads ksw_global2's initial eh[j].h
     {
-        const int zsize = n_col * tlen;
-        int i = tlen - 1;
-        int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
-        int state = 0, nc = 0, cur_op = -1, cur_len = 0;
-        auto push = [&](int op, int len) {
-            if (len <= 0) return;
-            if (op == cur_op) { cur_len += len; return; }
-            if (cur_op >= 0) {
-                if (lane == 0) L.ring[nc & 63] = (uint32_t)cur_len << 4 | (uint32_t)cur_op;
-                ++nc;
-            }
-            cur_op = op; cur_len = len;
-        };
-        while (i >= 0 && k >= 0) {
-            const int it = i - (state != 2 ? lane : 0), kt = k - (state != 1 ? lane : 0);
-            int wt = -1;
-            if (it >= 0 && kt >= 0) {
-                const int idx = it * n_col + (kt - (it > w ? it - w : 0));
-                if (idx >= 0 && idx < zsize) wt = z[idx] >> (state << 1) & 3;
-            }
-            const uint64_t stop = __ballot(wt != state);
-            const int r = stop ? __ffsll((unsigned long long)stop) - 1 : 64;
-            const int op_state = state == 0 ? 0 : (state == 1 ? 2 : 1);
-            push(op_state, r);
-            if (state != 2) i -= r;
-            if (state != 1) k -= r;
-            if (r == 64) continue;
-            if (i < 0 || k < 0) break;
-            const int which = bcast(wt, r);
-            if (which < 0) break;  // walked off the stored matrix (not reachable from a valid score)
-            if (which == 0) { push(0, 1); --i; --k; }
-            else if (which == 1) { push(2, 1); --i; }
-            else { push(1, 1); --k; }
-            state = which;
-        }
-        if (i >= 0) push(2, i + 1);
-        if (k >= 0) push(1, k + 1);
-        push(-2, 1);  // flush
-        if (lane == 0) L.misc[2] = nc;
+        const int j = k - w;
+        Hd = (band && j == 0) ? 0
+                              : ((band && j >= 1 && j <= w && j <= qlen) ? -(p.o_ins + p.e_ins * j) : AF_NEG_INF);
     }
-    wave_sync();
-    PROF(L.misc[3] += (int)(clock64() - tb0);)
+    int Eo = AF_NEG_INF;  // E(i+1, j) produced by this lane's cell of row i
+    int ti_next = tlen > 0 ? t[0] : 4;
+    int qn = (band && k - w >= 0 && k - w < qlen) ? q[k - w] : 4;
+    for (int i = 0; i < tlen; ++i) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
+        const int j = i - w + k;
+        const int qc = qn;
+        qn = (band && j + 1 >= 0 && j + 1 < qlen) ? q[j + 1] : 4;
+        const int beg = i > w ? i - w : 0;
+        const bool in = band && j >= 0 && j < qlen;
+        const int e = dpp<0x130>(AF_NEG_INF, Eo);  // wave_shl:1
+        const int m = Hd + scd(p, ti, qc);
+        const int seed = AF_NEG_INF + (beg - 1) * p.e_ins;
+        const int run = in ? max(seed, m - oe_ins + j * p.e_ins) : seed;
+        const int P = max(wave_shr1(seed, wave_incl_max(run)), seed);
+        const int f = P - (j - 1) * p.e_ins;
+        int d = m >= e ? 0 : 1;
+        int h = m >= e ? m : e;
+        d = h >= f ? d : 2;
+        h = h >= f ? h : f;
+        const int tt = m - oe_del, ee = e - p.e_del;
+        d |= ee > tt ? 1 << 2 : 0;
+        const int tf = m - oe_ins, ff = f - p.e_ins;
+        d |= ff > tf ? 2 << 4 : 0;
+        if (in) z[(size_t)i * n_col + (j - beg)] = (uint8_t)d;
+        Eo = in ? (ee > tt ? ee : tt) : AF_NEG_INF;
+        Hd = in ? h : ((j == -1 && beg == 0) ? -(p.o_del + p.e_del * (i + 1)) : AF_NEG_INF);
+    }
+    const int score = bcast(Hd, qlen - tlen + w);  // eh[qlen].h = H(tlen-1, qlen-1)
+    global_traceback(qlen, tlen, w, z, L, lane);
     return score;
 }
 
@@ -588,8 +646,9 @@ __device__ __forceinline__ int gen_cigar_wave(const DevIndex &ix, const af_param
         w = w > min_w ? w : min_w;
         const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
         uint8_t *z = ((size_t)n_col * rlen <= ZLDS) ? L.z : zg;
-        score = lq + 1 <= 64 ? global_dp_wave<1>(lq, L.qs, rlen, L.t, p, w, z, L, lane)
-                             : global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        if (lq + 1 <= 64) score = global_dp_wave<1>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        else if (w <= 31) score = global_dp_band(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        else score = global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
     }
     return score;
 }
