@@ -307,7 +307,8 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
     }
     const int qc = j < qlen ? q[j] : 4;
     const bool qn = qc > 3;
-    const int jE = j * p.e_ins, jE1 = (j - 1) * p.e_ins, tailA = (qlen - j) * p.a;
+    // lane constants: run = max(M - oe_ins, 0) + jE = max(M + jEo, jE); f = P - jE1
+    const int jE = j * p.e_ins, jEo = jE - oe_ins, jE1 = (j - 1) * p.e_ins, tailA = (qlen - j) * p.a;
     {
         int max_ins = (int)((double)(qlen * p.a + end_bonus - p.o_ins) / p.e_ins + 1.);
         max_ins = max_ins > 1 ? max_ins : 1;
@@ -334,24 +335,29 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
             }
             break;
         }
+        // Lanes left of beg are never read again (beg only grows), so they may hold anything;
+        // lanes right of end keep their H/E exactly as bwa's untouched eh[] entries.  Every
+        // lane outside [beg, end) has M = 0, so its run term (jE) never wins the f scan over the
+        // in-band term at j - 1 (>= 0), and at j == beg the scan gives f = 0 (beg > 0) or a
+        // large negative (beg == 0), both below max(M, E) >= 0: no per-lane masking of f.
         const bool in = j >= beg && j < end;
-        // score: a / -b, -1 when either base is N (ti is wave-uniform)
-        const int sa = ti > 3 ? -1 : p.a, sb = ti > 3 ? -1 : -p.b;
-        const int sc = qn ? -1 : (qc == ti ? sa : sb);
+        // score: a / -b, -1 when either base is N (ti is wave-uniform: keep it in an SGPR)
+        const int tiu = __builtin_amdgcn_readfirstlane(ti);
+        const int s_eq = tiu > 3 ? -1 : p.a, s_ne = tiu > 3 ? -1 : -p.b;
+        const int sc = qc == tiu ? s_eq : (qn ? -1 : s_ne);
         const int M = (in && H != 0) ? H + sc : 0;
-        const int run = in ? max(M - oe_ins, 0) + jE : kMaxId;
-        const int P = wave_shr1(kNeg, wave_incl_max(run));
-        const int f = j > beg ? P - jE1 : 0;
+        const int P = wave_shr1(kNeg, wave_incl_max(max(M + jEo, jE)));
+        const int f = P - jE1;
         const int h = max(max(M, E), f);
-        const int En = in ? max(E - p.e_del, max(M - oe_del, 0)) : E;
         const int key = in ? ((h << 10) | j) : -1;
         const int kmax = wave_max(key);
         const int m = kmax < 0 ? 0 : kmax >> 10;
         const int mj = kmax < 0 ? -1 : (kmax & 1023);
         const int hq = bcast(h, qlen - 1);
-        const int from_left = wave_shr1(0, h);
-        H = j == beg ? h1s : ((j > beg && j <= end) ? from_left : H);
-        E = j == end ? 0 : En;
+        const int from_left = __builtin_amdgcn_mov_dpp(h, 0x138, 0xf, 0xf, true);  // wave_shr:1, lane 0 <- 0
+        const int Eu = max(max(E - p.e_del, M - oe_del), 0);
+        H = j <= end ? (j == beg ? h1s : from_left) : H;
+        E = j < end ? Eu : (j == end ? 0 : E);
         if (end == qlen) {
             max_ie = gscore > hq ? max_ie : i;
             gscore = gscore > hq ? gscore : hq;
