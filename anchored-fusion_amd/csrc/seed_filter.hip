@@ -29,6 +29,9 @@
 #ifndef AF_K1_ABL
 #define AF_K1_ABL 0    // 1 = stream-only timing build (scripts/k1_ablate.sh); 0 = the product kernel
 #endif
+#ifndef AF_K1_DEPTH
+#define AF_K1_DEPTH 4  // chunk loads in flight per wave in k_seed_stream
+#endif
 #ifndef AF_K1_PASS
 #define AF_K1_PASS 8   // full tiles per streaming pass of k_seed_stream (8-bit counters in LDS)
 #endif
@@ -150,7 +153,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
     const int nchunks = __builtin_amdgcn_readfirstlane((int)((bytes + 15) >> 4));
     const int nblk = (nchunks + 62) / 63;                            // 63-chunk wave blocks
     const int nround = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of this wave
-    const bool l63 = lane < 63;
+    [[maybe_unused]] const bool l63 = lane < 63;
     for (int r = 0; r < nround; ++r) {
         const int c = AF_CH(r) + lane;
         const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     const int KF = full_tiles > B ? (int)((full_tiles - B + G - 1) / G) : 0;  // this block's full tiles
     const int NCH = (AF_SEED_BTILE * stride) >> 4;  // chunks per full tile (2048 * stride is 16-aligned)
     const int NR = ((NCH + 62) / 63 + AF_SEED_WAVES - 1) / AF_SEED_WAVES;   // rounds per wave per tile
-    const bool l63 = lane < 63;
+    [[maybe_unused]] const bool l63 = lane < 63;
     const int64_t tile_bytes = (int64_t)AF_SEED_BTILE * stride;
     for (int p0 = 0; p0 < KF; p0 += AF_K1_PASS) {
         const int nt = min(AF_K1_PASS, KF - p0);
@@ -275,14 +278,12 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
         // the compiler barriers pin the issue order (b0 oldest), so the waits below count to
         // vmcnt(3) on the loop's entry edge as on its back edge
 #define AF_PIN asm volatile("" ::: "memory")
-        uint4 b0 = next_load();
-        AF_PIN;
-        uint4 b1 = next_load();
-        AF_PIN;
-        uint4 b2 = next_load();
-        AF_PIN;
-        uint4 b3 = next_load();
-        AF_PIN;
+        uint4 b[AF_K1_DEPTH];
+#pragma unroll
+        for (int u = 0; u < AF_K1_DEPTH; ++u) {
+            b[u] = next_load();
+            AF_PIN;
+        }
         int st = 0, sr = 0;
 #if AF_K1_ABL
         uint32_t abl = 0;
@@ -297,16 +298,18 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
             if (++sr == NR) { sr = 0; ++st; }
         };
         int g = 0;
-        for (; g + 4 <= total; g += 4) {
-            scan(b0); b0 = next_load(); AF_PIN;
-            scan(b1); b1 = next_load(); AF_PIN;
-            scan(b2); b2 = next_load(); AF_PIN;
-            scan(b3); b3 = next_load(); AF_PIN;
+        for (; g + AF_K1_DEPTH <= total; g += AF_K1_DEPTH) {
+#pragma unroll
+            for (int u = 0; u < AF_K1_DEPTH; ++u) {
+                scan(b[u]);
+                b[u] = next_load();
+                AF_PIN;
+            }
         }
 #undef AF_PIN
-        if (g < total) scan(b0);
-        if (g + 1 < total) scan(b1);
-        if (g + 2 < total) scan(b2);
+#pragma unroll
+        for (int u = 0; u < AF_K1_DEPTH - 1; ++u)
+            if (g + u < total) scan(b[u]);
 #if AF_K1_ABL
         if (abl == 0x12345679u) cntp[0] = abl;  // keep the ablated work live
 #endif
