@@ -54,10 +54,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; AF_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # devices round-robin) -- the driver's runs use RCCL ("nccl") with one GPU per rank
+    backend = os.environ.get("AF_BENCH_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
     L = args.read_len
@@ -67,7 +74,7 @@ def main():
     reads_t = torch.from_numpy(reads).to(dev)
     out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
     out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
-    al = AnchorAligner(anchor, device=local)
+    al = AnchorAligner(anchor, device=gpu)
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
@@ -99,7 +106,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     k1_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
