@@ -42,6 +42,7 @@ struct __attribute__((aligned(16))) AlnLds {
     uint32_t ring[64];     // traceback CIGAR ring
     int32_t misc[8];       // [0] nmem (total found), [2] n traceback ops
     uint8_t q[AF_MAX_READ + 16];
+    uint8_t qs_pad[16];    // qs_pad[15] = qs[-1] (read as N by the band DP)
     uint8_t qs[AF_MAX_READ + 16];
     uint8_t t[1024];
     uint8_t z[ZLDS];
@@ -567,34 +568,37 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
 // lane per row.  Lanes outside [beg, end) carry -inf, except the H(i, -1) boundary of rows with
 // beg == 0.  Same recurrences, tie-breaks and direction codes as global_dp_wave.
 __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
-                              uint8_t *z, AlnLds &L, int lane) {
+                              uint8_t *__restrict__ zg, AlnLds &L, int lane) {
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
-    const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+    const int n_col = 2 * w + 1;  // qlen >= 64 > 2w + 1
     const int k = lane;
     const bool band = k <= 2 * w;
+    // q[-1] and q[qlen] read as N: the query base of any lane is one clamped LDS read
+    if (lane == 0) { L.qs_pad[15] = 4; L.qs[qlen] = 4; }
     int Hd;  // H(i-1, j-1) for this lane's cell of row i; row 0 reads ksw_global2's initial eh[j].h
     {
         const int j = k - w;
         Hd = (band && j == 0) ? 0
                               : ((band && j >= 1 && j <= w && j <= qlen) ? -(p.o_ins + p.e_ins * j) : AF_NEG_INF);
     }
-    int Eo = AF_NEG_INF;  // E(i+1, j) produced by this lane's cell of row i
+    int Eo = AF_NEG_INF;     // E(i+1, j) produced by this lane's cell of row i
+    int j = k - w;           // this lane's column in row i (advances one per row)
+    int jE1 = (j - 1) * p.e_ins, jEo = j * p.e_ins - oe_ins;
+    wave_sync();
+    int qc = q[min(max(j, -1), qlen)];
     int ti_next = tlen > 0 ? t[0] : 4;
-    int qn = (band && k - w >= 0 && k - w < qlen) ? q[k - w] : 4;
     for (int i = 0; i < tlen; ++i) {
-        const int ti = ti_next;
+        const int ti = __builtin_amdgcn_readfirstlane(ti_next);
         if (i + 1 < tlen) ti_next = t[i + 1];
-        const int j = i - w + k;
-        const int qc = qn;
-        qn = (band && j + 1 >= 0 && j + 1 < qlen) ? q[j + 1] : 4;
         const int beg = i > w ? i - w : 0;
-        const bool in = band && j >= 0 && j < qlen;
-        const int e = dpp<0x130>(AF_NEG_INF, Eo);  // wave_shl:1
-        const int m = Hd + scd(p, ti, qc);
+        const bool in = band && (unsigned)j < (unsigned)qlen;
+        const int qn = q[min(max(j + 1, -1), qlen)];  // next row's base for this lane
+        const int s_eq = ti > 3 ? -1 : p.a, s_ne = ti > 3 ? -1 : -p.b;
+        const int m = Hd + (qc == ti ? s_eq : (qc > 3 ? -1 : s_ne));
+        const int e = dpp<0x130>(AF_NEG_INF, Eo);  // wave_shl:1: E(i, j) from lane k + 1
         const int seed = AF_NEG_INF + (beg - 1) * p.e_ins;
-        const int run = in ? max(seed, m - oe_ins + j * p.e_ins) : seed;
-        const int P = max(wave_shr1(seed, wave_incl_max(run)), seed);
-        const int f = P - (j - 1) * p.e_ins;
+        const int run = in ? max(seed, m + jEo) : seed;
+        const int f = wave_shr1(seed, wave_incl_max(run)) - jE1;
         int d = m >= e ? 0 : 1;
         int h = m >= e ? m : e;
         d = h >= f ? d : 2;
@@ -603,12 +607,17 @@ __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_
         d |= ee > tt ? 1 << 2 : 0;
         const int tf = m - oe_ins, ff = f - p.e_ins;
         d |= ff > tf ? 2 << 4 : 0;
-        if (in) z[(size_t)i * n_col + (j - beg)] = (uint8_t)d;
+        // z row i, column j - beg = k - max(w - i, 0): a uniform row base plus the lane
+        if (in) zg[(uint32_t)(i * n_col - (w - i > 0 ? w - i : 0)) + (uint32_t)k] = (uint8_t)d;
         Eo = in ? (ee > tt ? ee : tt) : AF_NEG_INF;
         Hd = in ? h : ((j == -1 && beg == 0) ? -(p.o_del + p.e_del * (i + 1)) : AF_NEG_INF);
+        qc = qn;
+        ++j;
+        jE1 += p.e_ins;
+        jEo += p.e_ins;
     }
     const int score = bcast(Hd, qlen - tlen + w);  // eh[qlen].h = H(tlen-1, qlen-1)
-    global_traceback(qlen, tlen, w, z, L, lane);
+    global_traceback(qlen, tlen, w, zg, L, lane);
     return score;
 }
 
@@ -653,7 +662,7 @@ __device__ __forceinline__ int gen_cigar_wave(const DevIndex &ix, const af_param
         const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
         uint8_t *z = ((size_t)n_col * rlen <= ZLDS) ? L.z : zg;
         if (lq + 1 <= 64) score = global_dp_wave<1>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
-        else if (w <= 31) score = global_dp_band(lq, L.qs, rlen, L.t, p, w, z, L, lane);
+        else if (w <= 31) score = global_dp_band(lq, L.qs, rlen, L.t, p, w, zg, L, lane);
         else score = global_dp_wave<CPL>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
     }
     return score;
