@@ -41,6 +41,8 @@ struct __attribute__((aligned(16))) AlnLds {
     int32_t regs[16][8];   // score, truesc, qb, qe, rb, re, seedlen0, w
     uint32_t ring[64];     // traceback CIGAR ring
     int32_t misc[8];       // [0] nmem (total found), [2] n traceback ops
+    uint32_t pk[AF_MAX_READ / 16 + 2];  // the read as 2-bit codes, 16 bases per word (base i at bits 2i)
+    uint32_t nm[AF_MAX_READ / 16 + 2];  // N bits of the same bases (positions >= l set)
     uint8_t q[AF_MAX_READ + 16];
     uint8_t qs_pad[16];    // qs_pad[15] = qs[-1] (read as N by the band DP)
     uint8_t qs[AF_MAX_READ + 16];
@@ -732,17 +734,32 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
         if (lane == 0) L.misc[0] = 0;
         PROF(if (lane < 8 && lane >= 3) L.misc[lane] = 0;)
         wave_sync();
+        // pack the codes: lane w owns bases 16w..16w+15 (2-bit codes + an N mask that also
+        // covers every position >= l), so any lane can form a 16-mer with one funnel shift
+        if (lane < AF_MAX_READ / 16 + 2) {
+            const int b0 = lane * 16;
+            uint32_t pw = 0, nw = 0;
+            if (b0 < l) {
+                const uint4 c = *reinterpret_cast<const uint4 *>(&L.q[b0]);
+                const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t y = cw[u] & 0x03030303u, t = y | (y >> 6);
+                    pw |= ((t & 0xFu) | ((t >> 12) & 0xF0u)) << (8 * u);
+                    nw |= ((((cw[u] >> 2) & 0x01010101u) * 0x01020408u) >> 24 & 0xFu) << (4 * u);
+                }
+            }
+            const int valid = l - b0;  // bases of this word inside the read
+            if (valid < 16) nw |= valid <= 0 ? 0xFFFFu : (0xFFFFu << valid) & 0xFFFFu;
+            L.pk[lane] = pw;
+            L.nm[lane] = nw;
+        }
+        wave_sync();
         // ---- 1. MEMs ------------------------------------------------------------------
         for (int qb = lane; qb + AF_K <= l; qb += 64) {
-            uint32_t k = 0;
-            bool ok = true;
-#pragma unroll
-            for (int u = 0; u < AF_K; ++u) {
-                const int c = L.q[qb + u];
-                ok &= c < 4;
-                k |= (uint32_t)(c & 3) << (2 * u);
-            }
-            if (!ok) continue;
+            const int wq = qb >> 4, sq = qb & 15;
+            const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
+            if (((L.nm[wq] | (L.nm[wq + 1] << 16)) >> sq) & 0xFFFFu) continue;
             uint32_t s = af_fmix(k) & hm;
             int cnt = 0, st = 0;
             for (;;) {
@@ -766,13 +783,9 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                     const int64_t room64 = min((int64_t)(l - qp), lim - rp);
                     if (room64 <= 0) break;
                     const int room = (int)min(room64, (int64_t)16);
-                    uint32_t qk = 0;
-                    int qn = 16;
-                    for (int u = 0; u < 16; ++u) {
-                        const int c = qp + u < l ? L.q[qp + u] : 4;
-                        if (c > 3 && qn == 16) qn = u;
-                        qk |= (uint32_t)(c & 3) << (2 * u);
-                    }
+                    const int wp = qp >> 4, sp = qp & 15;
+                    const uint32_t qk = __builtin_amdgcn_alignbit(L.pk[wp + 1], L.pk[wp], 2 * sp);
+                    const int qn = __builtin_ctz((((L.nm[wp] | (L.nm[wp + 1] << 16)) >> sp) & 0xFFFFu) | 0x10000u);
                     uint32_t dk, dn;
                     getD16(ix, rp, dk, dn);
                     const uint32_t x = qk ^ dk;
