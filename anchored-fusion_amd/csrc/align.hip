@@ -320,7 +320,13 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         max_del = max_del > 1 ? max_del : 1;
         w = w < max_del ? w : max_del;
     }
-    int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    // Split of the per-row bookkeeping between the two issue ports.  The scalar unit is shared
+    // by a CU's four SIMDs and bounds this loop, so the band (beg, end), the row index and the
+    // target base stay in SGPRs while the maxima, z-drop, gscore and early-exit state are
+    // wave-uniform values in VGPRs, updated with selects (`vz` is 0 but opaque to the
+    // compiler's uniformity analysis) and tested through one readfirstlane per decision.
+    const int vz = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);
+    int mx = h0 + vz, max_i = vz - 1, max_j = vz - 1, max_ie = vz - 1, gscore = vz - 1, max_off = vz;
     int beg = 0, end = qlen, rows = 0;
     int ti_next = tlen > 0 ? t[0] : 4;
     for (int i = 0; i < tlen; ++i) {
@@ -333,7 +339,7 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         if (beg == 0) h1s = max(h0 - (p.o_del + p.e_del * (i + 1)), 0);
         if (beg >= end) {
             if (beg == qlen) {
-                max_ie = gscore > h1s ? max_ie : i;
+                max_ie = gscore > h1s ? max_ie : i + vz;
                 gscore = gscore > h1s ? gscore : h1s;
             }
             break;
@@ -343,55 +349,56 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         // lane outside [beg, end) has M = 0, so its run term (jE) never wins the f scan over the
         // in-band term at j - 1 (>= 0), and at j == beg the scan gives f = 0 (beg > 0) or a
         // large negative (beg == 0), both below max(M, E) >= 0: no per-lane masking of f.
-        const bool in = j >= beg && j < end;
+        const bool in = (unsigned)(j - beg) < (unsigned)(end - beg);
         // score: a / -b, -1 when either base is N (ti is wave-uniform: keep it in an SGPR)
         const int tiu = __builtin_amdgcn_readfirstlane(ti);
         const int s_eq = tiu > 3 ? -1 : p.a, s_ne = tiu > 3 ? -1 : -p.b;
         const int sc = qc == tiu ? s_eq : (qn ? -1 : s_ne);
-        const int M = (in && H != 0) ? H + sc : 0;
+        int M = H != 0 ? H + sc : 0;
+        M = in ? M : 0;
         const int P = wave_shr1(kNeg, wave_incl_max(max(M + jEo, jE)));
         const int f = P - jE1;
         const int h = max(max(M, E), f);
         const int key = in ? ((h << 10) | j) : -1;
-        const int kmax = wave_max(key);
-        const int m = kmax < 0 ? 0 : kmax >> 10;
+        const int kmax = wave_max(key) + vz;
+        const int m = max(kmax, 0) >> 10;
         const int mj = kmax < 0 ? -1 : (kmax & 1023);
-        const int hq = bcast(h, qlen - 1);
+        const int hq = bcast(h, qlen - 1) + vz;
         const int from_left = __builtin_amdgcn_mov_dpp(h, 0x138, 0xf, 0xf, true);  // wave_shr:1, lane 0 <- 0
         const int Eu = max(max(E - p.e_del, M - oe_del), 0);
         H = j <= end ? (j == beg ? h1s : from_left) : H;
         E = j < end ? Eu : (j == end ? 0 : E);
-        if (end == qlen) {
-            max_ie = gscore > hq ? max_ie : i;
-            gscore = gscore > hq ? gscore : hq;
+        if (end == qlen) {  // scalar test, vector update
+            max_ie = gscore > hq ? max_ie : i + vz;
+            gscore = max(gscore, hq);
         }
-        if (m == 0) break;
-        if (m > mx) {
-            mx = m; max_i = i; max_j = mj;
-            const int off = mj - i < 0 ? i - mj : mj - i;
-            max_off = max_off > off ? max_off : off;
-        } else if (zdrop > 0) {
-            if (i - max_i > mj - max_j) {
-                if (mx - m - ((i - max_i) - (mj - max_j)) * p.e_del > zdrop) break;
-            } else {
-                if (mx - m - ((mj - max_j) - (i - max_i)) * p.e_ins > zdrop) break;
-            }
-        }
+        // bwa: break on m == 0; else a new maximum, or the z-drop test against the old one
+        const bool better = m > mx;
+        const int di = i - max_i, dj = mj - max_j;
+        const int zgap = di > dj ? mx - m - (di - dj) * p.e_del : mx - m - (dj - di) * p.e_ins;
+        const int zt = better ? INT_MIN : zgap;
+        const int off = mj - i < 0 ? i - mj : mj - i;
+        max_off = better ? max(max_off, off) : max_off;
+        max_i = better ? i + vz : max_i;
+        max_j = better ? mj : max_j;
+        mx = better ? m : mx;
+        const int stop = m == 0 ? 1 : (zt > zdrop ? zdrop : 0);  // zdrop > 0 for a z-drop break
+        if (__builtin_amdgcn_readfirstlane(stop) > 0) break;
         // band trimming: first non-zero eh in [beg, end), last in [beg, end]
-        const uint64_t nz = __ballot((H | E) != 0);
-        const uint64_t lo = ~0ull << beg;
-        const uint64_t f_m = nz & lo & ((1ull << end) - 1ull);  // end <= 63
-        const uint64_t l_m = nz & lo & (end >= 63 ? ~0ull : ((2ull << end) - 1ull));
+        const int x = (H | E) != 0 ? j - beg : 1 << 20;
+        const uint64_t f_m = __ballot((unsigned)x < (unsigned)(end - beg));
+        const uint64_t l_m = __ballot((unsigned)x <= (unsigned)(end - beg));
         const int beg_new = f_m ? (int)__builtin_ctzll(f_m) : end;
         const int lnz = l_m ? 63 - (int)__builtin_clzll(l_m) : -1;
         const int jstar = lnz >= beg_new ? lnz : beg_new - 1;
         beg = beg_new;
         end = jstar + 2 < qlen ? jstar + 2 : qlen;
-        // exact early exit (see ext_dp_wave)
-        if ((i & 1) && gscore > 0) {
-            const int u = (j >= beg && j <= qlen) ? max(H, E) + tailA : 0;
-            const int U = wave_max(u);
-            if (U <= mx && U < gscore) break;
+        // exact early exit (see ext_dp_wave), on odd rows
+        if (i & 1) {
+            const int u = (unsigned)(j - beg) <= (unsigned)(qlen - beg) ? max(H, E) + tailA : 0;
+            const int U = wave_max(u) + vz;
+            const int g = U <= mx ? (U < gscore ? gscore : 0) : 0;  // > 0 iff gscore > 0, U <= max, U < gscore
+            if (__builtin_amdgcn_readfirstlane(g) > 0) break;
         }
     }
     ExtRes r;
