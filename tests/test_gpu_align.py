@@ -159,3 +159,28 @@ def test_seed_filter_strides(aligner, oidx, anchor, stride):
     got = hits.cpu().numpy()
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     assert aligner.last_candidates() == int((want > 0).sum())
+
+
+@pytest.mark.parametrize("stride", [20, 33, 100, 151, 320])
+def test_seed_filter_ragged_strides(aligner, oidx, anchor, stride):
+    """K1's ragged path (per-read lengths, k_seed_ragged): hits equal the oracle's for reads of
+    every length 0..stride, including lengths below one 16-mer."""
+    import torch
+    n = 2 * 2048 * 2 + 313
+    reads = np.full((n, stride), ord("N"), dtype=np.uint8)
+    r, _, _ = synthetic_pairs(anchor, n // 2 + 1, min(max(stride, 40), 250), seed=1000 + stride)
+    w = min(stride, r.shape[1])
+    reads[:, :w] = r[:n, :w]
+    rng = np.random.default_rng(stride)
+    lens = rng.integers(0, stride + 1, size=n).astype(np.int32)
+    lens[:64] = np.arange(64) % (stride + 1)
+    dev = torch.device("cuda:0")
+    rt = torch.from_numpy(reads).to(dev)
+    lt = torch.from_numpy(lens).to(dev)
+    hits = torch.zeros(n, dtype=torch.int32, device=dev)
+    aligner.seed_filter_device(rt, n, stride, hits, lens_t=lt)
+    torch.cuda.synchronize()
+    want = oidx.seed_filter(reads, lens)
+    got = hits.cpu().numpy()
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert aligner.last_candidates() == int((want > 0).sum())
