@@ -234,135 +234,142 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
         one_tile<true>(k, reads, n_reads, tile, lens, cnt, gbal, gbase, hits, cand, cnt_g);
 }
 
-// Uniform-length batches.  A block's FULL tiles are streamed in passes of up to
-// AF_K1_PASS tiles: each wave keeps AF_K1_DEPTH chunk loads in flight straight through the
-// pass (tile boundaries included), counting into per-tile 8-bit counters in LDS.  The loop
-// body has no global stores, no atomics that return and no barriers, so every wait is a
-// counted `vmcnt(DEPTH-1)`.  One epilogue per pass writes the hits, and one device atomic per
-// pass reserves the candidate slots.  A partial last tile is finished unpipelined (one_tile).
+// Uniform-length batches.  Block B streams ONE contiguous range of reads, an equal share of
+// the batch (ranges differ by at most one alignment unit of u = 16 / gcd(stride, 16) reads,
+// so every range starts on a 16-byte boundary).  Inside the range the waves sweep 63-chunk
+// blocks round-robin with AF_K1_DEPTH chunk loads in flight per wave; the loop body has no
+// global stores, no returning atomics and no barriers, so every wait is a counted
+// `vmcnt(DEPTH-1)`.  Per-read 8-bit counters for the whole range live in LDS (ranges longer
+// than AF_K1_PASS * AF_SEED_BTILE reads are streamed in sub-ranges); one epilogue writes the
+// hits, and one device atomic reserves the candidate slots.  The first loads are issued
+// before the Bloom table is copied to LDS, so HBM streaming starts with the launch.
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const uint32_t *__restrict__ bloom_g,
     int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand, int32_t *__restrict__ cnt_g,
     int32_t *__restrict__ cnt_next) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int CAP = AF_K1_PASS * AF_SEED_BTILE;  // reads per sub-range (LDS counters)
     const int nw = 1 << bl_bits;
-    uint32_t *cntp = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);  // [AF_K1_PASS][AF_SEED_BTILE / 4]
-    uint64_t *gbal = reinterpret_cast<uint64_t *>(cntp + AF_K1_PASS * (AF_SEED_BTILE / 4));
-    int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);  // [CAP / 4]
+    uint64_t *gbal = reinterpret_cast<uint64_t *>(cnt + CAP / 4);
+    int *gbase = reinterpret_cast<int *>(gbal + CAP / 64);
     const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int lane = k.lane, wv = k.wv;
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
-    fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
-    const int64_t full_tiles = n_reads / AF_SEED_BTILE;
-    const int G = (int)gridDim.x, B = (int)blockIdx.x;
-    const int KF = full_tiles > B ? (int)((full_tiles - B + G - 1) / G) : 0;  // this block's full tiles
-    const int NCH = (AF_SEED_BTILE * stride) >> 4;  // chunks per full tile (2048 * stride is 16-aligned)
-    const int NR = ((NCH + 62) / 63 + AF_SEED_WAVES - 1) / AF_SEED_WAVES;   // rounds per wave per tile
+    // this block's range [ra, rb) in units of u reads
+    const int lowbit = stride & -stride;  // gcd(stride, 16) = min(lowbit, 16)
+    const int u = 16 / (lowbit < 16 ? lowbit : 16);
+    const int64_t nunits = (n_reads + u - 1) / u;
+    const int64_t G = gridDim.x, B = blockIdx.x;
+    const int64_t ra = min(n_reads, (B * nunits / G) * u), rb = min(n_reads, ((B + 1) * nunits / G) * u);
     [[maybe_unused]] const bool l63 = lane < 63;
-    const int64_t tile_bytes = (int64_t)AF_SEED_BTILE * stride;
-    for (int p0 = 0; p0 < KF; p0 += AF_K1_PASS) {
-        const int nt = min(AF_K1_PASS, KF - p0);
-        for (int i = threadIdx.x; i < nt * (AF_SEED_BTILE / 4); i += blockDim.x) cntp[i] = 0;
-        __syncthreads();
-        const int total = nt * NR;
-        // load position (lt, lr) runs AF_K1_DEPTH rounds ahead of the scan position (st, sr)
-        int lt = 0, lr = 0;
+    bool filled = false;
+    for (int64_t sa = ra; sa < rb; sa += CAP) {
+        const int nr = (int)min((int64_t)CAP, rb - sa);
+        const uint8_t *base = reads + sa * (int64_t)stride;
+        const int64_t bytes = (int64_t)nr * stride;
+        const int nfull = (int)(bytes >> 4), nchunks = (int)((bytes + 15) >> 4);
+        const int nblk = (nchunks + 62) / 63;
+        const int total = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of every wave
+        // round r of wave wv covers chunks AF_CH(r) + lane; chunks past the last full one are
+        // loaded (clamped) and then re-read byte-wise by load_tail in the scan
+        int lr = 0;
         auto next_load = [&]() -> uint4 {
-            const int t = lt < nt ? lt : nt - 1, r = lt < nt ? lr : NR - 1;  // past the pass: re-read
-            const uint4 *cb = reinterpret_cast<const uint4 *>(reads + (B + (int64_t)(p0 + t) * G) * tile_bytes);
-            const uint4 v = cb[min(AF_CH(r) + lane, NCH - 1)];
-            if (++lr == NR) { lr = 0; ++lt; }
-            return v;
+            const int c = min(AF_CH(min(lr, total - 1)) + lane, nfull > 0 ? nfull - 1 : 0);
+            ++lr;
+            return reinterpret_cast<const uint4 *>(base)[c];
         };
-        // the compiler barriers pin the issue order (b0 oldest), so the waits below count to
-        // vmcnt(3) on the loop's entry edge as on its back edge
 #define AF_PIN asm volatile("" ::: "memory")
         uint4 b[AF_K1_DEPTH];
 #pragma unroll
-        for (int u = 0; u < AF_K1_DEPTH; ++u) {
-            b[u] = next_load();
+        for (int q = 0; q < AF_K1_DEPTH; ++q) {
+            b[q] = next_load();
             AF_PIN;
         }
-        int st = 0, sr = 0;
+        if (!filled) {  // the Bloom table, while the first chunk loads are in flight
+            fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
+            filled = true;
+        }
+        for (int i = threadIdx.x; i < (nr + 3) / 4; i += blockDim.x) cnt[i] = 0;
+        __syncthreads();
+        int sr = 0;
 #if AF_K1_ABL
         uint32_t abl = 0;
 #endif
-        auto scan = [&](const uint4 &v) {
+        auto scan = [&](uint4 v) {
+            const int c = AF_CH(sr) + lane;
+            if (c >= nfull && c < nchunks) v = load_tail(base, c, bytes);  // the batch's last chunk
 #if AF_K1_ABL == 1
             abl ^= v.x ^ v.y ^ v.z ^ v.w;
 #else
-            scan_round(v, AF_CH(sr) + lane, l63 && AF_CH(sr) + lane < NCH, k.bloom, k.bshift, k.wmask4, stride,
-                       k.inv_stride, cntp + st * (AF_SEED_BTILE / 4));
+            scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
 #endif
-            if (++sr == NR) { sr = 0; ++st; }
+            ++sr;
         };
         int g = 0;
         for (; g + AF_K1_DEPTH <= total; g += AF_K1_DEPTH) {
 #pragma unroll
-            for (int u = 0; u < AF_K1_DEPTH; ++u) {
-                scan(b[u]);
-                b[u] = next_load();
+            for (int q = 0; q < AF_K1_DEPTH; ++q) {
+                scan(b[q]);
+                b[q] = next_load();
                 AF_PIN;
             }
         }
 #undef AF_PIN
 #pragma unroll
-        for (int u = 0; u < AF_K1_DEPTH - 1; ++u)
-            if (g + u < total) scan(b[u]);
+        for (int q = 0; q < AF_K1_DEPTH - 1; ++q)
+            if (g + q < total) scan(b[q]);
 #if AF_K1_ABL
-        if (abl == 0x12345679u) cntp[0] = abl;  // keep the ablated work live
+        if (abl == 0x12345679u) cnt[0] = abl;  // keep the ablated work live
 #endif
-        __syncthreads();  // the pass is counted
-        // epilogue: hits and ballots of every tile, one atomic for the pass
-        for (int q = wv; q < nt * AF_SEED_GROUPS; q += AF_SEED_WAVES) {
-            const int t = q / AF_SEED_GROUPS, gq = q - t * AF_SEED_GROUPS;
-            const int i = gq * 64 + lane;
-            const uint32_t *cnt = cntp + t * (AF_SEED_BTILE / 4);
-            const uint32_t h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-            hits[(B + (int64_t)(p0 + t) * G) * AF_SEED_BTILE + i] = (int32_t)h;
+        __syncthreads();  // the sub-range is counted
+        // epilogue: hits and 64-read ballots, one atomic for the sub-range
+        const int ng = (nr + 63) / 64;
+        for (int q = wv; q < ng; q += AF_SEED_WAVES) {
+            const int i = q * 64 + lane;
+            uint32_t h = 0;
+            if (i < nr) {
+                h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                hits[sa + i] = (int32_t)h;
+            }
             const uint64_t bal = __ballot(h != 0);
             if (lane == 0) gbal[q] = bal;
         }
         __syncthreads();
         if (wv == 0) {
-            // exclusive prefix over the pass's nt*32 groups, 64 per step
-            int carry = 0;
-            for (int q0 = 0; q0 < nt * AF_SEED_GROUPS; q0 += 64) {
+            int carry = 0;  // exclusive prefix over the groups, 64 per step
+            for (int q0 = 0; q0 < ng; q0 += 64) {
                 const int q = q0 + lane;
-                const int c = q < nt * AF_SEED_GROUPS ? (int)__popcll(gbal[q]) : 0;
+                const int c = q < ng ? (int)__popcll(gbal[q]) : 0;
                 int incl = c;
                 for (int d = 1; d < 64; d <<= 1) {
-                    const int u = __shfl_up(incl, d);
-                    if (lane >= d) incl += u;
+                    const int t = __shfl_up(incl, d);
+                    if (lane >= d) incl += t;
                 }
-                if (q < nt * AF_SEED_GROUPS) gbase[q] = carry + incl - c;
+                if (q < ng) gbase[q] = carry + incl - c;
                 carry += __shfl(incl, 63);
             }
             int bse = 0;
             if (lane == 0 && carry) bse = atomicAdd(cnt_g, carry);
             bse = __shfl(bse, 0);
-            for (int q = lane; q < nt * AF_SEED_GROUPS; q += 64) gbase[q] += bse;
+            for (int q = lane; q < ng; q += 64) gbase[q] += bse;
         }
         __syncthreads();
-        for (int q = wv; q < nt * AF_SEED_GROUPS; q += AF_SEED_WAVES) {
-            const int t = q / AF_SEED_GROUPS, gq = q - t * AF_SEED_GROUPS;
+        for (int q = wv; q < ng; q += AF_SEED_WAVES) {
             const uint64_t bal = gbal[q];
             if ((bal >> lane) & 1ull)
-                cand[gbase[q] + __popcll(bal & ((1ull << lane) - 1ull))] =
-                    (int32_t)((B + (int64_t)(p0 + t) * G) * AF_SEED_BTILE + gq * 64 + lane);
+                cand[gbase[q] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(sa + q * 64 + lane);
         }
         __syncthreads();
     }
-    // partial last tile (n_reads not a multiple of the tile), on the block that owns it
-    if (n_reads % AF_SEED_BTILE != 0 && full_tiles % G == B)
-        one_tile<false>(k, reads, n_reads, full_tiles, nullptr, cntp, gbal, gbase, hits, cand, cnt_g);
 }
 #undef AF_CH
 
 }  // namespace
 
-// dynamic LDS: Bloom words, then per-pass 8-bit read counters, then ballots and bases
+// dynamic LDS: Bloom words, then 8-bit read counters (AF_K1_PASS * AF_SEED_BTILE reads),
+// then 64-read ballots and candidate bases
 size_t af_seed_filter_lds(int bl_bits) {
     return ((size_t)1 << bl_bits) * 4 + AF_K1_PASS * AF_SEED_BTILE + AF_K1_PASS * AF_SEED_GROUPS * 12;
 }
