@@ -55,7 +55,9 @@ __host__ __device__ static inline uint32_t af_k1_key(uint32_t packed) {
 // so neither word's bits come from the half of h that indexes it.  On the device a mask is
 // one v_and + one v_perm_b32 over the one-hot bytes 01 02 .. 80.
 #define AF_K1_MUL 0x9E3779B1u
+#ifndef AF_K1_MAX_BITS
 #define AF_K1_MAX_BITS 15
+#endif
 __host__ __device__ static inline uint64_t af_k1_hash(uint32_t key) { return (uint64_t)key * AF_K1_MUL; }
 __host__ __device__ static inline uint32_t af_k1_mask(uint32_t v) {
     uint32_t m = 0;

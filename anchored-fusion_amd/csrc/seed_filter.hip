@@ -32,6 +32,9 @@
 #ifndef AF_K1_DEPTH
 #define AF_K1_DEPTH 4  // chunk loads in flight per wave in k_seed_stream
 #endif
+#ifndef AF_K1_NT
+#define AF_K1_NT 0     // 1 = nontemporal (nt) stream loads of the reads
+#endif
 #ifndef AF_K1_PASS
 #define AF_K1_PASS 8   // full tiles per streaming pass of k_seed_stream (8-bit counters in LDS)
 #endif
@@ -72,17 +75,46 @@ __device__ __forceinline__ void fill_lds(uint2 *dst, const uint2 *__restrict__ s
     for (int i = i0 + (int)threadIdx.x; i < n; i += 1024) dst[i] = src[i];
 }
 
+// the last round(s) of a range: the chunk that straddles the range end is re-read byte-wise
+// (out of line, so the common rounds carry no per-lane test)
+__device__ __noinline__ uint4 tail_fix(uint4 v, int c, int nfull, int nchunks, const uint8_t *__restrict__ base,
+                                       int64_t bytes) {
+    return c >= nfull && c < nchunks ? load_tail(base, c, bytes) : v;
+}
+
 // One Bloom probe of a key (af_k1_hash): both words are read from LDS, no branches.
 __device__ __forceinline__ uint32_t onehot_bytes(uint32_t v) {  // af_k1_mask
     return __builtin_amdgcn_perm(0x80402010u, 0x08040201u, v & 0x07070707u);
 }
-__device__ __forceinline__ bool probe(uint32_t key, const unsigned char *bloom, int bshift, uint32_t wmask4) {
+// The Bloom table starts at LDS address 0 (the kernels have no static LDS; the launcher checks),
+// so a probe addresses it with plain byte offsets and no base add.
+__device__ __forceinline__ uint32_t lds_word(uint32_t byte_off) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((size_t)byte_off);
+}
+__device__ __forceinline__ bool probe(uint32_t key, int bshift, uint32_t wmask4) {
     const uint64_t h = af_k1_hash(key);
     const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
-    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(bloom + (hi & wmask4));
-    const uint32_t w2 = *reinterpret_cast<const uint32_t *>(bloom + ((lo >> bshift) << 2));
+    const uint32_t w1 = lds_word(hi & wmask4);
+    const uint32_t w2 = lds_word((lo >> bshift) << 2);
     const uint32_t m1 = onehot_bytes(lo), m2 = onehot_bytes(hi);
     return ((m1 & ~w1) | (m2 & ~w2)) == 0u;
+}
+// Four probes with the eight LDS reads issued back to back (one wait for the round).
+__device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uint32_t wmask4, bool (&p)[4]) {
+    uint32_t lo[4], hi[4], w1[4], w2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t h = af_k1_hash(key[i]);
+        lo[i] = (uint32_t)h;
+        hi[i] = (uint32_t)(h >> 32);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        w1[i] = lds_word(hi[i] & wmask4);
+        w2[i] = lds_word((lo[i] >> bshift) << 2);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p[i] = ((onehot_bytes(lo[i]) & ~w1[i]) | (onehot_bytes(hi[i]) & ~w2[i])) == 0u;
 }
 
 // One round of a wave: lane l holds chunk c (16 read bytes = 4 code words); lanes >= 63 or
@@ -92,21 +124,24 @@ __device__ __forceinline__ bool probe(uint32_t key, const unsigned char *bloom, 
 // The positives' read index: r = floor((off + 0.5) / stride) in f32 is exact here (off < 2^23
 // is a tile-relative byte offset, stride <= AF_MAX_READ, so the quotient sits >= 0.5 / stride
 // from an integer, far beyond f32 error); a chunk spans at most two reads, so at most two adds.
-__device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const unsigned char *bloom, int bshift,
+__device__ __forceinline__ void scan_round(const uint4 v, int c, int c_end, int bshift,
                                            uint32_t wmask4, int32_t stride, float inv_stride, uint32_t *cnt) {
     const uint32_t c0 = codes_w(v.x), c1 = codes_w(v.y), c2 = codes_w(v.z), c3 = codes_w(v.w);
     const uint32_t a0 = c0 | (c1 << 2), a1 = c1 | (c2 << 2), a2 = c2 | (c3 << 2);
     const uint32_t a3 = c3 | (next_lane(c0) << 2);
     const uint32_t a4 = next_lane(a0), a5 = next_lane(a1);
-    const bool p0 = probe(a0 | (a2 << 4), bloom, bshift, wmask4);
-    const bool p1 = probe(a1 | (a3 << 4), bloom, bshift, wmask4);
-    const bool p2 = probe(a2 | (a4 << 4), bloom, bshift, wmask4);
-    const bool p3 = probe(a3 | (a5 << 4), bloom, bshift, wmask4);
+    const uint32_t key[4] = {a0 | (a2 << 4), a1 | (a3 << 4), a2 | (a4 << 4), a3 | (a5 << 4)};
+    bool p[4];
+    probe4(key, bshift, wmask4, p);
+    const bool p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3];
+    // lanes that own no chunk (lane 63, chunks >= c_end) probed clamped data: drop them here,
+    // on the rare positive path, not with a compare per round
 #if AF_K1_ABL == 4  // timing only: positives are kept live but not counted
-    if (in && (p0 | p1 | p2 | p3) && c == -12345) {
+    if ((p0 | p1 | p2 | p3) && c == -12345) {
 #else
-    if (in && (p0 | p1 | p2 | p3)) {
+    if (p0 | p1 | p2 | p3) {
 #endif
+        if ((int)__lane_id() == 63 || c >= c_end) return;
         const uint32_t off = (uint32_t)c * 16u;
         const uint32_t r = (uint32_t)(((float)off + 0.5f) * inv_stride);
         const int o = (int)(off - r * (uint32_t)stride);
@@ -125,7 +160,6 @@ __device__ __forceinline__ void scan_round(const uint4 v, int c, bool in, const 
 
 // All tiles a block processes share this state (LDS pointers and wave coordinates).
 struct K1 {
-    const unsigned char *bloom;
     int bshift;
     uint32_t wmask4;
     float inv_stride;
@@ -159,7 +193,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
         const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
                                   : (c < nchunks ? load_tail(base, c, bytes)
                                                  : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu));
-        scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
+        scan_round(v, c, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
     }
     __syncthreads();
     if (HAS_LENS) {
@@ -174,7 +208,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
                 uint32_t key = 0;
                 for (int u = 0; u < AF_K; ++u)
                     key |= af_k1_code(reads[rb + o + u]) << (8 * (u & 3) + 2 * (u >> 2));
-                h += probe(key, k.bloom, k.bshift, k.wmask4);
+                h += probe(key, k.bshift, k.wmask4);
             }
             const uint32_t sh = 8 * (i & 3);
             const uint32_t old = (cnt[i >> 2] >> sh) & 0xFFu;
@@ -225,7 +259,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);
     uint64_t *gbal = reinterpret_cast<uint64_t *>(cnt + AF_K1_PASS * (AF_SEED_BTILE / 4));
     int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
-    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
+    const K1 k{32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;  // next epoch's count (see af_internal.h)
     fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
@@ -253,7 +287,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);  // [CAP / 4]
     uint64_t *gbal = reinterpret_cast<uint64_t *>(cnt + CAP / 4);
     int *gbase = reinterpret_cast<int *>(gbal + CAP / 64);
-    const K1 k{smem, 32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
+    const K1 k{32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int lane = k.lane, wv = k.wv;
     if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
@@ -274,11 +308,19 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
         const int total = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of every wave
         // round r of wave wv covers chunks AF_CH(r) + lane; chunks past the last full one are
         // loaded (clamped) and then re-read byte-wise by load_tail in the scan
+        // (32-bit byte offsets from the sub-range base: one add and one min per load)
         int lr = 0;
+        const uint32_t last_off = nfull > 0 ? 16u * (uint32_t)(nfull - 1) : 0u, lane_off = 16u * (uint32_t)lane;
         auto next_load = [&]() -> uint4 {
-            const int c = min(AF_CH(min(lr, total - 1)) + lane, nfull > 0 ? nfull - 1 : 0);
+            const uint32_t off = min(16u * (uint32_t)AF_CH(min(lr, total - 1)) + lane_off, last_off);
             ++lr;
-            return reinterpret_cast<const uint4 *>(base)[c];
+#if AF_K1_NT
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off));
+            return make_uint4(v.x, v.y, v.z, v.w);
+#else
+            return *reinterpret_cast<const uint4 *>(base + off);
+#endif
         };
 #define AF_PIN asm volatile("" ::: "memory")
         uint4 b[AF_K1_DEPTH];
@@ -299,11 +341,11 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
 #endif
         auto scan = [&](uint4 v) {
             const int c = AF_CH(sr) + lane;
-            if (c >= nfull && c < nchunks) v = load_tail(base, c, bytes);  // the batch's last chunk
+            if (AF_CH(sr) + 63 >= nfull) v = tail_fix(v, c, nfull, nchunks, base, bytes);  // wave-uniform test
 #if AF_K1_ABL == 1
             abl ^= v.x ^ v.y ^ v.z ^ v.w;
 #else
-            scan_round(v, c, l63 && c < nchunks, k.bloom, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
+            scan_round(v, c, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
 #endif
             ++sr;
         };
@@ -392,6 +434,7 @@ hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64
         for (const void *fn : fns) {
             hipFuncAttributes fa;
             hipError_t e = hipFuncGetAttributes(&fa, fn);
+            if (e == hipSuccess && fa.sharedSizeBytes != 0) e = hipErrorInvalidKernelFile;  // lds_word: table at 0
             if (e == hipSuccess)
                 e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)(160 * 1024 - fa.sharedSizeBytes));
