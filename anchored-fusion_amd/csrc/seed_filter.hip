@@ -77,8 +77,9 @@ __device__ __forceinline__ void fill_lds(uint2 *dst, const uint2 *__restrict__ s
 
 // the last round(s) of a range: the chunk that straddles the range end is re-read byte-wise
 // (out of line, so the common rounds carry no per-lane test)
-__device__ __noinline__ uint4 tail_fix(uint4 v, int c, int nfull, int nchunks, const uint8_t *__restrict__ base,
+__device__ __noinline__ uint4 tail_fix(uint4 v, int cb, int nfull, int nchunks, const uint8_t *__restrict__ base,
                                        int64_t bytes) {
+    const int c = cb + (int)__lane_id();
     return c >= nfull && c < nchunks ? load_tail(base, c, bytes) : v;
 }
 
@@ -99,8 +100,9 @@ __device__ __forceinline__ bool probe(uint32_t key, int bshift, uint32_t wmask4)
     const uint32_t m1 = onehot_bytes(lo), m2 = onehot_bytes(hi);
     return ((m1 & ~w1) | (m2 & ~w2)) == 0u;
 }
-// Four probes with the eight LDS reads issued back to back (one wait for the round).
-__device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uint32_t wmask4, bool (&p)[4]) {
+// Four probes with the eight LDS reads issued back to back (one wait for the round).  The
+// residual of a probe is zero iff all its bits are set (the key may be in the anchor).
+__device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uint32_t wmask4, uint32_t (&res)[4]) {
     uint32_t lo[4], hi[4], w1[4], w2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -110,11 +112,16 @@ __device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uin
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+#if AF_K1_ABL == 5  // timing only: no LDS reads (address-dependent stand-ins)
+        w1[i] = (hi[i] & wmask4) * 0x01010101u;
+        w2[i] = ((lo[i] >> bshift) << 2) * 0x01010101u;
+#else
         w1[i] = lds_word(hi[i] & wmask4);
         w2[i] = lds_word((lo[i] >> bshift) << 2);
+#endif
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) p[i] = ((onehot_bytes(lo[i]) & ~w1[i]) | (onehot_bytes(hi[i]) & ~w2[i])) == 0u;
+    for (int i = 0; i < 4; ++i) res[i] = (onehot_bytes(lo[i]) & ~w1[i]) | (onehot_bytes(hi[i]) & ~w2[i]);
 }
 
 // One round of a wave: lane l holds chunk c (16 read bytes = 4 code words); lanes >= 63 or
@@ -124,24 +131,27 @@ __device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uin
 // The positives' read index: r = floor((off + 0.5) / stride) in f32 is exact here (off < 2^23
 // is a tile-relative byte offset, stride <= AF_MAX_READ, so the quotient sits >= 0.5 / stride
 // from an integer, far beyond f32 error); a chunk spans at most two reads, so at most two adds.
-__device__ __forceinline__ void scan_round(const uint4 v, int c, int c_end, int bshift,
+__device__ __forceinline__ void scan_round(const uint4 v, int cb, int c_end, int bshift,
                                            uint32_t wmask4, int32_t stride, float inv_stride, uint32_t *cnt) {
     const uint32_t c0 = codes_w(v.x), c1 = codes_w(v.y), c2 = codes_w(v.z), c3 = codes_w(v.w);
     const uint32_t a0 = c0 | (c1 << 2), a1 = c1 | (c2 << 2), a2 = c2 | (c3 << 2);
     const uint32_t a3 = c3 | (next_lane(c0) << 2);
     const uint32_t a4 = next_lane(a0), a5 = next_lane(a1);
     const uint32_t key[4] = {a0 | (a2 << 4), a1 | (a3 << 4), a2 | (a4 << 4), a3 | (a5 << 4)};
-    bool p[4];
-    probe4(key, bshift, wmask4, p);
-    const bool p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3];
+    uint32_t res[4];
+    probe4(key, bshift, wmask4, res);
+    // one compare for the round: some probe passed iff the least residual is zero
+    const uint32_t rmin = min(min(min(res[0], res[1]), res[2]), res[3]);
     // lanes that own no chunk (lane 63, chunks >= c_end) probed clamped data: drop them here,
     // on the rare positive path, not with a compare per round
 #if AF_K1_ABL == 4  // timing only: positives are kept live but not counted
-    if ((p0 | p1 | p2 | p3) && c == -12345) {
+    if (rmin == 0u && cb == -12345) {
 #else
-    if (p0 | p1 | p2 | p3) {
+    if (rmin == 0u) {
 #endif
+        const int c = cb + (int)__lane_id();
         if ((int)__lane_id() == 63 || c >= c_end) return;
+        const bool p0 = res[0] == 0u, p1 = res[1] == 0u, p2 = res[2] == 0u, p3 = res[3] == 0u;
         const uint32_t off = (uint32_t)c * 16u;
         const uint32_t r = (uint32_t)(((float)off + 0.5f) * inv_stride);
         const int o = (int)(off - r * (uint32_t)stride);
@@ -193,7 +203,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
         const uint4 v = c < nfull ? *reinterpret_cast<const uint4 *>(base + 16 * (int64_t)c)
                                   : (c < nchunks ? load_tail(base, c, bytes)
                                                  : make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu));
-        scan_round(v, c, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
+        scan_round(v, c - lane, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
     }
     __syncthreads();
     if (HAS_LENS) {
@@ -309,17 +319,21 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
         // round r of wave wv covers chunks AF_CH(r) + lane; chunks past the last full one are
         // loaded (clamped) and then re-read byte-wise by load_tail in the scan
         // (32-bit byte offsets from the sub-range base: one add and one min per load)
+        // (scalar chunk base clamped to the last full chunk, then one v_min per load)
         int lr = 0;
-        const uint32_t last_off = nfull > 0 ? 16u * (uint32_t)(nfull - 1) : 0u, lane_off = 16u * (uint32_t)lane;
+        const int clast = nfull > 0 ? nfull - 1 : 0;
+        const uint32_t lane_off = 16u * (uint32_t)lane;
         auto next_load = [&]() -> uint4 {
-            const uint32_t off = min(16u * (uint32_t)AF_CH(min(lr, total - 1)) + lane_off, last_off);
+            const int cb = min(AF_CH(min(lr, total - 1)), clast);
+            const uint8_t *rbase = base + 16 * (int64_t)cb;
+            const uint32_t off = min(lane_off, 16u * (uint32_t)(clast - cb));
             ++lr;
 #if AF_K1_NT
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(base + off));
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rbase + off));
             return make_uint4(v.x, v.y, v.z, v.w);
 #else
-            return *reinterpret_cast<const uint4 *>(base + off);
+            return *reinterpret_cast<const uint4 *>(rbase + off);
 #endif
         };
 #define AF_PIN asm volatile("" ::: "memory")
@@ -340,12 +354,12 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
         uint32_t abl = 0;
 #endif
         auto scan = [&](uint4 v) {
-            const int c = AF_CH(sr) + lane;
-            if (AF_CH(sr) + 63 >= nfull) v = tail_fix(v, c, nfull, nchunks, base, bytes);  // wave-uniform test
+            const int cb = AF_CH(sr);
+            if (cb + 63 >= nfull) v = tail_fix(v, cb, nfull, nchunks, base, bytes);  // wave-uniform test
 #if AF_K1_ABL == 1
             abl ^= v.x ^ v.y ^ v.z ^ v.w;
 #else
-            scan_round(v, c, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
+            scan_round(v, cb, nchunks, k.bshift, k.wmask4, stride, k.inv_stride, cnt);
 #endif
             ++sr;
         };
