@@ -93,9 +93,16 @@ __device__ __forceinline__ int scd(const af_params &p, int x, int y) {
     return (x > 3 || y > 3) ? -1 : (x == y ? p.a : -p.b);
 }
 
+// (int)((double)x / y + c) as bwa computes it (y >= 1): the default gap-extension cost 1 takes one add
+// instead of a double-precision division
+__device__ __forceinline__ int div_plus(int x, int y, int c) {
+    if (y == 1) return x + c;
+    return (int)((double)x / y + (double)c);
+}
+
 __device__ __forceinline__ int cal_max_gap(const af_params &p, int qlen) {
-    int l_del = (int)((double)(qlen * p.a - p.o_del) / p.e_del + 1.);
-    int l_ins = (int)((double)(qlen * p.a - p.o_ins) / p.e_ins + 1.);
+    int l_del = div_plus(qlen * p.a - p.o_del, p.e_del, 1);
+    int l_ins = div_plus(qlen * p.a - p.o_ins, p.e_ins, 1);
     int l = l_del > l_ins ? l_del : l_ins;
     l = l > 1 ? l : 1;
     return l < p.w << 1 ? l : p.w << 1;
@@ -103,7 +110,7 @@ __device__ __forceinline__ int cal_max_gap(const af_params &p, int qlen) {
 
 __device__ __forceinline__ int infer_bw(int l1, int l2, int score, int a, int q, int r) {
     if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
-    int w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
+    int w = div_plus((l1 < l2 ? l1 : l2) * a - score - q, r, 2);
     int d = l1 - l2 < 0 ? l2 - l1 : l1 - l2;
     return w < d ? d : w;
 }
@@ -148,10 +155,10 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
     }
     {
         const int mx = p.a;
-        int max_ins = (int)((double)(qlen * mx + end_bonus - p.o_ins) / p.e_ins + 1.);
+        int max_ins = div_plus(qlen * mx + end_bonus - p.o_ins, p.e_ins, 1);
         max_ins = max_ins > 1 ? max_ins : 1;
         w = w < max_ins ? w : max_ins;
-        int max_del = (int)((double)(qlen * mx + end_bonus - p.o_del) / p.e_del + 1.);
+        int max_del = div_plus(qlen * mx + end_bonus - p.o_del, p.e_del, 1);
         max_del = max_del > 1 ? max_del : 1;
         w = w < max_del ? w : max_del;
     }
@@ -311,12 +318,15 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
     const int qc = j < qlen ? q[j] : 4;
     const bool qn = qc > 3;
     // lane constants: run = max(M - oe_ins, 0) + jE = max(M + jEo, jE); f = P - jE1
-    const int jE = j * p.e_ins, jEo = jE - oe_ins, jE1 = (j - 1) * p.e_ins, tailA = (qlen - j) * p.a;
+    // (lane 0's f must lose to every M/E >= 0: the scan's shift brings 0 into lane 0, and its
+    // jE1 is 2^30, so f = -2^30 there -- no -inf operand to rematerialise per row)
+    const int jE = j * p.e_ins, jEo = jE - oe_ins, jE1 = j == 0 ? (1 << 30) : (j - 1) * p.e_ins,
+              tailA = (qlen - j) * p.a;
     {
-        int max_ins = (int)((double)(qlen * p.a + end_bonus - p.o_ins) / p.e_ins + 1.);
+        int max_ins = div_plus(qlen * p.a + end_bonus - p.o_ins, p.e_ins, 1);
         max_ins = max_ins > 1 ? max_ins : 1;
         w = w < max_ins ? w : max_ins;
-        int max_del = (int)((double)(qlen * p.a + end_bonus - p.o_del) / p.e_del + 1.);
+        int max_del = div_plus(qlen * p.a + end_bonus - p.o_del, p.e_del, 1);
         max_del = max_del > 1 ? max_del : 1;
         w = w < max_del ? w : max_del;
     }
@@ -356,7 +366,7 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         const int sc = qc == tiu ? s_eq : (qn ? -1 : s_ne);
         int M = H != 0 ? H + sc : 0;
         M = in ? M : 0;
-        const int P = wave_shr1(kNeg, wave_incl_max(max(M + jEo, jE)));
+        const int P = __builtin_amdgcn_mov_dpp(wave_incl_max(max(M + jEo, jE)), 0x138, 0xf, 0xf, true);
         const int f = P - jE1;
         const int h = max(max(M, E), f);
         const int key = in ? ((h << 10) | j) : -1;
@@ -375,7 +385,8 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         // bwa: break on m == 0; else a new maximum, or the z-drop test against the old one
         const bool better = m > mx;
         const int di = i - max_i, dj = mj - max_j;
-        const int zgap = di > dj ? mx - m - (di - dj) * p.e_del : mx - m - (dj - di) * p.e_ins;
+        // (24-bit multiplies: full-rate VALU; |di - dj| < 2^12 and the gap costs are small)
+        const int zgap = di > dj ? mx - m - __mul24(di - dj, p.e_del) : mx - m - __mul24(dj - di, p.e_ins);
         const int zt = better ? INT_MIN : zgap;
         const int off = mj - i < 0 ? i - mj : mj - i;
         max_off = better ? max(max_off, off) : max_off;
@@ -659,8 +670,8 @@ __device__ __forceinline__ int gen_cigar_wave(const DevIndex &ix, const af_param
         if (lane == 0) { L.ring[0] = (uint32_t)lq << 4; L.misc[2] = 1; }
         wave_sync();
     } else {
-        int max_ins = (int)((double)(((lq + 1) >> 1) * p.a - p.o_ins) / p.e_ins + 1.);
-        int max_del = (int)((double)(((lq + 1) >> 1) * p.a - p.o_del) / p.e_del + 1.);
+        int max_ins = div_plus(((lq + 1) >> 1) * p.a - p.o_ins, p.e_ins, 1);
+        int max_del = div_plus(((lq + 1) >> 1) * p.a - p.o_del, p.e_del, 1);
         int max_gap = max_ins > max_del ? max_ins : max_del;
         max_gap = max_gap > 1 ? max_gap : 1;
         const int d = rlen - lq < 0 ? lq - rlen : rlen - lq;
