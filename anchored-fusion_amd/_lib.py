@@ -33,7 +33,8 @@ EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates", "af_place",
+    "af_last_candidates", "af_place", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
+    "af_fastq_close",
 )
 
 
@@ -104,6 +105,16 @@ def lib():
     L.af_last_candidates.restype = _i64
     L.af_place.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _i32, _vp, _vp]
     L.af_place.restype = ctypes.c_int
+    L.af_fastq_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_vp)]
+    L.af_fastq_open.restype = ctypes.c_int
+    L.af_fastq_next.argtypes = [_vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i32), ctypes.POINTER(_i64)]
+    L.af_fastq_next.restype = ctypes.c_int
+    L.af_fastq_export.argtypes = [_vp, _i32, _vp, _vp, _vp, _i64, _vp]
+    L.af_fastq_export.restype = ctypes.c_int
+    L.af_fastq_error.argtypes = [_vp]
+    L.af_fastq_error.restype = ctypes.c_char_p
+    L.af_fastq_close.argtypes = [_vp]
+    L.af_fastq_close.restype = None
     _L = L
     return L
 

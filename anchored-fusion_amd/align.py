@@ -103,6 +103,54 @@ class AnchorAligner:
                    "af_align_pairs")
         return AlignResult(**out)
 
+    def align_fastq(self, fq1, fq2, batch_pairs=1 << 20, threads=0):
+        """FASTQ(.gz) pair -> records, streamed: the native reader (io.iter_pairs) parses batch
+        k + 1 on host threads while batch k is aligned (both ctypes calls release the GIL).
+        Returns ``(names, reads, lens, AlignResult)`` over all pairs, as io.read_pairs + align_pairs
+        would (lens None when every read has the common length)."""
+        import threading
+
+        from . import io as afio
+        it = afio.iter_pairs(fq1, fq2, batch_pairs=batch_pairs, threads=threads)
+        box = {}
+
+        def fetch():
+            try:
+                box["next"] = next(it, None)
+            except BaseException as e:  # re-raised on the caller's thread
+                box["err"] = e
+
+        parts = []
+        th = threading.Thread(target=fetch)
+        th.start()
+        while True:
+            th.join()
+            if "err" in box:
+                raise box.pop("err")
+            cur = box.pop("next")
+            if cur is None:
+                break
+            th = threading.Thread(target=fetch)
+            th.start()
+            names, reads, lens = cur
+            uniform = bool((lens == reads.shape[1]).all())
+            parts.append((names, reads, lens, self.align_pairs(reads, None if uniform else lens)))
+        if not parts:
+            empty = np.zeros(0, np.int32)
+            return (afio.Names(b"", np.zeros(0, np.int64)), np.full((0, 1), ord("N"), np.uint8), None,
+                    AlignResult(empty, empty, empty, empty, np.zeros((0, _lib.AF_MAX_CIGAR), np.uint32), empty))
+        stride = max(r.shape[1] for _, r, _, _ in parts)
+        reads = np.full((sum(r.shape[0] for _, r, _, _ in parts), stride), ord("N"), np.uint8)
+        row = 0
+        for _, r, _, _ in parts:
+            reads[row:row + r.shape[0], :r.shape[1]] = r
+            row += r.shape[0]
+        lens = np.concatenate([x for _, _, x, _ in parts])
+        res = AlignResult(**{k: np.concatenate([getattr(a, k) for _, _, _, a in parts])
+                             for k in ("flag", "pos", "score", "n_cigar", "cigar", "hits")})
+        names = afio.Names.concat([nm for nm, _, _, _ in parts])
+        return names, reads, (None if (lens == stride).all() else lens), res
+
     # ---- device-resident entry points (torch tensors as HBM buffers) ----------------------
     def align_pairs_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None):
         """Enqueues S2 on ``stream`` (torch.cuda.Stream or raw handle); all tensors on-device.

@@ -51,7 +51,8 @@ def qname(raw):
 
 
 def read_fastq(path):
-    """Returns (names, seqs) with names as bwa QNAMEs and seqs as bytes."""
+    """Returns (names, seqs) with names as bwa QNAMEs and seqs as bytes (single-file reader for
+    small inputs; paired input goes through the native reader, ``read_pairs``)."""
     names, seqs = [], []
     with _open(path) as fh:
         while True:
@@ -85,20 +86,93 @@ def pack_reads(seqs, stride=None):
     return mat, lens
 
 
-def read_pairs(fq1, fq2):
-    """Reads a FASTQ pair into the pair-major layout.
+class Names:
+    """QNAMEs of a batch of pairs, kept as one NUL-terminated arena plus an offset per pair
+    (a 50 M-pair run holds no per-read Python objects); indexes like a list of str."""
+
+    def __init__(self, arena, off):
+        self.arena = arena  # bytes
+        self.off = off      # int64 [n]
+
+    def __len__(self):
+        return len(self.off)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        o = int(self.off[i])
+        return self.arena[o:self.arena.index(b"\0", o)].decode()
+
+    def __iter__(self):
+        return (self[k] for k in range(len(self)))
+
+    @staticmethod
+    def concat(parts):
+        if len(parts) == 1:
+            return parts[0]
+        arenas, offs, base = [], [], 0
+        for p in parts:
+            arenas.append(p.arena)
+            offs.append(p.off + base)
+            base += len(p.arena)
+        return Names(b"".join(arenas), np.concatenate(offs) if offs else np.zeros(0, np.int64))
+
+
+def iter_pairs(fq1, fq2, batch_pairs=1 << 20, threads=0):
+    """Streams a FASTQ(.gz) pair through the native reader (csrc/ingest.cpp, af_fastq_*):
+    yields ``(names, reads[2n, stride] uint8, lens[2n] int32)`` per batch of <= batch_pairs
+    pairs, with stride = the batch's longest read."""
+    import ctypes
+
+    from . import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.af_fastq_open(os.fsencode(fq1), os.fsencode(fq2), int(threads), ctypes.byref(h))
+    try:
+        if rc != 0:
+            raise _lib.AFError(f"af_fastq_open failed (rc={rc}): {L.af_fastq_error(h).decode(errors='replace')}")
+        while True:
+            n, ml, nb = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int64()
+            rc = L.af_fastq_next(h, int(batch_pairs), ctypes.byref(n), ctypes.byref(ml), ctypes.byref(nb))
+            if rc != 0:
+                raise ValueError(f"{fq1}, {fq2}: {L.af_fastq_error(h).decode(errors='replace')}")
+            if n.value == 0:
+                return
+            stride = max(int(ml.value), 1)
+            reads = np.empty((2 * n.value, stride), dtype=np.uint8)
+            lens = np.empty(2 * n.value, dtype=np.int32)
+            arena = np.empty(max(int(nb.value), 1), dtype=np.uint8)
+            off = np.empty(n.value, dtype=np.int64)
+            rc = L.af_fastq_export(h, stride, reads.ctypes.data, lens.ctypes.data, arena.ctypes.data,
+                                   arena.size, off.ctypes.data)
+            if rc != 0:
+                raise _lib.AFError(f"af_fastq_export failed (rc={rc}): {L.af_fastq_error(h).decode()}")
+            yield Names(arena.tobytes(), off), reads, lens
+    finally:
+        L.af_fastq_close(h)
+
+
+def read_pairs(fq1, fq2, threads=0):
+    """Reads a FASTQ(.gz) pair into the pair-major layout (native reader, ``iter_pairs``).
 
     Returns ``(names, reads[2N, stride] uint8, lens[2N] int32 or None)``; ``names[p]`` is the
-    QNAME of pair p (mates must agree, as bwa requires for paired input)."""
-    n1, s1 = read_fastq(fq1)
-    n2, s2 = read_fastq(fq2)
-    if len(s1) != len(s2):
-        raise ValueError(f"paired FASTQs differ in length: {len(s1)} vs {len(s2)}")
-    inter = [None] * (2 * len(s1))
-    inter[0::2] = s1
-    inter[1::2] = s2
-    mat, lens = pack_reads(inter)
-    return n1, mat, lens
+    QNAME of pair p (mates must agree, as bwa requires for paired input); ``lens`` is None when
+    every read has length ``stride``."""
+    parts = list(iter_pairs(fq1, fq2, threads=threads))
+    if not parts:
+        return Names(b"", np.zeros(0, np.int64)), np.full((0, 1), ord("N"), np.uint8), None
+    stride = max(r.shape[1] for _, r, _ in parts)
+    if all(r.shape[1] == stride for _, r, _ in parts):
+        reads = np.concatenate([r for _, r, _ in parts]) if len(parts) > 1 else parts[0][1]
+    else:
+        reads = np.full((sum(r.shape[0] for _, r, _ in parts), stride), ord("N"), np.uint8)
+        row = 0
+        for _, r, _ in parts:
+            reads[row:row + r.shape[0], :r.shape[1]] = r
+            row += r.shape[0]
+    lens = np.concatenate([x for _, _, x in parts]) if len(parts) > 1 else parts[0][2]
+    names = Names.concat([nm for nm, _, _ in parts])
+    return names, reads, (None if (lens == stride).all() else lens)
 
 
 def anchor_sequence(path, index=0):

@@ -123,6 +123,24 @@ int64_t af_last_candidates(af_ctx *ctx);
 int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,
              const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits);
 
+/* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
+ * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as
+ * bwa's reader takes them (name = header up to the first blank, "/<digit>" trimmed; multi-line
+ * records; FASTA records allowed), the two files paired record by record with equal names.
+ * Usage: af_fastq_open; then repeatedly af_fastq_next (parses the next <= max_pairs pairs:
+ * *n_pairs = 0 at the end of input; the longest read and the NUL-terminated name bytes of the
+ * batch are reported) and af_fastq_export (rows of `stride` >= the longest read, 'N'-padded;
+ * lens[2 * n]; names arena + name_off[n]; any output pointer may be NULL); af_fastq_close.
+ * Errors return AF_E_* with the message in af_fastq_error (also after a failed open, whose
+ * handle must still be closed). */
+typedef struct af_fastq af_fastq;
+int af_fastq_open(const char *fq1, const char *fq2, int threads, af_fastq **out);
+int af_fastq_next(af_fastq *f, int64_t max_pairs, int64_t *n_pairs, int32_t *max_len, int64_t *names_bytes);
+int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, char *names, int64_t names_cap,
+                    int64_t *name_off);
+const char *af_fastq_error(const af_fastq *f);
+void af_fastq_close(af_fastq *f);
+
 #ifdef __cplusplus
 }
 #endif

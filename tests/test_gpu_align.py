@@ -44,6 +44,17 @@ def test_bundled_parity(aligner, oidx, bundled_pairs):
     assert ((g["flag"] & 4) == 0).sum() == 1261
 
 
+def test_align_fastq_streamed_matches_oracle(aligner, oidx, bundled_pairs):
+    # native FASTQ.gz ingest overlapped with alignment, in 3,000-pair batches (the last ragged)
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    names, reads, lens, res = aligner.align_fastq(os.path.join(gold, "test_sample_1.fastq.gz"),
+                                                  os.path.join(gold, "test_sample_2.fastq.gz"), batch_pairs=3000)
+    n0, r0, l0 = bundled_pairs
+    assert lens is None and l0 is None and (reads == r0).all() and list(names) == list(n0)
+    assert_records_equal(res.as_dict(), oidx.align_pairs(reads, None, threads=8), reads)
+
+
 def test_edge_parity(aligner, oidx, anchor):
     reads, lens = edge_pairs(anchor)
     g, r = _both(aligner, oidx, reads, lens)
