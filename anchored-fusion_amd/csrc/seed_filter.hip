@@ -30,7 +30,10 @@
 #define AF_K1_ABL 0    // 1 = stream-only timing build (scripts/k1_ablate.sh); 0 = the product kernel
 #endif
 #ifndef AF_K1_DEPTH
-#define AF_K1_DEPTH 4  // chunk loads in flight per wave in k_seed_stream
+#define AF_K1_DEPTH 2  // chunk loads in flight per wave in k_seed_stream (2: 40.6 us, 3: 40.9, 4: 41.5, 6: 43.3, 8: 43.6)
+#endif
+#ifndef AF_K1_TWO_STAGE
+#define AF_K1_TWO_STAGE 0  // 1 = word 2 of a probe read only where word 1 passed
 #endif
 #ifndef AF_K1_NT
 #define AF_K1_NT 0     // 1 = nontemporal (nt) stream loads of the reads
@@ -110,6 +113,20 @@ __device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uin
         lo[i] = (uint32_t)h;
         hi[i] = (uint32_t)(h >> 32);
     }
+#if AF_K1_TWO_STAGE
+    // Word 1 of every probe first; word 2 only where word 1 passed (P ~ 1e-4 per probe for a
+    // key that is not in the anchor), under an exec mask: the LDS array -- the busiest unit of
+    // this kernel -- serves half the random reads.  The outcome is the same conjunction.
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w1[i] = lds_word(hi[i] & wmask4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) res[i] = onehot_bytes(lo[i]) & ~w1[i];
+    if (min(min(res[0], res[1]), min(res[2], res[3])) == 0u) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (res[i] == 0u) res[i] = onehot_bytes(hi[i]) & ~lds_word((lo[i] >> bshift) << 2);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #if AF_K1_ABL == 5  // timing only: no LDS reads (address-dependent stand-ins)
@@ -122,6 +139,7 @@ __device__ __forceinline__ void probe4(const uint32_t (&key)[4], int bshift, uin
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) res[i] = (onehot_bytes(lo[i]) & ~w1[i]) | (onehot_bytes(hi[i]) & ~w2[i]);
+#endif
 }
 
 // One round of a wave: lane l holds chunk c (16 read bytes = 4 code words); lanes >= 63 or
