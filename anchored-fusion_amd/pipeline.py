@@ -94,33 +94,47 @@ class Searches:
         return out
 
 
-def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory, out_prefix, log=print):
-    """One anchored gene (the body of AF:121-227).  Returns the candidate list."""
-    anchor_rec = [(gene, anchor)]
+def align_anchor(anchor, reads, lens, aligner_factory):
+    """S1 + S2 for one anchor (AF:167-182): index it and align every pair."""
     aligner = aligner_factory(anchor.encode())
     try:
-        res = aligner.align_pairs(reads, lens)
+        return aligner.align_pairs(reads, lens)
     finally:
         close = getattr(aligner, "close", None)
         if close:
             close()
+
+
+def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory, out_prefix, log=print):
+    """One anchored gene (the body of AF:121-227).  Returns the candidate list."""
+    res = align_anchor(anchor, reads, lens, aligner_factory)
+    return consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=log)
+
+
+def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=print):
+    """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads``."""
+    anchor_rec = [(gene, anchor)]
     flag, pos = res.flag, res.pos
-    seqs = [bytes(reads[r, : (lens[r] if lens is not None else reads.shape[1])]).decode() for r in range(len(reads))]
+    width = reads.shape[1]
+
+    def seq(r):  # only the reads the partitions select are decoded
+        return bytes(reads[r, : (lens[r] if lens is not None else width)]).decode()
+
     tmp1, tmp2, anchored = partition(res)
     log(f"[{gene}] S2: {int(((flag & 4) == 0).sum())} of {len(flag)} reads on the anchor; "
         f"{len(tmp1)} one-end-anchored pairs; {len(anchored)} anchored records")
     # S4: one-end-anchored pairs on the genome (samtools fastq restores the sequenced orientation)
     q4 = []
     for a, b in zip(tmp1, tmp2):
-        q4 += [(names[a // 2], seqs[a]), (names[b // 2], seqs[b])]
+        q4 += [(names[a // 2], seq(a)), (names[b // 2], seq(b))]
     s4 = [ln for recs in (searches.genome_sam(q4) if q4 else []) for ln in recs]
     homo = [row[3] for row in homo_rows]
     # anchored.bam as `samtools view` prints it (SEQ reverse-complemented for 0x10)
     anch_lines = []
     for r in anchored:
         cig = res.cigar_str(r)
-        seq = revcomp(seqs[r]) if flag[r] & 0x10 else seqs[r]
-        anch_lines.append(sam_line(names[r // 2], int(flag[r]) & 0xFFFF, gene, int(pos[r]) + 1, cig, seq))
+        sq = revcomp(seq(r)) if flag[r] & 0x10 else seq(r)
+        anch_lines.append(sam_line(names[r // 2], int(flag[r]) & 0xFFFF, gene, int(pos[r]) + 1, cig, sq))
     # S5: split reads vs the genome
     fasta = genome_check.split_read_fasta(anch_lines)
     gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam(fasta) if fasta else []) for ln in recs]

@@ -1,0 +1,170 @@
+"""Single-cell fusion detection (Anchored_Fusion_singlecell.py, SURVEY.md §8 f rank 3).
+
+The reference runs the whole bulk pipeline once per cell and per anchored gene, each cell
+through its own `bwa mem` (SC:205-256), then merges the per-cell prediction tables
+(SC:258-287).  Here the cells are batched: every cell's FASTQ pair is ingested once
+(native reader), and per gene the pairs of whole cells are concatenated into batches of up to
+``batch_pairs`` pairs, each aligned by ONE pass of the GPU path (S1 + S2).  The records are then
+split back per cell and each cell runs S3-S8 + Final_fusion on its own records, exactly as a
+separate run on that cell would (the S3 sort and every consumer see only the cell's reads).
+
+| reference step | here |
+|---|---|
+| SC:86-113 cell FASTQ discovery | `discover_cells` |
+| SC:172-203 anchor FASTA, index, `Find_homo_genes` once per gene | `partner.homolog_genes` once per gene |
+| SC:205-217 per-cell `bwa mem` vs the anchor | one `align_pairs` per batch of cells |
+| SC:218-256 per-cell S3-S8, `Final_fusion` | `pipeline.consume_gene` per cell |
+| SC:258-287 merge by the first five columns, count cells | `merge_cell_tables` |
+
+Deviation, on purpose: the reference's merge reads the span/split counts from columns 6 and
+7 of each cell's `_predictions.txt`, the filter-model layout (column 5 = Natural_score).  With
+`--not_filter_false_positive` (the only mode built here: the filter model is outside §8) the
+counts are columns 5 and 6, and column 7 holds read names, on which the reference's `int()`
+raises.  The merge reads the counts from the columns the table actually has.
+"""
+import os
+import re
+
+import numpy as np
+
+from . import partner
+from .align import AlignResult
+from .annotation import ExonIndex
+from .io import read_fasta, read_pairs
+from .pipeline import Searches, consume_gene, gene_names_from_fasta, gene_names_from_file
+
+
+def discover_cells(fastq_dir):
+    """(cell, fq1, fq2) triples as SC:86-113 pairs them: directory entries in sorted order; an
+    entry matching ``<cell>_1.fastq`` (then ``.fastq.gz``, ``.fq.gz``, ``.fq``) pairs with the
+    NEXT entry if that is the same cell's ``_2`` file.  The patterns are the reference's
+    regular expressions (unescaped dots included)."""
+    entries = sorted(os.listdir(fastq_dir + "/"))
+    cells = []
+    for i, e in enumerate(entries):
+        for sfx in ("fastq", "fastq.gz", "fq.gz", "fq"):
+            m = re.findall(r"(\S+)_1." + sfx + "$", e)
+            if m:
+                name = m[0]
+                if i + 1 >= len(entries):  # the reference indexes past the end here (IndexError)
+                    raise ValueError(f"{fastq_dir}: {e} has no {name}_2.{sfx} after it")
+                if re.match(r"" + name + "_2." + sfx + "$", entries[i + 1]):
+                    cells.append((name, f"{name}_1.{sfx}", f"{name}_2.{sfx}"))
+                break
+    return cells
+
+
+def slice_result(res, r0, r1):
+    """Rows [r0, r1) of an AlignResult."""
+    return AlignResult(res.flag[r0:r1], res.pos[r0:r1], res.score[r0:r1], res.n_cigar[r0:r1], res.cigar[r0:r1],
+                       res.hits[r0:r1])
+
+
+def _concat(cells):
+    """Pair-major reads of several cells in one matrix (common stride; lens when ragged)."""
+    stride = max(r.shape[1] for _, r, _ in cells)
+    rows = sum(r.shape[0] for _, r, _ in cells)
+    reads = np.full((rows, max(stride, 1)), ord("N"), np.uint8)
+    lens = np.empty(rows, np.int32)
+    o = 0
+    for _, r, ln in cells:
+        reads[o:o + r.shape[0], :r.shape[1]] = r
+        lens[o:o + r.shape[0]] = r.shape[1] if ln is None else ln
+        o += r.shape[0]
+    return reads, (None if (lens == stride).all() else lens)
+
+
+def merge_cell_tables(cells, work_folder, out_name, out_prefix):
+    """SC:258-287: the per-cell `_predictions.txt` tables merged into
+    `<out_prefix>_gene_cell_predictions{,_abridged}.txt` (rows keyed by the first five columns,
+    in first-seen order; counts summed; cells listed).  Counts from the no-filter layout."""
+    head = ["Fusion_gene", "Anchored_gene_X", "X_clip_location", "Partner_gene_Y", "Y_clip_location"]
+    merged = {}
+    with open(out_prefix + "_gene_cell_predictions.txt", "w") as fo:
+        fo.write("\t".join(["Cell_name"] + head + ["Spanning_read_count", "Breakpoint_read_count"]) + "\n")
+        for cell, _, _ in cells:
+            path = os.path.join(work_folder, cell, out_name + "_predictions.txt")
+            with open(path) as fh:
+                lines = fh.readlines()
+            if len(lines) <= 1:
+                continue
+            for line in lines[1:]:
+                arr = line.split("\t")
+                key = "$".join(arr[:5])
+                span, split = int(arr[5]), int(arr[6])
+                if key not in merged:
+                    merged[key] = [span, split, 1, [cell]]
+                else:
+                    v = merged[key]
+                    v[0] += span
+                    v[1] += split
+                    v[2] += 1
+                    v[3].append(cell)
+                fo.write(cell + "\t" + "\t".join(arr[0:5] + arr[5:7]) + "\n")
+    with open(out_prefix + "_gene_cell_predictions_abridged.txt", "w") as fa:
+        fa.write("\t".join(head + ["All_Spanning_read_count", "All_Breakpoint_read_count", "Single_cells_count",
+                                   "Single_cells_name"]) + "\n")
+        for key, v in merged.items():
+            fa.write("\t".join(key.split("$")) + f"\t{v[0]}\t{v[1]}\t{v[2]}\t" + ";".join(v[3]) + "\n")
+    return merged
+
+
+def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
+        aligner_factory=None, batch_pairs=1 << 22, log=print):
+    """All genes x all cells; writes `<out>/<G>/<G>_fusion_gene_cell_predictions*.txt` and the
+    per-cell tables under `<out>/<G>/work_dir/<cell>/`.  Returns {gene: merged rows}."""
+    genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
+        else gene_names_from_fasta(anchored_cds)
+    anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
+    genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
+    with open(ref_ann) as fh:
+        gtf = fh.readlines()
+    index = ExonIndex.from_lines(gtf)
+    cells = discover_cells(fastq_dir)
+    data = [read_pairs(os.path.join(fastq_dir, f1), os.path.join(fastq_dir, f2)) for _, f1, f2 in cells]
+    if searches is None:
+        searches = Searches(genome, device=device)
+    if aligner_factory is None:
+        from .align import AnchorAligner
+
+        def aligner_factory(anchor):
+            return AnchorAligner(anchor, device=device)
+    # whole cells per GPU batch
+    groups, cur, n = [], [], 0
+    for k, (_, reads, _) in enumerate(data):
+        if cur and n + reads.shape[0] // 2 > batch_pairs:
+            groups.append(cur)
+            cur, n = [], 0
+        cur.append(k)
+        n += reads.shape[0] // 2
+    if cur:
+        groups.append(cur)
+    results = {}
+    for gene, anchor in zip(genes, anchors):
+        out_name = gene + "_fusion"
+        temp_folder = os.path.join(out_folder, gene)
+        work = os.path.join(temp_folder, "work_dir")
+        os.makedirs(work, exist_ok=True)
+        homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+        aligner = aligner_factory(anchor.encode())
+        try:
+            for grp in groups:
+                reads, lens = _concat([data[k] for k in grp])
+                res = aligner.align_pairs(reads, lens)
+                log(f"[{gene}] S2 batch of {len(grp)} cells, {reads.shape[0] // 2} pairs: "
+                    f"{int(((res.flag & 4) == 0).sum())} reads on the anchor")
+                row = 0
+                for k in grp:
+                    cell = cells[k][0]
+                    names, creads, clens = data[k]
+                    nr = creads.shape[0]
+                    os.makedirs(os.path.join(work, cell), exist_ok=True)
+                    consume_gene(gene, anchor, names, creads, clens, slice_result(res, row, row + nr), index,
+                                 homo_rows, searches, os.path.join(work, cell, out_name), log=log)
+                    row += nr
+        finally:
+            close = getattr(aligner, "close", None)
+            if close:
+                close()
+        results[gene] = merge_cell_tables(cells, work, out_name, os.path.join(temp_folder, out_name))
+    return results
