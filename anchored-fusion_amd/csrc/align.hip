@@ -1083,10 +1083,10 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
         if (hits[r] > 0) R[m] = recs[r];
         else { R[m].flag = 0x4; R[m].pos = 0; R[m].score = 0; R[m].n_cigar = 0; }
     }
+    int o_flag[2], o_pos[2], o_score[2], o_nc[2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) {
         const ReadRec &x = R[m], &y = R[m ^ 1];
-        const int64_t r = 2 * pp + m;
         const int xf = x.flag, yf = y.flag;
         int f = 0x1 | (m ? 0x80 : 0x40) | (xf & ~0x4 & 0x30000);
         int pos = x.pos;
@@ -1096,11 +1096,18 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
         else f |= (yf & 0x10) ? 0x20 : 0;
         if ((xf & 0x4) && !(yf & 0x4)) { pos = y.pos; f |= (yf & 0x10); }
         if ((xf & 0x4) && (yf & 0x4)) pos = -1;
-        out.flag[r] = f;
-        out.pos[r] = pos;
-        out.score[r] = x.score;
-        out.n_cigar[r] = (xf & 0x4) ? 0 : x.n_cigar;
+        o_flag[m] = f;
+        o_pos[m] = pos;
+        o_score[m] = x.score;
+        o_nc[m] = (xf & 0x4) ? 0 : x.n_cigar;
     }
+    // both mates in one 8-byte nontemporal store per field: the 16 B/pair of records go out to
+    // HBM during this kernel instead of staying dirty in L2/MALL for the next launch to flush
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(i32x2{o_flag[0], o_flag[1]}, reinterpret_cast<i32x2 *>(out.flag) + pp);
+    __builtin_nontemporal_store(i32x2{o_pos[0], o_pos[1]}, reinterpret_cast<i32x2 *>(out.pos) + pp);
+    __builtin_nontemporal_store(i32x2{o_score[0], o_score[1]}, reinterpret_cast<i32x2 *>(out.score) + pp);
+    __builtin_nontemporal_store(i32x2{o_nc[0], o_nc[1]}, reinterpret_cast<i32x2 *>(out.n_cigar) + pp);
 }
 
 }  // namespace

@@ -338,6 +338,8 @@ int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_r
     if (n_pairs <= 0) return n_pairs == 0 ? AF_OK : fail(c, AF_E_INVALID, "n_pairs < 0");
     if (!o->flag || !o->pos || !o->score || !o->n_cigar || !o->hits || !o->cigar)
         return fail(c, AF_E_INVALID, "output arrays must all be non-NULL");
+    if ((((uintptr_t)o->flag | (uintptr_t)o->pos | (uintptr_t)o->score | (uintptr_t)o->n_cigar) & 7) != 0)
+        return fail(c, AF_E_INVALID, "flag/pos/score/n_cigar arrays must be 8-byte aligned");
     if (2 * n_pairs > c->cap_reads) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
     const int64_t nr = 2 * n_pairs;
     if ((rc = ensure_zscratch(c))) return rc;
