@@ -33,7 +33,7 @@ EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates", "af_place", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
+    "af_last_candidates", "af_place", "af_index_build_genome", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close",
 )
 
@@ -83,6 +83,8 @@ def lib():
     L.af_params_default.restype = None
     L.af_index_build.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
     L.af_index_build.restype = ctypes.c_int
+    L.af_index_build_genome.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
+    L.af_index_build_genome.restype = ctypes.c_int
     L.af_index_free.argtypes = [_vp]
     L.af_index_free.restype = None
     L.af_index_anchor_len.argtypes = [_vp]

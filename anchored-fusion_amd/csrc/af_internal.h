@@ -27,12 +27,25 @@ struct DevIndex {
     const int32_t *hcnt;    //   occurrences (0 = empty slot)
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
     const uint32_t *bloom;  // Bloom filter of the anchor 16-mers (2^bl_bits words, see af_k1_hash)
+    // direct (genome-scale) indexes instead of the hash: kend[k] = end of 16-mer k's run of
+    // forward-strand positions in kposu (4^16 entries; the run starts at kend[k - 1]).  Null
+    // for hash indexes.
+    const uint32_t *kend;
+    const uint32_t *kposu;
     int64_t n;              // anchor length
     int32_t hbits;          // log2 position-hash slots
     int32_t bl_bits;        // log2 Bloom words
 };
 
 __host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
+// reverse complement of a 2-bit packed 16-mer (base i at bits 2i; A0 C1 G2 T3, complement = 3 - c)
+__host__ __device__ static inline uint32_t af_rc16(uint32_t k) {
+    uint32_t x = ~k;
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);  // swap 2-bit fields in nibbles
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);  // nibbles in bytes
+    x = ((x >> 8) & 0x00FF00FFu) | ((x & 0x00FF00FFu) << 8);  // bytes in halves
+    return (x >> 16) | (x << 16);
+}
 
 // ---- K1 seed-filter keys and Bloom filter --------------------------------
 // Base code of a read byte: a 2-bit table indexed by the byte's low 3 bits (A/a 1 -> 0,
@@ -103,6 +116,10 @@ hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *
 hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
                            const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
                            int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
+size_t af_genome_index_table_bytes();
+int af_genome_scan_blocks();
+hipError_t af_build_genome_index(const uint8_t *seq, int64_t n, uint8_t *D, uint32_t *D2, uint32_t *Dn,
+                                 uint32_t *S, uint32_t *kposu, uint32_t *scan_sums, int n_cu, hipStream_t s);
 size_t af_align_lane_lds(int32_t stride);
 bool af_lane_params_ok(const af_params &p, int32_t stride);
 hipError_t af_launch_align_lane(const DevIndex &ix, const uint8_t *reads, int32_t stride, const int32_t *lens,

@@ -38,7 +38,8 @@ constexpr int ZLDS = AF_K2_ZLDS;  // traceback bytes per wave kept in LDS (large
 struct __attribute__((aligned(16))) AlnLds {
     uint64_t mem[MEMCAP];
     uint64_t smem[MEMCAP];
-    int32_t regs[16][8];   // score, truesc, qb, qe, rb, re, seedlen0, w
+    int32_t regs[16][8];   // score, truesc, qb, qe, -, -, seedlen0, w
+    int64_t rpos[16][2];   // rb, re of the regions (genome-scale references exceed 2^31)
     uint32_t ring[64];     // traceback CIGAR ring
     int32_t misc[8];       // [0] nmem (total found), [2] n traceback ops
     uint32_t pk[AF_MAX_READ / 16 + 2];  // the read as 2-bit codes, 16 bases per word (base i at bits 2i)
@@ -778,17 +779,31 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
             const int wq = qb >> 4, sq = qb & 15;
             const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
             if (((L.nm[wq] | (L.nm[wq + 1] << 16)) >> sq) & 0xFFFFu) continue;
-            uint32_t s = af_fmix(k) & hm;
-            int cnt = 0, st = 0;
-            for (;;) {
-                const int cc = ix.hcnt[s];
-                if (cc == 0) break;
-                if (ix.hkey[s] == k) { cnt = cc; st = ix.hstart[s]; break; }
-                s = (s + 1) & hm;
+            // occurrences in the doubled reference: a hash index holds both strands' 16-mers; a
+            // direct (genome-scale) index holds the forward strand only, so k's occurrences are
+            // its forward run plus the reverse-strand images n2 - 16 - q of rc(k)'s forward run
+            int cnt = 0, st = 0, n_fwd = 0;
+            uint32_t b_fwd = 0, b_rc = 0;
+            if (ix.kend) {
+                const uint32_t rk = af_rc16(k);
+                b_fwd = k ? ix.kend[k - 1] : 0u;
+                b_rc = rk ? ix.kend[rk - 1] : 0u;
+                n_fwd = (int)(ix.kend[k] - b_fwd);
+                cnt = n_fwd + (int)(ix.kend[rk] - b_rc);
+            } else {
+                uint32_t s = af_fmix(k) & hm;
+                for (;;) {
+                    const int cc = ix.hcnt[s];
+                    if (cc == 0) break;
+                    if (ix.hkey[s] == k) { cnt = cc; st = ix.hstart[s]; break; }
+                    s = (s + 1) & hm;
+                }
             }
             if (cnt == 0 || cnt > p.max_occ) continue;
             for (int o = 0; o < cnt; ++o) {
-                const int64_t rb = ix.kpos[st + o];
+                const int64_t rb = !ix.kend ? (int64_t)ix.kpos[st + o]
+                                            : (o < n_fwd ? (int64_t)ix.kposu[b_fwd + o]
+                                                         : n2 - AF_K - (int64_t)ix.kposu[b_rc + (o - n_fwd)]);
                 if (qb > 0 && rb != 0 && rb != n) {
                     const int qc = L.q[qb - 1];
                     if (qc < 4 && qc == ix.D[rb - 1]) continue;
@@ -846,7 +861,8 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                 bool skip = false;
                 for (int rr = 0; rr < n_reg; ++rr) {
                     const int *a = L.regs[rr];
-                    const int aqb = a[2], aqe = a[3], arb = a[4], are = a[5], asl = a[6], aw = a[7];
+                    const int aqb = a[2], aqe = a[3], asl = a[6], aw = a[7];
+                    const int64_t arb = L.rpos[rr][0], are = L.rpos[rr][1];
                     if (srb < arb || srb + slen > are || sqb < aqb || sqb + slen > aqe) continue;
                     if (10 * (slen - asl) > l) continue;
                     int qd = sqb - aqb, rd = (int)(srb - arb);
@@ -926,7 +942,8 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                 if (lane == 0) {
                     int *a = L.regs[n_reg];
                     a[0] = a_score; a[1] = a_truesc; a[2] = a_qb; a[3] = a_qe;
-                    a[4] = (int)a_rb; a[5] = (int)a_re; a[6] = slen; a[7] = aw0 > aw1 ? aw0 : aw1;
+                    a[4] = 0; a[5] = 0; a[6] = slen; a[7] = aw0 > aw1 ? aw0 : aw1;
+                    L.rpos[n_reg][0] = a_rb; L.rpos[n_reg][1] = a_re;
                 }
                 wave_sync();
                 ++n_reg;
@@ -936,10 +953,11 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
             // Lane 0 writes the assembled ops to `co` and the record fields; with `want_mt`
             // every lane also gets the identical-base count and reference span of the
             // alignment (the oracle's emit_region, over its first AF_MAX_CIGAR ops).
-            auto emit = [&](const int *a, uint32_t *co, int &o_flag, int &o_pos, int &o_score, int &o_nc,
+            auto emit = [&](int ri, uint32_t *co, int &o_flag, int64_t &o_pos, int &o_score, int &o_nc,
                             bool want_mt, int &o_mt, int &o_span) {
+                const int *a = L.regs[ri];
                 const int a_score = a[0], a_truesc = a[1], aqb = a[2], aqe = a[3], awb = a[7];
-                const int64_t arb = a[4], are = a[5];
+                const int64_t arb = L.rpos[ri][0], are = L.rpos[ri][1];
                 const bool is_rev = arb >= n;
                 const int lq = aqe - aqb;
                 const int tmpw = infer_bw(lq, (int)(are - arb), a_truesc, p.a, p.o_del, p.e_del);
@@ -1004,7 +1022,7 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                     }
                     if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
                     o_flag = (is_rev ? 0x10 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
-                    o_pos = (int)pos;
+                    o_pos = pos;
                     o_score = a_score;
                     o_nc = nf;
                 }
@@ -1016,8 +1034,10 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                     if (best < 0 || L.regs[rr][0] > L.regs[best][0]) best = rr;
                 if (best >= 0 && L.regs[best][0] >= p.T) {
                     int mt_unused = 0, span_unused = 0;
-                    emit(L.regs[best], cigar + r * AF_MAX_CIGAR, flag, out_pos, out_score, out_nc, false, mt_unused,
+                    int64_t pos64 = 0;
+                    emit(best, cigar + r * AF_MAX_CIGAR, flag, pos64, out_score, out_nc, false, mt_unused,
                          span_unused);
+                    out_pos = (int)pos64;  // hash (anchor) indexes only: < 2^31 (af_align_* check)
                 }
             } else {
                 // every region scoring >= T, best first (ties: region order), at most max_hits
@@ -1037,12 +1057,13 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                     const int *a = L.regs[order[k]];
                     if (a[0] < p.T) break;
                     af_hit *h = hits + r * max_hits + nh;
-                    int hf = 0, hp = 0, hs = 0, hn = 0, mt = 0, span = 0;
-                    emit(a, h->cigar, hf, hp, hs, hn, true, mt, span);
+                    int hf = 0, hs = 0, hn = 0, mt = 0, span = 0;
+                    int64_t hp = 0;
+                    emit(order[k], h->cigar, hf, hp, hs, hn, true, mt, span);
                     if (lane == 0) {
                         h->query = (int32_t)r; h->flag = hf; h->score = hs;
                         h->q_start = a[2]; h->q_end = a[3]; h->q_size = l; h->matches = mt;
-                        h->n_cigar = hn; h->t_start = hp; h->t_end = (int64_t)hp + span;
+                        h->n_cigar = hn; h->t_start = hp; h->t_end = hp + span;
                         for (int c = hn; c < AF_MAX_CIGAR; ++c) h->cigar[c] = 0;
                     }
                     ++nh;

@@ -272,6 +272,62 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     return AF_OK;
 }
 
+int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out) {
+    if (!c || !seq || !out) return fail(c, AF_E_INVALID, "null argument");
+    *out = nullptr;
+    if (len < AF_K) return fail(c, AF_E_INVALID, "reference shorter than %d", AF_K);
+    if (len >= (1LL << 32) - 1) return fail(c, AF_E_UNSUPPORTED, "reference of 2^32 bases or more");
+    (void)hipSetDevice(c->device);
+    af_index *ix = new (std::nothrow) af_index;
+    if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
+    ix->ctx = c;
+    const int64_t n = len, n2 = 2 * len;
+    const size_t d2w = (size_t)((n2 + 15) / 16 + 2), dnw = (size_t)((n2 + 31) / 32 + 2);
+    const size_t nq = (size_t)(n - AF_K + 1);
+    void *p_seq = nullptr, *p_D = nullptr, *p_D2 = nullptr, *p_Dn = nullptr, *p_S = nullptr, *p_pos = nullptr,
+         *p_sums = nullptr;
+    auto bail = [&](hipError_t e, const char *what) {
+        af_free(p_seq); af_free(p_sums);
+        af_index_free(ix);
+        return fail(c, AF_E_HIP, "af_index_build_genome: %s: %s", what, hipGetErrorString(e));
+    };
+    auto alloc = [&](void **pp, size_t bytes, bool keep) {
+        hipError_t e = hipMalloc(pp, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess && keep) ix->allocs[ix->n_allocs++] = *pp;
+        return e;
+    };
+    hipError_t e;
+    if ((e = alloc(&p_seq, (size_t)n, false)) != hipSuccess) return bail(e, "hipMalloc(sequence)");
+    if ((e = alloc(&p_D, (size_t)n2, true)) != hipSuccess) return bail(e, "hipMalloc(D)");
+    if ((e = alloc(&p_D2, 4 * d2w, true)) != hipSuccess) return bail(e, "hipMalloc(D2)");
+    if ((e = alloc(&p_Dn, 4 * dnw, true)) != hipSuccess) return bail(e, "hipMalloc(Dn)");
+    if ((e = alloc(&p_S, af_genome_index_table_bytes(), true)) != hipSuccess) return bail(e, "hipMalloc(16-mer table)");
+    if ((e = alloc(&p_pos, 4 * nq, true)) != hipSuccess) return bail(e, "hipMalloc(positions)");
+    if ((e = alloc(&p_sums, 4 * (size_t)af_genome_scan_blocks(), false)) != hipSuccess) return bail(e, "hipMalloc(scan)");
+    if ((e = hipMemcpyAsync(p_seq, seq, (size_t)n, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(p_D2, 0, 4 * d2w, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(p_Dn, 0, 4 * dnw, c->stream)) != hipSuccess)
+        return bail(e, "upload");
+    if ((e = af_build_genome_index(static_cast<const uint8_t *>(p_seq), n, static_cast<uint8_t *>(p_D),
+                                   static_cast<uint32_t *>(p_D2), static_cast<uint32_t *>(p_Dn),
+                                   static_cast<uint32_t *>(p_S), static_cast<uint32_t *>(p_pos),
+                                   static_cast<uint32_t *>(p_sums), c->n_cu, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return bail(e, "build kernels");
+    af_free(p_seq);
+    af_free(p_sums);
+    ix->dev.D = static_cast<const uint8_t *>(p_D);
+    ix->dev.D2 = static_cast<const uint32_t *>(p_D2);
+    ix->dev.Dn = static_cast<const uint32_t *>(p_Dn);
+    ix->dev.kend = static_cast<const uint32_t *>(p_S) + 1;
+    ix->dev.kposu = static_cast<const uint32_t *>(p_pos);
+    ix->dev.n = n;
+    ix->dev.hbits = 0;
+    ix->dev.bl_bits = -1;
+    *out = ix;
+    return AF_OK;
+}
+
 void af_index_free(af_index *ix) {
     if (!ix) return;
     if (ix->ctx) (void)hipSetDevice(ix->ctx->device);
@@ -280,7 +336,9 @@ void af_index_free(af_index *ix) {
 }
 
 int64_t af_index_anchor_len(const af_index *ix) { return ix ? ix->dev.n : -1; }
-int32_t af_index_filter_words(const af_index *ix) { return ix ? (1 << ix->dev.bl_bits) : -1; }
+int32_t af_index_filter_words(const af_index *ix) {
+    return ix ? (ix->dev.bl_bits < 0 ? 0 : (1 << ix->dev.bl_bits)) : -1;
+}
 
 int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
     if (!ix || !out) return AF_E_INVALID;
@@ -291,6 +349,7 @@ int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
 
 int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
                           const int32_t *d_lens, int32_t *d_hits, void *stream) {
+    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || (!d_reads && n_reads) || !d_hits) return fail(c, AF_E_INVALID, "null argument");
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
     if (((uintptr_t)d_reads & 15) != 0) return fail(c, AF_E_INVALID, "reads buffer must be 16-byte aligned");
@@ -332,6 +391,7 @@ int af_align_pairs_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
 int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
                                int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
                                void *stream) {
+    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
     if (rc) return rc;
@@ -370,6 +430,7 @@ int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_r
 
 int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t n_pairs, int32_t stride,
                    const int32_t *lens, const af_params *p, af_aln_out *out) {
+    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || !out || (!reads && n_pairs)) return fail(c, AF_E_INVALID, "null argument");
     if (n_pairs == 0) return AF_OK;
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);

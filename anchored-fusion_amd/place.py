@@ -88,6 +88,20 @@ def concat_contigs(contigs):
     return (blob if blob else b"N"), offsets
 
 
+GENOME_INDEX_MIN = 1 << 25  # references from 32 Mbp up get the GPU-built genome index
+
+
+def index_kind(total):
+    """"hash" (host-built 16-mer hash of both strands, af_index_build) or "genome" (GPU-built
+    direct table, af_index_build_genome) for a reference of `total` bases; AF_INDEX_KIND=hash|genome
+    forces one."""
+    import os
+    k = os.environ.get("AF_INDEX_KIND", "auto")
+    if k in ("hash", "genome"):
+        return k
+    return "genome" if total >= GENOME_INDEX_MIN else "hash"
+
+
 class Reference:
     """Contigs [(name, seq)] indexed on the GPU for af_place."""
 
@@ -103,7 +117,10 @@ class Reference:
             _lib.check(None, L.af_ctx_create(int(device), ctypes.byref(ctx)), "af_ctx_create")
         self.ctx = ctx
         self.idx = ctypes.c_void_p()
-        _lib.check(self.ctx, L.af_index_build(self.ctx, blob, len(blob), ctypes.byref(self.idx)), "af_index_build")
+        self.kind = index_kind(len(blob))
+        build = L.af_index_build_genome if self.kind == "genome" else L.af_index_build
+        _lib.check(self.ctx, build(self.ctx, blob, len(blob), ctypes.byref(self.idx)),
+                   "af_index_build_genome" if self.kind == "genome" else "af_index_build")
 
     def close(self):
         L = _lib.lib()

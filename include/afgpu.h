@@ -113,6 +113,12 @@ int af_align_candidates_device(af_ctx *ctx, const af_index *idx, const uint8_t *
 /* number of candidate reads found by the last seed-filter pass on this context (synchronises) */
 int64_t af_last_candidates(af_ctx *ctx);
 
+/* Genome-scale index for af_place (replaces `bwa index <genome>`, Anchored_Fusion.py:173-178, and
+ * BLAT's per-call tile index): built on the GPU and HBM-resident (a direct table of all 4^16
+ * 16-mers, 16 GiB, plus 4 B per forward position and 2.6 B per base of sequence).  References of
+ * up to 2^32 - 2 bases (contigs joined by N runs); af_align_* reject it. */
+int af_index_build_genome(af_ctx *ctx, const char *seq, int64_t len, af_index **out);
+
 /* Multi-hit placement of queries (ASCII, `stride` bytes per row, optional lens) on an index
  * built with af_index_build over any reference (anchor, candidate blocks, or contigs joined by
  * N runs).  Every seed-extended region scoring >= p->T is reported, best score first, at most

@@ -55,3 +55,73 @@ def test_placer_psl_rows():
         assert f[13] in names and 0 <= int(f[15]) < int(f[16]) <= int(f[14])
         assert 0 <= int(f[11]) < int(f[12]) <= int(f[10])
     pl.close()
+
+
+def _repeat_contigs(seed=5):
+    """Contigs with exact repeats on both strands, a palindromic 16-mer run and N runs: 16-mers
+    whose occurrences mix forward and reverse-strand images (the genome index adds the latter
+    from the reverse complement's forward run)."""
+    from place_cases import rc
+    rng = np.random.default_rng(seed)
+    base = "".join(rng.choice(list("ACGT"), 9000))
+    unit = base[1000:1400]
+    pal = "ACGTTGCAACGTTGCA" * 3  # rc(pal) == pal
+    c1 = base[:3000] + unit + base[3000:5000] + rc(unit) + "N" * 40 + base[5000:7000] + pal + base[7000:]
+    c2 = "".join(rng.choice(list("ACGT"), 12000))
+    c2 = c2[:4000] + unit + c2[4000:8000] + rc(c1[200:500]) + c2[8000:]
+    return [("chrA", c1), ("chrB", c2)]
+
+
+@pytest.mark.parametrize("case", ["random", "repeats"])
+def test_place_parity_genome_index(monkeypatch, case):
+    # the GPU-built direct 16-mer table (af_index_build_genome) gives the same hits as the oracle
+    monkeypatch.setenv("AF_INDEX_KIND", "genome")
+    ctgs = contigs(seed=3) if case == "random" else _repeat_contigs()
+    blob, _ = place.concat_contigs(ctgs)
+    qs = queries(ctgs, 1200, seed=9, lens=(20, 40, 60, 100, 150))
+    if case == "repeats":
+        qs += [("u", ctgs[0][1][2990:3100], None), ("p", "TT" + "ACGTTGCAACGTTGCA" * 3 + "GG", None)]
+    seqs = [q for _, q, _ in qs]
+    ref = place.Reference(ctgs)
+    assert ref.kind == "genome"
+    for T, seed_len in ((20, 16), (30, 19)):
+        p = place._lib.default_params()
+        p.T, p.min_seed_len = T, seed_len
+        g, gn = ref.raw_hits(seqs, p, 8)
+        buf, ln = place.pack_queries(seqs)
+        po = oracle.default_params()
+        po.T, po.min_seed_len = T, seed_len
+        r, rn = oracle.OracleIndex(blob).place(buf, ln, po, 8, threads=8)
+        _same(g, gn, r, rn)
+    ref.close()
+
+
+def test_genome_index_large_reference():
+    # 320 Mbp in 4 contigs (auto-selects the genome index): reads drawn from known positions,
+    # half reverse-complemented, are placed there (no oracle at this size)
+    from place_cases import rc
+    rng = np.random.default_rng(17)
+    lens = (80_000_000,) * 4
+    ctgs = [(f"chr{k + 1}", rng.choice(np.frombuffer(b"ACGT", np.uint8), n).tobytes().decode())
+            for k, n in enumerate(lens)]
+    ref = place.Reference(ctgs)
+    assert ref.kind == "genome"
+    seqs, truth = [], []
+    for i in range(2000):
+        k = int(rng.integers(4))
+        s = int(rng.integers(0, lens[k] - 150))
+        q = ctgs[k][1][s:s + 150]
+        rev = i % 2 == 1
+        seqs.append(rc(q) if rev else q)
+        truth.append((k, s, rev))
+    p = place._lib.default_params()
+    g, gn = ref.raw_hits(seqs, p, 4)
+    ok = 0
+    for i, (k, s, rev) in enumerate(truth):
+        if gn[i] < 1:
+            continue
+        h = g[i, 0]
+        loc = ref.locate(h["t_start"], h["t_end"])
+        ok += loc is not None and loc[0] == k and loc[1] == s and bool(h["flag"] & 0x10) == rev and h["score"] == 150
+    assert ok == len(truth)
+    ref.close()
