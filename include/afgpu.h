@@ -13,6 +13,10 @@
  *   af_align_pairs_device <- same, device-resident buffers, enqueued on a HIP stream
  *   af_seed_filter_device <- the seeding pass of the same call (the HBM-bound kernel)
  *   af_align_candidates_device <- the extension/CIGAR/pairing pass of the same call
+ *   af_place              <- the genome `bwa mem` calls (AF:188, functions.py:716) and the BLAT
+ *                            calls (functions.py:341, 530, 1007, 1071, 1122, 1244)
+ *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
+ *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
  * Conventions: plain pointers and sizes only; every function returns AF_OK (0) or a
  * negative AF_E_* code and sets a message readable with af_last_error().  No C++
