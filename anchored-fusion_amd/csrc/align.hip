@@ -443,8 +443,11 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     return ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
 }
 
-// Traceback of a filled ksw_global2 direction matrix z (n_col = min(qlen, 2w+1) bytes per row),
-// leaving the CIGAR (reverse order) in L.ring with L.misc[2] ops.
+// Traceback of a filled ksw_global2 direction matrix z, leaving the CIGAR (reverse order) in
+// L.ring with L.misc[2] ops.  Byte layout (global_dp_wave): n_col = min(qlen, 2w+1) bytes per
+// row from column beg, codes which | E-extend << 2 | F-extend << 4.  BAND layout (global_dp_band):
+// a nibble per band lane k = j - i + w, 2w + 2 nibbles per row, codes which | E << 2 | F << 3.
+template <bool BAND>
 __device__ __forceinline__ void global_traceback(int qlen, int tlen, int w, const uint8_t *z, AlnLds &L, int lane) {
     const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
     wave_sync();
@@ -472,7 +475,14 @@ __device__ __forceinline__ void global_traceback(int qlen, int tlen, int w, cons
         while (i >= 0 && k >= 0) {
             const int it = i - (state != 2 ? lane : 0), kt = k - (state != 1 ? lane : 0);
             int wt = -1;
-            if (it >= 0 && kt >= 0) {
+            if (BAND) {
+                const int kk = kt - it + w;
+                if (it >= 0 && kt >= 0 && (unsigned)kk <= (unsigned)(2 * w)) {
+                    const uint32_t nib = (uint32_t)it * (uint32_t)(2 * w + 2) + (uint32_t)kk;
+                    const int v = (z[nib >> 1] >> ((nib & 1u) << 2)) & 15;
+                    wt = state == 0 ? (v & 3) : (state == 1 ? ((v >> 2) & 1) : ((v >> 2) & 2));
+                }
+            } else if (it >= 0 && kt >= 0) {
                 const int idx = it * n_col + (kt - (it > w ? it - w : 0));
                 if (idx >= 0 && idx < zsize) wt = z[idx] >> (state << 1) & 3;
             }
@@ -579,7 +589,7 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
         }
     }
     const int score = bcast(pick<CPL>(eh_h, qlen - (qlen / cpl) * cpl), qlen / cpl);
-    global_traceback(qlen, tlen, w, z, L, lane);
+    global_traceback<false>(qlen, tlen, w, z, L, lane);
     return score;
 }
 
@@ -591,8 +601,7 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
 __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
                               uint8_t *__restrict__ zg, AlnLds &L, int lane) {
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
-    const int n_col = 2 * w + 1;  // qlen >= 64 > 2w + 1
-    const int k = lane;
+    const int k = lane;  // qlen >= 64 > 2w + 1: every band lane exists
     const bool band = k <= 2 * w;
     // q[-1] and q[qlen] read as N: the query base of any lane is one clamped LDS read
     if (lane == 0) { L.qs_pad[15] = 4; L.qs[qlen] = 4; }
@@ -627,9 +636,12 @@ __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_
         const int tt = m - oe_del, ee = e - p.e_del;
         d |= ee > tt ? 1 << 2 : 0;
         const int tf = m - oe_ins, ff = f - p.e_ins;
-        d |= ff > tf ? 2 << 4 : 0;
-        // z row i, column j - beg = k - max(w - i, 0): a uniform row base plus the lane
-        if (in) zg[(uint32_t)(i * n_col - (w - i > 0 ? w - i : 0)) + (uint32_t)k] = (uint8_t)d;
+        d |= ff > tf ? 1 << 3 : 0;
+        // z row i: one nibble per band lane (2w + 2 per row), lanes 2m and 2m + 1 in one byte
+        // written by the even lane (nibbles of lanes whose cell is outside the matrix are never
+        // read by the traceback)
+        const int dup = __builtin_amdgcn_mov_dpp(d, 0x130, 0xf, 0xf, true);  // wave_shl:1: lane k + 1
+        if (!(k & 1) && k <= 2 * w) zg[(uint32_t)i * (uint32_t)(w + 1) + (uint32_t)(k >> 1)] = (uint8_t)(d | (dup << 4));
         Eo = in ? (ee > tt ? ee : tt) : AF_NEG_INF;
         Hd = in ? h : ((j == -1 && beg == 0) ? -(p.o_del + p.e_del * (i + 1)) : AF_NEG_INF);
         qc = qn;
@@ -638,7 +650,7 @@ __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_
         jEo += p.e_ins;
     }
     const int score = bcast(Hd, qlen - tlen + w);  // eh[qlen].h = H(tlen-1, qlen-1)
-    global_traceback(qlen, tlen, w, zg, L, lane);
+    global_traceback<true>(qlen, tlen, w, zg, L, lane);
     return score;
 }
 
