@@ -22,9 +22,9 @@ struct DevIndex {
     const uint8_t *D;       // doubled reference codes (anchor ++ revcomp), N = 4, length 2n
     const uint32_t *D2;     // 2-bit packed D, 16 bases per word (base i at bits 2i), padded
     const uint32_t *Dn;     // N bitmap of D, 32 bases per word, padded
-    const uint32_t *hkey;   // 16-mer position hash: key
-    const int32_t *hstart;  //   first index into kpos
-    const int32_t *hcnt;    //   occurrences (0 = empty slot)
+    // 16-mer position hash, one 16-byte slot per entry (one load per probe): {key, first index
+    // into kpos, occurrences (0 = empty slot), kpos[first] (a unique 16-mer needs no kpos load)}
+    const int4 *hslot;
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
     const uint32_t *bloom;  // Bloom filter of the anchor 16-mers (2^bl_bits words, see af_k1_hash)
     // direct (genome-scale) indexes instead of the hash: kend[k] = end of 16-mer k's run of

@@ -794,7 +794,7 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
             // occurrences in the doubled reference: a hash index holds both strands' 16-mers; a
             // direct (genome-scale) index holds the forward strand only, so k's occurrences are
             // its forward run plus the reverse-strand images n2 - 16 - q of rc(k)'s forward run
-            int cnt = 0, st = 0, n_fwd = 0;
+            int cnt = 0, st = 0, n_fwd = 0, pos0 = 0;
             uint32_t b_fwd = 0, b_rc = 0;
             if (ix.kend) {
                 const uint32_t rk = af_rc16(k);
@@ -805,15 +805,15 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
             } else {
                 uint32_t s = af_fmix(k) & hm;
                 for (;;) {
-                    const int cc = ix.hcnt[s];
-                    if (cc == 0) break;
-                    if (ix.hkey[s] == k) { cnt = cc; st = ix.hstart[s]; break; }
+                    const int4 e = ix.hslot[s];
+                    if (e.z == 0) break;
+                    if ((uint32_t)e.x == k) { cnt = e.z; st = e.y; pos0 = e.w; break; }
                     s = (s + 1) & hm;
                 }
             }
             if (cnt == 0 || cnt > p.max_occ) continue;
             for (int o = 0; o < cnt; ++o) {
-                const int64_t rb = !ix.kend ? (int64_t)ix.kpos[st + o]
+                const int64_t rb = !ix.kend ? (int64_t)(o == 0 ? pos0 : ix.kpos[st + o])
                                             : (o < n_fwd ? (int64_t)ix.kposu[b_fwd + o]
                                                          : n2 - AF_K - (int64_t)ix.kposu[b_rc + (o - n_fwd)]);
                 if (qb > 0 && rb != 0 && rb != n) {

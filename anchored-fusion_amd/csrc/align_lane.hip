@@ -289,9 +289,9 @@ __device__ bool lane_align_read(const DevIndex &ix, const LaneCtx &L, const Lane
         uint32_t s = af_fmix(k) & hm;
         int cnt = 0, st = 0;
         for (;;) {
-            const int cc = ix.hcnt[s];
-            if (cc == 0) break;
-            if (ix.hkey[s] == k) { cnt = cc; st = ix.hstart[s]; break; }
+            const int4 e = ix.hslot[s];
+            if (e.z == 0) break;
+            if ((uint32_t)e.x == k) { cnt = e.z; st = e.y; break; }
             s = (s + 1) & hm;
         }
         if (cnt == 0 || cnt > P.max_occ) continue;

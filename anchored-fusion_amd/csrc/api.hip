@@ -233,12 +233,11 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     int hbits = 10;
     while ((1LL << hbits) < 2 * nd) ++hbits;
     const uint32_t hm = (1u << hbits) - 1u;
-    std::vector<uint32_t> hkey(1u << hbits, 0);
-    std::vector<int32_t> hstart(1u << hbits, 0), hcnt(1u << hbits, 0);
+    std::vector<int4> hslot(1u << hbits, int4{0, 0, 0, 0});
     for (int64_t i = 0; i < nd; ++i) {
         uint32_t s = af_fmix(keys[i]) & hm;
-        while (hcnt[s]) s = (s + 1) & hm;
-        hkey[s] = keys[i]; hstart[s] = starts[i]; hcnt[s] = cnts[i];
+        while (hslot[s].z) s = (s + 1) & hm;
+        hslot[s] = int4{(int)keys[i], starts[i], cnts[i], kpos[starts[i]]};
     }
     // Bloom filter of the distinct 16-mers (seed filter K1): 2^bl_bits 32-bit words, ~2.4 words
     // per key (at most 2^15 words = 128 KiB, a 6.8 kb anchor), four bits in each of two words
@@ -258,8 +257,7 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     int rc = AF_OK;
     const uint32_t *bld = nullptr;
     if ((rc = dev_upload(c, ix, D, &ix->dev.D)) || (rc = dev_upload(c, ix, D2, &ix->dev.D2)) ||
-        (rc = dev_upload(c, ix, Dn, &ix->dev.Dn)) || (rc = dev_upload(c, ix, hkey, &ix->dev.hkey)) ||
-        (rc = dev_upload(c, ix, hstart, &ix->dev.hstart)) || (rc = dev_upload(c, ix, hcnt, &ix->dev.hcnt)) ||
+        (rc = dev_upload(c, ix, Dn, &ix->dev.Dn)) || (rc = dev_upload(c, ix, hslot, &ix->dev.hslot)) ||
         (rc = dev_upload(c, ix, kpos, &ix->dev.kpos)) || (rc = dev_upload(c, ix, bloom, &bld))) {
         af_index_free(ix);
         return rc;

@@ -425,7 +425,11 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
                 carry += __shfl(incl, 63);
             }
             int bse = 0;
+#if AF_K1_ABL == 6  // timing only: no returning device atomic (candidate slots overlap)
+            if (lane == 0 && carry) bse = (int)(blockIdx.x & 7);
+#else
             if (lane == 0 && carry) bse = atomicAdd(cnt_g, carry);
+#endif
             bse = __shfl(bse, 0);
             for (int q = lane; q < ng; q += 64) gbase[q] += bse;
         }
