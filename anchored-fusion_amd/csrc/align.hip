@@ -20,7 +20,7 @@ namespace {
 #ifdef AF_K2_PROF
 // profiling build only (make prof -> libafgpu_prof.so): per-candidate phase timings
 __device__ int32_t *g_k2prof = nullptr;
-constexpr int PROF_W = 16;
+constexpr int PROF_W = 20;  // [16] slot, [17]/[18] s_memrealtime (100 MHz) at item start/end
 #define PROF(...) __VA_ARGS__
 #else
 #define PROF(...)
@@ -745,6 +745,7 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
             if (item >= ncand) break;
         }
         const int64_t r = cand ? cand[item] : item;
+        PROF(const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();)
         PROF(const int64_t pt0 = clock64(); int64_t pt1 = pt0, pt2 = pt0; int p_ext_rows = 0, p_cig_rows = 0,
              p_ext_calls = 0, p_nreg = 0, p_ext_dp = 0;)
         int l = lens ? lens[r] : stride;
@@ -1093,6 +1094,8 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
         if (lane == 0 && g_k2prof) {
             const int64_t pt3 = clock64();
             int32_t *o = g_k2prof + (int64_t)item * PROF_W;
+            o[16] = (int32_t)blockIdx.x; o[17] = (int32_t)rt0;
+            o[18] = (int32_t)__builtin_amdgcn_s_memrealtime();
             o[0] = (int32_t)r; o[1] = (int32_t)(pt3 - pt0); o[2] = (int32_t)(pt1 - pt0);
             o[3] = (int32_t)(pt2 - pt1); o[4] = (int32_t)(pt3 - pt2); o[5] = nm_total; o[6] = p_nreg; o[9] = p_ext_dp;
             o[7] = p_ext_rows; o[8] = p_cig_rows; o[10] = p_ext_calls;

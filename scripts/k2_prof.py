@@ -69,4 +69,21 @@ for nm, (cc, rr) in (("ext w1", (12, 13)), ("ext gen", (14, 15))):
 A = np.stack([buf[:, 7], buf[:, 8], np.ones(nc)], 1).astype(np.float64)
 coef, *_ = np.linalg.lstsq(A, (buf[:, 3] + buf[:, 4]).astype(np.float64), rcond=None)
 print(f"  fit ext+cigar cycles ~ {coef[0]:.0f}*ext_rows + {coef[1]:.0f}*cig_rows + {coef[2]:.0f}")
-
+if W >= 19:
+    # schedule: per-slot busy spans from s_memrealtime (100 MHz), the makespan and its tail
+    slot, t0, t1 = buf[:, 16], buf[:, 17].astype(np.int64), buf[:, 18].astype(np.int64)
+    base = t0.min()
+    t0, t1 = (t0 - base) & 0xFFFFFFFF, (t1 - base) & 0xFFFFFFFF
+    span = t1.max()
+    last = np.zeros(slot.max() + 1, np.int64)
+    np.maximum.at(last, slot, t1)
+    busy = np.zeros(slot.max() + 1, np.int64)
+    np.add.at(busy, slot, t1 - t0)
+    q = np.percentile(last, [1, 50, 99])
+    print(f"  schedule: makespan {span / 100:.1f} us; slot finish p1 {q[0] / 100:.1f} p50 {q[1] / 100:.1f} "
+          f"p99 {q[2] / 100:.1f} us; mean slot busy {busy.mean() / 100:.1f} us; "
+          f"items started after 90% of the makespan {(t0 > 0.9 * span).sum()}; longest item {(t1 - t0).max() / 100:.1f} us")
+    late = np.argsort(t1)[-5:]
+    for k in late:
+        print(f"    late item {k}: start {t0[k] / 100:.1f} end {t1[k] / 100:.1f} us, hits {int(out['hits'][int(buf[k, 0])])}, "
+              f"nmem {buf[k, 5]} nreg {buf[k, 6]} ext_rows {buf[k, 7]} cig_rows {buf[k, 8]}")
