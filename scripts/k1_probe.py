@@ -33,3 +33,12 @@ e1.record(s)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / iters
 print(f"k1 {ms * 1e3:.1f} us/launch  {reads.nbytes / (ms * 1e-3) / 1e9:.1f} GB/s  cand={al.last_candidates()}")
+# the bench's way: events around each launch (the step's other kernels absent)
+evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(iters)]
+for k in range(iters):
+    evs[k][0].record(s)
+    al.seed_filter_device(rt, reads.shape[0], L, hits, stream=s)
+    evs[k][1].record(s)
+torch.cuda.synchronize()
+ms1 = sum(a.elapsed_time(b) for a, b in evs) / iters
+print(f"k1 per-launch events {ms1 * 1e3:.1f} us/launch")
