@@ -419,6 +419,132 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
     return r;
 }
 
+// ksw_extend2 for 64 <= qlen <= 127: lane l owns query columns 2l and 2l + 1 (column qlen is the
+// eh[qlen] slot).  Same recurrences, tie-breaks and bookkeeping split as ext_dp_w1; the F chain
+// takes one wave scan of the lane pairs' maxima (column 2l + 1 adds column 2l's term in-lane) and
+// the band trimming two ballots per column parity.
+__device__ __noinline__ ExtRes ext_dp_w2(int qlen_, int qsel_, int qoff_, int tlen_, Sc p_, int w_, int end_bonus_,
+                                         int zdrop_, int h0_) {
+#define AF_U(x) __builtin_amdgcn_readfirstlane(x)
+    const int qlen = AF_U(qlen_), tlen = AF_U(tlen_), end_bonus = AF_U(end_bonus_), zdrop = AF_U(zdrop_),
+              h0 = AF_U(h0_), qoff = AF_U(qoff_);
+    int w = AF_U(w_);
+    const Sc p{AF_U(p_.a), AF_U(p_.b), AF_U(p_.o_del), AF_U(p_.e_del), AF_U(p_.o_ins), AF_U(p_.e_ins)};
+    const uint8_t *q = (AF_U(qsel_) ? g_aln.q : g_aln.qs) + qoff;
+    const uint8_t *t = g_aln.t;
+#undef AF_U
+    const int lane = threadIdx.x;
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int j0 = 2 * lane, j1 = j0 + 1;
+    int H0, H1, E0 = 0, E1 = 0;
+    {
+        const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+        const int va = v1 - (j0 - 1) * p.e_ins, vb = v1 - (j1 - 1) * p.e_ins;
+        H0 = j0 > qlen ? 0 : (j0 == 0 ? h0 : (va > 0 ? va : 0));
+        H1 = j1 > qlen ? 0 : (j1 == 1 ? v1 : (vb > 0 ? vb : 0));
+    }
+    const int qc0 = j0 < qlen ? q[j0] : 4, qc1 = j1 < qlen ? q[j1] : 4;
+    const bool qn0 = qc0 > 3, qn1 = qc1 > 3;
+    // per-column constants as in ext_dp_w1 (column 0's jE1 is 2^30: its f loses to M/E >= 0)
+    const int jEa = j0 * p.e_ins, jEoa = jEa - oe_ins, jE1a = j0 == 0 ? (1 << 30) : (j0 - 1) * p.e_ins;
+    const int jEb = j1 * p.e_ins, jEob = jEb - oe_ins, jE1b = j0 * p.e_ins;
+    const int tailA0 = (qlen - j0) * p.a, tailA1 = (qlen - j1) * p.a;
+    {
+        int max_ins = div_plus(qlen * p.a + end_bonus - p.o_ins, p.e_ins, 1);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = div_plus(qlen * p.a + end_bonus - p.o_del, p.e_del, 1);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    const int vz = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);
+    int mx = h0 + vz, max_i = vz - 1, max_j = vz - 1, max_ie = vz - 1, gscore = vz - 1, max_off = vz;
+    int beg = 0, end = qlen, rows = 0;
+    const int lq_lane = (qlen - 1) >> 1, lq_odd = (qlen - 1) & 1;
+    int ti_next = tlen > 0 ? t[0] : 4;
+    for (int i = 0; i < tlen; ++i) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
+        ++rows;
+        beg = max(beg, i - w);
+        end = min(min(end, i + w + 1), qlen);
+        int h1s = 0;
+        if (beg == 0) h1s = max(h0 - (p.o_del + p.e_del * (i + 1)), 0);
+        if (beg >= end) {
+            if (beg == qlen) {
+                max_ie = gscore > h1s ? max_ie : i + vz;
+                gscore = gscore > h1s ? gscore : h1s;
+            }
+            break;
+        }
+        const bool in0 = (unsigned)(j0 - beg) < (unsigned)(end - beg);
+        const bool in1 = (unsigned)(j1 - beg) < (unsigned)(end - beg);
+        const int tiu = __builtin_amdgcn_readfirstlane(ti);
+        const int s_eq = tiu > 3 ? -1 : p.a, s_ne = tiu > 3 ? -1 : -p.b;
+        const int sc0 = qc0 == tiu ? s_eq : (qn0 ? -1 : s_ne);
+        const int sc1 = qc1 == tiu ? s_eq : (qn1 ? -1 : s_ne);
+        const int M0 = (in0 && H0 != 0) ? H0 + sc0 : 0;
+        const int M1 = (in1 && H1 != 0) ? H1 + sc1 : 0;
+        const int va = max(M0 + jEoa, jEa), vb = max(M1 + jEob, jEb);
+        // exclusive prefix over lanes of the pair maxima (0 into lane 0: every term is >= 0)
+        const int X = __builtin_amdgcn_mov_dpp(wave_incl_max(max(va, vb)), 0x138, 0xf, 0xf, true);
+        const int f0 = X - jE1a, f1 = max(X, va) - jE1b;
+        const int hA = max(max(M0, E0), f0), hB = max(max(M1, E1), f1);
+        const int key = max(in0 ? ((hA << 10) | j0) : -1, in1 ? ((hB << 10) | j1) : -1);
+        const int kmax = wave_max(key) + vz;
+        const int m = max(kmax, 0) >> 10;
+        const int mj = kmax < 0 ? -1 : (kmax & 1023);
+        const int hq = bcast(lq_odd ? hB : hA, lq_lane) + vz;
+        const int from_left = __builtin_amdgcn_mov_dpp(hB, 0x138, 0xf, 0xf, true);  // column j0 - 1
+        const int Eu0 = max(max(E0 - p.e_del, M0 - oe_del), 0);
+        const int Eu1 = max(max(E1 - p.e_del, M1 - oe_del), 0);
+        H0 = j0 <= end ? (j0 == beg ? h1s : from_left) : H0;
+        H1 = j1 <= end ? (j1 == beg ? h1s : hA) : H1;
+        E0 = j0 < end ? Eu0 : (j0 == end ? 0 : E0);
+        E1 = j1 < end ? Eu1 : (j1 == end ? 0 : E1);
+        if (end == qlen) {
+            max_ie = gscore > hq ? max_ie : i + vz;
+            gscore = max(gscore, hq);
+        }
+        const bool better = m > mx;
+        const int di = i - max_i, dj = mj - max_j;
+        const int zgap = di > dj ? mx - m - __mul24(di - dj, p.e_del) : mx - m - __mul24(dj - di, p.e_ins);
+        const int zt = better ? INT_MIN : zgap;
+        const int off = mj - i < 0 ? i - mj : mj - i;
+        max_off = better ? max(max_off, off) : max_off;
+        max_i = better ? i + vz : max_i;
+        max_j = better ? mj : max_j;
+        mx = better ? m : mx;
+        const int stop = m == 0 ? 1 : (zt > zdrop ? zdrop : 0);
+        if (__builtin_amdgcn_readfirstlane(stop) > 0) break;
+        // band trimming: first non-zero eh in [beg, end), last in [beg, end]; even and odd
+        // columns on separate ballots
+        const int x0 = (H0 | E0) != 0 ? j0 - beg : 1 << 20, x1 = (H1 | E1) != 0 ? j1 - beg : 1 << 20;
+        const uint32_t span = (uint32_t)(end - beg);
+        const uint64_t fa = __ballot((unsigned)x0 < span), fb = __ballot((unsigned)x1 < span);
+        const uint64_t la = __ballot((unsigned)x0 <= span), lb = __ballot((unsigned)x1 <= span);
+        const int fza = fa ? 2 * (int)__builtin_ctzll(fa) : (1 << 20), fzb = fb ? 2 * (int)__builtin_ctzll(fb) + 1 : (1 << 20);
+        const int fz = min(fza, fzb);
+        const int beg_new = fz < (1 << 20) ? fz : end;
+        const int lza = la ? 2 * (63 - (int)__builtin_clzll(la)) : -1, lzb = lb ? 2 * (63 - (int)__builtin_clzll(lb)) + 1 : -1;
+        const int lnz = max(lza, lzb);
+        const int jstar = lnz >= beg_new ? lnz : beg_new - 1;
+        beg = beg_new;
+        end = jstar + 2 < qlen ? jstar + 2 : qlen;
+        if (i & 1) {
+            const int ua = (unsigned)(j0 - beg) <= (unsigned)(qlen - beg) ? max(H0, E0) + tailA0 : 0;
+            const int ub = (unsigned)(j1 - beg) <= (unsigned)(qlen - beg) ? max(H1, E1) + tailA1 : 0;
+            const int U = wave_max(max(ua, ub)) + vz;
+            const int g = U <= mx ? (U < gscore ? gscore : 0) : 0;
+            if (__builtin_amdgcn_readfirstlane(g) > 0) break;
+        }
+    }
+    ExtRes r;
+    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off;
+    r.rows = rows;
+    return r;
+}
+
 // one column per lane when the query fits a wave (the common case: a 100-bp read's flanks),
 // otherwise CPL columns per lane; the per-row VALU cost scales with the columns per lane
 template <int CPL>
@@ -431,6 +557,9 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     if (one)
         r = ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
                       Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
+    else if (qlen + 1 <= 128)
+        r = ext_dp_w2(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
+                      Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
     else
         r = ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
     const int dc = (int)(clock64() - c0);
@@ -439,6 +568,9 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
 #endif
     if (CPL == 1 || qlen + 1 <= 64)
         return ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
+                         Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
+    if (qlen + 1 <= 128)
+        return ext_dp_w2(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
                          Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
     return ext_dp_wave<CPL>(qlen, q, tlen, t, p, w, end_bonus, zdrop, h0, lane);
 }
