@@ -21,6 +21,8 @@ struct af_ctx {
     int32_t *ctrl = nullptr;   // af_internal.h: candidate counts (2 epochs) + K2 dequeue heads
     int64_t epoch = 0;         // seed-filter calls so far; the last call used count slot (epoch - 1) & 1
     int32_t *cand = nullptr;
+    uint32_t *d_packed = nullptr;  // af_align_pairs: the candidates' CIGAR rows, gathered for one D2H
+    int64_t cap_packed = 0;
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
     uint8_t *zscratch = nullptr;
@@ -72,6 +74,16 @@ int fail(af_ctx *c, int code, const char *fmt, ...) {
         hipError_t _e = (expr);                                                                 \
         if (_e != hipSuccess) return fail(ctx, AF_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
+
+// CIGAR rows of the candidate reads (the only rows K2 writes) packed for one device-to-host copy
+__global__ void k_gather_cigar(const int32_t *__restrict__ cand, int64_t n, const uint32_t *__restrict__ cigar,
+                               uint32_t *__restrict__ packed) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * (AF_MAX_CIGAR / 4);
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / (AF_MAX_CIGAR / 4), w = t % (AF_MAX_CIGAR / 4);
+        reinterpret_cast<uint4 *>(packed)[t] = reinterpret_cast<const uint4 *>(cigar + (int64_t)cand[i] * AF_MAX_CIGAR)[w];
+    }
+}
 
 inline uint8_t nt4(uint8_t c) {
     switch (c) {
@@ -177,7 +189,7 @@ int af_ctx_create(int device, af_ctx **out) {
 void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->d_packed);
     af_free(c->lane_scratch); af_free(c->defer);
     af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
     af_free(c->d_reads); af_free(c->d_lens);
@@ -459,7 +471,6 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
             if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
         HIPCHK(c, hipMemcpyAsync(c->d_lens, lens, 4 * nr, hipMemcpyHostToDevice, s));
     }
-    HIPCHK(c, hipMemsetAsync(c->d_cigar, 0, sizeof(uint32_t) * AF_MAX_CIGAR * nr, s));
     af_aln_out d{c->d_flag, c->d_pos, c->d_score, c->d_ncig, c->d_hits, c->d_cigar};
     int rc = af_align_pairs_device(c, ix, c->d_reads, n_pairs, stride, lens ? c->d_lens : nullptr, p, &d, s);
     if (rc) return rc;
@@ -468,9 +479,31 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
     if (out->score) HIPCHK(c, hipMemcpyAsync(out->score, c->d_score, 4 * nr, hipMemcpyDeviceToHost, s));
     if (out->n_cigar) HIPCHK(c, hipMemcpyAsync(out->n_cigar, c->d_ncig, 4 * nr, hipMemcpyDeviceToHost, s));
     if (out->hits) HIPCHK(c, hipMemcpyAsync(out->hits, c->d_hits, 4 * nr, hipMemcpyDeviceToHost, s));
-    if (out->cigar)
-        HIPCHK(c, hipMemcpyAsync(out->cigar, c->d_cigar, sizeof(uint32_t) * AF_MAX_CIGAR * nr, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    if (out->cigar) {
+        // only candidate reads have CIGARs: gather their rows on the device and copy those
+        const int slot = (int)((c->epoch - 1) & 1);
+        int32_t nc = 0;
+        HIPCHK(c, hipMemcpy(&nc, c->ctrl + AF_HEAD_STRIDE * slot, sizeof nc, hipMemcpyDeviceToHost));
+        if (nc > 0) {
+            if (nc > c->cap_packed) {
+                af_free(c->d_packed); c->d_packed = nullptr; c->cap_packed = 0;
+                HIPCHK(c, hipMalloc(&c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * (size_t)nc));
+                c->cap_packed = nc;
+            }
+            hipLaunchKernelGGL(k_gather_cigar, dim3((unsigned)std::min<int64_t>(4096, (nc * 8 + 255) / 256)), dim3(256),
+                               0, s, c->cand, (int64_t)nc, c->d_cigar, c->d_packed);
+            HIPCHK(c, hipGetLastError());
+            std::vector<int32_t> ids((size_t)nc);
+            std::vector<uint32_t> rows((size_t)nc * AF_MAX_CIGAR);
+            HIPCHK(c, hipMemcpyAsync(ids.data(), c->cand, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(rows.data(), c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * nc, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            for (int32_t i = 0; i < nc; ++i)
+                memcpy(out->cigar + (int64_t)ids[i] * AF_MAX_CIGAR, rows.data() + (size_t)i * AF_MAX_CIGAR,
+                       sizeof(uint32_t) * AF_MAX_CIGAR);
+        }
+    }
     return AF_OK;
 }
 

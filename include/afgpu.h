@@ -26,6 +26,7 @@
  * Reads are pair-major, one byte per base (ASCII): row 2p = mate 1, row 2p+1 = mate 2,
  * `stride` bytes per row; `lens` may be NULL when every read has length `stride`.
  * Output arrays are caller-owned (flag/pos/score/n_cigar 8-byte aligned), 2*n_pairs entries each (cigar: 2*n_pairs*AF_MAX_CIGAR,
+ * of which only the first n_cigar entries of a row are written,
  * BAM op encoding len<<4|op, M=0 I=1 D=2 S=4).  pos is the 0-based leftmost position of
  * the primary alignment (or of the mate, for an unmapped read with a mapped mate, as bwa
  * prints it); flag carries the SAM bits 0x1 0x4 0x8 0x10 0x20 0x40 0x80 plus
