@@ -76,6 +76,19 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 }
 // lane l receives lane l-1's value; lane 0 receives `old`
 __device__ __forceinline__ int wave_shr1(int old, int v) { return dpp<0x138>(old, v); }
+// inclusive prefix max over lanes 0..SPAN-1 (SPAN = 16, 32 or 64); lanes >= SPAN get partial values
+template <int SPAN>
+__device__ __forceinline__ int span_incl_max(int v) {
+    v = max(v, dpp<0x111>(kMaxId, v));
+    v = max(v, dpp<0x112>(kMaxId, v));
+    v = max(v, dpp<0x114>(kMaxId, v));
+    v = max(v, dpp<0x118>(kMaxId, v));
+    if (SPAN > 16) v = max(v, dpp<0x142, 0xa>(kMaxId, v));
+    if (SPAN > 32) v = max(v, dpp<0x143, 0xc>(kMaxId, v));
+    return v;
+}
+template <int SPAN>
+__device__ __forceinline__ int span_max(int v) { return __builtin_amdgcn_readlane(span_incl_max<SPAN>(v), SPAN - 1); }
 __device__ __forceinline__ int bcast(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ int wave_max(int v) { return bcast(wave_incl_max(v), 63); }
 __device__ __forceinline__ int wave_sum(int v) {
@@ -296,6 +309,9 @@ __device__ ExtRes ext_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
 // Kept out of line: inlined into k_align its loop ran out of SGPRs and spilled to VGPR lanes
 // on every row; as a call it gets its own register allocation (one save/restore per call).
 struct Sc { int a, b, o_del, e_del, o_ins, e_ins; };
+// SPAN: the lanes the row's scans and maxima cover (qlen + 1 <= SPAN; lanes past qlen hold no
+// band cell and never feed a lane to their left), so short flanks skip the cross-row DPP steps
+template <int SPAN>
 __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tlen_, Sc p_, int w_, int end_bonus_,
                                          int zdrop_, int h0_) {
     // arguments of an out-of-line call arrive in VGPRs: re-assert wave uniformity
@@ -367,11 +383,11 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         const int sc = qc == tiu ? s_eq : (qn ? -1 : s_ne);
         int M = H != 0 ? H + sc : 0;
         M = in ? M : 0;
-        const int P = __builtin_amdgcn_mov_dpp(wave_incl_max(max(M + jEo, jE)), 0x138, 0xf, 0xf, true);
+        const int P = __builtin_amdgcn_mov_dpp(span_incl_max<SPAN>(max(M + jEo, jE)), 0x138, 0xf, 0xf, true);
         const int f = P - jE1;
         const int h = max(max(M, E), f);
         const int key = in ? ((h << 10) | j) : -1;
-        const int kmax = wave_max(key) + vz;
+        const int kmax = span_max<SPAN>(key) + vz;
         const int m = max(kmax, 0) >> 10;
         const int mj = kmax < 0 ? -1 : (kmax & 1023);
         const int hq = bcast(h, qlen - 1) + vz;
@@ -408,7 +424,7 @@ __device__ __noinline__ ExtRes ext_dp_w1(int qlen_, int qsel_, int qoff_, int tl
         // exact early exit (see ext_dp_wave), on odd rows
         if (i & 1) {
             const int u = (unsigned)(j - beg) <= (unsigned)(qlen - beg) ? max(H, E) + tailA : 0;
-            const int U = wave_max(u) + vz;
+            const int U = span_max<SPAN>(u) + vz;
             const int g = U <= mx ? (U < gscore ? gscore : 0) : 0;  // > 0 iff gscore > 0, U <= max, U < gscore
             if (__builtin_amdgcn_readfirstlane(g) > 0) break;
         }
@@ -545,6 +561,16 @@ __device__ __noinline__ ExtRes ext_dp_w2(int qlen_, int qsel_, int qoff_, int tl
     return r;
 }
 
+// ext_dp_w1 at the narrowest scan span that covers the query (qlen + 1 <= 64)
+__device__ __forceinline__ ExtRes ext_dp_w1s(int qlen, const uint8_t *q, int tlen, const af_params &p, int w,
+                                             int end_bonus, int zdrop, int h0) {
+    const int qsel = q == g_aln.qs ? 0 : 1, qoff = (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q));
+    const Sc sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins};
+    if (qlen + 1 <= 16) return ext_dp_w1<16>(qlen, qsel, qoff, tlen, sc, w, end_bonus, zdrop, h0);
+    if (qlen + 1 <= 32) return ext_dp_w1<32>(qlen, qsel, qoff, tlen, sc, w, end_bonus, zdrop, h0);
+    return ext_dp_w1<64>(qlen, qsel, qoff, tlen, sc, w, end_bonus, zdrop, h0);
+}
+
 // one column per lane when the query fits a wave (the common case: a 100-bp read's flanks),
 // otherwise CPL columns per lane; the per-row VALU cost scales with the columns per lane
 template <int CPL>
@@ -555,8 +581,7 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     ExtRes r;
     const bool one = CPL == 1 || qlen + 1 <= 64;
     if (one)
-        r = ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
-                      Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
+        r = ext_dp_w1s(qlen, q, tlen, p, w, end_bonus, zdrop, h0);
     else if (qlen + 1 <= 128)
         r = ext_dp_w2(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
                       Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
@@ -567,8 +592,7 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     return r;
 #endif
     if (CPL == 1 || qlen + 1 <= 64)
-        return ext_dp_w1(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
-                         Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
+        return ext_dp_w1s(qlen, q, tlen, p, w, end_bonus, zdrop, h0);
     if (qlen + 1 <= 128)
         return ext_dp_w2(qlen, q == g_aln.qs ? 0 : 1, (int)(q - (q == g_aln.qs ? g_aln.qs : g_aln.q)), tlen,
                          Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
