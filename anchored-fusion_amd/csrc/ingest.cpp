@@ -14,10 +14,14 @@
 // QNAMEs of the pairs NUL-terminated in one arena with an offset per pair.
 //
 // Threads: af_fastq_next parses the two files concurrently (one thread each: zlib inflate +
-// line scan with memchr); af_fastq_export copies rows with up to `threads` threads.
+// line scan with memchr); af_fastq_export copies rows with up to `threads` threads.  BGZF
+// input (blocked gzip, as bgzip/htslib write it: each member carries its compressed size in a
+// "BC" extra field) is inflated block-parallel: batches of up to 512 blocks, threads/2 per
+// file, each block checked against its CRC32.
 #include <zlib.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -30,6 +34,11 @@ namespace {
 // A line source over gzread (zlib reads plain files as they are).
 struct Src {
     gzFile gz = nullptr;
+    FILE *fp = nullptr;            // BGZF input (read raw, inflated block-parallel)
+    int n_threads = 1;
+    std::vector<char> dec;         // BGZF: inflated bytes not yet handed to `buf`
+    size_t dec_pos = 0;
+    bool bgzf_eof = false;
     std::string path;
     std::vector<char> buf = std::vector<char>(1 << 22);
     size_t beg = 0, end = 0;
@@ -41,9 +50,32 @@ struct Src {
 
     ~Src() {
         if (gz) gzclose(gz);
+        if (fp) fclose(fp);
     }
-    bool open(const char *p) {
+    // block size of the BGZF member whose 12-byte fixed header + extra field is at h (or -1)
+    static long bgzf_bsize(const unsigned char *h, size_t n) {
+        if (n < 18 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return -1;
+        const size_t xlen = h[10] | (h[11] << 8);
+        for (size_t o = 12; o + 4 <= 12 + xlen && o + 4 <= n;) {
+            const size_t slen = h[o + 2] | (h[o + 3] << 8);
+            if (h[o] == 66 && h[o + 1] == 67 && slen == 2 && o + 6 <= n) return (long)(h[o + 4] | (h[o + 5] << 8)) + 1;
+            o += 4 + slen;
+        }
+        return -1;
+    }
+    bool open(const char *p, int threads) {
         path = p;
+        n_threads = threads > 0 ? threads : 1;
+        if (FILE *f = fopen(p, "rb")) {  // BGZF?  (the first member has the BC field)
+            unsigned char h[64];
+            const size_t n = fread(h, 1, sizeof h, f);
+            if (bgzf_bsize(h, n) > 0) {
+                rewind(f);
+                fp = f;
+                return true;
+            }
+            fclose(f);
+        }
         gz = gzopen(p, "rb");
         if (!gz) {
             err = "cannot open " + path;
@@ -77,17 +109,94 @@ struct Src {
             end -= beg;
             beg = 0;
             if (end == buf.size()) buf.resize(buf.size() * 2);  // a line longer than the buffer
-            const int r = gzread(gz, buf.data() + end, (unsigned)std::min<size_t>(buf.size() - end, 1u << 30));
+            const long r = read_some(buf.data() + end, std::min<size_t>(buf.size() - end, 1u << 30));
             if (r < 0) {
-                int zerr = 0;
-                const char *m = gzerror(gz, &zerr);
-                err = path + ": read error: " + (m ? m : "?");
                 eof = true;
                 return false;
             }
             if (r == 0) eof = true;
             end += (size_t)r;
         }
+    }
+    // up to cap decompressed bytes into dst; 0 at the end of input, -1 on error (err set)
+    long read_some(char *dst, size_t cap) {
+        if (!fp) {
+            const int r = gzread(gz, dst, (unsigned)cap);
+            if (r < 0) {
+                int zerr = 0;
+                const char *m = gzerror(gz, &zerr);
+                err = path + ": read error: " + (m ? m : "?");
+            }
+            return r;
+        }
+        while (dec_pos == dec.size() && !bgzf_eof)  // (a batch may hold only empty blocks)
+            if (!bgzf_batch()) return -1;
+        const size_t k = std::min(cap, dec.size() - dec_pos);
+        memcpy(dst, dec.data() + dec_pos, k);
+        dec_pos += k;
+        return (long)k;
+    }
+    // reads up to 512 BGZF blocks and inflates them in parallel into `dec`
+    bool bgzf_batch() {
+        std::vector<std::vector<unsigned char>> blocks;
+        std::vector<size_t> out_off{0};
+        while (blocks.size() < 512) {
+            unsigned char h[18];
+            const size_t n = fread(h, 1, 12, fp);
+            if (n == 0) {
+                bgzf_eof = true;
+                break;
+            }
+            if (n < 12) return fail_bgzf("truncated BGZF block header");
+            const size_t xlen = h[10] | (h[11] << 8);
+            std::vector<unsigned char> b(12 + xlen);
+            memcpy(b.data(), h, 12);
+            if (fread(b.data() + 12, 1, xlen, fp) != xlen) return fail_bgzf("truncated BGZF extra field");
+            const long bsize = bgzf_bsize(b.data(), b.size());
+            if (bsize < (long)(12 + xlen + 8)) return fail_bgzf("gzip member without a BGZF size (mixed input?)");
+            b.resize((size_t)bsize);
+            if (fread(b.data() + 12 + xlen, 1, (size_t)bsize - 12 - xlen, fp) != (size_t)bsize - 12 - xlen)
+                return fail_bgzf("truncated BGZF block");
+            const unsigned char *t = b.data() + bsize - 4;
+            const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+            out_off.push_back(out_off.back() + isize);
+            blocks.push_back(std::move(b));
+        }
+        dec.assign(out_off.back(), 0);
+        dec_pos = 0;
+        std::vector<int> bad(blocks.size(), 0);
+        auto work = [&](size_t t0, size_t step) {
+            for (size_t i = t0; i < blocks.size(); i += step) {
+                const std::vector<unsigned char> &b = blocks[i];
+                const size_t xlen = b[10] | (b[11] << 8), cstart = 12 + xlen, clen = b.size() - cstart - 8;
+                const size_t isize = out_off[i + 1] - out_off[i];
+                z_stream z{};
+                if (inflateInit2(&z, -15) != Z_OK) { bad[i] = 1; continue; }
+                z.next_in = const_cast<unsigned char *>(b.data() + cstart);
+                z.avail_in = (uInt)clen;
+                z.next_out = reinterpret_cast<unsigned char *>(dec.data() + out_off[i]);
+                z.avail_out = (uInt)isize;
+                const int rc = inflate(&z, Z_FINISH);
+                inflateEnd(&z);
+                const unsigned char *c = b.data() + b.size() - 8;
+                const uLong crc = (uLong)c[0] | ((uLong)c[1] << 8) | ((uLong)c[2] << 16) | ((uLong)c[3] << 24);
+                if (rc != Z_STREAM_END || z.total_out != isize ||
+                    crc32(0L, reinterpret_cast<const Bytef *>(dec.data() + out_off[i]), (uInt)isize) != crc)
+                    bad[i] = 1;
+            }
+        };
+        const size_t T = std::min<size_t>((size_t)n_threads, std::max<size_t>(1, blocks.size()));
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < T; ++k) th.emplace_back(work, k, T);
+        work(0, T);
+        for (auto &x : th) x.join();
+        for (size_t i = 0; i < blocks.size(); ++i)
+            if (bad[i]) return fail_bgzf("corrupt BGZF block (inflate or CRC32)");
+        return true;
+    }
+    bool fail_bgzf(const char *what) {
+        err = path + ": " + what;
+        return false;
     }
     void push_back(const char *p, size_t n) {
         pending.assign(p, n);
@@ -185,7 +294,8 @@ int af_fastq_open(const char *fq1, const char *fq2, int threads, af_fastq **out)
     af_fastq *f = new (std::nothrow) af_fastq;
     if (!f) return AF_E_NOMEM;
     f->threads = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (!f->src[0].open(fq1) || !f->src[1].open(fq2)) {
+    const int per_file = std::max(1, f->threads / 2);
+    if (!f->src[0].open(fq1, per_file) || !f->src[1].open(fq2, per_file)) {
         f->err = f->src[0].err.empty() ? f->src[1].err : f->src[0].err;
         *out = f;  // the handle carries the message; the caller closes it
         return AF_E_INVALID;

@@ -45,20 +45,37 @@ def fastq_bytes(mate):
     return out.tobytes()
 
 
+def write_bgzf(p, data, block=65280):
+    import struct
+    import zlib
+    with open(p, "wb") as fh:
+        for o in list(range(0, len(data), block)) + [len(data)]:
+            chunk = data[o:o + block] if o < len(data) else b""
+            c = zlib.compressobj(1, zlib.DEFLATED, -15)
+            cdata = c.compress(chunk) + c.flush()
+            fh.write(b"\x1f\x8b\x08\x04\0\0\0\0\0\xff" + struct.pack("<H", 6) + b"BC" +
+                     struct.pack("<HH", 2, 12 + 6 + len(cdata) + 8 - 1) + cdata +
+                     struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+            if o >= len(data):
+                break
+
+
 paths = {}
-for gz in (False, True):
+for kind in ("plain", "gzip-1", "bgzf-1"):
     ps = []
     for m in (0, 1):
-        p = os.path.join(d, f"r_{m + 1}.fq" + (".gz" if gz else ""))
+        p = os.path.join(d, f"r_{kind}_{m + 1}.fq" + ("" if kind == "plain" else ".gz"))
         data = fastq_bytes(m)
-        if gz:
+        if kind == "gzip-1":
             with gzip.open(p, "wb", compresslevel=1) as fh:
                 fh.write(data)
+        elif kind == "bgzf-1":
+            write_bgzf(p, data)
         else:
             with open(p, "wb") as fh:
                 fh.write(data)
         ps.append(p)
-    paths[gz] = ps
+    paths[kind] = ps
 for gz, (p1, p2) in paths.items():
     afio.read_pairs(p1, p2)  # warm the page cache
     t0 = time.perf_counter()
@@ -66,7 +83,7 @@ for gz, (p1, p2) in paths.items():
     dt = time.perf_counter() - t0
     assert (got == reads).all() and names[n - 1] == f"p{n - 1}"
     size = os.path.getsize(p1) + os.path.getsize(p2)
-    print(f"{'gzip-1' if gz else 'plain '}: {n} pairs in {dt:.2f} s = {n / dt / 1e6:.2f} M pairs/s "
+    print(f"{gz}: {n} pairs in {dt:.2f} s = {n / dt / 1e6:.2f} M pairs/s "
           f"({size / dt / 1e6:.0f} MB/s of input files)")
 for ps in paths.values():
     for p in ps:

@@ -113,3 +113,52 @@ def test_malformed_pairs_raise(tmp_path, t1, t2, msg):
 def test_missing_file_raises(tmp_path):
     with pytest.raises(Exception, match="cannot open"):
         afio.read_pairs(str(tmp_path / "nope_1.fq"), str(tmp_path / "nope_2.fq"))
+
+
+def _write_bgzf(path, text, block=60000, level=6):
+    """BGZF as bgzip writes it: raw-deflate members of <= 64 KiB input with a 'BC' extra
+    subfield holding the member size - 1, then the empty end-of-file member."""
+    import struct
+    import zlib
+    data = text.encode()
+    with open(path, "wb") as fh:
+        for o in list(range(0, len(data), block)) + [len(data)]:
+            chunk = data[o:o + block] if o < len(data) else b""
+            c = zlib.compressobj(level, zlib.DEFLATED, -15)
+            cdata = c.compress(chunk) + c.flush()
+            bsize = 12 + 6 + len(cdata) + 8
+            fh.write(b"\x1f\x8b\x08\x04" + b"\0\0\0\0" + b"\0\xff" + struct.pack("<H", 6) + b"BC" +
+                     struct.pack("<HH", 2, bsize - 1) + cdata +
+                     struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+            if o >= len(data):
+                break
+    return str(path)
+
+
+def test_bgzf_block_parallel(tmp_path):
+    # BGZF input takes the block-parallel inflate path; records identical to the plain files,
+    # including records that straddle block boundaries (small blocks force many of them)
+    rng = np.random.default_rng(3)
+    recs1 = [(f"b{i}/1", "".join(rng.choice(list("ACGTN"), int(rng.integers(1, 151))))) for i in range(5000)]
+    recs2 = [(f"b{i}/2", "".join(rng.choice(list("ACGT"), 100))) for i in range(5000)]
+    t1, t2 = _fq(recs1), _fq(recs2)
+    plain = afio.read_pairs(_write(tmp_path / "p_1.fq", t1), _write(tmp_path / "p_2.fq", t2))
+    for block in (997, 65280):
+        b1 = _write_bgzf(tmp_path / f"b{block}_1.fq.gz", t1, block)
+        b2 = _write_bgzf(tmp_path / f"b{block}_2.fq.gz", t2, block)
+        assert gzip.open(b1).read().decode() == t1  # a valid multi-member gzip file as well
+        for threads in (1, 8):
+            names, reads, lens = afio.read_pairs(b1, b2, threads=threads)
+            assert list(names) == list(plain[0])
+            assert (reads == plain[1]).all() and (lens == plain[2]).all()
+
+
+def test_bgzf_corrupt_block_raises(tmp_path):
+    t = _fq([(f"c{i}", "ACGT" * 20) for i in range(3000)])
+    b1 = _write_bgzf(tmp_path / "c_1.fq.gz", t, 4000)
+    raw = bytearray(open(b1, "rb").read())
+    raw[len(raw) // 2] ^= 0x55  # inside some member's deflate data
+    open(b1, "wb").write(bytes(raw))
+    b2 = _write_bgzf(tmp_path / "c_2.fq.gz", t, 4000)
+    with pytest.raises(ValueError, match="BGZF"):
+        afio.read_pairs(b1, b2)
