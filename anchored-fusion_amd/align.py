@@ -200,16 +200,15 @@ def partition(res: AlignResult):
     each in realign.bam order.
     """
     flag = res.flag
-    n = len(flag)
-    pos = res.pos.astype(np.int64)
-    rev = ((flag & 0x10) != 0).astype(np.int64)
-    placed = pos >= 0
-    # samtools coordinate order: placed records by (pos, is_rev), then unplaced; stable
-    key = np.where(placed, pos * 2 + rev, np.int64(1) << 62)
-    order = np.argsort(key, kind="stable")
+    pos = res.pos
+    # samtools coordinate order: placed records by (pos, is_rev), ties in input order, then the
+    # unplaced ones.  Every record the three filters keep is placed (a mapped read, or an
+    # unmapped read carrying its mapped mate's position), so only the placed few % are sorted.
+    placed = np.nonzero(pos >= 0)[0]
+    key = pos[placed].astype(np.int64) * 2 + ((flag[placed] & 0x10) != 0)
+    order = placed[np.argsort(key, kind="stable")]
     f = flag[order]
     tmp1 = order[((f & 0x8) != 0) & ((f & 260) == 0)]
     tmp2 = order[((f & 0x4) != 0) & ((f & 264) == 0)]
     anchored = order[(f & 772) == 0]
-    del n
     return tmp1, tmp2, anchored

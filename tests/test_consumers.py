@@ -136,3 +136,43 @@ def test_partner_chain():
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "partner_chain.py")],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_partition_matches_full_sort():
+    # align.partition (S3, AF:183-194) sorts only placed records; check it against sorting every
+    # record by samtools' key (placed by (pos, strand), ties in input order, unplaced last)
+    import numpy as np
+    from anchored_fusion_amd.align import AlignResult, partition
+    rng = np.random.default_rng(5)
+    n = 20000
+    flag = np.zeros(n, np.int32)
+    pos = np.full(n, -1, np.int32)
+    for p in range(n // 2):
+        m = rng.random(2) < 0.3
+        rv = rng.random(2) < 0.5
+        x = rng.integers(0, 300, 2)
+        for k in (0, 1):
+            r = 2 * p + k
+            f = 0x1 | (0x40 if k == 0 else 0x80)
+            if m[k]:
+                f |= 0x10 if rv[k] else 0
+                pos[r] = x[k]
+            else:
+                f |= 0x4
+            if not m[1 - k]:
+                f |= 0x8
+            elif rv[1 - k]:
+                f |= 0x20
+            flag[r] = f
+        for k in (0, 1):  # unmapped mate of a mapped read: the mate's position
+            if not m[k] and m[1 - k]:
+                pos[2 * p + k] = pos[2 * p + 1 - k]
+    z = np.zeros(n, np.int32)
+    res = AlignResult(flag, pos, z, z, np.zeros((n, 32), np.uint32), z)
+    key = np.where(pos >= 0, pos.astype(np.int64) * 2 + ((flag & 0x10) != 0), np.int64(1) << 62)
+    order = np.argsort(key, kind="stable")
+    f = flag[order]
+    want = (order[((f & 0x8) != 0) & ((f & 260) == 0)], order[((f & 0x4) != 0) & ((f & 264) == 0)],
+            order[(f & 772) == 0])
+    for a, b in zip(partition(res), want):
+        assert np.array_equal(a, b)
