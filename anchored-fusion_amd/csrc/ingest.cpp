@@ -14,15 +14,19 @@
 // QNAMEs of the pairs NUL-terminated in one arena with an offset per pair.
 //
 // Threads: af_fastq_next parses the two files concurrently (one thread each: zlib inflate +
-// line scan with memchr); af_fastq_export copies rows with up to `threads` threads.  BGZF
+// line scan with memchr, the decompression running ahead on a reader thread of its own, up to
+// three 8 MiB chunks in flight); af_fastq_export copies rows with up to `threads` threads.  BGZF
 // input (blocked gzip, as bgzip/htslib write it: each member carries its compressed size in a
 // "BC" extra field) is inflated block-parallel: batches of up to 512 blocks, threads/2 per
 // file, each block checked against its CRC32.
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -47,10 +51,61 @@ struct Src {
     std::string pending;  // one pushed-back line
     bool has_pending = false;
     std::string err;
+    // reader thread: decompressed chunks queued ahead of the line scan
+    std::thread reader;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::vector<char>> chunks;
+    size_t chunk_pos = 0;
+    bool r_done = false, r_error = false, r_stop = false;
 
     ~Src() {
+        if (reader.joinable()) {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                r_stop = true;
+            }
+            cv.notify_all();
+            reader.join();
+        }
         if (gz) gzclose(gz);
         if (fp) fclose(fp);
+    }
+    void start_reader() {
+        reader = std::thread([this] {
+            for (;;) {
+                std::vector<char> c(8u << 20);
+                const long r = read_some(c.data(), c.size());
+                std::unique_lock<std::mutex> g(mu);
+                if (r <= 0) {
+                    r_error = r < 0;
+                    r_done = true;
+                    cv.notify_all();
+                    return;
+                }
+                c.resize((size_t)r);
+                chunks.push_back(std::move(c));
+                cv.notify_all();
+                cv.wait(g, [this] { return chunks.size() < 3 || r_stop; });
+                if (r_stop) return;
+            }
+        });
+    }
+    // the next decompressed bytes from the reader thread (0 at the end, -1 on error)
+    long pull(char *dst, size_t cap) {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [this] { return !chunks.empty() || r_done; });
+        if (chunks.empty()) return r_error ? -1 : 0;
+        std::vector<char> &c = chunks.front();
+        const size_t k = std::min(cap, c.size() - chunk_pos);
+        memcpy(dst, c.data() + chunk_pos, k);
+        chunk_pos += k;
+        if (chunk_pos == c.size()) {
+            chunks.pop_front();
+            chunk_pos = 0;
+            cv.notify_all();
+        }
+        return (long)k;
     }
     // block size of the BGZF member whose 12-byte fixed header + extra field is at h (or -1)
     static long bgzf_bsize(const unsigned char *h, size_t n) {
@@ -72,6 +127,7 @@ struct Src {
             if (bgzf_bsize(h, n) > 0) {
                 rewind(f);
                 fp = f;
+                start_reader();
                 return true;
             }
             fclose(f);
@@ -82,6 +138,8 @@ struct Src {
             return false;
         }
         gzbuffer(gz, 1 << 20);
+        char c0;  // plain text reads as fast as it is scanned: no reader thread for it
+        if (gzread(gz, &c0, 0) >= 0 && !gzdirect(gz)) start_reader();
         return true;
     }
     // Next line as [p, p + n), terminator and a trailing '\r' removed; valid until the next
@@ -109,7 +167,8 @@ struct Src {
             end -= beg;
             beg = 0;
             if (end == buf.size()) buf.resize(buf.size() * 2);  // a line longer than the buffer
-            const long r = read_some(buf.data() + end, std::min<size_t>(buf.size() - end, 1u << 30));
+            const size_t cap = std::min<size_t>(buf.size() - end, 1u << 30);
+            const long r = reader.joinable() ? pull(buf.data() + end, cap) : read_some(buf.data() + end, cap);
             if (r < 0) {
                 eof = true;
                 return false;
