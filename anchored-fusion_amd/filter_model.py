@@ -25,11 +25,14 @@ the same outputs in eval mode and, under the same torch seed, in train mode; and
 own `Test_model` (file in, scores out, seeded before the network is built) gives the scores
 `score_test_file` gives under the same seed, which also pins the parameter-creation order.
 
-Not built: `get_test_reads` (fn:1642-1721), the input-window builder.  It parses
-`bedtools getfasta -s -nameOnly` headers with `line[1:-3]`, whose result depends on the
-bedtools version's header format (with a "(+)" suffix the flank tag never equals 'left', and
-every flank base lands in the right-hand sequence); the pipeline therefore runs as
-`--not_filter_false_positive`.
+Not built: `get_test_reads` (fn:1642-1721), the input-window builder.  It reads the flank tag of
+each `bedtools getfasta -s -nameOnly` header as `line[1:-3].split('$')[2]`, which cuts "ft\n"
+(">0$+$left\n" gives 'le') or "+)\n" (">0$+$left(+)\n" gives 'left(') and so never equals
+'left': every flank base, left and right of the partner breakpoint (about 200), lands in the
+right-hand sequence.  MS windows, and SM windows on the '-' strand, then come out about 301
+positions long instead of the 201 the model is trained on, so `Test_model` cannot load a
+trained `model.pt` (position table 22 vs 33 rows), and a file mixing both lengths is ragged
+for `read_lines`.  The pipeline therefore runs as `--not_filter_false_positive`.
 """
 import os
 
