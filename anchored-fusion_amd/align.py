@@ -181,6 +181,75 @@ class AnchorAligner:
         return int(_lib.lib().af_last_candidates(self._ctx))
 
 
+class AlignerGroup:
+    """Several device-resident batches in flight on one GPU: one AnchorAligner context and one
+    stream per batch slot.  ``run_device`` enqueues a group of batches so that their seed-filter
+    launches (K1) run back to back and their alignment launches (K2 + K3) then run on all the
+    slots' streams at once (see run_device): K2 is a persistent kernel whose waves leave one by one as the
+    candidate queue drains, and the next batch's K2 waves take the CUs they free, so one K2's
+    tail overlaps the next K2's body instead of idling the chip.  K1 (a whole CU's LDS per
+    workgroup) cannot share a CU with K2 waves, so the next group's K1s wait for this group's
+    K2s.  Records are those of ``AnchorAligner.align_pairs_device`` per batch."""
+
+    def __init__(self, anchor: bytes, device: int = 0, inflight: int = 4, params=None):
+        import torch
+        if inflight < 1:
+            raise ValueError("inflight must be >= 1")
+        self.aligners = [AnchorAligner(anchor, device=device, params=params) for _ in range(inflight)]
+        self.streams = [torch.cuda.Stream(torch.device("cuda", device)) for _ in range(inflight)]
+        self.inflight = inflight
+
+    def close(self):
+        for a in self.aligners:
+            a.close()
+
+    def run_device(self, batches, events=None, wait=None):
+        """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t]) with
+        every tensor on the device.  Enqueues them and returns without synchronising.
+
+        All K1s go to slot 0's stream, back to back (no cross-queue wait between them); batch
+        j's K2 + K3 go to slot j's stream after one wait for the last K1.  wait (optional):
+        events slot 0's stream waits for first (pass the previous group's return value when
+        buffers or slots are reused).  events (optional): two timing events, recorded on slot
+        0's stream before the first K1 and after the last.  Returns the events marking each
+        batch's completion."""
+        import torch
+        if len(batches) > self.inflight:
+            raise ValueError(f"{len(batches)} batches for {self.inflight} slots")
+        s0 = self.streams[0]
+        for e in wait or ():
+            s0.wait_event(e)
+        if events is not None:
+            events[0].record(s0)
+        for j, b in enumerate(batches):
+            reads_t, n_pairs, stride, out_t = b[:4]
+            lens_t = b[4] if len(b) > 4 else None
+            self.aligners[j].seed_filter_device(reads_t, 2 * n_pairs, stride, out_t["hits"], lens_t, stream=s0)
+        if events is not None:
+            events[1].record(s0)
+        k1_done = torch.cuda.Event()
+        k1_done.record(s0)
+        done = []
+        for j, b in enumerate(batches):
+            s = self.streams[j]
+            if j:
+                s.wait_event(k1_done)
+            reads_t, n_pairs, stride, out_t = b[:4]
+            lens_t = b[4] if len(b) > 4 else None
+            self.aligners[j].align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s)
+            e = torch.cuda.Event()
+            e.record(s)
+            done.append(e)
+        return done
+
+    def join(self, done, stream=None):
+        """Makes ``stream`` (default: torch's current stream) wait for a group's events."""
+        import torch
+        s = stream or torch.cuda.current_stream()
+        for e in done:
+            s.wait_event(e)
+
+
 def _stream_handle(stream):
     if stream is None:
         return None

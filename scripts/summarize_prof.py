@@ -23,7 +23,7 @@ def short(name):
     for k, v in SHORT.items():
         if k + "<" in name or k + "(" in name:
             return v
-    return name.split("(")[0][:60]
+    return name.replace("(anonymous namespace)::", "").split("(")[0][:60]
 
 
 stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)

@@ -108,6 +108,38 @@ def test_device_api_matches_host_api(aligner, anchor):
     assert_records_equal(got, host, reads)
 
 
+def test_aligner_group_matches_oracle(anchor, oidx):
+    """AlignerGroup (the bench's schedule): three different batches in flight, two groups in a
+    row over reused buffers, every batch's records equal to the oracle's; ragged lengths too."""
+    import torch
+    from anchored_fusion_amd.align import AlignerGroup
+    dev = torch.device("cuda:0")
+    cases = [synthetic_pairs(anchor, 3000, 100, seed=41 + k)[0] for k in range(3)]
+    rg, rl = ragged(*synthetic_pairs(anchor, 2000, 150, seed=44)[:1], seed=45)
+    grp = AlignerGroup(anchor, device=0, inflight=3)
+    try:
+        def outs(nr):
+            o = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+            o["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
+            return o
+        done = None
+        for group in ([(c, None) for c in cases], [(cases[2], None), (rg, rl)]):
+            bufs = [outs(r.shape[0]) for r, _ in group]
+            batch = []
+            for (r, ln), o in zip(group, bufs):
+                b = (torch.from_numpy(r).to(dev), r.shape[0] // 2, r.shape[1], o)
+                batch.append(b if ln is None else b + (torch.from_numpy(ln).to(dev),))
+            done = grp.run_device(batch, wait=done)
+            grp.join(done)
+            torch.cuda.synchronize()
+            for (r, ln), o in zip(group, bufs):
+                got = {k: v.cpu().numpy() for k, v in o.items()}
+                got["cigar"] = got["cigar"].view(np.uint32)
+                assert_records_equal(got, oidx.align_pairs(r, ln, threads=8), r)
+    finally:
+        grp.close()
+
+
 def test_full_size_properties(aligner, anchor):
     """Config-2 size (1 M pairs x 2x100): properties that do not need the oracle."""
     import torch
