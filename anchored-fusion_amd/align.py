@@ -177,6 +177,24 @@ class AnchorAligner:
             self._ctx, self._idx, reads_t.data_ptr(), int(n_reads), int(stride),
             None if lens_t is None else lens_t.data_ptr(), hits_t.data_ptr(), sh), "af_seed_filter_device")
 
+    def split_tails_device(self, reads_t, stride, out_t, tails_t, tail_lens_t, tail_read_t, n_tails_t,
+                           min_clip=20, lens_t=None, stream=None):
+        """af_split_tails_device over the records in out_t (rows of reads_t): the soft-clipped
+        tails of split reads (CIGAR exactly M+S / S+M, clip >= min_clip) into tails_t
+        (uint8 [cap, stride]), their lengths and read rows; *n_tails_t = number of split reads
+        (may exceed cap).  Asynchronous on stream; tail order varies between runs."""
+        o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        cap = int(tails_t.shape[0])
+        if tail_lens_t.numel() < cap or tail_read_t.numel() < cap:
+            raise ValueError("tail_lens_t / tail_read_t hold fewer than cap entries")
+        if tails_t.shape[1] != stride:
+            raise ValueError("tails_t rows must be `stride` bytes")
+        _lib.check(self._ctx, _lib.lib().af_split_tails_device(
+            self._ctx, reads_t.data_ptr(), int(reads_t.shape[0]), int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(o), int(min_clip), cap, tails_t.data_ptr(),
+            tail_lens_t.data_ptr(), tail_read_t.data_ptr(), n_tails_t.data_ptr(), _stream_handle(stream)),
+            "af_split_tails_device")
+
     def last_candidates(self):
         return int(_lib.lib().af_last_candidates(self._ctx))
 

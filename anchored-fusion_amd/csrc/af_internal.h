@@ -116,6 +116,10 @@ hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *
 hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
                            const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
                            int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
+hipError_t af_launch_split_tails(const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
+                                 const af_aln_out &out, int32_t min_clip, int64_t cap, uint8_t *tails,
+                                 int32_t *tail_lens, int32_t *tail_read, int32_t *n_tails, hipStream_t s);
+hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);
 size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();
 hipError_t af_build_genome_index(const uint8_t *seq, int64_t n, uint8_t *D, uint32_t *D2, uint32_t *Dn,

@@ -554,4 +554,42 @@ int af_place(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_qu
     return AF_OK;
 }
 
+int af_place_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
+                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_params *p, int32_t max_hits,
+                    af_hit *d_hits, int32_t *d_n_hits, void *stream) {
+    if (!c || !ix || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_hits || !d_n_hits)))
+        return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_params(c, p);
+    if (rc) return rc;
+    if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    if (max_hits < 1 || max_hits > 16) return fail(c, AF_E_INVALID, "max_hits must be in [1, 16]");
+    if (cap_queries == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_zscratch(c))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
+    HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
+    HIPCHK(c, af_launch_place(ix->dev, d_queries, c->ctrl + AF_CTRL_PLACE_N, stride, d_lens, *p,
+                              c->ctrl + AF_CTRL_PLACE_HEADS, c->zscratch, c->n_slots, d_hits, d_n_hits, max_hits, s));
+    return AF_OK;
+}
+
+int af_split_tails_device(af_ctx *c, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
+                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t cap,
+                          uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read, int32_t *d_n_tails,
+                          void *stream) {
+    if (!c || !d_out || !d_n_tails || (n_reads > 0 && !d_reads) || (cap > 0 && (!d_tails || !d_tail_lens || !d_tail_read)))
+        return fail(c, AF_E_INVALID, "null argument");
+    if (n_reads < 0 || n_reads > (1LL << 31) - 1) return fail(c, AF_E_INVALID, "n_reads out of range");
+    if (cap < 0) return fail(c, AF_E_INVALID, "cap < 0");
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    if (n_reads > 0 && (!d_out->flag || !d_out->n_cigar || !d_out->cigar))
+        return fail(c, AF_E_INVALID, "d_out needs flag, n_cigar and cigar");
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, af_launch_split_tails(d_reads, n_reads, stride, d_lens, *d_out, min_clip < 1 ? 1 : min_clip, cap,
+                                    d_tails, d_tail_lens, d_tail_read, d_n_tails, (hipStream_t)stream));
+    return AF_OK;
+}
+
 }  // extern "C"

@@ -15,6 +15,9 @@
  *   af_align_candidates_device <- the extension/CIGAR/pairing pass of the same call
  *   af_place              <- the genome `bwa mem` calls (AF:188, functions.py:716) and the BLAT
  *                            calls (functions.py:341, 530, 1007, 1071, 1122, 1244)
+ *   af_place_device       <- same, device-resident buffers and query count, on a HIP stream
+ *   af_split_tails_device <- the split-read selection + query FASTA of the partner search
+ *                            (functions.py:705-716, 1001-1005), from device-resident records
  *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
@@ -133,6 +136,27 @@ int af_index_build_genome(af_ctx *ctx, const char *seq, int64_t len, af_index **
  * `bwa mem` calls (AF:188, fn:716). */
 int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,
              const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits);
+/* af_place with device buffers, asynchronous on `stream`: the query count is read on the
+ * device from *d_n_queries (clamped to cap_queries, the rows d_queries / d_lens / d_n_hits hold;
+ * d_hits holds cap_queries * max_hits), so it can follow af_split_tails_device without a host
+ * round trip.  d_lens may be NULL (every query `stride` long). */
+int af_place_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
+                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_params *p, int32_t max_hits,
+                    af_hit *d_hits, int32_t *d_n_hits, void *stream);
+/* Split-read tails on the device, from the records of af_align_pairs_device /
+ * af_align_candidates_device (d_out; device buffers, asynchronous on `stream`).  A split read is
+ * a mapped read whose CIGAR is exactly M + S or S + M (deal_cigar's two-operation case,
+ * functions.py:713) with a clip of at least min_clip bases; its tail is the clipped part of
+ * SEQ in SAM orientation (the read reverse-complemented for 0x10), the query of the partner
+ * search (functions.py:1001-1005).  Writes up to cap tails: row t of d_tails (`stride` bytes,
+ * bytes past d_tail_lens[t] undefined), d_tail_lens[t], d_tail_read[t] = the read's row; the
+ * number of split reads (which may exceed cap) goes to *d_n_tails.  Tail order varies between
+ * runs; d_tail_read identifies them.  Replaces the split-read selection and FASTA writing of
+ * functions.py:705-716 and fn:1001-1005. */
+int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
+                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t cap,
+                          uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read, int32_t *d_n_tails,
+                          void *stream);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as

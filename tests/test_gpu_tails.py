@@ -1,0 +1,139 @@
+"""Device-side partner placement (af_split_tails_device -> af_place_device), the bench's
+S2 + placement step: the tails equal a host restatement of the split-read rule over the same
+records (deal_cigar's two-operation M/S case, functions.py:713; SAM-orientation clipped part,
+fn:1001-1005), and the device placements equal af_place's host API on the same tails, which
+tests/test_gpu_place.py pins against the oracle.  Integer work: bit-exact."""
+import numpy as np
+import pytest
+
+from cases import ragged, synthetic_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def aligner(anchor):
+    from anchored_fusion_amd.align import AnchorAligner
+    a = AnchorAligner(anchor, device=0)
+    yield a
+    a.close()
+
+
+_COMP = bytes.maketrans(b"ACGTNacgtn", b"TGCANTGCAN")
+
+
+def host_tails(reads, lens, res, min_clip):
+    """{read row: tail bytes} from host records (AlignResult)."""
+    out = {}
+    for r in np.nonzero(res.mapped())[0]:
+        ops = res.cigar_ops(r)
+        if len(ops) != 2 or sorted(op for _, op in ops) != ["M", "S"]:
+            continue
+        n = int(lens[r]) if lens is not None else reads.shape[1]
+        clip = ops[0][0] if ops[0][1] == "S" else ops[1][0]
+        if clip < min_clip or clip > n:
+            continue
+        seq = reads[r, :n].tobytes()
+        if res.flag[r] & 0x10:
+            seq = seq[::-1].translate(_COMP)
+        out[int(r)] = seq[:clip] if ops[0][1] == "S" else seq[n - clip:]
+    return out
+
+
+def _device_records(aligner, reads, lens, dev):
+    import torch
+    nr = reads.shape[0]
+    rt = torch.from_numpy(reads).to(dev)
+    lt = None if lens is None else torch.from_numpy(lens).to(dev)
+    out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+    out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
+    aligner.align_pairs_device(rt, nr // 2, reads.shape[1], out, lens_t=lt)
+    return rt, lt, out
+
+
+def _tails(aligner, rt, lt, out, stride, cap, min_clip, dev):
+    import torch
+    tails = torch.zeros((cap, stride), dtype=torch.uint8, device=dev)
+    tl = torch.zeros(cap, dtype=torch.int32, device=dev)
+    tr = torch.zeros(cap, dtype=torch.int32, device=dev)
+    nt = torch.zeros(1, dtype=torch.int32, device=dev)
+    aligner.split_tails_device(rt, stride, out, tails, tl, tr, nt, min_clip=min_clip, lens_t=lt)
+    return tails, tl, tr, nt
+
+
+@pytest.mark.parametrize("ragged_lens", [False, True])
+def test_split_tails_match_host_rule(aligner, anchor, ragged_lens):
+    import torch
+    dev = torch.device("cuda:0")
+    reads, _, _ = synthetic_pairs(anchor, 4000, 100, seed=51)
+    lens = None
+    if ragged_lens:
+        reads, lens = ragged(reads, seed=52)
+    res = aligner.align_pairs(reads, lens)
+    want = host_tails(reads, lens, res, 20)
+    assert len(want) > (5 if ragged_lens else 50)  # the fusion-rich synthetic set has split reads
+    rt, lt, out = _device_records(aligner, reads, lens, dev)
+    tails, tl, tr, nt = _tails(aligner, rt, lt, out, reads.shape[1], 2 * len(want), 20, dev)
+    torch.cuda.synchronize()
+    n = int(nt.item())
+    assert n == len(want)
+    t, ln, rd = tails.cpu().numpy(), tl.cpu().numpy(), tr.cpu().numpy()
+    got = {int(rd[i]): t[i, :ln[i]].tobytes() for i in range(n)}
+    assert got == want
+
+
+def test_split_tails_capacity(aligner, anchor):
+    """cap below the number of split reads: the count is still exact, only cap rows written."""
+    import torch
+    dev = torch.device("cuda:0")
+    reads, _, _ = synthetic_pairs(anchor, 2000, 100, seed=53)
+    res = aligner.align_pairs(reads)
+    want = host_tails(reads, None, res, 20)
+    rt, lt, out = _device_records(aligner, reads, None, dev)
+    cap = max(1, len(want) // 3)
+    tails, tl, tr, nt = _tails(aligner, rt, lt, out, reads.shape[1], cap, 20, dev)
+    torch.cuda.synchronize()
+    assert int(nt.item()) == len(want)
+    t, ln, rd = tails.cpu().numpy(), tl.cpu().numpy(), tr.cpu().numpy()
+    for i in range(cap):
+        assert t[i, :ln[i]].tobytes() == want[int(rd[i])]
+
+
+def test_place_device_matches_host_api(aligner, anchor):
+    import torch
+    from anchored_fusion_amd import place
+    dev = torch.device("cuda:0")
+    reads, _, world = synthetic_pairs(anchor, 4000, 100, seed=54)
+    rng = np.random.default_rng(55)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    ctgs = [("anchor", anchor.decode())] + [(f"p{k}", s.decode()) for k, s in enumerate(world["partners"])]
+    ctgs += [(f"r{k}", acgt[rng.integers(0, 4, 200_000)].tobytes().decode()) for k in range(3)]
+    ref = place.Reference(ctgs)
+    try:
+        rt, lt, out = _device_records(aligner, reads, None, dev)
+        cap = 4096
+        tails, tl, tr, nt = _tails(aligner, rt, lt, out, reads.shape[1], cap, 20, dev)
+        hits_t = torch.zeros(cap * 16 * place.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        nh_t = torch.zeros(cap, dtype=torch.int32, device=dev)
+        ref.place_device(tails, nt, reads.shape[1], hits_t, nh_t, lens_t=tl)
+        torch.cuda.synchronize()
+        n = int(nt.item())
+        assert 20 < n <= cap
+        t, ln = tails.cpu().numpy(), tl.cpu().numpy()
+        queries = [t[i, :ln[i]].tobytes() for i in range(n)]
+        hits_h, nh_h = ref.raw_hits(queries)
+        hits_d = hits_t.cpu().numpy().view(place.HIT_DTYPE).reshape(cap, 16)
+        nh_d = nh_t.cpu().numpy()
+        assert np.array_equal(nh_d[:n], nh_h)
+        for q in range(n):
+            for k in range(nh_h[q]):
+                a, b = hits_d[q, k], hits_h[q, k]
+                for f in ("flag", "score", "q_start", "q_end", "q_size", "matches", "n_cigar", "t_start", "t_end"):
+                    assert a[f] == b[f], (q, k, f)
+                assert np.array_equal(a["cigar"][:a["n_cigar"]], b["cigar"][:b["n_cigar"]])
+        # placed tails (score >= T = 30: tails of 30+ bases) land on a partner or the anchor
+        placed = [q for q in range(n) if nh_h[q] > 0]
+        on = sum(1 for q in placed if ref.names[ref.locate(hits_h[q, 0]["t_start"], hits_h[q, 0]["t_end"])[0]][0] in "ap")
+        assert len(placed) > 10 and on == len(placed)
+    finally:
+        ref.close()
