@@ -13,6 +13,8 @@
 #ifndef AF_K2_WPS
 #define AF_K2_WPS 6             // k_align waves per SIMD (launch bound; persistent slots = 4 x this per CU)
 #endif
+#define AF_RESEED_STEP 4          // af_place: MEM minimum length step while a query has > max_mems MEMs
+#define AF_RESEED_MAX 64          // ... up to this minimum length (then the query is flagged n_hits = -1)
 #define AF_CPL 6                // DP columns per lane: 6*64 = 384 >= AF_MAX_READ+1
 #define AF_ZCAP 12288           // LDS traceback bytes per wave; larger DPs use global scratch
 #define AF_TMAX (AF_MAX_READ + 2 * 100 * 4 + 64)  // max target window held in LDS

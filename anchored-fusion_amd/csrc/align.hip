@@ -944,6 +944,11 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
         }
         wave_sync();
         // ---- 1. MEMs ------------------------------------------------------------------
+        // placement (MULTI) re-seeds with the minimum MEM length raised by AF_RESEED_STEP while
+        // a query has more than max_mems MEMs (random 16-mer hits on a genome-scale reference)
+        int seed_min = p.min_seed_len;
+        int nm_total;
+        for (;;) {
         for (int qb = lane; qb + AF_K <= l; qb += 64) {
             const int wq = qb >> 4, sq = qb & 15;
             const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
@@ -997,15 +1002,26 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
                     len += step;
                     if (step < 16) break;
                 }
-                if (len < p.min_seed_len) continue;
+                if (len < seed_min) continue;
                 const int slot = atomicAdd(&L.misc[0], 1);
                 if (slot < MEMCAP)
                     L.mem[slot] = ((uint64_t)(1023 - len) << 50) | ((uint64_t)qb << 40) | (uint64_t)rb;
             }
         }
         wave_sync();
+        nm_total = L.misc[0];
+        if constexpr (MULTI) {
+            if (nm_total > max_mems && seed_min + AF_RESEED_STEP <= AF_RESEED_MAX) {
+                seed_min += AF_RESEED_STEP;
+                wave_sync();  // every lane has read the count
+                if (lane == 0) L.misc[0] = 0;
+                wave_sync();
+                continue;
+            }
+        }
+        break;
+        }
         PROF(pt1 = clock64();)
-        const int nm_total = L.misc[0];
         int flag = 0x4;
         int out_pos = 0, out_score = 0, out_nc = 0;
         if (nm_total > max_mems) {

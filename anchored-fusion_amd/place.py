@@ -249,6 +249,15 @@ def sam_records(ref, queries, hits, nh, flag_extra=0):
     return out
 
 
+def preset_params(preset):
+    """af_params for one of the reference's BLAT / bwa option sets (PRESET_PARAMS)."""
+    T, _ = PRESET_PARAMS[preset]
+    p = _lib.default_params()
+    p.T = T
+    p.min_seed_len = _lib.AF_K
+    return p
+
+
 class Placer:
     """The `place(targets, queries, preset)` callback of partner.py on the GPU.
 
@@ -268,11 +277,7 @@ class Placer:
         return ref
 
     def params(self, preset):
-        T, _ = PRESET_PARAMS[preset]
-        p = _lib.default_params()
-        p.T = T
-        p.min_seed_len = _lib.AF_K
-        return p
+        return preset_params(preset)
 
     def __call__(self, targets, queries, preset):
         header = ["psLayout version 3\n", "\n"]

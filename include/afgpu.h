@@ -130,8 +130,10 @@ int af_index_build_genome(af_ctx *ctx, const char *seq, int64_t len, af_index **
 /* Multi-hit placement of queries (ASCII, `stride` bytes per row, optional lens) on an index
  * built with af_index_build over any reference (anchor, candidate blocks, or contigs joined by
  * N runs).  Every seed-extended region scoring >= p->T is reported, best score first, at most
- * max_hits (1..16) per query: hits[q * max_hits + k] for k < n_hits[q]; n_hits[q] = -1 marks a
- * query with more than p->max_mems MEMs.  Host buffers; synchronous.
+ * max_hits (1..16) per query: hits[q * max_hits + k] for k < n_hits[q].  A query with more than
+ * p->max_mems MEMs (random 16-mer hits on a genome-scale reference) is re-seeded with the
+ * minimum MEM length raised by 4 until at most max_mems remain; past a minimum of 64,
+ * n_hits[q] = -1.  Host buffers; synchronous.
  * Replaces: functions.py BLAT calls (fn:341, 530, 1007, 1071, 1122, 1244) and the genome
  * `bwa mem` calls (AF:188, fn:716). */
 int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,

@@ -474,11 +474,19 @@ static int gen_cigar(const afo_index *I, const afo_params *p, int w_, int lq, co
 /* seeds -> extended regions for one read (the body of mem_align1_core restated for one
  * anchor-like reference); returns n_reg, -1 on MEM overflow.  q: the read's codes. */
 static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, uint8_t *q,
-                        reg_t *regs) {
+                        reg_t *regs, int reseed) {
     mem_t *mems = (mem_t *)malloc(sizeof(mem_t) * (p->max_mems > 0 ? p->max_mems : 1));
     int n_reg = 0, overflow = 0;
     for (int i = 0; i < l; ++i) q[i] = nt4(ascii[i]);
-    int nm = find_mems(I, q, l, p, mems, &overflow);
+    /* placement (reseed): while more than max_mems MEMs, raise the minimum MEM length by
+     * AFO_RESEED_STEP up to AFO_RESEED_MAX (the GPU's AF_RESEED_STEP / AF_RESEED_MAX) */
+    afo_params ps = *p;
+    int nm;
+    for (;;) {
+        nm = find_mems(I, q, l, &ps, mems, &overflow);
+        if (!overflow || !reseed || ps.min_seed_len + AFO_RESEED_STEP > AFO_RESEED_MAX) break;
+        ps.min_seed_len += AFO_RESEED_STEP;
+    }
     if (overflow) { free(mems); return -1; }
     qsort(mems, nm, sizeof(mem_t), cmp_mem);
     int max_ext = p->max_ext < 64 ? p->max_ext : 64;
@@ -512,7 +520,7 @@ static void align_read(const afo_index *I, const uint8_t *ascii, int l, const af
     memset(out, 0, sizeof(*out));
     out->flag = 0x4;
     if (l > AFO_MAX_READ) l = AFO_MAX_READ;
-    int n_reg = read_regions(I, ascii, l, p, q, regs);
+    int n_reg = read_regions(I, ascii, l, p, q, regs, 0);
     if (n_reg < 0) { out->flag |= FLAG_MEM_OVERFLOW; return; }
     int best = -1;
     for (int r = 0; r < n_reg; ++r)
@@ -649,7 +657,7 @@ int afo_place(const afo_index *I, const uint8_t *reads, int64_t n_queries, int32
         reg_t regs[64];
         int l = lens ? lens[r] : stride;
         if (l > AFO_MAX_READ) l = AFO_MAX_READ;
-        int n_reg = read_regions(I, reads + r * (int64_t)stride, l, p, q, regs);
+        int n_reg = read_regions(I, reads + r * (int64_t)stride, l, p, q, regs, 1);
         int nh = 0;
         if (n_reg < 0) { n_hits[r] = -1; continue; }
         int order[64];

@@ -22,6 +22,8 @@ extern "C" {
 #endif
 
 #define AFO_K 16
+#define AFO_RESEED_STEP 4 /* afo_place: minimum MEM length step while a query has > max_mems MEMs */
+#define AFO_RESEED_MAX 64
 #define AFO_MAX_CIGAR 32
 #define AFO_MAX_READ 512
 

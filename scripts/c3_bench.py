@@ -65,6 +65,17 @@ out = {k: torch.zeros(2 * N, dtype=torch.int32, device=dev) for k in ("flag", "p
 out["cigar"] = torch.zeros((2 * N, 32), dtype=torch.int32, device=dev)
 al = AnchorAligner(anchor, device=0)
 s = torch.cuda.current_stream(dev)
+# partner placement buffers: tails of split reads (S6's queries) placed on the genome index
+MIN_CLIP, MAX_HITS = 20, 16
+CAP = max(1024, 2 * N // 200)
+if genome_ref is not None:
+    tails_t = torch.zeros((CAP, L), dtype=torch.uint8, device=dev)
+    tl_t = torch.zeros(CAP, dtype=torch.int32, device=dev)
+    tr_t = torch.zeros(CAP, dtype=torch.int32, device=dev)
+    nt_t = torch.zeros(1, dtype=torch.int32, device=dev)
+    hits_t = torch.zeros(CAP * MAX_HITS * place.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    nh_t = torch.zeros(CAP, dtype=torch.int32, device=dev)
+    pp = place.preset_params("split_tail")  # BLAT -minScore=20 (functions.py:530)
 free, total = torch.cuda.mem_get_info(dev)
 print(f"HBM in use {(total - free) / 2**30:.1f} GiB of {total / 2**30:.0f} GiB", flush=True)
 
@@ -78,73 +89,54 @@ def step(ev=None):
     al.align_candidates_device(reads_t, N, L, out, stream=s)
     if ev:
         ev[2].record(s)
+    if genome_ref is not None:
+        al.split_tails_device(reads_t, L, out, tails_t, tl_t, tr_t, nt_t, min_clip=MIN_CLIP, stream=s)
+        genome_ref.place_device(tails_t, nt_t, L, hits_t, nh_t, lens_t=tl_t, params=pp, max_hits=MAX_HITS, stream=s)
+    if ev:
+        ev[3].record(s)
 
 
 step()
 torch.cuda.synchronize()
-evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
 t0 = time.perf_counter()
 for k in range(args.steps):
     step(evs[k])
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / args.steps
 k1 = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+k23 = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+kpl = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
 mapped = int(((out["flag"] & 4) == 0).sum().item())
 bpp = 2 * L + 8
-print(json.dumps({
+res = {
     "metric": "paired reads/sec through anchored split-read align", "value": round(N / dt, 1), "unit": "pairs/s",
     "n_gpus": 1, "steps": args.steps, "ms_per_step": round(dt * 1e3, 3), "dtype": "int32",
     "data": f"synthetic: {U} simulated 2x{L} pairs tiled to {N}",
-    "config": {"workload": f"configs[2]: {N} x 2x{L} pairs, genome index {args.genome / 1e9:.1f} Gbp resident",
+    "config": {"workload": f"configs[2]: {N} x 2x{L} pairs, genome index {args.genome / 1e9:.1f} Gbp resident"
+                           + (", S2 + partner placement of the split-read tails" if genome_ref is not None else ""),
                "candidates_per_step": al.last_candidates(), "mapped_reads_per_step": mapped},
-    "kernels_ms": {"seed_filter": round(k1, 4)},
+    "kernels_ms": {"seed_filter": round(k1, 4), "align_candidates_and_pairs": round(k23, 4),
+                   "split_tails_and_place": round(kpl, 4)},
     "roofline": {"kernel": "k_seed_filter", "bound": "hbm", "achieved": round(bpp * N / (k1 * 1e-3) / 1e9, 1),
                  "peak": 8000.0, "unit": "GB/s", "frac": round(bpp * N / (k1 * 1e-3) / 8e12, 4),
-                 "bytes_per_launch": bpp * N}}), flush=True)
+                 "bytes_per_launch": bpp * N}}
 if genome_ref is not None:
-    # partner placement (S6-S8's genome search) of the split reads' soft-clipped tails with
-    # af_place on the resident genome index: the tails of the U distinct pairs (checked against
-    # the embedded loci), then those tails tiled N/U times = the whole batch's tails, one call
-    from anchored_fusion_amd.align import AlignResult
-    h = {k: v[:2 * U].cpu().numpy() for k, v in out.items()}
-    h["cigar"] = h["cigar"].view(np.uint32)
-    res = AlignResult(**h)
-    tails = []
-    for r in np.nonzero(res.mapped())[0]:
-        ops = res.cigar_ops(r)
-        if len(ops) != 2 or "S" not in (ops[0][1], ops[1][1]):
-            continue
-        seq = uniq[r].tobytes()
-        if res.flag[r] & 0x10:
-            seq = seq[::-1].translate(bytes.maketrans(b"ACGTN", b"TGCAN"))
-        n_clip = ops[0][0] if ops[0][1] == "S" else ops[1][0]
-        if n_clip < 20:
-            continue
-        tails.append(seq[:n_clip] if ops[0][1] == "S" else seq[-n_clip:])
-    genome_ref.raw_hits(tails[:1000])
-    t0 = time.perf_counter()
-    hits, nh = genome_ref.raw_hits(tails)
-    t_place = time.perf_counter() - t0
-    # the tails of the whole N-pair batch (the U-pair tails tiled N/U times) in one call
-    t0 = time.perf_counter()
-    genome_ref.raw_hits(tails * (N // U))
-    t_place_n = time.perf_counter() - t0
-    on_partner = 0
-    for q in range(len(tails)):
-        if nh[q] > 0:
-            loc = genome_ref.locate(hits[q, 0]["t_start"], hits[q, 0]["t_end"])
-            if loc is not None:
-                name = genome_ref.names[loc[0]]
-                if name in loci and loci[name][0] <= loc[1] < loci[name][1]:
-                    on_partner += 1
-    print(json.dumps({
-        "placement": {"split_tails": len(tails), "of_pairs": U, "seconds": round(t_place, 4),
-                      "tails_per_s": round(len(tails) / t_place, 1),
-                      "best_hit_on_embedded_partner_or_anchor": on_partner,
-                      "note": "af_place host API (H2D queries, D2H hits) on the 3.1 Gbp genome index; soft clip >= 20"},
-        "s2_plus_placement": {"value": round(N / (dt + t_place_n), 1), "unit": "pairs/s",
-                              "note": f"N / (S2 step + one af_place call on the {len(tails) * (N // U)} tails "
-                                      f"of the N pairs = {t_place_n:.4f} s)"}}),
-          flush=True)
+    n_t = int(nt_t.item())
+    n_q = min(n_t, CAP)
+    nh = nh_t[:n_q].cpu().numpy()
+    best = hits_t.view(-1)[:n_q * MAX_HITS * place.HIT_DTYPE.itemsize].cpu().numpy().view(place.HIT_DTYPE)
+    best = best.reshape(n_q, MAX_HITS)[:, 0]
+    on = 0
+    for q in np.nonzero(nh > 0)[0]:
+        loc = genome_ref.locate(best[q]["t_start"], best[q]["t_end"])
+        if loc is not None:
+            name = genome_ref.names[loc[0]]
+            on += name in loci and loci[name][0] <= loc[1] < loci[name][1]
+    res["placement"] = {"split_tails_per_step": n_t, "placed": int((nh > 0).sum()),
+                        "best_hit_in_embedded_partner_or_anchor": int(on), "min_clip": MIN_CLIP,
+                        "params": "T=20 (BLAT -minScore=20, functions.py:530), up to 16 hits per tail"}
+print(json.dumps(res), flush=True)
+if genome_ref is not None:
     genome_ref.close()
 al.close()

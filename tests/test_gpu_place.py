@@ -125,3 +125,40 @@ def test_genome_index_large_reference():
         ok += loc is not None and loc[0] == k and loc[1] == s and bool(h["flag"] & 0x10) == rev and h["score"] == 150
     assert ok == len(truth)
     ref.close()
+
+
+@pytest.mark.parametrize("kind", ["hash", "genome"])
+def test_place_reseed_on_mem_overflow(monkeypatch, kind):
+    """Queries with more than max_mems MEMs at the minimum length: twelve diverged copies of a
+    2 kb unit (a substitution every 18 bases, so the copies share many 16-mers but few 20-mers)
+    plus one exact source.  The placement re-seeds with the minimum MEM length raised (+4 at a
+    time) until at most max_mems MEMs remain; GPU and oracle agree and the exact source wins."""
+    monkeypatch.setenv("AF_INDEX_KIND", kind)
+    rng = np.random.default_rng(61)
+    unit = rng.choice(list("ACGT"), 2000)
+    parts = ["".join(rng.choice(list("ACGT"), 3000))]
+    for _ in range(12):
+        u = unit.copy()
+        for i in range(int(rng.integers(0, 18)), len(u), 18):
+            u[i] = "ACGT"[("ACGT".index(u[i]) + int(rng.integers(1, 4))) % 4]
+        parts += ["".join(u), "".join(rng.choice(list("ACGT"), 500))]
+    src = 3000 + 12 * 2500
+    parts += ["".join(unit), "".join(rng.choice(list("ACGT"), 3000))]
+    ctgs = [("rep", "".join(parts))]
+    blob, _ = place.concat_contigs(ctgs)
+    seqs = ["".join(unit[s:s + 90]) for s in range(0, 1800, 37)]
+    ref = place.Reference(ctgs)
+    assert ref.kind == kind
+    p = place._lib.default_params()
+    p.T, p.min_seed_len = 20, 16
+    g, gn = ref.raw_hits(seqs, p, 4)
+    buf, ln = place.pack_queries(seqs)
+    po = oracle.default_params()
+    po.T, po.min_seed_len = 20, 16
+    r, rn = oracle.OracleIndex(blob).place(buf, ln, po, 4, threads=8)
+    _same(g, gn, r, rn)
+    # without re-seeding these queries would overflow (12 copies x ~40 shared 16-mers > 64)
+    assert (gn > 0).all()
+    for i, s in enumerate(range(0, 1800, 37)):
+        assert g[i, 0]["t_start"] == src + s and g[i, 0]["score"] == 90
+    ref.close()
