@@ -171,6 +171,22 @@ class AnchorAligner:
             None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o),
             _stream_handle(stream)), "af_align_candidates_device")
 
+    def align_candidates_tails_device(self, reads_t, n_pairs, stride, out_t, tails, lens_t=None, stream=None):
+        """align_candidates_device that also cuts the split-read tails in the pair-flag pass.
+        tails: dict(tails=uint8 [cap, stride], lens=int32 [cap], read=int32 [cap], n=int32 [1],
+        min_clip=20, read_base=0, append=False), as split_tails_device."""
+        o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        tt = tails["tails"]
+        cap = int(tt.shape[0])
+        if tt.shape[1] != stride or tails["lens"].numel() < cap or tails["read"].numel() < cap:
+            raise ValueError("tails buffers: [cap, stride] bytes and cap lens / read entries")
+        _lib.check(self._ctx, _lib.lib().af_align_candidates_tails_device(
+            self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o),
+            int(tails.get("min_clip", 20)), int(tails.get("read_base", 0)), int(bool(tails.get("append", False))), cap,
+            tt.data_ptr(), tails["lens"].data_ptr(), tails["read"].data_ptr(), tails["n"].data_ptr(),
+            _stream_handle(stream)), "af_align_candidates_tails_device")
+
     def seed_filter_device(self, reads_t, n_reads, stride, hits_t, lens_t=None, stream=None):
         sh = _stream_handle(stream)
         _lib.check(self._ctx, _lib.lib().af_seed_filter_device(
@@ -178,11 +194,12 @@ class AnchorAligner:
             None if lens_t is None else lens_t.data_ptr(), hits_t.data_ptr(), sh), "af_seed_filter_device")
 
     def split_tails_device(self, reads_t, stride, out_t, tails_t, tail_lens_t, tail_read_t, n_tails_t,
-                           min_clip=20, lens_t=None, stream=None):
+                           min_clip=20, lens_t=None, stream=None, read_base=0, append=False):
         """af_split_tails_device over the records in out_t (rows of reads_t): the soft-clipped
         tails of split reads (CIGAR exactly M+S / S+M, clip >= min_clip) into tails_t
-        (uint8 [cap, stride]), their lengths and read rows; *n_tails_t = number of split reads
-        (may exceed cap).  Asynchronous on stream; tail order varies between runs."""
+        (uint8 [cap, stride]), their lengths and read rows (+ read_base); *n_tails_t = number
+        of split reads (may exceed cap), added to the current value when append=True.
+        Asynchronous on stream; tail order varies between runs."""
         o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
         cap = int(tails_t.shape[0])
         if tail_lens_t.numel() < cap or tail_read_t.numel() < cap:
@@ -191,9 +208,15 @@ class AnchorAligner:
             raise ValueError("tails_t rows must be `stride` bytes")
         _lib.check(self._ctx, _lib.lib().af_split_tails_device(
             self._ctx, reads_t.data_ptr(), int(reads_t.shape[0]), int(stride),
-            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(o), int(min_clip), cap, tails_t.data_ptr(),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(o), int(min_clip), int(read_base),
+            int(bool(append)), cap, tails_t.data_ptr(),
             tail_lens_t.data_ptr(), tail_read_t.data_ptr(), n_tails_t.data_ptr(), _stream_handle(stream)),
             "af_split_tails_device")
+
+    @property
+    def ctx(self):
+        """The raw af_ctx handle (e.g. for place.Reference.place_device on this slot's stream)."""
+        return self._ctx
 
     def last_candidates(self):
         return int(_lib.lib().af_last_candidates(self._ctx))
@@ -221,7 +244,7 @@ class AlignerGroup:
         for a in self.aligners:
             a.close()
 
-    def run_device(self, batches, events=None, wait=None):
+    def run_device(self, batches, events=None, wait=None, post=None, finish=None, tails=None):
         """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t]) with
         every tensor on the device.  Enqueues them and returns without synchronising.
 
@@ -229,8 +252,12 @@ class AlignerGroup:
         j's K2 + K3 go to slot j's stream after one wait for the last K1.  wait (optional):
         events slot 0's stream waits for first (pass the previous group's return value when
         buffers or slots are reused).  events (optional): two timing events, recorded on slot
-        0's stream before the first K1 and after the last.  Returns the events marking each
-        batch's completion."""
+        0's stream before the first K1 and after the last.  post (optional): post(j, aligner,
+        stream) enqueues more work for batch j after its K2 + K3.  tails (optional): tails(j)
+        gives batch j's split-read tails spec (align_candidates_tails_device), cut in its K3.
+        finish (optional): finish(stream) enqueues work for the whole group on slot 0's
+        stream once every batch is done (e.g. one placement launch over all the group's tails).
+        Returns the events marking the group's completion."""
         import torch
         if len(batches) > self.inflight:
             raise ValueError(f"{len(batches)} batches for {self.inflight} slots")
@@ -254,10 +281,23 @@ class AlignerGroup:
                 s.wait_event(k1_done)
             reads_t, n_pairs, stride, out_t = b[:4]
             lens_t = b[4] if len(b) > 4 else None
-            self.aligners[j].align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s)
+            if tails is not None:
+                self.aligners[j].align_candidates_tails_device(reads_t, n_pairs, stride, out_t, tails(j), lens_t,
+                                                               stream=s)
+            else:
+                self.aligners[j].align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s)
+            if post is not None:
+                post(j, self.aligners[j], s)
             e = torch.cuda.Event()
             e.record(s)
             done.append(e)
+        if finish is not None:
+            for e in done[1:]:
+                s0.wait_event(e)
+            finish(s0)
+            e = torch.cuda.Event()
+            e.record(s0)
+            done = [e]
         return done
 
     def join(self, done, stream=None):

@@ -88,6 +88,46 @@ struct ReadRec {
     int32_t n_cigar;
 };
 
+// split-read tails output (af_split_tails_device / af_align_candidates_tails_device)
+struct AfTails {
+    uint8_t *tails;       // cap rows of `stride` bytes
+    int32_t *tail_lens, *tail_read, *n_tails;
+    int64_t cap, read_base;
+    int32_t min_clip;
+};
+
+// One read's tail (tails.hip): mapped read with n_cigar == 2 (checked by the caller), CIGAR
+// exactly S+M or M+S with clip >= min_clip -> SEQ's clipped part (SAM orientation) appended.
+__device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *reads, int32_t stride,
+                                             const int32_t *lens, int64_t r, int f, const uint32_t *cig) {
+    const uint32_t c0 = cig[0], c1 = cig[1];
+    const int op0 = c0 & 0xf, op1 = c1 & 0xf;  // 0 = M, 4 = S
+    int clip, head;
+    if (op0 == 4 && op1 == 0) { clip = (int)(c0 >> 4); head = 1; }
+    else if (op0 == 0 && op1 == 4) { clip = (int)(c1 >> 4); head = 0; }
+    else return;
+    const int len = lens ? lens[r] : stride;
+    if (clip < t.min_clip || clip > len) return;
+    const int slot = atomicAdd(t.n_tails, 1);
+    if (slot >= t.cap) return;
+    const uint8_t *q = reads + r * (int64_t)stride;
+    uint8_t *o = t.tails + (int64_t)slot * stride;
+    const bool rev = (f & 0x10) != 0;
+    // SEQ[i] = rev ? comp(read[len - 1 - i]) : read[i]; the tail is SEQ[0, clip) or SEQ[len - clip, len)
+    const int s0 = head ? 0 : len - clip;
+    for (int i = 0; i < clip; ++i) {
+        const int k = s0 + i;
+        uint8_t c = q[rev ? len - 1 - k : k];
+        if (rev) {
+            const uint8_t lc = c | 0x20;
+            c = lc == 'a' ? 'T' : lc == 'c' ? 'G' : lc == 'g' ? 'C' : lc == 't' ? 'A' : 'N';
+        }
+        o[i] = c;
+    }
+    t.tail_lens[slot] = clip;
+    t.tail_read[slot] = (int32_t)(t.read_base + r);
+}
+
 // launch helpers (defined in the .hip files)
 // ctrl (AF_CTRL_BYTES, one 128-B line per word, no memsets on the hot path):
 //  [AF_HEAD_STRIDE * e], e = 0, 1: candidate count of K1 epoch e (K1 of epoch e zeroes the
@@ -114,13 +154,13 @@ hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_r
                            int32_t *heads, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
                            hipStream_t s);
 hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
-                           int32_t *ctrl, hipStream_t s);
+                           int32_t *ctrl, hipStream_t s, const uint8_t *reads = nullptr, int32_t stride = 0,
+                           const int32_t *lens = nullptr, const AfTails *tails = nullptr);
 hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
                            const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
                            int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
 hipError_t af_launch_split_tails(const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
-                                 const af_aln_out &out, int32_t min_clip, int64_t cap, uint8_t *tails,
-                                 int32_t *tail_lens, int32_t *tail_read, int32_t *n_tails, hipStream_t s);
+                                 const af_aln_out &out, const AfTails &t, bool append, hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);
 size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();

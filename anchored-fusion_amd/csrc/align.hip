@@ -1278,8 +1278,10 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
     }
 }
 
+template <bool TAILS>
 __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const ReadRec *__restrict__ recs,
-                        af_aln_out out, int32_t *__restrict__ ctrl) {
+                        af_aln_out out, int32_t *__restrict__ ctrl, const uint8_t *__restrict__ reads, int32_t stride,
+                        const int32_t *__restrict__ lens, AfTails tails) {
     const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 17)  // K2 ran: reset both head sets and the deferred count
         ctrl[AF_CTRL_HEADS + AF_HEAD_STRIDE * threadIdx.x] = 0;
@@ -1316,6 +1318,12 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
     __builtin_nontemporal_store(i32x2{o_pos[0], o_pos[1]}, reinterpret_cast<i32x2 *>(out.pos) + pp);
     __builtin_nontemporal_store(i32x2{o_score[0], o_score[1]}, reinterpret_cast<i32x2 *>(out.score) + pp);
     __builtin_nontemporal_store(i32x2{o_nc[0], o_nc[1]}, reinterpret_cast<i32x2 *>(out.n_cigar) + pp);
+    if (TAILS) {  // split-read tails for the partner search (af_emit_tail, af_internal.h)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+            if (!(o_flag[m] & 0x4) && o_nc[m] == 2)
+                af_emit_tail(tails, reads, stride, lens, 2 * pp + m, o_flag[m], out.cigar + (2 * pp + m) * AF_MAX_CIGAR);
+    }
 }
 
 }  // namespace
@@ -1369,9 +1377,15 @@ hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32
 }
 
 hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
-                           int32_t *ctrl, hipStream_t s) {
+                           int32_t *ctrl, hipStream_t s, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                           const AfTails *tails) {
     const int bs = 256;
     const int64_t nb = n_pairs > 0 ? (n_pairs + bs - 1) / bs : 1;
-    hipLaunchKernelGGL(k_pairs, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, ctrl);
+    if (tails)
+        hipLaunchKernelGGL(k_pairs<true>, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, ctrl, reads,
+                           stride, lens, *tails);
+    else
+        hipLaunchKernelGGL(k_pairs<false>, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, hits, recs, out, ctrl,
+                           nullptr, 0, nullptr, AfTails{});
     return hipGetLastError();
 }

@@ -398,9 +398,33 @@ int af_align_pairs_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
     return af_align_candidates_device(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream);
 }
 
+static int align_candidates(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
+                            const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream,
+                            const AfTails *tails, bool append);
+
 int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
                                int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
                                void *stream) {
+    return align_candidates(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream, nullptr, false);
+}
+
+int af_align_candidates_tails_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
+                                     int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
+                                     int32_t min_clip, int64_t read_base, int32_t append, int64_t cap,
+                                     uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read,
+                                     int32_t *d_n_tails, void *stream) {
+    if (!d_n_tails || (cap > 0 && (!d_tails || !d_tail_lens || !d_tail_read)))
+        return fail(c, AF_E_INVALID, "null tails argument");
+    if (cap < 0) return fail(c, AF_E_INVALID, "cap < 0");
+    if (read_base < 0 || read_base + 2 * n_pairs > (1LL << 31) - 1)
+        return fail(c, AF_E_INVALID, "read_base + reads exceeds int32");
+    const AfTails t{d_tails, d_tail_lens, d_tail_read, d_n_tails, cap, read_base, min_clip < 1 ? 1 : min_clip};
+    return align_candidates(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream, &t, append != 0);
+}
+
+static int align_candidates(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
+                            const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream,
+                            const AfTails *tails, bool append) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
@@ -434,7 +458,8 @@ int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_r
         HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, n_cand,
                                   c->ctrl + AF_CTRL_HEADS2, c->recs, o->cigar, c->zscratch, c->n_slots, s));
     }
-    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, c->ctrl, s));
+    if (tails && !append) HIPCHK(c, hipMemsetAsync(tails->n_tails, 0, 4, s));
+    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, c->ctrl, s, d_reads, stride, d_lens, tails));
     return AF_OK;
 }
 
@@ -576,19 +601,20 @@ int af_place_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, con
 }
 
 int af_split_tails_device(af_ctx *c, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
-                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t cap,
-                          uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read, int32_t *d_n_tails,
-                          void *stream) {
+                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t read_base,
+                          int32_t append, int64_t cap, uint8_t *d_tails, int32_t *d_tail_lens,
+                          int32_t *d_tail_read, int32_t *d_n_tails, void *stream) {
     if (!c || !d_out || !d_n_tails || (n_reads > 0 && !d_reads) || (cap > 0 && (!d_tails || !d_tail_lens || !d_tail_read)))
         return fail(c, AF_E_INVALID, "null argument");
     if (n_reads < 0 || n_reads > (1LL << 31) - 1) return fail(c, AF_E_INVALID, "n_reads out of range");
     if (cap < 0) return fail(c, AF_E_INVALID, "cap < 0");
+    if (read_base < 0 || read_base + n_reads > (1LL << 31) - 1) return fail(c, AF_E_INVALID, "read_base + n_reads exceeds int32");
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
     if (n_reads > 0 && (!d_out->flag || !d_out->n_cigar || !d_out->cigar))
         return fail(c, AF_E_INVALID, "d_out needs flag, n_cigar and cigar");
     (void)hipSetDevice(c->device);
-    HIPCHK(c, af_launch_split_tails(d_reads, n_reads, stride, d_lens, *d_out, min_clip < 1 ? 1 : min_clip, cap,
-                                    d_tails, d_tail_lens, d_tail_read, d_n_tails, (hipStream_t)stream));
+    const AfTails t{d_tails, d_tail_lens, d_tail_read, d_n_tails, cap, read_base, min_clip < 1 ? 1 : min_clip};
+    HIPCHK(c, af_launch_split_tails(d_reads, n_reads, stride, d_lens, *d_out, t, append != 0, (hipStream_t)stream));
     return AF_OK;
 }
 

@@ -152,10 +152,13 @@ class Reference:
         return hits, nh
 
     def place_device(self, queries_t, n_queries_t, stride, hits_t, n_hits_t, lens_t=None, params=None,
-                     max_hits=16, stream=None):
+                     max_hits=16, stream=None, ctx=None):
         """af_place_device: queries_t uint8 [cap, stride] on the device, n_queries_t an int32
         device scalar (clamped to cap), hits_t a device buffer of cap * max_hits * 176 bytes
-        (view it on the host with HIT_DTYPE), n_hits_t int32 [cap].  Asynchronous on stream."""
+        (view it on the host with HIT_DTYPE), n_hits_t int32 [cap].  Asynchronous on stream.
+        ctx: the context whose queue heads and scratch the launch uses (default this
+        Reference's); placements running concurrently on several streams need one each, e.g.
+        the AnchorAligner of each AlignerGroup slot (``aligner.ctx``)."""
         from .align import _stream_handle
         cap = int(queries_t.shape[0])
         if hits_t.numel() * hits_t.element_size() < cap * max_hits * HIT_DTYPE.itemsize:
@@ -163,8 +166,9 @@ class Reference:
         if n_hits_t.numel() < cap:
             raise ValueError("n_hits_t holds fewer than cap entries")
         p = params or _lib.default_params()
-        _lib.check(self.ctx, _lib.lib().af_place_device(
-            self.ctx, self.idx, queries_t.data_ptr(), n_queries_t.data_ptr(), cap, int(stride),
+        c = self.ctx if ctx is None else ctx
+        _lib.check(c, _lib.lib().af_place_device(
+            c, self.idx, queries_t.data_ptr(), n_queries_t.data_ptr(), cap, int(stride),
             None if lens_t is None else lens_t.data_ptr(), ctypes.byref(p), int(max_hits), hits_t.data_ptr(),
             n_hits_t.data_ptr(), _stream_handle(stream)), "af_place_device")
 

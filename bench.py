@@ -7,7 +7,10 @@ anchor transcript (the bundled BCR NM_004327.4, 6,783 nt), 5 % of pairs from anc
 fusions, the rest from a random background transcriptome (wgsim-style simulator, seeded).
 A step = one pass of the GPU path over the resident batch: seed filter (K1), candidate
 seed/extend/CIGAR (K2) and pair flags (K3), i.e. the records `bwa mem -M` hands to samtools
-at Anchored_Fusion.py:182.  Inputs are resident in HBM before timing starts.  Steps run
+at Anchored_Fusion.py:182, then the partner placement of the split reads' soft-clipped tails
+(af_split_tails_device + af_place_device, the BLAT search of functions.py:530) on the
+workload's transcripts (SURVEY §8 d: S2 + partner placement; --no-placement drops it, and
+`s2_only` reports the same steps without it).  Inputs are resident in HBM before timing starts.  Steps run
 --inflight (default 8) batches at a time through align.AlignerGroup, as a streaming deployment
 keeps several batches in flight: a group's K1 launches run back to back, then its K2+K3
 launches run concurrently on one stream per batch so that each K2's tail overlaps the next
@@ -42,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much wall time")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-placement", action="store_true", help="skip the S2 + partner placement leg")
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: no timing events in the timed region")
     ap.add_argument("--inflight", type=int, default=8,
                     help="batches in flight (AlignerGroup): their K1s back to back, then their K2s at once")
@@ -76,7 +80,7 @@ def main():
 
     anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
     L = args.read_len
-    _, reads, _, _ = sim.fusion_reads(anchor, args.pairs, read_len=L, fusion_frac=args.fusion_frac,
+    _, reads, _, fworld = sim.fusion_reads(anchor, args.pairs, read_len=L, fusion_frac=args.fusion_frac,
                                       seed=20251015 + 7919 * rank)
     nr = reads.shape[0]
     reads_t = torch.from_numpy(reads).to(dev)
@@ -90,14 +94,23 @@ def main():
     bufs = [outs() for _ in range(G)]
     grp = AlignerGroup(anchor, device=gpu, inflight=G)
 
-    def run(n_batches, evs=None):
+    post = None if args.no_placement else Placement(fworld, anchor, nr, L, G, dev)
+
+    def run(n_batches, evs=None, with_placement=True):
         """n_batches steps (one batch each), G at a time; every group waits for the last.
         evs: per group a pair of timing events around its back-to-back K1 launches."""
         done = None
         for k0 in range(0, n_batches, G):
             g = min(G, n_batches - k0)
+            wait = list(done or [])
+            if with_placement and post is not None:
+                wait += post.pending()
             done = grp.run_device([(reads_t, args.pairs, L, bufs[j]) for j in range(g)],
-                                  events=None if evs is None else evs[k0 // G], wait=done)
+                                  events=None if evs is None else evs[k0 // G], wait=wait,
+                                  tails=post.tails if with_placement and post is not None else None,
+                                  finish=post.finish if with_placement and post is not None else None)
+        if with_placement and post is not None:
+            post.join(torch.cuda.current_stream(dev))
         return done
 
     run(args.warmup)
@@ -155,7 +168,8 @@ def main():
         "data": "synthetic (wgsim-style simulator, seed 20251015 + rank)",
         "config": {
             "workload": f"configs[1]: {args.pairs} synthetic 2x{L} bp pairs per GPU, one anchor "
-                        f"(BCR NM_004327.4, {len(anchor)} nt), {args.fusion_frac:.0%} fusion pairs",
+                        f"(BCR NM_004327.4, {len(anchor)} nt), {args.fusion_frac:.0%} fusion pairs"
+                        + ("" if args.no_placement else "; S2 + partner placement of the split-read tails"),
             "pairs_per_gpu": args.pairs, "read_len": L, "anchor_len": len(anchor),
             "parallelism": f"dp{world}", "candidates_per_step": n_cand, "mapped_reads_per_step": mapped,
         },
@@ -170,6 +184,21 @@ def main():
             "bytes_per_launch": bytes_per_launch,
         },
     }
+    if post is not None:
+        res["partner_placement"] = post.report(G)
+        # the same steps without the placement (S2 alone), for reference
+        run(G, with_placement=False)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        run(args.steps, with_placement=False)
+        torch.cuda.synchronize(dev)
+        t_s2 = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([t_s2], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_s2 = float(tt.item())
+        res["s2_only"] = {"value": round(args.pairs * world * args.steps / t_s2, 1), "unit": "pairs/s",
+                          "ms_per_step": round(t_s2 / args.steps * 1e3, 4)}
     if rank == 0 and world == 1:
         # the host-buffer API on the same batch: H2D of the reads + the three kernels + D2H of
         # the records (reported beside `value`, never as it)
@@ -187,6 +216,78 @@ def main():
     grp.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+class Placement:
+    """Partner placement inside the step (SURVEY §8 d: S2 + partner placement).  Each batch's K3
+    (af_align_candidates_tails_device) appends the split reads' soft-clipped tails (clip >= 20)
+    to a group-wide buffer; once the group's batches are done,
+    one af_place_device launch places all of them (BLAT -minScore=20, functions.py:530; up to
+    16 hits per tail) on a reference of the workload's transcripts (anchor, fusion partners,
+    background; hash index) -- the bench workload has no genome.  Two tail buffers are used in
+    turn."""
+
+    MIN_CLIP, MAX_HITS = 20, 16
+
+    def __init__(self, fworld, anchor, n_reads, L, G, dev):
+        import torch
+
+        from anchored_fusion_amd import place
+        ctgs = [("anchor", anchor.decode())] + [(f"partner{k}", t.decode()) for k, t in enumerate(fworld["partners"])]
+        ctgs += [(f"bg{k}", t.decode()) for k, t in enumerate(fworld["background"])]
+        self.ref = place.Reference(ctgs, device=dev.index)
+        self.params = place.preset_params("split_tail")
+        self.n_reads, self.L = n_reads, L
+        self.cap = G * max(1024, n_reads // 100)
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+        self.buf = [dict(tails=z(self.cap, L, dt=torch.uint8), tl=z(self.cap), tr=z(self.cap), nt=z(1),
+                         hits=z(self.cap * self.MAX_HITS * place.HIT_DTYPE.itemsize, dt=torch.uint8),
+                         nh=z(self.cap), done=None) for _ in range(2)]
+        self.nt_last = z(1)
+        self.groups = 0
+
+    def pending(self):
+        """The event the next group's first K1 waits for: the placement that last used the
+        tail buffer this group will fill."""
+        e = self.buf[self.groups & 1]["done"]
+        return [] if e is None else [e]
+
+    def tails(self, j):
+        """Batch j's tails spec: appended (in its K3) to the group's buffer."""
+        b = self.buf[self.groups & 1]
+        self.g = max(getattr(self, "g", 0), j + 1)
+        return dict(tails=b["tails"], lens=b["tl"], read=b["tr"], n=b["nt"], min_clip=self.MIN_CLIP,
+                    read_base=j * self.n_reads, append=True)
+
+    def finish(self, s0):
+        import torch
+        b = self.buf[self.groups & 1]
+        # on slot 0's stream after every batch of the group, with the Reference's own context
+        # (queue heads, scratch); the next group's K1s follow it.  (On a stream of its own,
+        # beside the next group's K1s and K2s, it measured the same step time and slowed K1.)
+        self.ref.place_device(b["tails"], b["nt"], self.L, b["hits"], b["nh"], lens_t=b["tl"], params=self.params,
+                              max_hits=self.MAX_HITS, stream=s0)
+        with torch.cuda.stream(s0):
+            self.nt_last.copy_(b["nt"])
+            b["nt"].zero_()
+        b["done"] = torch.cuda.Event()
+        b["done"].record(s0)
+        self.last, self.last_g, self.g = b, self.g, 0
+        self.groups += 1
+
+    def join(self, stream):
+        for b in self.buf:
+            if b["done"] is not None:
+                stream.wait_event(b["done"])
+
+    def report(self, G):
+        n_t = int(self.nt_last.item())
+        placed = int((self.last["nh"][:min(n_t, self.cap)] > 0).sum().item())
+        self.ref.close()
+        return {"split_tails_per_batch": round(n_t / self.last_g, 1), "placed_fraction": round(placed / max(n_t, 1), 4),
+                "min_clip": self.MIN_CLIP,
+                "reference": "the workload's transcripts (anchor, 8 partners, 400 background), hash index",
+                "params": "T=20 (BLAT -minScore=20, functions.py:530), up to 16 hits per tail, one launch per group"}
 
 
 def cpu_baseline(anchor, reads, args):

@@ -18,6 +18,7 @@
  *   af_place_device       <- same, device-resident buffers and query count, on a HIP stream
  *   af_split_tails_device <- the split-read selection + query FASTA of the partner search
  *                            (functions.py:705-716, 1001-1005), from device-resident records
+ *   af_align_candidates_tails_device <- af_align_candidates_device + the same tails, fused
  *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
@@ -118,6 +119,13 @@ int af_seed_filter_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_rea
 int af_align_candidates_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
                                int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
                                void *stream);
+/* af_align_candidates_device that also writes the split-read tails of af_split_tails_device
+ * (same arguments and semantics, see below) from the pair-flag pass, without a pass of its own. */
+int af_align_candidates_tails_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
+                                     int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
+                                     int32_t min_clip, int64_t read_base, int32_t append, int64_t cap,
+                                     uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read,
+                                     int32_t *d_n_tails, void *stream);
 /* number of candidate reads found by the last seed-filter pass on this context (synchronises) */
 int64_t af_last_candidates(af_ctx *ctx);
 
@@ -151,14 +159,16 @@ int af_place_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, 
  * functions.py:713) with a clip of at least min_clip bases; its tail is the clipped part of
  * SEQ in SAM orientation (the read reverse-complemented for 0x10), the query of the partner
  * search (functions.py:1001-1005).  Writes up to cap tails: row t of d_tails (`stride` bytes,
- * bytes past d_tail_lens[t] undefined), d_tail_lens[t], d_tail_read[t] = the read's row; the
- * number of split reads (which may exceed cap) goes to *d_n_tails.  Tail order varies between
- * runs; d_tail_read identifies them.  Replaces the split-read selection and FASTA writing of
- * functions.py:705-716 and fn:1001-1005. */
+ * bytes past d_tail_lens[t] undefined), d_tail_lens[t], d_tail_read[t] = read_base + the read's
+ * row; the number of split reads (which may exceed cap) goes to *d_n_tails, which is zeroed
+ * first unless `append` is non-zero (then the tails add to those already there: several
+ * batches, even on different streams, can fill one buffer for one af_place_device launch).
+ * Tail order varies between runs; d_tail_read identifies them.  Replaces the split-read
+ * selection and FASTA writing of functions.py:705-716 and fn:1001-1005. */
 int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
-                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t cap,
-                          uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read, int32_t *d_n_tails,
-                          void *stream);
+                          const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t read_base,
+                          int32_t append, int64_t cap, uint8_t *d_tails, int32_t *d_tail_lens,
+                          int32_t *d_tail_read, int32_t *d_n_tails, void *stream);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as

@@ -137,3 +137,31 @@ def test_place_device_matches_host_api(aligner, anchor):
         assert len(placed) > 10 and on == len(placed)
     finally:
         ref.close()
+
+
+def test_fused_tails_and_append(aligner, anchor):
+    """af_align_candidates_tails_device (tails cut in K3) gives the same tails as the host rule;
+    two batches appended into one buffer keep their read_base offsets."""
+    import torch
+    dev = torch.device("cuda:0")
+    batches = [synthetic_pairs(anchor, 3000, 100, seed=56 + k)[0] for k in range(2)]
+    want = {}
+    for k, reads in enumerate(batches):
+        for r, t in host_tails(reads, None, aligner.align_pairs(reads), 20).items():
+            want[k * 100_000 + r] = t
+    cap = 2 * len(want) + 16
+    tb = dict(tails=torch.zeros((cap, 100), dtype=torch.uint8, device=dev),
+              lens=torch.zeros(cap, dtype=torch.int32, device=dev), read=torch.zeros(cap, dtype=torch.int32, device=dev),
+              n=torch.full((1,), 12345, dtype=torch.int32, device=dev), min_clip=20)
+    for k, reads in enumerate(batches):
+        nr = reads.shape[0]
+        rt = torch.from_numpy(reads).to(dev)
+        out = {f: torch.zeros(nr, dtype=torch.int32, device=dev) for f in ("flag", "pos", "score", "n_cigar", "hits")}
+        out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
+        aligner.seed_filter_device(rt, nr, 100, out["hits"])
+        aligner.align_candidates_tails_device(rt, nr // 2, 100, out, dict(tb, read_base=k * 100_000, append=k > 0))
+        torch.cuda.synchronize()
+    n = int(tb["n"].item())
+    assert n == len(want)
+    t, ln, rd = tb["tails"].cpu().numpy(), tb["lens"].cpu().numpy(), tb["read"].cpu().numpy()
+    assert {int(rd[i]): t[i, :ln[i]].tobytes() for i in range(n)} == want
