@@ -210,7 +210,7 @@ def main():
         res["pcie_inclusive"] = {"value": round(args.pairs / dt, 1), "unit": "pairs/s",
                                  "note": "af_align_pairs with host buffers (H2D reads, D2H records), 1 call"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(anchor, reads, args)
+        res["cpu_baseline"] = cpu_baseline(anchor, reads, args, None if args.no_placement else fworld)
     if rank == 0:
         print(json.dumps(res), flush=True)
     grp.close()
@@ -290,23 +290,70 @@ class Placement:
                 "params": "T=20 (BLAT -minScore=20, functions.py:530), up to 16 hits per tail, one launch per group"}
 
 
-def cpu_baseline(anchor, reads, args):
-    """The CPU oracle (a port of the same algorithm; bwa itself is absent) timed on a bounded
-    sample of this rank's batch: the first --cpu-sample pairs, repeated until --cpu-seconds."""
+def _split_tails(reads, rec, min_clip):
+    """Host form of the split-read tail rule (af_emit_tail): mapped, CIGAR exactly S+M / M+S,
+    clip >= min_clip; the clipped part of SEQ (reverse-complemented read for 0x10)."""
+    import numpy as np
+    comp = bytes.maketrans(b"ACGTNacgtn", b"TGCANTGCAN")
+    rows = np.nonzero(((rec["flag"] & 4) == 0) & (rec["n_cigar"] == 2))[0]
+    out = []
+    for r in rows:
+        c0, c1 = int(rec["cigar"][r, 0]), int(rec["cigar"][r, 1])
+        if (c0 & 15, c1 & 15) == (4, 0):
+            clip, head = c0 >> 4, True
+        elif (c0 & 15, c1 & 15) == (0, 4):
+            clip, head = c1 >> 4, False
+        else:
+            continue
+        n = reads.shape[1]
+        if clip < min_clip or clip > n:
+            continue
+        seq = reads[r].tobytes()
+        if rec["flag"][r] & 0x10:
+            seq = seq[::-1].translate(comp)
+        out.append(seq[:clip] if head else seq[n - clip:])
+    return out
+
+
+def cpu_baseline(anchor, reads, args, fworld=None):
+    """The CPU oracle (a port of the same algorithm; bwa and BLAT themselves are absent) timed on
+    a bounded sample of this rank's batch: the first --cpu-sample pairs, repeated until
+    --cpu-seconds.  With fworld, each pass also cuts the split-read tails and places them
+    (afo_place, BLAT -minScore=20) on the same transcripts reference as the GPU step."""
+    import numpy as np
+
     import oracle
+    from anchored_fusion_amd import place
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     n = min(args.cpu_sample, reads.shape[0] // 2)
     sample = reads[: 2 * n]
     ix = oracle.OracleIndex(anchor)
-    passes, dt = 0, 0.0
+    ref_ix = po = None
+    if fworld is not None:
+        ctgs = [("anchor", anchor.decode())] + [(f"p{k}", t.decode()) for k, t in enumerate(fworld["partners"])]
+        ctgs += [(f"bg{k}", t.decode()) for k, t in enumerate(fworld["background"])]
+        ref_ix = oracle.OracleIndex(place.concat_contigs(ctgs)[0])
+        po = oracle.default_params()
+        po.T, po.min_seed_len = 20, 16
+    ix.align_pairs(sample, threads=threads)  # untimed warm-up pass (thread pool, first-touch pages)
+    passes, dt, n_tails = 0, 0.0, 0
     while passes == 0 or dt < args.cpu_seconds:
         t0 = time.perf_counter()
-        ix.align_pairs(sample, threads=threads)
+        rec = ix.align_pairs(sample, threads=threads)
+        if ref_ix is not None:
+            tails = _split_tails(sample, rec, Placement.MIN_CLIP)
+            n_tails = len(tails)
+            if tails:
+                buf, ln = place.pack_queries(tails)
+                ref_ix.place(buf, ln, po, Placement.MAX_HITS, threads=threads)
         dt += time.perf_counter() - t0
         passes += 1
+    what = "S2 + tail placement" if ref_ix is not None else "S2"
     return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} pairs of rank 0's batch x {passes} passes ({dt:.1f} s), oracle/af_oracle.c "
-                      f"(C restatement of bwa-mem's algorithm; bwa itself is absent), OpenMP {threads} threads"}
+            "sample": f"first {n} pairs of rank 0's batch x {passes} passes ({dt:.1f} s), {what}"
+                      + (f" ({n_tails} tails per pass)" if ref_ix is not None else "")
+                      + f", oracle/af_oracle.c (C restatement of bwa-mem's algorithm; bwa and BLAT are absent), "
+                        f"OpenMP {threads} threads"}
 
 
 if __name__ == "__main__":
