@@ -20,6 +20,8 @@ SHORT = {"k_seed_stream": "K1 k_seed_stream", "k_seed_ragged": "K1 k_seed_ragged
 
 
 def short(name):
+    if "k_align<" in name and ", true>" in name:
+        return "K2 k_align (placement)"
     for k, v in SHORT.items():
         if k + "<" in name or k + "(" in name:
             return v
