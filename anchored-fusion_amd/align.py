@@ -244,7 +244,7 @@ class AlignerGroup:
         for a in self.aligners:
             a.close()
 
-    def run_device(self, batches, events=None, wait=None, post=None, finish=None, tails=None):
+    def run_device(self, batches, events=None, wait=None, post=None, finish=None, tails=None, before=None):
         """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t]) with
         every tensor on the device.  Enqueues them and returns without synchronising.
 
@@ -253,7 +253,8 @@ class AlignerGroup:
         events slot 0's stream waits for first (pass the previous group's return value when
         buffers or slots are reused).  events (optional): two timing events, recorded on slot
         0's stream before the first K1 and after the last.  post (optional): post(j, aligner,
-        stream) enqueues more work for batch j after its K2 + K3.  tails (optional): tails(j)
+        stream) enqueues more work for batch j after its K2 + K3; before (optional), the same
+        signature, enqueues work ahead of batch j's K2 (after the group's K1s).  tails (optional): tails(j)
         gives batch j's split-read tails spec (align_candidates_tails_device), cut in its K3.
         finish (optional): finish(stream) enqueues work for the whole group on slot 0's
         stream once every batch is done (e.g. one placement launch over all the group's tails).
@@ -281,6 +282,8 @@ class AlignerGroup:
                 s.wait_event(k1_done)
             reads_t, n_pairs, stride, out_t = b[:4]
             lens_t = b[4] if len(b) > 4 else None
+            if before is not None:
+                before(j, self.aligners[j], s)
             if tails is not None:
                 self.aligners[j].align_candidates_tails_device(reads_t, n_pairs, stride, out_t, tails(j), lens_t,
                                                                stream=s)

@@ -102,15 +102,18 @@ def main():
         done = None
         for k0 in range(0, n_batches, G):
             g = min(G, n_batches - k0)
-            wait = list(done or [])
-            if with_placement and post is not None:
-                wait += post.pending()
+            pl = with_placement and post is not None
             done = grp.run_device([(reads_t, args.pairs, L, bufs[j]) for j in range(g)],
-                                  events=None if evs is None else evs[k0 // G], wait=wait,
-                                  tails=post.tails if with_placement and post is not None else None,
-                                  finish=post.finish if with_placement and post is not None else None)
+                                  events=None if evs is None else evs[k0 // G], wait=done,
+                                  tails=post.tails if pl else None, before=post.before if pl else None)
+            if pl:
+                post.end_group()
         if with_placement and post is not None:
-            post.join(torch.cuda.current_stream(dev))
+            s0 = grp.streams[0]
+            for e in done:
+                s0.wait_event(e)
+            post.flush(s0)
+            torch.cuda.current_stream(dev).wait_stream(s0)
         return done
 
     run(args.warmup)
@@ -185,7 +188,7 @@ def main():
         },
     }
     if post is not None:
-        res["partner_placement"] = post.report(G)
+        res["partner_placement"] = post.report()
         # the same steps without the placement (S2 alone), for reference
         run(G, with_placement=False)
         torch.cuda.synchronize(dev)
@@ -221,11 +224,13 @@ def main():
 class Placement:
     """Partner placement inside the step (SURVEY §8 d: S2 + partner placement).  Each batch's K3
     (af_align_candidates_tails_device) appends the split reads' soft-clipped tails (clip >= 20)
-    to a group-wide buffer; once the group's batches are done,
-    one af_place_device launch places all of them (BLAT -minScore=20, functions.py:530; up to
-    16 hits per tail) on a reference of the workload's transcripts (anchor, fusion partners,
-    background; hash index) -- the bench workload has no genome.  Two tail buffers are used in
-    turn."""
+    to a group-wide buffer; one af_place_device launch per group places them (BLAT
+    -minScore=20, functions.py:530; up to 16 hits per tail) on a reference of the workload's
+    transcripts (anchor, fusion partners, background; hash index) -- the bench workload has no
+    genome.  A group's placement is enqueued in the next group, after its K1s and ahead of
+    its first K2, so it runs beside that group's other K2s instead of idling the chip between
+    groups; the last group's placement is flushed at the end of the timed steps.  Two tail
+    buffers are used in turn."""
 
     MIN_CLIP, MAX_HITS = 20, 16
 
@@ -242,45 +247,48 @@ class Placement:
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
         self.buf = [dict(tails=z(self.cap, L, dt=torch.uint8), tl=z(self.cap), tr=z(self.cap), nt=z(1),
                          hits=z(self.cap * self.MAX_HITS * place.HIT_DTYPE.itemsize, dt=torch.uint8),
-                         nh=z(self.cap), done=None) for _ in range(2)]
+                         nh=z(self.cap)) for _ in range(2)]
         self.nt_last = z(1)
-        self.groups = 0
-
-    def pending(self):
-        """The event the next group's first K1 waits for: the placement that last used the
-        tail buffer this group will fill."""
-        e = self.buf[self.groups & 1]["done"]
-        return [] if e is None else [e]
+        self.fill, self.to_place, self.g, self.last, self.last_g = 0, None, 0, None, 1
 
     def tails(self, j):
-        """Batch j's tails spec: appended (in its K3) to the group's buffer."""
-        b = self.buf[self.groups & 1]
-        self.g = max(getattr(self, "g", 0), j + 1)
+        """Batch j's tails spec: appended (in its K3) to the buffer this group fills."""
+        b = self.buf[self.fill]
+        self.g = max(self.g, j + 1)
         return dict(tails=b["tails"], lens=b["tl"], read=b["tr"], n=b["nt"], min_clip=self.MIN_CLIP,
                     read_base=j * self.n_reads, append=True)
 
-    def finish(self, s0):
+    def _place(self, k, stream):
         import torch
-        b = self.buf[self.groups & 1]
-        # on slot 0's stream after every batch of the group, with the Reference's own context
-        # (queue heads, scratch); the next group's K1s follow it.  (On a stream of its own,
-        # beside the next group's K1s and K2s, it measured the same step time and slowed K1.)
+        b = self.buf[k]
+        # the Reference's own context (queue heads, scratch): one placement at a time
         self.ref.place_device(b["tails"], b["nt"], self.L, b["hits"], b["nh"], lens_t=b["tl"], params=self.params,
-                              max_hits=self.MAX_HITS, stream=s0)
-        with torch.cuda.stream(s0):
+                              max_hits=self.MAX_HITS, stream=stream)
+        with torch.cuda.stream(stream):
             self.nt_last.copy_(b["nt"])
             b["nt"].zero_()
-        b["done"] = torch.cuda.Event()
-        b["done"].record(s0)
-        self.last, self.last_g, self.g = b, self.g, 0
-        self.groups += 1
+        self.last = b
 
-    def join(self, stream):
-        for b in self.buf:
-            if b["done"] is not None:
-                stream.wait_event(b["done"])
+    def before(self, j, aligner, stream):
+        """Ahead of the first K2 of a group: the previous group's placement."""
+        if j == 0 and self.to_place is not None:
+            self._place(self.to_place[0], stream)
+            self.last_g = self.to_place[1]
+            self.to_place = None
 
-    def report(self, G):
+    def end_group(self):
+        self.to_place = (self.fill, self.g)
+        self.fill ^= 1
+        self.g = 0
+
+    def flush(self, stream):
+        """The last group's placement (stream must follow every batch of that group)."""
+        if self.to_place is not None:
+            self._place(self.to_place[0], stream)
+            self.last_g = self.to_place[1]
+            self.to_place = None
+
+    def report(self):
         n_t = int(self.nt_last.item())
         placed = int((self.last["nh"][:min(n_t, self.cap)] > 0).sum().item())
         self.ref.close()
