@@ -165,3 +165,35 @@ def test_fused_tails_and_append(aligner, anchor):
     assert n == len(want)
     t, ln, rd = tb["tails"].cpu().numpy(), tb["lens"].cpu().numpy(), tb["read"].cpu().numpy()
     assert {int(rd[i]): t[i, :ln[i]].tobytes() for i in range(n)} == want
+
+
+def test_place_device_clamps_count(anchor):
+    """A device query count above cap_queries is clamped: the rows [0, cap) are placed as by
+    the host API and nothing past the buffers is read or written."""
+    import torch
+    from anchored_fusion_amd import place
+    from place_cases import contigs, queries
+    dev = torch.device("cuda:0")
+    ctgs = contigs(seed=71)
+    seqs = [q for _, q, _ in queries(ctgs, 300, seed=72, lens=(60, 100))]
+    ref = place.Reference(ctgs)
+    try:
+        cap, stride, mh = 200, 100, 4
+        buf, ln = place.pack_queries(seqs[:cap])
+        q = torch.zeros((cap, stride), dtype=torch.uint8, device=dev)
+        q[:, :buf.shape[1]] = torch.from_numpy(buf).to(dev)
+        lt = torch.from_numpy(ln).to(dev)
+        n_t = torch.tensor([cap + 100], dtype=torch.int32, device=dev)
+        hits = torch.zeros((cap + 8) * mh * place.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        nh = torch.full((cap + 8,), -7, dtype=torch.int32, device=dev)
+        ref.place_device(q, n_t, stride, hits, nh, lens_t=lt, max_hits=mh)
+        torch.cuda.synchronize()
+        hh, nhh = ref.raw_hits(seqs[:cap], max_hits=mh)
+        nd = nh.cpu().numpy()
+        assert np.array_equal(nd[:cap], nhh) and (nd[cap:] == -7).all()
+        hd = hits.cpu().numpy().view(place.HIT_DTYPE).reshape(cap + 8, mh)
+        for i in range(cap):
+            for k in range(nhh[i]):
+                assert hd[i, k]["t_start"] == hh[i, k]["t_start"] and hd[i, k]["score"] == hh[i, k]["score"]
+    finally:
+        ref.close()
