@@ -132,19 +132,14 @@ __device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *re
 // ctrl (AF_CTRL_BYTES, one 128-B line per word, no memsets on the hot path):
 //  [AF_HEAD_STRIDE * e], e = 0, 1: candidate count of K1 epoch e (K1 of epoch e zeroes the
 //                                  other epoch's count for the next call);
-//  [AF_HEAD_STRIDE * (2 + x)], x = 0..7: dequeue heads of the lane-per-read K2;
-//  [AF_HEAD_STRIDE * (10 + x)]: dequeue heads of the wave-per-read K2 (deferred reads);
-//  [AF_HEAD_STRIDE * 18]: deferred-read count.  k_pairs zeroes heads and count after K2.
+//  [AF_HEAD_STRIDE * (10 + x)], x = 0..7: dequeue heads of K2 (k_pairs zeroes them after K2);
+//  (words 2..9 and 18 are unused).
 #define AF_HEAD_STRIDE 32
 #define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 29)
-#define AF_CTRL_HEADS (2 * AF_HEAD_STRIDE)
 #define AF_CTRL_HEADS2 (10 * AF_HEAD_STRIDE)
-#define AF_CTRL_NDEFER (18 * AF_HEAD_STRIDE)
 //  [AF_HEAD_STRIDE * (19 + x)]: dequeue heads of af_place; [AF_HEAD_STRIDE * 27]: its query count.
 #define AF_CTRL_PLACE_HEADS (19 * AF_HEAD_STRIDE)
 #define AF_CTRL_PLACE_N (27 * AF_HEAD_STRIDE)
-#define AF_LANE_Z 8192                          // traceback bytes per lane (larger: deferred)
-#define AF_LANE_SCRATCH (1024 + AF_LANE_Z + 256)  // per-lane global scratch of the lane K2
 size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next, int n_cu,
@@ -166,9 +161,3 @@ size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();
 hipError_t af_build_genome_index(const uint8_t *seq, int64_t n, uint8_t *D, uint32_t *D2, uint32_t *Dn,
                                  uint32_t *S, uint32_t *kposu, uint32_t *scan_sums, int n_cu, hipStream_t s);
-size_t af_align_lane_lds(int32_t stride);
-bool af_lane_params_ok(const af_params &p, int32_t stride);
-hipError_t af_launch_align_lane(const DevIndex &ix, const uint8_t *reads, int32_t stride, const int32_t *lens,
-                                const af_params &p, const int32_t *cand, const int32_t *n_cand, int32_t *heads,
-                                ReadRec *recs, uint32_t *cigar, uint8_t *scratch, int32_t n_waves, int32_t *defer,
-                                int32_t *n_defer, hipStream_t s);

@@ -905,7 +905,9 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_align(DevIndex ix, const uint
         PROF(const int64_t pt0 = clock64(); int64_t pt1 = pt0, pt2 = pt0; int p_ext_rows = 0, p_cig_rows = 0,
              p_ext_calls = 0, p_nreg = 0, p_ext_dp = 0;)
         int l = lens ? lens[r] : stride;
+        if (l > stride) l = stride;  // a length past the row (device-side lens are unchecked)
         if (l > AF_MAX_READ) l = AF_MAX_READ;
+        if (l < 0) l = 0;
         const uint8_t *rd = reads + r * (int64_t)stride;
         for (int x = lane; x < l; x += 64) {
             const uint8_t c = rd[x];
@@ -1283,8 +1285,8 @@ __global__ void k_pairs(int64_t n_pairs, const int32_t *__restrict__ hits, const
                         af_aln_out out, int32_t *__restrict__ ctrl, const uint8_t *__restrict__ reads, int32_t stride,
                         const int32_t *__restrict__ lens, AfTails tails) {
     const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < 17)  // K2 ran: reset both head sets and the deferred count
-        ctrl[AF_CTRL_HEADS + AF_HEAD_STRIDE * threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 8)  // K2 ran: reset its dequeue heads
+        ctrl[AF_CTRL_HEADS2 + AF_HEAD_STRIDE * threadIdx.x] = 0;
     if (pp >= n_pairs) return;
     ReadRec R[2];
 #pragma unroll

@@ -26,15 +26,11 @@ struct af_ctx {
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
     uint8_t *zscratch = nullptr;
-    uint8_t *lane_scratch = nullptr;  // lane-per-read K2: AF_LANE_SCRATCH bytes per lane
-    int32_t *defer = nullptr;         // reads the lane K2 hands to the wave K2
-    int lane_waves = 0;
     // af_place staging (host-buffer API)
     uint8_t *p_q = nullptr;
     int32_t *p_lens = nullptr, *p_nhits = nullptr;
     af_hit *p_hits = nullptr;
     int64_t p_cap_bytes = 0, p_cap_q = 0, p_cap_hits = 0;
-    int lane_stride = 0;
     // host-API staging (device)
     uint8_t *d_reads = nullptr;
     int64_t cap_bytes = 0;
@@ -108,29 +104,12 @@ int dev_upload(af_ctx *ctx, af_index *ix, const std::vector<T> &v, const T **out
 
 int ensure_reads_cap(af_ctx *c, int64_t n_reads) {
     if (n_reads <= c->cap_reads) return AF_OK;
-    af_free(c->cand); af_free(c->recs); af_free(c->defer);
-    c->cand = nullptr; c->recs = nullptr; c->defer = nullptr; c->cap_reads = 0;
+    af_free(c->cand); af_free(c->recs);
+    c->cand = nullptr; c->recs = nullptr; c->cap_reads = 0;
     const int64_t cap = std::max<int64_t>(n_reads, 1 << 16);
     HIPCHK(c, hipMalloc(&c->cand, sizeof(int32_t) * cap));
     HIPCHK(c, hipMalloc(&c->recs, sizeof(ReadRec) * cap));
-    HIPCHK(c, hipMalloc(&c->defer, sizeof(int32_t) * cap));
     c->cap_reads = cap;
-    return AF_OK;
-}
-
-// lane-per-read K2: waves per CU from the LDS footprint (q + eh rows for this stride)
-int ensure_lane(af_ctx *c, int32_t stride) {
-    if (c->lane_scratch && c->lane_stride == stride) return AF_OK;
-    const size_t lds = af_align_lane_lds(stride);
-    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
-    const int waves = c->n_cu * per_cu;
-    if (!c->lane_scratch || waves > c->lane_waves) {
-        af_free(c->lane_scratch);
-        c->lane_scratch = nullptr;
-        HIPCHK(c, hipMalloc(&c->lane_scratch, (size_t)waves * 64 * AF_LANE_SCRATCH));
-    }
-    c->lane_waves = waves;
-    c->lane_stride = stride;
     return AF_OK;
 }
 
@@ -190,7 +169,6 @@ void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->d_packed);
-    af_free(c->lane_scratch); af_free(c->defer);
     af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
@@ -441,23 +419,8 @@ static int align_candidates(af_ctx *c, const af_index *ix, const uint8_t *d_read
     if (c->epoch == 0) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
     const int slot = (int)((c->epoch - 1) & 1);
     int32_t *n_cand = c->ctrl + AF_HEAD_STRIDE * slot;
-    // The lane-per-read K2 (align_lane.hip) is exact but, as written, slower than the
-    // wave-per-read K2 on the bench workload (divergence across lanes, latency-bound per-lane
-    // loops); it is opt-in (AF_K2_LANE=1) until it wins.
-    const char *lane_env = getenv("AF_K2_LANE");
-    if (lane_env && lane_env[0] == '1' && af_lane_params_ok(*p, stride)) {
-        // lane-per-read K2 over all candidates; reads whose traceback does not fit a lane's
-        // scratch are handed to the wave-per-read K2 (deferred list)
-        if ((rc = ensure_lane(c, stride))) return rc;
-        HIPCHK(c, af_launch_align_lane(ix->dev, d_reads, stride, d_lens, *p, c->cand, n_cand,
-                                       c->ctrl + AF_CTRL_HEADS, c->recs, o->cigar, c->lane_scratch, c->lane_waves,
-                                       c->defer, c->ctrl + AF_CTRL_NDEFER, s));
-        HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->defer, c->ctrl + AF_CTRL_NDEFER,
-                                  c->ctrl + AF_CTRL_HEADS2, c->recs, o->cigar, c->zscratch, c->n_slots, s));
-    } else {
-        HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, n_cand,
-                                  c->ctrl + AF_CTRL_HEADS2, c->recs, o->cigar, c->zscratch, c->n_slots, s));
-    }
+    HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, n_cand, c->ctrl + AF_CTRL_HEADS2,
+                              c->recs, o->cigar, c->zscratch, c->n_slots, s));
     if (tails && !append) HIPCHK(c, hipMemsetAsync(tails->n_tails, 0, 4, s));
     HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, c->ctrl, s, d_reads, stride, d_lens, tails));
     return AF_OK;

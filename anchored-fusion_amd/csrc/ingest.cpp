@@ -26,6 +26,8 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <exception>
+#include <new>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -74,8 +76,15 @@ struct Src {
     void start_reader() {
         reader = std::thread([this] {
             for (;;) {
-                std::vector<char> c(8u << 20);
-                const long r = read_some(c.data(), c.size());
+                std::vector<char> c;
+                long r;
+                try {  // no exception may leave the thread (std::terminate): report it as a read error
+                    c.resize(8u << 20);
+                    r = read_some(c.data(), c.size());
+                } catch (const std::exception &ex) {
+                    err = path + ": " + ex.what();
+                    r = -1;
+                }
                 std::unique_lock<std::mutex> g(mu);
                 if (r <= 0) {
                     r_error = r < 0;
@@ -218,6 +227,7 @@ struct Src {
                 return fail_bgzf("truncated BGZF block");
             const unsigned char *t = b.data() + bsize - 4;
             const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+            if (isize > 65536) return fail_bgzf("corrupt BGZF block (ISIZE above the 64 KiB BGZF maximum)");
             out_off.push_back(out_off.back() + isize);
             blocks.push_back(std::move(b));
         }
@@ -345,9 +355,7 @@ struct af_fastq {
     std::string err;
 };
 
-extern "C" {
-
-int af_fastq_open(const char *fq1, const char *fq2, int threads, af_fastq **out) {
+static int af_fastq_open_impl(const char *fq1, const char *fq2, int threads, af_fastq **out) {
     if (!out || !fq1 || !fq2) return AF_E_INVALID;
     *out = nullptr;
     af_fastq *f = new (std::nothrow) af_fastq;
@@ -367,11 +375,18 @@ const char *af_fastq_error(const af_fastq *f) { return f ? f->err.c_str() : "nul
 
 void af_fastq_close(af_fastq *f) { delete f; }
 
-int af_fastq_next(af_fastq *f, int64_t max_pairs, int64_t *n_pairs, int32_t *max_len, int64_t *names_bytes) {
+static int af_fastq_next_impl(af_fastq *f, int64_t max_pairs, int64_t *n_pairs, int32_t *max_len, int64_t *names_bytes) {
     if (!f || !n_pairs || max_pairs < 0) return AF_E_INVALID;
     *n_pairs = 0;
     bool ok[2] = {true, true};
-    std::thread t([&] { ok[1] = parse(f->src[1], max_pairs, f->bat[1]); });
+    std::thread t([&] {
+        try {  // an exception may not leave the thread
+            ok[1] = parse(f->src[1], max_pairs, f->bat[1]);
+        } catch (const std::exception &ex) {
+            f->src[1].err = ex.what();
+            ok[1] = false;
+        }
+    });
     ok[0] = parse(f->src[0], max_pairs, f->bat[0]);
     t.join();
     for (int m = 0; m < 2; ++m)
@@ -401,7 +416,7 @@ int af_fastq_next(af_fastq *f, int64_t max_pairs, int64_t *n_pairs, int32_t *max
     return AF_OK;
 }
 
-int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, char *names, int64_t names_cap,
+static int af_fastq_export_impl(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, char *names, int64_t names_cap,
                     int64_t *name_off) {
     if (!f || stride < 0) return AF_E_INVALID;
     const Batch &b1 = f->bat[0], &b2 = f->bat[1];
@@ -437,6 +452,42 @@ int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, 
         for (int64_t i = 0; i < n; ++i) name_off[i] = b1.name_off[i];
     for (auto &x : th) x.join();
     return AF_OK;
+}
+
+// No C++ exception crosses the C-ABI: allocation failures and anything else thrown below become
+// AF_E_* codes (the message goes to af_fastq_error when a handle exists).
+template <class F>
+static int af_guard(af_fastq *f, F &&body) {
+    try {
+        return body();
+    } catch (const std::bad_alloc &) {
+        if (f) f->err = "out of host memory";
+        return AF_E_NOMEM;
+    } catch (const std::exception &ex) {
+        if (f) f->err = ex.what();
+        return AF_E_INVALID;
+    }
+}
+
+extern "C" {
+
+int af_fastq_open(const char *fq1, const char *fq2, int threads, af_fastq **out) {
+    try {
+        return af_fastq_open_impl(fq1, fq2, threads, out);
+    } catch (const std::bad_alloc &) {
+        return AF_E_NOMEM;
+    } catch (const std::exception &) {
+        return AF_E_INVALID;
+    }
+}
+
+int af_fastq_next(af_fastq *f, int64_t max_pairs, int64_t *n_pairs, int32_t *max_len, int64_t *names_bytes) {
+    return af_guard(f, [&] { return af_fastq_next_impl(f, max_pairs, n_pairs, max_len, names_bytes); });
+}
+
+int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, char *names, int64_t names_cap,
+                    int64_t *name_off) {
+    return af_guard(f, [&] { return af_fastq_export_impl(f, stride, reads, lens, names, names_cap, name_off); });
 }
 
 }  // extern "C"

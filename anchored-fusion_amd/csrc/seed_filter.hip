@@ -1,23 +1,22 @@
 // seed_filter.hip -- K1: HBM-streaming anchor seed filter (the seeding
 // pass of `bwa mem` at Anchored_Fusion.py:182).
 //
-// Layout and schedule (DESIGN.md §K1):
-//  * persistent grid, one or two 1024-thread workgroups per CU (LDS-bound); block tiles of AF_SEED_BTILE whole
-//    reads taken round-robin; the 16 waves of a workgroup sweep a tile together, so every
-//    round moves ~16 KiB of contiguous bytes (lane l of wave w loads one 16-byte chunk: one
-//    coalesced 1-KiB global_load_dwordx4 per wave), unrolled x3 with two rounds in flight;
-//  * wave blocks overlap by one chunk (63 new chunks per block): lane 63 only feeds lane 62,
-//    so the loop carries no scalar loads and no cross-wave data;
-//  * ASCII -> 2-bit codes by SWAR ((c>>1)^(c>>2))&3, four bases per byte; each lane forms the
-//    four 16-mers starting at its 4-byte-aligned offsets, taking the next lane's packed chunk
-//    through a DPP wave shift;
-//  * each 16-mer is tested against a blocked Bloom filter of the anchor's 16-mers held in
-//    LDS: one ds_read_b64 returns two 32-bit words, three hash-chosen bits must be set in
-//    each (~1e-7 false positives per probe for a 6.8 kb anchor), no data-dependent control
-//    flow on the hot path;
-//  * Bloom-positive 16-mers add to 8-bit per-read counters in LDS; after the tile each wave
-//    writes one int32 per read; the tile's reads with hits are appended to the candidate
-//    list with ONE global atomic per tile (LDS prefix over the tile's 64-read ballots).
+// Layout and schedule (DESIGN.md §5 K1):
+//  * persistent grid, one 1024-thread workgroup per CU (the 128 KiB Bloom table sets the LDS
+//    budget); block B streams ONE contiguous range of reads, an equal share of the batch (ranges
+//    start on 16-byte boundaries); the first chunk loads are issued before the table is copied
+//    to LDS;
+//  * the 16 waves sweep the range together in 63-chunk wave blocks (one coalesced 1-KiB
+//    global_load_dwordx4 per wave and round, blocks overlapping by one 16-byte chunk), two
+//    loads in flight per wave, no stores, barriers or returning atomics in the loop;
+//  * a byte's 2-bit code is a table lookup on its low 3 bits (v_and + v_perm_b32 for four
+//    bytes); 16-mer keys are "word-transposed" (base 4w+b at bits 8b+2w) so the chunk's code
+//    words and the next lane's (DPP wave_shl:1) form the four keys at its 4-aligned offsets;
+//  * probe: one 32x32->64 multiply per key; two ds_read_b32 (absolute LDS offsets) into the
+//    2^bits-word table, four one-hot bits per word must be set (af_k1_hash/af_k1_mask);
+//  * positives add to 8-bit per-read counters in LDS; the epilogue writes one int32 per read,
+//    ballots per 64 reads and an LDS prefix, and ONE device atomic reserves the block's
+//    candidate-list slots.
 //
 // Exactness: any MEM >= 19 nt (bwa -k 19) contains a 16-mer starting at an offset that is a
 // multiple of 4 and a Bloom filter has no false negatives, so hits == 0 implies no seed; the

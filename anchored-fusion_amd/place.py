@@ -156,11 +156,17 @@ class Reference:
         """af_place_device: queries_t uint8 [cap, stride] on the device, n_queries_t an int32
         device scalar (clamped to cap), hits_t a device buffer of cap * max_hits * 176 bytes
         (view it on the host with HIT_DTYPE), n_hits_t int32 [cap].  Asynchronous on stream.
-        ctx: the context whose queue heads and scratch the launch uses (default this
-        Reference's); placements running concurrently on several streams need one each, e.g.
-        the AnchorAligner of each AlignerGroup slot (``aligner.ctx``)."""
+        ctx: the context whose queue heads and traceback scratch the launch uses (default this
+        Reference's).  A context's placement must be stream-ordered with every other K2 or
+        placement enqueued on that context (they share its scratch): placements running
+        concurrently on several streams need a context of their own each, and an AlignerGroup
+        slot's ``aligner.ctx`` may only be used on that slot's own stream."""
         from .align import _stream_handle
         cap = int(queries_t.shape[0])
+        if queries_t.dim() != 2 or int(queries_t.shape[1]) < int(stride):
+            raise ValueError("queries_t must be [cap, >= stride]")
+        if lens_t is not None and lens_t.numel() < cap:
+            raise ValueError("lens_t holds fewer than cap entries")
         if hits_t.numel() * hits_t.element_size() < cap * max_hits * HIT_DTYPE.itemsize:
             raise ValueError("hits_t holds fewer than cap * max_hits hits")
         if n_hits_t.numel() < cap:

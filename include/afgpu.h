@@ -149,7 +149,10 @@ int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n
 /* af_place with device buffers, asynchronous on `stream`: the query count is read on the
  * device from *d_n_queries (clamped to cap_queries, the rows d_queries / d_lens / d_n_hits hold;
  * d_hits holds cap_queries * max_hits), so it can follow af_split_tails_device without a host
- * round trip.  d_lens may be NULL (every query `stride` long). */
+ * round trip.  d_lens may be NULL (every query `stride` long); lengths above stride are read
+ * as stride.  A context runs one placement or alignment at a time: its traceback scratch and
+ * queue heads are shared, so calls on one context must be ordered on one stream (use one context
+ * per concurrent stream). */
 int af_place_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
                     int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_params *p, int32_t max_hits,
                     af_hit *d_hits, int32_t *d_n_hits, void *stream);

@@ -16,7 +16,7 @@ src, out = sys.argv[1], sys.argv[2]
 os.makedirs(out, exist_ok=True)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"k_seed_stream": "K1 k_seed_stream", "k_seed_ragged": "K1 k_seed_ragged", "k_align": "K2 k_align",
-         "k_pairs": "K3 k_pairs", "k_align_lane": "K2 k_align_lane"}
+         "k_pairs": "K3 k_pairs"}
 
 
 def short(name):

@@ -167,17 +167,6 @@ def test_full_size_properties(aligner, anchor):
     assert torch.equal(f2, out["flag"])
 
 
-def test_lane_kernel_parity(anchor, oidx, monkeypatch):
-    """The opt-in lane-per-read K2 (AF_K2_LANE=1) is held to the same bit-exact bar."""
-    from anchored_fusion_amd.align import AnchorAligner
-    monkeypatch.setenv("AF_K2_LANE", "1")
-    reads, _, _ = synthetic_pairs(anchor, 3000, 100, seed=11)
-    with AnchorAligner(anchor, device=0) as a:
-        g = a.align_pairs(reads).as_dict()
-    r = oidx.align_pairs(reads, threads=8)
-    assert_records_equal(g, r, reads)
-
-
 @pytest.mark.parametrize("stride", [16, 17, 20, 27, 28, 29, 33, 64, 99, 100, 101, 150, 251, 320])
 def test_seed_filter_strides(aligner, oidx, anchor, stride):
     """K1 alone: per-read Bloom hits equal the oracle's for every stride class (reads that end

@@ -162,3 +162,18 @@ def test_bgzf_corrupt_block_raises(tmp_path):
     b2 = _write_bgzf(tmp_path / "c_2.fq.gz", t, 4000)
     with pytest.raises(ValueError, match="BGZF"):
         afio.read_pairs(b1, b2)
+
+
+def test_bgzf_corrupt_isize_raises(tmp_path):
+    # a member whose ISIZE field claims more than BGZF's 64 KiB maximum is rejected as corrupt
+    # before any allocation is sized from it (no std::bad_alloc escaping the reader thread)
+    import struct
+    t = _fq([(f"s{i}", "ACGT" * 20) for i in range(300)])
+    b1 = _write_bgzf(tmp_path / "s_1.fq.gz", t, 4000)
+    raw = bytearray(open(b1, "rb").read())
+    bsize = struct.unpack_from("<H", raw, 16)[0] + 1  # first member
+    struct.pack_into("<I", raw, bsize - 4, 0xFFFFFFF0)
+    open(b1, "wb").write(bytes(raw))
+    b2 = _write_bgzf(tmp_path / "s_2.fq.gz", t, 4000)
+    with pytest.raises(ValueError, match="ISIZE"):
+        afio.read_pairs(b1, b2)
