@@ -30,7 +30,7 @@ AF_FLAG_CIGAR_OVERFLOW = 0x20000
 
 # every symbol include/afgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = (
-    "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_index_build",
+    "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_pe_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
     "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
@@ -46,6 +46,13 @@ class Params(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "a", "b", "o_del", "e_del", "o_ins", "e_ins", "pen_clip5", "pen_clip3", "w", "zdrop",
         "min_seed_len", "max_occ", "T", "max_ext", "max_mems")]
+
+
+class Pe(ctypes.Structure):
+    """af_pe: bwa mem paired-end options and the batch's place in bwa's input stream."""
+    _fields_ = [("pen_unpaired", ctypes.c_int32), ("max_ins", ctypes.c_int32), ("max_matesw", ctypes.c_int32),
+                ("split_width", ctypes.c_int32), ("max_mem_intv", ctypes.c_int32), ("max_chain_gap", ctypes.c_int32),
+                ("chunk_bases", ctypes.c_int64), ("pair_base", ctypes.c_int64)]
 
 
 class AlnOut(ctypes.Structure):
@@ -93,12 +100,15 @@ def lib():
     L.af_index_filter_words.restype = _i32
     L.af_index_filter_table.argtypes = [_vp, _vp, _i64]
     L.af_index_filter_table.restype = ctypes.c_int
-    L.af_align_pairs.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), ctypes.POINTER(AlnOut)]
+    L.af_pe_default.argtypes = [ctypes.POINTER(Pe)]
+    L.af_pe_default.restype = None
+    _pe = ctypes.POINTER(Pe)
+    L.af_align_pairs.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _pe, ctypes.POINTER(AlnOut)]
     L.af_align_pairs.restype = ctypes.c_int
-    L.af_align_pairs_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params),
+    L.af_align_pairs_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _pe,
                                         ctypes.POINTER(AlnOut), _vp]
     L.af_align_pairs_device.restype = ctypes.c_int
-    L.af_align_candidates_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params),
+    L.af_align_candidates_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _pe,
                                              ctypes.POINTER(AlnOut), _vp]
     L.af_align_candidates_device.restype = ctypes.c_int
     L.af_seed_filter_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]
@@ -112,7 +122,7 @@ def lib():
     L.af_split_tails_device.argtypes = [_vp, _vp, _i64, _i32, _vp, ctypes.POINTER(AlnOut), _i32, _i64, _i32, _i64,
                                         _vp, _vp, _vp, _vp, _vp]
     L.af_split_tails_device.restype = ctypes.c_int
-    L.af_align_candidates_tails_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params),
+    L.af_align_candidates_tails_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _pe,
                                                    ctypes.POINTER(AlnOut), _i32, _i64, _i32, _i64, _vp, _vp, _vp,
                                                    _vp, _vp]
     L.af_align_candidates_tails_device.restype = ctypes.c_int
@@ -134,6 +144,15 @@ def default_params():
     p = Params()
     lib().af_params_default(ctypes.byref(p))
     return p
+
+
+def default_pe(**kw):
+    """af_pe_default (bwa 0.7.17 paired-end options, 10 Mbase chunks) with overrides."""
+    e = Pe()
+    lib().af_pe_default(ctypes.byref(e))
+    for k, v in kw.items():
+        setattr(e, k, v)
+    return e
 
 
 def check(ctx, rc, what):

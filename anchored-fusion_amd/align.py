@@ -44,7 +44,7 @@ class AlignResult:
 class AnchorAligner:
     """One GPU context + one anchor index.  Not thread-safe (one host thread per GPU)."""
 
-    def __init__(self, anchor: bytes, device: int = 0, params=None):
+    def __init__(self, anchor: bytes, device: int = 0, params=None, pe=None):
         L = _lib.lib()
         self._ctx = ctypes.c_void_p()
         rc = L.af_ctx_create(int(device), ctypes.byref(self._ctx))
@@ -55,7 +55,14 @@ class AnchorAligner:
         _lib.check(self._ctx, L.af_index_build(self._ctx, self.anchor, len(self.anchor), ctypes.byref(self._idx)),
                    "af_index_build")
         self.params = params or _lib.default_params()
+        self.pe = pe or _lib.default_pe()
         self.device = device
+
+    def _pe(self, pair_base):
+        """af_pe for a batch starting at global pair index pair_base (bwa's read ids)."""
+        e = _lib.Pe.from_buffer_copy(self.pe)
+        e.pair_base = int(pair_base)
+        return e
 
     def close(self):
         L = _lib._L
@@ -87,8 +94,9 @@ class AnchorAligner:
         _lib.check(self._ctx, L.af_index_filter_table(self._idx, out.ctypes.data, out.size), "af_index_filter_table")
         return out
 
-    def align_pairs(self, reads, lens=None) -> AlignResult:
-        """reads: uint8 [2N, stride] pair-major ASCII; lens: optional int32 [2N]."""
+    def align_pairs(self, reads, lens=None, pair_base=0) -> AlignResult:
+        """reads: uint8 [2N, stride] pair-major ASCII; lens: optional int32 [2N].  The batch is
+        bwa's input from pair ``pair_base`` on, starting at one of its chunk boundaries."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
         nr, stride = reads.shape
         if nr % 2:
@@ -99,13 +107,16 @@ class AnchorAligner:
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
         _lib.check(self._ctx, _lib.lib().af_align_pairs(self._ctx, self._idx, reads.ctypes.data, nr // 2, stride,
                                                         None if lp is None else lp.ctypes.data,
-                                                        ctypes.byref(self.params), ctypes.byref(o)),
+                                                        ctypes.byref(self.params), ctypes.byref(self._pe(pair_base)),
+                                                        ctypes.byref(o)),
                    "af_align_pairs")
         return AlignResult(**out)
 
     def align_fastq(self, fq1, fq2, batch_pairs=1 << 20, threads=0):
         """FASTQ(.gz) pair -> records, streamed: the native reader (io.iter_pairs) parses batch
         k + 1 on host threads while batch k is aligned (both ctypes calls release the GIL).
+        Alignment calls end on bwa chunk boundaries (``chunk_ends``), so insert-size statistics
+        and read ids are those of one ``bwa mem`` run over the whole input.
         Returns ``(names, reads, lens, AlignResult)`` over all pairs, as io.read_pairs + align_pairs
         would (lens None when every read has the common length)."""
         import threading
@@ -120,7 +131,8 @@ class AnchorAligner:
             except BaseException as e:  # re-raised on the caller's thread
                 box["err"] = e
 
-        parts = []
+        parts, pend = [], []
+        done = 0
         th = threading.Thread(target=fetch)
         th.start()
         while True:
@@ -128,13 +140,24 @@ class AnchorAligner:
             if "err" in box:
                 raise box.pop("err")
             cur = box.pop("next")
+            if cur is not None:
+                th = threading.Thread(target=fetch)
+                th.start()
+                pend.append(cur)
+            if not pend:
+                break
+            names, reads, lens = _concat_batches(pend)
+            pb = lens.reshape(-1, 2).sum(axis=1)
+            cut = len(pb) if cur is None else complete_chunks(pb, int(self.pe.chunk_bases))
+            pend = [] if cut == len(pb) else [(names.slice(cut, len(pb)), reads[2 * cut:], lens[2 * cut:])]
+            if cut:
+                sub_reads, sub_lens = reads[:2 * cut], lens[:2 * cut]
+                uniform = bool((sub_lens == sub_reads.shape[1]).all())
+                parts.append((names.slice(0, cut), sub_reads, sub_lens,
+                              self.align_pairs(sub_reads, None if uniform else sub_lens, pair_base=done)))
+                done += cut
             if cur is None:
                 break
-            th = threading.Thread(target=fetch)
-            th.start()
-            names, reads, lens = cur
-            uniform = bool((lens == reads.shape[1]).all())
-            parts.append((names, reads, lens, self.align_pairs(reads, None if uniform else lens)))
         if not parts:
             empty = np.zeros(0, np.int32)
             return (afio.Names(b"", np.zeros(0, np.int64)), np.full((0, 1), ord("N"), np.uint8), None,
@@ -152,26 +175,27 @@ class AnchorAligner:
         return names, reads, (None if (lens == stride).all() else lens), res
 
     # ---- device-resident entry points (torch tensors as HBM buffers) ----------------------
-    def align_pairs_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None):
+    def align_pairs_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None, pair_base=0):
         """Enqueues S2 on ``stream`` (torch.cuda.Stream or raw handle); all tensors on-device.
         out_t: dict flag/pos/score/n_cigar/hits (int32 [2N]) and cigar (int32/uint32 [2N, 32])."""
         o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
         sh = _stream_handle(stream)
         _lib.check(self._ctx, _lib.lib().af_align_pairs_device(
             self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
-            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o), sh),
-            "af_align_pairs_device")
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(self._pe(pair_base)),
+            ctypes.byref(o), sh), "af_align_pairs_device")
 
-    def align_candidates_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None):
+    def align_candidates_device(self, reads_t, n_pairs, stride, out_t, lens_t=None, stream=None, pair_base=0):
         """Second half of align_pairs_device; seed_filter_device(hits_t=out_t['hits']) must have
         run on the same stream for this batch."""
         o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
         _lib.check(self._ctx, _lib.lib().af_align_candidates_device(
             self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
-            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o),
-            _stream_handle(stream)), "af_align_candidates_device")
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(self._pe(pair_base)),
+            ctypes.byref(o), _stream_handle(stream)), "af_align_candidates_device")
 
-    def align_candidates_tails_device(self, reads_t, n_pairs, stride, out_t, tails, lens_t=None, stream=None):
+    def align_candidates_tails_device(self, reads_t, n_pairs, stride, out_t, tails, lens_t=None, stream=None,
+                                      pair_base=0):
         """align_candidates_device that also cuts the split-read tails in the pair-flag pass.
         tails: dict(tails=uint8 [cap, stride], lens=int32 [cap], read=int32 [cap], n=int32 [1],
         min_clip=20, read_base=0, append=False), as split_tails_device."""
@@ -182,8 +206,8 @@ class AnchorAligner:
             raise ValueError("tails buffers: [cap, stride] bytes and cap lens / read entries")
         _lib.check(self._ctx, _lib.lib().af_align_candidates_tails_device(
             self._ctx, self._idx, reads_t.data_ptr(), int(n_pairs), int(stride),
-            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(o),
-            int(tails.get("min_clip", 20)), int(tails.get("read_base", 0)), int(bool(tails.get("append", False))), cap,
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(self.params), ctypes.byref(self._pe(pair_base)),
+            ctypes.byref(o), int(tails.get("min_clip", 20)), int(tails.get("read_base", 0)), int(bool(tails.get("append", False))), cap,
             tt.data_ptr(), tails["lens"].data_ptr(), tails["read"].data_ptr(), tails["n"].data_ptr(),
             _stream_handle(stream)), "af_align_candidates_tails_device")
 
@@ -309,6 +333,49 @@ class AlignerGroup:
         s = stream or torch.cuda.current_stream()
         for e in done:
             s.wait_event(e)
+
+
+def chunk_ends(pair_bases, chunk_bases):
+    """End (exclusive pair index) of each bwa input chunk: bseq_read stops after the pair that
+    brings the chunk to >= chunk_bases bases (10,000,000 x threads).  The last entry is the
+    input's end when the final chunk is short."""
+    cum = np.cumsum(np.asarray(pair_bases, dtype=np.int64))
+    ends, start, before = [], 0, 0
+    n = len(cum)
+    while start < n:
+        e = int(np.searchsorted(cum, before + chunk_bases, side="left"))
+        end = n if e >= n else e + 1
+        ends.append(end)
+        before = int(cum[end - 1])
+        start = end
+    return np.asarray(ends, dtype=np.int64)
+
+
+def complete_chunks(pair_bases, chunk_bases):
+    """Pairs in the complete bwa chunks at the start of ``pair_bases`` (the last chunk of a
+    stream that may still grow is left out)."""
+    cum = np.cumsum(np.asarray(pair_bases, dtype=np.int64))
+    ends = chunk_ends(pair_bases, chunk_bases)
+    cut, before = 0, 0
+    for e in ends:
+        if int(cum[e - 1]) - before < chunk_bases:
+            break
+        cut, before = int(e), int(cum[e - 1])
+    return cut
+
+
+def _concat_batches(batches):
+    """(names, reads, lens) batches of io.iter_pairs joined into one (rows padded with N)."""
+    from . import io as afio
+    if len(batches) == 1:
+        return batches[0]
+    stride = max(r.shape[1] for _, r, _ in batches)
+    reads = np.full((sum(r.shape[0] for _, r, _ in batches), stride), ord("N"), np.uint8)
+    row = 0
+    for _, r, _ in batches:
+        reads[row:row + r.shape[0], :r.shape[1]] = r
+        row += r.shape[0]
+    return afio.Names.concat([b[0] for b in batches]), reads, np.concatenate([b[2] for b in batches])
 
 
 def _stream_handle(stream):

@@ -80,6 +80,62 @@ __host__ __device__ static inline uint32_t af_k1_mask(uint32_t v) {
     return m;
 }
 
+// ---- S2: bwa mem paired-end (s2.hip; the contract is oracle/bwa_pe.c) ---------------------
+// Per-read caps, identical to the oracle's AFO_PE_MAX_* (a read past one is reported unmapped
+// with AF_FLAG_MEM_OVERFLOW on both sides).
+#define AF_S2_MAX_PMEM 128
+#define AF_S2_MAX_SEED 64
+#define AF_S2_MAX_OCC 128
+#define AF_S2_MAX_CHAIN 32
+#define AF_S2_MAX_REG 32
+#define AF_S2_MAX_TSPAN 1024  // longest reference span mem_patch_reg merges (the DP target window)
+
+// The bwa text of the anchor (bns_fasta2bntseq: forward pac with N -> lrand48() & 3, then its
+// reverse complement), its suffix ranks (bwt_sa order) and a position hash of ALL its 16-mers
+// (including those across the strand boundary: SMEM counts see them, as bwa's BWT does).
+struct DevText {
+    const uint8_t *T;        // codes 0..3, length 2n
+    const uint32_t *T2;      // 2-bit packed T, 16 bases per word, padded
+    const int32_t *rank;     // suffix rank of T[i..]
+    const int4 *hslot;       // {key, first index into kpos, count, kpos[first]}
+    const int32_t *kpos;
+    int64_t n;
+    int32_t hbits;
+    int32_t base_cnt[4];     // occurrences of each base in T
+};
+
+// one alignment region (mem_alnreg_t fields the paired-end stage reads)
+struct S2Reg {
+    int64_t rb, re;
+    int32_t qb, qe, score, truesc, w, seedlen0;
+};
+// insert-size statistics of one chunk and orientation (mem_pestat_t)
+struct S2Pes {
+    int32_t low, high, failed, pad;
+    double avg, std;
+};
+// bwa options of the paired-end path that af_params does not carry (af_pe)
+struct S2Opt {
+    int32_t pen_unpaired, max_ins, max_matesw, split_width, max_mem_intv, max_chain_gap;
+    int64_t pair_base;
+};
+// per-context device scratch of the S2 kernels
+struct S2Work {
+    S2Reg *pool;        // region pool (K2 allocates with one atomic per read)
+    int64_t pool_cap;
+    int32_t *pool_n;    // pool fill (ctrl word of the current epoch)
+    int2 *rmap;         // per read: {pool offset, n regions (-1 overflow)}; candidate reads only
+    int32_t *plist;     // candidate pairs (K3a), consumed by K3c
+    int32_t *n_plist;
+    int32_t *ilist;     // insert sizes, dir << 30 | isize, stored from each chunk's first pair
+    int32_t *icnt;      // per chunk: insert sizes stored
+    S2Pes *pes;         // [n_chunks][4]
+    const int64_t *cstart;  // chunk start pairs, *n_chunks + 1 entries
+    const int32_t *n_chunks;  // device word
+    int32_t max_chunks;
+    int32_t *heads_k2, *heads_k3;  // per-XCD dequeue heads (8 lines each)
+};
+
 // Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
 struct ReadRec {
     int32_t flag;    // 0x4 unmapped, 0x10 reverse, AF_FLAG_* overflow bits
@@ -135,15 +191,22 @@ __device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *re
 //  [AF_HEAD_STRIDE * (10 + x)], x = 0..7: dequeue heads of K2 (k_pairs zeroes them after K2);
 //  (words 2..9 and 18 are unused).
 #define AF_HEAD_STRIDE 32
-#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 29)
+#define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 41)
 #define AF_CTRL_HEADS2 (10 * AF_HEAD_STRIDE)
 //  [AF_HEAD_STRIDE * (19 + x)]: dequeue heads of af_place; [AF_HEAD_STRIDE * 27]: its query count.
+//  [AF_HEAD_STRIDE * (29 + x)]: dequeue heads of the S2 pair kernel (K3c);
+//  [AF_HEAD_STRIDE * (37 + e)], e = 0, 1: S2 region-pool fill of epoch e;
+//  [AF_HEAD_STRIDE * (39 + e)]: S2 candidate-pair count of epoch e (K1 of epoch e zeroes both
+//  words of its epoch).
 #define AF_CTRL_PLACE_HEADS (19 * AF_HEAD_STRIDE)
 #define AF_CTRL_PLACE_N (27 * AF_HEAD_STRIDE)
+#define AF_CTRL_S2_HEADS3 (29 * AF_HEAD_STRIDE)
+#define AF_CTRL_S2_POOL (37 * AF_HEAD_STRIDE)
+#define AF_CTRL_S2_NPAIRS (39 * AF_HEAD_STRIDE)
 size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next, int n_cu,
-                                 hipStream_t s);
+                                 const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next,
+                                 int32_t *s2z, int n_cu, hipStream_t s);
 hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                            const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
                            int32_t *heads, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
@@ -154,6 +217,13 @@ hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *
 hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
                            const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
                            int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
+hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
+                        const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
+                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
+                        const AfTails *tails, hipStream_t s);
+hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *lens, int64_t chunk_bases,
+                               int64_t *cstart, int64_t *scan_tmp, int32_t max_chunks, int32_t *n_chunks_dev,
+                               hipStream_t s);
 hipError_t af_launch_split_tails(const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
                                  const af_aln_out &out, const AfTails &t, bool append, hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);

@@ -26,6 +26,17 @@ struct af_ctx {
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
     uint8_t *zscratch = nullptr;
+    // S2 (bwa mem paired-end) scratch, s2.hip
+    S2Reg *s2_pool = nullptr;
+    int64_t s2_pool_cap = 0;
+    int2 *s2_rmap = nullptr;
+    int32_t *s2_plist = nullptr, *s2_ilist = nullptr;
+    int64_t *s2_scan = nullptr;
+    int64_t s2_cap_pairs = 0;
+    int32_t *s2_icnt = nullptr, *s2_nchunks = nullptr;
+    S2Pes *s2_pes = nullptr;
+    int64_t *s2_cstart = nullptr;
+    int32_t s2_max_chunks = 0;
     // af_place staging (host-buffer API)
     uint8_t *p_q = nullptr;
     int32_t *p_lens = nullptr, *p_nhits = nullptr;
@@ -45,7 +56,12 @@ struct af_index {
     af_ctx *ctx = nullptr;
     DevIndex dev{};
     std::vector<uint32_t> bloom_host;
-    void *allocs[16] = {};
+    // S2: the bwa text of the anchor (built with the index), its suffix ranks and 16-mer hash
+    // (built on first use by an af_align_* call)
+    std::vector<uint8_t> text;
+    DevText s2{};
+    bool s2_ready = false;
+    void *allocs[24] = {};
     int n_allocs = 0;
 };
 
@@ -71,13 +87,15 @@ int fail(af_ctx *c, int code, const char *fmt, ...) {
         if (_e != hipSuccess) return fail(ctx, AF_E_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
 
-// CIGAR rows of the candidate reads (the only rows K2 writes) packed for one device-to-host copy
-__global__ void k_gather_cigar(const int32_t *__restrict__ cand, int64_t n, const uint32_t *__restrict__ cigar,
+// CIGAR rows of the reads of the listed pairs (the only rows the pair kernel writes), row i =
+// read (i & 1) of pair plist[i >> 1], packed for one device-to-host copy
+__global__ void k_gather_cigar(const int32_t *__restrict__ plist, int64_t n, const uint32_t *__restrict__ cigar,
                                uint32_t *__restrict__ packed) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n * (AF_MAX_CIGAR / 4);
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = t / (AF_MAX_CIGAR / 4), w = t % (AF_MAX_CIGAR / 4);
-        reinterpret_cast<uint4 *>(packed)[t] = reinterpret_cast<const uint4 *>(cigar + (int64_t)cand[i] * AF_MAX_CIGAR)[w];
+        const int64_t r = 2 * (int64_t)plist[i >> 1] + (i & 1);
+        reinterpret_cast<uint4 *>(packed)[t] = reinterpret_cast<const uint4 *>(cigar + r * AF_MAX_CIGAR)[w];
     }
 }
 
@@ -89,6 +107,55 @@ inline uint8_t nt4(uint8_t c) {
     case 'T': case 't': return 3;
     default: return 4;
     }
+}
+
+// srand48(11) / lrand48() of the POSIX drand48 family (glibc): bns_fasta2bntseq replaces every
+// ambiguous base of the reference by lrand48() & 3 after srand48(bns->seed = 11)
+struct Rand48 {
+    uint64_t x;
+    explicit Rand48(long seed) : x(((uint64_t)(uint32_t)seed << 16) | 0x330Eu) {}
+    long next() {
+        x = (0x5DEECE66DULL * x + 0xBULL) & ((1ULL << 48) - 1);
+        return (long)(x >> 17);
+    }
+};
+
+// the bwa text of a one-contig reference: forward pac (N substituted) ++ its reverse complement
+std::vector<uint8_t> bwa_text(const char *seq, int64_t n) {
+    std::vector<uint8_t> T((size_t)(2 * n));
+    Rand48 r(11);
+    for (int64_t i = 0; i < n; ++i) {
+        int c = nt4((uint8_t)seq[i]);
+        if (c >= 4) c = (int)(r.next() & 3);
+        T[i] = (uint8_t)c;
+        T[2 * n - 1 - i] = (uint8_t)(3 - c);
+    }
+    return T;
+}
+
+// suffix ranks of T (a suffix that ends first sorts first: bwa's '$'), prefix doubling
+std::vector<int32_t> suffix_ranks(const std::vector<uint8_t> &T) {
+    const int64_t N = (int64_t)T.size();
+    std::vector<int64_t> rk(N), tmp(N);
+    std::vector<int32_t> idx(N);
+    for (int64_t i = 0; i < N; ++i) { rk[i] = T[i]; idx[i] = (int32_t)i; }
+    for (int64_t h = 1;; h <<= 1) {
+        auto key2 = [&](int32_t i) { return i + h < N ? rk[i + h] : (int64_t)-1; };
+        std::sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) {
+            if (rk[a] != rk[b]) return rk[a] < rk[b];
+            return key2(a) < key2(b);
+        });
+        int64_t r = 0;
+        for (int64_t j = 0; j < N; ++j) {
+            if (j > 0 && (rk[idx[j]] != rk[idx[j - 1]] || key2(idx[j]) != key2(idx[j - 1]))) ++r;
+            tmp[idx[j]] = r;
+        }
+        rk.swap(tmp);
+        if (r == N - 1 || h >= N) break;
+    }
+    std::vector<int32_t> out(N);
+    for (int64_t i = 0; i < N; ++i) out[i] = (int32_t)rk[i];
+    return out;
 }
 
 template <class T>
@@ -120,6 +187,96 @@ int ensure_zscratch(af_ctx *c) {
     return AF_OK;
 }
 
+// S2 structures of an anchor index: suffix ranks of the bwa text, its 16-mer hash (every
+// position, including the strand boundary), packed text, base counts
+int ensure_s2_text(af_ctx *c, af_index *ix) {
+    if (ix->s2_ready) return AF_OK;
+    const std::vector<uint8_t> &T = ix->text;
+    const int64_t N = (int64_t)T.size(), n = N / 2;
+    if (N < AF_K) return fail(c, AF_E_INVALID, "anchor shorter than %d", AF_K / 2);
+    std::vector<int32_t> rank = suffix_ranks(T);
+    std::vector<uint32_t> T2((N + 15) / 16 + 2, 0);
+    for (int64_t i = 0; i < N; ++i) T2[i >> 4] |= (uint32_t)T[i] << (2 * (i & 15));
+    std::vector<uint64_t> occ;
+    occ.reserve(N);
+    for (int64_t q = 0; q + AF_K <= N; ++q) {
+        uint32_t k = 0;
+        for (int u = 0; u < AF_K; ++u) k |= (uint32_t)T[q + u] << (2 * u);
+        occ.push_back((uint64_t)k << 32 | (uint64_t)q);
+    }
+    std::sort(occ.begin(), occ.end());
+    std::vector<uint32_t> keys;
+    std::vector<int32_t> starts, cnts, kpos(occ.size());
+    for (size_t i = 0; i < occ.size(); ++i) {
+        const uint32_t k = (uint32_t)(occ[i] >> 32);
+        kpos[i] = (int32_t)(occ[i] & 0xffffffffu);
+        if (i == 0 || k != keys.back()) { keys.push_back(k); starts.push_back((int32_t)i); cnts.push_back(0); }
+        ++cnts.back();
+    }
+    const int64_t nd = (int64_t)keys.size();
+    int hbits = 10;
+    while ((1LL << hbits) < 2 * nd) ++hbits;
+    const uint32_t hm = (1u << hbits) - 1u;
+    std::vector<int4> hslot(1u << hbits, int4{0, 0, 0, 0});
+    for (int64_t i = 0; i < nd; ++i) {
+        uint32_t sl = af_fmix(keys[i]) & hm;
+        while (hslot[sl].z) sl = (sl + 1) & hm;
+        hslot[sl] = int4{(int)keys[i], starts[i], cnts[i], kpos[starts[i]]};
+    }
+    if (ix->n_allocs + 5 > 24) return fail(c, AF_E_INVALID, "index allocation table full");
+    int rc;
+    DevText X{};
+    if ((rc = dev_upload(c, ix, T, &X.T)) || (rc = dev_upload(c, ix, T2, &X.T2)) ||
+        (rc = dev_upload(c, ix, rank, &X.rank)) || (rc = dev_upload(c, ix, hslot, &X.hslot)) ||
+        (rc = dev_upload(c, ix, kpos, &X.kpos)))
+        return rc;
+    X.n = n;
+    X.hbits = hbits;
+    for (int b = 0; b < 4; ++b) X.base_cnt[b] = 0;
+    for (int64_t i = 0; i < N; ++i) ++X.base_cnt[T[i]];
+    ix->s2 = X;
+    ix->s2_ready = true;
+    return AF_OK;
+}
+
+// per-context S2 scratch for a batch of n_pairs (chunks of >= chunk_bases bases)
+int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bases) {
+    if (n_pairs > c->s2_cap_pairs) {
+        af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ilist); af_free(c->s2_scan);
+        c->s2_pool = nullptr; c->s2_rmap = nullptr; c->s2_plist = c->s2_ilist = nullptr; c->s2_scan = nullptr;
+        c->s2_cap_pairs = 0;
+        const int64_t cap = std::max<int64_t>(n_pairs, 1 << 16);
+        c->s2_pool_cap = 2 * cap + (1 << 20);  // regions: candidates are a few % of the reads
+        HIPCHK(c, hipMalloc(&c->s2_pool, sizeof(S2Reg) * c->s2_pool_cap));
+        HIPCHK(c, hipMalloc(&c->s2_rmap, sizeof(int2) * 2 * cap));
+        HIPCHK(c, hipMalloc(&c->s2_plist, sizeof(int32_t) * cap));
+        HIPCHK(c, hipMalloc(&c->s2_ilist, sizeof(int32_t) * cap));
+        HIPCHK(c, hipMalloc(&c->s2_scan, sizeof(int64_t) * cap));
+        c->s2_cap_pairs = cap;
+    }
+    const int64_t mc = std::min<int64_t>(n_pairs, 2 * n_pairs * (int64_t)stride / std::max<int64_t>(chunk_bases, 1) + 2) + 1;
+    if (mc > c->s2_max_chunks) {
+        af_free(c->s2_icnt); af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
+        c->s2_icnt = nullptr; c->s2_pes = nullptr; c->s2_cstart = nullptr; c->s2_nchunks = nullptr;
+        c->s2_max_chunks = 0;
+        const int64_t m = std::max<int64_t>(mc, 64);
+        HIPCHK(c, hipMalloc(&c->s2_icnt, sizeof(int32_t) * m));
+        HIPCHK(c, hipMemset(c->s2_icnt, 0, sizeof(int32_t) * m));
+        HIPCHK(c, hipMalloc(&c->s2_pes, sizeof(S2Pes) * 4 * m));
+        HIPCHK(c, hipMalloc(&c->s2_cstart, sizeof(int64_t) * (m + 1)));
+        HIPCHK(c, hipMalloc(&c->s2_nchunks, sizeof(int32_t)));
+        c->s2_max_chunks = (int32_t)m;
+    }
+    return AF_OK;
+}
+
+int check_pe(af_ctx *c, const af_pe *e) {
+    if (e->pen_unpaired < 0 || e->max_ins < 1 || e->max_ins > 16383 || e->max_matesw < 0 || e->split_width < 0 ||
+        e->max_mem_intv < 0 || e->max_chain_gap < 1 || e->chunk_bases < 1 || e->pair_base < 0)
+        return fail(c, AF_E_INVALID, "invalid af_pe (1 <= max_ins <= 16383, chunk_bases >= 1, pair_base >= 0)");
+    return AF_OK;
+}
+
 int check_params(af_ctx *c, const af_params *p) {
     if (!p) return fail(c, AF_E_INVALID, "params is NULL");
     if (p->a <= 0 || p->b < 0 || p->o_del < 0 || p->e_del <= 0 || p->o_ins < 0 || p->e_ins <= 0 || p->w < 0 ||
@@ -138,6 +295,14 @@ void af_params_default(af_params *p) {
     p->a = 1; p->b = 4; p->o_del = 6; p->e_del = 1; p->o_ins = 6; p->e_ins = 1;
     p->pen_clip5 = 5; p->pen_clip3 = 5; p->w = 100; p->zdrop = 100;
     p->min_seed_len = 19; p->max_occ = 500; p->T = 30; p->max_ext = 16; p->max_mems = 64;
+}
+
+void af_pe_default(af_pe *e) {
+    // bwa 0.7.17 mem_opt_init paired-end options; chunk = 10,000,000 bases x threads (the
+    // reference runs `bwa mem -t <--thread>`, default 1: Anchored_Fusion.py:29)
+    e->pen_unpaired = 17; e->max_ins = 10000; e->max_matesw = 50; e->split_width = 10;
+    e->max_mem_intv = 20; e->max_chain_gap = 10000;
+    e->chunk_bases = 10000000; e->pair_base = 0;
 }
 
 int af_ctx_create(int device, af_ctx **out) {
@@ -173,6 +338,8 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
     af_free(c->d_cigar);
+    af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ilist); af_free(c->s2_scan);
+    af_free(c->s2_icnt); af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -229,13 +396,26 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
         while (hslot[s].z) s = (s + 1) & hm;
         hslot[s] = int4{(int)keys[i], starts[i], cnts[i], kpos[starts[i]]};
     }
-    // Bloom filter of the distinct 16-mers (seed filter K1): 2^bl_bits 32-bit words, ~2.4 words
-    // per key (at most 2^15 words = 128 KiB, a 6.8 kb anchor), four bits in each of two words
+    // Bloom filter of the distinct 16-mers of the bwa text that do not cross the strand boundary
+    // (K1; S2 seeds never cross it): 2^bl_bits 32-bit words, ~2.4 words per key (at most 2^15
+    // words = 128 KiB, a 6.8 kb anchor), four bits in each of two words
+    std::vector<uint8_t> T = bwa_text(anchor, n);
+    std::vector<uint32_t> tkeys;
+    tkeys.reserve(n2);
+    for (int64_t q = 0; q + AF_K <= n2; ++q) {
+        if (q < n && q + AF_K > n) continue;
+        uint32_t k = 0;
+        for (int u = 0; u < AF_K; ++u) k |= (uint32_t)T[q + u] << (2 * u);
+        tkeys.push_back(k);
+    }
+    std::sort(tkeys.begin(), tkeys.end());
+    tkeys.erase(std::unique(tkeys.begin(), tkeys.end()), tkeys.end());
+    const int64_t ntd = (int64_t)tkeys.size();
     int bl_bits = 8;
-    while ((double)(1LL << bl_bits) < 2.4 * (double)nd && bl_bits < AF_K1_MAX_BITS) ++bl_bits;
+    while ((double)(1LL << bl_bits) < 2.4 * (double)ntd && bl_bits < AF_K1_MAX_BITS) ++bl_bits;
     std::vector<uint32_t> bloom((size_t)1 << bl_bits, 0);
-    for (int64_t i = 0; i < nd; ++i) {
-        const uint64_t h = af_k1_hash(af_k1_key(keys[i]));
+    for (int64_t i = 0; i < ntd; ++i) {
+        const uint64_t h = af_k1_hash(af_k1_key(tkeys[i]));
         const uint32_t lo = (uint32_t)h, hi = (uint32_t)(h >> 32);
         bloom[(hi >> 2) & ((1u << bl_bits) - 1u)] |= af_k1_mask(lo);
         bloom[lo >> (32 - bl_bits)] |= af_k1_mask(hi);
@@ -244,6 +424,7 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
     ix->ctx = c;
     ix->bloom_host = bloom;
+    ix->text.swap(T);
     int rc = AF_OK;
     const uint32_t *bld = nullptr;
     if ((rc = dev_upload(c, ix, D, &ix->dev.D)) || (rc = dev_upload(c, ix, D2, &ix->dev.D2)) ||
@@ -347,7 +528,8 @@ int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
     if (rc) return rc;
     const int slot = (int)(c->epoch & 1);
     HIPCHK(c, af_launch_seed_filter(ix->dev, d_reads, n_reads, stride, d_lens, d_hits, c->cand,
-                                    c->ctrl + AF_HEAD_STRIDE * slot, c->ctrl + AF_HEAD_STRIDE * (slot ^ 1), c->n_cu, s));
+                                    c->ctrl + AF_HEAD_STRIDE * slot, c->ctrl + AF_HEAD_STRIDE * (slot ^ 1),
+                                    c->ctrl + AF_CTRL_S2_POOL + AF_HEAD_STRIDE * slot, c->n_cu, s));
     ++c->epoch;
     return AF_OK;
 }
@@ -364,7 +546,7 @@ int64_t af_last_candidates(af_ctx *c) {
 }
 
 int af_align_pairs_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
-                          const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream) {
+                          const int32_t *d_lens, const af_params *p, const af_pe *pe, af_aln_out *o, void *stream) {
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
     if (rc) return rc;
@@ -373,21 +555,23 @@ int af_align_pairs_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads,
     if (!o->flag || !o->pos || !o->score || !o->n_cigar || !o->hits || !o->cigar)
         return fail(c, AF_E_INVALID, "output arrays must all be non-NULL");
     if ((rc = af_seed_filter_device(c, ix, d_reads, 2 * n_pairs, stride, d_lens, o->hits, stream))) return rc;
-    return af_align_candidates_device(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream);
+    return af_align_candidates_device(c, ix, d_reads, n_pairs, stride, d_lens, p, pe, o, stream);
 }
 
-static int align_candidates(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
-                            const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream,
+static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
+                            const int32_t *d_lens, const af_params *p, const af_pe *pe, af_aln_out *o, void *stream,
                             const AfTails *tails, bool append);
 
 int af_align_candidates_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
-                               int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
-                               void *stream) {
-    return align_candidates(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream, nullptr, false);
+                               int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                               af_aln_out *o, void *stream) {
+    return align_candidates(c, const_cast<af_index *>(ix), d_reads, n_pairs, stride, d_lens, p, pe, o, stream, nullptr,
+                            false);
 }
 
 int af_align_candidates_tails_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs,
-                                     int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *o,
+                                     int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                                     af_aln_out *o,
                                      int32_t min_clip, int64_t read_base, int32_t append, int64_t cap,
                                      uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read,
                                      int32_t *d_n_tails, void *stream) {
@@ -397,37 +581,57 @@ int af_align_candidates_tails_device(af_ctx *c, const af_index *ix, const uint8_
     if (read_base < 0 || read_base + 2 * n_pairs > (1LL << 31) - 1)
         return fail(c, AF_E_INVALID, "read_base + reads exceeds int32");
     const AfTails t{d_tails, d_tail_lens, d_tail_read, d_n_tails, cap, read_base, min_clip < 1 ? 1 : min_clip};
-    return align_candidates(c, ix, d_reads, n_pairs, stride, d_lens, p, o, stream, &t, append != 0);
+    return align_candidates(c, const_cast<af_index *>(ix), d_reads, n_pairs, stride, d_lens, p, pe, o, stream, &t,
+                            append != 0);
 }
 
-static int align_candidates(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
-                            const int32_t *d_lens, const af_params *p, af_aln_out *o, void *stream,
+static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
+                            const int32_t *d_lens, const af_params *p, const af_pe *pe_in, af_aln_out *o, void *stream,
                             const AfTails *tails, bool append) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
     if (rc) return rc;
+    if (p->w > 300) return fail(c, AF_E_INVALID, "af_align_*: band w %d above 300", p->w);
+    af_pe pe;
+    if (pe_in) pe = *pe_in;
+    else af_pe_default(&pe);
+    if ((rc = check_pe(c, &pe))) return rc;
     if (n_pairs <= 0) return n_pairs == 0 ? AF_OK : fail(c, AF_E_INVALID, "n_pairs < 0");
+    if (n_pairs > (1LL << 30)) return fail(c, AF_E_INVALID, "n_pairs above 2^30");
     if (!o->flag || !o->pos || !o->score || !o->n_cigar || !o->hits || !o->cigar)
         return fail(c, AF_E_INVALID, "output arrays must all be non-NULL");
     if ((((uintptr_t)o->flag | (uintptr_t)o->pos | (uintptr_t)o->score | (uintptr_t)o->n_cigar) & 7) != 0)
         return fail(c, AF_E_INVALID, "flag/pos/score/n_cigar arrays must be 8-byte aligned");
     if (2 * n_pairs > c->cap_reads) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
-    const int64_t nr = 2 * n_pairs;
+    (void)hipSetDevice(c->device);
     if ((rc = ensure_zscratch(c))) return rc;
+    if ((rc = ensure_s2_text(c, ix))) return rc;
+    if ((rc = ensure_s2_work(c, n_pairs, stride, pe.chunk_bases))) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (c->epoch == 0) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
     const int slot = (int)((c->epoch - 1) & 1);
     int32_t *n_cand = c->ctrl + AF_HEAD_STRIDE * slot;
-    HIPCHK(c, af_launch_align(ix->dev, d_reads, nr, stride, d_lens, *p, c->cand, n_cand, c->ctrl + AF_CTRL_HEADS2,
-                              c->recs, o->cigar, c->zscratch, c->n_slots, s));
+    S2Work w{};
+    w.pool = c->s2_pool; w.pool_cap = c->s2_pool_cap;
+    w.pool_n = c->ctrl + AF_CTRL_S2_POOL + AF_HEAD_STRIDE * slot;
+    w.rmap = c->s2_rmap;
+    w.plist = c->s2_plist;
+    w.n_plist = c->ctrl + AF_CTRL_S2_NPAIRS + AF_HEAD_STRIDE * slot;
+    w.ilist = c->s2_ilist; w.icnt = c->s2_icnt; w.pes = c->s2_pes;
+    w.cstart = c->s2_cstart; w.n_chunks = c->s2_nchunks; w.max_chunks = c->s2_max_chunks;
+    w.heads_k2 = c->ctrl + AF_CTRL_HEADS2; w.heads_k3 = c->ctrl + AF_CTRL_S2_HEADS3;
+    S2Opt opt{pe.pen_unpaired, pe.max_ins, pe.max_matesw, pe.split_width, pe.max_mem_intv, pe.max_chain_gap, pe.pair_base};
+    HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, pe.chunk_bases, c->s2_cstart, c->s2_scan, c->s2_max_chunks,
+                                  c->s2_nchunks, s));
     if (tails && !append) HIPCHK(c, hipMemsetAsync(tails->n_tails, 0, 4, s));
-    HIPCHK(c, af_launch_pairs(n_pairs, o->hits, c->recs, *o, c->ctrl, s, d_reads, stride, d_lens, tails));
+    HIPCHK(c, af_launch_s2(ix->s2, d_reads, n_pairs, stride, d_lens, *p, opt, o->hits, c->cand, n_cand, w, *o,
+                           c->zscratch, c->n_cu, tails, s));
     return AF_OK;
 }
 
 int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t n_pairs, int32_t stride,
-                   const int32_t *lens, const af_params *p, af_aln_out *out) {
+                   const int32_t *lens, const af_params *p, const af_pe *pe, af_aln_out *out) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (!c || !ix || !out || (!reads && n_pairs)) return fail(c, AF_E_INVALID, "null argument");
     if (n_pairs == 0) return AF_OK;
@@ -460,7 +664,7 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
         HIPCHK(c, hipMemcpyAsync(c->d_lens, lens, 4 * nr, hipMemcpyHostToDevice, s));
     }
     af_aln_out d{c->d_flag, c->d_pos, c->d_score, c->d_ncig, c->d_hits, c->d_cigar};
-    int rc = af_align_pairs_device(c, ix, c->d_reads, n_pairs, stride, lens ? c->d_lens : nullptr, p, &d, s);
+    int rc = af_align_pairs_device(c, ix, c->d_reads, n_pairs, stride, lens ? c->d_lens : nullptr, p, pe, &d, s);
     if (rc) return rc;
     if (out->flag) HIPCHK(c, hipMemcpyAsync(out->flag, c->d_flag, 4 * nr, hipMemcpyDeviceToHost, s));
     if (out->pos) HIPCHK(c, hipMemcpyAsync(out->pos, c->d_pos, 4 * nr, hipMemcpyDeviceToHost, s));
@@ -469,27 +673,30 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
     if (out->hits) HIPCHK(c, hipMemcpyAsync(out->hits, c->d_hits, 4 * nr, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (out->cigar) {
-        // only candidate reads have CIGARs: gather their rows on the device and copy those
+        // only reads of listed pairs (a K1 candidate in the pair) have CIGARs: gather the rows of
+        // both reads of every listed pair on the device and copy those
         const int slot = (int)((c->epoch - 1) & 1);
-        int32_t nc = 0;
-        HIPCHK(c, hipMemcpy(&nc, c->ctrl + AF_HEAD_STRIDE * slot, sizeof nc, hipMemcpyDeviceToHost));
-        if (nc > 0) {
-            if (nc > c->cap_packed) {
+        int32_t np = 0;
+        HIPCHK(c, hipMemcpy(&np, c->ctrl + AF_CTRL_S2_NPAIRS + AF_HEAD_STRIDE * slot, sizeof np, hipMemcpyDeviceToHost));
+        if (np > 0) {
+            const int64_t nrows = 2 * (int64_t)np;
+            if (nrows > c->cap_packed) {
                 af_free(c->d_packed); c->d_packed = nullptr; c->cap_packed = 0;
-                HIPCHK(c, hipMalloc(&c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * (size_t)nc));
-                c->cap_packed = nc;
+                HIPCHK(c, hipMalloc(&c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * (size_t)nrows));
+                c->cap_packed = nrows;
             }
-            hipLaunchKernelGGL(k_gather_cigar, dim3((unsigned)std::min<int64_t>(4096, (nc * 8 + 255) / 256)), dim3(256),
-                               0, s, c->cand, (int64_t)nc, c->d_cigar, c->d_packed);
+            hipLaunchKernelGGL(k_gather_cigar, dim3((unsigned)std::min<int64_t>(4096, (nrows * 8 + 255) / 256)),
+                               dim3(256), 0, s, c->s2_plist, nrows, c->d_cigar, c->d_packed);
             HIPCHK(c, hipGetLastError());
-            std::vector<int32_t> ids((size_t)nc);
-            std::vector<uint32_t> rows((size_t)nc * AF_MAX_CIGAR);
-            HIPCHK(c, hipMemcpyAsync(ids.data(), c->cand, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipMemcpyAsync(rows.data(), c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * nc, hipMemcpyDeviceToHost, s));
+            std::vector<int32_t> ids((size_t)np);
+            std::vector<uint32_t> rows((size_t)nrows * AF_MAX_CIGAR);
+            HIPCHK(c, hipMemcpyAsync(ids.data(), c->s2_plist, sizeof(int32_t) * np, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(rows.data(), c->d_packed, sizeof(uint32_t) * AF_MAX_CIGAR * nrows,
+                                     hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
-            for (int32_t i = 0; i < nc; ++i)
-                memcpy(out->cigar + (int64_t)ids[i] * AF_MAX_CIGAR, rows.data() + (size_t)i * AF_MAX_CIGAR,
-                       sizeof(uint32_t) * AF_MAX_CIGAR);
+            for (int64_t i = 0; i < nrows; ++i)
+                memcpy(out->cigar + (2 * (int64_t)ids[i >> 1] + (i & 1)) * AF_MAX_CIGAR,
+                       rows.data() + (size_t)i * AF_MAX_CIGAR, sizeof(uint32_t) * AF_MAX_CIGAR);
         }
     }
     return AF_OK;

@@ -1,0 +1,1827 @@
+// s2.hip -- S2 on the GPU: `bwa mem -M -t T <anchor.fa> fq1 fq2` (Anchored_Fusion.py:182) as
+// bwa 0.7.17 computes it in paired-end mode.  oracle/bwa_pe.c is the bit-exact contract; each
+// device routine names the bwa routine (and oracle function) it restates.
+//
+// Kernels, one launch each per batch, all on the caller's stream (after K1, seed_filter.hip):
+//   K2  k_s2_regions   one wave per candidate read (K1 list, per-XCD dequeue heads): SMEM
+//                      seeds (mem_collect_intv's three passes, from the read's MEMs against the
+//                      bwa text) -> mem_chain (klib kbtree) -> mem_chain_flt -> mem_chain2aln
+//                      (ksw_extend2 on the wave, ksw_dp.h) -> mem_sort_dedup_patch; the regions
+//                      go to a pool, one atomic per read
+//   K3a k_s2_classify  one thread per pair: pairs without a candidate read get their unmapped
+//                      records here (the bulk of the batch, 16 B/pair of nontemporal stores);
+//                      the rest are listed; unique pairs add an insert size to their chunk
+//   K3b k_s2_pestat    one workgroup per bwa chunk: mem_pestat from an LDS histogram
+//   K3c k_s2_pairs     one wave per listed pair: mate rescue (mem_matesw, ksw_align2 with the
+//                      striped-SW semantics), mem_mark_primary_se (hash tie-break), mem_pair,
+//                      mem_sam_pe's record choice, mem_reg2aln (bwa_gen_cigar2 on the wave) and
+//                      mem_aln2sam's flags; split-read tails for the partner search
+//
+// Serial parts of bwa (kbtree, klib introsort, the chain and pair loops) run on lane 0 over
+// per-wave LDS state; the DP and the list scans run on the whole wave.  Double-precision
+// arithmetic (pestat, patching, pair scores) is kept unfused so it rounds as the C oracle does.
+#include "ksw_dp.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+#ifndef AF_S2_WPS
+#define AF_S2_WPS 5  // k_s2_regions waves per SIMD (LDS: ~7 KB per wave)
+#endif
+
+struct S2Pm { int16_t s, t; int32_t r; };          // a MEM: query [s, t), text position r
+struct S2Si { int16_t qb, qe, cnt, occ0; };        // a seed interval and its occurrences
+struct S2Seed { int32_t rbeg; int16_t qbeg, len; };  // mem_seed_t (score = len)
+struct S2Chain { int16_t n, first, kept, seed0; int32_t w, pos; };  // mem_chain_t
+constexpr int KB_T = 5, KB_MAXK = 2 * KB_T - 1, KB_NODES = 2 * AF_S2_MAX_CHAIN + 4;
+struct S2Kb { uint8_t n, internal, key[KB_MAXK], ptr[KB_MAXK + 1]; };
+
+struct __attribute__((aligned(16))) S2Lds {
+    union {
+        S2Pm pm[AF_S2_MAX_PMEM];          // seeding: the read's MEMs
+        S2Kb kb[KB_NODES];                // chaining: the kbtree
+        S2Chain chtmp[AF_S2_MAX_CHAIN];   // chain reordering
+        S2Reg reg[AF_S2_MAX_REG];         // extension: regions
+    } x;
+    union {
+        struct { S2Si si[AF_S2_MAX_SEED]; int32_t occ[AF_S2_MAX_OCC]; int32_t tmp[AF_S2_MAX_OCC]; } a;
+        struct { S2Seed seed[AF_S2_MAX_OCC]; int16_t srt[AF_S2_MAX_OCC]; } c;
+    } y;
+    S2Seed pool[AF_S2_MAX_OCC];
+    int16_t next[AF_S2_MAX_OCC];
+    S2Chain ch[AF_S2_MAX_CHAIN];
+    int16_t last_of[AF_S2_MAX_CHAIN];
+    uint8_t order[AF_S2_MAX_CHAIN];
+    int32_t cnt[8];   // [0] MEMs [1] intervals [2] occurrences [3] overflow [4] chains [5] kb root [6] kb nodes [7] regions
+    int64_t rmax[2];
+    int32_t misc[4];
+};
+__shared__ S2Lds g_s2;
+
+// ---- small wave helpers --------------------------------------------------------------------
+__device__ __forceinline__ int wave_min(int v) { return -wave_max(-v); }
+__device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
+    return __builtin_popcountll(m & ((1ull << lane) - 1ull));
+}
+__device__ __forceinline__ uint32_t getT16(const DevText &X, int64_t pos) {
+    const int64_t wi = pos >> 4;
+    const int sh = (int)(pos & 15) * 2;
+    const uint32_t lo = X.T2[wi], hi = X.T2[wi + 1];
+    return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+}
+
+// ---- klib ksort.h introsort (lane 0; unstable -- tie orders are bwa's) --------------------
+template <class T, class LT>
+__device__ void ks_ins(T *a, int s, int t, LT lt) {
+    for (int i = s + 1; i < t; ++i)
+        for (int j = i; j > s && lt(a[j], a[j - 1]); --j) { T sw = a[j]; a[j] = a[j - 1]; a[j - 1] = sw; }
+}
+template <class T, class LT>
+__device__ void ks_comb(T *a, int n, LT lt) {
+    const double shrink_factor = 1.2473309501039786540366528676643;
+    int do_swap;
+    size_t gap = (size_t)n;
+    do {
+        if (gap > 2) {
+            gap = (size_t)((double)gap / shrink_factor);
+            if (gap == 9 || gap == 10) gap = 11;
+        }
+        do_swap = 0;
+        for (int i = 0; i < n - (int)gap; ++i) {
+            const int j = i + (int)gap;
+            if (lt(a[j], a[i])) { T t = a[i]; a[i] = a[j]; a[j] = t; do_swap = 1; }
+        }
+    } while (do_swap || gap > 2);
+    if (gap != 1) ks_ins(a, 0, n, lt);
+}
+template <class T, class LT>
+__device__ void ks_introsort(T *a, int n, LT lt) {
+    if (n < 1) return;
+    if (n == 2) {
+        if (lt(a[1], a[0])) { T sw = a[0]; a[0] = a[1]; a[1] = sw; }
+        return;
+    }
+    int d;
+    for (d = 2; (1ul << d) < (unsigned long)n; ++d) ;
+    int stl[24], str[24], std_[24], top = 0;
+    int s = 0, t = n - 1;
+    d <<= 1;
+    for (;;) {
+        if (s < t) {
+            if (--d == 0) { ks_comb(a + s, t - s + 1, lt); t = s; continue; }
+            int i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            if (lt(a[k], a[i])) {
+                if (lt(a[k], a[j])) k = j;
+            } else k = lt(a[j], a[i]) ? i : j;
+            const T rp = a[k];
+            if (k != t) { T sw = a[k]; a[k] = a[t]; a[t] = sw; }
+            for (;;) {
+                do ++i; while (lt(a[i], rp));
+                do --j; while (i <= j && lt(rp, a[j]));
+                if (j <= i) break;
+                T sw = a[i]; a[i] = a[j]; a[j] = sw;
+            }
+            { T sw = a[i]; a[i] = a[t]; a[t] = sw; }
+            if (i - s > t - i) {
+                if (i - s > 16) { stl[top] = s; str[top] = i - 1; std_[top] = d; ++top; }
+                s = t - i > 16 ? i + 1 : t;
+            } else {
+                if (t - i > 16) { stl[top] = i + 1; str[top] = t; std_[top] = d; ++top; }
+                s = i - s > 16 ? s : i - 1;
+            }
+        } else {
+            if (top == 0) { ks_ins(a, 0, n, lt); return; }
+            --top; s = stl[top]; t = str[top]; d = std_[top];
+        }
+    }
+}
+
+// utils.h hash_64
+__device__ __forceinline__ uint64_t hash_64(uint64_t key) {
+    key += ~(key << 32);
+    key ^= (key >> 22);
+    key += ~(key << 13);
+    key ^= (key >> 8);
+    key += (key << 3);
+    key ^= (key >> 15);
+    key += ~(key << 27);
+    key ^= (key >> 31);
+    return key;
+}
+
+// =========================================================================== K2: seeds
+// MEMs >= min_seed_len of the read (L.q / L.pk / L.nm) against the bwa text T: lanes over
+// query offsets, the 16-mer hash in L2, right extension by 2-bit word compares (oracle
+// find_pmems)
+__device__ void s2_pmems(const DevText &X, int l, int msl, int lane) {
+    DpLds &L = g_dp;
+    S2Lds &S = g_s2;
+    const int64_t N = 2 * X.n;
+    const uint32_t hm = (1u << X.hbits) - 1u;
+    for (int s = lane; s + AF_K <= l; s += 64) {
+        const int wq = s >> 4, sq = s & 15;
+        const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
+        if (((L.nm[wq] | (L.nm[wq + 1] << 16)) >> sq) & 0xFFFFu) continue;
+        int cnt = 0, st = 0, pos0 = 0;
+        uint32_t sl = af_fmix(k) & hm;
+        for (;;) {
+            const int4 e = X.hslot[sl];
+            if (e.z == 0) break;
+            if ((uint32_t)e.x == k) { cnt = e.z; st = e.y; pos0 = e.w; break; }
+            sl = (sl + 1) & hm;
+        }
+        for (int o = 0; o < cnt; ++o) {
+            const int64_t r0 = o == 0 ? (int64_t)pos0 : (int64_t)X.kpos[st + o];
+            if (s > 0) {
+                const int qc = L.q[s - 1];
+                if (qc < 4 && r0 > 0 && X.T[r0 - 1] == qc) continue;  // not left-maximal
+            }
+            int len = AF_K;
+            for (;;) {
+                const int qp = s + len;
+                const int64_t rp = r0 + len;
+                const int64_t room64 = min((int64_t)(l - qp), N - rp);
+                if (room64 <= 0) break;
+                const int room = (int)min(room64, (int64_t)16);
+                const int wp = qp >> 4, sp = qp & 15;
+                const uint32_t qk = __builtin_amdgcn_alignbit(L.pk[wp + 1], L.pk[wp], 2 * sp);
+                const int qn = __builtin_ctz((((L.nm[wp] | (L.nm[wp + 1] << 16)) >> sp) & 0xFFFFu) | 0x10000u);
+                const uint32_t x = qk ^ getT16(X, rp);
+                const int eq = x ? (__builtin_ctz(x) >> 1) : 16;
+                const int step = min(min(eq, room), qn);
+                len += step;
+                if (step < 16) break;
+            }
+            if (len < msl) continue;
+            const int slot = atomicAdd(&S.cnt[0], 1);
+            if (slot < AF_S2_MAX_PMEM) S.x.pm[slot] = S2Pm{(int16_t)s, (int16_t)(s + len), (int32_t)r0};
+        }
+    }
+}
+
+// occurrences of q[b, e) (e - b >= min_seed_len) = the MEMs covering it (oracle count_cov)
+__device__ __forceinline__ int s2_count_cov(int npm, int b, int e, int lane) {
+    int c = 0;
+    for (int k0 = 0; k0 < npm; k0 += 64) {
+        const int k = k0 + lane;
+        bool v = false;
+        if (k < npm) {
+            const S2Pm m = g_s2.x.pm[k];
+            v = m.s <= b && e <= m.t;
+        }
+        c += __builtin_popcountll(__ballot(v));
+    }
+    return c;
+}
+
+// push seed interval [b, e) with its occurrences in suffix-rank (bwt_sa) order (oracle
+// push_intv).  cnt0 >= 0 forces an occurrence-free interval (bwt_smem1 on an absent base).
+__device__ void s2_push_intv(const DevText &X, int npm, int b, int e, int lane, bool empty = false) {
+    S2Lds &S = g_s2;
+    if (S.cnt[3]) return;
+    const int si = S.cnt[1], occ0 = S.cnt[2];
+    if (si >= AF_S2_MAX_SEED) {
+        wave_sync();
+        if (lane == 0) S.cnt[3] = 1;
+        wave_sync();
+        return;
+    }
+    int c = 0;
+    if (!empty) {
+        for (int k0 = 0; k0 < npm; k0 += 64) {
+            const int k = k0 + lane;
+            bool v = false;
+            S2Pm m{};
+            if (k < npm) {
+                m = S.x.pm[k];
+                v = m.s <= b && e <= m.t;
+            }
+            const uint64_t msk = __ballot(v);
+            if (v) {
+                const int idx = occ0 + c + lanes_below(msk, lane);
+                if (idx < AF_S2_MAX_OCC) {
+                    const int32_t pos = m.r + (b - m.s);
+                    S.y.a.occ[idx] = pos;
+                    S.y.a.tmp[idx] = X.rank[pos];
+                }
+            }
+            c += __builtin_popcountll(msk);
+        }
+    }
+    wave_sync();
+    if (occ0 + c > AF_S2_MAX_OCC) {
+        if (lane == 0) S.cnt[3] = 1;
+        wave_sync();
+        return;
+    }
+    // rank sort of occ[occ0, occ0 + c): each lane takes up to two entries (c <= 128)
+    int pa = 0, ra = 0, pb = 0, rb = 0, da = -1, db = -1;
+    if (lane < c) { pa = S.y.a.occ[occ0 + lane]; ra = S.y.a.tmp[occ0 + lane]; }
+    if (lane + 64 < c) { pb = S.y.a.occ[occ0 + lane + 64]; rb = S.y.a.tmp[occ0 + lane + 64]; }
+    if (lane < c || lane + 64 < c) {
+        int ca = 0, cb = 0;
+        for (int j = 0; j < c; ++j) {
+            const int rj = S.y.a.tmp[occ0 + j];
+            ca += rj < ra;
+            cb += rj < rb;
+        }
+        if (lane < c) da = ca;
+        if (lane + 64 < c) db = cb;
+    }
+    wave_sync();
+    if (da >= 0) S.y.a.occ[occ0 + da] = pa;
+    if (db >= 0) S.y.a.occ[occ0 + db] = pb;
+    if (lane == 0) {
+        S.y.a.si[si] = S2Si{(int16_t)b, (int16_t)e, (int16_t)c, (int16_t)occ0};
+        S.cnt[1] = si + 1;
+        S.cnt[2] = occ0 + c;
+    }
+    wave_sync();
+}
+
+// bwt_smem1(x, min_intv = m) restricted to outputs >= min_seed_len (oracle smem_at)
+__device__ void s2_smem_at(const DevText &X, int npm, int l, int msl, int x, int m, int lane) {
+    DpLds &L = g_dp;
+    S2Lds &S = g_s2;
+    const int c0 = X.base_cnt[L.q[x]];
+    if (c0 < m) {  // degenerate: the single base occurs fewer than m times
+        if (x + msl > l) return;
+        for (int i = x + 1; i < x + msl; ++i) if (L.q[i] > 3) return;
+        if (s2_count_cov(npm, x, x + msl, lane) != c0) return;
+        int e1 = x + msl;
+        while (e1 < l && L.q[e1] < 4 && s2_count_cov(npm, x, e1 + 1, lane) == c0) ++e1;
+        s2_push_intv(X, npm, x, e1, lane, c0 == 0);
+        return;
+    }
+    int prev_b = -1, prev_e = -1;
+    for (;;) {
+        // the next distinct start among MEMs holding x
+        int bmin = 1 << 30;
+        for (int k0 = 0; k0 < npm; k0 += 64) {
+            const int k = k0 + lane;
+            if (k < npm) {
+                const S2Pm mm = S.x.pm[k];
+                if (mm.s <= x && x < mm.t && mm.s > prev_b) bmin = min(bmin, (int)mm.s);
+            }
+        }
+        const int b = wave_min(bmin);
+        if (b >= (1 << 30)) break;
+        // e(b): the largest end t_j (MEMs holding x, s <= b) with >= m such MEMs ending at or after t_j
+        int cand = -1;
+        for (int k0 = 0; k0 < npm; k0 += 64) {
+            const int j = k0 + lane;
+            if (j < npm) {
+                const S2Pm mj = S.x.pm[j];
+                if (mj.s <= b && x < mj.t) {
+                    int cj = 0;
+                    for (int u = 0; u < npm; ++u) {
+                        const S2Pm mu = S.x.pm[u];
+                        cj += mu.s <= b && x < mu.t && mu.t >= mj.t;
+                    }
+                    if (cj >= m) cand = max(cand, (int)mj.t);
+                }
+            }
+        }
+        const int e = wave_max(cand);
+        if (e >= 0 && e > prev_e) {
+            if (e - b >= msl) s2_push_intv(X, npm, b, e, lane);
+            prev_e = e;
+        }
+        prev_b = b;
+    }
+}
+
+// mem_collect_intv (oracle collect_intv): pass 1 SMEMs, pass 2 re-seeding, pass 3
+// bwt_seed_strategy1; then the intervals sorted by (qb, qe).  Sets S.cnt[3] on overflow.
+__device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Opt &o, int l, int lane) {
+    DpLds &L = g_dp;
+    S2Lds &S = g_s2;
+    const int msl = p.min_seed_len;
+    s2_pmems(X, l, msl, lane);
+    wave_sync();
+    const int npm_all = S.cnt[0];
+    if (npm_all > AF_S2_MAX_PMEM) {
+        if (lane == 0) S.cnt[3] = 1;
+        wave_sync();
+        return;
+    }
+    const int npm = npm_all;
+    // pass 1: maximal MEM query intervals, each once (keep the lowest index of equal ones)
+    for (int k0 = 0; k0 < npm; k0 += 64) {
+        const int k = k0 + lane;
+        bool keep = false;
+        int s = 0, t = 0;
+        if (k < npm) {
+            s = S.x.pm[k].s; t = S.x.pm[k].t;
+            keep = true;
+            for (int j = 0; j < npm && keep; ++j) {
+                const S2Pm mj = S.x.pm[j];
+                if (mj.s == s && mj.t == t) { if (j < k) keep = false; continue; }
+                if (mj.s <= s && t <= mj.t) keep = false;
+            }
+        }
+        uint64_t msk = __ballot(keep);
+        while (msk) {
+            const int ln = __builtin_ctzll(msk);
+            msk &= msk - 1;
+            const int bs = __builtin_amdgcn_readlane(s, ln), bt = __builtin_amdgcn_readlane(t, ln);
+            s2_push_intv(X, npm, bs, bt, lane);
+        }
+    }
+    if (S.cnt[3]) return;
+    // pass 2
+    const int split_len = (int)((float)msl * 1.5f + .499);
+    const int n1 = S.cnt[1];
+    for (int k = 0; k < n1 && !S.cnt[3]; ++k) {
+        const S2Si v = S.y.a.si[k];
+        if (v.qe - v.qb < split_len || v.cnt > o.split_width) continue;
+        s2_smem_at(X, npm, l, msl, (v.qb + v.qe) >> 1, v.cnt + 1, lane);
+    }
+    // pass 3 (bwt_seed_strategy1 with min_len = min_seed_len, max_intv = max_mem_intv)
+    if (o.max_mem_intv > 0) {
+        const int mi = o.max_mem_intv;
+        int x = 0;
+        while (x < l && !S.cnt[3]) {
+            if (L.q[x] > 3) { ++x; continue; }
+            // e* = the first end >= x + msl + 1 at which q[x, e) occurs < max_mem_intv times
+            int na = 0;
+            for (int k0 = 0; k0 < npm; k0 += 64) {
+                const int k = k0 + lane;
+                na += __builtin_popcountll(__ballot(k < npm && S.x.pm[k].s <= x && S.x.pm[k].t > x + msl));
+            }
+            int em = -1;
+            if (na >= mi) {
+                int cand = -1;
+                for (int k0 = 0; k0 < npm; k0 += 64) {
+                    const int j = k0 + lane;
+                    if (j < npm && S.x.pm[j].s <= x) {
+                        const int tj = S.x.pm[j].t;
+                        int cj = 0;
+                        for (int u = 0; u < npm; ++u) cj += S.x.pm[u].s <= x && S.x.pm[u].t >= tj;
+                        if (cj >= mi) cand = max(cand, tj);
+                    }
+                }
+                em = wave_max(cand);
+            }
+            const int es = max(x + msl + 1, em + 1);
+            int pn = l;  // first N after x
+            for (int i = x + 1 + lane; i < min(es, l); i += 64)
+                if (L.q[i] > 3) { pn = min(pn, i); }
+            pn = wave_min(pn);
+            if (pn < min(es, l)) { x = pn + 1; continue; }
+            if (es > l) { x = l; continue; }
+            const int c = s2_count_cov(npm, x, es, lane);
+            if (c > 0) s2_push_intv(X, npm, x, es, lane);
+            x = es;
+        }
+    }
+    if (S.cnt[3]) return;
+    // sort by (qb, qe): equal intervals are identical, any order among them
+    const int ns = S.cnt[1];
+    S2Si mine{};
+    int dest = -1;
+    if (lane < ns) {
+        mine = S.y.a.si[lane];
+        const int key = (int)mine.qb << 16 | (int)mine.qe;
+        int d = 0;
+        for (int j = 0; j < ns; ++j) {
+            const S2Si sj = S.y.a.si[j];
+            const int kj = (int)sj.qb << 16 | (int)sj.qe;
+            d += kj < key || (kj == key && j < lane);
+        }
+        dest = d;
+    }
+    wave_sync();
+    if (dest >= 0) S.y.a.si[dest] = mine;
+    wave_sync();
+}
+
+// =========================================================================== K2: chains
+// klib kbtree (t = 5) over chain indices keyed by chain pos; lane 0 only (oracle kb_*)
+__device__ __forceinline__ int kb_cmp(int x, int32_t kpos) {
+    const int32_t a = g_s2.ch[x].pos;
+    return (kpos < a) - (a < kpos);
+}
+__device__ int kb_getp_aux(const S2Kb &x, int32_t kpos, int *r) {
+    int tr, *rr, begin = 0, end = x.n;
+    if (x.n == 0) return -1;
+    rr = r ? r : &tr;
+    while (begin < end) {
+        const int mid = (begin + end) >> 1;
+        if (kb_cmp(x.key[mid], kpos) < 0) begin = mid + 1;
+        else end = mid;
+    }
+    if (begin == x.n) { *rr = 1; return x.n - 1; }
+    if ((*rr = -kb_cmp(x.key[begin], kpos)) < 0) --begin;
+    return begin;
+}
+__device__ int kb_new(int internal) {
+    S2Lds &S = g_s2;
+    const int zi = S.cnt[6]++;
+    S2Kb &z = S.x.kb[zi];
+    z.n = 0; z.internal = (uint8_t)internal;
+    return zi;
+}
+__device__ int kb_lower(int32_t kpos) {
+    S2Lds &S = g_s2;
+    int r = 0, lower = -1, xi = S.cnt[5];
+    while (xi >= 0) {
+        const S2Kb &x = S.x.kb[xi];
+        const int i = kb_getp_aux(x, kpos, &r);
+        if (i >= 0 && r == 0) return x.key[i];
+        if (i >= 0) lower = x.key[i];
+        if (!x.internal) return lower;
+        xi = x.ptr[i + 1];
+    }
+    return lower;
+}
+__device__ void kb_split(int xi, int i, int yi) {
+    S2Lds &S = g_s2;
+    const int zi = kb_new(S.x.kb[yi].internal);
+    S2Kb &x = S.x.kb[xi], &y = S.x.kb[yi], &z = S.x.kb[zi];
+    z.n = KB_T - 1;
+    for (int u = 0; u < KB_T - 1; ++u) z.key[u] = y.key[KB_T + u];
+    if (y.internal)
+        for (int u = 0; u < KB_T; ++u) z.ptr[u] = y.ptr[KB_T + u];
+    y.n = KB_T - 1;
+    for (int u = x.n; u >= i + 1; --u) x.ptr[u + 1] = x.ptr[u];
+    x.ptr[i + 1] = (uint8_t)zi;
+    for (int u = x.n - 1; u >= i; --u) x.key[u + 1] = x.key[u];
+    x.key[i] = y.key[KB_T - 1];
+    ++x.n;
+}
+__device__ void kb_putp(int k) {
+    S2Lds &S = g_s2;
+    const int32_t kpos = S.ch[k].pos;
+    int xi = S.cnt[5];
+    if (S.x.kb[xi].n == KB_MAXK) {
+        const int si = kb_new(1);
+        S.x.kb[si].ptr[0] = (uint8_t)xi;
+        S.cnt[5] = si;
+        kb_split(si, 0, xi);
+        xi = si;
+    }
+    for (;;) {  // __kb_putp_aux, iteratively
+        S2Kb &x = S.x.kb[xi];
+        if (!x.internal) {
+            const int i = kb_getp_aux(x, kpos, nullptr);
+            for (int u = x.n - 1; u >= i + 1; --u) x.key[u + 1] = x.key[u];
+            x.key[i + 1] = (uint8_t)k;
+            ++x.n;
+            return;
+        }
+        int i = kb_getp_aux(x, kpos, nullptr) + 1;
+        if (S.x.kb[x.ptr[i]].n == KB_MAXK) {
+            kb_split(xi, i, x.ptr[i]);
+            if (kb_cmp(S.x.kb[xi].key[i], kpos) > 0) ++i;
+        }
+        xi = S.x.kb[xi].ptr[i];
+    }
+}
+__device__ int kb_traverse() {
+    S2Lds &S = g_s2;
+    int stk_node[8], stk_i[8], top = 0, n = 0;
+    stk_node[0] = S.cnt[5]; stk_i[0] = 0;
+    // in-order: for a node, child[i] then key[i] for i < n, then child[n]
+    if (!S.x.kb[stk_node[0]].internal) {
+        const S2Kb &x = S.x.kb[stk_node[0]];
+        for (int i = 0; i < x.n; ++i) S.order[n++] = x.key[i];
+        return n;
+    }
+    top = 1;
+    while (top > 0) {
+        const int xi = stk_node[top - 1];
+        const int i = stk_i[top - 1];
+        const S2Kb &x = S.x.kb[xi];
+        if (!x.internal) {
+            for (int u = 0; u < x.n; ++u) S.order[n++] = x.key[u];
+            --top;
+            continue;
+        }
+        if (i > x.n) { --top; continue; }
+        stk_i[top - 1] = i + 1;
+        if (i > 0) S.order[n++] = x.key[i - 1];
+        stk_node[top] = x.ptr[i]; stk_i[top] = 0; ++top;
+    }
+    return n;
+}
+
+// test_and_merge (lane 0; oracle test_and_merge)
+__device__ int s2_test_and_merge(int ci, const S2Seed &p, int64_t l_pac, int w, int max_chain_gap) {
+    S2Lds &S = g_s2;
+    S2Chain &c = S.ch[ci];
+    const S2Seed first = S.pool[c.seed0], last = S.pool[S.last_of[ci]];
+    const int64_t qend = (int64_t)last.qbeg + last.len, rend = (int64_t)last.rbeg + last.len;
+    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && (int64_t)p.rbeg + p.len <= rend)
+        return 1;
+    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return 0;
+    const int64_t x = p.qbeg - last.qbeg, y = (int64_t)p.rbeg - last.rbeg;
+    if (y >= 0 && x - y <= w && y - x <= w && x - last.len < max_chain_gap && y - last.len < max_chain_gap) {
+        if (S.cnt[2] >= AF_S2_MAX_OCC) return -1;
+        const int k = S.cnt[2]++;
+        S.pool[k] = p;
+        S.next[k] = -1;
+        S.next[S.last_of[ci]] = (int16_t)k;
+        S.last_of[ci] = (int16_t)k;
+        ++c.n;
+        return 1;
+    }
+    return 0;
+}
+
+// mem_chain (lane 0; oracle mem_chain): returns the chain count, -1 on overflow.  On return the
+// chains are in S.ch in tree order, their seeds contiguous in S.y.c.seed.
+__device__ int s2_mem_chain(const DevText &X, const af_params &p, const S2Opt &o) {
+    S2Lds &S = g_s2;
+    const int64_t l_pac = X.n;
+    const int nsi = S.cnt[1];
+    // the interval list (si/occ) stays in S.y.a while the pool fills; the pool count reuses cnt[2]
+    int nocc_used = 0;
+    (void)nocc_used;
+    S.cnt[2] = 0;
+    S.cnt[4] = 0;
+    S.cnt[5] = -1;
+    S.cnt[6] = 0;
+    S.cnt[5] = kb_new(0);
+    for (int i = 0; i < nsi; ++i) {
+        const S2Si v = S.y.a.si[i];
+        const int slen = v.qe - v.qb;
+        const int step = v.cnt > p.max_occ ? v.cnt / p.max_occ : 1;
+        for (int k = 0, count = 0; k < v.cnt && count < p.max_occ; k += step, ++count) {
+            S2Seed s;
+            s.rbeg = S.y.a.occ[v.occ0 + k];
+            s.qbeg = v.qb;
+            s.len = (int16_t)slen;
+            if (s.rbeg < l_pac && (int64_t)s.rbeg + s.len > l_pac) continue;  // bns_intv2rid < 0
+            bool to_add = false;
+            if (S.cnt[4]) {
+                const int lower = kb_lower(s.rbeg);
+                if (lower < 0) to_add = true;
+                else {
+                    const int r = s2_test_and_merge(lower, s, l_pac, p.w, o.max_chain_gap);
+                    if (r < 0) return -1;
+                    if (!r) to_add = true;
+                }
+            } else to_add = true;
+            if (to_add) {
+                if (S.cnt[4] >= AF_S2_MAX_CHAIN || S.cnt[2] >= AF_S2_MAX_OCC) return -1;
+                const int kk = S.cnt[2]++;
+                S.pool[kk] = s;
+                S.next[kk] = -1;
+                const int nc = S.cnt[4];
+                S.ch[nc] = S2Chain{1, -1, 0, (int16_t)kk, 0, s.rbeg};
+                S.last_of[nc] = (int16_t)kk;
+                kb_putp(nc);
+                S.cnt[4] = nc + 1;
+            }
+        }
+    }
+    const int no = kb_traverse();
+    // reorder the chains (tree order) and compact their seeds
+    for (int a = 0; a < no; ++a) S.x.chtmp[a] = S.ch[S.order[a]];
+    int ns = 0;
+    for (int a = 0; a < no; ++a) {
+        S2Chain c = S.x.chtmp[a];
+        const int s0 = ns;
+        for (int k = c.seed0; k >= 0; k = S.next[k]) S.y.c.seed[ns++] = S.pool[k];
+        c.seed0 = (int16_t)s0;
+        S.ch[a] = c;
+    }
+    return no;
+}
+
+__device__ int s2_chain_weight(const S2Chain &c) {
+    const S2Seed *sd = g_s2.y.c.seed + c.seed0;
+    int64_t end = 0;
+    int w = 0, tmp;
+    for (int j = 0; j < c.n; ++j) {
+        const S2Seed s = sd[j];
+        if (s.qbeg >= end) w += s.len;
+        else if (s.qbeg + s.len > end) w += (int)(s.qbeg + s.len - end);
+        end = end > s.qbeg + s.len ? end : s.qbeg + s.len;
+    }
+    tmp = w; w = 0; end = 0;
+    for (int j = 0; j < c.n; ++j) {
+        const S2Seed s = sd[j];
+        if (s.rbeg >= end) w += s.len;
+        else if ((int64_t)s.rbeg + s.len > end) w += (int)((int64_t)s.rbeg + s.len - end);
+        end = end > (int64_t)s.rbeg + s.len ? end : (int64_t)s.rbeg + s.len;
+    }
+    w = w < tmp ? w : tmp;
+    return w < 1 << 30 ? w : (1 << 30) - 1;
+}
+
+struct LtFlt {
+    __device__ bool operator()(const S2Chain &a, const S2Chain &b) const { return a.w > b.w; }
+};
+
+// mem_chain_flt (lane 0; oracle mem_chain_flt): returns the kept chain count
+__device__ int s2_chain_flt(int n_chn, const af_params &p, const S2Opt &o) {
+    S2Lds &S = g_s2;
+    S2Chain *a = S.ch;
+    if (n_chn == 0) return 0;
+    for (int i = 0; i < n_chn; ++i) { a[i].first = -1; a[i].kept = 0; a[i].w = s2_chain_weight(a[i]); }
+    ks_introsort(a, n_chn, LtFlt());
+    auto beg = [&](const S2Chain &c) { return (int)S.y.c.seed[c.seed0].qbeg; };
+    auto endq = [&](const S2Chain &c) {
+        const S2Seed t = S.y.c.seed[c.seed0 + c.n - 1];
+        return (int)t.qbeg + t.len;
+    };
+    uint8_t chains[AF_S2_MAX_CHAIN];
+    int nc = 0;
+    a[0].kept = 3;
+    chains[nc++] = 0;
+    for (int i = 1; i < n_chn; ++i) {
+        int large_ovlp = 0, k;
+        for (k = 0; k < nc; ++k) {
+            const int j = chains[k];
+            const int b_max = beg(a[j]) > beg(a[i]) ? beg(a[j]) : beg(a[i]);
+            const int e_min = endq(a[j]) < endq(a[i]) ? endq(a[j]) : endq(a[i]);
+            if (e_min > b_max) {
+                const int li = endq(a[i]) - beg(a[i]), lj = endq(a[j]) - beg(a[j]);
+                const int min_l = li < lj ? li : lj;
+                if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
+                    large_ovlp = 1;
+                    if (a[j].first < 0) a[j].first = (int16_t)i;
+                    if ((float)a[i].w < (float)a[j].w * 0.5f && a[j].w - a[i].w >= p.min_seed_len << 1) break;
+                }
+            }
+        }
+        if (k == nc) {
+            chains[nc++] = (uint8_t)i;
+            a[i].kept = (int16_t)(large_ovlp ? 2 : 3);
+        }
+    }
+    for (int i = 0; i < nc; ++i) {
+        const S2Chain &c = a[chains[i]];
+        if (c.first >= 0) a[c.first].kept = 1;
+    }
+    int k = 0;
+    for (int i = 0; i < n_chn; ++i)
+        if (a[i].kept != 0) a[k++] = a[i];
+    return k;
+}
+
+// ====================================================================== K2: extension
+// mem_chain2aln (oracle mem_chain2aln) for chain ci; regions appended to S.x.reg (S.cnt[7])
+template <int CPL>
+__device__ void s2_chain2aln(const DevText &X, const af_params &p, int l, int ci, int lane) {
+    DpLds &L = g_dp;
+    S2Lds &S = g_s2;
+    const int64_t l_pac = X.n;
+    const S2Chain c = S.ch[ci];
+    const S2Seed *sd = S.y.c.seed + c.seed0;
+    if (lane == 0) {
+        int64_t r0 = l_pac << 1, r1 = 0;
+        for (int i = 0; i < c.n; ++i) {
+            const S2Seed t = sd[i];
+            const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(p, t.qbeg));
+            const int rem = l - t.qbeg - t.len;
+            const int64_t e = (int64_t)t.rbeg + t.len + (rem + cal_max_gap(p, rem));
+            r0 = r0 < b ? r0 : b;
+            r1 = r1 > e ? r1 : e;
+        }
+        r0 = r0 > 0 ? r0 : 0;
+        r1 = r1 < l_pac << 1 ? r1 : l_pac << 1;
+        if (r0 < l_pac && l_pac < r1) {
+            if (sd[0].rbeg < l_pac) r1 = l_pac;
+            else r0 = l_pac;
+        }
+        const int64_t fb = sd[0].rbeg < l_pac ? 0 : l_pac, fe = sd[0].rbeg < l_pac ? l_pac : l_pac << 1;
+        S.rmax[0] = r0 > fb ? r0 : fb;
+        S.rmax[1] = r1 < fe ? r1 : fe;
+        // srt: seed indices by (score << 32 | i) ascending
+        for (int i = 0; i < c.n; ++i) S.y.c.srt[i] = (int16_t)i;
+        for (int i = 1; i < c.n; ++i)
+            for (int j = i; j > 0; --j) {
+                const S2Seed u = sd[S.y.c.srt[j]], v = sd[S.y.c.srt[j - 1]];
+                const bool lt = u.len < v.len || (u.len == v.len && S.y.c.srt[j] < S.y.c.srt[j - 1]);
+                if (!lt) break;
+                const int16_t t = S.y.c.srt[j]; S.y.c.srt[j] = S.y.c.srt[j - 1]; S.y.c.srt[j - 1] = t;
+            }
+    }
+    wave_sync();
+    const int64_t rmax0 = S.rmax[0], rmax1 = S.rmax[1];
+    for (int k = c.n - 1; k >= 0; --k) {
+        const int si = S.y.c.srt[k];
+        const S2Seed s = sd[si];
+        const int nreg = S.cnt[7];
+        // test whether extension has been made before (any region satisfying)
+        bool hit = false;
+        if (lane < nreg) {
+            const S2Reg pr = S.x.reg[lane];
+            if (!(s.rbeg < pr.rb || (int64_t)s.rbeg + s.len > pr.re || s.qbeg < pr.qb || s.qbeg + s.len > pr.qe) &&
+                !((double)(s.len - pr.seedlen0) > .1 * l)) {
+                int qd = s.qbeg - pr.qb;
+                int64_t rd = s.rbeg - pr.rb;
+                int mg = cal_max_gap(p, (int)(qd < rd ? (int64_t)qd : rd));
+                int ww = mg < pr.w ? mg : pr.w;
+                if (qd - rd < ww && rd - qd < ww) hit = true;
+                else {
+                    qd = pr.qe - (s.qbeg + s.len);
+                    rd = pr.re - ((int64_t)s.rbeg + s.len);
+                    mg = cal_max_gap(p, (int)(qd < rd ? (int64_t)qd : rd));
+                    ww = mg < pr.w ? mg : pr.w;
+                    if (qd - rd < ww && rd - qd < ww) hit = true;
+                }
+            }
+        }
+        if (__ballot(hit)) {
+            // contained: extend only if a long overlapping seed on another diagonal follows
+            bool ov = false;
+            for (int i = k + 1 + lane; i < c.n; i += 64) {
+                const int ti = S.y.c.srt[i];
+                if (ti < 0) continue;
+                const S2Seed t = sd[ti];
+                if ((double)t.len < s.len * .95) continue;
+                if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                    (int64_t)(t.qbeg - s.qbeg) != (int64_t)t.rbeg - s.rbeg) ov = true;
+                if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                    (int64_t)(s.qbeg - t.qbeg) != (int64_t)s.rbeg - t.rbeg) ov = true;
+            }
+            if (!__ballot(ov)) {
+                wave_sync();
+                if (lane == 0) S.y.c.srt[k] = -1;
+                wave_sync();
+                continue;
+            }
+        }
+        if (nreg >= AF_S2_MAX_REG) {
+            wave_sync();
+            if (lane == 0) S.cnt[3] = 1;
+            wave_sync();
+            return;
+        }
+        int a_score = -1, a_truesc = -1, a_qb = 0, a_qe = 0;
+        int64_t a_rb = 0, a_re = 0;
+        int aw0 = p.w, aw1 = p.w;
+        if (s.qbeg) {  // left extension
+            const int64_t tmp = s.rbeg - rmax0;
+            const int tl = (int)min(tmp, (int64_t)(s.qbeg + 2 * p.w + 1));
+            for (int x = lane; x < s.qbeg; x += 64) L.qs[x] = L.q[s.qbeg - 1 - x];
+            for (int x = lane; x < tl; x += 64) L.t[x] = X.T[s.rbeg - 1 - x];
+            wave_sync();
+            ExtRes er;
+            for (int it = 0; it < 2; ++it) {
+                const int prev = a_score;
+                aw0 = p.w << it;
+                er = ext_dp<CPL>(s.qbeg, L.qs, tl, L.t, p, aw0, p.pen_clip5, p.zdrop, s.len * p.a, lane);
+                a_score = er.max;
+                if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+            }
+            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip5) {
+                a_qb = s.qbeg - er.qle; a_rb = s.rbeg - er.tle; a_truesc = a_score;
+            } else {
+                a_qb = 0; a_rb = s.rbeg - er.gtle; a_truesc = er.gscore;
+            }
+            wave_sync();
+        } else {
+            a_score = a_truesc = s.len * p.a; a_qb = 0; a_rb = s.rbeg;
+        }
+        if (s.qbeg + s.len != l) {  // right extension
+            const int qe = s.qbeg + s.len;
+            const int64_t re = (int64_t)s.rbeg + s.len - rmax0;
+            const int sc0 = a_score;
+            const int tl = (int)min(rmax1 - rmax0 - re, (int64_t)((l - qe) + 2 * p.w + 1));
+            for (int x = lane; x < tl; x += 64) L.t[x] = X.T[rmax0 + re + x];
+            wave_sync();
+            ExtRes er;
+            for (int it = 0; it < 2; ++it) {
+                const int prev = a_score;
+                aw1 = p.w << it;
+                er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                a_score = er.max;
+                if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+            }
+            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip3) {
+                a_qe = qe + er.qle; a_re = rmax0 + re + er.tle; a_truesc += a_score - sc0;
+            } else {
+                a_qe = l; a_re = rmax0 + re + er.gtle; a_truesc += er.gscore - sc0;
+            }
+            wave_sync();
+        } else {
+            a_qe = l; a_re = (int64_t)s.rbeg + s.len;
+        }
+        if (lane == 0) {
+            S2Reg &a = S.x.reg[nreg];
+            a.rb = a_rb; a.re = a_re; a.qb = a_qb; a.qe = a_qe; a.score = a_score; a.truesc = a_truesc;
+            a.w = aw0 > aw1 ? aw0 : aw1; a.seedlen0 = s.len;
+            S.cnt[7] = nreg + 1;
+        }
+        wave_sync();
+    }
+}
+
+// mem_patch_reg (oracle mem_patch_reg): the merged score, 0 if not merged; *w_out its band
+template <int CPL>
+__device__ int s2_patch_reg(const DevText &X, const af_params &p, const S2Reg &a, const S2Reg &b, int *w_out,
+                            uint8_t *zg, int lane) {
+    const int64_t l_pac = X.n;
+    if (a.rb < l_pac && b.rb >= l_pac) return 0;
+    if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) return 0;
+    if (b.re - a.rb > AF_S2_MAX_TSPAN) return 0;  // the oracle's AFO_PE_MAX_TSPAN (L.t holds 1 KiB)
+    int w = (int)((a.re - b.rb) - (a.qe - b.qb));
+    w = w > 0 ? w : -w;
+    double r = (double)(a.re - b.rb) / (double)(b.re - a.rb) - (double)(a.qe - b.qb) / (double)(b.qe - a.qb);
+    r = r > 0. ? r : -r;
+    if (a.re < b.rb || a.qe < b.qb) {
+        if (w > p.w << 1 || r >= (double)0.05f) return 0;
+    } else if (w > p.w << 2 || r >= (double)(0.05f * 2)) return 0;
+    w += a.w + b.w;
+    w = w < p.w << 2 ? w : p.w << 2;
+    const int lq = b.qe - a.qb;
+    const int score = gen_cigar_wave<CPL, false>(X.T, l_pac, p, w, lq, a.qb, a.rb, b.re, g_dp, zg, lane);
+    const int q_s = (int)((double)(b.qe - a.qb) / (double)((b.qe - b.qb) + (a.qe - a.qb)) * (double)(b.score + a.score) + .499);
+    const int r_s = (int)((double)(b.re - a.rb) / (double)((b.re - b.rb) + (a.re - a.rb)) * (double)(b.score + a.score) + .499);
+    if ((double)score / (double)(q_s > r_s ? q_s : r_s) < (double)0.90f) return 0;
+    *w_out = w;
+    return score;
+}
+
+struct LtArs2 {
+    __device__ bool operator()(const S2Reg &a, const S2Reg &b) const { return a.re < b.re; }
+};
+struct LtArs {
+    __device__ bool operator()(const S2Reg &a, const S2Reg &b) const {
+        return a.score > b.score || (a.score == b.score && (a.rb < b.rb || (a.rb == b.rb && a.qb < b.qb)));
+    }
+};
+
+// mem_sort_dedup_patch with patching (oracle mem_sort_dedup_patch, patch = 1) over S.x.reg
+template <int CPL>
+__device__ int s2_dedup_patch(const DevText &X, const af_params &p, const S2Opt &o, int n, uint8_t *zg, int lane) {
+    S2Lds &S = g_s2;
+    S2Reg *a = S.x.reg;
+    if (n <= 1) return n;
+    if (lane == 0) ks_introsort(a, n, LtArs2());
+    wave_sync();
+    for (int i = 1; i < n; ++i) {
+        if (a[i].rb >= a[i - 1].re + o.max_chain_gap) continue;
+        for (int j = i - 1; j >= 0 && a[i].rb < a[j].re + o.max_chain_gap; --j) {
+            const S2Reg q = a[j], pp = a[i];
+            if (q.qe == q.qb) continue;
+            const int64_t or_ = q.re - pp.rb;
+            const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
+            const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
+            const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
+            if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
+                const bool drop_p = pp.score < q.score;
+                wave_sync();
+                if (lane == 0) {
+                    if (drop_p) a[i].qe = a[i].qb;
+                    else a[j].qe = a[j].qb;
+                }
+                wave_sync();
+                if (drop_p) break;
+            } else if (q.rb < pp.rb) {
+                int w = 0;
+                const int score = s2_patch_reg<CPL>(X, p, q, pp, &w, zg, lane);
+                if (score > 0) {
+                    wave_sync();
+                    if (lane == 0) {
+                        a[i].qb = q.qb; a[i].rb = q.rb;
+                        a[i].truesc = a[i].score = score;
+                        a[i].w = w;
+                        a[j].qb = a[j].qe;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+    }
+    int m = 0;
+    if (lane == 0) {
+        for (int i = 0; i < n; ++i)
+            if (a[i].qe > a[i].qb) a[m++] = a[i];
+        ks_introsort(a, m, LtArs());
+        for (int i = 1; i < m; ++i)
+            if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
+        int mm = 1;
+        for (int i = 1; i < m; ++i)
+            if (a[i].qe > a[i].qb) a[mm++] = a[i];
+        S.misc[0] = mm;  // (bwa returns 1 for an emptied list, which cannot occur)
+    }
+    wave_sync();
+    return S.misc[0];
+}
+
+// K2: mem_align1_core for every candidate read (one wave per read)
+template <int CPL>
+__global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const uint8_t *__restrict__ reads,
+                                                             int32_t stride, const int32_t *__restrict__ lens,
+                                                             af_params p, S2Opt o, const int32_t *__restrict__ cand,
+                                                             const int32_t *__restrict__ n_cand, S2Work w,
+                                                             uint8_t *__restrict__ zscratch, size_t zstride) {
+    DpLds &L = g_dp;
+    S2Lds &S = g_s2;
+    const int lane = threadIdx.x;
+    const int ncand = *n_cand;
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        int item = ncand;
+        while (heads_left > 0) {
+            int v = 0;
+            if (lane == 0) v = atomicAdd(&w.heads_k2[AF_HEAD_STRIDE * head], 1);
+            v = __builtin_amdgcn_readfirstlane(v);
+            const int64_t it = head + 8 * (int64_t)v;
+            if (it < ncand) { item = (int)it; break; }
+            head = (head + 1) & 7;
+            --heads_left;
+        }
+        if (item >= ncand) break;
+        const int64_t r = cand[item];
+        int l = lens ? lens[r] : stride;
+        if (l > stride) l = stride;
+        if (l > AF_MAX_READ) l = AF_MAX_READ;
+        if (l < 0) l = 0;
+        const uint8_t *rd = reads + r * (int64_t)stride;
+        for (int x = lane; x < l; x += 64) {
+            const uint8_t ch = rd[x];
+            uint8_t v = 4;
+            switch (ch) {
+            case 'A': case 'a': v = 0; break;
+            case 'C': case 'c': v = 1; break;
+            case 'G': case 'g': v = 2; break;
+            case 'T': case 't': v = 3; break;
+            default: v = 4;
+            }
+            L.q[x] = v;
+        }
+        if (lane < 8) S.cnt[lane] = 0;
+        wave_sync();
+        if (lane < AF_MAX_READ / 16 + 2) {
+            const int b0 = lane * 16;
+            uint32_t pw = 0, nw = 0;
+            if (b0 < l) {
+                const uint4 cc = *reinterpret_cast<const uint4 *>(&L.q[b0]);
+                const uint32_t cw[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t y = cw[u] & 0x03030303u, t = y | (y >> 6);
+                    pw |= ((t & 0xFu) | ((t >> 12) & 0xF0u)) << (8 * u);
+                    nw |= ((((cw[u] >> 2) & 0x01010101u) * 0x01020408u) >> 24 & 0xFu) << (4 * u);
+                }
+            }
+            const int valid = l - b0;
+            if (valid < 16) nw |= valid <= 0 ? 0xFFFFu : (0xFFFFu << valid) & 0xFFFFu;
+            L.pk[lane] = pw;
+            L.nm[lane] = nw;
+        }
+        wave_sync();
+        int n_reg = 0;
+        if (l >= p.min_seed_len) {
+            s2_collect_intv(X, p, o, l, lane);
+            int n_chn = 0;
+            if (!S.cnt[3]) {
+                if (lane == 0) {
+                    int nc = s2_mem_chain(X, p, o);
+                    if (nc < 0) S.cnt[3] = 1;
+                    else nc = s2_chain_flt(nc, p, o);
+                    S.misc[1] = nc;
+                    S.cnt[7] = 0;
+                }
+                wave_sync();
+                n_chn = S.misc[1];
+            }
+            for (int ci = 0; ci < n_chn && !S.cnt[3]; ++ci) s2_chain2aln<CPL>(X, p, l, ci, lane);
+            if (!S.cnt[3]) n_reg = s2_dedup_patch<CPL>(X, p, o, S.cnt[7], zg, lane);
+        }
+        const bool ovf = S.cnt[3] != 0;
+        int off = 0;
+        if (!ovf && n_reg > 0) {
+            if (lane == 0) S.misc[2] = atomicAdd(w.pool_n, n_reg);
+            wave_sync();
+            off = S.misc[2];
+        }
+        const bool pool_ovf = !ovf && n_reg > 0 && (int64_t)off + n_reg > w.pool_cap;
+        if (!ovf && !pool_ovf)
+            for (int k = lane; k < n_reg; k += 64) w.pool[off + k] = S.x.reg[k];
+        if (lane == 0) w.rmap[r] = (ovf || pool_ovf) ? int2{0, -1} : int2{off, n_reg};
+        wave_sync();
+    }
+}
+
+// ============================================================================ K3a
+__device__ __forceinline__ int s2_chunk_of(const S2Work &w, int64_t pp) {
+    int lo = 0, hi = *w.n_chunks;  // cstart[lo] <= pp < cstart[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (w.cstart[mid] <= pp) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ int s2_infer_dir(int64_t l_pac, int64_t b1, int64_t b2, int64_t *dist) {
+    const int r1 = b1 >= l_pac, r2 = b2 >= l_pac;
+    const int64_t p2 = r1 == r2 ? b2 : (l_pac << 1) - 1 - b2;
+    *dist = p2 > b1 ? p2 - b1 : b1 - p2;
+    return (r1 == r2 ? 0 : 1) ^ (p2 > b1 ? 0 : 3);
+}
+
+// cal_sub (oracle cal_sub) over a pool region list
+__device__ int s2_cal_sub(const S2Reg *a, int n, int msl, int asc) {
+    const S2Reg a0 = a[0];
+    int j;
+    for (j = 1; j < n; ++j) {
+        const S2Reg aj = a[j];
+        const int b_max = aj.qb > a0.qb ? aj.qb : a0.qb;
+        const int e_min = aj.qe < a0.qe ? aj.qe : a0.qe;
+        if (e_min > b_max) {
+            const int min_l = aj.qe - aj.qb < a0.qe - a0.qb ? aj.qe - aj.qb : a0.qe - a0.qb;
+            if ((float)(e_min - b_max) >= (float)min_l * 0.5f) break;
+        }
+    }
+    return j < n ? a[j].score : msl * asc;
+}
+
+__global__ void k_s2_classify(int64_t n_pairs, int64_t l_pac, const int32_t *__restrict__ hits, af_params p, S2Opt o,
+                              S2Work w, af_aln_out out) {
+    const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 8) {  // K2 ran; the previous call's K3c ran
+        w.heads_k2[AF_HEAD_STRIDE * threadIdx.x] = 0;
+        w.heads_k3[AF_HEAD_STRIDE * threadIdx.x] = 0;
+    }
+    bool listed = false;
+    if (pp < n_pairs) {
+        const int h0 = hits[2 * pp], h1 = hits[2 * pp + 1];
+        if (h0 == 0 && h1 == 0) {
+            // both reads unmapped: flags 0x1|0x4|0x8|0x40 / 0x80, no position (bwa prints 0 and '*')
+            typedef int i32x2 __attribute__((ext_vector_type(2)));
+            __builtin_nontemporal_store(i32x2{0x4D, 0x8D}, reinterpret_cast<i32x2 *>(out.flag) + pp);
+            __builtin_nontemporal_store(i32x2{-1, -1}, reinterpret_cast<i32x2 *>(out.pos) + pp);
+            __builtin_nontemporal_store(i32x2{0, 0}, reinterpret_cast<i32x2 *>(out.score) + pp);
+            __builtin_nontemporal_store(i32x2{0, 0}, reinterpret_cast<i32x2 *>(out.n_cigar) + pp);
+        } else {
+            listed = true;
+            const int2 m0 = h0 > 0 ? w.rmap[2 * pp] : int2{0, 0};
+            const int2 m1 = h1 > 0 ? w.rmap[2 * pp + 1] : int2{0, 0};
+            if (m0.y > 0 && m1.y > 0) {  // mem_pestat's candidate unique pairs
+                const S2Reg *a0 = w.pool + m0.x, *a1 = w.pool + m1.x;
+                const int s0 = a0[0].score, s1 = a1[0].score;
+                if (!((double)s2_cal_sub(a0, m0.y, p.min_seed_len, p.a) > 0.8 * s0) &&
+                    !((double)s2_cal_sub(a1, m1.y, p.min_seed_len, p.a) > 0.8 * s1)) {
+                    int64_t is;
+                    const int dir = s2_infer_dir(l_pac, a0[0].rb, a1[0].rb, &is);
+                    if (is && is <= o.max_ins) {
+                        const int c = s2_chunk_of(w, pp);
+                        const int k = atomicAdd(&w.icnt[c], 1);
+                        w.ilist[w.cstart[c] + k] = dir << 30 | (int)is;
+                    }
+                }
+            }
+        }
+    }
+    // wave-aggregated append to the pair list
+    const uint64_t msk = __ballot(listed);
+    if (msk) {
+        const int lane = (int)(threadIdx.x & 63), leader = __builtin_ctzll(msk);
+        int base = 0;
+        if (lane == leader) base = atomicAdd(w.n_plist, __builtin_popcountll(msk));
+        base = __shfl(base, leader);
+        if (listed) w.plist[base + lanes_below(msk, lane)] = (int32_t)pp;
+    }
+}
+
+// ============================================================================ K3b
+// mem_pestat (oracle mem_pestat) for one chunk: insert sizes -> LDS histogram per orientation
+constexpr int PES_MAXINS = 16383;
+__global__ __launch_bounds__(256) void k_s2_pestat(S2Work w, int32_t max_ins) {
+    __shared__ int hist[PES_MAXINS + 1];
+    __shared__ int red[4][8];
+    __shared__ int nn[4];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    if (c >= *w.n_chunks) return;
+    const int64_t base = w.cstart[c];
+    const int n = w.icnt[c];
+    const int nb = max_ins + 1;
+    // counts per orientation
+    {
+        int cnt[4] = {0, 0, 0, 0};
+        for (int i = tid; i < n; i += 256) ++cnt[(uint32_t)w.ilist[base + i] >> 30];
+        for (int d = 0; d < 4; ++d) {
+            int v = cnt[d];
+            for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
+            if ((tid & 63) == 0) red[d][tid >> 6] = v;
+        }
+        __syncthreads();
+        if (tid < 4) nn[tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+        __syncthreads();
+    }
+    S2Pes res[4];
+    for (int d = 0; d < 4; ++d) {
+        S2Pes &r = res[d];
+        r.low = r.high = 0; r.failed = 0; r.pad = 0; r.avg = 0; r.std = 0;
+        const int nd = nn[d];
+        if (nd < 10) { r.failed = 1; continue; }  // MIN_DIR_CNT
+        for (int i = tid; i < nb; i += 256) hist[i] = 0;
+        __syncthreads();
+        for (int i = tid; i < n; i += 256) {
+            const uint32_t v = (uint32_t)w.ilist[base + i];
+            if ((int)(v >> 30) == d) atomicAdd(&hist[v & 0x3FFFFFFFu], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // percentiles: q[(int)(f * n + .499)] of the sorted sizes
+            const int k25 = (int)(.25 * nd + .499), k50 = (int)(.50 * nd + .499), k75 = (int)(.75 * nd + .499);
+            int p25 = 0, p50 = 0, p75 = 0, cum = 0;
+            bool g25 = false, g50 = false, g75 = false;
+            for (int v = 0; v < nb; ++v) {
+                cum += hist[v];
+                if (!g25 && cum > k25) { p25 = v; g25 = true; }
+                if (!g50 && cum > k50) { p50 = v; g50 = true; }
+                if (!g75 && cum > k75) { p75 = v; g75 = true; break; }
+            }
+            (void)p50;
+            r.low = (int)(p25 - 2.0 * (p75 - p25) + .499);
+            if (r.low < 1) r.low = 1;
+            r.high = (int)(p75 + 2.0 * (p75 - p25) + .499);
+            long long sum = 0;
+            int x = 0;
+            for (int v = r.low; v <= r.high && v < nb; ++v) { sum += (long long)v * hist[v]; x += hist[v]; }
+            double avg = 0;
+            // bwa adds the sizes in sorted order in double: integers, exact below 2^53
+            avg = (double)sum;
+            avg /= x;
+            double sd = 0;
+            for (int v = r.low; v <= r.high && v < nb; ++v)
+                for (int k = 0; k < hist[v]; ++k) sd += ((double)v - avg) * ((double)v - avg);
+            sd = sqrt(sd / x);
+            r.avg = avg; r.std = sd;
+            r.low = (int)(p25 - 3.0 * (p75 - p25) + .499);
+            r.high = (int)(p75 + 3.0 * (p75 - p25) + .499);
+            if (r.low > avg - 4.0 * sd) r.low = (int)(avg - 4.0 * sd + .499);
+            if (r.high < avg + 4.0 * sd) r.high = (int)(avg + 4.0 * sd + .499);
+            if (r.low < 1) r.low = 1;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        int mx = 0;
+        for (int d = 0; d < 4; ++d) mx = mx > nn[d] ? mx : nn[d];
+        for (int d = 0; d < 4; ++d) {
+            if (res[d].failed == 0 && (double)nn[d] < mx * 0.05) res[d].failed = 1;
+            w.pes[(int64_t)c * 4 + d] = res[d];
+        }
+        w.icnt[c] = 0;  // for the next call
+    }
+}
+
+// ============================================================================ K3c
+struct PeReg {
+    S2Reg r;
+    uint64_t hash;
+    int32_t secondary, pad;
+};
+struct __attribute__((aligned(16))) PeLds {
+    PeReg a[2][AF_S2_MAX_REG];
+    int64_t brb[2][AF_S2_MAX_REG];
+    uint8_t q[2][AF_MAX_READ + 16];
+    uint8_t rq[AF_MAX_READ + 16];      // the rescue query (mate, maybe reverse-complemented)
+    uint8_t rq2[AF_MAX_READ + 16];     // its reversed prefix (ksw_align2's start pass)
+    S2Pes pes[4];
+    int32_t na[2], nb[2], ovf[2], len[2];
+    int32_t z[2], which[2], extra, misc[8];
+    int32_t o_rid[2], o_rev[2], o_flag[2], o_score[2], o_nc[2];
+    int64_t o_pos[2];
+};
+__shared__ PeLds g_pe;
+
+struct SwRes { int score, te, qe; };
+
+// One pass of ksw_u8 / ksw_i16 (oracle ksw_sw) on the wave.  The striped kernel's result is
+// H(i,j) = max(G, F) with G = max(H(i-1,j-1) + S, E, 0) and F the full horizontal-gap term,
+// while E(i+1,j) is fed by the first-pass value max(G, F within the query's stripe block
+// [blk * slen, (blk + 1) * slen)) -- the lazy-F loop does not revisit E.  Lanes hold query
+// columns; both F terms are prefix maxima (one plain, one keyed by block).  The target base of
+// row i is target[i] (rev: target[te0 - i] for i <= te0, as the start pass's partly reversed
+// target).  Stops at the first row reaching endsc.
+__device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *target, int tlen, int rev_te, int P,
+                             const af_params &p, int endsc, int lane) {
+    const int slen = (qlen + P - 1) / P;
+    const int cpl = (qlen + 63) >> 6;  // <= 5 (AF_MAX_READ 320)
+    const int shift = p.b > 1 ? p.b : 1;  // ksw_qinit: minus the smallest score of the matrix (N: -1)
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int j0 = lane * cpl;
+    int H[5], E[5], qc[5], blk[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const int j = j0 + c;
+        H[c] = 0; E[c] = 0;
+        qc[c] = (c < cpl && j < qlen) ? q[j] : 4;
+        blk[c] = (c < cpl && j < qlen) ? j / slen : 0;
+    }
+    SwRes r{0, -1, -1};
+    int gmax = 0;
+    for (int i = 0; i < tlen; ++i) {
+        const int ti = __builtin_amdgcn_readfirstlane((int)(rev_te >= 0 && i <= rev_te ? target[rev_te - i] : target[i]));
+        const int from_left = wave_shr1(0, pick<5>(H, cpl - 1));
+        int G[5], runX = kNeg, runK = -1, bxX[5], bxK[5];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j < qlen;
+            const int hd = c == 0 ? from_left : H[c - 1];
+            const int s = (ti > 3 || qc[c] > 3) ? -1 : (ti == qc[c] ? p.a : -p.b);
+            const int D = max(hd + s, 0);
+            G[c] = max(D, E[c]);
+            bxX[c] = runX; bxK[c] = runK;
+            if (in) {
+                const int X = G[c] - oe_ins + j * p.e_ins;
+                runX = max(runX, X);
+                runK = max(runK, (blk[c] << 20) | (X + (1 << 19)));
+            }
+        }
+        const int lexX = wave_shr1(kNeg, wave_incl_max(runX));
+        const int lexK = wave_shr1(-1, wave_incl_max(runK));
+        int rowmax = 0;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            const int j = j0 + c;
+            const bool in = c < cpl && j < qlen;
+            const int PX = max(lexX, bxX[c]);
+            const int F = PX <= kNeg / 2 ? 0 : max(PX - (j - 1) * p.e_ins, 0);
+            const int PK = max(lexK, bxK[c]);
+            const int Fs = (PK >= 0 && (PK >> 20) == blk[c]) ? max((PK & 0xFFFFF) - (1 << 19) - (j - 1) * p.e_ins, 0) : 0;
+            const int h = max(G[c], F);
+            const int hfp = max(G[c], Fs);
+            E[c] = max(max(E[c] - p.e_del, hfp - oe_del), 0);
+            H[c] = in ? h : 0;
+            if (in) rowmax = max(rowmax, h);
+        }
+        rowmax = wave_max(rowmax);
+        if (rowmax > gmax) {
+            gmax = rowmax;
+            r.te = i;
+            int qj = 1 << 30;
+#pragma unroll
+            for (int c = 0; c < 5; ++c)
+                if (c < cpl && j0 + c < qlen && H[c] == gmax) qj = min(qj, j0 + c);
+            r.qe = wave_min(qj);
+            if ((P == 16 && gmax + shift >= 255) || gmax >= endsc) break;
+        }
+    }
+    r.score = (P == 16 && gmax + shift >= 255) ? 255 : gmax;
+    if (r.score == 255) r.qe = -1;
+    return r;
+}
+
+// ksw_align2 with KSW_XSUBO | KSW_XSTART (oracle ksw_align2): score, te, qe and the start (tb, qb)
+__device__ void s2_ksw_align2(const uint8_t *q, int qlen, const uint8_t *target, int tlen, int P, int minsc,
+                              const af_params &p, int &score, int &te, int &qe, int &tb, int &qb, int lane) {
+    PeLds &E = g_pe;
+    const SwRes r = s2_ksw_pass(q, qlen, target, tlen, -1, P, p, 0x10000, lane);
+    score = r.score; te = r.te; qe = r.qe; tb = -1; qb = -1;
+    if (r.score < minsc || r.qe < 0) return;
+    for (int x = lane; x <= r.qe; x += 64) E.rq2[x] = q[r.qe - x];
+    wave_sync();
+    const SwRes rr = s2_ksw_pass(E.rq2, r.qe + 1, target, tlen, r.te, P, p, r.score, lane);
+    wave_sync();
+    if (r.score == rr.score) { tb = r.te - rr.te; qb = r.qe - rr.qe; }
+}
+
+struct LtArsR {
+    __device__ bool operator()(const PeReg &a, const PeReg &b) const { return LtArs()(a.r, b.r); }
+};
+struct LtArs2R {
+    __device__ bool operator()(const PeReg &a, const PeReg &b) const { return a.r.re < b.r.re; }
+};
+struct LtArsHash {
+    __device__ bool operator()(const PeReg &a, const PeReg &b) const {
+        return a.r.score > b.r.score || (a.r.score == b.r.score && a.hash < b.hash);
+    }
+};
+
+// mem_sort_dedup_patch without patching (mate-SW context), lane 0
+__device__ int s2_dedup_nopatch(PeReg *a, int n, int max_chain_gap) {
+    if (n <= 1) return n;
+    ks_introsort(a, n, LtArs2R());
+    for (int i = 1; i < n; ++i) {
+        PeReg &pp = a[i];
+        if (pp.r.rb >= a[i - 1].r.re + max_chain_gap) continue;
+        for (int j = i - 1; j >= 0 && pp.r.rb < a[j].r.re + max_chain_gap; --j) {
+            PeReg &q = a[j];
+            if (q.r.qe == q.r.qb) continue;
+            const int64_t or_ = q.r.re - pp.r.rb;
+            const int64_t oq = q.r.qb < pp.r.qb ? q.r.qe - pp.r.qb : pp.r.qe - q.r.qb;
+            const int64_t mr = q.r.re - q.r.rb < pp.r.re - pp.r.rb ? q.r.re - q.r.rb : pp.r.re - pp.r.rb;
+            const int64_t mq = q.r.qe - q.r.qb < pp.r.qe - pp.r.qb ? q.r.qe - q.r.qb : pp.r.qe - pp.r.qb;
+            if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
+                if (pp.r.score < q.r.score) { pp.r.qe = pp.r.qb; break; }
+                else q.r.qe = q.r.qb;
+            }
+        }
+    }
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if (a[i].r.qe > a[i].r.qb) a[m++] = a[i];
+    n = m;
+    ks_introsort(a, n, LtArsR());
+    for (int i = 1; i < n; ++i)
+        if (a[i].r.score == a[i - 1].r.score && a[i].r.rb == a[i - 1].r.rb && a[i].r.qb == a[i - 1].r.qb)
+            a[i].r.qe = a[i].r.qb;
+    int mm = 1;
+    for (int i = 1; i < n; ++i)
+        if (a[i].r.qe > a[i].r.qb) a[mm++] = a[i];
+    return n ? mm : 0;
+}
+
+// mem_matesw (oracle mem_matesw): rescue read mi in the insert-size window of a region at a_rb
+// of its mate.  Returns false on a region-cap overflow of read mi.
+__device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, int mi, int64_t a_rb, int lane) {
+    PeLds &E = g_pe;
+    const int64_t l_pac = X.n;
+    const int l_ms = E.len[mi];
+    int skip[4];
+    for (int r = 0; r < 4; ++r) skip[r] = E.pes[r].failed ? 1 : 0;
+    for (int i = 0; i < E.na[mi]; ++i) {
+        int64_t dist;
+        const int r = s2_infer_dir(l_pac, a_rb, E.a[mi][i].r.rb, &dist);
+        if (dist >= E.pes[r].low && dist <= E.pes[r].high) skip[r] = 1;
+    }
+    if (skip[0] + skip[1] + skip[2] + skip[3] == 4) return true;
+    int n = 0, rid = -1;
+    for (int r = 0; r < 4; ++r) {
+        if (skip[r]) continue;
+        const bool is_rev = (r >> 1) != (r & 1);
+        const bool is_larger = !(r >> 1);
+        int64_t rb, re;
+        if (!is_rev) {
+            rb = is_larger ? a_rb + E.pes[r].low : a_rb - E.pes[r].high;
+            re = (is_larger ? a_rb + E.pes[r].high : a_rb - E.pes[r].low) + l_ms;
+        } else {
+            rb = (is_larger ? a_rb + E.pes[r].low : a_rb - E.pes[r].high) - l_ms;
+            re = is_larger ? a_rb + E.pes[r].high : a_rb - E.pes[r].low;
+        }
+        if (rb < 0) rb = 0;
+        if (re > l_pac << 1) re = l_pac << 1;
+        if (rb < re) {
+            const int64_t mid = (rb + re) >> 1;
+            const int64_t fb = mid < l_pac ? 0 : l_pac, fe = mid < l_pac ? l_pac : l_pac << 1;
+            rb = rb > fb ? rb : fb;
+            re = re < fe ? re : fe;
+            rid = 0;
+        }
+        if (rid == 0 && re - rb >= p.min_seed_len) {
+            for (int x = lane; x < l_ms; x += 64) {
+                const int c = E.q[mi][is_rev ? l_ms - 1 - x : x];
+                E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
+            }
+            wave_sync();
+            const int P = l_ms * p.a < 250 ? 16 : 8;
+            int sc, te, qe, tb, qb;
+            s2_ksw_align2(E.rq, l_ms, X.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb, qb, lane);
+            if (sc >= p.min_seed_len && qb >= 0) {
+                bool ok = true;
+                if (lane == 0) {
+                    PeReg b{};
+                    b.r.qb = is_rev ? l_ms - (qe + 1) : qb;
+                    b.r.qe = is_rev ? l_ms - qb : qe + 1;
+                    b.r.rb = is_rev ? (l_pac << 1) - (rb + te + 1) : rb + tb;
+                    b.r.re = is_rev ? (l_pac << 1) - (rb + tb) : rb + te + 1;
+                    b.r.score = sc;
+                    b.r.truesc = 0; b.r.w = 0; b.r.seedlen0 = 0;
+                    b.secondary = -1;
+                    const int na = E.na[mi];
+                    if (na >= AF_S2_MAX_REG) ok = false;
+                    else {
+                        PeReg *ma = E.a[mi];
+                        int i;
+                        for (i = 0; i < na; ++i)
+                            if (ma[i].r.score < b.r.score) break;
+                        for (int u = na; u > i; --u) ma[u] = ma[u - 1];
+                        ma[i] = b;
+                        E.na[mi] = na + 1;
+                    }
+                    E.misc[0] = ok;
+                }
+                wave_sync();
+                if (!E.misc[0]) return false;
+            }
+            ++n;
+        }
+        if (n) {
+            if (lane == 0) E.na[mi] = s2_dedup_nopatch(E.a[mi], E.na[mi], o.max_chain_gap);
+            wave_sync();
+        }
+    }
+    return true;
+}
+
+// mem_mark_primary_se (no ALT contigs), lane 0
+__device__ void s2_mark_primary(PeReg *a, int n, int64_t id, const af_params &p) {
+    if (n == 0) return;
+    for (int i = 0; i < n; ++i) { a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i)); }
+    ks_introsort(a, n, LtArsHash());
+    int z[AF_S2_MAX_REG], nz = 0;
+    z[nz++] = 0;
+    for (int i = 1; i < n; ++i) {
+        int k;
+        for (k = 0; k < nz; ++k) {
+            const int j = z[k];
+            const int b_max = a[j].r.qb > a[i].r.qb ? a[j].r.qb : a[i].r.qb;
+            const int e_min = a[j].r.qe < a[i].r.qe ? a[j].r.qe : a[i].r.qe;
+            if (e_min > b_max) {
+                const int min_l = a[i].r.qe - a[i].r.qb < a[j].r.qe - a[j].r.qb ? a[i].r.qe - a[i].r.qb : a[j].r.qe - a[j].r.qb;
+                if ((float)(e_min - b_max) >= (float)min_l * 0.5f) break;
+            }
+        }
+        if (k == nz) z[nz++] = i;
+        else a[i].secondary = z[k];
+    }
+}
+
+struct P64 { uint64_t x, y; };
+struct LtP64 {
+    __device__ bool operator()(const P64 &a, const P64 &b) const { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+};
+
+// mem_pair (oracle mem_pair), lane 0: the best pair's score (0 if none) and z[]
+__device__ int s2_mem_pair(int64_t l_pac, const af_params &p, const S2Pes *pes, int id, int z[2]) {
+    PeLds &E = g_pe;
+    P64 v[2 * AF_S2_MAX_REG];
+    int nv = 0;
+    for (int r = 0; r < 2; ++r)
+        for (int i = 0; i < E.na[r]; ++i) {
+            const S2Reg &e = E.a[r][i].r;
+            P64 key;
+            key.x = (uint64_t)(e.rb < l_pac ? e.rb : (l_pac << 1) - 1 - e.rb);
+            key.y = (uint64_t)(uint32_t)e.score << 32 | (uint64_t)i << 2 | (uint64_t)(e.rb >= l_pac) << 1 | (uint64_t)r;
+            v[nv++] = key;
+        }
+    ks_introsort(v, nv, LtP64());
+    int y[4] = {-1, -1, -1, -1};
+    bool have = false;
+    P64 best{0, 0};
+    for (int i = 0; i < nv; ++i) {
+        for (int r = 0; r < 2; ++r) {
+            const int dir = r << 1 | (int)(v[i].y >> 1 & 1);
+            if (pes[dir].failed) continue;
+            const int which = r << 1 | (int)((v[i].y & 1) ^ 1);
+            if (y[which] < 0) continue;
+            for (int k = y[which]; k >= 0; --k) {
+                if ((int)(v[k].y & 3) != which) continue;
+                const int64_t dist = (int64_t)v[i].x - (int64_t)v[k].x;
+                if (dist > pes[dir].high) break;
+                if (dist < pes[dir].low) continue;
+                const double ns = ((double)dist - pes[dir].avg) / pes[dir].std;
+                int q = (int)((double)((v[i].y >> 32) + (v[k].y >> 32)) + .721 * log(2. * erfc(fabs(ns) * 0.70710678118654752440)) * p.a + .499);
+                if (q < 0) q = 0;
+                P64 u;
+                u.y = (uint64_t)k << 32 | (uint64_t)i;
+                u.x = (uint64_t)q << 32 | (hash_64(u.y ^ (uint64_t)(int64_t)(int32_t)((uint32_t)id << 8)) & 0xffffffffU);
+                if (!have || LtP64()(best, u)) { best = u; have = true; }
+            }
+        }
+        y[v[i].y & 3] = i;
+    }
+    if (!have) return 0;
+    const int i = (int)(best.y >> 32), k = (int)(best.y << 32 >> 32);
+    z[v[i].y & 1] = (int)(v[i].y << 32 >> 34);
+    z[v[k].y & 1] = (int)(v[k].y << 32 >> 34);
+    return (int)(best.x >> 32);
+}
+
+// K3c: mem_sam_pe for every listed pair (one wave per pair)
+template <int CPL>
+__global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
+                                                 const int32_t *__restrict__ lens, af_params p, S2Opt o,
+                                                 const int32_t *__restrict__ hits, S2Work w, af_aln_out out,
+                                                 uint8_t *__restrict__ zscratch, size_t zstride, AfTails tails,
+                                                 int use_tails) {
+    DpLds &L = g_dp;
+    PeLds &E = g_pe;
+    const int lane = threadIdx.x;
+    const int64_t l_pac = X.n;
+    const int npl = *w.n_plist;
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        int item = npl;
+        while (heads_left > 0) {
+            int v = 0;
+            if (lane == 0) v = atomicAdd(&w.heads_k3[AF_HEAD_STRIDE * head], 1);
+            v = __builtin_amdgcn_readfirstlane(v);
+            const int64_t it = head + 8 * (int64_t)v;
+            if (it < npl) { item = (int)it; break; }
+            head = (head + 1) & 7;
+            --heads_left;
+        }
+        if (item >= npl) break;
+        const int64_t pp = w.plist[item];
+        // reads and their regions
+        for (int m = 0; m < 2; ++m) {
+            const int64_t r = 2 * pp + m;
+            int l = lens ? lens[r] : stride;
+            if (l > stride) l = stride;
+            if (l > AF_MAX_READ) l = AF_MAX_READ;
+            if (l < 0) l = 0;
+            const uint8_t *rd = reads + r * (int64_t)stride;
+            for (int x = lane; x < l; x += 64) {
+                const uint8_t ch = rd[x];
+                uint8_t v = 4;
+                switch (ch) {
+                case 'A': case 'a': v = 0; break;
+                case 'C': case 'c': v = 1; break;
+                case 'G': case 'g': v = 2; break;
+                case 'T': case 't': v = 3; break;
+                default: v = 4;
+                }
+                E.q[m][x] = v;
+            }
+            const int h = hits[r];
+            const int2 mp = h > 0 ? w.rmap[r] : int2{0, 0};
+            const int na = mp.y > 0 ? mp.y : 0;
+            for (int k = lane; k < na; k += 64) E.a[m][k].r = w.pool[mp.x + k];
+            if (lane == 0) { E.len[m] = l; E.na[m] = na; E.ovf[m] = mp.y < 0; }
+        }
+        if (lane < 4) E.pes[lane] = w.pes[(int64_t)s2_chunk_of(w, pp) * 4 + lane];
+        wave_sync();
+        // mate rescue for the top hits of each end
+        if (lane == 0) {
+            for (int i = 0; i < 2; ++i) {
+                int nb = 0;
+                for (int j = 0; j < E.na[i]; ++j)
+                    if (E.a[i][j].r.score >= E.a[i][0].r.score - o.pen_unpaired) E.brb[i][nb++] = E.a[i][j].r.rb;
+                E.nb[i] = nb;
+            }
+        }
+        wave_sync();
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < E.nb[i] && j < o.max_matesw; ++j) {
+                if (E.ovf[!i]) continue;
+                if (!s2_matesw(X, p, o, !i, E.brb[i][j], lane)) {
+                    wave_sync();
+                    if (lane == 0) { E.ovf[!i] = 1; E.na[!i] = 0; }
+                    wave_sync();
+                }
+            }
+        // primary marking, pairing and the record choice (mem_sam_pe)
+        if (lane == 0) {
+            const uint64_t id = (uint64_t)(o.pair_base + pp);
+            s2_mark_primary(E.a[0], E.na[0], (int64_t)(id << 1 | 0), p);
+            s2_mark_primary(E.a[1], E.na[1], (int64_t)(id << 1 | 1), p);
+            int z[2] = {0, 0}, extra = 1, which[2] = {-1, -1};
+            bool paired = false;
+            int o_sc = 0;
+            if (E.na[0] && E.na[1] && (o_sc = s2_mem_pair(l_pac, p, E.pes, (int)(uint32_t)id, z)) > 0) {
+                int is_multi = 0;
+                for (int i = 0; i < 2; ++i) {
+                    int j;
+                    for (j = 1; j < E.na[i]; ++j)
+                        if (E.a[i][j].secondary < 0 && E.a[i][j].r.score >= p.T) break;
+                    is_multi |= j < E.na[i];
+                }
+                if (!is_multi) {
+                    const int score_un = E.a[0][0].r.score + E.a[1][0].r.score - o.pen_unpaired;
+                    if (o_sc > score_un) {
+                        for (int i = 0; i < 2; ++i)
+                            if (E.a[i][z[i]].secondary >= 0) E.a[i][z[i]].secondary = -2;
+                        extra |= 2;
+                    } else {
+                        z[0] = z[1] = 0;
+                    }
+                    which[0] = z[0]; which[1] = z[1];
+                    paired = true;
+                }
+            }
+            if (!paired) {
+                for (int i = 0; i < 2; ++i) which[i] = (E.na[i] && E.a[i][0].r.score >= p.T) ? 0 : -1;
+                if (which[0] >= 0 && which[1] >= 0) {
+                    int64_t dist;
+                    const int d = s2_infer_dir(l_pac, E.a[0][0].r.rb, E.a[1][0].r.rb, &dist);
+                    if (!E.pes[d].failed && dist >= E.pes[d].low && dist <= E.pes[d].high) extra |= 2;
+                }
+            }
+            E.which[0] = which[0]; E.which[1] = which[1]; E.extra = extra;
+        }
+        wave_sync();
+        // mem_reg2aln of each read's record
+        for (int m = 0; m < 2; ++m) {
+            const int wi = E.which[m];
+            const int64_t r = 2 * pp + m;
+            if (wi < 0) {
+                if (lane == 0) { E.o_rid[m] = -1; E.o_pos[m] = -1; E.o_rev[m] = 0; E.o_flag[m] = 0x4; E.o_score[m] = 0; E.o_nc[m] = 0; }
+                wave_sync();
+                continue;
+            }
+            const S2Reg ar = E.a[m][wi].r;
+            const int secondary = E.a[m][wi].secondary;
+            const int l = E.len[m];
+            for (int x = lane; x < l; x += 64) L.q[x] = E.q[m][x];
+            wave_sync();
+            const bool is_rev = ar.rb >= l_pac;
+            const int lq = ar.qe - ar.qb;
+            const int tmpw = infer_bw(lq, (int)(ar.re - ar.rb), ar.truesc, p.a, p.o_del, p.e_del);
+            int w2 = infer_bw(lq, (int)(ar.re - ar.rb), ar.truesc, p.a, p.o_ins, p.e_ins);
+            w2 = w2 > tmpw ? w2 : tmpw;
+            if (w2 > p.w) w2 = w2 < ar.w ? w2 : ar.w;
+            int score = 0, last_sc = -(1 << 30), it = 0;
+            do {
+                w2 = w2 < p.w << 2 ? w2 : p.w << 2;
+                score = gen_cigar_wave<CPL>(X.T, l_pac, p, w2, lq, ar.qb, ar.rb, ar.re, L, zg, lane);
+                if (score == last_sc || w2 == p.w << 2) break;
+                last_sc = score;
+                w2 <<= 1;
+            } while (++it < 3 && score < ar.truesc - p.a);
+            if (lane == 0) {
+                uint32_t *co = out.cigar + r * AF_MAX_CIGAR;
+                const int nc = L.misc[2];
+                const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
+                bool of = nc > AF_MAX_CIGAR;
+                int64_t pos = is_rev ? (l_pac << 1) - ar.re : ar.rb;
+                int xs = 0, xe = ncap;
+                const uint32_t first = L.ring[(nc - 1) & 63];
+                const uint32_t last = L.ring[(nc - ncap) & 63];
+                if (ncap > 0) {
+                    if ((first & 0xf) == 2) { pos += first >> 4; xs = 1; }
+                    else if ((last & 0xf) == 2) xe = ncap - 1;
+                }
+                const int clip5 = is_rev ? l - ar.qe : ar.qb;
+                const int clip3 = is_rev ? ar.qb : l - ar.qe;
+                int nf = 0;
+                if (clip5) co[nf++] = (uint32_t)clip5 << 4 | 4;
+                for (int x = xs; x < xe; ++x) {
+                    if (nf < AF_MAX_CIGAR) co[nf] = L.ring[(nc - 1 - x) & 63];
+                    ++nf;
+                }
+                if (clip3) {
+                    if (nf < AF_MAX_CIGAR) co[nf] = (uint32_t)clip3 << 4 | 4;
+                    ++nf;
+                }
+                if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
+                E.o_rid[m] = 0; E.o_pos[m] = pos; E.o_rev[m] = is_rev;
+                E.o_flag[m] = (secondary >= 0 ? 0x100 : 0) | (of ? AF_FLAG_CIGAR_OVERFLOW : 0);
+                E.o_score[m] = ar.score; E.o_nc[m] = nf;
+            }
+            wave_sync();
+        }
+        // mem_aln2sam's flags and the mate copy rules
+        if (lane == 0) {
+            for (int m = 0; m < 2; ++m) {
+                const int mm = m ^ 1;
+                int prid = E.o_rid[m], mrid = E.o_rid[mm];
+                int64_t ppos = E.o_pos[m];
+                int prev = E.o_rev[m], mrev = E.o_rev[mm];
+                int flag = E.o_flag[m] | (m ? 0x80 : 0x40) | E.extra | 0x1;
+                flag |= prid < 0 ? 0x4 : 0;
+                flag |= mrid < 0 ? 0x8 : 0;
+                if (prid < 0 && mrid >= 0) { ppos = E.o_pos[mm]; prev = mrev; }
+                if (mrid < 0 && prid >= 0) mrev = prev;
+                flag |= prev ? 0x10 : 0;
+                flag |= mrev ? 0x20 : 0;
+                if (E.ovf[m]) flag |= AF_FLAG_MEM_OVERFLOW;
+                const int64_t r = 2 * pp + m;
+                out.flag[r] = flag;
+                out.pos[r] = (prid >= 0 || mrid >= 0) ? (int32_t)ppos : -1;
+                out.score[r] = prid >= 0 ? E.o_score[m] : 0;
+                out.n_cigar[r] = prid >= 0 ? E.o_nc[m] : 0;
+                if (use_tails && prid >= 0 && E.o_nc[m] == 2)
+                    af_emit_tail(tails, reads, stride, lens, r, flag, out.cigar + r * AF_MAX_CIGAR);
+            }
+        }
+        wave_sync();
+    }
+}
+
+// chunk boundaries of a ragged batch (bseq_read: a chunk ends after the pair that brings its
+// bases to >= chunk_bases): prefix sums of pair lengths, then one binary search per chunk
+__global__ __launch_bounds__(1024) void k_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *__restrict__ lens,
+                                                     int64_t chunk_bases, int64_t *__restrict__ cstart,
+                                                     int64_t *__restrict__ S, int32_t max_chunks,
+                                                     int32_t *__restrict__ n_chunks) {
+    __shared__ int64_t part[1024];
+    const int tid = threadIdx.x;
+    if (!lens) {
+        if (tid == 0) {
+            const int64_t ppc = (chunk_bases + 2 * (int64_t)stride - 1) / (2 * (int64_t)stride);
+            const int64_t per = ppc > 0 ? ppc : 1;
+            int nc = 0;
+            for (int64_t c0 = 0; c0 < n_pairs && nc < max_chunks; c0 += per) cstart[nc++] = c0;
+            cstart[nc] = n_pairs;
+            *n_chunks = nc;
+        }
+        return;
+    }
+    const int64_t per = (n_pairs + 1023) / 1024;
+    const int64_t b0 = tid * per, b1 = min(n_pairs, b0 + per);
+    int64_t s = 0;
+    for (int64_t q = b0; q < b1; ++q) {
+        const int64_t l0 = min(lens[2 * q], stride), l1 = min(lens[2 * q + 1], stride);
+        s += max(l0, (int64_t)0) + max(l1, (int64_t)0);
+    }
+    part[tid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        int64_t acc = 0;
+        for (int t = 0; t < 1024; ++t) { const int64_t v = part[t]; part[t] = acc; acc += v; }
+    }
+    __syncthreads();
+    s = part[tid];
+    for (int64_t q = b0; q < b1; ++q) {
+        const int64_t l0 = min(lens[2 * q], stride), l1 = min(lens[2 * q + 1], stride);
+        s += max(l0, (int64_t)0) + max(l1, (int64_t)0);
+        S[q] = s;  // bases of pairs [0, q]
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int nc = 0;
+        int64_t c0 = 0;
+        while (c0 < n_pairs && nc < max_chunks) {
+            cstart[nc++] = c0;
+            const int64_t before = c0 > 0 ? S[c0 - 1] : 0;
+            int64_t lo = c0, hi = n_pairs - 1;  // first q >= c0 with S[q] - before >= chunk_bases
+            if (S[hi] - before < chunk_bases) { c0 = n_pairs; break; }
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (S[mid] - before >= chunk_bases) hi = mid;
+                else lo = mid + 1;
+            }
+            c0 = lo + 1;
+        }
+        cstart[nc] = n_pairs;
+        *n_chunks = nc;
+    }
+}
+
+}  // namespace
+
+hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *lens, int64_t chunk_bases,
+                               int64_t *cstart, int64_t *scan_tmp, int32_t max_chunks, int32_t *n_chunks_dev,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_s2_chunks, dim3(1), dim3(1024), 0, s, n_pairs, stride, lens, chunk_bases, cstart, scan_tmp,
+                       max_chunks, n_chunks_dev);
+    return hipGetLastError();
+}
+
+hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
+                        const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
+                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
+                        const AfTails *tails, hipStream_t s) {
+    // zscratch holds n_cu * 4 * AF_K2_WPS slots (api.hip ensure_zscratch), enough for both grids
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    const int cpl = (stride + 1 + 63) / 64;
+    dim3 g(n_cu * 4 * AF_S2_WPS), g3(n_cu * 16), b(64);
+#define AF_GO(C) hipLaunchKernelGGL((k_s2_regions<C>), g, b, 0, s, X, reads, stride, lens, p, o, cand, n_cand, w, \
+                                    zscratch, zstride)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    const int bs = 256;
+    const int64_t nb = n_pairs > 0 ? (n_pairs + bs - 1) / bs : 1;
+    hipLaunchKernelGGL(k_s2_classify, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, X.n, hits, p, o, w, out);
+    hipLaunchKernelGGL(k_s2_pestat, dim3((unsigned)w.max_chunks), dim3(256), 0, s, w, o.max_ins);
+    const AfTails t = tails ? *tails : AfTails{};
+#define AF_GO(C) hipLaunchKernelGGL((k_s2_pairs<C>), g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, out, zscratch, \
+                                    zstride, t, tails ? 1 : 0)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}

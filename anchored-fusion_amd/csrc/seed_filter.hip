@@ -280,7 +280,7 @@ __device__ void one_tile(const K1 &k, const uint8_t *__restrict__ reads, int64_t
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const int32_t *__restrict__ lens,
     const uint32_t *__restrict__ bloom_g, int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand,
-    int32_t *__restrict__ cnt_g, int32_t *__restrict__ cnt_next) {
+    int32_t *__restrict__ cnt_g, int32_t *__restrict__ cnt_next, int32_t *__restrict__ s2z) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nw = 1 << bl_bits;
     uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + (size_t)nw * 4);
@@ -288,7 +288,11 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
     int *gbase = reinterpret_cast<int *>(gbal + AF_K1_PASS * AF_SEED_GROUPS);
     const K1 k{32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;  // next epoch's count (see af_internal.h)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // next epoch's count; this epoch's S2 words (af_internal.h)
+        *cnt_next = 0;
+        s2z[0] = 0;
+        s2z[2 * AF_HEAD_STRIDE] = 0;
+    }
     fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
     const int64_t ntiles = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_ragged(
 __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     const uint8_t *__restrict__ reads, int64_t n_reads, int32_t stride, const uint32_t *__restrict__ bloom_g,
     int bl_bits, int32_t *__restrict__ hits, int32_t *__restrict__ cand, int32_t *__restrict__ cnt_g,
-    int32_t *__restrict__ cnt_next) {
+    int32_t *__restrict__ cnt_next, int32_t *__restrict__ s2z) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int CAP = AF_K1_PASS * AF_SEED_BTILE;  // reads per sub-range (LDS counters)
     const int nw = 1 << bl_bits;
@@ -317,7 +321,11 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     const K1 k{32 - bl_bits, (uint32_t)(nw - 1) << 2, 1.0f / (float)stride, stride, (int)(threadIdx.x & 63),
                __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))};
     const int lane = k.lane, wv = k.wv;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *cnt_next = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *cnt_next = 0;
+        s2z[0] = 0;
+        s2z[2 * AF_HEAD_STRIDE] = 0;
+    }
     // this block's range [ra, rb) in units of u reads
     const int lowbit = stride & -stride;  // gcd(stride, 16) = min(lowbit, 16)
     const int u = 16 / (lowbit < 16 ? lowbit : 16);
@@ -453,10 +461,12 @@ size_t af_seed_filter_lds(int bl_bits) {
 
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next,
-                                 int n_cu, hipStream_t s) {
+                                 int32_t *s2z, int n_cu, hipStream_t s) {
     if (n_reads <= 0) {
         hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int32_t), s);
-        return e == hipSuccess ? hipMemsetAsync(cnt_next, 0, sizeof(int32_t), s) : e;
+        if (e == hipSuccess) e = hipMemsetAsync(cnt_next, 0, sizeof(int32_t), s);
+        if (e == hipSuccess) e = hipMemsetAsync(s2z, 0, sizeof(int32_t), s);
+        return e == hipSuccess ? hipMemsetAsync(s2z + 2 * AF_HEAD_STRIDE, 0, sizeof(int32_t), s) : e;
     }
     const int64_t want = (n_reads + AF_SEED_BTILE - 1) / AF_SEED_BTILE;
     const size_t lds = af_seed_filter_lds(ix.bl_bits);
@@ -480,9 +490,9 @@ hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64
     dim3 grid((unsigned)blocks), block(64 * AF_SEED_WAVES);
     if (lens)
         hipLaunchKernelGGL(k_seed_ragged, grid, block, lds, s, reads, n_reads, stride, lens, ix.bloom, ix.bl_bits,
-                           hits, cand, cnt, cnt_next);
+                           hits, cand, cnt, cnt_next, s2z);
     else
         hipLaunchKernelGGL(k_seed_stream, grid, block, lds, s, reads, n_reads, stride, ix.bloom, ix.bl_bits, hits,
-                           cand, cnt, cnt_next);
+                           cand, cnt, cnt_next, s2z);
     return hipGetLastError();
 }

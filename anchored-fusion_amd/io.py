@@ -106,6 +106,10 @@ class Names:
     def __iter__(self):
         return (self[k] for k in range(len(self)))
 
+    def slice(self, a, b):
+        """Names of pairs [a, b) (shares the arena)."""
+        return Names(self.arena, self.off[a:b])
+
     @staticmethod
     def concat(parts):
         if len(parts) == 1:

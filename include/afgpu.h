@@ -78,6 +78,21 @@ typedef struct {
     uint32_t *cigar;
 } af_aln_out;
 
+/* bwa mem paired-end options (bwa 0.7.17 defaults, af_pe_default) and the batch's place in
+ * bwa's input stream.  bwa estimates insert sizes per chunk of >= chunk_bases bases
+ * (10,000,000 x the -t thread count); a batch must start at a chunk boundary, pair_base being
+ * the global index of its first pair (bwa's read-id hash tie-breaks depend on it). */
+typedef struct {
+    int32_t pen_unpaired;   /* -U, 17 */
+    int32_t max_ins;        /* 10000 (<= 16383 here) */
+    int32_t max_matesw;     /* 50 */
+    int32_t split_width;    /* 10: re-seed SMEMs occurring at most this often */
+    int32_t max_mem_intv;   /* 20: third seeding pass (-y) */
+    int32_t max_chain_gap;  /* 10000 */
+    int64_t chunk_bases;    /* 10,000,000 x threads (-K) */
+    int64_t pair_base;
+} af_pe;
+
 /* One placement of a query on a reference (af_place).  Replaces one PSL row of the
  * reference's BLAT searches (functions.py:341, 530, 1007, 1071, 1122, 1244) and one SAM record
  * of its genome `bwa mem` calls (Anchored_Fusion.py:188, functions.py:716). */
@@ -96,6 +111,7 @@ int af_ctx_create(int device, af_ctx **out);
 void af_ctx_destroy(af_ctx *ctx);
 const char *af_last_error(const af_ctx *ctx);
 void af_params_default(af_params *p);
+void af_pe_default(af_pe *pe);
 
 /* anchor index (doubled reference anchor ++ revcomp, 16-mer position map, Bloom seed filter) */
 int af_index_build(af_ctx *ctx, const char *anchor, int64_t len, af_index **out);
@@ -107,22 +123,23 @@ int af_index_filter_table(const af_index *idx, uint32_t *out, int64_t cap);
 
 /* host buffers in, host buffers out; synchronous */
 int af_align_pairs(af_ctx *ctx, const af_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
-                   const int32_t *lens, const af_params *p, af_aln_out *out);
+                   const int32_t *lens, const af_params *p, const af_pe *pe, af_aln_out *out);
 /* device buffers in/out, asynchronous on `stream` (hipStream_t; NULL = default stream) */
 int af_align_pairs_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
-                          int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
-                          void *stream);
+                          int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                          af_aln_out *d_out, void *stream);
 int af_seed_filter_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_reads,
                           int32_t stride, const int32_t *d_lens, int32_t *d_hits, void *stream);
 /* the rest of af_align_pairs_device after af_seed_filter_device ran on the same context and
  * stream with d_hits = d_out->hits for these reads: candidate alignment + pair flags */
 int af_align_candidates_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
-                               int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
-                               void *stream);
+                               int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                               af_aln_out *d_out, void *stream);
 /* af_align_candidates_device that also writes the split-read tails of af_split_tails_device
  * (same arguments and semantics, see below) from the pair-flag pass, without a pass of its own. */
 int af_align_candidates_tails_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_reads, int64_t n_pairs,
-                                     int32_t stride, const int32_t *d_lens, const af_params *p, af_aln_out *d_out,
+                                     int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                                     af_aln_out *d_out,
                                      int32_t min_clip, int64_t read_base, int32_t append, int64_t cap,
                                      uint8_t *d_tails, int32_t *d_tail_lens, int32_t *d_tail_read,
                                      int32_t *d_n_tails, void *stream);

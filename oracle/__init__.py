@@ -22,6 +22,13 @@ class Params(ctypes.Structure):
         "min_seed_len", "max_occ", "T", "max_ext", "max_mems")]
 
 
+class Pe(ctypes.Structure):
+    """bwa mem paired-end options + the batch's place in bwa's input stream (afo_pe)."""
+    _fields_ = [("pen_unpaired", ctypes.c_int32), ("max_ins", ctypes.c_int32), ("max_matesw", ctypes.c_int32),
+                ("split_width", ctypes.c_int32), ("max_mem_intv", ctypes.c_int32), ("max_chain_gap", ctypes.c_int32),
+                ("chunk_bases", ctypes.c_int64), ("pair_base", ctypes.c_int64)]
+
+
 class _Out(ctypes.Structure):
     _fields_ = [("flag", ctypes.c_void_p), ("pos", ctypes.c_void_p), ("score", ctypes.c_void_p),
                 ("n_cigar", ctypes.c_void_p), ("hits", ctypes.c_void_p), ("cigar", ctypes.c_void_p)]
@@ -55,8 +62,9 @@ def lib():
         L.afo_place.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
                                 ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.afo_align_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-                                      ctypes.c_void_p, ctypes.POINTER(Params), ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.POINTER(Params), ctypes.POINTER(Pe), ctypes.c_int,
                                       ctypes.POINTER(_Out)]
+        L.afo_pe_default.argtypes = [ctypes.POINTER(Pe)]
         _lib = L
     return _lib
 
@@ -65,6 +73,14 @@ def default_params():
     p = Params()
     lib().afo_params_default(ctypes.byref(p))
     return p
+
+
+def default_pe(**kw):
+    pe = Pe()
+    lib().afo_pe_default(ctypes.byref(pe))
+    for k, v in kw.items():
+        setattr(pe, k, v)
+    return pe
 
 
 class OracleIndex:
@@ -93,8 +109,10 @@ class OracleIndex:
                               None if lp is None else lp.ctypes.data, hits.ctypes.data)
         return hits
 
-    def align_pairs(self, reads, lens=None, params=None, threads=0):
-        """reads: [2N, stride] uint8 pair-major.  Returns dict of per-read arrays."""
+    def align_pairs(self, reads, lens=None, params=None, threads=0, pe=None, pair_base=0, chunk_bases=None):
+        """bwa mem -M paired-end restatement (bwa_pe.c).  reads: [2N, stride] uint8 pair-major,
+        starting at a bwa chunk boundary; pair_base = global index of the first pair.
+        Returns a dict of per-read arrays (one primary record per read)."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
         nr = reads.shape[0]
         assert nr % 2 == 0
@@ -102,10 +120,14 @@ class OracleIndex:
         out["cigar"] = np.zeros((nr, MAX_CIGAR), dtype=np.uint32)
         o = _Out(*(out[k].ctypes.data for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
         p = params or default_params()
+        e = pe or default_pe()
+        e.pair_base = int(pair_base)
+        if chunk_bases is not None:
+            e.chunk_bases = int(chunk_bases)
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
         rc = lib().afo_align_pairs(self.h, reads.ctypes.data, nr // 2, reads.shape[1],
-                                   None if lp is None else lp.ctypes.data, ctypes.byref(p), int(threads),
-                                   ctypes.byref(o))
+                                   None if lp is None else lp.ctypes.data, ctypes.byref(p), ctypes.byref(e),
+                                   int(threads), ctypes.byref(o))
         if rc != 0:
             raise RuntimeError(f"afo_align_pairs failed: {rc}")
         return out

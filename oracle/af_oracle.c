@@ -7,6 +7,7 @@
  * algorithm it restates; nothing here is called by the product path.
  */
 #include "af_oracle.h"
+#include "af_oracle_int.h"
 #include <stdlib.h>
 #include <string.h>
 #include <math.h>
@@ -23,11 +24,14 @@ struct afo_index {
     uint32_t *kmer;     /* sorted by (kmer, pos)                            */
     int32_t *kpos;
     int32_t bl_bits;    /* log2 Bloom words                                */
-    uint32_t *bloom;    /* 2 words per block                               */
+    uint32_t *bloom;    /* K1 filter over the bwa text's 16-mers            */
+    afo_text *X;        /* S2: the bwa text (bwa_pe.c)                      */
 };
 
+const afo_text *afo_index_text(const afo_index *I) { return I->X; }
+
 /* ---- encoding ---------------------------------------------------------------------- */
-static inline uint8_t nt4(uint8_t c) {
+uint8_t afo_nt4(uint8_t c) {
     switch (c) {
     case 'A': case 'a': return 0;
     case 'C': case 'c': return 1;
@@ -83,7 +87,7 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
     I->n = n;
     I->D = (uint8_t *)malloc(2 * n);
     for (int64_t i = 0; i < n; ++i) {
-        uint8_t c = nt4((uint8_t)anchor[i]);
+        uint8_t c = afo_nt4((uint8_t)anchor[i]);
         I->D[i] = c;
         I->D[2 * n - 1 - i] = c < 4 ? 3 - c : 4;
     }
@@ -100,33 +104,39 @@ afo_index *afo_index_build(const char *anchor, int64_t n) {
     I->nk = m;
     I->kmer = (uint32_t *)malloc(sizeof(uint32_t) * (m + 1));
     I->kpos = (int32_t *)malloc(sizeof(int32_t) * (m + 1));
-    int64_t nd = 0;
     for (int64_t i = 0; i < m; ++i) {
         I->kmer[i] = (uint32_t)(tmp[i] >> 32);
         I->kpos[i] = (int32_t)(tmp[i] & 0xffffffffu);
-        if (i == 0 || I->kmer[i] != I->kmer[i - 1]) ++nd;
     }
-    /* Bloom filter of the distinct 16-mers: 2^bl_bits 32-bit words, ~2.4 words per key (at
-     * most 2^15), four bits set in each of two words */
+    /* Bloom filter of the distinct 16-mers of the bwa text T that do not cross the strand
+     * boundary (seeds never do): 2^bl_bits 32-bit words, ~2.4 words per key (at most 2^15),
+     * four bits set in each of two words */
+    I->X = afo_text_build(anchor, n);
+    int64_t mk = 0;
+    uint64_t *tk = afo_text_kmers_noncrossing(I->X, &mk);
+    int64_t nd = 0;
+    for (int64_t i = 0; i < mk; ++i)
+        if (i == 0 || (tk[i] >> 32) != (tk[i - 1] >> 32)) ++nd;
     int bits = 8;
     while ((double)(1LL << bits) < 2.4 * (double)nd && bits < 15) ++bits;
     I->bl_bits = bits;
     I->bloom = (uint32_t *)calloc((size_t)1 << bits, sizeof(uint32_t));
-    for (int64_t i = 0; i < m; ++i) {
-        if (i > 0 && I->kmer[i] == I->kmer[i - 1]) continue;
-        uint32_t key = 0;  /* base j of the 16-mer (bits 2j of kmer) to bits 8(j&3)+2(j>>2) */
-        for (int j = 0; j < AFO_K; ++j) key |= ((I->kmer[i] >> (2 * j)) & 3u) << (8 * (j & 3) + 2 * (j >> 2));
+    for (int64_t i = 0; i < mk; ++i) {
+        if (i > 0 && (tk[i] >> 32) == (tk[i - 1] >> 32)) continue;
+        uint32_t km = (uint32_t)(tk[i] >> 32), key = 0;  /* base j (bits 2j) to bits 8(j&3)+2(j>>2) */
+        for (int j = 0; j < AFO_K; ++j) key |= ((km >> (2 * j)) & 3u) << (8 * (j & 3) + 2 * (j >> 2));
         uint64_t h = k1_hash(key);
         I->bloom[k1_w1(h, bits)] |= k1_mask((uint32_t)h);
         I->bloom[k1_w2(h, bits)] |= k1_mask((uint32_t)(h >> 32));
     }
+    free(tk);
     free(tmp);
     return I;
 }
 
 void afo_index_free(afo_index *I) {
     if (!I) return;
-    free(I->D); free(I->kmer); free(I->kpos); free(I->bloom); free(I);
+    free(I->D); free(I->kmer); free(I->kpos); free(I->bloom); afo_text_free(I->X); free(I);
 }
 int64_t afo_index_len(const afo_index *I) { return I->n; }
 int32_t afo_filter_words(const afo_index *I) { return 1 << I->bl_bits; }
@@ -163,15 +173,14 @@ void afo_seed_filter(const afo_index *I, const uint8_t *reads, int64_t n_reads, 
 }
 
 /* ---- score matrix (bwa_fill_scmat): a / -b for ACGT, -1 for anything with N -------- */
-static inline int sc(const afo_params *p, uint8_t x, uint8_t y) {
+int afo_sc(const afo_params *p, uint8_t x, uint8_t y) {
     if (x > 3 || y > 3) return -1;
     return x == y ? p->a : -p->b;
 }
 
 /* ---- ksw_extend restated (bwa ksw.c ksw_extend2): target rows, query columns ------- */
-typedef struct { int32_t h, e; } eh_t;
 
-static int ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
+int afo_ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
                   int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
                   int *_gscore, int *_max_off) {
     eh_t eh[AFO_MAX_READ + 2];
@@ -208,7 +217,7 @@ static int ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *targe
             eh_t *q = &eh[j];
             int h, M = q->h, e = q->e;
             q->h = h1;
-            M = M ? M + sc(p, ti, query[j]) : 0;
+            M = M ? M + afo_sc(p, ti, query[j]) : 0;
             h = M > e ? M : e;
             h = h > f ? h : f;
             h1 = h;
@@ -248,14 +257,14 @@ static int ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *targe
 }
 
 /* ---- ksw_global restated (bwa ksw.c ksw_global2) with traceback -------------------- */
-static inline int push_cigar(uint32_t *cig, int n, int cap, int op, int len) {
+static int push_cigar(uint32_t *cig, int n, int cap, int op, int len) {
     if (n > 0 && (int)(cig[n - 1] & 0xf) == op) { cig[n - 1] += (uint32_t)len << 4; return n; }
     if (n < cap) cig[n] = (uint32_t)len << 4 | (uint32_t)op;
     return n + 1;
 }
 
 /* returns score; writes cigar (ops M=0 I=1 D=2), *n_cig may exceed cap (overflow) */
-static int global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
+int afo_global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
                      int w, uint32_t *cig, int cap, int *n_cig) {
     int oe_del = p->o_del + p->e_del, oe_ins = p->o_ins + p->e_ins;
     int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
@@ -276,7 +285,7 @@ static int global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *ta
             int32_t h, m = q->h, e = q->e;
             uint8_t d;
             q->h = h1;
-            m += sc(p, target[i], query[j]);
+            m += afo_sc(p, target[i], query[j]);
             d = m >= e ? 0 : 1;
             h = m >= e ? m : e;
             d = h >= f ? d : 2;
@@ -317,7 +326,7 @@ static int global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *ta
 }
 
 /* ---- bwa helpers restated (bwamem.c cal_max_gap / infer_bw) ------------------------ */
-static inline int cal_max_gap(const afo_params *p, int qlen) {
+int afo_cal_max_gap(const afo_params *p, int qlen) {
     int l_del = (int)((double)(qlen * p->a - p->o_del) / p->e_del + 1.);
     int l_ins = (int)((double)(qlen * p->a - p->o_ins) / p->e_ins + 1.);
     int l = l_del > l_ins ? l_del : l_ins;
@@ -325,7 +334,7 @@ static inline int cal_max_gap(const afo_params *p, int qlen) {
     return l < p->w << 1 ? l : p->w << 1;
 }
 
-static inline int infer_bw(int l1, int l2, int score, int a, int q, int r) {
+int afo_infer_bw(int l1, int l2, int score, int a, int q, int r) {
     int w;
     if (l1 == l2 && l1 * a - score < (q + r - a) << 1) return 0;
     w = (int)((double)((l1 < l2 ? l1 : l2) * a - score - q) / r + 2.);
@@ -386,9 +395,9 @@ static int find_mems(const afo_index *I, const uint8_t *q, int l, const afo_para
 /* mem_chain2aln restated for a single-seed chain */
 static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t *s, const afo_params *p, reg_t *a) {
     int64_t n2 = 2 * I->n;
-    int64_t b = s->rb - (s->qb + cal_max_gap(p, s->qb));
+    int64_t b = s->rb - (s->qb + afo_cal_max_gap(p, s->qb));
     int rem = l - s->qb - s->len;
-    int64_t e = s->rb + s->len + (rem + cal_max_gap(p, rem));
+    int64_t e = s->rb + s->len + (rem + afo_cal_max_gap(p, rem));
     int64_t rmax0 = b > 0 ? b : 0, rmax1 = e < n2 ? e : n2;
     if (rmax0 < I->n && I->n < rmax1) {
         if (s->rb < I->n) rmax1 = I->n; else rmax0 = I->n;
@@ -405,7 +414,7 @@ static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t
         for (int it = 0; it < 2; ++it) {
             int prev = a->score;
             aw0 = p->w << it;
-            a->score = ext_dp(s->qb, qs, tmp, rs, p, aw0, p->pen_clip5, p->zdrop, s->len * p->a, &qle, &tle,
+            a->score = afo_ext_dp(s->qb, qs, tmp, rs, p, aw0, p->pen_clip5, p->zdrop, s->len * p->a, &qle, &tle,
                               &gtle, &gscore, &max_off);
             if (a->score == prev || max_off < (aw0 >> 1) + (aw0 >> 2)) break;
         }
@@ -424,7 +433,7 @@ static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t
         for (int it = 0; it < 2; ++it) {
             int prev = a->score;
             aw1 = p->w << it;
-            a->score = ext_dp(l - qe, q + qe, (int)(rmax1 - rmax0 - re), rseq + re, p, aw1, p->pen_clip3, p->zdrop,
+            a->score = afo_ext_dp(l - qe, q + qe, (int)(rmax1 - rmax0 - re), rseq + re, p, aw1, p->pen_clip3, p->zdrop,
                               sc0, &qle, &tle, &gtle, &gscore, &max_off);
             if (a->score == prev || max_off < (aw1 >> 1) + (aw1 >> 2)) break;
         }
@@ -441,21 +450,21 @@ static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t
 }
 
 /* bwa_gen_cigar2 restated; query/ref segments in forward-reference orientation */
-static int gen_cigar(const afo_index *I, const afo_params *p, int w_, int lq, const uint8_t *qseg, int64_t rb,
-                     int64_t re, uint32_t *cig, int *n_cig) {
+int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
+                  int64_t rb, int64_t re, uint32_t *cig, int *n_cig) {
     uint8_t qq[AFO_MAX_READ], rr[2 * AFO_MAX_READ + 512];
     int rlen = (int)(re - rb);
     int score = 0;
     for (int i = 0; i < lq; ++i) qq[i] = qseg[i];
-    for (int i = 0; i < rlen; ++i) rr[i] = I->D[rb + i];
-    if (rb >= I->n) { /* reverse both so indels land leftmost in forward coordinates */
+    for (int i = 0; i < rlen; ++i) rr[i] = text[rb + i];
+    if (rb >= n) { /* reverse both so indels land leftmost in forward coordinates */
         for (int i = 0; i < lq >> 1; ++i) { uint8_t t = qq[i]; qq[i] = qq[lq - 1 - i]; qq[lq - 1 - i] = t; }
         for (int i = 0; i < rlen >> 1; ++i) { uint8_t t = rr[i]; rr[i] = rr[rlen - 1 - i]; rr[rlen - 1 - i] = t; }
     }
     if (lq == rlen && w_ == 0) {
         cig[0] = (uint32_t)lq << 4;
         *n_cig = 1;
-        for (int i = 0; i < lq; ++i) score += sc(p, rr[i], qq[i]);
+        for (int i = 0; i < lq; ++i) score += afo_sc(p, rr[i], qq[i]);
     } else {
         int max_ins = (int)((double)(((lq + 1) >> 1) * p->a - p->o_ins) / p->e_ins + 1.);
         int max_del = (int)((double)(((lq + 1) >> 1) * p->a - p->o_del) / p->e_del + 1.);
@@ -466,7 +475,7 @@ static int gen_cigar(const afo_index *I, const afo_params *p, int w_, int lq, co
         w = w < w_ ? w : w_;
         int min_w = d + 3;
         w = w > min_w ? w : min_w;
-        score = global_dp(lq, qq, rlen, rr, p, w, cig, AFO_MAX_CIGAR, n_cig);
+        score = afo_global_dp(lq, qq, rlen, rr, p, w, cig, AFO_MAX_CIGAR, n_cig);
     }
     return score;
 }
@@ -477,7 +486,7 @@ static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const a
                         reg_t *regs, int reseed) {
     mem_t *mems = (mem_t *)malloc(sizeof(mem_t) * (p->max_mems > 0 ? p->max_mems : 1));
     int n_reg = 0, overflow = 0;
-    for (int i = 0; i < l; ++i) q[i] = nt4(ascii[i]);
+    for (int i = 0; i < l; ++i) q[i] = afo_nt4(ascii[i]);
     /* placement (reseed): while more than max_mems MEMs, raise the minimum MEM length by
      * AFO_RESEED_STEP up to AFO_RESEED_MAX (the GPU's AF_RESEED_STEP / AF_RESEED_MAX) */
     afo_params ps = *p;
@@ -498,11 +507,11 @@ static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const a
             if (s->rb < a->rb || s->rb + s->len > a->re || s->qb < a->qb || s->qb + s->len > a->qe) continue;
             if (10 * (s->len - a->seedlen0) > l) continue;
             int qd = s->qb - a->qb, rd = s->rb - a->rb;
-            int mg = cal_max_gap(p, qd < rd ? qd : rd);
+            int mg = afo_cal_max_gap(p, qd < rd ? qd : rd);
             int ww = mg < a->w ? mg : a->w;
             if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
             qd = a->qe - (s->qb + s->len); rd = a->re - (s->rb + s->len);
-            mg = cal_max_gap(p, qd < rd ? qd : rd);
+            mg = afo_cal_max_gap(p, qd < rd ? qd : rd);
             ww = mg < a->w ? mg : a->w;
             if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
         }
@@ -514,21 +523,6 @@ static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const a
     return n_reg;
 }
 
-static void align_read(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, rec_t *out) {
-    uint8_t q[AFO_MAX_READ];
-    reg_t regs[64];
-    memset(out, 0, sizeof(*out));
-    out->flag = 0x4;
-    if (l > AFO_MAX_READ) l = AFO_MAX_READ;
-    int n_reg = read_regions(I, ascii, l, p, q, regs, 0);
-    if (n_reg < 0) { out->flag |= FLAG_MEM_OVERFLOW; return; }
-    int best = -1;
-    for (int r = 0; r < n_reg; ++r)
-        if (best < 0 || regs[r].score > regs[best].score) best = r;
-    if (best < 0 || regs[best].score < p->T) return;
-    emit_region(I, q, l, p, &regs[best], out, NULL, NULL);
-}
-
 /* CIGAR and record of one region (the tail of align_read, shared with afo_place).  *matches
  * (optional) = identical aligned bases; *ref_span (optional) = reference bases covered. */
 static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_params *p, const reg_t *a,
@@ -538,15 +532,15 @@ static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_p
      * segment for reverse hits (bwa_gen_cigar2), i.e. aligns in forward-ref order */
     const uint8_t *qseg = q + a->qb;
     int lq = a->qe - a->qb;
-    int tmp_w = infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_del, p->e_del);
-    int w2 = infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_ins, p->e_ins);
+    int tmp_w = afo_infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_del, p->e_del);
+    int w2 = afo_infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_ins, p->e_ins);
     w2 = w2 > tmp_w ? w2 : tmp_w;
     if (w2 > p->w) w2 = w2 < a->w ? w2 : a->w;
     uint32_t cig[AFO_MAX_CIGAR];
     int nc = 0, score = 0, last_sc = -(1 << 30), it = 0;
     do {
         w2 = w2 < p->w << 2 ? w2 : p->w << 2;
-        score = gen_cigar(I, p, w2, lq, qseg, a->rb, a->re, cig, &nc);
+        score = afo_gen_cigar(I->D, I->n, p, w2, lq, qseg, a->rb, a->re, cig, &nc);
         if (score == last_sc || w2 == p->w << 2) break;
         last_sc = score;
         w2 <<= 1;
@@ -601,46 +595,6 @@ static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_p
     out->flag = (is_rev ? 0x10 : 0) | (of ? FLAG_CIGAR_OVERFLOW : 0);
     out->pos = (int32_t)pos;
     out->score = a->score;
-}
-
-int afo_align_pairs(const afo_index *I, const uint8_t *reads, int64_t n_pairs, int32_t stride,
-                    const int32_t *lens, const afo_params *p, int n_threads, afo_out *out) {
-    int64_t nr = 2 * n_pairs;
-    rec_t *recs = (rec_t *)malloc(sizeof(rec_t) * (nr > 0 ? nr : 1));
-    if (out->hits) afo_seed_filter(I, reads, nr, stride, lens, out->hits);
-#ifdef _OPENMP
-    if (n_threads > 0) omp_set_num_threads(n_threads);
-#pragma omp parallel for schedule(dynamic, 256)
-#endif
-    for (int64_t r = 0; r < nr; ++r) {
-        int l = lens ? lens[r] : stride;
-        align_read(I, reads + r * (int64_t)stride, l, p, &recs[r]);
-    }
-    /* pair flags (mem_aln2sam conventions): 0x1 paired, 0x40/0x80 mate order, 0x8/0x20 mate
-     * state; an unmapped read with a mapped mate takes the mate's position and strand */
-    for (int64_t pp = 0; pp < n_pairs; ++pp) {
-        for (int m = 0; m < 2; ++m) {
-            rec_t *x = &recs[2 * pp + m], *y = &recs[2 * pp + (m ^ 1)];
-            int64_t r = 2 * pp + m;
-            int xf = x->flag, yf = y->flag;
-            int f = 0x1 | (m ? 0x80 : 0x40) | (xf & ~0x4 & 0x30000);
-            int32_t pos = x->pos;
-            if (!(xf & 0x4)) f |= xf & 0x10;
-            else f |= 0x4;
-            if (yf & 0x4) f |= 0x8;
-            else f |= (yf & 0x10) ? 0x20 : 0;
-            if ((xf & 0x4) && !(yf & 0x4)) { pos = y->pos; f |= (yf & 0x10); }
-            if ((xf & 0x4) && (yf & 0x4)) pos = -1;
-            out->flag[r] = f;
-            out->pos[r] = pos;
-            out->score[r] = x->score;
-            out->n_cigar[r] = (xf & 0x4) ? 0 : x->n_cigar;
-            for (int c = 0; c < AFO_MAX_CIGAR; ++c)
-                out->cigar[r * AFO_MAX_CIGAR + c] = (!(xf & 0x4) && c < x->n_cigar) ? x->cigar[c] : 0;
-        }
-    }
-    free(recs);
-    return 0;
 }
 
 /* Multi-hit placement (the searches behind S4-S8: every region of a query scoring >= T, best

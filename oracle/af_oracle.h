@@ -9,6 +9,11 @@
  * third-party, NOT vendored under /root/reference) at Anchored_Fusion.py:182.  bwa is
  * absent from this image, so this file restates bwa-mem's published algorithm
  * (Li 2013, arXiv:1303.3997; ksw extension/global DP as published in bwa 0.7.17):
+ * S2 (bwa_pe.c) restates bwa 0.7.17's paired-end path: SMEM seeding with re-seeding and the
+ * third pass, chaining and the chain filter, seed extension, dedup/patch, insert-size
+ * estimation per chunk, mate rescue (ksw_align2), -M primary marking with bwa's hash
+ * tie-break, pair selection, and the record/flag rules of mem_aln2sam.
+ * afo_place (af_oracle.c) is the multi-hit placement behind the genome/BLAT searches:
  * MEM seeds >= 19 nt on the doubled reference (anchor ++ revcomp), per-seed banded
  * extension with z-drop and clipping penalty, band inference + global DP for CIGAR.
  * Parity with the bwa binary itself is UNPINNED; the oracle is
@@ -56,6 +61,27 @@ typedef struct {
 
 typedef struct afo_index afo_index;
 
+/* bwa mem paired-end options (bwa 0.7.17 mem_opt_init defaults, afo_pe_default) and the
+ * batch's place in bwa's input stream */
+typedef struct {
+    int32_t pen_unpaired;   /* -U 17                                                         */
+    int32_t max_ins;        /* 10000: insert sizes above are ignored by mem_pestat             */
+    int32_t max_matesw;     /* 50: mate-SW rounds per end                                      */
+    int32_t split_width;    /* 10: re-seed an SMEM occurring at most this often (-r 1.5 split) */
+    int32_t max_mem_intv;   /* 20: third seeding pass (-y)                                      */
+    int32_t max_chain_gap;  /* 10000                                                           */
+    int64_t chunk_bases;    /* bases per bwa batch: 10,000,000 x threads (-K)                   */
+    int64_t pair_base;      /* global index of the first pair (bwa's n_processed / 2)           */
+} afo_pe;
+
+/* per-read caps of the S2 restatement (AF_S2_MAX_* on the GPU); overflow -> unmapped + flag */
+#define AFO_PE_MAX_PMEM 128
+#define AFO_PE_MAX_SEED 64
+#define AFO_PE_MAX_OCC 128
+#define AFO_PE_MAX_CHAIN 32
+#define AFO_PE_MAX_REG 32
+#define AFO_PE_MAX_TSPAN 1024  /* longest reference span mem_patch_reg merges */
+
 void afo_params_default(afo_params *p);
 afo_index *afo_index_build(const char *anchor, int64_t n);
 void afo_index_free(afo_index *idx);
@@ -65,9 +91,12 @@ const uint32_t *afo_filter_table(const afo_index *idx);
 /* K1 restatement: per read, number of sampled 16-mers passing the anchor filter */
 void afo_seed_filter(const afo_index *idx, const uint8_t *reads, int64_t n_reads, int32_t stride,
                      const int32_t *lens, int32_t *hits);
-/* S2 restatement: SE alignment of every read + pair flags (reads pair-major: 2p, 2p+1) */
+/* S2 restatement (bwa_pe.c): bwa mem paired-end alignment of every pair (reads pair-major:
+ * 2p, 2p+1), one primary record per read.  The batch starts at a bwa chunk boundary; chunks of
+ * >= pe->chunk_bases bases share insert-size statistics.  pe may be NULL (defaults). */
+void afo_pe_default(afo_pe *pe);
 int afo_align_pairs(const afo_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
-                    const int32_t *lens, const afo_params *p, int n_threads, afo_out *out);
+                    const int32_t *lens, const afo_params *p, const afo_pe *pe, int n_threads, afo_out *out);
 
 /* multi-hit placement: hits[r * max_hits + k], n_hits[r] (-1 = MEM overflow) */
 int afo_place(const afo_index *idx, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,

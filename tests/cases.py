@@ -69,3 +69,42 @@ def ragged(reads, seed):
     for i in range(n):
         out[i, lens[i]:] = ord("N")
     return out, lens
+
+
+def rescue_pairs(anchor: bytes, n_normal=60, read_len=100, insert=250, seed=5):
+    """n_normal proper FR pairs from the anchor (insert-size model) plus one probe pair whose
+    mate 2 carries a mismatch every 12 bases: no exact 19-mer (K1 finds nothing) but a local
+    alignment score far above min_seed_len at the right distance.  Returns (reads, probe pair)."""
+    rng = np.random.default_rng(seed)
+    rc = sim.revcomp
+    seqs = []
+    n = len(anchor)
+    for k in range(n_normal):
+        a = int(rng.integers(0, n - insert - 1))
+        ins = insert + int(rng.integers(-15, 16))
+        frag = anchor[a:a + ins]
+        seqs += [frag[:read_len], rc(frag[-read_len:])]
+    a = 2000
+    frag = anchor[a:a + insert]
+    m2 = bytearray(rc(frag[-read_len:]))
+    for k in range(6, read_len, 12):
+        m2[k] = ord("A") if m2[k] != ord("A") else ord("G")
+    seqs += [frag[:read_len], bytes(m2)]
+    reads, _ = _pad(seqs, read_len)
+    return reads, n_normal
+
+
+def repeat_anchor_pairs(anchor: bytes, read_len=100, n=12, seed=9):
+    """An anchor with a 400-nt segment duplicated at its end, and pairs whose mate 1 lies inside
+    the segment (two equal-score hits) with mate 2 in unique sequence far away (no pairing
+    decides between the copies)."""
+    seg = anchor[1000:1400]
+    anc2 = anchor + b"ACGTTGCA" * 4 + seg
+    rng = np.random.default_rng(seed)
+    rc = sim.revcomp
+    seqs = []
+    for k in range(n):
+        a = 1000 + int(rng.integers(0, 400 - read_len))
+        b = 4000 + int(rng.integers(0, 1000))
+        seqs += [anchor[a:a + read_len], rc(anchor[b:b + read_len])]
+    return anc2, _pad(seqs, read_len)[0]

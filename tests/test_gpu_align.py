@@ -27,9 +27,9 @@ def oidx(anchor):
     return oracle.OracleIndex(anchor)
 
 
-def _both(aligner, oidx, reads, lens=None):
-    g = aligner.align_pairs(reads, lens).as_dict()
-    r = oidx.align_pairs(reads, lens, threads=8)
+def _both(aligner, oidx, reads, lens=None, pair_base=0):
+    g = aligner.align_pairs(reads, lens, pair_base=pair_base).as_dict()
+    r = oidx.align_pairs(reads, lens, threads=8, pair_base=pair_base, chunk_bases=int(aligner.pe.chunk_bases))
     return g, r
 
 
@@ -41,7 +41,7 @@ def test_bundled_parity(aligner, oidx, bundled_pairs):
     names, reads, lens = bundled_pairs
     g, r = _both(aligner, oidx, reads, lens)
     assert_records_equal(g, r, reads)
-    assert ((g["flag"] & 4) == 0).sum() == 1261
+    assert ((g["flag"] & 4) == 0).sum() == 1264  # 1,261 seeded + 3 rescued mates (test_oracle.py)
 
 
 def test_align_fastq_streamed_matches_oracle(aligner, oidx, bundled_pairs):
@@ -53,6 +53,45 @@ def test_align_fastq_streamed_matches_oracle(aligner, oidx, bundled_pairs):
     n0, r0, l0 = bundled_pairs
     assert lens is None and l0 is None and (reads == r0).all() and list(names) == list(n0)
     assert_records_equal(res.as_dict(), oidx.align_pairs(reads, None, threads=8), reads)
+
+
+def test_rescue_parity(aligner, oidx, anchor):
+    """mem_matesw on the GPU: the unseedable mate is rescued exactly as by the oracle."""
+    from cases import rescue_pairs
+    reads, probe = rescue_pairs(anchor)
+    g, r = _both(aligner, oidx, reads)
+    assert_records_equal(g, r, reads)
+    assert g["hits"][2 * probe + 1] == 0 and not g["flag"][2 * probe + 1] & 4
+
+
+def test_tie_break_parity(anchor):
+    """Equal-score hits on a duplicated segment: the hash_64(read id) primary choice, for several
+    pair_base values (bwa's global read ids)."""
+    from anchored_fusion_amd.align import AnchorAligner
+    from cases import repeat_anchor_pairs
+    anc2, reads = repeat_anchor_pairs(anchor)
+    ix = oracle.OracleIndex(anc2)
+    picks = set()
+    with AnchorAligner(anc2, device=0) as a:
+        for base in (0, 1, 7, 1000, 123456, (1 << 31) - 5):
+            g, r = _both(a, ix, reads, pair_base=base)
+            assert_records_equal(g, r, reads)
+            picks.add(tuple(g["pos"][0::2]))
+    assert len(picks) > 1
+
+
+@pytest.mark.parametrize("chunk_pairs", [6, 250, 1013])
+def test_chunked_insert_stats_parity(anchor, oidx, chunk_pairs):
+    """Several bwa chunks in one batch (insert-size statistics per chunk), uniform and ragged."""
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.align import AnchorAligner
+    reads, _, _ = synthetic_pairs(anchor, 3000, 100, seed=61, fusion_frac=0.9)
+    with AnchorAligner(anchor, device=0, pe=_lib.default_pe(chunk_bases=200 * chunk_pairs)) as a:
+        g, r = _both(a, oidx, reads)
+        assert_records_equal(g, r, reads)
+        rr, lens = ragged(reads, 62)
+        g, r = _both(a, oidx, rr, lens)
+        assert_records_equal(g, r, rr)
 
 
 def test_edge_parity(aligner, oidx, anchor):
@@ -155,7 +194,17 @@ def test_full_size_properties(aligner, anchor):
     f = out["flag"].cpu().numpy()
     h = out["hits"].cpu().numpy()
     mapped = (f & 4) == 0
-    assert (h[mapped] > 0).all()                       # filter never drops a seeded read
+    # the filter never drops a seeded read: a mapped read without a K1 hit is a rescued mate
+    rescued = mapped & (h == 0)
+    assert (~np.repeat(((f[0::2] | f[1::2]) & 4) != 0, 2) | ~rescued).all()
+    assert rescued.sum() < 0.01 * mapped.sum()
+    # bwa's chunks (50,000 pairs of 2x100) are independent: two of them against the oracle alone
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    got["cigar"] = got["cigar"].view(np.uint32)
+    for c in (0, 10):
+        lo, hi = 50_000 * c, 50_000 * (c + 1)
+        want = oracle.OracleIndex(anchor).align_pairs(reads[2 * lo:2 * hi], threads=16, pair_base=lo)
+        assert_records_equal({k: v[2 * lo:2 * hi] for k, v in got.items()}, want, reads[2 * lo:2 * hi])
     nf = len(world["fusions"])
     from_fusion = np.repeat(truth["tid"] < nf, 2)
     assert mapped[~from_fusion].mean() < 1e-3          # background essentially never maps

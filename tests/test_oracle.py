@@ -37,11 +37,19 @@ def junctions(out):
 
 def test_bundled_only_bcr_fusion_reads_map(bundled_pairs, bundled_out):
     names = bundled_pairs[0]
-    mapped = (bundled_out["flag"] & 4) == 0
+    f, sc = bundled_out["flag"], bundled_out["score"]
+    mapped = (f & 4) == 0
     src = collections.Counter(names[r // 2].split("_")[0] for r in np.nonzero(mapped)[0])
     # every mapped read comes from the BCR-ABL1 transcript (EU216071.1); none from the 5 others
     assert set(src) == {"EU216071.1"}
-    assert src["EU216071.1"] == 1261  # = the 20-mer-seeded read count of SURVEY.md §4 item 2
+    # 1,261 reads seed and map on their own (the 20-mer-seeded count of SURVEY.md §4 item 2);
+    # mate rescue (mem_matesw) adds 3 mates whose anchor part is too short or too mismatched to
+    # seed: they score below -T 30 and are printed only because they pair properly
+    assert int((mapped & (sc >= 30)).sum()) == 1261
+    rescued = np.nonzero(mapped & (sc < 30))[0]
+    assert len(rescued) == 3
+    for r in rescued:
+        assert f[r] & 0x2 and not (f[r ^ 1] & 0x4) and bundled_out["hits"][r] >= 0
 
 
 def test_bundled_junction_known_answers(bundled_out):
@@ -56,15 +64,22 @@ def test_filter_is_superset_of_seeded(oidx, bundled_out):
 
 
 def test_pair_flags_consistent(bundled_out):
+    """mem_aln2sam's flag rules for one primary record per read."""
     f = bundled_out["flag"]
     assert ((f & 1) == 1).all()
     assert ((f[0::2] & 0x40) != 0).all() and ((f[1::2] & 0x80) != 0).all()
     m1, m2 = (f[0::2] & 4) == 0, (f[1::2] & 4) == 0
     assert (((f[0::2] & 8) != 0) == ~m2).all() and (((f[1::2] & 8) != 0) == ~m1).all()
-    # an unmapped read with a mapped mate is placed at its mate's position
+    # an unmapped read with a mapped mate is placed at its mate's position and strand
     p = bundled_out["pos"]
     one = m1 & ~m2
     assert (p[1::2][one] == p[0::2][one]).all()
+    assert ((f[1::2][one] & 0x10) == (f[0::2][one] & 0x10)).all()
+    # ... and the mapped read copies its own strand to the mate: 0x20 iff 0x10
+    assert (((f[0::2][one] & 0x20) != 0) == ((f[0::2][one] & 0x10) != 0)).all()
+    # the proper-pair bit only on pairs with both ends mapped; no secondary primary records
+    assert ((f & 0x2) == 0)[~np.repeat(m1 & m2, 2)].all()
+    assert ((f & 0x100) == 0).all()
 
 
 def test_synthetic_truth_positions(anchor, oidx):
@@ -103,3 +118,48 @@ def test_ragged_runs(anchor, oidx):
     rr, lens = ragged(reads, 5)
     out = oidx.align_pairs(rr, lens)
     assert ((out["flag"] & 4) == 0).sum() > 0
+
+
+def test_mate_rescue_changes_s3_partitions(anchor, oidx):
+    """A mate too mismatched to seed (no exact 19-mer, K1 hits 0) at the proper insert distance is
+    rescued by mem_matesw, so the pair leaves S3's one-end-anchored sets (-f 8 / -f 4,
+    Anchored_Fusion.py:186-187) and both reads reach anchored.bam (-F 772)."""
+    from anchored_fusion_amd.align import AlignResult, partition
+    from cases import rescue_pairs
+    reads, probe = rescue_pairs(anchor)
+    out = oidx.align_pairs(reads)
+    f = out["flag"]
+    r1, r2 = 2 * probe, 2 * probe + 1
+    assert out["hits"][r2] == 0                         # the mate cannot seed
+    assert not f[r1] & 4 and not f[r2] & 4 and f[r1] & 2  # ... yet maps, properly paired
+    res = AlignResult(**out)
+    tmp1, tmp2, anchored = partition(res)
+    assert r1 not in tmp1 and r2 not in tmp2 and r2 in anchored
+    # without a proper-pair model (too few pairs in the chunk) the same mate stays unmapped
+    lone = oidx.align_pairs(reads[2 * probe:2 * probe + 2])
+    assert lone["flag"][1] & 4 and lone["flag"][0] & 8
+    t1, t2, _ = partition(AlignResult(**lone))
+    assert 0 in t1 and 1 in t2
+
+
+def test_tie_break_follows_read_ids(anchor):
+    """A read matching two copies of a segment equally well: mem_mark_primary_se picks by
+    hash_64(read id), so the primary copy depends on the pair's global index (pair_base)."""
+    from cases import repeat_anchor_pairs
+    anc2, reads = repeat_anchor_pairs(anchor)
+    ix = oracle.OracleIndex(anc2)
+    picks = set()
+    for base in (0, 1, 7, 1000, 123456):
+        out = ix.align_pairs(reads, pair_base=base)
+        picks.add(tuple(out["pos"][0::2]))
+    assert len(picks) > 1
+
+
+def test_chunks_change_insert_stats(anchor, oidx):
+    """Insert-size statistics are per bwa chunk (bseq_read: >= chunk_bases bases): a rescue that
+    needs its chunk's pairs fails when the chunk is cut smaller."""
+    from cases import rescue_pairs
+    reads, probe = rescue_pairs(anchor)
+    big = oidx.align_pairs(reads)
+    small = oidx.align_pairs(reads, chunk_bases=200 * 6)   # 6 pairs of 2x100 per chunk
+    assert not big["flag"][2 * probe + 1] & 4 and small["flag"][2 * probe + 1] & 4

@@ -37,22 +37,3 @@ def test_place_recovers_tails():
     assert found >= 0.95 * total, (found, total)
 
 
-def test_place_matches_align_primary():
-    """The best placement of a query is the alignment record af_align_pairs would report."""
-    ctgs = contigs(n=2, length=8000)
-    blob, _ = concat_contigs(ctgs)
-    ix = oracle.OracleIndex(blob)
-    qs = queries(ctgs, 200, lens=(100,))
-    buf, lens = pack_queries([q for _, q, _ in qs] + ([qs[0][1]] if len(qs) % 2 else []))
-    p = oracle.default_params()
-    hits, nh = ix.place(buf, lens, p, max_hits=4, threads=4)
-    rec = ix.align_pairs(buf, lens, p, threads=4)
-    for i in range(len(qs)):
-        if nh[i] <= 0:
-            assert rec["flag"][i] & 4
-            continue
-        h = hits[i, 0]
-        assert not rec["flag"][i] & 4
-        assert rec["pos"][i] == h["t_start"] and rec["score"][i] == h["score"]
-        assert rec["n_cigar"][i] == h["n_cigar"]
-        assert (rec["cigar"][i][: h["n_cigar"]] == h["cigar"][: h["n_cigar"]]).all()
