@@ -127,13 +127,15 @@ struct S2Work {
     int2 *rmap;         // per read: {pool offset, n regions (-1 overflow)}; candidate reads only
     int32_t *plist;     // candidate pairs (K3a), consumed by K3c
     int32_t *n_plist;
-    int32_t *ilist;     // insert sizes, dir << 30 | isize, stored from each chunk's first pair
-    int32_t *icnt;      // per chunk: insert sizes stored
+    int32_t *ghist;     // [chunk][orientation][max_ins + 1] insert-size counts (zeroed by K3b after use)
     S2Pes *pes;         // [n_chunks][4]
-    const int64_t *cstart;  // chunk start pairs, *n_chunks + 1 entries
-    const int32_t *n_chunks;  // device word
+    int64_t ppc;        // pairs per chunk when every read has length stride (0: ragged, use cstart)
+    const int64_t *cstart;  // ragged: chunk start pairs, *n_chunks + 1 entries
+    const int32_t *n_chunks;  // ragged: device word
+    int32_t n_chunks_u; // uniform: the chunk count
     int32_t max_chunks;
     int32_t *heads_k2, *heads_k3;  // per-XCD dequeue heads (8 lines each)
+    void *plan;         // per listed pair: the record choice of K3c for K3d (s2.hip S2Plan)
 };
 
 // Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
@@ -221,6 +223,7 @@ hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs,
                         const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
                         const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
                         const AfTails *tails, hipStream_t s);
+size_t af_s2_plan_bytes();
 hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *lens, int64_t chunk_bases,
                                int64_t *cstart, int64_t *scan_tmp, int32_t max_chunks, int32_t *n_chunks_dev,
                                hipStream_t s);

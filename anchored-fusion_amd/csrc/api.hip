@@ -30,10 +30,12 @@ struct af_ctx {
     S2Reg *s2_pool = nullptr;
     int64_t s2_pool_cap = 0;
     int2 *s2_rmap = nullptr;
-    int32_t *s2_plist = nullptr, *s2_ilist = nullptr;
+    int32_t *s2_plist = nullptr, *s2_ghist = nullptr;
+    int64_t s2_ghist_ints = 0;
     int64_t *s2_scan = nullptr;
+    void *s2_plan = nullptr;
     int64_t s2_cap_pairs = 0;
-    int32_t *s2_icnt = nullptr, *s2_nchunks = nullptr;
+    int32_t *s2_nchunks = nullptr;
     S2Pes *s2_pes = nullptr;
     int64_t *s2_cstart = nullptr;
     int32_t s2_max_chunks = 0;
@@ -240,32 +242,40 @@ int ensure_s2_text(af_ctx *c, af_index *ix) {
 }
 
 // per-context S2 scratch for a batch of n_pairs (chunks of >= chunk_bases bases)
-int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bases) {
+int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bases, int32_t max_ins) {
     if (n_pairs > c->s2_cap_pairs) {
-        af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ilist); af_free(c->s2_scan);
-        c->s2_pool = nullptr; c->s2_rmap = nullptr; c->s2_plist = c->s2_ilist = nullptr; c->s2_scan = nullptr;
+        af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_scan); af_free(c->s2_plan);
+        c->s2_pool = nullptr; c->s2_rmap = nullptr; c->s2_plist = nullptr; c->s2_scan = nullptr; c->s2_plan = nullptr;
         c->s2_cap_pairs = 0;
         const int64_t cap = std::max<int64_t>(n_pairs, 1 << 16);
         c->s2_pool_cap = 2 * cap + (1 << 20);  // regions: candidates are a few % of the reads
         HIPCHK(c, hipMalloc(&c->s2_pool, sizeof(S2Reg) * c->s2_pool_cap));
         HIPCHK(c, hipMalloc(&c->s2_rmap, sizeof(int2) * 2 * cap));
         HIPCHK(c, hipMalloc(&c->s2_plist, sizeof(int32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->s2_ilist, sizeof(int32_t) * cap));
         HIPCHK(c, hipMalloc(&c->s2_scan, sizeof(int64_t) * cap));
+        HIPCHK(c, hipMalloc(&c->s2_plan, af_s2_plan_bytes() * cap));
         c->s2_cap_pairs = cap;
     }
     const int64_t mc = std::min<int64_t>(n_pairs, 2 * n_pairs * (int64_t)stride / std::max<int64_t>(chunk_bases, 1) + 2) + 1;
     if (mc > c->s2_max_chunks) {
-        af_free(c->s2_icnt); af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
-        c->s2_icnt = nullptr; c->s2_pes = nullptr; c->s2_cstart = nullptr; c->s2_nchunks = nullptr;
+        af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
+        c->s2_pes = nullptr; c->s2_cstart = nullptr; c->s2_nchunks = nullptr;
         c->s2_max_chunks = 0;
         const int64_t m = std::max<int64_t>(mc, 64);
-        HIPCHK(c, hipMalloc(&c->s2_icnt, sizeof(int32_t) * m));
-        HIPCHK(c, hipMemset(c->s2_icnt, 0, sizeof(int32_t) * m));
         HIPCHK(c, hipMalloc(&c->s2_pes, sizeof(S2Pes) * 4 * m));
         HIPCHK(c, hipMalloc(&c->s2_cstart, sizeof(int64_t) * (m + 1)));
         HIPCHK(c, hipMalloc(&c->s2_nchunks, sizeof(int32_t)));
         c->s2_max_chunks = (int32_t)m;
+    }
+    // insert-size histograms [chunk][orientation][max_ins + 1], zero between calls (K3b clears them)
+    const int64_t hints = (int64_t)c->s2_max_chunks * 4 * (max_ins + 1);
+    if (hints > c->s2_ghist_ints) {
+        af_free(c->s2_ghist);
+        c->s2_ghist = nullptr;
+        c->s2_ghist_ints = 0;
+        HIPCHK(c, hipMalloc(&c->s2_ghist, sizeof(int32_t) * hints));
+        HIPCHK(c, hipMemset(c->s2_ghist, 0, sizeof(int32_t) * hints));
+        c->s2_ghist_ints = hints;
     }
     return AF_OK;
 }
@@ -338,8 +348,9 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
     af_free(c->d_cigar);
-    af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ilist); af_free(c->s2_scan);
-    af_free(c->s2_icnt); af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
+    af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ghist); af_free(c->s2_scan);
+    af_free(c->s2_plan);
+    af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -607,7 +618,7 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
     (void)hipSetDevice(c->device);
     if ((rc = ensure_zscratch(c))) return rc;
     if ((rc = ensure_s2_text(c, ix))) return rc;
-    if ((rc = ensure_s2_work(c, n_pairs, stride, pe.chunk_bases))) return rc;
+    if ((rc = ensure_s2_work(c, n_pairs, stride, pe.chunk_bases, pe.max_ins))) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (c->epoch == 0) return fail(c, AF_E_INVALID, "seed filter was not run for this batch");
     const int slot = (int)((c->epoch - 1) & 1);
@@ -618,12 +629,18 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
     w.rmap = c->s2_rmap;
     w.plist = c->s2_plist;
     w.n_plist = c->ctrl + AF_CTRL_S2_NPAIRS + AF_HEAD_STRIDE * slot;
-    w.ilist = c->s2_ilist; w.icnt = c->s2_icnt; w.pes = c->s2_pes;
+    w.ghist = c->s2_ghist; w.pes = c->s2_pes;
     w.cstart = c->s2_cstart; w.n_chunks = c->s2_nchunks; w.max_chunks = c->s2_max_chunks;
+    if (!d_lens) {  // every read has length stride: pairs per chunk is arithmetic (bseq_read)
+        w.ppc = (pe.chunk_bases + 2 * (int64_t)stride - 1) / (2 * (int64_t)stride);
+        w.n_chunks_u = (int32_t)((n_pairs + w.ppc - 1) / w.ppc);
+    }
     w.heads_k2 = c->ctrl + AF_CTRL_HEADS2; w.heads_k3 = c->ctrl + AF_CTRL_S2_HEADS3;
+    w.plan = c->s2_plan;
     S2Opt opt{pe.pen_unpaired, pe.max_ins, pe.max_matesw, pe.split_width, pe.max_mem_intv, pe.max_chain_gap, pe.pair_base};
-    HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, pe.chunk_bases, c->s2_cstart, c->s2_scan, c->s2_max_chunks,
-                                  c->s2_nchunks, s));
+    if (d_lens)
+        HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, pe.chunk_bases, c->s2_cstart, c->s2_scan,
+                                      c->s2_max_chunks, c->s2_nchunks, s));
     if (tails && !append) HIPCHK(c, hipMemsetAsync(tails->n_tails, 0, 4, s));
     HIPCHK(c, af_launch_s2(ix->s2, d_reads, n_pairs, stride, d_lens, *p, opt, o->hits, c->cand, n_cand, w, *o,
                            c->zscratch, c->n_cu, tails, s));

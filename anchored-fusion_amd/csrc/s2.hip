@@ -59,6 +59,14 @@ struct __attribute__((aligned(16))) S2Lds {
 };
 __shared__ S2Lds g_s2;
 
+#ifdef AF_K2_PROF
+// profiling build only (make prof): per-item phase cycles of K2 and K3c (scripts/s2_prof.py)
+__device__ int32_t *g_s2prof = nullptr;  // K2 items at [item * 16], K3c items at [(1 << 22) + item * 16]
+#define SPROF(...) __VA_ARGS__
+#else
+#define SPROF(...)
+#endif
+
 // ---- small wave helpers --------------------------------------------------------------------
 __device__ __forceinline__ int wave_min(int v) { return -wave_max(-v); }
 __device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
@@ -972,6 +980,7 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
         }
         if (item >= ncand) break;
         const int64_t r = cand[item];
+        SPROF(const int64_t t0 = clock64(); int64_t t1 = t0, t2 = t0, t3 = t0, t4 = t0;)
         int l = lens ? lens[r] : stride;
         if (l > stride) l = stride;
         if (l > AF_MAX_READ) l = AF_MAX_READ;
@@ -1011,8 +1020,10 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
         }
         wave_sync();
         int n_reg = 0;
+        SPROF(int pr_npm = 0, pr_nsi = 0, pr_nch = 0, pr_nreg0 = 0;)
         if (l >= p.min_seed_len) {
             s2_collect_intv(X, p, o, l, lane);
+            SPROF(t1 = clock64(); pr_npm = S.cnt[0]; pr_nsi = S.cnt[1];)
             int n_chn = 0;
             if (!S.cnt[3]) {
                 if (lane == 0) {
@@ -1025,8 +1036,11 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
                 wave_sync();
                 n_chn = S.misc[1];
             }
+            SPROF(t2 = clock64(); pr_nch = n_chn;)
             for (int ci = 0; ci < n_chn && !S.cnt[3]; ++ci) s2_chain2aln<CPL>(X, p, l, ci, lane);
+            SPROF(t3 = clock64(); pr_nreg0 = S.cnt[7];)
             if (!S.cnt[3]) n_reg = s2_dedup_patch<CPL>(X, p, o, S.cnt[7], zg, lane);
+            SPROF(t4 = clock64();)
         }
         const bool ovf = S.cnt[3] != 0;
         int off = 0;
@@ -1039,12 +1053,20 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
         if (!ovf && !pool_ovf)
             for (int k = lane; k < n_reg; k += 64) w.pool[off + k] = S.x.reg[k];
         if (lane == 0) w.rmap[r] = (ovf || pool_ovf) ? int2{0, -1} : int2{off, n_reg};
+        SPROF(if (lane == 0 && g_s2prof) {
+            int32_t *pf = g_s2prof + (int64_t)item * 16;
+            const int64_t t5 = clock64();
+            pf[0] = (int32_t)r; pf[1] = (int32_t)(t5 - t0); pf[2] = (int32_t)(t1 - t0); pf[3] = (int32_t)(t2 - t1);
+            pf[4] = (int32_t)(t3 - t2); pf[5] = (int32_t)(t4 - t3); pf[6] = pr_npm; pf[7] = pr_nsi; pf[8] = pr_nch;
+            pf[9] = pr_nreg0; pf[10] = n_reg; pf[11] = l;
+        })
         wave_sync();
     }
 }
 
 // ============================================================================ K3a
 __device__ __forceinline__ int s2_chunk_of(const S2Work &w, int64_t pp) {
+    if (w.ppc) return (int)(pp / w.ppc);
     int lo = 0, hi = *w.n_chunks;  // cstart[lo] <= pp < cstart[hi]
     while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
@@ -1077,126 +1099,126 @@ __device__ int s2_cal_sub(const S2Reg *a, int n, int msl, int asc) {
     return j < n ? a[j].score : msl * asc;
 }
 
-__global__ void k_s2_classify(int64_t n_pairs, int64_t l_pac, const int32_t *__restrict__ hits, af_params p, S2Opt o,
-                              S2Work w, af_aln_out out) {
-    const int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < 8) {  // K2 ran; the previous call's K3c ran
-        w.heads_k2[AF_HEAD_STRIDE * threadIdx.x] = 0;
-        w.heads_k3[AF_HEAD_STRIDE * threadIdx.x] = 0;
+// One workgroup per AF_S2_CLS_PAIRS consecutive pairs: the listed pairs are gathered in LDS and
+// appended with one atomic per workgroup; insert sizes go to the chunk histograms.
+constexpr int CLS_THREADS = 256, CLS_PER = 16, AF_S2_CLS_PAIRS = CLS_THREADS * CLS_PER;
+__global__ __launch_bounds__(CLS_THREADS) void k_s2_classify(int64_t n_pairs, int64_t l_pac,
+                                                             const int32_t *__restrict__ hits, af_params p, S2Opt o,
+                                                             S2Work w, af_aln_out out) {
+    __shared__ int32_t lst[AF_S2_CLS_PAIRS];
+    __shared__ int32_t nl, base;
+    const int tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < 8) {  // K2 ran; the previous call's K3c ran
+        w.heads_k2[AF_HEAD_STRIDE * tid] = 0;
+        w.heads_k3[AF_HEAD_STRIDE * tid] = 0;
     }
-    bool listed = false;
-    if (pp < n_pairs) {
-        const int h0 = hits[2 * pp], h1 = hits[2 * pp + 1];
-        if (h0 == 0 && h1 == 0) {
+    if (tid == 0) nl = 0;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blockIdx.x * AF_S2_CLS_PAIRS;
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    for (int k = 0; k < CLS_PER; ++k) {
+        const int64_t pp = b0 + k * CLS_THREADS + tid;
+        if (pp >= n_pairs) break;
+        const i32x2 h = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(hits) + pp);
+        if (h.x == 0 && h.y == 0) {
             // both reads unmapped: flags 0x1|0x4|0x8|0x40 / 0x80, no position (bwa prints 0 and '*')
-            typedef int i32x2 __attribute__((ext_vector_type(2)));
             __builtin_nontemporal_store(i32x2{0x4D, 0x8D}, reinterpret_cast<i32x2 *>(out.flag) + pp);
             __builtin_nontemporal_store(i32x2{-1, -1}, reinterpret_cast<i32x2 *>(out.pos) + pp);
             __builtin_nontemporal_store(i32x2{0, 0}, reinterpret_cast<i32x2 *>(out.score) + pp);
             __builtin_nontemporal_store(i32x2{0, 0}, reinterpret_cast<i32x2 *>(out.n_cigar) + pp);
-        } else {
-            listed = true;
-            const int2 m0 = h0 > 0 ? w.rmap[2 * pp] : int2{0, 0};
-            const int2 m1 = h1 > 0 ? w.rmap[2 * pp + 1] : int2{0, 0};
-            if (m0.y > 0 && m1.y > 0) {  // mem_pestat's candidate unique pairs
-                const S2Reg *a0 = w.pool + m0.x, *a1 = w.pool + m1.x;
-                const int s0 = a0[0].score, s1 = a1[0].score;
-                if (!((double)s2_cal_sub(a0, m0.y, p.min_seed_len, p.a) > 0.8 * s0) &&
-                    !((double)s2_cal_sub(a1, m1.y, p.min_seed_len, p.a) > 0.8 * s1)) {
-                    int64_t is;
-                    const int dir = s2_infer_dir(l_pac, a0[0].rb, a1[0].rb, &is);
-                    if (is && is <= o.max_ins) {
-                        const int c = s2_chunk_of(w, pp);
-                        const int k = atomicAdd(&w.icnt[c], 1);
-                        w.ilist[w.cstart[c] + k] = dir << 30 | (int)is;
-                    }
+            continue;
+        }
+        lst[atomicAdd(&nl, 1)] = (int32_t)pp;
+        const int2 m0 = h.x > 0 ? w.rmap[2 * pp] : int2{0, 0};
+        const int2 m1 = h.y > 0 ? w.rmap[2 * pp + 1] : int2{0, 0};
+        if (m0.y > 0 && m1.y > 0) {  // mem_pestat's candidate unique pairs
+            const S2Reg *a0 = w.pool + m0.x, *a1 = w.pool + m1.x;
+            const int s0 = a0[0].score, s1 = a1[0].score;
+            if (!((double)s2_cal_sub(a0, m0.y, p.min_seed_len, p.a) > 0.8 * s0) &&
+                !((double)s2_cal_sub(a1, m1.y, p.min_seed_len, p.a) > 0.8 * s1)) {
+                int64_t is;
+                const int dir = s2_infer_dir(l_pac, a0[0].rb, a1[0].rb, &is);
+                if (is && is <= o.max_ins) {
+                    const int c = s2_chunk_of(w, pp);
+                    atomicAdd(&w.ghist[((int64_t)c * 4 + dir) * (o.max_ins + 1) + is], 1);
                 }
             }
         }
     }
-    // wave-aggregated append to the pair list
-    const uint64_t msk = __ballot(listed);
-    if (msk) {
-        const int lane = (int)(threadIdx.x & 63), leader = __builtin_ctzll(msk);
-        int base = 0;
-        if (lane == leader) base = atomicAdd(w.n_plist, __builtin_popcountll(msk));
-        base = __shfl(base, leader);
-        if (listed) w.plist[base + lanes_below(msk, lane)] = (int32_t)pp;
-    }
+    __syncthreads();
+    if (tid == 0) base = nl ? atomicAdd(w.n_plist, nl) : 0;
+    __syncthreads();
+    for (int i = tid; i < nl; i += CLS_THREADS) w.plist[base + i] = lst[i];
 }
 
 // ============================================================================ K3b
-// mem_pestat (oracle mem_pestat) for one chunk: insert sizes -> LDS histogram per orientation
-constexpr int PES_MAXINS = 16383;
+// mem_pestat (oracle mem_pestat) for one chunk: per orientation, the chunk's insert-size
+// histogram (counted by K3a) gives the percentiles by a block scan and the mean / standard
+// deviation in bwa's summation order (sizes ascending); the histogram is zeroed for the next call
 __global__ __launch_bounds__(256) void k_s2_pestat(S2Work w, int32_t max_ins) {
-    __shared__ int hist[PES_MAXINS + 1];
-    __shared__ int red[4][8];
-    __shared__ int nn[4];
+    __shared__ int part[256];
+    __shared__ int nn[4], pv[3];
     const int c = blockIdx.x, tid = threadIdx.x;
-    if (c >= *w.n_chunks) return;
-    const int64_t base = w.cstart[c];
-    const int n = w.icnt[c];
+    const int nch = w.ppc ? w.n_chunks_u : *w.n_chunks;
+    if (c >= nch) return;
     const int nb = max_ins + 1;
-    // counts per orientation
-    {
-        int cnt[4] = {0, 0, 0, 0};
-        for (int i = tid; i < n; i += 256) ++cnt[(uint32_t)w.ilist[base + i] >> 30];
-        for (int d = 0; d < 4; ++d) {
-            int v = cnt[d];
-            for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
-            if ((tid & 63) == 0) red[d][tid >> 6] = v;
-        }
-        __syncthreads();
-        if (tid < 4) nn[tid] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
-        __syncthreads();
-    }
+    const int per = (nb + 255) / 256;
     S2Pes res[4];
     for (int d = 0; d < 4; ++d) {
-        S2Pes &r = res[d];
-        r.low = r.high = 0; r.failed = 0; r.pad = 0; r.avg = 0; r.std = 0;
-        const int nd = nn[d];
-        if (nd < 10) { r.failed = 1; continue; }  // MIN_DIR_CNT
-        for (int i = tid; i < nb; i += 256) hist[i] = 0;
-        __syncthreads();
-        for (int i = tid; i < n; i += 256) {
-            const uint32_t v = (uint32_t)w.ilist[base + i];
-            if ((int)(v >> 30) == d) atomicAdd(&hist[v & 0x3FFFFFFFu], 1);
-        }
+        int *hist = w.ghist + ((int64_t)c * 4 + d) * nb;
+        // this thread's bins [tid * per, (tid + 1) * per): its count, then an exclusive block scan
+        int cnt = 0;
+        for (int v = tid * per; v < min(nb, (tid + 1) * per); ++v) cnt += hist[v];
+        part[tid] = cnt;
         __syncthreads();
         if (tid == 0) {
-            // percentiles: q[(int)(f * n + .499)] of the sorted sizes
-            const int k25 = (int)(.25 * nd + .499), k50 = (int)(.50 * nd + .499), k75 = (int)(.75 * nd + .499);
-            int p25 = 0, p50 = 0, p75 = 0, cum = 0;
-            bool g25 = false, g50 = false, g75 = false;
-            for (int v = 0; v < nb; ++v) {
-                cum += hist[v];
-                if (!g25 && cum > k25) { p25 = v; g25 = true; }
-                if (!g50 && cum > k50) { p50 = v; g50 = true; }
-                if (!g75 && cum > k75) { p75 = v; g75 = true; break; }
-            }
-            (void)p50;
-            r.low = (int)(p25 - 2.0 * (p75 - p25) + .499);
-            if (r.low < 1) r.low = 1;
-            r.high = (int)(p75 + 2.0 * (p75 - p25) + .499);
-            long long sum = 0;
-            int x = 0;
-            for (int v = r.low; v <= r.high && v < nb; ++v) { sum += (long long)v * hist[v]; x += hist[v]; }
-            double avg = 0;
-            // bwa adds the sizes in sorted order in double: integers, exact below 2^53
-            avg = (double)sum;
-            avg /= x;
-            double sd = 0;
-            for (int v = r.low; v <= r.high && v < nb; ++v)
-                for (int k = 0; k < hist[v]; ++k) sd += ((double)v - avg) * ((double)v - avg);
-            sd = sqrt(sd / x);
-            r.avg = avg; r.std = sd;
-            r.low = (int)(p25 - 3.0 * (p75 - p25) + .499);
-            r.high = (int)(p75 + 3.0 * (p75 - p25) + .499);
-            if (r.low > avg - 4.0 * sd) r.low = (int)(avg - 4.0 * sd + .499);
-            if (r.high < avg + 4.0 * sd) r.high = (int)(avg + 4.0 * sd + .499);
-            if (r.low < 1) r.low = 1;
+            int acc = 0;
+            for (int t = 0; t < 256; ++t) { const int x = part[t]; part[t] = acc; acc += x; }
+            nn[d] = acc;
         }
         __syncthreads();
+        const int nd = nn[d];
+        S2Pes &r = res[d];
+        r.low = r.high = 0; r.failed = 0; r.pad = 0; r.avg = 0; r.std = 0;
+        if (nd < 10) {  // MIN_DIR_CNT (the histogram may still hold a few sizes)
+            r.failed = 1;
+        } else {
+            // percentiles q[(int)(f * n + .499)] of the sorted sizes
+            const int kk[3] = {(int)(.25 * nd + .499), (int)(.50 * nd + .499), (int)(.75 * nd + .499)};
+            int cum = part[tid];
+            for (int v = tid * per; v < min(nb, (tid + 1) * per); ++v) {
+                const int h = hist[v];
+                for (int q = 0; q < 3; ++q)
+                    if (cum <= kk[q] && kk[q] < cum + h) pv[q] = v;
+                cum += h;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                const int p25 = pv[0], p75 = pv[2];
+                r.low = (int)(p25 - 2.0 * (p75 - p25) + .499);
+                if (r.low < 1) r.low = 1;
+                r.high = (int)(p75 + 2.0 * (p75 - p25) + .499);
+                long long sum = 0;
+                int x = 0;
+                for (int v = r.low; v <= r.high && v < nb; ++v) { sum += (long long)v * hist[v]; x += hist[v]; }
+                // bwa adds the sizes in sorted order in double: integers, exact below 2^53
+                double avg = (double)sum;
+                avg /= x;
+                double sd = 0;
+                for (int v = r.low; v <= r.high && v < nb; ++v)
+                    for (int k = 0, h = hist[v]; k < h; ++k) sd += ((double)v - avg) * ((double)v - avg);
+                sd = sqrt(sd / x);
+                r.avg = avg; r.std = sd;
+                r.low = (int)(p25 - 3.0 * (p75 - p25) + .499);
+                r.high = (int)(p75 + 3.0 * (p75 - p25) + .499);
+                if (r.low > avg - 4.0 * sd) r.low = (int)(avg - 4.0 * sd + .499);
+                if (r.high < avg + 4.0 * sd) r.high = (int)(avg + 4.0 * sd + .499);
+                if (r.low < 1) r.low = 1;
+            }
+        }
+        __syncthreads();
+        if (nd > 0)
+            for (int v = tid * per; v < min(nb, (tid + 1) * per); ++v) hist[v] = 0;
     }
     if (tid == 0) {
         int mx = 0;
@@ -1205,7 +1227,6 @@ __global__ __launch_bounds__(256) void k_s2_pestat(S2Work w, int32_t max_ins) {
             if (res[d].failed == 0 && (double)nn[d] < mx * 0.05) res[d].failed = 1;
             w.pes[(int64_t)c * 4 + d] = res[d];
         }
-        w.icnt[c] = 0;  // for the next call
     }
 }
 
@@ -1215,58 +1236,68 @@ struct PeReg {
     uint64_t hash;
     int32_t secondary, pad;
 };
+struct P64 { uint64_t x, y; };
+constexpr int PE_TW = 2048;  // rescue windows up to this many bases are staged in LDS
 struct __attribute__((aligned(16))) PeLds {
     PeReg a[2][AF_S2_MAX_REG];
     int64_t brb[2][AF_S2_MAX_REG];
+    P64 v[2 * AF_S2_MAX_REG];          // mem_pair's hit list
+    int32_t zz[AF_S2_MAX_REG];         // mem_mark_primary_se_core's kept hits
     uint8_t q[2][AF_MAX_READ + 16];
     uint8_t rq[AF_MAX_READ + 16];      // the rescue query (mate, maybe reverse-complemented)
     uint8_t rq2[AF_MAX_READ + 16];     // its reversed prefix (ksw_align2's start pass)
+    uint8_t tw[PE_TW];                 // the rescue window of the reference
     S2Pes pes[4];
     int32_t na[2], nb[2], ovf[2], len[2];
-    int32_t z[2], which[2], extra, misc[8];
-    int32_t o_rid[2], o_rev[2], o_flag[2], o_score[2], o_nc[2];
-    int64_t o_pos[2];
+    int32_t which[2], extra, misc[8];
 };
 __shared__ PeLds g_pe;
+
+// the decision K3c hands to the record kernel K3d, per listed pair
+struct S2Plan {
+    S2Reg r[2];
+    int32_t which[2], sec[2], extra, ovf;
+};
 
 struct SwRes { int score, te, qe; };
 
 // One pass of ksw_u8 / ksw_i16 (oracle ksw_sw) on the wave.  The striped kernel's result is
 // H(i,j) = max(G, F) with G = max(H(i-1,j-1) + S, E, 0) and F the full horizontal-gap term,
 // while E(i+1,j) is fed by the first-pass value max(G, F within the query's stripe block
-// [blk * slen, (blk + 1) * slen)) -- the lazy-F loop does not revisit E.  Lanes hold query
-// columns; both F terms are prefix maxima (one plain, one keyed by block).  The target base of
-// row i is target[i] (rev: target[te0 - i] for i <= te0, as the start pass's partly reversed
-// target).  Stops at the first row reaching endsc.
-__device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *target, int tlen, int rev_te, int P,
+// [blk * slen, (blk + 1) * slen)) -- the lazy-F loop does not revisit E.  Lanes hold C query
+// columns each; both F terms are prefix maxima (one plain, one keyed by block).  The target base
+// of row i is tg[i] (rev: tg[te0 - i] for i <= te0, as the start pass's partly reversed target);
+// tg is the LDS window when it holds the whole target.  Stops at the first row reaching endsc.
+template <int C>
+__device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *tg, int tlen, int rev_te, int P,
                              const af_params &p, int endsc, int lane) {
     const int slen = (qlen + P - 1) / P;
-    const int cpl = (qlen + 63) >> 6;  // <= 5 (AF_MAX_READ 320)
-    const int shift = p.b > 1 ? p.b : 1;  // ksw_qinit: minus the smallest score of the matrix (N: -1)
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
-    const int j0 = lane * cpl;
-    int H[5], E[5], qc[5], blk[5];
+    const int shift = p.b > 1 ? p.b : 1;  // ksw_qinit: minus the smallest score of the matrix (N: -1)
+    const int j0 = lane * C;
+    int H[C], E[C], qc[C], blk[C];
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
+    for (int c = 0; c < C; ++c) {
         const int j = j0 + c;
         H[c] = 0; E[c] = 0;
-        qc[c] = (c < cpl && j < qlen) ? q[j] : 4;
-        blk[c] = (c < cpl && j < qlen) ? j / slen : 0;
+        qc[c] = j < qlen ? q[j] : 4;
+        blk[c] = j < qlen ? j / slen : 0;
     }
     SwRes r{0, -1, -1};
     int gmax = 0;
+    int t_next = tlen > 0 ? tg[rev_te >= 0 ? rev_te : 0] : 4;
     for (int i = 0; i < tlen; ++i) {
-        const int ti = __builtin_amdgcn_readfirstlane((int)(rev_te >= 0 && i <= rev_te ? target[rev_te - i] : target[i]));
-        const int from_left = wave_shr1(0, pick<5>(H, cpl - 1));
-        int G[5], runX = kNeg, runK = -1, bxX[5], bxK[5];
+        const int ti = __builtin_amdgcn_readfirstlane(t_next);
+        if (i + 1 < tlen) t_next = tg[rev_te >= 0 && i + 1 <= rev_te ? rev_te - i - 1 : i + 1];
+        const int from_left = wave_shr1(0, H[C - 1]);
+        int G[C], runX = kNeg, runK = -1, bxX[C], bxK[C];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) {
+        for (int c = 0; c < C; ++c) {
             const int j = j0 + c;
-            const bool in = c < cpl && j < qlen;
+            const bool in = j < qlen;
             const int hd = c == 0 ? from_left : H[c - 1];
             const int s = (ti > 3 || qc[c] > 3) ? -1 : (ti == qc[c] ? p.a : -p.b);
-            const int D = max(hd + s, 0);
-            G[c] = max(D, E[c]);
+            G[c] = max(max(hd + s, 0), E[c]);
             bxX[c] = runX; bxK[c] = runK;
             if (in) {
                 const int X = G[c] - oe_ins + j * p.e_ins;
@@ -1278,9 +1309,9 @@ __device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *target, 
         const int lexK = wave_shr1(-1, wave_incl_max(runK));
         int rowmax = 0;
 #pragma unroll
-        for (int c = 0; c < 5; ++c) {
+        for (int c = 0; c < C; ++c) {
             const int j = j0 + c;
-            const bool in = c < cpl && j < qlen;
+            const bool in = j < qlen;
             const int PX = max(lexX, bxX[c]);
             const int F = PX <= kNeg / 2 ? 0 : max(PX - (j - 1) * p.e_ins, 0);
             const int PK = max(lexK, bxK[c]);
@@ -1297,8 +1328,8 @@ __device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *target, 
             r.te = i;
             int qj = 1 << 30;
 #pragma unroll
-            for (int c = 0; c < 5; ++c)
-                if (c < cpl && j0 + c < qlen && H[c] == gmax) qj = min(qj, j0 + c);
+            for (int c = 0; c < C; ++c)
+                if (j0 + c < qlen && H[c] == gmax) qj = min(qj, j0 + c);
             r.qe = wave_min(qj);
             if ((P == 16 && gmax + shift >= 255) || gmax >= endsc) break;
         }
@@ -1308,16 +1339,26 @@ __device__ SwRes s2_ksw_pass(const uint8_t *q, int qlen, const uint8_t *target, 
     return r;
 }
 
+__device__ SwRes s2_ksw_pass_any(const uint8_t *q, int qlen, const uint8_t *tg, int tlen, int rev_te, int P,
+                                 const af_params &p, int endsc, int lane) {
+    const int cpl = (qlen + 63) >> 6;  // <= 5 (AF_MAX_READ 320)
+    if (cpl <= 1) return s2_ksw_pass<1>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 2) return s2_ksw_pass<2>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 3) return s2_ksw_pass<3>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 4) return s2_ksw_pass<4>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    return s2_ksw_pass<5>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+}
+
 // ksw_align2 with KSW_XSUBO | KSW_XSTART (oracle ksw_align2): score, te, qe and the start (tb, qb)
 __device__ void s2_ksw_align2(const uint8_t *q, int qlen, const uint8_t *target, int tlen, int P, int minsc,
                               const af_params &p, int &score, int &te, int &qe, int &tb, int &qb, int lane) {
     PeLds &E = g_pe;
-    const SwRes r = s2_ksw_pass(q, qlen, target, tlen, -1, P, p, 0x10000, lane);
+    const SwRes r = s2_ksw_pass_any(q, qlen, target, tlen, -1, P, p, 0x10000, lane);
     score = r.score; te = r.te; qe = r.qe; tb = -1; qb = -1;
     if (r.score < minsc || r.qe < 0) return;
     for (int x = lane; x <= r.qe; x += 64) E.rq2[x] = q[r.qe - x];
     wave_sync();
-    const SwRes rr = s2_ksw_pass(E.rq2, r.qe + 1, target, tlen, r.te, P, p, r.score, lane);
+    const SwRes rr = s2_ksw_pass_any(E.rq2, r.qe + 1, target, tlen, r.te, P, p, r.score, lane);
     wave_sync();
     if (r.score == rr.score) { tb = r.te - rr.te; qb = r.qe - rr.qe; }
 }
@@ -1409,10 +1450,15 @@ __device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, 
                 const int c = E.q[mi][is_rev ? l_ms - 1 - x : x];
                 E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
             }
+            const bool staged = re - rb <= PE_TW;
+            if (staged)
+                for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = X.T[rb + x];
             wave_sync();
             const int P = l_ms * p.a < 250 ? 16 : 8;
+            SPROF(if (lane == 0) E.misc[7] += (int)(re - rb);)
             int sc, te, qe, tb, qb;
-            s2_ksw_align2(E.rq, l_ms, X.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb, qb, lane);
+            s2_ksw_align2(E.rq, l_ms, staged ? E.tw : X.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe,
+                          tb, qb, lane);
             if (sc >= p.min_seed_len && qb >= 0) {
                 bool ok = true;
                 if (lane == 0) {
@@ -1455,7 +1501,8 @@ __device__ void s2_mark_primary(PeReg *a, int n, int64_t id, const af_params &p)
     if (n == 0) return;
     for (int i = 0; i < n; ++i) { a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i)); }
     ks_introsort(a, n, LtArsHash());
-    int z[AF_S2_MAX_REG], nz = 0;
+    int32_t *z = g_pe.zz;
+    int nz = 0;
     z[nz++] = 0;
     for (int i = 1; i < n; ++i) {
         int k;
@@ -1473,7 +1520,6 @@ __device__ void s2_mark_primary(PeReg *a, int n, int64_t id, const af_params &p)
     }
 }
 
-struct P64 { uint64_t x, y; };
 struct LtP64 {
     __device__ bool operator()(const P64 &a, const P64 &b) const { return a.x < b.x || (a.x == b.x && a.y < b.y); }
 };
@@ -1481,7 +1527,7 @@ struct LtP64 {
 // mem_pair (oracle mem_pair), lane 0: the best pair's score (0 if none) and z[]
 __device__ int s2_mem_pair(int64_t l_pac, const af_params &p, const S2Pes *pes, int id, int z[2]) {
     PeLds &E = g_pe;
-    P64 v[2 * AF_S2_MAX_REG];
+    P64 *v = E.v;
     int nv = 0;
     for (int r = 0; r < 2; ++r)
         for (int i = 0; i < E.na[r]; ++i) {
@@ -1524,19 +1570,16 @@ __device__ int s2_mem_pair(int64_t l_pac, const af_params &p, const S2Pes *pes, 
     return (int)(best.x >> 32);
 }
 
-// K3c: mem_sam_pe for every listed pair (one wave per pair)
-template <int CPL>
+// K3c: mem_sam_pe up to the record choice for every listed pair (one wave per pair): mate
+// rescue, primary marking, pairing; the choice (S2Plan) goes to K3d
 __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
                                                  const int32_t *__restrict__ lens, af_params p, S2Opt o,
-                                                 const int32_t *__restrict__ hits, S2Work w, af_aln_out out,
-                                                 uint8_t *__restrict__ zscratch, size_t zstride, AfTails tails,
-                                                 int use_tails) {
-    DpLds &L = g_dp;
+                                                 const int32_t *__restrict__ hits, S2Work w,
+                                                 S2Plan *__restrict__ plan) {
     PeLds &E = g_pe;
     const int lane = threadIdx.x;
     const int64_t l_pac = X.n;
     const int npl = *w.n_plist;
-    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
     int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
         int item = npl;
@@ -1551,6 +1594,7 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
         }
         if (item >= npl) break;
         const int64_t pp = w.plist[item];
+        SPROF(const int64_t c0 = clock64(); int64_t c1 = c0, c2 = c0, c3 = c0; int nsw = 0;)
         // reads and their regions
         for (int m = 0; m < 2; ++m) {
             const int64_t r = 2 * pp + m;
@@ -1589,6 +1633,7 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
             }
         }
         wave_sync();
+        SPROF(c1 = clock64(); if (lane == 0) E.misc[7] = 0;)
         for (int i = 0; i < 2; ++i)
             for (int j = 0; j < E.nb[i] && j < o.max_matesw; ++j) {
                 if (E.ovf[!i]) continue;
@@ -1598,6 +1643,7 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
                     wave_sync();
                 }
             }
+        SPROF(c2 = clock64(); nsw = E.misc[7];)
         // primary marking, pairing and the record choice (mem_sam_pe)
         if (lane == 0) {
             const uint64_t id = (uint64_t)(o.pair_base + pp);
@@ -1638,19 +1684,74 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
             E.which[0] = which[0]; E.which[1] = which[1]; E.extra = extra;
         }
         wave_sync();
+        SPROF(c3 = clock64();)
+        if (lane == 0) {
+            S2Plan &pl = plan[item];
+            for (int m = 0; m < 2; ++m) {
+                pl.which[m] = E.which[m];
+                if (E.which[m] >= 0) {
+                    pl.r[m] = E.a[m][E.which[m]].r;
+                    pl.sec[m] = E.a[m][E.which[m]].secondary;
+                }
+            }
+            pl.extra = E.extra;
+            pl.ovf = E.ovf[0] | E.ovf[1] << 1;
+        }
+        SPROF(if (lane == 0 && g_s2prof) {
+            int32_t *pf = g_s2prof + (1 << 22) + (int64_t)item * 16;
+            const int64_t c4 = clock64();
+            pf[0] = (int32_t)pp; pf[1] = (int32_t)(c4 - c0); pf[2] = (int32_t)(c1 - c0); pf[3] = (int32_t)(c2 - c1);
+            pf[4] = (int32_t)(c3 - c2); pf[6] = nsw; pf[7] = E.na[0]; pf[8] = E.na[1];
+        })
+        wave_sync();
+    }
+}
+
+// K3d: mem_reg2aln + mem_aln2sam for both reads of every listed pair (one wave per pair): the
+// CIGAR of each chosen region (bwa_gen_cigar2 with bwa's band retries), flags, split-read tails
+struct __attribute__((aligned(16))) RecLds {
+    int32_t o_rid[2], o_rev[2], o_flag[2], o_score[2], o_nc[2];
+    int64_t o_pos[2];
+};
+__shared__ RecLds g_rec;
+
+template <int CPL>
+__global__ __launch_bounds__(64, 6) void k_s2_records(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
+                                                      const int32_t *__restrict__ lens, af_params p, S2Work w,
+                                                      const S2Plan *__restrict__ plan, af_aln_out out,
+                                                      uint8_t *__restrict__ zscratch, size_t zstride, AfTails tails,
+                                                      int use_tails) {
+    DpLds &L = g_dp;
+    RecLds &E = g_rec;
+    const int lane = threadIdx.x;
+    const int64_t l_pac = X.n;
+    const int npl = *w.n_plist;
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    for (int item = blockIdx.x; item < npl; item += gridDim.x) {
+        const int64_t pp = w.plist[item];
+        const S2Plan &pl = plan[item];
+        SPROF(const int64_t c0 = clock64();)
         // mem_reg2aln of each read's record
         for (int m = 0; m < 2; ++m) {
-            const int wi = E.which[m];
+            const int wi = pl.which[m];
             const int64_t r = 2 * pp + m;
             if (wi < 0) {
                 if (lane == 0) { E.o_rid[m] = -1; E.o_pos[m] = -1; E.o_rev[m] = 0; E.o_flag[m] = 0x4; E.o_score[m] = 0; E.o_nc[m] = 0; }
                 wave_sync();
                 continue;
             }
-            const S2Reg ar = E.a[m][wi].r;
-            const int secondary = E.a[m][wi].secondary;
-            const int l = E.len[m];
-            for (int x = lane; x < l; x += 64) L.q[x] = E.q[m][x];
+            const S2Reg ar = pl.r[m];
+            const int secondary = pl.sec[m];
+            int l = lens ? lens[r] : stride;
+            if (l > stride) l = stride;
+            if (l > AF_MAX_READ) l = AF_MAX_READ;
+            if (l < 0) l = 0;
+            const uint8_t *rd = reads + r * (int64_t)stride;
+            for (int x = lane; x < l; x += 64) {
+                const uint8_t ch = rd[x];
+                L.q[x] = ch == 'A' || ch == 'a' ? 0 : ch == 'C' || ch == 'c' ? 1 : ch == 'G' || ch == 'g' ? 2
+                       : ch == 'T' || ch == 't' ? 3 : 4;
+            }
             wave_sync();
             const bool is_rev = ar.rb >= l_pac;
             const int lq = ar.qe - ar.qb;
@@ -1705,14 +1806,14 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
                 int prid = E.o_rid[m], mrid = E.o_rid[mm];
                 int64_t ppos = E.o_pos[m];
                 int prev = E.o_rev[m], mrev = E.o_rev[mm];
-                int flag = E.o_flag[m] | (m ? 0x80 : 0x40) | E.extra | 0x1;
+                int flag = E.o_flag[m] | (m ? 0x80 : 0x40) | pl.extra | 0x1;
                 flag |= prid < 0 ? 0x4 : 0;
                 flag |= mrid < 0 ? 0x8 : 0;
                 if (prid < 0 && mrid >= 0) { ppos = E.o_pos[mm]; prev = mrev; }
                 if (mrid < 0 && prid >= 0) mrev = prev;
                 flag |= prev ? 0x10 : 0;
                 flag |= mrev ? 0x20 : 0;
-                if (E.ovf[m]) flag |= AF_FLAG_MEM_OVERFLOW;
+                if ((pl.ovf >> m) & 1) flag |= AF_FLAG_MEM_OVERFLOW;
                 const int64_t r = 2 * pp + m;
                 out.flag[r] = flag;
                 out.pos[r] = (prid >= 0 || mrid >= 0) ? (int32_t)ppos : -1;
@@ -1722,6 +1823,7 @@ __global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__res
                     af_emit_tail(tails, reads, stride, lens, r, flag, out.cigar + r * AF_MAX_CIGAR);
             }
         }
+        SPROF(if (lane == 0 && g_s2prof) g_s2prof[(1 << 22) + (int64_t)item * 16 + 5] = (int32_t)(clock64() - c0);)
         wave_sync();
     }
 }
@@ -1734,17 +1836,6 @@ __global__ __launch_bounds__(1024) void k_s2_chunks(int64_t n_pairs, int32_t str
                                                      int32_t *__restrict__ n_chunks) {
     __shared__ int64_t part[1024];
     const int tid = threadIdx.x;
-    if (!lens) {
-        if (tid == 0) {
-            const int64_t ppc = (chunk_bases + 2 * (int64_t)stride - 1) / (2 * (int64_t)stride);
-            const int64_t per = ppc > 0 ? ppc : 1;
-            int nc = 0;
-            for (int64_t c0 = 0; c0 < n_pairs && nc < max_chunks; c0 += per) cstart[nc++] = c0;
-            cstart[nc] = n_pairs;
-            *n_chunks = nc;
-        }
-        return;
-    }
     const int64_t per = (n_pairs + 1023) / 1024;
     const int64_t b0 = tid * per, b1 = min(n_pairs, b0 + per);
     int64_t s = 0;
@@ -1788,6 +1879,25 @@ __global__ __launch_bounds__(1024) void k_s2_chunks(int64_t n_pairs, int32_t str
 
 }  // namespace
 
+#ifdef AF_K2_PROF
+extern "C" int af_debug_s2_prof_enable() {
+    int32_t *d = nullptr;
+    const size_t n = (size_t)2 << 22;
+    if (hipMalloc(&d, sizeof(int32_t) * n) != hipSuccess) return -1;
+    (void)hipMemset(d, 0, sizeof(int32_t) * n);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_s2prof), &d, sizeof d) == hipSuccess ? 16 : -1;
+}
+extern "C" int af_debug_s2_prof_read(int32_t *host, int64_t n_k2, int64_t n_k3) {
+    int32_t *d = nullptr;
+    if (hipMemcpyFromSymbol(&d, HIP_SYMBOL(g_s2prof), sizeof d) != hipSuccess || !d) return -1;
+    if (hipMemcpy(host, d, sizeof(int32_t) * 16 * n_k2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return hipMemcpy(host + 16 * n_k2, d + (1 << 22), sizeof(int32_t) * 16 * n_k3, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0 : -1;
+}
+#endif
+
+size_t af_s2_plan_bytes() { return sizeof(S2Plan); }
+
 hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *lens, int64_t chunk_bases,
                                int64_t *cstart, int64_t *scan_tmp, int32_t max_chunks, int32_t *n_chunks_dev,
                                hipStream_t s) {
@@ -1803,7 +1913,7 @@ hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs,
     // zscratch holds n_cu * 4 * AF_K2_WPS slots (api.hip ensure_zscratch), enough for both grids
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
-    dim3 g(n_cu * 4 * AF_S2_WPS), g3(n_cu * 16), b(64);
+    dim3 g(n_cu * 4 * AF_S2_WPS), g3(n_cu * 16), g4(n_cu * 4 * 6), b(64);
 #define AF_GO(C) hipLaunchKernelGGL((k_s2_regions<C>), g, b, 0, s, X, reads, stride, lens, p, o, cand, n_cand, w, \
                                     zscratch, zstride)
     if (cpl <= 2) AF_GO(2);
@@ -1811,12 +1921,14 @@ hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs,
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
-    const int bs = 256;
-    const int64_t nb = n_pairs > 0 ? (n_pairs + bs - 1) / bs : 1;
-    hipLaunchKernelGGL(k_s2_classify, dim3((unsigned)nb), dim3(bs), 0, s, n_pairs, X.n, hits, p, o, w, out);
-    hipLaunchKernelGGL(k_s2_pestat, dim3((unsigned)w.max_chunks), dim3(256), 0, s, w, o.max_ins);
+    const int64_t nb = n_pairs > 0 ? (n_pairs + AF_S2_CLS_PAIRS - 1) / AF_S2_CLS_PAIRS : 1;
+    hipLaunchKernelGGL(k_s2_classify, dim3((unsigned)nb), dim3(CLS_THREADS), 0, s, n_pairs, X.n, hits, p, o, w, out);
+    hipLaunchKernelGGL(k_s2_pestat, dim3((unsigned)(w.ppc ? w.n_chunks_u : w.max_chunks)), dim3(256), 0, s, w,
+                       o.max_ins);
     const AfTails t = tails ? *tails : AfTails{};
-#define AF_GO(C) hipLaunchKernelGGL((k_s2_pairs<C>), g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, out, zscratch, \
+    S2Plan *plan = static_cast<S2Plan *>(w.plan);
+    hipLaunchKernelGGL(k_s2_pairs, g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, plan);
+#define AF_GO(C) hipLaunchKernelGGL((k_s2_records<C>), g4, b, 0, s, X, reads, stride, lens, p, w, plan, out, zscratch, \
                                     zstride, t, tails ? 1 : 0)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
