@@ -63,6 +63,7 @@ __shared__ S2Lds g_s2;
 // profiling build only (make prof): per-item phase cycles of K2 and K3c (scripts/s2_prof.py)
 __device__ int32_t *g_s2prof = nullptr;  // K2 items at [item * 16], K3c items at [(1 << 22) + item * 16]
 #define SPROF(...) __VA_ARGS__
+__shared__ int64_t g_sub[5];  // K2 seeding sub-phase marks (pmems, pass 1, pass 2, pass 3)
 #else
 #define SPROF(...)
 #endif
@@ -112,7 +113,9 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
     }
     int d;
     for (d = 2; (1ul << d) < (unsigned long)n; ++d) ;
-    int stl[24], str[24], std_[24], top = 0;
+    // klib pushes the larger part and continues with the smaller, so the stack holds at most
+    // log2(n / 17) + 1 segments: 8 covers n <= 17 << 7 (every call site sorts <= 128 items)
+    int stl[8], str[8], std_[8], top = 0;
     int s = 0, t = n - 1;
     d <<= 1;
     for (;;) {
@@ -346,8 +349,10 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
     DpLds &L = g_dp;
     S2Lds &S = g_s2;
     const int msl = p.min_seed_len;
+    SPROF(if (lane == 0) g_sub[0] = clock64();)
     s2_pmems(X, l, msl, lane);
     wave_sync();
+    SPROF(if (lane == 0) g_sub[1] = g_sub[2] = g_sub[3] = g_sub[4] = clock64();)
     const int npm_all = S.cnt[0];
     if (npm_all > AF_S2_MAX_PMEM) {
         if (lane == 0) S.cnt[3] = 1;
@@ -377,6 +382,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
             s2_push_intv(X, npm, bs, bt, lane);
         }
     }
+    SPROF(if (lane == 0) g_sub[2] = g_sub[3] = g_sub[4] = clock64();)
     if (S.cnt[3]) return;
     // pass 2
     const int split_len = (int)((float)msl * 1.5f + .499);
@@ -386,6 +392,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
         if (v.qe - v.qb < split_len || v.cnt > o.split_width) continue;
         s2_smem_at(X, npm, l, msl, (v.qb + v.qe) >> 1, v.cnt + 1, lane);
     }
+    SPROF(if (lane == 0) g_sub[3] = g_sub[4] = clock64();)
     // pass 3 (bwt_seed_strategy1 with min_len = min_seed_len, max_intv = max_mem_intv)
     if (o.max_mem_intv > 0) {
         const int mi = o.max_mem_intv;
@@ -424,6 +431,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
             x = es;
         }
     }
+    SPROF(if (lane == 0) g_sub[4] = clock64();)
     if (S.cnt[3]) return;
     // sort by (qb, qe): equal intervals are identical, any order among them
     const int ns = S.cnt[1];
@@ -1059,6 +1067,9 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
             pf[0] = (int32_t)r; pf[1] = (int32_t)(t5 - t0); pf[2] = (int32_t)(t1 - t0); pf[3] = (int32_t)(t2 - t1);
             pf[4] = (int32_t)(t3 - t2); pf[5] = (int32_t)(t4 - t3); pf[6] = pr_npm; pf[7] = pr_nsi; pf[8] = pr_nch;
             pf[9] = pr_nreg0; pf[10] = n_reg; pf[11] = l;
+            pf[12] = (int32_t)(g_sub[0] - t0); pf[13] = (int32_t)(g_sub[1] - g_sub[0]);
+            pf[14] = (int32_t)(g_sub[2] - g_sub[1]); pf[15] = (int32_t)(g_sub[3] - g_sub[2]);
+            pf[6] |= (int32_t)min(g_sub[4] - g_sub[3], (int64_t)0x7FFFFF) << 8;
         })
         wave_sync();
     }
@@ -1572,7 +1583,7 @@ __device__ int s2_mem_pair(int64_t l_pac, const af_params &p, const S2Pes *pes, 
 
 // K3c: mem_sam_pe up to the record choice for every listed pair (one wave per pair): mate
 // rescue, primary marking, pairing; the choice (S2Plan) goes to K3d
-__global__ __launch_bounds__(64) void k_s2_pairs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
+__global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
                                                  const int32_t *__restrict__ lens, af_params p, S2Opt o,
                                                  const int32_t *__restrict__ hits, S2Work w,
                                                  S2Plan *__restrict__ plan) {

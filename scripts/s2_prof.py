@@ -46,6 +46,10 @@ k2 = buf[:16 * n_k2].reshape(-1, 16).astype(np.int64)
 k3 = buf[16 * n_k2:].reshape(-1, 16).astype(np.int64)
 print(f"K2: {n_k2} reads; mean cycles total {k2[:, 1].mean():.0f}: seed {k2[:, 2].mean():.0f}, chain "
       f"{k2[:, 3].mean():.0f}, extend {k2[:, 4].mean():.0f}, dedup {k2[:, 5].mean():.0f}")
+sub = k2[:, 6] >> 8
+k2[:, 6] &= 0xFF
+print(f"    seeding: read load {k2[:, 12].mean():.0f}, MEMs {k2[:, 13].mean():.0f}, pass 1 {k2[:, 14].mean():.0f}, "
+      f"pass 2 {k2[:, 15].mean():.0f}, pass 3 {sub.mean():.0f}")
 print(f"    MEMs {k2[:, 6].mean():.2f}, intervals {k2[:, 7].mean():.2f}, chains {k2[:, 8].mean():.2f}, "
       f"regions {k2[:, 9].mean():.2f} -> {k2[:, 10].mean():.2f}")
 resc = k3[:, 6] > 0
