@@ -162,51 +162,73 @@ __device__ __forceinline__ uint64_t hash_64(uint64_t key) {
 }
 
 // =========================================================================== K2: seeds
-// MEMs >= min_seed_len of the read (L.q / L.pk / L.nm) against the bwa text T: lanes over
-// query offsets, the 16-mer hash in L2, right extension by 2-bit word compares (oracle
-// find_pmems)
+// MEMs >= min_seed_len of the read (L.q / L.pk / L.nm) against the bwa text T (oracle
+// find_pmems).  Lanes over query offsets probe the 16-mer hash (in L2) and test left-maximality
+// of each occurrence; every left-maximal (s, r0) is then extended by the whole wave at once:
+// lane j compares the 16 bases at s + 16 (j + 1) with T, and the first lane short of 16 equal
+// bases ends the match -- one round of loads instead of one per 16 bases.
 __device__ void s2_pmems(const DevText &X, int l, int msl, int lane) {
     DpLds &L = g_dp;
     S2Lds &S = g_s2;
     const int64_t N = 2 * X.n;
     const uint32_t hm = (1u << X.hbits) - 1u;
-    for (int s = lane; s + AF_K <= l; s += 64) {
-        const int wq = s >> 4, sq = s & 15;
-        const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
-        if (((L.nm[wq] | (L.nm[wq + 1] << 16)) >> sq) & 0xFFFFu) continue;
+    for (int s0 = 0; s0 + AF_K <= l; s0 += 64) {
+        const int s = s0 + lane;
         int cnt = 0, st = 0, pos0 = 0;
-        uint32_t sl = af_fmix(k) & hm;
-        for (;;) {
-            const int4 e = X.hslot[sl];
-            if (e.z == 0) break;
-            if ((uint32_t)e.x == k) { cnt = e.z; st = e.y; pos0 = e.w; break; }
-            sl = (sl + 1) & hm;
+        if (s + AF_K <= l) {
+            const int wq = s >> 4, sq = s & 15;
+            const uint32_t k = __builtin_amdgcn_alignbit(L.pk[wq + 1], L.pk[wq], 2 * sq);
+            if (!(((L.nm[wq] | (L.nm[wq + 1] << 16)) >> sq) & 0xFFFFu)) {
+                uint32_t sl = af_fmix(k) & hm;
+                for (;;) {
+                    const int4 e = X.hslot[sl];
+                    if (e.z == 0) break;
+                    if ((uint32_t)e.x == k) { cnt = e.z; st = e.y; pos0 = e.w; break; }
+                    sl = (sl + 1) & hm;
+                }
+            }
         }
-        for (int o = 0; o < cnt; ++o) {
-            const int64_t r0 = o == 0 ? (int64_t)pos0 : (int64_t)X.kpos[st + o];
-            if (s > 0) {
-                const int qc = L.q[s - 1];
-                if (qc < 4 && r0 > 0 && X.T[r0 - 1] == qc) continue;  // not left-maximal
+        const int qcl = s > 0 && s + AF_K <= l ? L.q[s - 1] : 4;
+        const int ocnt = wave_max(cnt);
+        for (int o = 0; o < ocnt; ++o) {
+            bool lm = false;
+            int64_t r0 = 0;
+            if (o < cnt) {
+                r0 = o == 0 ? (int64_t)pos0 : (int64_t)X.kpos[st + o];
+                lm = !(qcl < 4 && r0 > 0 && X.T[r0 - 1] == qcl);
             }
-            int len = AF_K;
-            for (;;) {
-                const int qp = s + len;
-                const int64_t rp = r0 + len;
+            uint64_t msk = __ballot(lm);
+            while (msk) {
+                const int ln = __builtin_ctzll(msk);
+                msk &= msk - 1;
+                const int cs = __builtin_amdgcn_readlane(s, ln);
+                const int cr = __builtin_amdgcn_readlane((int)r0, ln);
+                // word lane + 1 of the match: query [cs + 16 (lane + 1), +16) vs T at cr + same
+                const int qp = cs + AF_K + 16 * lane;
+                const int64_t rp = (int64_t)cr + AF_K + 16 * lane;
                 const int64_t room64 = min((int64_t)(l - qp), N - rp);
-                if (room64 <= 0) break;
-                const int room = (int)min(room64, (int64_t)16);
-                const int wp = qp >> 4, sp = qp & 15;
-                const uint32_t qk = __builtin_amdgcn_alignbit(L.pk[wp + 1], L.pk[wp], 2 * sp);
-                const int qn = __builtin_ctz((((L.nm[wp] | (L.nm[wp + 1] << 16)) >> sp) & 0xFFFFu) | 0x10000u);
-                const uint32_t x = qk ^ getT16(X, rp);
-                const int eq = x ? (__builtin_ctz(x) >> 1) : 16;
-                const int step = min(min(eq, room), qn);
-                len += step;
-                if (step < 16) break;
+                int step = 0;
+                if (room64 > 0) {
+                    const int room = (int)min(room64, (int64_t)16);
+                    const int wp = qp >> 4, sp = qp & 15;
+                    const uint32_t qk = __builtin_amdgcn_alignbit(L.pk[wp + 1], L.pk[wp], 2 * sp);
+                    const int qn = __builtin_ctz((((L.nm[wp] | (L.nm[wp + 1] << 16)) >> sp) & 0xFFFFu) | 0x10000u);
+                    const uint32_t x = qk ^ getT16(X, rp);
+                    const int eq = x ? (__builtin_ctz(x) >> 1) : 16;
+                    step = min(min(eq, room), qn);
+                }
+                const uint64_t stop = __ballot(step < 16);  // lanes past the read's end stop too
+                const int js = stop ? (int)__builtin_ctzll(stop) : 63;
+                const int len = AF_K + 16 * js + __builtin_amdgcn_readlane(step, js);
+                if (len >= msl) {
+                    if (lane == 0) {
+                        const int slot = S.cnt[0];
+                        if (slot < AF_S2_MAX_PMEM) S.x.pm[slot] = S2Pm{(int16_t)cs, (int16_t)(cs + len), (int32_t)cr};
+                        S.cnt[0] = slot + 1;
+                    }
+                    wave_sync();
+                }
             }
-            if (len < msl) continue;
-            const int slot = atomicAdd(&S.cnt[0], 1);
-            if (slot < AF_S2_MAX_PMEM) S.x.pm[slot] = S2Pm{(int16_t)s, (int16_t)(s + len), (int32_t)r0};
         }
     }
 }
@@ -251,11 +273,7 @@ __device__ void s2_push_intv(const DevText &X, int npm, int b, int e, int lane, 
             const uint64_t msk = __ballot(v);
             if (v) {
                 const int idx = occ0 + c + lanes_below(msk, lane);
-                if (idx < AF_S2_MAX_OCC) {
-                    const int32_t pos = m.r + (b - m.s);
-                    S.y.a.occ[idx] = pos;
-                    S.y.a.tmp[idx] = X.rank[pos];
-                }
+                if (idx < AF_S2_MAX_OCC) S.y.a.occ[idx] = m.r + (b - m.s);
             }
             c += __builtin_popcountll(msk);
         }
@@ -266,11 +284,15 @@ __device__ void s2_push_intv(const DevText &X, int npm, int b, int e, int lane, 
         wave_sync();
         return;
     }
-    // rank sort of occ[occ0, occ0 + c): each lane takes up to two entries (c <= 128)
+    // rank sort of occ[occ0, occ0 + c): each lane takes up to two entries (c <= 128); a single
+    // occurrence needs no rank
     int pa = 0, ra = 0, pb = 0, rb = 0, da = -1, db = -1;
-    if (lane < c) { pa = S.y.a.occ[occ0 + lane]; ra = S.y.a.tmp[occ0 + lane]; }
-    if (lane + 64 < c) { pb = S.y.a.occ[occ0 + lane + 64]; rb = S.y.a.tmp[occ0 + lane + 64]; }
-    if (lane < c || lane + 64 < c) {
+    if (c > 1) {
+        if (lane < c) { pa = S.y.a.occ[occ0 + lane]; ra = X.rank[pa]; S.y.a.tmp[occ0 + lane] = ra; }
+        if (lane + 64 < c) { pb = S.y.a.occ[occ0 + lane + 64]; rb = X.rank[pb]; S.y.a.tmp[occ0 + lane + 64] = rb; }
+        wave_sync();
+    }
+    if (c > 1 && (lane < c || lane + 64 < c)) {
         int ca = 0, cb = 0;
         for (int j = 0; j < c; ++j) {
             const int rj = S.y.a.tmp[occ0 + j];
@@ -295,7 +317,8 @@ __device__ void s2_push_intv(const DevText &X, int npm, int b, int e, int lane, 
 __device__ void s2_smem_at(const DevText &X, int npm, int l, int msl, int x, int m, int lane) {
     DpLds &L = g_dp;
     S2Lds &S = g_s2;
-    const int c0 = X.base_cnt[L.q[x]];
+    const int bx = __builtin_amdgcn_readfirstlane((int)L.q[x]);  // < 4 (callers skip N)
+    const int c0 = bx == 0 ? X.base_cnt[0] : bx == 1 ? X.base_cnt[1] : bx == 2 ? X.base_cnt[2] : X.base_cnt[3];
     if (c0 < m) {  // degenerate: the single base occurs fewer than m times
         if (x + msl > l) return;
         for (int i = x + 1; i < x + msl; ++i) if (L.q[i] > 3) return;
