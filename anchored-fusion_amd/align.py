@@ -112,6 +112,47 @@ class AnchorAligner:
                    "af_align_pairs")
         return AlignResult(**out)
 
+    def align_segments(self, reads, lens, seg_pairs) -> AlignResult:
+        """One batch holding several independent inputs (e.g. single-cell cells), each aligned
+        as its own ``bwa mem`` run: read ids from 0 and insert-size chunks from the segment's
+        first pair.  ``seg_pairs``: pairs per segment, in row order.  One H2D copy of the
+        batch, one device call per segment on one stream, one D2H copy of the records."""
+        import torch
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        nr, stride = reads.shape
+        if nr % 2 or 2 * int(sum(seg_pairs)) != nr:
+            raise ValueError("seg_pairs must cover the batch's pairs exactly")
+        dev = torch.device("cuda", self.device)
+        # segments start on 16-byte boundaries of one device buffer (the seed filter's loads)
+        starts, off = [], 0
+        for n in seg_pairs:
+            starts.append(off)
+            off = (off + 2 * int(n) * stride + 15) // 16 * 16
+        host = np.zeros(max(off, 16), np.uint8)
+        r0 = 0
+        for n, b in zip(seg_pairs, starts):
+            r1 = r0 + 2 * int(n)
+            host[b:b + (r1 - r0) * stride] = reads[r0:r1].reshape(-1)
+            r0 = r1
+        flat = torch.from_numpy(host).to(dev)
+        lt = None if lens is None else torch.from_numpy(np.ascontiguousarray(lens, dtype=np.int32)).to(dev)
+        out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+        out["cigar"] = torch.zeros((nr, _lib.AF_MAX_CIGAR), dtype=torch.int32, device=dev)
+        s = torch.cuda.current_stream(dev)
+        r0 = 0
+        for n, b in zip(seg_pairs, starts):
+            n = int(n)
+            if n:
+                r1 = r0 + 2 * n
+                rt = flat[b:b + 2 * n * stride].view(2 * n, stride)
+                self.align_pairs_device(rt, n, stride, {k: v[r0:r1] for k, v in out.items()},
+                                        None if lt is None else lt[r0:r1], stream=s, pair_base=0)
+                r0 = r1
+        torch.cuda.synchronize(dev)
+        got = {k: v.cpu().numpy() for k, v in out.items()}
+        got["cigar"] = got["cigar"].view(np.uint32)
+        return AlignResult(**got)
+
     def align_fastq(self, fq1, fq2, batch_pairs=1 << 20, threads=0):
         """FASTQ(.gz) pair -> records, streamed: the native reader (io.iter_pairs) parses batch
         k + 1 on host threads while batch k is aligned (both ctypes calls release the GIL).

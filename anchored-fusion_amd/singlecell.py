@@ -4,7 +4,8 @@ The reference runs the whole bulk pipeline once per cell and per anchored gene, 
 through its own `bwa mem` (SC:205-256), then merges the per-cell prediction tables
 (SC:258-287).  Here the cells are batched: every cell's FASTQ pair is ingested once
 (native reader), and per gene the pairs of whole cells are concatenated into batches of up to
-``batch_pairs`` pairs, each aligned by ONE pass of the GPU path (S1 + S2).  The records are then
+``batch_pairs`` pairs: one H2D copy per batch and one device call per cell (each cell is its own
+``bwa mem`` run, so read ids and insert-size chunks restart per cell).  The records are then
 split back per cell and each cell runs S3-S8 + Final_fusion on its own records, exactly as a
 separate run on that cell would (the S3 sort and every consumer see only the cell's reads).
 
@@ -72,6 +73,17 @@ def _concat(cells):
         lens[o:o + r.shape[0]] = r.shape[1] if ln is None else ln
         o += r.shape[0]
     return reads, (None if (lens == stride).all() else lens)
+
+
+def _per_segment(aligner, reads, lens, seg_pairs):
+    """align_segments for aligners without a device path (one align_pairs call per cell)."""
+    parts, r0 = [], 0
+    for n in seg_pairs:
+        r1 = r0 + 2 * n
+        parts.append(aligner.align_pairs(reads[r0:r1], None if lens is None else lens[r0:r1]))
+        r0 = r1
+    return AlignResult(*(np.concatenate([getattr(p, k) for p in parts])
+                         for k in ("flag", "pos", "score", "n_cigar", "cigar", "hits")))
 
 
 def merge_cell_tables(cells, work_folder, out_name, out_prefix):
@@ -150,7 +162,10 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
         try:
             for grp in groups:
                 reads, lens = _concat([data[k] for k in grp])
-                res = aligner.align_pairs(reads, lens)
+                # every cell is its own bwa run (read ids and insert-size chunks restart per cell)
+                seg = [data[k][1].shape[0] // 2 for k in grp]
+                segs = getattr(aligner, "align_segments", None)
+                res = segs(reads, lens, seg) if segs else _per_segment(aligner, reads, lens, seg)
                 log(f"[{gene}] S2 batch of {len(grp)} cells, {reads.shape[0] // 2} pairs: "
                     f"{int(((res.flag & 4) == 0).sum())} reads on the anchor")
                 row = 0

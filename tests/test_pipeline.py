@@ -3,7 +3,9 @@ fusion sample.
 
 The CPU test swaps the GPU search services for the oracle (tests/oracle_backends.py). The
 GPU test runs the product path. Both must report the planted BCRX-ABLX fusion, with its anchor
-breakpoint within a few bases of the junction.
+breakpoint within a few bases of the junction; and on the same world the GPU pipeline's
+candidate tables must equal the oracle pipeline's byte for byte (the whole §8 a chain:
+S2 records -> partitions -> genome/partner searches -> clustering -> Final_fusion).
 """
 import os
 
@@ -28,16 +30,40 @@ def _check(out_folder, truth):
     return hit
 
 
-def test_pipeline_cpu_backends(tmp_path):
+def _run_oracle(paths, out):
     from oracle_backends import OracleAligner, OracleReference
     from anchored_fusion_amd.place import Placer
-    paths, truth = make_world(str(tmp_path / "world"))
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
     searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference))
-    out = str(tmp_path / "out")
     pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out,
                  searches=searches, aligner_factory=OracleAligner, log=lambda *_: None)
+
+
+def test_pipeline_cpu_backends(tmp_path):
+    paths, truth = make_world(str(tmp_path / "world"))
+    out = str(tmp_path / "out")
+    _run_oracle(paths, out)
     _check(out, truth)
+
+
+TABLES = ("BCRX_fusion_predictions.txt", "BCRX_fusion_predictions_abridged.txt")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n_fusion", [(2024, 400), (7, 400), (99, 60), (5, 1200)])
+def test_pipeline_gpu_tables_equal_oracle(tmp_path, seed, n_fusion):
+    """GPU pipeline vs the CPU-oracle pipeline on the same world: identical TSVs."""
+    paths, truth = make_world(str(tmp_path / "world"), seed=seed, n_fusion=n_fusion)
+    gpu, cpu = str(tmp_path / "gpu"), str(tmp_path / "cpu")
+    pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], gpu,
+                 log=lambda *_: None)
+    _run_oracle(paths, cpu)
+    for t in TABLES:
+        a = open(os.path.join(gpu, "BCRX_fusion", t), "rb").read()
+        b = open(os.path.join(cpu, "BCRX_fusion", t), "rb").read()
+        assert a == b, (t, a[:2000], b[:2000])
+    rows = [ln.split("\t") for ln in open(os.path.join(gpu, "BCRX_fusion", TABLES[1]))][1:]
+    assert any("ABLX" in r[0] for r in rows)
 
 
 @pytest.mark.gpu

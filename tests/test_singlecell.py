@@ -114,3 +114,28 @@ def test_singlecell_gpu(tmp_path):
         genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
         return pipeline.Searches(genome)
     _run_and_compare(tmp_path, searches, None)
+
+
+@pytest.mark.gpu
+def test_singlecell_gpu_tables_equal_oracle(tmp_path):
+    """Single-cell on the GPU (cells batched, one device call per cell) vs the same driver with
+    the CPU-oracle backends: every per-cell table and both merged tables identical."""
+    from oracle_backends import OracleAligner, OracleReference
+    from anchored_fusion_amd.place import Placer
+    paths, truth = make_world(str(tmp_path / "world"))
+    fqd = str(tmp_path / "cells")
+    cells = _split_cells(paths, fqd, n_cells=4)
+    genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
+    gpu, cpu = str(tmp_path / "gpu"), str(tmp_path / "cpu")
+    singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], gpu, searches=pipeline.Searches(genome),
+                   batch_pairs=1200, log=lambda *_: None)
+    singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], cpu,
+                   searches=pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference)),
+                   aligner_factory=OracleAligner, batch_pairs=1200, log=lambda *_: None)
+    files = [os.path.join("BCRX", "work_dir", c, "BCRX_fusion_predictions" + x) for c in cells
+             for x in (".txt", "_abridged.txt")]
+    files += [os.path.join("BCRX", "BCRX_fusion_gene_cell_predictions" + x) for x in (".txt", "_abridged.txt")]
+    for f in files:
+        a = open(os.path.join(gpu, f), "rb").read()
+        b = open(os.path.join(cpu, f), "rb").read()
+        assert a == b, f
