@@ -33,7 +33,7 @@ EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_pe_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
+    "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close",
 )
 
@@ -111,6 +111,8 @@ def lib():
     L.af_align_candidates_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _pe,
                                              ctypes.POINTER(AlnOut), _vp]
     L.af_align_candidates_device.restype = ctypes.c_int
+    L.af_partition_device.argtypes = [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp]
+    L.af_partition_device.restype = ctypes.c_int
     L.af_seed_filter_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp]
     L.af_seed_filter_device.restype = ctypes.c_int
     L.af_last_candidates.argtypes = [_vp]

@@ -278,6 +278,28 @@ class AnchorAligner:
             tail_lens_t.data_ptr(), tail_read_t.data_ptr(), n_tails_t.data_ptr(), _stream_handle(stream)),
             "af_split_tails_device")
 
+    def partition_device(self, flag_t, pos_t, outs=None, stream=None):
+        """S3 on the device (af_partition_device; AF:182 `samtools sort` + AF:186-194): read rows
+        of tmp1 / tmp2 / anchored in samtools' coordinate order, as ``partition`` returns them.
+        outs: optional (tmp1, tmp2, anchored, counts) device tensors to reuse (int32 [n_reads] x 3,
+        int64 [3]).  Returns (tmp1, tmp2, anchored, counts); the first three are the full-size
+        buffers, valid up to counts[k] (read counts with .cpu() when needed)."""
+        import torch
+        n = int(flag_t.numel())
+        if pos_t.numel() != n:
+            raise ValueError("flag and pos must have one entry per read")
+        if outs is None:
+            dev = flag_t.device
+            outs = tuple(torch.empty(max(n, 1), dtype=torch.int32, device=dev) for _ in range(3)) + (
+                torch.zeros(3, dtype=torch.int64, device=dev),)
+        t1, t2, an, cnt = outs
+        if min(t1.numel(), t2.numel(), an.numel()) < n or cnt.numel() < 3:
+            raise ValueError("partition outputs need n_reads rows each and 3 counts")
+        _lib.check(self._ctx, _lib.lib().af_partition_device(
+            self._ctx, flag_t.data_ptr(), pos_t.data_ptr(), n, max(1, len(self.anchor)), t1.data_ptr(),
+            t2.data_ptr(), an.data_ptr(), cnt.data_ptr(), _stream_handle(stream)), "af_partition_device")
+        return t1, t2, an, cnt
+
     @property
     def ctx(self):
         """The raw af_ctx handle (e.g. for place.Reference.place_device on this slot's stream)."""

@@ -234,3 +234,9 @@ size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();
 hipError_t af_build_genome_index(const uint8_t *seq, int64_t n, uint8_t *D, uint32_t *D2, uint32_t *Dn,
                                  uint32_t *S, uint32_t *kposu, uint32_t *scan_sums, int n_cu, hipStream_t s);
+// s3.hip: S3 (samtools sort + flag filters) on the device
+size_t af_s3_temp_bytes(int64_t n_reads);
+hipError_t af_launch_s3(const int32_t *flag, const int32_t *pos, int64_t n_reads, int64_t ref_len, uint64_t *keys,
+                        uint64_t *keys_alt, void *temp, size_t temp_bytes, int64_t *counts, int32_t *tmp1,
+                        int32_t *tmp2, int32_t *anchored, hipStream_t s);
+

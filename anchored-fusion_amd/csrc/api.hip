@@ -39,6 +39,12 @@ struct af_ctx {
     S2Pes *s2_pes = nullptr;
     int64_t *s2_cstart = nullptr;
     int32_t s2_max_chunks = 0;
+    // S3 (s3.hip)
+    uint64_t *s3_keys = nullptr;
+    void *s3_temp = nullptr;
+    int64_t s3_cap = 0;
+    size_t s3_temp_bytes = 0;
+    int64_t *s3_counts = nullptr;
     // af_place staging (host-buffer API)
     uint8_t *p_q = nullptr;
     int32_t *p_lens = nullptr, *p_nhits = nullptr;
@@ -351,6 +357,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->s2_pool); af_free(c->s2_rmap); af_free(c->s2_plist); af_free(c->s2_ghist); af_free(c->s2_scan);
     af_free(c->s2_plan);
     af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
+    af_free(c->s3_keys); af_free(c->s3_temp); af_free(c->s3_counts);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -784,6 +791,38 @@ int af_place_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, con
     HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
     HIPCHK(c, af_launch_place(ix->dev, d_queries, c->ctrl + AF_CTRL_PLACE_N, stride, d_lens, *p,
                               c->ctrl + AF_CTRL_PLACE_HEADS, c->zscratch, c->n_slots, d_hits, d_n_hits, max_hits, s));
+    return AF_OK;
+}
+
+int af_partition_device(af_ctx *c, const int32_t *d_flag, const int32_t *d_pos, int64_t n_reads, int64_t ref_len,
+                        int32_t *d_tmp1, int32_t *d_tmp2, int32_t *d_anchored, int64_t *d_counts, void *stream) {
+    if (!c || !d_counts || (n_reads > 0 && (!d_flag || !d_pos || !d_tmp1 || !d_tmp2 || !d_anchored)))
+        return fail(c, AF_E_INVALID, "null argument");
+    if (n_reads < 0 || n_reads > (1LL << 31) - 1) return fail(c, AF_E_INVALID, "n_reads out of range");
+    if (ref_len <= 0 || ref_len > (1LL << 31) - 1) return fail(c, AF_E_INVALID, "ref_len outside [1, 2^31)");
+    (void)hipSetDevice(c->device);
+    const hipStream_t s = (hipStream_t)stream;
+    if (n_reads == 0) {
+        HIPCHK(c, hipMemsetAsync(d_counts, 0, 3 * sizeof(int64_t), s));
+        return AF_OK;
+    }
+    if (n_reads > c->s3_cap) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (c->s3_keys) (void)hipFree(c->s3_keys);
+        if (c->s3_temp) (void)hipFree(c->s3_temp);
+        c->s3_keys = nullptr; c->s3_temp = nullptr; c->s3_cap = 0;
+        const size_t tb = af_s3_temp_bytes(n_reads);
+        if (hipMalloc(&c->s3_keys, 2 * sizeof(uint64_t) * (size_t)n_reads) != hipSuccess ||
+            hipMalloc(&c->s3_temp, tb) != hipSuccess)
+            return fail(c, AF_E_NOMEM, "S3 scratch for %lld reads", (long long)n_reads);
+        c->s3_cap = n_reads;
+        c->s3_temp_bytes = tb;
+    }
+    if (!c->s3_counts && hipMalloc(&c->s3_counts, 4 * sizeof(int64_t)) != hipSuccess)
+        return fail(c, AF_E_NOMEM, "S3 counts");
+    HIPCHK(c, af_launch_s3(d_flag, d_pos, n_reads, ref_len, c->s3_keys, c->s3_keys + c->s3_cap, c->s3_temp,
+                           c->s3_temp_bytes, c->s3_counts, d_tmp1, d_tmp2, d_anchored, s));
+    HIPCHK(c, hipMemcpyAsync(d_counts, c->s3_counts, 3 * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
     return AF_OK;
 }
 

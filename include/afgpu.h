@@ -19,6 +19,8 @@
  *   af_split_tails_device <- the split-read selection + query FASTA of the partner search
  *                            (functions.py:705-716, 1001-1005), from device-resident records
  *   af_align_candidates_tails_device <- af_align_candidates_device + the same tails, fused
+ *   af_partition_device   <- `| samtools sort` of the same call and the three
+ *                            `samtools view -f/-F` filters of Anchored_Fusion.py:186-194
  *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
@@ -189,6 +191,18 @@ int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, 
                           const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t read_base,
                           int32_t append, int64_t cap, uint8_t *d_tails, int32_t *d_tail_lens,
                           int32_t *d_tail_read, int32_t *d_n_tails, void *stream);
+
+/* S3 on the device (Anchored_Fusion.py:182 `| samtools sort`, then AF:186-194): the records
+ * d_flag/d_pos of n_reads reads (pair-major, as written by af_align_pairs*) in samtools'
+ * coordinate order -- placed records by (pos, strand), ties in input order -- filtered into
+ *   d_tmp1      `samtools view -f 8 -F 260`   (AF:186, mapped primary, mate unmapped)
+ *   d_tmp2      `samtools view -f 4 -F 264`   (AF:187, unmapped, mate mapped)
+ *   d_anchored  `samtools view -F 772`        (AF:194, mapped primary)
+ * as read rows in that order; d_counts[0..2] = their lengths (int64, device).  Each output
+ * needs room for n_reads rows in the worst case.  ref_len bounds pos (the anchor length).
+ * Enqueued on `stream`; synchronizes it once (the selected count sizes the sort). */
+int af_partition_device(af_ctx *ctx, const int32_t *d_flag, const int32_t *d_pos, int64_t n_reads, int64_t ref_len,
+                        int32_t *d_tmp1, int32_t *d_tmp2, int32_t *d_anchored, int64_t *d_counts, void *stream);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as

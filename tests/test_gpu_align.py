@@ -265,3 +265,56 @@ def test_seed_filter_ragged_strides(aligner, oidx, anchor, stride):
     got = hits.cpu().numpy()
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     assert aligner.last_candidates() == int((want > 0).sum())
+
+
+def _random_records(n, seed, max_pos=300):
+    """Flag/pos columns with bwa's pair conventions (as test_consumers.test_partition_matches_full_sort)."""
+    rng = np.random.default_rng(seed)
+    flag = np.zeros(n, np.int32)
+    pos = np.full(n, -1, np.int32)
+    m = rng.random((n // 2, 2)) < 0.3
+    rv = rng.random((n // 2, 2)) < 0.5
+    x = rng.integers(0, max_pos, (n // 2, 2))
+    sec = rng.random((n // 2, 2)) < 0.02
+    for k in (0, 1):
+        f = np.full(n // 2, 0x1 | (0x40 if k == 0 else 0x80), np.int32)
+        f |= np.where(m[:, k], np.where(rv[:, k], 0x10, 0), 0x4).astype(np.int32)
+        f |= np.where(~m[:, 1 - k], 0x8, np.where(rv[:, 1 - k], 0x20, 0)).astype(np.int32)
+        f |= np.where(sec[:, k] & m[:, k], 0x100, 0).astype(np.int32)
+        flag[k::2] = f
+        pos[k::2] = np.where(m[:, k], x[:, k], np.where(m[:, 1 - k], x[:, 1 - k], -1))
+    return flag, pos
+
+
+@pytest.mark.parametrize("n,seed,max_pos", [(2, 1, 5), (20000, 5, 300), (400000, 6, 7000), (1 << 20, 7, 40)])
+def test_partition_device_matches_host(aligner, n, seed, max_pos):
+    """S3 on the device (af_partition_device) vs align.partition: identical row lists."""
+    import torch
+    from anchored_fusion_amd.align import AlignResult, partition
+    flag, pos = _random_records(n, seed, max_pos)
+    z = np.zeros(n, np.int32)
+    want = partition(AlignResult(flag, pos, z, z, np.zeros((n, 1), np.uint32), z))
+    dev = torch.device("cuda:0")
+    t1, t2, an, cnt = aligner.partition_device(torch.from_numpy(flag).to(dev), torch.from_numpy(pos).to(dev))
+    c = cnt.cpu().numpy()
+    for g, k, w in zip((t1, t2, an), c, want):
+        assert np.array_equal(g[:k].cpu().numpy(), w)
+
+
+def test_partition_device_on_s2_records(aligner, anchor):
+    """S3 after S2 on the device, both in HBM: equal to the host partition of the same records."""
+    import torch
+    from anchored_fusion_amd.align import AlignResult, partition
+    reads, _, _ = synthetic_pairs(anchor, 20000, 150, seed=71, fusion_frac=0.5)
+    dev = torch.device("cuda:0")
+    nr = reads.shape[0]
+    out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+    out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
+    aligner.align_pairs_device(torch.from_numpy(reads).to(dev), nr // 2, 150, out)
+    t1, t2, an, cnt = aligner.partition_device(out["flag"], out["pos"])
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    want = partition(AlignResult(got["flag"], got["pos"], got["score"], got["n_cigar"], got["cigar"], got["hits"]))
+    c = cnt.cpu().numpy()
+    assert c[2] > 1000
+    for g, k, w in zip((t1, t2, an), c, want):
+        assert np.array_equal(g[:k].cpu().numpy(), w)
