@@ -27,13 +27,14 @@ AF_MAX_READ = 320
 AF_K = 16
 AF_FLAG_MEM_OVERFLOW = 0x10000
 AF_FLAG_CIGAR_OVERFLOW = 0x20000
+AF_GATHER_SEQUENCED, AF_GATHER_SPLIT_SAM = 0, 1
 
 # every symbol include/afgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_pe_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
+    "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_index_build_genome_device", "af_gather_reads_device", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close",
 )
 
@@ -92,6 +93,8 @@ def lib():
     L.af_index_build.restype = ctypes.c_int
     L.af_index_build_genome.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
     L.af_index_build_genome.restype = ctypes.c_int
+    L.af_index_build_genome_device.argtypes = [_vp, _vp, _i64, ctypes.POINTER(_vp)]
+    L.af_index_build_genome_device.restype = ctypes.c_int
     L.af_index_free.argtypes = [_vp]
     L.af_index_free.restype = None
     L.af_index_anchor_len.argtypes = [_vp]
@@ -128,6 +131,9 @@ def lib():
                                                    ctypes.POINTER(AlnOut), _i32, _i64, _i32, _i64, _vp, _vp, _vp,
                                                    _vp, _vp]
     L.af_align_candidates_tails_device.restype = ctypes.c_int
+    L.af_gather_reads_device.argtypes = [_vp, _vp, _i32, _vp, _vp, _i64, _i32, ctypes.POINTER(AlnOut), _i64, _i64,
+                                         _i64, _vp, _vp, _vp, _vp, _vp]
+    L.af_gather_reads_device.restype = ctypes.c_int
     L.af_fastq_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_vp)]
     L.af_fastq_open.restype = ctypes.c_int
     L.af_fastq_next.argtypes = [_vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i32), ctypes.POINTER(_i64)]

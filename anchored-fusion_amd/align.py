@@ -300,6 +300,31 @@ class AnchorAligner:
             t2.data_ptr(), an.data_ptr(), cnt.data_ptr(), _stream_handle(stream)), "af_partition_device")
         return t1, t2, an, cnt
 
+    def gather_reads_device(self, reads_t, stride, rows_t, n_rows, mode, q_t, q_lens_t, q_rows_t=None, n_q_t=None,
+                            out_t=None, lens_t=None, first=0, step=1, stream=None):
+        """af_gather_reads_device: queries of the genome searches from an S3 row list (rows_t, the
+        first n_rows entries; n_rows a host count).  mode _lib.AF_GATHER_SEQUENCED (S4's `samtools
+        fastq`, AF:186-188) or _lib.AF_GATHER_SPLIT_SAM (S5's split reads, functions.py:705-716;
+        out_t gives FLAG / CIGAR).  Query k goes to row first + k * step of q_t (uint8 [cap, stride]);
+        n_q_t (int32 [1], optional) receives the slot count for af_place_device."""
+        cap = int(q_t.shape[0])
+        if q_t.dim() != 2 or int(q_t.shape[1]) != int(stride) or q_lens_t.numel() < cap:
+            raise ValueError("q_t must be [cap, stride] and q_lens_t hold cap entries")
+        if q_rows_t is not None and q_rows_t.numel() < cap:
+            raise ValueError("q_rows_t holds fewer than cap entries")
+        if int(n_rows) > rows_t.numel():
+            raise ValueError("n_rows exceeds the row list")
+        o = None
+        if out_t is not None:
+            o = _lib.AlnOut(*(out_t[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+        elif mode == _lib.AF_GATHER_SPLIT_SAM:
+            raise ValueError("AF_GATHER_SPLIT_SAM needs out_t")
+        _lib.check(self._ctx, _lib.lib().af_gather_reads_device(
+            self._ctx, reads_t.data_ptr(), int(stride), None if lens_t is None else lens_t.data_ptr(),
+            rows_t.data_ptr(), int(n_rows), int(mode), None if o is None else ctypes.byref(o), int(first), int(step),
+            cap, q_t.data_ptr(), q_lens_t.data_ptr(), None if q_rows_t is None else q_rows_t.data_ptr(),
+            None if n_q_t is None else n_q_t.data_ptr(), _stream_handle(stream)), "af_gather_reads_device")
+
     @property
     def ctx(self):
         """The raw af_ctx handle (e.g. for place.Reference.place_device on this slot's stream)."""
@@ -332,8 +357,8 @@ class AlignerGroup:
             a.close()
 
     def run_device(self, batches, events=None, wait=None, post=None, finish=None, tails=None, before=None):
-        """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t]) with
-        every tensor on the device.  Enqueues them and returns without synchronising.
+        """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t[, pair_base]])
+        with every tensor on the device (pair_base: the batch's first pair in bwa's input stream).  Enqueues them and returns without synchronising.
 
         All K1s go to slot 0's stream, back to back (no cross-queue wait between them); batch
         j's K2 + K3 go to slot j's stream after one wait for the last K1.  wait (optional):
@@ -371,11 +396,13 @@ class AlignerGroup:
             lens_t = b[4] if len(b) > 4 else None
             if before is not None:
                 before(j, self.aligners[j], s)
+            pb = b[5] if len(b) > 5 else 0
             if tails is not None:
                 self.aligners[j].align_candidates_tails_device(reads_t, n_pairs, stride, out_t, tails(j), lens_t,
-                                                               stream=s)
+                                                               stream=s, pair_base=pb)
             else:
-                self.aligners[j].align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s)
+                self.aligners[j].align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s,
+                                                         pair_base=pb)
             if post is not None:
                 post(j, self.aligners[j], s)
             e = torch.cuda.Event()

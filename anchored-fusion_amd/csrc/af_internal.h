@@ -229,6 +229,11 @@ hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *l
                                hipStream_t s);
 hipError_t af_launch_split_tails(const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
                                  const af_aln_out &out, const AfTails &t, bool append, hipStream_t s);
+size_t af_gather_temp_bytes(int64_t n_rows);
+hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t *lens, const int32_t *rows,
+                            int64_t n_rows, int32_t mode, const af_aln_out &out, int64_t first, int64_t step,
+                            int64_t cap, uint8_t *q, int32_t *q_lens, int32_t *q_rows, int32_t *n_q, int32_t *sel,
+                            int64_t *sel_n, void *temp, size_t temp_bytes, hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);
 size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();

@@ -45,6 +45,11 @@ struct af_ctx {
     int64_t s3_cap = 0;
     size_t s3_temp_bytes = 0;
     int64_t *s3_counts = nullptr;
+    int32_t *g_sel = nullptr;   // af_gather_reads_device: selected rows, their count, select scratch
+    int64_t *g_sel_n = nullptr;
+    void *g_temp = nullptr;
+    int64_t g_cap = 0;
+    size_t g_temp_bytes = 0;
     // af_place staging (host-buffer API)
     uint8_t *p_q = nullptr;
     int32_t *p_lens = nullptr, *p_nhits = nullptr;
@@ -358,6 +363,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->s2_plan);
     af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
     af_free(c->s3_keys); af_free(c->s3_temp); af_free(c->s3_counts);
+    af_free(c->g_sel); af_free(c->g_sel_n); af_free(c->g_temp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -459,7 +465,7 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     return AF_OK;
 }
 
-int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out) {
+static int build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out, hipMemcpyKind kind) {
     if (!c || !seq || !out) return fail(c, AF_E_INVALID, "null argument");
     *out = nullptr;
     if (len < AF_K) return fail(c, AF_E_INVALID, "reference shorter than %d", AF_K);
@@ -491,7 +497,7 @@ int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **ou
     if ((e = alloc(&p_S, af_genome_index_table_bytes(), true)) != hipSuccess) return bail(e, "hipMalloc(16-mer table)");
     if ((e = alloc(&p_pos, 4 * nq, true)) != hipSuccess) return bail(e, "hipMalloc(positions)");
     if ((e = alloc(&p_sums, 4 * (size_t)af_genome_scan_blocks(), false)) != hipSuccess) return bail(e, "hipMalloc(scan)");
-    if ((e = hipMemcpyAsync(p_seq, seq, (size_t)n, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(p_seq, seq, (size_t)n, kind, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(p_D2, 0, 4 * d2w, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(p_Dn, 0, 4 * dnw, c->stream)) != hipSuccess)
         return bail(e, "upload");
@@ -513,6 +519,14 @@ int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **ou
     ix->dev.bl_bits = -1;
     *out = ix;
     return AF_OK;
+}
+
+int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out) {
+    return build_genome(c, seq, len, out, hipMemcpyHostToDevice);
+}
+
+int af_index_build_genome_device(af_ctx *c, const char *d_seq, int64_t len, af_index **out) {
+    return build_genome(c, d_seq, len, out, hipMemcpyDeviceToDevice);
 }
 
 void af_index_free(af_index *ix) {
@@ -841,6 +855,37 @@ int af_split_tails_device(af_ctx *c, const uint8_t *d_reads, int64_t n_reads, in
     (void)hipSetDevice(c->device);
     const AfTails t{d_tails, d_tail_lens, d_tail_read, d_n_tails, cap, read_base, min_clip < 1 ? 1 : min_clip};
     HIPCHK(c, af_launch_split_tails(d_reads, n_reads, stride, d_lens, *d_out, t, append != 0, (hipStream_t)stream));
+    return AF_OK;
+}
+
+int af_gather_reads_device(af_ctx *c, const uint8_t *d_reads, int32_t stride, const int32_t *d_lens,
+                           const int32_t *d_rows, int64_t n_rows, int32_t mode, const af_aln_out *d_out,
+                           int64_t first, int64_t step, int64_t cap, uint8_t *d_q, int32_t *d_q_lens,
+                           int32_t *d_q_rows, int32_t *d_n_q, void *stream) {
+    if (!c) return AF_E_INVALID;
+    if (n_rows < 0 || cap < 0 || first < 0 || step < 1 || stride < 1 || stride > AF_MAX_READ)
+        return fail(c, AF_E_INVALID, "af_gather_reads_device: n_rows, cap, first >= 0, step >= 1, 1 <= stride <= %d",
+                    AF_MAX_READ);
+    if (mode != AF_GATHER_SEQUENCED && mode != AF_GATHER_SPLIT_SAM)
+        return fail(c, AF_E_INVALID, "af_gather_reads_device: unknown mode %d", mode);
+    if ((n_rows > 0 && (!d_reads || !d_rows || !d_q || !d_q_lens)) ||
+        (mode == AF_GATHER_SPLIT_SAM && (!d_out || !d_out->flag || !d_out->n_cigar || !d_out->cigar)))
+        return fail(c, AF_E_INVALID, "af_gather_reads_device: null buffer");
+    (void)hipSetDevice(c->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (mode == AF_GATHER_SPLIT_SAM && n_rows > c->g_cap) {
+        af_free(c->g_sel); af_free(c->g_temp);
+        c->g_sel = nullptr; c->g_temp = nullptr; c->g_cap = 0;
+        const size_t tb = af_gather_temp_bytes(n_rows);
+        HIPCHK(c, hipMalloc(&c->g_sel, sizeof(int32_t) * (size_t)n_rows));
+        HIPCHK(c, hipMalloc(&c->g_temp, std::max<size_t>(tb, 16)));
+        c->g_cap = n_rows;
+        c->g_temp_bytes = tb;
+    }
+    if (mode == AF_GATHER_SPLIT_SAM && !c->g_sel_n) HIPCHK(c, hipMalloc(&c->g_sel_n, sizeof(int64_t)));
+    af_aln_out none{};
+    HIPCHK(c, af_launch_gather(d_reads, stride, d_lens, d_rows, n_rows, mode, d_out ? *d_out : none, first, step, cap,
+                               d_q, d_q_lens, d_q_rows, d_n_q, c->g_sel, c->g_sel_n, c->g_temp, c->g_temp_bytes, s));
     return AF_OK;
 }
 

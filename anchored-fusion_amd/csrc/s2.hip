@@ -80,6 +80,14 @@ __device__ __forceinline__ uint32_t getT16(const DevText &X, int64_t pos) {
     return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
 }
 
+// debug build only (make dbg): progress prints of K2 (one wave)
+#ifdef AF_S2_DEBUG
+#define S2DBG(...) do { if (threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#define S2DBGL(...) printf(__VA_ARGS__)
+#else
+#define S2DBGL(...) do { } while (0)
+#define S2DBG(...) do { } while (0)
+#endif
 // ---- klib ksort.h introsort (lane 0; unstable -- tie orders are bwa's) --------------------
 template <class T, class LT>
 __device__ void ks_ins(T *a, int s, int t, LT lt) {
@@ -113,12 +121,14 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
     }
     int d;
     for (d = 2; (1ul << d) < (unsigned long)n; ++d) ;
-    // klib pushes the larger part and continues with the smaller, so the stack holds at most
+    // klib pushes the larger part and continues with the smaller (segments of <= 16 are left to
+    // the final insertion sort), so the stack holds at most
     // log2(n / 17) + 1 segments: 8 covers n <= 17 << 7 (every call site sorts <= 128 items)
     int stl[8], str[8], std_[8], top = 0;
     int s = 0, t = n - 1;
     d <<= 1;
     for (;;) {
+        S2DBGL("introsort s %d t %d d %d top %d\n", s, t, d, top);
         if (s < t) {
             if (--d == 0) { ks_comb(a + s, t - s + 1, lt); t = s; continue; }
             int i = s, j = t, k = i + ((j - i) >> 1) + 1;
@@ -128,18 +138,23 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
             const T rp = a[k];
             if (k != t) { T sw = a[k]; a[k] = a[t]; a[t] = sw; }
             for (;;) {
-                do ++i; while (lt(a[i], rp));
+                // a[t] == rp ends the first scan; the explicit bound keeps a broken comparator from
+                // walking off the array
+                do ++i; while (i < t && lt(a[i], rp));
+                S2DBGL("introsort scan i %d lt(a[t], rp) %d\n", i, (int)lt(a[t], rp));
                 do --j; while (i <= j && lt(rp, a[j]));
                 if (j <= i) break;
                 T sw = a[i]; a[i] = a[j]; a[j] = sw;
+                S2DBGL("introsort swap i %d j %d\n", i, j);
             }
+            S2DBGL("introsort part i %d j %d k %d\n", i, j, k);
             { T sw = a[i]; a[i] = a[t]; a[t] = sw; }
             if (i - s > t - i) {
                 if (i - s > 16) { stl[top] = s; str[top] = i - 1; std_[top] = d; ++top; }
                 s = t - i > 16 ? i + 1 : t;
             } else {
                 if (t - i > 16) { stl[top] = i + 1; str[top] = t; std_[top] = d; ++top; }
-                s = i - s > 16 ? s : i - 1;
+                t = i - s > 16 ? i - 1 : s;
             }
         } else {
             if (top == 0) { ks_ins(a, 0, n, lt); return; }
@@ -373,8 +388,10 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
     S2Lds &S = g_s2;
     const int msl = p.min_seed_len;
     SPROF(if (lane == 0) g_sub[0] = clock64();)
+    S2DBG("k2 pmems start\n");
     s2_pmems(X, l, msl, lane);
     wave_sync();
+    S2DBG("k2 pmems %d\n", S.cnt[0]);
     SPROF(if (lane == 0) g_sub[1] = g_sub[2] = g_sub[3] = g_sub[4] = clock64();)
     const int npm_all = S.cnt[0];
     if (npm_all > AF_S2_MAX_PMEM) {
@@ -406,6 +423,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
         }
     }
     SPROF(if (lane == 0) g_sub[2] = g_sub[3] = g_sub[4] = clock64();)
+    S2DBG("k2 pass1 seeds %d ovf %d\n", S.cnt[1], S.cnt[3]);
     if (S.cnt[3]) return;
     // pass 2
     const int split_len = (int)((float)msl * 1.5f + .499);
@@ -416,6 +434,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
         s2_smem_at(X, npm, l, msl, (v.qb + v.qe) >> 1, v.cnt + 1, lane);
     }
     SPROF(if (lane == 0) g_sub[3] = g_sub[4] = clock64();)
+    S2DBG("k2 pass2 seeds %d ovf %d\n", S.cnt[1], S.cnt[3]);
     // pass 3 (bwt_seed_strategy1 with min_len = min_seed_len, max_intv = max_mem_intv)
     if (o.max_mem_intv > 0) {
         const int mi = o.max_mem_intv;
@@ -455,6 +474,7 @@ __device__ void s2_collect_intv(const DevText &X, const af_params &p, const S2Op
         }
     }
     SPROF(if (lane == 0) g_sub[4] = clock64();)
+    S2DBG("k2 pass3 seeds %d ovf %d\n", S.cnt[1], S.cnt[3]);
     if (S.cnt[3]) return;
     // sort by (qb, qe): equal intervals are identical, any order among them
     const int ns = S.cnt[1];
@@ -933,8 +953,10 @@ __device__ int s2_dedup_patch(const DevText &X, const af_params &p, const S2Opt 
     S2Lds &S = g_s2;
     S2Reg *a = S.x.reg;
     if (n <= 1) return n;
+    S2DBG("dedup n %d\n", n);
     if (lane == 0) ks_introsort(a, n, LtArs2());
     wave_sync();
+    S2DBG("dedup sorted\n");
     for (int i = 1; i < n; ++i) {
         if (a[i].rb >= a[i - 1].re + o.max_chain_gap) continue;
         for (int j = i - 1; j >= 0 && a[i].rb < a[j].re + o.max_chain_gap; --j) {
@@ -944,6 +966,8 @@ __device__ int s2_dedup_patch(const DevText &X, const af_params &p, const S2Opt 
             const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
             const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
             const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
+            S2DBG("dedup i %d j %d q [%d,%d) r [%ld,%ld) s %d | pp [%d,%d) r [%ld,%ld) s %d\n", i, j, q.qb, q.qe,
+                  (long)q.rb, (long)q.re, q.score, pp.qb, pp.qe, (long)pp.rb, (long)pp.re, pp.score);
             if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
                 const bool drop_p = pp.score < q.score;
                 wave_sync();
@@ -955,7 +979,10 @@ __device__ int s2_dedup_patch(const DevText &X, const af_params &p, const S2Opt 
                 if (drop_p) break;
             } else if (q.rb < pp.rb) {
                 int w = 0;
+                S2DBG("patch i %d j %d q [%d,%d) r [%ld,%ld) w %d | pp [%d,%d) r [%ld,%ld) w %d\n", i, j, q.qb, q.qe,
+                      (long)q.rb, (long)q.re, q.w, pp.qb, pp.qe, (long)pp.rb, (long)pp.re, pp.w);
                 const int score = s2_patch_reg<CPL>(X, p, q, pp, &w, zg, lane);
+                S2DBG("patch score %d\n", score);
                 if (score > 0) {
                     wave_sync();
                     if (lane == 0) {
@@ -970,10 +997,13 @@ __device__ int s2_dedup_patch(const DevText &X, const af_params &p, const S2Opt 
         }
     }
     int m = 0;
+    S2DBG("dedup final\n");
     if (lane == 0) {
         for (int i = 0; i < n; ++i)
             if (a[i].qe > a[i].qb) a[m++] = a[i];
+        S2DBG("dedup final m %d\n", m);
         ks_introsort(a, m, LtArs());
+        S2DBG("dedup final sorted\n");
         for (int i = 1; i < m; ++i)
             if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
         int mm = 1;
@@ -1068,10 +1098,13 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
                 n_chn = S.misc[1];
             }
             SPROF(t2 = clock64(); pr_nch = n_chn;)
+            S2DBG("k2 read %d chains %d ovf %d\n", (int)r, n_chn, S.cnt[3]);
             for (int ci = 0; ci < n_chn && !S.cnt[3]; ++ci) s2_chain2aln<CPL>(X, p, l, ci, lane);
             SPROF(t3 = clock64(); pr_nreg0 = S.cnt[7];)
+            S2DBG("k2 read %d regions %d\n", (int)r, S.cnt[7]);
             if (!S.cnt[3]) n_reg = s2_dedup_patch<CPL>(X, p, o, S.cnt[7], zg, lane);
             SPROF(t4 = clock64();)
+            S2DBG("k2 read %d dedup %d\n", (int)r, n_reg);
         }
         const bool ovf = S.cnt[3] != 0;
         int off = 0;
@@ -1628,6 +1661,7 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
         }
         if (item >= npl) break;
         const int64_t pp = w.plist[item];
+        S2DBG("k3c pair %d start\n", (int)pp);
         SPROF(const int64_t c0 = clock64(); int64_t c1 = c0, c2 = c0, c3 = c0; int nsw = 0;)
         // reads and their regions
         for (int m = 0; m < 2; ++m) {
@@ -1764,6 +1798,7 @@ __global__ __launch_bounds__(64, 6) void k_s2_records(DevText X, const uint8_t *
     for (int item = blockIdx.x; item < npl; item += gridDim.x) {
         const int64_t pp = w.plist[item];
         const S2Plan &pl = plan[item];
+        S2DBG("k3d pair %d start\n", (int)pp);
         SPROF(const int64_t c0 = clock64();)
         // mem_reg2aln of each read's record
         for (int m = 0; m < 2; ++m) {

@@ -1,0 +1,219 @@
+"""Candidate discovery over a read set resident in HBM: S2, S3 and the genome searches of the
+partner stages, all on the device with no host round trip for the data.
+
+| reference step | device work here |
+|---|---|
+| AF:182 `bwa mem -M anchor fq1 fq2` | K1 + K2 + K3 per batch (`AlignerGroup`), batches on bwa's chunk grid |
+| AF:182 `\\| samtools sort`, AF:186-194 filters | `af_partition_device` over every record of the set |
+| AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_place_device` |
+| fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + the same launch |
+| fn:530 BLAT of the split reads' tails (S6) | tails cut in K3 + `af_place_device` (-minScore=20) |
+
+`run()` enqueues one pass; S3 synchronises twice (its select count sizes the sort; the partition
+counts size the gathers).  Everything else stays on the device: the records, the row lists, the
+queries and the hits, which `exchange()` all-gathers between ranks (one process per GPU, RCCL).
+"""
+import os
+import sys
+
+from . import _lib
+from . import place as _place
+from .align import AlignerGroup
+from .shard import chunk_pairs
+
+MIN_CLIP = 20       # split-read tails placed by S6 (functions.py:530 queries; clip >= 20)
+MAX_HITS = 16
+EX_HITS = 4         # hits per query carried by exchange()
+HIT_WORDS = 44      # af_hit as int32 words (176 B)
+EX_WORDS = 39 + EX_HITS * HIT_WORDS
+_DEBUG = os.environ.get("AF_DEBUG_DISCOVER") == "1"
+
+
+def _log(msg):
+    print(f"[discover] {msg}", file=sys.stderr, flush=True)
+
+
+class CandidateDiscovery:
+    """S2 + S3 + S4/S5/S6 genome searches for `n_pairs` resident pairs of `read_len` bases.
+
+    reference: place.Reference (the genome, HBM-resident).  pair_base: the set's first pair in
+    bwa's input stream (a chunk boundary).  batch_chunks: bwa chunks per S2 batch; inflight:
+    batches in flight (AlignerGroup)."""
+
+    def __init__(self, anchor: bytes, reference, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
+                 pair_base=0, chunk_bases=10_000_000, query_frac=0.02, tail_frac=0.01):
+        import torch
+        self.dev = torch.device("cuda", device)
+        self.anchor, self.ref = bytes(anchor), reference
+        self.n_pairs, self.L, self.pair_base = int(n_pairs), int(read_len), int(pair_base)
+        pc = chunk_pairs(self.L, chunk_bases)
+        if self.pair_base % pc:
+            raise ValueError("pair_base must be on bwa's chunk grid")
+        bp = pc * max(1, int(batch_chunks))
+        self.batches = [(p, min(bp, self.n_pairs - p)) for p in range(0, self.n_pairs, bp)]
+        self.grp = AlignerGroup(self.anchor, device=device, inflight=inflight)
+        for a in self.grp.aligners:
+            a.pe.chunk_bases = chunk_bases
+        nr = 2 * self.n_pairs
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
+        self.out = {k: z(max(nr, 1)) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+        self.out["cigar"] = z(max(nr, 1), _lib.AF_MAX_CIGAR)
+        self.s3 = (z(max(nr, 1)), z(max(nr, 1)), z(max(nr, 1)), z(3, dt=torch.int64))
+        # S6 tails (cut in K3, appended by every batch) and the S4 + S5 queries
+        self.tcap = max(4096, int(nr * tail_frac))
+        self.tails = dict(tails=z(self.tcap, self.L, dt=torch.uint8), lens=z(self.tcap), read=z(self.tcap), n=z(1))
+        self.t_hits = z(self.tcap * MAX_HITS * _place.HIT_DTYPE.itemsize, dt=torch.uint8)
+        self.t_nh = z(self.tcap)
+        self.qcap = max(4096, int(nr * query_frac))
+        self.q = z(self.qcap, self.L, dt=torch.uint8)
+        self.q_lens, self.q_rows, self.n_q = z(self.qcap), z(self.qcap), z(1)
+        self.q_hits = z(self.qcap * MAX_HITS * _place.HIT_DTYPE.itemsize, dt=torch.uint8)
+        self.q_nh = z(self.qcap)
+        self.p_genome = _place.preset_params("genome_bwa")
+        self.p_tail = _place.preset_params("split_tail")
+        self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
+
+    def close(self):
+        self.grp.close()
+
+    def _tails(self, j, row0):
+        t = self.tails
+        return dict(tails=t["tails"], lens=t["lens"], read=t["read"], n=t["n"], min_clip=MIN_CLIP, read_base=row0,
+                    append=True)
+
+    def run(self, reads_t, k1_events=None, phase_events=None):
+        """One pass over reads_t (uint8 [2 n_pairs, read_len] on the device).  k1_events: per group
+        a pair of timing events around its K1 launches; phase_events: 4 events recorded on the
+        first slot's stream after S2, S3, the gathers and the placements."""
+        import torch
+        G = self.grp.inflight
+        s0 = self.grp.streams[0]
+        with torch.cuda.stream(s0):
+            self.tails["n"].zero_()
+        done = None
+        for gi, k0 in enumerate(range(0, len(self.batches), G)):
+            group = self.batches[k0:k0 + G]
+            specs, rows0 = [], []
+            for p, n in group:
+                r0, r1 = 2 * p, 2 * (p + n)
+                specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()}, None,
+                              self.pair_base + p))
+                rows0.append(r0)
+            done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done,
+                                       tails=lambda j, rows0=rows0: self._tails(j, rows0[j]))
+        for e in done:
+            s0.wait_event(e)
+        if _DEBUG:
+            s0.synchronize()
+            _log("S2 done")
+        if phase_events:
+            phase_events[0].record(s0)
+        # S3: samtools sort + the three flag filters over every record
+        al = self.grp.aligners[0]
+        t1, t2, an, cnt = al.partition_device(self.out["flag"], self.out["pos"], outs=self.s3, stream=s0)
+        if phase_events:
+            phase_events[1].record(s0)
+        s0.synchronize()
+        n1, n2, na = (int(v) for v in cnt.cpu())
+        if _DEBUG:
+            _log(f"S3 done: tmp1 {n1}, tmp2 {n2}, anchored {na}")
+        # S4 queries: tmp1 / tmp2 interleaved as bwa pairs its two FASTQs; S5: anchored split reads
+        npair = min(n1, n2, self.qcap // 2)
+        al.gather_reads_device(reads_t, self.L, t1, npair, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens,
+                               self.q_rows, None, first=0, step=2, stream=s0)
+        al.gather_reads_device(reads_t, self.L, t2, npair, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens,
+                               self.q_rows, self.n_q, first=1, step=2, stream=s0)
+        al.gather_reads_device(reads_t, self.L, an, na, _lib.AF_GATHER_SPLIT_SAM, self.q, self.q_lens, self.q_rows,
+                               self.n_q, out_t=self.out, first=2 * npair, step=1, stream=s0)
+        if _DEBUG:
+            s0.synchronize()
+            _log(f"gathered {int(self.n_q.item())} queries, {int(self.tails['n'].item())} tails")
+        if phase_events:
+            phase_events[2].record(s0)
+        # S4 + S5 on the genome (bwa mem -M defaults), S6 tails (BLAT -minScore=20)
+        self.ref.place_device(self.q, self.n_q, self.L, self.q_hits, self.q_nh, lens_t=self.q_lens,
+                              params=self.p_genome, max_hits=MAX_HITS, stream=s0)
+        self.ref.place_device(self.tails["tails"], self.tails["n"], self.L, self.t_hits, self.t_nh,
+                              lens_t=self.tails["lens"], params=self.p_tail, max_hits=MAX_HITS, stream=s0)
+        if _DEBUG:
+            s0.synchronize()
+            _log("placements done")
+        if phase_events:
+            phase_events[3].record(s0)
+        self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s4_pairs=npair)
+        return s0
+
+    def summary(self):
+        """Host-side counts of the last pass (synchronises)."""
+        import torch
+        torch.cuda.synchronize(self.dev)
+        nq = int(self.n_q.item())
+        nt = int(self.tails["n"].item())
+        qn = self.q_nh[:min(nq, self.qcap)].cpu().numpy()
+        tn = self.t_nh[:min(nt, self.tcap)].cpu().numpy()
+        c = dict(self.counts or {})
+        c.update(queries_s4_s5=nq, s5_split_reads=nq - 2 * c.get("s4_pairs", 0), queries_placed=int((qn > 0).sum()),
+                 tails=nt, tails_placed=int((tn > 0).sum()),
+                 mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()))
+        return c
+
+    def tail_best_hits(self):
+        """(read rows, best hit per tail) of the last pass, on the host."""
+        nt = min(int(self.tails["n"].item()), self.tcap)
+        hits = self.t_hits[:nt * MAX_HITS * _place.HIT_DTYPE.itemsize].cpu().numpy().view(_place.HIT_DTYPE)
+        return (self.tails["read"][:nt].cpu().numpy(), self.t_nh[:nt].cpu().numpy(),
+                hits.reshape(nt, MAX_HITS)[:, 0] if nt else hits)
+
+    def pack(self):
+        """The breakpoint candidates of the last pass as int32 rows [k, EX_WORDS] on the device:
+        every S4 / S5 query and every S6 tail -- the read's global row (2 words), kind (0 query,
+        1 tail), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the hit count and its first
+        EX_HITS hits.  These are the only records the stages after S6 read (SURVEY §8 e)."""
+        import torch
+        torch.cuda.synchronize(self.dev)
+        nq = min(int(self.n_q.item()), self.qcap)
+        nt = min(int(self.tails["n"].item()), self.tcap)
+        parts = []
+        for kind, n, rows, nh, hits in ((0, nq, self.q_rows, self.q_nh, self.q_hits),
+                                        (1, nt, self.tails["read"], self.t_nh, self.t_hits)):
+            if n == 0:
+                continue
+            r = rows[:n].long()
+            p = torch.empty((n, EX_WORDS), dtype=torch.int32, device=self.dev)
+            g = r + 2 * self.pair_base
+            p[:, 0] = (g & 0xFFFFFFFF).to(torch.int32)
+            p[:, 1] = (g >> 32).to(torch.int32)
+            p[:, 2] = kind
+            p[:, 3] = self.out["flag"][r]
+            p[:, 4] = self.out["pos"][r]
+            p[:, 5] = self.out["n_cigar"][r]
+            p[:, 6:38] = self.out["cigar"][r]
+            p[:, 38] = nh[:n]
+            h = hits[:n * MAX_HITS * HIT_WORDS * 4].view(torch.int32).view(n, MAX_HITS, HIT_WORDS)
+            p[:, 39:] = h[:, :EX_HITS].reshape(n, EX_HITS * HIT_WORDS)
+            parts.append(p)
+        if not parts:
+            return torch.zeros((0, EX_WORDS), dtype=torch.int32, device=self.dev)
+        return torch.cat(parts) if len(parts) > 1 else parts[0]
+
+    def exchange(self, group=None):
+        """All-gatherv of pack() across the ranks (counts all-gather, then one max-padded
+        all_gather: RCCL has no v-variant).  Returns the gathered rows on the device, rank order."""
+        import torch
+        import torch.distributed as dist
+        rows = self.pack()
+        world = dist.get_world_size(group)
+        cdev = self.dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=cdev)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt, group=group)
+        counts = [int(c.item()) for c in cnts]
+        mx = max(counts)
+        if mx == 0:
+            return rows
+        pad = torch.zeros((mx, EX_WORDS), dtype=torch.int32, device=cdev)
+        pad[:rows.shape[0]] = rows.to(cdev)
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)]).to(self.dev)
+

@@ -122,6 +122,29 @@ class Reference:
         _lib.check(self.ctx, build(self.ctx, blob, len(blob), ctypes.byref(self.idx)),
                    "af_index_build_genome" if self.kind == "genome" else "af_index_build")
 
+    @classmethod
+    def from_device(cls, blob_t, names, lens, offsets, device=0, ctx=None):
+        """A genome already joined in HBM (torch uint8 tensor laid out as concat_contigs does: contigs
+        at `offsets`, SEP N's between them) indexed by af_index_build_genome_device."""
+        self = cls.__new__(cls)
+        self.names, self.lens, self.offsets = list(names), [int(v) for v in lens], [int(v) for v in offsets]
+        self.total = int(blob_t.numel())
+        if self.total < 1 or not blob_t.is_cuda or not blob_t.is_contiguous():
+            raise ValueError("blob_t must be a non-empty contiguous device tensor")
+        if self.offsets[-1] + self.lens[-1] > self.total:
+            raise ValueError("contigs extend past the blob")
+        L = _lib.lib()
+        self._own_ctx = ctx is None
+        if ctx is None:
+            ctx = ctypes.c_void_p()
+            _lib.check(None, L.af_ctx_create(int(device), ctypes.byref(ctx)), "af_ctx_create")
+        self.ctx = ctx
+        self.idx = ctypes.c_void_p()
+        self.kind = "genome"
+        _lib.check(self.ctx, L.af_index_build_genome_device(self.ctx, blob_t.data_ptr(), self.total,
+                                                             ctypes.byref(self.idx)), "af_index_build_genome_device")
+        return self
+
     def close(self):
         L = _lib.lib()
         if getattr(self, "idx", None):

@@ -22,9 +22,16 @@ CHUNK_BASES = 10_000_000   # bwa mem's batch size (-K default) the shard boundar
 ROW_WORDS = 2 + 2 * (5 + 32)
 
 
+def chunk_pairs(read_len, chunk_bases=CHUNK_BASES):
+    """Pairs per bwa input chunk when every read is read_len long."""
+    return max(1, -(-chunk_bases // (2 * max(1, read_len))))
+
+
 def shard_range(n_pairs, rank, world, read_len=100):
-    """[lo, hi) of pairs for `rank`: contiguous, boundaries on the 10 Mbase chunk grid."""
-    chunk = max(1, CHUNK_BASES // (2 * max(1, read_len)))
+    """[lo, hi) of pairs for `rank`: contiguous, boundaries on the 10 Mbase chunk grid (bwa's
+    bseq_read ends a chunk with the pair that brings it to >= CHUNK_BASES bases, so a chunk of
+    uniform 2 x read_len pairs holds ceil(CHUNK_BASES / (2 read_len)) of them)."""
+    chunk = chunk_pairs(read_len)
     n_chunks = (n_pairs + chunk - 1) // chunk
     per = [n_chunks // world + (1 if r < n_chunks % world else 0) for r in range(world)]
     lo = sum(per[:rank]) * chunk

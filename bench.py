@@ -1,25 +1,29 @@
 #!/usr/bin/env python3
-"""Benchmark of the anchored split-read alignment hot path (BASELINE.json metric:
-paired reads/sec through anchored split-read align on 1/2/4/8 MI355X).
+"""Benchmark of the anchored split-read alignment hot path (BASELINE.json metric: paired reads/sec
+through anchored split-read align on 1/2/4/8 MI355X).
 
-Workload (BASELINE.json configs[1]): 1 M synthetic 2x100 bp pairs per GPU against one
-anchor transcript (the bundled BCR NM_004327.4, 6,783 nt), 5 % of pairs from anchor
-fusions, the rest from a random background transcriptome (wgsim-style simulator, seeded).
-A step = one pass of the GPU path over the resident batch: seed filter (K1), candidate
-seed/extend/CIGAR (K2) and pair flags (K3), i.e. the records `bwa mem -M` hands to samtools
-at Anchored_Fusion.py:182, then the partner placement of the split reads' soft-clipped tails
-(af_split_tails_device + af_place_device, the BLAT search of functions.py:530) on the
-workload's transcripts (SURVEY §8 d: S2 + partner placement; --no-placement drops it, and
-`s2_only` reports the same steps without it).  Inputs are resident in HBM before timing starts.  Steps run
---inflight (default 8) batches at a time through align.AlignerGroup, as a streaming deployment
-keeps several batches in flight: a group's K1 launches run back to back, then its K2+K3
-launches run concurrently on one stream per batch so that each K2's tail overlaps the next
-K2's body; each batch is still the full 1 M-pair batch with all its kernels inside the timed
-region (--inflight 1 = one batch at a time, strictly serial).
+Default workload (--config c3, BASELINE.json configs[2]; configs[3] at N > 1): 50 M distinct
+synthetic 2x150 bp pairs against one anchor transcript (the bundled BCR NM_004327.4) with an
+hg38-scale genome index resident in HBM.  The world is made on the device by libafsim.so
+(simworld.py): 3.09 Gbp in hg38's 24 contig sizes with repeat families, satellites and segmental
+duplications, the anchor and 8 partner genes embedded as exons; 5 % of the pairs come from the
+anchor fusions, the rest from the genome (wgsim's read model, seeded per pair).  A step is one
+pass of discover.CandidateDiscovery over the resident pairs:
+  S2  K1 + K2 + K3 per batch of 30 bwa chunks (`bwa mem -M anchor fq1 fq2`, Anchored_Fusion.py:182),
+      8 batches in flight, the split-read tails cut in K3;
+  S3  the samtools coordinate sort and the -f 8 / -f 4 / -F 772 partitions (AF:182, 186-194);
+  S4  the one-end-anchored pairs (tmp1 / tmp2) and S5 the anchored split reads placed on the genome
+      (`bwa mem -M genome`, AF:188 and functions.py:716);
+  S6  the split reads' tails placed on the genome (BLAT -minScore=20, functions.py:530);
+  and at N > 1 the all-gatherv of the breakpoint candidates (RCCL).
+Inputs are resident in HBM before timing starts.  At N > 1 the 50 M pairs are sharded on bwa's
+10 Mbase chunk grid (strong scaling, configs[3]).
+
+--config c2 is configs[1]: 1 M synthetic 2x100 pairs per GPU, the step S2 + split-tail placement on
+the workload's transcripts, 8 batches in flight (round-1 headline; weak scaling).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver uses
-torch.distributed.run; each rank aligns its own shard (no data-path collective: pairs are
-independent), and the time is the max over ranks.
+torch.distributed.run, one rank per GPU.  The time is the max over ranks.
 """
 import argparse
 import json
@@ -36,32 +40,46 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pairs", type=int, default=1_000_000, help="pairs per GPU")
-    ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--config", choices=("c3", "c2"), default="c3")
+    ap.add_argument("--steps", type=int, default=None, help="default 12 (c3) / 20 (c2)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 2 (c3) / 3 (c2)")
+    ap.add_argument("--pairs", type=int, default=None, help="c3: total pairs (50 M); c2: pairs per GPU (1 M)")
+    ap.add_argument("--read-len", type=int, default=None, help="default 150 (c3) / 100 (c2)")
+    ap.add_argument("--genome-scale", type=float, default=1.0, help="c3: genome size as a fraction of hg38")
+    ap.add_argument("--batch-chunks", type=int, default=30, help="c3: bwa chunks per S2 batch")
     ap.add_argument("--fusion-frac", type=float, default=0.05)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="pairs timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much wall time")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host CPU share (OMP_NUM_THREADS, else all cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-placement", action="store_true", help="skip the S2 + partner placement leg")
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: no timing events in the timed region")
     ap.add_argument("--inflight", type=int, default=8,
                     help="batches in flight (AlignerGroup): their K1s back to back, then their K2s at once")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c3 = a.config == "c3"
+    a.steps = a.steps if a.steps is not None else (12 if c3 else 20)
+    a.warmup = a.warmup if a.warmup is not None else (2 if c3 else 3)
+    a.pairs = a.pairs if a.pairs is not None else (50_000_000 if c3 else 1_000_000)
+    a.read_len = a.read_len if a.read_len is not None else (150 if c3 else 100)
+    return a
+
+
+def cpu_threads(args):
+    """The host CPU share: OMP_NUM_THREADS (16 per GPU on the box, where os.cpu_count() shows the
+    whole machine), else every core."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() and int(env) > 0 else (os.cpu_count() or 1)
 
 
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
     import afpkg  # noqa: F401
-    from anchored_fusion_amd import io as afio
-    from anchored_fusion_amd import simulate as sim
-    from anchored_fusion_amd.align import AlignerGroup
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -77,7 +95,33 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    ctx = dict(world=world, rank=rank, gpu=gpu, dev=dev, backend=backend)
+    if args.config == "c3":
+        bench_c3(args, **ctx)
+    else:
+        bench_c2(args, **ctx)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def max_over_ranks(t, world, dev, backend):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return t
+    tt = torch.tensor([t], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def bench_c2(args, world, rank, gpu, dev, backend):
+    """configs[1]: S2 + split-tail placement on 1 M 2x100 pairs per GPU (weak scaling)."""
+    import torch
+    import torch.distributed as dist
+
+    from anchored_fusion_amd import io as afio
+    from anchored_fusion_amd import simulate as sim
+    from anchored_fusion_amd.align import AlignerGroup
     anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
     L = args.read_len
     _, reads, _, fworld = sim.fusion_reads(anchor, args.pairs, read_len=L, fusion_frac=args.fusion_frac,
@@ -170,7 +214,7 @@ def main():
         "dtype": "int32",
         "data": "synthetic (wgsim-style simulator, seed 20251015 + rank)",
         "config": {
-            "workload": f"configs[1]: {args.pairs} synthetic 2x{L} bp pairs per GPU, one anchor "
+            "workload": f"configs[1] (--config c2): {args.pairs} synthetic 2x{L} bp pairs per GPU, one anchor "
                         f"(BCR NM_004327.4, {len(anchor)} nt), {args.fusion_frac:.0%} fusion pairs"
                         + ("" if args.no_placement else "; S2 + partner placement of the split-read tails"),
             "pairs_per_gpu": args.pairs, "read_len": L, "anchor_len": len(anchor),
@@ -217,8 +261,162 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     grp.close()
+
+
+def bench_c3(args, world, rank, gpu, dev, backend):
+    """configs[2] (N = 1) / configs[3] (N > 1): S2 + S3 + the S4/S5/S6 genome searches over 50 M
+    2x150 pairs with an hg38-scale genome index resident (strong scaling across ranks)."""
+    import torch
+    import torch.distributed as dist
+
+    from anchored_fusion_amd import discover, simworld
+    from anchored_fusion_amd import io as afio
+    from anchored_fusion_amd.shard import shard_range
+    anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
+    L, N = args.read_len, args.pairs
+
+    def log(msg):
+        if rank == 0:
+            print(f"[bench c3] {msg}", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
+    W = simworld.GenomeWorld(anchor, device=gpu, seed=20251015, scale=args.genome_scale)
+    t_gen = time.perf_counter() - t0
+    log(f"genome {W.total / 1e9:.2f} Gbp made in {t_gen:.1f} s")
+    t0 = time.perf_counter()
+    ref = W.reference()
+    t_idx = time.perf_counter() - t0
+    log(f"genome index built in {t_idx:.1f} s")
+    lo, hi = shard_range(N, rank, world, L)
+    n = hi - lo
+    reads_t = torch.empty((2 * max(n, 1), L), dtype=torch.uint8, device=dev)
+    if n:
+        W.simulate_pairs(n, read_len=L, seed=20251015, pair_base=lo, out=reads_t[:2 * n])
+    torch.cuda.synchronize(dev)
+    log(f"{n} pairs simulated")
+    W.blob = None  # the index keeps its own copy
+    torch.cuda.empty_cache()
+    disc = discover.CandidateDiscovery(anchor, ref, n, L, device=gpu, inflight=max(1, args.inflight),
+                                       batch_chunks=args.batch_chunks, pair_base=lo)
+    G = disc.grp.inflight
+    n_groups = (len(disc.batches) + G - 1) // G
+
+    def step(k1=None, ph=None):
+        disc.run(reads_t, k1_events=k1, phase_events=ph)
+        if world > 1:
+            disc.exchange()
+
+    for w in range(args.warmup):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        log(f"warm-up pass {w}: {time.perf_counter() - t0:.3f} s, {disc.summary()}")
+    free, total = torch.cuda.mem_get_info(dev)
+    E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    k1 = [[[E(), E()] for _ in range(n_groups)] for _ in range(args.steps)]
+    ph = [[E() for _ in range(5)] for _ in range(args.steps)]
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        s0 = disc.grp.streams[0]
+        ph[k][0].record(s0)
+        step(None if args.no_kernel_events else k1[k], ph[k][1:])
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev, backend)
+    ms = elapsed / args.steps * 1e3
+    summ = disc.summary()
+    n_launch = len(disc.batches)
+    k1_ms = float("nan") if args.no_kernel_events else \
+        sum(e[0].elapsed_time(e[1]) for st in k1 for e in st) / args.steps
+    phase = lambda a, b: sum(p[a].elapsed_time(p[b]) for p in ph) / args.steps  # noqa: E731
+    bp = max(b for _, b in disc.batches) if disc.batches else 0
+    bytes_per_launch = bp * (2 * L + 8)  # SURVEY §8 d: 2L bases + 2 x int32 per pair, one batch per K1 launch
+    k1_launch_ms = k1_ms / max(1, n_launch)
+    achieved = bytes_per_launch / (k1_launch_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_seed_filter.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("pairs") == bp and pm.get("read_len") == L:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    res = {
+        "metric": "paired reads/sec through anchored split-read align",
+        "value": round(N / elapsed * args.steps, 1),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic, made on the device (simworld.py / libafsim.so, seed 20251015): hg38-sized genome with "
+                "repeat families, 5% anchor-fusion pairs, wgsim read model, every pair distinct",
+        "config": {
+            "workload": f"configs[{2 if world == 1 else 3}]: {N} synthetic 2x{L} bp pairs"
+                        + (f" sharded over {world} GPUs" if world > 1 else "")
+                        + f", genome index {ref.total / 1e9:.2f} Gbp HBM-resident, one anchor (BCR NM_004327.4); "
+                          "step = S2 + S3 sort/partition + S4/S5 genome placement + S6 tail placement"
+                        + (" + all-gatherv of candidates" if world > 1 else ""),
+            "pairs_total": N, "pairs_per_gpu": n, "read_len": L, "genome_bp": ref.total, "anchor_len": len(anchor),
+            "parallelism": f"dp{world}", "batches": n_launch, "pairs_per_batch": bp, "inflight": G,
+        },
+        "counts_per_step": summ,
+        "phases_ms": {"s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
+                      "gather_queries": round(phase(2, 3), 3), "genome_placement": round(phase(3, 4), 3),
+                      "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3"},
+        "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
+        "roofline": {
+            "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch,
+            "note": "HIP events around each group's back-to-back K1 launches (distinct read ranges, no reuse)",
+        },
+        "setup_s": {"genome": round(t_gen, 2), "index": round(t_idx, 2)},
+        "hbm_in_use_gib": round((total - free) / 2**30, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_c3(anchor, reads_t, args)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    disc.close()
+    ref.close()
+
+
+def cpu_baseline_c3(anchor, reads_t, args):
+    """The CPU oracle on a bounded sample of the same pairs: S2 (oracle/bwa_pe.c, bwa-mem PE
+    restated) + S3 (samtools order and filters), repeated for --cpu-seconds.  The genome searches
+    are not in this leg: an oracle index of the 3.1 Gbp genome takes longer to build than the whole
+    bench runs."""
+    import numpy as np
+
+    import oracle
+    from anchored_fusion_amd.align import AlignResult, partition
+    threads = cpu_threads(args)
+    n = min(args.cpu_sample, reads_t.shape[0] // 2)
+    sample = reads_t[: 2 * n].cpu().numpy()
+    ix = oracle.OracleIndex(anchor)
+    ix.align_pairs(sample[: 2 * min(n, 20000)], threads=threads)  # warm-up
+    passes, dt = 0, 0.0
+    while passes == 0 or dt < args.cpu_seconds:
+        t0 = time.perf_counter()
+        rec = ix.align_pairs(sample, threads=threads)
+        partition(AlignResult(rec["flag"], rec["pos"], rec["score"], rec["n_cigar"], rec["cigar"], rec["hits"]))
+        dt += time.perf_counter() - t0
+        passes += 1
+    return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": os.cpu_count(),
+            "sample": f"first {n} pairs of the batch x {passes} passes ({dt:.1f} s): S2 + S3 on oracle/bwa_pe.c "
+                      f"(C restatement of bwa-mem PE; bwa, BLAT and samtools are absent), OpenMP {threads} threads "
+                      "(the GPU's host CPU share); genome searches not included"}
 
 
 class Placement:
@@ -332,7 +530,7 @@ def cpu_baseline(anchor, reads, args, fworld=None):
 
     import oracle
     from anchored_fusion_amd import place
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = cpu_threads(args)
     n = min(args.cpu_sample, reads.shape[0] // 2)
     sample = reads[: 2 * n]
     ix = oracle.OracleIndex(anchor)

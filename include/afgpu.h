@@ -21,6 +21,8 @@
  *   af_align_candidates_tails_device <- af_align_candidates_device + the same tails, fused
  *   af_partition_device   <- `| samtools sort` of the same call and the three
  *                            `samtools view -f/-F` filters of Anchored_Fusion.py:186-194
+ *   af_gather_reads_device <- `samtools fastq` of the S3 partitions (AF:186-188) and the split-read
+ *                            FASTA of functions.py:705-716: the genome searches' queries
  *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
@@ -153,6 +155,9 @@ int64_t af_last_candidates(af_ctx *ctx);
  * 16-mers, 16 GiB, plus 4 B per forward position and 2.6 B per base of sequence).  References of
  * up to 2^32 - 2 bases (contigs joined by N runs); af_align_* reject it. */
 int af_index_build_genome(af_ctx *ctx, const char *seq, int64_t len, af_index **out);
+/* af_index_build_genome from a device-resident sequence (d_seq: `len` bytes of ASCII in HBM, e.g.
+ * a genome generated or decompressed on the device); synchronous. */
+int af_index_build_genome_device(af_ctx *ctx, const char *d_seq, int64_t len, af_index **out);
 
 /* Multi-hit placement of queries (ASCII, `stride` bytes per row, optional lens) on an index
  * built with af_index_build over any reference (anchor, candidate blocks, or contigs joined by
@@ -203,6 +208,25 @@ int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, 
  * Enqueued on `stream`; synchronizes it once (the selected count sizes the sort). */
 int af_partition_device(af_ctx *ctx, const int32_t *d_flag, const int32_t *d_pos, int64_t n_reads, int64_t ref_len,
                         int32_t *d_tmp1, int32_t *d_tmp2, int32_t *d_anchored, int64_t *d_counts, void *stream);
+
+/* The genome searches' queries from S3's row lists (af_partition_device), on the device:
+ *   AF_GATHER_SEQUENCED  every listed read as sequenced -- `samtools fastq` of tmp1 / tmp2 for the
+ *                        paired genome search (Anchored_Fusion.py:186-188); call once per list with
+ *                        first = 0 / 1 and step = 2 to interleave them as bwa pairs its two files;
+ *   AF_GATHER_SPLIT_SAM  the listed mapped reads whose CIGAR deal_cigar reduces to two operations
+ *                        (one soft clip + the aligned part), SEQ as SAM prints it (reverse complement
+ *                        for 0x10): the split-read FASTA of functions.py:705-716; list order kept.
+ * Query k goes to slot first + k * step of d_q (`stride` bytes per row, N-padded), d_q_lens and
+ * d_q_rows (the read row; may be NULL); slots at or past cap are dropped.  *d_n_q (may be NULL) =
+ * min(cap, last slot written + 1, or `first` when no row is written): the query count
+ * af_place_device reads when the calls fill slots 0.. in order.  d_out supplies FLAG and
+ * CIGAR (AF_GATHER_SPLIT_SAM only).  Asynchronous on `stream`. */
+#define AF_GATHER_SEQUENCED 0
+#define AF_GATHER_SPLIT_SAM 1
+int af_gather_reads_device(af_ctx *ctx, const uint8_t *d_reads, int32_t stride, const int32_t *d_lens,
+                           const int32_t *d_rows, int64_t n_rows, int32_t mode, const af_aln_out *d_out,
+                           int64_t first, int64_t step, int64_t cap, uint8_t *d_q, int32_t *d_q_lens,
+                           int32_t *d_q_rows, int32_t *d_n_q, void *stream);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as

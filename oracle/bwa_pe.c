@@ -214,7 +214,7 @@ uint64_t *afo_text_kmers_noncrossing(const afo_text *X, int64_t *m) {
                     s = t - i > 16 ? i + 1 : t;                                                    \
                 } else {                                                                           \
                     if (t - i > 16) { top->left = i + 1; top->right = t; top->depth = d; ++top; }  \
-                    s = i - s > 16 ? s : i - 1;                                                    \
+                    t = i - s > 16 ? i - 1 : s;                                                    \
                 }                                                                                  \
             } else {                                                                               \
                 if (top == stack) { ins_##name(a, a + n); return; }                                \
