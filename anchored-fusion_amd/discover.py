@@ -49,7 +49,12 @@ class CandidateDiscovery:
         pc = chunk_pairs(self.L, chunk_bases)
         if self.pair_base % pc:
             raise ValueError("pair_base must be on bwa's chunk grid")
-        bp = pc * max(1, int(batch_chunks))
+        # batches start on 16-byte boundaries of reads_t (the seed filter's vector loads): a whole
+        # number of chunks whose bytes are a multiple of 16
+        m = 1
+        while (m * pc * 2 * self.L) % 16:
+            m += 1
+        bp = pc * m * max(1, -(-int(batch_chunks) // m))
         self.batches = [(p, min(bp, self.n_pairs - p)) for p in range(0, self.n_pairs, bp)]
         self.grp = AlignerGroup(self.anchor, device=device, inflight=inflight)
         for a in self.grp.aligners:
@@ -158,7 +163,9 @@ class CandidateDiscovery:
         return c
 
     def tail_best_hits(self):
-        """(read rows, best hit per tail) of the last pass, on the host."""
+        """(read rows, hit counts, best hit per tail) of the last pass, on the host (synchronises)."""
+        import torch
+        torch.cuda.synchronize(self.dev)
         nt = min(int(self.tails["n"].item()), self.tcap)
         hits = self.t_hits[:nt * MAX_HITS * _place.HIT_DTYPE.itemsize].cpu().numpy().view(_place.HIT_DTYPE)
         return (self.tails["read"][:nt].cpu().numpy(), self.t_nh[:nt].cpu().numpy(),

@@ -101,7 +101,7 @@ SAT_LEN = 171
 def repeat_library(seed=20251015):
     """Consensus sequences (codes 0-3): per family `n_sub` subfamilies diverged 6 % apart from a
     random root, then the satellite monomer.  Returns (codes uint8, [Family], sat_off)."""
-    rng = np.random.default_rng(seed)
+    rng = np.random.default_rng([seed, 1])  # its own stream: the genes must not copy the consensi
     parts, fams, off = [], [], 0
     for name, clen, nsub, (lo, hi), (dlo, dhi), step, prob, kind in FAMILIES:
         root = rng.integers(0, 4, clen, dtype=np.uint8)
@@ -148,7 +148,7 @@ class GenomeWorld:
         from . import place
         self.device = device
         dev = torch.device("cuda", device)
-        rng = np.random.default_rng(seed)
+        rng = np.random.default_rng([seed, 2])
         self.contigs = [(n, max(1 << 20, int(L * scale))) for n, L in HG38]
         self.names = [n for n, _ in self.contigs]
         self.lens = [L for _, L in self.contigs]

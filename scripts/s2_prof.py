@@ -23,10 +23,16 @@ from anchored_fusion_amd.align import AnchorAligner  # noqa: E402
 n = int(os.environ.get("PAIRS", "1000000"))
 L = int(os.environ.get("READ_LEN", "100"))
 anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
-_, reads, _, _ = sim.fusion_reads(anchor, n, read_len=L, fusion_frac=0.05, seed=20251015)
 dev = torch.device("cuda:0")
-rt = torch.from_numpy(reads).to(dev)
-nr = reads.shape[0]
+if os.environ.get("WORLD") == "c3":  # the configs[2] world (simworld): reads from the genome + fusions
+    from anchored_fusion_amd import simworld
+    W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=1.0)
+    rt = W.simulate_pairs(n, read_len=L, seed=20251015)
+    del W
+else:
+    _, reads, _, _ = sim.fusion_reads(anchor, n, read_len=L, fusion_frac=0.05, seed=20251015)
+    rt = torch.from_numpy(reads).to(dev)
+nr = rt.shape[0]
 out = {k: torch.zeros(nr, dtype=torch.int32, device=dev) for k in ("flag", "pos", "score", "n_cigar", "hits")}
 out["cigar"] = torch.zeros((nr, 32), dtype=torch.int32, device=dev)
 lib = _lib.lib()

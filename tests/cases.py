@@ -108,3 +108,32 @@ def repeat_anchor_pairs(anchor: bytes, read_len=100, n=12, seed=9):
         b = 4000 + int(rng.integers(0, 1000))
         seqs += [anchor[a:a + read_len], rc(anchor[b:b + read_len])]
     return anc2, _pad(seqs, read_len)[0]
+
+
+# A pair from the configs[2] world whose mate 1 opens with 41 bases of (CGC)n against the anchor's
+# CGCCGCCGCCGCCGCCGC (BCR 5' UTR): nine regions on the same repeat, three left after dedup with
+# equal scores -- the input that exposed the introsort else-branch and the unbounded partition scan
+# (K2 hung on it).
+TANDEM_PAIR = (
+    b"CGCCGCCGCCGCCGCCGCCGCCGCCGCCGCCGCCGCCGCCGGATCGTAAATAACAATTTAATATATTTCCGTTTAACCCACGCAGGAAATCGGGCATACTA"
+    b"TTGAAAAGCTGTAATGCGCCATAGGATGGCTATCTCTCAAGAATCGACG",
+    b"GAATGCAGGTGGGCTCTTGGGTGGGAAGTTTGCAAAAGTTTACTTAATTTGGAACAATGCATCCGTCGATTCTTGAGAGATAGCCCGCCTATAGCGCGCTAC"
+    b"AGCTTTGCAATAGTATGCCCAATTTCCTGCGTGGGTTAAACGGAAATA",
+)
+
+
+def tandem_pairs(anchor: bytes, n_extra=40, seed=11):
+    """TANDEM_PAIR, then (CGC)n / (GCC)n reads of several phases and lengths around the anchor's
+    repeat, paired with random mates, after some ordinary pairs."""
+    rng = np.random.default_rng(seed)
+    reads, _, _ = synthetic_pairs(anchor, n_extra, 150, seed=seed)
+    rows = [r.tobytes() for r in reads]
+    rows += list(TANDEM_PAIR)
+    tail = TANDEM_PAIR[0][41:]
+    for ph in range(3):
+        for k in (14, 20, 30, 45):
+            rep = (b"CGC" * 40)[ph:ph + 3 * k][:3 * k]
+            r1 = (rep + tail)[:150]
+            r2 = sim.random_seq(rng, 150)
+            rows += [r1.ljust(150, b"N"), r2]
+    return np.frombuffer(b"".join(rows), np.uint8).reshape(-1, 150).copy()

@@ -94,6 +94,14 @@ def test_chunked_insert_stats_parity(anchor, oidx, chunk_pairs):
         assert_records_equal(g, r, rr)
 
 
+def test_tandem_repeat_parity(aligner, oidx, anchor):
+    """Reads of a tandem repeat that occurs in the anchor: many equal-scoring regions."""
+    from cases import tandem_pairs
+    reads = tandem_pairs(anchor)
+    g, r = _both(aligner, oidx, reads)
+    assert_records_equal(g, r, reads)
+
+
 def test_edge_parity(aligner, oidx, anchor):
     reads, lens = edge_pairs(anchor)
     g, r = _both(aligner, oidx, reads, lens)

@@ -1,0 +1,147 @@
+"""configs[2] on the GPU: the device-made hg38-scale world (simworld) and the device pipeline
+(discover.CandidateDiscovery: S2 + S3 + the S4/S5/S6 genome searches).
+
+At full size (50 M pairs, 3.09 Gbp) the results are checked through properties; the first
+bwa chunks of the same pairs are checked bit-exactly against the CPU oracle (the GPU aligned them
+in the same place of the same input stream, so read ids and insert-size chunks agree)."""
+import numpy as np
+import pytest
+
+import oracle
+from helpers import assert_records_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _world(anchor, scale):
+    from anchored_fusion_amd import simworld
+    return simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=scale)
+
+
+def test_world_is_deterministic_and_distinct(anchor):
+    import torch
+    W1, W2 = _world(anchor, 0.01), _world(anchor, 0.01)
+    assert torch.equal(W1.blob, W2.blob)
+    a = W1.simulate_pairs(20000, read_len=150, seed=3)
+    b = W2.simulate_pairs(20000, read_len=150, seed=3)
+    assert torch.equal(a, b)
+    c = W1.simulate_pairs(20000, read_len=150, seed=3, pair_base=20000)
+    assert not torch.equal(a, c)
+    g = W1.blob.cpu().numpy()
+    vals = set(np.unique(g).tolist())
+    assert vals <= set(b"ACGTN")
+    # the embedded genes are in the genome as exons
+    for name, spans in W1.loci.items():
+        seq = W1.anchor if name == "anchor" else W1.partners[int(name[7:])]
+        got = b"".join(bytes(g[W1.offsets[W1.names.index(c)] + s:W1.offsets[W1.names.index(c)] + e])
+                       for c, s, e in spans)
+        assert got == seq
+    # repeats: far more repeated 16-mers than a random sequence of the same size would hold
+    # (~1e6^2 / 2 / 4^16 ~ 0.01 % of the 16-mers of 1 Mb of random sequence repeat)
+    body = g[W1.offsets[0] + 20000:W1.offsets[0] + 1_020_000]
+    codes = np.searchsorted(np.frombuffer(b"ACGT", np.uint8), body).clip(0, 3).astype(np.uint64)
+    k = np.zeros(len(codes) - 15, np.uint64)
+    for u in range(16):
+        k = (k << np.uint64(2)) | codes[u:u + len(k)]
+    _, cnt = np.unique(k, return_counts=True)
+    assert (cnt[cnt > 1].sum()) / len(k) > 0.02
+
+
+def test_discovery_matches_oracle_reduced(anchor):
+    """A reduced world end to end: records, S3 lists and the S4/S5 queries vs the host rules."""
+    import torch
+
+    from anchored_fusion_amd import discover
+    from anchored_fusion_amd.align import AlignResult, partition
+    W = _world(anchor, 0.02)
+    ref = W.reference()
+    n = 140_000
+    reads_t = W.simulate_pairs(n, read_len=150, seed=9)
+    d = discover.CandidateDiscovery(anchor, ref, n, 150, device=0, inflight=3, batch_chunks=1)
+    d.run(reads_t)
+    torch.cuda.synchronize()
+    reads = reads_t.cpu().numpy()
+    got = {k: v.cpu().numpy() for k, v in d.out.items()}
+    got["cigar"] = got["cigar"].view(np.uint32)
+    ref_rec = oracle.OracleIndex(anchor).align_pairs(reads, threads=8)
+    assert_records_equal(got, ref_rec, reads)
+    res = AlignResult(got["flag"], got["pos"], got["score"], got["n_cigar"], got["cigar"], got["hits"])
+    t1, t2, an = partition(res)
+    c = d.counts
+    assert (c["tmp1"], c["tmp2"], c["anchored"]) == (len(t1), len(t2), len(an))
+    assert np.array_equal(d.s3[0][:len(t1)].cpu().numpy(), t1)
+    assert np.array_equal(d.s3[2][:len(an)].cpu().numpy(), an)
+    # S4 queries interleave tmp1 / tmp2 as sequenced; S5 = anchored split reads as SAM prints them
+    from anchored_fusion_amd.cigar import normalize
+    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+    want = []
+    for a, b in zip(t1, t2):
+        want += [(int(a), reads[a].tobytes()), (int(b), reads[b].tobytes())]
+    for r in an:
+        cig = res.cigar_str(r)
+        s = reads[r].tobytes()
+        if len(normalize(cig, s.decode())[0]) == 2:
+            want.append((int(r), s[::-1].translate(comp) if got["flag"][r] & 0x10 else s))
+    nq = int(d.n_q.item())
+    assert nq == len(want)
+    q = d.q[:nq].cpu().numpy()
+    rows = d.q_rows[:nq].cpu().numpy()
+    for k, (r, s) in enumerate(want):
+        assert rows[k] == r and q[k].tobytes() == s
+    summ = d.summary()
+    assert summ["tails"] > 0 and summ["tails_placed"] > 0.8 * summ["tails"]
+    d.close()
+    ref.close()
+
+
+def test_c3_full_size(anchor):
+    """configs[2] at full size: 50 M pairs on the 3.09 Gbp world.  Properties: every read with an
+    exact 19-mer of the anchor (either strand) passes the seed filter; the placed split-read
+    tails' best hits lie in the embedded genes; the first two bwa chunks are bit-exact vs the
+    oracle."""
+    import torch
+
+    from anchored_fusion_amd import discover
+    from anchored_fusion_amd.shard import chunk_pairs
+    W = _world(anchor, 1.0)
+    ref = W.reference()
+    N, L = 50_000_000, 150
+    reads_t = W.simulate_pairs(N, read_len=L, seed=20251015)
+    torch.cuda.synchronize()
+    W.blob = None
+    d = discover.CandidateDiscovery(anchor, ref, N, L, device=0)
+    d.run(reads_t)
+    summ = d.summary()
+    assert summ["tmp1"] == summ["tmp2"] > 1000 and summ["anchored"] > 1_000_000
+    # oracle on the first two chunks (bwa's read ids and insert-size chunks are the same)
+    m = 2 * chunk_pairs(L)
+    sub = reads_t[:2 * m].cpu().numpy()
+    got = {k: v[:2 * m].cpu().numpy() for k, v in d.out.items()}
+    got["cigar"] = got["cigar"].view(np.uint32)
+    assert_records_equal(got, oracle.OracleIndex(anchor).align_pairs(sub, threads=8), sub)
+    # seed filter: no read holding an anchor 19-mer is dropped (sampled rows)
+    comp = bytes.maketrans(b"ACGT", b"TGCA")
+    an = anchor.upper()
+    kmers = {an[i:i + 19] for i in range(len(an) - 18)}
+    kmers |= {k[::-1].translate(comp) for k in kmers}
+    rng = np.random.default_rng(1)
+    rows = np.sort(rng.choice(2 * N, 40_000, replace=False))
+    hits = d.out["hits"].cpu().numpy()[rows]
+    sample = reads_t[torch.from_numpy(rows).cuda()].cpu().numpy()
+    for r, h in zip(sample, hits):
+        s = r.tobytes()
+        if h == 0:
+            assert not any(s[i:i + 19] in kmers for i in range(L - 18))
+    # tails: best hits inside the anchor or a partner gene locus (exons and introns: reads from
+    # the genome's copy of the anchor gene that cross an exon end leave intronic tails)
+    spans = [(W.names.index(v[0][0]), v[0][1] - 1000, v[-1][2] + 1000) for v in W.loci.values()]
+    _, nh, best = d.tail_best_hits()
+    placed = np.nonzero(nh > 0)[0]
+    inside = 0
+    for t in placed:
+        loc = ref.locate(best[t]["t_start"], best[t]["t_end"])
+        inside += loc is not None and any(k == loc[0] and s <= loc[1] < e for k, s, e in spans)
+    print(f"tails placed {len(placed)}, best hit in a gene locus {inside}")
+    assert len(placed) > 50_000 and inside >= 0.95 * len(placed)
+    d.close()
+    ref.close()

@@ -163,3 +163,11 @@ def test_chunks_change_insert_stats(anchor, oidx):
     big = oidx.align_pairs(reads)
     small = oidx.align_pairs(reads, chunk_bases=200 * 6)   # 6 pairs of 2x100 per chunk
     assert not big["flag"][2 * probe + 1] & 4 and small["flag"][2 * probe + 1] & 4
+
+
+def test_tandem_repeat_runs(anchor, oidx):
+    """The oracle aligns (CGC)n reads against the anchor's own CGC repeat (many equal regions)."""
+    from cases import tandem_pairs
+    reads = tandem_pairs(anchor)
+    out = oidx.align_pairs(reads, threads=4)
+    assert len(out["flag"]) == reads.shape[0]
