@@ -9,8 +9,8 @@ hg38-scale genome index resident in HBM.  The world is made on the device by lib
 duplications, the anchor and 8 partner genes embedded as exons; 5 % of the pairs come from the
 anchor fusions, the rest from the genome (wgsim's read model, seeded per pair).  A step is one
 pass of discover.CandidateDiscovery over the resident pairs:
-  S2  K1 + K2 + K3 per batch of 30 bwa chunks (`bwa mem -M anchor fq1 fq2`, Anchored_Fusion.py:182),
-      8 batches in flight, the split-read tails cut in K3;
+  S2  K1 + K2 + K3 per batch of 240 bwa chunks (8 M pairs; `bwa mem -M anchor fq1 fq2`,
+      Anchored_Fusion.py:182), 4 batches in flight, the split-read tails cut in K3;
   S3  the samtools coordinate sort and the -f 8 / -f 4 / -F 772 partitions (AF:182, 186-194);
   S4  the one-end-anchored pairs (tmp1 / tmp2) and S5 the anchored split reads placed on the genome
       (`bwa mem -M genome`, AF:188 and functions.py:716);
@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--pairs", type=int, default=None, help="c3: total pairs (50 M); c2: pairs per GPU (1 M)")
     ap.add_argument("--read-len", type=int, default=None, help="default 150 (c3) / 100 (c2)")
     ap.add_argument("--genome-scale", type=float, default=1.0, help="c3: genome size as a fraction of hg38")
-    ap.add_argument("--batch-chunks", type=int, default=30, help="c3: bwa chunks per S2 batch")
+    ap.add_argument("--batch-chunks", type=int, default=240,
+                    help="c3: bwa chunks per S2 batch (240 x 33,334 pairs = 8 M pairs; sweep in DESIGN.md)")
     ap.add_argument("--fusion-frac", type=float, default=0.05)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="pairs timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much wall time")
@@ -54,14 +55,16 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-placement", action="store_true", help="skip the S2 + partner placement leg")
     ap.add_argument("--no-kernel-events", action="store_true", help="diagnostic: no timing events in the timed region")
-    ap.add_argument("--inflight", type=int, default=8,
-                    help="batches in flight (AlignerGroup): their K1s back to back, then their K2s at once")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batches in flight (AlignerGroup): their K1s back to back, then their K2s at once "
+                         "(default 4 for c3, 8 for c2)")
     a = ap.parse_args()
     c3 = a.config == "c3"
     a.steps = a.steps if a.steps is not None else (12 if c3 else 20)
     a.warmup = a.warmup if a.warmup is not None else (2 if c3 else 3)
     a.pairs = a.pairs if a.pairs is not None else (50_000_000 if c3 else 1_000_000)
     a.read_len = a.read_len if a.read_len is not None else (150 if c3 else 100)
+    a.inflight = a.inflight if a.inflight is not None else (4 if c3 else 8)
     return a
 
 

@@ -65,3 +65,8 @@ print(f"    pairs with a rescue SW {resc.sum()} (window rows {k3[resc, 6].mean()
       f"their rescue cycles {k3[resc, 3].mean() if resc.any() else 0:.0f}, others {k3[~resc, 3].mean():.0f}")
 for q in (50, 90, 99):
     print(f"    p{q}: K2 total {np.percentile(k2[:, 1], q):.0f}, K3c total {np.percentile(k3[:, 1], q):.0f}")
+top = np.argsort(-k3[:, 1])[:12]
+print("K3c slowest pairs: pair, total, load, rescue, primary, records, rescue rows, regions m1/m2")
+for t in top:
+    print("   ", k3[t, [0, 1, 2, 3, 4, 5, 6, 7, 8]].tolist())
+print(f"K3c cycles: sum {k3[:, 1].sum():.3g}, of which rescue {k3[:, 3].sum():.3g}; max {k3[:, 1].max()}")
