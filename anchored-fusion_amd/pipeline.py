@@ -7,9 +7,9 @@ Anchored_Fusion.py:121-227 with its shell calls replaced).
 | AF:144-172 anchor FASTA + `bwa index` | `AnchorAligner(anchor)` (GPU index) |
 | AF:182 `bwa mem -M anchor fq1 fq2 \\| samtools sort` | `AnchorAligner.align_pairs` (K1+K2+K3) |
 | AF:186-194 samtools flag partitions | `align.partition` |
-| AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam` (af_place on the genome) |
+| AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam_pe` (af_place on the genome + bwa_records) |
 | AF:198 `Find_homo_genes` | `partner.homolog_genes` |
-| AF:204 `del_too_many_reads` | `genome_check` + `Searches.genome_sam` |
+| AF:204 `del_too_many_reads` | `genome_check` + `Searches.genome_sam_se` |
 | AF:205-206 `Find_blocks`, `Find_fine_block` | `blocks.spanning_blocks`, `blocks.add_fine_blocks` |
 | AF:207 `Build_candidate_fasta` | `partner.candidate_targets` |
 | AF:208 `contact_reads` | `splitreads.cluster_split_reads` |
@@ -64,22 +64,35 @@ def sam_line(name, flag, rname, pos1, cigar, seq):
 
 
 class Searches:
-    """The two search services the partner stages need, on the GPU by default.
+    """The search services the partner stages need, on the GPU by default.
 
     `place(targets, queries, preset)` -> PSL lines (partner.py callback);
-    `genome_sam(queries)` -> one list of SAM lines per query (primary first)."""
+    `genome_sam_se(queries)` -> per query the SAM lines of `bwa mem -M genome q.fa` (fn:716);
+    `genome_sam_pe(pairs)` -> the SAM lines of `bwa mem -M genome fq1 fq2` (AF:188).
+    Both render the genome placement's hits with bwa's record rules (bwa_records)."""
 
     def __init__(self, genome_contigs, device=0, placer=None):
-        from .place import Placer, sam_records
+        from . import bwa_records
+        from .place import Placer
         self.genome = genome_contigs
         self.place = placer or Placer(device=device)
 
-        def genome_sam(queries):
+        def _hits(seqs):
             ref = self.place.reference(self.genome)   # shared with the genome PSL searches
-            hits, nh = ref.raw_hits([s for _, s in queries], self.place.params("genome_bwa"), 16)
-            return [sam_records(ref, [q], hits[i:i + 1], nh[i:i + 1]) for i, q in enumerate(queries)]
+            p = self.place.params("genome_bwa")
+            hits, nh = ref.raw_hits(seqs, p, 16)
+            return ref, p, hits, nh
 
-        self.genome_sam = genome_sam
+        def genome_sam_se(queries):
+            ref, p, hits, nh = _hits([s for _, s in queries])
+            return [bwa_records.se_records(ref, n, s, hits[i], nh[i], i, p.T) for i, (n, s) in enumerate(queries)]
+
+        def genome_sam_pe(pairs):
+            ref, p, hits, nh = _hits([s for _, a, b in pairs for s in (a, b)])
+            return bwa_records.pe_records(ref, pairs, hits, nh, p.T, p.min_seed_len)
+
+        self.genome_sam_se = genome_sam_se
+        self.genome_sam_pe = genome_sam_pe
 
     def getfasta(self, rows):
         """bedtools getfasta -name: rows (chrom, start, end, name) -> [(name::chrom:start-end, seq)];
@@ -123,11 +136,10 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     tmp1, tmp2, anchored = partition(res)
     log(f"[{gene}] S2: {int(((flag & 4) == 0).sum())} of {len(flag)} reads on the anchor; "
         f"{len(tmp1)} one-end-anchored pairs; {len(anchored)} anchored records")
-    # S4: one-end-anchored pairs on the genome (samtools fastq restores the sequenced orientation)
-    q4 = []
-    for a, b in zip(tmp1, tmp2):
-        q4 += [(names[a // 2], seq(a)), (names[b // 2], seq(b))]
-    s4 = [ln for recs in (searches.genome_sam(q4) if q4 else []) for ln in recs]
+    # S4: one-end-anchored pairs on the genome, paired as bwa pairs tmp1.fq / tmp2.fq (samtools
+    # fastq restores the sequenced orientation of both ends)
+    q4 = [(names[a // 2], seq(a), seq(b)) for a, b in zip(tmp1, tmp2)]
+    s4 = searches.genome_sam_pe(q4) if q4 else []
     homo = [row[3] for row in homo_rows]
     # anchored.bam as `samtools view` prints it (SEQ reverse-complemented for 0x10)
     anch_lines = []
@@ -137,7 +149,7 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
         anch_lines.append(sam_line(names[r // 2], int(flag[r]) & 0xFFFF, gene, int(pos[r]) + 1, cig, sq))
     # S5: split reads vs the genome
     fasta = genome_check.split_read_fasta(anch_lines)
-    gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam(fasta) if fasta else []) for ln in recs]
+    gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam_se(fasta) if fasta else []) for ln in recs]
     split_sam = genome_check.filter_genome_hits(gsam)
     log(f"[{gene}] S5: {len(fasta)} split reads, {len(split_sam)} kept")
     blocks_chr = blk.spanning_blocks(s4, index, homo)

@@ -16,8 +16,8 @@ mode) serves all of them:
 - Every query gets up to 16 local alignments scoring at least T, best first. Each has a CIGAR,
   forward query coordinates and the identical-base count.
 - `Placer` is the `place(targets, queries, preset)` callback the partner stages take
-  (partner.py). It renders hits as PSL rows, and `sam_records` renders them as SAM records for
-  the genome-alignment consumers.
+  (partner.py). It renders hits as PSL rows; bwa_records renders them as the SAM records
+  `bwa mem -M` prints for the genome-alignment consumers.
 
 Placement parity with BLAT / bwa themselves is unpinned: neither is available (SURVEY.md §8 c).
 The kernel is bit-exact against oracle/af_oracle.c `afo_place` (tests/test_gpu_place.py).
@@ -259,35 +259,13 @@ def psl_rows(ref, queries, hits, nh, min_identity=0):
     return out
 
 
-def sam_records(ref, queries, hits, nh, flag_extra=0):
-    """SAM lines (primary first, the rest 0x100) of the hits of queries [(name, seq)]."""
-    comp = str.maketrans("ACGTNacgtn", "TGCANtgcan")
-    out = []
-    for qi, (qname, qseq) in enumerate(queries):
-        n = max(int(nh[qi]), 0)
-        if n == 0:
-            out.append(f"{qname}\t{4 | flag_extra}\t*\t0\t0\t*\t*\t0\t0\t{qseq}\t*\n")
-            continue
-        for k in range(n):
-            h = hits[qi, k]
-            loc = ref.locate(h["t_start"], h["t_end"])
-            if loc is None:
-                continue
-            tk, ts, _ = loc
-            rev = bool(h["flag"] & 0x10)
-            seq = qseq.translate(comp)[::-1] if rev else qseq
-            flag = (0x10 if rev else 0) | (0x100 if k else 0) | flag_extra
-            out.append(f"{qname}\t{flag}\t{ref.names[tk]}\t{ts + 1}\t60\t{cigar_string(h['cigar'][:int(h['n_cigar'])])}"
-                       f"\t*\t0\t0\t{seq}\t*\n")
-    return out
-
-
 def preset_params(preset):
-    """af_params for one of the reference's BLAT / bwa option sets (PRESET_PARAMS)."""
+    """af_params for one of the reference's BLAT / bwa option sets (PRESET_PARAMS): the bwa genome
+    calls keep bwa mem's -k 19, the BLAT presets seed from the index's 16-mers."""
     T, _ = PRESET_PARAMS[preset]
     p = _lib.default_params()
     p.T = T
-    p.min_seed_len = _lib.AF_K
+    p.min_seed_len = 19 if preset == "genome_bwa" else _lib.AF_K
     return p
 
 

@@ -16,6 +16,7 @@ class OracleReference:
         self.names = [n for n, _ in contigs]
         self.lens = [len(s) for _, s in contigs]
         blob, self.offsets = concat_contigs(contigs)
+        self.total = len(blob)
         self.ix = oracle.OracleIndex(blob)
 
     def raw_hits(self, seqs, params=None, max_hits=16):
