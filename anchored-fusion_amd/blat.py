@@ -1,0 +1,174 @@
+"""The BLAT searches of the partner stages on the GPU (af_tile_index_build / af_blat, csrc/blat.hip).
+
+The reference shells out to BLAT at functions.py:341 (homologs), 530 (split-read tails), 966
+(anchor vs candidate blocks), 1007/1071 (partner halves vs candidate blocks), 1122 (anchored
+halves vs the anchor) and 1244 (candidate validation vs the genome), each with its own options.
+`PRESETS` carries those options; `TileReference` is a target indexed for one step size;
+`psl_lines` renders the rows in BLAT's PSL column layout (psLayout version 3), which the
+consumers read (partner.py, blocks.py).  The search itself is restated (include/afgpu.h,
+af_blat_params), bit-exact vs oracle/blat.c; parity with the BLAT binary is
+unpinned.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .place import concat_contigs, pack_queries
+
+PSL_DTYPE = np.dtype([(n, "<i4") for n in (
+    "query", "strand", "score", "matches", "mismatches", "n_count", "q_num_insert", "q_base_insert", "t_num_insert",
+    "t_base_insert", "q_start", "q_end", "q_size", "block_count")] + [
+    ("t_start", "<i8"), ("t_end", "<i8"), ("block_sizes", "<i4", (16,)), ("q_starts", "<i4", (16,)),
+    ("t_starts", "<i8", (16,))])
+assert PSL_DTYPE.itemsize == 328
+TILE = 11
+MAX_ROWS = 16
+
+# the reference's option sets (functions.py call sites); rep_match None = BLAT's default
+PRESETS = {
+    "homologs": dict(step_size=3, rep_match=10000, min_score=50, min_identity=80),          # fn:341
+    "split_tail": dict(min_score=20),                                                        # fn:530
+    "candidate_homolog": dict(step_size=3, min_score=20, min_match=2, min_identity=0),      # fn:966
+    "anchored_split": dict(step_size=3, min_score=12, min_match=2, min_identity=90),        # fn:1007/1071/1122
+    "genome_validate": dict(step_size=3, min_score=20, min_match=3, min_identity=90),       # fn:1244
+}
+
+
+class BlatParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("step_size", "min_match", "rep_match", "min_score", "min_identity",
+                                                "max_gap", "max_intron")]
+
+
+def params(preset=None, **kw):
+    """af_blat_params: BLAT's defaults, the preset's options, then kw.  Without an explicit
+    -repMatch, BLAT's default of 1024 (11-mer tiles) scales with tileSize / stepSize."""
+    p = BlatParams()
+    _lib.lib().af_blat_params_default(ctypes.byref(p))
+    opts = dict(PRESETS[preset]) if preset else {}
+    opts.update(kw)
+    for k, v in opts.items():
+        setattr(p, k, v)
+    if "rep_match" not in opts:
+        p.rep_match = 1024 * TILE // p.step_size
+    return p
+
+
+class TileReference:
+    """Contigs [(name, seq)] (or a joined device blob, from_device) as a BLAT target with one
+    tile step."""
+
+    def __init__(self, contigs, step_size=TILE, device=0, ctx=None):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob, self.offsets = concat_contigs(contigs)
+        self.total = len(blob)
+        self.step = int(step_size)
+        self._open(device, ctx)
+        _lib.check(self.ctx, _lib.lib().af_tile_index_build(self.ctx, blob, len(blob), self.step, ctypes.byref(self.idx)),
+                   "af_tile_index_build")
+
+    def _open(self, device, ctx):
+        self._own_ctx = ctx is None
+        if ctx is None:
+            ctx = ctypes.c_void_p()
+            _lib.check(None, _lib.lib().af_ctx_create(int(device), ctypes.byref(ctx)), "af_ctx_create")
+        self.ctx = ctx
+        self.idx = ctypes.c_void_p()
+
+    @classmethod
+    def from_device(cls, blob_t, names, lens, offsets, step_size=TILE, device=0, ctx=None):
+        self = cls.__new__(cls)
+        self.names, self.lens, self.offsets = list(names), [int(v) for v in lens], [int(v) for v in offsets]
+        self.total = int(blob_t.numel())
+        self.step = int(step_size)
+        if not blob_t.is_cuda or not blob_t.is_contiguous():
+            raise ValueError("blob_t must be a contiguous device tensor")
+        self._open(device, ctx)
+        _lib.check(self.ctx, _lib.lib().af_tile_index_build_device(self.ctx, blob_t.data_ptr(), self.total, self.step,
+                                                                    ctypes.byref(self.idx)),
+                   "af_tile_index_build_device")
+        return self
+
+    def close(self):
+        L = _lib.lib()
+        if getattr(self, "idx", None):
+            L.af_index_free(self.idx)
+            self.idx = None
+        if getattr(self, "_own_ctx", False) and getattr(self, "ctx", None):
+            L.af_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def search(self, seqs, p, max_rows=MAX_ROWS):
+        """af_blat -> (rows [n, max_rows] PSL_DTYPE, n_rows [n])."""
+        buf, lens = pack_queries(seqs)
+        n = len(seqs)
+        rows = np.zeros((n, max_rows), dtype=PSL_DTYPE)
+        nr = np.zeros(n, dtype=np.int32)
+        if n:
+            _lib.check(self.ctx, _lib.lib().af_blat(self.ctx, self.idx, buf.ctypes.data, n, buf.shape[1],
+                                                   lens.ctypes.data, ctypes.byref(p), max_rows, rows.ctypes.data,
+                                                   nr.ctypes.data), "af_blat")
+        return rows, nr
+
+    def search_device(self, queries_t, n_queries_t, stride, rows_t, n_rows_t, lens_t=None, p=None, max_rows=MAX_ROWS,
+                      stream=None):
+        """af_blat_device on device buffers (rows_t: cap * max_rows * 328 bytes)."""
+        from .align import _stream_handle
+        cap = int(queries_t.shape[0])
+        if queries_t.dim() != 2 or int(queries_t.shape[1]) < int(stride):
+            raise ValueError("queries_t must be [cap, >= stride]")
+        if rows_t.numel() * rows_t.element_size() < cap * max_rows * PSL_DTYPE.itemsize or n_rows_t.numel() < cap:
+            raise ValueError("rows_t / n_rows_t too small for cap queries")
+        if lens_t is not None and lens_t.numel() < cap:
+            raise ValueError("lens_t holds fewer than cap entries")
+        _lib.check(self.ctx, _lib.lib().af_blat_device(
+            self.ctx, self.idx, queries_t.data_ptr(), n_queries_t.data_ptr(), cap, int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(p or params()), int(max_rows),
+            rows_t.data_ptr(), n_rows_t.data_ptr(), _stream_handle(stream)), "af_blat_device")
+
+    def locate(self, t_start, t_end):
+        import bisect
+        k = bisect.bisect_right(self.offsets, int(t_start)) - 1
+        if k < 0:
+            return None
+        s, e = int(t_start) - self.offsets[k], int(t_end) - self.offsets[k]
+        if s < 0 or e > self.lens[k] or e <= s:
+            return None
+        return k, s, e
+
+
+def psl_lines(ref, queries, rows, nr, offsets=None, full_sizes=None):
+    """PSL lines (21 columns, psLayout 3) of the rows of queries [(name, seq)].  offsets /
+    full_sizes: a query that is a window of a longer sequence reports the full query's size and
+    coordinates (offset added; '-' strand blocks mapped on the full reverse complement)."""
+    out = []
+    for i, (name, seq) in enumerate(queries):
+        off = 0 if offsets is None else int(offsets[i])
+        full = len(seq) if full_sizes is None else int(full_sizes[i])
+        for k in range(max(int(nr[i]), 0)):
+            r = rows[i, k]
+            loc = ref.locate(r["t_start"], r["t_end"])
+            if loc is None:
+                continue
+            tk, ts, te = loc
+            base = ref.offsets[tk]
+            nb = int(r["block_count"])
+            strand = "-" if r["strand"] else "+"
+            if r["strand"]:  # rc-window coordinates -> rc-full coordinates
+                qs = [full - (off + len(seq)) + int(v) for v in r["q_starts"][:nb]]
+            else:
+                qs = [off + int(v) for v in r["q_starts"][:nb]]
+            f = [int(r["matches"]), int(r["mismatches"]), 0, int(r["n_count"]), int(r["q_num_insert"]),
+                 int(r["q_base_insert"]), int(r["t_num_insert"]), int(r["t_base_insert"]), strand, name, full,
+                 off + int(r["q_start"]), off + int(r["q_end"]), ref.names[tk], ref.lens[tk], ts, te, nb,
+                 ",".join(str(int(v)) for v in r["block_sizes"][:nb]) + ",", ",".join(map(str, qs)) + ",",
+                 ",".join(str(int(v) - base) for v in r["t_starts"][:nb]) + ","]
+            out.append("\t".join(map(str, f)) + "\n")
+    return out

@@ -39,6 +39,15 @@ struct DevIndex {
     int32_t bl_bits;        // log2 Bloom words
 };
 
+// BLAT tile index (blat.hip): target codes, every step-th 11-mer's positions grouped by key
+// (start[key] .. start[key + 1]) ascending, N counts before each 4096-base block
+struct DevTile {
+    const uint8_t *T;
+    const uint32_t *start, *pos, *ncum;
+    int64_t n;
+    int32_t step;
+};
+
 __host__ __device__ static inline uint32_t af_fmix(uint32_t k) { return (k ^ (k >> 16)) * 0x45D9F3Bu; }
 // reverse complement of a 2-bit packed 16-mer (base i at bits 2i; A0 C1 G2 T3, complement = 3 - c)
 __host__ __device__ static inline uint32_t af_rc16(uint32_t k) {
@@ -234,6 +243,15 @@ hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t 
                             int64_t n_rows, int32_t mode, const af_aln_out &out, int64_t first, int64_t step,
                             int64_t cap, uint8_t *q, int32_t *q_lens, int32_t *q_rows, int32_t *n_q, int32_t *sel,
                             int64_t *sel_n, void *temp, size_t temp_bytes, hipStream_t s);
+// k_blat's per-wave global scratch (blat.hip layout) and its resident waves on n_cu CUs
+constexpr size_t AF_BLAT_SLOT_BYTES = 704 << 10;
+int af_blat_slots(int n_cu);
+hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+                          int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
+                          uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
+                          hipStream_t s);
+hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, DevTile *X, void **allocs, int *na,
+                               hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);
 size_t af_genome_index_table_bytes();
 int af_genome_scan_blocks();

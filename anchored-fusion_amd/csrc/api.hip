@@ -26,6 +26,8 @@ struct af_ctx {
     ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
     uint8_t *zscratch = nullptr;
+    uint8_t *bscratch = nullptr;  // k_blat: AF_BLAT_SLOT_BYTES per resident wave (blat_slots)
+    int blat_slots = 0;
     // S2 (bwa mem paired-end) scratch, s2.hip
     S2Reg *s2_pool = nullptr;
     int64_t s2_pool_cap = 0;
@@ -74,6 +76,8 @@ struct af_index {
     std::vector<uint8_t> text;
     DevText s2{};
     bool s2_ready = false;
+    DevTile tile{};        // BLAT tile index (af_tile_index_build*), else unused
+    bool is_tile = false;
     void *allocs[24] = {};
     int n_allocs = 0;
 };
@@ -197,6 +201,13 @@ int ensure_zscratch(af_ctx *c) {
     if (c->zscratch) return AF_OK;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     HIPCHK(c, hipMalloc(&c->zscratch, zstride * c->n_slots));
+    return AF_OK;
+}
+
+int ensure_bscratch(af_ctx *c) {
+    if (c->bscratch) return AF_OK;
+    c->blat_slots = af_blat_slots(c->n_cu);
+    HIPCHK(c, hipMalloc(&c->bscratch, (size_t)AF_BLAT_SLOT_BYTES * c->blat_slots));
     return AF_OK;
 }
 
@@ -354,7 +365,7 @@ int af_ctx_create(int device, af_ctx **out) {
 void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->d_packed);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->bscratch); af_free(c->d_packed);
     af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
@@ -551,6 +562,7 @@ int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
 int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
                           const int32_t *d_lens, int32_t *d_hits, void *stream) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
+    if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || (!d_reads && n_reads) || !d_hits) return fail(c, AF_E_INVALID, "null argument");
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
     if (((uintptr_t)d_reads & 15) != 0) return fail(c, AF_E_INVALID, "reads buffer must be 16-byte aligned");
@@ -621,6 +633,7 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
                             const int32_t *d_lens, const af_params *p, const af_pe *pe_in, af_aln_out *o, void *stream,
                             const AfTails *tails, bool append) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
+    if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
     if (rc) return rc;
@@ -671,6 +684,7 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
 int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t n_pairs, int32_t stride,
                    const int32_t *lens, const af_params *p, const af_pe *pe, af_aln_out *out) {
     if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
+    if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || !out || (!reads && n_pairs)) return fail(c, AF_E_INVALID, "null argument");
     if (n_pairs == 0) return AF_OK;
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
@@ -744,6 +758,7 @@ int af_place(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_qu
              const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits) {
     static_assert(sizeof(af_hit) == 176, "af_hit layout is part of the C-ABI");
     if (!c || !ix || !hits || !n_hits || (!queries && n_queries)) return fail(c, AF_E_INVALID, "null argument");
+    if (ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     int rc = check_params(c, p);
     if (rc) return rc;
     if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
@@ -792,6 +807,7 @@ int af_place_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, con
                     af_hit *d_hits, int32_t *d_n_hits, void *stream) {
     if (!c || !ix || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_hits || !d_n_hits)))
         return fail(c, AF_E_INVALID, "null argument");
+    if (ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     int rc = check_params(c, p);
     if (rc) return rc;
     if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
@@ -886,6 +902,129 @@ int af_gather_reads_device(af_ctx *c, const uint8_t *d_reads, int32_t stride, co
     af_aln_out none{};
     HIPCHK(c, af_launch_gather(d_reads, stride, d_lens, d_rows, n_rows, mode, d_out ? *d_out : none, first, step, cap,
                                d_q, d_q_lens, d_q_rows, d_n_q, c->g_sel, c->g_sel_n, c->g_temp, c->g_temp_bytes, s));
+    return AF_OK;
+}
+
+void af_blat_params_default(af_blat_params *p) {
+    // blat's defaults for DNA (usage text of blat v.35): tileSize 11, stepSize = tileSize,
+    // minMatch 2, repMatch 1024, minScore 30, minIdentity 90, maxGap 2, maxIntron 750000
+    p->step_size = AF_TILE; p->min_match = 2; p->rep_match = 1024; p->min_score = 30;
+    p->min_identity = 90; p->max_gap = 2; p->max_intron = 750000;
+}
+
+static int tile_build(af_ctx *c, const char *seq, int64_t len, int32_t step, af_index **out, bool dev) {
+    if (!c || !seq || !out) return fail(c, AF_E_INVALID, "null argument");
+    *out = nullptr;
+    if (len < AF_TILE) return fail(c, AF_E_INVALID, "reference shorter than a tile (%d)", AF_TILE);
+    if (len >= (1LL << 32) - 1) return fail(c, AF_E_UNSUPPORTED, "reference of 2^32 bases or more");
+    if (step < 1 || step > AF_TILE) return fail(c, AF_E_INVALID, "step_size %d outside [1, %d]", step, AF_TILE);
+    (void)hipSetDevice(c->device);
+    af_index *ix = new (std::nothrow) af_index;
+    if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
+    ix->ctx = c;
+    ix->is_tile = true;
+    const uint8_t *d = reinterpret_cast<const uint8_t *>(seq);
+    void *tmp = nullptr;
+    hipError_t e = hipSuccess;
+    if (!dev) {
+        if ((e = hipMalloc(&tmp, (size_t)len)) != hipSuccess ||
+            (e = hipMemcpyAsync(tmp, seq, (size_t)len, hipMemcpyHostToDevice, c->stream)) != hipSuccess) {
+            af_free(tmp);
+            af_index_free(ix);
+            return fail(c, AF_E_HIP, "af_tile_index_build: upload: %s", hipGetErrorString(e));
+        }
+        d = static_cast<const uint8_t *>(tmp);
+    }
+    e = af_build_tile_index(d, len, step, &ix->tile, ix->allocs, &ix->n_allocs, c->stream);
+    af_free(tmp);
+    if (e != hipSuccess) {
+        af_index_free(ix);
+        return fail(c, AF_E_HIP, "af_tile_index_build: %s", hipGetErrorString(e));
+    }
+    ix->dev.n = len;
+    *out = ix;
+    return AF_OK;
+}
+
+int af_tile_index_build(af_ctx *c, const char *seq, int64_t len, int32_t step, af_index **out) {
+    return tile_build(c, seq, len, step, out, false);
+}
+
+int af_tile_index_build_device(af_ctx *c, const char *d_seq, int64_t len, int32_t step, af_index **out) {
+    return tile_build(c, d_seq, len, step, out, true);
+}
+
+static int check_blat(af_ctx *c, const af_index *ix, const af_blat_params *p, int32_t stride, int32_t max_rows) {
+    if (!ix || !ix->is_tile) return fail(c, AF_E_INVALID, "af_blat needs a tile index (af_tile_index_build)");
+    if (!p) return fail(c, AF_E_INVALID, "params is NULL");
+    if (p->step_size != ix->tile.step)
+        return fail(c, AF_E_INVALID, "step_size %d differs from the index's %d", p->step_size, ix->tile.step);
+    if (p->min_match < 1 || p->rep_match < 1 || p->min_identity < 0 || p->min_identity > 100 || p->max_gap < 0 ||
+        p->max_intron < 0)
+        return fail(c, AF_E_INVALID, "invalid af_blat_params");
+    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
+    if (max_rows < 1 || max_rows > AF_BLAT_MAX_ROWS)
+        return fail(c, AF_E_INVALID, "max_rows must be in [1, %d]", AF_BLAT_MAX_ROWS);
+    return AF_OK;
+}
+
+int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_queries, int32_t stride,
+            const int32_t *lens, const af_blat_params *p, int32_t max_rows, af_psl *rows, int32_t *n_rows) {
+    static_assert(sizeof(af_psl) == 328, "af_psl layout is part of the C-ABI");
+    if (!c || !rows || !n_rows || (!queries && n_queries)) return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_blat(c, ix, p, stride, max_rows);
+    if (rc) return rc;
+    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
+    if (n_queries == 0) return AF_OK;
+    if (lens)
+        for (int64_t i = 0; i < n_queries; ++i)
+            if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_bscratch(c))) return rc;
+    const int64_t bytes = n_queries * (int64_t)stride, nr = n_queries * (int64_t)max_rows;
+    uint8_t *d_q = nullptr;
+    int32_t *d_lens = nullptr, *d_nrows = nullptr;
+    af_psl *d_rows = nullptr;
+    auto done = [&](int code) {
+        af_free(d_q); af_free(d_lens); af_free(d_nrows); af_free(d_rows);
+        return code;
+    };
+    if (hipMalloc(&d_q, bytes + 64) != hipSuccess || hipMalloc(&d_lens, 4 * n_queries + 64) != hipSuccess ||
+        hipMalloc(&d_nrows, 4 * n_queries + 64) != hipSuccess || hipMalloc(&d_rows, sizeof(af_psl) * nr) != hipSuccess)
+        return done(fail(c, AF_E_NOMEM, "af_blat: device buffers"));
+    hipStream_t s = c->stream;
+    const int32_t nq = (int32_t)n_queries;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(d_q, queries, bytes, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (lens && (e = hipMemcpyAsync(d_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s)) != hipSuccess) ||
+        (e = hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, n_queries, stride, lens ? d_lens : nullptr, *p,
+                            c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows, s)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(n_rows, d_nrows, 4 * n_queries, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return done(fail(c, AF_E_HIP, "af_blat: %s", hipGetErrorString(e)));
+    return done(AF_OK);
+}
+
+int af_blat_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
+                   int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
+                   int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
+    if (!c || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_rows || !d_n_rows)))
+        return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_blat(c, ix, p, stride, max_rows);
+    if (rc) return rc;
+    if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
+    if (cap_queries == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_bscratch(c))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
+    HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
+    HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, cap_queries, stride, d_lens, *p,
+                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows, s));
     return AF_OK;
 }
 

@@ -1,0 +1,639 @@
+// blat.hip -- the BLAT searches of the partner stages on the GPU (functions.py:341, 530, 966, 1007,
+// 1071, 1122, 1244): the tile index and k_blat, one wave per query.  oracle/blat.c is the
+// bit-exact contract; the restated algorithm and its choices are in afgpu.h (af_blat_params).
+//
+// Tile index (af_tile_index_build*): codes of the target (1 B/base), every step_size-th 11-mer
+// without N as (key, position) pairs radix-sorted by key (stable: positions ascending within a
+// key), key starts by a count + scan over all 4^11 keys, and N counts per 4096-base block (the
+// stitcher never joins parts across an N run, i.e. across contigs).
+//
+// k_blat per query and strand (strand 1 = the reverse-complemented query):
+//   hits     the query's 11-mer keys (lanes over offsets); then, offset by offset, the wave reads a
+//            key's positions coalesced and stores every hit, the first NMAX in (offset, position)
+//            order, as a 64-bit key (diagonal + 1024) << 9 | offset in the slot's scratch
+//   sort     stable LSD radix sort of the keys by diagonal (8-bit digits over the diagonal bits
+//            the target needs; LDS histogram, wave scan, ballot-ranked scatter), so the hits of
+//            a diagonal stay in offset order
+//   clumps   run starts (diagonal step > max_gap + 2) compacted by ballots; lanes over runs keep
+//            the runs of min_match hits (the first MAXCL, diagonal order), seed = least (offset,
+//            position); a 2-pass radix sort orders them (hits desc, diagonal)
+//   align    per clump, unless its seed tile lies in an earlier part: ksw_extend2 both ways and
+//            bwa_gen_cigar2 (ksw_dp.h, the wave DP of the placement kernel) with BLAT-like scores
+//   stitch   chain DP over the parts (<= 16) with overlap trimming; N checks over the gaps on
+//            the wave; every chain passing minScore / minIdentity becomes a PSL row
+//   output   rows of both strands ordered (score desc, strand, tStart, qStart), max_rows kept
+#include <hipcub/hipcub.hpp>
+
+#include "ksw_dp.h"
+
+namespace {
+
+constexpr int TILE = AF_TILE;
+constexpr uint32_t NKEYS = 1u << (2 * TILE);
+constexpr int NMAX = 32768, MAXCL = 4096, MAXR = 16, MAXROWS = 4 * MAXR, NBLK_SHIFT = 12;
+// per-slot scratch layout (bytes; the traceback of gen_cigar uses the first 64 KB)
+constexpr size_t SC_KEYS_A = 64 << 10, SC_KEYS_B = SC_KEYS_A + NMAX * 8, SC_CLUMP = SC_KEYS_B + NMAX * 8,
+                 SC_REGS = SC_CLUMP + MAXCL * 24, SC_ROWS = SC_REGS + (8 << 10), SC_END = SC_ROWS + (24 << 10);
+static_assert(SC_END == AF_BLAT_SLOT_BYTES, "BLAT slot layout");
+
+struct Clump { int64_t diag, t; int32_t cnt, q; };
+struct Reg {
+    int32_t qb, qe, score, matches, mismatches, ncount, qni, qbi, tni, tbi, nb, used;
+    int64_t tb, te;
+    int32_t bsz[AF_PSL_MAX_BLOCKS], bq[AF_PSL_MAX_BLOCKS];
+    int64_t bt[AF_PSL_MAX_BLOCKS];
+};
+
+struct __attribute__((aligned(16))) BlatLds {
+    uint32_t hist[256];            // radix digit counts / bucket starts
+    uint8_t q0[AF_MAX_READ + 16];  // the query's codes (strand 0)
+    int32_t key[AF_MAX_READ];      // tile key per query offset of the current strand, -1 = none
+    int32_t nh, ncl, nr, nrow, tmp[8];
+    int32_t order[MAXR], best[MAXR], prev[MAXR], chain[MAXR];
+};
+__shared__ BlatLds g_bl;
+
+__device__ __forceinline__ uint8_t nt4(uint8_t c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+__device__ __forceinline__ int lanes_below_blat(uint64_t m, int lane) {
+    return lane ? __builtin_popcountll(m << (64 - lane)) : 0;
+}
+
+__device__ __forceinline__ bool tile_key(const uint8_t *Q, int q, uint32_t &k) {
+    k = 0;
+    bool ok = true;
+    for (int u = 0; u < TILE; ++u) {
+        const uint8_t b = Q[q + u];
+        ok = ok && b < 4;
+        k |= (uint32_t)(b & 3) << (2 * u);
+    }
+    return ok;
+}
+
+__device__ __forceinline__ int wave_incl_sum(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(v, d);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+
+// stable LSD radix sort of a[0, n) by bits [lo, lo + 8 * passes) on the wave, ping-ponging with
+// b; returns the buffer holding the result
+__device__ uint64_t *wave_radix_sort(uint64_t *a, uint64_t *b, int n, int lo, int passes, int lane) {
+    uint32_t *H = g_bl.hist;
+    for (int p = 0; p < passes; ++p) {
+        const int sh = lo + 8 * p;
+        for (int x = lane; x < 256; x += 64) H[x] = 0;
+        wave_sync();
+        for (int i = lane; i < n; i += 64) atomicAdd(&H[(uint32_t)(a[i] >> sh) & 255u], 1u);
+        wave_sync();
+        const uint32_t v0 = H[4 * lane], v1 = H[4 * lane + 1], v2 = H[4 * lane + 2], v3 = H[4 * lane + 3];
+        const int tot = (int)(v0 + v1 + v2 + v3);
+        const uint32_t ex = (uint32_t)(wave_incl_sum(tot, lane) - tot);
+        H[4 * lane] = ex; H[4 * lane + 1] = ex + v0; H[4 * lane + 2] = ex + v0 + v1; H[4 * lane + 3] = ex + v0 + v1 + v2;
+        wave_sync();
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const bool valid = i < n;
+            const uint64_t k = valid ? a[i] : 0;
+            const uint32_t d = (uint32_t)(k >> sh) & 255u;
+            uint64_t m = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+                const bool on = (d >> bit) & 1u;
+                const uint64_t bl = __ballot(valid && on);
+                m &= on ? bl : ~bl;
+            }
+            const uint32_t base = H[d];
+            if (valid) b[base + lanes_below_blat(m, lane)] = k;
+            wave_sync();
+            if (valid && (m >> lane) == 1ull) H[d] = base + (uint32_t)__builtin_popcountll(m);
+            wave_sync();
+        }
+        __threadfence_block();
+        wave_sync();
+        uint64_t *t = a; a = b; b = t;
+    }
+    return a;
+}
+
+// N bases in T[a, b), on the wave (the oracle's n_in)
+__device__ int64_t n_in(const DevTile &X, int64_t a, int64_t b, int lane) {
+    if (b <= a) return 0;
+    const int64_t ba = a >> NBLK_SHIFT, bb = b >> NBLK_SHIFT;
+    int c = 0;
+    if (ba == bb) {
+        for (int64_t i = a + lane; i < b; i += 64) c += X.T[i] > 3;
+        return wave_sum(c);
+    }
+    for (int64_t i = a + lane; i < ((ba + 1) << NBLK_SHIFT); i += 64) c += X.T[i] > 3;
+    for (int64_t i = (bb << NBLK_SHIFT) + lane; i < b; i += 64) c += X.T[i] > 3;
+    return (int64_t)wave_sum(c) + (int64_t)(X.ncum[bb] - X.ncum[ba + 1]);
+}
+
+// r without its first k aligned bases (lane 0; 0 if k does not fit the first block)
+__device__ bool trim_front(const DevTile &X, const uint8_t *Q, const Reg &r, int k, Reg &o) {
+    o = r;
+    if (k <= 0) return true;
+    if (k >= r.bsz[0]) return false;
+    for (int u = 0; u < k; ++u) {
+        const uint8_t a = Q[r.bq[0] + u], b = X.T[r.bt[0] + u];
+        if (a > 3 || b > 3) --o.ncount;
+        else if (a == b) --o.matches;
+        else --o.mismatches;
+    }
+    o.bsz[0] -= k; o.bq[0] += k; o.bt[0] += k;
+    o.qb = o.bq[0]; o.tb = o.bt[0];
+    o.score = o.matches - o.mismatches - o.qni - o.tni;
+    return true;
+}
+
+__device__ __forceinline__ int chain_trim(const Reg &a, const Reg &b) {
+    int64_t k = a.qe - b.qb;
+    if (a.te - b.tb > k) k = a.te - b.tb;
+    return k > 0 ? (int)k : 0;
+}
+
+__device__ int psl_millibad(const af_psl &o) {
+    const int q_ali = o.q_end - o.q_start;
+    const int64_t t_ali = o.t_end - o.t_start;
+    const int64_t ali = q_ali < t_ali ? q_ali : t_ali;
+    if (ali <= 0) return 0;
+    int64_t size_dif = q_ali - t_ali;
+    if (size_dif < 0) size_dif = 0;
+    const int total = o.matches + o.mismatches;
+    if (total == 0) return 0;
+    return (int)((1000 * (o.mismatches + o.q_num_insert + round(3 * log(1. + (double)size_dif)))) / total);
+}
+
+__device__ __forceinline__ bool psl_before(const af_psl &x, const af_psl &y) {
+    if (x.score != y.score) return x.score > y.score;
+    if (x.strand != y.strand) return x.strand < y.strand;
+    if (x.t_start != y.t_start) return x.t_start < y.t_start;
+    if (x.q_start != y.q_start) return x.q_start < y.q_start;
+    if (x.t_end != y.t_end) return x.t_end < y.t_end;
+    return x.q_end < y.q_end;
+}
+
+// one clump seed (q, t) -> Reg r (written by lane 0); false if dropped.  L.q holds the strand.
+template <int CPL>
+__device__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, uint8_t *zg, int lane) {
+    DpLds &D = g_dp;
+    af_params P{};
+    P.a = 1; P.b = 1; P.o_del = 3; P.e_del = 1; P.o_ins = 3; P.e_ins = 1; P.w = 16; P.zdrop = 20;
+    int score, truesc, qb, qe;
+    int64_t tb, te;
+    if (q > 0) {
+        const int tl = (int)(t < q + P.w ? t : q + P.w);
+        for (int x = lane; x < q; x += 64) D.qs[x] = D.q[q - 1 - x];
+        for (int x = lane; x < tl; x += 64) D.t[x] = X.T[t - 1 - x];
+        wave_sync();
+        const ExtRes er = ext_dp<CPL>(q, D.qs, tl, D.t, P, P.w, 0, P.zdrop, TILE * P.a, lane);
+        score = er.max;
+        if (er.gscore <= 0 || er.gscore <= score) { qb = q - er.qle; tb = t - er.tle; truesc = score; }
+        else { qb = 0; tb = t - er.gtle; truesc = er.gscore; }
+        wave_sync();
+    } else {
+        score = truesc = TILE * P.a; qb = 0; tb = t;
+    }
+    if (q + TILE < L) {
+        const int qs0 = q + TILE;
+        const int64_t t0 = t + TILE, room = X.n - t0;
+        const int tl = (int)(room < (L - qs0) + P.w ? room : (int64_t)(L - qs0) + P.w);
+        const int sc0 = score;
+        for (int x = lane; x < tl; x += 64) D.t[x] = X.T[t0 + x];
+        wave_sync();
+        const ExtRes er = ext_dp<CPL>(L - qs0, D.q + qs0, tl, D.t, P, P.w, 0, P.zdrop, sc0, lane);
+        score = er.max;
+        if (er.gscore <= 0 || er.gscore <= score) { qe = qs0 + er.qle; te = t0 + er.tle; truesc += score - sc0; }
+        else { qe = L; te = t0 + er.gtle; truesc += er.gscore - sc0; }
+        wave_sync();
+    } else {
+        qe = L; te = t + TILE;
+    }
+    const int lq = qe - qb, rl = (int)(te - tb);
+    if (lq <= 0 || rl <= 0) return false;
+    int w2 = infer_bw(lq, rl, truesc, P.a, P.o_del, P.e_del);
+    const int w3 = infer_bw(lq, rl, truesc, P.a, P.o_ins, P.e_ins);
+    w2 = w2 > w3 ? w2 : w3;
+    w2 = w2 < 64 ? w2 : 64;
+    gen_cigar_wave<CPL>(X.T, (int64_t)1 << 62, P, w2, lq, qb, tb, te, D, zg, lane);
+    const int nc = D.misc[2];
+    if (nc > AF_MAX_CIGAR) return false;
+    bool ok = true;
+    if (lane == 0) {
+        // ring holds the ops in reverse order: forward op x is ring[(nc - 1 - x) & 63]
+        int xs = 0, xe = nc;
+        const uint32_t f0 = nc > 0 ? D.ring[(nc - 1) & 63] : 0u, fl = nc > 0 ? D.ring[0] : 0u;
+        if (nc > 0 && (f0 & 0xf) == 2) { tb += f0 >> 4; xs = 1; }
+        else if (nc > 0 && (fl & 0xf) == 2) { te -= fl >> 4; xe = nc - 1; }
+        Reg o{};
+        int32_t x = qb;
+        int64_t y = tb;
+        for (int k = xs; k < xe && ok; ++k) {
+            const uint32_t op4 = D.ring[(nc - 1 - k) & 63];
+            const int len = (int)(op4 >> 4), op = (int)(op4 & 0xf);
+            if (op == 0) {
+                if (o.nb >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
+                o.bsz[o.nb] = len; o.bq[o.nb] = x; o.bt[o.nb] = y; ++o.nb;
+                for (int u = 0; u < len; ++u) {
+                    const uint8_t a = D.q[x + u], b = X.T[y + u];
+                    if (a > 3 || b > 3) ++o.ncount;
+                    else if (a == b) ++o.matches;
+                    else ++o.mismatches;
+                }
+                x += len; y += len;
+            } else if (op == 1) {
+                ++o.qni; o.qbi += len; x += len;
+            } else {
+                ++o.tni; o.tbi += len; y += len;
+            }
+        }
+        if (o.nb == 0) ok = false;
+        o.qb = qb; o.qe = qe; o.tb = tb; o.te = te;
+        o.score = o.matches - o.mismatches - o.qni - o.tni;
+        if (ok) r = o;
+        g_bl.tmp[0] = ok ? 1 : 0;
+    }
+    wave_sync();
+    return g_bl.tmp[0] != 0;
+}
+
+template <int CPL>
+__global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
+                                                        int32_t stride, const int32_t *__restrict__ lens,
+                                                        af_blat_params bp, const int32_t *__restrict__ n_q,
+                                                        int64_t cap, int32_t *__restrict__ heads,
+                                                        uint8_t *__restrict__ bscratch, int32_t diag_passes,
+                                                        af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
+                                                        int32_t max_rows) {
+    DpLds &D = g_dp;
+    BlatLds &B = g_bl;
+    const int lane = threadIdx.x;
+    const int64_t nq64 = *n_q < cap ? *n_q : cap;
+    const int nq = (int)(nq64 < 0 ? 0 : nq64);
+    uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
+    uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
+    Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
+    Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
+    af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        int item = nq;
+        while (heads_left > 0) {
+            int v = 0;
+            if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
+            v = __builtin_amdgcn_readfirstlane(v);
+            const int64_t it = head + 8 * (int64_t)v;
+            if (it < nq) { item = (int)it; break; }
+            head = (head + 1) & 7;
+            --heads_left;
+        }
+        if (item >= nq) break;
+        const int64_t qi = item;
+        int L = lens ? lens[qi] : stride;
+        if (L > stride) L = stride;
+        if (L > AF_MAX_READ) L = AF_MAX_READ;
+        if (L < 0) L = 0;
+        for (int x = lane; x < L; x += 64) B.q0[x] = nt4(queries[qi * (int64_t)stride + x]);
+        if (lane == 0) B.nrow = 0;
+        wave_sync();
+        for (int strand = 0; strand < 2; ++strand) {
+            for (int x = lane; x < L; x += 64) {
+                const uint8_t c = B.q0[strand ? L - 1 - x : x];
+                D.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
+            }
+            wave_sync();
+            // ---- the query's tile keys (-1: N inside or a tile over rep_match / absent) ---------------
+            for (int q = lane; q < L; q += 64) {
+                uint32_t k;
+                int32_t v = -1;
+                if (q + TILE <= L && tile_key(D.q, q, k)) {
+                    const uint32_t c = X.start[k + 1] - X.start[k];
+                    if (c > 0 && (int64_t)c <= bp.rep_match) v = (int32_t)k;
+                }
+                B.key[q] = v;
+            }
+            wave_sync();
+            // ---- every hit, the first NMAX in (offset, position) order ------------------------------
+            int nh = 0;
+            for (int q = 0; q + TILE <= L && nh < NMAX; ++q) {
+                const int32_t k = B.key[q];
+                if (k < 0) continue;
+                const uint32_t lo = X.start[k], c = X.start[k + 1] - lo;
+                for (uint32_t u0 = 0; u0 < c && nh < NMAX; u0 += 64) {
+                    const uint32_t u = u0 + lane;
+                    if (u < c && nh + (int)(u - u0) < NMAX)
+                        KA[nh + (u - u0)] = ((uint64_t)((int64_t)X.pos[lo + u] - q + 1024) << 9) | (uint32_t)q;
+                    nh = min(NMAX, nh + (int)min(64u, c - u0));
+                }
+            }
+            __threadfence_block();
+            wave_sync();
+            if (nh == 0) continue;
+            // ---- sort by diagonal (stable: offsets ascending within a diagonal) ------------------
+            const uint64_t *S = wave_radix_sort(KA, KB, nh, 9, diag_passes, lane);
+            uint32_t *ST = reinterpret_cast<uint32_t *>(S == KA ? KB : KA);
+            // ---- run starts, then the clumps (runs of min_match hits) in diagonal order -----------
+            const int64_t drift = (int64_t)bp.max_gap + 2;
+            int nrun = 0;
+            for (int i0 = 0; i0 < nh; i0 += 64) {
+                const int i = i0 + lane;
+                bool st = false;
+                if (i < nh) st = i == 0 || (int64_t)(S[i] >> 9) - (int64_t)(S[i - 1] >> 9) > drift;
+                const uint64_t m = __ballot(st);
+                if (st) ST[nrun + lanes_below_blat(m, lane)] = (uint32_t)i;
+                nrun += (int)__builtin_popcountll(m);
+            }
+            __threadfence_block();
+            wave_sync();
+            int ncl = 0;
+            for (int r0 = 0; r0 < nrun && ncl < MAXCL; r0 += 64) {
+                const int r = r0 + lane;
+                bool keep = false;
+                Clump cc{};
+                if (r < nrun) {
+                    const int s0 = (int)ST[r], e0 = r + 1 < nrun ? (int)ST[r + 1] : nh;
+                    if (e0 - s0 >= bp.min_match) {
+                        keep = true;
+                        int bq = 1 << 30;
+                        int64_t bt = 0;
+                        for (int i = s0; i < e0; ++i) {
+                            const int qq = (int)(S[i] & 511u);
+                            const int64_t tt = (int64_t)(S[i] >> 9) - 1024 + qq;
+                            if (qq < bq || (qq == bq && tt < bt)) { bq = qq; bt = tt; }
+                        }
+                        cc.cnt = e0 - s0; cc.q = bq; cc.t = bt; cc.diag = bt - bq;
+                    }
+                }
+                const uint64_t m = __ballot(keep);
+                const int slot = ncl + lanes_below_blat(m, lane);
+                if (keep && slot < MAXCL) CL[slot] = cc;
+                ncl = min(MAXCL, ncl + (int)__builtin_popcountll(m));
+            }
+            __threadfence_block();
+            wave_sync();
+            if (ncl == 0) continue;
+            // ---- clump order: hits desc, then diagonal (= run order) ------------------------------
+            for (int i = lane; i < ncl; i += 64)
+                KA[i] = ((uint64_t)(65535 - CL[i].cnt) << 32) | (uint32_t)i;
+            __threadfence_block();
+            wave_sync();
+            const uint64_t *CO = wave_radix_sort(KA, KB, ncl, 32, 2, lane);
+            // ---- parts: one per clump whose seed lies in no earlier part -------------------------
+            int nr = 0;
+            for (int c = 0; c < ncl && nr < MAXR; ++c) {
+                const Clump cc = CL[(uint32_t)CO[c]];
+                bool skip = false;
+                for (int r = 0; r < nr && !skip; ++r) {
+                    const Reg &g = RG[r];
+                    skip = g.qb <= cc.q && cc.q + TILE <= g.qe && g.tb <= cc.t && cc.t + TILE <= g.te;
+                }
+                if (skip) continue;
+                if (align_clump<CPL>(X, L, cc.q, cc.t, RG[nr], zg, lane)) ++nr;
+                __threadfence_block();
+                wave_sync();
+            }
+            if (nr == 0) continue;
+            // ---- parts in (qb, tb, qe) order, then chains, best first -----------------------------
+            if (lane == 0) {
+                for (int i = 1; i < nr; ++i)
+                    for (int j = i; j > 0; --j) {
+                        const Reg &a = RG[j - 1], &b = RG[j];
+                        const bool gt = a.qb > b.qb || (a.qb == b.qb && (a.tb > b.tb || (a.tb == b.tb && a.qe > b.qe)));
+                        if (!gt) break;
+                        const Reg tmp = RG[j - 1];
+                        RG[j - 1] = RG[j];
+                        RG[j] = tmp;
+                    }
+                for (int i = 0; i < nr; ++i) RG[i].used = 0;
+            }
+            __threadfence_block();
+            wave_sync();
+            for (;;) {
+                int bi = -1;
+                for (int i = 0; i < nr; ++i) {
+                    if (RG[i].used) continue;
+                    int best = RG[i].score, prev = -1;
+                    for (int j = 0; j < i; ++j) {
+                        if (RG[j].used) continue;
+                        const Reg &a = RG[j], &ri = RG[i];
+                        if (ri.qe <= a.qe || ri.te <= a.te) continue;
+                        const int k = chain_trim(a, ri);
+                        if (k > 0 && k >= ri.bsz[0]) continue;
+                        // the trimmed part's start and score (trim_front, uniform on every lane)
+                        int dsc = 0;
+                        for (int u = 0; u < k; ++u) {
+                            const uint8_t x = D.q[ri.bq[0] + u], y = X.T[ri.bt[0] + u];
+                            dsc += (x > 3 || y > 3) ? 0 : (x == y ? 1 : -1);
+                        }
+                        const int bqb = ri.qb + k;
+                        const int64_t btb = ri.tb + k;
+                        if (btb - a.te > bp.max_intron) continue;
+                        if (n_in(X, a.te, btb, lane)) continue;
+                        const int s = B.best[j] + (ri.score - dsc) - (bqb > a.qe) - (btb > a.te);
+                        if (s > best) { best = s; prev = j; }
+                    }
+                    if (lane == 0) { B.best[i] = best; B.prev[i] = prev; }
+                    wave_sync();
+                    if (bi < 0 || best > B.best[bi]) bi = i;
+                }
+                if (bi < 0) break;
+                if (lane == 0) {
+                    int m = 0;
+                    for (int i = bi; i >= 0; i = B.prev[i]) B.chain[m++] = i;
+                    af_psl o{};
+                    o.query = (int32_t)qi; o.strand = strand; o.q_size = L;
+                    bool ok = true;
+                    Reg part[2];  // the previous part (trimmed) and the current one
+                    Reg first{}, last{};
+                    for (int c = m - 1; c >= 0; --c) {
+                        RG[B.chain[c]].used = 1;
+                        Reg cur;
+                        if (c == m - 1) cur = RG[B.chain[c]];
+                        else trim_front(X, D.q, RG[B.chain[c]], chain_trim(part[0], RG[B.chain[c]]), cur);
+                        if (c < m - 1) {
+                            const Reg &a = part[0];
+                            if (cur.qb > a.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - a.qe; }
+                            if (cur.tb > a.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - a.te); }
+                        }
+                        o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
+                        o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi;
+                        o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
+                        for (int b = 0; b < cur.nb; ++b) {
+                            if (o.block_count >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
+                            o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
+                            o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
+                        }
+                        if (c == m - 1) first = cur;
+                        if (c == 0) last = cur;
+                        part[0] = cur;
+                    }
+                    o.q_start = strand ? L - last.qe : first.qb;
+                    o.q_end = strand ? L - first.qb : last.qe;
+                    o.t_start = first.tb; o.t_end = last.te;
+                    o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
+                    if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10 &&
+                        B.nrow < MAXROWS)
+                        RW[B.nrow++] = o;
+                }
+                __threadfence_block();
+                wave_sync();
+            }
+        }
+        // ---- rows of both strands, best first ---------------------------------------------------
+        if (lane == 0) {
+            const int n = B.nrow;
+            for (int i = 1; i < n; ++i)
+                for (int j = i; j > 0 && psl_before(RW[j], RW[j - 1]); --j) {
+                    const af_psl tmp = RW[j - 1];
+                    RW[j - 1] = RW[j];
+                    RW[j] = tmp;
+                }
+            const int m = n < max_rows ? n : max_rows;
+            for (int k = 0; k < m; ++k) rows[qi * max_rows + k] = RW[k];
+            n_rows[qi] = m;
+        }
+        __threadfence_block();
+        wave_sync();
+    }
+}
+
+// ---- tile index build -------------------------------------------------------------------------
+__global__ void k_tile_codes(const uint8_t *__restrict__ seq, int64_t n, uint8_t *__restrict__ T) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) T[i] = nt4(seq[i]);
+}
+
+__global__ void k_tile_keys(const uint8_t *__restrict__ T, int64_t n, int32_t step, int64_t n_tiles,
+                            uint32_t *__restrict__ keys, uint32_t *__restrict__ pos, uint32_t *__restrict__ cnt) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_tiles) return;
+    const int64_t p = k * step;
+    uint32_t key = 0;
+    bool ok = p + TILE <= n;
+    for (int u = 0; u < TILE && ok; ++u) {
+        const uint8_t b = T[p + u];
+        ok = b < 4;
+        key |= (uint32_t)(b & 3) << (2 * u);
+    }
+    keys[k] = ok ? key : NKEYS;  // invalid tiles sort last
+    pos[k] = (uint32_t)p;
+    if (ok) atomicAdd(&cnt[key], 1u);
+}
+
+__global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, uint32_t *__restrict__ nblk) {
+    const int64_t b = blockIdx.x;  // one workgroup per 4096-base block; nblk[b + 1] = its N count
+    const int64_t a = b << NBLK_SHIFT;
+    int c = 0;
+    for (int64_t i = a + threadIdx.x; i < n && i < a + (1 << NBLK_SHIFT); i += blockDim.x) c += T[i] > 3;
+    __shared__ int part[256];
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) nblk[b + 1] = (uint32_t)part[0];
+}
+
+}  // namespace
+
+hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+                          int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
+                          uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
+                          hipStream_t s) {
+    // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
+    int bits = 64 - __builtin_clzll((unsigned long long)(X.n + 1024));
+    const int diag_passes = (bits + 7) / 8;
+    const int cpl = (stride + 1 + 63) / 64;
+    dim3 g(n_slots), b(64);
+#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, cap, heads, \
+                                    bscratch, diag_passes, rows, n_rows, max_rows)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}
+
+int af_blat_slots(int n_cu) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(k_blat<AF_CPL>), 64, 0) !=
+            hipSuccess || occ < 1)
+        occ = 8;
+    return n_cu * occ;
+}
+
+// builds X's device arrays from d_seq (device bytes): allocations go to allocs[*na] (freed with
+// the index); returns a HIP error or hipSuccess
+hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, DevTile *X, void **allocs, int *na,
+                               hipStream_t s) {
+    hipError_t e;
+    const int64_t n_tiles = n >= TILE ? (n - TILE) / step + 1 : 0;
+    const int64_t nb = (n >> NBLK_SHIFT) + 2;
+    uint8_t *T = nullptr;
+    uint32_t *start = nullptr, *pos = nullptr, *ncum = nullptr;
+    uint32_t *keys = nullptr, *keys2 = nullptr, *pos2 = nullptr, *cnt = nullptr;
+    void *temp = nullptr;
+    auto cleanup = [&]() {
+        if (keys) (void)hipFree(keys);
+        if (keys2) (void)hipFree(keys2);
+        if (pos2) (void)hipFree(pos2);
+        if (cnt) (void)hipFree(cnt);
+        if (temp) (void)hipFree(temp);
+    };
+    if ((e = hipMalloc(&T, (size_t)n)) != hipSuccess) return e;
+    allocs[(*na)++] = T;
+    if ((e = hipMalloc(&start, sizeof(uint32_t) * (NKEYS + 1))) != hipSuccess) return e;
+    allocs[(*na)++] = start;
+    if ((e = hipMalloc(&pos, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess) return e;
+    allocs[(*na)++] = pos;
+    if ((e = hipMalloc(&ncum, sizeof(uint32_t) * (size_t)nb)) != hipSuccess) return e;
+    allocs[(*na)++] = ncum;
+    if ((e = hipMalloc(&keys, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
+        (e = hipMalloc(&keys2, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
+        (e = hipMalloc(&pos2, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
+        (e = hipMalloc(&cnt, sizeof(uint32_t) * (NKEYS + 1))) != hipSuccess) {
+        cleanup();
+        return e;
+    }
+    size_t tb_sort = 0, tb_scan = 0, tb_scan2 = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, keys, keys2, pos, pos2, n_tiles, 0, 2 * TILE + 1);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, cnt, start, NKEYS + 1);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan2, ncum, ncum, nb);
+    size_t tb = std::max(tb_sort, std::max(tb_scan, tb_scan2));
+    if ((e = hipMalloc(&temp, tb > 0 ? tb : 16)) != hipSuccess) { cleanup(); return e; }
+    const int bs = 256;
+    if ((e = hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (NKEYS + 1), s)) != hipSuccess ||
+        (e = hipMemsetAsync(ncum, 0, sizeof(uint32_t) * (size_t)nb, s)) != hipSuccess) { cleanup(); return e; }
+    hipLaunchKernelGGL(k_tile_codes, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, d_seq, n, T);
+    if (n_tiles > 0)
+        hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)((n_tiles + bs - 1) / bs)), dim3(bs), 0, s, T, n, step, n_tiles,
+                           keys, pos2, cnt);
+    hipLaunchKernelGGL(k_tile_nblocks, dim3((unsigned)(nb - 1)), dim3(256), 0, s, T, n, ncum);
+    if ((e = hipGetLastError()) != hipSuccess) { cleanup(); return e; }
+    size_t t1 = tb;
+    if (n_tiles > 0 &&
+        (e = hipcub::DeviceRadixSort::SortPairs(temp, t1, keys, keys2, pos2, pos, n_tiles, 0, 2 * TILE + 1, s)) !=
+            hipSuccess) { cleanup(); return e; }
+    t1 = tb;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t1, cnt, start, NKEYS + 1, s)) != hipSuccess) { cleanup(); return e; }
+    t1 = tb;
+    if ((e = hipcub::DeviceScan::InclusiveSum(temp, t1, ncum, ncum, nb, s)) != hipSuccess) { cleanup(); return e; }
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) { cleanup(); return e; }
+    cleanup();
+    X->T = T; X->start = start; X->pos = pos; X->ncum = ncum; X->n = n; X->step = step;
+    return hipSuccess;
+}

@@ -7,7 +7,7 @@ partner stages, all on the device with no host round trip for the data (SURVEY.m
 | AF:182 `\\| samtools sort`, AF:186-194 filters | `af_partition_device` over every record of the set |
 | AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_place_device` |
 | fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + the same launch |
-| fn:530 BLAT of the split reads' tails (S6) | tails cut in K3 + `af_place_device` (-minScore=20) |
+| fn:530 BLAT of the split reads' tails (S6) | tails cut in K3 + `af_blat_device` (BLAT restatement, -minScore=20) |
 
 `run()` enqueues one pass; S3 synchronises twice (its select count sizes the sort; the partition
 counts size the gathers).  Everything else stays on the device: the records, the row lists, the
@@ -17,6 +17,7 @@ import os
 import sys
 
 from . import _lib
+from . import blat as _blat
 from . import place as _place
 from .align import AlignerGroup
 from .shard import chunk_pairs
@@ -25,6 +26,7 @@ MIN_CLIP = 20       # split-read tails placed by S6 (functions.py:530 queries; c
 MAX_HITS = 16
 EX_HITS = 4         # hits per query carried by exchange()
 HIT_WORDS = 44      # af_hit as int32 words (176 B)
+PSL_WORDS = 82      # af_psl as int32 words (328 B)
 EX_WORDS = 39 + EX_HITS * HIT_WORDS
 _DEBUG = os.environ.get("AF_DEBUG_DISCOVER") == "1"
 
@@ -36,15 +38,16 @@ def _log(msg):
 class CandidateDiscovery:
     """S2 + S3 + S4/S5/S6 genome searches for `n_pairs` resident pairs of `read_len` bases.
 
-    reference: place.Reference (the genome, HBM-resident).  pair_base: the set's first pair in
+    reference: place.Reference (the genome, HBM-resident, for the bwa calls); tiles:
+    blat.TileReference of the same genome at BLAT's default step (S6).  pair_base: the set's first pair in
     bwa's input stream (a chunk boundary).  batch_chunks: bwa chunks per S2 batch; inflight:
     batches in flight (AlignerGroup)."""
 
-    def __init__(self, anchor: bytes, reference, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
-                 pair_base=0, chunk_bases=10_000_000, query_frac=0.02, tail_frac=0.01):
+    def __init__(self, anchor: bytes, reference, tiles, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
+                 pair_base=0, chunk_bases=10_000_000, query_frac=0.004, tail_frac=0.002):
         import torch
         self.dev = torch.device("cuda", device)
-        self.anchor, self.ref = bytes(anchor), reference
+        self.anchor, self.ref, self.tiles_ref = bytes(anchor), reference, tiles
         self.n_pairs, self.L, self.pair_base = int(n_pairs), int(read_len), int(pair_base)
         pc = chunk_pairs(self.L, chunk_bases)
         if self.pair_base % pc:
@@ -67,7 +70,7 @@ class CandidateDiscovery:
         # S6 tails (cut in K3, appended by every batch) and the S4 + S5 queries
         self.tcap = max(4096, int(nr * tail_frac))
         self.tails = dict(tails=z(self.tcap, self.L, dt=torch.uint8), lens=z(self.tcap), read=z(self.tcap), n=z(1))
-        self.t_hits = z(self.tcap * MAX_HITS * _place.HIT_DTYPE.itemsize, dt=torch.uint8)
+        self.t_rows = z(self.tcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
         self.t_nh = z(self.tcap)
         self.qcap = max(4096, int(nr * query_frac))
         self.q = z(self.qcap, self.L, dt=torch.uint8)
@@ -75,7 +78,7 @@ class CandidateDiscovery:
         self.q_hits = z(self.qcap * MAX_HITS * _place.HIT_DTYPE.itemsize, dt=torch.uint8)
         self.q_nh = z(self.qcap)
         self.p_genome = _place.preset_params("genome_bwa")
-        self.p_tail = _place.preset_params("split_tail")
+        self.p_tail = _blat.params("split_tail")
         self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
 
     def close(self):
@@ -138,8 +141,8 @@ class CandidateDiscovery:
         # S4 + S5 on the genome (bwa mem -M defaults), S6 tails (BLAT -minScore=20)
         self.ref.place_device(self.q, self.n_q, self.L, self.q_hits, self.q_nh, lens_t=self.q_lens,
                               params=self.p_genome, max_hits=MAX_HITS, stream=s0)
-        self.ref.place_device(self.tails["tails"], self.tails["n"], self.L, self.t_hits, self.t_nh,
-                              lens_t=self.tails["lens"], params=self.p_tail, max_hits=MAX_HITS, stream=s0)
+        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
+                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s0)
         if _DEBUG:
             s0.synchronize()
             _log("placements done")
@@ -163,30 +166,32 @@ class CandidateDiscovery:
         return c
 
     def tail_best_hits(self):
-        """(read rows, hit counts, best hit per tail) of the last pass, on the host (synchronises)."""
+        """(read rows, row counts, best BLAT row per tail) of the last pass, on the host (synchronises)."""
         import torch
         torch.cuda.synchronize(self.dev)
         nt = min(int(self.tails["n"].item()), self.tcap)
-        hits = self.t_hits[:nt * MAX_HITS * _place.HIT_DTYPE.itemsize].cpu().numpy().view(_place.HIT_DTYPE)
+        rows = self.t_rows[:nt * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
         return (self.tails["read"][:nt].cpu().numpy(), self.t_nh[:nt].cpu().numpy(),
-                hits.reshape(nt, MAX_HITS)[:, 0] if nt else hits)
+                rows.reshape(nt, _blat.MAX_ROWS)[:, 0] if nt else rows)
 
     def pack(self):
         """The breakpoint candidates of the last pass as int32 rows [k, EX_WORDS] on the device:
         every S4 / S5 query and every S6 tail -- the read's global row (2 words), kind (0 query,
         1 tail), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the hit count and its first
-        EX_HITS hits.  These are the only records the stages after S6 read (SURVEY §8 e)."""
+        EX_HITS hits (af_hit for the genome bwa calls, the first af_psl rows for BLAT).  These are
+        the only records the stages after S6 read (SURVEY §8 e)."""
         import torch
         torch.cuda.synchronize(self.dev)
         nq = min(int(self.n_q.item()), self.qcap)
         nt = min(int(self.tails["n"].item()), self.tcap)
         parts = []
-        for kind, n, rows, nh, hits in ((0, nq, self.q_rows, self.q_nh, self.q_hits),
-                                        (1, nt, self.tails["read"], self.t_nh, self.t_hits)):
+        for kind, n, rows, nh, hits, width, per in (
+                (0, nq, self.q_rows, self.q_nh, self.q_hits, HIT_WORDS, MAX_HITS),
+                (1, nt, self.tails["read"], self.t_nh, self.t_rows, PSL_WORDS, _blat.MAX_ROWS)):
             if n == 0:
                 continue
             r = rows[:n].long()
-            p = torch.empty((n, EX_WORDS), dtype=torch.int32, device=self.dev)
+            p = torch.zeros((n, EX_WORDS), dtype=torch.int32, device=self.dev)
             g = r + 2 * self.pair_base
             p[:, 0] = (g & 0xFFFFFFFF).to(torch.int32)
             p[:, 1] = (g >> 32).to(torch.int32)
@@ -196,8 +201,9 @@ class CandidateDiscovery:
             p[:, 5] = self.out["n_cigar"][r]
             p[:, 6:38] = self.out["cigar"][r]
             p[:, 38] = nh[:n]
-            h = hits[:n * MAX_HITS * HIT_WORDS * 4].view(torch.int32).view(n, MAX_HITS, HIT_WORDS)
-            p[:, 39:] = h[:, :EX_HITS].reshape(n, EX_HITS * HIT_WORDS)
+            h = hits[:n * per * width * 4].view(torch.int32).view(n, per, width)
+            k = min(EX_HITS * HIT_WORDS // width, per)
+            p[:, 39:39 + k * width] = h[:, :k].reshape(n, k * width)
             parts.append(p)
         if not parts:
             return torch.zeros((0, EX_WORDS), dtype=torch.int32, device=self.dev)

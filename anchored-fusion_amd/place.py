@@ -1,33 +1,20 @@
-"""GPU tail placement: the searches behind the partner stages (SURVEY.md §8 a4, a5, a7, a9,
-a10, a11, a13).
+"""GPU placement services behind the partner stages.
 
 The reference shells out for each of these searches:
 
-- `bwa mem` of the one-end-anchored pairs vs the genome (Anchored_Fusion.py:188);
-- `bwa mem` of the anchored split reads vs the genome (functions.py:716);
+- `bwa mem -M` of the one-end-anchored pairs vs the genome (Anchored_Fusion.py:188) and of the
+  anchored split reads (functions.py:716): `Reference` + `af_place`, the K2 seed-and-extend in
+  placement mode (every region scoring >= T per query), rendered by bwa_records with bwa's
+  record rules;
 - BLAT of tails and candidates vs the genome, the candidate blocks and the anchor
-  (functions.py:341, 530, 966, 1007, 1071, 1122, 1244).
+  (functions.py:341, 530, 966, 1007, 1071, 1122, 1244): `Placer`, the `place(targets, queries,
+  preset)` callback of partner.py, runs the BLAT restatement (blat.py, csrc/blat.hip) with each
+  call's options and returns PSL lines.
 
-Here one GPU multi-hit placement kernel (`af_place`, the K2 seed-and-extend in placement
-mode) serves all of them:
-
-- `Reference` joins contigs with runs of 512 N and indexes them once. Seeds cannot cross an
-  N run, and extension cannot score across one.
-- Every query gets up to 16 local alignments scoring at least T, best first. Each has a CIGAR,
-  forward query coordinates and the identical-base count.
-- `Placer` is the `place(targets, queries, preset)` callback the partner stages take
-  (partner.py). It renders hits as PSL rows; bwa_records renders them as the SAM records
-  `bwa mem -M` prints for the genome-alignment consumers.
-
-Placement parity with BLAT / bwa themselves is unpinned: neither is available (SURVEY.md §8 c).
-The kernel is bit-exact against oracle/af_oracle.c `afo_place` (tests/test_gpu_place.py).
-BLAT presets map onto the local aligner as follows:
-
-- minScore -> T;
-- minIdentity -> matches / max(query span, target span);
-- stepSize / minMatch / repMatch have no counterpart.
-
-Seeds are 16-mers, the smallest the index supports.
+`Reference` joins contigs with runs of 512 N and indexes them once; seeds cannot cross an N run
+and extension cannot score across one.  Parity with bwa / BLAT themselves is unpinned: neither
+is available (SURVEY.md §8 c).  The kernels are bit-exact against oracle/af_oracle.c `afo_place`
+and oracle/blat.c `afo_blat` (tests/test_gpu_place.py, tests/test_gpu_blat.py).
 """
 import bisect
 import ctypes
@@ -44,14 +31,9 @@ HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_s
                       ("t_end", "<i8"), ("cigar", "<u4", (32,))])
 assert HIT_DTYPE.itemsize == 176
 
-# BLAT option sets used by the reference -> (T, min identity %)
+# the genome bwa calls (AF:188, fn:716): bwa mem defaults (-k 19 -T 30)
 PRESET_PARAMS = {
-    "homologs": (50, 80),            # fn:341
-    "split_tail": (20, 0),           # fn:530
-    "candidate_homolog": (20, 0),    # fn:966
-    "anchored_split": (12, 90),      # fn:1007, 1071, 1122
-    "genome_validate": (20, 90),     # fn:1244
-    "genome_bwa": (30, 0),           # AF:188, fn:716 (bwa mem -T 30)
+    "genome_bwa": (30, 0),
 }
 
 _OPS = "MIDNSHP=X"
@@ -212,91 +194,60 @@ class Reference:
         return k, s, e
 
 
-def _cigar_counts(ops):
-    """(q inserts, q inserted bases, t inserts, t inserted bases, block sizes, q starts, t starts)."""
-    qi = qb = ti = tb = 0
-    sizes, qs, ts = [], [], []
-    x = y = 0
-    for c in ops:
-        n, o = int(c) >> 4, int(c) & 15
-        if o == 0:
-            sizes.append(n); qs.append(x); ts.append(y)
-            x += n; y += n
-        elif o == 1:
-            qi += 1; qb += n; x += n
-        elif o == 2:
-            ti += 1; tb += n; y += n
-        elif o == 4:
-            x += n
-    return qi, qb, ti, tb, sizes, qs, ts
-
-
-def psl_rows(ref, queries, hits, nh, min_identity=0):
-    """PSL lines (BLAT column layout) for the hits of queries [(name, seq)]."""
-    out = []
-    for qi, (qname, qseq) in enumerate(queries):
-        for k in range(max(int(nh[qi]), 0)):
-            h = hits[qi, k]
-            loc = ref.locate(h["t_start"], h["t_end"])
-            if loc is None:
-                continue
-            tk, ts, te = loc
-            qsp, tsp = int(h["q_end"] - h["q_start"]), te - ts
-            if min_identity and 100 * int(h["matches"]) < min_identity * max(qsp, tsp, 1):
-                continue
-            ops = h["cigar"][:int(h["n_cigar"])]
-            q_ins, q_ins_b, t_ins, t_ins_b, sizes, qst, tst = _cigar_counts(ops)
-            strand = "-" if h["flag"] & 0x10 else "+"
-            aligned = sum(sizes)
-            mism = aligned - int(h["matches"])
-            lead = int(ops[0]) >> 4 if len(ops) and (int(ops[0]) & 15) == 4 else 0
-            qs_list = ",".join(str(lead + v) for v in qst) + ","
-            ts_list = ",".join(str(ts + v) for v in tst) + ","
-            f = [int(h["matches"]), mism, 0, 0, q_ins, q_ins_b, t_ins, t_ins_b, strand, qname, len(qseq),
-                 int(h["q_start"]), int(h["q_end"]), ref.names[tk], ref.lens[tk], ts, te, len(sizes),
-                 ",".join(map(str, sizes)) + ",", qs_list, ts_list]
-            out.append("\t".join(map(str, f)) + "\n")
-    return out
-
-
-def preset_params(preset):
-    """af_params for one of the reference's BLAT / bwa option sets (PRESET_PARAMS): the bwa genome
-    calls keep bwa mem's -k 19, the BLAT presets seed from the index's 16-mers."""
+def preset_params(preset="genome_bwa"):
+    """af_params of the genome bwa calls: bwa mem's defaults (-k 19 -T 30)."""
     T, _ = PRESET_PARAMS[preset]
     p = _lib.default_params()
     p.T = T
-    p.min_seed_len = 19 if preset == "genome_bwa" else _lib.AF_K
+    p.min_seed_len = 19
     return p
 
 
 class Placer:
-    """The `place(targets, queries, preset)` callback of partner.py on the GPU.
+    """The `place(targets, queries, preset)` callback of partner.py (BLAT with the preset's
+    options, blat.PRESETS) and the genome `Reference` of the bwa calls.
 
-    Targets are indexed once per distinct target set (by identity of the list or its content)."""
+    Targets are indexed once per distinct target set (and tile step)."""
 
-    def __init__(self, device=0, max_hits=16, reference_factory=None):
+    def __init__(self, device=0, max_hits=16, reference_factory=None, tile_factory=None):
+        from . import blat
         self.device, self.max_hits = device, max_hits
         self.factory = reference_factory or (lambda contigs: Reference(contigs, device=device))
-        self._refs = {}
+        self.tile_factory = tile_factory or (lambda contigs, step: blat.TileReference(contigs, step, device=device))
+        self._refs, self._tiles = {}, {}
+
+    @staticmethod
+    def _key(targets):
+        return tuple((n, hash(s)) for n, s in targets)
 
     def reference(self, targets):
-        key = tuple((n, hash(s)) for n, s in targets)
+        key = self._key(targets)
         ref = self._refs.get(key)
         if ref is None:
             ref = self.factory([(n, s) for n, s in targets])
             self._refs[key] = ref
         return ref
 
+    def tiles(self, targets, step):
+        key = (self._key(targets), int(step))
+        ref = self._tiles.get(key)
+        if ref is None:
+            ref = self.tile_factory([(n, s) for n, s in targets], int(step))
+            self._tiles[key] = ref
+        return ref
+
     def params(self, preset):
         return preset_params(preset)
 
     def __call__(self, targets, queries, preset):
+        from . import blat
         header = ["psLayout version 3\n", "\n"]
         if not targets or not queries:
             return header
-        ref = self.reference(targets)
+        p = blat.params(preset)
+        ref = self.tiles(targets, p.step_size)
         # queries longer than the kernel's read limit (the anchor transcript itself, fn:341/966)
-        # are searched as overlapping windows; rows keep the full query's name and size
+        # are searched as overlapping windows; rows keep the full query's name, size and coordinates
         pieces = []  # (name, window seq, offset, full length)
         for name, seq in queries:
             if len(seq) <= _lib.AF_MAX_READ:
@@ -304,25 +255,15 @@ class Placer:
             else:
                 for off in range(0, max(1, len(seq) - WINDOW // 2), WINDOW // 2):
                     pieces.append((name, seq[off:off + WINDOW], off, len(seq)))
-        hits, nh = ref.raw_hits([w for _, w, _, _ in pieces], self.params(preset), self.max_hits)
-        min_id = PRESET_PARAMS[preset][1]
-        out = list(header)
-        for i, (name, w, off, full) in enumerate(pieces):
-            rows = psl_rows(ref, [(name, w)], hits[i:i + 1], nh[i:i + 1], min_id)
-            if off == 0 and full == len(w):
-                out += rows
-                continue
-            for r in rows:
-                f = r.rstrip("\n").split("\t")
-                f[10], f[11], f[12] = str(full), str(int(f[11]) + off), str(int(f[12]) + off)
-                f[19] = "".join(f"{int(v) + off}," for v in f[19].split(",") if v)
-                out.append("\t".join(f) + "\n")
-        return out
+        rows, nr = ref.search([w for _, w, _, _ in pieces], p, blat.MAX_ROWS)
+        return header + blat.psl_lines(ref, [(nm, w) for nm, w, _, _ in pieces], rows, nr,
+                                       offsets=[o for _, _, o, _ in pieces], full_sizes=[f for _, _, _, f in pieces])
 
     def close(self):
-        for r in self._refs.values():
+        for r in list(self._refs.values()) + list(self._tiles.values()):
             r.close()
         self._refs.clear()
+        self._tiles.clear()
 
 
 _FASTA_NAME = re.compile(r"^>(\S+)")

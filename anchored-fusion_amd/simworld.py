@@ -231,6 +231,12 @@ class GenomeWorld:
         from . import place
         return place.Reference.from_device(self.blob, self.names, self.lens, self.offsets, device=self.device)
 
+    def tiles(self, step_size=11):
+        """blat.TileReference over the genome in HBM (af_tile_index_build_device)."""
+        from . import blat
+        return blat.TileReference.from_device(self.blob, self.names, self.lens, self.offsets, step_size,
+                                              device=self.device)
+
     def simulate_pairs(self, n_pairs, read_len=150, seed=20251015, fusion_frac=0.05, frag_mean=200, frag_sd=20,
                        err=0.02, indel_frac=0.01, n_rate=0.0005, pair_base=0, out=None, src=None):
         """n_pairs distinct pairs into out (torch uint8 [2 n_pairs, read_len] on the device; made if

@@ -14,7 +14,8 @@ pass of discover.CandidateDiscovery over the resident pairs:
   S3  the samtools coordinate sort and the -f 8 / -f 4 / -F 772 partitions (AF:182, 186-194);
   S4  the one-end-anchored pairs (tmp1 / tmp2) and S5 the anchored split reads placed on the genome
       (`bwa mem -M genome`, AF:188 and functions.py:716);
-  S6  the split reads' tails placed on the genome (BLAT -minScore=20, functions.py:530);
+  S6  the split reads' tails searched on the genome with the BLAT restatement (-minScore=20,
+      functions.py:530; 11-mer tile index of the genome);
   and at N > 1 the all-gatherv of the breakpoint candidates (RCCL).
 Inputs are resident in HBM before timing starts.  At N > 1 the 50 M pairs are sharded on bwa's
 10 Mbase chunk grid (strong scaling, configs[3]).
@@ -287,8 +288,9 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     log(f"genome {W.total / 1e9:.2f} Gbp made in {t_gen:.1f} s")
     t0 = time.perf_counter()
     ref = W.reference()
+    tiles = W.tiles()
     t_idx = time.perf_counter() - t0
-    log(f"genome index built in {t_idx:.1f} s")
+    log(f"genome indexes (bwa-style 16-mer table, BLAT 11-mer tiles) built in {t_idx:.1f} s")
     lo, hi = shard_range(N, rank, world, L)
     n = hi - lo
     reads_t = torch.empty((2 * max(n, 1), L), dtype=torch.uint8, device=dev)
@@ -298,7 +300,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     log(f"{n} pairs simulated")
     W.blob = None  # the index keeps its own copy
     torch.cuda.empty_cache()
-    disc = discover.CandidateDiscovery(anchor, ref, n, L, device=gpu, inflight=max(1, args.inflight),
+    disc = discover.CandidateDiscovery(anchor, ref, tiles, n, L, device=gpu, inflight=max(1, args.inflight),
                                        batch_chunks=args.batch_chunks, pair_base=lo)
     G = disc.grp.inflight
     n_groups = (len(disc.batches) + G - 1) // G
@@ -392,6 +394,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         print(json.dumps(res), flush=True)
     disc.close()
     ref.close()
+    tiles.close()
 
 
 def cpu_baseline_c3(anchor, reads_t, args):
@@ -425,8 +428,8 @@ def cpu_baseline_c3(anchor, reads_t, args):
 class Placement:
     """Partner placement inside the step (SURVEY §8 d: S2 + partner placement).  Each batch's K3
     (af_align_candidates_tails_device) appends the split reads' soft-clipped tails (clip >= 20)
-    to a group-wide buffer; one af_place_device launch per group places them (BLAT
-    -minScore=20, functions.py:530; up to 16 hits per tail) on a reference of the workload's
+    to a group-wide buffer; one af_blat_device launch per group searches them (the BLAT
+    restatement with -minScore=20, functions.py:530) on a reference of the workload's
     transcripts (anchor, fusion partners, background; hash index) -- the bench workload has no
     genome.  A group's placement is enqueued in the next group, after its K1s and ahead of
     its first K2, so it runs beside that group's other K2s instead of idling the chip between
@@ -438,16 +441,17 @@ class Placement:
     def __init__(self, fworld, anchor, n_reads, L, G, dev):
         import torch
 
-        from anchored_fusion_amd import place
+        from anchored_fusion_amd import blat
         ctgs = [("anchor", anchor.decode())] + [(f"partner{k}", t.decode()) for k, t in enumerate(fworld["partners"])]
         ctgs += [(f"bg{k}", t.decode()) for k, t in enumerate(fworld["background"])]
-        self.ref = place.Reference(ctgs, device=dev.index)
-        self.params = place.preset_params("split_tail")
+        self.ref = blat.TileReference(ctgs, 11, device=dev.index)
+        self.params = blat.params("split_tail")
+        self.row_bytes = blat.PSL_DTYPE.itemsize * blat.MAX_ROWS
         self.n_reads, self.L = n_reads, L
         self.cap = G * max(1024, n_reads // 100)
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
         self.buf = [dict(tails=z(self.cap, L, dt=torch.uint8), tl=z(self.cap), tr=z(self.cap), nt=z(1),
-                         hits=z(self.cap * self.MAX_HITS * place.HIT_DTYPE.itemsize, dt=torch.uint8),
+                         hits=z(self.cap * self.row_bytes, dt=torch.uint8),
                          nh=z(self.cap)) for _ in range(2)]
         self.nt_last = z(1)
         self.fill, self.to_place, self.g, self.last, self.last_g = 0, None, 0, None, 1
@@ -462,9 +466,9 @@ class Placement:
     def _place(self, k, stream):
         import torch
         b = self.buf[k]
-        # the Reference's own context (queue heads, scratch): one placement at a time
-        self.ref.place_device(b["tails"], b["nt"], self.L, b["hits"], b["nh"], lens_t=b["tl"], params=self.params,
-                              max_hits=self.MAX_HITS, stream=stream)
+        # the TileReference's own context (queue heads, scratch): one search at a time
+        self.ref.search_device(b["tails"], b["nt"], self.L, b["hits"], b["nh"], lens_t=b["tl"], p=self.params,
+                               stream=stream)
         with torch.cuda.stream(stream):
             self.nt_last.copy_(b["nt"])
             b["nt"].zero_()
@@ -496,7 +500,7 @@ class Placement:
         return {"split_tails_per_batch": round(n_t / self.last_g, 1), "placed_fraction": round(placed / max(n_t, 1), 4),
                 "min_clip": self.MIN_CLIP,
                 "reference": "the workload's transcripts (anchor, 8 partners, 400 background), hash index",
-                "params": "T=20 (BLAT -minScore=20, functions.py:530), up to 16 hits per tail, one launch per group"}
+                "params": "BLAT restatement, -minScore=20 (functions.py:530), 11-mer tiles, one launch per group"}
 
 
 def _split_tails(reads, rec, min_clip):
@@ -527,8 +531,8 @@ def _split_tails(reads, rec, min_clip):
 def cpu_baseline(anchor, reads, args, fworld=None):
     """The CPU oracle (a port of the same algorithm; bwa and BLAT themselves are absent) timed on
     a bounded sample of this rank's batch: the first --cpu-sample pairs, repeated until
-    --cpu-seconds.  With fworld, each pass also cuts the split-read tails and places them
-    (afo_place, BLAT -minScore=20) on the same transcripts reference as the GPU step."""
+    --cpu-seconds.  With fworld, each pass also cuts the split-read tails and searches them
+    (afo_blat, -minScore=20) on the same transcripts reference as the GPU step."""
     import numpy as np
 
     import oracle
@@ -541,9 +545,8 @@ def cpu_baseline(anchor, reads, args, fworld=None):
     if fworld is not None:
         ctgs = [("anchor", anchor.decode())] + [(f"p{k}", t.decode()) for k, t in enumerate(fworld["partners"])]
         ctgs += [(f"bg{k}", t.decode()) for k, t in enumerate(fworld["background"])]
-        ref_ix = oracle.OracleIndex(place.concat_contigs(ctgs)[0])
-        po = oracle.default_params()
-        po.T, po.min_seed_len = 20, 16
+        ref_ix = oracle.OracleTiles(place.concat_contigs(ctgs)[0], 11)
+        po = oracle.blat_params(min_score=20)
     ix.align_pairs(sample, threads=threads)  # untimed warm-up pass (thread pool, first-touch pages)
     passes, dt, n_tails = 0, 0.0, 0
     while passes == 0 or dt < args.cpu_seconds:
@@ -554,7 +557,7 @@ def cpu_baseline(anchor, reads, args, fworld=None):
             n_tails = len(tails)
             if tails:
                 buf, ln = place.pack_queries(tails)
-                ref_ix.place(buf, ln, po, Placement.MAX_HITS, threads=threads)
+                ref_ix.blat(buf, ln, po, 16, threads=threads)
         dt += time.perf_counter() - t0
         passes += 1
     what = "S2 + tail placement" if ref_ix is not None else "S2"

@@ -23,7 +23,9 @@
  *                            `samtools view -f/-F` filters of Anchored_Fusion.py:186-194
  *   af_gather_reads_device <- `samtools fastq` of the S3 partitions (AF:186-188) and the split-read
  *                            FASTA of functions.py:705-716: the genome searches' queries
- *   af_index_build_genome <- `bwa index <genome>` (AF:173-178) / BLAT's tile index, GPU-built
+ *   af_index_build_genome <- `bwa index <genome>` (AF:173-178), GPU-built
+ *   af_tile_index_build / af_blat(_device) <- `blat [opts] target.fa query.fa out.psl`
+ *                            (functions.py:341, 530, 966, 1007, 1071, 1122, 1244)
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
  *
  * Conventions: plain pointers and sizes only; every function returns AF_OK (0) or a
@@ -196,6 +198,58 @@ int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, 
                           const int32_t *d_lens, const af_aln_out *d_out, int32_t min_clip, int64_t read_base,
                           int32_t append, int64_t cap, uint8_t *d_tails, int32_t *d_tail_lens,
                           int32_t *d_tail_read, int32_t *d_n_tails, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * BLAT searches (functions.py:341, 530, 966, 1007, 1071, 1122, 1244).  BLAT (Kent 2002) is a
+ * third-party binary, absent here; its published search is restated:
+ *   index   non-overlapping 11-mer tiles of the target every step_size bases (-stepSize, default
+ *           the tile size), tiles with N skipped, tiles occurring > rep_match times ignored;
+ *   hits    every 11-mer of the query and of its reverse complement looked up;
+ *   clumps  hits sorted by diagonal, split where successive diagonals drift by > max_gap + 2;
+ *           a clump needs >= min_match hits (-minMatch);
+ *   align   each clump's first tile extended both ways by banded DP (match +1, mismatch -1,
+ *           gap 3 + 1 per base, band 16, z-drop 20) and aligned globally for its blocks;
+ *   stitch  colinear alignments of one strand and target up to max_intron apart joined into one
+ *           multi-block hit (each joint one q / t insert), best chain first;
+ *   filter  PSL score = matches + repMatches/2 - misMatches - qNumInsert - tNumInsert >= min_score
+ *           and identity 100 - milliBad / 10 >= min_identity (pslCalcMilliBad, mRNA mode).
+ * One row per hit, the PSL columns (qStarts on the reverse-complemented query for '-'). */
+typedef struct {
+    int32_t step_size;     /* -stepSize (the index's; checked against it)                    */
+    int32_t min_match;     /* -minMatch (2)                                                   */
+    int32_t rep_match;     /* -repMatch (1024 x 11 / stepSize when not given)                 */
+    int32_t min_score;     /* -minScore (30)                                                  */
+    int32_t min_identity;  /* -minIdentity, percent (90)                                      */
+    int32_t max_gap;       /* -maxGap (2)                                                     */
+    int32_t max_intron;    /* -maxIntron (750000)                                             */
+} af_blat_params;
+
+#define AF_TILE 11
+#define AF_PSL_MAX_BLOCKS 16
+#define AF_BLAT_MAX_ROWS 16
+typedef struct {
+    int32_t query, strand;            /* strand 0 '+', 1 '-'                                       */
+    int32_t score;                    /* PSL score                                                 */
+    int32_t matches, mismatches, n_count;
+    int32_t q_num_insert, q_base_insert, t_num_insert, t_base_insert;
+    int32_t q_start, q_end, q_size, block_count;
+    int64_t t_start, t_end;           /* forward coordinates of the indexed sequence               */
+    int32_t block_sizes[AF_PSL_MAX_BLOCKS], q_starts[AF_PSL_MAX_BLOCKS];
+    int64_t t_starts[AF_PSL_MAX_BLOCKS];
+} af_psl;
+
+void af_blat_params_default(af_blat_params *p);
+/* tile index of `seq` (host or device bytes) for af_blat; step_size 1..11 */
+int af_tile_index_build(af_ctx *ctx, const char *seq, int64_t len, int32_t step_size, af_index **out);
+int af_tile_index_build_device(af_ctx *ctx, const char *d_seq, int64_t len, int32_t step_size, af_index **out);
+/* BLAT search of queries (host buffers, synchronous): rows[q * max_rows + k] for k < n_rows[q],
+ * best score first; max_rows 1..AF_BLAT_MAX_ROWS */
+int af_blat(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,
+            const int32_t *lens, const af_blat_params *p, int32_t max_rows, af_psl *rows, int32_t *n_rows);
+/* the same on device buffers, the query count read on the device (clamped to cap_queries) */
+int af_blat_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
+                   int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
+                   int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
 
 /* S3 on the device (Anchored_Fusion.py:182 `| samtools sort`, then AF:186-194): the records
  * d_flag/d_pos of n_reads reads (pair-major, as written by af_align_pairs*) in samtools'

@@ -150,3 +150,63 @@ class OracleIndex:
 HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_start", "<i4"), ("q_end", "<i4"),
                       ("q_size", "<i4"), ("matches", "<i4"), ("n_cigar", "<i4"), ("t_start", "<i8"),
                       ("t_end", "<i8"), ("cigar", "<u4", (32,))])
+
+PSL_DTYPE = np.dtype([(n, "<i4") for n in (
+    "query", "strand", "score", "matches", "mismatches", "n_count", "q_num_insert", "q_base_insert", "t_num_insert",
+    "t_base_insert", "q_start", "q_end", "q_size", "block_count")] + [
+    ("t_start", "<i8"), ("t_end", "<i8"), ("block_sizes", "<i4", (16,)), ("q_starts", "<i4", (16,)),
+    ("t_starts", "<i8", (16,))])
+assert PSL_DTYPE.itemsize == 328
+
+
+class BlatParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("step_size", "min_match", "rep_match", "min_score", "min_identity",
+                                                "max_gap", "max_intron")]
+
+
+def blat_params(**kw):
+    L = lib()
+    L.afo_blat_params_default.argtypes = [ctypes.POINTER(BlatParams)]
+    p = BlatParams()
+    L.afo_blat_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class OracleTiles:
+    """BLAT restatement (blat.c): the tile index of `seq` and its searches."""
+
+    def __init__(self, seq: bytes, step_size=11):
+        L = lib()
+        L.afo_tiles_build.restype = ctypes.c_void_p
+        L.afo_tiles_build.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int32]
+        L.afo_tiles_free.argtypes = [ctypes.c_void_p]
+        L.afo_blat.restype = ctypes.c_int
+        L.afo_blat.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                               ctypes.POINTER(BlatParams), ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_int]
+        self.seq = bytes(seq)
+        self.step = int(step_size)
+        self.h = L.afo_tiles_build(self.seq, len(self.seq), self.step)
+        if not self.h:
+            raise ValueError("reference shorter than a tile or bad step")
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.afo_tiles_free(self.h)
+            self.h = None
+
+    def blat(self, queries, lens=None, params=None, max_rows=16, threads=0):
+        """(rows [n, max_rows] PSL_DTYPE, n_rows [n])."""
+        q = np.ascontiguousarray(queries, dtype=np.uint8)
+        n = q.shape[0]
+        rows = np.zeros((n, max_rows), dtype=PSL_DTYPE)
+        nr = np.zeros(n, dtype=np.int32)
+        p = params or blat_params(step_size=self.step)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = lib().afo_blat(self.h, q.ctypes.data, n, q.shape[1], None if lp is None else lp.ctypes.data,
+                            ctypes.byref(p), max_rows, rows.ctypes.data, nr.ctypes.data, int(threads))
+        if rc != 0:
+            raise RuntimeError(f"afo_blat failed: {rc}")
+        return rows, nr

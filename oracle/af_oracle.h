@@ -102,6 +102,27 @@ int afo_align_pairs(const afo_index *idx, const uint8_t *reads, int64_t n_pairs,
 int afo_place(const afo_index *idx, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,
               const afo_params *p, int32_t max_hits, int n_threads, afo_hit *hits, int32_t *n_hits);
 
+/* BLAT restatement (blat.c): tile index, options, PSL rows (layout of af_psl, afgpu.h) */
+#define AFO_PSL_MAX_BLOCKS 16
+#define AFO_BLAT_MAX_ROWS 16
+typedef struct afo_tiles afo_tiles;
+typedef struct {
+    int32_t step_size, min_match, rep_match, min_score, min_identity, max_gap, max_intron;
+} afo_blat_params;
+typedef struct {
+    int32_t query, strand, score, matches, mismatches, n_count;
+    int32_t q_num_insert, q_base_insert, t_num_insert, t_base_insert;
+    int32_t q_start, q_end, q_size, block_count;
+    int64_t t_start, t_end;
+    int32_t block_sizes[AFO_PSL_MAX_BLOCKS], q_starts[AFO_PSL_MAX_BLOCKS];
+    int64_t t_starts[AFO_PSL_MAX_BLOCKS];
+} afo_psl;
+afo_tiles *afo_tiles_build(const char *seq, int64_t n, int32_t step);
+void afo_tiles_free(afo_tiles *X);
+void afo_blat_params_default(afo_blat_params *p);
+int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
+             const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads);
+
 #ifdef __cplusplus
 }
 #endif

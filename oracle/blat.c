@@ -1,0 +1,390 @@
+/*
+ * blat.c -- TEST INFRASTRUCTURE ONLY: CPU restatement of the BLAT searches of the partner
+ * stages (functions.py:341, 530, 966, 1007, 1071, 1122, 1244), the contract of the GPU kernel
+ * anchored-fusion_amd/csrc/blat.hip (bit-exact).
+ *
+ * BLAT (Kent 2002, Genome Res. 12:656; blat >= v.35, README.md:19) is a third-party binary,
+ * absent from /root/reference and from this image.  Its published search is restated with the
+ * options the reference passes (-stepSize, -minMatch, -repMatch, -minScore, -minIdentity,
+ * defaults otherwise); the steps and the choices this restatement makes are in afgpu.h
+ * (af_blat_params) and DESIGN.md §2.  Parity with the BLAT binary is unpinned.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "af_oracle.h"
+#include "af_oracle_int.h"
+
+#define TILE 11
+#define NKEYS (1u << (2 * TILE))
+#define MAXH 32768     /* tile hits per query strand (the first MAXH in query order) */
+#define MAXCL 4096     /* clumps per query strand (the first MAXCL in diagonal order) */
+#define MAXR 16        /* aligned clumps per query strand */
+#define NBLK_SHIFT 12  /* N counts per 4096-base block: stitching never crosses an N */
+
+struct afo_tiles {
+    uint8_t *T;        /* codes 0-3, 4 = N */
+    int64_t n;
+    int32_t step;
+    uint32_t *start;   /* NKEYS + 1 */
+    uint32_t *pos;     /* tile positions, ascending per key */
+    uint32_t *ncum;    /* N count before each 4096-base block */
+};
+
+afo_tiles *afo_tiles_build(const char *seq, int64_t n, int32_t step) {
+    if (n < TILE || step < 1 || step > TILE) return NULL;
+    afo_tiles *X = (afo_tiles *)calloc(1, sizeof(afo_tiles));
+    X->n = n; X->step = step;
+    X->T = (uint8_t *)malloc(n);
+    for (int64_t i = 0; i < n; ++i) X->T[i] = afo_nt4((uint8_t)seq[i]);
+    X->start = (uint32_t *)calloc(NKEYS + 1, sizeof(uint32_t));
+    int64_t nt = 0;
+    for (int64_t p = 0; p + TILE <= n; p += step) {
+        uint32_t k = 0;
+        int ok = 1;
+        for (int u = 0; u < TILE; ++u) {
+            if (X->T[p + u] > 3) { ok = 0; break; }
+            k |= (uint32_t)X->T[p + u] << (2 * u);
+        }
+        if (ok) { ++X->start[k + 1]; ++nt; }
+    }
+    for (uint32_t k = 0; k < NKEYS; ++k) X->start[k + 1] += X->start[k];
+    X->pos = (uint32_t *)malloc(sizeof(uint32_t) * (nt > 0 ? nt : 1));
+    uint32_t *fill = (uint32_t *)malloc(sizeof(uint32_t) * NKEYS);
+    memcpy(fill, X->start, sizeof(uint32_t) * NKEYS);
+    for (int64_t p = 0; p + TILE <= n; p += step) {
+        uint32_t k = 0;
+        int ok = 1;
+        for (int u = 0; u < TILE; ++u) {
+            if (X->T[p + u] > 3) { ok = 0; break; }
+            k |= (uint32_t)X->T[p + u] << (2 * u);
+        }
+        if (ok) X->pos[fill[k]++] = (uint32_t)p;
+    }
+    free(fill);
+    int64_t nb = (n >> NBLK_SHIFT) + 2;
+    X->ncum = (uint32_t *)calloc(nb, sizeof(uint32_t));
+    for (int64_t b = 0; b + 1 < nb; ++b) {
+        uint32_t c = 0;
+        for (int64_t i = b << NBLK_SHIFT; i < n && i < (b + 1) << NBLK_SHIFT; ++i) c += X->T[i] > 3;
+        X->ncum[b + 1] = X->ncum[b] + c;
+    }
+    return X;
+}
+
+void afo_tiles_free(afo_tiles *X) {
+    if (!X) return;
+    free(X->T); free(X->start); free(X->pos); free(X->ncum); free(X);
+}
+
+/* N bases in T[a, b) */
+static int64_t n_in(const afo_tiles *X, int64_t a, int64_t b) {
+    int64_t c = 0;
+    int64_t ba = a >> NBLK_SHIFT, bb = b >> NBLK_SHIFT;
+    if (ba == bb) {
+        for (int64_t i = a; i < b; ++i) c += X->T[i] > 3;
+        return c;
+    }
+    for (int64_t i = a; i < (ba + 1) << NBLK_SHIFT; ++i) c += X->T[i] > 3;
+    c += X->ncum[bb] - X->ncum[ba + 1];
+    for (int64_t i = bb << NBLK_SHIFT; i < b; ++i) c += X->T[i] > 3;
+    return c;
+}
+
+void afo_blat_params_default(afo_blat_params *p) {
+    p->step_size = TILE; p->min_match = 2; p->rep_match = 1024; p->min_score = 30;
+    p->min_identity = 90; p->max_gap = 2; p->max_intron = 750000;
+}
+
+/* the alignment scores of a clump's extension (afgpu.h) */
+static void blat_dp_params(afo_params *p) {
+    memset(p, 0, sizeof(*p));
+    p->a = 1; p->b = 1; p->o_del = 3; p->e_del = 1; p->o_ins = 3; p->e_ins = 1;
+    p->pen_clip5 = 0; p->pen_clip3 = 0; p->w = 16; p->zdrop = 20;
+}
+
+typedef struct { int64_t diag, t; int32_t q; } hit_t;
+typedef struct {
+    int32_t qb, qe, score, matches, mismatches, ncount, qni, qbi, tni, tbi, nb;
+    int64_t tb, te;
+    int32_t bsz[AFO_PSL_MAX_BLOCKS], bq[AFO_PSL_MAX_BLOCKS];
+    int64_t bt[AFO_PSL_MAX_BLOCKS];
+    int used;
+} reg_b;
+typedef struct { int32_t cnt, q; int64_t diag, t; } clump_t;
+
+static int cmp_hit(const void *a, const void *b) {
+    const hit_t *x = (const hit_t *)a, *y = (const hit_t *)b;
+    if (x->diag != y->diag) return x->diag < y->diag ? -1 : 1;
+    return x->q - y->q;
+}
+static int cmp_clump(const void *a, const void *b) {
+    const clump_t *x = (const clump_t *)a, *y = (const clump_t *)b;
+    if (x->cnt != y->cnt) return y->cnt - x->cnt;
+    if (x->diag != y->diag) return x->diag < y->diag ? -1 : 1;
+    return x->q - y->q;
+}
+
+/* one clump's seed tile (q, t) -> an aligned region with blocks; 0 if dropped */
+static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, int64_t t, reg_b *r) {
+    afo_params P;
+    blat_dp_params(&P);
+    int qle, tle, gtle, gscore, max_off;
+    int score, truesc, qb, qe;
+    int64_t tb, te;
+    if (q > 0) {
+        uint8_t qs[AFO_MAX_READ], ts[AFO_MAX_READ + 64];
+        int tl = (int)(t < q + P.w ? t : q + P.w);
+        for (int i = 0; i < q; ++i) qs[i] = Q[q - 1 - i];
+        for (int i = 0; i < tl; ++i) ts[i] = X->T[t - 1 - i];
+        score = afo_ext_dp(q, qs, tl, ts, &P, P.w, 0, P.zdrop, TILE * P.a, &qle, &tle, &gtle, &gscore, &max_off);
+        if (gscore <= 0 || gscore <= score) { qb = q - qle; tb = t - tle; truesc = score; }
+        else { qb = 0; tb = t - gtle; truesc = gscore; }
+    } else {
+        score = truesc = TILE * P.a; qb = 0; tb = t;
+    }
+    if (q + TILE < L) {
+        int qs0 = q + TILE;
+        int64_t t0 = t + TILE;
+        int64_t room = X->n - t0;
+        int tl = (int)(room < (L - qs0) + P.w ? room : (L - qs0) + P.w);
+        int sc0 = score;
+        score = afo_ext_dp(L - qs0, Q + qs0, tl, X->T + t0, &P, P.w, 0, P.zdrop, sc0, &qle, &tle, &gtle, &gscore,
+                           &max_off);
+        if (gscore <= 0 || gscore <= score) { qe = qs0 + qle; te = t0 + tle; truesc += score - sc0; }
+        else { qe = L; te = t0 + gtle; truesc += gscore - sc0; }
+    } else {
+        qe = L; te = t + TILE;
+    }
+    int lq = qe - qb, rl = (int)(te - tb);
+    if (lq <= 0 || rl <= 0) return 0;
+    int w2 = afo_infer_bw(lq, rl, truesc, P.a, P.o_del, P.e_del);
+    int w3 = afo_infer_bw(lq, rl, truesc, P.a, P.o_ins, P.e_ins);
+    w2 = w2 > w3 ? w2 : w3;
+    w2 = w2 < 64 ? w2 : 64;
+    uint32_t cig[AFO_MAX_CIGAR];
+    int nc = 0;
+    afo_gen_cigar(X->T, (int64_t)1 << 62, &P, w2, lq, Q + qb, tb, te, cig, &nc);
+    if (nc > AFO_MAX_CIGAR) return 0;
+    int xs = 0, xe = nc;
+    if (nc > 0 && (cig[0] & 0xf) == 2) { tb += cig[0] >> 4; xs = 1; }
+    else if (nc > 0 && (cig[nc - 1] & 0xf) == 2) { te -= cig[nc - 1] >> 4; xe = nc - 1; }
+    memset(r, 0, sizeof(*r));
+    int32_t x = qb;
+    int64_t y = tb;
+    for (int k = xs; k < xe; ++k) {
+        int len = (int)(cig[k] >> 4), op = (int)(cig[k] & 0xf);
+        if (op == 0) {
+            if (r->nb >= AFO_PSL_MAX_BLOCKS) return 0;
+            r->bsz[r->nb] = len; r->bq[r->nb] = x; r->bt[r->nb] = y; ++r->nb;
+            for (int u = 0; u < len; ++u) {
+                uint8_t a = Q[x + u], b = X->T[y + u];
+                if (a > 3 || b > 3) ++r->ncount;
+                else if (a == b) ++r->matches;
+                else ++r->mismatches;
+            }
+            x += len; y += len;
+        } else if (op == 1) {
+            ++r->qni; r->qbi += len; x += len;
+        } else {
+            ++r->tni; r->tbi += len; y += len;
+        }
+    }
+    if (r->nb == 0) return 0;
+    r->qb = qb; r->qe = qe; r->tb = tb; r->te = te;
+    r->score = r->matches - r->mismatches - r->qni - r->tni;
+    return 1;
+}
+
+/* r without its first k aligned bases (k inside the first block): the chain's query / target
+ * overlap with the previous part is given to that part; 0 if k does not fit */
+static int trim_front(const afo_tiles *X, const uint8_t *Q, const reg_b *r, int k, reg_b *o) {
+    *o = *r;
+    if (k <= 0) return 1;
+    if (k >= r->bsz[0]) return 0;
+    for (int u = 0; u < k; ++u) {
+        uint8_t a = Q[r->bq[0] + u], b = X->T[r->bt[0] + u];
+        if (a > 3 || b > 3) --o->ncount;
+        else if (a == b) --o->matches;
+        else --o->mismatches;
+    }
+    o->bsz[0] -= k; o->bq[0] += k; o->bt[0] += k;
+    o->qb = o->bq[0]; o->tb = o->bt[0];
+    o->score = o->matches - o->mismatches - o->qni - o->tni;
+    return 1;
+}
+
+/* trim of region b chained after region a: max(query overlap, target overlap, 0) */
+static int chain_trim(const reg_b *a, const reg_b *b) {
+    int64_t k = a->qe - b->qb;
+    if (a->te - b->tb > k) k = a->te - b->tb;
+    return k > 0 ? (int)k : 0;
+}
+
+static int psl_millibad(const afo_psl *o) {
+    int q_ali = o->q_end - o->q_start;
+    int64_t t_ali = o->t_end - o->t_start;
+    int64_t ali = q_ali < t_ali ? q_ali : t_ali;
+    if (ali <= 0) return 0;
+    int64_t size_dif = q_ali - t_ali;
+    if (size_dif < 0) size_dif = 0;  /* mRNA: a shorter query span is an intron, not an error */
+    int total = o->matches + o->mismatches;
+    if (total == 0) return 0;
+    return (int)((1000 * (o->mismatches + o->q_num_insert + round(3 * log(1. + (double)size_dif)))) / total);
+}
+
+static int tile_key(const uint8_t *Q, int q, uint32_t *k) {
+    *k = 0;
+    for (int u = 0; u < TILE; ++u) {
+        if (Q[q + u] > 3) return 0;
+        *k |= (uint32_t)Q[q + u] << (2 * u);
+    }
+    return 1;
+}
+
+/* one strand of one query: rows appended to out (n_out in/out) */
+static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, int L, int strand,
+                        int32_t qi, afo_psl *out, int *n_out, int cap_out, hit_t *hits, reg_b *regs) {
+    int nh = 0;
+    for (int q = 0; q + TILE <= L && nh < MAXH; ++q) {
+        uint32_t k;
+        if (!tile_key(Q, q, &k)) continue;
+        uint32_t lo = X->start[k], hi = X->start[k + 1];
+        if (hi == lo || (int64_t)(hi - lo) > bp->rep_match) continue;
+        for (uint32_t i = lo; i < hi && nh < MAXH; ++i) {
+            hits[nh].t = X->pos[i]; hits[nh].q = q; hits[nh].diag = (int64_t)X->pos[i] - q;
+            ++nh;
+        }
+    }
+    if (nh == 0) return;
+    qsort(hits, nh, sizeof(hit_t), cmp_hit);
+    clump_t *cl = (clump_t *)malloc(sizeof(clump_t) * MAXCL);
+    int ncl = 0;
+    for (int i = 0; i < nh && ncl < MAXCL;) {
+        int j = i, bq = i;
+        while (j + 1 < nh && hits[j + 1].diag - hits[j].diag <= bp->max_gap + 2) {
+            ++j;
+            if (hits[j].q < hits[bq].q || (hits[j].q == hits[bq].q && hits[j].t < hits[bq].t)) bq = j;
+        }
+        if (j - i + 1 >= bp->min_match) {
+            cl[ncl].cnt = j - i + 1; cl[ncl].q = hits[bq].q; cl[ncl].t = hits[bq].t; cl[ncl].diag = hits[bq].diag;
+            ++ncl;
+        }
+        i = j + 1;
+    }
+    qsort(cl, ncl, sizeof(clump_t), cmp_clump);  /* (hits desc, diagonal): keys are unique */
+    int nr = 0;
+    for (int c = 0; c < ncl && nr < MAXR; ++c) {
+        int32_t q = cl[c].q;
+        int64_t t = cl[c].t;
+        int skip = 0;
+        for (int r = 0; r < nr; ++r)
+            if (regs[r].qb <= q && q + TILE <= regs[r].qe && regs[r].tb <= t && t + TILE <= regs[r].te) { skip = 1; break; }
+        if (skip) continue;
+        if (align_clump(X, Q, L, q, t, &regs[nr])) ++nr;
+    }
+    free(cl);
+    /* regions in (qb, tb, qe) order for the chain DP */
+    for (int i = 1; i < nr; ++i)
+        for (int j = i; j > 0; --j) {
+            reg_b *a = &regs[j - 1], *b = &regs[j];
+            int gt = a->qb > b->qb || (a->qb == b->qb && (a->tb > b->tb || (a->tb == b->tb && a->qe > b->qe)));
+            if (!gt) break;
+            reg_b tmp = *a; *a = *b; *b = tmp;
+        }
+    int best[MAXR], prev[MAXR];
+    for (;;) {
+        int bi = -1;
+        for (int i = 0; i < nr; ++i) {
+            if (regs[i].used) continue;
+            best[i] = regs[i].score; prev[i] = -1;
+            for (int j = 0; j < i; ++j) {
+                if (regs[j].used) continue;
+                const reg_b *a = &regs[j];
+                reg_b b;
+                if (regs[i].qe <= a->qe || regs[i].te <= a->te) continue;
+                if (!trim_front(X, Q, &regs[i], chain_trim(a, &regs[i]), &b)) continue;
+                if (b.tb - a->te > bp->max_intron || n_in(X, a->te, b.tb)) continue;
+                int s = best[j] + b.score - (b.qb > a->qe) - (b.tb > a->te);
+                if (s > best[i]) { best[i] = s; prev[i] = j; }
+            }
+            if (bi < 0 || best[i] > best[bi]) bi = i;
+        }
+        if (bi < 0) break;
+        int chain[MAXR], m = 0;
+        for (int i = bi; i >= 0; i = prev[i]) chain[m++] = i;
+        afo_psl o;
+        memset(&o, 0, sizeof(o));
+        o.query = qi; o.strand = strand; o.q_size = L;
+        int ok = 1;
+        reg_b part[MAXR];
+        for (int c = m - 1; c >= 0; --c) {
+            regs[chain[c]].used = 1;
+            if (c == m - 1) part[c] = regs[chain[c]];
+            else trim_front(X, Q, &regs[chain[c]], chain_trim(&part[c + 1], &regs[chain[c]]), &part[c]);
+            const reg_b *r = &part[c];
+            if (c < m - 1) {
+                const reg_b *a = &part[c + 1];
+                if (r->qb > a->qe) { ++o.q_num_insert; o.q_base_insert += r->qb - a->qe; }
+                if (r->tb > a->te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(r->tb - a->te); }
+            }
+            o.matches += r->matches; o.mismatches += r->mismatches; o.n_count += r->ncount;
+            o.q_num_insert += r->qni; o.q_base_insert += r->qbi; o.t_num_insert += r->tni; o.t_base_insert += r->tbi;
+            for (int b = 0; b < r->nb; ++b) {
+                if (o.block_count >= AFO_PSL_MAX_BLOCKS) { ok = 0; break; }
+                o.block_sizes[o.block_count] = r->bsz[b]; o.q_starts[o.block_count] = r->bq[b];
+                o.t_starts[o.block_count] = r->bt[b]; ++o.block_count;
+            }
+        }
+        const reg_b *f = &part[m - 1], *l = &part[0];
+        o.q_start = strand ? L - l->qe : f->qb;
+        o.q_end = strand ? L - f->qb : l->qe;
+        o.t_start = f->tb; o.t_end = l->te;
+        o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
+        if (!ok || o.score < bp->min_score || psl_millibad(&o) > (100 - bp->min_identity) * 10) continue;
+        if (*n_out < cap_out) out[(*n_out)++] = o;
+    }
+}
+
+static int cmp_psl(const void *a, const void *b) {
+    const afo_psl *x = (const afo_psl *)a, *y = (const afo_psl *)b;
+    if (x->score != y->score) return y->score - x->score;
+    if (x->strand != y->strand) return x->strand - y->strand;
+    if (x->t_start != y->t_start) return x->t_start < y->t_start ? -1 : 1;
+    if (x->q_start != y->q_start) return x->q_start - y->q_start;
+    if (x->t_end != y->t_end) return x->t_end < y->t_end ? -1 : 1;
+    return x->q_end - y->q_end;
+}
+
+int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
+             const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads) {
+    if (!X || max_rows < 1 || max_rows > AFO_BLAT_MAX_ROWS || bp->step_size != X->step) return -1;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads > 0 ? threads : 1)
+    for (int64_t qi = 0; qi < n_queries; ++qi) {
+        int L = lens ? lens[qi] : stride;
+        if (L > stride) L = stride;
+        if (L > AFO_MAX_READ) L = AFO_MAX_READ;
+        if (L < 0) L = 0;
+        uint8_t Q[2][AFO_MAX_READ];
+        for (int i = 0; i < L; ++i) {
+            uint8_t c = afo_nt4(queries[qi * stride + i]);
+            Q[0][i] = c;
+            Q[1][L - 1 - i] = c > 3 ? 4 : 3 - c;
+        }
+        hit_t *hits = (hit_t *)malloc(sizeof(hit_t) * MAXH);
+        reg_b regs[MAXR];
+        afo_psl cand[2 * 2 * MAXR];
+        int nc = 0;
+        for (int s = 0; s < 2; ++s) {
+            memset(regs, 0, sizeof(regs));
+            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand, &nc, 2 * 2 * MAXR, hits, regs);
+        }
+        free(hits);
+        qsort(cand, nc, sizeof(afo_psl), cmp_psl);
+        int m = nc < max_rows ? nc : max_rows;
+        for (int k = 0; k < m; ++k) rows[qi * max_rows + k] = cand[k];
+        n_rows[qi] = m;
+    }
+    return 0;
+}

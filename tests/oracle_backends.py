@@ -40,6 +40,28 @@ class OracleReference:
         pass
 
 
+class OracleTileReference:
+    """The BLAT restatement's CPU contract (oracle/blat.c) behind Placer's tile_factory."""
+
+    def __init__(self, contigs, step):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob, self.offsets = concat_contigs(contigs)
+        self.total = len(blob)
+        self.step = int(step)
+        self.tiles = oracle.OracleTiles(blob, self.step)
+
+    def search(self, seqs, p, max_rows=16):
+        buf, lens = pack_queries(seqs)
+        op = oracle.blat_params(**{f: getattr(p, f) for f, _ in p._fields_})
+        return self.tiles.blat(buf, lens, op, max_rows, threads=8)
+
+    locate = OracleReference.locate
+
+    def close(self):
+        pass
+
+
 class OracleAligner:
     def __init__(self, anchor):
         self.ix = oracle.OracleIndex(anchor)

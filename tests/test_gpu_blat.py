@@ -1,0 +1,170 @@
+"""GPU BLAT restatement (af_tile_index_build / af_blat, csrc/blat.hip) vs the CPU contract
+(oracle/blat.c): every PSL field bit-exact, for each of the reference's option sets."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle_backends import OracleTileReference
+
+pytestmark = pytest.mark.gpu
+
+_B = np.frombuffer(b"ACGT", np.uint8)
+_COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+
+
+def _world(seed, n_ctg=3, ctg_len=400_000, repeats=True):
+    rng = np.random.default_rng(seed)
+    ctgs = []
+    rep = _B[rng.integers(0, 4, 300)].tobytes()
+    for k in range(n_ctg):
+        s = bytearray(_B[rng.integers(0, 4, ctg_len)].tobytes())
+        if repeats:  # a 300-nt family at ~2 % divergence, 1,500 copies per contig (repMatch, hit caps)
+            for _ in range(1500):
+                p = int(rng.integers(0, ctg_len - 300))
+                c = bytearray(rep)
+                for j in np.nonzero(rng.random(300) < 0.02)[0]:
+                    c[j] = b"ACGT"[(b"ACGT".index(c[j]) + int(rng.integers(1, 4))) % 4]
+                s[p:p + 300] = c
+        s[1000:1100] = b"N" * 100
+        ctgs.append((f"c{k}", s.decode()))
+    return ctgs, rep
+
+
+def _queries(ctgs, rep, seed, n=600):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, len(ctgs)))
+        g = ctgs[k][1].encode()
+        kind = i % 6
+        if kind == 0:  # short exact tails (12-40 nt)
+            ln = int(rng.integers(12, 41))
+            p = int(rng.integers(0, len(g) - ln))
+            q = g[p:p + ln]
+        elif kind == 1:  # reads with substitutions and an indel
+            ln = int(rng.integers(60, 151))
+            p = int(rng.integers(0, len(g) - ln - 5))
+            q = bytearray(g[p:p + ln])
+            for j in np.nonzero(rng.random(ln) < 0.03)[0]:
+                q[j] = b"ACGT"[(b"ACGT".index(q[j]) + 1) % 4] if q[j] in b"ACGT" else q[j]
+            j = int(rng.integers(10, ln - 10))
+            q = bytes(q[:j] + q[j + int(rng.integers(1, 4)):])
+        elif kind == 2:  # junction: two parts up to 50 kb apart (a stitched multi-block hit)
+            a, b = int(rng.integers(25, 90)), int(rng.integers(25, 90))
+            p = int(rng.integers(0, len(g) - 60_000))
+            p2 = p + a + int(rng.integers(100, 50_000))
+            q = g[p:p + a] + g[p2:p2 + b]
+        elif kind == 3:  # reverse strand
+            ln = int(rng.integers(20, 200))
+            p = int(rng.integers(0, len(g) - ln))
+            q = g[p:p + ln][::-1].translate(_COMP)
+        elif kind == 4:  # repeat-derived
+            q = rep[int(rng.integers(0, 150)):][:int(rng.integers(30, 150))]
+        else:  # random
+            q = _B[rng.integers(0, 4, int(rng.integers(11, 120)))].tobytes()
+        out.append(q.decode())
+    return out
+
+
+def _gpu_ref(ctgs, step):
+    from anchored_fusion_amd import blat
+    return blat.TileReference(ctgs, step)
+
+
+PRESETS = ["split_tail", "anchored_split", "genome_validate", "homologs", "candidate_homolog"]
+
+
+@pytest.mark.parametrize("preset", PRESETS)
+def test_blat_parity(preset):
+    from anchored_fusion_amd import blat
+    ctgs, rep = _world(11)
+    qs = _queries(ctgs, rep, 3)
+    p = blat.params(preset)
+    g = _gpu_ref(ctgs, p.step_size)
+    o = OracleTileReference(ctgs, p.step_size)
+    rg, ng = g.search(qs, p)
+    ro, no = o.search(qs, p)
+    assert np.array_equal(ng, no), np.nonzero(ng != no)[0][:10]
+    for i in range(len(qs)):
+        for k in range(ng[i]):
+            a, b = rg[i, k], ro[i, k]
+            for f in blat.PSL_DTYPE.names:
+                assert np.array_equal(a[f], b[f]), (preset, i, k, f, a[f], b[f])
+    assert ng.sum() > 0
+    g.close()
+
+
+def test_blat_finds_what_blat_finds():
+    """Behaviours the restatement keeps from BLAT: a 14-15 nt tail places with -stepSize=3
+    -minMatch=2 when two tiles fall on it, never with the default step 11; a two-exon read is one
+    multi-block hit; -minIdentity drops a diverged hit that -minScore keeps."""
+    from anchored_fusion_amd import blat
+    ctgs, _ = _world(5, n_ctg=1, repeats=False)
+    g = ctgs[0][1]
+    ref3, ref11 = _gpu_ref(ctgs, 3), _gpu_ref(ctgs, 11)
+    p3 = blat.params("anchored_split")
+    t15 = g[3002:3017]  # tiles at 3003 and 3006 (step 3) both inside
+    r, n = ref3.search([t15], p3)
+    assert n[0] >= 1 and r[0, 0]["t_start"] == 3002 and r[0, 0]["matches"] == 15
+    r, n = ref11.search([t15], blat.params("split_tail", min_score=12))
+    assert n[0] == 0
+    junction = g[50_000:50_070] + g[58_000:58_060]
+    r, n = ref11.search([junction], blat.params("split_tail"))
+    assert n[0] >= 1 and r[0, 0]["block_count"] == 2 and r[0, 0]["t_num_insert"] == 1
+    assert (r[0, 0]["t_start"], r[0, 0]["t_end"]) == (50_000, 58_060)
+    diverged = bytearray(g[90_000:90_125].encode())
+    for j in range(27, 27 + 6 * 13, 6):  # 13 mismatches: identity 89.6 %
+        diverged[j] = b"ACGT"[(b"ACGT".index(diverged[j]) + 1) % 4]
+    r, n = ref3.search([diverged.decode()], blat.params("genome_validate"))
+    assert n[0] == 0
+    r, n = ref3.search([diverged.decode()], blat.params("candidate_homolog"))
+    assert n[0] >= 1
+    ref3.close()
+    ref11.close()
+
+
+def test_blat_device_matches_host():
+    import torch
+
+    from anchored_fusion_amd import blat
+    from anchored_fusion_amd.place import pack_queries
+    ctgs, rep = _world(2, n_ctg=2)
+    qs = _queries(ctgs, rep, 9, n=300)
+    p = blat.params("split_tail")
+    ref = _gpu_ref(ctgs, p.step_size)
+    rh, nh = ref.search(qs, p)
+    buf, lens = pack_queries(qs)
+    dev = torch.device("cuda:0")
+    cap = len(qs) + 17
+    qt = torch.zeros((cap, buf.shape[1]), dtype=torch.uint8, device=dev)
+    qt[:len(qs)] = torch.from_numpy(buf).to(dev)
+    lt = torch.zeros(cap, dtype=torch.int32, device=dev)
+    lt[:len(qs)] = torch.from_numpy(lens).to(dev)
+    nq = torch.tensor([len(qs)], dtype=torch.int32, device=dev)
+    rows = torch.zeros(cap * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    nr = torch.zeros(cap, dtype=torch.int32, device=dev)
+    ref.search_device(qt, nq, buf.shape[1], rows, nr, lens_t=lt, p=p, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    nd = nr[:len(qs)].cpu().numpy()
+    rd = rows.cpu().numpy().view(blat.PSL_DTYPE).reshape(cap, blat.MAX_ROWS)[:len(qs)]
+    assert np.array_equal(nd, nh)
+    for i in range(len(qs)):
+        assert rd[i, :nd[i]].tobytes() == rh[i, :nh[i]].tobytes()
+    ref.close()
+
+
+def test_blat_tile_index_from_device_matches_host():
+    import torch
+
+    from anchored_fusion_amd import blat
+    from anchored_fusion_amd.place import concat_contigs
+    ctgs, rep = _world(4, n_ctg=2)
+    blob, offs = concat_contigs(ctgs)
+    bt = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda()
+    a = blat.TileReference.from_device(bt, [n for n, _ in ctgs], [len(s) for _, s in ctgs], offs, 3)
+    b = _gpu_ref(ctgs, 3)
+    qs = _queries(ctgs, rep, 1, n=120)
+    p = blat.params("anchored_split")
+    ra, na = a.search(qs, p)
+    rb, nb = b.search(qs, p)
+    assert np.array_equal(na, nb) and ra.tobytes() == rb.tobytes()

