@@ -45,13 +45,24 @@ struct Reg {
 };
 
 struct __attribute__((aligned(16))) BlatLds {
-    uint32_t hist[256];            // radix digit counts / bucket starts
+    uint32_t hist[AF_MAX_READ];    // radix digit counts (256) / per offset: first position index - first hit index
     uint8_t q0[AF_MAX_READ + 16];  // the query's codes (strand 0)
-    int32_t key[AF_MAX_READ];      // tile key per query offset of the current strand, -1 = none
+    int32_t base[AF_MAX_READ + 1];  // first hit index per query offset (exclusive scan of the counts)
     int32_t nh, ncl, nr, nrow, tmp[8];
     int32_t order[MAXR], best[MAXR], prev[MAXR], chain[MAXR];
 };
 __shared__ BlatLds g_bl;
+
+#ifdef AF_K2_PROF
+// profiling build only: per query [0..4] cycles in hits / sort / clumps / align / chain, [5] hits,
+// [6] clumps, [7] parts, [8] length, [9] total cycles, [10] drift-filter cycles, [11] hits kept
+__device__ int32_t *g_blprof = nullptr;
+#define BP(...) __VA_ARGS__
+#define BPM(k) BP({ const int64_t _n = clock64(); pc[k] += _n - tq; tq = _n; })
+#else
+#define BP(...)
+#define BPM(k)
+#endif
 
 __device__ __forceinline__ uint8_t nt4(uint8_t c) {
     switch (c) {
@@ -85,6 +96,60 @@ __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
         if (lane >= d) v += u;
     }
     return v;
+}
+
+__device__ __forceinline__ uint32_t bucket_hash(uint64_t b, int round, int bits) {
+    return (uint32_t)(((b ^ (0x632BE59BD9B4E019ull * (uint64_t)(round + 1))) * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+
+// The drift filter: a key (diagonal = key >> 9) is kept when another key may lie within drift of
+// its diagonal.  Buckets of 1 << wsh diagonals hashed into a 16K-bit "seen" map (g_z) and an
+// 8K-bit "seen twice" map (g_dp.t); a hash collision only keeps a key.
+__device__ __forceinline__ void drift_clear(int lane) {
+    static_assert(ZLDS >= 2048, "the drift filter needs 2 KB of g_z");
+    uint32_t *once = reinterpret_cast<uint32_t *>(g_z), *twice = reinterpret_cast<uint32_t *>(g_dp.t);
+    for (int x = lane; x < 512; x += 64) once[x] = 0;
+    for (int x = lane; x < 256; x += 64) twice[x] = 0;
+}
+__device__ __forceinline__ void drift_mark(uint64_t key, int wsh, int round) {
+    uint32_t *once = reinterpret_cast<uint32_t *>(g_z), *twice = reinterpret_cast<uint32_t *>(g_dp.t);
+    const uint32_t h = bucket_hash(key >> (9 + wsh), round, 14), bit = 1u << (h & 31);
+    if (atomicOr(&once[h >> 5], bit) & bit) {
+        const uint32_t g = h & 8191;
+        atomicOr(&twice[g >> 5], 1u << (g & 31));
+    }
+}
+// src[0, n) (marked for this round) -> dst: the keys kept, in order; returns their count
+__device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh, int round, int lane) {
+    const uint32_t *once = reinterpret_cast<const uint32_t *>(g_z), *twice = reinterpret_cast<const uint32_t *>(g_dp.t);
+    int nk = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = false;
+        uint64_t k = 0;
+        if (i < n) {
+            k = src[i];
+            const int64_t d = (int64_t)(k >> 9);
+            const uint64_t b = (uint64_t)d >> wsh, b0 = (uint64_t)(d - drift) >> wsh, b1 = (uint64_t)(d + drift) >> wsh;
+            const uint32_t h = bucket_hash(b, round, 14), g = h & 8191;
+            keep = (twice[g >> 5] >> (g & 31)) & 1u;
+            if (b0 != b) { const uint32_t h0 = bucket_hash(b0, round, 14); keep = keep || ((once[h0 >> 5] >> (h0 & 31)) & 1u); }
+            if (b1 != b) { const uint32_t h1 = bucket_hash(b1, round, 14); keep = keep || ((once[h1 >> 5] >> (h1 & 31)) & 1u); }
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) dst[nk + lanes_below_blat(m, lane)] = k;
+        nk += (int)__builtin_popcountll(m);
+    }
+    __threadfence_block();
+    wave_sync();
+    return nk;
+}
+__device__ int drift_filter(const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh, int round, int lane) {
+    drift_clear(lane);
+    wave_sync();
+    for (int i = lane; i < n; i += 64) drift_mark(src[i], wsh, round);
+    wave_sync();
+    return drift_keep(src, dst, n, drift, wsh, round, lane);
 }
 
 // stable LSD radix sort of a[0, n) by bits [lo, lo + 8 * passes) on the wave, ping-ponging with
@@ -308,44 +373,94 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
         for (int x = lane; x < L; x += 64) B.q0[x] = nt4(queries[qi * (int64_t)stride + x]);
         if (lane == 0) B.nrow = 0;
         wave_sync();
+        const int64_t drift = (int64_t)bp.max_gap + 2;
+        int wsh = 3;  // bucket width 1 << wsh >= 2 * drift: [d - drift, d + drift] meets <= 2 buckets
+        while ((1ll << wsh) < 2 * drift) ++wsh;
+        BP(int64_t tq0 = clock64(), tq = tq0; int64_t pc[6] = {0, 0, 0, 0, 0, 0}; int ch = 0, cc_ = 0, cr = 0, cs = 0;)
         for (int strand = 0; strand < 2; ++strand) {
             for (int x = lane; x < L; x += 64) {
                 const uint8_t c = B.q0[strand ? L - 1 - x : x];
                 D.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
             }
             wave_sync();
-            // ---- the query's tile keys (-1: N inside or a tile over rep_match / absent) ---------------
-            for (int q = lane; q < L; q += 64) {
-                uint32_t k;
-                int32_t v = -1;
+            // ---- per offset: its tile's position range (count 0: N inside, absent or over rep_match) --
+            const bool filt = bp.min_match >= 2;
+            if (filt) drift_clear(lane);  // round 0 of the drift filter is marked while collecting
+            uint32_t *DEL = B.hist;       // first position index - first hit index, per offset
+            int carry = 0;
+            for (int q0 = 0; q0 < L; q0 += 64) {
+                const int q = q0 + lane;
+                uint32_t k, c = 0, lo = 0;
                 if (q + TILE <= L && tile_key(D.q, q, k)) {
-                    const uint32_t c = X.start[k + 1] - X.start[k];
-                    if (c > 0 && (int64_t)c <= bp.rep_match) v = (int32_t)k;
+                    lo = X.start[k];
+                    c = X.start[k + 1] - lo;
+                    if ((int64_t)c > bp.rep_match) c = 0;
                 }
-                B.key[q] = v;
+                const int inc = wave_incl_sum((int)c, lane);
+                const int bq = carry + inc - (int)c;
+                if (q < L) { DEL[q] = lo - (uint32_t)bq; B.base[q] = bq; }
+                carry += __builtin_amdgcn_readlane(inc, 63);
             }
             wave_sync();
-            // ---- every hit, the first NMAX in (offset, position) order ------------------------------
-            int nh = 0;
-            for (int q = 0; q + TILE <= L && nh < NMAX; ++q) {
-                const int32_t k = B.key[q];
-                if (k < 0) continue;
-                const uint32_t lo = X.start[k], c = X.start[k + 1] - lo;
-                for (uint32_t u0 = 0; u0 < c && nh < NMAX; u0 += 64) {
-                    const uint32_t u = u0 + lane;
-                    if (u < c && nh + (int)(u - u0) < NMAX)
-                        KA[nh + (u - u0)] = ((uint64_t)((int64_t)X.pos[lo + u] - q + 1024) << 9) | (uint32_t)q;
-                    nh = min(NMAX, nh + (int)min(64u, c - u0));
+            // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
+            // in flight --------------------------------------------------------------------------
+            const int nh_all = min(carry, NMAX);
+            for (int h0 = 0; h0 < nh_all; h0 += 256) {
+                int qv[4];
+                uint32_t pv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int h = h0 + 64 * j + lane;
+                    int lo_q = 0, hi_q = L - 1;  // the last offset whose first hit index is <= h
+                    while (lo_q < hi_q) {
+                        const int mid = (lo_q + hi_q + 1) >> 1;
+                        if (B.base[mid] <= h) lo_q = mid;
+                        else hi_q = mid - 1;
+                    }
+                    qv[j] = lo_q;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int h = h0 + 64 * j + lane;
+                    pv[j] = h < nh_all ? X.pos[DEL[qv[j]] + (uint32_t)h] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int h = h0 + 64 * j + lane;
+                    if (h < nh_all) {
+                        const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
+                        KA[h] = key;
+                        if (filt) drift_mark(key, wsh, 0);
+                    }
                 }
             }
+            int nh = nh_all;
             __threadfence_block();
             wave_sync();
             if (nh == 0) continue;
+            BPM(0);
+            BP(ch += nh;)
+            // ---- drop hits with no other hit within the drift (they cannot join a clump of
+            // min_match >= 2 hits, and removing them changes no other run): hashed bucket bitmaps,
+            // false keeps only, a few rounds while they pay ---------------------------------------
+            uint64_t *H0 = KA, *H1 = KB;
+            if (filt)
+                for (int round = 0; round < 3 && (round == 0 || nh > 256); ++round) {
+                    const int nk = round == 0 ? drift_keep(H0, H1, nh, drift, wsh, 0, lane)
+                                              : drift_filter(H0, H1, nh, drift, wsh, round, lane);
+                    uint64_t *t = H0; H0 = H1; H1 = t;
+                    const bool stop = nk * 8 > nh * 7;
+                    nh = nk;
+                    if (stop) break;
+                }
+            BPM(5);
+            BP(cs += nh;)
+            if (nh == 0) continue;
             // ---- sort by diagonal (stable: offsets ascending within a diagonal) ------------------
-            const uint64_t *S = wave_radix_sort(KA, KB, nh, 9, diag_passes, lane);
-            uint32_t *ST = reinterpret_cast<uint32_t *>(S == KA ? KB : KA);
+            const uint64_t *S = wave_radix_sort(H0, H1, nh, 9, diag_passes, lane);
+            uint32_t *ST = reinterpret_cast<uint32_t *>(S == H0 ? H1 : H0);
+            BPM(1);
             // ---- run starts, then the clumps (runs of min_match hits) in diagonal order -----------
-            const int64_t drift = (int64_t)bp.max_gap + 2;
             int nrun = 0;
             for (int i0 = 0; i0 < nh; i0 += 64) {
                 const int i = i0 + lane;
@@ -390,6 +505,8 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
             __threadfence_block();
             wave_sync();
             const uint64_t *CO = wave_radix_sort(KA, KB, ncl, 32, 2, lane);
+            BPM(2);
+            BP(cc_ += ncl;)
             // ---- parts: one per clump whose seed lies in no earlier part -------------------------
             int nr = 0;
             for (int c = 0; c < ncl && nr < MAXR; ++c) {
@@ -405,6 +522,8 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
                 wave_sync();
             }
             if (nr == 0) continue;
+            BPM(3);
+            BP(cr += nr;)
             // ---- parts in (qb, tb, qe) order, then chains, best first -----------------------------
             if (lane == 0) {
                 for (int i = 1; i < nr; ++i)
@@ -491,6 +610,7 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
                 wave_sync();
             }
         }
+        BPM(4);
         // ---- rows of both strands, best first ---------------------------------------------------
         if (lane == 0) {
             const int n = B.nrow;
@@ -503,6 +623,13 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
             const int m = n < max_rows ? n : max_rows;
             for (int k = 0; k < m; ++k) rows[qi * max_rows + k] = RW[k];
             n_rows[qi] = m;
+            BP(if (g_blprof && qi < (1 << 22)) {
+                int32_t *pf = g_blprof + qi * 16;
+                for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
+                pf[5] = ch; pf[6] = cc_; pf[7] = cr; pf[8] = L;
+                pf[9] = (int32_t)min(clock64() - tq0, (int64_t)0x7fffffff);
+                pf[10] = (int32_t)min(pc[5], (int64_t)0x7fffffff); pf[11] = cs;
+            })
         }
         __threadfence_block();
         wave_sync();
@@ -575,6 +702,20 @@ int af_blat_slots(int n_cu) {
         occ = 8;
     return n_cu * occ;
 }
+
+#ifdef AF_K2_PROF
+extern "C" int af_debug_blat_prof_enable() {
+    int32_t *d = nullptr;
+    if (hipMalloc(&d, sizeof(int32_t) * 16 << 22) != hipSuccess) return -1;
+    (void)hipMemset(d, 0, sizeof(int32_t) * 16 << 22);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_blprof), &d, sizeof d) == hipSuccess ? 16 : -1;
+}
+extern "C" int af_debug_blat_prof_read(int32_t *host, int64_t n) {
+    int32_t *d = nullptr;
+    if (hipMemcpyFromSymbol(&d, HIP_SYMBOL(g_blprof), sizeof d) != hipSuccess || !d) return -1;
+    return hipMemcpy(host, d, sizeof(int32_t) * 16 * n, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // builds X's device arrays from d_seq (device bytes): allocations go to allocs[*na] (freed with
 // the index); returns a HIP error or hipSuccess

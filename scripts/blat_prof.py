@@ -1,0 +1,46 @@
+"""Per-query phase cycles of k_blat on the configs[2] tails (profiling build libafgpu_prof.so).
+
+python scripts/blat_prof.py [pairs] [out.json]   (GPU; make -C anchored-fusion_amd/csrc prof first)
+"""
+import json
+import os
+import sys
+
+os.environ["AF_GPU_LIB"] = "libafgpu_prof.so"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import afpkg  # noqa: F401,E402
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from anchored_fusion_amd import _lib, discover, simworld  # noqa: E402
+from anchored_fusion_amd import io as afio  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8_000_160
+out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/blat_prof.json"
+anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
+W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=1.0)
+ref, tiles = W.reference(), W.tiles()
+reads = W.simulate_pairs(N, read_len=150, seed=20251015)
+L = _lib.lib()
+assert L.af_debug_blat_prof_enable() == 16
+d = discover.CandidateDiscovery(anchor, ref, tiles, N, 150, device=0)
+d.run(reads)
+torch.cuda.synchronize()
+nt = min(int(d.tails["n"].item()), d.tcap)
+P = np.zeros((nt, 16), dtype=np.int32)
+assert L.af_debug_blat_prof_read(P.ctypes.data_as(__import__("ctypes").c_void_p), nt) == 0
+names = ["hits", "sort", "clumps", "align", "chain"]
+tot = P[:, 9].astype(np.int64)
+res = dict(tails=nt, mean_cycles={n: float(P[:, k].mean()) for k, n in enumerate(names)},
+           mean_total=float(tot.mean()), mean_filter_cycles=float(P[:, 10].mean()), mean_kept=float(P[:, 11].mean()), pct_total={p: float(np.percentile(tot, p)) for p in (50, 90, 99, 99.9)},
+           mean_hits=float(P[:, 5].mean()), mean_clumps=float(P[:, 6].mean()), mean_parts=float(P[:, 7].mean()),
+           mean_len=float(P[:, 8].mean()),
+           slowest=[dict(zip(names + ["hits_n", "clumps_n", "parts_n", "len", "total"], map(int, P[i, :10])))
+                    for i in np.argsort(-tot)[:20]])
+# share of the summed cycles in the slowest 1% of the queries
+o = np.sort(tot)[::-1]
+res["top1pct_share"] = float(o[:max(1, nt // 100)].sum() / max(1, o.sum()))
+os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps({k: v for k, v in res.items() if k != "slowest"}, indent=1))
