@@ -40,6 +40,23 @@ class AlignResult:
     def mapped(self):
         return (self.flag & 0x4) == 0
 
+    # the record API consume_gene reads (shared with shard.SparseCandidates)
+    @property
+    def n_reads(self):
+        return len(self.flag)
+
+    def flag_at(self, r):
+        return int(self.flag[r])
+
+    def pos_at(self, r):
+        return int(self.pos[r])
+
+    def n_mapped(self):
+        return int(((self.flag & 4) == 0).sum())
+
+    def partition(self):
+        return partition(self)
+
 
 class AnchorAligner:
     """One GPU context + one anchor index.  Not thread-safe (one host thread per GPU)."""

@@ -9,8 +9,16 @@ working, and do nothing:
 - the filter-model flags (Model.py is outside SURVEY.md §8), so every run behaves as
   `--not_filter_false_positive`;
 - `--thread` (host threads; the searches run on the GPU).
+
+`--gpus N` (N > 1) runs one process per GPU: the command relaunches itself under
+`torch.distributed.run` (a child process; this process never touches the GPU), each rank takes
+GPU LOCAL_RANK and joins an RCCL process group; S2 is sharded over the ranks (pipeline.run,
+shard.py) and single-cell batches are dealt out to them (singlecell.run).
 """
 import argparse
+import os
+import socket
+import subprocess
 import sys
 
 from . import pipeline
@@ -33,6 +41,7 @@ def parser():
     ap.add_argument("--negative_samples", type=str, default="./Model/negative_samples.txt", help="(accepted, unused)")
     ap.add_argument("--thread", type=str, default="1", help="(accepted, unused)")
     ap.add_argument("--gpu_number", type=str, default="-1", help="GPU index (-1: the first visible GPU)")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node to shard the pairs over (one process each)")
     return ap
 
 
@@ -54,23 +63,75 @@ def parser_singlecell():
     ap.add_argument("--thread", type=str, default="1", help="(accepted, unused)")
     ap.add_argument("--gpu_number", type=str, default="-1", help="GPU index (-1: the first visible GPU)")
     ap.add_argument("--batch_pairs", type=int, default=1 << 22, help="pairs of whole cells per GPU alignment batch")
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node to deal the cell batches to (one process each)")
     return ap
+
+
+def _launch(n, script, argv):
+    """Runs `script argv` as n ranks under torch.distributed.run (127.0.0.1 rendezvous) in a
+    child process and returns its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", script] + list(argv)
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def _rank_device(args):
+    """Inside a launched job: join the process group (RCCL on GPUs, gloo otherwise) and return
+    this rank's GPU (LOCAL_RANK); outside one: --gpu_number."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+        return local
+    dev = int(args.gpu_number)
+    return dev if dev >= 0 else 0
+
+
+def _finish():
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _script(name):
+    return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), name)
 
 
 def main_singlecell(argv=None):
     from . import singlecell
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parser_singlecell().parse_args(argv)
-    dev = int(args.gpu_number)
-    singlecell.run(args.file_anchored_cds, args.fastq_dir, args.file_ref_seq, args.file_ref_ann, args.out_folder,
-                   gene_names=args.gene_names or None, device=dev if dev >= 0 else 0, batch_pairs=args.batch_pairs)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch(args.gpus, _script("run_anchored_fusion_singlecell.py"), argv)
+    dev = _rank_device(args)
+    try:
+        singlecell.run(args.file_anchored_cds, args.fastq_dir, args.file_ref_seq, args.file_ref_ann,
+                       args.out_folder, gene_names=args.gene_names or None, device=dev, batch_pairs=args.batch_pairs)
+    finally:
+        _finish()
     return 0
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parser().parse_args(argv)
-    dev = int(args.gpu_number)
-    pipeline.run(args.file_anchored_cds, args.fastq1, args.fastq2, args.file_ref_seq, args.file_ref_ann,
-                 args.out_folder, gene_names=args.gene_names or None, device=dev if dev >= 0 else 0)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch(args.gpus, _script("run_anchored_fusion.py"), argv)
+    dev = _rank_device(args)
+    try:
+        pipeline.run(args.file_anchored_cds, args.fastq1, args.fastq2, args.file_ref_seq, args.file_ref_ann,
+                     args.out_folder, gene_names=args.gene_names or None, device=dev)
+    finally:
+        _finish()
     return 0
 
 

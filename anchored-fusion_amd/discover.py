@@ -210,23 +210,12 @@ class CandidateDiscovery:
         return torch.cat(parts) if len(parts) > 1 else parts[0]
 
     def exchange(self, group=None):
-        """All-gatherv of pack() across the ranks (counts all-gather, then one max-padded
-        all_gather: RCCL has no v-variant).  Returns the gathered rows on the device, rank order."""
-        import torch
+        """All-gatherv of pack() across the ranks (shard.allgatherv_device: counts all-gather, then
+        one max-padded all_gather; RCCL has no v-variant).  Returns the gathered rows on the
+        device, rank order.  A gloo group (CPU tests) gathers host copies."""
         import torch.distributed as dist
+        from .shard import allgatherv_device
         rows = self.pack()
-        world = dist.get_world_size(group)
-        cdev = self.dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
-        cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=cdev)
-        cnts = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(cnts, cnt, group=group)
-        counts = [int(c.item()) for c in cnts]
-        mx = max(counts)
-        if mx == 0:
-            return rows
-        pad = torch.zeros((mx, EX_WORDS), dtype=torch.int32, device=cdev)
-        pad[:rows.shape[0]] = rows.to(cdev)
-        bufs = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(bufs, pad, group=group)
-        return torch.cat([b[:c] for b, c in zip(bufs, counts)]).to(self.dev)
-
+        if dist.get_backend(group) == "nccl":
+            return allgatherv_device(rows, group)
+        return allgatherv_device(rows.cpu(), group).to(self.dev)

@@ -28,7 +28,6 @@ import re
 
 from . import blocks as blk
 from . import genome_check, partner, report, splitreads
-from .align import partition
 from .annotation import ExonIndex
 from .io import read_fasta, read_pairs
 
@@ -127,14 +126,13 @@ def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, align
 def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=print):
     """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads``."""
     anchor_rec = [(gene, anchor)]
-    flag, pos = res.flag, res.pos
     width = reads.shape[1]
 
     def seq(r):  # only the reads the partitions select are decoded
         return bytes(reads[r, : (lens[r] if lens is not None else width)]).decode()
 
-    tmp1, tmp2, anchored = partition(res)
-    log(f"[{gene}] S2: {int(((flag & 4) == 0).sum())} of {len(flag)} reads on the anchor; "
+    tmp1, tmp2, anchored = res.partition()
+    log(f"[{gene}] S2: {res.n_mapped()} of {res.n_reads} reads on the anchor; "
         f"{len(tmp1)} one-end-anchored pairs; {len(anchored)} anchored records")
     # S4: one-end-anchored pairs on the genome, paired as bwa pairs tmp1.fq / tmp2.fq (samtools
     # fastq restores the sequenced orientation of both ends)
@@ -144,9 +142,9 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     # anchored.bam as `samtools view` prints it (SEQ reverse-complemented for 0x10)
     anch_lines = []
     for r in anchored:
-        cig = res.cigar_str(r)
-        sq = revcomp(seq(r)) if flag[r] & 0x10 else seq(r)
-        anch_lines.append(sam_line(names[r // 2], int(flag[r]) & 0xFFFF, gene, int(pos[r]) + 1, cig, sq))
+        cig, f = res.cigar_str(r), res.flag_at(r)
+        sq = revcomp(seq(r)) if f & 0x10 else seq(r)
+        anch_lines.append(sam_line(names[r // 2], f & 0xFFFF, gene, res.pos_at(r) + 1, cig, sq))
     # S5: split reads vs the genome
     fasta = genome_check.split_read_fasta(anch_lines)
     gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam_se(fasta) if fasta else []) for ln in recs]
@@ -169,9 +167,29 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     return cands
 
 
+def dist_world(group=None):
+    """(rank, world) of the torch.distributed job this process is in, (0, 1) outside one."""
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover - torch is part of the image
+        return 0, 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
 def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, log=print):
-    """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt."""
+        aligner_factory=None, log=print, group=None):
+    """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt.
+
+    Inside a torch.distributed job of N > 1 ranks (cli --gpus N: one process per GPU, `device`
+    = this rank's GPU), S2 is sharded: every rank aligns whole bwa chunks of the pairs and the
+    candidate records are all-gathered on the device (shard.align_sharded); rank 0 then runs
+    S3-S8 and writes the tables, the other ranks return {}."""
+    rank, world = dist_world(group)
+    if world > 1:
+        return _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device,
+                            searches, aligner_factory, log, group, rank, world)
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
@@ -196,3 +214,47 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
                                  os.path.join(folder, gene + "_fusion"), log=log)
     return results
 
+
+
+def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device, searches,
+                 aligner_factory, log, group, rank, world):
+    import torch
+    import torch.distributed as dist
+    from . import shard
+    genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
+        else gene_names_from_fasta(anchored_cds)
+    anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
+    names, reads, lens = read_pairs(fastq1, fastq2)
+    if aligner_factory is None:
+        from .align import AnchorAligner
+
+        def aligner_factory(anchor):
+            return AnchorAligner(anchor, device=device)
+    on_gpu = torch.cuda.is_available() and dist.get_backend(group) == "nccl"
+    dev = f"cuda:{device}" if on_gpu else None
+    genome = gtf = index = None
+    if rank == 0:
+        genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
+        with open(ref_ann) as fh:
+            gtf = fh.readlines()
+        index = ExonIndex.from_lines(gtf)
+        if searches is None:
+            searches = Searches(genome, device=device)
+    results = {}
+    for gene, anchor in zip(genes, anchors):
+        aligner = aligner_factory(anchor.encode())
+        try:
+            res = shard.align_sharded(aligner, reads, lens, rank, world, group=group, device=dev)
+        finally:
+            close = getattr(aligner, "close", None)
+            if close:
+                close()
+        if rank == 0:
+            folder = os.path.join(out_folder, gene + "_fusion")
+            os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
+            log(f"[{gene}] S2 over {world} ranks: {len(res.reads)} candidate records gathered")
+            homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+            results[gene] = consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches,
+                                         os.path.join(folder, gene + "_fusion"), log=log)
+    dist.barrier(group)
+    return results

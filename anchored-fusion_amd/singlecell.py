@@ -32,7 +32,7 @@ from . import partner
 from .align import AlignResult
 from .annotation import ExonIndex
 from .io import read_fasta, read_pairs
-from .pipeline import Searches, consume_gene, gene_names_from_fasta, gene_names_from_file
+from .pipeline import Searches, consume_gene, dist_world, gene_names_from_fasta, gene_names_from_file
 
 
 def discover_cells(fastq_dir):
@@ -133,7 +133,12 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
         gtf = fh.readlines()
     index = ExonIndex.from_lines(gtf)
     cells = discover_cells(fastq_dir)
-    data = [read_pairs(os.path.join(fastq_dir, f1), os.path.join(fastq_dir, f2)) for _, f1, f2 in cells]
+    # one process per GPU (cli --gpus N): the cells are dealt out round-robin and every rank
+    # ingests and runs S2-S8 on its own cells only (no data exchange: each cell is its own run,
+    # SC:205-256); rank 0 merges the per-cell tables once every rank is done
+    rank, world = dist_world()
+    data = {k: read_pairs(os.path.join(fastq_dir, cells[k][1]), os.path.join(fastq_dir, cells[k][2]))
+            for k in range(rank, len(cells), world)}
     if searches is None:
         searches = Searches(genome, device=device)
     if aligner_factory is None:
@@ -142,15 +147,15 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
         def aligner_factory(anchor):
             return AnchorAligner(anchor, device=device)
     # whole cells per GPU batch
-    groups, cur, n = [], [], 0
-    for k, (_, reads, _) in enumerate(data):
+    mine, cur, n = [], [], 0
+    for k, (_, reads, _) in data.items():
         if cur and n + reads.shape[0] // 2 > batch_pairs:
-            groups.append(cur)
+            mine.append(cur)
             cur, n = [], 0
         cur.append(k)
         n += reads.shape[0] // 2
     if cur:
-        groups.append(cur)
+        mine.append(cur)
     results = {}
     for gene, anchor in zip(genes, anchors):
         out_name = gene + "_fusion"
@@ -160,7 +165,7 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
         homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
         aligner = aligner_factory(anchor.encode())
         try:
-            for grp in groups:
+            for grp in mine:
                 reads, lens = _concat([data[k] for k in grp])
                 # every cell is its own bwa run (read ids and insert-size chunks restart per cell)
                 seg = [data[k][1].shape[0] // 2 for k in grp]
@@ -181,5 +186,9 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
             close = getattr(aligner, "close", None)
             if close:
                 close()
-        results[gene] = merge_cell_tables(cells, work, out_name, os.path.join(temp_folder, out_name))
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        if rank == 0:
+            results[gene] = merge_cell_tables(cells, work, out_name, os.path.join(temp_folder, out_name))
     return results

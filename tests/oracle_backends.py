@@ -63,11 +63,12 @@ class OracleTileReference:
 
 
 class OracleAligner:
-    def __init__(self, anchor):
+    def __init__(self, anchor, chunk_bases=None):
         self.ix = oracle.OracleIndex(anchor)
+        self.chunk_bases = chunk_bases
 
-    def align_pairs(self, reads, lens=None):
-        o = self.ix.align_pairs(reads, lens, threads=8)
+    def align_pairs(self, reads, lens=None, pair_base=0):
+        o = self.ix.align_pairs(reads, lens, threads=8, pair_base=pair_base, chunk_bases=self.chunk_bases)
         return AlignResult(o["flag"], o["pos"], o["score"], o["n_cigar"], o["cigar"], o["hits"])
 
     def close(self):
