@@ -61,7 +61,8 @@ __shared__ S2Lds g_s2;
 
 #ifdef AF_K2_PROF
 // profiling build only (make prof): per-item phase cycles of K2 and K3c (scripts/s2_prof.py)
-__device__ int32_t *g_s2prof = nullptr;  // K2 items at [item * 16], K3c items at [(1 << 22) + item * 16]
+__device__ int32_t *g_s2prof = nullptr;  // K2 items at [item * 16], K3c items at [S2PROF_K3 + item * 16] (1 M items each)
+constexpr int64_t S2PROF_K3 = (int64_t)1 << 24;
 #define SPROF(...) __VA_ARGS__
 __shared__ int64_t g_sub[5];  // K2 seeding sub-phase marks (pmems, pass 1, pass 2, pass 3)
 #else
@@ -1766,7 +1767,7 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
             pl.ovf = E.ovf[0] | E.ovf[1] << 1;
         }
         SPROF(if (lane == 0 && g_s2prof) {
-            int32_t *pf = g_s2prof + (1 << 22) + (int64_t)item * 16;
+            int32_t *pf = g_s2prof + S2PROF_K3 + (int64_t)item * 16;
             const int64_t c4 = clock64();
             pf[0] = (int32_t)pp; pf[1] = (int32_t)(c4 - c0); pf[2] = (int32_t)(c1 - c0); pf[3] = (int32_t)(c2 - c1);
             pf[4] = (int32_t)(c3 - c2); pf[6] = nsw; pf[7] = E.na[0]; pf[8] = E.na[1];
@@ -1892,7 +1893,7 @@ __global__ __launch_bounds__(64, 6) void k_s2_records(DevText X, const uint8_t *
                     af_emit_tail(tails, reads, stride, lens, r, flag, out.cigar + r * AF_MAX_CIGAR);
             }
         }
-        SPROF(if (lane == 0 && g_s2prof) g_s2prof[(1 << 22) + (int64_t)item * 16 + 5] = (int32_t)(clock64() - c0);)
+        SPROF(if (lane == 0 && g_s2prof) g_s2prof[S2PROF_K3 + (int64_t)item * 16 + 5] = (int32_t)(clock64() - c0);)
         wave_sync();
     }
 }
@@ -1951,7 +1952,7 @@ __global__ __launch_bounds__(1024) void k_s2_chunks(int64_t n_pairs, int32_t str
 #ifdef AF_K2_PROF
 extern "C" int af_debug_s2_prof_enable() {
     int32_t *d = nullptr;
-    const size_t n = (size_t)2 << 22;
+    const size_t n = (size_t)2 << 24;
     if (hipMalloc(&d, sizeof(int32_t) * n) != hipSuccess) return -1;
     (void)hipMemset(d, 0, sizeof(int32_t) * n);
     return hipMemcpyToSymbol(HIP_SYMBOL(g_s2prof), &d, sizeof d) == hipSuccess ? 16 : -1;
@@ -1960,7 +1961,7 @@ extern "C" int af_debug_s2_prof_read(int32_t *host, int64_t n_k2, int64_t n_k3) 
     int32_t *d = nullptr;
     if (hipMemcpyFromSymbol(&d, HIP_SYMBOL(g_s2prof), sizeof d) != hipSuccess || !d) return -1;
     if (hipMemcpy(host, d, sizeof(int32_t) * 16 * n_k2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    return hipMemcpy(host + 16 * n_k2, d + (1 << 22), sizeof(int32_t) * 16 * n_k3, hipMemcpyDeviceToHost) == hipSuccess
+    return hipMemcpy(host + 16 * n_k2, d + S2PROF_K3, sizeof(int32_t) * 16 * n_k3, hipMemcpyDeviceToHost) == hipSuccess
                ? 0 : -1;
 }
 #endif
