@@ -26,6 +26,10 @@
 
 #include "ksw_dp.h"
 
+#ifndef AF_BLAT_WPS
+#define AF_BLAT_WPS 6  // k_blat waves per SIMD (launch bound: VGPR budget)
+#endif
+
 namespace {
 
 constexpr int TILE = AF_TILE;
@@ -99,7 +103,8 @@ __device__ __forceinline__ int wave_incl_sum(int v, int lane) {
 }
 
 __device__ __forceinline__ uint32_t bucket_hash(uint64_t b, int round, int bits) {
-    return (uint32_t)(((b ^ (0x632BE59BD9B4E019ull * (uint64_t)(round + 1))) * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+    const uint32_t x = (uint32_t)b ^ (uint32_t)(b >> 32) ^ (0x632BE59Bu * (uint32_t)(round + 1));
+    return (x * 0x9E3779B1u) >> (32 - bits);
 }
 
 // The drift filter: a key (diagonal = key >> 9) is kept when another key may lie within drift of
@@ -133,8 +138,8 @@ __device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t dri
             const uint64_t b = (uint64_t)d >> wsh, b0 = (uint64_t)(d - drift) >> wsh, b1 = (uint64_t)(d + drift) >> wsh;
             const uint32_t h = bucket_hash(b, round, 14), g = h & 8191;
             keep = (twice[g >> 5] >> (g & 31)) & 1u;
-            if (b0 != b) { const uint32_t h0 = bucket_hash(b0, round, 14); keep = keep || ((once[h0 >> 5] >> (h0 & 31)) & 1u); }
-            if (b1 != b) { const uint32_t h1 = bucket_hash(b1, round, 14); keep = keep || ((once[h1 >> 5] >> (h1 & 31)) & 1u); }
+            const uint64_t bn = b0 != b ? b0 : b1;  // the bucket width is >= 2 drift: one neighbour at most
+            if (bn != b) { const uint32_t hn = bucket_hash(bn, round, 14); keep = keep || ((once[hn >> 5] >> (hn & 31)) & 1u); }
         }
         const uint64_t m = __ballot(keep);
         if (keep) dst[nk + lanes_below_blat(m, lane)] = k;
@@ -335,7 +340,7 @@ __device__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, u
 }
 
 template <int CPL>
-__global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
+__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
                                                         int32_t stride, const int32_t *__restrict__ lens,
                                                         af_blat_params bp, const int32_t *__restrict__ n_q,
                                                         int64_t cap, int32_t *__restrict__ heads,
@@ -405,20 +410,19 @@ __global__ __launch_bounds__(64, AF_K2_WPS) void k_blat(DevTile X, const uint8_t
             // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
             // in flight --------------------------------------------------------------------------
             const int nh_all = min(carry, NMAX);
+            int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
             for (int h0 = 0; h0 < nh_all; h0 += 256) {
                 int qv[4];
                 uint32_t pv[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int h = h0 + 64 * j + lane;
-                    int lo_q = 0, hi_q = L - 1;  // the last offset whose first hit index is <= h
-                    while (lo_q < hi_q) {
-                        const int mid = (lo_q + hi_q + 1) >> 1;
-                        if (B.base[mid] <= h) lo_q = mid;
-                        else hi_q = mid - 1;
-                    }
-                    qv[j] = lo_q;
+                    int q = qc;  // the last offset whose first hit index is <= h
+                    if (h < nh_all)
+                        while (q + 1 < L && B.base[q + 1] <= h) ++q;
+                    qv[j] = q;
                 }
+                qc = __builtin_amdgcn_readlane(qv[3], 63);  // (a full group: lane 63 of chunk 3 is a hit)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int h = h0 + 64 * j + lane;
