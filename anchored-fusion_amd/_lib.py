@@ -35,7 +35,7 @@ EXPORTS = (
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
     "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_index_build_genome_device", "af_gather_reads_device", "af_blat_params_default", "af_tile_index_build",
-    "af_tile_index_build_device", "af_blat", "af_blat_device", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
+    "af_tile_index_build_device", "af_blat", "af_blat_device", "af_blat_device_range", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close",
 )
 
@@ -145,6 +145,8 @@ def lib():
     L.af_blat.restype = ctypes.c_int
     L.af_blat_device.argtypes = [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp, _vp]
     L.af_blat_device.restype = ctypes.c_int
+    L.af_blat_device_range.argtypes = [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp, _vp]
+    L.af_blat_device_range.restype = ctypes.c_int
     L.af_fastq_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_vp)]
     L.af_fastq_open.restype = ctypes.c_int
     L.af_fastq_next.argtypes = [_vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i32), ctypes.POINTER(_i64)]

@@ -118,8 +118,9 @@ class TileReference:
         return rows, nr
 
     def search_device(self, queries_t, n_queries_t, stride, rows_t, n_rows_t, lens_t=None, p=None, max_rows=MAX_ROWS,
-                      stream=None):
-        """af_blat_device on device buffers (rows_t: cap * max_rows * 328 bytes)."""
+                      stream=None, first_t=None):
+        """af_blat_device on device buffers (rows_t: cap * max_rows * 328 bytes); first_t (an int32
+        device word, optional): search only the queries from *first_t on (af_blat_device_range)."""
         from .align import _stream_handle
         cap = int(queries_t.shape[0])
         if queries_t.dim() != 2 or int(queries_t.shape[1]) < int(stride):
@@ -128,10 +129,11 @@ class TileReference:
             raise ValueError("rows_t / n_rows_t too small for cap queries")
         if lens_t is not None and lens_t.numel() < cap:
             raise ValueError("lens_t holds fewer than cap entries")
-        _lib.check(self.ctx, _lib.lib().af_blat_device(
-            self.ctx, self.idx, queries_t.data_ptr(), n_queries_t.data_ptr(), cap, int(stride),
-            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(p or params()), int(max_rows),
-            rows_t.data_ptr(), n_rows_t.data_ptr(), _stream_handle(stream)), "af_blat_device")
+        _lib.check(self.ctx, _lib.lib().af_blat_device_range(
+            self.ctx, self.idx, queries_t.data_ptr(), None if first_t is None else first_t.data_ptr(),
+            n_queries_t.data_ptr(), cap, int(stride), None if lens_t is None else lens_t.data_ptr(),
+            ctypes.byref(p or params()), int(max_rows), rows_t.data_ptr(), n_rows_t.data_ptr(),
+            _stream_handle(stream)), "af_blat_device_range")
 
     def locate(self, t_start, t_end):
         import bisect

@@ -246,7 +246,8 @@ hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t 
 // k_blat's per-wave global scratch (blat.hip layout) and its resident waves on n_cu CUs
 constexpr size_t AF_BLAT_SLOT_BYTES = 704 << 10;
 int af_blat_slots(int n_cu);
-hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
+                          int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
                           hipStream_t s);

@@ -999,7 +999,7 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         (lens && (e = hipMemcpyAsync(d_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s)) != hipSuccess ||
         (e = hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
-        (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, n_queries, stride, lens ? d_lens : nullptr, *p,
+        (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride, lens ? d_lens : nullptr, *p,
                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows, s)) !=
             hipSuccess ||
         (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -1012,6 +1012,13 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
 int af_blat_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
                    int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
+    return af_blat_device_range(c, ix, d_queries, nullptr, d_n_queries, cap_queries, stride, d_lens, p, max_rows,
+                                d_rows, d_n_rows, stream);
+}
+
+int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_first,
+                         const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
+                         const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
     if (!c || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_rows || !d_n_rows)))
         return fail(c, AF_E_INVALID, "null argument");
     int rc = check_blat(c, ix, p, stride, max_rows);
@@ -1023,7 +1030,7 @@ int af_blat_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, cons
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
     HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
-    HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, cap_queries, stride, d_lens, *p,
+    HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
                              c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows, s));
     return AF_OK;
 }

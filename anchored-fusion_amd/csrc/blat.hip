@@ -343,7 +343,8 @@ template <int CPL>
 __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
                                                         int32_t stride, const int32_t *__restrict__ lens,
                                                         af_blat_params bp, const int32_t *__restrict__ n_q,
-                                                        int64_t cap, int32_t *__restrict__ heads,
+                                                        const int32_t *__restrict__ q_first, int64_t cap,
+                                                        int32_t *__restrict__ heads,
                                                         uint8_t *__restrict__ bscratch, int32_t diag_passes,
                                                         af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
                                                         int32_t max_rows) {
@@ -352,6 +353,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
     const int lane = threadIdx.x;
     const int64_t nq64 = *n_q < cap ? *n_q : cap;
     const int nq = (int)(nq64 < 0 ? 0 : nq64);
+    const int q0 = q_first ? max(0, min(*q_first, nq)) : 0;  // queries [q0, nq)
     uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
     uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
     Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             int v = 0;
             if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
             v = __builtin_amdgcn_readfirstlane(v);
-            const int64_t it = head + 8 * (int64_t)v;
+            const int64_t it = q0 + head + 8 * (int64_t)v;
             if (it < nq) { item = (int)it; break; }
             head = (head + 1) & 7;
             --heads_left;
@@ -680,7 +682,8 @@ __global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, uint32_
 
 }  // namespace
 
-hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
+                          int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
                           hipStream_t s) {
@@ -689,7 +692,8 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
     const int diag_passes = (bits + 7) / 8;
     const int cpl = (stride + 1 + 63) / 64;
     dim3 g(n_slots), b(64);
-#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, cap, heads, \
+#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, q_first, cap, \
+                                    heads, \
                                     bscratch, diag_passes, rows, n_rows, max_rows)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);

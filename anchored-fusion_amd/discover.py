@@ -109,8 +109,21 @@ class CandidateDiscovery:
                 rows0.append(r0)
             done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done,
                                        tails=lambda j, rows0=rows0: self._tails(j, rows0[j]))
+        # S6 (BLAT -minScore=20 of the split-read tails that K3d cut during S2) needs no S3: it
+        # runs on a stream of its own (the tile index has its own context and scratch) beside S3,
+        # the gathers and S4 / S5, whose sort syncs and placement tail leave the chip part idle.
+        # (Searching each group's tails while the next group aligns was slower: both are
+        # compute-bound, 156 vs 145 ms per C3 step.)
+        # The stream is slot 1's (idle once S2 is done): a stream of its own would share one of
+        # the 4 hardware queues (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work.
+        s6 = self.grp.streams[1] if G > 1 else s0
         for e in done:
+            s6.wait_event(e)
             s0.wait_event(e)
+        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
+                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s6)
+        s6_done = torch.cuda.Event()
+        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
         if _DEBUG:
             s0.synchronize()
             _log("S2 done")
@@ -138,11 +151,10 @@ class CandidateDiscovery:
             _log(f"gathered {int(self.n_q.item())} queries, {int(self.tails['n'].item())} tails")
         if phase_events:
             phase_events[2].record(s0)
-        # S4 + S5 on the genome (bwa mem -M defaults), S6 tails (BLAT -minScore=20)
+        # S4 + S5 on the genome (bwa mem -M defaults); then join S6
         self.ref.place_device(self.q, self.n_q, self.L, self.q_hits, self.q_nh, lens_t=self.q_lens,
                               params=self.p_genome, max_hits=MAX_HITS, stream=s0)
-        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
-                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s0)
+        s0.wait_event(s6_done)
         if _DEBUG:
             s0.synchronize()
             _log("placements done")

@@ -250,6 +250,13 @@ int af_blat(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_
 int af_blat_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
                    int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
+/* af_blat_device over the queries [*d_first, min(*d_n_queries, cap_queries)) only (both device
+ * words, read when the launch runs): a batch of queries still being appended to a buffer (the
+ * split-read tails of the S2 batches done so far) is searched while later batches append.
+ * Rows of query k still go to d_rows[k * max_rows ..]. */
+int af_blat_device_range(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_first,
+                         const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
+                         const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
 
 /* S3 on the device (Anchored_Fusion.py:182 `| samtools sort`, then AF:186-194): the records
  * d_flag/d_pos of n_reads reads (pair-major, as written by af_align_pairs*) in samtools'
