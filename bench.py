@@ -83,6 +83,18 @@ def pmc_traffic(pairs, read_len):
     return None
 
 
+def issue_roofline():
+    """The compute-bound kernels of the C3 step against their VALU issue roofline, from the
+    committed counter pass (profiles/r02/pmc_valu_c3.json; one batch in flight), or None."""
+    try:
+        pm = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_valu_c3.json")))
+    except (OSError, ValueError):
+        return None
+    return {"source": "profiles/r02/pmc_valu_c3.json", "model": pm.get("issue_model"),
+            "kernels": {k: {f: e[f] for f in ("avg_duration_us", "unit", "valu_per_unit", "issue_frac", "wait_any_frac")}
+                        for k, e in pm.get("kernels", {}).items()}}
+
+
 def cpu_threads(args):
     """The host CPU share: OMP_NUM_THREADS (16 per GPU on the box, where os.cpu_count() shows the
     whole machine), else every core."""
@@ -380,7 +392,9 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         "counts_per_step": summ,
         "phases_ms": {"s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
                       "gather_queries": round(phase(2, 3), 3), "genome_placement": round(phase(3, 4), 3),
-                      "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3"},
+                      "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
+                              "the S6 BLAT runs on slot 1's stream from the end of s2, beside s3_partition, "
+                              "gather_queries and genome_placement, which ends by joining it"},
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
             "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -393,6 +407,9 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         "setup_s": {"genome": round(t_gen, 2), "index": round(t_idx, 2)},
         "hbm_in_use_gib": round((total - free) / 2**30, 1),
     }
+    issue = issue_roofline()
+    if issue:
+        res["issue_roofline"] = issue
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline_c3(anchor, reads_t, args)
     if rank == 0:
