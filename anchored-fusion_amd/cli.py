@@ -5,10 +5,11 @@
 
 Outputs go to `<out_folder>/<G>_fusion/<G>_fusion_predictions{,_abridged}.txt`, as in
 AF:138-141 and Final_fusion. Some flags are accepted only so that existing command lines keep
-working, and do nothing:
-- the filter-model flags (Model.py is outside SURVEY.md §8), so every run behaves as
-  `--not_filter_false_positive`;
-- `--thread` (host threads; the searches run on the GPU).
+working, and do nothing: `--not_train_filter_model`, `--positive_samples`, `--homo_gene_file`,
+`--negative_samples` (training is outside SURVEY.md §8) and `--thread` (host threads; the searches
+run on the GPU).  Without `--not_filter_false_positive` the filter model `--model_file` scores
+the candidates (AF:212-225); a missing model file is reported and the run continues unfiltered,
+as the reference does.
 
 `--gpus N` (N > 1) runs one process per GPU: the command relaunches itself under
 `torch.distributed.run` (a child process; this process never touches the GPU), each rank takes
@@ -33,9 +34,9 @@ def parser():
     ap.add_argument("--out_folder", type=str, default="./", help="The folder of the output file")
     ap.add_argument("--file_ref_seq", type=str, required=True, help="The reference sequence file")
     ap.add_argument("--file_ref_ann", type=str, required=True, help="The reference annotation file")
-    ap.add_argument("--not_filter_false_positive", action="store_true", help="(always on: no filter model)")
+    ap.add_argument("--not_filter_false_positive", action="store_true", help="Do not score candidates with the filter model")
     ap.add_argument("--not_train_filter_model", action="store_true", help="(accepted, unused)")
-    ap.add_argument("--model_file", type=str, default="./data/model.pt", help="(accepted, unused)")
+    ap.add_argument("--model_file", type=str, default="./data/model.pt", help="The filter model (Model.py state_dict)")
     ap.add_argument("--positive_samples", type=str, default="./data/positive_samples.txt", help="(accepted, unused)")
     ap.add_argument("--homo_gene_file", type=str, default="./data/homo_gene.npy", help="(accepted, unused)")
     ap.add_argument("--negative_samples", type=str, default="./Model/negative_samples.txt", help="(accepted, unused)")
@@ -54,9 +55,9 @@ def parser_singlecell():
     ap.add_argument("--out_folder", type=str, default="./", help="The folder of the output file")
     ap.add_argument("--file_ref_seq", type=str, required=True, help="The reference sequence file")
     ap.add_argument("--file_ref_ann", type=str, required=True, help="The reference annotation file")
-    ap.add_argument("--not_filter_false_positive", action="store_true", help="(always on: no filter model)")
+    ap.add_argument("--not_filter_false_positive", action="store_true", help="Do not score candidates with the filter model")
     ap.add_argument("--not_train_filter_model", action="store_true", help="(accepted, unused)")
-    ap.add_argument("--model_file", type=str, default="./data/model.pt", help="(accepted, unused)")
+    ap.add_argument("--model_file", type=str, default="./data/model.pt", help="The filter model (Model.py state_dict)")
     ap.add_argument("--positive_samples", type=str, default="./data/positive_samples.txt", help="(accepted, unused)")
     ap.add_argument("--homo_gene_file", type=str, default="./data/homo_gene.npy", help="(accepted, unused)")
     ap.add_argument("--negative_samples", type=str, default="./Model/negative_samples.txt", help="(accepted, unused)")
@@ -102,6 +103,14 @@ def _finish():
             dist.destroy_process_group()
 
 
+def _filter(args, dev):
+    """The filter step's settings (AF:212-225), None with --not_filter_false_positive."""
+    if args.not_filter_false_positive:
+        return None
+    import torch
+    return dict(model_file=args.model_file, device=f"cuda:{dev}" if torch.cuda.is_available() else "cpu")
+
+
 def _script(name):
     return os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), name)
 
@@ -115,7 +124,8 @@ def main_singlecell(argv=None):
     dev = _rank_device(args)
     try:
         singlecell.run(args.file_anchored_cds, args.fastq_dir, args.file_ref_seq, args.file_ref_ann,
-                       args.out_folder, gene_names=args.gene_names or None, device=dev, batch_pairs=args.batch_pairs)
+                       args.out_folder, gene_names=args.gene_names or None, device=dev, batch_pairs=args.batch_pairs,
+                       filt=_filter(args, dev))
     finally:
         _finish()
     return 0
@@ -129,7 +139,7 @@ def main(argv=None):
     dev = _rank_device(args)
     try:
         pipeline.run(args.file_anchored_cds, args.fastq1, args.fastq2, args.file_ref_seq, args.file_ref_ann,
-                     args.out_folder, gene_names=args.gene_names or None, device=dev)
+                     args.out_folder, gene_names=args.gene_names or None, device=dev, filt=_filter(args, dev))
     finally:
         _finish()
     return 0

@@ -25,14 +25,21 @@ the same outputs in eval mode and, under the same torch seed, in train mode; and
 own `Test_model` (file in, scores out, seeded before the network is built) gives the scores
 `score_test_file` gives under the same seed, which also pins the parameter-creation order.
 
-Not built: `get_test_reads` (fn:1642-1721), the input-window builder.  It reads the flank tag of
-each `bedtools getfasta -s -nameOnly` header as `line[1:-3].split('$')[2]`, which cuts "ft\n"
-(">0$+$left\n" gives 'le') or "+)\n" (">0$+$left(+)\n" gives 'left(') and so never equals
-'left': every flank base, left and right of the partner breakpoint (about 200), lands in the
-right-hand sequence.  MS windows, and SM windows on the '-' strand, then come out about 301
-positions long instead of the 201 the model is trained on, so `Test_model` cannot load a
-trained `model.pt` (position table 22 vs 33 rows), and a file mixing both lengths is ragged
-for `read_lines`.  The pipeline therefore runs as `--not_filter_false_positive`.
+`get_test_reads` (fn:1642-1721), the input-window builder, is `get_test_reads` here: per distinct
+candidate breakpoint, 100 exon bases on each side of the partner breakpoint (`find_positions`,
+`ExonIndex.walk`) fetched as `bedtools getfasta -s -nameOnly` would (the BED rows carry the
+strand in column 5, the score column, so `-s` sees no strand and nothing is reverse-complemented),
+and 100 anchor bases on each side of the anchor breakpoint.  Its quirks are kept: the flank tag is
+read as `line[1:-3].split('$')[2]`, which cuts "ft\n" (">0$+$left\n" gives 'le') or "+)\n" and
+so never equals 'left' -- every partner flank base (about 200) lands in the right-hand sequence;
+the id written beside each window is the previous header's; a '-' strand swaps and
+reverse-complements the partner flanks of the NEXT candidate (`strand_last`).  MS windows, and
+SM windows after a '-' strand, are therefore about 301 positions long instead of the 201 a
+trained model expects; scoring such a file fails in the reference's `Test_model` as it does in
+`score_test_file` (ragged windows, or a 33-row position table against a model trained on 22).
+Only a missing model file is caught (AF:214-225): the run then proceeds as
+`--not_filter_false_positive`, which is what the reference does with its default
+`--model_file ./data/model.pt` (not shipped).
 """
 import os
 
@@ -180,3 +187,104 @@ def score_test_file(test_file, model_file, device="cpu"):
     with open(test_file) as fh:
         windows = [ln.split("\t")[0].upper().replace("\n", "") for ln in fh]
     return score_windows(windows, model_file, device)
+
+
+_RC = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N", "H": "H"}
+
+
+def _reverse(seq):
+    """functions.py:498 `reverse`: reverse complement over A/C/G/T/N/H (KeyError otherwise)."""
+    return "".join(_RC[c] for c in seq[::-1])
+
+
+def get_test_reads(candidates, anchor_seq, index, getfasta):
+    """get_test_reads (fn:1642-1721): the `<window>\t<id>` lines of the test file, in the
+    reference's order and with its quirks (module docstring).  candidates: report.Candidate list
+    (Find_candidate_genes' order); anchor_seq: the anchored transcript (the FASTA's sequence lines
+    joined, fn:1646-1649); index: annotation.ExonIndex; getfasta(rows): `bedtools getfasta` of
+    (chrom, start, end, name) rows -> [(header, seq)], intervals outside a contig skipped."""
+    bed, seen, id_ = [], [], 0
+    for cand in candidates:
+        pos, _ = cand.find_max_pos()
+        target_bp, chrom, other_bp, strand = pos[0], pos[1], pos[2], pos[3]
+        key = (target_bp, chrom, other_bp, strand)
+        if key in seen:
+            continue
+        seen.append(key)
+        t = cand.type_
+        at = other_bp + 1 if (t == "SM" and strand == "+") or (t == "MS" and strand == "-") else other_bp
+        flag = "left"
+        for p in index.walk(chrom, at, 100):
+            if p[0] == "H":
+                flag = "right"
+                continue
+            bed.append((chrom, int(p[0]), int(p[1]), f"{id_}${strand}${flag}"))
+        id_ += 1
+    # bedtools getfasta -s -nameOnly: one header line (the name) and one sequence line per row
+    lines = []
+    for hdr, seq in getfasta(bed):  # rows outside a contig are skipped, as bedtools does
+        lines.append(">" + hdr.split("::")[0] + "\n")
+        lines.append(seq + "\n")
+    if not lines:
+        raise IndexError("get_test_reads: no flank sequence (the reference indexes lines[0] here)")
+    out, seen = [], []
+    last_id = "0"
+    strand_last = lines[0][1:-3].split("$")[1]
+    fusion_id, strand, dir_ = last_id, strand_last, ""
+    i = 0
+    for cand in candidates:
+        pos, _ = cand.find_max_pos()
+        target_bp, chrom, other_bp, strand_c = pos[0], pos[1], pos[2], pos[3]
+        key = (target_bp, chrom, other_bp, strand_c)
+        if key in seen:
+            continue
+        seen.append(key)
+        seq_left2 = seq_right2 = ""
+        while i < len(lines):
+            if lines[i].startswith(">"):
+                fusion_id, strand, dir_ = lines[i][1:-3].split("$")
+                if fusion_id != last_id or i == len(lines) - 1:
+                    break
+            else:
+                if dir_ == "left":
+                    seq_left2 += lines[i][:-1].upper()
+                else:
+                    seq_right2 += lines[i][:-1].upper()
+            i += 1
+        if strand_last == "-":
+            seq_left2, seq_right2 = _reverse(seq_right2), _reverse(seq_left2)
+        lo = target_bp - min(101, target_bp)
+        seq_left1 = anchor_seq[lo:target_bp - 1]
+        seq_right1 = anchor_seq[target_bp - 1:min(target_bp + 99, len(anchor_seq))]
+        if cand.type_ == "MS":
+            w = "N" * (100 - len(seq_left1)) + seq_left1 + "H" + seq_right2 + "N" * (100 - len(seq_right2))
+        else:
+            w = "N" * (100 - len(seq_left2)) + seq_left2 + "H" + seq_right1 + "N" * (100 - len(seq_right1))
+        out.append(w + "\t" + last_id + "\n")
+        last_id = fusion_id
+        strand_last = strand
+    return out
+
+
+
+def score_candidates(candidates, anchor_seq, index, getfasta, model_file, out_prefix, device="cpu", log=print):
+    """The filter step of Anchored_Fusion.py:212-225: (scores, no_filter).  A missing model file
+    is reported and the run continues without the filter, as the reference's FileNotFoundError
+    branch does; otherwise the windows are written to `<out_prefix>_test_reads.txt`
+    (get_test_reads), scored by Test_model and set on the candidates by candidate index (a
+    duplicate breakpoint leaves fewer windows than candidates and raises IndexError there, as in
+    the reference)."""
+    try:
+        with open(model_file):
+            pass
+    except FileNotFoundError:
+        log("Error: model file not found!, not performing filter false positives.")
+        return [], True
+    lines = get_test_reads(candidates, anchor_seq, index, getfasta)
+    test_file = out_prefix + "_test_reads.txt"
+    with open(test_file, "w") as fh:
+        fh.writelines(lines)
+    scores = [float(x) for x in score_test_file(test_file, model_file, device)]
+    for i, cand in enumerate(candidates):
+        cand.score = scores[i]
+    return scores, False

@@ -20,8 +20,10 @@ Searches are injectable (`Searches`):
 - the default runs everything on the GPU;
 - tests may pass the CPU oracle. It is test infrastructure and is never a fallback here.
 
-The filter model (Model.py, `--not_filter_false_positive` off) is outside SURVEY.md §8 and not
-built, so runs behave as `--not_filter_false_positive`.
+The false-positive filter (AF:212-225) runs when `filt` names a model file
+(`--model_file` without `--not_filter_false_positive`): `filter_model.score_candidates` builds the
+windows (get_test_reads), scores them on PyTorch-ROCm (Test_model) and Final_fusion writes the
+Natural_score layout; a missing model file falls back to the no-filter tables, as in the reference.
 """
 import os
 import re
@@ -117,13 +119,16 @@ def align_anchor(anchor, reads, lens, aligner_factory):
             close()
 
 
-def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory, out_prefix, log=print):
+def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory, out_prefix, log=print,
+             filt=None):
     """One anchored gene (the body of AF:121-227).  Returns the candidate list."""
     res = align_anchor(anchor, reads, lens, aligner_factory)
-    return consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=log)
+    return consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=log,
+                        filt=filt)
 
 
-def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=print):
+def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=print, filt=None):
+    """filt: None (`--not_filter_false_positive`) or dict(model_file=..., device=...)."""
     """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads``."""
     anchor_rec = [(gene, anchor)]
     width = reads.shape[1]
@@ -163,7 +168,12 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     cands, cnt_max = partner.candidate_genes(good, bps, blocks_chr, searches.place, searches.genome)
     log(f"[{gene}] blocks {sum(len(v) for v in blocks_chr.values())}, breakpoints {len(bps)}, "
         f"placed {len(good)}, candidates {len(cands)}")
-    report.write_predictions(out_prefix, cands, gene, index, [], cnt_max, True)
+    scores, no_filter = [], True
+    if filt is not None and len(cands) != 0:
+        from .filter_model import score_candidates
+        scores, no_filter = score_candidates(cands, anchor, index, searches.getfasta, filt["model_file"], out_prefix,
+                                             device=filt.get("device", "cpu"), log=log)
+    report.write_predictions(out_prefix, cands, gene, index, scores, cnt_max, no_filter)
     return cands
 
 
@@ -179,7 +189,7 @@ def dist_world(group=None):
 
 
 def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, log=print, group=None):
+        aligner_factory=None, log=print, group=None, filt=None):
     """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt.
 
     Inside a torch.distributed job of N > 1 ranks (cli --gpus N: one process per GPU, `device`
@@ -189,7 +199,7 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     rank, world = dist_world(group)
     if world > 1:
         return _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device,
-                            searches, aligner_factory, log, group, rank, world)
+                            searches, aligner_factory, log, group, rank, world, filt)
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
@@ -211,13 +221,13 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
         os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
         homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
         results[gene] = run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory,
-                                 os.path.join(folder, gene + "_fusion"), log=log)
+                                 os.path.join(folder, gene + "_fusion"), log=log, filt=filt)
     return results
 
 
 
 def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device, searches,
-                 aligner_factory, log, group, rank, world):
+                 aligner_factory, log, group, rank, world, filt=None):
     import torch
     import torch.distributed as dist
     from . import shard
@@ -255,6 +265,6 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
             log(f"[{gene}] S2 over {world} ranks: {len(res.reads)} candidate records gathered")
             homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
             results[gene] = consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches,
-                                         os.path.join(folder, gene + "_fusion"), log=log)
+                                         os.path.join(folder, gene + "_fusion"), log=log, filt=filt)
     dist.barrier(group)
     return results

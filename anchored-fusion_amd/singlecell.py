@@ -122,7 +122,7 @@ def merge_cell_tables(cells, work_folder, out_name, out_prefix):
 
 
 def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, batch_pairs=1 << 22, log=print):
+        aligner_factory=None, batch_pairs=1 << 22, log=print, filt=None):
     """All genes x all cells; writes `<out>/<G>/<G>_fusion_gene_cell_predictions*.txt` and the
     per-cell tables under `<out>/<G>/work_dir/<cell>/`.  Returns {gene: merged rows}."""
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
@@ -180,7 +180,7 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
                     nr = creads.shape[0]
                     os.makedirs(os.path.join(work, cell), exist_ok=True)
                     consume_gene(gene, anchor, names, creads, clens, slice_result(res, row, row + nr), index,
-                                 homo_rows, searches, os.path.join(work, cell, out_name), log=log)
+                                 homo_rows, searches, os.path.join(work, cell, out_name), log=log, filt=filt)
                     row += nr
         finally:
             close = getattr(aligner, "close", None)

@@ -88,3 +88,46 @@ def test_cli_gpu(tmp_path):
                         "--not_filter_false_positive", "--thread", "4"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     _check(out, truth)
+
+
+def test_pipeline_filter_step_cpu_backends(tmp_path):
+    """AF:212-225 wired: with a model file the candidates are scored (get_test_reads ->
+    Test_model) and Final_fusion writes the Natural_score layout; a missing model file gives the
+    unfiltered tables, as in the reference."""
+    import torch
+    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
+    from anchored_fusion_amd import filter_model
+    from anchored_fusion_amd.annotation import ExonIndex
+    from anchored_fusion_amd.place import Placer
+    paths, truth = make_world(str(tmp_path / "world"))
+    genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
+    searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference,
+                                                       tile_factory=OracleTileReference))
+    kw = dict(searches=searches, aligner_factory=OracleAligner, log=lambda *_: None)
+    base = str(tmp_path / "base")
+    res = pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], base, **kw)
+    cands = res["BCRX"]
+    assert cands
+    anchor = [s.decode().upper() for _, s in pipeline.read_fasta(paths["anchor"])][0]
+    index = ExonIndex.from_lines(open(paths["gtf"]).readlines())
+    windows = filter_model.get_test_reads(cands, anchor, index, searches.getfasta)
+    L = len(windows[0].split("\t")[0])
+    torch.manual_seed(3)
+    model = str(tmp_path / "model.pt")
+    torch.save(filter_model.FusionFilter(L).double().state_dict(), model)
+    missing = str(tmp_path / "missing")
+    pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], missing,
+                 filt=dict(model_file=str(tmp_path / "nope.pt")), **kw)
+    for t in TABLES:
+        assert open(os.path.join(missing, "BCRX_fusion", t)).read() == open(os.path.join(base, "BCRX_fusion", t)).read()
+    if len({len(w.split("\t")[0]) for w in windows}) > 1 or len(windows) < len(cands):
+        raise AssertionError("the test world should give one window per candidate")
+    torch.manual_seed(0)
+    scored = str(tmp_path / "scored")
+    pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], scored,
+                 filt=dict(model_file=model, device="cpu"), **kw)
+    ab = [ln.rstrip("\n").split("\t") for ln in open(os.path.join(scored, "BCRX_fusion", TABLES[1]))]
+    assert ab[0][5] == "Natural_score"
+    for row in ab[1:]:
+        assert 0.0 <= float(row[5]) <= 1.0
+    assert os.path.exists(os.path.join(scored, "BCRX_fusion", "BCRX_fusion_test_reads.txt"))
