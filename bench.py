@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--pairs", type=int, default=None, help="c3: total pairs (50 M); c2: pairs per GPU (1 M)")
     ap.add_argument("--read-len", type=int, default=None, help="default 150 (c3) / 100 (c2)")
     ap.add_argument("--genome-scale", type=float, default=1.0, help="c3: genome size as a fraction of hg38")
-    ap.add_argument("--batch-chunks", type=int, default=240,
-                    help="c3: bwa chunks per S2 batch (240 x 33,334 pairs = 8 M pairs; sweep in DESIGN.md)")
+    ap.add_argument("--batch-chunks", type=int, default=0,
+                    help="c3: bwa chunks per S2 batch; 0 = min(240, the rank's chunks / batches in flight), so a "
+                         "rank's share is at least one full group (240 x 33,334 pairs = 8 M pairs; sweep in DESIGN.md)")
     ap.add_argument("--fusion-frac", type=float, default=0.05)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="pairs timed on the CPU oracle (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample until this much wall time")
@@ -310,6 +311,9 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     t_idx = time.perf_counter() - t0
     log(f"genome indexes (bwa-style 16-mer table, BLAT 11-mer tiles) built in {t_idx:.1f} s")
     lo, hi = shard_range(N, rank, world, L)
+    from anchored_fusion_amd.shard import chunk_pairs
+    rank_chunks = -(-(hi - lo) // chunk_pairs(L))
+    batch_chunks = args.batch_chunks or max(1, min(240, -(-rank_chunks // max(1, args.inflight))))
     n = hi - lo
     reads_t = torch.empty((2 * max(n, 1), L), dtype=torch.uint8, device=dev)
     if n:
@@ -319,7 +323,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     W.blob = None  # the index keeps its own copy
     torch.cuda.empty_cache()
     disc = discover.CandidateDiscovery(anchor, ref, tiles, n, L, device=gpu, inflight=max(1, args.inflight),
-                                       batch_chunks=args.batch_chunks, pair_base=lo)
+                                       batch_chunks=batch_chunks, pair_base=lo)
     G = disc.grp.inflight
     n_groups = (len(disc.batches) + G - 1) // G
 
