@@ -250,7 +250,12 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          hipStream_t s);
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, hipStream_t s);
+// k_blat's schedule: the queries by estimated cost, heaviest first (work: af_blat_order_bytes(cap))
+size_t af_blat_order_bytes(int64_t cap);
+hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+                                int32_t stride, const int32_t *lens, int32_t rep_match, void *work,
+                                int32_t *order, hipStream_t s);
 hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, DevTile *X, void **allocs, int *na,
                                hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);

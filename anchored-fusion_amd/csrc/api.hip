@@ -28,6 +28,12 @@ struct af_ctx {
     uint8_t *zscratch = nullptr;
     uint8_t *bscratch = nullptr;  // k_blat: AF_BLAT_SLOT_BYTES per resident wave (blat_slots)
     int blat_slots = 0;
+    void *blat_ord_work = nullptr;  // k_blat's cost-ordered schedule (af_launch_blat_order)
+    int32_t *blat_order = nullptr;
+    int64_t blat_ord_cap = 0;
+    af_psl *blat_stage = nullptr;   // per (query, strand) rows before k_blat_merge
+    int32_t *blat_stage_n = nullptr;
+    int64_t blat_stage_rows = 0, blat_stage_items = 0;
     // S2 (bwa mem paired-end) scratch, s2.hip
     S2Reg *s2_pool = nullptr;
     int64_t s2_pool_cap = 0;
@@ -204,6 +210,28 @@ int ensure_zscratch(af_ctx *c) {
     return AF_OK;
 }
 
+int ensure_blat_order(af_ctx *c, int64_t cap) {
+    if (cap <= c->blat_ord_cap) return AF_OK;
+    af_free(c->blat_ord_work); af_free(c->blat_order);
+    c->blat_ord_work = nullptr; c->blat_order = nullptr; c->blat_ord_cap = 0;
+    HIPCHK(c, hipMalloc(&c->blat_ord_work, af_blat_order_bytes(cap)));
+    HIPCHK(c, hipMalloc(&c->blat_order, sizeof(int32_t) * cap));
+    c->blat_ord_cap = cap;
+    return AF_OK;
+}
+
+int ensure_blat_stage(af_ctx *c, int64_t cap, int32_t max_rows) {
+    const int64_t need = 2 * cap * max_rows;
+    if (c->blat_stage && need <= c->blat_stage_rows && 2 * cap <= c->blat_stage_items) return AF_OK;
+    af_free(c->blat_stage); af_free(c->blat_stage_n);
+    c->blat_stage = nullptr; c->blat_stage_n = nullptr; c->blat_stage_rows = c->blat_stage_items = 0;
+    HIPCHK(c, hipMalloc(&c->blat_stage, sizeof(af_psl) * need));
+    HIPCHK(c, hipMalloc(&c->blat_stage_n, sizeof(int32_t) * 2 * cap));
+    c->blat_stage_rows = need;
+    c->blat_stage_items = 2 * cap;
+    return AF_OK;
+}
+
 int ensure_bscratch(af_ctx *c) {
     if (c->bscratch) return AF_OK;
     c->blat_slots = af_blat_slots(c->n_cu);
@@ -365,7 +393,7 @@ int af_ctx_create(int device, af_ctx **out) {
 void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->bscratch); af_free(c->d_packed);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->bscratch); af_free(c->blat_ord_work); af_free(c->blat_order); af_free(c->blat_stage); af_free(c->blat_stage_n); af_free(c->d_packed);
     af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
@@ -980,7 +1008,9 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         for (int64_t i = 0; i < n_queries; ++i)
             if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
     (void)hipSetDevice(c->device);
-    if ((rc = ensure_bscratch(c))) return rc;
+    if ((rc = ensure_bscratch(c)) || (rc = ensure_blat_order(c, n_queries)) ||
+        (rc = ensure_blat_stage(c, n_queries, max_rows)))
+        return rc;
     const int64_t bytes = n_queries * (int64_t)stride, nr = n_queries * (int64_t)max_rows;
     uint8_t *d_q = nullptr;
     int32_t *d_lens = nullptr, *d_nrows = nullptr;
@@ -999,8 +1029,12 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         (lens && (e = hipMemcpyAsync(d_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s)) != hipSuccess ||
         (e = hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = af_launch_blat_order(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, n_queries, stride,
+                                  lens ? d_lens : nullptr, p->rep_match, c->blat_ord_work, c->blat_order, s)) !=
+            hipSuccess ||
         (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride, lens ? d_lens : nullptr, *p,
-                            c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows, s)) !=
+                            c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows,
+                            c->blat_order, c->blat_stage, c->blat_stage_n, s)) !=
             hipSuccess ||
         (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipMemcpyAsync(n_rows, d_nrows, 4 * n_queries, hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -1026,12 +1060,20 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
     if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
     if (cap_queries == 0) return AF_OK;
     (void)hipSetDevice(c->device);
-    if ((rc = ensure_bscratch(c))) return rc;
+    if ((rc = ensure_bscratch(c)) || (rc = ensure_blat_stage(c, cap_queries, max_rows))) return rc;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
     HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
+    const int32_t *order = nullptr;  // a subrange keeps query order; the whole set runs heaviest first
+    if (!d_first) {
+        if ((rc = ensure_blat_order(c, cap_queries))) return rc;
+        HIPCHK(c, af_launch_blat_order(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, cap_queries, stride, d_lens,
+                                       p->rep_match, c->blat_ord_work, c->blat_order, s));
+        order = c->blat_order;
+    }
     HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
-                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows, s));
+                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows,
+                             order, c->blat_stage, c->blat_stage_n, s));
     return AF_OK;
 }
 

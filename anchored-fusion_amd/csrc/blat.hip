@@ -346,8 +346,8 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                                                         const int32_t *__restrict__ q_first, int64_t cap,
                                                         int32_t *__restrict__ heads,
                                                         uint8_t *__restrict__ bscratch, int32_t diag_passes,
-                                                        af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
-                                                        int32_t max_rows) {
+                                                        af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
+                                                        int32_t max_rows, const int32_t *__restrict__ order) {
     DpLds &D = g_dp;
     BlatLds &B = g_bl;
     const int lane = threadIdx.x;
@@ -359,20 +359,30 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
     Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
     Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
     af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
+    // work items are (query, strand): item 2k + s is strand s of the k-th query (of the cost order
+    // when given: heaviest first), so a heavy query's strands run on two waves at once
+    const int64_t i0 = 2 * (int64_t)q0, i1 = 2 * (int64_t)nq;
     int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
-        int item = nq;
+        int64_t item = i1;
         while (heads_left > 0) {
             int v = 0;
             if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
             v = __builtin_amdgcn_readfirstlane(v);
-            const int64_t it = q0 + head + 8 * (int64_t)v;
-            if (it < nq) { item = (int)it; break; }
+            const int64_t it = i0 + head + 8 * (int64_t)v;
+            if (it < i1) { item = it; break; }
             head = (head + 1) & 7;
             --heads_left;
         }
-        if (item >= nq) break;
-        const int64_t qi = item;
+        if (item >= i1) break;
+        const int s_item = (int)(item & 1);
+        const int64_t qi = order ? order[item >> 1] : (item >> 1);
+#ifdef AF_BLAT_CHECK
+        if (qi < 0 || qi >= cap) {
+            if (lane == 0) printf("k_blat: item %ld -> query %ld outside [0, %ld)\n", (long)item, (long)qi, (long)cap);
+            continue;
+        }
+#endif
         int L = lens ? lens[qi] : stride;
         if (L > stride) L = stride;
         if (L > AF_MAX_READ) L = AF_MAX_READ;
@@ -384,7 +394,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
         int wsh = 3;  // bucket width 1 << wsh >= 2 * drift: [d - drift, d + drift] meets <= 2 buckets
         while ((1ll << wsh) < 2 * drift) ++wsh;
         BP(int64_t tq0 = clock64(), tq = tq0; int64_t pc[6] = {0, 0, 0, 0, 0, 0}; int ch = 0, cc_ = 0, cr = 0, cs = 0;)
-        for (int strand = 0; strand < 2; ++strand) {
+        for (int strand = s_item; strand <= s_item; ++strand) {
             for (int x = lane; x < L; x += 64) {
                 const uint8_t c = B.q0[strand ? L - 1 - x : x];
                 D.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
@@ -627,8 +637,9 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                     RW[j] = tmp;
                 }
             const int m = n < max_rows ? n : max_rows;
-            for (int k = 0; k < m; ++k) rows[qi * max_rows + k] = RW[k];
-            n_rows[qi] = m;
+            const int64_t sl = 2 * qi + s_item;  // this strand's rows, best first, for k_blat_merge
+            for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
+            stage_n[sl] = m;
             BP(if (g_blprof && qi < (1 << 22)) {
                 int32_t *pf = g_blprof + qi * 16;
                 for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
@@ -682,11 +693,89 @@ __global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, uint32_
 
 }  // namespace
 
+// the rows of a query's two strands (each sorted, <= max_rows) merged in psl_before order: the
+// stable sort of the union, as one wave doing both strands would have produced
+__global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__restrict__ stage_n,
+                             const int32_t *__restrict__ n_q, const int32_t *__restrict__ q_first, int64_t cap,
+                             int32_t max_rows, af_psl *__restrict__ rows, int32_t *__restrict__ n_rows) {
+    const int64_t nq = *n_q < cap ? *n_q : cap;
+    const int64_t q0 = q_first ? max((int64_t)0, min((int64_t)*q_first, nq)) : 0;
+    const int64_t qi = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq) return;
+    const af_psl *A = stage + 2 * qi * max_rows, *Bs = A + max_rows;
+    const int na = stage_n[2 * qi], nb = stage_n[2 * qi + 1];
+#ifdef AF_BLAT_CHECK
+    if (na < 0 || na > max_rows || nb < 0 || nb > max_rows) {
+        printf("k_blat_merge: query %ld rows %d %d\n", (long)qi, na, nb);
+        return;
+    }
+#endif
+    int i = 0, j = 0, k = 0;
+    for (; k < max_rows && (i < na || j < nb); ++k) {
+        const bool take_b = j < nb && (i >= na || psl_before(Bs[j], A[i]));
+        rows[qi * max_rows + k] = take_b ? Bs[j++] : A[i++];
+    }
+    n_rows[qi] = k;
+}
+
+// the queries' forward tile hits (tiles over repMatch excluded): the scheduling key of k_blat,
+// heaviest first (the order changes no result, only which wave takes a query when)
+__global__ void k_blat_cost(DevTile X, const uint8_t *__restrict__ queries, int32_t stride,
+                            const int32_t *__restrict__ lens, const int32_t *__restrict__ n_q, int64_t cap,
+                            int32_t rep_match, uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    const int64_t nq = *n_q < cap ? *n_q : cap;
+    vals[i] = (int32_t)i;
+    if (i >= nq) { keys[i] = 0xFFFFFFFFu; return; }
+    int L = lens ? lens[i] : stride;
+    L = max(0, min(L, min(stride, AF_MAX_READ)));
+    const uint8_t *q = queries + i * (int64_t)stride;
+    uint64_t cost = 0;
+    uint32_t k = 0;
+    int run = 0;
+    for (int j = 0; j < L; ++j) {
+        const uint8_t b = nt4(q[j]);
+        if (b > 3) { run = 0; continue; }
+        k = (k >> 2) | ((uint32_t)b << (2 * (TILE - 1)));
+        if (++run >= TILE) {
+            const uint32_t c = X.start[k + 1] - X.start[k];
+            if ((int64_t)c <= rep_match) cost += c;
+        }
+    }
+    keys[i] = 0xFFFFFFFEu - (uint32_t)(cost < 0xFFFFFFFEull ? cost : 0xFFFFFFFEull);
+}
+
+
+size_t af_blat_order_bytes(int64_t cap) {
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (int32_t *)nullptr, (int32_t *)nullptr, (int)cap, 0, 32);
+    return 16 * (size_t)cap + ((tb + 255) & ~(size_t)255) + 256;
+}
+
+// order[0, cap): the queries [0, *n_queries) by k_blat_cost, heaviest first, then the empty slots
+hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,
+                                int32_t stride, const int32_t *lens, int32_t rep_match, void *work,
+                                int32_t *order, hipStream_t s) {
+    uint8_t *w = static_cast<uint8_t *>(work);
+    uint32_t *k0 = reinterpret_cast<uint32_t *>(w), *k1 = k0 + cap;
+    int32_t *v0 = reinterpret_cast<int32_t *>(k1 + cap);
+    void *temp = w + 16 * (size_t)cap;
+    size_t tb = af_blat_order_bytes(cap) - 16 * (size_t)cap - 256;
+    hipLaunchKernelGGL(k_blat_cost, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, X, queries, stride, lens,
+                       n_queries, cap, rep_match, k0, v0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairs(temp, tb, k0, k1, v0, order, (int)cap, 0, 32, s);
+}
+
+
 hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          hipStream_t s) {
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, hipStream_t s) {
     // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
     int bits = 64 - __builtin_clzll((unsigned long long)(X.n + 1024));
     const int diag_passes = (bits + 7) / 8;
@@ -694,12 +783,14 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
     dim3 g(n_slots), b(64);
 #define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, q_first, cap, \
                                     heads, \
-                                    bscratch, diag_passes, rows, n_rows, max_rows)
+                                    bscratch, diag_passes, stage, stage_n, max_rows, order)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
+    hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, stage, stage_n, n_queries,
+                       q_first, cap, max_rows, rows, n_rows);
     return hipGetLastError();
 }
 
