@@ -168,3 +168,36 @@ def test_blat_tile_index_from_device_matches_host():
     ra, na = a.search(qs, p)
     rb, nb = b.search(qs, p)
     assert np.array_equal(na, nb) and ra.tobytes() == rb.tobytes()
+
+
+@pytest.mark.gpu
+def test_blat_device_range_matches_host():
+    """af_blat_device_range: queries [first, n) only, rows at their own indices; the rest of the
+    output untouched."""
+    import torch
+
+    from anchored_fusion_amd import blat
+    from anchored_fusion_amd.place import pack_queries
+    ctgs, rep = _world(3, n_ctg=2)
+    qs = _queries(ctgs, rep, 11, n=200)
+    p = blat.params("split_tail")
+    ref = _gpu_ref(ctgs, p.step_size)
+    rh, nh = ref.search(qs, p)
+    buf, lens = pack_queries(qs)
+    dev = torch.device("cuda:0")
+    qt = torch.from_numpy(buf).to(dev)
+    lt = torch.from_numpy(lens).to(dev)
+    nq = torch.tensor([len(qs)], dtype=torch.int32, device=dev)
+    first = torch.tensor([77], dtype=torch.int32, device=dev)
+    rows = torch.zeros(len(qs) * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    nr = torch.full((len(qs),), -5, dtype=torch.int32, device=dev)
+    ref.search_device(qt, nq, buf.shape[1], rows, nr, lens_t=lt, p=p, stream=torch.cuda.current_stream(),
+                      first_t=first)
+    torch.cuda.synchronize()
+    nd = nr.cpu().numpy()
+    rd = rows.cpu().numpy().view(blat.PSL_DTYPE).reshape(len(qs), blat.MAX_ROWS)
+    assert (nd[:77] == -5).all()
+    assert np.array_equal(nd[77:], nh[77:])
+    for i in range(77, len(qs)):
+        assert rd[i, :nd[i]].tobytes() == rh[i, :nh[i]].tobytes()
+    ref.close()
