@@ -150,3 +150,51 @@ def test_c3_full_size(anchor):
     d.close()
     ref.close()
     tiles.close()
+
+
+def test_discovery_rank_shard_and_exchange(anchor):
+    """A rank's shard (pair_base on the bwa chunk grid, as bench.py's ranks run it): records
+    bit-exact vs the oracle with the same read ids, and the candidate exchange over a one-rank
+    RCCL group returns exactly the packed rows, with global read rows."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from anchored_fusion_amd import discover
+    from anchored_fusion_amd.shard import chunk_pairs
+    W = _world(anchor, 0.02)
+    ref = W.reference()
+    tiles = W.tiles()
+    n, pb = 60_000, 3 * chunk_pairs(150)
+    reads_t = W.simulate_pairs(n, read_len=150, seed=13, pair_base=pb)
+    d = discover.CandidateDiscovery(anchor, ref, tiles, n, 150, device=0, inflight=2, batch_chunks=1, pair_base=pb)
+    d.run(reads_t)
+    torch.cuda.synchronize()
+    reads = reads_t.cpu().numpy()
+    got = {k: v.cpu().numpy() for k, v in d.out.items()}
+    got["cigar"] = got["cigar"].view(np.uint32)
+    assert_records_equal(got, oracle.OracleIndex(anchor).align_pairs(reads, threads=8, pair_base=pb), reads)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        packed = d.pack()
+        ex = d.exchange()
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+    assert ex.shape == packed.shape and torch.equal(ex.cpu(), packed.cpu()) and ex.shape[0] > 0
+    p = packed.cpu().numpy()
+    grow = p[:, 0].view(np.uint32).astype(np.int64) | (p[:, 1].astype(np.int64) << 32)
+    nq = int(d.n_q.item())
+    assert np.array_equal(grow[:nq], d.q_rows[:nq].cpu().numpy().astype(np.int64) + 2 * pb)
+    assert (p[:nq, 2] == 0).all() and (p[nq:, 2] == 1).all()
+    local = grow - 2 * pb
+    assert np.array_equal(p[:, 3], got["flag"][local]) and np.array_equal(p[:, 4], got["pos"][local])
+    d.close()
+    ref.close()
+    tiles.close()
