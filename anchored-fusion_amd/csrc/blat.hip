@@ -22,6 +22,8 @@
 //   stitch   chain DP over the parts (<= 16) with overlap trimming; N checks over the gaps on
 //            the wave; every chain passing minScore / minIdentity becomes a PSL row
 //   output   rows of both strands ordered (score desc, strand, tStart, qStart), max_rows kept
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "ksw_dp.h"
@@ -795,6 +797,10 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
 }
 
 int af_blat_slots(int n_cu) {
+    if (const char *e = getenv("AF_BLAT_WAVES_PER_CU")) {  // experiment knob: resident BLAT waves per CU
+        const int w = atoi(e);
+        if (w > 0) return n_cu * w;
+    }
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(k_blat<AF_CPL>), 64, 0) !=
             hipSuccess || occ < 1)

@@ -201,3 +201,28 @@ def test_blat_device_range_matches_host():
     for i in range(77, len(qs)):
         assert rd[i, :nd[i]].tobytes() == rh[i, :nh[i]].tobytes()
     ref.close()
+
+
+def test_blat_edge_cases():
+    """Empty and sub-tile queries, all-N, the maximum length (AF_MAX_READ), queries across the
+    N run and at contig ends, a query set of one, and no queries: GPU == oracle, field by field."""
+    from anchored_fusion_amd import _lib, blat
+    ctgs, rep = _world(5, n_ctg=2, ctg_len=200_000)
+    g0 = ctgs[0][1]
+    qs = ["", "A", "ACGTACGTAC", "N" * 60, g0[900:1000] + g0[1100:1180],  # the N run cut out: a junction
+          g0[950:1150],                                                 # across the N run
+          g0[:70], g0[-90:], g0[5000:5000 + _lib.AF_MAX_READ],           # contig ends, the maximum length
+          rep[:_lib.AF_MAX_READ // 2] * 2, g0[7000:7011]]               # repeat-heavy, exactly one tile
+    for preset in ("split_tail", "anchored_split"):
+        p = blat.params(preset)
+        g = _gpu_ref(ctgs, p.step_size)
+        o = OracleTileReference(ctgs, p.step_size)
+        for batch in (qs, qs[8:9]):
+            rg, ng = g.search(batch, p)
+            ro, no = o.search(batch, p)
+            assert np.array_equal(ng, no), (preset, ng, no)
+            for i in range(len(batch)):
+                assert rg[i, :ng[i]].tobytes() == ro[i, :no[i]].tobytes(), (preset, i)
+        rg, ng = g.search([], p)
+        assert len(ng) == 0
+        g.close()
