@@ -28,6 +28,12 @@
 
 #include "ksw_dp.h"
 
+#ifndef AF_BLAT_ROUNDS
+#define AF_BLAT_ROUNDS 6  // drift-filter rounds at most (round 0 is marked while the hits are collected; 1 / 2 / 3 / 4 / 6: 160 / 147 / 145 / 144 / 144 ms per C3 step)
+#endif
+#ifndef AF_BLAT_FILTER_MIN
+#define AF_BLAT_FILTER_MIN 256  // hits below which another drift-filter round is not worth its passes
+#endif
 #ifndef AF_BLAT_WPS
 #define AF_BLAT_WPS 6  // k_blat waves per SIMD (launch bound: VGPR budget)
 #endif
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             // false keeps only, a few rounds while they pay ---------------------------------------
             uint64_t *H0 = KA, *H1 = KB;
             if (filt)
-                for (int round = 0; round < 3 && (round == 0 || nh > 256); ++round) {
+                for (int round = 0; round < AF_BLAT_ROUNDS && (round == 0 || nh > AF_BLAT_FILTER_MIN); ++round) {
                     const int nk = round == 0 ? drift_keep(H0, H1, nh, drift, wsh, 0, lane)
                                               : drift_filter(H0, H1, nh, drift, wsh, round, lane);
                     uint64_t *t = H0; H0 = H1; H1 = t;
