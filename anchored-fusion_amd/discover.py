@@ -99,7 +99,22 @@ class CandidateDiscovery:
         with torch.cuda.stream(s0):
             self.tails["n"].zero_()
         done = None
-        for gi, k0 in enumerate(range(0, len(self.batches), G)):
+        if os.environ.get("AF_S2_ROLL") == "1":
+            # batch k on slot k % G, K1 + K2 + K3 on that slot's stream: no group barrier
+            start = torch.cuda.Event()
+            start.record(s0)  # the previous pass's S3 - S6 read self.out / the tails
+            for s in self.grp.streams[1:G]:
+                s.wait_event(start)
+            last = {}
+            for k, (p, n) in enumerate(self.batches):
+                j = k % G
+                r0, r1 = 2 * p, 2 * (p + n)
+                spec = (reads_t[r0:r1], n, self.L, {key: v[r0:r1] for key, v in self.out.items()}, None,
+                        self.pair_base + p)
+                last[j] = self.grp.run_slot(j, spec, events=None if k1_events is None else k1_events[k],
+                                            tails=self._tails(j, r0))
+            done = list(last.values())
+        for gi, k0 in enumerate(range(0, len(self.batches), G) if done is None else ()):
             group = self.batches[k0:k0 + G]
             specs, rows0 = [], []
             for p, n in group:
@@ -110,20 +125,15 @@ class CandidateDiscovery:
             done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done,
                                        tails=lambda j, rows0=rows0: self._tails(j, rows0[j]))
         # S6 (BLAT -minScore=20 of the split-read tails that K3d cut during S2) needs no S3: it
-        # runs on a stream of its own (the tile index has its own context and scratch) beside S3,
-        # the gathers and S4 / S5, whose sort syncs and placement tail leave the chip part idle.
-        # (Searching each group's tails while the next group aligns was slower: both are
-        # compute-bound, 156 vs 145 ms per C3 step.)
-        # The stream is slot 1's (idle once S2 is done): a stream of its own would share one of
-        # the 4 hardware queues (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work.
+        # runs on slot 1's stream (the tile index has its own context and scratch; slot 1 is idle
+        # once S2 is done -- a stream of its own would share one of the 4 hardware queues
+        # (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work) beside S4 / S5.  It is
+        # launched after S3 and the gathers: launched beside them, its resident waves starved
+        # S3's sort kernels (S3 20.3 ms instead of 2.9; C3 step 144.0 -> 141.2 ms).  (Searching
+        # each group's tails while the next group aligns was slower: both are compute-bound.)
         s6 = self.grp.streams[1] if G > 1 else s0
         for e in done:
-            s6.wait_event(e)
             s0.wait_event(e)
-        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
-                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s6)
-        s6_done = torch.cuda.Event()
-        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
         if _DEBUG:
             s0.synchronize()
             _log("S2 done")
@@ -151,6 +161,11 @@ class CandidateDiscovery:
             _log(f"gathered {int(self.n_q.item())} queries, {int(self.tails['n'].item())} tails")
         if phase_events:
             phase_events[2].record(s0)
+        s6.wait_stream(s0)
+        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
+                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s6)
+        s6_done = torch.cuda.Event()
+        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
         # S4 + S5 on the genome (bwa mem -M defaults); then join S6
         self.ref.place_device(self.q, self.n_q, self.L, self.q_hits, self.q_nh, lens_t=self.q_lens,
                               params=self.p_genome, max_hits=MAX_HITS, stream=s0)

@@ -339,7 +339,8 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         log(f"warm-up pass {w}: {time.perf_counter() - t0:.3f} s, {disc.summary()}")
     free, total = torch.cuda.mem_get_info(dev)
     E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    k1 = [[[E(), E()] for _ in range(n_groups)] for _ in range(args.steps)]
+    n_k1 = len(disc.batches) if os.environ.get("AF_S2_ROLL") == "1" else n_groups  # K1 event pairs per step
+    k1 = [[[E(), E()] for _ in range(n_k1)] for _ in range(args.steps)]
     ph = [[E() for _ in range(5)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -397,8 +398,8 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         "phases_ms": {"s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
                       "gather_queries": round(phase(2, 3), 3), "genome_placement": round(phase(3, 4), 3),
                       "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
-                              "the S6 BLAT runs on slot 1's stream from the end of s2, beside s3_partition, "
-                              "gather_queries and genome_placement, which ends by joining it"},
+                              "the S6 BLAT runs on slot 1's stream from the end of gather_queries, beside "
+                              "genome_placement, which ends by joining it"},
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
             "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
