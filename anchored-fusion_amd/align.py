@@ -373,29 +373,6 @@ class AlignerGroup:
         for a in self.aligners:
             a.close()
 
-    def run_slot(self, j, batch, events=None, tails=None):
-        """Enqueues one batch's K1 + K2 + K3 on slot j's stream (stream order after the slot's
-        previous batch, so consecutive batches roll through the slots with no group barrier).
-        batch: (reads_t, n_pairs, stride, out_t, lens_t, pair_base); events (optional): two timing
-        events recorded around the K1 on that stream; tails (optional): the split-read tails spec.
-        Returns the event marking the batch's completion."""
-        import torch
-        s = self.streams[j]
-        reads_t, n_pairs, stride, out_t, lens_t, pb = batch
-        a = self.aligners[j]
-        if events is not None:
-            events[0].record(s)
-        a.seed_filter_device(reads_t, 2 * n_pairs, stride, out_t["hits"], lens_t, stream=s)
-        if events is not None:
-            events[1].record(s)
-        if tails is not None:
-            a.align_candidates_tails_device(reads_t, n_pairs, stride, out_t, tails, lens_t, stream=s, pair_base=pb)
-        else:
-            a.align_candidates_device(reads_t, n_pairs, stride, out_t, lens_t, stream=s, pair_base=pb)
-        e = torch.cuda.Event()
-        e.record(s)
-        return e
-
     def run_device(self, batches, events=None, wait=None, post=None, finish=None, tails=None, before=None):
         """batches: up to ``inflight`` tuples (reads_t, n_pairs, stride, out_t[, lens_t[, pair_base]])
         with every tensor on the device (pair_base: the batch's first pair in bwa's input stream).  Enqueues them and returns without synchronising.

@@ -99,22 +99,7 @@ class CandidateDiscovery:
         with torch.cuda.stream(s0):
             self.tails["n"].zero_()
         done = None
-        if os.environ.get("AF_S2_ROLL") == "1":
-            # batch k on slot k % G, K1 + K2 + K3 on that slot's stream: no group barrier
-            start = torch.cuda.Event()
-            start.record(s0)  # the previous pass's S3 - S6 read self.out / the tails
-            for s in self.grp.streams[1:G]:
-                s.wait_event(start)
-            last = {}
-            for k, (p, n) in enumerate(self.batches):
-                j = k % G
-                r0, r1 = 2 * p, 2 * (p + n)
-                spec = (reads_t[r0:r1], n, self.L, {key: v[r0:r1] for key, v in self.out.items()}, None,
-                        self.pair_base + p)
-                last[j] = self.grp.run_slot(j, spec, events=None if k1_events is None else k1_events[k],
-                                            tails=self._tails(j, r0))
-            done = list(last.values())
-        for gi, k0 in enumerate(range(0, len(self.batches), G) if done is None else ()):
+        for gi, k0 in enumerate(range(0, len(self.batches), G)):
             group = self.batches[k0:k0 + G]
             specs, rows0 = [], []
             for p, n in group:

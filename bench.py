@@ -339,8 +339,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         log(f"warm-up pass {w}: {time.perf_counter() - t0:.3f} s, {disc.summary()}")
     free, total = torch.cuda.mem_get_info(dev)
     E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    n_k1 = len(disc.batches) if os.environ.get("AF_S2_ROLL") == "1" else n_groups  # K1 event pairs per step
-    k1 = [[[E(), E()] for _ in range(n_k1)] for _ in range(args.steps)]
+    k1 = [[[E(), E()] for _ in range(n_groups)] for _ in range(args.steps)]
     ph = [[E() for _ in range(5)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
