@@ -333,48 +333,56 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
     const int64_t G = gridDim.x, B = blockIdx.x;
     const int64_t ra = min(n_reads, (B * nunits / G) * u), rb = min(n_reads, ((B + 1) * nunits / G) * u);
     [[maybe_unused]] const bool l63 = lane < 63;
-    bool filled = false;
-    for (int64_t sa = ra; sa < rb; sa += CAP) {
-        const int nr = (int)min((int64_t)CAP, rb - sa);
-        const uint8_t *base = reads + sa * (int64_t)stride;
-        const int64_t bytes = (int64_t)nr * stride;
-        const int nfull = (int)(bytes >> 4), nchunks = (int)((bytes + 15) >> 4);
+    // sub-range state: [sa, sa + nr) of the block's range, its bytes and 16-byte chunks
+    int64_t sa = ra;
+    int nr = 0, nfull = 0, nchunks = 0, total = 0, clast = 0, lr = 0, sr = 0;
+    int64_t bytes = 0;
+    const uint8_t *base = reads;
+    auto setup = [&]() {
+        nr = (int)min((int64_t)CAP, rb - sa);
+        base = reads + sa * (int64_t)stride;
+        bytes = (int64_t)nr * stride;
+        nfull = (int)(bytes >> 4);
+        nchunks = (int)((bytes + 15) >> 4);
         const int nblk = (nchunks + 62) / 63;
-        const int total = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of every wave
-        // round r of wave wv covers chunks AF_CH(r) + lane; chunks past the last full one are
-        // loaded (clamped) and then re-read byte-wise by load_tail in the scan
-        // (32-bit byte offsets from the sub-range base: one add and one min per load)
-        // (scalar chunk base clamped to the last full chunk, then one v_min per load)
-        int lr = 0;
-        const int clast = nfull > 0 ? nfull - 1 : 0;
-        const uint32_t lane_off = 16u * (uint32_t)lane;
-        auto next_load = [&]() -> uint4 {
-            const int cb = min(AF_CH(min(lr, total - 1)), clast);
-            const uint8_t *rbase = base + 16 * (int64_t)cb;
-            const uint32_t off = min(lane_off, 16u * (uint32_t)(clast - cb));
-            ++lr;
+        total = (nblk + AF_SEED_WAVES - 1) / AF_SEED_WAVES;  // rounds of every wave
+        clast = nfull > 0 ? nfull - 1 : 0;
+        lr = 0;
+        sr = 0;
+    };
+    // round r of wave wv covers chunks AF_CH(r) + lane; chunks past the last full one are
+    // loaded (clamped) and then re-read byte-wise by load_tail in the scan
+    // (32-bit byte offsets from the sub-range base: one add and one min per load)
+    // (scalar chunk base clamped to the last full chunk, then one v_min per load)
+    const uint32_t lane_off = 16u * (uint32_t)lane;
+    auto next_load = [&]() -> uint4 {
+        const int cb = min(AF_CH(min(lr, total - 1)), clast);
+        const uint8_t *rbase = base + 16 * (int64_t)cb;
+        const uint32_t off = min(lane_off, 16u * (uint32_t)(clast - cb));
+        ++lr;
 #if AF_K1_NT
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rbase + off));
-            return make_uint4(v.x, v.y, v.z, v.w);
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(rbase + off));
+        return make_uint4(v.x, v.y, v.z, v.w);
 #else
-            return *reinterpret_cast<const uint4 *>(rbase + off);
+        return *reinterpret_cast<const uint4 *>(rbase + off);
 #endif
-        };
+    };
 #define AF_PIN asm volatile("" ::: "memory")
-        uint4 b[AF_K1_DEPTH];
+    uint4 b[AF_K1_DEPTH];
+    if (sa < rb) {
+        setup();
 #pragma unroll
         for (int q = 0; q < AF_K1_DEPTH; ++q) {
             b[q] = next_load();
             AF_PIN;
         }
-        if (!filled) {  // the Bloom table, while the first chunk loads are in flight
-            fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
-            filled = true;
-        }
+    }
+    // the Bloom table, while the first chunk loads are in flight
+    fill_lds(reinterpret_cast<uint2 *>(smem), reinterpret_cast<const uint2 *>(bloom_g), nw / 2);
+    while (sa < rb) {
         for (int i = threadIdx.x; i < (nr + 3) / 4; i += blockDim.x) cnt[i] = 0;
         __syncthreads();
-        int sr = 0;
 #if AF_K1_ABL
         uint32_t abl = 0;
 #endif
@@ -397,22 +405,33 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
                 AF_PIN;
             }
         }
-#undef AF_PIN
 #pragma unroll
         for (int q = 0; q < AF_K1_DEPTH - 1; ++q)
             if (g + q < total) scan(b[q]);
 #if AF_K1_ABL
         if (abl == 0x12345679u) cnt[0] = abl;  // keep the ablated work live
 #endif
+        // the next sub-range's first loads go out before this one's epilogue (no stream bubble)
+        const int64_t sa_c = sa;
+        const int nr_c = nr;
+        sa += CAP;
+        if (sa < rb) {
+            setup();
+#pragma unroll
+            for (int q = 0; q < AF_K1_DEPTH; ++q) {
+                b[q] = next_load();
+                AF_PIN;
+            }
+        }
         __syncthreads();  // the sub-range is counted
         // epilogue: hits and 64-read ballots, one atomic for the sub-range
-        const int ng = (nr + 63) / 64;
+        const int ng = (nr_c + 63) / 64;
         for (int q = wv; q < ng; q += AF_SEED_WAVES) {
             const int i = q * 64 + lane;
             uint32_t h = 0;
-            if (i < nr) {
+            if (i < nr_c) {
                 h = (cnt[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-                hits[sa + i] = (int32_t)h;
+                hits[sa_c + i] = (int32_t)h;
             }
             const uint64_t bal = __ballot(h != 0);
             if (lane == 0) gbal[q] = bal;
@@ -444,10 +463,11 @@ __global__ __launch_bounds__(64 * AF_SEED_WAVES) void k_seed_stream(
         for (int q = wv; q < ng; q += AF_SEED_WAVES) {
             const uint64_t bal = gbal[q];
             if ((bal >> lane) & 1ull)
-                cand[gbase[q] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(sa + q * 64 + lane);
+                cand[gbase[q] + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(sa_c + q * 64 + lane);
         }
         __syncthreads();
     }
+#undef AF_PIN
 }
 #undef AF_CH
 

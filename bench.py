@@ -405,7 +405,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "bytes_per_launch": round(bytes_per_launch),
             "note": "HIP events on K1's stream around each group's back-to-back K1 launches (distinct read "
-                    "ranges, no reuse; K2s of the previous group run concurrently on the other streams); "
+                    "ranges, no reuse; a group's K1s start once the previous group is done, so no other kernel shares the chip); "
                     "traffic: the committed FETCH_SIZE + WRITE_SIZE passes of this batch shape",
         },
         "setup_s": {"genome": round(t_gen, 2), "index": round(t_idx, 2)},
