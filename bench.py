@@ -313,12 +313,9 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     lo, hi = shard_range(N, rank, world, L)
     from anchored_fusion_amd.shard import chunk_pairs
     rank_chunks = -(-(hi - lo) // chunk_pairs(L))
-    # equal batches that fill whole groups of `inflight` (each group waits for the previous one),
-    # at most 240 bwa chunks (8 M pairs of 2x150) each: 188 chunks x 8 at N = 1, 47 x 4 at N = 8
+    # at most 240 bwa chunks (8 M pairs of 2x150) per batch, at least `inflight` batches per rank
     # (profiles/r02/c3_n1_batch_sweep.txt, c3_n8_batch_sweep.txt)
-    inf = max(1, args.inflight)
-    n_grp = max(1, -(-rank_chunks // (inf * 240)))
-    batch_chunks = args.batch_chunks or max(1, -(-rank_chunks // (inf * n_grp)))
+    batch_chunks = args.batch_chunks or max(1, min(240, -(-rank_chunks // max(1, args.inflight))))
     n = hi - lo
     reads_t = torch.empty((2 * max(n, 1), L), dtype=torch.uint8, device=dev)
     if n:
