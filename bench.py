@@ -84,6 +84,27 @@ def pmc_traffic(pairs, read_len):
     return None
 
 
+def rocprof_k1(bytes_per_launch, n_launch):
+    """K1's roofline fraction from the committed rocprofv3 kernel trace of the same command
+    (profiles/r02/kernel_stats_c3.csv: average k_seed_stream duration over every launch of the
+    traced steps, the same mix of full and remainder batches), beside the live HIP-event figure."""
+    import csv
+    path = os.path.join(ROOT, "profiles", "r02", "kernel_stats_c3.csv")
+    try:
+        for r in csv.DictReader(open(path)):
+            if "k_seed_stream" in r["Name"]:
+                calls, avg_ns = int(r["Calls"]), float(r["AverageNs"])
+                if calls % max(1, n_launch):
+                    return None  # a different batch shape
+                gbs = bytes_per_launch / avg_ns
+                return {"source": "profiles/r02/kernel_stats_c3.csv", "launches": calls,
+                        "avg_us": round(avg_ns / 1e3, 1), "achieved": round(gbs, 1),
+                        "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    except (OSError, KeyError, ValueError):
+        return None
+    return None
+
+
 def issue_roofline():
     """The compute-bound kernels of the C3 step against their VALU issue roofline, from the
     committed counter pass (profiles/r02/pmc_valu_c3.json; one batch in flight), or None."""
@@ -409,6 +430,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
             "note": "HIP events on K1's stream around each group's back-to-back K1 launches (distinct read "
                     "ranges, no reuse; a group's K1s start once the previous group is done, so no other kernel shares the chip); "
                     "traffic: the committed FETCH_SIZE + WRITE_SIZE passes of this batch shape",
+            "rocprof_check": rocprof_k1(bytes_per_launch, n_launch),
         },
         "setup_s": {"genome": round(t_gen, 2), "index": round(t_idx, 2)},
         "hbm_in_use_gib": round((total - free) / 2**30, 1),
