@@ -1981,6 +1981,9 @@ hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs,
                         const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
                         const AfTails *tails, hipStream_t s) {
     // zscratch holds n_cu * 4 * AF_K2_WPS slots (api.hip ensure_zscratch), enough for both grids
+    // (a build with fewer slots than either grid would index past it: refuse to compile)
+    static_assert(AF_S2_WPS <= AF_K2_WPS && 6 <= AF_K2_WPS,
+                  "k_s2_regions / k_s2_records grids exceed the n_cu * 4 * AF_K2_WPS zscratch slots");
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
     dim3 g(n_cu * 4 * AF_S2_WPS), g3(n_cu * 16), g4(n_cu * 4 * 6), b(64);
