@@ -54,6 +54,12 @@ class AlignResult:
     def n_mapped(self):
         return int(((self.flag & 4) == 0).sum())
 
+    def n_overflow(self):
+        """Reads reported unmapped because a per-read cap of the S2 restatement bound
+        (AF_FLAG_MEM_OVERFLOW: MEMs / seeds / chains / regions or the region pool;
+        AF_FLAG_CIGAR_OVERFLOW: a CIGAR past AF_MAX_CIGAR ops).  bwa has no such caps."""
+        return int(((self.flag & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW)) != 0).sum())
+
     def partition(self):
         return partition(self)
 

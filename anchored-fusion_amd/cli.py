@@ -6,8 +6,9 @@
 Outputs go to `<out_folder>/<G>_fusion/<G>_fusion_predictions{,_abridged}.txt`, as in
 AF:138-141 and Final_fusion. Some flags are accepted only so that existing command lines keep
 working, and do nothing: `--not_train_filter_model`, `--positive_samples`, `--homo_gene_file`,
-`--negative_samples` (training is outside SURVEY.md §8) and `--thread` (host threads; the searches
-run on the GPU).  Without `--not_filter_false_positive` the filter model `--model_file` scores
+`--negative_samples` (training is outside SURVEY.md §8).  `--thread T` sets bwa's input chunk to
+10,000,000 x T bases (`bwa mem -t T` at AF:182/188 estimates insert sizes per chunk, so the records
+depend on it); the work itself runs on the GPU.  Without `--not_filter_false_positive` the filter model `--model_file` scores
 the candidates (AF:212-225); a missing model file is reported and the run continues unfiltered,
 as the reference does.
 
@@ -17,12 +18,15 @@ GPU LOCAL_RANK and joins an RCCL process group; S2 is sharded over the ranks (pi
 shard.py) and single-cell batches are dealt out to them (singlecell.run).
 """
 import argparse
+import datetime
 import os
 import socket
 import subprocess
 import sys
 
 from . import pipeline
+
+_PG_TIMEOUT = datetime.timedelta(hours=12)
 
 
 def parser():
@@ -40,7 +44,7 @@ def parser():
     ap.add_argument("--positive_samples", type=str, default="./data/positive_samples.txt", help="(accepted, unused)")
     ap.add_argument("--homo_gene_file", type=str, default="./data/homo_gene.npy", help="(accepted, unused)")
     ap.add_argument("--negative_samples", type=str, default="./Model/negative_samples.txt", help="(accepted, unused)")
-    ap.add_argument("--thread", type=str, default="1", help="(accepted, unused)")
+    ap.add_argument("--thread", type=str, default="1", help="bwa threads: sets the 10,000,000 x T base input chunk")
     ap.add_argument("--gpu_number", type=str, default="-1", help="GPU index (-1: the first visible GPU)")
     ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node to shard the pairs over (one process each)")
     return ap
@@ -61,11 +65,19 @@ def parser_singlecell():
     ap.add_argument("--positive_samples", type=str, default="./data/positive_samples.txt", help="(accepted, unused)")
     ap.add_argument("--homo_gene_file", type=str, default="./data/homo_gene.npy", help="(accepted, unused)")
     ap.add_argument("--negative_samples", type=str, default="./Model/negative_samples.txt", help="(accepted, unused)")
-    ap.add_argument("--thread", type=str, default="1", help="(accepted, unused)")
+    ap.add_argument("--thread", type=str, default="1", help="bwa threads: sets the 10,000,000 x T base input chunk")
     ap.add_argument("--gpu_number", type=str, default="-1", help="GPU index (-1: the first visible GPU)")
     ap.add_argument("--batch_pairs", type=int, default=1 << 22, help="pairs of whole cells per GPU alignment batch")
     ap.add_argument("--gpus", type=int, default=1, help="GPUs of this node to deal the cell batches to (one process each)")
     return ap
+
+
+def _chunk_bases(args):
+    """bwa's input chunk for --thread T (bwa mem: 10,000,000 x T bases, no -K)."""
+    t = int(args.thread)
+    if t < 1:
+        raise SystemExit("--thread must be >= 1")
+    return 10_000_000 * t
 
 
 def _launch(n, script, argv):
@@ -88,9 +100,11 @@ def _rank_device(args):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # rank 0 runs S3-S8 of each gene while the others wait in the next collective: a
+            # generous timeout instead of the watchdog default
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=_PG_TIMEOUT)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=_PG_TIMEOUT)
         return local
     dev = int(args.gpu_number)
     return dev if dev >= 0 else 0
@@ -125,7 +139,7 @@ def main_singlecell(argv=None):
     try:
         singlecell.run(args.file_anchored_cds, args.fastq_dir, args.file_ref_seq, args.file_ref_ann,
                        args.out_folder, gene_names=args.gene_names or None, device=dev, batch_pairs=args.batch_pairs,
-                       filt=_filter(args, dev))
+                       filt=_filter(args, dev), chunk_bases=_chunk_bases(args))
     finally:
         _finish()
     return 0
@@ -139,7 +153,8 @@ def main(argv=None):
     dev = _rank_device(args)
     try:
         pipeline.run(args.file_anchored_cds, args.fastq1, args.fastq2, args.file_ref_seq, args.file_ref_ann,
-                     args.out_folder, gene_names=args.gene_names or None, device=dev, filt=_filter(args, dev))
+                     args.out_folder, gene_names=args.gene_names or None, device=dev, filt=_filter(args, dev),
+                     chunk_bases=_chunk_bases(args))
     finally:
         _finish()
     return 0

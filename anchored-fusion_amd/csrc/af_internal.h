@@ -230,8 +230,8 @@ hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32
                            int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
 hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
                         const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
-                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
-                        const AfTails *tails, hipStream_t s);
+                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_slots,
+                        int32_t n_cu, const AfTails *tails, hipStream_t s);
 size_t af_s2_plan_bytes();
 hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *lens, int64_t chunk_bases,
                                int64_t *cstart, int64_t *scan_tmp, int32_t max_chunks, int32_t *n_chunks_dev,

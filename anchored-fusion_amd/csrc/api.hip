@@ -705,7 +705,7 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
                                       c->s2_max_chunks, c->s2_nchunks, s));
     if (tails && !append) HIPCHK(c, hipMemsetAsync(tails->n_tails, 0, 4, s));
     HIPCHK(c, af_launch_s2(ix->s2, d_reads, n_pairs, stride, d_lens, *p, opt, o->hits, c->cand, n_cand, w, *o,
-                           c->zscratch, c->n_cu, tails, s));
+                           c->zscratch, c->n_slots, c->n_cu, tails, s));
     return AF_OK;
 }
 

@@ -1978,15 +1978,18 @@ hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *l
 
 hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
                         const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
-                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_cu,
-                        const AfTails *tails, hipStream_t s) {
-    // zscratch holds n_cu * 4 * AF_K2_WPS slots (api.hip ensure_zscratch), enough for both grids
-    // (a build with fewer slots than either grid would index past it: refuse to compile)
+                        const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_slots,
+                        int32_t n_cu, const AfTails *tails, hipStream_t s) {
+    // zscratch holds n_slots = n_cu * 4 * AF_K2_WPS per-block slots (api.hip ensure_zscratch),
+    // indexed by blockIdx in k_s2_regions and k_s2_records: a build with fewer slots than either
+    // grid is refused at compile time, and a context whose slot count does not cover the grids
+    // (a runtime change of either) is refused here instead of faulting
     static_assert(AF_S2_WPS <= AF_K2_WPS && 6 <= AF_K2_WPS,
                   "k_s2_regions / k_s2_records grids exceed the n_cu * 4 * AF_K2_WPS zscratch slots");
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
     dim3 g(n_cu * 4 * AF_S2_WPS), g3(n_cu * 16), g4(n_cu * 4 * 6), b(64);
+    if ((int64_t)g.x > n_slots || (int64_t)g4.x > n_slots) return hipErrorInvalidConfiguration;
 #define AF_GO(C) hipLaunchKernelGGL((k_s2_regions<C>), g, b, 0, s, X, reads, stride, lens, p, o, cand, n_cand, w, \
                                     zscratch, zstride)
     if (cpl <= 2) AF_GO(2);

@@ -72,7 +72,7 @@ class Searches:
     `genome_sam_pe(pairs)` -> the SAM lines of `bwa mem -M genome fq1 fq2` (AF:188).
     Both render the genome placement's hits with bwa's record rules (bwa_records)."""
 
-    def __init__(self, genome_contigs, device=0, placer=None):
+    def __init__(self, genome_contigs, device=0, placer=None, chunk_bases=10_000_000):
         from . import bwa_records
         from .place import Placer
         self.genome = genome_contigs
@@ -90,7 +90,7 @@ class Searches:
 
         def genome_sam_pe(pairs):
             ref, p, hits, nh = _hits([s for _, a, b in pairs for s in (a, b)])
-            return bwa_records.pe_records(ref, pairs, hits, nh, p.T, p.min_seed_len)
+            return bwa_records.pe_records(ref, pairs, hits, nh, p.T, p.min_seed_len, chunk_bases=chunk_bases)
 
         self.genome_sam_se = genome_sam_se
         self.genome_sam_pe = genome_sam_pe
@@ -139,6 +139,10 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     tmp1, tmp2, anchored = res.partition()
     log(f"[{gene}] S2: {res.n_mapped()} of {res.n_reads} reads on the anchor; "
         f"{len(tmp1)} one-end-anchored pairs; {len(anchored)} anchored records")
+    n_ovf = res.n_overflow() if hasattr(res, "n_overflow") else 0
+    if n_ovf:
+        log(f"[{gene}] WARNING: {n_ovf} reads hit a per-read cap of the S2 restatement and are reported "
+            f"unmapped (AF_FLAG_MEM_OVERFLOW / AF_FLAG_CIGAR_OVERFLOW; bwa has no caps)")
     # S4: one-end-anchored pairs on the genome, paired as bwa pairs tmp1.fq / tmp2.fq (samtools
     # fastq restores the sequenced orientation of both ends)
     q4 = [(names[a // 2], seq(a), seq(b)) for a, b in zip(tmp1, tmp2)]
@@ -189,17 +193,20 @@ def dist_world(group=None):
 
 
 def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, log=print, group=None, filt=None):
+        aligner_factory=None, log=print, group=None, filt=None, chunk_bases=10_000_000):
     """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt.
 
     Inside a torch.distributed job of N > 1 ranks (cli --gpus N: one process per GPU, `device`
     = this rank's GPU), S2 is sharded: every rank aligns whole bwa chunks of the pairs and the
     candidate records are all-gathered on the device (shard.align_sharded); rank 0 then runs
-    S3-S8 and writes the tables, the other ranks return {}."""
+    S3-S8 and writes the tables, the other ranks return {}.
+
+    chunk_bases: bwa's input chunk, 10,000,000 x --thread (AF:182/188 `bwa mem -t T`): S2 and S4
+    estimate insert sizes per chunk, so the records depend on it as the reference's do."""
     rank, world = dist_world(group)
     if world > 1:
         return _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device,
-                            searches, aligner_factory, log, group, rank, world, filt)
+                            searches, aligner_factory, log, group, rank, world, filt, chunk_bases)
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
@@ -209,12 +216,9 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     index = ExonIndex.from_lines(gtf)
     names, reads, lens = read_pairs(fastq1, fastq2)
     if searches is None:
-        searches = Searches(genome, device=device)
+        searches = Searches(genome, device=device, chunk_bases=chunk_bases)
     if aligner_factory is None:
-        from .align import AnchorAligner
-
-        def aligner_factory(anchor):
-            return AnchorAligner(anchor, device=device)
+        aligner_factory = _default_aligner(device, chunk_bases)
     results = {}
     for gene, anchor in zip(genes, anchors):
         folder = os.path.join(out_folder, gene + "_fusion")
@@ -226,8 +230,18 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
 
 
 
+def _default_aligner(device, chunk_bases):
+    from .align import AnchorAligner
+
+    def factory(anchor):
+        a = AnchorAligner(anchor, device=device)
+        a.pe.chunk_bases = int(chunk_bases)
+        return a
+    return factory
+
+
 def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device, searches,
-                 aligner_factory, log, group, rank, world, filt=None):
+                 aligner_factory, log, group, rank, world, filt=None, chunk_bases=10_000_000):
     import torch
     import torch.distributed as dist
     from . import shard
@@ -236,10 +250,7 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
     names, reads, lens = read_pairs(fastq1, fastq2)
     if aligner_factory is None:
-        from .align import AnchorAligner
-
-        def aligner_factory(anchor):
-            return AnchorAligner(anchor, device=device)
+        aligner_factory = _default_aligner(device, chunk_bases)
     on_gpu = torch.cuda.is_available() and dist.get_backend(group) == "nccl"
     dev = f"cuda:{device}" if on_gpu else None
     genome = gtf = index = None
@@ -249,12 +260,13 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
             gtf = fh.readlines()
         index = ExonIndex.from_lines(gtf)
         if searches is None:
-            searches = Searches(genome, device=device)
+            searches = Searches(genome, device=device, chunk_bases=chunk_bases)
     results = {}
     for gene, anchor in zip(genes, anchors):
         aligner = aligner_factory(anchor.encode())
         try:
-            res = shard.align_sharded(aligner, reads, lens, rank, world, group=group, device=dev)
+            res = shard.align_sharded(aligner, reads, lens, rank, world, group=group, device=dev,
+                                      chunk_bases=chunk_bases)
         finally:
             close = getattr(aligner, "close", None)
             if close:

@@ -17,11 +17,12 @@ separate run on that cell would (the S3 sort and every consumer see only the cel
 | SC:218-256 per-cell S3-S8, `Final_fusion` | `pipeline.consume_gene` per cell |
 | SC:258-287 merge by the first five columns, count cells | `merge_cell_tables` |
 
-Deviation, on purpose: the reference's merge reads the span/split counts from columns 6 and
-7 of each cell's `_predictions.txt`, the filter-model layout (column 5 = Natural_score).  With
-`--not_filter_false_positive` (the only mode built here: the filter model is outside §8) the
-counts are columns 5 and 6, and column 7 holds read names, on which the reference's `int()`
-raises.  The merge reads the counts from the columns the table actually has.
+The merge reads the span/split counts from columns 6 and 7 of each cell's `_predictions.txt`,
+as SC:277-283 does: that is the filter-model layout (column 5 = Natural_score), the default
+mode whenever the model file exists.  With `--not_filter_false_positive` (or a missing model
+file, which the reference also turns into the no-filter tables) the counts are columns 5 and 6
+and column 7 holds read names, on which the reference's `int()` raises; there, on purpose, the
+merge reads columns 5 and 6.  Each cell table's header says which layout it has.
 """
 import os
 import re
@@ -89,7 +90,9 @@ def _per_segment(aligner, reads, lens, seg_pairs):
 def merge_cell_tables(cells, work_folder, out_name, out_prefix):
     """SC:258-287: the per-cell `_predictions.txt` tables merged into
     `<out_prefix>_gene_cell_predictions{,_abridged}.txt` (rows keyed by the first five columns,
-    in first-seen order; counts summed; cells listed).  Counts from the no-filter layout."""
+    in first-seen order; counts summed; cells listed).  A table whose header has Natural_score
+    (the filter layout) gives its counts from columns 6-7, exactly as SC:277-283; a no-filter
+    table from columns 5-6 (module docstring)."""
     head = ["Fusion_gene", "Anchored_gene_X", "X_clip_location", "Partner_gene_Y", "Y_clip_location"]
     merged = {}
     with open(out_prefix + "_gene_cell_predictions.txt", "w") as fo:
@@ -100,10 +103,11 @@ def merge_cell_tables(cells, work_folder, out_name, out_prefix):
                 lines = fh.readlines()
             if len(lines) <= 1:
                 continue
+            c0 = 6 if "Natural_score" in lines[0].split("\t") else 5
             for line in lines[1:]:
                 arr = line.split("\t")
                 key = "$".join(arr[:5])
-                span, split = int(arr[5]), int(arr[6])
+                span, split = int(arr[c0]), int(arr[c0 + 1])
                 if key not in merged:
                     merged[key] = [span, split, 1, [cell]]
                 else:
@@ -112,7 +116,7 @@ def merge_cell_tables(cells, work_folder, out_name, out_prefix):
                     v[1] += split
                     v[2] += 1
                     v[3].append(cell)
-                fo.write(cell + "\t" + "\t".join(arr[0:5] + arr[5:7]) + "\n")
+                fo.write(cell + "\t" + "\t".join(arr[0:5] + arr[c0:c0 + 2]) + "\n")
     with open(out_prefix + "_gene_cell_predictions_abridged.txt", "w") as fa:
         fa.write("\t".join(head + ["All_Spanning_read_count", "All_Breakpoint_read_count", "Single_cells_count",
                                    "Single_cells_name"]) + "\n")
@@ -122,7 +126,7 @@ def merge_cell_tables(cells, work_folder, out_name, out_prefix):
 
 
 def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, batch_pairs=1 << 22, log=print, filt=None):
+        aligner_factory=None, batch_pairs=1 << 22, log=print, filt=None, chunk_bases=10_000_000):
     """All genes x all cells; writes `<out>/<G>/<G>_fusion_gene_cell_predictions*.txt` and the
     per-cell tables under `<out>/<G>/work_dir/<cell>/`.  Returns {gene: merged rows}."""
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
@@ -140,12 +144,10 @@ def run(anchored_cds, fastq_dir, ref_seq, ref_ann, out_folder, gene_names=None, 
     data = {k: read_pairs(os.path.join(fastq_dir, cells[k][1]), os.path.join(fastq_dir, cells[k][2]))
             for k in range(rank, len(cells), world)}
     if searches is None:
-        searches = Searches(genome, device=device)
+        searches = Searches(genome, device=device, chunk_bases=chunk_bases)
     if aligner_factory is None:
-        from .align import AnchorAligner
-
-        def aligner_factory(anchor):
-            return AnchorAligner(anchor, device=device)
+        from .pipeline import _default_aligner
+        aligner_factory = _default_aligner(device, chunk_bases)
     # whole cells per GPU batch
     mine, cur, n = [], [], 0
     for k, (_, reads, _) in data.items():

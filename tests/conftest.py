@@ -23,7 +23,7 @@ def _native_builds():
     # make's dependency rules rebuild a library older than its sources (a stale .so shipped to
     # the GPU box would otherwise be tested); up to date, each call is a no-op
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "anchored-fusion_amd", "csrc")], check=True)
+    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "anchored-fusion_amd", "csrc")], check=True)
     yield
 
 

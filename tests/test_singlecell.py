@@ -60,6 +60,64 @@ def test_merge_cell_tables(tmp_path):
                         "c3\tG--P\tG\tG:10\tP:p1\tchr2:500\t5\t6"]
 
 
+def test_merge_cell_tables_filter_layout(tmp_path):
+    """SC:277-283 on the filter-model layout (column 5 = Natural_score): counts from columns 6-7."""
+    work = str(tmp_path / "work")
+    head = "Fusion_gene\tAnchored_gene_X\tX_clip_location\tPartner_gene_Y\tY_clip_location\tNatural_score\t" \
+           "Spanning_read_count\tBreakpoint_read_count\tSpanning_reads\tBreakpoint_reads\tHomo_genes\n"
+    rows = {"c1": ["G--P\tG\tG:10\tP:p1\tchr2:500\t0.93\t3\t4\tr1;r2;r3\ts1;s2;s3;s4\t\n"],
+            "c2": ["G--P\tG\tG:10\tP:p1\tchr2:500\t0.5\t1\t2\tr7\ts5;s6\t\n"]}
+    for c, rs in rows.items():
+        os.makedirs(os.path.join(work, c))
+        with open(os.path.join(work, c, "G_fusion_predictions.txt"), "w") as fh:
+            fh.write(head + "".join(rs))
+    merged = singlecell.merge_cell_tables([(c, "", "") for c in rows], work, "G_fusion", str(tmp_path / "G_fusion"))
+    assert merged["G--P$G$G:10$P:p1$chr2:500"][:3] == [4, 6, 2]
+    full = open(str(tmp_path / "G_fusion_gene_cell_predictions.txt")).read().splitlines()
+    assert full[1:] == ["c1\tG--P\tG\tG:10\tP:p1\tchr2:500\t3\t4", "c2\tG--P\tG\tG:10\tP:p1\tchr2:500\t1\t2"]
+
+
+def test_singlecell_filter_model_cpu_backends(tmp_path):
+    """singlecell.run with a filter model present (the default mode of SC:241-256): each cell's
+    table has the Natural_score layout and the merge sums its span/split columns (SC:277-283)."""
+    import torch
+    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
+    from anchored_fusion_amd import filter_model
+    from anchored_fusion_amd.place import Placer
+    paths, _ = make_world(str(tmp_path / "world"))
+    fqd = str(tmp_path / "cells")
+    cells = _split_cells(paths, fqd, n_cells=2)
+    genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
+
+    def searches():
+        return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference,
+                                                       tile_factory=OracleTileReference))
+    torch.manual_seed(3)
+    model = str(tmp_path / "model.pt")
+    # the world's windows are 301 long (get_test_reads: 100 + left + 'H' + right + 100 pad)
+    torch.save(filter_model.FusionFilter(301).double().state_dict(), model)
+    out = str(tmp_path / "sc")
+    singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], out, searches=searches(),
+                   aligner_factory=OracleAligner, batch_pairs=4000, log=lambda *_: None,
+                   filt=dict(model_file=model, device="cpu"))
+    sums, n_rows = {}, 0
+    for c in cells:
+        lines = open(os.path.join(out, "BCRX", "work_dir", c, "BCRX_fusion_predictions.txt")).read().splitlines()
+        assert lines[0].split("\t")[5] == "Natural_score"
+        for ln in lines[1:]:
+            a = ln.split("\t")
+            v = sums.setdefault("$".join(a[:5]), [0, 0])
+            v[0] += int(a[6])
+            v[1] += int(a[7])
+            n_rows += 1
+    assert n_rows > 0
+    ab = [ln.split("\t") for ln in open(os.path.join(out, "BCRX", "BCRX_fusion_gene_cell_predictions_abridged.txt"))
+          .read().splitlines()[1:]]
+    assert {"$".join(r[:5]): [int(r[5]), int(r[6])] for r in ab} == sums
+    full = open(os.path.join(out, "BCRX", "BCRX_fusion_gene_cell_predictions.txt")).read().splitlines()
+    assert len(full) == 1 + n_rows
+
+
 def _split_cells(paths, d, n_cells=3):
     """Writes the world's pairs as n_cells cells (contiguous slices) under d."""
     n1, s1 = afio.read_fastq(paths["fq1"])
