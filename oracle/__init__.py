@@ -210,3 +210,142 @@ class OracleTiles:
         if rc != 0:
             raise RuntimeError(f"afo_blat failed: {rc}")
         return rows, nr
+
+
+# ---- the genome calls S4 / S5 (bwa_pe.c, FM mode) ---------------------------------------
+G_MAX_REC = 8
+GREC_DTYPE = np.dtype([("read", "<i4"), ("flag", "<i4"), ("rid", "<i4"), ("mrid", "<i4"), ("pos", "<i8"),
+                       ("mpos", "<i8"), ("score", "<i4"), ("n_cigar", "<i4"), ("seq_b", "<i4"), ("seq_e", "<i4"),
+                       ("cigar", "<u4", (MAX_CIGAR,))])
+assert GREC_DTYPE.itemsize == 176
+REG_DTYPE = np.dtype([("rb", "<i8"), ("re", "<i8"), ("qb", "<i4"), ("qe", "<i4"), ("rid", "<i4"), ("score", "<i4"),
+                      ("truesc", "<i4"), ("w", "<i4"), ("seedcov", "<i4"), ("seedlen0", "<i4")])
+assert REG_DTYPE.itemsize == 48
+
+
+def _glib():
+    L = lib()
+    if not getattr(L, "_genome_bound", False):
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.afo_genome_build.restype = vp
+        L.afo_genome_build.argtypes = [ctypes.c_char_p, vp, vp, ctypes.c_int, ctypes.c_int]
+        L.afo_genome_free.argtypes = [vp]
+        L.afo_genome_lpac.restype = i64
+        L.afo_genome_lpac.argtypes = [vp]
+        L.afo_genome_text.restype = vp
+        L.afo_genome_text.argtypes = [vp]
+        L.afo_genome_sa.restype = vp
+        L.afo_genome_sa.argtypes = [vp]
+        L.afo_genome_primary.restype = i64
+        L.afo_genome_primary.argtypes = [vp]
+        L.afo_genome_seeds.restype = ctypes.c_int
+        L.afo_genome_seeds.argtypes = [vp, vp, i32, ctypes.POINTER(Params), ctypes.POINTER(Pe), ctypes.c_int, vp, vp,
+                                       vp, i32]
+        L.afo_genome_regions.restype = ctypes.c_int
+        L.afo_genome_regions.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe),
+                                         ctypes.c_int, i32, vp, vp]
+        L.afo_genome_align_se.restype = ctypes.c_int
+        L.afo_genome_align_se.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe), i64,
+                                          ctypes.c_int, i32, vp, vp]
+        L.afo_genome_align_pe.restype = ctypes.c_int
+        L.afo_genome_align_pe.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe),
+                                          ctypes.c_int, i32, vp, vp]
+        L._genome_bound = True
+    return L
+
+
+class OracleGenome:
+    """bwa's index of a multi-contig genome (bns_fasta2bntseq + the FM index) and the genome calls
+    S4 (`bwa mem -M genome fq1 fq2`, AF:188) and S5 (`bwa mem -M genome reads.fa`, fn:716).
+
+    contigs: [(name, seq)].  memset_too: also build the MEM-set seeding structures (the anchor's
+    restatement) for the seed cross-check."""
+
+    def __init__(self, contigs, memset_too=False):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob = b"".join(s.encode() if isinstance(s, str) else bytes(s) for _, s in contigs)
+        off = np.concatenate([[0], np.cumsum(self.lens)[:-1]]).astype(np.int64)
+        ln = np.asarray(self.lens, dtype=np.int64)
+        self._blob = blob
+        self.h = _glib().afo_genome_build(blob, off.ctypes.data, ln.ctypes.data, len(contigs), int(bool(memset_too)))
+        if not self.h:
+            raise ValueError("empty genome")
+        self.l_pac = int(_glib().afo_genome_lpac(self.h))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.afo_genome_free(self.h)
+            self.h = None
+
+    def text(self):
+        p = _glib().afo_genome_text(self.h)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * (2 * self.l_pac)).from_address(p)).copy()
+
+    def sa(self):
+        p = _glib().afo_genome_sa(self.h)
+        return np.ctypeslib.as_array((ctypes.c_int64 * (2 * self.l_pac + 1)).from_address(p)).copy()
+
+    def primary(self):
+        return int(_glib().afo_genome_primary(self.h))
+
+    def seeds(self, read, params=None, pe=None, memset=False, cap=1 << 16):
+        """mem_chain's seed walk for one read: (rbeg int64, qbeg, len) arrays."""
+        r = np.frombuffer(read.encode() if isinstance(read, str) else bytes(read), dtype=np.uint8).copy()
+        rb = np.zeros(cap, np.int64)
+        qb = np.zeros(cap, np.int32)
+        ln = np.zeros(cap, np.int32)
+        n = _glib().afo_genome_seeds(self.h, r.ctypes.data, len(r), ctypes.byref(params or default_params()),
+                                     ctypes.byref(pe or default_pe()), int(memset), rb.ctypes.data, qb.ctypes.data,
+                                     ln.ctypes.data, cap)
+        if n < 0:
+            raise OverflowError(f"afo_genome_seeds: {n}")
+        return rb[:n], qb[:n], ln[:n]
+
+    def regions(self, reads, lens=None, params=None, pe=None, max_reg=64, threads=0):
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        regs = np.zeros((n, max_reg), dtype=REG_DTYPE)
+        nreg = np.zeros(n, dtype=np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = _glib().afo_genome_regions(self.h, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
+                                        ctypes.byref(params or default_params()), ctypes.byref(pe or default_pe()),
+                                        int(threads), max_reg, regs.ctypes.data, nreg.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"afo_genome_regions failed: {rc}")
+        return regs, nreg
+
+    def align_se(self, reads, lens=None, params=None, pe=None, id_base=0, threads=0, max_rec=G_MAX_REC):
+        """S5: (records [n, max_rec] GREC_DTYPE, counts [n])."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        recs = np.zeros((n, max_rec), dtype=GREC_DTYPE)
+        nrec = np.zeros(n, dtype=np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = _glib().afo_genome_align_se(self.h, reads.ctypes.data, n, reads.shape[1],
+                                         None if lp is None else lp.ctypes.data, ctypes.byref(params or default_params()),
+                                         ctypes.byref(pe or default_pe()), int(id_base), int(threads), max_rec,
+                                         recs.ctypes.data, nrec.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"afo_genome_align_se failed: {rc}")
+        return recs, nrec
+
+    def align_pe(self, reads, lens=None, params=None, pe=None, pair_base=0, chunk_bases=None, threads=0,
+                 max_rec=G_MAX_REC):
+        """S4 on pair-major reads [2N, stride]: (records [2N, max_rec] GREC_DTYPE, counts [2N])."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        nr = reads.shape[0]
+        assert nr % 2 == 0
+        recs = np.zeros((nr, max_rec), dtype=GREC_DTYPE)
+        nrec = np.zeros(nr, dtype=np.int32)
+        e = pe or default_pe()
+        e.pair_base = int(pair_base)
+        if chunk_bases is not None:
+            e.chunk_bases = int(chunk_bases)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = _glib().afo_genome_align_pe(self.h, reads.ctypes.data, nr // 2, reads.shape[1],
+                                         None if lp is None else lp.ctypes.data, ctypes.byref(params or default_params()),
+                                         ctypes.byref(e), int(threads), max_rec, recs.ctypes.data, nrec.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"afo_genome_align_pe failed: {rc}")
+        return recs, nrec

@@ -82,6 +82,51 @@ typedef struct {
 #define AFO_PE_MAX_REG 32
 #define AFO_PE_MAX_TSPAN 1024  /* longest reference span mem_patch_reg merges */
 
+/* ---- the genome calls S4 / S5 (bwa_pe.c, FM mode): `bwa mem -M` against a multi-contig genome.
+ * Per-read caps of the restatement (the GPU's AF_G_MAX_*); past one the read is reported
+ * unmapped with AF_FLAG_MEM_OVERFLOW (bwa has none). */
+#define AFO_G_MAX_PMEM 65536   /* MEM-set cross-check mode only */
+#define AFO_G_MAX_INTV 512     /* seed intervals (mem_collect_intv) */
+#define AFO_G_MAX_OCC 8192     /* chain seeds (max_occ-sampled occurrences) */
+#define AFO_G_MAX_CHAIN 8192
+#define AFO_G_MAX_REG 1024
+#define AFO_G_MAX_REC 8        /* SAM records per read (primary + -M parts) */
+typedef struct afo_text afo_genome;
+/* one printed SAM record (mem_aln2sam): FLAG as printed (0x100 for -M parts), contig / 0-based
+ * position (-1: '*'), the mate's, AS, CIGAR in BAM op codes (H = 5 on parts after the first),
+ * SEQ = the read in the record's orientation, sliced [seq_b, seq_e) */
+typedef struct {
+    int32_t read, flag, rid, mrid;
+    int64_t pos, mpos;
+    int32_t score, n_cigar, seq_b, seq_e;
+    uint32_t cigar[AFO_MAX_CIGAR];
+} afo_grec;
+/* one region of mem_align1_core (mem_alnreg_t) */
+typedef struct {
+    int64_t rb, re;
+    int32_t qb, qe, rid, score, truesc, w, seedcov, seedlen0;
+} afo_reg;
+/* blob: the contigs at ctg_off[k], ctg_len[k] (bytes between them ignored); memset_too: also
+ * the MEM-set seeding structures (suffix ranks, 16-mer positions) for the cross-check */
+afo_genome *afo_genome_build(const char *blob, const int64_t *ctg_off, const int64_t *ctg_len, int n_ctg,
+                             int memset_too);
+void afo_genome_free(afo_genome *G);
+int64_t afo_genome_lpac(const afo_genome *G);
+const uint8_t *afo_genome_text(const afo_genome *G);   /* the bwa text T, 2 l_pac codes */
+const int64_t *afo_genome_sa(const afo_genome *G);     /* suffix array rows 0..2 l_pac */
+int64_t afo_genome_primary(const afo_genome *G);
+int afo_genome_seeds(const afo_genome *G, const uint8_t *read, int32_t l, const afo_params *p, const afo_pe *pe,
+                     int memset_mode, int64_t *rbeg, int32_t *qbeg, int32_t *len, int32_t cap);
+int afo_genome_regions(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                       const afo_params *p, const afo_pe *pe, int n_threads, int32_t max_reg, afo_reg *regs,
+                       int32_t *n_reg);
+int afo_genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                        const afo_params *p, const afo_pe *pe, int64_t id_base, int n_threads, int32_t max_rec,
+                        afo_grec *recs, int32_t *n_rec);
+int afo_genome_align_pe(const afo_genome *G, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
+                        const afo_params *p, const afo_pe *pe, int n_threads, int32_t max_rec, afo_grec *recs,
+                        int32_t *n_rec);
+
 void afo_params_default(afo_params *p);
 afo_index *afo_index_build(const char *anchor, int64_t n);
 void afo_index_free(afo_index *idx);
