@@ -36,8 +36,12 @@ EXPORTS = (
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
     "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_index_build_genome_device", "af_gather_reads_device", "af_blat_params_default", "af_tile_index_build",
     "af_tile_index_build_device", "af_blat", "af_blat_device", "af_blat_device_range", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
-    "af_fastq_close",
+    "af_fastq_close", "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
+    "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
+    "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats",
 )
+AF_G_MAX_REC = 8
+AF_GSTAT_N = 4
 
 
 class AFError(RuntimeError):
@@ -157,6 +161,31 @@ def lib():
     L.af_fastq_error.restype = ctypes.c_char_p
     L.af_fastq_close.argtypes = [_vp]
     L.af_fastq_close.restype = None
+    _pp = ctypes.POINTER(Params)
+    L.af_genome_build.argtypes = [_vp, _vp, _i64, _vp, _vp, _i32, ctypes.POINTER(_vp)]
+    L.af_genome_build.restype = ctypes.c_int
+    L.af_genome_build_device.argtypes = [_vp, _vp, _i64, _vp, _vp, _i32, ctypes.POINTER(_vp)]
+    L.af_genome_build_device.restype = ctypes.c_int
+    L.af_genome_free.argtypes = [_vp]
+    L.af_genome_free.restype = None
+    L.af_genome_lpac.argtypes = [_vp]
+    L.af_genome_lpac.restype = _i64
+    L.af_genome_primary.argtypes = [_vp]
+    L.af_genome_primary.restype = _i64
+    L.af_genome_read.argtypes = [_vp, _vp, _i32, _i64, _i64, _vp]
+    L.af_genome_read.restype = ctypes.c_int
+    L.af_genome_align_se_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _i64, _vp, _vp, _vp]
+    L.af_genome_align_se_device.restype = ctypes.c_int
+    L.af_genome_align_pe_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _vp, _vp, _vp]
+    L.af_genome_align_pe_device.restype = ctypes.c_int
+    L.af_genome_align_se.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _i64, _vp, _vp]
+    L.af_genome_align_se.restype = ctypes.c_int
+    L.af_genome_align_pe.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _vp, _vp]
+    L.af_genome_align_pe.restype = ctypes.c_int
+    L.af_genome_regions.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _i32, _vp, _vp]
+    L.af_genome_regions.restype = ctypes.c_int
+    L.af_genome_stats.argtypes = [_vp, _vp]
+    L.af_genome_stats.restype = ctypes.c_int
     _L = L
     return L
 

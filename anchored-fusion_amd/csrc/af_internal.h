@@ -195,12 +195,69 @@ __device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *re
     t.tail_read[slot] = (int32_t)(t.read_base + r);
 }
 
+// ---- the genome index of S4 / S5 (fmindex.hip; `bwa index <genome.fa>`) -----------------
+// The bwa text T of l_pac contig bases (N = 2 l_pac), its suffix array (rows 0..N, '$' smallest)
+// and the FM occurrence table: per 128 rows, counts of A/C/G/T before the block then the rows'
+// BWT characters at 2 bits (row k of the block at bits 2 (k & 31) of word k >> 5); the '$' row
+// (`primary`) is stored as A and corrected on lookup.
+struct DevGenome {
+    const uint8_t *T = nullptr;    // codes 0..3
+    int64_t *sa = nullptr;
+    uint64_t *occ = nullptr;
+    int64_t *ctg_off_d = nullptr, *ctg_len_d = nullptr;  // contigs in pac (bns anns)
+    int64_t l_pac = 0, N = 0, primary = -1, n_blk = 0;
+    int64_t C[4] = {0, 0, 0, 0};   // first row of the suffixes starting with c
+    int64_t base_cnt[4] = {0, 0, 0, 0};
+    int32_t n_ctg = 0;
+};
+hipError_t af_fm_build(const uint8_t *d_blob, const int64_t *src_off, const int64_t *src_len, int n_ctg, DevGenome *G,
+                       hipStream_t s);
+void af_fm_free(DevGenome *G);
+
+// ---- S4 / S5 on the genome (bwa_genome.hip) -------------------------------------------------
+using GOpt = S2Opt;
+struct GIv { int64_t sa_k, s; int32_t qb, qe; };     // a seed interval: SA rows [sa_k, sa_k + s), query [qb, qe)
+struct GReg {                                        // mem_alnreg_t
+    int64_t rb, re;
+    int32_t qb, qe, rid, score, truesc, w, seedcov, seedlen0, secondary, sub;
+    uint64_t hash;
+};
+// per-call pools and counters of the genome kernels (per context)
+struct GWork {
+    GIv *iv;                    // intervals of every read (G1)
+    int64_t iv_cap;
+    unsigned long long *iv_fill;
+    int64_t *iv_off;
+    int32_t *iv_n;              // per read; -1 overflow
+    GReg *reg;                  // regions of every read (G2)
+    int64_t reg_cap;
+    int32_t *reg_fill;
+    int32_t *reg_off, *reg_n;   // per read; reg_n -1 overflow
+    int32_t *heads;             // G2 dequeue heads (8 lines)
+    int32_t *stats;             // AF_GSTAT_*
+};
+size_t af_g1_slot_bytes();
+size_t af_g2_slot_bytes();
+hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                                    const int32_t *d_n, int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
+                                    uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
+                                    uint8_t *zscratch, hipStream_t s);
+hipError_t af_launch_genome_se(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const GWork &w,
+                               uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs, int32_t *n_rec,
+                               hipStream_t s);
+hipError_t af_launch_genome_pe(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                               const int32_t *d_npairs, int64_t cap_pairs, const af_params &p, const GOpt &o,
+                               const GWork &w, const S2Work &sw, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch,
+                               af_grec *recs, int32_t *n_rec, hipStream_t s);
+hipError_t af_launch_s2_pestat(const S2Work &w, int32_t max_ins, hipStream_t s);
+
 // launch helpers (defined in the .hip files)
 // ctrl (AF_CTRL_BYTES, one 128-B line per word, no memsets on the hot path):
 //  [AF_HEAD_STRIDE * e], e = 0, 1: candidate count of K1 epoch e (K1 of epoch e zeroes the
 //                                  other epoch's count for the next call);
 //  [AF_HEAD_STRIDE * (10 + x)], x = 0..7: dequeue heads of K2 (k_pairs zeroes them after K2);
-//  (words 2..9 and 18 are unused).
+//  (word 18 is unused).
 #define AF_HEAD_STRIDE 32
 #define AF_CTRL_BYTES (4 * AF_HEAD_STRIDE * 41)
 #define AF_CTRL_HEADS2 (10 * AF_HEAD_STRIDE)
@@ -210,6 +267,8 @@ __device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *re
 //  [AF_HEAD_STRIDE * (39 + e)]: S2 candidate-pair count of epoch e (K1 of epoch e zeroes both
 //  words of its epoch).
 #define AF_CTRL_PLACE_HEADS (19 * AF_HEAD_STRIDE)
+//  [AF_HEAD_STRIDE * (2 + x)], x = 0..7: dequeue heads of the genome region kernel (bwa_genome.hip)
+#define AF_CTRL_G_HEADS (2 * AF_HEAD_STRIDE)
 #define AF_CTRL_PLACE_N (27 * AF_HEAD_STRIDE)
 #define AF_CTRL_S2_HEADS3 (29 * AF_HEAD_STRIDE)
 #define AF_CTRL_S2_POOL (37 * AF_HEAD_STRIDE)

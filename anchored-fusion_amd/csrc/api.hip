@@ -71,6 +71,28 @@ struct af_ctx {
     uint32_t *d_cigar = nullptr;
     int64_t cap_out = 0;
     hipStream_t stream = nullptr;
+    // the genome calls S4 / S5 (bwa_genome.hip): per-lane / per-wave scratch, per-call pools
+    uint8_t *g1_scr = nullptr, *g2_scr = nullptr;
+    int g1_threads = 0, g2_waves = 0;
+    GIv *g_iv = nullptr;
+    GReg *g_reg = nullptr;
+    int64_t g_iv_cap = 0, g_reg_cap = 0, g_cap_reads = 0;
+    unsigned long long *g_iv_fill = nullptr;
+    int32_t *g_reg_fill = nullptr, *g_stats = nullptr, *g_iv_n = nullptr, *g_reg_off = nullptr, *g_reg_n = nullptr;
+    int64_t *g_iv_off = nullptr;
+    int32_t *g_ghist = nullptr, *g_nchunks = nullptr;
+    int64_t g_ghist_ints = 0, *g_cstart = nullptr, *g_scan = nullptr, g_scan_cap = 0;
+    S2Pes *g_pes = nullptr;
+    int32_t g_max_chunks = 0;
+    af_grec *g_recs = nullptr;      // host-buffer API staging
+    int32_t *g_nrec = nullptr, *g_hlens = nullptr;
+    uint8_t *g_hreads = nullptr;
+    int64_t g_cap_recs = 0, g_cap_hbytes = 0;
+};
+
+struct af_genome {
+    af_ctx *ctx = nullptr;
+    DevGenome dev{};
 };
 
 struct af_index {
@@ -346,6 +368,124 @@ int check_params(af_ctx *c, const af_params *p) {
     return AF_OK;
 }
 
+
+// ---- genome calls (bwa_genome.hip) ------------------------------------------------------
+// per-lane G1 scratch (2 waves per CU) and per-wave G2-G4 scratch (8 waves per CU, <= n_slots of
+// the context's traceback scratch)
+int ensure_genome_scratch(af_ctx *c) {
+    if (c->g1_scr) return AF_OK;
+    c->g1_threads = c->n_cu * 2 * 64;
+    c->g2_waves = std::min(c->n_cu * 8, c->n_slots);
+    HIPCHK(c, hipMalloc(&c->g1_scr, af_g1_slot_bytes() * (size_t)c->g1_threads));
+    HIPCHK(c, hipMalloc(&c->g2_scr, af_g2_slot_bytes() * (size_t)c->g2_waves));
+    HIPCHK(c, hipMalloc(&c->g_iv_fill, sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->g_reg_fill, sizeof(int32_t)));
+    HIPCHK(c, hipMalloc(&c->g_stats, sizeof(int32_t) * AF_GSTAT_N));
+    HIPCHK(c, hipMemset(c->g_stats, 0, sizeof(int32_t) * AF_GSTAT_N));
+    return ensure_zscratch(c);
+}
+
+// pools for a call over n_reads reads: intervals (96 per read on average; a read's list is at
+// most AF_G_MAX_INTV) and regions (16 per read on average)
+int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
+    if (n_reads <= c->g_cap_reads) return AF_OK;
+    af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_off); af_free(c->g_iv_n); af_free(c->g_reg_off);
+    af_free(c->g_reg_n);
+    c->g_iv = nullptr; c->g_reg = nullptr; c->g_iv_off = nullptr; c->g_iv_n = nullptr; c->g_reg_off = nullptr;
+    c->g_reg_n = nullptr; c->g_cap_reads = 0;
+    const int64_t cap = std::max<int64_t>(n_reads, 1 << 14);
+    c->g_iv_cap = cap * 96 + AF_G_MAX_INTV;
+    c->g_reg_cap = cap * 16 + AF_G_MAX_REG;
+    HIPCHK(c, hipMalloc(&c->g_iv, sizeof(GIv) * c->g_iv_cap));
+    HIPCHK(c, hipMalloc(&c->g_reg, sizeof(GReg) * c->g_reg_cap));
+    HIPCHK(c, hipMalloc(&c->g_iv_off, sizeof(int64_t) * cap));
+    HIPCHK(c, hipMalloc(&c->g_iv_n, sizeof(int32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->g_reg_off, sizeof(int32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->g_reg_n, sizeof(int32_t) * cap));
+    c->g_cap_reads = cap;
+    return AF_OK;
+}
+
+GWork genome_work(af_ctx *c) {
+    GWork w;
+    w.iv = c->g_iv; w.iv_cap = c->g_iv_cap; w.iv_fill = c->g_iv_fill; w.iv_off = c->g_iv_off; w.iv_n = c->g_iv_n;
+    w.reg = c->g_reg; w.reg_cap = c->g_reg_cap; w.reg_fill = c->g_reg_fill; w.reg_off = c->g_reg_off;
+    w.reg_n = c->g_reg_n;
+    w.heads = c->ctrl + AF_CTRL_G_HEADS;
+    w.stats = c->g_stats;
+    return w;
+}
+
+int check_genome_call(af_ctx *c, const af_genome *g, const af_params *p, const af_pe *e, int32_t stride) {
+    if (!c || !g || !g->dev.sa) return fail(c, AF_E_INVALID, "null context or genome");
+    if (!p || p->a <= 0 || p->b < 0 || p->o_del < 0 || p->e_del <= 0 || p->o_ins < 0 || p->e_ins <= 0 || p->w < 0 ||
+        p->min_seed_len < 1 || p->max_occ < 1)
+        return fail(c, AF_E_INVALID, "invalid af_params");
+    if (stride < 1) return fail(c, AF_E_INVALID, "stride must be >= 1");
+    return e ? check_pe(c, e) : AF_OK;
+}
+
+// S2Work view of the S4 chunk statistics (k_s2_pestat; ragged chunk starts from the lengths)
+int ensure_genome_pe(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bases, int32_t max_ins) {
+    const int64_t mc = std::min<int64_t>(n_pairs, 2 * n_pairs * (int64_t)stride / std::max<int64_t>(chunk_bases, 1) + 2) + 1;
+    if (mc > c->g_max_chunks) {
+        af_free(c->g_pes); af_free(c->g_cstart); af_free(c->g_nchunks);
+        c->g_pes = nullptr; c->g_cstart = nullptr; c->g_nchunks = nullptr; c->g_max_chunks = 0;
+        const int64_t m = std::max<int64_t>(mc, 16);
+        HIPCHK(c, hipMalloc(&c->g_pes, sizeof(S2Pes) * 4 * m));
+        HIPCHK(c, hipMalloc(&c->g_cstart, sizeof(int64_t) * (m + 1)));
+        HIPCHK(c, hipMalloc(&c->g_nchunks, sizeof(int32_t)));
+        c->g_max_chunks = (int32_t)m;
+    }
+    if (n_pairs > c->g_scan_cap) {
+        af_free(c->g_scan);
+        c->g_scan = nullptr; c->g_scan_cap = 0;
+        HIPCHK(c, hipMalloc(&c->g_scan, sizeof(int64_t) * std::max<int64_t>(n_pairs, 1)));
+        c->g_scan_cap = std::max<int64_t>(n_pairs, 1);
+    }
+    const int64_t hints = (int64_t)c->g_max_chunks * 4 * (max_ins + 1);
+    if (hints > c->g_ghist_ints) {
+        af_free(c->g_ghist);
+        c->g_ghist = nullptr; c->g_ghist_ints = 0;
+        HIPCHK(c, hipMalloc(&c->g_ghist, sizeof(int32_t) * hints));
+        HIPCHK(c, hipMemset(c->g_ghist, 0, sizeof(int32_t) * hints));
+        c->g_ghist_ints = hints;
+    }
+    return AF_OK;
+}
+
+int genome_build(af_ctx *c, const char *blob, int64_t n_blob, const int64_t *ctg_off, const int64_t *ctg_len,
+                 int32_t n_ctg, af_genome **out, bool on_device) {
+    if (!c || !blob || !ctg_off || !ctg_len || !out || n_ctg < 1 || n_blob < 1)
+        return fail(c, AF_E_INVALID, "null or empty argument");
+    *out = nullptr;
+    for (int k = 0; k < n_ctg; ++k)
+        if (ctg_off[k] < 0 || ctg_len[k] < 1 || ctg_off[k] + ctg_len[k] > n_blob)
+            return fail(c, AF_E_INVALID, "contig %d outside the blob", k);
+    (void)hipSetDevice(c->device);
+    const uint8_t *d_blob = reinterpret_cast<const uint8_t *>(blob);
+    uint8_t *tmp = nullptr;
+    if (!on_device) {
+        HIPCHK(c, hipMalloc(&tmp, n_blob));
+        if (hipMemcpy(tmp, blob, n_blob, hipMemcpyHostToDevice) != hipSuccess) {
+            af_free(tmp);
+            return fail(c, AF_E_HIP, "genome copy to the device failed");
+        }
+        d_blob = tmp;
+    }
+    af_genome *g = new (std::nothrow) af_genome;
+    if (!g) { af_free(tmp); return fail(c, AF_E_NOMEM, "out of host memory"); }
+    g->ctx = c;
+    const hipError_t e = af_fm_build(d_blob, ctg_off, ctg_len, n_ctg, &g->dev, c->stream);
+    af_free(tmp);
+    if (e != hipSuccess) {
+        delete g;
+        return fail(c, e == hipErrorOutOfMemory ? AF_E_NOMEM : AF_E_HIP, "genome index build: %s", hipGetErrorString(e));
+    }
+    *out = g;
+    return AF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -403,6 +543,10 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
     af_free(c->s3_keys); af_free(c->s3_temp); af_free(c->s3_counts);
     af_free(c->g_sel); af_free(c->g_sel_n); af_free(c->g_temp);
+    af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
+    af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n);
+    af_free(c->g_iv_off); af_free(c->g_ghist); af_free(c->g_nchunks); af_free(c->g_cstart); af_free(c->g_scan);
+    af_free(c->g_pes); af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens); af_free(c->g_hreads);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1077,4 +1221,201 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
     return AF_OK;
 }
 
+// ---- genome calls S4 / S5 ------------------------------------------------------------------
+int af_genome_build(af_ctx *c, const char *blob, int64_t n_blob, const int64_t *ctg_off, const int64_t *ctg_len,
+                    int32_t n_ctg, af_genome **out) {
+    return genome_build(c, blob, n_blob, ctg_off, ctg_len, n_ctg, out, false);
+}
+int af_genome_build_device(af_ctx *c, const char *d_blob, int64_t n_blob, const int64_t *ctg_off,
+                           const int64_t *ctg_len, int32_t n_ctg, af_genome **out) {
+    return genome_build(c, d_blob, n_blob, ctg_off, ctg_len, n_ctg, out, true);
+}
+void af_genome_free(af_genome *g) {
+    if (!g) return;
+    if (g->ctx) (void)hipSetDevice(g->ctx->device);
+    af_fm_free(&g->dev);
+    delete g;
+}
+int64_t af_genome_lpac(const af_genome *g) { return g ? g->dev.l_pac : -1; }
+int64_t af_genome_primary(const af_genome *g) { return g ? g->dev.primary : -1; }
+
+int af_genome_read(af_ctx *c, const af_genome *g, int32_t what, int64_t first, int64_t n, void *out) {
+    if (!c || !g || !out || first < 0 || n < 0) return fail(c, AF_E_INVALID, "bad argument");
+    const int64_t rows = what == 0 ? g->dev.N : g->dev.N + 1;
+    if (what < 0 || what > 1 || first + n > rows) return fail(c, AF_E_INVALID, "range outside the text / suffix array");
+    (void)hipSetDevice(c->device);
+    if (what == 0) HIPCHK(c, hipMemcpy(out, g->dev.T + first, n, hipMemcpyDeviceToHost));
+    else HIPCHK(c, hipMemcpy(out, g->dev.sa + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    return AF_OK;
+}
+
+static GOpt genome_opt(const af_pe *e) {
+    af_pe d;
+    if (!e) { af_pe_default(&d); e = &d; }
+    return GOpt{e->pen_unpaired, e->max_ins, e->max_matesw, e->split_width, e->max_mem_intv, e->max_chain_gap,
+                e->pair_base};
+}
+
+int af_genome_align_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                              const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
+                              af_grec *d_recs, int32_t *d_n_rec, void *stream) {
+    int rc = check_genome_call(c, g, p, pe, stride);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!d_reads || !d_recs || !d_n_rec))) return fail(c, AF_E_INVALID, "null argument");
+    if (n == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const GOpt o = genome_opt(pe);
+    const GWork w = genome_work(c);
+    HIPCHK(c, af_launch_genome_regions(g->dev, d_reads, stride, d_lens, nullptr, n, *p, o, w, c->g1_scr, c->g1_threads,
+                                       c->g2_scr, c->g2_waves, c->zscratch, s));
+    HIPCHK(c, af_launch_genome_se(g->dev, d_reads, stride, d_lens, nullptr, n, *p, id_base, w, c->g2_scr, c->g2_waves,
+                                  c->zscratch, d_recs, d_n_rec, s));
+    return AF_OK;
+}
+
+int af_genome_align_pe_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs,
+                              int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                              af_grec *d_recs, int32_t *d_n_rec, void *stream) {
+    af_pe e;
+    if (pe) e = *pe;
+    else af_pe_default(&e);
+    int rc = check_genome_call(c, g, p, &e, stride);
+    if (rc) return rc;
+    if (n_pairs < 0 || (n_pairs > 0 && (!d_reads || !d_lens || !d_recs || !d_n_rec)))
+        return fail(c, AF_E_INVALID, "null argument (paired-end calls need the read lengths)");
+    if (n_pairs == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, 2 * n_pairs)) ||
+        (rc = ensure_genome_pe(c, n_pairs, stride, e.chunk_bases, e.max_ins)))
+        return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const GOpt o = genome_opt(&e);
+    const GWork w = genome_work(c);
+    S2Work sw{};
+    sw.ghist = c->g_ghist; sw.pes = c->g_pes; sw.ppc = 0; sw.cstart = c->g_cstart; sw.n_chunks = c->g_nchunks;
+    sw.max_chunks = c->g_max_chunks;
+    HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, e.chunk_bases, c->g_cstart, c->g_scan, c->g_max_chunks,
+                                  c->g_nchunks, s));
+    HIPCHK(c, af_launch_genome_regions(g->dev, d_reads, stride, d_lens, nullptr, 2 * n_pairs, *p, o, w, c->g1_scr,
+                                       c->g1_threads, c->g2_scr, c->g2_waves, c->zscratch, s));
+    HIPCHK(c, af_launch_genome_pe(g->dev, d_reads, stride, d_lens, nullptr, n_pairs, *p, o, w, sw, c->g2_scr,
+                                  c->g2_waves, c->zscratch, d_recs, d_n_rec, s));
+    return AF_OK;
+}
+
+// host-buffer forms: reads / lens staged through the context's buffers
+static int genome_stage(af_ctx *c, const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
+                        bool need_lens, const int32_t **d_lens) {
+    const int64_t bytes = n_reads * (int64_t)stride;
+    if (bytes > c->g_cap_hbytes) {
+        af_free(c->g_hreads); c->g_hreads = nullptr; c->g_cap_hbytes = 0;
+        HIPCHK(c, hipMalloc(&c->g_hreads, bytes + 16));
+        c->g_cap_hbytes = bytes;
+    }
+    if (n_reads > c->g_cap_recs) {
+        af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens);
+        c->g_recs = nullptr; c->g_nrec = nullptr; c->g_hlens = nullptr; c->g_cap_recs = 0;
+        HIPCHK(c, hipMalloc(&c->g_recs, sizeof(af_grec) * AF_G_MAX_REC * n_reads));
+        HIPCHK(c, hipMalloc(&c->g_nrec, sizeof(int32_t) * n_reads));
+        HIPCHK(c, hipMalloc(&c->g_hlens, sizeof(int32_t) * n_reads));
+        c->g_cap_recs = n_reads;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->g_hreads, reads, bytes, hipMemcpyHostToDevice, c->stream));
+    *d_lens = nullptr;
+    if (lens || need_lens) {
+        if (lens) HIPCHK(c, hipMemcpyAsync(c->g_hlens, lens, sizeof(int32_t) * n_reads, hipMemcpyHostToDevice, c->stream));
+        else {
+            std::vector<int32_t> u((size_t)n_reads, stride);
+            HIPCHK(c, hipMemcpyAsync(c->g_hlens, u.data(), sizeof(int32_t) * n_reads, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
+        *d_lens = c->g_hlens;
+    }
+    return AF_OK;
+}
+
+static int genome_unstage(af_ctx *c, int64_t n_reads, af_grec *recs, int32_t *n_rec) {
+    HIPCHK(c, hipMemcpyAsync(recs, c->g_recs, sizeof(af_grec) * AF_G_MAX_REC * n_reads, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(n_rec, c->g_nrec, sizeof(int32_t) * n_reads, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return AF_OK;
+}
+
+int af_genome_align_se(af_ctx *c, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                       const int32_t *lens, const af_params *p, const af_pe *pe, int64_t id_base, af_grec *recs,
+                       int32_t *n_rec) {
+    int rc = check_genome_call(c, g, p, pe, stride);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!reads || !recs || !n_rec))) return fail(c, AF_E_INVALID, "null argument");
+    if (n == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    const int32_t *d_lens = nullptr;
+    if ((rc = genome_stage(c, reads, n, stride, lens, false, &d_lens))) return rc;
+    if ((rc = af_genome_align_se_device(c, g, c->g_hreads, n, stride, d_lens, p, pe, id_base, c->g_recs, c->g_nrec,
+                                        c->stream)))
+        return rc;
+    return genome_unstage(c, n, recs, n_rec);
+}
+
+int af_genome_align_pe(af_ctx *c, const af_genome *g, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                       const int32_t *lens, const af_params *p, const af_pe *pe, af_grec *recs, int32_t *n_rec) {
+    int rc = check_genome_call(c, g, p, pe, stride);
+    if (rc) return rc;
+    if (n_pairs < 0 || (n_pairs > 0 && (!reads || !recs || !n_rec))) return fail(c, AF_E_INVALID, "null argument");
+    if (n_pairs == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    const int32_t *d_lens = nullptr;
+    if ((rc = genome_stage(c, reads, 2 * n_pairs, stride, lens, true, &d_lens))) return rc;
+    if ((rc = af_genome_align_pe_device(c, g, c->g_hreads, n_pairs, stride, d_lens, p, pe, c->g_recs, c->g_nrec,
+                                        c->stream)))
+        return rc;
+    return genome_unstage(c, 2 * n_pairs, recs, n_rec);
+}
+
+int af_genome_regions(af_ctx *c, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                      const int32_t *lens, const af_params *p, const af_pe *pe, int32_t max_reg, int64_t *regs,
+                      int32_t *n_reg) {
+    int rc = check_genome_call(c, g, p, pe, stride);
+    if (rc) return rc;
+    if (n < 0 || max_reg < 1 || (n > 0 && (!reads || !regs || !n_reg))) return fail(c, AF_E_INVALID, "bad argument");
+    if (n == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    const int32_t *d_lens = nullptr;
+    if ((rc = genome_stage(c, reads, n, stride, lens, false, &d_lens))) return rc;
+    if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
+    const GWork w = genome_work(c);
+    HIPCHK(c, af_launch_genome_regions(g->dev, c->g_hreads, stride, d_lens, nullptr, n, *p, genome_opt(pe), w, c->g1_scr,
+                                       c->g1_threads, c->g2_scr, c->g2_waves, c->zscratch, c->stream));
+    std::vector<int32_t> off((size_t)n);
+    int32_t fill = 0;
+    HIPCHK(c, hipMemcpyAsync(n_reg, c->g_reg_n, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(off.data(), c->g_reg_off, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&fill, c->g_reg_fill, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<GReg> pool((size_t)std::max<int64_t>(std::min<int64_t>(fill, c->g_reg_cap), 1));
+    if (fill > 0) HIPCHK(c, hipMemcpy(pool.data(), c->g_reg, sizeof(GReg) * std::min<int64_t>(fill, c->g_reg_cap),
+                                      hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < n; ++r) {
+        for (int k = 0; k < n_reg[r] && k < max_reg; ++k) {
+            const GReg &a = pool[(size_t)off[r] + k];
+            int64_t *o = regs + (r * max_reg + k) * 12;
+            o[0] = a.rb; o[1] = a.re; o[2] = a.qb; o[3] = a.qe; o[4] = a.rid; o[5] = a.score; o[6] = a.truesc;
+            o[7] = a.w; o[8] = a.seedcov; o[9] = a.seedlen0; o[10] = 0; o[11] = 0;
+        }
+    }
+    return AF_OK;
+}
+
+int af_genome_stats(af_ctx *c, int32_t *out) {
+    if (!c || !out) return fail(c, AF_E_INVALID, "null argument");
+    if (!c->g_stats) { for (int k = 0; k < AF_GSTAT_N; ++k) out[k] = 0; return AF_OK; }
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->g_stats, sizeof(int32_t) * AF_GSTAT_N, hipMemcpyDeviceToHost));
+    return AF_OK;
+}
+
 }  // extern "C"
+

@@ -1,0 +1,201 @@
+// bwa_dev.h -- device restatements of bwa / klib routines shared by the S2 kernels (s2.hip,
+// the anchor) and the genome calls S4 / S5 (bwa_genome.hip): klib's introsort (unstable, so its
+// exact tie order is part of bwa's behaviour), utils.h hash_64, and one pass of ksw.c's striped
+// local SW (ksw_u8 / ksw_i16) on the wave.  Header-only, anonymous namespace (see ksw_dp.h).
+#pragma once
+#include "ksw_dp.h"
+
+#ifndef S2DBGL
+#ifdef AF_S2_DEBUG
+#define S2DBGL(...) printf(__VA_ARGS__)
+#else
+#define S2DBGL(...) do { } while (0)
+#endif
+#endif
+
+namespace {
+
+__device__ __forceinline__ int wave_min(int v) { return -wave_max(-v); }
+__device__ __forceinline__ int lanes_below(uint64_t m, int lane) {
+    return __builtin_popcountll(m & ((1ull << lane) - 1ull));
+}
+
+// ---- klib ksort.h introsort (lane 0; unstable -- tie orders are bwa's) --------------------
+template <class T, class LT>
+__device__ void ks_ins(T *a, int s, int t, LT lt) {
+    for (int i = s + 1; i < t; ++i)
+        for (int j = i; j > s && lt(a[j], a[j - 1]); --j) { T sw = a[j]; a[j] = a[j - 1]; a[j - 1] = sw; }
+}
+template <class T, class LT>
+__device__ void ks_comb(T *a, int n, LT lt) {
+    const double shrink_factor = 1.2473309501039786540366528676643;
+    int do_swap;
+    size_t gap = (size_t)n;
+    do {
+        if (gap > 2) {
+            gap = (size_t)((double)gap / shrink_factor);
+            if (gap == 9 || gap == 10) gap = 11;
+        }
+        do_swap = 0;
+        for (int i = 0; i < n - (int)gap; ++i) {
+            const int j = i + (int)gap;
+            if (lt(a[j], a[i])) { T t = a[i]; a[i] = a[j]; a[j] = t; do_swap = 1; }
+        }
+    } while (do_swap || gap > 2);
+    if (gap != 1) ks_ins(a, 0, n, lt);
+}
+template <class T, class LT>
+__device__ void ks_introsort(T *a, int n, LT lt) {
+    if (n < 1) return;
+    if (n == 2) {
+        if (lt(a[1], a[0])) { T sw = a[0]; a[0] = a[1]; a[1] = sw; }
+        return;
+    }
+    int d;
+    for (d = 2; (1ul << d) < (unsigned long)n; ++d) ;
+    // klib pushes the larger part and continues with the smaller (segments of <= 16 are left to
+    // the final insertion sort), so the stack holds at most
+    // log2(n / 17) + 1 segments: 20 covers n <= 17 << 19 (call sites sort <= 16384 items)
+    int stl[20], str[20], std_[20], top = 0;
+    int s = 0, t = n - 1;
+    d <<= 1;
+    for (;;) {
+        S2DBGL("introsort s %d t %d d %d top %d\n", s, t, d, top);
+        if (s < t) {
+            if (--d == 0) { ks_comb(a + s, t - s + 1, lt); t = s; continue; }
+            int i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            if (lt(a[k], a[i])) {
+                if (lt(a[k], a[j])) k = j;
+            } else k = lt(a[j], a[i]) ? i : j;
+            const T rp = a[k];
+            if (k != t) { T sw = a[k]; a[k] = a[t]; a[t] = sw; }
+            for (;;) {
+                // a[t] == rp ends the first scan; the explicit bound keeps a broken comparator from
+                // walking off the array
+                do ++i; while (i < t && lt(a[i], rp));
+                S2DBGL("introsort scan i %d lt(a[t], rp) %d\n", i, (int)lt(a[t], rp));
+                do --j; while (i <= j && lt(rp, a[j]));
+                if (j <= i) break;
+                T sw = a[i]; a[i] = a[j]; a[j] = sw;
+                S2DBGL("introsort swap i %d j %d\n", i, j);
+            }
+            S2DBGL("introsort part i %d j %d k %d\n", i, j, k);
+            { T sw = a[i]; a[i] = a[t]; a[t] = sw; }
+            if (i - s > t - i) {
+                if (i - s > 16) { stl[top] = s; str[top] = i - 1; std_[top] = d; ++top; }
+                s = t - i > 16 ? i + 1 : t;
+            } else {
+                if (t - i > 16) { stl[top] = i + 1; str[top] = t; std_[top] = d; ++top; }
+                t = i - s > 16 ? i - 1 : s;
+            }
+        } else {
+            if (top == 0) { ks_ins(a, 0, n, lt); return; }
+            --top; s = stl[top]; t = str[top]; d = std_[top];
+        }
+    }
+}
+
+// utils.h hash_64
+__device__ __forceinline__ uint64_t hash_64(uint64_t key) {
+    key += ~(key << 32);
+    key ^= (key >> 22);
+    key += ~(key << 13);
+    key ^= (key >> 8);
+    key += (key << 3);
+    key ^= (key >> 15);
+    key += ~(key << 27);
+    key ^= (key >> 31);
+    return key;
+}
+
+struct SwRes { int score, te, qe; };
+
+// One pass of ksw_u8 / ksw_i16 (oracle ksw_sw) on the wave.  The striped kernel's result is
+// H(i,j) = max(G, F) with G = max(H(i-1,j-1) + S, E, 0) and F the full horizontal-gap term,
+// while E(i+1,j) is fed by the first-pass value max(G, F within the query's stripe block
+// [blk * slen, (blk + 1) * slen)) -- the lazy-F loop does not revisit E.  Lanes hold C query
+// columns each; both F terms are prefix maxima (one plain, one keyed by block).  The target base
+// of row i is tg[i] (rev: tg[te0 - i] for i <= te0, as the start pass's partly reversed target);
+// tg is the LDS window when it holds the whole target.  Stops at the first row reaching endsc.
+template <int C>
+__device__ SwRes ksw_pass(const uint8_t *q, int qlen, const uint8_t *tg, int tlen, int rev_te, int P,
+                             const af_params &p, int endsc, int lane) {
+    const int slen = (qlen + P - 1) / P;
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    const int shift = p.b > 1 ? p.b : 1;  // ksw_qinit: minus the smallest score of the matrix (N: -1)
+    const int j0 = lane * C;
+    int H[C], E[C], qc[C], blk[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int j = j0 + c;
+        H[c] = 0; E[c] = 0;
+        qc[c] = j < qlen ? q[j] : 4;
+        blk[c] = j < qlen ? j / slen : 0;
+    }
+    SwRes r{0, -1, -1};
+    int gmax = 0;
+    int t_next = tlen > 0 ? tg[rev_te >= 0 ? rev_te : 0] : 4;
+    for (int i = 0; i < tlen; ++i) {
+        const int ti = __builtin_amdgcn_readfirstlane(t_next);
+        if (i + 1 < tlen) t_next = tg[rev_te >= 0 && i + 1 <= rev_te ? rev_te - i - 1 : i + 1];
+        const int from_left = wave_shr1(0, H[C - 1]);
+        int G[C], runX = kNeg, runK = -1, bxX[C], bxK[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int j = j0 + c;
+            const bool in = j < qlen;
+            const int hd = c == 0 ? from_left : H[c - 1];
+            const int s = (ti > 3 || qc[c] > 3) ? -1 : (ti == qc[c] ? p.a : -p.b);
+            G[c] = max(max(hd + s, 0), E[c]);
+            bxX[c] = runX; bxK[c] = runK;
+            if (in) {
+                const int X = G[c] - oe_ins + j * p.e_ins;
+                runX = max(runX, X);
+                runK = max(runK, (blk[c] << 20) | (X + (1 << 19)));
+            }
+        }
+        const int lexX = wave_shr1(kNeg, wave_incl_max(runX));
+        const int lexK = wave_shr1(-1, wave_incl_max(runK));
+        int rowmax = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int j = j0 + c;
+            const bool in = j < qlen;
+            const int PX = max(lexX, bxX[c]);
+            const int F = PX <= kNeg / 2 ? 0 : max(PX - (j - 1) * p.e_ins, 0);
+            const int PK = max(lexK, bxK[c]);
+            const int Fs = (PK >= 0 && (PK >> 20) == blk[c]) ? max((PK & 0xFFFFF) - (1 << 19) - (j - 1) * p.e_ins, 0) : 0;
+            const int h = max(G[c], F);
+            const int hfp = max(G[c], Fs);
+            E[c] = max(max(E[c] - p.e_del, hfp - oe_del), 0);
+            H[c] = in ? h : 0;
+            if (in) rowmax = max(rowmax, h);
+        }
+        rowmax = wave_max(rowmax);
+        if (rowmax > gmax) {
+            gmax = rowmax;
+            r.te = i;
+            int qj = 1 << 30;
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                if (j0 + c < qlen && H[c] == gmax) qj = min(qj, j0 + c);
+            r.qe = wave_min(qj);
+            if ((P == 16 && gmax + shift >= 255) || gmax >= endsc) break;
+        }
+    }
+    r.score = (P == 16 && gmax + shift >= 255) ? 255 : gmax;
+    if (r.score == 255) r.qe = -1;
+    return r;
+}
+
+__device__ SwRes ksw_pass_any(const uint8_t *q, int qlen, const uint8_t *tg, int tlen, int rev_te, int P,
+                                 const af_params &p, int endsc, int lane) {
+    const int cpl = (qlen + 63) >> 6;  // <= 5 (AF_MAX_READ 320)
+    if (cpl <= 1) return ksw_pass<1>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 2) return ksw_pass<2>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 3) return ksw_pass<3>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    if (cpl == 4) return ksw_pass<4>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+    return ksw_pass<5>(q, qlen, tg, tlen, rev_te, P, p, endsc, lane);
+}
+
+}  // namespace

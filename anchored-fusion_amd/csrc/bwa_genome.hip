@@ -1,0 +1,1575 @@
+// bwa_genome.hip -- the genome calls of the reference on the GPU, as bwa 0.7.17 computes them:
+//     S4  bwa mem -M -t T <genome.fa> tmp1.fq tmp2.fq   (Anchored_Fusion.py:188), paired-end
+//     S5  bwa mem -M -t T <genome.fa> split_reads.fa    (functions.py:716), single-end
+// over the genome index of fmindex.hip.  oracle/bwa_pe.c (FM mode) is the bit-exact contract;
+// each device routine names the bwa routine it restates.
+//
+// Kernels (one launch each per call, on the caller's stream):
+//   G1 k_g_seeds     one LANE per read (the FM walk is a chain of dependent lookups, so a wave
+//                    keeps 64 reads' lookups in flight): mem_collect_intv -- bwt_smem1 passes 1
+//                    and 2, bwt_seed_strategy1 -- on the bidirectional FM index; the read's
+//                    intervals (SA row range, size, query span) sorted by (qb, qe) into a pool
+//   G2 k_g_regions   one wave per read: mem_chain (occurrences sampled at max_occ in SA order,
+//                    64 SA rows gathered per step; klib kbtree on lane 0), mem_chain_flt,
+//                    mem_chain2aln (ksw_extend2 on the wave, ksw_dp.h, windows clipped to the
+//                    seed's contig: bns_fetch_seq), mem_sort_dedup_patch (same contig only) ->
+//                    the read's regions into a pool
+//   G3 k_g_se        one wave per read (S5): mem_mark_primary_se (hash_64 tie-break on the read
+//                    id), mem_reg2sam with -M (mem_reg2aln: band inference + ksw_global2 on the
+//                    wave; -M parts as 0x100 with hard clips) -> af_grec records
+//   PE               k_g_pe_hist (one lane per pair: mem_pestat's insert sizes per bwa chunk),
+//                    k_s2_pestat (s2.hip), k_g_pe (one wave per pair: mem_matesw with ksw_align2
+//                    on the wave, mem_mark_primary_se, mem_pair, mem_sam_pe's branches and
+//                    mem_reg2sam / mem_aln2sam for every record of both ends)
+//
+// Per-read state that can grow with repeats (seed lists, chains, the kbtree, regions) lives in
+// per-wave global scratch (L2 / Infinity Cache resident for the common short lists); the DP
+// rows, query and target windows in LDS (ksw_dp.h g_dp).  Caps equal the oracle's AFO_G_MAX_*;
+// a read past one is reported unmapped with AF_FLAG_MEM_OVERFLOW, counted in the call's stats.
+#include "bwa_dev.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int G_LIST = AF_MAX_READ + 2;
+constexpr int G_KB_T = 5, G_KB_MAXK = 2 * G_KB_T - 1;
+constexpr int G_KB_NODES = AF_G_MAX_CHAIN / 2 + 64;  // t = 5: >= 4 keys per non-root node
+
+struct GBi { int64_t k, l, s; int32_t qb, qe; };     // bwtintv_t (x[0], x[1], x[2], info)
+struct GSeed { int64_t rbeg; int32_t qbeg, len; };   // mem_seed_t (score = len)
+struct GChain { int64_t pos; int32_t n, first, rid, w, kept, seed0; };  // mem_chain_t
+struct GKb { int16_t n, internal; int16_t key[G_KB_MAXK]; int16_t ptr[G_KB_MAXK + 1]; };
+
+// ================================================================== FM index (bwt.c)
+// occurrences of c among the first m (<= 32) 2-bit fields of w
+__device__ __forceinline__ int cnt_code(uint64_t w, int c, int m) {
+    const uint64_t t = ~(w ^ (0x5555555555555555ull * (uint64_t)c));
+    uint64_t y = t & (t >> 1) & 0x5555555555555555ull;
+    if (m < 32) y &= (1ull << (2 * m)) - 1ull;
+    return __builtin_popcountll(y);
+}
+// bwt_occ4: occurrences of A/C/G/T in the BWT rows [0, i)
+__device__ __forceinline__ void fm_occ4(const DevGenome &G, int64_t i, int64_t o[4]) {
+    const int64_t b = i >> 7;
+    const int r = (int)(i & 127);
+    const uint4 *blk = reinterpret_cast<const uint4 *>(G.occ + b * 8);
+    const uint4 c01 = blk[0], c23 = blk[1], w01 = blk[2], w23 = blk[3];
+    const uint64_t cnt[4] = {(uint64_t)c01.x | (uint64_t)c01.y << 32, (uint64_t)c01.z | (uint64_t)c01.w << 32,
+                             (uint64_t)c23.x | (uint64_t)c23.y << 32, (uint64_t)c23.z | (uint64_t)c23.w << 32};
+    const uint64_t w[4] = {(uint64_t)w01.x | (uint64_t)w01.y << 32, (uint64_t)w01.z | (uint64_t)w01.w << 32,
+                           (uint64_t)w23.x | (uint64_t)w23.y << 32, (uint64_t)w23.z | (uint64_t)w23.w << 32};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int64_t v = (int64_t)cnt[c];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int m = r - 32 * k;
+            if (m > 0) v += cnt_code(w[k], c, m > 32 ? 32 : m);
+        }
+        o[c] = v;
+    }
+    if (G.primary >= (b << 7) && G.primary < i) o[0] -= 1;  // the '$' row is stored as A
+}
+// bwt_extend, backward: ok[c] = the bi-interval of cW (oracle fm_back4)
+__device__ __forceinline__ void fm_back4(const DevGenome &G, const GBi &ik, GBi ok[4]) {
+    int64_t a[4], b[4];
+    fm_occ4(G, ik.k, a);
+    fm_occ4(G, ik.k + ik.s, b);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { ok[c].k = G.C[c] + a[c]; ok[c].s = b[c] - a[c]; }
+    ok[3].l = ik.l + (ik.k <= G.primary && ik.k + ik.s - 1 >= G.primary);
+    ok[2].l = ok[3].l + ok[3].s;
+    ok[1].l = ok[2].l + ok[2].s;
+    ok[0].l = ok[1].l + ok[1].s;
+}
+// bwt_extend, forward (is_back = 0): ok[c'] for W -> W comp(c')
+__device__ __forceinline__ void fm_fwd4(const DevGenome &G, const GBi &ik, GBi ok[4]) {
+    GBi sw = ik;
+    sw.k = ik.l; sw.l = ik.k;
+    GBi o[4];
+    fm_back4(G, sw, o);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { ok[c].k = o[c].l; ok[c].l = o[c].k; ok[c].s = o[c].s; }
+}
+__device__ __forceinline__ GBi fm_set(const DevGenome &G, int c) {
+    GBi b;
+    b.k = G.C[c]; b.s = G.base_cnt[c]; b.l = G.C[3 - c]; b.qb = 0; b.qe = 0;
+    return b;
+}
+
+// ============================================================= G1: mem_collect_intv
+// bwt_smem1 (oracle fm_smem1): q = the read's codes in this lane's scratch
+__device__ int g_smem1(const DevGenome &G, const uint8_t *q, int len, int x, int64_t min_intv, GBi *mem, int *n_mem,
+                       GBi *prev, GBi *curr) {
+    int i, j, c, ret, np = 0, nc = 0;
+    GBi ik, ok[4];
+    *n_mem = 0;
+    if (q[x] > 3) return x + 1;
+    if (min_intv < 1) min_intv = 1;
+    ik = fm_set(G, q[x]);
+    ik.qe = x + 1;
+    for (i = x + 1; i < len; ++i) {  // forward search
+        if (q[i] < 4) {
+            c = 3 - q[i];
+            fm_fwd4(G, ik, ok);
+            if (ok[c].s != ik.s) {
+                curr[nc++] = ik;
+                if (ok[c].s < min_intv) break;
+            }
+            ik = ok[c]; ik.qe = i + 1;
+        } else {
+            curr[nc++] = ik;
+            break;
+        }
+    }
+    if (i == len) curr[nc++] = ik;
+    for (j = 0; j < nc >> 1; ++j) { GBi t = curr[j]; curr[j] = curr[nc - 1 - j]; curr[nc - 1 - j] = t; }
+    ret = curr[0].qe;
+    { GBi *sw = curr; curr = prev; prev = sw; }
+    np = nc;
+    for (i = x - 1; i >= -1; --i) {  // backward search for MEMs
+        c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
+        nc = 0;
+        for (j = 0; j < np; ++j) {
+            const GBi p = prev[j];
+            if (c >= 0) fm_back4(G, p, ok);
+            if (c < 0 || ok[c].s < min_intv) {
+                if (nc == 0) {
+                    if (*n_mem == 0 || i + 1 < mem[*n_mem - 1].qb) {
+                        GBi t = p;
+                        t.qb = i + 1;
+                        mem[(*n_mem)++] = t;
+                    }
+                }
+            } else if (nc == 0 || ok[c].s != curr[nc - 1].s) {
+                GBi t = ok[c];
+                t.qe = p.qe; t.qb = 0;
+                curr[nc++] = t;
+            }
+        }
+        if (nc == 0) break;
+        { GBi *sw = curr; curr = prev; prev = sw; }
+        np = nc;
+    }
+    for (j = 0; j < *n_mem >> 1; ++j) { GBi t = mem[j]; mem[j] = mem[*n_mem - 1 - j]; mem[*n_mem - 1 - j] = t; }
+    return ret;
+}
+
+// bwt_seed_strategy1 (oracle fm_seed_strategy1)
+__device__ int g_seed_strategy1(const DevGenome &G, const uint8_t *q, int len, int x, int min_len, int max_intv,
+                                GBi *mem) {
+    GBi ik, ok[4];
+    mem->s = 0;
+    if (q[x] > 3) return x + 1;
+    ik = fm_set(G, q[x]);
+    for (int i = x + 1; i < len; ++i) {
+        if (q[i] < 4) {
+            const int c = 3 - q[i];
+            fm_fwd4(G, ik, ok);
+            if (ok[c].s < max_intv && i - x >= min_len) {
+                *mem = ok[c];
+                mem->qb = x; mem->qe = i + 1;
+                return i + 1;
+            }
+            ik = ok[c];
+        } else return i + 1;
+    }
+    return len;
+}
+
+__device__ __forceinline__ uint8_t nt4(uint8_t ch) {
+    return ch == 'A' || ch == 'a' ? 0 : ch == 'C' || ch == 'c' ? 1 : ch == 'G' || ch == 'g' ? 2
+         : ch == 'T' || ch == 't' ? 3 : 4;
+}
+__device__ __forceinline__ int read_len(const int32_t *lens, int64_t r, int32_t stride) {
+    int l = lens ? lens[r] : stride;
+    if (l > stride) l = stride;
+    if (l > AF_MAX_READ) l = AF_MAX_READ;
+    return l < 0 ? 0 : l;
+}
+
+// per-lane scratch of G1: prev / curr / mem1 lists, the interval list, the read's codes
+constexpr int64_t G1_SLOT_BIV = 3 * G_LIST + AF_G_MAX_INTV + G_LIST;
+constexpr int64_t G1_SLOT_BYTES = G1_SLOT_BIV * (int64_t)sizeof(GBi) + AF_MAX_READ + 16;
+
+__global__ __launch_bounds__(64) void k_g_seeds(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
+                                                int64_t cap, int64_t read0, af_params p, GOpt o,
+                                                uint8_t *__restrict__ scratch, GWork w) {
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+    int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
+    if (n > cap) n = cap;
+    GBi *base = reinterpret_cast<GBi *>(scratch + tid * G1_SLOT_BYTES);
+    GBi *prev = base, *curr = base + G_LIST, *m1 = base + 2 * G_LIST, *fmm = base + 3 * G_LIST;
+    uint8_t *q = reinterpret_cast<uint8_t *>(base + G1_SLOT_BIV);
+    const int msl = p.min_seed_len;
+    const int split_len = (int)((float)msl * 1.5f + .499);
+    for (int64_t rr = read0 + tid; rr < n; rr += nthr) {
+        const int len = read_len(lens, rr, stride);
+        const uint8_t *rd = reads + rr * (int64_t)stride;
+        for (int x = 0; x < len; ++x) q[x] = nt4(rd[x]);
+        int ni = 0, n1 = 0;
+        bool ovf = false;
+        if (len >= msl) {
+            int x = 0;
+            while (x < len && !ovf) {  // pass 1: SMEMs
+                if (q[x] < 4) {
+                    x = g_smem1(G, q, len, x, 1, m1, &n1, prev, curr);
+                    for (int i = 0; i < n1; ++i)
+                        if (m1[i].qe - m1[i].qb >= msl) {
+                            if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
+                            fmm[ni++] = m1[i];
+                        }
+                } else ++x;
+            }
+            const int old_n = ni;
+            for (int k = 0; k < old_n && !ovf; ++k) {  // pass 2: re-seeding
+                const GBi pk = fmm[k];
+                if (pk.qe - pk.qb < split_len || pk.s > o.split_width) continue;
+                g_smem1(G, q, len, (pk.qb + pk.qe) >> 1, pk.s + 1, m1, &n1, prev, curr);
+                for (int i = 0; i < n1; ++i)
+                    if (m1[i].qe - m1[i].qb >= msl) {
+                        if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
+                        fmm[ni++] = m1[i];
+                    }
+            }
+            if (o.max_mem_intv > 0) {  // pass 3: bwt_seed_strategy1
+                x = 0;
+                while (x < len && !ovf) {
+                    if (q[x] < 4) {
+                        GBi m;
+                        x = g_seed_strategy1(G, q, len, x, msl, o.max_mem_intv, &m);
+                        if (m.s > 0) {
+                            if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
+                            fmm[ni++] = m;
+                        }
+                    } else ++x;
+                }
+            }
+        }
+        if (ovf) { w.iv_n[rr] = -1; continue; }
+        // sort by (qb, qe): equal keys are identical intervals (any order)
+        for (int i = 1; i < ni; ++i) {
+            const GBi t = fmm[i];
+            const uint64_t kt = (uint64_t)t.qb << 32 | (uint32_t)t.qe;
+            int j = i;
+            while (j > 0 && ((uint64_t)fmm[j - 1].qb << 32 | (uint32_t)fmm[j - 1].qe) > kt) { fmm[j] = fmm[j - 1]; --j; }
+            fmm[j] = t;
+        }
+        const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
+        if (ni && off + ni > w.iv_cap) {  // the pool is sized from the call's read count
+            atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
+            w.iv_n[rr] = -1;
+            continue;
+        }
+        for (int i = 0; i < ni; ++i) w.iv[off + i] = GIv{fmm[i].k, fmm[i].s, fmm[i].qb, fmm[i].qe};
+        w.iv_off[rr] = off;
+        w.iv_n[rr] = ni;
+    }
+}
+
+// ============================================================= G2: mem_align1_core
+struct G2Scr {           // one wave's scratch (global memory)
+    GSeed *pool;         // chain seeds, linked per chain (next)
+    int32_t *next;
+    GChain *ch, *ch2;    // chains (mem_chain), then in tree order
+    int32_t *last_of;
+    int32_t *order;
+    GKb *kb;
+    GSeed *seed;         // compacted: each chain's seeds contiguous
+    uint64_t *srt;
+    GReg *reg;
+    int32_t *kept;
+};
+constexpr size_t g2_slot_bytes() {
+    return ((size_t)AF_G_MAX_OCC * sizeof(GSeed) + (size_t)AF_G_MAX_OCC * 4 + 2 * (size_t)AF_G_MAX_CHAIN * sizeof(GChain) +
+            3 * (size_t)AF_G_MAX_CHAIN * 4 + (size_t)G_KB_NODES * sizeof(GKb) + (size_t)AF_G_MAX_OCC * sizeof(GSeed) +
+            (size_t)AF_G_MAX_OCC * 8 + (size_t)AF_G_MAX_REG * sizeof(GReg) + 1024) & ~(size_t)255;
+}
+__device__ G2Scr g2_scr(uint8_t *base) {
+    G2Scr s;
+    uint8_t *p = base;
+    auto take = [&](size_t b) { uint8_t *r = p; p += (b + 15) & ~(size_t)15; return r; };
+    s.pool = (GSeed *)take((size_t)AF_G_MAX_OCC * sizeof(GSeed));
+    s.next = (int32_t *)take((size_t)AF_G_MAX_OCC * 4);
+    s.ch = (GChain *)take((size_t)AF_G_MAX_CHAIN * sizeof(GChain));
+    s.ch2 = (GChain *)take((size_t)AF_G_MAX_CHAIN * sizeof(GChain));
+    s.last_of = (int32_t *)take((size_t)AF_G_MAX_CHAIN * 4);
+    s.order = (int32_t *)take((size_t)AF_G_MAX_CHAIN * 4);
+    s.kept = (int32_t *)take((size_t)AF_G_MAX_CHAIN * 4);
+    s.kb = (GKb *)take((size_t)G_KB_NODES * sizeof(GKb));
+    s.seed = (GSeed *)take((size_t)AF_G_MAX_OCC * sizeof(GSeed));
+    s.srt = (uint64_t *)take((size_t)AF_G_MAX_OCC * 8);
+    s.reg = (GReg *)take((size_t)AF_G_MAX_REG * sizeof(GReg));
+    return s;
+}
+
+struct G2Lds {
+    int64_t occ[64];      // a batch of sampled occurrences (SA rows gathered by the wave)
+    int32_t misc[8];
+    int64_t rmax[2];
+};
+__shared__ G2Lds g_g2;
+
+// ---- bntseq.c on the device
+__device__ __forceinline__ int g_pos2rid(const DevGenome &G, int64_t pos_f) {
+    if (pos_f >= G.l_pac) return -1;
+    int left = 0, mid = 0, right = G.n_ctg;
+    while (left < right) {
+        mid = (left + right) >> 1;
+        if (pos_f >= G.ctg_off_d[mid]) {
+            if (mid == G.n_ctg - 1) break;
+            if (pos_f < G.ctg_off_d[mid + 1]) break;
+            left = mid + 1;
+        } else right = mid;
+    }
+    return mid;
+}
+__device__ __forceinline__ int64_t g_depos(const DevGenome &G, int64_t pos, int *is_rev) {
+    return (*is_rev = (pos >= G.l_pac)) ? (G.l_pac << 1) - 1 - pos : pos;
+}
+__device__ __forceinline__ int g_intv2rid(const DevGenome &G, int64_t rb, int64_t re) {
+    int is_rev;
+    if (rb < G.l_pac && re > G.l_pac) return -2;
+    const int rid_b = g_pos2rid(G, g_depos(G, rb, &is_rev));
+    const int rid_e = rb < re ? g_pos2rid(G, g_depos(G, re - 1, &is_rev)) : rid_b;
+    return rid_b == rid_e ? rid_b : -1;
+}
+__device__ __forceinline__ void g_fetch_clip(const DevGenome &G, int64_t *beg, int64_t mid, int64_t *end, int *rid) {
+    int is_rev;
+    if (*end < *beg) { const int64_t t = *end; *end = *beg; *beg = t; }
+    *rid = g_pos2rid(G, g_depos(G, mid, &is_rev));
+    int64_t fb = G.ctg_off_d[*rid], fe = fb + G.ctg_len_d[*rid];
+    if (is_rev) { const int64_t t = fb; fb = (G.l_pac << 1) - fe; fe = (G.l_pac << 1) - t; }
+    *beg = *beg > fb ? *beg : fb;
+    *end = *end < fe ? *end : fe;
+}
+
+// ---- klib kbtree (t = 5) over chain indices keyed by chain pos; lane 0 (oracle kb_*)
+struct GTree { GKb *node; int nn, root; const GChain *ch; };
+__device__ __forceinline__ int gkb_cmp(const GTree &b, int x, int64_t kpos) {
+    const int64_t a = b.ch[x].pos;
+    return (kpos < a) - (a < kpos);
+}
+__device__ int gkb_getp_aux(const GTree &b, const GKb &x, int64_t kpos, int *r) {
+    int tr, *rr, begin = 0, end = x.n;
+    if (x.n == 0) return -1;
+    rr = r ? r : &tr;
+    while (begin < end) {
+        const int mid = (begin + end) >> 1;
+        if (gkb_cmp(b, x.key[mid], kpos) < 0) begin = mid + 1;
+        else end = mid;
+    }
+    if (begin == x.n) { *rr = 1; return x.n - 1; }
+    if ((*rr = -gkb_cmp(b, x.key[begin], kpos)) < 0) --begin;
+    return begin;
+}
+__device__ int gkb_new(GTree &b, int internal) {
+    GKb &z = b.node[b.nn];
+    z.n = 0; z.internal = (int16_t)internal;
+    return b.nn++;
+}
+__device__ int gkb_lower(const GTree &b, int64_t kpos) {
+    int r = 0, lower = -1, xi = b.root;
+    while (xi >= 0) {
+        const GKb &x = b.node[xi];
+        const int i = gkb_getp_aux(b, x, kpos, &r);
+        if (i >= 0 && r == 0) return x.key[i];
+        if (i >= 0) lower = x.key[i];
+        if (!x.internal) return lower;
+        xi = x.ptr[i + 1];
+    }
+    return lower;
+}
+__device__ void gkb_split(GTree &b, int xi, int i, int yi) {
+    const int zi = gkb_new(b, b.node[yi].internal);
+    GKb &x = b.node[xi], &y = b.node[yi], &z = b.node[zi];
+    z.n = G_KB_T - 1;
+    for (int u = 0; u < G_KB_T - 1; ++u) z.key[u] = y.key[G_KB_T + u];
+    if (y.internal)
+        for (int u = 0; u < G_KB_T; ++u) z.ptr[u] = y.ptr[G_KB_T + u];
+    y.n = G_KB_T - 1;
+    for (int u = x.n; u >= i + 1; --u) x.ptr[u + 1] = x.ptr[u];
+    x.ptr[i + 1] = (int16_t)zi;
+    for (int u = x.n - 1; u >= i; --u) x.key[u + 1] = x.key[u];
+    x.key[i] = y.key[G_KB_T - 1];
+    ++x.n;
+}
+__device__ bool gkb_putp(GTree &b, int k) {
+    const int64_t kpos = b.ch[k].pos;
+    int xi = b.root;
+    if (b.nn + 16 >= G_KB_NODES) return false;  // one insertion adds at most depth + 1 nodes
+    if (b.node[xi].n == G_KB_MAXK) {
+        const int si = gkb_new(b, 1);
+        b.node[si].ptr[0] = (int16_t)xi;
+        b.root = si;
+        gkb_split(b, si, 0, xi);
+        xi = si;
+    }
+    for (;;) {  // __kb_putp_aux, iteratively
+        GKb &x = b.node[xi];
+        if (!x.internal) {
+            const int i = gkb_getp_aux(b, x, kpos, nullptr);
+            for (int u = x.n - 1; u >= i + 1; --u) x.key[u + 1] = x.key[u];
+            x.key[i + 1] = (int16_t)k;
+            ++x.n;
+            return true;
+        }
+        int i = gkb_getp_aux(b, x, kpos, nullptr) + 1;
+        if (b.node[x.ptr[i]].n == G_KB_MAXK) {
+            gkb_split(b, xi, i, x.ptr[i]);
+            if (gkb_cmp(b, b.node[xi].key[i], kpos) > 0) ++i;
+        }
+        xi = b.node[xi].ptr[i];
+    }
+}
+// in-order traversal into order[] (iterative; depth <= 8 for 8192 keys at t = 5)
+__device__ int gkb_traverse(const GTree &b, int32_t *order) {
+    int stk_node[16], stk_i[16], top = 1, n = 0;
+    stk_node[0] = b.root; stk_i[0] = 0;
+    while (top > 0) {
+        const int xi = stk_node[top - 1];
+        const int i = stk_i[top - 1];
+        const GKb &x = b.node[xi];
+        if (!x.internal) {
+            for (int u = 0; u < x.n; ++u) order[n++] = x.key[u];
+            --top;
+            continue;
+        }
+        if (i > x.n) { --top; continue; }
+        stk_i[top - 1] = i + 1;
+        if (i > 0) order[n++] = x.key[i - 1];
+        stk_node[top] = x.ptr[i]; stk_i[top] = 0; ++top;
+    }
+    return n;
+}
+
+// test_and_merge (oracle test_and_merge), lane 0: 1 merged / contained, 0 not, -1 overflow
+__device__ int g_test_and_merge(const G2Scr &S, int ci, const GSeed &p, int rid, int64_t l_pac, int w,
+                                int max_chain_gap, int *npool) {
+    GChain &c = S.ch[ci];
+    const GSeed first = S.pool[c.seed0], last = S.pool[S.last_of[ci]];
+    const int64_t qend = (int64_t)last.qbeg + last.len, rend = last.rbeg + last.len;
+    if (rid != c.rid) return 0;
+    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend) return 1;
+    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return 0;
+    const int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
+    if (y >= 0 && x - y <= w && y - x <= w && x - last.len < max_chain_gap && y - last.len < max_chain_gap) {
+        if (*npool >= AF_G_MAX_OCC) return -1;
+        const int k = (*npool)++;
+        S.pool[k] = p;
+        S.next[k] = -1;
+        S.next[S.last_of[ci]] = k;
+        S.last_of[ci] = k;
+        ++c.n;
+        return 1;
+    }
+    return 0;
+}
+
+// mem_chain over the read's intervals (oracle mem_chain): returns the chain count (tree order,
+// seeds compacted in S.seed), -1 on overflow.  The wave gathers 64 SA rows at a time; lane 0
+// walks them in order.
+__device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, int niv, const af_params &p,
+                           const GOpt &o, int lane) {
+    G2Lds &E = g_g2;
+    int nch = 0, npool = 0;
+    bool ovf = false;
+    GTree tree{S.kb, 0, 0, S.ch};
+    if (lane == 0) tree.root = gkb_new(tree, 0);
+    for (int i = 0; i < niv && !ovf; ++i) {
+        const GIv v = iv[i];
+        const int slen = v.qe - v.qb;
+        const int64_t step = v.s > p.max_occ ? v.s / p.max_occ : 1;
+        const int64_t cnt = v.s > p.max_occ ? (int64_t)p.max_occ : v.s;  // k < s && count < max_occ
+        for (int64_t c0 = 0; c0 < cnt && !ovf; c0 += 64) {
+            const int64_t c = c0 + lane;
+            const int nb = (int)min((int64_t)64, cnt - c0);
+            wave_sync();
+            if (c < cnt) E.occ[lane] = G.sa[v.sa_k + c * step];
+            wave_sync();
+            if (lane == 0) {
+                for (int u = 0; u < nb && !ovf; ++u) {
+                    GSeed s;
+                    s.rbeg = E.occ[u];
+                    s.qbeg = v.qb;
+                    s.len = slen;
+                    const int rid = g_intv2rid(G, s.rbeg, s.rbeg + s.len);
+                    if (rid < 0) continue;
+                    bool to_add = false;
+                    if (nch) {
+                        const int lower = gkb_lower(tree, s.rbeg);
+                        if (lower < 0) to_add = true;
+                        else {
+                            const int r = g_test_and_merge(S, lower, s, rid, G.l_pac, p.w, o.max_chain_gap, &npool);
+                            if (r < 0) ovf = true;
+                            else if (!r) to_add = true;
+                        }
+                    } else to_add = true;
+                    if (to_add && !ovf) {
+                        if (nch >= AF_G_MAX_CHAIN || npool >= AF_G_MAX_OCC) { ovf = true; break; }
+                        const int kk = npool++;
+                        S.pool[kk] = s;
+                        S.next[kk] = -1;
+                        S.ch[nch] = GChain{s.rbeg, 1, -1, rid, 0, 0, kk};
+                        S.last_of[nch] = kk;
+                        if (!gkb_putp(tree, nch)) { ovf = true; break; }
+                        ++nch;
+                    }
+                }
+                E.misc[0] = ovf;
+            }
+            wave_sync();
+            ovf = E.misc[0] != 0;
+        }
+    }
+    int no = 0;
+    if (lane == 0 && !ovf) {
+        no = gkb_traverse(tree, S.order);
+        int ns = 0;
+        for (int a = 0; a < no; ++a) {
+            GChain c = S.ch[S.order[a]];
+            const int s0 = ns;
+            for (int k = c.seed0; k >= 0; k = S.next[k]) S.seed[ns++] = S.pool[k];
+            c.seed0 = s0;
+            S.ch2[a] = c;
+        }
+        E.misc[1] = no;
+    }
+    wave_sync();
+    return ovf ? -1 : E.misc[1];
+}
+
+__device__ int g_chain_weight(const G2Scr &S, const GChain &c) {
+    const GSeed *sd = S.seed + c.seed0;
+    int64_t end = 0;
+    int w = 0, tmp;
+    for (int j = 0; j < c.n; ++j) {
+        const GSeed s = sd[j];
+        if (s.qbeg >= end) w += s.len;
+        else if (s.qbeg + s.len > end) w += (int)(s.qbeg + s.len - end);
+        end = end > s.qbeg + s.len ? end : s.qbeg + s.len;
+    }
+    tmp = w; w = 0; end = 0;
+    for (int j = 0; j < c.n; ++j) {
+        const GSeed s = sd[j];
+        if (s.rbeg >= end) w += s.len;
+        else if (s.rbeg + s.len > end) w += (int)(s.rbeg + s.len - end);
+        end = end > s.rbeg + s.len ? end : s.rbeg + s.len;
+    }
+    w = w < tmp ? w : tmp;
+    return w < 1 << 30 ? w : (1 << 30) - 1;
+}
+struct GLtFlt {
+    __device__ bool operator()(const GChain &a, const GChain &b) const { return a.w > b.w; }
+};
+
+// mem_chain_flt (oracle mem_chain_flt), lane 0 over S.ch2: returns the kept count
+__device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const GOpt &o) {
+    GChain *a = S.ch2;
+    if (n_chn == 0) return 0;
+    for (int i = 0; i < n_chn; ++i) { a[i].first = -1; a[i].kept = 0; a[i].w = g_chain_weight(S, a[i]); }
+    ks_introsort(a, n_chn, GLtFlt());
+    auto beg = [&](const GChain &c) { return (int)S.seed[c.seed0].qbeg; };
+    auto endq = [&](const GChain &c) {
+        const GSeed t = S.seed[c.seed0 + c.n - 1];
+        return (int)t.qbeg + t.len;
+    };
+    int32_t *chains = S.kept;
+    int nc = 0;
+    a[0].kept = 3;
+    chains[nc++] = 0;
+    for (int i = 1; i < n_chn; ++i) {
+        int large_ovlp = 0, k;
+        for (k = 0; k < nc; ++k) {
+            const int j = chains[k];
+            const int b_max = beg(a[j]) > beg(a[i]) ? beg(a[j]) : beg(a[i]);
+            const int e_min = endq(a[j]) < endq(a[i]) ? endq(a[j]) : endq(a[i]);
+            if (e_min > b_max) {
+                const int li = endq(a[i]) - beg(a[i]), lj = endq(a[j]) - beg(a[j]);
+                const int min_l = li < lj ? li : lj;
+                if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
+                    large_ovlp = 1;
+                    if (a[j].first < 0) a[j].first = i;
+                    if ((float)a[i].w < (float)a[j].w * 0.5f && a[j].w - a[i].w >= p.min_seed_len << 1) break;
+                }
+            }
+        }
+        if (k == nc) {
+            chains[nc++] = i;
+            a[i].kept = large_ovlp ? 2 : 3;
+        }
+    }
+    for (int i = 0; i < nc; ++i) {
+        const GChain &c = a[chains[i]];
+        if (c.first >= 0) a[c.first].kept = 1;
+    }
+    int k = 0;
+    for (int i = 0; i < n_chn; ++i)
+        if (a[i].kept != 0) a[k++] = a[i];
+    return k;
+}
+
+// mem_chain2aln (oracle mem_chain2aln) for chain ci of S.ch2; regions appended to S.reg.
+// Returns false on a region-cap overflow.
+template <int CPL>
+__device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params &p, int l, int ci, int *nreg_io,
+                            int lane) {
+    DpLds &L = g_dp;
+    G2Lds &E = g_g2;
+    const int64_t l_pac = G.l_pac;
+    const GChain c = S.ch2[ci];
+    const GSeed *sd = S.seed + c.seed0;
+    if (lane == 0) {
+        int64_t r0 = l_pac << 1, r1 = 0;
+        for (int i = 0; i < c.n; ++i) {
+            const GSeed t = sd[i];
+            const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(p, t.qbeg));
+            const int rem = l - t.qbeg - t.len;
+            const int64_t e = t.rbeg + t.len + (rem + cal_max_gap(p, rem));
+            r0 = r0 < b ? r0 : b;
+            r1 = r1 > e ? r1 : e;
+        }
+        r0 = r0 > 0 ? r0 : 0;
+        r1 = r1 < l_pac << 1 ? r1 : l_pac << 1;
+        if (r0 < l_pac && l_pac < r1) {
+            if (sd[0].rbeg < l_pac) r1 = l_pac;
+            else r0 = l_pac;
+        }
+        int rid;
+        g_fetch_clip(G, &r0, sd[0].rbeg, &r1, &rid);
+        E.rmax[0] = r0; E.rmax[1] = r1;
+    }
+    // srt: seed indices by (score << 32 | i) ascending (keys distinct): rank sort on the wave
+    for (int i0 = 0; i0 < c.n; i0 += 64) {
+        const int i = i0 + lane;
+        if (i < c.n) {
+            const uint64_t ki = (uint64_t)(uint32_t)sd[i].len << 32 | (uint32_t)i;
+            int rk = 0;
+            for (int j = 0; j < c.n; ++j) rk += ((uint64_t)(uint32_t)sd[j].len << 32 | (uint32_t)j) < ki;
+            S.srt[rk] = ki;
+        }
+    }
+    wave_sync();
+    const int64_t rmax0 = E.rmax[0], rmax1 = E.rmax[1];
+    for (int k = c.n - 1; k >= 0; --k) {
+        const uint64_t sk = S.srt[k];
+        const GSeed s = sd[(uint32_t)sk];
+        const int nreg = *nreg_io;
+        // test whether extension has been made before (any region satisfying)
+        bool hit = false;
+        for (int i0 = 0; i0 < nreg && !hit; i0 += 64) {
+            const int i = i0 + lane;
+            bool h = false;
+            if (i < nreg) {
+                const GReg pr = S.reg[i];
+                if (!(s.rbeg < pr.rb || s.rbeg + s.len > pr.re || s.qbeg < pr.qb || s.qbeg + s.len > pr.qe) &&
+                    !((double)(s.len - pr.seedlen0) > .1 * l)) {
+                    int qd = s.qbeg - pr.qb;
+                    int64_t rd = s.rbeg - pr.rb;
+                    int mg = cal_max_gap(p, (int)(qd < rd ? (int64_t)qd : rd));
+                    int ww = mg < pr.w ? mg : pr.w;
+                    if (qd - rd < ww && rd - qd < ww) h = true;
+                    else {
+                        qd = pr.qe - (s.qbeg + s.len);
+                        rd = pr.re - (s.rbeg + s.len);
+                        mg = cal_max_gap(p, (int)(qd < rd ? (int64_t)qd : rd));
+                        ww = mg < pr.w ? mg : pr.w;
+                        if (qd - rd < ww && rd - qd < ww) h = true;
+                    }
+                }
+            }
+            hit = __ballot(h) != 0;
+        }
+        if (hit) {
+            // contained: extend only if a long overlapping seed on another diagonal follows
+            bool ov = false;
+            for (int i = k + 1 + lane; i < c.n; i += 64) {
+                const uint64_t ti = S.srt[i];
+                if (ti == 0) continue;
+                const GSeed t = sd[(uint32_t)ti];
+                if ((double)t.len < s.len * .95) continue;
+                if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 &&
+                    (int64_t)(t.qbeg - s.qbeg) != t.rbeg - s.rbeg) ov = true;
+                if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 &&
+                    (int64_t)(s.qbeg - t.qbeg) != s.rbeg - t.rbeg) ov = true;
+            }
+            if (!__ballot(ov)) {
+                wave_sync();
+                if (lane == 0) S.srt[k] = 0;
+                wave_sync();
+                continue;
+            }
+        }
+        if (nreg >= AF_G_MAX_REG) return false;
+        int a_score = -1, a_truesc = -1, a_qb = 0, a_qe = 0;
+        int64_t a_rb = 0, a_re = 0;
+        int aw0 = p.w, aw1 = p.w;
+        if (s.qbeg) {  // left extension
+            const int64_t tmp = s.rbeg - rmax0;
+            const int tl = (int)min(tmp, (int64_t)(s.qbeg + 2 * p.w + 1));
+            for (int x = lane; x < s.qbeg; x += 64) L.qs[x] = L.q[s.qbeg - 1 - x];
+            for (int x = lane; x < tl; x += 64) L.t[x] = G.T[s.rbeg - 1 - x];
+            wave_sync();
+            ExtRes er;
+            for (int it = 0; it < 2; ++it) {
+                const int prev = a_score;
+                aw0 = p.w << it;
+                er = ext_dp<CPL>(s.qbeg, L.qs, tl, L.t, p, aw0, p.pen_clip5, p.zdrop, s.len * p.a, lane);
+                a_score = er.max;
+                if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+            }
+            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip5) {
+                a_qb = s.qbeg - er.qle; a_rb = s.rbeg - er.tle; a_truesc = a_score;
+            } else {
+                a_qb = 0; a_rb = s.rbeg - er.gtle; a_truesc = er.gscore;
+            }
+            wave_sync();
+        } else {
+            a_score = a_truesc = s.len * p.a; a_qb = 0; a_rb = s.rbeg;
+        }
+        if (s.qbeg + s.len != l) {  // right extension
+            const int qe = s.qbeg + s.len;
+            const int64_t re = s.rbeg + s.len - rmax0;
+            const int sc0 = a_score;
+            const int tl = (int)min(rmax1 - rmax0 - re, (int64_t)((l - qe) + 2 * p.w + 1));
+            for (int x = lane; x < tl; x += 64) L.t[x] = G.T[rmax0 + re + x];
+            wave_sync();
+            ExtRes er;
+            for (int it = 0; it < 2; ++it) {
+                const int prev = a_score;
+                aw1 = p.w << it;
+                er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                a_score = er.max;
+                if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+            }
+            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip3) {
+                a_qe = qe + er.qle; a_re = rmax0 + re + er.tle; a_truesc += a_score - sc0;
+            } else {
+                a_qe = l; a_re = rmax0 + re + er.gtle; a_truesc += er.gscore - sc0;
+            }
+            wave_sync();
+        } else {
+            a_qe = l; a_re = s.rbeg + s.len;
+        }
+        // seedcov: the chain's seeds inside the region
+        int cov = 0;
+        for (int i = lane; i < c.n; i += 64) {
+            const GSeed t = sd[i];
+            if (t.qbeg >= a_qb && t.qbeg + t.len <= a_qe && t.rbeg >= a_rb && t.rbeg + t.len <= a_re) cov += t.len;
+        }
+        cov = wave_sum(cov);
+        if (lane == 0) {
+            GReg &a = S.reg[nreg];
+            a.rb = a_rb; a.re = a_re; a.qb = a_qb; a.qe = a_qe; a.rid = c.rid; a.score = a_score; a.truesc = a_truesc;
+            a.w = aw0 > aw1 ? aw0 : aw1; a.seedlen0 = s.len; a.seedcov = cov; a.secondary = -1; a.sub = 0; a.hash = 0;
+        }
+        *nreg_io = nreg + 1;
+        wave_sync();
+    }
+    return true;
+}
+
+// mem_patch_reg (oracle mem_patch_reg): the merged score, 0 if not merged; *w_out its band
+template <int CPL>
+__device__ int g_patch_reg(const DevGenome &G, const af_params &p, const GReg &a, const GReg &b, int *w_out,
+                           uint8_t *zg, int lane) {
+    const int64_t l_pac = G.l_pac;
+    if (a.rb < l_pac && b.rb >= l_pac) return 0;
+    if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) return 0;
+    if (b.re - a.rb > AF_S2_MAX_TSPAN) return 0;  // the oracle's AFO_PE_MAX_TSPAN (L.t holds 1 KiB)
+    int w = (int)((a.re - b.rb) - (a.qe - b.qb));
+    w = w > 0 ? w : -w;
+    double r = (double)(a.re - b.rb) / (double)(b.re - a.rb) - (double)(a.qe - b.qb) / (double)(b.qe - a.qb);
+    r = r > 0. ? r : -r;
+    if (a.re < b.rb || a.qe < b.qb) {
+        if (w > p.w << 1 || r >= (double)0.05f) return 0;
+    } else if (w > p.w << 2 || r >= (double)(0.05f * 2)) return 0;
+    w += a.w + b.w;
+    w = w < p.w << 2 ? w : p.w << 2;
+    const int lq = b.qe - a.qb;
+    const int score = gen_cigar_wave<CPL, false>(G.T, l_pac, p, w, lq, a.qb, a.rb, b.re, g_dp, zg, lane);
+    const int q_s = (int)((double)(b.qe - a.qb) / (double)((b.qe - b.qb) + (a.qe - a.qb)) * (double)(b.score + a.score) + .499);
+    const int r_s = (int)((double)(b.re - a.rb) / (double)((b.re - b.rb) + (a.re - a.rb)) * (double)(b.score + a.score) + .499);
+    if ((double)score / (double)(q_s > r_s ? q_s : r_s) < (double)0.90f) return 0;
+    *w_out = w;
+    return score;
+}
+
+struct GLtArs2 {
+    __device__ bool operator()(const GReg &a, const GReg &b) const { return a.re < b.re; }
+};
+struct GLtArs {
+    __device__ bool operator()(const GReg &a, const GReg &b) const {
+        return a.score > b.score || (a.score == b.score && (a.rb < b.rb || (a.rb == b.rb && a.qb < b.qb)));
+    }
+};
+struct GLtArsHash {
+    __device__ bool operator()(const GReg &a, const GReg &b) const {
+        return a.score > b.score || (a.score == b.score && a.hash < b.hash);
+    }
+};
+
+// mem_sort_dedup_patch (oracle mem_sort_dedup_patch) over a[0, n); patch: merge colinear hits
+template <int CPL>
+__device__ int g_dedup_patch(const DevGenome &G, const af_params &p, const GOpt &o, GReg *a, int n, bool patch,
+                             uint8_t *zg, int lane) {
+    G2Lds &E = g_g2;
+    if (n <= 1) return n;
+    if (lane == 0) ks_introsort(a, n, GLtArs2());
+    wave_sync();
+    for (int i = 1; i < n; ++i) {
+        if (a[i].rid != a[i - 1].rid || a[i].rb >= a[i - 1].re + o.max_chain_gap) continue;
+        for (int j = i - 1; j >= 0 && a[i].rid == a[j].rid && a[i].rb < a[j].re + o.max_chain_gap; --j) {
+            const GReg q = a[j], pp = a[i];
+            if (q.qe == q.qb) continue;
+            const int64_t or_ = q.re - pp.rb;
+            const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
+            const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
+            const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
+            if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
+                const bool drop_p = pp.score < q.score;
+                wave_sync();
+                if (lane == 0) {
+                    if (drop_p) a[i].qe = a[i].qb;
+                    else a[j].qe = a[j].qb;
+                }
+                wave_sync();
+                if (drop_p) break;
+            } else if (q.rb < pp.rb && patch) {
+                int w = 0;
+                const int score = g_patch_reg<CPL>(G, p, q, pp, &w, zg, lane);
+                if (score > 0) {
+                    wave_sync();
+                    if (lane == 0) {
+                        GReg &P = a[i];
+                        P.seedcov = P.seedcov > q.seedcov ? P.seedcov : q.seedcov;
+                        P.sub = P.sub > q.sub ? P.sub : q.sub;
+                        P.qb = q.qb; P.rb = q.rb;
+                        P.truesc = P.score = score;
+                        P.w = w;
+                        a[j].qb = a[j].qe;
+                    }
+                    wave_sync();
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        int m = 0;
+        for (int i = 0; i < n; ++i)
+            if (a[i].qe > a[i].qb) a[m++] = a[i];
+        ks_introsort(a, m, GLtArs());
+        for (int i = 1; i < m; ++i)
+            if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
+        int mm = m ? 1 : 0;
+        for (int i = 1; i < m; ++i)
+            if (a[i].qe > a[i].qb) a[mm++] = a[i];
+        E.misc[2] = mm;
+    }
+    wave_sync();
+    return E.misc[2];
+}
+
+__device__ __forceinline__ void g_load_read(const uint8_t *reads, int64_t r, int32_t stride, int l, int lane) {
+    DpLds &L = g_dp;
+    const uint8_t *rd = reads + r * (int64_t)stride;
+    for (int x = lane; x < l; x += 64) L.q[x] = nt4(rd[x]);
+    wave_sync();
+}
+
+__device__ __forceinline__ int g_next_item(int32_t *heads, int &head, int &heads_left, int64_t n, int lane) {
+    while (heads_left > 0) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
+        v = __builtin_amdgcn_readfirstlane(v);
+        const int64_t it = head + 8 * (int64_t)v;
+        if (it < n) return (int)it;
+        head = (head + 1) & 7;
+        --heads_left;
+    }
+    return -1;
+}
+
+// G2: mem_align1_core for every read (one wave per read)
+template <int CPL>
+__global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                     const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
+                                                     int64_t cap, int64_t read0, af_params p, GOpt o, GWork w,
+                                                     uint8_t *__restrict__ scr_base, size_t scr_stride,
+                                                     uint8_t *__restrict__ zscratch, size_t zstride) {
+    const int lane = threadIdx.x;
+    int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
+    if (n > cap) n = cap;
+    const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        const int it = g_next_item(w.heads, head, heads_left, n - read0, lane);
+        if (it < 0) break;
+        const int64_t r = read0 + it;
+        const int l = read_len(lens, r, stride);
+        const int niv = w.iv_n[r];
+        int nreg = 0;
+        bool ovf = niv < 0;
+        if (!ovf && l >= p.min_seed_len && niv > 0) {
+            g_load_read(reads, r, stride, l, lane);
+            const int nch0 = g_mem_chain(G, S, w.iv + w.iv_off[r], niv, p, o, lane);
+            if (nch0 < 0) ovf = true;
+            else {
+                if (lane == 0) g_g2.misc[3] = g_chain_flt(S, nch0, p, o);
+                wave_sync();
+                const int nch = g_g2.misc[3];
+                for (int ci = 0; ci < nch && !ovf; ++ci)
+                    if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane)) ovf = true;
+                if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+            }
+        }
+        int off = 0;
+        if (!ovf && nreg > 0) {
+            if (lane == 0) g_g2.misc[4] = atomicAdd(w.reg_fill, nreg);
+            wave_sync();
+            off = g_g2.misc[4];
+            if ((int64_t)off + nreg > w.reg_cap) {
+                if (lane == 0) atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
+                ovf = true;
+            }
+        }
+        if (!ovf)
+            for (int k = lane; k < nreg; k += 64) w.reg[off + k] = S.reg[k];
+        if (lane == 0) {
+            w.reg_off[r] = off;
+            w.reg_n[r] = ovf ? -1 : nreg;
+            if (ovf) atomicAdd(&w.stats[AF_GSTAT_OVERFLOW], 1);
+        }
+        wave_sync();
+    }
+}
+
+// ==================================================================== records
+// mem_mark_primary_se (oracle mark_primary_se), lane 0: a[0, n) sorted by (score desc, hash),
+// secondaries marked; z: scratch
+__device__ void g_mark_primary(GReg *a, int n, int64_t id, const af_params &p, int32_t *z) {
+    if (n == 0) return;
+    for (int i = 0; i < n; ++i) { a[i].sub = 0; a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i)); }
+    ks_introsort(a, n, GLtArsHash());
+    int nz = 0;
+    z[nz++] = 0;
+    for (int i = 1; i < n; ++i) {
+        int k;
+        for (k = 0; k < nz; ++k) {
+            const int j = z[k];
+            const int b_max = a[j].qb > a[i].qb ? a[j].qb : a[i].qb;
+            const int e_min = a[j].qe < a[i].qe ? a[j].qe : a[i].qe;
+            if (e_min > b_max) {
+                const int min_l = a[i].qe - a[i].qb < a[j].qe - a[j].qb ? a[i].qe - a[i].qb : a[j].qe - a[j].qb;
+                if ((float)(e_min - b_max) >= (float)min_l * 0.5f) {
+                    if (a[j].sub == 0) a[j].sub = a[i].score;
+                    break;
+                }
+            }
+        }
+        if (k == nz) z[nz++] = i;
+        else a[i].secondary = z[k];
+    }
+}
+
+// one mem_aln_t (oracle aln_t)
+struct GAln { int rid; int64_t pos; int is_rev, flag, score, n_cigar, of; uint32_t cigar[AF_MAX_CIGAR]; };
+
+// mem_reg2aln (oracle reg2aln) on the wave; the read's codes in L.q; result on lane 0
+template <int CPL>
+__device__ void g_reg2aln(const DevGenome &G, const af_params &p, int l, const GReg *ar, GAln &o, uint8_t *zg,
+                          int lane) {
+    DpLds &L = g_dp;
+    const int64_t l_pac = G.l_pac;
+    o.flag = 0; o.n_cigar = 0; o.of = 0; o.score = 0; o.is_rev = 0;
+    if (!ar || ar->rb < 0 || ar->re < 0) { o.rid = -1; o.pos = -1; o.flag = 0x4; return; }
+    const GReg a = *ar;
+    if (a.secondary >= 0) o.flag |= 0x100;
+    const int lq = a.qe - a.qb;
+    const int tmpw = infer_bw(lq, (int)(a.re - a.rb), a.truesc, p.a, p.o_del, p.e_del);
+    int w2 = infer_bw(lq, (int)(a.re - a.rb), a.truesc, p.a, p.o_ins, p.e_ins);
+    w2 = w2 > tmpw ? w2 : tmpw;
+    if (w2 > p.w) w2 = w2 < a.w ? w2 : a.w;
+    int score = 0, last_sc = -(1 << 30), it = 0;
+    do {
+        w2 = w2 < p.w << 2 ? w2 : p.w << 2;
+        score = gen_cigar_wave<CPL>(G.T, l_pac, p, w2, lq, a.qb, a.rb, a.re, L, zg, lane);
+        if (score == last_sc || w2 == p.w << 2) break;
+        last_sc = score;
+        w2 <<= 1;
+    } while (++it < 3 && score < a.truesc - p.a);
+    (void)score;
+    if (lane == 0) {
+        const int nc = L.misc[2];
+        const int ncap = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
+        bool of = nc > AF_MAX_CIGAR;
+        int is_rev;
+        int64_t pos = g_depos(G, a.rb < l_pac ? a.rb : a.re - 1, &is_rev);
+        int xs = 0, xe = ncap;
+        const uint32_t first = L.ring[(nc - 1) & 63];
+        const uint32_t last = L.ring[(nc - ncap) & 63];
+        if (ncap > 0) {
+            if ((first & 0xf) == 2) { pos += first >> 4; xs = 1; }
+            else if ((last & 0xf) == 2) xe = ncap - 1;
+        }
+        const int clip5 = is_rev ? l - a.qe : a.qb;
+        const int clip3 = is_rev ? a.qb : l - a.qe;
+        int nf = 0;
+        if (clip5) o.cigar[nf++] = (uint32_t)clip5 << 4 | 4;
+        for (int x = xs; x < xe; ++x) {
+            if (nf < AF_MAX_CIGAR) o.cigar[nf] = L.ring[(nc - 1 - x) & 63];
+            ++nf;
+        }
+        if (clip3) {
+            if (nf < AF_MAX_CIGAR) o.cigar[nf] = (uint32_t)clip3 << 4 | 4;
+            ++nf;
+        }
+        if (nf > AF_MAX_CIGAR) { of = true; nf = AF_MAX_CIGAR; }
+        o.n_cigar = nf;
+        o.of = of;
+        o.rid = g_pos2rid(G, pos);
+        o.pos = pos - G.ctg_off_d[o.rid];
+        o.is_rev = is_rev;
+        o.score = a.score;
+    }
+}
+
+// mem_aln2sam (oracle aln2grec), lane 0: record `which` of a read, mate m (nullptr: single-end)
+__device__ void g_aln2rec(const GAln &p_, const GAln *m_, int which, int l_seq, int32_t read, af_grec &o) {
+    GAln p = p_, m{};
+    if (m_) m = *m_;
+    p.flag |= m_ ? 0x1 : 0;
+    p.flag |= p.rid < 0 ? 0x4 : 0;
+    p.flag |= m_ && m.rid < 0 ? 0x8 : 0;
+    if (p.rid < 0 && m_ && m.rid >= 0) { p.rid = m.rid; p.pos = m.pos; p.is_rev = m.is_rev; p.n_cigar = 0; }
+    if (m_ && m.rid < 0 && p.rid >= 0) { m.rid = p.rid; m.pos = p.pos; m.is_rev = p.is_rev; m.n_cigar = 0; }
+    p.flag |= p.is_rev ? 0x10 : 0;
+    p.flag |= m_ && m.is_rev ? 0x20 : 0;
+    o.read = read;
+    o.flag = (p.flag & 0xffff) | ((p.flag & 0x10000) ? 0x100 : 0) | (p_.of ? AF_FLAG_CIGAR_OVERFLOW : 0);
+    o.rid = p.rid;
+    o.pos = p.rid >= 0 ? p.pos : -1;
+    o.score = p.rid >= 0 && p_.rid >= 0 ? p.score : 0;
+    o.n_cigar = p.n_cigar;
+    for (int c = 0; c < AF_MAX_CIGAR; ++c) {
+        uint32_t v = 0;
+        if (c < p.n_cigar) {
+            uint32_t op = p.cigar[c] & 0xf;
+            if (op == 4 && which) op = 5;
+            v = (p.cigar[c] & ~0xfu) | op;
+        }
+        o.cigar[c] = v;
+    }
+    o.mrid = m_ && m.rid >= 0 ? m.rid : -1;
+    o.mpos = m_ && m.rid >= 0 ? m.pos : -1;
+    o.seq_b = 0; o.seq_e = l_seq;
+    if (p.n_cigar && which) {
+        if ((p.cigar[0] & 0xf) == 4) o.seq_b = (int32_t)(p.cigar[0] >> 4);
+        if ((p.cigar[p.n_cigar - 1] & 0xf) == 4) o.seq_e = l_seq - (int32_t)(p.cigar[p.n_cigar - 1] >> 4);
+    }
+}
+
+struct G3Lds {
+    GAln al;              // the record being built
+    GAln mate[2];         // mem_sam_pe's h[]
+    int32_t misc[8];
+};
+__shared__ G3Lds g_g3;
+
+// mem_reg2sam (-M): records of one read from its marked regions a[0, n); returns the record
+// count (more than AF_G_MAX_REC: the read is flagged by the caller)
+template <int CPL>
+__device__ int g_reg2sam(const DevGenome &G, const af_params &p, int l, const GReg *a, int n, int extra_flag,
+                         const GAln *m, int32_t read, af_grec *out, uint8_t *zg, int lane) {
+    G3Lds &E = g_g3;
+    int na = 0;
+    for (int k = 0; k < n; ++k) {
+        if (a[k].score < p.T || a[k].secondary >= 0) continue;
+        if (na < AF_G_MAX_REC) {
+            g_reg2aln<CPL>(G, p, l, &a[k], E.al, zg, lane);
+            if (lane == 0) {
+                E.al.flag |= extra_flag;
+                if (na) E.al.flag |= 0x10000;  // -M: supplementary -> 0x100
+                g_aln2rec(E.al, m, na, l, read, out[na]);
+            }
+            wave_sync();
+        }
+        ++na;
+    }
+    if (na == 0) {
+        if (lane == 0) {
+            GAln t;
+            t.rid = -1; t.pos = -1; t.flag = 0x4 | extra_flag; t.n_cigar = 0; t.of = 0; t.score = 0; t.is_rev = 0;
+            g_aln2rec(t, m, 0, l, read, out[0]);
+        }
+        wave_sync();
+        return 1;
+    }
+    return na;
+}
+
+// G3: S5 records (one wave per read): mark_primary_se + mem_reg2sam
+template <int CPL>
+__global__ __launch_bounds__(64, 2) void k_g_se(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
+                                                int64_t cap, af_params p, int64_t id_base, GWork w,
+                                                uint8_t *__restrict__ scr_base, size_t scr_stride,
+                                                uint8_t *__restrict__ zscratch, size_t zstride,
+                                                af_grec *__restrict__ recs, int32_t *__restrict__ n_rec) {
+    const int lane = threadIdx.x;
+    int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
+    if (n > cap) n = cap;
+    const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const int l = read_len(lens, r, stride);
+        const int nr = w.reg_n[r];
+        const bool ovf = nr < 0;
+        const int na = ovf ? 0 : nr;
+        for (int k = lane; k < na; k += 64) S.reg[k] = w.reg[w.reg_off[r] + k];
+        wave_sync();
+        if (lane == 0) g_mark_primary(S.reg, na, id_base + r, p, S.kept);
+        g_load_read(reads, r, stride, l, lane);
+        af_grec *out = recs + r * AF_G_MAX_REC;
+        const int nrec = g_reg2sam<CPL>(G, p, l, S.reg, na, 0, nullptr, (int32_t)r, out, zg, lane);
+        if (lane == 0) {
+            n_rec[r] = nrec;
+            if (ovf || nrec > AF_G_MAX_REC) {
+                for (int j = 0; j < (nrec < AF_G_MAX_REC ? nrec : AF_G_MAX_REC); ++j) out[j].flag |= AF_FLAG_MEM_OVERFLOW;
+                if (nrec > AF_G_MAX_REC) atomicAdd(&w.stats[AF_GSTAT_RECS], 1);
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ==================================================================== paired end (S4)
+__device__ __forceinline__ int g_infer_dir(int64_t l_pac, int64_t b1, int64_t b2, int64_t *dist) {
+    const int r1 = b1 >= l_pac, r2 = b2 >= l_pac;
+    const int64_t p2 = r1 == r2 ? b2 : (l_pac << 1) - 1 - b2;
+    *dist = p2 > b1 ? p2 - b1 : b1 - p2;
+    return (r1 == r2 ? 0 : 1) ^ (p2 > b1 ? 0 : 3);
+}
+__device__ int g_cal_sub(const GReg *a, int n, int msl, int asc) {
+    int j;
+    for (j = 1; j < n; ++j) {
+        const int b_max = a[j].qb > a[0].qb ? a[j].qb : a[0].qb;
+        const int e_min = a[j].qe < a[0].qe ? a[j].qe : a[0].qe;
+        if (e_min > b_max) {
+            const int min_l = a[j].qe - a[j].qb < a[0].qe - a[0].qb ? a[j].qe - a[j].qb : a[0].qe - a[0].qb;
+            if ((float)(e_min - b_max) >= (float)min_l * 0.5f) break;
+        }
+    }
+    return j < n ? a[j].score : msl * asc;
+}
+__device__ __forceinline__ int g_chunk_of(const S2Work &w, int64_t pp) {
+    int lo = 0, hi = *w.n_chunks;  // cstart[lo] <= pp < cstart[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (w.cstart[mid] <= pp) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// mem_pestat's insert sizes (one lane per pair) into the chunks' histograms
+__global__ void k_g_pe_hist(const int32_t *__restrict__ n_pairs_ptr, int64_t cap, int64_t l_pac, af_params p, GOpt o,
+                            GWork w, S2Work sw) {
+    int64_t n = n_pairs_ptr ? (int64_t)*n_pairs_ptr : cap;
+    if (n > cap) n = cap;
+    for (int64_t pp = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; pp < n; pp += (int64_t)gridDim.x * blockDim.x) {
+        const int n0 = w.reg_n[2 * pp], n1 = w.reg_n[2 * pp + 1];
+        if (n0 <= 0 || n1 <= 0) continue;
+        const GReg *a0 = w.reg + w.reg_off[2 * pp], *a1 = w.reg + w.reg_off[2 * pp + 1];
+        if ((double)g_cal_sub(a0, n0, p.min_seed_len, p.a) > 0.8 * a0[0].score) continue;
+        if ((double)g_cal_sub(a1, n1, p.min_seed_len, p.a) > 0.8 * a1[0].score) continue;
+        if (a0[0].rid != a1[0].rid) continue;
+        int64_t is;
+        const int dir = g_infer_dir(l_pac, a0[0].rb, a1[0].rb, &is);
+        if (is && is <= o.max_ins) {
+            const int c = g_chunk_of(sw, pp);
+            atomicAdd(&sw.ghist[((int64_t)c * 4 + dir) * (o.max_ins + 1) + is], 1);
+        }
+    }
+}
+
+struct GPeLds {
+    S2Pes pes[4];
+    uint8_t q[2][AF_MAX_READ + 16];
+    uint8_t rq[AF_MAX_READ + 16];
+    uint8_t rq2[AF_MAX_READ + 16];
+    uint8_t tw[2048];
+    int32_t na[2], nb[2], ovf[2], len[2], misc[8];
+};
+__shared__ GPeLds g_gpe;
+
+// ksw_align2 with KSW_XSUBO | KSW_XSTART (oracle ksw_align2)
+__device__ void g_ksw_align2(const uint8_t *q, int qlen, const uint8_t *target, int tlen, int P, int minsc,
+                             const af_params &p, int &score, int &te, int &qe, int &tb, int &qb, int lane) {
+    GPeLds &E = g_gpe;
+    const SwRes r = ksw_pass_any(q, qlen, target, tlen, -1, P, p, 0x10000, lane);
+    score = r.score; te = r.te; qe = r.qe; tb = -1; qb = -1;
+    if (r.score < minsc || r.qe < 0) return;
+    for (int x = lane; x <= r.qe; x += 64) E.rq2[x] = q[r.qe - x];
+    wave_sync();
+    const SwRes rr = ksw_pass_any(E.rq2, r.qe + 1, target, tlen, r.te, P, p, r.score, lane);
+    wave_sync();
+    if (r.score == rr.score) { tb = r.te - rr.te; qb = r.qe - rr.qe; }
+}
+
+// mem_matesw (oracle mem_matesw): rescue read mi (regions ma[0, *na)) in the insert-size window
+// of its mate's region a.  Returns false on a region-cap overflow.
+__device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, const G2Scr &S, int mi, GReg *ma,
+                         const GReg &a, uint8_t *zg, int lane) {
+    GPeLds &E = g_gpe;
+    const int64_t l_pac = G.l_pac;
+    const int l_ms = E.len[mi];
+    int skip[4];
+    for (int r = 0; r < 4; ++r) skip[r] = E.pes[r].failed ? 1 : 0;
+    for (int i = 0; i < E.na[mi]; ++i) {
+        int64_t dist;
+        const int r = g_infer_dir(l_pac, a.rb, ma[i].rb, &dist);
+        if (dist >= E.pes[r].low && dist <= E.pes[r].high) skip[r] = 1;
+    }
+    if (skip[0] + skip[1] + skip[2] + skip[3] == 4) return true;
+    int n = 0, rid = -1;
+    for (int r = 0; r < 4; ++r) {
+        if (skip[r]) continue;
+        const bool is_rev = (r >> 1) != (r & 1);
+        const bool is_larger = !(r >> 1);
+        int64_t rb, re;
+        if (!is_rev) {
+            rb = is_larger ? a.rb + E.pes[r].low : a.rb - E.pes[r].high;
+            re = (is_larger ? a.rb + E.pes[r].high : a.rb - E.pes[r].low) + l_ms;
+        } else {
+            rb = (is_larger ? a.rb + E.pes[r].low : a.rb - E.pes[r].high) - l_ms;
+            re = is_larger ? a.rb + E.pes[r].high : a.rb - E.pes[r].low;
+        }
+        if (rb < 0) rb = 0;
+        if (re > l_pac << 1) re = l_pac << 1;
+        if (rb < re) g_fetch_clip(G, &rb, (rb + re) >> 1, &re, &rid);
+        if (a.rid == rid && re - rb >= p.min_seed_len) {
+            for (int x = lane; x < l_ms; x += 64) {
+                const int c = E.q[mi][is_rev ? l_ms - 1 - x : x];
+                E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
+            }
+            const bool staged = re - rb <= (int64_t)sizeof(E.tw);
+            if (staged)
+                for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = G.T[rb + x];
+            wave_sync();
+            const int P = l_ms * p.a < 250 ? 16 : 8;
+            int sc, te, qe, tb, qb;
+            g_ksw_align2(E.rq, l_ms, staged ? E.tw : G.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb,
+                         qb, lane);
+            if (sc >= p.min_seed_len && qb >= 0) {
+                if (lane == 0) {
+                    GReg b{};
+                    b.rid = a.rid;
+                    b.qb = is_rev ? l_ms - (qe + 1) : qb;
+                    b.qe = is_rev ? l_ms - qb : qe + 1;
+                    b.rb = is_rev ? (l_pac << 1) - (rb + te + 1) : rb + tb;
+                    b.re = is_rev ? (l_pac << 1) - (rb + tb) : rb + te + 1;
+                    b.score = sc;
+                    b.secondary = -1;
+                    b.seedcov = (int)((b.re - b.rb < b.qe - b.qb ? b.re - b.rb : b.qe - b.qb) >> 1);
+                    const int na = E.na[mi];
+                    bool ok = na < AF_G_MAX_REG;
+                    if (ok) {
+                        int i;
+                        for (i = 0; i < na; ++i)
+                            if (ma[i].score < b.score) break;
+                        for (int u = na; u > i; --u) ma[u] = ma[u - 1];
+                        ma[i] = b;
+                        E.na[mi] = na + 1;
+                    }
+                    E.misc[0] = ok;
+                }
+                wave_sync();
+                if (!E.misc[0]) return false;
+            }
+            ++n;
+        }
+        if (n) {
+            const int m = g_dedup_patch<2>(G, p, o, ma, E.na[mi], false, zg, lane);
+            if (lane == 0) E.na[mi] = m;
+            wave_sync();
+        }
+    }
+    return true;
+}
+
+struct P64g { uint64_t x, y; };
+struct GLtP64 {
+    __device__ bool operator()(const P64g &a, const P64g &b) const { return a.x < b.x || (a.x == b.x && a.y < b.y); }
+};
+
+// mem_pair (oracle mem_pair), lane 0: the best pair's score (0 if none) and z[]
+__device__ int g_mem_pair(const DevGenome &G, const af_params &p, const S2Pes *pes, GReg *a0, int n0, GReg *a1, int n1,
+                          int id, int z[2], P64g *v) {
+    const int64_t l_pac = G.l_pac;
+    int nv = 0;
+    GReg *aa[2] = {a0, a1};
+    const int nn[2] = {n0, n1};
+    for (int r = 0; r < 2; ++r)
+        for (int i = 0; i < nn[r]; ++i) {
+            const GReg &e = aa[r][i];
+            P64g key;
+            const int64_t x = e.rb < l_pac ? e.rb : (l_pac << 1) - 1 - e.rb;
+            key.x = (uint64_t)e.rid << 32 | (uint64_t)(x - G.ctg_off_d[e.rid]);
+            key.y = (uint64_t)(uint32_t)e.score << 32 | (uint64_t)i << 2 | (uint64_t)(e.rb >= l_pac) << 1 | (uint64_t)r;
+            v[nv++] = key;
+        }
+    ks_introsort(v, nv, GLtP64());
+    int y[4] = {-1, -1, -1, -1};
+    bool have = false;
+    P64g best{0, 0};
+    for (int i = 0; i < nv; ++i) {
+        for (int r = 0; r < 2; ++r) {
+            const int dir = r << 1 | (int)(v[i].y >> 1 & 1);
+            if (pes[dir].failed) continue;
+            const int which = r << 1 | (int)((v[i].y & 1) ^ 1);
+            if (y[which] < 0) continue;
+            for (int k = y[which]; k >= 0; --k) {
+                if ((int)(v[k].y & 3) != which) continue;
+                const int64_t dist = (int64_t)v[i].x - (int64_t)v[k].x;
+                if (dist > pes[dir].high) break;
+                if (dist < pes[dir].low) continue;
+                const double ns = ((double)dist - pes[dir].avg) / pes[dir].std;
+                int q = (int)((double)((v[i].y >> 32) + (v[k].y >> 32)) + .721 * log(2. * erfc(fabs(ns) * 0.70710678118654752440)) * p.a + .499);
+                if (q < 0) q = 0;
+                P64g u;
+                u.y = (uint64_t)k << 32 | (uint64_t)i;
+                u.x = (uint64_t)q << 32 | (hash_64(u.y ^ (uint64_t)(int64_t)(int32_t)((uint32_t)id << 8)) & 0xffffffffU);
+                if (!have || GLtP64()(best, u)) { best = u; have = true; }
+            }
+        }
+        y[v[i].y & 3] = i;
+    }
+    if (!have) return 0;
+    const int i = (int)(best.y >> 32), k = (int)(best.y << 32 >> 32);
+    z[v[i].y & 1] = (int)(v[i].y << 32 >> 34);
+    z[v[k].y & 1] = (int)(v[k].y << 32 >> 34);
+    return (int)(best.x >> 32);
+}
+
+// G4: mem_sam_pe for every pair (one wave per pair); records of read 2pp + m at
+// recs[(2 pp + m) * AF_G_MAX_REC ..], counts n_rec[2 pp + m]
+template <int CPL>
+__global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                const int32_t *__restrict__ lens, const int32_t *__restrict__ n_pairs_ptr,
+                                                int64_t cap, af_params p, GOpt o, GWork w, S2Work sw,
+                                                uint8_t *__restrict__ scr_base, size_t scr_stride,
+                                                uint8_t *__restrict__ zscratch, size_t zstride,
+                                                af_grec *__restrict__ recs, int32_t *__restrict__ n_rec) {
+    GPeLds &E = g_gpe;
+    G3Lds &H = g_g3;
+    const int lane = threadIdx.x;
+    int64_t n = n_pairs_ptr ? (int64_t)*n_pairs_ptr : cap;
+    if (n > cap) n = cap;
+    const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    // region lists of both ends (and the rescue copies) in the wave's scratch
+    GReg *A[2] = {S.reg, reinterpret_cast<GReg *>(S.pool)};
+    GReg *B = reinterpret_cast<GReg *>(S.ch);
+    P64g *V = reinterpret_cast<P64g *>(S.seed);
+    static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "pool holds a region list");
+    static_assert((size_t)AF_G_MAX_CHAIN * sizeof(GChain) >= 2 * (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "ch holds 2 lists");
+    static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= 2 * (size_t)(AF_G_MAX_REG + 4) * sizeof(P64g), "seed holds v");
+    for (int64_t pp = blockIdx.x; pp < n; pp += gridDim.x) {
+        for (int m = 0; m < 2; ++m) {
+            const int64_t r = 2 * pp + m;
+            const int l = read_len(lens, r, stride);
+            const uint8_t *rd = reads + r * (int64_t)stride;
+            for (int x = lane; x < l; x += 64) E.q[m][x] = nt4(rd[x]);
+            const int nr = w.reg_n[r];
+            const int na = nr > 0 ? nr : 0;
+            for (int k = lane; k < na; k += 64) A[m][k] = w.reg[w.reg_off[r] + k];
+            if (lane == 0) { E.len[m] = l; E.na[m] = na; E.ovf[m] = nr < 0; }
+        }
+        if (lane < 4) E.pes[lane] = sw.pes[(int64_t)g_chunk_of(sw, pp) * 4 + lane];
+        wave_sync();
+        // mate rescue for the top hits of each end (copies taken before any rescue)
+        if (lane == 0) {
+            for (int i = 0; i < 2; ++i) {
+                int nb = 0;
+                for (int j = 0; j < E.na[i]; ++j)
+                    if (A[i][j].score >= A[i][0].score - o.pen_unpaired) B[i * (AF_G_MAX_REG + 1) + nb++] = A[i][j];
+                E.nb[i] = nb;
+            }
+        }
+        wave_sync();
+        for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < E.nb[i] && j < o.max_matesw; ++j) {
+                if (E.ovf[!i]) continue;
+                const GReg bj = B[i * (AF_G_MAX_REG + 1) + j];
+                if (!g_matesw(G, p, o, S, !i, A[!i], bj, zg, lane)) {
+                    wave_sync();
+                    if (lane == 0) { E.ovf[!i] = 1; E.na[!i] = 0; }
+                    wave_sync();
+                }
+            }
+        // primary marking, pairing and the record choice (mem_sam_pe)
+        if (lane == 0) {
+            const uint64_t id = (uint64_t)(o.pair_base + pp);
+            g_mark_primary(A[0], E.na[0], (int64_t)(id << 1 | 0), p, S.kept);
+            g_mark_primary(A[1], E.na[1], (int64_t)(id << 1 | 1), p, S.kept);
+            int z[2] = {0, 0}, extra = 1, mode = 0;  // mode 1: paired records
+            int o_sc = 0;
+            if (E.na[0] && E.na[1] && (o_sc = g_mem_pair(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)id, z, V)) > 0) {
+                int is_multi = 0;
+                for (int i = 0; i < 2; ++i) {
+                    int j;
+                    for (j = 1; j < E.na[i]; ++j)
+                        if (A[i][j].secondary < 0 && A[i][j].score >= p.T) break;
+                    is_multi |= j < E.na[i];
+                }
+                if (!is_multi) {
+                    const int score_un = A[0][0].score + A[1][0].score - o.pen_unpaired;
+                    if (o_sc > score_un) {
+                        for (int i = 0; i < 2; ++i) {
+                            GReg &c = A[i][z[i]];
+                            if (c.secondary >= 0) { c.sub = A[i][c.secondary].score; c.secondary = -2; }
+                        }
+                        extra |= 2;
+                    } else {
+                        z[0] = z[1] = 0;
+                    }
+                    mode = 1;
+                }
+            }
+            E.misc[1] = mode; E.misc[2] = z[0]; E.misc[3] = z[1]; E.misc[4] = extra;
+        }
+        wave_sync();
+        const int mode = E.misc[1];
+        int extra = E.misc[4];
+        const int zz[2] = {E.misc[2], E.misc[3]};
+        // h[i] = mem_reg2aln of each end's chosen region (paired) or top region >= T
+        for (int i = 0; i < 2; ++i) {
+            const int l = E.len[i];
+            DpLds &L = g_dp;
+            for (int x = lane; x < l; x += 64) L.q[x] = E.q[i][x];
+            wave_sync();
+            const GReg *ar = nullptr;
+            if (mode == 1) ar = &A[i][zz[i]];
+            else if (E.na[i] && A[i][0].score >= p.T) ar = &A[i][0];
+            g_reg2aln<CPL>(G, p, l, ar, H.mate[i], zg, lane);
+            wave_sync();
+        }
+        if (mode == 1) {
+            if (lane == 0) {
+                for (int i = 0; i < 2; ++i) {
+                    H.mate[i].flag |= 0x40 << i | extra;
+                }
+                for (int i = 0; i < 2; ++i) {
+                    const int64_t r = 2 * pp + i;
+                    g_aln2rec(H.mate[i], &H.mate[!i], 0, E.len[i], (int32_t)r, recs[r * AF_G_MAX_REC]);
+                    n_rec[r] = 1;
+                }
+            }
+            wave_sync();
+        } else {
+            if (H.mate[0].rid == H.mate[1].rid && H.mate[0].rid >= 0) {
+                int64_t dist;
+                const int d = g_infer_dir(G.l_pac, A[0][0].rb, A[1][0].rb, &dist);
+                if (!E.pes[d].failed && dist >= E.pes[d].low && dist <= E.pes[d].high) extra |= 2;
+            }
+            for (int i = 0; i < 2; ++i) {
+                const int64_t r = 2 * pp + i;
+                const int l = E.len[i];
+                DpLds &L = g_dp;
+                for (int x = lane; x < l; x += 64) L.q[x] = E.q[i][x];
+                wave_sync();
+                const GAln mate = H.mate[!i];
+                const int nrec = g_reg2sam<CPL>(G, p, l, A[i], E.na[i], (0x40 << i) | extra, &mate, (int32_t)r,
+                                                recs + r * AF_G_MAX_REC, zg, lane);
+                if (lane == 0) n_rec[r] = nrec;
+                wave_sync();
+            }
+        }
+        if (lane == 0) {
+            for (int i = 0; i < 2; ++i) {
+                const int64_t r = 2 * pp + i;
+                const int nr = n_rec[r];
+                if (E.ovf[i] || nr > AF_G_MAX_REC) {
+                    for (int j = 0; j < (nr < AF_G_MAX_REC ? nr : AF_G_MAX_REC); ++j)
+                        recs[r * AF_G_MAX_REC + j].flag |= AF_FLAG_MEM_OVERFLOW;
+                    if (nr > AF_G_MAX_REC) atomicAdd(&w.stats[AF_GSTAT_RECS], 1);
+                }
+            }
+        }
+        wave_sync();
+    }
+}
+
+__global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; }
+    if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
+    if (t < AF_GSTAT_N) w.stats[t] = 0;
+    (void)n_reads;
+}
+
+}  // namespace
+
+size_t af_g1_slot_bytes() { return (size_t)G1_SLOT_BYTES; }
+size_t af_g2_slot_bytes() { return g2_slot_bytes(); }
+
+// S4 / S5 up to the regions: G1 + G2 over reads [0, *d_n) (or cap) of a call
+hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                                    const int32_t *d_n, int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
+                                    uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
+                                    uint8_t *zscratch, hipStream_t s) {
+    hipLaunchKernelGGL(k_g_zero, dim3(1), dim3(64), 0, s, w, cap, w.heads);
+    hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)(n_g1_threads / 64)), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
+                       (int64_t)0, p, o, g1_scratch, w);
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    const int cpl = (stride + 1 + 63) / 64;
+#define AF_GO(C) hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap, \
+                                    (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}
+
+hipError_t af_launch_genome_se(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const GWork &w,
+                               uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs, int32_t *n_rec,
+                               hipStream_t s) {
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    const int cpl = (stride + 1 + 63) / 64;
+#define AF_GO(C) hipLaunchKernelGGL((k_g_se<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap, p, \
+                                    id_base, w, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}
+
+hipError_t af_launch_genome_pe(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                               const int32_t *d_npairs, int64_t cap_pairs, const af_params &p, const GOpt &o,
+                               const GWork &w, const S2Work &sw, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch,
+                               af_grec *recs, int32_t *n_rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_g_pe_hist, dim3((unsigned)std::max<int64_t>(1, (cap_pairs + 255) / 256)), dim3(256), 0, s,
+                       d_npairs, cap_pairs, G.l_pac, p, o, w, sw);
+    hipError_t e = af_launch_s2_pestat(sw, o.max_ins, s);
+    if (e != hipSuccess) return e;
+    const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
+    const int cpl = (stride + 1 + 63) / 64;
+#define AF_GO(C) hipLaunchKernelGGL((k_g_pe<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_npairs, \
+                                    cap_pairs, p, o, w, sw, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec)
+    if (cpl <= 2) AF_GO(2);
+    else if (cpl <= 3) AF_GO(3);
+    else if (cpl <= 4) AF_GO(4);
+    else AF_GO(AF_CPL);
+#undef AF_GO
+    return hipGetLastError();
+}

@@ -1,0 +1,214 @@
+"""The genome `bwa mem` calls of the partner stages on the GPU.
+
+The reference runs bwa 0.7.17 against the whole genome twice per anchor gene:
+
+- S4, paired: ``bwa mem -M -t T genome tmp1.fq tmp2.fq`` (Anchored_Fusion.py:188), whose every
+  record `Find_blocks` reads (functions.py:376-496);
+- S5, single-end: ``bwa mem -M -t T genome split_reads.fa`` (functions.py:716), whose every
+  record `del_too_many_reads` reads (fn:705-768).
+
+`GenomeIndex` is ``bwa index genome.fa`` (AF:173-178) built on the GPU (csrc/fmindex.hip: the
+bwa text with bns_fasta2bntseq's lrand48 substitution of ambiguous bases, its suffix array and
+FM index) and the two calls (csrc/bwa_genome.hip: SMEM seeding with max_occ sampling in
+suffix-array order, chains and the chain filter, extension, dedup/patch, -M primary marking,
+paired-end statistics, mate rescue and pairing, mem_reg2sam's records).  The records come back
+as `af_grec` rows (REC_DTYPE) and are printed as bwa prints them by `sam_lines`.  Bit-exact
+contract: oracle/bwa_pe.c in FM mode (tests/test_gpu_genome.py); parity with the bwa binary is
+unpinned (absent here), the seeding restatement is cross-checked against the MEM-set form the
+anchor path uses (tests/test_oracle_fm.py).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+MAX_REC = _lib.AF_G_MAX_REC
+REC_DTYPE = np.dtype([("read", "<i4"), ("flag", "<i4"), ("rid", "<i4"), ("mrid", "<i4"), ("pos", "<i8"),
+                      ("mpos", "<i8"), ("score", "<i4"), ("n_cigar", "<i4"), ("seq_b", "<i4"), ("seq_e", "<i4"),
+                      ("cigar", "<u4", (_lib.AF_MAX_CIGAR,))])
+assert REC_DTYPE.itemsize == 176
+_OPS = "MIDNSHP=X"
+_COMP = str.maketrans("ACGTNacgtn", "TGCANtgcan")
+STAT_NAMES = ("cap_overflow", "pool_overflow", "record_overflow")
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    return stream if isinstance(stream, int) else stream.cuda_stream
+
+
+class GenomeIndex:
+    """`bwa index` of contigs [(name, seq)] (host strings/bytes) on GPU `device`."""
+
+    def __init__(self, contigs, device=0, ctx=None):
+        self.names = [n for n, _ in contigs]
+        self.lens = [len(s) for _, s in contigs]
+        blob = b"".join(s.encode() if isinstance(s, str) else bytes(s) for _, s in contigs)
+        off = np.concatenate([[0], np.cumsum(self.lens)[:-1]]).astype(np.int64)
+        self._open(ctx, device)
+        ln = np.asarray(self.lens, dtype=np.int64)
+        self.g = ctypes.c_void_p()
+        _lib.check(self.ctx, _lib.lib().af_genome_build(self.ctx, blob, len(blob), off.ctypes.data, ln.ctypes.data,
+                                                        len(contigs), ctypes.byref(self.g)), "af_genome_build")
+        self.l_pac = int(_lib.lib().af_genome_lpac(self.g))
+
+    @classmethod
+    def from_device(cls, blob_t, names, offsets, lens, device=0, ctx=None):
+        """Contigs already in HBM: blob_t a uint8 device tensor holding contig k at offsets[k]
+        (lens[k] bytes; bytes between contigs are ignored)."""
+        self = cls.__new__(cls)
+        self.names, self.lens = list(names), [int(v) for v in lens]
+        off = np.asarray(offsets, dtype=np.int64)
+        ln = np.asarray(self.lens, dtype=np.int64)
+        self._open(ctx, device)
+        self.g = ctypes.c_void_p()
+        _lib.check(self.ctx, _lib.lib().af_genome_build_device(
+            self.ctx, blob_t.data_ptr(), int(blob_t.numel()), off.ctypes.data, ln.ctypes.data, len(self.names),
+            ctypes.byref(self.g)), "af_genome_build_device")
+        self.l_pac = int(_lib.lib().af_genome_lpac(self.g))
+        return self
+
+    def _open(self, ctx, device):
+        self._own_ctx = ctx is None
+        if ctx is None:
+            ctx = ctypes.c_void_p()
+            _lib.check(None, _lib.lib().af_ctx_create(int(device), ctypes.byref(ctx)), "af_ctx_create")
+        self.ctx = ctx
+
+    def close(self):
+        L = _lib._L
+        if L is None:
+            return
+        if getattr(self, "g", None):
+            L.af_genome_free(self.g)
+            self.g = None
+        if getattr(self, "_own_ctx", False) and getattr(self, "ctx", None):
+            L.af_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    # ---- index access (tests) -------------------------------------------------------------
+    def text(self, first=0, n=None):
+        n = 2 * self.l_pac - first if n is None else n
+        out = np.zeros(n, np.uint8)
+        _lib.check(self.ctx, _lib.lib().af_genome_read(self.ctx, self.g, 0, first, n, out.ctypes.data), "af_genome_read")
+        return out
+
+    def sa(self, first=0, n=None):
+        n = 2 * self.l_pac + 1 - first if n is None else n
+        out = np.zeros(n, np.int64)
+        _lib.check(self.ctx, _lib.lib().af_genome_read(self.ctx, self.g, 1, first, n, out.ctypes.data), "af_genome_read")
+        return out
+
+    def primary(self):
+        return int(_lib.lib().af_genome_primary(self.g))
+
+    def stats(self):
+        out = np.zeros(_lib.AF_GSTAT_N, np.int32)
+        _lib.check(self.ctx, _lib.lib().af_genome_stats(self.ctx, out.ctypes.data), "af_genome_stats")
+        return dict(zip(STAT_NAMES, (int(v) for v in out)))
+
+    # ---- the calls (host buffers) ----------------------------------------------------------
+    def align_se(self, reads, lens=None, params=None, pe=None, id_base=0):
+        """S5 on reads uint8 [n, stride]: (records [n, MAX_REC] REC_DTYPE, counts [n])."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        recs = np.zeros((n, MAX_REC), REC_DTYPE)
+        nrec = np.zeros(n, np.int32)
+        if n == 0:
+            return recs, nrec
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        _lib.check(self.ctx, _lib.lib().af_genome_align_se(
+            self.ctx, self.g, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), int(id_base),
+            recs.ctypes.data, nrec.ctypes.data), "af_genome_align_se")
+        return recs, nrec
+
+    def align_pe(self, reads, lens=None, params=None, pe=None):
+        """S4 on pair-major reads uint8 [2N, stride]: (records [2N, MAX_REC], counts [2N])."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        nr = reads.shape[0]
+        if nr % 2:
+            raise ValueError("pair-major reads: an even number of rows")
+        recs = np.zeros((nr, MAX_REC), REC_DTYPE)
+        nrec = np.zeros(nr, np.int32)
+        if nr == 0:
+            return recs, nrec
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        _lib.check(self.ctx, _lib.lib().af_genome_align_pe(
+            self.ctx, self.g, reads.ctypes.data, nr // 2, reads.shape[1], None if lp is None else lp.ctypes.data,
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), recs.ctypes.data,
+            nrec.ctypes.data), "af_genome_align_pe")
+        return recs, nrec
+
+    def regions(self, reads, lens=None, params=None, pe=None, max_reg=64):
+        """mem_align1_core's regions per read (tests): int64 [n, max_reg, 12], counts [n]."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        regs = np.zeros((n, max_reg, 12), np.int64)
+        nreg = np.zeros(n, np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        _lib.check(self.ctx, _lib.lib().af_genome_regions(
+            self.ctx, self.g, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), max_reg,
+            regs.ctypes.data, nreg.ctypes.data), "af_genome_regions")
+        return regs, nreg
+
+    # ---- the calls (device buffers, asynchronous) -----------------------------------------
+    def align_se_device(self, reads_t, n, stride, recs_t, nrec_t, lens_t=None, params=None, pe=None, id_base=0,
+                        stream=None, ctx=None):
+        c = self.ctx if ctx is None else ctx
+        _lib.check(c, _lib.lib().af_genome_align_se_device(
+            c, self.g, reads_t.data_ptr(), int(n), int(stride), None if lens_t is None else lens_t.data_ptr(),
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), int(id_base),
+            recs_t.data_ptr(), nrec_t.data_ptr(), _stream_handle(stream)), "af_genome_align_se_device")
+
+    def align_pe_device(self, reads_t, n_pairs, stride, lens_t, recs_t, nrec_t, params=None, pe=None, stream=None,
+                        ctx=None):
+        c = self.ctx if ctx is None else ctx
+        _lib.check(c, _lib.lib().af_genome_align_pe_device(
+            c, self.g, reads_t.data_ptr(), int(n_pairs), int(stride), lens_t.data_ptr(),
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), recs_t.data_ptr(),
+            nrec_t.data_ptr(), _stream_handle(stream)), "af_genome_align_pe_device")
+
+    # ---- SAM text --------------------------------------------------------------------------
+    def sam_lines(self, name, seq, recs, n):
+        """The SAM lines bwa prints for one read (its af_grec rows recs[:n]): QNAME FLAG RNAME POS
+        MAPQ CIGAR RNEXT PNEXT TLEN SEQ QUAL.  MAPQ (60 / 0 unmapped) and TLEN (0) are not
+        bwa's: no consumer reads them (SURVEY.md §8 b)."""
+        return sam_lines(self.names, name, seq, recs, n)
+
+
+def sam_lines(names, name, seq, recs, n):
+    out = []
+    rc = None
+    for k in range(min(int(n), MAX_REC)):
+        e = recs[k]
+        flag = int(e["flag"])
+        rid = int(e["rid"])
+        if flag & 0x10:
+            if rc is None:
+                rc = seq.translate(_COMP)[::-1]
+            s = rc
+        else:
+            s = seq
+        s = s[int(e["seq_b"]):int(e["seq_e"])]
+        nc = int(e["n_cigar"])
+        cig = "".join(f"{int(c) >> 4}{_OPS[int(c) & 15]}" for c in e["cigar"][:nc]) if nc else "*"
+        mrid = int(e["mrid"])
+        if mrid < 0:
+            rnext, pnext = "*", 0
+        else:
+            rnext, pnext = ("=" if mrid == rid else names[mrid]), int(e["mpos"]) + 1
+        rname = names[rid] if rid >= 0 else "*"
+        pos1 = int(e["pos"]) + 1 if rid >= 0 else 0
+        mapq = 0 if flag & 4 else 60
+        out.append(f"{name}\t{flag & 0xFFFF}\t{rname}\t{pos1}\t{mapq}\t{cig}\t{rnext}\t{pnext}\t0\t{s}\t*\n")
+    return out

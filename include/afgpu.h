@@ -23,7 +23,12 @@
  *                            `samtools view -f/-F` filters of Anchored_Fusion.py:186-194
  *   af_gather_reads_device <- `samtools fastq` of the S3 partitions (AF:186-188) and the split-read
  *                            FASTA of functions.py:705-716: the genome searches' queries
- *   af_index_build_genome <- `bwa index <genome>` (AF:173-178), GPU-built
+ *   af_genome_build(_device) <- `bwa index <genome.fa>` (AF:173-178): the bwa text, suffix array
+ *                            and FM index of a multi-contig genome, built on the GPU
+ *   af_genome_align_pe(_device) <- `bwa mem -M -t T <genome> tmp1.fq tmp2.fq` (AF:188, S4): every
+ *                            SAM record of every pair, as bwa prints them (Find_blocks input)
+ *   af_genome_align_se(_device) <- `bwa mem -M -t T <genome> split_reads.fa` (functions.py:716, S5)
+ *   af_index_build_genome <- the placement index of af_place (16-mer table; BLAT-side helper)
  *   af_tile_index_build / af_blat(_device) <- `blat [opts] target.fa query.fa out.psl`
  *                            (functions.py:341, 530, 966, 1007, 1071, 1122, 1244)
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
@@ -288,6 +293,77 @@ int af_gather_reads_device(af_ctx *ctx, const uint8_t *d_reads, int32_t stride, 
                            const int32_t *d_rows, int64_t n_rows, int32_t mode, const af_aln_out *d_out,
                            int64_t first, int64_t step, int64_t cap, uint8_t *d_q, int32_t *d_q_lens,
                            int32_t *d_q_rows, int32_t *d_n_q, void *stream);
+
+/* ---- the genome `bwa mem` calls S4 / S5 ---------------------------------------------------
+ * bwa 0.7.17's algorithm restated on the GPU over bwa's own index construction: contigs joined
+ * without separators, ambiguous bases -> lrand48() & 3 after srand48(11) (bns_fasta2bntseq), the
+ * suffix array of pac ++ revcomp(pac), SMEM seeding with re-seeding and the third pass
+ * (bwt_smem1, bwt_seed_strategy1), max_occ sampling in suffix-array order, chains and the chain
+ * filter, ksw extension, dedup/patch, -M primary marking, and for S4 the paired-end statistics per
+ * chunk, mate rescue and pairing.  Contract: oracle/bwa_pe.c (FM mode), bit-exact.
+ * Per-read caps (bwa has none): a read past one is reported unmapped with AF_FLAG_MEM_OVERFLOW and
+ * counted in af_genome_stats. */
+#define AF_G_MAX_INTV 512     /* seed intervals (SMEMs, re-seeds, third-pass seeds) */
+#define AF_G_MAX_OCC 8192     /* chain seeds (occurrences after max_occ sampling) */
+#define AF_G_MAX_CHAIN 8192
+#define AF_G_MAX_REG 1024     /* regions (after extension; with mate-rescue hits) */
+#define AF_G_MAX_REC 8        /* SAM records per read (primary + -M parts) */
+typedef struct af_genome af_genome;
+/* One printed SAM record (mem_aln2sam): FLAG as printed (0x100 marks -M parts; AF_FLAG_* bits
+ * above 0xFFFF), contig index and 0-based POS (-1: '*'), the mate's (paired-end), AS, CIGAR in BAM
+ * op codes (H = 5 on the parts after the first), and SEQ = the read in the record's orientation
+ * (reverse complement for 0x10) sliced [seq_b, seq_e). */
+typedef struct {
+    int32_t read, flag, rid, mrid;
+    int64_t pos, mpos;
+    int32_t score, n_cigar, seq_b, seq_e;
+    uint32_t cigar[AF_MAX_CIGAR];
+} af_grec;
+/* counters of the last genome call on a context: [0] reads past a per-read cap, [1] reads whose
+ * intervals / regions did not fit the call's pools (also flagged), [2] reads with more than
+ * AF_G_MAX_REC records */
+#define AF_GSTAT_OVERFLOW 0
+#define AF_GSTAT_POOL 1
+#define AF_GSTAT_RECS 2
+#define AF_GSTAT_N 4
+/* blob: contig k is blob[ctg_off[k], ctg_off[k] + ctg_len[k]) (host arrays; bytes between contigs
+ * are ignored, as a FASTA's headers are).  Synchronous; the index stays in HBM. */
+int af_genome_build(af_ctx *ctx, const char *blob, int64_t n_blob, const int64_t *ctg_off, const int64_t *ctg_len,
+                    int32_t n_ctg, af_genome **out);
+int af_genome_build_device(af_ctx *ctx, const char *d_blob, int64_t n_blob, const int64_t *ctg_off,
+                           const int64_t *ctg_len, int32_t n_ctg, af_genome **out);
+void af_genome_free(af_genome *g);
+int64_t af_genome_lpac(const af_genome *g);
+int64_t af_genome_primary(const af_genome *g);
+/* copies rows [first, first + n) of the bwa text (what = 0, uint8 codes) or of the suffix array
+ * (what = 1, int64, rows 0..2 l_pac) to host memory (tests) */
+int af_genome_read(af_ctx *ctx, const af_genome *g, int32_t what, int64_t first, int64_t n, void *out);
+/* S5 (single-end): records of reads [0, n) (`stride` bytes per row, d_lens may be NULL) into
+ * d_recs[r * AF_G_MAX_REC + k] for k < d_n_rec[r]; read ids id_base + r (bwa's hash tie-breaks).
+ * Device buffers, asynchronous on `stream`; calls on one context must be stream-ordered. */
+int af_genome_align_se_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                              const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
+                              af_grec *d_recs, int32_t *d_n_rec, void *stream);
+/* S4 (paired-end): pair-major reads [0, 2 n_pairs) with their lengths (d_lens required); every
+ * record of read 2i + m at d_recs[(2i + m) * AF_G_MAX_REC ..]; pe->chunk_bases / pair_base as for
+ * af_align_pairs (insert-size statistics per bwa chunk). */
+int af_genome_align_pe_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs,
+                              int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
+                              af_grec *d_recs, int32_t *d_n_rec, void *stream);
+/* host-buffer forms (synchronous) */
+int af_genome_align_se(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                       const int32_t *lens, const af_params *p, const af_pe *pe, int64_t id_base, af_grec *recs,
+                       int32_t *n_rec);
+int af_genome_align_pe(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n_pairs, int32_t stride,
+                       const int32_t *lens, const af_params *p, const af_pe *pe, af_grec *recs, int32_t *n_rec);
+/* regions after mem_align1_core (rb, re on bwa's doubled text; parity tests): regs[r * max_reg +
+ * k] as 12 int64 words {rb, re, qb, qe, rid, score, truesc, w, seedcov, seedlen0, 0, 0}, n_reg[r]
+ * (-1: overflow); host buffers */
+int af_genome_regions(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                      const int32_t *lens, const af_params *p, const af_pe *pe, int32_t max_reg, int64_t *regs,
+                      int32_t *n_reg);
+/* the counters of the last genome call on ctx (AF_GSTAT_N int32; synchronises) */
+int af_genome_stats(af_ctx *ctx, int32_t *out);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as
