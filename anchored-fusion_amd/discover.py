@@ -5,27 +5,29 @@ partner stages, all on the device with no host round trip for the data (SURVEY.m
 |---|---|
 | AF:182 `bwa mem -M anchor fq1 fq2` | K1 + K2 + K3 per batch (`AlignerGroup`), batches on bwa's chunk grid |
 | AF:182 `\\| samtools sort`, AF:186-194 filters | `af_partition_device` over every record of the set |
-| AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_place_device` |
-| fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + the same launch |
+| AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_genome_align_pe_device` |
+| fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + `af_genome_align_se_device` |
 | fn:530 BLAT of the split reads' tails (S6) | tails cut in K3 + `af_blat_device` (BLAT restatement, -minScore=20) |
 
 `run()` enqueues one pass; S3 synchronises twice (its select count sizes the sort; the partition
-counts size the gathers).  Everything else stays on the device: the records, the row lists, the
-queries and the hits, which `exchange()` all-gathers between ranks (one process per GPU, RCCL).
+counts size the gathers) and the gathers once (the split-read count sizes S5).  Everything else
+stays on the device: the records, the row lists, the queries and the genome calls' SAM records
+(af_grec), which `exchange()` all-gathers between ranks (one process per GPU, RCCL).  Per-call
+caps (query and tail buffers, the genome calls' per-read caps) are counted in `summary()`.
 """
 import os
 import sys
 
 from . import _lib
 from . import blat as _blat
-from . import place as _place
+from . import genome as _genome
 from .align import AlignerGroup
 from .shard import chunk_pairs
 
 MIN_CLIP = 20       # split-read tails placed by S6 (functions.py:530 queries; clip >= 20)
-MAX_HITS = 16
-EX_HITS = 4         # hits per query carried by exchange()
-HIT_WORDS = 44      # af_hit as int32 words (176 B)
+MAX_REC = _genome.MAX_REC
+EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
+HIT_WORDS = 44      # af_grec as int32 words (176 B)
 PSL_WORDS = 82      # af_psl as int32 words (328 B)
 EX_WORDS = 39 + EX_HITS * HIT_WORDS
 _DEBUG = os.environ.get("AF_DEBUG_DISCOVER") == "1"
@@ -38,13 +40,14 @@ def _log(msg):
 class CandidateDiscovery:
     """S2 + S3 + S4/S5/S6 genome searches for `n_pairs` resident pairs of `read_len` bases.
 
-    reference: place.Reference (the genome, HBM-resident, for the bwa calls); tiles:
+    reference: genome.GenomeIndex (`bwa index` of the genome, HBM-resident, for the bwa calls); tiles:
     blat.TileReference of the same genome at BLAT's default step (S6).  pair_base: the set's first pair in
     bwa's input stream (a chunk boundary).  batch_chunks: bwa chunks per S2 batch; inflight:
     batches in flight (AlignerGroup)."""
 
     def __init__(self, anchor: bytes, reference, tiles, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
                  pair_base=0, chunk_bases=10_000_000, query_frac=0.004, tail_frac=0.002):
+        self.chunk_bases = int(chunk_bases)
         import torch
         self.dev = torch.device("cuda", device)
         self.anchor, self.ref, self.tiles_ref = bytes(anchor), reference, tiles
@@ -75,9 +78,9 @@ class CandidateDiscovery:
         self.qcap = max(4096, int(nr * query_frac))
         self.q = z(self.qcap, self.L, dt=torch.uint8)
         self.q_lens, self.q_rows, self.n_q = z(self.qcap), z(self.qcap), z(1)
-        self.q_hits = z(self.qcap * MAX_HITS * _place.HIT_DTYPE.itemsize, dt=torch.uint8)
-        self.q_nh = z(self.qcap)
-        self.p_genome = _place.preset_params("genome_bwa")
+        self.q_recs = z(self.qcap * MAX_REC * _genome.REC_DTYPE.itemsize, dt=torch.uint8)
+        self.q_nh = z(self.qcap)   # SAM records per query
+        self.p_genome = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), AF:188 / fn:716
         self.p_tail = _blat.params("split_tail")
         self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
 
@@ -141,9 +144,6 @@ class CandidateDiscovery:
                                self.q_rows, self.n_q, first=1, step=2, stream=s0)
         al.gather_reads_device(reads_t, self.L, an, na, _lib.AF_GATHER_SPLIT_SAM, self.q, self.q_lens, self.q_rows,
                                self.n_q, out_t=self.out, first=2 * npair, step=1, stream=s0)
-        if _DEBUG:
-            s0.synchronize()
-            _log(f"gathered {int(self.n_q.item())} queries, {int(self.tails['n'].item())} tails")
         if phase_events:
             phase_events[2].record(s0)
         s6.wait_stream(s0)
@@ -151,30 +151,47 @@ class CandidateDiscovery:
                                      lens_t=self.tails["lens"], p=self.p_tail, stream=s6)
         s6_done = torch.cuda.Event()
         s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
-        # S4 + S5 on the genome (bwa mem -M defaults); then join S6
-        self.ref.place_device(self.q, self.n_q, self.L, self.q_hits, self.q_nh, lens_t=self.q_lens,
-                              params=self.p_genome, max_hits=MAX_HITS, stream=s0)
+        # S4 (`bwa mem -M genome tmp1 tmp2`): the pairs' records, bwa's chunks over this input
+        pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
+        recs = self.q_recs.view(torch.int32)
+        if npair:
+            self.ref.align_pe_device(self.q, npair, self.L, self.q_lens, recs, self.q_nh, params=self.p_genome, pe=pe,
+                                     stream=s0)
+        # S5 (`bwa mem -M genome split_reads.fa`): its read count sizes the launch
+        s0.synchronize()
+        nq = min(int(self.n_q.item()), self.qcap)
+        n5 = max(0, nq - 2 * npair)
+        if n5:
+            w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+            self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
+                                     lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0, stream=s0)
         s0.wait_event(s6_done)
         if _DEBUG:
             s0.synchronize()
-            _log("placements done")
+            _log("genome calls done")
         if phase_events:
             phase_events[3].record(s0)
-        self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s4_pairs=npair)
+        self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s4_pairs=npair, s5_split_reads=n5,
+                           s4_pairs_dropped=max(0, min(n1, n2) - npair), s5_dropped=max(0, int(self.n_q.item()) - nq))
         return s0
 
     def summary(self):
         """Host-side counts of the last pass (synchronises)."""
         import torch
         torch.cuda.synchronize(self.dev)
-        nq = int(self.n_q.item())
+        nq = min(int(self.n_q.item()), self.qcap)
         nt = int(self.tails["n"].item())
-        qn = self.q_nh[:min(nq, self.qcap)].cpu().numpy()
         tn = self.t_nh[:min(nt, self.tcap)].cpu().numpy()
+        rec = self.q_recs[:nq * MAX_REC * _genome.REC_DTYPE.itemsize].cpu().numpy().view(_genome.REC_DTYPE)
+        rec = rec.reshape(nq, MAX_REC)
+        first = rec[:, 0]["flag"] if nq else rec
         c = dict(self.counts or {})
-        c.update(queries_s4_s5=nq, s5_split_reads=nq - 2 * c.get("s4_pairs", 0), queries_placed=int((qn > 0).sum()),
-                 tails=nt, tails_placed=int((tn > 0).sum()),
-                 mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()))
+        c.update(queries_s4_s5=nq, queries_placed=int(((first & 4) == 0).sum()) if nq else 0,
+                 genome_records=int(self.q_nh[:nq].sum().item()), tails=nt, tails_placed=int((tn > 0).sum()),
+                 tails_dropped=max(0, nt - self.tcap), mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()),
+                 s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))
+                                        != 0).sum().item()))
+        c.update({f"genome_{k}": v for k, v in self.ref.stats().items()})
         return c
 
     def tail_best_hits(self):
@@ -189,16 +206,16 @@ class CandidateDiscovery:
     def pack(self):
         """The breakpoint candidates of the last pass as int32 rows [k, EX_WORDS] on the device:
         every S4 / S5 query and every S6 tail -- the read's global row (2 words), kind (0 query,
-        1 tail), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the hit count and its first
-        EX_HITS hits (af_hit for the genome bwa calls, the first af_psl rows for BLAT).  These are
-        the only records the stages after S6 read (SURVEY §8 e)."""
+        1 tail), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the record / row count and the first
+        EX_HITS of them (af_grec SAM records of the genome bwa calls, af_psl rows for BLAT).  These
+        are the only records the stages after S6 read (SURVEY §8 e)."""
         import torch
         torch.cuda.synchronize(self.dev)
         nq = min(int(self.n_q.item()), self.qcap)
         nt = min(int(self.tails["n"].item()), self.tcap)
         parts = []
         for kind, n, rows, nh, hits, width, per in (
-                (0, nq, self.q_rows, self.q_nh, self.q_hits, HIT_WORDS, MAX_HITS),
+                (0, nq, self.q_rows, self.q_nh, self.q_recs, HIT_WORDS, MAX_REC),
                 (1, nt, self.tails["read"], self.t_nh, self.t_rows, PSL_WORDS, _blat.MAX_ROWS)):
             if n == 0:
                 continue

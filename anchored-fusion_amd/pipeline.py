@@ -7,7 +7,8 @@ Anchored_Fusion.py:121-227 with its shell calls replaced).
 | AF:144-172 anchor FASTA + `bwa index` | `AnchorAligner(anchor)` (GPU index) |
 | AF:182 `bwa mem -M anchor fq1 fq2 \\| samtools sort` | `AnchorAligner.align_pairs` (K1+K2+K3) |
 | AF:186-194 samtools flag partitions | `align.partition` |
-| AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam_pe` (af_place on the genome + bwa_records) |
+| AF:173-178 `bwa index genome` | `genome.GenomeIndex` (suffix array + FM index built on the GPU) |
+| AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam_pe` (bwa-mem PE on the GPU, csrc/bwa_genome.hip) |
 | AF:198 `Find_homo_genes` | `partner.homolog_genes` |
 | AF:204 `del_too_many_reads` | `genome_check` + `Searches.genome_sam_se` |
 | AF:205-206 `Find_blocks`, `Find_fine_block` | `blocks.spanning_blocks`, `blocks.add_fine_blocks` |
@@ -67,33 +68,61 @@ def sam_line(name, flag, rname, pos1, cigar, seq):
 class Searches:
     """The search services the partner stages need, on the GPU by default.
 
-    `place(targets, queries, preset)` -> PSL lines (partner.py callback);
-    `genome_sam_se(queries)` -> per query the SAM lines of `bwa mem -M genome q.fa` (fn:716);
-    `genome_sam_pe(pairs)` -> the SAM lines of `bwa mem -M genome fq1 fq2` (AF:188).
-    Both render the genome placement's hits with bwa's record rules (bwa_records)."""
+    `place(targets, queries, preset)` -> PSL lines (partner.py callback; BLAT restatement);
+    `genome_sam_se(queries)` -> per query the SAM lines of `bwa mem -M genome q.fa` (fn:716, S5);
+    `genome_sam_pe(pairs)` -> the SAM lines of `bwa mem -M genome fq1 fq2` (AF:188, S4), per pair
+    mate 1's records then mate 2's.
+    The genome calls run bwa-mem restated on the GPU over `bwa index` of the genome
+    (genome.GenomeIndex, built once); genome_factory(contigs) may supply another engine with the
+    same interface (the CPU oracle in tests)."""
 
-    def __init__(self, genome_contigs, device=0, placer=None, chunk_bases=10_000_000):
-        from . import bwa_records
+    def __init__(self, genome_contigs, device=0, placer=None, chunk_bases=10_000_000, genome_factory=None):
+        from . import _lib
         from .place import Placer
         self.genome = genome_contigs
         self.place = placer or Placer(device=device)
+        self.chunk_bases = int(chunk_bases)
+        self._gfac = genome_factory
+        self._device = device
+        self._gidx = None
+        self.params = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), as AF:188 / fn:716 run it
 
-        def _hits(seqs):
-            ref = self.place.reference(self.genome)   # shared with the genome PSL searches
-            p = self.place.params("genome_bwa")
-            hits, nh = ref.raw_hits(seqs, p, 16)
-            return ref, p, hits, nh
+    def genome_index(self):
+        if self._gidx is None:
+            if self._gfac is not None:
+                self._gidx = self._gfac(self.genome)
+            else:
+                from .genome import GenomeIndex
+                self._gidx = GenomeIndex(self.genome, device=self._device)
+        return self._gidx
 
-        def genome_sam_se(queries):
-            ref, p, hits, nh = _hits([s for _, s in queries])
-            return [bwa_records.se_records(ref, n, s, hits[i], nh[i], i, p.T) for i, (n, s) in enumerate(queries)]
+    def _pe(self):
+        from . import _lib
+        return _lib.default_pe(chunk_bases=self.chunk_bases)
 
-        def genome_sam_pe(pairs):
-            ref, p, hits, nh = _hits([s for _, a, b in pairs for s in (a, b)])
-            return bwa_records.pe_records(ref, pairs, hits, nh, p.T, p.min_seed_len, chunk_bases=chunk_bases)
+    def genome_sam_se(self, queries):
+        from .genome import sam_lines
+        from .place import pack_queries
+        if not queries:
+            return []
+        g = self.genome_index()
+        buf, lens = pack_queries([s for _, s in queries])
+        recs, nrec = g.align_se(buf, lens, self.params, self._pe(), id_base=0)
+        return [sam_lines(g.names, n, s, recs[i], nrec[i]) for i, (n, s) in enumerate(queries)]
 
-        self.genome_sam_se = genome_sam_se
-        self.genome_sam_pe = genome_sam_pe
+    def genome_sam_pe(self, pairs):
+        from .genome import sam_lines
+        from .place import pack_queries
+        if not pairs:
+            return []
+        g = self.genome_index()
+        buf, lens = pack_queries([s for _, a, b in pairs for s in (a, b)])
+        recs, nrec = g.align_pe(buf, lens, self.params, self._pe())
+        out = []
+        for i, (name, a, b) in enumerate(pairs):
+            out += sam_lines(g.names, name, a, recs[2 * i], nrec[2 * i])
+            out += sam_lines(g.names, name, b, recs[2 * i + 1], nrec[2 * i + 1])
+        return out
 
     def getfasta(self, rows):
         """bedtools getfasta -name: rows (chrom, start, end, name) -> [(name::chrom:start-end, seq)];

@@ -231,6 +231,11 @@ class GenomeWorld:
         from . import place
         return place.Reference.from_device(self.blob, self.names, self.lens, self.offsets, device=self.device)
 
+    def genome_index(self):
+        """genome.GenomeIndex (`bwa index`, csrc/fmindex.hip) over the contigs in HBM."""
+        from .genome import GenomeIndex
+        return GenomeIndex.from_device(self.blob, self.names, self.offsets, self.lens, device=self.device)
+
     def tiles(self, step_size=11):
         """blat.TileReference over the genome in HBM (af_tile_index_build_device)."""
         from . import blat

@@ -62,6 +62,49 @@ class OracleTileReference:
         pass
 
 
+class OracleGenomeIndex:
+    """The genome calls S4 / S5 restated on the CPU (oracle/bwa_pe.c FM mode), with
+    genome.GenomeIndex's interface (Searches' genome_factory)."""
+
+    def __init__(self, contigs):
+        self.g = oracle.OracleGenome(contigs)
+        self.names = self.g.names
+
+    @staticmethod
+    def _params(params):
+        p = oracle.default_params()
+        if params is not None:
+            for f, _ in p._fields_:
+                setattr(p, f, getattr(params, f))
+        return p
+
+    @staticmethod
+    def _pe(pe):
+        e = oracle.default_pe()
+        if pe is not None:
+            for f, _ in e._fields_:
+                setattr(e, f, getattr(pe, f))
+        return e
+
+    def align_se(self, reads, lens=None, params=None, pe=None, id_base=0):
+        return self.g.align_se(reads, lens, self._params(params), self._pe(pe), id_base=id_base, threads=8)
+
+    def align_pe(self, reads, lens=None, params=None, pe=None):
+        e = self._pe(pe)
+        return self.g.align_pe(reads, lens, self._params(params), e, pair_base=e.pair_base, threads=8)
+
+    def close(self):
+        pass
+
+
+def oracle_searches(genome, chunk_bases=10_000_000):
+    """pipeline.Searches with every service on the CPU oracles."""
+    from anchored_fusion_amd import pipeline
+    from anchored_fusion_amd.place import Placer
+    return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference),
+                             chunk_bases=chunk_bases, genome_factory=OracleGenomeIndex)
+
+
 class OracleAligner:
     def __init__(self, anchor, chunk_bases=None):
         self.ix = oracle.OracleIndex(anchor)

@@ -19,11 +19,9 @@ CHUNK = 300_000  # bases per bwa chunk in these runs: the sample spans several, 
 
 
 def _backends(paths):
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
-    from anchored_fusion_amd.place import Placer
+    from oracle_backends import OracleAligner, oracle_searches
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-    searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference,
-                                                       tile_factory=OracleTileReference))
+    searches = oracle_searches(genome)
     return searches, (lambda a: OracleAligner(a, chunk_bases=CHUNK))
 
 

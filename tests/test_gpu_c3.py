@@ -54,7 +54,7 @@ def test_discovery_matches_oracle_reduced(anchor):
     from anchored_fusion_amd import discover
     from anchored_fusion_amd.align import AlignResult, partition
     W = _world(anchor, 0.02)
-    ref = W.reference()
+    ref = W.genome_index()
     tiles = W.tiles()
     n = 140_000
     reads_t = W.simulate_pairs(n, read_len=150, seed=9)
@@ -89,11 +89,36 @@ def test_discovery_matches_oracle_reduced(anchor):
     rows = d.q_rows[:nq].cpu().numpy()
     for k, (r, s) in enumerate(want):
         assert rows[k] == r and q[k].tobytes() == s
+    # S4 / S5 records (af_grec) of the device calls == the same engine's host-buffer calls on the
+    # same queries (the engine itself is pinned bit-exact vs oracle/bwa_pe.c by test_gpu_genome.py)
+    _check_genome_records(d, ref, q, nq, c["s4_pairs"])
     summ = d.summary()
     assert summ["tails"] > 0 and summ["tails_placed"] > 0.5 * summ["tails"]
+    assert summ["queries_placed"] > 0.9 * nq and summ["genome_cap_overflow"] == 0
     d.close()
     ref.close()
     tiles.close()
+
+
+def _check_genome_records(d, ref, q, nq, npair):
+    from anchored_fusion_amd import _lib, discover, genome
+    recs = d.q_recs[:nq * discover.MAX_REC * genome.REC_DTYPE.itemsize].cpu().numpy().view(genome.REC_DTYPE)
+    recs = recs.reshape(nq, discover.MAX_REC)
+    nrec = d.q_nh[:nq].cpu().numpy()
+    lens = d.q_lens[:nq].cpu().numpy()
+    pe = _lib.default_pe(chunk_bases=d.chunk_bases, pair_base=0)
+    r4, n4 = ref.align_pe(q[:2 * npair], lens[:2 * npair], pe=pe)
+    r5, n5 = ref.align_se(q[2 * npair:nq], lens[2 * npair:nq], pe=pe)
+    want_r, want_n = np.concatenate([r4, r5]), np.concatenate([n4, n5])
+    assert np.array_equal(nrec, want_n)
+    assert (nrec >= 1).all()
+    for r in range(nq):
+        for k in range(min(int(nrec[r]), discover.MAX_REC)):
+            a, b = recs[r, k], want_r[r, k]
+            nc = int(a["n_cigar"])
+            assert all(int(a[f]) == int(b[f]) for f in ("flag", "rid", "mrid", "pos", "mpos", "score", "n_cigar",
+                                                         "seq_b", "seq_e")), (r, k)
+            assert np.array_equal(a["cigar"][:nc], b["cigar"][:nc]), (r, k)
 
 
 def test_c3_full_size(anchor):
@@ -106,7 +131,7 @@ def test_c3_full_size(anchor):
     from anchored_fusion_amd import discover
     from anchored_fusion_amd.shard import chunk_pairs
     W = _world(anchor, 1.0)
-    ref = W.reference()
+    ref = W.genome_index()
     tiles = W.tiles()
     N, L = 50_000_000, 150
     reads_t = W.simulate_pairs(N, read_len=L, seed=20251015)
@@ -116,6 +141,7 @@ def test_c3_full_size(anchor):
     d.run(reads_t)
     summ = d.summary()
     assert summ["tmp1"] == summ["tmp2"] > 1000 and summ["anchored"] > 1_000_000
+    assert summ["genome_cap_overflow"] == 0 and summ["queries_placed"] > 0.9 * summ["queries_s4_s5"]
     # oracle on the first two chunks (bwa's read ids and insert-size chunks are the same)
     m = 2 * chunk_pairs(L)
     sub = reads_t[:2 * m].cpu().numpy()
@@ -165,7 +191,7 @@ def test_discovery_rank_shard_and_exchange(anchor):
     from anchored_fusion_amd import discover
     from anchored_fusion_amd.shard import chunk_pairs
     W = _world(anchor, 0.02)
-    ref = W.reference()
+    ref = W.genome_index()
     tiles = W.tiles()
     n, pb = 60_000, 3 * chunk_pairs(150)
     reads_t = W.simulate_pairs(n, read_len=150, seed=13, pair_base=pb)
@@ -188,6 +214,8 @@ def test_discovery_rank_shard_and_exchange(anchor):
     finally:
         dist.destroy_process_group()
     assert ex.shape == packed.shape and torch.equal(ex.cpu(), packed.cpu()) and ex.shape[0] > 0
+    q = d.q[:int(d.n_q.item())].cpu().numpy()
+    _check_genome_records(d, ref, q, q.shape[0], d.counts["s4_pairs"])
     p = packed.cpu().numpy()
     grow = p[:, 0].view(np.uint32).astype(np.int64) | (p[:, 1].astype(np.int64) << 32)
     nq = int(d.n_q.item())

@@ -31,10 +31,9 @@ def _check(out_folder, truth):
 
 
 def _run_oracle(paths, out):
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
-    from anchored_fusion_amd.place import Placer
+    from oracle_backends import OracleAligner, oracle_searches
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-    searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference))
+    searches = oracle_searches(genome)
     pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out,
                  searches=searches, aligner_factory=OracleAligner, log=lambda *_: None)
 
@@ -95,14 +94,12 @@ def test_pipeline_filter_step_cpu_backends(tmp_path):
     Test_model) and Final_fusion writes the Natural_score layout; a missing model file gives the
     unfiltered tables, as in the reference."""
     import torch
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
+    from oracle_backends import OracleAligner, oracle_searches
     from anchored_fusion_amd import filter_model
     from anchored_fusion_amd.annotation import ExonIndex
-    from anchored_fusion_amd.place import Placer
     paths, truth = make_world(str(tmp_path / "world"))
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-    searches = pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference,
-                                                       tile_factory=OracleTileReference))
+    searches = oracle_searches(genome)
     kw = dict(searches=searches, aligner_factory=OracleAligner, log=lambda *_: None)
     base = str(tmp_path / "base")
     res = pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], base, **kw)

@@ -81,17 +81,15 @@ def test_singlecell_filter_model_cpu_backends(tmp_path):
     """singlecell.run with a filter model present (the default mode of SC:241-256): each cell's
     table has the Natural_score layout and the merge sums its span/split columns (SC:277-283)."""
     import torch
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
+    from oracle_backends import OracleAligner, oracle_searches
     from anchored_fusion_amd import filter_model
-    from anchored_fusion_amd.place import Placer
     paths, _ = make_world(str(tmp_path / "world"))
     fqd = str(tmp_path / "cells")
     cells = _split_cells(paths, fqd, n_cells=2)
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
 
     def searches():
-        return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference,
-                                                       tile_factory=OracleTileReference))
+        return oracle_searches(genome)
     torch.manual_seed(3)
     model = str(tmp_path / "model.pt")
     # the world's windows are 301 long (get_test_reads: 100 + left + 'H' + right + 100 pad)
@@ -157,12 +155,11 @@ def _run_and_compare(tmp_path, searches_factory, aligner_factory):
 
 
 def test_singlecell_cpu_backends(tmp_path):
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
-    from anchored_fusion_amd.place import Placer
+    from oracle_backends import OracleAligner, oracle_searches
 
     def searches(paths):
         genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-        return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference))
+        return oracle_searches(genome)
     _run_and_compare(tmp_path, searches, OracleAligner)
 
 
@@ -178,8 +175,7 @@ def test_singlecell_gpu(tmp_path):
 def test_singlecell_gpu_tables_equal_oracle(tmp_path):
     """Single-cell on the GPU (cells batched, one device call per cell) vs the same driver with
     the CPU-oracle backends: every per-cell table and both merged tables identical."""
-    from oracle_backends import OracleAligner, OracleReference, OracleTileReference
-    from anchored_fusion_amd.place import Placer
+    from oracle_backends import OracleAligner, oracle_searches
     paths, truth = make_world(str(tmp_path / "world"))
     fqd = str(tmp_path / "cells")
     cells = _split_cells(paths, fqd, n_cells=4)
@@ -188,7 +184,7 @@ def test_singlecell_gpu_tables_equal_oracle(tmp_path):
     singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], gpu, searches=pipeline.Searches(genome),
                    batch_pairs=1200, log=lambda *_: None)
     singlecell.run(paths["anchor"], fqd, paths["genome"], paths["gtf"], cpu,
-                   searches=pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference)),
+                   searches=oracle_searches(genome),
                    aligner_factory=OracleAligner, batch_pairs=1200, log=lambda *_: None)
     files = [os.path.join("BCRX", "work_dir", c, "BCRX_fusion_predictions" + x) for c in cells
              for x in (".txt", "_abridged.txt")]
