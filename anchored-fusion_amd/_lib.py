@@ -34,7 +34,7 @@ EXPORTS = (
     "af_ctx_create", "af_ctx_destroy", "af_last_error", "af_params_default", "af_pe_default", "af_index_build",
     "af_index_free", "af_index_anchor_len", "af_index_filter_words", "af_index_filter_table",
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
-    "af_last_candidates", "af_place", "af_place_device", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_index_build_genome", "af_index_build_genome_device", "af_gather_reads_device", "af_blat_params_default", "af_tile_index_build",
+    "af_last_candidates", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_gather_reads_device", "af_blat_params_default", "af_tile_index_build",
     "af_tile_index_build_device", "af_blat", "af_blat_device", "af_blat_device_range", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close", "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
@@ -96,10 +96,6 @@ def lib():
     L.af_params_default.restype = None
     L.af_index_build.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
     L.af_index_build.restype = ctypes.c_int
-    L.af_index_build_genome.argtypes = [_vp, ctypes.c_char_p, _i64, ctypes.POINTER(_vp)]
-    L.af_index_build_genome.restype = ctypes.c_int
-    L.af_index_build_genome_device.argtypes = [_vp, _vp, _i64, ctypes.POINTER(_vp)]
-    L.af_index_build_genome_device.restype = ctypes.c_int
     L.af_index_free.argtypes = [_vp]
     L.af_index_free.restype = None
     L.af_index_anchor_len.argtypes = [_vp]
@@ -125,10 +121,6 @@ def lib():
     L.af_seed_filter_device.restype = ctypes.c_int
     L.af_last_candidates.argtypes = [_vp]
     L.af_last_candidates.restype = _i64
-    L.af_place.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _i32, _vp, _vp]
-    L.af_place.restype = ctypes.c_int
-    L.af_place_device.argtypes = [_vp, _vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(Params), _i32, _vp, _vp, _vp]
-    L.af_place_device.restype = ctypes.c_int
     L.af_split_tails_device.argtypes = [_vp, _vp, _i64, _i32, _vp, ctypes.POINTER(AlnOut), _i32, _i64, _i32, _i64,
                                         _vp, _vp, _vp, _vp, _vp]
     L.af_split_tails_device.restype = ctypes.c_int

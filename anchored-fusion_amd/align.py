@@ -350,7 +350,7 @@ class AnchorAligner:
 
     @property
     def ctx(self):
-        """The raw af_ctx handle (e.g. for place.Reference.place_device on this slot's stream)."""
+        """The raw af_ctx handle (e.g. for a search on this slot's stream)."""
         return self._ctx
 
     def last_candidates(self):

@@ -9,15 +9,10 @@
 #define AF_SEED_BTILE 2048      // reads per workgroup tile in the seed filter
 #define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
 #define AF_SEED_GROUPS (AF_SEED_BTILE / 64)  // 64-read ballot groups per tile
-#define AF_ALN_WAVES 4          // waves per alignment workgroup
 #ifndef AF_K2_WPS
-#define AF_K2_WPS 6             // k_align waves per SIMD (launch bound; persistent slots = 4 x this per CU)
+#define AF_K2_WPS 6             // S2 K2 waves per SIMD (launch bound; persistent slots = 4 x this per CU)
 #endif
-#define AF_RESEED_STEP 4          // af_place: MEM minimum length step while a query has > max_mems MEMs
-#define AF_RESEED_MAX 64          // ... up to this minimum length (then the query is flagged n_hits = -1)
 #define AF_CPL 6                // DP columns per lane: 6*64 = 384 >= AF_MAX_READ+1
-#define AF_ZCAP 12288           // LDS traceback bytes per wave; larger DPs use global scratch
-#define AF_TMAX (AF_MAX_READ + 2 * 100 * 4 + 64)  // max target window held in LDS
 
 // Device view of an anchor index (all pointers are device memory).
 struct DevIndex {
@@ -29,11 +24,6 @@ struct DevIndex {
     const int4 *hslot;
     const int32_t *kpos;    // positions grouped by 16-mer, ascending
     const uint32_t *bloom;  // Bloom filter of the anchor 16-mers (2^bl_bits words, see af_k1_hash)
-    // direct (genome-scale) indexes instead of the hash: kend[k] = end of 16-mer k's run of
-    // forward-strand positions in kposu (4^16 entries; the run starts at kend[k - 1]).  Null
-    // for hash indexes.
-    const uint32_t *kend;
-    const uint32_t *kposu;
     int64_t n;              // anchor length
     int32_t hbits;          // log2 position-hash slots
     int32_t bl_bits;        // log2 Bloom words
@@ -145,14 +135,6 @@ struct S2Work {
     int32_t max_chunks;
     int32_t *heads_k2, *heads_k3;  // per-XCD dequeue heads (8 lines each)
     void *plan;         // per listed pair: the record choice of K3c for K3d (s2.hip S2Plan)
-};
-
-// Per-read result of the alignment kernel (candidates only), consumed by the pair kernel.
-struct ReadRec {
-    int32_t flag;    // 0x4 unmapped, 0x10 reverse, AF_FLAG_* overflow bits
-    int32_t pos;
-    int32_t score;
-    int32_t n_cigar;
 };
 
 // split-read tails output (af_split_tails_device / af_align_candidates_tails_device)
@@ -277,16 +259,6 @@ size_t af_seed_filter_lds(int bl_bits);
 hipError_t af_launch_seed_filter(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
                                  const int32_t *lens, int32_t *hits, int32_t *cand, int32_t *cnt, int32_t *cnt_next,
                                  int32_t *s2z, int n_cu, hipStream_t s);
-hipError_t af_launch_align(const DevIndex &ix, const uint8_t *reads, int64_t n_reads, int32_t stride,
-                           const int32_t *lens, const af_params &p, const int32_t *cand, const int32_t *n_cand,
-                           int32_t *heads, ReadRec *recs, uint32_t *cigar, uint8_t *zscratch, int32_t n_slots,
-                           hipStream_t s);
-hipError_t af_launch_pairs(int64_t n_pairs, const int32_t *hits, const ReadRec *recs, af_aln_out out,
-                           int32_t *ctrl, hipStream_t s, const uint8_t *reads = nullptr, int32_t stride = 0,
-                           const int32_t *lens = nullptr, const AfTails *tails = nullptr);
-hipError_t af_launch_place(const DevIndex &ix, const uint8_t *reads, const int32_t *n_queries, int32_t stride,
-                           const int32_t *lens, const af_params &p, int32_t *heads, uint8_t *zscratch,
-                           int32_t n_slots, af_hit *hits, int32_t *n_hits, int32_t max_hits, hipStream_t s);
 hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
                         const af_params &p, const S2Opt &o, const int32_t *hits, const int32_t *cand,
                         const int32_t *n_cand, const S2Work &w, af_aln_out out, uint8_t *zscratch, int32_t n_slots,
@@ -318,10 +290,6 @@ hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const 
 hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, DevTile *X, void **allocs, int *na,
                                hipStream_t s);
 hipError_t af_launch_clamp_count(const int32_t *count, int64_t cap, int32_t *dst, hipStream_t s);
-size_t af_genome_index_table_bytes();
-int af_genome_scan_blocks();
-hipError_t af_build_genome_index(const uint8_t *seq, int64_t n, uint8_t *D, uint32_t *D2, uint32_t *Dn,
-                                 uint32_t *S, uint32_t *kposu, uint32_t *scan_sums, int n_cu, hipStream_t s);
 // s3.hip: S3 (samtools sort + flag filters) on the device
 size_t af_s3_temp_bytes(int64_t n_reads);
 hipError_t af_launch_s3(const int32_t *flag, const int32_t *pos, int64_t n_reads, int64_t ref_len, uint64_t *keys,

@@ -23,7 +23,6 @@ struct af_ctx {
     int32_t *cand = nullptr;
     uint32_t *d_packed = nullptr;  // af_align_pairs: the candidates' CIGAR rows, gathered for one D2H
     int64_t cap_packed = 0;
-    ReadRec *recs = nullptr;
     int64_t cap_reads = 0;
     uint8_t *zscratch = nullptr;
     uint8_t *bscratch = nullptr;  // k_blat: AF_BLAT_SLOT_BYTES per resident wave (blat_slots)
@@ -58,11 +57,6 @@ struct af_ctx {
     void *g_temp = nullptr;
     int64_t g_cap = 0;
     size_t g_temp_bytes = 0;
-    // af_place staging (host-buffer API)
-    uint8_t *p_q = nullptr;
-    int32_t *p_lens = nullptr, *p_nhits = nullptr;
-    af_hit *p_hits = nullptr;
-    int64_t p_cap_bytes = 0, p_cap_q = 0, p_cap_hits = 0;
     // host-API staging (device)
     uint8_t *d_reads = nullptr;
     int64_t cap_bytes = 0;
@@ -216,11 +210,10 @@ int dev_upload(af_ctx *ctx, af_index *ix, const std::vector<T> &v, const T **out
 
 int ensure_reads_cap(af_ctx *c, int64_t n_reads) {
     if (n_reads <= c->cap_reads) return AF_OK;
-    af_free(c->cand); af_free(c->recs);
-    c->cand = nullptr; c->recs = nullptr; c->cap_reads = 0;
+    af_free(c->cand);
+    c->cand = nullptr; c->cap_reads = 0;
     const int64_t cap = std::max<int64_t>(n_reads, 1 << 16);
     HIPCHK(c, hipMalloc(&c->cand, sizeof(int32_t) * cap));
-    HIPCHK(c, hipMalloc(&c->recs, sizeof(ReadRec) * cap));
     c->cap_reads = cap;
     return AF_OK;
 }
@@ -533,8 +526,7 @@ int af_ctx_create(int device, af_ctx **out) {
 void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    af_free(c->ctrl); af_free(c->cand); af_free(c->recs); af_free(c->zscratch); af_free(c->bscratch); af_free(c->blat_ord_work); af_free(c->blat_order); af_free(c->blat_stage); af_free(c->blat_stage_n); af_free(c->d_packed);
-    af_free(c->p_q); af_free(c->p_lens); af_free(c->p_nhits); af_free(c->p_hits);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->zscratch); af_free(c->bscratch); af_free(c->blat_ord_work); af_free(c->blat_order); af_free(c->blat_stage); af_free(c->blat_stage_n); af_free(c->d_packed);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
     af_free(c->d_cigar);
@@ -648,70 +640,6 @@ int af_index_build(af_ctx *c, const char *anchor, int64_t len, af_index **out) {
     return AF_OK;
 }
 
-static int build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out, hipMemcpyKind kind) {
-    if (!c || !seq || !out) return fail(c, AF_E_INVALID, "null argument");
-    *out = nullptr;
-    if (len < AF_K) return fail(c, AF_E_INVALID, "reference shorter than %d", AF_K);
-    if (len >= (1LL << 32) - 1) return fail(c, AF_E_UNSUPPORTED, "reference of 2^32 bases or more");
-    (void)hipSetDevice(c->device);
-    af_index *ix = new (std::nothrow) af_index;
-    if (!ix) return fail(c, AF_E_NOMEM, "out of host memory");
-    ix->ctx = c;
-    const int64_t n = len, n2 = 2 * len;
-    const size_t d2w = (size_t)((n2 + 15) / 16 + 2), dnw = (size_t)((n2 + 31) / 32 + 2);
-    const size_t nq = (size_t)(n - AF_K + 1);
-    void *p_seq = nullptr, *p_D = nullptr, *p_D2 = nullptr, *p_Dn = nullptr, *p_S = nullptr, *p_pos = nullptr,
-         *p_sums = nullptr;
-    auto bail = [&](hipError_t e, const char *what) {
-        af_free(p_seq); af_free(p_sums);
-        af_index_free(ix);
-        return fail(c, AF_E_HIP, "af_index_build_genome: %s: %s", what, hipGetErrorString(e));
-    };
-    auto alloc = [&](void **pp, size_t bytes, bool keep) {
-        hipError_t e = hipMalloc(pp, std::max<size_t>(bytes, 16));
-        if (e == hipSuccess && keep) ix->allocs[ix->n_allocs++] = *pp;
-        return e;
-    };
-    hipError_t e;
-    if ((e = alloc(&p_seq, (size_t)n, false)) != hipSuccess) return bail(e, "hipMalloc(sequence)");
-    if ((e = alloc(&p_D, (size_t)n2, true)) != hipSuccess) return bail(e, "hipMalloc(D)");
-    if ((e = alloc(&p_D2, 4 * d2w, true)) != hipSuccess) return bail(e, "hipMalloc(D2)");
-    if ((e = alloc(&p_Dn, 4 * dnw, true)) != hipSuccess) return bail(e, "hipMalloc(Dn)");
-    if ((e = alloc(&p_S, af_genome_index_table_bytes(), true)) != hipSuccess) return bail(e, "hipMalloc(16-mer table)");
-    if ((e = alloc(&p_pos, 4 * nq, true)) != hipSuccess) return bail(e, "hipMalloc(positions)");
-    if ((e = alloc(&p_sums, 4 * (size_t)af_genome_scan_blocks(), false)) != hipSuccess) return bail(e, "hipMalloc(scan)");
-    if ((e = hipMemcpyAsync(p_seq, seq, (size_t)n, kind, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(p_D2, 0, 4 * d2w, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(p_Dn, 0, 4 * dnw, c->stream)) != hipSuccess)
-        return bail(e, "upload");
-    if ((e = af_build_genome_index(static_cast<const uint8_t *>(p_seq), n, static_cast<uint8_t *>(p_D),
-                                   static_cast<uint32_t *>(p_D2), static_cast<uint32_t *>(p_Dn),
-                                   static_cast<uint32_t *>(p_S), static_cast<uint32_t *>(p_pos),
-                                   static_cast<uint32_t *>(p_sums), c->n_cu, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return bail(e, "build kernels");
-    af_free(p_seq);
-    af_free(p_sums);
-    ix->dev.D = static_cast<const uint8_t *>(p_D);
-    ix->dev.D2 = static_cast<const uint32_t *>(p_D2);
-    ix->dev.Dn = static_cast<const uint32_t *>(p_Dn);
-    ix->dev.kend = static_cast<const uint32_t *>(p_S) + 1;
-    ix->dev.kposu = static_cast<const uint32_t *>(p_pos);
-    ix->dev.n = n;
-    ix->dev.hbits = 0;
-    ix->dev.bl_bits = -1;
-    *out = ix;
-    return AF_OK;
-}
-
-int af_index_build_genome(af_ctx *c, const char *seq, int64_t len, af_index **out) {
-    return build_genome(c, seq, len, out, hipMemcpyHostToDevice);
-}
-
-int af_index_build_genome_device(af_ctx *c, const char *d_seq, int64_t len, af_index **out) {
-    return build_genome(c, d_seq, len, out, hipMemcpyDeviceToDevice);
-}
-
 void af_index_free(af_index *ix) {
     if (!ix) return;
     if (ix->ctx) (void)hipSetDevice(ix->ctx->device);
@@ -733,7 +661,6 @@ int af_index_filter_table(const af_index *ix, uint32_t *out, int64_t cap) {
 
 int af_seed_filter_device(af_ctx *c, const af_index *ix, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
                           const int32_t *d_lens, int32_t *d_hits, void *stream) {
-    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || (!d_reads && n_reads) || !d_hits) return fail(c, AF_E_INVALID, "null argument");
     if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
@@ -804,7 +731,6 @@ int af_align_candidates_tails_device(af_ctx *c, const af_index *ix, const uint8_
 static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int64_t n_pairs, int32_t stride,
                             const int32_t *d_lens, const af_params *p, const af_pe *pe_in, af_aln_out *o, void *stream,
                             const AfTails *tails, bool append) {
-    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || !o) return fail(c, AF_E_INVALID, "null argument");
     int rc = check_params(c, p);
@@ -855,7 +781,6 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
 
 int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t n_pairs, int32_t stride,
                    const int32_t *lens, const af_params *p, const af_pe *pe, af_aln_out *out) {
-    if (ix && ix->dev.kend) return fail(c, AF_E_UNSUPPORTED, "a genome-scale index serves af_place only");
     if (ix && ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
     if (!c || !ix || !out || (!reads && n_pairs)) return fail(c, AF_E_INVALID, "null argument");
     if (n_pairs == 0) return AF_OK;
@@ -923,76 +848,6 @@ int af_align_pairs(af_ctx *c, const af_index *ix, const uint8_t *reads, int64_t 
                        rows.data() + (size_t)i * AF_MAX_CIGAR, sizeof(uint32_t) * AF_MAX_CIGAR);
         }
     }
-    return AF_OK;
-}
-
-int af_place(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_queries, int32_t stride,
-             const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits) {
-    static_assert(sizeof(af_hit) == 176, "af_hit layout is part of the C-ABI");
-    if (!c || !ix || !hits || !n_hits || (!queries && n_queries)) return fail(c, AF_E_INVALID, "null argument");
-    if (ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
-    int rc = check_params(c, p);
-    if (rc) return rc;
-    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
-    if (n_queries == 0) return AF_OK;
-    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
-    if (max_hits < 1 || max_hits > 16) return fail(c, AF_E_INVALID, "max_hits must be in [1, 16]");
-    if (lens)
-        for (int64_t i = 0; i < n_queries; ++i)
-            if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
-    (void)hipSetDevice(c->device);
-    if ((rc = ensure_zscratch(c))) return rc;
-    const int64_t bytes = n_queries * (int64_t)stride, nh = n_queries * (int64_t)max_hits;
-    if (bytes > c->p_cap_bytes) {
-        af_free(c->p_q); c->p_q = nullptr; c->p_cap_bytes = 0;
-        HIPCHK(c, hipMalloc(&c->p_q, bytes + 64));
-        c->p_cap_bytes = bytes;
-    }
-    if (n_queries > c->p_cap_q) {
-        af_free(c->p_lens); af_free(c->p_nhits); c->p_lens = c->p_nhits = nullptr; c->p_cap_q = 0;
-        HIPCHK(c, hipMalloc(&c->p_lens, 4 * n_queries + 64));
-        HIPCHK(c, hipMalloc(&c->p_nhits, 4 * n_queries + 64));
-        c->p_cap_q = n_queries;
-    }
-    if (nh > c->p_cap_hits) {
-        af_free(c->p_hits); c->p_hits = nullptr; c->p_cap_hits = 0;
-        HIPCHK(c, hipMalloc(&c->p_hits, sizeof(af_hit) * nh));
-        c->p_cap_hits = nh;
-    }
-    hipStream_t s = c->stream;
-    const int32_t nq = (int32_t)n_queries;
-    HIPCHK(c, hipMemcpyAsync(c->p_q, queries, bytes, hipMemcpyHostToDevice, s));
-    if (lens) HIPCHK(c, hipMemcpyAsync(c->p_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
-    HIPCHK(c, hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s));
-    HIPCHK(c, af_launch_place(ix->dev, c->p_q, c->ctrl + AF_CTRL_PLACE_N, stride, lens ? c->p_lens : nullptr, *p,
-                              c->ctrl + AF_CTRL_PLACE_HEADS, c->zscratch, c->n_slots, c->p_hits, c->p_nhits, max_hits,
-                              s));
-    HIPCHK(c, hipMemcpyAsync(hits, c->p_hits, sizeof(af_hit) * nh, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(n_hits, c->p_nhits, 4 * n_queries, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    return AF_OK;
-}
-
-int af_place_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
-                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_params *p, int32_t max_hits,
-                    af_hit *d_hits, int32_t *d_n_hits, void *stream) {
-    if (!c || !ix || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_hits || !d_n_hits)))
-        return fail(c, AF_E_INVALID, "null argument");
-    if (ix->is_tile) return fail(c, AF_E_UNSUPPORTED, "a tile index serves af_blat only");
-    int rc = check_params(c, p);
-    if (rc) return rc;
-    if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
-    if (stride <= 0 || stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "stride %d outside [1, %d]", stride, AF_MAX_READ);
-    if (max_hits < 1 || max_hits > 16) return fail(c, AF_E_INVALID, "max_hits must be in [1, 16]");
-    if (cap_queries == 0) return AF_OK;
-    (void)hipSetDevice(c->device);
-    if ((rc = ensure_zscratch(c))) return rc;
-    hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
-    HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
-    HIPCHK(c, af_launch_place(ix->dev, d_queries, c->ctrl + AF_CTRL_PLACE_N, stride, d_lens, *p,
-                              c->ctrl + AF_CTRL_PLACE_HEADS, c->zscratch, c->n_slots, d_hits, d_n_hits, max_hits, s));
     return AF_OK;
 }
 

@@ -138,7 +138,7 @@ def _mutate(rng, codes, d):
 
 class GenomeWorld:
     """The configs[2] world in HBM.  `blob` (torch uint8 tensor) is the joined genome (contigs with
-    place.SEP N's between them, the layout place.Reference indexes); `loci[name]` lists each embedded
+    place.SEP N's between them; the indexes read the contigs at `offsets`); `loci[name]` lists each embedded
     gene's exons as (contig, start, end) 0-based; `fusions` the fusion transcripts with their
     junctions (anchor exon end, partner exon start)."""
 
@@ -225,11 +225,6 @@ class GenomeWorld:
     def contig_list(self):
         """(name, length) per contig."""
         return list(zip(self.names, self.lens))
-
-    def reference(self):
-        """place.Reference over the genome in HBM (af_index_build_genome_device)."""
-        from . import place
-        return place.Reference.from_device(self.blob, self.names, self.lens, self.offsets, device=self.device)
 
     def genome_index(self):
         """genome.GenomeIndex (`bwa index`, csrc/fmindex.hip) over the contigs in HBM."""

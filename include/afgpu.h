@@ -13,9 +13,6 @@
  *   af_align_pairs_device <- same, device-resident buffers, enqueued on a HIP stream
  *   af_seed_filter_device <- the seeding pass of the same call (the HBM-bound kernel)
  *   af_align_candidates_device <- the extension/CIGAR/pairing pass of the same call
- *   af_place              <- the genome `bwa mem` calls (AF:188, functions.py:716) and the BLAT
- *                            calls (functions.py:341, 530, 1007, 1071, 1122, 1244)
- *   af_place_device       <- same, device-resident buffers and query count, on a HIP stream
  *   af_split_tails_device <- the split-read selection + query FASTA of the partner search
  *                            (functions.py:705-716, 1001-1005), from device-resident records
  *   af_align_candidates_tails_device <- af_align_candidates_device + the same tails, fused
@@ -28,7 +25,6 @@
  *   af_genome_align_pe(_device) <- `bwa mem -M -t T <genome> tmp1.fq tmp2.fq` (AF:188, S4): every
  *                            SAM record of every pair, as bwa prints them (Find_blocks input)
  *   af_genome_align_se(_device) <- `bwa mem -M -t T <genome> split_reads.fa` (functions.py:716, S5)
- *   af_index_build_genome <- the placement index of af_place (16-mer table; BLAT-side helper)
  *   af_tile_index_build / af_blat(_device) <- `blat [opts] target.fa query.fa out.psl`
  *                            (functions.py:341, 530, 966, 1007, 1071, 1122, 1244)
  *   af_fastq_*            <- the fq1/fq2 inputs of the AF:182 call (host-side reader)
@@ -104,20 +100,6 @@ typedef struct {
     int64_t pair_base;
 } af_pe;
 
-/* One placement of a query on a reference (af_place).  Replaces one PSL row of the
- * reference's BLAT searches (functions.py:341, 530, 1007, 1071, 1122, 1244) and one SAM record
- * of its genome `bwa mem` calls (Anchored_Fusion.py:188, functions.py:716). */
-typedef struct {
-    int32_t query;                  /* query index                                               */
-    int32_t flag;                   /* 0x10 reverse strand | AF_FLAG_CIGAR_OVERFLOW              */
-    int32_t score;                  /* local alignment score (bwa extension score)               */
-    int32_t q_start, q_end, q_size; /* forward query coordinates (PSL qStart, qEnd, qSize)       */
-    int32_t matches;                /* identical aligned bases (PSL matches)                     */
-    int32_t n_cigar;
-    int64_t t_start, t_end;         /* reference span, 0-based forward coordinates of the index  */
-    uint32_t cigar[AF_MAX_CIGAR];   /* SAM CIGAR with soft clips (reverse hits: revcomp query)   */
-} af_hit;
-
 int af_ctx_create(int device, af_ctx **out);
 void af_ctx_destroy(af_ctx *ctx);
 const char *af_last_error(const af_ctx *ctx);
@@ -157,36 +139,6 @@ int af_align_candidates_tails_device(af_ctx *ctx, const af_index *idx, const uin
 /* number of candidate reads found by the last seed-filter pass on this context (synchronises) */
 int64_t af_last_candidates(af_ctx *ctx);
 
-/* Genome-scale index for af_place (replaces `bwa index <genome>`, Anchored_Fusion.py:173-178, and
- * BLAT's per-call tile index): built on the GPU and HBM-resident (a direct table of all 4^16
- * 16-mers, 16 GiB, plus 4 B per forward position and 2.6 B per base of sequence).  References of
- * up to 2^32 - 2 bases (contigs joined by N runs); af_align_* reject it. */
-int af_index_build_genome(af_ctx *ctx, const char *seq, int64_t len, af_index **out);
-/* af_index_build_genome from a device-resident sequence (d_seq: `len` bytes of ASCII in HBM, e.g.
- * a genome generated or decompressed on the device); synchronous. */
-int af_index_build_genome_device(af_ctx *ctx, const char *d_seq, int64_t len, af_index **out);
-
-/* Multi-hit placement of queries (ASCII, `stride` bytes per row, optional lens) on an index
- * built with af_index_build over any reference (anchor, candidate blocks, or contigs joined by
- * N runs).  Every seed-extended region scoring >= p->T is reported, best score first, at most
- * max_hits (1..16) per query: hits[q * max_hits + k] for k < n_hits[q].  A query with more than
- * p->max_mems MEMs (random 16-mer hits on a genome-scale reference) is re-seeded with the
- * minimum MEM length raised by 4 until at most max_mems remain; past a minimum of 64,
- * n_hits[q] = -1.  Host buffers; synchronous.
- * Replaces: functions.py BLAT calls (fn:341, 530, 1007, 1071, 1122, 1244) and the genome
- * `bwa mem` calls (AF:188, fn:716). */
-int af_place(af_ctx *ctx, const af_index *idx, const uint8_t *queries, int64_t n_queries, int32_t stride,
-             const int32_t *lens, const af_params *p, int32_t max_hits, af_hit *hits, int32_t *n_hits);
-/* af_place with device buffers, asynchronous on `stream`: the query count is read on the
- * device from *d_n_queries (clamped to cap_queries, the rows d_queries / d_lens / d_n_hits hold;
- * d_hits holds cap_queries * max_hits), so it can follow af_split_tails_device without a host
- * round trip.  d_lens may be NULL (every query `stride` long); lengths above stride are read
- * as stride.  A context runs one placement or alignment at a time: its traceback scratch and
- * queue heads are shared, so calls on one context must be ordered on one stream (use one context
- * per concurrent stream). */
-int af_place_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
-                    int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_params *p, int32_t max_hits,
-                    af_hit *d_hits, int32_t *d_n_hits, void *stream);
 /* Split-read tails on the device, from the records of af_align_pairs_device /
  * af_align_candidates_device (d_out; device buffers, asynchronous on `stream`).  A split read is
  * a mapped read whose CIGAR is exactly M + S or S + M (deal_cigar's two-operation case,
@@ -196,7 +148,7 @@ int af_place_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, 
  * bytes past d_tail_lens[t] undefined), d_tail_lens[t], d_tail_read[t] = read_base + the read's
  * row; the number of split reads (which may exceed cap) goes to *d_n_tails, which is zeroed
  * first unless `append` is non-zero (then the tails add to those already there: several
- * batches, even on different streams, can fill one buffer for one af_place_device launch).
+ * batches, even on different streams, can fill one buffer for one af_blat_device launch).
  * Tail order varies between runs; d_tail_read identifies them.  Replaces the split-read
  * selection and FASTA writing of functions.py:705-716 and fn:1001-1005. */
 int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, int32_t stride,
@@ -284,8 +236,8 @@ int af_partition_device(af_ctx *ctx, const int32_t *d_flag, const int32_t *d_pos
  *                        for 0x10): the split-read FASTA of functions.py:705-716; list order kept.
  * Query k goes to slot first + k * step of d_q (`stride` bytes per row, N-padded), d_q_lens and
  * d_q_rows (the read row; may be NULL); slots at or past cap are dropped.  *d_n_q (may be NULL) =
- * min(cap, last slot written + 1, or `first` when no row is written): the query count
- * af_place_device reads when the calls fill slots 0.. in order.  d_out supplies FLAG and
+ * min(cap, last slot written + 1, or `first` when no row is written): the query count of the
+ * genome calls (af_genome_align_pe_device / _se_device) when the calls fill slots 0.. in order.  d_out supplies FLAG and
  * CIGAR (AF_GATHER_SPLIT_SAM only).  Asynchronous on `stream`. */
 #define AF_GATHER_SEQUENCED 0
 #define AF_GATHER_SPLIT_SAM 1

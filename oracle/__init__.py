@@ -58,9 +58,6 @@ def lib():
         L.afo_seed_filter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.c_void_p]
         L.afo_align_pairs.restype = ctypes.c_int
-        L.afo_place.restype = ctypes.c_int
-        L.afo_place.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
-                                ctypes.POINTER(Params), ctypes.c_int32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.afo_align_pairs.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                       ctypes.c_void_p, ctypes.POINTER(Params), ctypes.POINTER(Pe), ctypes.c_int,
                                       ctypes.POINTER(_Out)]
@@ -109,7 +106,7 @@ class OracleIndex:
                               None if lp is None else lp.ctypes.data, hits.ctypes.data)
         return hits
 
-    def align_pairs(self, reads, lens=None, params=None, threads=0, pe=None, pair_base=0, chunk_bases=None):
+    def align_pairs(self, reads, lens=None, params=None, threads=0, pe=None, pair_base=None, chunk_bases=None):
         """bwa mem -M paired-end restatement (bwa_pe.c).  reads: [2N, stride] uint8 pair-major,
         starting at a bwa chunk boundary; pair_base = global index of the first pair.
         Returns a dict of per-read arrays (one primary record per read)."""
@@ -121,7 +118,8 @@ class OracleIndex:
         o = _Out(*(out[k].ctypes.data for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
         p = params or default_params()
         e = pe or default_pe()
-        e.pair_base = int(pair_base)
+        if pair_base is not None:
+            e.pair_base = int(pair_base)
         if chunk_bases is not None:
             e.chunk_bases = int(chunk_bases)
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
@@ -132,24 +130,6 @@ class OracleIndex:
             raise RuntimeError(f"afo_align_pairs failed: {rc}")
         return out
 
-    def place(self, reads, lens=None, params=None, max_hits=16, threads=0):
-        """Multi-hit placement (afo_place): (hits [n, max_hits] structured, n_hits [n])."""
-        reads = np.ascontiguousarray(reads, dtype=np.uint8)
-        n = reads.shape[0]
-        hits = np.zeros((n, max_hits), dtype=HIT_DTYPE)
-        nh = np.zeros(n, dtype=np.int32)
-        p = params or default_params()
-        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
-        rc = lib().afo_place(self.h, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
-                             ctypes.byref(p), max_hits, int(threads), hits.ctypes.data, nh.ctypes.data)
-        if rc != 0:
-            raise RuntimeError(f"afo_place failed: {rc}")
-        return hits, nh
-
-
-HIT_DTYPE = np.dtype([("query", "<i4"), ("flag", "<i4"), ("score", "<i4"), ("q_start", "<i4"), ("q_end", "<i4"),
-                      ("q_size", "<i4"), ("matches", "<i4"), ("n_cigar", "<i4"), ("t_start", "<i8"),
-                      ("t_end", "<i8"), ("cigar", "<u4", (32,))])
 
 PSL_DTYPE = np.dtype([(n, "<i4") for n in (
     "query", "strand", "score", "matches", "mismatches", "n_count", "q_num_insert", "q_base_insert", "t_num_insert",
@@ -330,7 +310,7 @@ class OracleGenome:
             raise RuntimeError(f"afo_genome_align_se failed: {rc}")
         return recs, nrec
 
-    def align_pe(self, reads, lens=None, params=None, pe=None, pair_base=0, chunk_bases=None, threads=0,
+    def align_pe(self, reads, lens=None, params=None, pe=None, pair_base=None, chunk_bases=None, threads=0,
                  max_rec=G_MAX_REC):
         """S4 on pair-major reads [2N, stride]: (records [2N, max_rec] GREC_DTYPE, counts [2N])."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
@@ -339,7 +319,8 @@ class OracleGenome:
         recs = np.zeros((nr, max_rec), dtype=GREC_DTYPE)
         nrec = np.zeros(nr, dtype=np.int32)
         e = pe or default_pe()
-        e.pair_base = int(pair_base)
+        if pair_base is not None:
+            e.pair_base = int(pair_base)
         if chunk_bases is not None:
             e.chunk_bases = int(chunk_bases)
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)

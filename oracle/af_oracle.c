@@ -343,112 +343,6 @@ int afo_infer_bw(int l1, int l2, int score, int a, int q, int r) {
     return w;
 }
 
-typedef struct { int32_t qb, rb, len; } mem_t;
-typedef struct { int32_t score, truesc, qb, qe, rb, re, seedlen0, w; } reg_t;
-
-static int cmp_mem(const void *a, const void *b) {
-    const mem_t *x = (const mem_t *)a, *y = (const mem_t *)b;
-    if (x->len != y->len) return y->len - x->len;
-    if (x->qb != y->qb) return x->qb - y->qb;
-    return x->rb - y->rb;
-}
-
-typedef struct { int32_t flag, pos, score, n_cigar; uint32_t cigar[AFO_MAX_CIGAR]; } rec_t;
-
-#define FLAG_MEM_OVERFLOW 0x10000
-#define FLAG_CIGAR_OVERFLOW 0x20000
-
-static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_params *p, const reg_t *a,
-                        rec_t *out, int *matches, int *ref_span);
-
-/* MEM search on the doubled reference (SMEM seeding of bwa mem, restated as all MEMs
- * >= min_seed_len whose first 16-mer occurs <= max_occ times) */
-static int find_mems(const afo_index *I, const uint8_t *q, int l, const afo_params *p, mem_t *mems, int *overflow) {
-    int nm = 0;
-    int64_t n = I->n;
-    *overflow = 0;
-    for (int qb = 0; qb + AFO_K <= l; ++qb) {
-        uint32_t k;
-        if (!pack16(q + qb, &k)) continue;
-        /* equal range of k in sorted kmer[] */
-        int64_t lo = 0, hi = I->nk;
-        while (lo < hi) { int64_t mid = (lo + hi) >> 1; if (I->kmer[mid] < k) lo = mid + 1; else hi = mid; }
-        int64_t e = lo;
-        while (e < I->nk && I->kmer[e] == k) ++e;
-        int64_t cnt = e - lo;
-        if (cnt == 0 || cnt > p->max_occ) continue;
-        for (int64_t x = lo; x < e; ++x) {
-            int64_t rb = I->kpos[x];
-            if (qb > 0 && rb != 0 && rb != n && q[qb - 1] < 4 && q[qb - 1] == I->D[rb - 1]) continue;
-            int64_t lim = rb < n ? n : 2 * n;
-            int len = AFO_K;
-            while (qb + len < l && rb + len < lim && q[qb + len] < 4 && q[qb + len] == I->D[rb + len]) ++len;
-            if (len < p->min_seed_len) continue;
-            if (nm >= p->max_mems) { *overflow = 1; return nm; }
-            mems[nm].qb = qb; mems[nm].rb = (int32_t)rb; mems[nm].len = len;
-            ++nm;
-        }
-    }
-    return nm;
-}
-
-/* mem_chain2aln restated for a single-seed chain */
-static void extend_seed(const afo_index *I, const uint8_t *q, int l, const mem_t *s, const afo_params *p, reg_t *a) {
-    int64_t n2 = 2 * I->n;
-    int64_t b = s->rb - (s->qb + afo_cal_max_gap(p, s->qb));
-    int rem = l - s->qb - s->len;
-    int64_t e = s->rb + s->len + (rem + afo_cal_max_gap(p, rem));
-    int64_t rmax0 = b > 0 ? b : 0, rmax1 = e < n2 ? e : n2;
-    if (rmax0 < I->n && I->n < rmax1) {
-        if (s->rb < I->n) rmax1 = I->n; else rmax0 = I->n;
-    }
-    const uint8_t *rseq = I->D + rmax0;
-    int aw0 = p->w, aw1 = p->w;
-    int qle, tle, gtle, gscore, max_off;
-    memset(a, 0, sizeof(*a));
-    if (s->qb) {
-        uint8_t qs[AFO_MAX_READ], rs[2 * AFO_MAX_READ + 512];
-        int tmp = (int)(s->rb - rmax0);
-        for (int i = 0; i < s->qb; ++i) qs[i] = q[s->qb - 1 - i];
-        for (int i = 0; i < tmp; ++i) rs[i] = rseq[tmp - 1 - i];
-        for (int it = 0; it < 2; ++it) {
-            int prev = a->score;
-            aw0 = p->w << it;
-            a->score = afo_ext_dp(s->qb, qs, tmp, rs, p, aw0, p->pen_clip5, p->zdrop, s->len * p->a, &qle, &tle,
-                              &gtle, &gscore, &max_off);
-            if (a->score == prev || max_off < (aw0 >> 1) + (aw0 >> 2)) break;
-        }
-        if (gscore <= 0 || gscore <= a->score - p->pen_clip5) {
-            a->qb = s->qb - qle; a->rb = s->rb - tle; a->truesc = a->score;
-        } else {
-            a->qb = 0; a->rb = s->rb - gtle; a->truesc = gscore;
-        }
-    } else {
-        a->score = a->truesc = s->len * p->a; a->qb = 0; a->rb = s->rb;
-    }
-    if (s->qb + s->len != l) {
-        int qe = s->qb + s->len;
-        int re = (int)(s->rb + s->len - rmax0);
-        int sc0 = a->score;
-        for (int it = 0; it < 2; ++it) {
-            int prev = a->score;
-            aw1 = p->w << it;
-            a->score = afo_ext_dp(l - qe, q + qe, (int)(rmax1 - rmax0 - re), rseq + re, p, aw1, p->pen_clip3, p->zdrop,
-                              sc0, &qle, &tle, &gtle, &gscore, &max_off);
-            if (a->score == prev || max_off < (aw1 >> 1) + (aw1 >> 2)) break;
-        }
-        if (gscore <= 0 || gscore <= a->score - p->pen_clip3) {
-            a->qe = qe + qle; a->re = (int32_t)(rmax0 + re + tle); a->truesc += a->score - sc0;
-        } else {
-            a->qe = l; a->re = (int32_t)(rmax0 + re + gtle); a->truesc += gscore - sc0;
-        }
-    } else {
-        a->qe = l; a->re = s->rb + s->len;
-    }
-    a->seedlen0 = s->len;
-    a->w = aw0 > aw1 ? aw0 : aw1;
-}
-
 /* bwa_gen_cigar2 restated; query/ref segments in forward-reference orientation */
 int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
                   int64_t rb, int64_t re, uint32_t *cig, int *n_cig) {
@@ -480,161 +374,3 @@ int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, i
     return score;
 }
 
-/* seeds -> extended regions for one read (the body of mem_align1_core restated for one
- * anchor-like reference); returns n_reg, -1 on MEM overflow.  q: the read's codes. */
-static int read_regions(const afo_index *I, const uint8_t *ascii, int l, const afo_params *p, uint8_t *q,
-                        reg_t *regs, int reseed) {
-    mem_t *mems = (mem_t *)malloc(sizeof(mem_t) * (p->max_mems > 0 ? p->max_mems : 1));
-    int n_reg = 0, overflow = 0;
-    for (int i = 0; i < l; ++i) q[i] = afo_nt4(ascii[i]);
-    /* placement (reseed): while more than max_mems MEMs, raise the minimum MEM length by
-     * AFO_RESEED_STEP up to AFO_RESEED_MAX (the GPU's AF_RESEED_STEP / AF_RESEED_MAX) */
-    afo_params ps = *p;
-    int nm;
-    for (;;) {
-        nm = find_mems(I, q, l, &ps, mems, &overflow);
-        if (!overflow || !reseed || ps.min_seed_len + AFO_RESEED_STEP > AFO_RESEED_MAX) break;
-        ps.min_seed_len += AFO_RESEED_STEP;
-    }
-    if (overflow) { free(mems); return -1; }
-    qsort(mems, nm, sizeof(mem_t), cmp_mem);
-    int max_ext = p->max_ext < 64 ? p->max_ext : 64;
-    for (int si = 0; si < nm; ++si) {
-        const mem_t *s = &mems[si];
-        int skip = 0;
-        for (int r = 0; r < n_reg; ++r) {
-            const reg_t *a = &regs[r];
-            if (s->rb < a->rb || s->rb + s->len > a->re || s->qb < a->qb || s->qb + s->len > a->qe) continue;
-            if (10 * (s->len - a->seedlen0) > l) continue;
-            int qd = s->qb - a->qb, rd = s->rb - a->rb;
-            int mg = afo_cal_max_gap(p, qd < rd ? qd : rd);
-            int ww = mg < a->w ? mg : a->w;
-            if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
-            qd = a->qe - (s->qb + s->len); rd = a->re - (s->rb + s->len);
-            mg = afo_cal_max_gap(p, qd < rd ? qd : rd);
-            ww = mg < a->w ? mg : a->w;
-            if (qd - rd < ww && rd - qd < ww) { skip = 1; break; }
-        }
-        if (skip) continue;
-        if (n_reg >= max_ext) break;
-        extend_seed(I, q, l, s, p, &regs[n_reg++]);
-    }
-    free(mems);
-    return n_reg;
-}
-
-/* CIGAR and record of one region (the tail of align_read, shared with afo_place).  *matches
- * (optional) = identical aligned bases; *ref_span (optional) = reference bases covered. */
-static void emit_region(const afo_index *I, const uint8_t *q, int l, const afo_params *p, const reg_t *a,
-                        rec_t *out, int *matches, int *ref_span) {
-    int is_rev = a->rb >= I->n;
-    /* forward-read segment; gen_cigar reverses it together with the revcomp-reference
-     * segment for reverse hits (bwa_gen_cigar2), i.e. aligns in forward-ref order */
-    const uint8_t *qseg = q + a->qb;
-    int lq = a->qe - a->qb;
-    int tmp_w = afo_infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_del, p->e_del);
-    int w2 = afo_infer_bw(lq, a->re - a->rb, a->truesc, p->a, p->o_ins, p->e_ins);
-    w2 = w2 > tmp_w ? w2 : tmp_w;
-    if (w2 > p->w) w2 = w2 < a->w ? w2 : a->w;
-    uint32_t cig[AFO_MAX_CIGAR];
-    int nc = 0, score = 0, last_sc = -(1 << 30), it = 0;
-    do {
-        w2 = w2 < p->w << 2 ? w2 : p->w << 2;
-        score = afo_gen_cigar(I->D, I->n, p, w2, lq, qseg, a->rb, a->re, cig, &nc);
-        if (score == last_sc || w2 == p->w << 2) break;
-        last_sc = score;
-        w2 <<= 1;
-    } while (++it < 3 && score < a->truesc - p->a);
-    if (matches || ref_span) {
-        /* walk the alignment in forward-reference orientation (as gen_cigar aligned it) */
-        int mt = 0, x = 0, y = 0, rs = 0;
-        int ncap0 = nc < AFO_MAX_CIGAR ? nc : AFO_MAX_CIGAR;
-        for (int k = 0; k < ncap0; ++k) {
-            int len = (int)(cig[k] >> 4), op = (int)(cig[k] & 0xf);
-            if (op == 0) {
-                for (int u = 0; u < len; ++u) {
-                    int qx = is_rev ? qseg[lq - 1 - (x + u)] : qseg[x + u];
-                    int64_t ty = is_rev ? a->re - 1 - (y + u) : a->rb + y + u;
-                    if (qx < 4 && qx == I->D[ty]) ++mt;
-                }
-                x += len; y += len; rs += len;
-            } else if (op == 1) {
-                x += len;
-            } else {
-                y += len; rs += len;
-            }
-        }
-        if (ncap0 > 0 && (cig[0] & 0xf) == 2) rs -= (int)(cig[0] >> 4);
-        else if (ncap0 > 0 && (cig[ncap0 - 1] & 0xf) == 2) rs -= (int)(cig[ncap0 - 1] >> 4);
-        if (matches) *matches = mt;
-        if (ref_span) *ref_span = rs;
-    }
-    int64_t pos = is_rev ? 2 * I->n - a->re : a->rb;
-    int ncap = nc < AFO_MAX_CIGAR ? nc : AFO_MAX_CIGAR;
-    int of = nc > AFO_MAX_CIGAR;
-    /* squeeze out a leading or trailing deletion */
-    if (ncap > 0) {
-        if ((cig[0] & 0xf) == 2) {
-            pos += cig[0] >> 4;
-            memmove(cig, cig + 1, sizeof(uint32_t) * (ncap - 1));
-            --ncap;
-        } else if ((cig[ncap - 1] & 0xf) == 2) {
-            --ncap;
-        }
-    }
-    int clip5 = is_rev ? l - a->qe : a->qb;
-    int clip3 = is_rev ? a->qb : l - a->qe;
-    uint32_t fin[AFO_MAX_CIGAR + 2];
-    int nf = 0;
-    if (clip5) fin[nf++] = (uint32_t)clip5 << 4 | 4;
-    for (int x = 0; x < ncap; ++x) fin[nf++] = cig[x];
-    if (clip3) fin[nf++] = (uint32_t)clip3 << 4 | 4;
-    if (nf > AFO_MAX_CIGAR) { of = 1; nf = AFO_MAX_CIGAR; }
-    memcpy(out->cigar, fin, sizeof(uint32_t) * nf);
-    out->n_cigar = nf;
-    out->flag = (is_rev ? 0x10 : 0) | (of ? FLAG_CIGAR_OVERFLOW : 0);
-    out->pos = (int32_t)pos;
-    out->score = a->score;
-}
-
-/* Multi-hit placement (the searches behind S4-S8: every region of a query scoring >= T, best
- * score first, ties in region order, at most max_hits; each with its CIGAR as for a primary). */
-int afo_place(const afo_index *I, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,
-              const afo_params *p, int32_t max_hits, int n_threads, afo_hit *hits, int32_t *n_hits) {
-    if (max_hits < 1 || max_hits > 16) return -1;
-#ifdef _OPENMP
-    if (n_threads > 0) omp_set_num_threads(n_threads);
-#pragma omp parallel for schedule(dynamic, 16)
-#endif
-    for (int64_t r = 0; r < n_queries; ++r) {
-        uint8_t q[AFO_MAX_READ];
-        reg_t regs[64];
-        int l = lens ? lens[r] : stride;
-        if (l > AFO_MAX_READ) l = AFO_MAX_READ;
-        int n_reg = read_regions(I, reads + r * (int64_t)stride, l, p, q, regs, 1);
-        int nh = 0;
-        if (n_reg < 0) { n_hits[r] = -1; continue; }
-        int order[64];
-        for (int k = 0; k < n_reg; ++k) {   /* rank: score desc, then region order */
-            int rank = 0;
-            for (int u = 0; u < n_reg; ++u)
-                rank += regs[u].score > regs[k].score || (regs[u].score == regs[k].score && u < k);
-            order[rank] = k;
-        }
-        for (int k = 0; k < n_reg && nh < max_hits; ++k) {
-            const reg_t *a = &regs[order[k]];
-            if (a->score < p->T) break;
-            rec_t rec;
-            int mt = 0, rs = 0;
-            emit_region(I, q, l, p, a, &rec, &mt, &rs);
-            afo_hit *h = &hits[r * max_hits + nh];
-            h->query = (int32_t)r; h->flag = rec.flag; h->score = rec.score;
-            h->q_start = a->qb; h->q_end = a->qe; h->q_size = l; h->matches = mt;
-            h->t_start = rec.pos; h->t_end = rec.pos + rs; h->n_cigar = rec.n_cigar;
-            for (int c = 0; c < AFO_MAX_CIGAR; ++c) h->cigar[c] = c < rec.n_cigar ? rec.cigar[c] : 0;
-            ++nh;
-        }
-        n_hits[r] = nh;
-    }
-    return 0;
-}

@@ -13,9 +13,8 @@
  * third pass, chaining and the chain filter, seed extension, dedup/patch, insert-size
  * estimation per chunk, mate rescue (ksw_align2), -M primary marking with bwa's hash
  * tie-break, pair selection, and the record/flag rules of mem_aln2sam.
- * afo_place (af_oracle.c) is the multi-hit placement behind the genome/BLAT searches:
- * MEM seeds >= 19 nt on the doubled reference (anchor ++ revcomp), per-seed banded
- * extension with z-drop and clipping penalty, band inference + global DP for CIGAR.
+ * The same restatement runs the genome calls S4 / S5 (bwa_pe.c, afo_genome_*: bwa index of a
+ * multi-contig genome with an FM index, bwt_smem1 / bwt_seed_strategy1 / bwt_sa).
  * Parity with the bwa binary itself is UNPINNED; the oracle is
  * pinned by the wgsim truth in the bundled test FASTQ names and the junction known-answers.
  */
@@ -27,8 +26,6 @@ extern "C" {
 #endif
 
 #define AFO_K 16
-#define AFO_RESEED_STEP 4 /* afo_place: minimum MEM length step while a query has > max_mems MEMs */
-#define AFO_RESEED_MAX 64
 #define AFO_MAX_CIGAR 32
 #define AFO_MAX_READ 512
 
@@ -49,15 +46,6 @@ typedef struct {
     int32_t *flag, *pos, *score, *n_cigar, *hits;
     uint32_t *cigar; /* [n_reads * AFO_MAX_CIGAR], BAM op encoding len<<4|op */
 } afo_out;
-
-typedef struct {
-    int32_t query, flag, score;
-    int32_t q_start, q_end, q_size;   /* forward query coordinates (PSL qStart/qEnd/qSize)      */
-    int32_t matches;                  /* identical aligned bases                                 */
-    int32_t n_cigar;
-    int64_t t_start, t_end;           /* forward reference coordinates of the aligned span       */
-    uint32_t cigar[AFO_MAX_CIGAR];    /* SAM-orientation CIGAR with soft clips (as for a primary) */
-} afo_hit;
 
 typedef struct afo_index afo_index;
 
@@ -142,10 +130,6 @@ void afo_seed_filter(const afo_index *idx, const uint8_t *reads, int64_t n_reads
 void afo_pe_default(afo_pe *pe);
 int afo_align_pairs(const afo_index *idx, const uint8_t *reads, int64_t n_pairs, int32_t stride,
                     const int32_t *lens, const afo_params *p, const afo_pe *pe, int n_threads, afo_out *out);
-
-/* multi-hit placement: hits[r * max_hits + k], n_hits[r] (-1 = MEM overflow) */
-int afo_place(const afo_index *idx, const uint8_t *reads, int64_t n_queries, int32_t stride, const int32_t *lens,
-              const afo_params *p, int32_t max_hits, int n_threads, afo_hit *hits, int32_t *n_hits);
 
 /* BLAT restatement (blat.c): tile index, options, PSL rows (layout of af_psl, afgpu.h) */
 #define AFO_PSL_MAX_BLOCKS 16

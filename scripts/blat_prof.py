@@ -20,7 +20,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 8_000_160
 out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/blat_prof.json"
 anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
 W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=1.0)
-ref, tiles = W.reference(), W.tiles()
+ref, tiles = W.genome_index(), W.tiles()
 reads = W.simulate_pairs(N, read_len=150, seed=20251015)
 L = _lib.lib()
 assert L.af_debug_blat_prof_enable() == 16

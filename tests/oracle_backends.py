@@ -11,35 +11,6 @@ from anchored_fusion_amd.align import AlignResult
 from anchored_fusion_amd.place import concat_contigs, pack_queries
 
 
-class OracleReference:
-    def __init__(self, contigs):
-        self.names = [n for n, _ in contigs]
-        self.lens = [len(s) for _, s in contigs]
-        blob, self.offsets = concat_contigs(contigs)
-        self.total = len(blob)
-        self.ix = oracle.OracleIndex(blob)
-
-    def raw_hits(self, seqs, params=None, max_hits=16):
-        buf, lens = pack_queries(seqs)
-        p = oracle.default_params()
-        if params is not None:
-            for f, _ in p._fields_:
-                setattr(p, f, getattr(params, f))
-        return self.ix.place(buf, lens, p, max_hits, threads=8)
-
-    def locate(self, t_start, t_end):
-        k = bisect.bisect_right(self.offsets, int(t_start)) - 1
-        if k < 0:
-            return None
-        s, e = int(t_start) - self.offsets[k], int(t_end) - self.offsets[k]
-        if s < 0 or e > self.lens[k] or e <= s:
-            return None
-        return k, s, e
-
-    def close(self):
-        pass
-
-
 class OracleTileReference:
     """The BLAT restatement's CPU contract (oracle/blat.c) behind Placer's tile_factory."""
 
@@ -56,7 +27,14 @@ class OracleTileReference:
         op = oracle.blat_params(**{f: getattr(p, f) for f, _ in p._fields_})
         return self.tiles.blat(buf, lens, op, max_rows, threads=8)
 
-    locate = OracleReference.locate
+    def locate(self, t_start, t_end):
+        k = bisect.bisect_right(self.offsets, int(t_start)) - 1
+        if k < 0:
+            return None
+        s, e = int(t_start) - self.offsets[k], int(t_end) - self.offsets[k]
+        if s < 0 or e > self.lens[k] or e <= s:
+            return None
+        return k, s, e
 
     def close(self):
         pass
@@ -101,7 +79,7 @@ def oracle_searches(genome, chunk_bases=10_000_000):
     """pipeline.Searches with every service on the CPU oracles."""
     from anchored_fusion_amd import pipeline
     from anchored_fusion_amd.place import Placer
-    return pipeline.Searches(genome, placer=Placer(reference_factory=OracleReference, tile_factory=OracleTileReference),
+    return pipeline.Searches(genome, placer=Placer(tile_factory=OracleTileReference),
                              chunk_bases=chunk_bases, genome_factory=OracleGenomeIndex)
 
 

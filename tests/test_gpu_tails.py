@@ -1,8 +1,7 @@
-"""Device-side partner placement (af_split_tails_device -> af_place_device), the bench's
-S2 + placement step: the tails equal a host restatement of the split-read rule over the same
-records (deal_cigar's two-operation M/S case, functions.py:713; SAM-orientation clipped part,
-fn:1001-1005), and the device placements equal af_place's host API on the same tails, which
-tests/test_gpu_place.py pins against the oracle.  Integer work: bit-exact."""
+"""Split-read tails on the device (af_split_tails_device, and fused into K3 by
+af_align_candidates_tails_device), the queries of the S6 BLAT: the tails equal a host
+restatement of the split-read rule over the same records (deal_cigar's two-operation M/S case,
+functions.py:713; SAM-orientation clipped part, fn:1001-1005).  Integer work: bit-exact."""
 import numpy as np
 import pytest
 
@@ -99,46 +98,6 @@ def test_split_tails_capacity(aligner, anchor):
         assert t[i, :ln[i]].tobytes() == want[int(rd[i])]
 
 
-def test_place_device_matches_host_api(aligner, anchor):
-    import torch
-    from anchored_fusion_amd import place
-    dev = torch.device("cuda:0")
-    reads, _, world = synthetic_pairs(anchor, 4000, 100, seed=54)
-    rng = np.random.default_rng(55)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    ctgs = [("anchor", anchor.decode())] + [(f"p{k}", s.decode()) for k, s in enumerate(world["partners"])]
-    ctgs += [(f"r{k}", acgt[rng.integers(0, 4, 200_000)].tobytes().decode()) for k in range(3)]
-    ref = place.Reference(ctgs)
-    try:
-        rt, lt, out = _device_records(aligner, reads, None, dev)
-        cap = 4096
-        tails, tl, tr, nt = _tails(aligner, rt, lt, out, reads.shape[1], cap, 20, dev)
-        hits_t = torch.zeros(cap * 16 * place.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        nh_t = torch.zeros(cap, dtype=torch.int32, device=dev)
-        ref.place_device(tails, nt, reads.shape[1], hits_t, nh_t, lens_t=tl)
-        torch.cuda.synchronize()
-        n = int(nt.item())
-        assert 20 < n <= cap
-        t, ln = tails.cpu().numpy(), tl.cpu().numpy()
-        queries = [t[i, :ln[i]].tobytes() for i in range(n)]
-        hits_h, nh_h = ref.raw_hits(queries)
-        hits_d = hits_t.cpu().numpy().view(place.HIT_DTYPE).reshape(cap, 16)
-        nh_d = nh_t.cpu().numpy()
-        assert np.array_equal(nh_d[:n], nh_h)
-        for q in range(n):
-            for k in range(nh_h[q]):
-                a, b = hits_d[q, k], hits_h[q, k]
-                for f in ("flag", "score", "q_start", "q_end", "q_size", "matches", "n_cigar", "t_start", "t_end"):
-                    assert a[f] == b[f], (q, k, f)
-                assert np.array_equal(a["cigar"][:a["n_cigar"]], b["cigar"][:b["n_cigar"]])
-        # placed tails (score >= T = 30: tails of 30+ bases) land on a partner or the anchor
-        placed = [q for q in range(n) if nh_h[q] > 0]
-        on = sum(1 for q in placed if ref.names[ref.locate(hits_h[q, 0]["t_start"], hits_h[q, 0]["t_end"])[0]][0] in "ap")
-        assert len(placed) > 10 and on == len(placed)
-    finally:
-        ref.close()
-
-
 def test_fused_tails_and_append(aligner, anchor):
     """af_align_candidates_tails_device (tails cut in K3) gives the same tails as the host rule;
     two batches appended into one buffer keep their read_base offsets."""
@@ -165,35 +124,3 @@ def test_fused_tails_and_append(aligner, anchor):
     assert n == len(want)
     t, ln, rd = tb["tails"].cpu().numpy(), tb["lens"].cpu().numpy(), tb["read"].cpu().numpy()
     assert {int(rd[i]): t[i, :ln[i]].tobytes() for i in range(n)} == want
-
-
-def test_place_device_clamps_count(anchor):
-    """A device query count above cap_queries is clamped: the rows [0, cap) are placed as by
-    the host API and nothing past the buffers is read or written."""
-    import torch
-    from anchored_fusion_amd import place
-    from place_cases import contigs, queries
-    dev = torch.device("cuda:0")
-    ctgs = contigs(seed=71)
-    seqs = [q for _, q, _ in queries(ctgs, 300, seed=72, lens=(60, 100))]
-    ref = place.Reference(ctgs)
-    try:
-        cap, stride, mh = 200, 100, 4
-        buf, ln = place.pack_queries(seqs[:cap])
-        q = torch.zeros((cap, stride), dtype=torch.uint8, device=dev)
-        q[:, :buf.shape[1]] = torch.from_numpy(buf).to(dev)
-        lt = torch.from_numpy(ln).to(dev)
-        n_t = torch.tensor([cap + 100], dtype=torch.int32, device=dev)
-        hits = torch.zeros((cap + 8) * mh * place.HIT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        nh = torch.full((cap + 8,), -7, dtype=torch.int32, device=dev)
-        ref.place_device(q, n_t, stride, hits, nh, lens_t=lt, max_hits=mh)
-        torch.cuda.synchronize()
-        hh, nhh = ref.raw_hits(seqs[:cap], max_hits=mh)
-        nd = nh.cpu().numpy()
-        assert np.array_equal(nd[:cap], nhh) and (nd[cap:] == -7).all()
-        hd = hits.cpu().numpy().view(place.HIT_DTYPE).reshape(cap + 8, mh)
-        for i in range(cap):
-            for k in range(nhh[i]):
-                assert hd[i, k]["t_start"] == hh[i, k]["t_start"] and hd[i, k]["score"] == hh[i, k]["score"]
-    finally:
-        ref.close()
