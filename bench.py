@@ -326,6 +326,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     W = simworld.GenomeWorld(anchor, device=gpu, seed=20251015, scale=args.genome_scale)
     t_gen = time.perf_counter() - t0
     log(f"genome {W.total / 1e9:.2f} Gbp made in {t_gen:.1f} s")
+    subset = genome_subset(W) if rank == 0 and world == 1 and not args.no_cpu else None
     t0 = time.perf_counter()
     ref = W.genome_index()
     torch.cuda.synchronize(dev)
@@ -444,7 +445,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     if issue:
         res["issue_roofline"] = issue
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline_c3(anchor, reads_t, args)
+        res["cpu_baseline"] = cpu_baseline_c3(anchor, reads_t, args, subset)
     if rank == 0:
         print(json.dumps(res), flush=True)
     disc.close()
@@ -452,32 +453,110 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     tiles.close()
 
 
-def cpu_baseline_c3(anchor, reads_t, args):
-    """The CPU oracle on a bounded sample of the same pairs: S2 (oracle/bwa_pe.c, bwa-mem PE
-    restated) + S3 (samtools order and filters), repeated for --cpu-seconds.  The genome searches
-    are not in this leg: an oracle index of the 3.1 Gbp genome takes longer to build than the whole
-    bench runs."""
+def genome_subset(W, flank=1_000_000):
+    """The CPU baseline's genome: a window of each embedded gene's locus +- flank (host copies,
+    taken before the bench frees the world's blob).  The step's S4/S5 queries and S6 tails come
+    from these loci (anchor reads, their mates in the partner genes or the anchor's introns)."""
+    spans = {}
+    for name, ex in W.loci.items():
+        c = ex[0][0]
+        a, b = min(s for _, s, _ in ex), max(e for _, _, e in ex)
+        spans.setdefault(c, []).append((max(0, a - flank), min(W.lens[W.names.index(c)], b + flank)))
+    out = []
+    for c, iv in spans.items():
+        iv.sort()
+        merged = [list(iv[0])]
+        for a, b in iv[1:]:
+            if a <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], b)
+            else:
+                merged.append([a, b])
+        off = W.offsets[W.names.index(c)]
+        for a, b in merged:
+            out.append((f"{c}:{a}-{b}", W.blob[off + a:off + b].cpu().numpy().tobytes()))
+    return out
+
+
+def _host_queries(sample, rec, res, partition):
+    """S3's lists of the sample and the genome searches' queries, as the device gathers make them
+    (af_gather_reads_device): S4 tmp1 / tmp2 interleaved as sequenced, S5 the anchored reads whose
+    CIGAR deal_cigar reduces to two operations in SAM orientation, S6 the split-read tails."""
+    import numpy as np
+
+    from anchored_fusion_amd.cigar import normalize
+    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+    t1, t2, an = partition(res)
+    npair = min(len(t1), len(t2))
+    s4 = np.empty((2 * npair, sample.shape[1]), np.uint8)
+    s4[0::2], s4[1::2] = sample[t1[:npair]], sample[t2[:npair]]
+    s5 = []
+    for r in an:
+        s = sample[r].tobytes()
+        if len(normalize(res.cigar_str(r), s.decode())[0]) == 2:
+            s5.append(s[::-1].translate(comp) if rec["flag"][r] & 0x10 else s)
+    return s4, s5, _split_tails(sample, rec, Placement.MIN_CLIP)
+
+
+def cpu_baseline_c3(anchor, reads_t, args, subset):
+    """The CPU oracle on a bounded sample of the same pairs, over the stages of the GPU step: S2
+    (oracle/bwa_pe.c, bwa-mem PE restated) + S3 (samtools order and filters) + the queries'
+    gathers + S4 / S5 (the same restatement's genome calls, FM index) + S6 (oracle/blat.c,
+    -minScore=20, 11-mer tiles), repeated for --cpu-seconds.  The genome of S4/S5/S6 is `subset`
+    (genome_subset: the gene loci +- 1 Mb) -- an oracle index of the whole 3.1 Gbp takes longer to
+    build than the bench runs."""
     import numpy as np
 
     import oracle
+    from anchored_fusion_amd import place
     from anchored_fusion_amd.align import AlignResult, partition
     threads = cpu_threads(args)
     n = min(args.cpu_sample, reads_t.shape[0] // 2)
     sample = reads_t[: 2 * n].cpu().numpy()
     ix = oracle.OracleIndex(anchor)
+    t0 = time.perf_counter()
+    og = oracle.OracleGenome(subset)
+    blob, _ = place.concat_contigs([(nm, sq.decode()) for nm, sq in subset])
+    tiles = oracle.OracleTiles(blob, 11)
+    t_index = time.perf_counter() - t0
+    po = oracle.blat_params(min_score=20)
+    pe = oracle.default_pe()
     ix.align_pairs(sample[: 2 * min(n, 20000)], threads=threads)  # warm-up
     passes, dt = 0, 0.0
+    st = dict(s2_s3=0.0, gather=0.0, s4=0.0, s5=0.0, s6=0.0)
+    counts = {}
     while passes == 0 or dt < args.cpu_seconds:
         t0 = time.perf_counter()
         rec = ix.align_pairs(sample, threads=threads)
-        partition(AlignResult(rec["flag"], rec["pos"], rec["score"], rec["n_cigar"], rec["cigar"], rec["hits"]))
-        dt += time.perf_counter() - t0
+        res = AlignResult(rec["flag"], rec["pos"], rec["score"], rec["n_cigar"], rec["cigar"], rec["hits"])
+        t1 = time.perf_counter()
+        s4, s5, tails = _host_queries(sample, rec, res, partition)
+        t2 = time.perf_counter()
+        if len(s4):
+            og.align_pe(s4, np.full(len(s4), s4.shape[1], np.int32), pe=pe, threads=threads)
+        t3 = time.perf_counter()
+        if s5:
+            buf, ln = place.pack_queries(s5)
+            og.align_se(buf, ln, threads=threads)
+        t4 = time.perf_counter()
+        if tails:
+            buf, ln = place.pack_queries(tails)
+            tiles.blat(buf, ln, po, 16, threads=threads)
+        t5 = time.perf_counter()
+        for k, v in zip(st, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)):
+            st[k] += v
+        dt += t5 - t0
         passes += 1
+        counts = dict(s4_pairs=len(s4) // 2, s5_split_reads=len(s5), s6_tails=len(tails))
     return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
             "host_cpus_visible": os.cpu_count(),
-            "sample": f"first {n} pairs of the batch x {passes} passes ({dt:.1f} s): S2 + S3 on oracle/bwa_pe.c "
-                      f"(C restatement of bwa-mem PE; bwa, BLAT and samtools are absent), OpenMP {threads} threads "
-                      "(the GPU's host CPU share); genome searches not included"}
+            "stages_s_per_pass": {k: round(v / passes, 3) for k, v in st.items()},
+            "queries_per_pass": counts,
+            "sample": f"first {n} pairs of the batch x {passes} passes ({dt:.1f} s): S2 + S3 + gathers + S4/S5 "
+                      f"genome bwa mem + S6 BLAT on the oracle (C restatements: oracle/bwa_pe.c, oracle/blat.c; "
+                      f"bwa, BLAT and samtools are absent), OpenMP {threads} threads = the GPU's host CPU share "
+                      f"(OMP_NUM_THREADS; host_cpus_visible is the whole machine's count); S4/S5/S6 genome = "
+                      f"the {len(subset)} gene-locus windows +- 1 Mb ({sum(len(q) for _, q in subset) / 1e6:.1f} Mbp, "
+                      f"oracle indexes built in {t_index:.1f} s, untimed)"}
 
 
 class Placement:
