@@ -38,7 +38,7 @@ EXPORTS = (
     "af_tile_index_build_device", "af_blat", "af_blat_device", "af_blat_device_range", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
     "af_fastq_close", "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
-    "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats",
+    "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats", "af_s5_filter_device",
 )
 AF_G_MAX_REC = 8
 AF_GSTAT_N = 4
@@ -178,6 +178,9 @@ def lib():
     L.af_genome_regions.restype = ctypes.c_int
     L.af_genome_stats.argtypes = [_vp, _vp]
     L.af_genome_stats.restype = ctypes.c_int
+    L.af_s5_filter_device.argtypes = [_vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, ctypes.POINTER(AlnOut), _i64, _vp, _i32,
+                                      _vp, _vp, _vp, _vp, _vp]
+    L.af_s5_filter_device.restype = ctypes.c_int
     _L = L
     return L
 

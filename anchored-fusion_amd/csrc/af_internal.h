@@ -270,6 +270,13 @@ hipError_t af_launch_s2_chunks(int64_t n_pairs, int32_t stride, const int32_t *l
 hipError_t af_launch_split_tails(const uint8_t *reads, int64_t n_reads, int32_t stride, const int32_t *lens,
                                  const af_aln_out &out, const AfTails &t, bool append, hipStream_t s);
 size_t af_gather_temp_bytes(int64_t n_rows);
+// s5s6.hip: the genome check of the split reads (fn:718-768) and the S6 query rows (fn:512-528)
+size_t af_s5_temp_bytes(int64_t n);
+hipError_t af_launch_s5_filter(const af_grec *recs, const int32_t *n_rec, int64_t n, const uint8_t *q, int32_t q_stride,
+                               const int32_t *q_lens, const int32_t *q_rows, const af_aln_out &s2, int64_t cap,
+                               uint8_t *out, int32_t out_stride, int32_t *out_lens, int32_t *out_src, int32_t *n_out,
+                               int32_t *n_over, uint8_t *keep, int32_t *sel, int64_t *n_sel, void *temp,
+                               size_t temp_bytes, hipStream_t s);
 hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t *lens, const int32_t *rows,
                             int64_t n_rows, int32_t mode, const af_aln_out &out, int64_t first, int64_t step,
                             int64_t cap, uint8_t *q, int32_t *q_lens, int32_t *q_rows, int32_t *n_q, int32_t *sel,

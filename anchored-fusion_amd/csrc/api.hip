@@ -82,6 +82,13 @@ struct af_ctx {
     int32_t *g_nrec = nullptr, *g_hlens = nullptr;
     uint8_t *g_hreads = nullptr;
     int64_t g_cap_recs = 0, g_cap_hbytes = 0;
+    // the S5 genome check + S6 queries (s5s6.hip)
+    uint8_t *s5_keep = nullptr;
+    int32_t *s5_sel = nullptr;
+    int64_t *s5_nsel = nullptr;
+    void *s5_temp = nullptr;
+    size_t s5_temp_bytes = 0;
+    int64_t s5_cap = 0;
 };
 
 struct af_genome {
@@ -539,6 +546,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n);
     af_free(c->g_iv_off); af_free(c->g_ghist); af_free(c->g_nchunks); af_free(c->g_cstart); af_free(c->g_scan);
     af_free(c->g_pes); af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens); af_free(c->g_hreads);
+    af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_nsel); af_free(c->s5_temp);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1269,6 +1277,36 @@ int af_genome_stats(af_ctx *c, int32_t *out) {
     (void)hipSetDevice(c->device);
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(out, c->g_stats, sizeof(int32_t) * AF_GSTAT_N, hipMemcpyDeviceToHost));
+    return AF_OK;
+}
+
+int af_s5_filter_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
+                        const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
+                        const af_aln_out *d_s2, int64_t cap, uint8_t *d_s6, int32_t s6_stride, int32_t *d_s6_lens,
+                        int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream) {
+    if (!c || !d_s2 || !d_n6) return fail(c, AF_E_INVALID, "null argument");
+    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
+    if (n_queries > 0 && (!d_recs || !d_n_rec || !d_q || !d_q_lens || !d_q_rows || !d_s2->flag || !d_s2->pos ||
+                          !d_s2->n_cigar || !d_s2->cigar))
+        return fail(c, AF_E_INVALID, "null argument");
+    if (cap < 0 || (cap > 0 && (!d_s6 || !d_s6_lens || !d_s6_src))) return fail(c, AF_E_INVALID, "null output buffer");
+    if (q_stride <= 0 || q_stride > AF_MAX_READ || s6_stride <= 0 || s6_stride > AF_MAX_READ)
+        return fail(c, AF_E_INVALID, "strides must be in [1, %d]", AF_MAX_READ);
+    (void)hipSetDevice(c->device);
+    if (n_queries > c->s5_cap) {
+        af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_temp);
+        c->s5_keep = nullptr; c->s5_sel = nullptr; c->s5_temp = nullptr; c->s5_cap = 0;
+        const int64_t n = std::max<int64_t>(n_queries, 1 << 16);
+        c->s5_temp_bytes = af_s5_temp_bytes(n);
+        HIPCHK(c, hipMalloc(&c->s5_keep, n));
+        HIPCHK(c, hipMalloc(&c->s5_sel, sizeof(int32_t) * n));
+        HIPCHK(c, hipMalloc(&c->s5_temp, std::max<size_t>(c->s5_temp_bytes, 16)));
+        c->s5_cap = n;
+    }
+    if (!c->s5_nsel) HIPCHK(c, hipMalloc(&c->s5_nsel, sizeof(int64_t)));
+    HIPCHK(c, af_launch_s5_filter(d_recs, d_n_rec, n_queries, d_q, q_stride, d_q_lens, d_q_rows, *d_s2, cap, d_s6,
+                                  s6_stride, d_s6_lens, d_s6_src, d_n6, d_n_over, c->s5_keep, c->s5_sel, c->s5_nsel, c->s5_temp,
+                                  c->s5_temp_bytes, (hipStream_t)stream));
     return AF_OK;
 }
 

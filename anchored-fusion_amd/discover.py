@@ -7,13 +7,15 @@ partner stages, all on the device with no host round trip for the data (SURVEY.m
 | AF:182 `\\| samtools sort`, AF:186-194 filters | `af_partition_device` over every record of the set |
 | AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_genome_align_pe_device` |
 | fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + `af_genome_align_se_device` |
-| fn:530 BLAT of the split reads' tails (S6) | tails cut in K3 + `af_blat_device` (BLAT restatement, -minScore=20) |
+| fn:718-768 genome check of the split reads, fn:506-528 S6 FASTA | `af_s5_filter_device` (survivors' processed SEQ) |
+| fn:530 `blat -minScore=20 genome split.fa` (S6) | `af_blat_device` (BLAT restatement) on the survivors |
 
 `run()` enqueues one pass; S3 synchronises twice (its select count sizes the sort; the partition
 counts size the gathers) and the gathers once (the split-read count sizes S5).  Everything else
-stays on the device: the records, the row lists, the queries and the genome calls' SAM records
-(af_grec), which `exchange()` all-gathers between ranks (one process per GPU, RCCL).  Per-call
-caps (query and tail buffers, the genome calls' per-read caps) are counted in `summary()`.
+stays on the device: the records, the row lists, the queries, the genome calls' SAM records
+(af_grec), the S6 queries and their PSL rows, which `exchange()` all-gathers between ranks (one
+process per GPU, RCCL).  S6 follows S5 (its queries are S5's survivors); S4 runs beside S6.
+Per-call caps (query buffers, the genome calls' per-read caps) are counted in `summary()`.
 """
 import os
 import sys
@@ -24,7 +26,6 @@ from . import genome as _genome
 from .align import AlignerGroup
 from .shard import chunk_pairs
 
-MIN_CLIP = 20       # split-read tails placed by S6 (functions.py:530 queries; clip >= 20)
 MAX_REC = _genome.MAX_REC
 EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
 HIT_WORDS = 44      # af_grec as int32 words (176 B)
@@ -46,7 +47,7 @@ class CandidateDiscovery:
     batches in flight (AlignerGroup)."""
 
     def __init__(self, anchor: bytes, reference, tiles, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
-                 pair_base=0, chunk_bases=10_000_000, query_frac=0.004, tail_frac=0.002):
+                 pair_base=0, chunk_bases=10_000_000, query_frac=0.004):
         self.chunk_bases = int(chunk_bases)
         import torch
         self.dev = torch.device("cuda", device)
@@ -70,55 +71,43 @@ class CandidateDiscovery:
         self.out = {k: z(max(nr, 1)) for k in ("flag", "pos", "score", "n_cigar", "hits")}
         self.out["cigar"] = z(max(nr, 1), _lib.AF_MAX_CIGAR)
         self.s3 = (z(max(nr, 1)), z(max(nr, 1)), z(max(nr, 1)), z(3, dt=torch.int64))
-        # S6 tails (cut in K3, appended by every batch) and the S4 + S5 queries
-        self.tcap = max(4096, int(nr * tail_frac))
-        self.tails = dict(tails=z(self.tcap, self.L, dt=torch.uint8), lens=z(self.tcap), read=z(self.tcap), n=z(1))
-        self.t_rows = z(self.tcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
-        self.t_nh = z(self.tcap)
+        # the S4 + S5 queries, their SAM records, and the S6 queries (S5's survivors) with their rows
         self.qcap = max(4096, int(nr * query_frac))
         self.q = z(self.qcap, self.L, dt=torch.uint8)
         self.q_lens, self.q_rows, self.n_q = z(self.qcap), z(self.qcap), z(1)
         self.q_recs = z(self.qcap * MAX_REC * _genome.REC_DTYPE.itemsize, dt=torch.uint8)
         self.q_nh = z(self.qcap)   # SAM records per query
+        self.s6 = dict(q=z(self.qcap, _lib.AF_MAX_READ, dt=torch.uint8), lens=z(self.qcap), src=z(self.qcap), n=z(1),
+                       over=z(1))
+        self.t_rows = z(self.qcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
+        self.t_nh = z(self.qcap)
         self.p_genome = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), AF:188 / fn:716
         self.p_tail = _blat.params("split_tail")
         self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
+        self._npair = 0
 
     def close(self):
         self.grp.close()
 
-    def _tails(self, j, row0):
-        t = self.tails
-        return dict(tails=t["tails"], lens=t["lens"], read=t["read"], n=t["n"], min_clip=MIN_CLIP, read_base=row0,
-                    append=True)
-
     def run(self, reads_t, k1_events=None, phase_events=None):
         """One pass over reads_t (uint8 [2 n_pairs, read_len] on the device).  k1_events: per group
         a pair of timing events around its K1 launches; phase_events: 4 events recorded on the
-        first slot's stream after S2, S3, the gathers and the placements."""
+        first slot's stream after S2, S3, the gathers and the genome searches."""
         import torch
         G = self.grp.inflight
         s0 = self.grp.streams[0]
-        with torch.cuda.stream(s0):
-            self.tails["n"].zero_()
         done = None
         for gi, k0 in enumerate(range(0, len(self.batches), G)):
             group = self.batches[k0:k0 + G]
-            specs, rows0 = [], []
+            specs = []
             for p, n in group:
                 r0, r1 = 2 * p, 2 * (p + n)
                 specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()}, None,
                               self.pair_base + p))
-                rows0.append(r0)
-            done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done,
-                                       tails=lambda j, rows0=rows0: self._tails(j, rows0[j]))
-        # S6 (BLAT -minScore=20 of the split-read tails that K3d cut during S2) needs no S3: it
-        # runs on slot 1's stream (the tile index has its own context and scratch; slot 1 is idle
-        # once S2 is done -- a stream of its own would share one of the 4 hardware queues
-        # (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work) beside S4 / S5.  It is
-        # launched after S3 and the gathers: launched beside them, its resident waves starved
-        # S3's sort kernels (S3 20.3 ms instead of 2.9; C3 step 144.0 -> 141.2 ms).  (Searching
-        # each group's tails while the next group aligns was slower: both are compute-bound.)
+            done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done)
+        # S6 runs on slot 1's stream (the tile index has its own context and scratch; slot 1 is
+        # idle once S2 is done -- a stream of its own would share one of the 4 hardware queues
+        # (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work) beside S4.
         s6 = self.grp.streams[1] if G > 1 else s0
         for e in done:
             s0.wait_event(e)
@@ -146,25 +135,32 @@ class CandidateDiscovery:
                                self.n_q, out_t=self.out, first=2 * npair, step=1, stream=s0)
         if phase_events:
             phase_events[2].record(s0)
-        s6.wait_stream(s0)
-        self.tiles_ref.search_device(self.tails["tails"], self.tails["n"], self.L, self.t_rows, self.t_nh,
-                                     lens_t=self.tails["lens"], p=self.p_tail, stream=s6)
-        s6_done = torch.cuda.Event()
-        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
-        # S4 (`bwa mem -M genome tmp1 tmp2`): the pairs' records, bwa's chunks over this input
+        s0.synchronize()   # the split-read count sizes S5
+        nq_all = int(self.n_q.item())
+        nq = min(nq_all, self.qcap)
+        n5 = max(0, nq - 2 * npair)
         pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
         recs = self.q_recs.view(torch.int32)
+        w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+        # S5 (`bwa mem -M genome split_reads.fa`, fn:716), its genome check (fn:718-768) and the S6
+        # queries (fn:506-528)
+        if n5:
+            self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
+                                     lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0, stream=s0)
+        _genome.s5_filter_device(self.ref.ctx, recs[2 * npair * w:], self.q_nh[2 * npair:], n5, self.q[2 * npair:],
+                                 self.L, self.q_lens[2 * npair:], self.q_rows[2 * npair:], self.out, self.qcap,
+                                 self.s6["q"], self.s6["lens"], self.s6["src"], self.s6["n"], self.s6["over"],
+                                 stream=s0)
+        # S6 (`blat -minScore=20 genome split.fa`, fn:530) beside S4
+        s6.wait_stream(s0)
+        self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
+                                     lens_t=self.s6["lens"], p=self.p_tail, stream=s6)
+        s6_done = torch.cuda.Event()
+        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
+        # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188): the pairs' records, bwa's chunks over this input
         if npair:
             self.ref.align_pe_device(self.q, npair, self.L, self.q_lens, recs, self.q_nh, params=self.p_genome, pe=pe,
                                      stream=s0)
-        # S5 (`bwa mem -M genome split_reads.fa`): its read count sizes the launch
-        s0.synchronize()
-        nq = min(int(self.n_q.item()), self.qcap)
-        n5 = max(0, nq - 2 * npair)
-        if n5:
-            w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
-            self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
-                                     lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0, stream=s0)
         s0.wait_event(s6_done)
         if _DEBUG:
             s0.synchronize()
@@ -172,7 +168,8 @@ class CandidateDiscovery:
         if phase_events:
             phase_events[3].record(s0)
         self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s4_pairs=npair, s5_split_reads=n5,
-                           s4_pairs_dropped=max(0, min(n1, n2) - npair), s5_dropped=max(0, int(self.n_q.item()) - nq))
+                           s4_pairs_dropped=max(0, min(n1, n2) - npair), s5_dropped=max(0, nq_all - nq))
+        self._npair = npair
         return s0
 
     def summary(self):
@@ -180,43 +177,48 @@ class CandidateDiscovery:
         import torch
         torch.cuda.synchronize(self.dev)
         nq = min(int(self.n_q.item()), self.qcap)
-        nt = int(self.tails["n"].item())
-        tn = self.t_nh[:min(nt, self.tcap)].cpu().numpy()
+        n6 = int(self.s6["n"].item())
+        tn = self.t_nh[:n6].cpu().numpy()
         rec = self.q_recs[:nq * MAX_REC * _genome.REC_DTYPE.itemsize].cpu().numpy().view(_genome.REC_DTYPE)
         rec = rec.reshape(nq, MAX_REC)
         first = rec[:, 0]["flag"] if nq else rec
         c = dict(self.counts or {})
         c.update(queries_s4_s5=nq, queries_placed=int(((first & 4) == 0).sum()) if nq else 0,
-                 genome_records=int(self.q_nh[:nq].sum().item()), tails=nt, tails_placed=int((tn > 0).sum()),
-                 tails_dropped=max(0, nt - self.tcap), mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()),
+                 genome_records=int(self.q_nh[:nq].sum().item()), s6_queries=n6,
+                 s6_placed=int((tn > 0).sum()), s6_at_row_cap=int((tn >= _blat.MAX_ROWS).sum()),
+                 s6_clipped=int(self.s6["over"].item()),
+                 mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()),
                  s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))
                                         != 0).sum().item()))
         c.update({f"genome_{k}": v for k, v in self.ref.stats().items()})
         return c
 
-    def tail_best_hits(self):
-        """(read rows, row counts, best BLAT row per tail) of the last pass, on the host (synchronises)."""
+    def s6_best_hits(self):
+        """(read rows, row counts, best BLAT row per S6 query) of the last pass, on the host (synchronises)."""
         import torch
         torch.cuda.synchronize(self.dev)
-        nt = min(int(self.tails["n"].item()), self.tcap)
-        rows = self.t_rows[:nt * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
-        return (self.tails["read"][:nt].cpu().numpy(), self.t_nh[:nt].cpu().numpy(),
-                rows.reshape(nt, _blat.MAX_ROWS)[:, 0] if nt else rows)
+        n6 = int(self.s6["n"].item())
+        rows = self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
+        src = self.s6["src"][:n6].long()
+        read = self.q_rows[self._npair * 2:][src] if n6 else self.s6["src"][:0]
+        return (read.cpu().numpy(), self.t_nh[:n6].cpu().numpy(),
+                rows.reshape(n6, _blat.MAX_ROWS)[:, 0] if n6 else rows)
 
     def pack(self):
         """The breakpoint candidates of the last pass as int32 rows [k, EX_WORDS] on the device:
-        every S4 / S5 query and every S6 tail -- the read's global row (2 words), kind (0 query,
-        1 tail), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the record / row count and the first
+        every S4 / S5 query and every S6 query -- the read's global row (2 words), kind (0 genome
+        query, 1 S6 query), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the record / row count and the first
         EX_HITS of them (af_grec SAM records of the genome bwa calls, af_psl rows for BLAT).  These
         are the only records the stages after S6 read (SURVEY §8 e)."""
         import torch
         torch.cuda.synchronize(self.dev)
         nq = min(int(self.n_q.item()), self.qcap)
-        nt = min(int(self.tails["n"].item()), self.tcap)
+        n6 = int(self.s6["n"].item())
+        s6_rows = self.q_rows[2 * self._npair:][self.s6["src"][:n6].long()] if n6 else self.q_rows[:0]
         parts = []
         for kind, n, rows, nh, hits, width, per in (
                 (0, nq, self.q_rows, self.q_nh, self.q_recs, HIT_WORDS, MAX_REC),
-                (1, nt, self.tails["read"], self.t_nh, self.t_rows, PSL_WORDS, _blat.MAX_ROWS)):
+                (1, n6, s6_rows, self.t_nh, self.t_rows, PSL_WORDS, _blat.MAX_ROWS)):
             if n == 0:
                 continue
             r = rows[:n].long()

@@ -186,6 +186,23 @@ class GenomeIndex:
         return sam_lines(self.names, name, seq, recs, n)
 
 
+def s5_filter_device(ctx, recs_t, nrec_t, n, q_t, q_stride, q_lens_t, q_rows_t, s2_out, cap, s6_t, s6_lens_t,
+                     s6_src_t, n6_t, n_over_t=None, stream=None):
+    """af_s5_filter_device: the genome check of the n S5 queries (`del_too_many_reads`,
+    functions.py:718-768) and the S6 query rows of the survivors (fn:506-528) on the device.
+    s2_out: the S2 record tensors (flag / pos / score / n_cigar / hits / cigar) the queries' rows
+    index; s6_t uint8 [cap, stride], s6_lens_t / s6_src_t int32 [cap], n6_t int32 [1]; n_over_t
+    (int32 [1], optional) counts rows whose processed sequence was clipped to the stride."""
+    if int(s6_t.shape[0]) < cap or s6_lens_t.numel() < cap or s6_src_t.numel() < cap:
+        raise ValueError("S6 buffers hold fewer than cap rows")
+    o = _lib.AlnOut(*(s2_out[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+    _lib.check(ctx, _lib.lib().af_s5_filter_device(
+        ctx, recs_t.data_ptr(), nrec_t.data_ptr(), int(n), q_t.data_ptr(), int(q_stride), q_lens_t.data_ptr(),
+        q_rows_t.data_ptr(), ctypes.byref(o), int(cap), s6_t.data_ptr(), int(s6_t.shape[1]), s6_lens_t.data_ptr(),
+        s6_src_t.data_ptr(), n6_t.data_ptr(), None if n_over_t is None else n_over_t.data_ptr(),
+        _stream_handle(stream)), "af_s5_filter_device")
+
+
 def sam_lines(names, name, seq, recs, n):
     out = []
     rc = None

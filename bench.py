@@ -10,12 +10,13 @@ duplications, the anchor and 8 partner genes embedded as exons; 5 % of the pairs
 anchor fusions, the rest from the genome (wgsim's read model, seeded per pair).  A step is one
 pass of discover.CandidateDiscovery over the resident pairs:
   S2  K1 + K2 + K3 per batch of 240 bwa chunks (8 M pairs; `bwa mem -M anchor fq1 fq2`,
-      Anchored_Fusion.py:182), 4 batches in flight, the split-read tails cut in K3;
+      Anchored_Fusion.py:182), 4 batches in flight;
   S3  the samtools coordinate sort and the -f 8 / -f 4 / -F 772 partitions (AF:182, 186-194);
   S4  the one-end-anchored pairs (tmp1 / tmp2) and S5 the anchored split reads placed on the genome
       (`bwa mem -M genome`, AF:188 and functions.py:716);
-  S6  the split reads' tails searched on the genome with the BLAT restatement (-minScore=20,
-      functions.py:530; 11-mer tile index of the genome);
+  S5 check  `del_too_many_reads`' genome check of the split reads (fn:718-768) on the device;
+  S6  the survivors searched on the genome with the BLAT restatement (-minScore=20, fn:530;
+      11-mer tile index of the genome);
   and at N > 1 the all-gatherv of the breakpoint candidates (RCCL).
 Inputs are resident in HBM before timing starts.  At N > 1 the 50 M pairs are sharded on bwa's
 10 Mbase chunk grid (strong scaling, configs[3]).
@@ -417,7 +418,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
             "workload": f"configs[{2 if world == 1 else 3}]: {N} synthetic 2x{L} bp pairs"
                         + (f" sharded over {world} GPUs" if world > 1 else "")
                         + f", bwa genome index {genome_bp / 1e9:.2f} Gbp HBM-resident, one anchor (BCR NM_004327.4); "
-                          "step = S2 + S3 sort/partition + S4/S5 genome bwa mem + S6 tail BLAT"
+                          "step = S2 + S3 sort/partition + S4/S5 genome bwa mem + S5 genome check + S6 BLAT"
                         + (" + all-gatherv of candidates" if world > 1 else ""),
             "pairs_total": N, "pairs_per_gpu": n, "read_len": L, "genome_bp": genome_bp, "anchor_len": len(anchor),
             "parallelism": f"dp{world}", "batches": n_launch, "pairs_per_batch": bp, "inflight": G,
@@ -426,8 +427,8 @@ def bench_c3(args, world, rank, gpu, dev, backend):
         "phases_ms": {"s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
                       "gather_queries": round(phase(2, 3), 3), "genome_bwa_s4_s5": round(phase(3, 4), 3),
                       "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
-                              "the S6 BLAT runs on slot 1's stream from the end of gather_queries, beside "
-                              "genome_bwa_s4_s5, which ends by joining it"},
+                              "genome_bwa_s4_s5 = S5, its genome check, then S4 on slot 0 beside the S6 BLAT "
+                              "of S5's survivors on slot 1's stream, joined at its end"},
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
             "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -478,30 +479,42 @@ def genome_subset(W, flank=1_000_000):
 
 
 def _host_queries(sample, rec, res, partition):
-    """S3's lists of the sample and the genome searches' queries, as the device gathers make them
-    (af_gather_reads_device): S4 tmp1 / tmp2 interleaved as sequenced, S5 the anchored reads whose
-    CIGAR deal_cigar reduces to two operations in SAM orientation, S6 the split-read tails."""
+    """S3's lists of the sample and the genome searches' queries as the reference makes them:
+    S4 tmp1 / tmp2 interleaved as sequenced (AF:186-188), S5 the split-read FASTA of the anchored
+    records (genome_check.split_read_fasta over their SAM lines, fn:705-715)."""
     import numpy as np
 
-    from anchored_fusion_amd.cigar import normalize
-    comp = bytes.maketrans(b"ACGTN", b"TGCAN")
+    from anchored_fusion_amd import genome_check
+    from anchored_fusion_amd.cigar import revcomp
+    from anchored_fusion_amd.pipeline import sam_line
     t1, t2, an = partition(res)
     npair = min(len(t1), len(t2))
     s4 = np.empty((2 * npair, sample.shape[1]), np.uint8)
     s4[0::2], s4[1::2] = sample[t1[:npair]], sample[t2[:npair]]
-    s5 = []
+    lines = []
     for r in an:
-        s = sample[r].tobytes()
-        if len(normalize(res.cigar_str(r), s.decode())[0]) == 2:
-            s5.append(s[::-1].translate(comp) if rec["flag"][r] & 0x10 else s)
-    return s4, s5, _split_tails(sample, rec, Placement.MIN_CLIP)
+        s = sample[r].tobytes().decode()
+        f = int(rec["flag"][r])
+        lines.append(sam_line(f"r{r // 2}", f & 0xFFFF, "ANCHOR", int(rec["pos"][r]) + 1, res.cigar_str(r),
+                              revcomp(s) if f & 0x10 else s))
+    return s4, genome_check.split_read_fasta(lines)
+
+
+def _host_s6_queries(names, fasta, recs, nrec):
+    """S5's genome check (genome_check.filter_genome_hits, fn:718-768) over the SAM text of the
+    S5 records and the S6 FASTA of the survivors (blocks.split_read_queries, fn:506-528)."""
+    from anchored_fusion_amd import blocks, genome, genome_check
+    gsam = ["@HD\tVN:1.6\n"]
+    for i, (name, sq) in enumerate(fasta):
+        gsam += genome.sam_lines(names, name, sq, recs[i], nrec[i])
+    return blocks.split_read_queries(genome_check.filter_genome_hits(gsam))[1]
 
 
 def cpu_baseline_c3(anchor, reads_t, args, subset):
     """The CPU oracle on a bounded sample of the same pairs, over the stages of the GPU step: S2
     (oracle/bwa_pe.c, bwa-mem PE restated) + S3 (samtools order and filters) + the queries'
-    gathers + S4 / S5 (the same restatement's genome calls, FM index) + S6 (oracle/blat.c,
-    -minScore=20, 11-mer tiles), repeated for --cpu-seconds.  The genome of S4/S5/S6 is `subset`
+    gathers + S4 / S5 (the same restatement's genome calls, FM index) + S5's genome check + S6
+    (oracle/blat.c, -minScore=20, 11-mer tiles, on S5's survivors), repeated for --cpu-seconds.  The genome of S4/S5/S6 is `subset`
     (genome_subset: the gene loci +- 1 Mb) -- an oracle index of the whole 3.1 Gbp takes longer to
     build than the bench runs."""
     import numpy as np
@@ -522,37 +535,43 @@ def cpu_baseline_c3(anchor, reads_t, args, subset):
     pe = oracle.default_pe()
     ix.align_pairs(sample[: 2 * min(n, 20000)], threads=threads)  # warm-up
     passes, dt = 0, 0.0
-    st = dict(s2_s3=0.0, gather=0.0, s4=0.0, s5=0.0, s6=0.0)
+    st = dict(s2_s3=0.0, gather=0.0, s4=0.0, s5=0.0, s5_check=0.0, s6=0.0)
     counts = {}
+    names = [nm for nm, _ in subset]
     while passes == 0 or dt < args.cpu_seconds:
         t0 = time.perf_counter()
         rec = ix.align_pairs(sample, threads=threads)
         res = AlignResult(rec["flag"], rec["pos"], rec["score"], rec["n_cigar"], rec["cigar"], rec["hits"])
         t1 = time.perf_counter()
-        s4, s5, tails = _host_queries(sample, rec, res, partition)
+        s4, fasta = _host_queries(sample, rec, res, partition)
         t2 = time.perf_counter()
         if len(s4):
             og.align_pe(s4, np.full(len(s4), s4.shape[1], np.int32), pe=pe, threads=threads)
         t3 = time.perf_counter()
-        if s5:
-            buf, ln = place.pack_queries(s5)
-            og.align_se(buf, ln, threads=threads)
-        t4 = time.perf_counter()
-        if tails:
-            buf, ln = place.pack_queries(tails)
-            tiles.blat(buf, ln, po, 16, threads=threads)
+        s6q = []
+        if fasta:
+            buf, ln = place.pack_queries([sq for _, sq in fasta])
+            r5, n5 = og.align_se(buf, ln, threads=threads)
+            t4 = time.perf_counter()
+            s6q = _host_s6_queries(names, fasta, r5, n5)
+        else:
+            t4 = time.perf_counter()
         t5 = time.perf_counter()
-        for k, v in zip(st, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)):
+        if s6q:
+            buf, ln = place.pack_queries([sq for _, sq in s6q])
+            tiles.blat(buf, ln, po, 16, threads=threads)
+        t6 = time.perf_counter()
+        for k, v in zip(st, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5)):
             st[k] += v
-        dt += t5 - t0
+        dt += t6 - t0
         passes += 1
-        counts = dict(s4_pairs=len(s4) // 2, s5_split_reads=len(s5), s6_tails=len(tails))
+        counts = dict(s4_pairs=len(s4) // 2, s5_split_reads=len(fasta), s6_queries=len(s6q))
     return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
             "host_cpus_visible": os.cpu_count(),
             "stages_s_per_pass": {k: round(v / passes, 3) for k, v in st.items()},
             "queries_per_pass": counts,
             "sample": f"first {n} pairs of the batch x {passes} passes ({dt:.1f} s): S2 + S3 + gathers + S4/S5 "
-                      f"genome bwa mem + S6 BLAT on the oracle (C restatements: oracle/bwa_pe.c, oracle/blat.c; "
+                      f"genome bwa mem + S5 genome check + S6 BLAT on the oracle (C restatements: oracle/bwa_pe.c, oracle/blat.c; "
                       f"bwa, BLAT and samtools are absent), OpenMP {threads} threads = the GPU's host CPU share "
                       f"(OMP_NUM_THREADS; host_cpus_visible is the whole machine's count); S4/S5/S6 genome = "
                       f"the {len(subset)} gene-locus windows +- 1 Mb ({sum(len(q) for _, q in subset) / 1e6:.1f} Mbp, "

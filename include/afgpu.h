@@ -317,6 +317,24 @@ int af_genome_regions(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int
 /* the counters of the last genome call on ctx (AF_GSTAT_N int32; synchronises) */
 int af_genome_stats(af_ctx *ctx, int32_t *out);
 
+/* The genome check of the split reads and the S6 queries, on the device (`del_too_many_reads`,
+ * functions.py:718-768, and the FASTA of `Find_fine_block`, fn:506-528).  Input: the n_queries
+ * S5 queries (d_q rows of q_stride bytes as af_gather_reads_device's AF_GATHER_SPLIT_SAM wrote
+ * them, d_q_lens, d_q_rows = the read rows), their af_genome_align_se_device records (d_recs,
+ * d_n_rec) and the S2 records d_s2 of af_align_*_device (FLAG / POS / CIGAR of the anchored
+ * read).  A query is dropped when a genome record aligns it as one deal_cigar operation or a
+ * genome M straddles the end of an anchored M by more than 20 % of it on both sides; records are
+ * grouped by consecutive QNAME (pair, POS, CIGAR), as the reference's file walk groups them.
+ * Each survivor, in query order, becomes S6 query row k of d_s6 (s6_stride bytes): deal_cigar's
+ * processed SEQ (N for each deleted base, inserted bases removed), d_s6_lens[k] (clipped to
+ * s6_stride; the clipped rows are counted in *d_n_over, which may be NULL), d_s6_src[k] = its S5
+ * query index; *d_n6 = min(survivors, cap): the query count af_blat_device reads.  Asynchronous
+ * on `stream`. */
+int af_s5_filter_device(af_ctx *ctx, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
+                        const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
+                        const af_aln_out *d_s2, int64_t cap, uint8_t *d_s6, int32_t s6_stride, int32_t *d_s6_lens,
+                        int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream);
+
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as
  * bwa's reader takes them (name = header up to the first blank, "/<digit>" trimmed; multi-line

@@ -92,8 +92,10 @@ def test_discovery_matches_oracle_reduced(anchor):
     # S4 / S5 records (af_grec) of the device calls == the same engine's host-buffer calls on the
     # same queries (the engine itself is pinned bit-exact vs oracle/bwa_pe.c by test_gpu_genome.py)
     _check_genome_records(d, ref, q, nq, c["s4_pairs"])
+    # S5's genome check and the S6 queries == the host chain over the same records
+    _check_s5_s6(d, ref, reads, got, an, c["s4_pairs"], nq)
     summ = d.summary()
-    assert summ["tails"] > 0 and summ["tails_placed"] > 0.5 * summ["tails"]
+    assert summ["s6_queries"] > 0 and summ["s6_placed"] > 0.5 * summ["s6_queries"]
     assert summ["queries_placed"] > 0.9 * nq and summ["genome_cap_overflow"] == 0
     d.close()
     ref.close()
@@ -119,6 +121,24 @@ def _check_genome_records(d, ref, q, nq, npair):
             assert all(int(a[f]) == int(b[f]) for f in ("flag", "rid", "mrid", "pos", "mpos", "score", "n_cigar",
                                                          "seq_b", "seq_e")), (r, k)
             assert np.array_equal(a["cigar"][:nc], b["cigar"][:nc]), (r, k)
+
+
+def _check_s5_s6(d, ref, reads, got, an, npair, nq):
+    from anchored_fusion_amd import discover, genome
+    from test_gpu_s5s6 import host_s5_s6
+    n5 = nq - 2 * npair
+    recs = d.q_recs[:nq * discover.MAX_REC * genome.REC_DTYPE.itemsize].cpu().numpy().view(genome.REC_DTYPE)
+    recs = recs.reshape(nq, discover.MAX_REC)[2 * npair:]
+    h = dict(got)
+    h["cigar"] = h["cigar"].view(np.int32)
+    fasta, split_sam, s6_fa = host_s5_s6(reads, h, an, recs, d.q_nh[2 * npair:nq].cpu().numpy(), ref.names)
+    assert len(fasta) == n5
+    n6 = int(d.s6["n"].item())
+    assert n6 == len(s6_fa)
+    rows, lens, src = d.s6["q"][:n6].cpu().numpy(), d.s6["lens"][:n6].cpu().numpy(), d.s6["src"][:n6].cpu().numpy()
+    for k in range(n6):
+        assert split_sam[k].split("\t")[0] == fasta[src[k]][0].split("$")[0]
+        assert rows[k, :lens[k]].tobytes().decode() == s6_fa[k][1], k
 
 
 def test_c3_full_size(anchor):
@@ -161,18 +181,17 @@ def test_c3_full_size(anchor):
         s = r.tobytes()
         if h == 0:
             assert not any(s[i:i + 19] in kmers for i in range(L - 18))
-    # tails (BLAT, -minScore=20): best rows inside the anchor or a partner gene locus (exons and
-    # introns: reads from the genome's copy of the anchor gene that cross an exon end leave
-    # intronic tails)
+    # S6 (BLAT -minScore=20 of S5's survivors): best rows inside the anchor or a partner gene
+    # locus (exons and introns)
     spans = [(W.names.index(v[0][0]), v[0][1] - 1000, v[-1][2] + 1000) for v in W.loci.values()]
-    _, nh, best = d.tail_best_hits()
+    _, nh, best = d.s6_best_hits()
     placed = np.nonzero(nh > 0)[0]
     inside = 0
     for t in placed:
         loc = tiles.locate(best[t]["t_start"], best[t]["t_end"])
         inside += loc is not None and any(k == loc[0] and s <= loc[1] < e for k, s, e in spans)
-    print(f"tails placed {len(placed)}, best hit in a gene locus {inside}")
-    assert len(placed) > 30_000 and inside >= 0.95 * len(placed)
+    print(f"S6 queries placed {len(placed)}, best hit in a gene locus {inside}")
+    assert len(placed) > 10_000 and inside >= 0.95 * len(placed)
     d.close()
     ref.close()
     tiles.close()
