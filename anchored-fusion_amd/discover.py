@@ -23,7 +23,7 @@ import sys
 from . import _lib
 from . import blat as _blat
 from . import genome as _genome
-from .align import AlignerGroup
+from .align import AlignerGroup, chunk_ends
 from .shard import chunk_pairs
 
 MAX_REC = _genome.MAX_REC
@@ -39,30 +39,42 @@ def _log(msg):
 
 
 class CandidateDiscovery:
-    """S2 + S3 + S4/S5/S6 genome searches for `n_pairs` resident pairs of `read_len` bases.
+    """S2 + S3 + S4/S5/S6 genome searches for `n_pairs` resident pairs, rows of `read_len` bytes.
 
     reference: genome.GenomeIndex (`bwa index` of the genome, HBM-resident, for the bwa calls); tiles:
     blat.TileReference of the same genome at BLAT's default step (S6).  pair_base: the set's first pair in
     bwa's input stream (a chunk boundary).  batch_chunks: bwa chunks per S2 batch; inflight:
-    batches in flight (AlignerGroup)."""
+    batches in flight (AlignerGroup).  pair_bases (optional, int [n_pairs]): the pairs' base counts
+    when the reads are ragged (run() then takes their lengths); bwa's chunks are cut on them, and
+    read_len (the row stride) must be a multiple of 8 so that every batch starts on a 16-byte
+    boundary."""
 
     def __init__(self, anchor: bytes, reference, tiles, n_pairs, read_len, device=0, inflight=8, batch_chunks=30,
-                 pair_base=0, chunk_bases=10_000_000, query_frac=0.004):
+                 pair_base=0, chunk_bases=10_000_000, query_frac=0.004, pair_bases=None):
         self.chunk_bases = int(chunk_bases)
+        import numpy as np
         import torch
         self.dev = torch.device("cuda", device)
         self.anchor, self.ref, self.tiles_ref = bytes(anchor), reference, tiles
         self.n_pairs, self.L, self.pair_base = int(n_pairs), int(read_len), int(pair_base)
-        pc = chunk_pairs(self.L, chunk_bases)
-        if self.pair_base % pc:
-            raise ValueError("pair_base must be on bwa's chunk grid")
-        # batches start on 16-byte boundaries of reads_t (the seed filter's vector loads): a whole
-        # number of chunks whose bytes are a multiple of 16
-        m = 1
-        while (m * pc * 2 * self.L) % 16:
-            m += 1
-        bp = pc * m * max(1, -(-int(batch_chunks) // m))
-        self.batches = [(p, min(bp, self.n_pairs - p)) for p in range(0, self.n_pairs, bp)]
+        if pair_bases is None:
+            pc = chunk_pairs(self.L, chunk_bases)
+            if self.pair_base % pc:
+                raise ValueError("pair_base must be on bwa's chunk grid")
+            # batches start on 16-byte boundaries of reads_t (the seed filter's vector loads): a
+            # whole number of chunks whose bytes are a multiple of 16
+            m = 1
+            while (m * pc * 2 * self.L) % 16:
+                m += 1
+            bp = pc * m * max(1, -(-int(batch_chunks) // m))
+            self.batches = [(p, min(bp, self.n_pairs - p)) for p in range(0, self.n_pairs, bp)]
+        else:
+            if self.L % 8:
+                raise ValueError("ragged reads: the row stride must be a multiple of 8")
+            ends = chunk_ends(np.asarray(pair_bases, dtype=np.int64), chunk_bases)
+            bc = max(1, int(batch_chunks))
+            starts = [0] + [int(ends[k - 1]) for k in range(bc, len(ends), bc)]
+            self.batches = [(a, b - a) for a, b in zip(starts, starts[1:] + [self.n_pairs]) if b > a]
         self.grp = AlignerGroup(self.anchor, device=device, inflight=inflight)
         for a in self.grp.aligners:
             a.pe.chunk_bases = chunk_bases
@@ -72,27 +84,36 @@ class CandidateDiscovery:
         self.out["cigar"] = z(max(nr, 1), _lib.AF_MAX_CIGAR)
         self.s3 = (z(max(nr, 1)), z(max(nr, 1)), z(max(nr, 1)), z(3, dt=torch.int64))
         # the S4 + S5 queries, their SAM records, and the S6 queries (S5's survivors) with their rows
-        self.qcap = max(4096, int(nr * query_frac))
+        self.n_q = z(1)
+        self._alloc_queries(max(4096, int(nr * query_frac)))
+        self.p_genome = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), AF:188 / fn:716
+        self.p_tail = _blat.params("split_tail")
+        self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
+        self._npair = 0
+
+    def _alloc_queries(self, cap):
+        """The query buffers (S4 + S5 queries, their records, the S6 queries and their rows) for cap
+        queries; run() grows them when S3's counts need more."""
+        import torch
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
+        self.qcap = int(cap)
         self.q = z(self.qcap, self.L, dt=torch.uint8)
-        self.q_lens, self.q_rows, self.n_q = z(self.qcap), z(self.qcap), z(1)
+        self.q_lens, self.q_rows = z(self.qcap), z(self.qcap)
         self.q_recs = z(self.qcap * MAX_REC * _genome.REC_DTYPE.itemsize, dt=torch.uint8)
         self.q_nh = z(self.qcap)   # SAM records per query
         self.s6 = dict(q=z(self.qcap, _lib.AF_MAX_READ, dt=torch.uint8), lens=z(self.qcap), src=z(self.qcap), n=z(1),
                        over=z(1))
         self.t_rows = z(self.qcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
         self.t_nh = z(self.qcap)
-        self.p_genome = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), AF:188 / fn:716
-        self.p_tail = _blat.params("split_tail")
-        self.counts = None   # host (tmp1, tmp2, anchored, S4 pairs, S5 split reads) after run()
-        self._npair = 0
 
     def close(self):
         self.grp.close()
 
-    def run(self, reads_t, k1_events=None, phase_events=None):
-        """One pass over reads_t (uint8 [2 n_pairs, read_len] on the device).  k1_events: per group
-        a pair of timing events around its K1 launches; phase_events: 4 events recorded on the
-        first slot's stream after S2, S3, the gathers and the genome searches."""
+    def run(self, reads_t, k1_events=None, phase_events=None, lens_t=None):
+        """One pass over reads_t (uint8 [2 n_pairs, read_len] on the device; lens_t: int32 [2 n_pairs]
+        read lengths, or None when every read is read_len long).  k1_events: per group a pair of
+        timing events around its K1 launches; phase_events: 4 events recorded on the first slot's
+        stream after S2, S3, the gathers and the genome searches."""
         import torch
         G = self.grp.inflight
         s0 = self.grp.streams[0]
@@ -102,8 +123,8 @@ class CandidateDiscovery:
             specs = []
             for p, n in group:
                 r0, r1 = 2 * p, 2 * (p + n)
-                specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()}, None,
-                              self.pair_base + p))
+                specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()},
+                              None if lens_t is None else lens_t[r0:r1], self.pair_base + p))
             done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done)
         # S6 runs on slot 1's stream (the tile index has its own context and scratch; slot 1 is
         # idle once S2 is done -- a stream of its own would share one of the 4 hardware queues
@@ -126,13 +147,17 @@ class CandidateDiscovery:
         if _DEBUG:
             _log(f"S3 done: tmp1 {n1}, tmp2 {n2}, anchored {na}")
         # S4 queries: tmp1 / tmp2 interleaved as bwa pairs its two FASTQs; S5: anchored split reads
+        # (the buffers grow to S3's counts: at most 2 min(tmp1, tmp2) + anchored queries)
+        need = 2 * min(n1, n2) + na
+        if need > self.qcap:
+            self._alloc_queries(int(need * 1.25) + 1024)
         npair = min(n1, n2, self.qcap // 2)
         al.gather_reads_device(reads_t, self.L, t1, npair, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens,
-                               self.q_rows, None, first=0, step=2, stream=s0)
+                               self.q_rows, None, lens_t=lens_t, first=0, step=2, stream=s0)
         al.gather_reads_device(reads_t, self.L, t2, npair, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens,
-                               self.q_rows, self.n_q, first=1, step=2, stream=s0)
+                               self.q_rows, self.n_q, lens_t=lens_t, first=1, step=2, stream=s0)
         al.gather_reads_device(reads_t, self.L, an, na, _lib.AF_GATHER_SPLIT_SAM, self.q, self.q_lens, self.q_rows,
-                               self.n_q, out_t=self.out, first=2 * npair, step=1, stream=s0)
+                               self.n_q, out_t=self.out, lens_t=lens_t, first=2 * npair, step=1, stream=s0)
         if phase_events:
             phase_events[2].record(s0)
         s0.synchronize()   # the split-read count sizes S5

@@ -5,21 +5,25 @@ Anchored_Fusion.py:121-227 with its shell calls replaced).
 |---|---|
 | AF:58-80 gene names | `gene_names_from_fasta` / `gene_names_from_file` |
 | AF:144-172 anchor FASTA + `bwa index` | `AnchorAligner(anchor)` (GPU index) |
-| AF:182 `bwa mem -M anchor fq1 fq2 \\| samtools sort` | `AnchorAligner.align_pairs` (K1+K2+K3) |
-| AF:186-194 samtools flag partitions | `align.partition` |
+| AF:182 `bwa mem -M anchor fq1 fq2 \\| samtools sort` | K1+K2+K3 per batch of bwa chunks (`discover.CandidateDiscovery`) |
+| AF:186-194 samtools flag partitions | `af_partition_device` (S3 in HBM) |
 | AF:173-178 `bwa index genome` | `genome.GenomeIndex` (suffix array + FM index built on the GPU) |
 | AF:188 `bwa mem -M genome tmp1 tmp2` | `Searches.genome_sam_pe` (bwa-mem PE on the GPU, csrc/bwa_genome.hip) |
 | AF:198 `Find_homo_genes` | `partner.homolog_genes` |
-| AF:204 `del_too_many_reads` | `genome_check` + `Searches.genome_sam_se` |
+| AF:204 `del_too_many_reads` | S5 + `af_s5_filter_device` (the genome check in HBM) |
+| AF:205 `Find_fine_block` BLAT (fn:530) | `af_blat_device` on the survivors |
 | AF:205-206 `Find_blocks`, `Find_fine_block` | `blocks.spanning_blocks`, `blocks.add_fine_blocks` |
 | AF:207 `Build_candidate_fasta` | `partner.candidate_targets` |
 | AF:208 `contact_reads` | `splitreads.cluster_split_reads` |
 | AF:209-210 `Find_Anchored_split`, `Find_candidate_genes` | `partner.*` |
 | AF:227 `Final_fusion` | `report.write_predictions` |
 
-Searches are injectable (`Searches`):
-- the default runs everything on the GPU;
-- tests may pass the CPU oracle. It is test infrastructure and is never a fallback here.
+By default a gene runs on the device path (`run_gene_device`): the reads are uploaded once,
+S2-S6 run in HBM, and only the gathered queries (S4 pairs, S5's survivors and their S6 rows)
+are rendered as the SAM / PSL text the host stages read (`device_products` ->
+`consume_products`).  Searches and the S2 aligner are injectable: tests pass the CPU oracle,
+which takes the host path (`run_gene` -> `consume_gene`: the same stages over host buffers).
+The oracle is test infrastructure and never a fallback.
 
 The false-positive filter (AF:212-225) runs when `filt` names a model file
 (`--model_file` without `--not_filter_false_positive`): `filter_model.score_candidates` builds the
@@ -157,9 +161,9 @@ def run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, align
 
 
 def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches, out_prefix, log=print, filt=None):
-    """filt: None (`--not_filter_false_positive`) or dict(model_file=..., device=...)."""
-    """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads``."""
-    anchor_rec = [(gene, anchor)]
+    """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads`` (host buffers;
+    the searches through ``searches``).  filt: None (`--not_filter_false_positive`) or
+    dict(model_file=..., device=...)."""
     width = reads.shape[1]
 
     def seq(r):  # only the reads the partitions select are decoded
@@ -176,22 +180,36 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     # fastq restores the sequenced orientation of both ends)
     q4 = [(names[a // 2], seq(a), seq(b)) for a, b in zip(tmp1, tmp2)]
     s4 = searches.genome_sam_pe(q4) if q4 else []
-    homo = [row[3] for row in homo_rows]
     # anchored.bam as `samtools view` prints it (SEQ reverse-complemented for 0x10)
     anch_lines = []
     for r in anchored:
         cig, f = res.cigar_str(r), res.flag_at(r)
         sq = revcomp(seq(r)) if f & 0x10 else seq(r)
         anch_lines.append(sam_line(names[r // 2], f & 0xFFFF, gene, res.pos_at(r) + 1, cig, sq))
-    # S5: split reads vs the genome
+    # S5: split reads vs the genome, the genome check
     fasta = genome_check.split_read_fasta(anch_lines)
     gsam = ["@HD\tVN:1.6\n"] + [ln for recs in (searches.genome_sam_se(fasta) if fasta else []) for ln in recs]
     split_sam = genome_check.filter_genome_hits(gsam)
     log(f"[{gene}] S5: {len(fasta)} split reads, {len(split_sam)} kept")
+    # S6: the survivors' BLAT on the genome
+    _, tail_fa = blk.split_read_queries(split_sam)
+    psl = searches.place(searches.genome, tail_fa, "split_tail") if tail_fa else []
+    return consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=log,
+                            filt=filt)
+
+
+def consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=print, filt=None):
+    """S6 consumer -> S7 / S8 -> Final_fusion (AF:205-227) from the texts the genome searches
+    produce: s4 = the SAM lines of `bwa mem -M genome tmp1 tmp2` (AF:188), split_sam = the lines
+    `del_too_many_reads` keeps (fn:735, 760), psl = the PSL of S6's BLAT of their processed
+    sequences (fn:530; empty when there is none).  Both the host path (consume_gene) and the
+    device path (run_gene_device) end here."""
+    anchor_rec = [(gene, anchor)]
+    homo = [row[3] for row in homo_rows]
     blocks_chr = blk.spanning_blocks(s4, index, homo)
     tails, tail_fa = blk.split_read_queries(split_sam)
     if tail_fa:
-        blk.add_fine_blocks(blocks_chr, tails, searches.place(searches.genome, tail_fa, "split_tail"), index, homo)
+        blk.add_fine_blocks(blocks_chr, tails, psl, index, homo)
     # the reference's widening can leave a non-integer end; its next step would raise
     for c in list(blocks_chr):
         blocks_chr[c] = [b for b in blocks_chr[c] if isinstance(b.start, int) and isinstance(b.end, int)]
@@ -208,6 +226,103 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
                                              device=filt.get("device", "cpu"), log=log)
     report.write_predictions(out_prefix, cands, gene, index, scores, cnt_max, no_filter)
     return cands
+
+
+_OPS = "MIDNSHP=X"
+
+
+def device_products(d, gene, names, genome_names):
+    """The texts consume_products reads, from a discover.CandidateDiscovery pass: S4's SAM lines
+    (af_grec records rendered by genome.sam_lines), the pseudo-SAM lines of S5's survivors (the
+    `del_too_many_reads` output format, fn:735/760) and the PSL lines of S6.  Only the gathered
+    queries are decoded on the host."""
+    import numpy as np
+    import torch
+
+    from . import blat
+    from .genome import MAX_REC, REC_DTYPE, sam_lines
+    torch.cuda.synchronize(d.dev)
+    nq = min(int(d.n_q.item()), d.qcap)
+    npair = d._npair
+    q, ql, rows = d.q[:nq].cpu().numpy(), d.q_lens[:nq].cpu().numpy(), d.q_rows[:nq].cpu().numpy()
+    recs = d.q_recs[:nq * MAX_REC * REC_DTYPE.itemsize].cpu().numpy().view(REC_DTYPE).reshape(nq, MAX_REC)
+    nrec = d.q_nh[:nq].cpu().numpy()
+
+    def seq(i):
+        return q[i, :ql[i]].tobytes().decode()
+    s4 = []
+    for k in range(npair):
+        name = names[int(rows[2 * k]) // 2]
+        s4 += sam_lines(genome_names, name, seq(2 * k), recs[2 * k], nrec[2 * k])
+        s4 += sam_lines(genome_names, name, seq(2 * k + 1), recs[2 * k + 1], nrec[2 * k + 1])
+    n6 = int(d.s6["n"].item())
+    split_sam, psl = [], []
+    if n6:
+        src = d.s6["src"][:n6].cpu().numpy()
+        r = rows[2 * npair + src]
+        rr = torch.from_numpy(r.astype(np.int64)).to(d.dev)
+        pos = d.out["pos"][rr].cpu().numpy()
+        ncig = d.out["n_cigar"][rr].cpu().numpy()
+        cig = d.out["cigar"][rr].cpu().numpy().view(np.uint32)
+        for k in range(n6):
+            c = "".join(f"{int(v) >> 4}{_OPS[int(v) & 15]}" for v in cig[k, :ncig[k]])
+            split_sam.append(f"{names[int(r[k]) // 2]}\t0\t{gene}\t{int(pos[k]) + 1}\t60\t{c}\t=\t1111\t0\t"
+                             f"{seq(2 * npair + int(src[k]))}\tA\n")
+        s6q, s6l = d.s6["q"][:n6].cpu().numpy(), d.s6["lens"][:n6].cpu().numpy()
+        t_rows = d.t_rows[:n6 * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize].cpu().numpy().view(blat.PSL_DTYPE)
+        psl = ["psLayout version 3\n", "\n"] + blat.psl_lines(
+            d.tiles_ref, [(str(k), s6q[k, :s6l[k]].tobytes().decode()) for k in range(n6)],
+            t_rows.reshape(n6, blat.MAX_ROWS), d.t_nh[:n6].cpu().numpy())
+    return s4, split_sam, psl
+
+
+def run_gene_device(gene, anchor, names, reads_t, lens_t, pair_bases, index, homo_rows, searches, out_prefix,
+                    device=0, chunk_bases=10_000_000, log=print, filt=None, inflight=4, batch_chunks=240):
+    """One anchored gene on the device path: S2 (K1 + K2 + K3 per batch of bwa chunks), S3, the
+    gathers, S4 / S5, S5's genome check and S6 in HBM (discover.CandidateDiscovery), then the host
+    stages on the gathered queries only (consume_products)."""
+    from . import blat
+    from .discover import CandidateDiscovery
+    gidx = searches.genome_index()
+    tiles = searches.place.tiles(searches.genome, blat.params("split_tail").step_size)
+    n_pairs, stride = reads_t.shape[0] // 2, reads_t.shape[1]
+    d = CandidateDiscovery(anchor.encode(), gidx, tiles, n_pairs, stride, device=device, inflight=inflight,
+                           batch_chunks=batch_chunks, chunk_bases=chunk_bases, pair_bases=pair_bases)
+    try:
+        d.run(reads_t, lens_t=lens_t)
+        c = d.summary()
+        log(f"[{gene}] S2: {c['mapped_reads']} of {2 * n_pairs} reads on the anchor; {c['tmp1']} one-end-anchored "
+            f"pairs; {c['anchored']} anchored records; S5: {c['s5_split_reads']} split reads, {c['s6_queries']} kept")
+        if c["s2_overflow_reads"]:
+            log(f"[{gene}] WARNING: {c['s2_overflow_reads']} reads hit a per-read cap of the S2 restatement and "
+                f"are reported unmapped (AF_FLAG_MEM_OVERFLOW / AF_FLAG_CIGAR_OVERFLOW; bwa has no caps)")
+        caps = {k: v for k, v in c.items() if k.startswith("genome_") or k in ("s6_clipped", "s4_pairs_dropped",
+                                                                                   "s5_dropped")}
+        if any(caps.values()):
+            log(f"[{gene}] WARNING: caps reached: {caps}")
+        s4, split_sam, psl = device_products(d, gene, names, gidx.names)
+    finally:
+        d.close()
+    return consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=log,
+                            filt=filt)
+
+
+def upload_reads(reads, lens, device):
+    """The reads in HBM for the device path: rows padded to a multiple of 8 bytes (every bwa
+    chunk's batch then starts on a 16-byte boundary), their lengths, and the pairs' base counts."""
+    import numpy as np
+    import torch
+    n, width = reads.shape
+    stride = max(8, -(-width // 8) * 8)
+    host = np.full((n, stride), ord("N"), dtype=np.uint8)
+    host[:, :width] = reads
+    ln = np.full(n, width, np.int32) if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+    dev = torch.device("cuda", device)
+    reads_t = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
+    lens_t = torch.from_numpy(ln).to(dev)
+    pair_bases = ln.astype(np.int64).reshape(-1, 2).sum(axis=1)
+    torch.cuda.synchronize(dev)
+    return reads_t, lens_t, pair_bases
 
 
 def dist_world(group=None):
@@ -244,17 +359,25 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
         gtf = fh.readlines()
     index = ExonIndex.from_lines(gtf)
     names, reads, lens = read_pairs(fastq1, fastq2)
+    # the device path (S2-S6 in HBM) unless a test injects host backends
+    on_device = searches is None and aligner_factory is None
     if searches is None:
         searches = Searches(genome, device=device, chunk_bases=chunk_bases)
     if aligner_factory is None:
         aligner_factory = _default_aligner(device, chunk_bases)
+    dev_reads = upload_reads(reads, lens, device) if on_device and reads.shape[0] else None
     results = {}
     for gene, anchor in zip(genes, anchors):
         folder = os.path.join(out_folder, gene + "_fusion")
         os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
         homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
-        results[gene] = run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory,
-                                 os.path.join(folder, gene + "_fusion"), log=log, filt=filt)
+        prefix = os.path.join(folder, gene + "_fusion")
+        if dev_reads is not None:
+            results[gene] = run_gene_device(gene, anchor, names, *dev_reads, index, homo_rows, searches, prefix,
+                                            device=device, chunk_bases=chunk_bases, log=log, filt=filt)
+        else:
+            results[gene] = run_gene(gene, anchor, names, reads, lens, index, homo_rows, searches, aligner_factory,
+                                     prefix, log=log, filt=filt)
     return results
 
 
