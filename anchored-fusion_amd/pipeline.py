@@ -91,6 +91,11 @@ class Searches:
         self._gidx = None
         self.params = _lib.default_params()  # bwa mem defaults (-k 19 -T 30), as AF:188 / fn:716 run it
 
+    @property
+    def on_device(self):
+        """True when every search runs on the GPU engines (the device path can use them)."""
+        return self._gfac is None and getattr(self.place, "on_device", False)
+
     def genome_index(self):
         if self._gidx is None:
             if self._gfac is not None:
@@ -360,7 +365,7 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     index = ExonIndex.from_lines(gtf)
     names, reads, lens = read_pairs(fastq1, fastq2)
     # the device path (S2-S6 in HBM) unless a test injects host backends
-    on_device = searches is None and aligner_factory is None
+    on_device = aligner_factory is None and (searches is None or getattr(searches, "on_device", False))
     if searches is None:
         searches = Searches(genome, device=device, chunk_bases=chunk_bases)
     if aligner_factory is None:

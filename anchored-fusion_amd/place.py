@@ -50,6 +50,7 @@ class Placer:
     def __init__(self, device=0, tile_factory=None):
         from . import blat
         self.device = device
+        self.on_device = tile_factory is None   # TileReference (GPU) searches; tests inject the oracle
         self.tile_factory = tile_factory or (lambda contigs, step: blat.TileReference(contigs, step, device=device))
         self._tiles = {}
 
