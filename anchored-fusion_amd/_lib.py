@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, os.environ.get("AF_GPU_LIB", "libafgpu.so"))
 CSRC = os.path.join(HERE, "csrc")
 
 AF_OK = 0
+AF_E_INVALID, AF_E_HIP, AF_E_CAPACITY, AF_E_NOMEM, AF_E_UNSUPPORTED = -1, -2, -3, -4, -5
 AF_MAX_CIGAR = 32
 AF_MAX_READ = 320
 AF_K = 16
@@ -36,7 +37,8 @@ EXPORTS = (
     "af_align_pairs", "af_align_pairs_device", "af_seed_filter_device", "af_align_candidates_device",
     "af_last_candidates", "af_split_tails_device", "af_partition_device", "af_align_candidates_tails_device", "af_gather_reads_device", "af_blat_params_default", "af_tile_index_build",
     "af_tile_index_build_device", "af_blat", "af_blat_device", "af_blat_device_range", "af_fastq_open", "af_fastq_next", "af_fastq_export", "af_fastq_error",
-    "af_fastq_close", "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
+    "af_fastq_close", "af_fastq_part_read", "af_fastq_part_export", "af_fastq_part_error", "af_fastq_part_free",
+    "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
     "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats", "af_s5_filter_device",
 )
@@ -153,6 +155,15 @@ def lib():
     L.af_fastq_error.restype = ctypes.c_char_p
     L.af_fastq_close.argtypes = [_vp]
     L.af_fastq_close.restype = None
+    L.af_fastq_part_read.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp),
+                                     ctypes.POINTER(_i64), ctypes.POINTER(_i32), ctypes.POINTER(_i64)]
+    L.af_fastq_part_read.restype = ctypes.c_int
+    L.af_fastq_part_export.argtypes = [_vp, _i32, _vp, _vp, _vp, _i64, _vp]
+    L.af_fastq_part_export.restype = ctypes.c_int
+    L.af_fastq_part_error.argtypes = [_vp]
+    L.af_fastq_part_error.restype = ctypes.c_char_p
+    L.af_fastq_part_free.argtypes = [_vp]
+    L.af_fastq_part_free.restype = None
     _pp = ctypes.POINTER(Params)
     L.af_genome_build.argtypes = [_vp, _vp, _i64, _vp, _vp, _i32, ctypes.POINTER(_vp)]
     L.af_genome_build.restype = ctypes.c_int

@@ -243,8 +243,9 @@ struct Src {
                 if (inflateInit2(&z, -15) != Z_OK) { bad[i] = 1; continue; }
                 z.next_in = const_cast<unsigned char *>(b.data() + cstart);
                 z.avail_in = (uInt)clen;
-                z.next_out = reinterpret_cast<unsigned char *>(dec.data() + out_off[i]);
-                z.avail_out = (uInt)isize;
+                unsigned char spare;  // an empty block (the EOF marker): zlib needs a non-null output
+                z.next_out = isize ? reinterpret_cast<unsigned char *>(dec.data() + out_off[i]) : &spare;
+                z.avail_out = isize ? (uInt)isize : 1u;
                 const int rc = inflate(&z, Z_FINISH);
                 inflateEnd(&z);
                 const unsigned char *c = b.data() + b.size() - 8;
@@ -345,7 +346,249 @@ bool parse(Src &src, int64_t max_n, Batch &b) {
     return true;
 }
 
+
+// ---- sharded ingest: the records of one part of one BGZF file ---------------------------------
+// Part p of P takes the BGZF blocks whose compressed offset lies in [p S / P, (p + 1) S / P)
+// (S = file size) and owns the FASTQ records whose header starts in their inflated bytes.  Part
+// 0 starts at a record; a later part syncs on the first line that opens a 4-line record ('@'
+// header, a sequence line, a '+' line, a quality line as long as the sequence, then a header or
+// the end).  A record that runs past the part's blocks is completed from the following blocks
+// (read ahead, doubled until it fits).  Record syntax as `parse` (FASTQ only).
+
+struct BgzfBlock {
+    int64_t off;
+    int64_t bsize, isize;
+};
+
+bool bgzf_index(FILE *fp, std::vector<BgzfBlock> &blk, std::string &err) {
+    if (fseeko(fp, 0, SEEK_END) != 0) { err = "seek failed"; return false; }
+    const int64_t size = ftello(fp);
+    int64_t off = 0;
+    while (off < size) {
+        unsigned char h[64];
+        if (fseeko(fp, off, SEEK_SET) != 0) { err = "seek failed"; return false; }
+        const size_t n = fread(h, 1, sizeof h, fp);
+        const long bsize = Src::bgzf_bsize(h, n);
+        if (bsize < 26 || off + bsize > size) { err = "not a BGZF file (or a truncated block)"; return false; }
+        unsigned char t[4];
+        if (fseeko(fp, off + bsize - 4, SEEK_SET) != 0 || fread(t, 1, 4, fp) != 4) { err = "truncated BGZF block"; return false; }
+        const int64_t isize = (int64_t)t[0] | ((int64_t)t[1] << 8) | ((int64_t)t[2] << 16) | ((int64_t)t[3] << 24);
+        if (isize > 65536) { err = "corrupt BGZF block (ISIZE above 64 KiB)"; return false; }
+        blk.push_back(BgzfBlock{off, bsize, isize});
+        off += bsize;
+    }
+    return true;
+}
+
+// blocks [b0, b1) inflated (block-parallel, CRC-checked) into out
+bool bgzf_inflate(FILE *fp, const std::vector<BgzfBlock> &blk, size_t b0, size_t b1, int threads, std::vector<char> &out,
+                  std::string &err) {
+    out.clear();
+    if (b0 >= b1) return true;
+    const int64_t c0 = blk[b0].off, c1 = blk[b1 - 1].off + blk[b1 - 1].bsize;
+    std::vector<unsigned char> comp((size_t)(c1 - c0));
+    if (fseeko(fp, c0, SEEK_SET) != 0 || fread(comp.data(), 1, comp.size(), fp) != comp.size()) {
+        err = "read error";
+        return false;
+    }
+    std::vector<int64_t> o(b1 - b0 + 1, 0);
+    for (size_t i = b0; i < b1; ++i) o[i - b0 + 1] = o[i - b0] + blk[i].isize;
+    out.assign((size_t)o.back(), 0);
+    std::vector<int> bad(b1 - b0, 0);
+    auto work = [&](size_t t0, size_t step) {
+        for (size_t i = t0; i < b1 - b0; i += step) {
+            const BgzfBlock &B = blk[b0 + i];
+            const unsigned char *b = comp.data() + (B.off - c0);
+            const size_t xlen = b[10] | (b[11] << 8), cstart = 12 + xlen, clen = (size_t)B.bsize - cstart - 8;
+            z_stream z{};
+            if (inflateInit2(&z, -15) != Z_OK) { bad[i] = 1; continue; }
+            z.next_in = const_cast<unsigned char *>(b + cstart);
+            z.avail_in = (uInt)clen;
+            unsigned char spare;  // an empty block (the EOF marker) still needs room to finish
+            z.next_out = B.isize ? reinterpret_cast<unsigned char *>(out.data() + o[i]) : &spare;
+            z.avail_out = B.isize ? (uInt)B.isize : 1u;
+            const int rc = inflate(&z, Z_FINISH);
+            inflateEnd(&z);
+            const unsigned char *c = b + B.bsize - 8;
+            const uLong crc = (uLong)c[0] | ((uLong)c[1] << 8) | ((uLong)c[2] << 16) | ((uLong)c[3] << 24);
+            if (rc != Z_STREAM_END || (int64_t)z.total_out != B.isize ||
+                crc32(0L, reinterpret_cast<const Bytef *>(out.data() + o[i]), (uInt)B.isize) != crc)
+                bad[i] = 1;
+        }
+    };
+    const size_t T = std::min<size_t>((size_t)std::max(1, threads), b1 - b0);
+    std::vector<std::thread> th;
+    for (size_t k = 1; k < T; ++k) th.emplace_back(work, k, T);
+    work(0, T);
+    for (auto &x : th) x.join();
+    for (int v : bad)
+        if (v) { err = "corrupt BGZF block (inflate or CRC32)"; return false; }
+    return true;
+}
+
+// the lines of D from pos: [s, e) without the terminator ('\r' dropped); false at the end
+struct MemLines {
+    const char *d;
+    size_t n, pos = 0;
+    bool next(size_t &s, size_t &e) {
+        if (pos >= n) return false;
+        const char *nl = static_cast<const char *>(memchr(d + pos, '\n', n - pos));
+        s = pos;
+        e = nl ? (size_t)(nl - d) : n;
+        pos = nl ? e + 1 : n;
+        if (e > s && d[e - 1] == '\r') --e;
+        return true;
+    }
+};
+
+bool seq_line(const char *p, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const char c = p[i];
+        if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '.' || c == '-' || c == '*')) return false;
+    }
+    return true;
+}
+
+// the first record start at or after line start `from` (4-line check); n if none
+size_t fastq_sync(const std::vector<char> &D, size_t from) {
+    const char *d = D.data();
+    const size_t n = D.size();
+    size_t p = from;
+    while (p < n) {
+        MemLines L{d, n, p};
+        size_t s[5], e[5];
+        int got = 0;
+        while (got < 5 && L.next(s[got], e[got])) ++got;
+        if (got >= 4 && e[0] > s[0] && d[s[0]] == '@' && seq_line(d + s[1], e[1] - s[1]) && e[2] > s[2] &&
+            d[s[2]] == '+' && e[3] - s[3] == e[1] - s[1] && (got < 5 || (e[4] > s[4] && d[s[4]] == '@')))
+            return p;
+        const char *nl = static_cast<const char *>(memchr(d + p, '\n', n - p));
+        if (!nl) break;
+        p = (size_t)(nl - d) + 1;
+    }
+    return n;
+}
+
+// records with a header at [start, lim) of D into b.  1 = done, 0 = a record runs past the end
+// of D (read more), -1 = malformed (err set)
+int parse_mem(const std::vector<char> &D, size_t start, size_t lim, bool at_eof, Batch &b, std::string &err) {
+    b.clear();
+    MemLines L{D.data(), D.size(), start};
+    const char *d = D.data();
+    for (;;) {
+        size_t s, e;
+        size_t hdr;
+        for (;;) {  // header (blank lines skipped)
+            hdr = L.pos;
+            if (hdr >= lim || !L.next(s, e)) return 1;
+            if (e > s) break;
+        }
+        if (d[s] != '@') { err = "sharded ingest: expected a FASTQ '@' header"; return -1; }
+        size_t x = s + 1;
+        while (x < e && d[x] != ' ' && d[x] != '\t') ++x;
+        size_t nl = x - s - 1;
+        if (nl > 2 && d[x - 2] == '/' && d[x - 1] >= '0' && d[x - 1] <= '9') nl -= 2;  // trim_readno
+        const size_t name0 = b.names.size(), seq0 = b.seqs.size();
+        b.names.insert(b.names.end(), d + s + 1, d + s + 1 + nl);
+        b.names.push_back('\0');
+        bool plus = false;
+        while (L.next(s, e)) {
+            if (e > s && d[s] == '+') { plus = true; break; }
+            b.seqs.insert(b.seqs.end(), d + s, d + e);
+        }
+        const size_t slen = b.seqs.size() - seq0;
+        size_t ql = 0;
+        while (plus && ql < slen && L.next(s, e)) ql += e - s;
+        if (!plus || ql < slen) {
+            if (!at_eof) {  // the record continues in the next blocks
+                b.names.resize(name0);
+                b.seqs.resize(seq0);
+                return 0;
+            }
+            err = "truncated FASTQ record";
+            return -1;
+        }
+        b.name_off.push_back((int64_t)b.names.size());
+        b.seq_off.push_back((int64_t)b.seqs.size());
+        (void)hdr;
+    }
+}
+
 }  // namespace
+
+struct af_fastq_part {
+    Batch b;
+    int threads = 1;
+    std::string err;
+};
+
+static int af_fastq_part_read_impl(const char *path, int part, int parts, int threads, af_fastq_part **out,
+                                   int64_t *n_records, int32_t *max_len, int64_t *names_bytes) {
+    if (!path || !out || parts < 1 || part < 0 || part >= parts) return AF_E_INVALID;
+    af_fastq_part *f = new (std::nothrow) af_fastq_part;
+    if (!f) return AF_E_NOMEM;
+    *out = f;
+    f->threads = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    FILE *fp = fopen(path, "rb");
+    if (!fp) { f->err = std::string("cannot open ") + path; return AF_E_INVALID; }
+    std::vector<BgzfBlock> blk;
+    bool ok = bgzf_index(fp, blk, f->err);
+    if (!ok) {
+        fclose(fp);
+        f->err = std::string(path) + ": " + f->err;
+        return AF_E_UNSUPPORTED;
+    }
+    const int64_t size = blk.empty() ? 0 : blk.back().off + blk.back().bsize;
+    const int64_t lo = size * part / parts, hi = size * (part + 1) / parts;
+    size_t b0 = 0, b1 = 0;
+    while (b0 < blk.size() && blk[b0].off < lo) ++b0;
+    b1 = b0;
+    while (b1 < blk.size() && blk[b1].off < hi) ++b1;
+    size_t lim = 0;
+    for (size_t i = b0; i < b1; ++i) lim += (size_t)blk[i].isize;
+    std::vector<char> D;
+    int rc = 1;
+    for (size_t ra = 8;; ra *= 2) {
+        const size_t be = std::min(blk.size(), b1 + ra);
+        if (!bgzf_inflate(fp, blk, b0, be, f->threads, D, f->err)) { rc = -1; break; }
+        const size_t start = part == 0 ? 0 : fastq_sync(D, 0);
+        if (start >= lim) { f->b.clear(); rc = 1; break; }  // no record starts in this part
+        rc = parse_mem(D, start, lim, be == blk.size(), f->b, f->err);
+        if (rc != 0) break;
+    }
+    fclose(fp);
+    if (rc < 0) {
+        f->err = std::string(path) + ": " + f->err;
+        return AF_E_INVALID;
+    }
+    int32_t ml = 0;
+    for (int64_t i = 0; i < f->b.n(); ++i) ml = std::max<int32_t>(ml, (int32_t)(f->b.seq_off[i + 1] - f->b.seq_off[i]));
+    if (n_records) *n_records = f->b.n();
+    if (max_len) *max_len = ml;
+    if (names_bytes) *names_bytes = (int64_t)f->b.names.size();
+    return AF_OK;
+}
+
+static int af_fastq_part_export_impl(af_fastq_part *f, int32_t stride, uint8_t *seqs, int32_t *lens, char *names,
+                                     int64_t names_cap, int64_t *name_off) {
+    if (!f || stride < 0) return AF_E_INVALID;
+    const Batch &b = f->b;
+    const int64_t n = b.n();
+    if (names && (int64_t)b.names.size() > names_cap) { f->err = "names arena too small"; return AF_E_CAPACITY; }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t l = b.seq_off[i + 1] - b.seq_off[i];
+        if (l > stride) { f->err = "read longer than stride " + std::to_string(stride); return AF_E_CAPACITY; }
+        if (seqs) {
+            uint8_t *row = seqs + i * (int64_t)stride;
+            memcpy(row, b.seqs.data() + b.seq_off[i], (size_t)l);
+            memset(row + l, 'N', (size_t)(stride - l));
+        }
+        if (lens) lens[i] = (int32_t)l;
+        if (name_off) name_off[i] = b.name_off[i];
+    }
+    if (names) memcpy(names, b.names.data(), b.names.size());
+    return AF_OK;
+}
 
 struct af_fastq {
     Src src[2];
@@ -489,5 +732,32 @@ int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, 
                     int64_t *name_off) {
     return af_guard(f, [&] { return af_fastq_export_impl(f, stride, reads, lens, names, names_cap, name_off); });
 }
+
+int af_fastq_part_read(const char *path, int part, int parts, int threads, af_fastq_part **out, int64_t *n_records,
+                       int32_t *max_len, int64_t *names_bytes) {
+    try {
+        return af_fastq_part_read_impl(path, part, parts, threads, out, n_records, max_len, names_bytes);
+    } catch (const std::bad_alloc &) {
+        if (out && *out) (*out)->err = "out of host memory";
+        return AF_E_NOMEM;
+    } catch (const std::exception &ex) {
+        if (out && *out) (*out)->err = ex.what();
+        return AF_E_INVALID;
+    }
+}
+
+int af_fastq_part_export(af_fastq_part *f, int32_t stride, uint8_t *seqs, int32_t *lens, char *names, int64_t names_cap,
+                         int64_t *name_off) {
+    try {
+        return af_fastq_part_export_impl(f, stride, seqs, lens, names, names_cap, name_off);
+    } catch (const std::exception &ex) {
+        if (f) f->err = ex.what();
+        return AF_E_INVALID;
+    }
+}
+
+const char *af_fastq_part_error(const af_fastq_part *f) { return f ? f->err.c_str() : "null af_fastq_part handle"; }
+
+void af_fastq_part_free(af_fastq_part *f) { delete f; }
 
 }  // extern "C"

@@ -156,6 +156,42 @@ def iter_pairs(fq1, fq2, batch_pairs=1 << 20, threads=0):
         L.af_fastq_close(h)
 
 
+class NotBGZF(ValueError):
+    """A sharded read of input that is not BGZF (blocked gzip)."""
+
+
+def read_part(path, part, parts, threads=0):
+    """Part `part` of `parts` of ONE BGZF FASTQ file (af_fastq_part_read: the records whose header
+    starts in that share of the compressed blocks): ``(names, seqs[n, stride] uint8, lens[n]
+    int32)``.  Raises NotBGZF for other input."""
+    import ctypes
+
+    from . import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    n, ml, nb = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int64()
+    rc = L.af_fastq_part_read(os.fsencode(path), int(part), int(parts), int(threads), ctypes.byref(h), ctypes.byref(n),
+                              ctypes.byref(ml), ctypes.byref(nb))
+    try:
+        if rc == _lib.AF_E_UNSUPPORTED:
+            raise NotBGZF(L.af_fastq_part_error(h).decode(errors="replace"))
+        if rc != 0:
+            raise ValueError(L.af_fastq_part_error(h).decode(errors="replace"))
+        stride = max(int(ml.value), 1)
+        seqs = np.empty((n.value, stride), dtype=np.uint8)
+        lens = np.empty(n.value, dtype=np.int32)
+        arena = np.empty(max(int(nb.value), 1), dtype=np.uint8)
+        off = np.empty(n.value, dtype=np.int64)
+        rc = L.af_fastq_part_export(h, stride, seqs.ctypes.data, lens.ctypes.data, arena.ctypes.data, arena.size,
+                                    off.ctypes.data)
+        if rc != 0:
+            raise _lib.AFError(f"af_fastq_part_export failed (rc={rc}): {L.af_fastq_part_error(h).decode()}")
+        return Names(arena.tobytes(), off), seqs, lens
+    finally:
+        if h:
+            L.af_fastq_part_free(h)
+
+
 def read_pairs(fq1, fq2, threads=0):
     """Reads a FASTQ(.gz) pair into the pair-major layout (native reader, ``iter_pairs``).
 

@@ -22,6 +22,7 @@ n_cigar, hits and 32 CIGAR words = 76 int32 (304 B).  At configs[3] (50 M pairs 
 import numpy as np
 
 from .align import AlignResult, chunk_ends
+from .io import Names, NotBGZF, read_pairs, read_part
 from .align import partition as _partition_dense
 
 CHUNK_BASES = 10_000_000   # bwa mem's batch size (-K default) the shard boundaries respect
@@ -215,3 +216,192 @@ def align_sharded(aligner, reads, lens, rank, world, group=None, device=None, ch
     else:
         rows_t = torch.zeros((0, ROW_WORDS), dtype=torch.int32, device=dev)
     return SparseCandidates(allgatherv_device(rows_t, group).cpu().numpy(), n_pairs)
+
+
+# ---- sharded ingest (each rank parses its share of a BGZF FASTQ pair) -----------------------------
+
+def _pack(names, seqs, lens):
+    """Rows (names Names [k], seqs uint8 [r, w], lens int32 [r]) as one uint8 payload."""
+    k, r = len(names), seqs.shape[0]
+    w = seqs.shape[1] if r else 1
+    nm = [names[i].encode() + b"\0" for i in range(k)]
+    arena = b"".join(nm)
+    off = np.zeros(k, np.int64)
+    if k > 1:
+        off[1:] = np.cumsum([len(x) for x in nm])[:-1]
+    head = np.array([k, r, w, len(arena)], np.int64)
+    return np.concatenate([head.view(np.uint8), off.view(np.uint8), np.frombuffer(arena, np.uint8),
+                           np.ascontiguousarray(lens, np.int32).view(np.uint8),
+                           np.ascontiguousarray(seqs, np.uint8).reshape(-1)])
+
+
+def _unpack(buf):
+    k, r, w, na = (int(v) for v in buf[:32].view(np.int64))
+    o = 32
+    off = buf[o:o + 8 * k].view(np.int64).copy()
+    o += 8 * k
+    arena = buf[o:o + na].tobytes()
+    o += na
+    lens = buf[o:o + 4 * r].view(np.int32).copy()
+    o += 4 * r
+    seqs = buf[o:o + r * w].reshape(r, w) if r else np.zeros((0, w), np.uint8)
+    return Names(arena, off), seqs, lens
+
+
+_EMPTY = (Names(b"", np.zeros(0, np.int64)), np.zeros((0, 1), np.uint8), np.zeros(0, np.int32))
+
+
+def _exchange(payloads, group):
+    """payloads[d] (uint8 numpy) to rank d, for every d; returns the payload from every rank
+    (point-to-point over `group`, a CPU (gloo) group: sizes first, then the bytes)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    got = [None] * world
+    got[rank] = payloads[rank]
+    for step in range(1, world):
+        dst, src = (rank + step) % world, (rank - step) % world
+        out_t = torch.from_numpy(np.ascontiguousarray(payloads[dst]))
+        sz = torch.tensor([out_t.numel()], dtype=torch.int64)
+        rsz = torch.zeros(1, dtype=torch.int64)
+        for q in (dist.isend(sz, _global(dst, group), group=group), dist.irecv(rsz, _global(src, group), group=group)):
+            q.wait()
+        rbuf = torch.empty(int(rsz.item()), dtype=torch.uint8)
+        reqs = [dist.isend(out_t, _global(dst, group), group=group)] if out_t.numel() else []
+        if rbuf.numel():
+            reqs.append(dist.irecv(rbuf, _global(src, group), group=group))
+        for q in reqs:
+            q.wait()
+        got[src] = rbuf.numpy()
+    return got
+
+
+def _global(r, group):
+    import torch.distributed as dist
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+def _gather_ints(vals, group):
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.int64)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return np.stack([o.numpy() for o in out])
+
+
+def _cat_rows(parts):
+    """Concatenation of (names, seqs, lens) parts (rows padded to the widest)."""
+    parts = [p for p in parts if p[2].size]
+    if not parts:
+        return _EMPTY
+    w = max(p[1].shape[1] for p in parts)
+    rows = np.full((sum(p[1].shape[0] for p in parts), w), ord("N"), np.uint8)
+    r = 0
+    for p in parts:
+        rows[r:r + p[1].shape[0], :p[1].shape[1]] = p[1]
+        r += p[1].shape[0]
+    return Names.concat([p[0] for p in parts]), rows, np.concatenate([p[2] for p in parts])
+
+
+def chunk_carry(bases, s_in, owner, rank, chunk_bases):
+    """bwa's chunking (bseq_read: a chunk ends with the pair that brings it to >= chunk_bases
+    bases) continued over one rank's pairs.  (s_in, owner): the bases of the chunk still open at
+    this rank's first pair and the rank it started on (owner -1: none).  Returns (head, s_out,
+    owner_out): the leading pairs that belong to the open chunk and the chunk open after the
+    last pair."""
+    n = len(bases)
+    cum = np.cumsum(np.asarray(bases, dtype=np.int64))
+    head = 0
+    if owner >= 0:
+        e = int(np.searchsorted(cum, chunk_bases - s_in, side="left"))
+        if e >= n:
+            return n, s_in + (int(cum[-1]) if n else 0), owner
+        head = e + 1
+    rest = np.asarray(bases[head:], dtype=np.int64)
+    if rest.size == 0:
+        return head, 0, -1
+    ends = chunk_ends(rest, chunk_bases)
+    last0 = int(ends[-2]) if len(ends) > 1 else 0
+    tail = int(rest[last0:].sum())
+    return (head, 0, -1) if tail >= chunk_bases else (head, tail, rank)
+
+
+def read_pairs_sharded(fq1, fq2, rank, world, group=None, chunk_bases=CHUNK_BASES, threads=0):
+    """This rank's whole bwa chunks of a FASTQ pair, each rank parsing only its share of BGZF
+    input: returns (names, reads [2n, stride], lens [2n] or None, lo, n_pairs_total) for the
+    pairs [lo, lo + n) of the sample -- contiguous, on the chunk grid of the whole input, so every
+    chunk's insert-size estimate and read ids are those of one `bwa mem` run (AF:182).
+
+    Each rank reads part `rank` of both files (io.read_part: the records whose header starts in
+    its share of the BGZF blocks).  The record counts are all-gathered; every mate 2 goes to the
+    rank holding its mate 1 (point-to-point over `group`, a CPU group); bwa's chunking is carried
+    from rank to rank (chunk_carry), and the pairs that close a chunk opened on an earlier rank
+    move to that rank.  Input that is not BGZF is read whole by every rank and sliced
+    (shard_pairs).  world == 1: read_pairs."""
+    if world == 1:
+        names, reads, lens = read_pairs(fq1, fq2, threads=threads)
+        return names, reads, lens, 0, reads.shape[0] // 2
+    import torch
+    import torch.distributed as dist
+    try:
+        p1, p2 = read_part(fq1, rank, world, threads), read_part(fq2, rank, world, threads)
+        ok = 1
+    except NotBGZF:
+        ok = 0
+    if not _gather_ints([ok], group).all():
+        names, reads, lens = read_pairs(fq1, fq2, threads=threads)
+        n_all = reads.shape[0] // 2
+        pb = np.full(n_all, 2 * reads.shape[1], np.int64) if lens is None else \
+            np.asarray(lens, np.int64).reshape(-1, 2).sum(axis=1)
+        lo, hi = shard_pairs(pb, rank, world, chunk_bases)
+        return names.slice(lo, hi), reads[2 * lo:2 * hi], None if lens is None else lens[2 * lo:2 * hi], lo, n_all
+    cnt = _gather_ints([len(p1[2]), len(p2[2])], group)
+    o1 = np.concatenate([[0], np.cumsum(cnt[:, 0])]).astype(np.int64)
+    o2 = np.concatenate([[0], np.cumsum(cnt[:, 1])]).astype(np.int64)
+    if o1[-1] != o2[-1]:
+        raise ValueError(f"paired FASTQs differ in length: {int(o1[-1])} vs {int(o2[-1])} records")
+    n_all = int(o1[-1])
+    # every mate 2 to the rank that holds its mate 1
+    pay = []
+    for d in range(world):
+        a = int(max(o1[d], o2[rank]) - o2[rank])
+        b = int(min(o1[d + 1], o2[rank + 1]) - o2[rank])
+        a, b = max(a, 0), max(b, 0)
+        pay.append(_pack(p2[0].slice(a, b) if b > a else _EMPTY[0], p2[1][a:b] if b > a else _EMPTY[1],
+                         p2[2][a:b] if b > a else _EMPTY[2]))
+    n2, s2, l2 = _cat_rows([_unpack(x) for x in _exchange(pay, group)])
+    n1, s1, l1 = p1
+    n = len(l1)
+    if len(l2) != n:
+        raise RuntimeError("sharded ingest: the mate exchange lost records")
+    for i in range(n):
+        if n1[i] != n2[i]:  # bwa: "paired reads have different names"
+            raise ValueError(f'paired reads have different names: "{n1[i]}", "{n2[i]}"')
+    w = max(s1.shape[1], s2.shape[1])
+    reads = np.full((2 * n, w), ord("N"), np.uint8)
+    reads[0::2, :s1.shape[1]] = s1
+    reads[1::2, :s2.shape[1]] = s2
+    lens = np.empty(2 * n, np.int32)
+    lens[0::2], lens[1::2] = l1, l2
+    # bwa's chunks, carried from rank to rank: (open chunk's bases, the rank it started on)
+    carry = torch.tensor([0, -1], dtype=torch.int64)
+    if rank > 0:
+        dist.recv(carry, _global(rank - 1, group), group=group)
+    s_in, owner = int(carry[0]), int(carry[1])
+    head, s_out, own_out = chunk_carry(lens.reshape(-1, 2).astype(np.int64).sum(axis=1), s_in, owner, rank,
+                                       chunk_bases)
+    if rank + 1 < world:
+        dist.send(torch.tensor([s_out, own_out], dtype=torch.int64), _global(rank + 1, group), group=group)
+    # the leading pairs close a chunk opened on rank `owner`: they move there
+    pay = [_pack(*_EMPTY)] * world
+    if head:
+        pay = list(pay)
+        pay[owner] = _pack(n1.slice(0, head), reads[:2 * head], lens[:2 * head])
+    got = _exchange(pay, group)
+    mine = (n1.slice(head, n), reads[2 * head:], lens[2 * head:])
+    names, reads, lens = _cat_rows([mine] + [_unpack(got[src]) for src in range(rank + 1, world)])
+    lo = int(o1[rank]) + head
+    if reads.shape[0]:
+        reads = np.ascontiguousarray(reads[:, :max(1, int(lens.max()))])
+    return names, reads, (None if (lens == reads.shape[1]).all() else lens), lo, n_all

@@ -352,6 +352,21 @@ int af_fastq_export(af_fastq *f, int32_t stride, uint8_t *reads, int32_t *lens, 
                     int64_t *name_off);
 const char *af_fastq_error(const af_fastq *f);
 void af_fastq_close(af_fastq *f);
+/* Sharded ingest (one process per GPU, cli --gpus N): part `part` of `parts` of ONE BGZF FASTQ
+ * file -- the records whose header starts in the BGZF blocks at compressed offsets
+ * [part S / parts, (part + 1) S / parts) of the file (S its size); a record that continues into
+ * the next blocks is completed from them, and a part after the first starts at the first line
+ * that opens a 4-line FASTQ record.  The parts of a file hold every record once, in order.
+ * Returns AF_E_UNSUPPORTED (handle set, message in af_fastq_part_error) for input that is not
+ * BGZF; then every rank reads the whole file (af_fastq_*).  Export: rows of `stride` bytes
+ * ('N'-padded), lens[n], the names (trim_readno applied) in one arena with an offset per record. */
+typedef struct af_fastq_part af_fastq_part;
+int af_fastq_part_read(const char *path, int part, int parts, int threads, af_fastq_part **out, int64_t *n_records,
+                       int32_t *max_len, int64_t *names_bytes);
+int af_fastq_part_export(af_fastq_part *p, int32_t stride, uint8_t *seqs, int32_t *lens, char *names, int64_t names_cap,
+                         int64_t *name_off);
+const char *af_fastq_part_error(const af_fastq_part *p);
+void af_fastq_part_free(af_fastq_part *p);
 
 #ifdef __cplusplus
 }
