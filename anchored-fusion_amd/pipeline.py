@@ -399,16 +399,23 @@ def _default_aligner(device, chunk_bases):
 
 def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device, searches,
                  aligner_factory, log, group, rank, world, filt=None, chunk_bases=10_000_000):
+    """cli --gpus N: every rank ingests its share of the FASTQ pair (shard.read_pairs_sharded:
+    BGZF parts, whole bwa chunks per rank) and runs S2 on it; the candidate pairs' records, reads
+    and names are exchanged (shard.align_local); rank 0 runs S3-S8 on them, exactly as one
+    process over the whole sample would."""
     import torch
     import torch.distributed as dist
     from . import shard
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
-    names, reads, lens = read_pairs(fastq1, fastq2)
+    on_gpu = torch.cuda.is_available() and dist.get_backend(group) == "nccl"
+    host_group = dist.new_group(backend="gloo") if on_gpu else group
+    names, reads, lens, lo, n_pairs = shard.read_pairs_sharded(fastq1, fastq2, rank, world, group=host_group,
+                                                               chunk_bases=chunk_bases)
+    log(f"[rank {rank}] ingested pairs {lo} .. {lo + reads.shape[0] // 2} of {n_pairs}")
     if aligner_factory is None:
         aligner_factory = _default_aligner(device, chunk_bases)
-    on_gpu = torch.cuda.is_available() and dist.get_backend(group) == "nccl"
     dev = f"cuda:{device}" if on_gpu else None
     genome = gtf = index = None
     if rank == 0:
@@ -422,8 +429,8 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
     for gene, anchor in zip(genes, anchors):
         aligner = aligner_factory(anchor.encode())
         try:
-            res = shard.align_sharded(aligner, reads, lens, rank, world, group=group, device=dev,
-                                      chunk_bases=chunk_bases)
+            res, cand = shard.align_local(aligner, reads, lens, lo, n_pairs, names, group=group, host_group=host_group,
+                                          device=dev)
         finally:
             close = getattr(aligner, "close", None)
             if close:
@@ -433,7 +440,8 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
             os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
             log(f"[{gene}] S2 over {world} ranks: {len(res.reads)} candidate records gathered")
             homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
-            results[gene] = consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, searches,
+            results[gene] = consume_gene(gene, anchor, cand.names, cand, cand.lens, res, index, homo_rows, searches,
                                          os.path.join(folder, gene + "_fusion"), log=log, filt=filt)
-    dist.barrier(group)
+    # the end-of-run sync on the CPU group (rank 0 may be busy long after the others finish S2)
+    dist.barrier(host_group)
     return results

@@ -3,7 +3,8 @@ inside a gloo process group of 2 ranks, with the oracle backends.  The tables ra
 must equal the single-process run's byte for byte (S2 sharded on the chunk grid + the
 candidate all-gatherv for bulk; cells dealt out to the ranks for single-cell).
 
-The read-name columns list Python sets, as the reference does (functions.py Final_fusion), so
+Bulk input in BGZF is parsed in parts, one per rank (shard.read_pairs_sharded); plain gzip is
+read whole by every rank.  The read-name columns list Python sets, as the reference does (functions.py Final_fusion), so
 their order follows the interpreter's string hash seed: both runs are spawned with the same
 PYTHONHASHSEED."""
 import os
@@ -68,6 +69,36 @@ def test_pipeline_two_ranks_equals_single(tmp_path):
     for t in ("BCRX_fusion_predictions.txt", "BCRX_fusion_predictions_abridged.txt"):
         a = open(os.path.join(one, "BCRX_fusion", t), "rb").read()
         b = open(os.path.join(two, "BCRX_fusion", t), "rb").read()
+        assert a == b and len(a.splitlines()) > 1, t
+
+
+def _bgzf_copy(paths, d):
+    """The world's FASTQ pair rewritten as BGZF (bgzip's layout): the sharded ingest then splits it."""
+    import gzip
+    from multiprocessing import Pool
+
+    from cells_world import write_bgzf
+    os.makedirs(d, exist_ok=True)
+    out = dict(paths)
+    with Pool(4) as pool:
+        for k in ("fq1", "fq2"):
+            data = gzip.open(paths[k], "rb").read()
+            out[k] = os.path.join(d, os.path.basename(paths[k]))
+            write_bgzf(out[k], data, pool)
+    return out
+
+
+def test_pipeline_three_ranks_bgzf_equals_single(tmp_path):
+    """BGZF input: each rank parses only its part of both files (sharded ingest), S2 on its whole
+    chunks, the candidates' records / reads / names exchanged; rank 0's tables equal one process's."""
+    paths, _ = make_world(str(tmp_path / "world"))
+    paths = _bgzf_copy(paths, str(tmp_path / "bgzf"))
+    one, three = str(tmp_path / "one"), str(tmp_path / "three")
+    _spawn(paths, one, "bulk", world=1)
+    _spawn(paths, three, "bulk", world=3)
+    for t in ("BCRX_fusion_predictions.txt", "BCRX_fusion_predictions_abridged.txt"):
+        a = open(os.path.join(one, "BCRX_fusion", t), "rb").read()
+        b = open(os.path.join(three, "BCRX_fusion", t), "rb").read()
         assert a == b and len(a.splitlines()) > 1, t
 
 
