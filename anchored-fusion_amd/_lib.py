@@ -41,6 +41,7 @@ EXPORTS = (
     "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
     "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats", "af_s5_filter_device",
+    "af_genome_align_se_ids_device",
 )
 AF_G_MAX_REC = 8
 AF_GSTAT_N = 4
@@ -179,6 +180,8 @@ def lib():
     L.af_genome_read.restype = ctypes.c_int
     L.af_genome_align_se_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _i64, _vp, _vp, _vp]
     L.af_genome_align_se_device.restype = ctypes.c_int
+    L.af_genome_align_se_ids_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _vp, _vp, _vp, _vp]
+    L.af_genome_align_se_ids_device.restype = ctypes.c_int
     L.af_genome_align_pe_device.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _vp, _vp, _vp]
     L.af_genome_align_pe_device.restype = ctypes.c_int
     L.af_genome_align_se.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _pp, _pe, _i64, _vp, _vp]
@@ -189,8 +192,8 @@ def lib():
     L.af_genome_regions.restype = ctypes.c_int
     L.af_genome_stats.argtypes = [_vp, _vp]
     L.af_genome_stats.restype = ctypes.c_int
-    L.af_s5_filter_device.argtypes = [_vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, ctypes.POINTER(AlnOut), _i64, _vp, _i32,
-                                      _vp, _vp, _vp, _vp, _vp]
+    L.af_s5_filter_device.argtypes = [_vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, ctypes.POINTER(AlnOut), _vp, _i64, _vp,
+                                      _i32, _vp, _vp, _vp, _vp, _vp]
     L.af_s5_filter_device.restype = ctypes.c_int
     _L = L
     return L

@@ -225,9 +225,9 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                                     uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
                                     uint8_t *zscratch, hipStream_t s);
 hipError_t af_launch_genome_se(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
-                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const GWork &w,
-                               uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs, int32_t *n_rec,
-                               hipStream_t s);
+                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const int64_t *ids,
+                               const GWork &w, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs,
+                               int32_t *n_rec, hipStream_t s);
 hipError_t af_launch_genome_pe(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
                                const int32_t *d_npairs, int64_t cap_pairs, const af_params &p, const GOpt &o,
                                const GWork &w, const S2Work &sw, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch,
@@ -273,7 +273,8 @@ size_t af_gather_temp_bytes(int64_t n_rows);
 // s5s6.hip: the genome check of the split reads (fn:718-768) and the S6 query rows (fn:512-528)
 size_t af_s5_temp_bytes(int64_t n);
 hipError_t af_launch_s5_filter(const af_grec *recs, const int32_t *n_rec, int64_t n, const uint8_t *q, int32_t q_stride,
-                               const int32_t *q_lens, const int32_t *q_rows, const af_aln_out &s2, int64_t cap,
+                               const int32_t *q_lens, const int32_t *q_rows, const af_aln_out &s2, const uint8_t *cont,
+                               int64_t cap,
                                uint8_t *out, int32_t out_stride, int32_t *out_lens, int32_t *out_src, int32_t *n_out,
                                int32_t *n_over, uint8_t *keep, int32_t *sel, int64_t *n_sel, void *temp,
                                size_t temp_bytes, hipStream_t s);

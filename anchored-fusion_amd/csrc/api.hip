@@ -1119,9 +1119,9 @@ static GOpt genome_opt(const af_pe *e) {
                 e->pair_base};
 }
 
-int af_genome_align_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
-                              const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
-                              af_grec *d_recs, int32_t *d_n_rec, void *stream) {
+static int genome_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                            const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
+                            const int64_t *d_ids, af_grec *d_recs, int32_t *d_n_rec, void *stream) {
     int rc = check_genome_call(c, g, p, pe, stride);
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!d_reads || !d_recs || !d_n_rec))) return fail(c, AF_E_INVALID, "null argument");
@@ -1133,9 +1133,22 @@ int af_genome_align_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_re
     const GWork w = genome_work(c);
     HIPCHK(c, af_launch_genome_regions(g->dev, d_reads, stride, d_lens, nullptr, n, *p, o, w, c->g1_scr, c->g1_threads,
                                        c->g2_scr, c->g2_waves, c->zscratch, s));
-    HIPCHK(c, af_launch_genome_se(g->dev, d_reads, stride, d_lens, nullptr, n, *p, id_base, w, c->g2_scr, c->g2_waves,
-                                  c->zscratch, d_recs, d_n_rec, s));
+    HIPCHK(c, af_launch_genome_se(g->dev, d_reads, stride, d_lens, nullptr, n, *p, id_base, d_ids, w, c->g2_scr,
+                                  c->g2_waves, c->zscratch, d_recs, d_n_rec, s));
     return AF_OK;
+}
+
+int af_genome_align_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                              const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
+                              af_grec *d_recs, int32_t *d_n_rec, void *stream) {
+    return genome_se_device(c, g, d_reads, n, stride, d_lens, p, pe, id_base, nullptr, d_recs, d_n_rec, stream);
+}
+
+int af_genome_align_se_ids_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                                  const int32_t *d_lens, const af_params *p, const af_pe *pe, const int64_t *d_ids,
+                                  af_grec *d_recs, int32_t *d_n_rec, void *stream) {
+    if (n > 0 && !d_ids) return fail(c, AF_E_INVALID, "null argument");
+    return genome_se_device(c, g, d_reads, n, stride, d_lens, p, pe, 0, d_ids, d_recs, d_n_rec, stream);
 }
 
 int af_genome_align_pe_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs,
@@ -1282,8 +1295,8 @@ int af_genome_stats(af_ctx *c, int32_t *out) {
 
 int af_s5_filter_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
                         const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
-                        const af_aln_out *d_s2, int64_t cap, uint8_t *d_s6, int32_t s6_stride, int32_t *d_s6_lens,
-                        int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream) {
+                        const af_aln_out *d_s2, const uint8_t *d_cont, int64_t cap, uint8_t *d_s6, int32_t s6_stride,
+                        int32_t *d_s6_lens, int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream) {
     if (!c || !d_s2 || !d_n6) return fail(c, AF_E_INVALID, "null argument");
     if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
     if (n_queries > 0 && (!d_recs || !d_n_rec || !d_q || !d_q_lens || !d_q_rows || !d_s2->flag || !d_s2->pos ||
@@ -1304,7 +1317,7 @@ int af_s5_filter_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec
         c->s5_cap = n;
     }
     if (!c->s5_nsel) HIPCHK(c, hipMalloc(&c->s5_nsel, sizeof(int64_t)));
-    HIPCHK(c, af_launch_s5_filter(d_recs, d_n_rec, n_queries, d_q, q_stride, d_q_lens, d_q_rows, *d_s2, cap, d_s6,
+    HIPCHK(c, af_launch_s5_filter(d_recs, d_n_rec, n_queries, d_q, q_stride, d_q_lens, d_q_rows, *d_s2, d_cont, cap, d_s6,
                                   s6_stride, d_s6_lens, d_s6_src, d_n6, d_n_over, c->s5_keep, c->s5_sel, c->s5_nsel, c->s5_temp,
                                   c->s5_temp_bytes, (hipStream_t)stream));
     return AF_OK;

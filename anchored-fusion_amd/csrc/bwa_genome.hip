@@ -1116,7 +1116,8 @@ __device__ int g_reg2sam(const DevGenome &G, const af_params &p, int l, const GR
 template <int CPL>
 __global__ __launch_bounds__(64, 2) void k_g_se(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
                                                 const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
-                                                int64_t cap, af_params p, int64_t id_base, GWork w,
+                                                int64_t cap, af_params p, int64_t id_base,
+                                                const int64_t *__restrict__ ids, GWork w,
                                                 uint8_t *__restrict__ scr_base, size_t scr_stride,
                                                 uint8_t *__restrict__ zscratch, size_t zstride,
                                                 af_grec *__restrict__ recs, int32_t *__restrict__ n_rec) {
@@ -1132,7 +1133,7 @@ __global__ __launch_bounds__(64, 2) void k_g_se(DevGenome G, const uint8_t *__re
         const int na = ovf ? 0 : nr;
         for (int k = lane; k < na; k += 64) S.reg[k] = w.reg[w.reg_off[r] + k];
         wave_sync();
-        if (lane == 0) g_mark_primary(S.reg, na, id_base + r, p, S.kept);
+        if (lane == 0) g_mark_primary(S.reg, na, ids ? ids[r] : id_base + r, p, S.kept);
         g_load_read(reads, r, stride, l, lane);
         af_grec *out = recs + r * AF_G_MAX_REC;
         const int nrec = g_reg2sam<CPL>(G, p, l, S.reg, na, 0, nullptr, (int32_t)r, out, zg, lane);
@@ -1539,13 +1540,13 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
 }
 
 hipError_t af_launch_genome_se(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
-                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const GWork &w,
-                               uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs, int32_t *n_rec,
-                               hipStream_t s) {
+                               const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const int64_t *ids,
+                               const GWork &w, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs,
+                               int32_t *n_rec, hipStream_t s) {
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C) hipLaunchKernelGGL((k_g_se<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap, p, \
-                                    id_base, w, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec)
+                                    id_base, ids, w, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);

@@ -103,6 +103,7 @@ struct S5In {
     const int32_t *q_rows;  // the read row of each S5 query (S2 record index)
     const int32_t *flag, *pos, *n_cigar;
     const uint32_t *cigar;
+    const uint8_t *cont;    // optional: cont[q] != 0 when query q continues the QNAME group of q - 1
 };
 
 // QNAME of query q: read name (the pair: row >> 1), gene, POS, CIGAR of the anchored record
@@ -115,6 +116,12 @@ __device__ bool same_qname(const S5In &in, int64_t a, int64_t b) {
     return true;
 }
 
+// query u continues the group of u - 1: the caller's flags (a shard of a wider query list,
+// whose neighbours in the global order are known to the caller), else the QNAMEs compared
+__device__ bool continues(const S5In &in, int64_t u) {
+    return in.cont ? in.cont[u] != 0 : same_qname(in, u - 1, u);
+}
+
 __device__ bool query_bad(const S5In &in, int64_t q, const NOp *bf, int nb) {
     const int nr = in.n_rec[q] < AF_G_MAX_REC ? in.n_rec[q] : AF_G_MAX_REC;
     for (int k = 0; k < nr; ++k)
@@ -125,12 +132,12 @@ __device__ bool query_bad(const S5In &in, int64_t q, const NOp *bf, int nb) {
 __global__ void k_s5_check(S5In in, int64_t n, uint8_t *__restrict__ keep) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= n) return;
-    if (q > 0 && same_qname(in, q - 1, q)) { keep[q] = 0; return; }
+    if (q > 0 && continues(in, q)) { keep[q] = 0; return; }
     const int r = in.q_rows[q];
     NOp bf[NOPS];
     const int nb = deal_ops(bf, parse_ops(in.cigar + (int64_t)r * AF_MAX_CIGAR, in.n_cigar[r], false, bf));
     bool bad = query_bad(in, q, bf, nb);
-    for (int64_t u = q + 1; !bad && u < n && same_qname(in, q, u); ++u) bad = query_bad(in, u, bf, nb);
+    for (int64_t u = q + 1; !bad && u < n && continues(in, u); ++u) bad = query_bad(in, u, bf, nb);
     keep[q] = bad ? 0 : 1;
 }
 
@@ -214,13 +221,14 @@ size_t af_s5_temp_bytes(int64_t n) {
 }
 
 hipError_t af_launch_s5_filter(const af_grec *recs, const int32_t *n_rec, int64_t n, const uint8_t *q, int32_t q_stride,
-                               const int32_t *q_lens, const int32_t *q_rows, const af_aln_out &s2, int64_t cap,
+                               const int32_t *q_lens, const int32_t *q_rows, const af_aln_out &s2, const uint8_t *cont,
+                               int64_t cap,
                                uint8_t *out, int32_t out_stride, int32_t *out_lens, int32_t *out_src, int32_t *n_out,
                                int32_t *n_over, uint8_t *keep, int32_t *sel, int64_t *n_sel, void *temp,
                                size_t temp_bytes, hipStream_t s) {
     hipError_t e;
     if (n_over && (e = hipMemsetAsync(n_over, 0, sizeof(int32_t), s)) != hipSuccess) return e;
-    const S5In in{recs, n_rec, q_rows, s2.flag, s2.pos, s2.n_cigar, s2.cigar};
+    const S5In in{recs, n_rec, q_rows, s2.flag, s2.pos, s2.n_cigar, s2.cigar, cont};
     if (n <= 0) {
         if ((e = hipMemsetAsync(n_sel, 0, sizeof(int64_t), s)) != hipSuccess) return e;
     } else {

@@ -170,6 +170,16 @@ class GenomeIndex:
             ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), int(id_base),
             recs_t.data_ptr(), nrec_t.data_ptr(), _stream_handle(stream)), "af_genome_align_se_device")
 
+    def align_se_ids_device(self, reads_t, n, stride, ids_t, recs_t, nrec_t, lens_t=None, params=None, pe=None,
+                            stream=None, ctx=None):
+        """S5 on a shard of a query list: read r's bwa id is ids_t[r] (int64, its ordinal in the
+        whole list), which decides mem_mark_primary_se's hash tie-breaks."""
+        c = self.ctx if ctx is None else ctx
+        _lib.check(c, _lib.lib().af_genome_align_se_ids_device(
+            c, self.g, reads_t.data_ptr(), int(n), int(stride), None if lens_t is None else lens_t.data_ptr(),
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), ids_t.data_ptr(),
+            recs_t.data_ptr(), nrec_t.data_ptr(), _stream_handle(stream)), "af_genome_align_se_ids_device")
+
     def align_pe_device(self, reads_t, n_pairs, stride, lens_t, recs_t, nrec_t, params=None, pe=None, stream=None,
                         ctx=None):
         c = self.ctx if ctx is None else ctx
@@ -187,18 +197,21 @@ class GenomeIndex:
 
 
 def s5_filter_device(ctx, recs_t, nrec_t, n, q_t, q_stride, q_lens_t, q_rows_t, s2_out, cap, s6_t, s6_lens_t,
-                     s6_src_t, n6_t, n_over_t=None, stream=None):
+                     s6_src_t, n6_t, n_over_t=None, stream=None, cont_t=None):
     """af_s5_filter_device: the genome check of the n S5 queries (`del_too_many_reads`,
     functions.py:718-768) and the S6 query rows of the survivors (fn:506-528) on the device.
     s2_out: the S2 record tensors (flag / pos / score / n_cigar / hits / cigar) the queries' rows
     index; s6_t uint8 [cap, stride], s6_lens_t / s6_src_t int32 [cap], n6_t int32 [1]; n_over_t
-    (int32 [1], optional) counts rows whose processed sequence was clipped to the stride."""
+    (int32 [1], optional) counts rows whose processed sequence was clipped to the stride; cont_t
+    (uint8 [n], optional): the QNAME groups given by the caller (cont_t[q] != 0: query q continues
+    the group of q - 1), for a shard of a wider query list."""
     if int(s6_t.shape[0]) < cap or s6_lens_t.numel() < cap or s6_src_t.numel() < cap:
         raise ValueError("S6 buffers hold fewer than cap rows")
     o = _lib.AlnOut(*(s2_out[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
     _lib.check(ctx, _lib.lib().af_s5_filter_device(
         ctx, recs_t.data_ptr(), nrec_t.data_ptr(), int(n), q_t.data_ptr(), int(q_stride), q_lens_t.data_ptr(),
-        q_rows_t.data_ptr(), ctypes.byref(o), int(cap), s6_t.data_ptr(), int(s6_t.shape[1]), s6_lens_t.data_ptr(),
+        q_rows_t.data_ptr(), ctypes.byref(o), None if cont_t is None else cont_t.data_ptr(), int(cap), s6_t.data_ptr(),
+        int(s6_t.shape[1]), s6_lens_t.data_ptr(),
         s6_src_t.data_ptr(), n6_t.data_ptr(), None if n_over_t is None else n_over_t.data_ptr(),
         _stream_handle(stream)), "af_s5_filter_device")
 

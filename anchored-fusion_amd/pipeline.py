@@ -169,6 +169,14 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     """S3-S8 + Final_fusion (AF:183-227) on the S2 records ``res`` of ``reads`` (host buffers;
     the searches through ``searches``).  filt: None (`--not_filter_false_positive`) or
     dict(model_file=..., device=...)."""
+    s4, split_sam, psl = host_products(gene, names, reads, lens, res, searches, log=log)
+    return consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=log,
+                            filt=filt)
+
+
+def host_products(gene, names, reads, lens, res, searches, log=print):
+    """S3 -> S6 over host buffers: (the SAM lines of S4, the split_sam lines S5's check keeps,
+    S6's PSL lines), the texts consume_products reads."""
     width = reads.shape[1]
 
     def seq(r):  # only the reads the partitions select are decoded
@@ -199,8 +207,7 @@ def consume_gene(gene, anchor, names, reads, lens, res, index, homo_rows, search
     # S6: the survivors' BLAT on the genome
     _, tail_fa = blk.split_read_queries(split_sam)
     psl = searches.place(searches.genome, tail_fa, "split_tail") if tail_fa else []
-    return consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=log,
-                            filt=filt)
+    return s4, split_sam, psl
 
 
 def consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=print, filt=None):

@@ -291,11 +291,16 @@ int64_t af_genome_primary(const af_genome *g);
  * (what = 1, int64, rows 0..2 l_pac) to host memory (tests) */
 int af_genome_read(af_ctx *ctx, const af_genome *g, int32_t what, int64_t first, int64_t n, void *out);
 /* S5 (single-end): records of reads [0, n) (`stride` bytes per row, d_lens may be NULL) into
- * d_recs[r * AF_G_MAX_REC + k] for k < d_n_rec[r]; read ids id_base + r (bwa's hash tie-breaks).
+ * d_recs[r * AF_G_MAX_REC + k] for k < d_n_rec[r]; read ids id_base + r (bwa's hash tie-breaks),
+ * or d_ids[r] with af_genome_align_se_ids_device (a shard of a query list: the reads' ordinals in
+ * the whole list).
  * Device buffers, asynchronous on `stream`; calls on one context must be stream-ordered. */
 int af_genome_align_se_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
                               const int32_t *d_lens, const af_params *p, const af_pe *pe, int64_t id_base,
                               af_grec *d_recs, int32_t *d_n_rec, void *stream);
+int af_genome_align_se_ids_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n, int32_t stride,
+                                  const int32_t *d_lens, const af_params *p, const af_pe *pe, const int64_t *d_ids,
+                                  af_grec *d_recs, int32_t *d_n_rec, void *stream);
 /* S4 (paired-end): pair-major reads [0, 2 n_pairs) with their lengths (d_lens required); every
  * record of read 2i + m at d_recs[(2i + m) * AF_G_MAX_REC ..]; pe->chunk_bases / pair_base as for
  * af_align_pairs (insert-size statistics per bwa chunk). */
@@ -324,7 +329,9 @@ int af_genome_stats(af_ctx *ctx, int32_t *out);
  * d_n_rec) and the S2 records d_s2 of af_align_*_device (FLAG / POS / CIGAR of the anchored
  * read).  A query is dropped when a genome record aligns it as one deal_cigar operation or a
  * genome M straddles the end of an anchored M by more than 20 % of it on both sides; records are
- * grouped by consecutive QNAME (pair, POS, CIGAR), as the reference's file walk groups them.
+ * grouped by consecutive QNAME (pair, POS, CIGAR), as the reference's file walk groups them, or,
+ * when d_cont is given (one process's share of a query list sharded over GPUs), by the caller's
+ * flags: d_cont[q] != 0 when query q continues the group of query q - 1.
  * Each survivor, in query order, becomes S6 query row k of d_s6 (s6_stride bytes): deal_cigar's
  * processed SEQ (N for each deleted base, inserted bases removed), d_s6_lens[k] (clipped to
  * s6_stride; the clipped rows are counted in *d_n_over, which may be NULL), d_s6_src[k] = its S5
@@ -332,8 +339,8 @@ int af_genome_stats(af_ctx *ctx, int32_t *out);
  * on `stream`. */
 int af_s5_filter_device(af_ctx *ctx, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
                         const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
-                        const af_aln_out *d_s2, int64_t cap, uint8_t *d_s6, int32_t s6_stride, int32_t *d_s6_lens,
-                        int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream);
+                        const af_aln_out *d_s2, const uint8_t *d_cont, int64_t cap, uint8_t *d_s6, int32_t s6_stride,
+                        int32_t *d_s6_lens, int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as

@@ -227,6 +227,9 @@ def _glib():
         L.afo_genome_align_se.restype = ctypes.c_int
         L.afo_genome_align_se.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe), i64,
                                           ctypes.c_int, i32, vp, vp]
+        L.afo_genome_align_se_ids.restype = ctypes.c_int
+        L.afo_genome_align_se_ids.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe), vp,
+                                              ctypes.c_int, i32, vp, vp]
         L.afo_genome_align_pe.restype = ctypes.c_int
         L.afo_genome_align_pe.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe),
                                           ctypes.c_int, i32, vp, vp]
@@ -295,17 +298,26 @@ class OracleGenome:
             raise RuntimeError(f"afo_genome_regions failed: {rc}")
         return regs, nreg
 
-    def align_se(self, reads, lens=None, params=None, pe=None, id_base=0, threads=0, max_rec=G_MAX_REC):
-        """S5: (records [n, max_rec] GREC_DTYPE, counts [n])."""
+    def align_se(self, reads, lens=None, params=None, pe=None, id_base=0, threads=0, max_rec=G_MAX_REC, ids=None):
+        """S5: (records [n, max_rec] GREC_DTYPE, counts [n]); read ids id_base + r, or ids[r]."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)
         n = reads.shape[0]
         recs = np.zeros((n, max_rec), dtype=GREC_DTYPE)
         nrec = np.zeros(n, dtype=np.int32)
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
-        rc = _glib().afo_genome_align_se(self.h, reads.ctypes.data, n, reads.shape[1],
-                                         None if lp is None else lp.ctypes.data, ctypes.byref(params or default_params()),
-                                         ctypes.byref(pe or default_pe()), int(id_base), int(threads), max_rec,
-                                         recs.ctypes.data, nrec.ctypes.data)
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, dtype=np.int64)
+            rc = _glib().afo_genome_align_se_ids(self.h, reads.ctypes.data, n, reads.shape[1],
+                                                 None if lp is None else lp.ctypes.data,
+                                                 ctypes.byref(params or default_params()),
+                                                 ctypes.byref(pe or default_pe()), ids.ctypes.data, int(threads),
+                                                 max_rec, recs.ctypes.data, nrec.ctypes.data)
+        else:
+            rc = _glib().afo_genome_align_se(self.h, reads.ctypes.data, n, reads.shape[1],
+                                             None if lp is None else lp.ctypes.data,
+                                             ctypes.byref(params or default_params()),
+                                             ctypes.byref(pe or default_pe()), int(id_base), int(threads), max_rec,
+                                             recs.ctypes.data, nrec.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"afo_genome_align_se failed: {rc}")
         return recs, nrec

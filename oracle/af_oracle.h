@@ -111,6 +111,9 @@ int afo_genome_regions(const afo_genome *G, const uint8_t *reads, int64_t n, int
 int afo_genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
                         const afo_params *p, const afo_pe *pe, int64_t id_base, int n_threads, int32_t max_rec,
                         afo_grec *recs, int32_t *n_rec);
+int afo_genome_align_se_ids(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                            const afo_params *p, const afo_pe *pe, const int64_t *ids, int n_threads, int32_t max_rec,
+                            afo_grec *recs, int32_t *n_rec);
 int afo_genome_align_pe(const afo_genome *G, const uint8_t *reads, int64_t n_pairs, int32_t stride, const int32_t *lens,
                         const afo_params *p, const afo_pe *pe, int n_threads, int32_t max_rec, afo_grec *recs,
                         int32_t *n_rec);

@@ -1999,10 +1999,11 @@ int afo_genome_align_pe(const afo_genome *G, const uint8_t *reads, int64_t n_pai
     return align_pairs_text(G, NULL, reads, n_pairs, stride, lens, p, pe, n_threads, NULL, recs, max_rec, n_rec);
 }
 
-/* S5: `bwa mem -M genome reads.fa` (single-end), read ids id_base + r */
-int afo_genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
-                        const afo_params *p, const afo_pe *pe_in, int64_t id_base, int n_threads, int32_t max_rec,
-                        afo_grec *recs, int32_t *n_rec) {
+/* S5: `bwa mem -M genome reads.fa` (single-end), read ids id_base + r, or ids[r] when ids is given
+ * (a shard of a wider query list: the reads' ordinals in that list) */
+static int genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                           const afo_params *p, const afo_pe *pe_in, int64_t id_base, const int64_t *ids, int n_threads,
+                           int32_t max_rec, afo_grec *recs, int32_t *n_rec) {
     afo_pe pe;
     if (pe_in) pe = *pe_in;
     else afo_pe_default(&pe);
@@ -2016,13 +2017,25 @@ int afo_genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, in
         int l = read_codes(reads, r, stride, lens, q);
         regv_t rg = {NULL, 0, 0};
         int ovf = align1_core(G, p, &pe, q, l, &rg) < 0;
-        mark_primary_se(p, rg.n, rg.a, id_base + r);
+        mark_primary_se(p, rg.n, rg.a, ids ? ids[r] : id_base + r);
         n_rec[r] = reg2sam(G, p, l, q, &rg, 0, NULL, (int32_t)r, recs + r * max_rec, max_rec);
         if (ovf || n_rec[r] > max_rec)
             for (int j = 0; j < (n_rec[r] < max_rec ? n_rec[r] : max_rec); ++j) recs[r * max_rec + j].flag |= FLAG_MEM_OVERFLOW;
         free(rg.a);
     }
     return 0;
+}
+
+int afo_genome_align_se(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                        const afo_params *p, const afo_pe *pe_in, int64_t id_base, int n_threads, int32_t max_rec,
+                        afo_grec *recs, int32_t *n_rec) {
+    return genome_align_se(G, reads, n, stride, lens, p, pe_in, id_base, NULL, n_threads, max_rec, recs, n_rec);
+}
+
+int afo_genome_align_se_ids(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                            const afo_params *p, const afo_pe *pe_in, const int64_t *ids, int n_threads, int32_t max_rec,
+                            afo_grec *recs, int32_t *n_rec) {
+    return genome_align_se(G, reads, n, stride, lens, p, pe_in, 0, ids, n_threads, max_rec, recs, n_rec);
 }
 
 /* mem_collect_intv + mem_chain's occurrence sampling for one read, as the seed list mem_chain
