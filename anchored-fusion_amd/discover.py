@@ -116,22 +116,11 @@ class CandidateDiscovery:
         stream after S2, S3, the gathers and the genome searches."""
         import torch
         G = self.grp.inflight
-        s0 = self.grp.streams[0]
-        done = None
-        for gi, k0 in enumerate(range(0, len(self.batches), G)):
-            group = self.batches[k0:k0 + G]
-            specs = []
-            for p, n in group:
-                r0, r1 = 2 * p, 2 * (p + n)
-                specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()},
-                              None if lens_t is None else lens_t[r0:r1], self.pair_base + p))
-            done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done)
+        s0 = self._s2(reads_t, lens_t, k1_events)
         # S6 runs on slot 1's stream (the tile index has its own context and scratch; slot 1 is
         # idle once S2 is done -- a stream of its own would share one of the 4 hardware queues
         # (GPU_MAX_HW_QUEUES) with a slot and serialise behind its S2 work) beside S4.
         s6 = self.grp.streams[1] if G > 1 else s0
-        for e in done:
-            s0.wait_event(e)
         if _DEBUG:
             s0.synchronize()
             _log("S2 done")
@@ -196,6 +185,118 @@ class CandidateDiscovery:
                            s4_pairs_dropped=max(0, min(n1, n2) - npair), s5_dropped=max(0, nq_all - nq))
         self._npair = npair
         return s0
+
+    def _s2(self, reads_t, lens_t=None, k1_events=None):
+        """S2 over every batch (K1s of a group back to back, then their K2 + K3 on the slots);
+        returns slot 0's stream, which waits for all of it."""
+        G = self.grp.inflight
+        s0 = self.grp.streams[0]
+        done = None
+        for gi, k0 in enumerate(range(0, len(self.batches), G)):
+            group = self.batches[k0:k0 + G]
+            specs = []
+            for p, n in group:
+                r0, r1 = 2 * p, 2 * (p + n)
+                specs.append((reads_t[r0:r1], n, self.L, {k: v[r0:r1] for k, v in self.out.items()},
+                              None if lens_t is None else lens_t[r0:r1], self.pair_base + p))
+            done = self.grp.run_device(specs, events=None if k1_events is None else k1_events[gi], wait=done)
+        for e in done or ():
+            s0.wait_event(e)
+        return s0
+
+    # ---- one rank of a sharded sample: the phases dist_discover drives --------------------------
+    def attach(self, reads_t, lens_t=None, k1_events=None):
+        """The reads (this rank's whole chunks, pairs pair_base ..) the phases below run on;
+        k1_events as run() takes them."""
+        self._in = (reads_t, lens_t, k1_events)
+        return self
+
+    def local_phase(self):
+        """S2 + S3 + the gathers of this rank: tmp1 reads at query rows [0, n1), tmp2 at [n1, n1 +
+        n2) (both as sequenced), the split reads (S5 queries, SAM orientation) after them."""
+        import numpy as np
+        import torch
+
+        from .dist_discover import LocalQueries
+        reads_t, lens_t, k1_events = self._in
+        s0 = self._s2(reads_t, lens_t, k1_events)
+        al = self.grp.aligners[0]
+        t1, t2, an, cnt = al.partition_device(self.out["flag"], self.out["pos"], outs=self.s3, stream=s0)
+        s0.synchronize()
+        n1, n2, na = (int(v) for v in cnt.cpu())
+        if n1 + n2 + na > self.qcap:
+            self._alloc_queries(int((n1 + n2 + na) * 1.25) + 1024)
+        al.gather_reads_device(reads_t, self.L, t1, n1, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens, self.q_rows,
+                               None, lens_t=lens_t, first=0, step=1, stream=s0)
+        al.gather_reads_device(reads_t, self.L, t2, n2, _lib.AF_GATHER_SEQUENCED, self.q, self.q_lens, self.q_rows,
+                               None, lens_t=lens_t, first=n1, step=1, stream=s0)
+        al.gather_reads_device(reads_t, self.L, an, na, _lib.AF_GATHER_SPLIT_SAM, self.q, self.q_lens, self.q_rows,
+                               self.n_q, out_t=self.out, lens_t=lens_t, first=n1 + n2, step=1, stream=s0)
+        s0.synchronize()
+        b = n1 + n2
+        n5 = max(0, min(int(self.n_q.item()), self.qcap) - b)
+        self._lay = (n1, n2, n5)
+        rows = self.q_rows[:b + n5].long()
+        pos = self.out["pos"][rows]
+        key = (pos.long() * 2 + ((self.out["flag"][rows] >> 4) & 1).long()).cpu().numpy()
+        q = self.q[:b + n5].cpu().numpy()
+        ql = self.q_lens[:b + n5].cpu().numpy()
+        r = rows.cpu().numpy()
+        seq = [q[i, :ql[i]] for i in range(b + n5)]
+        cig = self.out["cigar"][rows[b:]].cpu().numpy().view(np.uint32) if n5 else np.zeros((0, 32), np.uint32)
+        self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s5_split_reads=n5)
+        return LocalQueries(
+            dict(key=key[:n1], row=r[:n1], seq=seq[:n1], len=ql[:n1]),
+            dict(key=key[n1:b], row=r[n1:b], seq=seq[n1:b], len=ql[n1:b]),
+            dict(key=key[b:], row=r[b:], pos=pos[b:].cpu().numpy(), ncig=self.out["n_cigar"][rows[b:]].cpu().numpy(),
+                 cigar=cig, seq=seq[b:], len=ql[b:]))
+
+    def s5_s6_phase(self, ids, cont):
+        """S5 with the queries' global ids, its genome check with the given QNAME groups, S6."""
+        import numpy as np
+        import torch
+        n1, n2, n5 = self._lay
+        b = n1 + n2
+        s0 = self.grp.streams[0]
+        pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
+        recs = self.q_recs.view(torch.int32)
+        w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+        ids_t = torch.from_numpy(np.ascontiguousarray(ids, np.int64)).to(self.dev)
+        cont_t = torch.from_numpy(np.ascontiguousarray(cont, np.uint8)).to(self.dev)
+        if n5:
+            self.ref.align_se_ids_device(self.q[b:], n5, self.L, ids_t, recs[b * w:], self.q_nh[b:],
+                                         lens_t=self.q_lens[b:], params=self.p_genome, pe=pe, stream=s0)
+        _genome.s5_filter_device(self.ref.ctx, recs[b * w:], self.q_nh[b:], n5, self.q[b:], self.L, self.q_lens[b:],
+                                 self.q_rows[b:], self.out, self.qcap, self.s6["q"], self.s6["lens"], self.s6["src"],
+                                 self.s6["n"], self.s6["over"], stream=s0, cont_t=cont_t)
+        self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
+                                     lens_t=self.s6["lens"], p=self.p_tail, stream=s0)
+        s0.synchronize()
+        n6 = int(self.s6["n"].item())
+        q6, l6 = self.s6["q"][:n6].cpu().numpy(), self.s6["lens"][:n6].cpu().numpy()
+        rows = self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
+        rows = rows.reshape(n6, _blat.MAX_ROWS) if n6 else rows.reshape(0, _blat.MAX_ROWS)
+        self.counts["s6_queries"] = n6
+        return dict(src=self.s6["src"][:n6].cpu().numpy(), s6_seq=[q6[k, :l6[k]] for k in range(n6)],
+                    psl=[rows[k] for k in range(n6)], n_psl=self.t_nh[:n6].cpu().numpy())
+
+    def s4_phase(self, q, ql):
+        """S4 over the globally zipped pairs (rank 0): reads q uint8 [2P, w] pair-major, lens ql."""
+        import numpy as np
+        import torch
+        P2 = q.shape[0]
+        qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.dev)
+        lt = torch.from_numpy(np.ascontiguousarray(ql, np.int32)).to(self.dev)
+        recs_t = torch.zeros(P2 * MAX_REC * _genome.REC_DTYPE.itemsize // 4, dtype=torch.int32, device=self.dev)
+        nrec_t = torch.zeros(P2, dtype=torch.int32, device=self.dev)
+        s0 = self.grp.streams[0]
+        self.ref.align_pe_device(qt, P2 // 2, q.shape[1], lt, recs_t, nrec_t, params=self.p_genome,
+                                 pe=_lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0), stream=s0)
+        s0.synchronize()
+        return recs_t.cpu().numpy().view(_genome.REC_DTYPE).reshape(P2, MAX_REC), nrec_t.cpu().numpy()
+
+    def psl_lines(self, queries, rows, nrows):
+        return _blat.psl_lines(self.tiles_ref, queries, rows, nrows)
 
     def summary(self):
         """Host-side counts of the last pass (synchronises)."""

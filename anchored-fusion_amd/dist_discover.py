@@ -14,17 +14,19 @@ over the WHOLE sample, and three things depend on that order:
 So the ranks all-gather the sort keys of their tmp1 / tmp2 / split-read lists (samtools' key:
 2 pos + strand, ties by the global read row -- the rank order), which gives every rank each of
 its split reads' global ordinal and whether its predecessor in the global order has the same
-QNAME (then both are the same pair's mates, on the same rank).  S5, its check and S6 then run on
+QNAME (then both are mates of one pair, on the same rank).  S5, its check and S6 then run on
 every rank over its own queries with those ids and group flags (`af_genome_align_se_ids_device`,
 `af_s5_filter_device` with d_cont); S4 runs on rank 0 over the globally zipped pairs, whose reads
-the ranks send there.  Rank 0 gathers the survivors and their S6 rows, orders them by ordinal
-and returns the texts `pipeline.consume_products` reads.  The result is the one-process run's,
-byte for byte (tests/test_dist_discover.py).
+the ranks send there.  Rank 0 gathers the survivors and their S6 rows and orders them by
+ordinal.  `search` stops there (the bench step); `render` turns the result into the texts
+`pipeline.consume_products` reads, equal to the one-process run's byte for byte
+(tests/test_dist_discover.py).
 
 The per-rank work is done by a backend with three phases -- `local_phase` (S2 + S3 + the
 gathers), `s4_phase` (rank 0) and `s5_s6_phase` -- implemented by discover.CandidateDiscovery
-on the GPU; the tests also run the CPU oracle through the same driver.  Host data moves over
-`host_group`, a CPU (gloo) group.
+on the GPU; the tests run the CPU oracle through the same driver.  Every exchange is a tensor
+all-gatherv (counts, then one max-padded all_gather) on `device` over `group`: RCCL on GPUs,
+gloo on CPU; read names (for `render` only) go over `host_group` as objects.
 """
 import numpy as np
 
@@ -42,8 +44,9 @@ class LocalQueries:
     """A rank's lists after S2 + S3 + the gathers (host arrays; rows are local read rows).
 
     t1 / t2: the tmp1 / tmp2 rows in samtools order with their keys (2 pos + strand) and the reads
-    as sequenced (seqs [k, w], lens); s5: the split reads (the S5 queries) in order with keys, the
-    anchored record's POS and CIGAR (words, n), and the queries' SEQ in SAM orientation."""
+    as sequenced (seq uint8 [k, w], len); s5: the split reads (the S5 queries) in order with keys,
+    the anchored record's POS and CIGAR (cigar uint32 [k, 32], ncig), and the queries' SEQ in SAM
+    orientation (seq uint8 [k, w], len)."""
 
     def __init__(self, t1, t2, s5):
         self.t1, self.t2, self.s5 = t1, t2, s5
@@ -54,104 +57,212 @@ def merge_order(keys, rows):
     return np.lexsort((np.asarray(rows, np.int64), np.asarray(keys, np.int64)))
 
 
-def _all_gather(obj, group):
+def _allgatherv(arr, group, device):
+    """All-gatherv of a 2-D numpy array (rows) over `group` on `device`; the rows of every rank
+    in rank order (numpy)."""
+    import torch
     import torch.distributed as dist
-    out = [None] * dist.get_world_size(group)
-    dist.all_gather_object(out, obj, group=group)
+    from .shard import allgatherv_device
+    a = np.ascontiguousarray(arr)
+    if dist.get_world_size(group) == 1:
+        return a
+    width = a.dtype.itemsize * int(np.prod(a.shape[1:]))
+    t = torch.from_numpy(a.view(np.uint8).reshape(a.shape[0], width)).to(device)
+    return allgatherv_device(t, group).cpu().numpy().view(a.dtype).reshape(-1, *a.shape[1:])
+
+
+def _pad_rows(rows, w):
+    out = np.full((len(rows), w), ord("N"), np.uint8)
+    for i, r in enumerate(rows):
+        out[i, :len(r)] = r
     return out
 
 
-def _gather0(obj, group):
-    import torch.distributed as dist
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
-    out = [None] * world if rank == 0 else None
-    dist.gather_object(obj, out, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+def _i32(a):
+    return np.asarray(a, np.int64).astype(np.int32).reshape(-1, 1)
+
+
+def _u8(x):
+    """A sequence as uint8 (bytes, str or an array)."""
+    if isinstance(x, str):
+        return np.frombuffer(x.encode(), np.uint8)
+    if isinstance(x, (bytes, bytearray)):
+        return np.frombuffer(bytes(x), np.uint8)
+    return np.asarray(x, np.uint8)
+
+
+PSL_WORDS = 82  # af_psl / blat.PSL_DTYPE as int32 words (328 B)
+
+
+def psl_table(surv, ords):
+    """S6's rows of the survivors as int32 rows: ordinal (2 words) + one af_psl row."""
+    from .blat import PSL_DTYPE
+    parts = []
+    for k, o in enumerate(ords):
+        m = int(surv["n_psl"][k])
+        if m <= 0:
+            continue
+        r = np.ascontiguousarray(np.asarray(surv["psl"][k])[:m]).view(PSL_DTYPE)
+        parts.append(np.concatenate([np.full((m, 1), int(o), np.int64).view(np.int32).reshape(m, 2),
+                                     r.view(np.int32).reshape(m, PSL_WORDS)], axis=1))
+    return np.concatenate(parts) if parts else np.zeros((0, 2 + PSL_WORDS), np.int32)
+
+
+def psl_rows(table, n, npsl):
+    """table (ordinal-sorted psl_table rows of n survivors) -> per survivor a PSL_DTYPE array of
+    MAX_ROWS rows (the first npsl[k] valid)."""
+    from .blat import MAX_ROWS, PSL_DTYPE
+    out = np.zeros((n, MAX_ROWS), PSL_DTYPE)
+    r = 0
+    for k in range(n):
+        m = max(0, int(npsl[k]))
+        if m:
+            out[k, :m] = table[r:r + m, 2:].copy().view(PSL_DTYPE).reshape(m)
+        r += m
     return out
 
 
-def run(backend, lo, names, gene, genome_names, rank, world, host_group, log=print):
-    """S3-S6 of one gene over the ranks (backend already holds this rank's S2 input).  names: the
-    rank's pair names (local pair index).  Returns (s4 SAM lines, split_sam lines, S6 PSL lines)
-    on rank 0, None elsewhere, plus this rank's step counts."""
+def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_group=None):
+    """The distributed S3-S6 of one gene (backend already holds this rank's S2 input).  Returns,
+    on rank 0, dict(s4=(pair reads, lens, records, counts, t1 global rows), surv=(ordinal-sorted
+    survivor rows), psl=(their S6 rows), names=...) -- see render -- and None elsewhere, plus this
+    rank's counts.  names (the rank's pair names, optional: render needs them) are sent to rank 0
+    for the reads the texts name (S4's tmp1 reads, the survivors) over host_group."""
     L = backend.local_phase()
     g0 = 2 * int(lo)
-    mine = dict(t1=(L.t1["key"], L.t1["row"] + g0), t2=(L.t2["key"], L.t2["row"] + g0),
-                s5=(L.s5["key"], L.s5["row"] + g0))
-    every = _all_gather(mine, host_group) if world > 1 else [mine]
-    # S5: global ordinals (bwa's read ids in split.fa) and QNAME groups
-    k5 = np.concatenate([e["s5"][0] for e in every])
-    r5 = np.concatenate([e["s5"][1] for e in every])
-    o5 = merge_order(k5, r5)
-    pos_of = np.empty(len(o5), np.int64)
-    pos_of[o5] = np.arange(len(o5))
-    base = sum(len(e["s5"][0]) for e in every[:rank])
+
+    def kr(d):
+        return np.stack([np.asarray(d["key"], np.int64), np.asarray(d["row"], np.int64) + g0], axis=1) \
+            if len(d["key"]) else np.zeros((0, 2), np.int64)
+    # the lists' keys, every rank (S5 ids and groups; S4's global zip on rank 0)
+    K5 = _allgatherv(kr(L.s5), group, device)
+    n_before = _allgatherv(np.array([[len(L.s5["key"])]], np.int64), group, device)[:, 0]
+    o5 = merge_order(K5[:, 0], K5[:, 1])
+    ordinal = np.empty(len(o5), np.int64)
+    ordinal[o5] = np.arange(len(o5))
+    base = int(n_before[:rank].sum())
     n5 = len(L.s5["key"])
-    ids = pos_of[base:base + n5]
-    prev = np.full(n5, -1, np.int64)  # the global predecessor, as a local index when it is ours
-    loc_of = {int(r): i for i, r in enumerate(L.s5["row"] + g0)}
-    for i in range(n5):
-        if ids[i] > 0:
-            prev[i] = loc_of.get(int(r5[o5[ids[i] - 1]]), -1)
+    ids = ordinal[base:base + n5]
     cont = np.zeros(n5, np.uint8)
+    rows5 = np.asarray(L.s5["row"], np.int64) + g0
+    local_of = {int(r): i for i, r in enumerate(rows5)}
     for i in range(n5):
-        j = prev[i]
-        if j >= 0:
-            a, b = int(L.s5["row"][j]), int(L.s5["row"][i])
-            cont[i] = a // 2 == b // 2 and L.s5["pos"][j] == L.s5["pos"][i] and \
-                L.s5["ncig"][j] == L.s5["ncig"][i] and \
-                np.array_equal(L.s5["cigar"][j, :L.s5["ncig"][j]], L.s5["cigar"][i, :L.s5["ncig"][i]])
+        if ids[i] == 0:
+            continue
+        j = local_of.get(int(K5[o5[ids[i] - 1], 1]), -1)  # the global predecessor, when it is ours
+        if j < 0:
+            continue
+        a, b = int(L.s5["row"][j]), int(L.s5["row"][i])
+        cont[i] = a // 2 == b // 2 and L.s5["pos"][j] == L.s5["pos"][i] and L.s5["ncig"][j] == L.s5["ncig"][i] and \
+            np.array_equal(L.s5["cigar"][j, :L.s5["ncig"][j]], L.s5["cigar"][i, :L.s5["ncig"][i]])
     surv = backend.s5_s6_phase(ids, cont)
-    # the survivors to rank 0: ordinal, QNAME line fields, the S6 query and its rows
-    rows_out = []
-    for k, src in enumerate(surv["src"]):
-        src = int(src)
-        r = int(L.s5["row"][src])
-        rows_out.append((int(ids[src]), names[r // 2], int(L.s5["pos"][src]) + 1,
-                         cigar_string(L.s5["cigar"][src], L.s5["ncig"][src]), L.s5["seq"][src], surv["s6_seq"][k],
-                         surv["psl"][k], int(surv["n_psl"][k])))
-    # S4's reads to rank 0: the rank's tmp1 / tmp2 reads (sequenced orientation) with their rows
-    s4_mine = dict(t1=(L.t1["row"] + g0, L.t1["seq"], L.t1["len"], [names[int(r) // 2] for r in L.t1["row"]]),
-                   t2=(L.t2["row"] + g0, L.t2["seq"], L.t2["len"]))
-    got = _gather0((rows_out, s4_mine), host_group) if world > 1 else [(rows_out, s4_mine)]
-    counts = dict(tmp1=len(L.t1["key"]), tmp2=len(L.t2["key"]), s5_split_reads=n5, s6_queries=len(surv["src"]))
+    # the survivors (ordinal, POS, CIGAR, S5 SEQ, S6 query) and their S6 rows, to every rank
+    src = np.asarray(surv["src"], np.int64)
+    ns = len(src)
+    w5 = max(1, int(max((len(x) for x in L.s5["seq"]), default=1)))
+    w6 = max(1, int(max((len(x) for x in surv["s6_seq"]), default=1)))
+    w5, w6 = -(-w5 // 4) * 4, -(-w6 // 4) * 4
+    s5b = _pad_rows([_u8(L.s5["seq"][int(k)]) for k in src], w5)
+    s6b = _pad_rows([_u8(x) for x in surv["s6_seq"]], w6)
+    W5 = _allgatherv(np.array([[w5, w6]], np.int64), group, device).max(axis=0)
+    s5b = np.pad(s5b, ((0, 0), (0, int(W5[0]) - w5)), constant_values=ord("N"))
+    s6b = np.pad(s6b, ((0, 0), (0, int(W5[1]) - w6)), constant_values=ord("N"))
+    ords = ids[src] if ns else np.zeros(0, np.int64)
+    cig = np.asarray(L.s5["cigar"], np.uint32)[src] if ns else np.zeros((0, 32), np.uint32)
+    rows = np.concatenate([
+        ords.astype(np.int64).view(np.int32).reshape(-1, 2) if ns else np.zeros((0, 2), np.int32),
+        _i32(np.asarray(L.s5["pos"])[src] if ns else []), _i32(np.asarray(L.s5["ncig"])[src] if ns else []),
+        cig.view(np.int32).reshape(-1, 32),
+        _i32([len(L.s5["seq"][int(k)]) for k in src]), _i32([len(x) for x in surv["s6_seq"]]),
+        _i32(surv["n_psl"]), s5b.view(np.int32).reshape(ns, int(W5[0]) // 4),
+        s6b.view(np.int32).reshape(ns, int(W5[1]) // 4),
+        # the read's global row (render: names)
+        (rows5[src] if ns else np.zeros(0, np.int64)).view(np.int32).reshape(-1, 2)], axis=1)
+    psl = psl_table(surv, ords)
+    all_rows = _allgatherv(rows.astype(np.int32), group, device)
+    all_psl = _allgatherv(psl, group, device)
+    # S4's reads: the rank's tmp1 / tmp2 reads with their keys and global rows
+    w4 = max(1, int(max((len(_u8(x)) for x in list(L.t1["seq"]) + list(L.t2["seq"])), default=1)))
+    W4 = int(_allgatherv(np.array([[w4]], np.int64), group, device).max())
+    W4 = -(-W4 // 4) * 4
+
+    def reads_rows(d):
+        k = len(d["key"])
+        if not k:
+            return np.zeros((0, 5 + W4 // 4), np.int32)
+        return np.concatenate([np.stack([np.asarray(d["key"], np.int64), np.asarray(d["row"], np.int64) + g0],
+                                        axis=1).view(np.int32).reshape(k, 4), _i32(d["len"]),
+                               _pad_rows([_u8(x) for x in d["seq"]], W4).view(np.int32).reshape(k, W4 // 4)], axis=1)
+    T1 = _allgatherv(reads_rows(L.t1), group, device)
+    T2 = _allgatherv(reads_rows(L.t2), group, device)
+    counts = dict(tmp1=len(L.t1["key"]), tmp2=len(L.t2["key"]), s5_split_reads=n5, s6_queries=ns)
+    named = None
+    if names is not None:
+        want = list(np.asarray(L.t1["row"], np.int64)) + [int(r) - g0 for r in (rows5[src] if ns else [])]
+        mine = {int(r) + g0: names[int(r) // 2] for r in want}
+        if world > 1:
+            import torch.distributed as dist
+            parts = [None] * world
+            dist.all_gather_object(parts, mine, group=host_group)
+            named = {k: v for p in parts for k, v in p.items()}
+        else:
+            named = mine
     if rank != 0:
         return None, counts
-    # S4 on rank 0 over the globally zipped lists
-    k1 = np.concatenate([e["t1"][0] for e in every])
-    r1 = np.concatenate([e["t1"][1] for e in every])
-    k2 = np.concatenate([e["t2"][0] for e in every])
-    r2 = np.concatenate([e["t2"][1] for e in every])
-    o1, o2 = merge_order(k1, r1), merge_order(k2, r2)
-    n_pair = min(len(o1), len(o2))
-    seqs, lens, pname = {}, {}, {}
-    for _, s4 in got:
-        for rr, sq, ln, nm in zip(s4["t1"][0], s4["t1"][1], s4["t1"][2], s4["t1"][3]):
-            seqs[int(rr)], lens[int(rr)], pname[int(rr)] = sq, int(ln), nm
-        for rr, sq, ln in zip(s4["t2"][0], s4["t2"][1], s4["t2"][2]):
-            seqs[int(rr)], lens[int(rr)] = sq, int(ln)
-    s4_lines = []
+
+    def split_reads(T):
+        kg = T[:, :4].copy().view(np.int64).reshape(-1, 2)
+        o = merge_order(kg[:, 0], kg[:, 1])
+        seq = T[o, 5:].copy().view(np.uint8).reshape(len(o), -1)
+        return kg[o, 1], T[o, 4], seq
+    g1, l1, q1 = split_reads(T1)
+    g2, l2, q2 = split_reads(T2)
+    n_pair = min(len(g1), len(g2))
+    q = np.full((2 * n_pair, W4), ord("N"), np.uint8)
+    ql = np.zeros(2 * n_pair, np.int32)
     if n_pair:
-        a_rows = [int(r1[o1[k]]) for k in range(n_pair)]
-        b_rows = [int(r2[o2[k]]) for k in range(n_pair)]
-        w = max(max(len(seqs[r]) for r in a_rows), max(len(seqs[r]) for r in b_rows))
-        q = np.full((2 * n_pair, w), ord("N"), np.uint8)
-        ql = np.empty(2 * n_pair, np.int32)
-        for k, (a, b) in enumerate(zip(a_rows, b_rows)):
-            q[2 * k, :len(seqs[a])], q[2 * k + 1, :len(seqs[b])] = seqs[a], seqs[b]
-            ql[2 * k], ql[2 * k + 1] = lens[a], lens[b]
+        q[0::2], q[1::2] = q1[:n_pair], q2[:n_pair]
+        ql[0::2], ql[1::2] = l1[:n_pair], l2[:n_pair]
         recs, nrec = backend.s4_phase(q, ql)
-        for k, a in enumerate(a_rows):
+    else:
+        recs, nrec = None, np.zeros(0, np.int32)
+    order = np.argsort(all_rows[:, :2].copy().view(np.int64).reshape(-1), kind="stable")
+    pk = all_psl[:, :2].copy().view(np.int64).reshape(-1)
+    porder = np.argsort(pk, kind="stable")
+    counts["s4_pairs"] = n_pair
+    return dict(s4=(q, ql, recs, nrec, g1[:n_pair]), surv=all_rows[order], psl=all_psl[porder],
+                w=(int(W5[0]), int(W5[1])), names=named), counts
+
+
+def render(result, backend, gene, genome_names):
+    """The texts consume_products reads, from search's rank-0 result (searched with names): S4's
+    SAM lines, the split_sam lines of the survivors (split.fa order) and S6's PSL."""
+    q, ql, recs, nrec, g1 = result["s4"]
+    named = result["names"]
+    s4 = []
+    if len(g1):
+        pn = [named[int(g)] for g in g1]
+        for k in range(len(g1)):
             sa = q[2 * k, :ql[2 * k]].tobytes().decode()
             sb = q[2 * k + 1, :ql[2 * k + 1]].tobytes().decode()
-            s4_lines += sam_lines(genome_names, pname[a], sa, recs[2 * k], nrec[2 * k])
-            s4_lines += sam_lines(genome_names, pname[a], sb, recs[2 * k + 1], nrec[2 * k + 1])
-    # the survivors in split.fa order: split_sam lines and S6's PSL (ids = ordinals)
-    surv_all = sorted((x for rows, _ in got for x in rows), key=lambda x: x[0])
-    split_sam = [f"{nm}\t0\t{gene}\t{pos}\t60\t{cig}\t=\t1111\t0\t{seq}\tA\n"
-                 for _, nm, pos, cig, seq, _, _, _ in surv_all]
-    psl = []
-    if surv_all:
-        psl = PSL_HEADER + backend.psl_lines([(str(k), x[5]) for k, x in enumerate(surv_all)],
-                                             [x[6] for x in surv_all], [x[7] for x in surv_all])
-    counts["s4_pairs"] = n_pair
-    return (s4_lines, split_sam, psl), counts
+            s4 += sam_lines(genome_names, pn[k], sa, recs[2 * k], nrec[2 * k])
+            s4 += sam_lines(genome_names, pn[k], sb, recs[2 * k + 1], nrec[2 * k + 1])
+    S = result["surv"]
+    w5, w6 = result["w"]
+    n = S.shape[0]
+    split_sam, psl = [], []
+    if n:
+        pos, ncig = S[:, 2], S[:, 3]
+        cig = S[:, 4:36].copy().view(np.uint32)
+        l5, l6, npsl = S[:, 36], S[:, 37], S[:, 38]
+        s5 = S[:, 39:39 + w5 // 4].copy().view(np.uint8).reshape(n, w5)
+        s6 = S[:, 39 + w5 // 4:39 + (w5 + w6) // 4].copy().view(np.uint8).reshape(n, w6)
+        grow = S[:, 39 + (w5 + w6) // 4:].copy().view(np.int64).reshape(-1)
+        qn = [named[int(g)] for g in grow]
+        for k in range(n):
+            split_sam.append(f"{qn[k]}\t0\t{gene}\t{int(pos[k]) + 1}\t60\t{cigar_string(cig[k], ncig[k])}\t=\t1111\t0\t"
+                             f"{s5[k, :l5[k]].tobytes().decode()}\tA\n")
+        rows = psl_rows(result["psl"], n, npsl)
+        psl = PSL_HEADER + backend.psl_lines([(str(k), s6[k, :l6[k]].tobytes().decode()) for k in range(n)], rows,
+                                             npsl)
+    return s4, split_sam, psl

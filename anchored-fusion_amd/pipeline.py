@@ -349,7 +349,7 @@ def dist_world(group=None):
 
 
 def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=None, device=0, searches=None,
-        aligner_factory=None, log=print, group=None, filt=None, chunk_bases=10_000_000):
+        aligner_factory=None, log=print, group=None, filt=None, chunk_bases=10_000_000, backend_factory=None):
     """All genes of --file_anchored_cds; writes <out>/<G>_fusion/<G>_fusion_predictions*.txt.
 
     Inside a torch.distributed job of N > 1 ranks (cli --gpus N: one process per GPU, `device`
@@ -358,11 +358,12 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     S3-S8 and writes the tables, the other ranks return {}.
 
     chunk_bases: bwa's input chunk, 10,000,000 x --thread (AF:182/188 `bwa mem -t T`): S2 and S4
-    estimate insert sizes per chunk, so the records depend on it as the reference's do."""
+    estimate insert sizes per chunk, so the records depend on it as the reference's do.
+    backend_factory (sharded runs): the per-rank dist_discover backend, default gpu_backend."""
     rank, world = dist_world(group)
     if world > 1:
         return _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device,
-                            searches, aligner_factory, log, group, rank, world, filt, chunk_bases)
+                            searches, aligner_factory, log, group, rank, world, filt, chunk_bases, backend_factory)
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
@@ -404,15 +405,30 @@ def _default_aligner(device, chunk_bases):
     return factory
 
 
+def gpu_backend(device, chunk_bases=10_000_000, inflight=4, batch_chunks=240):
+    """The default per-rank backend of dist_discover: discover.CandidateDiscovery over the rank's
+    reads uploaded to its GPU, with the rank's genome index and tiles (built once per rank)."""
+    def make(anchor, reads, lens, lo, searches, gene):
+        from . import blat
+        from .discover import CandidateDiscovery
+        reads_t, lens_t, pair_bases = upload_reads(reads, lens, device)
+        d = CandidateDiscovery(anchor.encode(), searches.genome_index(),
+                               searches.place.tiles(searches.genome, blat.params("split_tail").step_size),
+                               reads_t.shape[0] // 2, reads_t.shape[1], device=device, inflight=inflight,
+                               batch_chunks=batch_chunks, pair_base=lo, chunk_bases=chunk_bases, pair_bases=pair_bases)
+        return d.attach(reads_t, lens_t)
+    return make
+
+
 def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names, device, searches,
-                 aligner_factory, log, group, rank, world, filt=None, chunk_bases=10_000_000):
+                 aligner_factory, log, group, rank, world, filt=None, chunk_bases=10_000_000, backend_factory=None):
     """cli --gpus N: every rank ingests its share of the FASTQ pair (shard.read_pairs_sharded:
-    BGZF parts, whole bwa chunks per rank) and runs S2 on it; the candidate pairs' records, reads
-    and names are exchanged (shard.align_local); rank 0 runs S3-S8 on them, exactly as one
-    process over the whole sample would."""
+    BGZF parts, whole bwa chunks per rank) and runs S2-S6 on it with the global order of one run
+    (dist_discover: S5's read ids and QNAME groups from all-gathered sort keys, S4 on rank 0 over
+    the globally zipped tmp1 / tmp2 lists); rank 0 renders the texts and runs the host stages."""
     import torch
     import torch.distributed as dist
-    from . import shard
+    from . import dist_discover, shard
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
@@ -421,34 +437,36 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
     names, reads, lens, lo, n_pairs = shard.read_pairs_sharded(fastq1, fastq2, rank, world, group=host_group,
                                                                chunk_bases=chunk_bases)
     log(f"[rank {rank}] ingested pairs {lo} .. {lo + reads.shape[0] // 2} of {n_pairs}")
-    if aligner_factory is None:
-        aligner_factory = _default_aligner(device, chunk_bases)
-    dev = f"cuda:{device}" if on_gpu else None
-    genome = gtf = index = None
+    genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
+    gtf = index = None
     if rank == 0:
-        genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
         with open(ref_ann) as fh:
             gtf = fh.readlines()
         index = ExonIndex.from_lines(gtf)
-        if searches is None:
-            searches = Searches(genome, device=device, chunk_bases=chunk_bases)
+    if searches is None:
+        searches = Searches(genome, device=device, chunk_bases=chunk_bases)
+    make = backend_factory or gpu_backend(device, chunk_bases)
+    dev = torch.device("cuda", device) if on_gpu else torch.device("cpu")
     results = {}
     for gene, anchor in zip(genes, anchors):
-        aligner = aligner_factory(anchor.encode())
+        backend = make(anchor, reads, lens, lo, searches, gene)
         try:
-            res, cand = shard.align_local(aligner, reads, lens, lo, n_pairs, names, group=group, host_group=host_group,
-                                          device=dev)
+            res, counts = dist_discover.search(backend, lo, rank, world, group=group, device=dev, names=names,
+                                               host_group=host_group)
+            log(f"[{gene}] rank {rank}: {counts}")
+            if rank == 0:
+                s4, split_sam, psl = dist_discover.render(res, backend, gene, [n for n, _ in genome])
         finally:
-            close = getattr(aligner, "close", None)
+            close = getattr(backend, "close", None)
             if close:
                 close()
         if rank == 0:
             folder = os.path.join(out_folder, gene + "_fusion")
             os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
-            log(f"[{gene}] S2 over {world} ranks: {len(res.reads)} candidate records gathered")
             homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
-            results[gene] = consume_gene(gene, anchor, cand.names, cand, cand.lens, res, index, homo_rows, searches,
-                                         os.path.join(folder, gene + "_fusion"), log=log, filt=filt)
-    # the end-of-run sync on the CPU group (rank 0 may be busy long after the others finish S2)
+            results[gene] = consume_products(gene, anchor, index, homo_rows, searches,
+                                             os.path.join(folder, gene + "_fusion"), s4, split_sam, psl, log=log,
+                                             filt=filt)
+    # the end-of-run sync on the CPU group (rank 0 may be busy long after the others finish)
     dist.barrier(host_group)
     return results

@@ -407,86 +407,3 @@ def read_pairs_sharded(fq1, fq2, rank, world, group=None, chunk_bases=CHUNK_BASE
     if reads.shape[0]:
         reads = np.ascontiguousarray(reads[:, :max(1, int(lens.max()))])
     return names, reads, (None if (lens == reads.shape[1]).all() else lens), lo, n_all
-
-
-# ---- the local S2 of a sharded ingest and the candidates' exchange --------------------------------
-
-class SparseReads:
-    """The reads of the candidate pairs only (gathered from the ranks), indexed as the whole
-    sample's pair-major matrix: reads[r, :n] for a global read row r (consume_gene's access);
-    `lens[r]` and `names[p]` likewise.  Rows of other pairs are never asked for: no filter keeps
-    a read without a candidate record."""
-
-    def __init__(self, gpairs, reads, lens, names, n_pairs):
-        self.gpairs = np.asarray(gpairs, dtype=np.int64)
-        self.reads, self.shape = reads, (2 * int(n_pairs), reads.shape[1] if reads.ndim == 2 else 1)
-        self.lens = _Rows(self, np.asarray(lens, dtype=np.int32))
-        self.names = _Names(self, names)
-
-    def _pair(self, p):
-        i = int(np.searchsorted(self.gpairs, p))
-        if i >= len(self.gpairs) or self.gpairs[i] != p:
-            raise KeyError(f"pair {p} is not a candidate pair")
-        return i
-
-    def __getitem__(self, key):
-        r, sl = key
-        return self.reads[2 * self._pair(int(r) // 2) + int(r) % 2][sl]
-
-
-class _Rows:
-    def __init__(self, owner, v):
-        self.owner, self.v = owner, v
-
-    def __getitem__(self, r):
-        return self.v[2 * self.owner._pair(int(r) // 2) + int(r) % 2]
-
-
-class _Names:
-    def __init__(self, owner, names):
-        self.owner, self.n = owner, names
-
-    def __getitem__(self, p):
-        return self.n[self.owner._pair(int(p))]
-
-
-def align_local(aligner, reads, lens, lo, n_pairs, names, group=None, host_group=None, device=None):
-    """S2 of this rank's whole chunks (pairs lo .. lo + n of an n_pairs sample, from
-    read_pairs_sharded), then the exchange: the candidate pairs' records (device all-gatherv over
-    `group`, RCCL on GPUs) and their reads and names (over `host_group`, a CPU group).  Every rank
-    returns (SparseCandidates, SparseReads) of the whole sample."""
-    import torch
-    import torch.distributed as dist
-    dev = torch.device(device) if device is not None else torch.device("cpu")
-    n = reads.shape[0] // 2
-    if n:
-        rows_t = pack_candidates_device(_shard_records_t(aligner, reads, lens, 0, n, dev, pair_base=lo), lo)
-    else:
-        rows_t = torch.zeros((0, ROW_WORDS), dtype=torch.int32, device=dev)
-    loc = rows_t[:, 0].cpu().numpy().view(np.uint32).astype(np.int64) - lo if rows_t.shape[0] else \
-        np.zeros(0, np.int64)
-    rr = np.stack([2 * loc, 2 * loc + 1], axis=1).reshape(-1)
-    ln = np.full(2 * n, reads.shape[1], np.int32) if lens is None else np.asarray(lens, np.int32)
-    mine = (loc + lo, reads[rr], ln[rr], [names[int(i)] for i in loc])
-    allc = SparseCandidates(allgatherv_device(rows_t, group).cpu().numpy(), n_pairs)
-    parts = [None] * dist.get_world_size(host_group)
-    dist.all_gather_object(parts, mine, group=host_group)
-    g = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.int64)
-    w = max([p[1].shape[1] for p in parts if p[1].size], default=1)
-    rd = np.full((2 * len(g), w), ord("N"), np.uint8)
-    ll = np.empty(2 * len(g), np.int32)
-    nm = []
-    k = 0
-    for p in parts:
-        m = len(p[0])
-        if m:
-            rd[2 * k:2 * (k + m), :p[1].shape[1]] = p[1]
-            ll[2 * k:2 * (k + m)] = p[2]
-        nm += p[3]
-        k += m
-    order = np.argsort(g, kind="stable")
-    rows2 = np.stack([2 * order, 2 * order + 1], axis=1).reshape(-1)
-    sr = SparseReads(g[order], rd[rows2], ll[rows2], [nm[i] for i in order], n_pairs)
-    if not np.array_equal(sr.gpairs, allc.reads[0::2] // 2):
-        raise RuntimeError("candidate exchange: records and reads disagree")
-    return allc, sr

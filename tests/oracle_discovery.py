@@ -47,7 +47,7 @@ class OracleDiscovery:
             s = self._seq(int(r)).tobytes()
             if len(normalize(res.cigar_str(r), s.decode())[0]) == 2:
                 rows5.append(int(r))
-                seqs5.append((s[::-1].translate(_COMP) if res.flag[r] & 0x10 else s).decode())
+                seqs5.append(s[::-1].translate(_COMP) if res.flag[r] & 0x10 else s)
         rows5 = np.asarray(rows5, np.int64)
         self.q5 = seqs5
         self._cig = res.cigar[rows5] if len(rows5) else np.zeros((0, 32), np.uint32)
@@ -71,7 +71,7 @@ class OracleDiscovery:
         buf = np.full((n5, max(len(s) for s in self.q5)), ord("N"), np.uint8)
         ql = np.zeros(n5, np.int32)
         for i, s in enumerate(self.q5):
-            buf[i, :len(s)] = np.frombuffer(s.encode(), np.uint8)
+            buf[i, :len(s)] = np.frombuffer(s, np.uint8)
             ql[i] = len(s)
         recs, nrec = self.og.align_se(buf, ql, ids=ids, threads=8)
         gid = np.zeros(n5, np.int64)
@@ -82,7 +82,7 @@ class OracleDiscovery:
         lines = ["@HD\tVN:1.6\n"]
         for i in range(n5):
             name = f"{gid[i]}${self.gene}$0${cigar_string(self._cig[i], self._ncig[i])}"
-            lines += genome.sam_lines(self.og.names, name, self.q5[i], recs[i], nrec[i])
+            lines += genome.sam_lines(self.og.names, name, self.q5[i].decode(), recs[i], nrec[i])
         split = genome_check.filter_genome_hits(lines)
         _, fa = blocks.split_read_queries(split)
         out["src"] = [int(ln.split("\t")[0]) for ln in split]

@@ -42,9 +42,9 @@ def _worker(rank, world, port, paths, out):
     lo, hi = shard.shard_pairs(ln.astype(np.int64).reshape(-1, 2).sum(axis=1), rank, world, CHUNK)
     og = oracle.OracleGenome(genome)
     backend = OracleDiscovery(anchor, og, tiles_for(genome), reads[2 * lo:2 * hi], ln[2 * lo:2 * hi], lo, CHUNK, GENE)
-    texts, counts = dist_discover.run(backend, lo, names.slice(lo, hi), GENE, og.names, rank, world, None,
-                                      log=lambda *_: None)
+    res, counts = dist_discover.search(backend, lo, rank, world, names=names.slice(lo, hi))
     if rank == 0:
+        texts = dist_discover.render(res, backend, GENE, og.names)
         with open(os.path.join(out, f"texts{world}.json"), "w") as fh:
             json.dump(texts, fh)
     dist.barrier()

@@ -22,8 +22,19 @@ CHUNK = 300_000  # bases per bwa chunk in these runs: the sample spans several, 
 def _backends(paths):
     from oracle_backends import OracleAligner, oracle_searches
     genome = [(h.split()[0], s.decode().upper()) for h, s in pipeline.read_fasta(paths["genome"])]
-    searches = oracle_searches(genome)
-    return searches, (lambda a: OracleAligner(a, chunk_bases=CHUNK))
+    searches = oracle_searches(genome, CHUNK)
+    return searches, (lambda a: OracleAligner(a, chunk_bases=CHUNK)), _discovery_factory(genome)
+
+
+def _discovery_factory(genome):
+    """The oracle as the per-rank dist_discover backend of a sharded run."""
+    import oracle
+    from oracle_discovery import OracleDiscovery, tiles_for
+    og, tiles = oracle.OracleGenome(genome), tiles_for(genome)
+
+    def make(anchor, reads, lens, lo, searches, gene):
+        return OracleDiscovery(anchor.encode(), og, tiles, reads, lens, lo, CHUNK, gene)
+    return make
 
 
 def _worker(rank, world, port, paths, out, mode):
@@ -34,10 +45,11 @@ def _worker(rank, world, port, paths, out, mode):
     shard.CHUNK_BASES = CHUNK
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    searches, factory = _backends(paths)
+    searches, factory, disc = _backends(paths)
     if mode == "bulk":
         pipeline.run(paths["anchor"], paths["fq1"], paths["fq2"], paths["genome"], paths["gtf"], out,
-                     searches=searches, aligner_factory=factory, log=lambda *_: None)
+                     searches=searches, aligner_factory=factory, log=lambda *_: None, chunk_bases=CHUNK,
+                     backend_factory=disc)
     else:
         singlecell.run(paths["anchor"], paths["cells"], paths["genome"], paths["gtf"], out, searches=searches,
                        aligner_factory=factory, batch_pairs=3000, log=lambda *_: None)
