@@ -57,14 +57,13 @@ def merge_order(keys, rows):
     return np.lexsort((np.asarray(rows, np.int64), np.asarray(keys, np.int64)))
 
 
-def _allgatherv(arr, group, device):
+def _allgatherv(arr, group, device, world):
     """All-gatherv of a 2-D numpy array (rows) over `group` on `device`; the rows of every rank
-    in rank order (numpy)."""
+    in rank order (numpy).  world == 1: the array itself (no process group needed)."""
     import torch
-    import torch.distributed as dist
     from .shard import allgatherv_device
     a = np.ascontiguousarray(arr)
-    if dist.get_world_size(group) == 1:
+    if world == 1:
         return a
     width = a.dtype.itemsize * int(np.prod(a.shape[1:]))
     t = torch.from_numpy(a.view(np.uint8).reshape(a.shape[0], width)).to(device)
@@ -135,8 +134,8 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
         return np.stack([np.asarray(d["key"], np.int64), np.asarray(d["row"], np.int64) + g0], axis=1) \
             if len(d["key"]) else np.zeros((0, 2), np.int64)
     # the lists' keys, every rank (S5 ids and groups; S4's global zip on rank 0)
-    K5 = _allgatherv(kr(L.s5), group, device)
-    n_before = _allgatherv(np.array([[len(L.s5["key"])]], np.int64), group, device)[:, 0]
+    K5 = _allgatherv(kr(L.s5), group, device, world)
+    n_before = _allgatherv(np.array([[len(L.s5["key"])]], np.int64), group, device, world)[:, 0]
     o5 = merge_order(K5[:, 0], K5[:, 1])
     ordinal = np.empty(len(o5), np.int64)
     ordinal[o5] = np.arange(len(o5))
@@ -164,7 +163,7 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     w5, w6 = -(-w5 // 4) * 4, -(-w6 // 4) * 4
     s5b = _pad_rows([_u8(L.s5["seq"][int(k)]) for k in src], w5)
     s6b = _pad_rows([_u8(x) for x in surv["s6_seq"]], w6)
-    W5 = _allgatherv(np.array([[w5, w6]], np.int64), group, device).max(axis=0)
+    W5 = _allgatherv(np.array([[w5, w6]], np.int64), group, device, world).max(axis=0)
     s5b = np.pad(s5b, ((0, 0), (0, int(W5[0]) - w5)), constant_values=ord("N"))
     s6b = np.pad(s6b, ((0, 0), (0, int(W5[1]) - w6)), constant_values=ord("N"))
     ords = ids[src] if ns else np.zeros(0, np.int64)
@@ -179,11 +178,11 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
         # the read's global row (render: names)
         (rows5[src] if ns else np.zeros(0, np.int64)).view(np.int32).reshape(-1, 2)], axis=1)
     psl = psl_table(surv, ords)
-    all_rows = _allgatherv(rows.astype(np.int32), group, device)
-    all_psl = _allgatherv(psl, group, device)
+    all_rows = _allgatherv(rows.astype(np.int32), group, device, world)
+    all_psl = _allgatherv(psl, group, device, world)
     # S4's reads: the rank's tmp1 / tmp2 reads with their keys and global rows
     w4 = max(1, int(max((len(_u8(x)) for x in list(L.t1["seq"]) + list(L.t2["seq"])), default=1)))
-    W4 = int(_allgatherv(np.array([[w4]], np.int64), group, device).max())
+    W4 = int(_allgatherv(np.array([[w4]], np.int64), group, device, world).max())
     W4 = -(-W4 // 4) * 4
 
     def reads_rows(d):
@@ -193,8 +192,8 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
         return np.concatenate([np.stack([np.asarray(d["key"], np.int64), np.asarray(d["row"], np.int64) + g0],
                                         axis=1).view(np.int32).reshape(k, 4), _i32(d["len"]),
                                _pad_rows([_u8(x) for x in d["seq"]], W4).view(np.int32).reshape(k, W4 // 4)], axis=1)
-    T1 = _allgatherv(reads_rows(L.t1), group, device)
-    T2 = _allgatherv(reads_rows(L.t2), group, device)
+    T1 = _allgatherv(reads_rows(L.t1), group, device, world)
+    T2 = _allgatherv(reads_rows(L.t2), group, device, world)
     counts = dict(tmp1=len(L.t1["key"]), tmp2=len(L.t2["key"]), s5_split_reads=n5, s6_queries=ns)
     named = None
     if names is not None:

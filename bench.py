@@ -314,7 +314,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     import torch
     import torch.distributed as dist
 
-    from anchored_fusion_amd import discover, simworld
+    from anchored_fusion_amd import discover, dist_discover, simworld
     from anchored_fusion_amd import io as afio
     from anchored_fusion_amd.shard import shard_range
     anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
@@ -357,16 +357,24 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     G = disc.grp.inflight
     n_groups = (len(disc.batches) + G - 1) // G
 
+    step_counts = {}
+
     def step(k1=None, ph=None):
-        disc.run(reads_t, k1_events=k1, phase_events=ph)
         if world > 1:
-            disc.exchange()
+            # the product's multi-GPU step (dist_discover): S2-S6 on this rank's chunks with the
+            # global read ids and QNAME groups, S4 on rank 0 over the globally zipped lists, the
+            # survivors and their S6 rows all-gathered over RCCL
+            _, c = dist_discover.search(disc.attach(reads_t, None, k1), lo, rank, world, device=dev)
+            step_counts.update(c)
+        else:
+            disc.run(reads_t, k1_events=k1, phase_events=ph)
 
     for w in range(args.warmup):
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize(dev)
-        log(f"warm-up pass {w}: {time.perf_counter() - t0:.3f} s, {disc.summary()}")
+        log(f"warm-up pass {w}: {time.perf_counter() - t0:.3f} s, "
+            f"{disc.summary() if world == 1 else step_counts}")
     free, total = torch.cuda.mem_get_info(dev)
     E = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     k1 = [[[E(), E()] for _ in range(n_groups)] for _ in range(args.steps)]
@@ -377,15 +385,16 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     t0 = time.perf_counter()
     for k in range(args.steps):
         s0 = disc.grp.streams[0]
-        ph[k][0].record(s0)
-        step(None if args.no_kernel_events else k1[k], ph[k][1:])
+        if world == 1:
+            ph[k][0].record(s0)
+        step(None if args.no_kernel_events else k1[k], ph[k][1:] if world == 1 else None)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(elapsed, world, dev, backend)
     ms = elapsed / args.steps * 1e3
-    summ = disc.summary()
+    summ = disc.summary() if world == 1 else dict(step_counts)
     n_launch = len(disc.batches)
     k1_ms = float("nan") if args.no_kernel_events else \
         sum(e[0].elapsed_time(e[1]) for st in k1 for e in st) / args.steps
@@ -419,16 +428,18 @@ def bench_c3(args, world, rank, gpu, dev, backend):
                         + (f" sharded over {world} GPUs" if world > 1 else "")
                         + f", bwa genome index {genome_bp / 1e9:.2f} Gbp HBM-resident, one anchor (BCR NM_004327.4); "
                           "step = S2 + S3 sort/partition + S4/S5 genome bwa mem + S5 genome check + S6 BLAT"
-                        + (" + all-gatherv of candidates" if world > 1 else ""),
+                        + (" per rank with the global order (dist_discover: keys all-gathered, S4 on rank 0, "
+                           "survivors all-gathered over RCCL)" if world > 1 else ""),
             "pairs_total": N, "pairs_per_gpu": n, "read_len": L, "genome_bp": genome_bp, "anchor_len": len(anchor),
             "parallelism": f"dp{world}", "batches": n_launch, "pairs_per_batch": bp, "inflight": G,
         },
         "counts_per_step": summ,
-        "phases_ms": {"s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
-                      "gather_queries": round(phase(2, 3), 3), "genome_bwa_s4_s5": round(phase(3, 4), 3),
-                      "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
-                              "genome_bwa_s4_s5 = S5, its genome check, then S4 on slot 0 beside the S6 BLAT "
-                              "of S5's survivors on slot 1's stream, joined at its end"},
+        "phases_ms": None if world > 1 else {
+            "s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
+            "gather_queries": round(phase(2, 3), 3), "genome_bwa_s4_s5": round(phase(3, 4), 3),
+            "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
+                    "genome_bwa_s4_s5 = S5, its genome check, then S4 on slot 0 beside the S6 BLAT "
+                    "of S5's survivors on slot 1's stream, joined at its end"},
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
             "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

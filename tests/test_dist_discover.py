@@ -80,3 +80,17 @@ def test_dist_discover_equals_host_path(world_and_host, world):
     assert got[0] == s4
     assert got[1] == split_sam
     assert got[2] == psl
+
+
+def test_dist_discover_one_process_without_group(world_and_host):
+    """world 1 needs no process group: the driver is also the one-GPU form of the step."""
+    import oracle
+    from anchored_fusion_amd import dist_discover
+    from oracle_discovery import OracleDiscovery, tiles_for
+    paths, _, host = world_and_host
+    names, reads, lens, genome, anchor = _inputs(paths)
+    og = oracle.OracleGenome(genome)
+    ln = np.full(reads.shape[0], reads.shape[1], np.int32) if lens is None else lens
+    backend = OracleDiscovery(anchor, og, tiles_for(genome), reads, ln, 0, CHUNK, GENE)
+    res, _ = dist_discover.search(backend, 0, 0, 1, names=names)
+    assert [list(x) for x in dist_discover.render(res, backend, GENE, og.names)] == host
