@@ -28,7 +28,7 @@ struct NOp {
 };
 
 // parse (running ends) of BAM ops; the first H (in CIGAR string order) read as S when h_as_s
-__device__ int parse_ops(const uint32_t *cig, int nc, bool h_as_s, NOp *o) {
+__host__ __device__ int parse_ops(const uint32_t *cig, int nc, bool h_as_s, NOp *o) {
     int e = 0;
     bool first_h = h_as_s;
     const int n = nc < AF_MAX_CIGAR ? nc : AF_MAX_CIGAR;
@@ -42,13 +42,13 @@ __device__ int parse_ops(const uint32_t *cig, int nc, bool h_as_s, NOp *o) {
     return n;
 }
 
-__device__ __forceinline__ void del_at(NOp *o, int &n, int k) {
+__host__ __device__ __forceinline__ void del_at(NOp *o, int &n, int k) {
     for (int j = k; j < n - 1; ++j) o[j] = o[j + 1];
     --n;
 }
 
 // deal_cigar's operation list (functions.py:656-702; cigar.py `normalize`), ops only
-__device__ int deal_ops(NOp *o, int n) {
+__host__ __device__ int deal_ops(NOp *o, int n) {
     int k = 0;
     while (k < n) {
         const int op = o[k].op;
@@ -75,7 +75,7 @@ __device__ int deal_ops(NOp *o, int n) {
 }
 
 // fn:752-756 for one genome record against the anchored ops `bf` (nb)
-__device__ bool record_bad(const af_grec &g, const NOp *bf, int nb) {
+__host__ __device__ bool record_bad(const af_grec &g, const NOp *bf, int nb) {
     NOp now[NOPS];
     const int flag = g.flag & 0xFFFF;
     const bool rev = flag > 15 && ((flag >> 4) & 1);
@@ -107,7 +107,7 @@ struct S5In {
 };
 
 // QNAME of query q: read name (the pair: row >> 1), gene, POS, CIGAR of the anchored record
-__device__ bool same_qname(const S5In &in, int64_t a, int64_t b) {
+__host__ __device__ bool same_qname(const S5In &in, int64_t a, int64_t b) {
     const int ra = in.q_rows[a], rb = in.q_rows[b];
     if ((ra >> 1) != (rb >> 1) || in.pos[ra] != in.pos[rb] || in.n_cigar[ra] != in.n_cigar[rb]) return false;
     const int nc = in.n_cigar[ra] < AF_MAX_CIGAR ? in.n_cigar[ra] : AF_MAX_CIGAR;
@@ -118,49 +118,48 @@ __device__ bool same_qname(const S5In &in, int64_t a, int64_t b) {
 
 // query u continues the group of u - 1: the caller's flags (a shard of a wider query list,
 // whose neighbours in the global order are known to the caller), else the QNAMEs compared
-__device__ bool continues(const S5In &in, int64_t u) {
+__host__ __device__ bool continues(const S5In &in, int64_t u) {
     return in.cont ? in.cont[u] != 0 : same_qname(in, u - 1, u);
 }
 
-__device__ bool query_bad(const S5In &in, int64_t q, const NOp *bf, int nb) {
+__host__ __device__ bool query_bad(const S5In &in, int64_t q, const NOp *bf, int nb) {
     const int nr = in.n_rec[q] < AF_G_MAX_REC ? in.n_rec[q] : AF_G_MAX_REC;
     for (int k = 0; k < nr; ++k)
         if (record_bad(in.recs[q * AF_G_MAX_REC + k], bf, nb)) return true;
     return false;
 }
 
-__global__ void k_s5_check(S5In in, int64_t n, uint8_t *__restrict__ keep) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n) return;
-    if (q > 0 && continues(in, q)) { keep[q] = 0; return; }
+// keep flag of query q of n: it starts a QNAME group and no record of the group is bad
+__host__ __device__ uint8_t s5_keep(const S5In &in, int64_t q, int64_t n) {
+    if (q > 0 && continues(in, q)) return 0;
     const int r = in.q_rows[q];
     NOp bf[NOPS];
     const int nb = deal_ops(bf, parse_ops(in.cigar + (int64_t)r * AF_MAX_CIGAR, in.n_cigar[r], false, bf));
     bool bad = query_bad(in, q, bf, nb);
     for (int64_t u = q + 1; !bad && u < n && continues(in, u); ++u) bad = query_bad(in, u, bf, nb);
-    keep[q] = bad ? 0 : 1;
+    return bad ? 0 : 1;
+}
+
+__global__ void k_s5_check(S5In in, int64_t n, uint8_t *__restrict__ keep) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    keep[q] = s5_keep(in, q, n);
 }
 
 // Python slice index (negative counts from the end, clamped to [0, len])
-__device__ __forceinline__ int py_idx(int i, int len) {
+__host__ __device__ __forceinline__ int py_idx(int i, int len) {
     if (i < 0) i += len;
     return i < 0 ? 0 : (i > len ? len : i);
 }
 
-// deal_cigar's processed SEQ of survivor k (S5 query sel[k]) into S6 row k.  The edits run in
-// place on the output row; bytes past out_stride are dropped and counted in *n_over (the BLAT
-// kernel takes at most AF_MAX_READ bases).
-__global__ void k_s6_rows(S5In in, const uint8_t *__restrict__ q, int32_t q_stride, const int32_t *__restrict__ q_lens,
-                          const int32_t *__restrict__ sel, const int64_t *__restrict__ n_sel, int64_t cap,
-                          uint8_t *__restrict__ out, int32_t out_stride, int32_t *__restrict__ out_lens,
-                          int32_t *__restrict__ out_src, int32_t *__restrict__ n_over) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t n = *n_sel < cap ? *n_sel : cap;
-    if (k >= n) return;
-    const int32_t qi = sel[k];
+// deal_cigar's processed SEQ of S5 query qi into `row` (out_stride bytes): the edits run in place
+// on the row; bytes past out_stride are dropped (the BLAT kernel takes at most AF_MAX_READ
+// bases).  Returns the row length; *over = a byte was dropped.
+__host__ __device__ int s6_row(const S5In &in, int32_t qi, const uint8_t *q, int32_t q_stride, const int32_t *q_lens,
+                               uint8_t *row, int32_t out_stride, bool *over_out) {
     const int r = in.q_rows[qi];
-    uint8_t *row = out + k * (int64_t)out_stride;
     int len = q_lens[qi] < q_stride ? q_lens[qi] : q_stride;
+    if (len > out_stride) { len = out_stride; *over_out = true; }
     for (int j = 0; j < len; ++j) row[j] = q[(int64_t)qi * q_stride + j];
     NOp o[NOPS];
     int n_op = parse_ops(in.cigar + (int64_t)r * AF_MAX_CIGAR, in.n_cigar[r], false, o);
@@ -199,7 +198,21 @@ __global__ void k_s6_rows(S5In in, const uint8_t *__restrict__ q, int32_t q_stri
             ++kk;
         }
     }
-    out_lens[k] = len;
+    if (over) *over_out = true;
+    return len;
+}
+
+// S6 row k = survivor k (S5 query sel[k]); rows with dropped bytes are counted in *n_over
+__global__ void k_s6_rows(S5In in, const uint8_t *__restrict__ q, int32_t q_stride, const int32_t *__restrict__ q_lens,
+                          const int32_t *__restrict__ sel, const int64_t *__restrict__ n_sel, int64_t cap,
+                          uint8_t *__restrict__ out, int32_t out_stride, int32_t *__restrict__ out_lens,
+                          int32_t *__restrict__ out_src, int32_t *__restrict__ n_over) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n = *n_sel < cap ? *n_sel : cap;
+    if (k >= n) return;
+    const int32_t qi = sel[k];
+    bool over = false;
+    out_lens[k] = s6_row(in, qi, q, q_stride, q_lens, out + k * (int64_t)out_stride, out_stride, &over);
     out_src[k] = qi;
     if (over && n_over) atomicAdd(n_over, 1);
 }
@@ -212,6 +225,27 @@ __global__ void k_s6_count(const int64_t *__restrict__ n_sel, int64_t cap, int32
 }
 
 }  // namespace
+
+// The per-query rules above compiled for the host, over host arrays (unit tests of the rules
+// against the consumer-stage restatements on machines without a GPU; the product path is
+// af_s5_filter_device).  keep[q] as k_s5_check writes it; rows[q] / out_lens[q] / over[q] =
+// k_s6_rows' output for EVERY query q (survivor or not).
+extern "C" int af_s5_rules_host(const af_grec *recs, const int32_t *n_rec, int64_t n, const int32_t *q_rows,
+                                const int32_t *pos, const int32_t *n_cigar, const uint32_t *cigar, const uint8_t *cont,
+                                const uint8_t *q, int32_t q_stride, const int32_t *q_lens, uint8_t *keep, uint8_t *rows,
+                                int32_t out_stride, int32_t *out_lens, uint8_t *over) {
+    if (n < 0 || (n > 0 && (!recs || !n_rec || !q_rows || !pos || !n_cigar || !cigar || !q || !q_lens || !keep ||
+                            !rows || !out_lens || !over)) || q_stride <= 0 || out_stride <= 0)
+        return AF_E_INVALID;
+    const S5In in{recs, n_rec, q_rows, nullptr, pos, n_cigar, cigar, cont};
+    for (int64_t k = 0; k < n; ++k) {
+        keep[k] = s5_keep(in, k, n);
+        bool o = false;
+        out_lens[k] = s6_row(in, (int32_t)k, q, q_stride, q_lens, rows + k * (int64_t)out_stride, out_stride, &o);
+        over[k] = o ? 1 : 0;
+    }
+    return AF_OK;
+}
 
 size_t af_s5_temp_bytes(int64_t n) {
     size_t b = 0;

@@ -341,6 +341,14 @@ int af_s5_filter_device(af_ctx *ctx, const af_grec *d_recs, const int32_t *d_n_r
                         const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
                         const af_aln_out *d_s2, const uint8_t *d_cont, int64_t cap, uint8_t *d_s6, int32_t s6_stride,
                         int32_t *d_s6_lens, int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream);
+/* Test hook: the same per-query rules (one source, compiled for the host too) over host arrays --
+ * the S2 fields indexed by the read rows q_rows (pos, n_cigar, cigar[row * AF_MAX_CIGAR ..]).
+ * keep[q] = 1 when af_s5_filter_device keeps query q; rows[q] (out_stride bytes), out_lens[q] and
+ * over[q] (bytes dropped) = the S6 row it writes for q, for every query.  Not a product path. */
+int af_s5_rules_host(const af_grec *recs, const int32_t *n_rec, int64_t n, const int32_t *q_rows, const int32_t *pos,
+                     const int32_t *n_cigar, const uint32_t *cigar, const uint8_t *cont, const uint8_t *q,
+                     int32_t q_stride, const int32_t *q_lens, uint8_t *keep, uint8_t *rows, int32_t out_stride,
+                     int32_t *out_lens, uint8_t *over);
 
 /* Paired FASTQ(.gz) ingest into the read layout above (host only, no GPU).  Replaces the
  * fq1/fq2 inputs of `bwa mem -M -t T anchor fq1 fq2` (Anchored_Fusion.py:182): records as
