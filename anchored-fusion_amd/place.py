@@ -13,7 +13,6 @@ import numpy as np
 from . import _lib
 
 SEP = 512  # N run between contigs
-WINDOW = 300  # long-query window (step WINDOW // 2)
 
 
 def pack_queries(seqs):
@@ -67,24 +66,34 @@ class Placer:
         return ref
 
     def __call__(self, targets, queries, preset):
-        from . import blat
+        from . import blat, stitch
         header = ["psLayout version 3\n", "\n"]
         if not targets or not queries:
             return header
         p = blat.params(preset)
         ref = self.tiles(targets, p.step_size)
         # queries longer than the kernel's read limit (the anchor transcript itself, fn:341/966)
-        # are searched as overlapping windows; rows keep the full query's name, size and coordinates
-        pieces = []  # (name, window seq, offset, full length)
-        for name, seq in queries:
-            if len(seq) <= _lib.AF_MAX_READ:
-                pieces.append((name, seq, 0, len(seq)))
-            else:
-                for off in range(0, max(1, len(seq) - WINDOW // 2), WINDOW // 2):
-                    pieces.append((name, seq[off:off + WINDOW], off, len(seq)))
-        rows, nr = ref.search([w for _, w, _, _ in pieces], p, blat.MAX_ROWS)
-        return header + blat.psl_lines(ref, [(nm, w) for nm, w, _, _ in pieces], rows, nr,
-                                       offsets=[o for _, _, o, _ in pieces], full_sizes=[f for _, _, _, f in pieces])
+        # are searched as windows with no score / identity floor and stitched (stitch.py)
+        lines = [[] for _ in queries]
+        short = [i for i, (_, sq) in enumerate(queries) if len(sq) <= _lib.AF_MAX_READ]
+        longs = [i for i, (_, sq) in enumerate(queries) if len(sq) > _lib.AF_MAX_READ]
+        if short:
+            rows, nr = ref.search([queries[i][1] for i in short], p, blat.MAX_ROWS)
+            for k, i in enumerate(short):
+                lines[i] = blat.psl_lines(ref, [queries[i]], rows[k:k + 1], nr[k:k + 1])
+        if longs:
+            pw = blat.params(preset, min_score=0, min_identity=0)
+            pieces = [stitch.windows(queries[i][1]) for i in longs]
+            rows, nr = ref.search([w for ps in pieces for _, w in ps], pw, blat.MAX_ROWS)
+            k = 0
+            for i, ps in zip(longs, pieces):
+                nm, sq = queries[i]
+                lines[i] = stitch.stitched_lines(ref, targets, nm, sq, rows[k:k + len(ps)], nr[k:k + len(ps)], ps, p)
+                k += len(ps)
+        out = list(header)
+        for ln in lines:
+            out += ln
+        return out
 
     def close(self):
         for r in self._tiles.values():
