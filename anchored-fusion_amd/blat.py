@@ -24,6 +24,7 @@ PSL_DTYPE = np.dtype([(n, "<i4") for n in (
 assert PSL_DTYPE.itemsize == 328
 TILE = 11
 MAX_ROWS = 16
+CAP_NAMES = ("hits", "clumps", "parts", "rows")  # af_blat_caps' counters, in order
 
 # the reference's option sets (functions.py call sites); rep_match None = BLAT's default
 PRESETS = {
@@ -134,6 +135,13 @@ class TileReference:
             n_queries_t.data_ptr(), cap, int(stride), None if lens_t is None else lens_t.data_ptr(),
             ctypes.byref(p or params()), int(max_rows), rows_t.data_ptr(), n_rows_t.data_ptr(),
             _stream_handle(stream)), "af_blat_device_range")
+
+    def caps(self, reset=True):
+        """af_blat_caps: query strands / queries at each of the search's caps since the last reset
+        (synchronises)."""
+        out = np.zeros(len(CAP_NAMES), np.int32)
+        _lib.check(self.ctx, _lib.lib().af_blat_caps(self.ctx, out.ctypes.data, int(bool(reset))), "af_blat_caps")
+        return dict(zip(CAP_NAMES, (int(v) for v in out)))
 
     def locate(self, t_start, t_end):
         import bisect

@@ -289,7 +289,7 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, hipStream_t s);
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, hipStream_t s);
 // k_blat's schedule: the queries by estimated cost, heaviest first (work: af_blat_order_bytes(cap))
 size_t af_blat_order_bytes(int64_t cap);
 hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,

@@ -30,6 +30,7 @@ struct af_ctx {
     void *blat_ord_work = nullptr;  // k_blat's cost-ordered schedule (af_launch_blat_order)
     int32_t *blat_order = nullptr;
     int64_t blat_ord_cap = 0;
+    int32_t *blat_caps = nullptr;   // AF_BLAT_CAP_N counters, cumulative until af_blat_caps resets them
     af_psl *blat_stage = nullptr;   // per (query, strand) rows before k_blat_merge
     int32_t *blat_stage_n = nullptr;
     int64_t blat_stage_rows = 0, blat_stage_items = 0;
@@ -258,6 +259,8 @@ int ensure_bscratch(af_ctx *c) {
     if (c->bscratch) return AF_OK;
     c->blat_slots = af_blat_slots(c->n_cu);
     HIPCHK(c, hipMalloc(&c->bscratch, (size_t)AF_BLAT_SLOT_BYTES * c->blat_slots));
+    HIPCHK(c, hipMalloc(&c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N));
+    HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
     return AF_OK;
 }
 
@@ -533,7 +536,7 @@ int af_ctx_create(int device, af_ctx **out) {
 void af_ctx_destroy(af_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    af_free(c->ctrl); af_free(c->cand); af_free(c->zscratch); af_free(c->bscratch); af_free(c->blat_ord_work); af_free(c->blat_order); af_free(c->blat_stage); af_free(c->blat_stage_n); af_free(c->d_packed);
+    af_free(c->ctrl); af_free(c->cand); af_free(c->zscratch); af_free(c->bscratch); af_free(c->blat_caps); af_free(c->blat_ord_work); af_free(c->blat_order); af_free(c->blat_stage); af_free(c->blat_stage_n); af_free(c->d_packed);
     af_free(c->d_reads); af_free(c->d_lens);
     af_free(c->d_flag); af_free(c->d_pos); af_free(c->d_score); af_free(c->d_ncig); af_free(c->d_hits);
     af_free(c->d_cigar);
@@ -1041,7 +1044,7 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
             hipSuccess ||
         (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride, lens ? d_lens : nullptr, *p,
                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows,
-                            c->blat_order, c->blat_stage, c->blat_stage_n, s)) !=
+                            c->blat_order, c->blat_stage, c->blat_stage_n, c->blat_caps, s)) !=
             hipSuccess ||
         (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipMemcpyAsync(n_rows, d_nrows, 4 * n_queries, hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -1080,7 +1083,17 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
     }
     HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
                              c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows,
-                             order, c->blat_stage, c->blat_stage_n, s));
+                             order, c->blat_stage, c->blat_stage_n, c->blat_caps, s));
+    return AF_OK;
+}
+
+int af_blat_caps(af_ctx *c, int32_t *out, int reset) {
+    if (!c || !out) return fail(c, AF_E_INVALID, "null argument");
+    if (!c->blat_caps) { for (int k = 0; k < AF_BLAT_CAP_N; ++k) out[k] = 0; return AF_OK; }
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N, hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
     return AF_OK;
 }
 

@@ -355,7 +355,8 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                                                         int32_t *__restrict__ heads,
                                                         uint8_t *__restrict__ bscratch, int32_t diag_passes,
                                                         af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
-                                                        int32_t max_rows, const int32_t *__restrict__ order) {
+                                                        int32_t max_rows, const int32_t *__restrict__ order,
+                                                        int32_t *__restrict__ caps) {
     DpLds &D = g_dp;
     BlatLds &B = g_bl;
     const int lane = threadIdx.x;
@@ -430,6 +431,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
             // in flight --------------------------------------------------------------------------
             const int nh_all = min(carry, NMAX);
+            if (lane == 0 && caps && carry > NMAX) atomicAdd(&caps[AF_BLAT_CAP_HITS], 1);
             int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
             for (int h0 = 0; h0 < nh_all; h0 += 256) {
                 int qv[4];
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             }
             __threadfence_block();
             wave_sync();
+            if (lane == 0 && caps && ncl == MAXCL) atomicAdd(&caps[AF_BLAT_CAP_CLUMPS], 1);
             if (ncl == 0) continue;
             // ---- clump order: hits desc, then diagonal (= run order) ------------------------------
             for (int i = lane; i < ncl; i += 64)
@@ -532,8 +535,8 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             BPM(2);
             BP(cc_ += ncl;)
             // ---- parts: one per clump whose seed lies in no earlier part -------------------------
-            int nr = 0;
-            for (int c = 0; c < ncl && nr < MAXR; ++c) {
+            int nr = 0, c = 0;
+            for (; c < ncl && nr < MAXR; ++c) {
                 const Clump cc = CL[(uint32_t)CO[c]];
                 bool skip = false;
                 for (int r = 0; r < nr && !skip; ++r) {
@@ -545,6 +548,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                 __threadfence_block();
                 wave_sync();
             }
+            if (lane == 0 && caps && nr == MAXR && c < ncl) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
             if (nr == 0) continue;
             BPM(3);
             BP(cr += nr;)
@@ -647,7 +651,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             const int m = n < max_rows ? n : max_rows;
             const int64_t sl = 2 * qi + s_item;  // this strand's rows, best first, for k_blat_merge
             for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
-            stage_n[sl] = m;
+            stage_n[sl] = n;  // all of the strand's rows (k_blat_merge takes the first max_rows)
             BP(if (g_blprof && qi < (1 << 22)) {
                 int32_t *pf = g_blprof + qi * 16;
                 for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
@@ -705,15 +709,18 @@ __global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, uint32_
 // stable sort of the union, as one wave doing both strands would have produced
 __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__restrict__ stage_n,
                              const int32_t *__restrict__ n_q, const int32_t *__restrict__ q_first, int64_t cap,
-                             int32_t max_rows, af_psl *__restrict__ rows, int32_t *__restrict__ n_rows) {
+                             int32_t max_rows, af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
+                             int32_t *__restrict__ caps) {
     const int64_t nq = *n_q < cap ? *n_q : cap;
     const int64_t q0 = q_first ? max((int64_t)0, min((int64_t)*q_first, nq)) : 0;
     const int64_t qi = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (qi >= nq) return;
     const af_psl *A = stage + 2 * qi * max_rows, *Bs = A + max_rows;
-    const int na = stage_n[2 * qi], nb = stage_n[2 * qi + 1];
+    const int sa = stage_n[2 * qi], sb = stage_n[2 * qi + 1];
+    const int na = sa < max_rows ? sa : max_rows, nb = sb < max_rows ? sb : max_rows;
+    if (caps && sa + sb > max_rows) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
 #ifdef AF_BLAT_CHECK
-    if (na < 0 || na > max_rows || nb < 0 || nb > max_rows) {
+    if (na < 0 || nb < 0) {
         printf("k_blat_merge: query %ld rows %d %d\n", (long)qi, na, nb);
         return;
     }
@@ -783,7 +790,7 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, hipStream_t s) {
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, hipStream_t s) {
     // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
     int bits = 64 - __builtin_clzll((unsigned long long)(X.n + 1024));
     const int diag_passes = (bits + 7) / 8;
@@ -791,14 +798,14 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
     dim3 g(n_slots), b(64);
 #define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, q_first, cap, \
                                     heads, \
-                                    bscratch, diag_passes, stage, stage_n, max_rows, order)
+                                    bscratch, diag_passes, stage, stage_n, max_rows, order, caps)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
     hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, stage, stage_n, n_queries,
-                       q_first, cap, max_rows, rows, n_rows);
+                       q_first, cap, max_rows, rows, n_rows, caps);
     return hipGetLastError();
 }
 

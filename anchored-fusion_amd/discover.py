@@ -317,6 +317,7 @@ class CandidateDiscovery:
                  s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))
                                         != 0).sum().item()))
         c.update({f"genome_{k}": v for k, v in self.ref.stats().items()})
+        c.update({f"blat_cap_{k}": v for k, v in self.tiles_ref.caps().items()})
         return c
 
     def s6_best_hits(self):

@@ -214,6 +214,17 @@ int af_blat_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, c
 int af_blat_device_range(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_first,
                          const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
                          const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
+/* How often the search's fixed caps bound (BLAT itself has none), counted per query strand on the
+ * context since the last reset: [HITS] tile hits past 32768 (the first 32768 in query order are
+ * clumped), [CLUMPS] 4096 clumps reached (the first in diagonal order kept), [PARTS] 16 aligned
+ * parts reached with clumps left; per query: [ROWS] rows past max_rows dropped.  Synchronises;
+ * reset != 0 zeroes the counters after reading. */
+#define AF_BLAT_CAP_HITS 0
+#define AF_BLAT_CAP_CLUMPS 1
+#define AF_BLAT_CAP_PARTS 2
+#define AF_BLAT_CAP_ROWS 3
+#define AF_BLAT_CAP_N 4
+int af_blat_caps(af_ctx *ctx, int32_t *out, int reset);
 
 /* S3 on the device (Anchored_Fusion.py:182 `| samtools sort`, then AF:186-194): the records
  * d_flag/d_pos of n_reads reads (pair-major, as written by af_align_pairs*) in samtools'

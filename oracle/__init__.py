@@ -162,10 +162,11 @@ class OracleTiles:
         L.afo_tiles_build.restype = ctypes.c_void_p
         L.afo_tiles_build.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int32]
         L.afo_tiles_free.argtypes = [ctypes.c_void_p]
-        L.afo_blat.restype = ctypes.c_int
-        L.afo_blat.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
-                               ctypes.POINTER(BlatParams), ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
-                               ctypes.c_int]
+        L.afo_blat_caps.restype = ctypes.c_int
+        L.afo_blat_caps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                    ctypes.POINTER(BlatParams), ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_void_p]
+        self.caps = np.zeros(4, np.int32)  # af_blat_caps' counters, cumulative (caps_read resets)
         self.seq = bytes(seq)
         self.step = int(step_size)
         self.h = L.afo_tiles_build(self.seq, len(self.seq), self.step)
@@ -185,11 +186,18 @@ class OracleTiles:
         nr = np.zeros(n, dtype=np.int32)
         p = params or blat_params(step_size=self.step)
         lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
-        rc = lib().afo_blat(self.h, q.ctypes.data, n, q.shape[1], None if lp is None else lp.ctypes.data,
-                            ctypes.byref(p), max_rows, rows.ctypes.data, nr.ctypes.data, int(threads))
+        rc = lib().afo_blat_caps(self.h, q.ctypes.data, n, q.shape[1], None if lp is None else lp.ctypes.data,
+                                 ctypes.byref(p), max_rows, rows.ctypes.data, nr.ctypes.data, int(threads),
+                                 self.caps.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"afo_blat failed: {rc}")
         return rows, nr
+
+    def caps_read(self, reset=True):
+        out = self.caps.copy()
+        if reset:
+            self.caps[:] = 0
+        return out
 
 
 # ---- the genome calls S4 / S5 (bwa_pe.c, FM mode) ---------------------------------------

@@ -245,8 +245,16 @@ static int tile_key(const uint8_t *Q, int q, uint32_t *k) {
 
 /* one strand of one query: rows appended to out (n_out in/out) */
 static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, int L, int strand,
-                        int32_t qi, afo_psl *out, int *n_out, int cap_out, hit_t *hits, reg_b *regs) {
+                        int32_t qi, afo_psl *out, int *n_out, int cap_out, hit_t *hits, reg_b *regs, int *cap) {
     int nh = 0;
+    int64_t all = 0;
+    for (int q = 0; q + TILE <= L; ++q) {
+        uint32_t k;
+        if (!tile_key(Q, q, &k)) continue;
+        const int64_t c = (int64_t)X->start[k + 1] - X->start[k];
+        if (c <= bp->rep_match) all += c;
+    }
+    if (all > MAXH) cap[0] = 1;
     for (int q = 0; q + TILE <= L && nh < MAXH; ++q) {
         uint32_t k;
         if (!tile_key(Q, q, &k)) continue;
@@ -273,9 +281,10 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         }
         i = j + 1;
     }
+    if (ncl == MAXCL) cap[1] = 1;
     qsort(cl, ncl, sizeof(clump_t), cmp_clump);  /* (hits desc, diagonal): keys are unique */
-    int nr = 0;
-    for (int c = 0; c < ncl && nr < MAXR; ++c) {
+    int nr = 0, c = 0;
+    for (; c < ncl && nr < MAXR; ++c) {
         int32_t q = cl[c].q;
         int64_t t = cl[c].t;
         int skip = 0;
@@ -284,6 +293,7 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         if (skip) continue;
         if (align_clump(X, Q, L, q, t, &regs[nr])) ++nr;
     }
+    if (nr == MAXR && c < ncl) cap[2] = 1;
     free(cl);
     /* regions in (qb, tb, qe) order for the chain DP */
     for (int i = 1; i < nr; ++i)
@@ -359,6 +369,12 @@ static int cmp_psl(const void *a, const void *b) {
 
 int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
              const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads) {
+    return afo_blat_caps(X, queries, n_queries, stride, lens, bp, max_rows, rows, n_rows, threads, NULL);
+}
+
+int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
+                  const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads,
+                  int32_t *caps) {
     if (!X || max_rows < 1 || max_rows > AFO_BLAT_MAX_ROWS || bp->step_size != X->step) return -1;
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads > 0 ? threads : 1)
     for (int64_t qi = 0; qi < n_queries; ++qi) {
@@ -376,9 +392,22 @@ int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int3
         reg_b regs[MAXR];
         afo_psl cand[2 * 2 * MAXR];
         int nc = 0;
+        int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
         for (int s = 0; s < 2; ++s) {
             memset(regs, 0, sizeof(regs));
-            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand, &nc, 2 * 2 * MAXR, hits, regs);
+            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand, &nc, 2 * 2 * MAXR, hits, regs, cap[s]);
+        }
+        if (caps) {
+            for (int s = 0; s < 2; ++s)
+                for (int k = 0; k < 3; ++k)
+                    if (cap[s][k]) {
+#pragma omp atomic
+                        caps[k] += 1;
+                    }
+            if (nc > max_rows) {
+#pragma omp atomic
+                caps[3] += 1;
+            }
         }
         free(hits);
         qsort(cand, nc, sizeof(afo_psl), cmp_psl);

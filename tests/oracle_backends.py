@@ -27,6 +27,10 @@ class OracleTileReference:
         op = oracle.blat_params(**{f: getattr(p, f) for f, _ in p._fields_})
         return self.tiles.blat(buf, lens, op, max_rows, threads=8)
 
+    def caps(self, reset=True):
+        from anchored_fusion_amd.blat import CAP_NAMES
+        return dict(zip(CAP_NAMES, (int(v) for v in self.tiles.caps_read(reset))))
+
     def locate(self, t_start, t_end):
         k = bisect.bisect_right(self.offsets, int(t_start)) - 1
         if k < 0:

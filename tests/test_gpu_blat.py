@@ -91,7 +91,27 @@ def test_blat_parity(preset):
             for f in blat.PSL_DTYPE.names:
                 assert np.array_equal(a[f], b[f]), (preset, i, k, f, a[f], b[f])
     assert ng.sum() > 0
+    assert g.caps() == o.caps(), preset  # the caps bind for the same query strands
     g.close()
+
+
+def test_blat_caps_match_oracle():
+    """Every cap counter of af_blat_caps (hits, clumps, parts, rows) on a world where each binds
+    (tests/test_blat_caps.py), equal to the oracle's."""
+    from anchored_fusion_amd import blat
+    from test_blat_caps import caps_world
+    ctgs, qs = caps_world()
+    for max_rows in (16, 1):
+        p = blat.params("homologs")
+        g = _gpu_ref(ctgs, p.step_size)
+        o = OracleTileReference(ctgs, p.step_size)
+        rg, ng = g.search(qs, p, max_rows)
+        ro, no = o.search(qs, p, max_rows)
+        assert np.array_equal(ng, no)
+        cg, co = g.caps(), o.caps()
+        assert cg == co, (max_rows, cg, co)
+        assert min(cg.values()) > 0 if max_rows == 1 else cg["hits"] > 0
+        g.close()
 
 
 def test_blat_finds_what_blat_finds():
