@@ -381,6 +381,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     ph = [[E() for _ in range(5)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
+    disc.tiles_ref.caps(reset=True)  # BLAT cap counters: from the timed steps only
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -395,6 +396,8 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     elapsed = max_over_ranks(elapsed, world, dev, backend)
     ms = elapsed / args.steps * 1e3
     summ = disc.summary() if world == 1 else dict(step_counts)
+    if world == 1:  # af_blat_caps accumulates over the timed steps: per step
+        summ.update({k: v / args.steps for k, v in summ.items() if k.startswith("blat_cap_")})
     n_launch = len(disc.batches)
     k1_ms = float("nan") if args.no_kernel_events else \
         sum(e[0].elapsed_time(e[1]) for st in k1 for e in st) / args.steps
