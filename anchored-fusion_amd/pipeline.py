@@ -31,6 +31,7 @@ windows (get_test_reads), scores them on PyTorch-ROCm (Test_model) and Final_fus
 Natural_score layout; a missing model file falls back to the no-filter tables, as in the reference.
 """
 import os
+import time
 import re
 
 from . import blocks as blk
@@ -295,8 +296,11 @@ def run_gene_device(gene, anchor, names, reads_t, lens_t, pair_bases, index, hom
     stages on the gathered queries only (consume_products)."""
     from . import blat
     from .discover import CandidateDiscovery
+    t0 = time.perf_counter()
     gidx = searches.genome_index()
     tiles = searches.place.tiles(searches.genome, blat.params("split_tail").step_size)
+    log(f"[{gene}] genome index and tiles ready ({time.perf_counter() - t0:.1f} s)")
+    t0 = time.perf_counter()
     n_pairs, stride = reads_t.shape[0] // 2, reads_t.shape[1]
     d = CandidateDiscovery(anchor.encode(), gidx, tiles, n_pairs, stride, device=device, inflight=inflight,
                            batch_chunks=batch_chunks, chunk_bases=chunk_bases, pair_bases=pair_bases)
@@ -313,6 +317,7 @@ def run_gene_device(gene, anchor, names, reads_t, lens_t, pair_bases, index, hom
         if any(caps.values()):
             log(f"[{gene}] WARNING: caps reached: {caps}")
         s4, split_sam, psl = device_products(d, gene, names, gidx.names)
+        log(f"[{gene}] S2-S6 on the device and the products on the host ({time.perf_counter() - t0:.1f} s)")
     finally:
         d.close()
     return consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, split_sam, psl, log=log,
@@ -367,11 +372,16 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     genes = gene_names_from_file(gene_names) if gene_names and os.path.exists(gene_names) \
         else gene_names_from_fasta(anchored_cds)
     anchors = [s.decode().upper() for _, s in read_fasta(anchored_cds)]
+    t0 = time.perf_counter()
     genome = [(h.split()[0], s.decode().upper()) for h, s in read_fasta(ref_seq)]
     with open(ref_ann) as fh:
         gtf = fh.readlines()
     index = ExonIndex.from_lines(gtf)
+    log(f"genome and annotation read: {len(genome)} contigs, {sum(len(s) for _, s in genome)} bp, "
+        f"{len(gtf)} GTF lines ({time.perf_counter() - t0:.1f} s)")
+    t0 = time.perf_counter()
     names, reads, lens = read_pairs(fastq1, fastq2)
+    log(f"ingest: {reads.shape[0] // 2} pairs ({time.perf_counter() - t0:.1f} s)")
     # the device path (S2-S6 in HBM) unless a test injects host backends
     on_device = aligner_factory is None and (searches is None or getattr(searches, "on_device", False))
     if searches is None:
@@ -383,7 +393,9 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     for gene, anchor in zip(genes, anchors):
         folder = os.path.join(out_folder, gene + "_fusion")
         os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
+        t0 = time.perf_counter()
         homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+        log(f"[{gene}] homologs: {len(homo_rows)} gene rows ({time.perf_counter() - t0:.1f} s)")
         prefix = os.path.join(folder, gene + "_fusion")
         if dev_reads is not None:
             results[gene] = run_gene_device(gene, anchor, names, *dev_reads, index, homo_rows, searches, prefix,
