@@ -33,6 +33,28 @@ _COMP = str.maketrans("ACGTNacgtn", "TGCANtgcan")
 STAT_NAMES = ("cap_overflow", "pool_overflow", "record_overflow")
 
 
+def _need(t, nbytes, what, dtype=None):
+    """A kernel operand: a contiguous device tensor of at least nbytes (checked on the host before
+    the launch, so a short buffer is an error, not an out-of-bounds access)."""
+    if t is None or not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{what}: a contiguous device tensor is required")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if t.numel() * t.element_size() < nbytes:
+        raise ValueError(f"{what}: {t.numel() * t.element_size()} bytes, the call reads or writes {nbytes}")
+
+
+def _check_se(reads_t, n, stride, recs_t, nrec_t, lens_t):
+    n, stride = int(n), int(stride)
+    if n < 0 or stride <= 0:
+        raise ValueError("n must be >= 0 and stride > 0")
+    _need(reads_t, n * stride, "reads_t")
+    _need(recs_t, n * MAX_REC * REC_DTYPE.itemsize, "recs_t")
+    _need(nrec_t, 4 * n, "nrec_t")
+    if lens_t is not None:
+        _need(lens_t, 4 * n, "lens_t")
+
+
 def _stream_handle(stream):
     if stream is None:
         return None
@@ -165,6 +187,7 @@ class GenomeIndex:
     def align_se_device(self, reads_t, n, stride, recs_t, nrec_t, lens_t=None, params=None, pe=None, id_base=0,
                         stream=None, ctx=None):
         c = self.ctx if ctx is None else ctx
+        _check_se(reads_t, n, stride, recs_t, nrec_t, lens_t)
         _lib.check(c, _lib.lib().af_genome_align_se_device(
             c, self.g, reads_t.data_ptr(), int(n), int(stride), None if lens_t is None else lens_t.data_ptr(),
             ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), int(id_base),
@@ -174,7 +197,10 @@ class GenomeIndex:
                             stream=None, ctx=None):
         """S5 on a shard of a query list: read r's bwa id is ids_t[r] (int64, its ordinal in the
         whole list), which decides mem_mark_primary_se's hash tie-breaks."""
+        import torch
         c = self.ctx if ctx is None else ctx
+        _check_se(reads_t, n, stride, recs_t, nrec_t, lens_t)
+        _need(ids_t, 8 * int(n), "ids_t", torch.int64)
         _lib.check(c, _lib.lib().af_genome_align_se_ids_device(
             c, self.g, reads_t.data_ptr(), int(n), int(stride), None if lens_t is None else lens_t.data_ptr(),
             ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), ids_t.data_ptr(),
@@ -183,6 +209,7 @@ class GenomeIndex:
     def align_pe_device(self, reads_t, n_pairs, stride, lens_t, recs_t, nrec_t, params=None, pe=None, stream=None,
                         ctx=None):
         c = self.ctx if ctx is None else ctx
+        _check_se(reads_t, 2 * int(n_pairs), stride, recs_t, nrec_t, lens_t)
         _lib.check(c, _lib.lib().af_genome_align_pe_device(
             c, self.g, reads_t.data_ptr(), int(n_pairs), int(stride), lens_t.data_ptr(),
             ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), recs_t.data_ptr(),
@@ -205,8 +232,23 @@ def s5_filter_device(ctx, recs_t, nrec_t, n, q_t, q_stride, q_lens_t, q_rows_t, 
     (int32 [1], optional) counts rows whose processed sequence was clipped to the stride; cont_t
     (uint8 [n], optional): the QNAME groups given by the caller (cont_t[q] != 0: query q continues
     the group of q - 1), for a shard of a wider query list."""
+    import torch
+    n, cap = int(n), int(cap)
     if int(s6_t.shape[0]) < cap or s6_lens_t.numel() < cap or s6_src_t.numel() < cap:
         raise ValueError("S6 buffers hold fewer than cap rows")
+    _need(recs_t, n * MAX_REC * REC_DTYPE.itemsize, "recs_t")
+    _need(nrec_t, 4 * n, "nrec_t")
+    _need(q_t, n * int(q_stride), "q_t")
+    _need(q_lens_t, 4 * n, "q_lens_t")
+    _need(q_rows_t, 4 * n, "q_rows_t", torch.int32)
+    _need(s6_t, cap * int(s6_t.shape[1]), "s6_t", torch.uint8)
+    _need(n6_t, 4, "n6_t")
+    if cont_t is not None:
+        _need(cont_t, n, "cont_t", torch.uint8)
+    for k in ("flag", "pos", "n_cigar"):
+        _need(s2_out[k], 4, f"s2_out[{k}]", torch.int32)
+    if s2_out["cigar"].numel() != s2_out["flag"].numel() * _lib.AF_MAX_CIGAR:
+        raise ValueError("s2_out['cigar'] must hold AF_MAX_CIGAR words per record")
     o = _lib.AlnOut(*(s2_out[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
     _lib.check(ctx, _lib.lib().af_s5_filter_device(
         ctx, recs_t.data_ptr(), nrec_t.data_ptr(), int(n), q_t.data_ptr(), int(q_stride), q_lens_t.data_ptr(),
