@@ -239,10 +239,9 @@ class CandidateDiscovery:
         rows = self.q_rows[:b + n5].long()
         pos = self.out["pos"][rows]
         key = (pos.long() * 2 + ((self.out["flag"][rows] >> 4) & 1).long()).cpu().numpy()
-        q = self.q[:b + n5].cpu().numpy()
+        seq = self.q[:b + n5].cpu().numpy()
         ql = self.q_lens[:b + n5].cpu().numpy()
         r = rows.cpu().numpy()
-        seq = [q[i, :ql[i]] for i in range(b + n5)]
         cig = self.out["cigar"][rows[b:]].cpu().numpy().view(np.uint32) if n5 else np.zeros((0, 32), np.uint32)
         self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s5_split_reads=n5)
         return LocalQueries(
@@ -277,8 +276,8 @@ class CandidateDiscovery:
         rows = self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
         rows = rows.reshape(n6, _blat.MAX_ROWS) if n6 else rows.reshape(0, _blat.MAX_ROWS)
         self.counts["s6_queries"] = n6
-        return dict(src=self.s6["src"][:n6].cpu().numpy(), s6_seq=[q6[k, :l6[k]] for k in range(n6)],
-                    psl=[rows[k] for k in range(n6)], n_psl=self.t_nh[:n6].cpu().numpy())
+        return dict(src=self.s6["src"][:n6].cpu().numpy(), s6_seq=q6, s6_len=l6, psl=rows,
+                    n_psl=self.t_nh[:n6].cpu().numpy())
 
     def s4_phase(self, q, ql):
         """S4 over the globally zipped pairs (rank 0): reads q uint8 [2P, w] pair-major, lens ql."""

@@ -44,9 +44,13 @@ class LocalQueries:
     """A rank's lists after S2 + S3 + the gathers (host arrays; rows are local read rows).
 
     t1 / t2: the tmp1 / tmp2 rows in samtools order with their keys (2 pos + strand) and the reads
-    as sequenced (seq uint8 [k, w], len); s5: the split reads (the S5 queries) in order with keys,
-    the anchored record's POS and CIGAR (cigar uint32 [k, 32], ncig), and the queries' SEQ in SAM
-    orientation (seq uint8 [k, w], len)."""
+    as sequenced (seq uint8 [k, w], len int32 [k]: bytes past a row's length are ignored); s5: the
+    split reads (the S5 queries) in order with keys, the anchored record's POS and CIGAR (cigar
+    uint32 [k, 32], ncig), and the queries' SEQ in SAM orientation (seq uint8 [k, w], len).
+
+    A backend's s5_s6_phase(ids, cont) returns dict(src int64 [m]: the survivors' S5 indices,
+    s6_seq uint8 [m, w] + s6_len int32 [m]: their S6 queries, psl PSL_DTYPE [m, MAX_ROWS] +
+    n_psl int32 [m]: their S6 rows)."""
 
     def __init__(self, t1, t2, s5):
         self.t1, self.t2, self.s5 = t1, t2, s5
@@ -70,41 +74,43 @@ def _allgatherv(arr, group, device, world):
     return allgatherv_device(t, group).cpu().numpy().view(a.dtype).reshape(-1, *a.shape[1:])
 
 
-def _pad_rows(rows, w):
-    out = np.full((len(rows), w), ord("N"), np.uint8)
-    for i, r in enumerate(rows):
-        out[i, :len(r)] = r
+def _block(seq, lens, idx, width):
+    """Rows idx of seq (uint8 [k, w]) as uint8 [len(idx), width], 'N' past each row's length."""
+    idx = np.asarray(idx, np.int64)
+    out = np.full((len(idx), width), ord("N"), np.uint8)
+    if len(idx):
+        w = min(width, int(seq.shape[1]))
+        out[:, :w] = np.asarray(seq)[idx, :w]
+        out[np.arange(width)[None, :] >= np.asarray(lens, np.int64)[idx][:, None]] = ord("N")
     return out
+
+
+def _width(lens):
+    """Row width for sequences of these lengths: the longest, at least 1, a multiple of 4."""
+    w = max(1, int(np.max(lens)) if len(lens) else 1)
+    return -(-w // 4) * 4
 
 
 def _i32(a):
     return np.asarray(a, np.int64).astype(np.int32).reshape(-1, 1)
 
 
-def _u8(x):
-    """A sequence as uint8 (bytes, str or an array)."""
-    if isinstance(x, str):
-        return np.frombuffer(x.encode(), np.uint8)
-    if isinstance(x, (bytes, bytearray)):
-        return np.frombuffer(bytes(x), np.uint8)
-    return np.asarray(x, np.uint8)
-
-
 PSL_WORDS = 82  # af_psl / blat.PSL_DTYPE as int32 words (328 B)
 
 
 def psl_table(surv, ords):
-    """S6's rows of the survivors as int32 rows: ordinal (2 words) + one af_psl row."""
+    """S6's rows of the survivors as int32 rows: ordinal (2 words) + one af_psl row, survivor by
+    survivor, each one's rows in order."""
     from .blat import PSL_DTYPE
-    parts = []
-    for k, o in enumerate(ords):
-        m = int(surv["n_psl"][k])
-        if m <= 0:
-            continue
-        r = np.ascontiguousarray(np.asarray(surv["psl"][k])[:m]).view(PSL_DTYPE)
-        parts.append(np.concatenate([np.full((m, 1), int(o), np.int64).view(np.int32).reshape(m, 2),
-                                     r.view(np.int32).reshape(m, PSL_WORDS)], axis=1))
-    return np.concatenate(parts) if parts else np.zeros((0, 2 + PSL_WORDS), np.int32)
+    n_psl = np.asarray(surv["n_psl"], np.int64)
+    if not len(n_psl):
+        return np.zeros((0, 2 + PSL_WORDS), np.int32)
+    P = np.asarray(surv["psl"]).view(PSL_DTYPE).reshape(len(n_psl), -1)
+    kk, rr = np.nonzero(np.arange(P.shape[1])[None, :] < n_psl[:, None])
+    m = len(kk)
+    sel = np.ascontiguousarray(P[kk, rr])
+    return np.concatenate([np.asarray(ords, np.int64)[kk].view(np.int32).reshape(m, 2),
+                           sel.view(np.int32).reshape(m, PSL_WORDS)], axis=1)
 
 
 def psl_rows(table, n, npsl):
@@ -144,46 +150,46 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     ids = ordinal[base:base + n5]
     cont = np.zeros(n5, np.uint8)
     rows5 = np.asarray(L.s5["row"], np.int64) + g0
-    local_of = {int(r): i for i, r in enumerate(rows5)}
-    for i in range(n5):
-        if ids[i] == 0:
-            continue
-        j = local_of.get(int(K5[o5[ids[i] - 1], 1]), -1)  # the global predecessor, when it is ours
-        if j < 0:
-            continue
-        a, b = int(L.s5["row"][j]), int(L.s5["row"][i])
-        cont[i] = a // 2 == b // 2 and L.s5["pos"][j] == L.s5["pos"][i] and L.s5["ncig"][j] == L.s5["ncig"][i] and \
-            np.array_equal(L.s5["cigar"][j, :L.s5["ncig"][j]], L.s5["cigar"][i, :L.s5["ncig"][i]])
+    has = np.nonzero(ids > 0)[0]
+    if len(has):
+        # the global predecessor of each query, when it is one of ours: then the same QNAME
+        # (pair, POS, CIGAR) continues its group
+        pred = K5[o5[ids[has] - 1], 1]
+        srt = np.argsort(rows5, kind="stable")
+        at = np.minimum(np.searchsorted(rows5[srt], pred), n5 - 1)
+        mine = rows5[srt][at] == pred
+        i, j = has[mine], srt[at][mine]
+        r5, p5, nc5 = (np.asarray(L.s5[k], np.int64) for k in ("row", "pos", "ncig"))
+        c5 = np.asarray(L.s5["cigar"], np.uint32)
+        live = np.arange(c5.shape[1])[None, :] < nc5[i][:, None]
+        same = (r5[j] // 2 == r5[i] // 2) & (p5[j] == p5[i]) & (nc5[j] == nc5[i]) & \
+            ((c5[j] == c5[i]) | ~live).all(axis=1)
+        cont[i] = same
     surv = backend.s5_s6_phase(ids, cont)
     # the survivors (ordinal, POS, CIGAR, S5 SEQ, S6 query) and their S6 rows, to every rank
     src = np.asarray(surv["src"], np.int64)
     ns = len(src)
-    w5 = max(1, int(max((len(x) for x in L.s5["seq"]), default=1)))
-    w6 = max(1, int(max((len(x) for x in surv["s6_seq"]), default=1)))
-    w5, w6 = -(-w5 // 4) * 4, -(-w6 // 4) * 4
-    s5b = _pad_rows([_u8(L.s5["seq"][int(k)]) for k in src], w5)
-    s6b = _pad_rows([_u8(x) for x in surv["s6_seq"]], w6)
-    W5 = _allgatherv(np.array([[w5, w6]], np.int64), group, device, world).max(axis=0)
-    s5b = np.pad(s5b, ((0, 0), (0, int(W5[0]) - w5)), constant_values=ord("N"))
-    s6b = np.pad(s6b, ((0, 0), (0, int(W5[1]) - w6)), constant_values=ord("N"))
+    l5 = np.asarray(L.s5["len"], np.int64)
+    l6 = np.asarray(surv["s6_len"], np.int64)
+    W5 = _allgatherv(np.array([[_width(l5), _width(l6)]], np.int64), group, device, world).max(axis=0)
+    s5b = _block(L.s5["seq"], l5, src, int(W5[0]))
+    s6b = _block(surv["s6_seq"], l6, np.arange(ns), int(W5[1]))
     ords = ids[src] if ns else np.zeros(0, np.int64)
     cig = np.asarray(L.s5["cigar"], np.uint32)[src] if ns else np.zeros((0, 32), np.uint32)
     rows = np.concatenate([
-        ords.astype(np.int64).view(np.int32).reshape(-1, 2) if ns else np.zeros((0, 2), np.int32),
+        ords.astype(np.int64).view(np.int32).reshape(-1, 2),
         _i32(np.asarray(L.s5["pos"])[src] if ns else []), _i32(np.asarray(L.s5["ncig"])[src] if ns else []),
-        cig.view(np.int32).reshape(-1, 32),
-        _i32([len(L.s5["seq"][int(k)]) for k in src]), _i32([len(x) for x in surv["s6_seq"]]),
-        _i32(surv["n_psl"]), s5b.view(np.int32).reshape(ns, int(W5[0]) // 4),
-        s6b.view(np.int32).reshape(ns, int(W5[1]) // 4),
+        cig.view(np.int32).reshape(-1, 32), _i32(l5[src]), _i32(l6), _i32(surv["n_psl"]),
+        s5b.view(np.int32).reshape(ns, int(W5[0]) // 4), s6b.view(np.int32).reshape(ns, int(W5[1]) // 4),
         # the read's global row (render: names)
         (rows5[src] if ns else np.zeros(0, np.int64)).view(np.int32).reshape(-1, 2)], axis=1)
     psl = psl_table(surv, ords)
     all_rows = _allgatherv(rows.astype(np.int32), group, device, world)
     all_psl = _allgatherv(psl, group, device, world)
     # S4's reads: the rank's tmp1 / tmp2 reads with their keys and global rows
-    w4 = max(1, int(max((len(_u8(x)) for x in list(L.t1["seq"]) + list(L.t2["seq"])), default=1)))
-    W4 = int(_allgatherv(np.array([[w4]], np.int64), group, device, world).max())
-    W4 = -(-W4 // 4) * 4
+    W4 = int(_allgatherv(np.array([[_width(np.concatenate([np.asarray(L.t1["len"], np.int64),
+                                                            np.asarray(L.t2["len"], np.int64)]))]], np.int64),
+                         group, device, world).max())
 
     def reads_rows(d):
         k = len(d["key"])
@@ -191,7 +197,8 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
             return np.zeros((0, 5 + W4 // 4), np.int32)
         return np.concatenate([np.stack([np.asarray(d["key"], np.int64), np.asarray(d["row"], np.int64) + g0],
                                         axis=1).view(np.int32).reshape(k, 4), _i32(d["len"]),
-                               _pad_rows([_u8(x) for x in d["seq"]], W4).view(np.int32).reshape(k, W4 // 4)], axis=1)
+                               _block(d["seq"], d["len"], np.arange(k), W4).view(np.int32).reshape(k, W4 // 4)],
+                              axis=1)
     T1 = _allgatherv(reads_rows(L.t1), group, device, world)
     T2 = _allgatherv(reads_rows(L.t2), group, device, world)
     counts = dict(tmp1=len(L.t1["key"]), tmp2=len(L.t2["key"]), s5_split_reads=n5, s6_queries=ns)

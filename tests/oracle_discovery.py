@@ -39,7 +39,8 @@ class OracleDiscovery:
             return res.pos[rows].astype(np.int64) * 2 + ((res.flag[rows] & 0x10) != 0)
 
         def seq_list(rows):
-            return [self._seq(int(r)).copy() for r in rows], self.lens[np.asarray(rows, np.int64)]
+            rows = np.asarray(rows, np.int64)
+            return self.reads[rows], self.lens[rows]
         s1, l1 = seq_list(t1)
         s2, l2 = seq_list(t2)
         rows5, seqs5 = [], []
@@ -57,7 +58,9 @@ class OracleDiscovery:
             dict(key=key(t2), row=np.asarray(t2, np.int64), seq=s2, len=l2),
             dict(key=key(rows5), row=rows5, pos=res.pos[rows5] if len(rows5) else np.zeros(0, np.int32),
                  ncig=res.n_cigar[rows5] if len(rows5) else np.zeros(0, np.int32),
-                 cigar=res.cigar[rows5] if len(rows5) else np.zeros((0, 32), np.uint32), seq=seqs5))
+                 cigar=res.cigar[rows5] if len(rows5) else np.zeros((0, 32), np.uint32),
+                 seq=_rows([np.frombuffer(x, np.uint8) for x in seqs5]),
+                 len=np.array([len(x) for x in seqs5], np.int32)))
 
     def s4_phase(self, q, ql):
         pe = oracle.default_pe(chunk_bases=self.chunk_bases)
@@ -65,7 +68,8 @@ class OracleDiscovery:
 
     def s5_s6_phase(self, ids, cont):
         n5 = len(self.q5)
-        out = dict(src=[], s6_seq=[], psl=[], n_psl=[])
+        out = dict(src=np.zeros(0, np.int64), s6_seq=np.zeros((0, 1), np.uint8), s6_len=np.zeros(0, np.int32),
+                   psl=np.zeros((0, blat.MAX_ROWS), blat.PSL_DTYPE), n_psl=np.zeros(0, np.int32))
         if not n5:
             return out
         buf = np.full((n5, max(len(s) for s in self.q5)), ord("N"), np.uint8)
@@ -85,16 +89,24 @@ class OracleDiscovery:
             lines += genome.sam_lines(self.og.names, name, self.q5[i].decode(), recs[i], nrec[i])
         split = genome_check.filter_genome_hits(lines)
         _, fa = blocks.split_read_queries(split)
-        out["src"] = [int(ln.split("\t")[0]) for ln in split]
-        out["s6_seq"] = [sq for _, sq in fa]
+        out["src"] = np.array([int(ln.split("\t")[0]) for ln in split], np.int64)
+        seqs = [sq for _, sq in fa]
+        out["s6_seq"] = _rows([np.frombuffer(x.encode(), np.uint8) for x in seqs])
+        out["s6_len"] = np.array([len(x) for x in seqs], np.int32)
         if fa:
-            rows, nr = self.tiles.search(out["s6_seq"], blat.params("split_tail"), blat.MAX_ROWS)
-            out["psl"] = [rows[k] for k in range(len(fa))]
-            out["n_psl"] = [int(nr[k]) for k in range(len(fa))]
+            out["psl"], out["n_psl"] = self.tiles.search(seqs, blat.params("split_tail"), blat.MAX_ROWS)
         return out
 
     def psl_lines(self, queries, rows, nrows):
         return blat.psl_lines(self.tiles, queries, np.stack(rows), np.asarray(nrows))
+
+
+def _rows(seqs):
+    """Sequences (uint8 arrays) as one uint8 [k, w] block ('N' padded)."""
+    out = np.full((len(seqs), max([1] + [len(x) for x in seqs])), ord("N"), np.uint8)
+    for i, x in enumerate(seqs):
+        out[i, :len(x)] = x
+    return out
 
 
 def tiles_for(genome_contigs):
