@@ -179,6 +179,84 @@ def spanning_blocks(sam_lines, index, homo_genes):
     return out
 
 
+class S4Records:
+    """S4's SAM records as `spanning_blocks` reads them, without the text: per record (in the
+    order bwa prints them: read 2k's records, then read 2k + 1's) its pair, RNAME (contig index,
+    -1 for '*'), POS (1-based, 0 for '*') and the length of its CIGAR's first M.  Built from the
+    af_grec rows (genome.REC_DTYPE [2 P, MAX_REC]) and counts of `bwa mem -M genome tmp1 tmp2`;
+    pair_names[k] is the QNAME of pair k."""
+
+    def __init__(self, pair_names, recs, nrec, contig_names):
+        import numpy as np
+        nrec = np.asarray(nrec, np.int64)
+        self.pair_names, self.contig_names = pair_names, list(contig_names)
+        if not len(nrec):
+            from .genome import REC_DTYPE
+            recs = np.zeros((0, 1), REC_DTYPE)
+        live = np.arange(recs.shape[1])[None, :] < np.minimum(nrec, recs.shape[1])[:, None]
+        rr, kk = np.nonzero(live)
+        e = recs[rr, kk]
+        self.pair = rr // 2
+        nc = e["n_cigar"].astype(np.int64)
+        cig = e["cigar"].astype(np.int64)
+        is_m = ((cig & 15) == 0) & (np.arange(cig.shape[1])[None, :] < nc[:, None])
+        self.ok = is_m.any(axis=1)
+        first = np.argmax(is_m, axis=1)
+        self.m_len = np.where(self.ok, cig[np.arange(len(first)), first] >> 4, 0)
+        rid = e["rid"].astype(np.int64)
+        self.rid = np.where(self.ok, rid, -1)
+        self.pos1 = np.where(rid >= 0, e["pos"].astype(np.int64) + 1, 0)
+        # QNAME groups (consecutive equal names): a record starts one where its pair's name
+        # differs from the previous record's
+        self.group_start = np.ones(len(rr), bool)
+        for t in np.flatnonzero(self.pair[1:] != self.pair[:-1]) + 1:
+            self.group_start[t] = pair_names[int(self.pair[t])] != pair_names[int(self.pair[t - 1])]
+        if len(rr):
+            self.group_start[1:] &= self.pair[1:] != self.pair[:-1]
+
+
+def spanning_blocks_records(R, index, homo_genes):
+    """`spanning_blocks` over S4Records (the same blocks; the groups no rule can keep -- one
+    record, or all on one contig within 2,000 nt -- are set aside vectorised)."""
+    import numpy as np
+    n = len(R.pair)
+    out = {}
+    if n:
+        starts = np.flatnonzero(R.group_start)
+        ends = np.r_[starts[1:], n]
+        c0 = np.where(R.ok, R.pos1 + 5, 5)
+        c1 = np.where(R.ok, R.pos1 + R.m_len - 1 - 5, -5)
+        lo = np.minimum.reduceat(np.minimum(c0, c1), starts)
+        hi = np.maximum.reduceat(np.maximum(c0, c1), starts)
+        one_chrom = np.minimum.reduceat(R.rid, starts) == np.maximum.reduceat(R.rid, starts)
+        keep = (ends - starts > 1) & ~(one_chrom & (hi - lo < 2000))
+        names = R.contig_names
+        for g in np.flatnonzero(keep):
+            a, b = int(starts[g]), int(ends[g])
+            homo_at = other_at = -1
+            other_gene = other_exon = None
+            for k2 in range(b - a):
+                r = a + k2
+                chrom = names[int(R.rid[r])] if R.ok[r] else ""
+                gene, exon = index.find_exon(chrom, int(c0[r]), int(c1[r]))
+                if gene[0] in homo_genes:
+                    homo_at = k2
+                elif gene[0] != "":
+                    if other_at == -1:
+                        other_at, other_gene, other_exon = k2, gene, exon
+                    elif gene[0] != other_gene[0]:
+                        other_at = -1
+                        break
+            if homo_at == -1 or other_at == -1:
+                continue
+            r = a + other_at
+            chrom = names[int(R.rid[r])] if R.ok[r] else ""
+            _insert(out.setdefault(chrom, []), index.dic.get(chrom), chrom, int(c0[r]), int(c1[r]), other_gene,
+                    other_exon, R.pair_names[int(R.pair[a])], "spanning")
+    widen(out, index)
+    return out
+
+
 def widen(blocks_chr, index):
     """Extend each block by 200 transcript bases on both sides (functions.py:490-495)."""
     for blocks in blocks_chr.values():

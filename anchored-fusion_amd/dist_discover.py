@@ -240,14 +240,18 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
                 w=(int(W5[0]), int(W5[1])), names=named), counts
 
 
-def render(result, backend, gene, genome_names):
-    """The texts consume_products reads, from search's rank-0 result (searched with names): S4's
-    SAM lines, the split_sam lines of the survivors (split.fa order) and S6's PSL."""
+def render(result, backend, gene, genome_names, s4_text=True):
+    """What consume_products reads, from search's rank-0 result (searched with names): S4's SAM
+    lines (blocks.S4Records, the fields Find_blocks reads, without s4_text), the split_sam lines
+    of the survivors (split.fa order) and S6's PSL."""
+    from .blocks import S4Records
     q, ql, recs, nrec, g1 = result["s4"]
     named = result["names"]
     s4 = []
-    if len(g1):
-        pn = [named[int(g)] for g in g1]
+    pn = [named[int(g)] for g in g1]
+    if not s4_text:
+        s4 = S4Records(pn, recs if len(g1) else None, nrec, genome_names)
+    elif len(g1):
         for k in range(len(g1)):
             sa = q[2 * k, :ql[2 * k]].tobytes().decode()
             sb = q[2 * k + 1, :ql[2 * k + 1]].tobytes().decode()

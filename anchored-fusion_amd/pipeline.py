@@ -219,7 +219,10 @@ def consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, s
     device path (run_gene_device) end here."""
     anchor_rec = [(gene, anchor)]
     homo = [row[3] for row in homo_rows]
-    blocks_chr = blk.spanning_blocks(s4, index, homo)
+    if isinstance(s4, blk.S4Records):
+        blocks_chr = blk.spanning_blocks_records(s4, index, homo)
+    else:
+        blocks_chr = blk.spanning_blocks(s4, index, homo)
     tails, tail_fa = blk.split_read_queries(split_sam)
     if tail_fa:
         blk.add_fine_blocks(blocks_chr, tails, psl, index, homo)
@@ -244,11 +247,11 @@ def consume_products(gene, anchor, index, homo_rows, searches, out_prefix, s4, s
 _OPS = "MIDNSHP=X"
 
 
-def device_products(d, gene, names, genome_names):
-    """The texts consume_products reads, from a discover.CandidateDiscovery pass: S4's SAM lines
-    (af_grec records rendered by genome.sam_lines), the pseudo-SAM lines of S5's survivors (the
-    `del_too_many_reads` output format, fn:735/760) and the PSL lines of S6.  Only the gathered
-    queries are decoded on the host."""
+def device_products(d, gene, names, genome_names, s4_text=False):
+    """What consume_products reads, from a discover.CandidateDiscovery pass: S4's records
+    (blocks.S4Records: the fields Find_blocks reads, no text; the SAM lines of genome.sam_lines
+    with s4_text), the pseudo-SAM lines of S5's survivors (the `del_too_many_reads` output
+    format, fn:735/760) and the PSL lines of S6.  Only the gathered queries reach the host."""
     import numpy as np
     import torch
 
@@ -263,11 +266,14 @@ def device_products(d, gene, names, genome_names):
 
     def seq(i):
         return q[i, :ql[i]].tobytes().decode()
-    s4 = []
-    for k in range(npair):
-        name = names[int(rows[2 * k]) // 2]
-        s4 += sam_lines(genome_names, name, seq(2 * k), recs[2 * k], nrec[2 * k])
-        s4 += sam_lines(genome_names, name, seq(2 * k + 1), recs[2 * k + 1], nrec[2 * k + 1])
+    pair_names = [names[int(r) // 2] for r in rows[0:2 * npair:2]]
+    if s4_text:
+        s4 = []
+        for k in range(npair):
+            s4 += sam_lines(genome_names, pair_names[k], seq(2 * k), recs[2 * k], nrec[2 * k])
+            s4 += sam_lines(genome_names, pair_names[k], seq(2 * k + 1), recs[2 * k + 1], nrec[2 * k + 1])
+    else:
+        s4 = blk.S4Records(pair_names, recs[:2 * npair], nrec[:2 * npair], genome_names)
     n6 = int(d.s6["n"].item())
     split_sam, psl = [], []
     if n6:
@@ -467,7 +473,7 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
                                                host_group=host_group)
             log(f"[{gene}] rank {rank}: {counts}")
             if rank == 0:
-                s4, split_sam, psl = dist_discover.render(res, backend, gene, [n for n, _ in genome])
+                s4, split_sam, psl = dist_discover.render(res, backend, gene, [n for n, _ in genome], s4_text=False)
         finally:
             close = getattr(backend, "close", None)
             if close:
