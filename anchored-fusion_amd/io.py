@@ -25,20 +25,29 @@ def _open(path):
 
 
 def read_fasta(path):
-    """Returns a list of (header_line_without_gt, sequence_bytes)."""
-    recs = []
-    name, chunks = None, []
+    """Returns a list of (header_line_without_gt, sequence_bytes): sequence lines joined with
+    their surrounding whitespace stripped, lines before the first header ignored.  Whole-buffer
+    form (C-speed joins: a 3.1 Gbp genome in seconds); records whose sequence lines carry blanks
+    or a CR outside a line end take the line-by-line rule."""
     with _open(path) as fh:
-        for line in fh:
-            line = line.rstrip(b"\r\n")
-            if line.startswith(b">"):
-                if name is not None:
-                    recs.append((name, b"".join(chunks)))
-                name, chunks = line[1:].decode(), []
-            elif name is not None:
-                chunks.append(line.strip())
-    if name is not None:
-        recs.append((name, b"".join(chunks)))
+        data = fh.read()
+    recs = []
+    at = 0 if data.startswith(b">") else data.find(b"\n>") + 1
+    if at == 0 and not data.startswith(b">"):
+        return recs
+    while at < len(data):
+        nxt = data.find(b"\n>", at)
+        end = len(data) if nxt < 0 else nxt + 1
+        rec = data[at:end]
+        nl = rec.find(b"\n")
+        head, body = (rec, b"") if nl < 0 else (rec[:nl], rec[nl + 1:])
+        name = head.rstrip(b"\r\n")[1:].decode()
+        if any(c in body for c in (b" ", b"\t", b"\x0b", b"\x0c")) or body.count(b"\r") != body.count(b"\r\n"):
+            seq = b"".join(ln.rstrip(b"\r\n").strip() for ln in body.split(b"\n"))
+        else:
+            seq = body.replace(b"\n", b"").replace(b"\r", b"")
+        recs.append((name, seq))
+        at = end
     return recs
 
 
