@@ -323,7 +323,9 @@ int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bas
         c->s2_pool = nullptr; c->s2_rmap = nullptr; c->s2_plist = nullptr; c->s2_scan = nullptr; c->s2_plan = nullptr;
         c->s2_cap_pairs = 0;
         const int64_t cap = std::max<int64_t>(n_pairs, 1 << 16);
-        c->s2_pool_cap = 2 * cap + (1 << 20);  // regions: candidates are a few % of the reads
+        // regions: 4 per read (40 B each) -- enough when every read is a candidate with a
+        // couple of regions (targeted input); a read past the pool is flagged and counted
+        c->s2_pool_cap = 8 * cap + (1 << 20);
         HIPCHK(c, hipMalloc(&c->s2_pool, sizeof(S2Reg) * c->s2_pool_cap));
         HIPCHK(c, hipMalloc(&c->s2_rmap, sizeof(int2) * 2 * cap));
         HIPCHK(c, hipMalloc(&c->s2_plist, sizeof(int32_t) * cap));
