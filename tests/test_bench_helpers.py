@@ -30,10 +30,10 @@ def test_cpu_baseline_c3_runs_every_stage(tmp_path):
 def test_genome_subset_windows():
     W = types.SimpleNamespace(names=["c1", "c2"], lens=[10_000, 5_000], offsets=[0, 10_512],
                               loci={"anchor": [("c1", 1000, 1200), ("c1", 3000, 3300)],
-                                    "p0": [("c2", 4000, 4100)]})
+                                    "p0": [("c2", 4700, 4900)]})
     blob = np.frombuffer(b"A" * 10_000 + b"N" * 512 + b"C" * 5_000, np.uint8)
     W.blob = torch.from_numpy(blob.copy())
     sub = bench.genome_subset(W, flank=500)
     # the anchor's exons on c1 -> one window (500 .. 3800); the partner's on c2 clipped at its end
-    assert [n for n, _ in sub] == ["c1:500-3800", "c2:3500-5000"]
-    assert sub[0][1] == b"A" * 3300 and sub[1][1] == b"C" * 1500
+    assert [n for n, _ in sub] == ["c1:500-3800", "c2:4200-5000"]
+    assert sub[0][1] == b"A" * 3300 and sub[1][1] == b"C" * 800
