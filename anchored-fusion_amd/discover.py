@@ -279,8 +279,9 @@ class CandidateDiscovery:
         return dict(src=self.s6["src"][:n6].cpu().numpy(), s6_seq=q6, s6_len=l6, psl=rows,
                     n_psl=self.t_nh[:n6].cpu().numpy())
 
-    def s4_phase(self, q, ql):
-        """S4 over the globally zipped pairs (rank 0): reads q uint8 [2P, w] pair-major, lens ql."""
+    def s4_phase(self, q, ql, pair_base=0):
+        """S4 over whole bwa chunks of the globally zipped pairs: reads q uint8 [2P, w] pair-major,
+        lens ql; pair_base = the first pair's index in that stream (read ids, chunk grid)."""
         import numpy as np
         import torch
         P2 = q.shape[0]
@@ -290,7 +291,7 @@ class CandidateDiscovery:
         nrec_t = torch.zeros(P2, dtype=torch.int32, device=self.dev)
         s0 = self.grp.streams[0]
         self.ref.align_pe_device(qt, P2 // 2, q.shape[1], lt, recs_t, nrec_t, params=self.p_genome,
-                                 pe=_lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0), stream=s0)
+                                 pe=_lib.default_pe(chunk_bases=self.chunk_bases, pair_base=int(pair_base)), stream=s0)
         s0.synchronize()
         return recs_t.cpu().numpy().view(_genome.REC_DTYPE).reshape(P2, MAX_REC), nrec_t.cpu().numpy()
 

@@ -16,14 +16,14 @@ So the ranks all-gather the sort keys of their tmp1 / tmp2 / split-read lists (s
 its split reads' global ordinal and whether its predecessor in the global order has the same
 QNAME (then both are mates of one pair, on the same rank).  S5, its check and S6 then run on
 every rank over its own queries with those ids and group flags (`af_genome_align_se_ids_device`,
-`af_s5_filter_device` with d_cont); S4 runs on rank 0 over the globally zipped pairs, whose reads
-the ranks send there.  Rank 0 gathers the survivors and their S6 rows and orders them by
+`af_s5_filter_device` with d_cont); S4 runs over the globally zipped pairs (all-gathered), each
+rank on its share of that stream's bwa chunks, the records gathered to rank 0.  Rank 0 gathers the survivors and their S6 rows and orders them by
 ordinal.  `search` stops there (the bench step); `render` turns the result into the texts
 `pipeline.consume_products` reads, equal to the one-process run's byte for byte
 (tests/test_dist_discover.py).
 
 The per-rank work is done by a backend with three phases -- `local_phase` (S2 + S3 + the
-gathers), `s4_phase` (rank 0) and `s5_s6_phase` -- implemented by discover.CandidateDiscovery
+gathers), `s4_phase(q, ql, pair_base)` (whole chunks of S4's stream) and `s5_s6_phase` -- implemented by discover.CandidateDiscovery
 on the GPU; the tests run the CPU oracle through the same driver.  Every exchange is a tensor
 all-gatherv (counts, then one max-padded all_gather) on `device` over `group`: RCCL on GPUs,
 gloo on CPU; read names (for `render` only) go over `host_group` as objects.
@@ -127,6 +127,39 @@ def psl_rows(table, n, npsl):
     return out
 
 
+def _s4_sharded(backend, q, ql, rank, world, group, device):
+    """S4 over the zipped pairs q / ql (every rank holds them): this rank aligns its share of the
+    stream's bwa chunks (shard.shard_pairs over the pairs' bases, pair_base = its first pair);
+    the records (compacted: one row per printed record, with its read and slot) are gathered
+    and rank 0 returns (recs REC_DTYPE [2 P, MAX_REC], nrec [2 P]); other ranks (None, None)."""
+    from .genome import MAX_REC, REC_DTYPE
+    from .shard import shard_pairs
+    P = len(ql) // 2
+    if not P:
+        return None, np.zeros(0, np.int32)
+    lo, hi = shard_pairs(ql.astype(np.int64).reshape(-1, 2).sum(axis=1), rank, world, backend.chunk_bases)
+    words = REC_DTYPE.itemsize // 4
+    if hi > lo:
+        r, n = backend.s4_phase(q[2 * lo:2 * hi], ql[2 * lo:2 * hi], pair_base=lo)
+        n = np.minimum(np.asarray(n, np.int64), MAX_REC)
+        rr, kk = np.nonzero(np.arange(MAX_REC)[None, :] < n[:, None])
+        body = np.ascontiguousarray(r[rr, kk]).view(np.int32).reshape(len(rr), words)
+        rows = np.concatenate([(rr + 2 * lo).astype(np.int64).view(np.int32).reshape(-1, 2),
+                               kk.astype(np.int32).reshape(-1, 1), body], axis=1)
+        cnt = n.astype(np.int32).reshape(-1, 1)
+    else:
+        rows = np.zeros((0, 3 + words), np.int32)
+        cnt = np.zeros((0, 1), np.int32)
+    rows = _allgatherv(rows, group, device, world)
+    cnt = _allgatherv(cnt, group, device, world)[:, 0]
+    if rank != 0:
+        return None, None
+    recs = np.zeros((2 * P, MAX_REC), REC_DTYPE)
+    read = rows[:, :2].copy().view(np.int64).reshape(-1)
+    recs[read, rows[:, 2]] = np.ascontiguousarray(rows[:, 3:]).view(REC_DTYPE).reshape(-1)
+    return recs, cnt
+
+
 def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_group=None):
     """The distributed S3-S6 of one gene (backend already holds this rank's S2 input).  Returns,
     on rank 0, dict(s4=(pair reads, lens, records, counts, t1 global rows), surv=(ordinal-sorted
@@ -213,14 +246,14 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
             named = {k: v for p in parts for k, v in p.items()}
         else:
             named = mine
-    if rank != 0:
-        return None, counts
-
     def split_reads(T):
         kg = T[:, :4].copy().view(np.int64).reshape(-1, 2)
         o = merge_order(kg[:, 0], kg[:, 1])
         seq = T[o, 5:].copy().view(np.uint8).reshape(len(o), -1)
         return kg[o, 1], T[o, 4], seq
+    # S4's input stream (tmp1 / tmp2 zipped in samtools order), the same on every rank; each rank
+    # aligns whole bwa chunks of it (its read ids and insert-size chunks those of one run) and
+    # rank 0 collects the records
     g1, l1, q1 = split_reads(T1)
     g2, l2, q2 = split_reads(T2)
     n_pair = min(len(g1), len(g2))
@@ -229,13 +262,13 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     if n_pair:
         q[0::2], q[1::2] = q1[:n_pair], q2[:n_pair]
         ql[0::2], ql[1::2] = l1[:n_pair], l2[:n_pair]
-        recs, nrec = backend.s4_phase(q, ql)
-    else:
-        recs, nrec = None, np.zeros(0, np.int32)
+    recs, nrec = _s4_sharded(backend, q, ql, rank, world, group, device)
+    counts["s4_pairs"] = n_pair
+    if rank != 0:
+        return None, counts
     order = np.argsort(all_rows[:, :2].copy().view(np.int64).reshape(-1), kind="stable")
     pk = all_psl[:, :2].copy().view(np.int64).reshape(-1)
     porder = np.argsort(pk, kind="stable")
-    counts["s4_pairs"] = n_pair
     return dict(s4=(q, ql, recs, nrec, g1[:n_pair]), surv=all_rows[order], psl=all_psl[porder],
                 w=(int(W5[0]), int(W5[1])), names=named), counts
 

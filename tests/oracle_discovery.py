@@ -62,9 +62,9 @@ class OracleDiscovery:
                  seq=_rows([np.frombuffer(x, np.uint8) for x in seqs5]),
                  len=np.array([len(x) for x in seqs5], np.int32)))
 
-    def s4_phase(self, q, ql):
+    def s4_phase(self, q, ql, pair_base=0):
         pe = oracle.default_pe(chunk_bases=self.chunk_bases)
-        return self.og.align_pe(q, ql, pe=pe, pair_base=0, threads=8)
+        return self.og.align_pe(q, ql, pe=pe, pair_base=pair_base, threads=8)
 
     def s5_s6_phase(self, ids, cont):
         n5 = len(self.q5)

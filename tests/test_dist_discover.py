@@ -27,7 +27,7 @@ def _inputs(paths):
     return names, reads, lens, genome, anchor
 
 
-def _worker(rank, world, port, paths, out):
+def _worker(rank, world, port, paths, out, chunk):
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
     import torch.distributed as dist
@@ -39,9 +39,9 @@ def _worker(rank, world, port, paths, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     names, reads, lens, genome, anchor = _inputs(paths)
     ln = np.full(reads.shape[0], reads.shape[1], np.int32) if lens is None else lens
-    lo, hi = shard.shard_pairs(ln.astype(np.int64).reshape(-1, 2).sum(axis=1), rank, world, CHUNK)
+    lo, hi = shard.shard_pairs(ln.astype(np.int64).reshape(-1, 2).sum(axis=1), rank, world, chunk)
     og = oracle.OracleGenome(genome)
-    backend = OracleDiscovery(anchor, og, tiles_for(genome), reads[2 * lo:2 * hi], ln[2 * lo:2 * hi], lo, CHUNK, GENE)
+    backend = OracleDiscovery(anchor, og, tiles_for(genome), reads[2 * lo:2 * hi], ln[2 * lo:2 * hi], lo, chunk, GENE)
     res, counts = dist_discover.search(backend, lo, rank, world, names=names.slice(lo, hi))
     if rank == 0:
         texts = dist_discover.render(res, backend, GENE, og.names)
@@ -51,11 +51,11 @@ def _worker(rank, world, port, paths, out):
     dist.destroy_process_group()
 
 
-def _run(paths, out, world):
+def _run(paths, out, world, chunk=CHUNK):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.start_processes(_worker, args=(world, port, paths, out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, paths, out, chunk), nprocs=world, join=True, start_method="spawn")
     with open(os.path.join(out, f"texts{world}.json")) as fh:
         return json.load(fh)
 
@@ -80,6 +80,21 @@ def test_dist_discover_equals_host_path(world_and_host, world):
     assert got[0] == s4
     assert got[1] == split_sam
     assert got[2] == psl
+
+
+def test_dist_discover_s4_over_several_chunks(world_and_host, tmp_path):
+    """bwa chunks of 20 kbases: S4's stream spans several chunks, so each of 3 ranks aligns its
+    share of them (pair_base = its first S4 pair) and rank 0 collects the records."""
+    from oracle_backends import OracleAligner, oracle_searches
+    paths, _, _ = world_and_host
+    chunk = 20_000
+    names, reads, lens, genome, anchor = _inputs(paths)
+    res = OracleAligner(anchor, chunk_bases=chunk).align_pairs(reads, lens)
+    host = pipeline.host_products(GENE, names, reads, lens, res, oracle_searches(genome, chunk), log=lambda *_: None)
+    s4_bases = sum(len(ln.split("\t")[9]) for ln in host[0] if int(ln.split("\t")[1]) & 0x900 == 0)
+    assert s4_bases > 3 * chunk  # every rank gets S4 work
+    got = _run(paths, str(tmp_path), 3, chunk)
+    assert [list(x) for x in host] == got
 
 
 def test_dist_discover_one_process_without_group(world_and_host):
