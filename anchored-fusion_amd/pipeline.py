@@ -442,7 +442,7 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
                  aligner_factory, log, group, rank, world, filt=None, chunk_bases=10_000_000, backend_factory=None):
     """cli --gpus N: every rank ingests its share of the FASTQ pair (shard.read_pairs_sharded:
     BGZF parts, whole bwa chunks per rank) and runs S2-S6 on it with the global order of one run
-    (dist_discover: S5's read ids and QNAME groups from all-gathered sort keys, S4 on rank 0 over
+    (dist_discover: S5's read ids and QNAME groups from all-gathered sort keys, S4 per rank on whole chunks of
     the globally zipped tmp1 / tmp2 lists); rank 0 renders the texts and runs the host stages."""
     import torch
     import torch.distributed as dist

@@ -362,7 +362,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     def step(k1=None, ph=None):
         if world > 1:
             # the product's multi-GPU step (dist_discover): S2-S6 on this rank's chunks with the
-            # global read ids and QNAME groups, S4 on rank 0 over the globally zipped lists, the
+            # global read ids and QNAME groups, S4 on whole chunks of the globally zipped stream per rank, the
             # survivors and their S6 rows all-gathered over RCCL
             _, c = dist_discover.search(disc.attach(reads_t, None, k1), lo, rank, world, device=dev)
             step_counts.update(c)
@@ -431,7 +431,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
                         + (f" sharded over {world} GPUs" if world > 1 else "")
                         + f", bwa genome index {genome_bp / 1e9:.2f} Gbp HBM-resident, one anchor (BCR NM_004327.4); "
                           "step = S2 + S3 sort/partition + S4/S5 genome bwa mem + S5 genome check + S6 BLAT"
-                        + (" per rank with the global order (dist_discover: keys all-gathered, S4 on rank 0, "
+                        + (" per rank with the global order (dist_discover: keys all-gathered, S4 sharded by its chunk grid, "
                            "survivors all-gathered over RCCL)" if world > 1 else ""),
             "pairs_total": N, "pairs_per_gpu": n, "read_len": L, "genome_bp": genome_bp, "anchor_len": len(anchor),
             "parallelism": f"dp{world}", "batches": n_launch, "pairs_per_batch": bp, "inflight": G,

@@ -1,6 +1,6 @@
 """The CPU oracle as a backend of anchored_fusion_amd.dist_discover -- TEST INFRASTRUCTURE ONLY.
 
-The three phases of a rank (S2 + S3 + the gathers; S4 on rank 0; S5 with the given read ids,
+The three phases of a rank (S2 + S3 + the gathers; S4 on whole chunks of its stream; S5 with the given read ids,
 its genome check with the given QNAME groups, S6) computed by oracle/bwa_pe.c, oracle/blat.c and
 the host restatements the consumer stages use (align.partition, genome_check, blocks), so the
 distributed driver can be checked on CPU with gloo against the one-process host path."""

@@ -1,5 +1,5 @@
 """dist_discover on CPU with gloo: S3-S6 of a sample sharded over 1-3 ranks, each rank on its own
-whole bwa chunks (S5 with the global read ids and QNAME groups, S4 on rank 0 over the globally
+whole bwa chunks (S5 with the global read ids and QNAME groups, S4 per rank on whole chunks of the globally
 zipped tmp1 / tmp2 lists), equal to the one-process host path (pipeline.host_products) text for
 text -- S4's SAM lines, the split_sam lines S5's check keeps, S6's PSL lines.  The backend is the
 CPU oracle (tests/oracle_discovery.py); the GPU backend is discover.CandidateDiscovery."""
