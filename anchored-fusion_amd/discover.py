@@ -214,7 +214,6 @@ class CandidateDiscovery:
     def local_phase(self):
         """S2 + S3 + the gathers of this rank: tmp1 reads at query rows [0, n1), tmp2 at [n1, n1 +
         n2) (both as sequenced), the split reads (S5 queries, SAM orientation) after them."""
-        import numpy as np
         import torch
 
         from .dist_discover import LocalQueries
@@ -236,23 +235,20 @@ class CandidateDiscovery:
         b = n1 + n2
         n5 = max(0, min(int(self.n_q.item()), self.qcap) - b)
         self._lay = (n1, n2, n5)
+        # the lists stay in HBM (dist_discover exchanges them over RCCL)
         rows = self.q_rows[:b + n5].long()
         pos = self.out["pos"][rows]
-        key = (pos.long() * 2 + ((self.out["flag"][rows] >> 4) & 1).long()).cpu().numpy()
-        seq = self.q[:b + n5].cpu().numpy()
-        ql = self.q_lens[:b + n5].cpu().numpy()
-        r = rows.cpu().numpy()
-        cig = self.out["cigar"][rows[b:]].cpu().numpy().view(np.uint32) if n5 else np.zeros((0, 32), np.uint32)
+        key = pos.long() * 2 + ((self.out["flag"][rows] >> 4) & 1).long()
+        seq, ql = self.q[:b + n5], self.q_lens[:b + n5]
         self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s5_split_reads=n5)
         return LocalQueries(
-            dict(key=key[:n1], row=r[:n1], seq=seq[:n1], len=ql[:n1]),
-            dict(key=key[n1:b], row=r[n1:b], seq=seq[n1:b], len=ql[n1:b]),
-            dict(key=key[b:], row=r[b:], pos=pos[b:].cpu().numpy(), ncig=self.out["n_cigar"][rows[b:]].cpu().numpy(),
-                 cigar=cig, seq=seq[b:], len=ql[b:]))
+            dict(key=key[:n1], row=rows[:n1], seq=seq[:n1], len=ql[:n1]),
+            dict(key=key[n1:b], row=rows[n1:b], seq=seq[n1:b], len=ql[n1:b]),
+            dict(key=key[b:], row=rows[b:], pos=pos[b:], ncig=self.out["n_cigar"][rows[b:]],
+                 cigar=self.out["cigar"][rows[b:]], seq=seq[b:], len=ql[b:]))
 
     def s5_s6_phase(self, ids, cont):
         """S5 with the queries' global ids, its genome check with the given QNAME groups, S6."""
-        import numpy as np
         import torch
         n1, n2, n5 = self._lay
         b = n1 + n2
@@ -260,8 +256,9 @@ class CandidateDiscovery:
         pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
         recs = self.q_recs.view(torch.int32)
         w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
-        ids_t = torch.from_numpy(np.ascontiguousarray(ids, np.int64)).to(self.dev)
-        cont_t = torch.from_numpy(np.ascontiguousarray(cont, np.uint8)).to(self.dev)
+        ids_t = ids.to(self.dev, torch.int64).contiguous()
+        cont_t = cont.to(self.dev, torch.uint8).contiguous()
+        s0.wait_stream(torch.cuda.current_stream(self.dev))  # ids / cont were made on the current stream
         if n5:
             self.ref.align_se_ids_device(self.q[b:], n5, self.L, ids_t, recs[b * w:], self.q_nh[b:],
                                          lens_t=self.q_lens[b:], params=self.p_genome, pe=pe, stream=s0)
@@ -272,28 +269,27 @@ class CandidateDiscovery:
                                      lens_t=self.s6["lens"], p=self.p_tail, stream=s0)
         s0.synchronize()
         n6 = int(self.s6["n"].item())
-        q6, l6 = self.s6["q"][:n6].cpu().numpy(), self.s6["lens"][:n6].cpu().numpy()
-        rows = self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
-        rows = rows.reshape(n6, _blat.MAX_ROWS) if n6 else rows.reshape(0, _blat.MAX_ROWS)
         self.counts["s6_queries"] = n6
-        return dict(src=self.s6["src"][:n6].cpu().numpy(), s6_seq=q6, s6_len=l6, psl=rows,
-                    n_psl=self.t_nh[:n6].cpu().numpy())
+        return dict(src=self.s6["src"][:n6], s6_seq=self.s6["q"][:n6], s6_len=self.s6["lens"][:n6],
+                    psl=self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].view(torch.int32),
+                    n_psl=self.t_nh[:n6])
 
     def s4_phase(self, q, ql, pair_base=0):
         """S4 over whole bwa chunks of the globally zipped pairs: reads q uint8 [2P, w] pair-major,
         lens ql; pair_base = the first pair's index in that stream (read ids, chunk grid)."""
-        import numpy as np
         import torch
-        P2 = q.shape[0]
-        qt = torch.from_numpy(np.ascontiguousarray(q)).to(self.dev)
-        lt = torch.from_numpy(np.ascontiguousarray(ql, np.int32)).to(self.dev)
-        recs_t = torch.zeros(P2 * MAX_REC * _genome.REC_DTYPE.itemsize // 4, dtype=torch.int32, device=self.dev)
+        P2 = int(q.shape[0])
+        qt = q.to(self.dev, torch.uint8).contiguous()
+        lt = ql.to(self.dev, torch.int32).contiguous()
+        words = _genome.REC_DTYPE.itemsize // 4
+        recs_t = torch.zeros((P2, MAX_REC, words), dtype=torch.int32, device=self.dev)
         nrec_t = torch.zeros(P2, dtype=torch.int32, device=self.dev)
         s0 = self.grp.streams[0]
-        self.ref.align_pe_device(qt, P2 // 2, q.shape[1], lt, recs_t, nrec_t, params=self.p_genome,
+        s0.wait_stream(torch.cuda.current_stream(self.dev))  # q / ql were made on the current stream
+        self.ref.align_pe_device(qt, P2 // 2, int(qt.shape[1]), lt, recs_t, nrec_t, params=self.p_genome,
                                  pe=_lib.default_pe(chunk_bases=self.chunk_bases, pair_base=int(pair_base)), stream=s0)
         s0.synchronize()
-        return recs_t.cpu().numpy().view(_genome.REC_DTYPE).reshape(P2, MAX_REC), nrec_t.cpu().numpy()
+        return recs_t, nrec_t
 
     def psl_lines(self, queries, rows, nrows):
         return _blat.psl_lines(self.tiles_ref, queries, rows, nrows)

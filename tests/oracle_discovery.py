@@ -58,18 +58,20 @@ class OracleDiscovery:
             dict(key=key(t2), row=np.asarray(t2, np.int64), seq=s2, len=l2),
             dict(key=key(rows5), row=rows5, pos=res.pos[rows5] if len(rows5) else np.zeros(0, np.int32),
                  ncig=res.n_cigar[rows5] if len(rows5) else np.zeros(0, np.int32),
-                 cigar=res.cigar[rows5] if len(rows5) else np.zeros((0, 32), np.uint32),
+                 cigar=(res.cigar[rows5] if len(rows5) else np.zeros((0, 32), np.uint32)).view(np.int32),
                  seq=_rows([np.frombuffer(x, np.uint8) for x in seqs5]),
                  len=np.array([len(x) for x in seqs5], np.int32)))
 
     def s4_phase(self, q, ql, pair_base=0):
         pe = oracle.default_pe(chunk_bases=self.chunk_bases)
-        return self.og.align_pe(q, ql, pe=pe, pair_base=pair_base, threads=8)
+        recs, nrec = self.og.align_pe(_np(q), _np(ql).astype(np.int32), pe=pe, pair_base=pair_base, threads=8)
+        return recs.view(np.int32).reshape(recs.shape[0], recs.shape[1], -1), nrec
 
     def s5_s6_phase(self, ids, cont):
+        ids, cont = _np(ids), _np(cont)
         n5 = len(self.q5)
         out = dict(src=np.zeros(0, np.int64), s6_seq=np.zeros((0, 1), np.uint8), s6_len=np.zeros(0, np.int32),
-                   psl=np.zeros((0, blat.MAX_ROWS), blat.PSL_DTYPE), n_psl=np.zeros(0, np.int32))
+                   psl=np.zeros((0, blat.MAX_ROWS, 82), np.int32), n_psl=np.zeros(0, np.int32))
         if not n5:
             return out
         buf = np.full((n5, max(len(s) for s in self.q5)), ord("N"), np.uint8)
@@ -94,11 +96,16 @@ class OracleDiscovery:
         out["s6_seq"] = _rows([np.frombuffer(x.encode(), np.uint8) for x in seqs])
         out["s6_len"] = np.array([len(x) for x in seqs], np.int32)
         if fa:
-            out["psl"], out["n_psl"] = self.tiles.search(seqs, blat.params("split_tail"), blat.MAX_ROWS)
+            rows, out["n_psl"] = self.tiles.search(seqs, blat.params("split_tail"), blat.MAX_ROWS)
+            out["psl"] = rows.view(np.int32).reshape(len(seqs), blat.MAX_ROWS, -1)
         return out
 
     def psl_lines(self, queries, rows, nrows):
         return blat.psl_lines(self.tiles, queries, np.stack(rows), np.asarray(nrows))
+
+
+def _np(x):
+    return x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
 
 
 def _rows(seqs):

@@ -42,7 +42,7 @@ def _worker(rank, world, port, paths, out, chunk):
     lo, hi = shard.shard_pairs(ln.astype(np.int64).reshape(-1, 2).sum(axis=1), rank, world, chunk)
     og = oracle.OracleGenome(genome)
     backend = OracleDiscovery(anchor, og, tiles_for(genome), reads[2 * lo:2 * hi], ln[2 * lo:2 * hi], lo, chunk, GENE)
-    res, counts = dist_discover.search(backend, lo, rank, world, names=names.slice(lo, hi))
+    res, counts = dist_discover.search(backend, lo, rank, world, names=names.slice(lo, hi), s4_reads=True)
     if rank == 0:
         texts = dist_discover.render(res, backend, GENE, og.names)
         with open(os.path.join(out, f"texts{world}.json"), "w") as fh:
@@ -107,5 +107,5 @@ def test_dist_discover_one_process_without_group(world_and_host):
     og = oracle.OracleGenome(genome)
     ln = np.full(reads.shape[0], reads.shape[1], np.int32) if lens is None else lens
     backend = OracleDiscovery(anchor, og, tiles_for(genome), reads, ln, 0, CHUNK, GENE)
-    res, _ = dist_discover.search(backend, 0, 0, 1, names=names)
+    res, _ = dist_discover.search(backend, 0, 0, 1, names=names, s4_reads=True)
     assert [list(x) for x in dist_discover.render(res, backend, GENE, og.names)] == host

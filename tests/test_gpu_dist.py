@@ -28,7 +28,7 @@ def test_gpu_backend_equals_oracle_host_path(tmp_path):
     searches = pipeline.Searches(genome, device=0, chunk_bases=CHUNK)
     backend = pipeline.gpu_backend(0, CHUNK)(anchor, reads, lens, 0, searches, GENE)
     try:
-        out, counts = dist_discover.search(backend, 0, 0, 1, device="cuda:0", names=names)
+        out, counts = dist_discover.search(backend, 0, 0, 1, device="cuda:0", names=names, s4_reads=True)
         got = dist_discover.render(out, backend, GENE, [n for n, _ in genome])
     finally:
         backend.close()

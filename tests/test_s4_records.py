@@ -41,8 +41,9 @@ def test_records_path_equals_text_path(tmp_path):
     og = oracle.OracleGenome(contigs)
     ln = np.full(reads.shape[0], reads.shape[1], np.int32) if lens is None else lens
     backend = OracleDiscovery(anchor, og, tiles_for(contigs), reads, ln, 0, CHUNK, GENE)
-    res, _ = dist_discover.search(backend, 0, 0, 1, names=names)
-    q, ql, recs, nrec, g1 = res["s4"]
+    res, _ = dist_discover.search(backend, 0, 0, 1, names=names, s4_reads=True)
+    q, ql, recs, nrec, g1 = (x.numpy() for x in res["s4"])
+    recs = recs.view(genome.REC_DTYPE).reshape(recs.shape[0], recs.shape[1])
     pn = [res["names"][int(g)] for g in g1]
     seqs = [q[r, :ql[r]].tobytes().decode() for r in range(len(ql))]
     homo = ["ENSG00000186716.21"]
