@@ -432,7 +432,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
                         + f", bwa genome index {genome_bp / 1e9:.2f} Gbp HBM-resident, one anchor (BCR NM_004327.4); "
                           "step = S2 + S3 sort/partition + S4/S5 genome bwa mem + S5 genome check + S6 BLAT"
                         + (" per rank with the global order (dist_discover: keys all-gathered, S4 sharded by its chunk grid, "
-                           "survivors all-gathered over RCCL)" if world > 1 else ""),
+                           "survivors and S4 records gathered to rank 0 over RCCL)" if world > 1 else ""),
             "pairs_total": N, "pairs_per_gpu": n, "read_len": L, "genome_bp": genome_bp, "anchor_len": len(anchor),
             "parallelism": f"dp{world}", "batches": n_launch, "pairs_per_batch": bp, "inflight": G,
         },
