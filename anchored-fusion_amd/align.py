@@ -329,7 +329,7 @@ class AnchorAligner:
         first n_rows entries; n_rows a host count).  mode _lib.AF_GATHER_SEQUENCED (S4's `samtools
         fastq`, AF:186-188) or _lib.AF_GATHER_SPLIT_SAM (S5's split reads, functions.py:705-716;
         out_t gives FLAG / CIGAR).  Query k goes to row first + k * step of q_t (uint8 [cap, stride]);
-        n_q_t (int32 [1], optional) receives the slot count for af_place_device."""
+        n_q_t (int32 [1], optional) receives the slot count (the query count the genome calls and BLAT read on the device)."""
         cap = int(q_t.shape[0])
         if q_t.dim() != 2 or int(q_t.shape[1]) != int(stride) or q_lens_t.numel() < cap:
             raise ValueError("q_t must be [cap, stride] and q_lens_t hold cap entries")
