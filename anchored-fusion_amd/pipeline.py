@@ -337,11 +337,13 @@ def upload_reads(reads, lens, device):
     import torch
     n, width = reads.shape
     stride = max(8, -(-width // 8) * 8)
-    host = np.full((n, stride), ord("N"), dtype=np.uint8)
-    host[:, :width] = reads
     ln = np.full(n, width, np.int32) if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
     dev = torch.device("cuda", device)
-    reads_t = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
+    # the rows go up as read (no padded host copy: 15 GB at configs[2]) and are padded in HBM
+    reads_t = torch.full((n, stride), ord("N"), dtype=torch.uint8, device=dev)
+    step = max(1, (1 << 30) // max(1, width))  # 1 GiB per host-to-device copy
+    for a in range(0, n, step):
+        reads_t[a:a + step, :width] = torch.from_numpy(np.ascontiguousarray(reads[a:a + step])).to(dev)
     lens_t = torch.from_numpy(ln).to(dev)
     pair_bases = ln.astype(np.int64).reshape(-1, 2).sum(axis=1)
     torch.cuda.synchronize(dev)
