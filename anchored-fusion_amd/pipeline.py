@@ -397,6 +397,8 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
     if aligner_factory is None:
         aligner_factory = _default_aligner(device, chunk_bases)
     dev_reads = upload_reads(reads, lens, device) if on_device and reads.shape[0] else None
+    if dev_reads is not None:
+        reads = lens = None  # the device copy is the one the genes read (15 GB at configs[2])
     results = {}
     for gene, anchor in zip(genes, anchors):
         folder = os.path.join(out_folder, gene + "_fusion")
