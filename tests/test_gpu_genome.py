@@ -92,3 +92,30 @@ def test_pe_records_equal_oracle(world):
         msg = _rec_equal(ro[r], rg[r], min(no[r], 8))
         assert msg is None, (r, msg)
     assert int(((rg[:, 0]["flag"] & 2) != 0).sum()) > 1500  # proper pairs found
+
+
+def test_pe_rescue_case_equals_oracle():
+    """tests/test_genome_rescue_blocks.py's crafted pairs (a mate placeable only by mem_matesw,
+    2.5 kb inserts): the kernel's records equal the oracle's with rescue on and off."""
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.genome import GenomeIndex
+    from test_genome_rescue_blocks import L, crafted
+    contigs, reads, _ = crafted()
+    og, gg = oracle.OracleGenome(contigs), GenomeIndex(contigs, device=0)
+    try:
+        lens = np.full(reads.shape[0], L, np.int32)
+        for matesw in (50, 0):
+            pe_o = oracle.default_pe()
+            pe_o.max_matesw = matesw
+            pe_g = _lib.default_pe()
+            pe_g.max_matesw = matesw
+            ro, no = og.align_pe(reads, lens, pe=pe_o, pair_base=0, threads=8)
+            rg, ng = gg.align_pe(reads, lens, pe=pe_g)
+            assert np.array_equal(no, ng), matesw
+            for r in range(len(no)):
+                msg = _rec_equal(ro[r], rg[r], min(no[r], 8))
+                assert msg is None, (matesw, r, msg)
+            probe = rg[len(reads) - 1, 0]
+            assert bool(probe["flag"] & 4) == (matesw == 0)
+    finally:
+        gg.close()
