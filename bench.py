@@ -468,7 +468,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     tiles.close()
 
 
-def genome_subset(W, flank=1_000_000):
+def genome_subset(W, flank=250_000):
     """The CPU baseline's genome: a window of each embedded gene's locus +- flank (host copies,
     taken before the bench frees the world's blob).  The step's S4/S5 queries and S6 tails come
     from these loci (anchor reads, their mates in the partner genes or the anchor's introns)."""
@@ -529,7 +529,7 @@ def cpu_baseline_c3(anchor, reads_t, args, subset):
     (oracle/bwa_pe.c, bwa-mem PE restated) + S3 (samtools order and filters) + the queries'
     gathers + S4 / S5 (the same restatement's genome calls, FM index) + S5's genome check + S6
     (oracle/blat.c, -minScore=20, 11-mer tiles, on S5's survivors), repeated for --cpu-seconds.  The genome of S4/S5/S6 is `subset`
-    (genome_subset: the gene loci +- 1 Mb) -- an oracle index of the whole 3.1 Gbp takes longer to
+    (genome_subset: the gene loci +- 250 kb) -- an oracle index of the whole 3.1 Gbp takes longer to
     build than the bench runs."""
     import numpy as np
 
@@ -588,7 +588,7 @@ def cpu_baseline_c3(anchor, reads_t, args, subset):
                       f"genome bwa mem + S5 genome check + S6 BLAT on the oracle (C restatements: oracle/bwa_pe.c, oracle/blat.c; "
                       f"bwa, BLAT and samtools are absent), OpenMP {threads} threads = the GPU's host CPU share "
                       f"(OMP_NUM_THREADS; host_cpus_visible is the whole machine's count); S4/S5/S6 genome = "
-                      f"the {len(subset)} gene-locus windows +- 1 Mb ({sum(len(q) for _, q in subset) / 1e6:.1f} Mbp, "
+                      f"the {len(subset)} gene-locus windows +- 250 kb ({sum(len(q) for _, q in subset) / 1e6:.1f} Mbp, "
                       f"oracle indexes built in {t_index:.1f} s, untimed)"}
 
 
