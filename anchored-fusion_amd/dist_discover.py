@@ -94,11 +94,6 @@ def _order(keys, rows):
     return o[torch.argsort(keys[o], stable=True)]
 
 
-def merge_order(keys, rows):
-    """numpy form of _order (tests, host callers)."""
-    return np.lexsort((np.asarray(rows, np.int64), np.asarray(keys, np.int64)))
-
-
 def _width(lens):
     """Row width for sequences of these lengths: the longest, at least 1, a multiple of 4."""
     w = max(1, int(lens.max()) if lens.numel() else 1)
