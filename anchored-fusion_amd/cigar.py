@@ -59,13 +59,6 @@ def normalize(cigar, seq):
     return merged, seq
 
 
-def split_type(ops):
-    """'SM' / 'MS' for a two-op split read, else None (functions.py:917-918, 930)."""
-    if len(ops) != 2:
-        return None
-    return "SM" if (ops[0][2] == "S" and ops[1][2] == "M") else "MS"
-
-
 _RC = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N", "H": "H"}
 
 
