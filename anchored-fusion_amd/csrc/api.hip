@@ -69,6 +69,10 @@ struct af_ctx {
     // the genome calls S4 / S5 (bwa_genome.hip): per-lane / per-wave scratch, per-call pools
     uint8_t *g1_scr = nullptr, *g2_scr = nullptr;
     int g1_threads = 0, g2_waves = 0;
+    // the paired-end records beside the single-end ones (af_genome_align_pe_se_device): their own
+    // per-wave scratch, and the event that orders them after the shared seed / region kernels
+    uint8_t *g2_scr_pe = nullptr, *zscratch_pe = nullptr;
+    hipEvent_t g_ev = nullptr;
     GIv *g_iv = nullptr;
     GReg *g_reg = nullptr;
     int64_t g_iv_cap = 0, g_reg_cap = 0, g_cap_reads = 0;
@@ -547,6 +551,8 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->s2_pes); af_free(c->s2_cstart); af_free(c->s2_nchunks);
     af_free(c->s3_keys); af_free(c->s3_temp); af_free(c->s3_counts);
     af_free(c->g_sel); af_free(c->g_sel_n); af_free(c->g_temp);
+    af_free(c->g2_scr_pe); af_free(c->zscratch_pe);
+    if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
     af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n);
     af_free(c->g_iv_off); af_free(c->g_ghist); af_free(c->g_nchunks); af_free(c->g_cstart); af_free(c->g_scan);
@@ -1193,6 +1199,66 @@ int af_genome_align_pe_device(af_ctx *c, const af_genome *g, const uint8_t *d_re
                                        c->g1_threads, c->g2_scr, c->g2_waves, c->zscratch, s));
     HIPCHK(c, af_launch_genome_pe(g->dev, d_reads, stride, d_lens, nullptr, n_pairs, *p, o, w, sw, c->g2_scr,
                                   c->g2_waves, c->zscratch, d_recs, d_n_rec, s));
+    return AF_OK;
+}
+
+int af_genome_align_pe_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs, int64_t n_se,
+                                 int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe_s4,
+                                 const af_pe *pe_s5, int64_t se_id_base, const int64_t *d_se_ids, af_grec *d_recs,
+                                 int32_t *d_n_rec, void *stream, void *stream_pe) {
+    af_pe e4, e5;
+    if (pe_s4) e4 = *pe_s4;
+    else af_pe_default(&e4);
+    if (pe_s5) e5 = *pe_s5;
+    else af_pe_default(&e5);
+    int rc = check_genome_call(c, g, p, &e4, stride);
+    if (rc || (rc = check_pe(c, &e5))) return rc;
+    if (n_pairs < 0 || n_se < 0 || (n_pairs + n_se > 0 && (!d_reads || !d_lens || !d_recs || !d_n_rec)))
+        return fail(c, AF_E_INVALID, "null argument (the reads' lengths are required)");
+    // one launch of the seed / region kernels holds both calls: their options must agree
+    if (e4.split_width != e5.split_width || e4.max_mem_intv != e5.max_mem_intv || e4.max_chain_gap != e5.max_chain_gap)
+        return fail(c, AF_E_INVALID, "S4 and S5 seeding options differ (split_width, max_mem_intv, max_chain_gap)");
+    const int64_t n = 2 * n_pairs + n_se;
+    if (n == 0) return AF_OK;
+    if (n > INT32_MAX / 16) return fail(c, AF_E_INVALID, "too many reads for one genome call");
+    (void)hipSetDevice(c->device);
+    if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n)) ||
+        (n_pairs && (rc = ensure_genome_pe(c, n_pairs, stride, e4.chunk_bases, e4.max_ins))))
+        return rc;
+    hipStream_t s = (hipStream_t)stream, spe = stream_pe ? (hipStream_t)stream_pe : s;
+    if (spe != s && !c->g2_scr_pe) {
+        HIPCHK(c, hipMalloc(&c->g2_scr_pe, af_g2_slot_bytes() * (size_t)c->g2_waves));
+        HIPCHK(c, hipMalloc(&c->zscratch_pe, (size_t)(AF_MAX_READ + 1) * 1024 * (size_t)c->n_slots));
+    }
+    if (!c->g_ev) HIPCHK(c, hipEventCreateWithFlags(&c->g_ev, hipEventDisableTiming));
+    const GOpt o = genome_opt(&e4);
+    const GWork w = genome_work(c);
+    if (n_pairs)
+        HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, e4.chunk_bases, c->g_cstart, c->g_scan, c->g_max_chunks,
+                                      c->g_nchunks, s));
+    HIPCHK(c, af_launch_genome_regions(g->dev, d_reads, stride, d_lens, nullptr, n, *p, o, w, c->g1_scr, c->g1_threads,
+                                       c->g2_scr, c->g2_waves, c->zscratch, s));
+    if (n_pairs) {
+        S2Work sw{};
+        sw.ghist = c->g_ghist; sw.pes = c->g_pes; sw.ppc = 0; sw.cstart = c->g_cstart; sw.n_chunks = c->g_nchunks;
+        sw.max_chunks = c->g_max_chunks;
+        if (spe != s) {
+            HIPCHK(c, hipEventRecord(c->g_ev, s));
+            HIPCHK(c, hipStreamWaitEvent(spe, c->g_ev, 0));
+        }
+        HIPCHK(c, af_launch_genome_pe(g->dev, d_reads, stride, d_lens, nullptr, n_pairs, *p, o, w, sw,
+                                      spe != s ? c->g2_scr_pe : c->g2_scr, c->g2_waves,
+                                      spe != s ? c->zscratch_pe : c->zscratch, d_recs, d_n_rec, spe));
+    }
+    if (n_se) {
+        // the single-end reads' view: rows [2 n_pairs, n) of the launch
+        const int64_t b = 2 * n_pairs;
+        GWork ws = w;
+        ws.reg_off += b; ws.reg_n += b; ws.iv_off += b; ws.iv_n += b;
+        HIPCHK(c, af_launch_genome_se(g->dev, d_reads + b * stride, stride, d_lens + b, nullptr, n_se, *p, se_id_base,
+                                      d_se_ids, ws, c->g2_scr, c->g2_waves, c->zscratch, d_recs + b * AF_G_MAX_REC,
+                                      d_n_rec + b, s));
+    }
     return AF_OK;
 }
 

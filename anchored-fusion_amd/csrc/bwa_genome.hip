@@ -32,6 +32,22 @@
 
 namespace {
 
+#ifdef AF_G_PROF
+// profiling build only (make gprof -> libafgpu_gprof.so, scripts/g_prof.py): per-read timings of
+// the genome calls, [call][read][GP_W]
+__device__ int32_t *g_gprof = nullptr;
+__device__ int64_t g_gprof_cap = 0;
+__device__ int32_t g_gprof_call = 0;
+constexpr int GP_W = 24;
+__device__ __forceinline__ int32_t *gp_row(int64_t r) {
+    return g_gprof && r < g_gprof_cap ? g_gprof + ((int64_t)g_gprof_call * g_gprof_cap + r) * GP_W : nullptr;
+}
+__device__ __forceinline__ uint32_t gp_rt() { return (uint32_t)wall_clock64(); }
+#define GPROF(...) __VA_ARGS__
+#else
+#define GPROF(...)
+#endif
+
 constexpr int G_LIST = AF_MAX_READ + 2;
 constexpr int G_KB_T = 5, G_KB_MAXK = 2 * G_KB_T - 1;
 constexpr int G_KB_NODES = AF_G_MAX_CHAIN / 2 + 64;  // t = 5: >= 4 keys per non-root node
@@ -207,6 +223,9 @@ __global__ __launch_bounds__(64) void k_g_seeds(DevGenome G, const uint8_t *__re
     const int msl = p.min_seed_len;
     const int split_len = (int)((float)msl * 1.5f + .499);
     for (int64_t rr = read0 + tid; rr < n; rr += nthr) {
+        GPROF(const uint64_t gp_c0 = clock64(); const uint32_t gp_t0 = gp_rt();
+              auto gp_end = [&](int ni_) { int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0);
+                  g[1] = ni_; g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid; } };)
         const int len = read_len(lens, rr, stride);
         const uint8_t *rd = reads + rr * (int64_t)stride;
         for (int x = 0; x < len; ++x) q[x] = nt4(rd[x]);
@@ -249,7 +268,7 @@ __global__ __launch_bounds__(64) void k_g_seeds(DevGenome G, const uint8_t *__re
                 }
             }
         }
-        if (ovf) { w.iv_n[rr] = -1; continue; }
+        if (ovf) { w.iv_n[rr] = -1; GPROF(gp_end(-1);) continue; }
         // sort by (qb, qe): equal keys are identical intervals (any order)
         for (int i = 1; i < ni; ++i) {
             const GBi t = fmm[i];
@@ -262,11 +281,13 @@ __global__ __launch_bounds__(64) void k_g_seeds(DevGenome G, const uint8_t *__re
         if (ni && off + ni > w.iv_cap) {  // the pool is sized from the call's read count
             atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
             w.iv_n[rr] = -1;
+            GPROF(gp_end(-2);)
             continue;
         }
         for (int i = 0; i < ni; ++i) w.iv[off + i] = GIv{fmm[i].k, fmm[i].s, fmm[i].qb, fmm[i].qe};
         w.iv_off[rr] = off;
         w.iv_n[rr] = ni;
+        GPROF(gp_end(ni);)
     }
 }
 
@@ -566,50 +587,88 @@ struct GLtFlt {
     __device__ bool operator()(const GChain &a, const GChain &b) const { return a.w > b.w; }
 };
 
-// mem_chain_flt (oracle mem_chain_flt), lane 0 over S.ch2: returns the kept count
-__device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const GOpt &o) {
+// mem_chain_flt (oracle mem_chain_flt) over S.ch2 on the wave: returns the kept count.  The
+// chains' weights, query spans and the overlap scan against the kept list are lane-parallel (the
+// scan's first breaking chain found by a ballot, so `first` is set exactly for the overlapping
+// kept chains the sequential scan visits); klib's introsort (its tie order is bwa's) and the
+// order-preserving compaction run as in the oracle.
+__device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const GOpt &o, int lane) {
     GChain *a = S.ch2;
     if (n_chn == 0) return 0;
-    for (int i = 0; i < n_chn; ++i) { a[i].first = -1; a[i].kept = 0; a[i].w = g_chain_weight(S, a[i]); }
-    ks_introsort(a, n_chn, GLtFlt());
-    auto beg = [&](const GChain &c) { return (int)S.seed[c.seed0].qbeg; };
-    auto endq = [&](const GChain &c) {
+    for (int i = lane; i < n_chn; i += 64) {
+        GChain c = a[i];
+        c.first = -1; c.kept = 0; c.w = g_chain_weight(S, c);
+        a[i] = c;
+    }
+    wave_sync();
+    if (lane == 0) ks_introsort(a, n_chn, GLtFlt());
+    wave_sync();
+    int32_t *cb = S.last_of, *ce = S.order, *cw = S.next;  // free after mem_chain
+    for (int i = lane; i < n_chn; i += 64) {
+        const GChain c = a[i];
         const GSeed t = S.seed[c.seed0 + c.n - 1];
-        return (int)t.qbeg + t.len;
-    };
+        cb[i] = S.seed[c.seed0].qbeg;
+        ce[i] = t.qbeg + t.len;
+        cw[i] = c.w;
+    }
     int32_t *chains = S.kept;
-    int nc = 0;
-    a[0].kept = 3;
-    chains[nc++] = 0;
+    if (lane == 0) { a[0].kept = 3; chains[0] = 0; }
+    wave_sync();
+    int nc = 1;
     for (int i = 1; i < n_chn; ++i) {
-        int large_ovlp = 0, k;
-        for (k = 0; k < nc; ++k) {
-            const int j = chains[k];
-            const int b_max = beg(a[j]) > beg(a[i]) ? beg(a[j]) : beg(a[i]);
-            const int e_min = endq(a[j]) < endq(a[i]) ? endq(a[j]) : endq(a[i]);
-            if (e_min > b_max) {
-                const int li = endq(a[i]) - beg(a[i]), lj = endq(a[j]) - beg(a[j]);
-                const int min_l = li < lj ? li : lj;
-                if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
-                    large_ovlp = 1;
-                    if (a[j].first < 0) a[j].first = i;
-                    if ((float)a[i].w < (float)a[j].w * 0.5f && a[j].w - a[i].w >= p.min_seed_len << 1) break;
+        const int bi = cb[i], ei = ce[i], wi = cw[i], li = ei - bi;
+        bool large_ovlp = false, brk = false;
+        for (int k0 = 0; k0 < nc && !brk; k0 += 64) {
+            const int k = k0 + lane;
+            bool ov = false, bk = false;
+            int j = 0;
+            if (k < nc) {
+                j = chains[k];
+                const int bj = cb[j], ej = ce[j];
+                const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
+                if (e_min > b_max) {
+                    const int lj = ej - bj, min_l = li < lj ? li : lj;
+                    if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
+                        ov = true;
+                        const int wj = cw[j];
+                        bk = (float)wi < (float)wj * 0.5f && wj - wi >= p.min_seed_len << 1;
+                    }
                 }
             }
+            const uint64_t bm = __ballot(bk);
+            uint64_t om = __ballot(ov);
+            if (bm) {
+                const int f = __builtin_ctzll(bm);
+                if (f < 63) om &= (2ull << f) - 1ull;
+                brk = true;
+            }
+            if (om) large_ovlp = true;
+            if ((om >> lane) & 1ull)
+                if (a[j].first < 0) a[j].first = i;
         }
-        if (k == nc) {
-            chains[nc++] = i;
-            a[i].kept = large_ovlp ? 2 : 3;
+        if (!brk) {
+            if (lane == 0) { chains[nc] = i; a[i].kept = large_ovlp ? 2 : 3; }
+            ++nc;
         }
+        wave_sync();
     }
-    for (int i = 0; i < nc; ++i) {
-        const GChain &c = a[chains[i]];
-        if (c.first >= 0) a[c.first].kept = 1;
+    for (int k = lane; k < nc; k += 64) {
+        const int f = a[chains[k]].first;
+        if (f >= 0) a[f].kept = 1;
     }
-    int k = 0;
-    for (int i = 0; i < n_chn; ++i)
-        if (a[i].kept != 0) a[k++] = a[i];
-    return k;
+    wave_sync();
+    int m = 0;
+    for (int i0 = 0; i0 < n_chn; i0 += 64) {
+        const int i = i0 + lane;
+        GChain c;
+        bool keep = false;
+        if (i < n_chn) { c = a[i]; keep = c.kept != 0; }
+        const uint64_t km = __ballot(keep);
+        if (keep) a[m + lanes_below(km, lane)] = c;
+        m += __builtin_popcountll(km);
+        wave_sync();
+    }
+    return m;
 }
 
 // mem_chain2aln (oracle mem_chain2aln) for chain ci of S.ch2; regions appended to S.reg.
@@ -914,19 +973,30 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
         const int niv = w.iv_n[r];
         int nreg = 0;
         bool ovf = niv < 0;
+        GPROF(uint64_t gp_c[5] = {(uint64_t)clock64(), 0, 0, 0, 0}; const uint32_t gp_t0 = gp_rt(); int gp_n[4] = {0, 0, 0, 0};
+              int64_t gp_occ = 0; if (niv > 0) for (int i = 0; i < niv; ++i) { const int64_t s_ = w.iv[w.iv_off[r] + i].s;
+                  gp_occ += s_ > p.max_occ ? p.max_occ : s_; })
         if (!ovf && l >= p.min_seed_len && niv > 0) {
             g_load_read(reads, r, stride, l, lane);
             const int nch0 = g_mem_chain(G, S, w.iv + w.iv_off[r], niv, p, o, lane);
+            GPROF(gp_c[1] = clock64(); gp_n[0] = nch0;)
             if (nch0 < 0) ovf = true;
             else {
-                if (lane == 0) g_g2.misc[3] = g_chain_flt(S, nch0, p, o);
-                wave_sync();
-                const int nch = g_g2.misc[3];
+                const int nch = g_chain_flt(S, nch0, p, o, lane);
+                GPROF(gp_c[2] = clock64(); gp_n[1] = nch;)
                 for (int ci = 0; ci < nch && !ovf; ++ci)
                     if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane)) ovf = true;
+                GPROF(gp_c[3] = clock64(); gp_n[2] = nreg;)
                 if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+                GPROF(gp_c[4] = clock64(); gp_n[3] = nreg;)
             }
         }
+        GPROF(if (lane == 0) { int32_t *g = gp_row(r); if (g) { const uint64_t ce = clock64();
+              g[3] = (int32_t)(ce - gp_c[0]);
+              g[4] = gp_c[1] ? (int32_t)(gp_c[1] - gp_c[0]) : 0; g[5] = gp_c[2] ? (int32_t)(gp_c[2] - gp_c[1]) : 0;
+              g[6] = gp_c[3] ? (int32_t)(gp_c[3] - gp_c[2]) : 0; g[7] = gp_c[4] ? (int32_t)(gp_c[4] - gp_c[3]) : 0;
+              g[8] = (int32_t)gp_occ; g[10] = gp_n[0]; g[11] = gp_n[1]; g[12] = gp_n[2]; g[13] = gp_n[3];
+              g[14] = (int32_t)blockIdx.x; g[15] = (int32_t)gp_t0; g[16] = (int32_t)gp_rt(); g[2] = l; } })
         int off = 0;
         if (!ovf && nreg > 0) {
             if (lane == 0) g_g2.misc[4] = atomicAdd(w.reg_fill, nreg);
@@ -1517,6 +1587,35 @@ __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
 }  // namespace
 
 size_t af_g1_slot_bytes() { return (size_t)G1_SLOT_BYTES; }
+
+#ifdef AF_G_PROF
+static int32_t *h_gprof = nullptr;
+static int64_t h_gprof_cap = 0;
+static int32_t h_gprof_calls = 0, h_gprof_next = 0;
+static int32_t h_gprof_ids[64];
+extern "C" int af_debug_g_prof_enable(int64_t cap, int32_t calls) {
+    if (h_gprof) { (void)hipFree(h_gprof); h_gprof = nullptr; }
+    if (hipMalloc(&h_gprof, sizeof(int32_t) * GP_W * cap * calls) != hipSuccess) return -1;
+    (void)hipMemset(h_gprof, 0, sizeof(int32_t) * GP_W * cap * calls);
+    h_gprof_cap = cap; h_gprof_calls = calls > 64 ? 64 : calls; h_gprof_next = 0;
+    for (int i = 0; i < 64; ++i) h_gprof_ids[i] = i;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gprof), &h_gprof, sizeof(h_gprof));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gprof_cap), &h_gprof_cap, sizeof(h_gprof_cap));
+    return GP_W;
+}
+extern "C" int af_debug_g_prof_read(void *dst, int64_t n_ints) {
+    (void)hipDeviceSynchronize();
+    if (!h_gprof || n_ints > (int64_t)GP_W * h_gprof_cap * h_gprof_calls) return -1;
+    return hipMemcpy(dst, h_gprof, sizeof(int32_t) * n_ints, hipMemcpyDeviceToHost) == hipSuccess ? h_gprof_next : -1;
+}
+// the next genome call's slot (calls past the last slot reuse it)
+static void gprof_next(hipStream_t s) {
+    if (!h_gprof) return;
+    const int k = h_gprof_next < h_gprof_calls ? h_gprof_next : h_gprof_calls - 1;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gprof_call), &h_gprof_ids[k], sizeof(int32_t), 0, hipMemcpyHostToDevice, s);
+    ++h_gprof_next;
+}
+#endif
 size_t af_g2_slot_bytes() { return g2_slot_bytes(); }
 
 // S4 / S5 up to the regions: G1 + G2 over reads [0, *d_n) (or cap) of a call
@@ -1524,6 +1623,7 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                                     const int32_t *d_n, int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
                                     uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
                                     uint8_t *zscratch, hipStream_t s) {
+    GPROF(gprof_next(s);)
     hipLaunchKernelGGL(k_g_zero, dim3(1), dim3(64), 0, s, w, cap, w.heads);
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)(n_g1_threads / 64)), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
                        (int64_t)0, p, o, g1_scratch, w);

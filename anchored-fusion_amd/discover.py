@@ -14,7 +14,7 @@ partner stages, all on the device with no host round trip for the data (SURVEY.m
 counts size the gathers) and the gathers once (the split-read count sizes S5).  Everything else
 stays on the device: the records, the row lists, the queries, the genome calls' SAM records
 (af_grec), the S6 queries and their PSL rows, which `exchange()` all-gathers between ranks (one
-process per GPU, RCCL).  S6 follows S5 (its queries are S5's survivors); S4 runs beside S6.
+process per GPU, RCCL).  S6 follows S5 (its queries are S5's survivors); S4's records are made beside S6.
 Per-call caps (query buffers, the genome calls' per-read caps) are counted in `summary()`.
 """
 import os
@@ -156,26 +156,26 @@ class CandidateDiscovery:
         pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
         recs = self.q_recs.view(torch.int32)
         w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
-        # S5 (`bwa mem -M genome split_reads.fa`, fn:716), its genome check (fn:718-768) and the S6
-        # queries (fn:506-528)
-        if n5:
-            self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
-                                     lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0, stream=s0)
+        # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188: bwa's chunks over this input) and S5 (`bwa mem
+        # -M genome split_reads.fa`, fn:716) with one launch of the seed / region kernels; S5's
+        # records on s0, S4's on slot 2's stream (idle once S2 is done)
+        spe = self.grp.streams[2] if G > 2 else s0
+        spe.wait_stream(s0)
+        if npair or n5:
+            self.ref.align_pe_se_device(self.q, npair, n5, self.L, self.q_lens, recs, self.q_nh,
+                                        params=self.p_genome, pe_s4=pe, pe_s5=pe, se_id_base=0, stream=s0,
+                                        stream_pe=spe)
+        # S5's genome check (fn:718-768) and the S6 queries (fn:506-528)
         _genome.s5_filter_device(self.ref.ctx, recs[2 * npair * w:], self.q_nh[2 * npair:], n5, self.q[2 * npair:],
                                  self.L, self.q_lens[2 * npair:], self.q_rows[2 * npair:], self.out, self.qcap,
                                  self.s6["q"], self.s6["lens"], self.s6["src"], self.s6["n"], self.s6["over"],
                                  stream=s0)
-        # S6 (`blat -minScore=20 genome split.fa`, fn:530) beside S4
+        # S6 (`blat -minScore=20 genome split.fa`, fn:530) beside S4's records
         s6.wait_stream(s0)
         self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
                                      lens_t=self.s6["lens"], p=self.p_tail, stream=s6)
-        s6_done = torch.cuda.Event()
-        s6_done.record(s6)  # (s6 is s0 when only one batch is in flight)
-        # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188): the pairs' records, bwa's chunks over this input
-        if npair:
-            self.ref.align_pe_device(self.q, npair, self.L, self.q_lens, recs, self.q_nh, params=self.p_genome, pe=pe,
-                                     stream=s0)
-        s0.wait_event(s6_done)
+        s0.wait_stream(s6)
+        s0.wait_stream(spe)
         if _DEBUG:
             s0.synchronize()
             _log("genome calls done")

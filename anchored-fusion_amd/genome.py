@@ -215,6 +215,27 @@ class GenomeIndex:
             ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), recs_t.data_ptr(),
             nrec_t.data_ptr(), _stream_handle(stream)), "af_genome_align_pe_device")
 
+    def align_pe_se_device(self, reads_t, n_pairs, n_se, stride, lens_t, recs_t, nrec_t, params=None, pe_s4=None,
+                           pe_s5=None, se_id_base=0, se_ids_t=None, stream=None, stream_pe=None, ctx=None):
+        """S4 (reads [0, 2 n_pairs), pair-major) and S5 (reads [2 n_pairs, 2 n_pairs + n_se)) of one
+        gene step with one launch of the seed / region kernels (af_genome_align_pe_se_device):
+        records of every read equal to align_pe_device + align_se_device (or align_se_ids_device
+        with se_ids_t).  S5's records are ordered on `stream`, S4's on `stream_pe`."""
+        import torch
+        c = self.ctx if ctx is None else ctx
+        n = 2 * int(n_pairs) + int(n_se)
+        _check_se(reads_t, n, stride, recs_t, nrec_t, lens_t)
+        if lens_t is None:
+            raise ValueError("lens_t: the reads' lengths are required")
+        if se_ids_t is not None:
+            _need(se_ids_t, 8 * int(n_se), "se_ids_t", torch.int64)
+        _lib.check(c, _lib.lib().af_genome_align_pe_se_device(
+            c, self.g, reads_t.data_ptr(), int(n_pairs), int(n_se), int(stride), lens_t.data_ptr(),
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe_s4 or _lib.default_pe()),
+            ctypes.byref(pe_s5 or _lib.default_pe()), int(se_id_base),
+            None if se_ids_t is None else se_ids_t.data_ptr(), recs_t.data_ptr(), nrec_t.data_ptr(),
+            _stream_handle(stream), _stream_handle(stream_pe)), "af_genome_align_pe_se_device")
+
     # ---- SAM text --------------------------------------------------------------------------
     def sam_lines(self, name, seq, recs, n):
         """The SAM lines bwa prints for one read (its af_grec rows recs[:n]): QNAME FLAG RNAME POS

@@ -318,6 +318,22 @@ int af_genome_align_se_ids_device(af_ctx *ctx, const af_genome *g, const uint8_t
 int af_genome_align_pe_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs,
                               int32_t stride, const int32_t *d_lens, const af_params *p, const af_pe *pe,
                               af_grec *d_recs, int32_t *d_n_rec, void *stream);
+/* S4 and S5 of one gene step with one launch of the seed and region kernels (bwa's per-read work
+ * up to mem_align1_core is the same for both calls; one launch fills the chip once instead of
+ * twice): reads [0, 2 n_pairs) are S4's pairs as af_genome_align_pe_device takes them (pe_s4),
+ * reads [2 n_pairs, 2 n_pairs + n_se) S5's queries as af_genome_align_se_device (id_base
+ * se_id_base) or af_genome_align_se_ids_device (d_se_ids, when not NULL) take them; d_lens covers
+ * every read.  Records at d_recs[r * AF_G_MAX_REC ..], d_n_rec[r] for every read r of the call,
+ * equal to the two calls made separately.  The seed / region kernels and S5's records run on
+ * `stream`; S4's records on `stream_pe` (ordered after the region kernels; NULL: `stream`), so
+ * the caller can run S5's consumers on `stream` beside them.  pe_s4 and pe_s5 must agree on the
+ * seeding options (split_width, max_mem_intv, max_chain_gap).
+ * Replaces Anchored_Fusion.py:188 (`bwa mem -M genome tmp1.fq tmp2.fq`) together with
+ * functions.py:716 (`bwa mem -M genome split.fa`) of the same gene. */
+int af_genome_align_pe_se_device(af_ctx *ctx, const af_genome *g, const uint8_t *d_reads, int64_t n_pairs,
+                                 int64_t n_se, int32_t stride, const int32_t *d_lens, const af_params *p,
+                                 const af_pe *pe_s4, const af_pe *pe_s5, int64_t se_id_base, const int64_t *d_se_ids,
+                                 af_grec *d_recs, int32_t *d_n_rec, void *stream, void *stream_pe);
 /* host-buffer forms (synchronous) */
 int af_genome_align_se(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
                        const int32_t *lens, const af_params *p, const af_pe *pe, int64_t id_base, af_grec *recs,

@@ -1,0 +1,97 @@
+"""Per-read profile of the genome calls of one configs[2] step on the profiling build
+libafgpu_gprof.so (make -C anchored-fusion_amd/csrc gprof; AF_GPU_LIB=libafgpu_gprof.so).
+
+Prints, per call, the distribution of G1 (k_g_seeds) and G2 (k_g_regions) cycles per read, the
+G2 phase shares (mem_chain, chain filter, chain2aln, dedup/patch), the heaviest reads with their
+interval / occurrence / chain / region counts, and the G2 schedule (per-wave busy time vs the
+makespan).
+"""
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("AF_GPU_LIB", "libafgpu_gprof.so")
+import afpkg  # noqa: E402,F401
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from anchored_fusion_amd import _lib, discover, simworld  # noqa: E402
+from anchored_fusion_amd import io as afio  # noqa: E402
+
+N = int(os.environ.get("PAIRS", "50000000"))
+L = 150
+SCALE = float(os.environ.get("SCALE", "1.0"))
+CAP = 400_000
+anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
+dev = torch.device("cuda:0")
+W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=SCALE)
+ref = W.genome_index()
+tiles = W.tiles()
+reads_t = torch.empty((2 * N, L), dtype=torch.uint8, device=dev)
+W.simulate_pairs(N, read_len=L, seed=20251015, pair_base=0, out=reads_t)
+W.blob = None
+torch.cuda.synchronize()
+disc = discover.CandidateDiscovery(anchor, ref, tiles, N, L, device=0, inflight=4, batch_chunks=240, pair_base=0)
+disc.run(reads_t)
+torch.cuda.synchronize()
+lib = _lib.lib()
+lib.af_debug_g_prof_enable.argtypes = [ctypes.c_int64, ctypes.c_int32]
+lib.af_debug_g_prof_read.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+GW = lib.af_debug_g_prof_enable(CAP, 4)
+assert GW > 0
+t0 = time.perf_counter()
+disc.run(reads_t)
+torch.cuda.synchronize()
+print(f"profiled pass {time.perf_counter() - t0:.3f} s; {disc.summary()}")
+buf = np.zeros((4, CAP, GW), dtype=np.int32)
+ncalls = lib.af_debug_g_prof_read(buf.ctypes.data, buf.size)
+pct = lambda v, q: np.percentile(v, q) if len(v) else 0  # noqa: E731
+for c in range(min(ncalls, 4)):
+    B = buf[c]
+    live = (B[:, 2] > 0) | (B[:, 0] != 0)
+    n = int(live.sum())
+    if not n:
+        continue
+    B = B[live].astype(np.int64)
+    names = os.environ.get("GPROF_NAMES", "S4+S5 one launch").split(",")
+    name = names[c] if c < len(names) else f"call {c}"
+    print(f"== call {c}: {name}: {n} reads")
+    g1 = B[:, 0] & 0xFFFFFFFF
+    print(f"  G1 cycles/read mean {g1.mean():.0f} p50 {pct(g1, 50):.0f} p90 {pct(g1, 90):.0f} p99 {pct(g1, 99):.0f} "
+          f"max {g1.max()}; intervals/read mean {B[:, 1].mean():.1f} max {B[:, 1].max()}")
+    lanes = B[:, 20]
+    lane_sum = np.bincount(lanes, weights=g1)
+    print(f"  G1 per-lane cycles: mean {lane_sum[lane_sum > 0].mean():.0f} max {lane_sum.max():.0f}")
+    g2 = B[:, 3] & 0xFFFFFFFF
+    ph = [B[:, k] & 0xFFFFFFFF for k in (4, 5, 6, 7)]
+    print(f"  G2 cycles/read mean {g2.mean():.0f} p50 {pct(g2, 50):.0f} p90 {pct(g2, 90):.0f} p99 {pct(g2, 99):.0f} "
+          f"p99.9 {pct(g2, 99.9):.0f} max {g2.max()}")
+    tot = max(g2.sum(), 1)
+    print("  G2 shares: " + ", ".join(f"{nm} {v.sum() / tot:.3f}" for nm, v in zip(("chain", "flt", "ext", "dedup"), ph)))
+    srt = np.argsort(-g2)
+    top = g2[srt[:100]].sum() / tot
+    print(f"  top-100 reads hold {top:.3f} of G2 cycles; top-1000 {g2[srt[:1000]].sum() / tot:.3f}")
+    print("  heaviest: cyc chain flt ext dedup | len niv occ nch kept nreg nreg2")
+    for i in srt[:12]:
+        r = B[i]
+        print(f"   {g2[i]:>11d} {ph[0][i]:>10d} {ph[1][i]:>9d} {ph[2][i]:>10d} {ph[3][i]:>9d} | {r[2]} {r[1]} {r[8]} "
+              f"{r[10]} {r[11]} {r[12]} {r[13]}")
+    for k, nm in ((8, "occ"), (10, "chains"), (11, "kept"), (12, "regions")):
+        v = B[:, k]
+        print(f"  {nm:8s} mean {v.mean():.1f} p90 {pct(v, 90):.0f} p99 {pct(v, 99):.0f} max {v.max()}")
+    # schedule (s_memrealtime, 100 MHz)
+    t0_, t1_ = B[:, 15] & 0xFFFFFFFF, B[:, 16] & 0xFFFFFFFF
+    base = t0_.min()
+    t0_, t1_ = t0_ - base, t1_ - base
+    span = t1_.max()
+    busy = np.bincount(B[:, 14], weights=(t1_ - t0_))
+    print(f"  G2 makespan {span / 100:.0f} us; per-wave busy mean {busy.mean() / 100:.0f} us max {busy.max() / 100:.0f} us "
+          f"over {len(busy)} waves; last read starts at {t0_.max() / 100:.0f} us")
+    tg0, tg1 = B[:, 17] & 0xFFFFFFFF, B[:, 18] & 0xFFFFFFFF
+    b1 = tg0.min()
+    print(f"  G1 makespan {(tg1 - b1).max() / 100:.0f} us; per-read wall p50 {pct(tg1 - tg0, 50) / 100:.1f} us "
+          f"p99 {pct(tg1 - tg0, 99) / 100:.1f} us max {(tg1 - tg0).max() / 100:.1f} us")
+disc.close()

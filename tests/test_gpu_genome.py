@@ -119,3 +119,45 @@ def test_pe_rescue_case_equals_oracle():
             assert bool(probe["flag"] & 4) == (matesw == 0)
     finally:
         gg.close()
+
+
+def test_pe_se_one_launch_equals_oracle(world):
+    """af_genome_align_pe_se_device: S4's pairs and S5's queries through one launch of the seed /
+    region kernels, S4's records on a second stream -- every record equal to the oracle's two
+    separate calls (S4 with its chunk grid, S5 with its read ids)."""
+    import torch
+
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.genome import MAX_REC, REC_DTYPE
+    contigs, og, gg = world
+    pairs = sample_pairs(contigs, 700, seed=31)
+    se, se_lens = sample_reads(contigs, 500, seed=32, chimeric=0.4)
+    L = max(pairs.shape[1], se.shape[1])
+    reads = np.zeros((pairs.shape[0] + se.shape[0], L), np.uint8)
+    reads[:pairs.shape[0], :pairs.shape[1]] = pairs
+    reads[pairs.shape[0]:, :se.shape[1]] = se
+    lens = np.concatenate([np.full(pairs.shape[0], pairs.shape[1], np.int32), se_lens.astype(np.int32)])
+    pe_o = oracle.default_pe(chunk_bases=150_000, pair_base=2)
+    ro4, no4 = og.align_pe(reads[:pairs.shape[0], :pairs.shape[1]], lens[:pairs.shape[0]], pe=pe_o, threads=8)
+    ro5, no5 = og.align_se(se, se_lens, id_base=11, threads=8)
+    dev = torch.device("cuda:0")
+    n = reads.shape[0]
+    rt = torch.from_numpy(reads).to(dev)
+    lt = torch.from_numpy(lens).to(dev)
+    recs = torch.zeros(n * MAX_REC * REC_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    nrec = torch.zeros(n, dtype=torch.int32, device=dev)
+    s_a, s_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    gg.align_pe_se_device(rt, pairs.shape[0] // 2, se.shape[0], L, lt, recs, nrec,
+                          pe_s4=_lib.default_pe(chunk_bases=150_000, pair_base=2), pe_s5=_lib.default_pe(),
+                          se_id_base=11, stream=s_a, stream_pe=s_b)
+    torch.cuda.synchronize(dev)
+    rg = recs.cpu().numpy().view(REC_DTYPE).reshape(n, MAX_REC)
+    ng = nrec.cpu().numpy()
+    P = pairs.shape[0]
+    assert np.array_equal(ng[:P], no4) and np.array_equal(ng[P:], no5)
+    for r in range(P):
+        msg = _rec_equal(ro4[r], rg[r], min(no4[r], 8))
+        assert msg is None, ("S4", r, msg)
+    for r in range(se.shape[0]):
+        msg = _rec_equal(ro5[r], rg[P + r], min(no5[r], 8))
+        assert msg is None, ("S5", r, msg)
