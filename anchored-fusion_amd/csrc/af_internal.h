@@ -9,6 +9,9 @@
 #define AF_SEED_BTILE 2048      // reads per workgroup tile in the seed filter
 #define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
 #define AF_SEED_GROUPS (AF_SEED_BTILE / 64)  // 64-read ballot groups per tile
+#ifndef AF_G1_WPS
+#define AF_G1_WPS 4             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish
+#endif
 #ifndef AF_K2_WPS
 #define AF_K2_WPS 6             // S2 K2 waves per SIMD (launch bound; persistent slots = 4 x this per CU)
 #endif
@@ -217,6 +220,7 @@ struct GWork {
     int32_t *reg_off, *reg_n;   // per read; reg_n -1 overflow
     int32_t *heads;             // G2 dequeue heads (8 lines)
     int32_t *stats;             // AF_GSTAT_*
+    unsigned long long *g1_next;  // G1: the next read to hand to an idle lane
 };
 size_t af_g1_slot_bytes();
 size_t af_g2_slot_bytes();
@@ -224,6 +228,9 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                                     const int32_t *d_n, int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
                                     uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
                                     uint8_t *zscratch, hipStream_t s);
+hipError_t af_launch_genome_intervals(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                                      int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
+                                      uint8_t *g1_scratch, int n_g1_threads, hipStream_t s);
 hipError_t af_launch_genome_se(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
                                const int32_t *d_n, int64_t cap, const af_params &p, int64_t id_base, const int64_t *ids,
                                const GWork &w, uint8_t *g2_scratch, int n_waves, uint8_t *zscratch, af_grec *recs,

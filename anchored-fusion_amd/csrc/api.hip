@@ -379,15 +379,15 @@ int check_params(af_ctx *c, const af_params *p) {
 
 
 // ---- genome calls (bwa_genome.hip) ------------------------------------------------------
-// per-lane G1 scratch (2 waves per CU) and per-wave G2-G4 scratch (8 waves per CU, <= n_slots of
+// per-lane G1 scratch (AF_G1_WPS waves per SIMD) and per-wave G2-G4 scratch (8 waves per CU, <= n_slots of
 // the context's traceback scratch)
 int ensure_genome_scratch(af_ctx *c) {
     if (c->g1_scr) return AF_OK;
-    c->g1_threads = c->n_cu * 2 * 64;
+    c->g1_threads = c->n_cu * 4 * AF_G1_WPS * 64;
     c->g2_waves = std::min(c->n_cu * 8, c->n_slots);
     HIPCHK(c, hipMalloc(&c->g1_scr, af_g1_slot_bytes() * (size_t)c->g1_threads));
     HIPCHK(c, hipMalloc(&c->g2_scr, af_g2_slot_bytes() * (size_t)c->g2_waves));
-    HIPCHK(c, hipMalloc(&c->g_iv_fill, sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->g_iv_fill, 2 * sizeof(unsigned long long)));
     HIPCHK(c, hipMalloc(&c->g_reg_fill, sizeof(int32_t)));
     HIPCHK(c, hipMalloc(&c->g_stats, sizeof(int32_t) * AF_GSTAT_N));
     HIPCHK(c, hipMemset(c->g_stats, 0, sizeof(int32_t) * AF_GSTAT_N));
@@ -398,6 +398,8 @@ int ensure_genome_scratch(af_ctx *c) {
 // most AF_G_MAX_INTV) and regions (16 per read on average)
 int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     if (n_reads <= c->g_cap_reads) return AF_OK;
+    // the region pool's fill and offsets are int32 (at most 16 regions per read on average)
+    if (n_reads > INT32_MAX / 16 - AF_G_MAX_REG) return fail(c, AF_E_INVALID, "too many reads for one genome call");
     af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_off); af_free(c->g_iv_n); af_free(c->g_reg_off);
     af_free(c->g_reg_n);
     c->g_iv = nullptr; c->g_reg = nullptr; c->g_iv_off = nullptr; c->g_iv_n = nullptr; c->g_reg_off = nullptr;
@@ -421,6 +423,7 @@ GWork genome_work(af_ctx *c) {
     w.reg = c->g_reg; w.reg_cap = c->g_reg_cap; w.reg_fill = c->g_reg_fill; w.reg_off = c->g_reg_off;
     w.reg_n = c->g_reg_n;
     w.heads = c->ctrl + AF_CTRL_G_HEADS;
+    w.g1_next = c->g_iv_fill + 1;
     w.stats = c->g_stats;
     return w;
 }
@@ -1362,6 +1365,38 @@ int af_genome_regions(af_ctx *c, const af_genome *g, const uint8_t *reads, int64
             o[7] = a.w; o[8] = a.seedcov; o[9] = a.seedlen0; o[10] = 0; o[11] = 0;
         }
     }
+    return AF_OK;
+}
+
+int af_genome_intervals(af_ctx *c, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                        const int32_t *lens, const af_params *p, const af_pe *pe, int32_t max_iv, int64_t *ivs,
+                        int32_t *n_iv) {
+    int rc = check_genome_call(c, g, p, pe, stride);
+    if (rc) return rc;
+    if (n < 0 || max_iv < 1 || (n > 0 && (!reads || !ivs || !n_iv))) return fail(c, AF_E_INVALID, "bad argument");
+    if (n == 0) return AF_OK;
+    (void)hipSetDevice(c->device);
+    const int32_t *d_lens = nullptr;
+    if ((rc = genome_stage(c, reads, n, stride, lens, false, &d_lens))) return rc;
+    if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
+    const GWork w = genome_work(c);
+    HIPCHK(c, af_launch_genome_intervals(g->dev, c->g_hreads, stride, d_lens, n, *p, genome_opt(pe), w, c->g1_scr,
+                                         c->g1_threads, c->stream));
+    std::vector<int64_t> off((size_t)n);
+    unsigned long long fill = 0;
+    HIPCHK(c, hipMemcpyAsync(n_iv, c->g_iv_n, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(off.data(), c->g_iv_off, sizeof(int64_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&fill, c->g_iv_fill, sizeof fill, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t nf = std::min<int64_t>((int64_t)fill, c->g_iv_cap);
+    std::vector<GIv> pool((size_t)std::max<int64_t>(nf, 1));
+    if (nf > 0) HIPCHK(c, hipMemcpy(pool.data(), c->g_iv, sizeof(GIv) * nf, hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < n; ++r)
+        for (int k = 0; k < n_iv[r] && k < max_iv; ++k) {
+            const GIv &v = pool[(size_t)off[r] + k];
+            int64_t *o = ivs + (r * max_iv + k) * 4;
+            o[0] = v.sa_k; o[1] = v.s; o[2] = v.qb; o[3] = v.qe;
+        }
     return AF_OK;
 }
 

@@ -48,150 +48,69 @@ __device__ __forceinline__ uint32_t gp_rt() { return (uint32_t)wall_clock64(); }
 #define GPROF(...)
 #endif
 
-constexpr int G_LIST = AF_MAX_READ + 2;
 constexpr int G_KB_T = 5, G_KB_MAXK = 2 * G_KB_T - 1;
 constexpr int G_KB_NODES = AF_G_MAX_CHAIN / 2 + 64;  // t = 5: >= 4 keys per non-root node
 
-struct GBi { int64_t k, l, s; int32_t qb, qe; };     // bwtintv_t (x[0], x[1], x[2], info)
 struct GSeed { int64_t rbeg; int32_t qbeg, len; };   // mem_seed_t (score = len)
 struct GChain { int64_t pos; int32_t n, first, rid, w, kept, seed0; };  // mem_chain_t
 struct GKb { int16_t n, internal; int16_t key[G_KB_MAXK]; int16_t ptr[G_KB_MAXK + 1]; };
 
 // ================================================================== FM index (bwt.c)
-// occurrences of c among the first m (<= 32) 2-bit fields of w
-__device__ __forceinline__ int cnt_code(uint64_t w, int c, int m) {
-    const uint64_t t = ~(w ^ (0x5555555555555555ull * (uint64_t)c));
-    uint64_t y = t & (t >> 1) & 0x5555555555555555ull;
-    if (m < 32) y &= (1ull << (2 * m)) - 1ull;
-    return __builtin_popcountll(y);
-}
-// bwt_occ4: occurrences of A/C/G/T in the BWT rows [0, i)
+// bwt_occ4: occurrences of A/C/G/T in the BWT rows [0, i).  A 128-row block holds its four
+// counts and 128 2-bit symbols (symbol t of a 32-bit word at bits 2t, 2t + 1); the symbols
+// below row i are counted for all four bases at once from three popcounts per word (low bits,
+// high bits, both): T = both, G = high - T, C = low - T, A = the rest.
 __device__ __forceinline__ void fm_occ4(const DevGenome &G, int64_t i, int64_t o[4]) {
     const int64_t b = i >> 7;
     const int r = (int)(i & 127);
     const uint4 *blk = reinterpret_cast<const uint4 *>(G.occ + b * 8);
     const uint4 c01 = blk[0], c23 = blk[1], w01 = blk[2], w23 = blk[3];
-    const uint64_t cnt[4] = {(uint64_t)c01.x | (uint64_t)c01.y << 32, (uint64_t)c01.z | (uint64_t)c01.w << 32,
-                             (uint64_t)c23.x | (uint64_t)c23.y << 32, (uint64_t)c23.z | (uint64_t)c23.w << 32};
-    const uint64_t w[4] = {(uint64_t)w01.x | (uint64_t)w01.y << 32, (uint64_t)w01.z | (uint64_t)w01.w << 32,
-                           (uint64_t)w23.x | (uint64_t)w23.y << 32, (uint64_t)w23.z | (uint64_t)w23.w << 32};
+    const uint32_t wv[8] = {w01.x, w01.y, w01.z, w01.w, w23.x, w23.y, w23.z, w23.w};
+    uint32_t nlo = 0, nhi = 0, n11 = 0;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int64_t v = (int64_t)cnt[c];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int m = r - 32 * k;
-            if (m > 0) v += cnt_code(w[k], c, m > 32 ? 32 : m);
-        }
-        o[c] = v;
+    for (int u = 0; u < 8; ++u) {
+        const int m = r - 16 * u;  // symbols of word u below row i
+        const uint32_t mask = m >= 16 ? 0xffffffffu : m <= 0 ? 0u : (1u << (2 * m)) - 1u;
+        const uint32_t x = wv[u] & mask;
+        const uint32_t lo = x & 0x55555555u, hi = (x >> 1) & 0x55555555u;
+        nlo += __builtin_popcount(lo);
+        nhi += __builtin_popcount(hi);
+        n11 += __builtin_popcount(lo & hi);
     }
+    o[0] = (int64_t)((uint64_t)c01.x | (uint64_t)c01.y << 32) + r - (int)(nlo + nhi - n11);
+    o[1] = (int64_t)((uint64_t)c01.z | (uint64_t)c01.w << 32) + (int)(nlo - n11);
+    o[2] = (int64_t)((uint64_t)c23.x | (uint64_t)c23.y << 32) + (int)(nhi - n11);
+    o[3] = (int64_t)((uint64_t)c23.z | (uint64_t)c23.w << 32) + (int)n11;
     if (G.primary >= (b << 7) && G.primary < i) o[0] -= 1;  // the '$' row is stored as A
 }
-// bwt_extend, backward: ok[c] = the bi-interval of cW (oracle fm_back4)
-__device__ __forceinline__ void fm_back4(const DevGenome &G, const GBi &ik, GBi ok[4]) {
+__device__ __forceinline__ int64_t sel4(const int64_t v[4], int c) {
+    return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
+}
+// bwt_extend restricted to one base (oracle fm_back4 / fm_fwd4, the c'th output): backward, the
+// bi-interval of cW from W = (k, l, s); forward (fwd, W -> W comp(c') with c = 3 - c'), the same
+// on the swapped interval, swapped back
+__device__ __forceinline__ void fm_ext1(const DevGenome &G, int64_t k, int64_t l, int64_t s, int c, bool fwd,
+                                       int64_t &ok, int64_t &ol, int64_t &os) {
+    if (fwd) { const int64_t t = k; k = l; l = t; }
     int64_t a[4], b[4];
-    fm_occ4(G, ik.k, a);
-    fm_occ4(G, ik.k + ik.s, b);
+    fm_occ4(G, k, a);
+    fm_occ4(G, k + s, b);
+    int64_t lo = l + (k <= G.primary && k + s - 1 >= G.primary);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) { ok[c].k = G.C[c] + a[c]; ok[c].s = b[c] - a[c]; }
-    ok[3].l = ik.l + (ik.k <= G.primary && ik.k + ik.s - 1 >= G.primary);
-    ok[2].l = ok[3].l + ok[3].s;
-    ok[1].l = ok[2].l + ok[2].s;
-    ok[0].l = ok[1].l + ok[1].s;
-}
-// bwt_extend, forward (is_back = 0): ok[c'] for W -> W comp(c')
-__device__ __forceinline__ void fm_fwd4(const DevGenome &G, const GBi &ik, GBi ok[4]) {
-    GBi sw = ik;
-    sw.k = ik.l; sw.l = ik.k;
-    GBi o[4];
-    fm_back4(G, sw, o);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) { ok[c].k = o[c].l; ok[c].l = o[c].k; ok[c].s = o[c].s; }
-}
-__device__ __forceinline__ GBi fm_set(const DevGenome &G, int c) {
-    GBi b;
-    b.k = G.C[c]; b.s = G.base_cnt[c]; b.l = G.C[3 - c]; b.qb = 0; b.qe = 0;
-    return b;
+    for (int d = 3; d > 0; --d)
+        if (d > c) lo += b[d] - a[d];
+    const int64_t Cc = c == 0 ? G.C[0] : c == 1 ? G.C[1] : c == 2 ? G.C[2] : G.C[3];
+    const int64_t kk = Cc + sel4(a, c);
+    os = sel4(b, c) - sel4(a, c);
+    if (fwd) { ok = lo; ol = kk; }
+    else { ok = kk; ol = lo; }
 }
 
-// ============================================================= G1: mem_collect_intv
-// bwt_smem1 (oracle fm_smem1): q = the read's codes in this lane's scratch
-__device__ int g_smem1(const DevGenome &G, const uint8_t *q, int len, int x, int64_t min_intv, GBi *mem, int *n_mem,
-                       GBi *prev, GBi *curr) {
-    int i, j, c, ret, np = 0, nc = 0;
-    GBi ik, ok[4];
-    *n_mem = 0;
-    if (q[x] > 3) return x + 1;
-    if (min_intv < 1) min_intv = 1;
-    ik = fm_set(G, q[x]);
-    ik.qe = x + 1;
-    for (i = x + 1; i < len; ++i) {  // forward search
-        if (q[i] < 4) {
-            c = 3 - q[i];
-            fm_fwd4(G, ik, ok);
-            if (ok[c].s != ik.s) {
-                curr[nc++] = ik;
-                if (ok[c].s < min_intv) break;
-            }
-            ik = ok[c]; ik.qe = i + 1;
-        } else {
-            curr[nc++] = ik;
-            break;
-        }
-    }
-    if (i == len) curr[nc++] = ik;
-    for (j = 0; j < nc >> 1; ++j) { GBi t = curr[j]; curr[j] = curr[nc - 1 - j]; curr[nc - 1 - j] = t; }
-    ret = curr[0].qe;
-    { GBi *sw = curr; curr = prev; prev = sw; }
-    np = nc;
-    for (i = x - 1; i >= -1; --i) {  // backward search for MEMs
-        c = i < 0 ? -1 : q[i] < 4 ? q[i] : -1;
-        nc = 0;
-        for (j = 0; j < np; ++j) {
-            const GBi p = prev[j];
-            if (c >= 0) fm_back4(G, p, ok);
-            if (c < 0 || ok[c].s < min_intv) {
-                if (nc == 0) {
-                    if (*n_mem == 0 || i + 1 < mem[*n_mem - 1].qb) {
-                        GBi t = p;
-                        t.qb = i + 1;
-                        mem[(*n_mem)++] = t;
-                    }
-                }
-            } else if (nc == 0 || ok[c].s != curr[nc - 1].s) {
-                GBi t = ok[c];
-                t.qe = p.qe; t.qb = 0;
-                curr[nc++] = t;
-            }
-        }
-        if (nc == 0) break;
-        { GBi *sw = curr; curr = prev; prev = sw; }
-        np = nc;
-    }
-    for (j = 0; j < *n_mem >> 1; ++j) { GBi t = mem[j]; mem[j] = mem[*n_mem - 1 - j]; mem[*n_mem - 1 - j] = t; }
-    return ret;
-}
-
-// bwt_seed_strategy1 (oracle fm_seed_strategy1)
-__device__ int g_seed_strategy1(const DevGenome &G, const uint8_t *q, int len, int x, int min_len, int max_intv,
-                                GBi *mem) {
-    GBi ik, ok[4];
-    mem->s = 0;
-    if (q[x] > 3) return x + 1;
-    ik = fm_set(G, q[x]);
-    for (int i = x + 1; i < len; ++i) {
-        if (q[i] < 4) {
-            const int c = 3 - q[i];
-            fm_fwd4(G, ik, ok);
-            if (ok[c].s < max_intv && i - x >= min_len) {
-                *mem = ok[c];
-                mem->qb = x; mem->qe = i + 1;
-                return i + 1;
-            }
-            ik = ok[c];
-        } else return i + 1;
-    }
-    return len;
+// the bi-interval of one base (oracle fm_set)
+__device__ __forceinline__ void fm_set(const DevGenome &G, int c, int64_t &k, int64_t &l, int64_t &s) {
+    k = c == 0 ? G.C[0] : c == 1 ? G.C[1] : c == 2 ? G.C[2] : G.C[3];
+    l = c == 0 ? G.C[3] : c == 1 ? G.C[2] : c == 2 ? G.C[1] : G.C[0];
+    s = c == 0 ? G.base_cnt[0] : c == 1 ? G.base_cnt[1] : c == 2 ? G.base_cnt[2] : G.base_cnt[3];
 }
 
 __device__ __forceinline__ uint8_t nt4(uint8_t ch) {
@@ -205,89 +124,217 @@ __device__ __forceinline__ int read_len(const int32_t *lens, int64_t r, int32_t 
     return l < 0 ? 0 : l;
 }
 
-// per-lane scratch of G1: prev / curr / mem1 lists, the interval list, the read's codes
-constexpr int64_t G1_SLOT_BIV = 3 * G_LIST + AF_G_MAX_INTV + G_LIST;
-constexpr int64_t G1_SLOT_BYTES = G1_SLOT_BIV * (int64_t)sizeof(GBi) + AF_MAX_READ + 16;
+// ============================================================= G1: mem_collect_intv
+// One lane per read, as a state machine whose every trip makes at most one FM extension per lane
+// (bwt_extend of one interval by one base: two 64-B occurrence blocks), so the 64 lanes of a wave
+// issue their dependent lookups together whatever phase each read is in: bwt_smem1's forward
+// scan, its backward scan (one list entry per trip), or bwt_seed_strategy1.  Between extensions a
+// lane runs its list bookkeeping; a lane whose read is done takes the next read (one atomic per
+// wave).  The three passes of mem_collect_intv (oracle fm_collect: SMEMs, re-seeding of long
+// SMEMs with few occurrences, bwt_seed_strategy1) and their list orders are bwa's.
+//
+// Per-lane lists in global scratch, lane-major (a lane's walk reads its lists sequentially),
+// one 16-byte packed interval each: k, l, s (33 bits each: at most 2 l_pac + 1 rows < 2^33,
+// checked when the index is built) and qb, qe (9 bits each).
+constexpr int G1_LIST = AF_MAX_READ + 2;              // prev / curr / mem lists of bwt_smem1
+constexpr int64_t G1_SLOT = 3 * G1_LIST + AF_G_MAX_INTV;  // + the read's interval list (uint4)
+struct G1Iv { int64_t k, l, s; int qb, qe; };
+__device__ __forceinline__ uint4 g1_pack(int64_t k, int64_t l, int64_t s, int qb, int qe) {
+    return make_uint4((uint32_t)k, (uint32_t)l, (uint32_t)s,
+                      (uint32_t)(k >> 32 & 1) | (uint32_t)(l >> 32 & 1) << 1 | (uint32_t)(s >> 32 & 1) << 2 |
+                          (uint32_t)qb << 3 | (uint32_t)qe << 12);
+}
+__device__ __forceinline__ G1Iv g1_unpack(uint4 v) {
+    G1Iv r;
+    r.k = (int64_t)v.x | (int64_t)(v.w & 1) << 32;
+    r.l = (int64_t)v.y | (int64_t)(v.w >> 1 & 1) << 32;
+    r.s = (int64_t)v.z | (int64_t)(v.w >> 2 & 1) << 32;
+    r.qb = (int)(v.w >> 3 & 511);
+    r.qe = (int)(v.w >> 12 & 511);
+    return r;
+}
+enum : int { G1_IDLE, G1_P1, G1_FWD, G1_BWD, G1_P2, G1_P3, G1_SS, G1_DONE, G1_EXIT };
 
-__global__ __launch_bounds__(64) void k_g_seeds(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
-                                                const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
-                                                int64_t cap, int64_t read0, af_params p, GOpt o,
-                                                uint8_t *__restrict__ scratch, GWork w) {
-    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+__global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const uint8_t *__restrict__ reads,
+                                                          int32_t stride, const int32_t *__restrict__ lens,
+                                                          const int32_t *__restrict__ n_ptr, int64_t cap,
+                                                          int64_t read0, af_params p, GOpt o,
+                                                          uint4 *__restrict__ scratch, GWork w) {
+    const int lane = threadIdx.x;
+    const int64_t tid = (int64_t)blockIdx.x * blockDim.x + lane;
     int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
     if (n > cap) n = cap;
-    GBi *base = reinterpret_cast<GBi *>(scratch + tid * G1_SLOT_BYTES);
-    GBi *prev = base, *curr = base + G_LIST, *m1 = base + 2 * G_LIST, *fmm = base + 3 * G_LIST;
-    uint8_t *q = reinterpret_cast<uint8_t *>(base + G1_SLOT_BIV);
+    uint4 *const base = scratch + tid * G1_SLOT;
+    uint4 *Lp = base, *Lc = base + G1_LIST;        // bwt_smem1's prev / curr (swapped by pointer)
+    uint4 *const Lm = base + 2 * G1_LIST, *const Lf = base + 3 * G1_LIST;  // its mems; the read's list
     const int msl = p.min_seed_len;
     const int split_len = (int)((float)msl * 1.5f + .499);
-    for (int64_t rr = read0 + tid; rr < n; rr += nthr) {
-        GPROF(const uint64_t gp_c0 = clock64(); const uint32_t gp_t0 = gp_rt();
-              auto gp_end = [&](int ni_) { int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0);
-                  g[1] = ni_; g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid; } };)
-        const int len = read_len(lens, rr, stride);
-        const uint8_t *rd = reads + rr * (int64_t)stride;
-        for (int x = 0; x < len; ++x) q[x] = nt4(rd[x]);
-        int ni = 0, n1 = 0;
-        bool ovf = false;
-        if (len >= msl) {
-            int x = 0;
-            while (x < len && !ovf) {  // pass 1: SMEMs
-                if (q[x] < 4) {
-                    x = g_smem1(G, q, len, x, 1, m1, &n1, prev, curr);
-                    for (int i = 0; i < n1; ++i)
-                        if (m1[i].qe - m1[i].qb >= msl) {
-                            if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
-                            fmm[ni++] = m1[i];
-                        }
-                } else ++x;
-            }
-            const int old_n = ni;
-            for (int k = 0; k < old_n && !ovf; ++k) {  // pass 2: re-seeding
-                const GBi pk = fmm[k];
-                if (pk.qe - pk.qb < split_len || pk.s > o.split_width) continue;
-                g_smem1(G, q, len, (pk.qb + pk.qe) >> 1, pk.s + 1, m1, &n1, prev, curr);
-                for (int i = 0; i < n1; ++i)
-                    if (m1[i].qe - m1[i].qb >= msl) {
-                        if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
-                        fmm[ni++] = m1[i];
-                    }
-            }
-            if (o.max_mem_intv > 0) {  // pass 3: bwt_seed_strategy1
-                x = 0;
-                while (x < len && !ovf) {
-                    if (q[x] < 4) {
-                        GBi m;
-                        x = g_seed_strategy1(G, q, len, x, msl, o.max_mem_intv, &m);
-                        if (m.s > 0) {
-                            if (ni >= AF_G_MAX_INTV) { ovf = true; break; }
-                            fmm[ni++] = m;
-                        }
-                    } else ++x;
+    // lane state
+    int st = G1_IDLE, len = 0, x = 0, i = 0, j = 0, np = 0, nc = 0, nm = 0, ret = 0, ni = 0, k2 = 0, old_n = 0;
+    int pass = 1, sx = 0, last_mem_qb = 0, ik_qe = 0, p_qe = 0;
+    bool ovf = false, rev = false;
+    int64_t rr = -1, min_intv = 1, ik_k = 0, ik_l = 0, ik_s = 0, last_s = 0;
+    const uint8_t *rd = nullptr;
+    GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0;)
+    auto code = [&](int t) -> int { return nt4(rd[t]); };
+    auto push_curr = [&](int64_t k, int64_t l, int64_t s, int qb, int qe) { Lc[nc++] = g1_pack(k, l, s, qb, qe); };
+    auto smem_start = [&](int x0, int64_t mi, int ps) {
+        const int c = code(x0);
+        sx = x0; min_intv = mi < 1 ? 1 : mi; pass = ps;
+        fm_set(G, c, ik_k, ik_l, ik_s);
+        ik_qe = x0 + 1; i = x0 + 1; nc = 0; nm = 0;
+        st = G1_FWD;
+    };
+    auto fwd_end = [&]() {  // curr holds the forward intervals in push order (bwa reverses them)
+        ret = (int)g1_unpack(Lc[nc - 1]).qe;
+        uint4 *t = Lp; Lp = Lc; Lc = t;
+        np = nc; nc = 0; rev = true; i = sx - 1; j = 0;
+        st = G1_BWD;
+    };
+    auto take = [&](const G1Iv &m) -> bool {  // an interval into the read's list
+        if (ni >= AF_G_MAX_INTV) { ovf = true; st = G1_DONE; return false; }
+        Lf[ni++] = g1_pack(m.k, m.l, m.s, m.qb, m.qe);
+        return true;
+    };
+    auto smem_end = [&]() {  // bwa reverses the mems; the caller keeps those of >= min_seed_len
+        for (int t = nm - 1; t >= 0; --t) {
+            const G1Iv m = g1_unpack(Lm[t]);
+            if (m.qe - m.qb >= msl && !take(m)) return;
+        }
+        if (pass == 1) { x = ret; st = G1_P1; }
+        else { ++k2; st = G1_P2; }
+    };
+    auto mem_push = [&](const G1Iv &pv, int qb) {  // a prev entry that cannot extend becomes a mem
+        if (nc == 0 && (nm == 0 || qb < last_mem_qb)) {
+            Lm[nm++] = g1_pack(pv.k, pv.l, pv.s, qb, pv.qe);
+            last_mem_qb = qb;
+        }
+    };
+    G1Iv pv{};
+    for (;;) {
+        // idle lanes take the next reads (one atomic per wave)
+        const uint64_t im = __ballot(st == G1_IDLE);
+        if (im) {
+            uint64_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(w.g1_next, (unsigned long long)__builtin_popcountll(im));
+            b0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b0) |
+                 (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b0 >> 32)) << 32;
+            if (st == G1_IDLE) {
+                rr = read0 + (int64_t)b0 + lanes_below(im, lane);
+                if (rr >= n) st = G1_EXIT;
+                else {
+                    len = read_len(lens, rr, stride);
+                    rd = reads + rr * (int64_t)stride;
+                    ni = 0; ovf = false; x = 0;
+                    st = len >= msl ? G1_P1 : G1_DONE;
+                    GPROF(gp_c0 = clock64(); gp_t0 = gp_rt();)
                 }
             }
         }
-        if (ovf) { w.iv_n[rr] = -1; GPROF(gp_end(-1);) continue; }
-        // sort by (qb, qe): equal keys are identical intervals (any order)
-        for (int i = 1; i < ni; ++i) {
-            const GBi t = fmm[i];
-            const uint64_t kt = (uint64_t)t.qb << 32 | (uint32_t)t.qe;
-            int j = i;
-            while (j > 0 && ((uint64_t)fmm[j - 1].qb << 32 | (uint32_t)fmm[j - 1].qe) > kt) { fmm[j] = fmm[j - 1]; --j; }
-            fmm[j] = t;
+        if (__ballot(st != G1_EXIT) == 0) break;
+        // advance each lane to its next FM extension
+        bool need = false;
+        int64_t ek = 0, el = 0, es = 0;
+        int ec = 0;
+        bool efwd = false;
+        while (!need && st != G1_IDLE && st != G1_EXIT) {
+            if (st == G1_P1) {  // pass 1: SMEMs covering each position
+                if (x >= len) { old_n = ni; k2 = 0; st = G1_P2; continue; }
+                if (code(x) > 3) { ++x; continue; }
+                smem_start(x, 1, 1);
+            } else if (st == G1_FWD) {  // bwt_smem1 forward search
+                if (i == len) { push_curr(ik_k, ik_l, ik_s, 0, ik_qe); fwd_end(); continue; }
+                const int c = code(i);
+                if (c > 3) { push_curr(ik_k, ik_l, ik_s, 0, ik_qe); fwd_end(); continue; }
+                need = true; ek = ik_k; el = ik_l; es = ik_s; ec = 3 - c; efwd = true;
+            } else if (st == G1_BWD) {  // backward search for MEMs: entry j of prev at position i
+                if (j == np) {
+                    if (nc == 0) { smem_end(); continue; }
+                    uint4 *t = Lp; Lp = Lc; Lc = t;
+                    np = nc; nc = 0; rev = false; --i; j = 0;
+                    continue;
+                }
+                pv = g1_unpack(Lp[rev ? np - 1 - j : j]);
+                const int c = i < 0 ? -1 : code(i);
+                if (c < 0 || c > 3) { mem_push(pv, i + 1); ++j; continue; }
+                need = true; ek = pv.k; el = pv.l; es = pv.s; ec = c; efwd = false; p_qe = pv.qe;
+            } else if (st == G1_P2) {  // pass 2: re-seed long SMEMs with few occurrences
+                if (k2 >= old_n) {
+                    if (o.max_mem_intv > 0) { x = 0; st = G1_P3; }
+                    else st = G1_DONE;
+                    continue;
+                }
+                const G1Iv pk = g1_unpack(Lf[k2]);
+                if (pk.qe - pk.qb < split_len || pk.s > o.split_width) { ++k2; continue; }
+                const int mid = (pk.qb + pk.qe) >> 1;
+                if (code(mid) > 3) { ++k2; continue; }
+                smem_start(mid, pk.s + 1, 2);
+            } else if (st == G1_P3) {  // pass 3: bwt_seed_strategy1 from each position
+                if (x >= len) { st = G1_DONE; continue; }
+                const int c = code(x);
+                if (c > 3) { ++x; continue; }
+                sx = x; i = x + 1;
+                fm_set(G, c, ik_k, ik_l, ik_s);
+                st = G1_SS;
+            } else if (st == G1_SS) {
+                if (i >= len) { x = len; st = G1_P3; continue; }
+                const int c = code(i);
+                if (c > 3) { x = i + 1; st = G1_P3; continue; }
+                need = true; ek = ik_k; el = ik_l; es = ik_s; ec = 3 - c; efwd = true;
+            } else {  // G1_DONE: the list sorted by (qb, qe) into the call's pool
+                if (ovf) w.iv_n[rr] = -1;
+                else {
+                    for (int a = 1; a < ni; ++a) {  // equal keys are identical intervals (any order)
+                        const uint4 t = Lf[a];
+                        const uint32_t kt = (t.w >> 3 & 511) << 9 | (t.w >> 12 & 511);
+                        int b = a;
+                        while (b > 0) {
+                            const uint4 u = Lf[b - 1];
+                            if (((u.w >> 3 & 511) << 9 | (u.w >> 12 & 511)) <= kt) break;
+                            Lf[b] = u;
+                            --b;
+                        }
+                        Lf[b] = t;
+                    }
+                    const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
+                    if (ni && off + ni > w.iv_cap) {  // the pool is sized from the call's read count
+                        atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
+                        w.iv_n[rr] = -1;
+                    } else {
+                        for (int a = 0; a < ni; ++a) {
+                            const G1Iv m = g1_unpack(Lf[a]);
+                            w.iv[off + a] = GIv{m.k, m.s, m.qb, m.qe};
+                        }
+                        w.iv_off[rr] = off;
+                        w.iv_n[rr] = ni;
+                    }
+                }
+                GPROF({ int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0); g[1] = ovf ? -1 : ni;
+                        g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid; } })
+                st = G1_IDLE;
+            }
         }
-        const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
-        if (ni && off + ni > w.iv_cap) {  // the pool is sized from the call's read count
-            atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
-            w.iv_n[rr] = -1;
-            GPROF(gp_end(-2);)
-            continue;
+        if (__ballot(need) == 0) continue;
+        // the extensions of this trip: every lane that needs one at once
+        int64_t rk = 0, rl = 0, rs = 0;
+        if (need) fm_ext1(G, ek, el, es, ec, efwd, rk, rl, rs);
+        if (!need) continue;
+        if (st == G1_FWD) {
+            if (rs != ik_s) {
+                push_curr(ik_k, ik_l, ik_s, 0, ik_qe);
+                if (rs < min_intv) { fwd_end(); continue; }
+            }
+            ik_k = rk; ik_l = rl; ik_s = rs; ik_qe = i + 1; ++i;
+        } else if (st == G1_BWD) {
+            if (rs < min_intv) mem_push(pv, i + 1);
+            else if (nc == 0 || rs != last_s) { push_curr(rk, rl, rs, 0, p_qe); last_s = rs; }
+            ++j;
+        } else {  // G1_SS
+            if (rs < o.max_mem_intv && i - sx >= msl) {  // the caller keeps a non-empty interval
+                if (rs > 0) take(G1Iv{rk, rl, rs, sx, i + 1});
+                if (st != G1_DONE) { x = i + 1; st = G1_P3; }
+            } else { ik_k = rk; ik_l = rl; ik_s = rs; ++i; }
         }
-        for (int i = 0; i < ni; ++i) w.iv[off + i] = GIv{fmm[i].k, fmm[i].s, fmm[i].qb, fmm[i].qe};
-        w.iv_off[rr] = off;
-        w.iv_n[rr] = ni;
-        GPROF(gp_end(ni);)
     }
 }
 
@@ -1578,7 +1625,7 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
 
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; }
+    if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
     if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
     if (t < AF_GSTAT_N) w.stats[t] = 0;
     (void)n_reads;
@@ -1586,7 +1633,7 @@ __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
 
 }  // namespace
 
-size_t af_g1_slot_bytes() { return (size_t)G1_SLOT_BYTES; }
+size_t af_g1_slot_bytes() { return (size_t)G1_SLOT * sizeof(uint4); }
 
 #ifdef AF_G_PROF
 static int32_t *h_gprof = nullptr;
@@ -1625,8 +1672,10 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                                     uint8_t *zscratch, hipStream_t s) {
     GPROF(gprof_next(s);)
     hipLaunchKernelGGL(k_g_zero, dim3(1), dim3(64), 0, s, w, cap, w.heads);
-    hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)(n_g1_threads / 64)), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
-                       (int64_t)0, p, o, g1_scratch, w);
+    // one lane per read, at most the scratch's lanes (idle lanes refill from w.g1_next)
+    const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));
+    hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
+                       (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C) hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap, \
@@ -1636,6 +1685,17 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
+    return hipGetLastError();
+}
+
+// G1 alone (af_genome_intervals, parity tests)
+hipError_t af_launch_genome_intervals(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
+                                      int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
+                                      uint8_t *g1_scratch, int n_g1_threads, hipStream_t s) {
+    hipLaunchKernelGGL(k_g_zero, dim3(1), dim3(64), 0, s, w, cap, w.heads);
+    const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));
+    hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, nullptr, cap,
+                       (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     return hipGetLastError();
 }
 

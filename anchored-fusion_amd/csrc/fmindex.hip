@@ -268,10 +268,14 @@ hipError_t af_fm_build(const uint8_t *d_blob, const int64_t *src_off, const int6
     unsigned long long *cur = nullptr;
     uint64_t *kA = nullptr, *kB = nullptr, *cnt = nullptr;
     int64_t *vA = nullptr, *vB = nullptr, *hv = nullptr, *gs = nullptr, *sel_n = nullptr;
+    int64_t *g2 = nullptr;  // a long group's boundary scan (freed at done: on error paths too)
     int64_t cap = 0;  // chunk arrays' capacity
     int64_t nU = 0;
     std::vector<unsigned long long> hist(NB);
     if (l_pac <= 0 || n_ctg < 1) return hipErrorInvalidValue;
+    // suffix ranks + 1 are packed in 33 bits (k_dbl_keys), as are the genome kernels' SA-row
+    // intervals (bwa_genome.hip G1): 2 l_pac + 1 rows must stay below 2^33
+    if (N + 1 >= (int64_t)1 << 33) return hipErrorInvalidValue;
     G->l_pac = l_pac; G->N = N; G->n_ctg = n_ctg;
     FMCHK(hipMalloc(&G->ctg_off_d, sizeof(int64_t) * n_ctg));
     FMCHK(hipMalloc(&G->ctg_len_d, sizeof(int64_t) * n_ctg));
@@ -409,15 +413,17 @@ hipError_t af_fm_build(const uint8_t *d_blob, const int64_t *src_off, const int6
                     int64_t gl = n;
                     for (;;) {
                         const int64_t m = std::min<int64_t>(2 * gl, nU - u0);
-                        int64_t *g2 = nullptr;
                         FMCHK(hipMalloc(&g2, sizeof(int64_t) * (m + 1)));
                         hipLaunchKernelGGL(k_gather_gs, grid_for(m), dim3(256), 0, s, U + u0, m, G->sa, isa, g2);
+                        FMCHK(hipGetLastError());
                         unsigned long long fb = ~0ull;
                         FMCHK(hipMemcpyAsync(cur, &fb, sizeof fb, hipMemcpyHostToDevice, s));
                         hipLaunchKernelGGL(k_first_boundary, grid_for(m), dim3(256), 0, s, g2, m - 1, cur);
+                        FMCHK(hipGetLastError());
                         FMCHK(hipMemcpyAsync(&fb, cur, sizeof fb, hipMemcpyDeviceToHost, s));
                         FMCHK(hipStreamSynchronize(s));
                         FMCHK(hipFree(g2));
+                        g2 = nullptr;
                         if (fb != ~0ull) { gl = (int64_t)fb; break; }
                         if (m == nU - u0) { gl = m; break; }
                         gl = m;
@@ -530,7 +536,7 @@ done:
     (void)hipStreamSynchronize(s);
     (void)hipFree(d_src); (void)hipFree(d_pacoff); (void)hipFree(amb); (void)hipFree(ord); (void)hipFree(isa); (void)hipFree(U);
     (void)hipFree(keep); (void)hipFree(tmp); (void)hipFree(cur); (void)hipFree(kA); (void)hipFree(kB); (void)hipFree(vA);
-    (void)hipFree(vB); (void)hipFree(hv); (void)hipFree(gs); (void)hipFree(sel_n); (void)hipFree(cnt);
+    (void)hipFree(vB); (void)hipFree(hv); (void)hipFree(gs); (void)hipFree(sel_n); (void)hipFree(cnt); (void)hipFree(g2);
     if (ok != hipSuccess) af_fm_free(G);
     return ok;
 }

@@ -170,6 +170,20 @@ class GenomeIndex:
             nrec.ctypes.data), "af_genome_align_pe")
         return recs, nrec
 
+    def intervals(self, reads, lens=None, params=None, pe=None, max_iv=512):
+        """mem_collect_intv's seed intervals per read (tests): int64 [n, max_iv, 4] {sa_k, s, qb, qe},
+        counts [n] (-1: overflow)."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        ivs = np.zeros((n, max_iv, 4), np.int64)
+        niv = np.zeros(n, np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        _lib.check(self.ctx, _lib.lib().af_genome_intervals(
+            self.ctx, self.g, reads.ctypes.data, n, reads.shape[1], None if lp is None else lp.ctypes.data,
+            ctypes.byref(params or _lib.default_params()), ctypes.byref(pe or _lib.default_pe()), max_iv,
+            ivs.ctypes.data, niv.ctypes.data), "af_genome_intervals")
+        return ivs, niv
+
     def regions(self, reads, lens=None, params=None, pe=None, max_reg=64):
         """mem_align1_core's regions per read (tests): int64 [n, max_reg, 12], counts [n]."""
         reads = np.ascontiguousarray(reads, dtype=np.uint8)

@@ -343,6 +343,12 @@ int af_genome_align_pe(af_ctx *ctx, const af_genome *g, const uint8_t *reads, in
 /* regions after mem_align1_core (rb, re on bwa's doubled text; parity tests): regs[r * max_reg +
  * k] as 12 int64 words {rb, re, qb, qe, rid, score, truesc, w, seedcov, seedlen0, 0, 0}, n_reg[r]
  * (-1: overflow); host buffers */
+/* mem_collect_intv's seed intervals per read (parity tests): ivs[(r * max_iv + k) * 4] as int64
+ * words {SA row k, occurrences s, qb, qe} in mem_chain's order, n_iv[r] (-1: overflow); host
+ * buffers */
+int af_genome_intervals(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
+                        const int32_t *lens, const af_params *p, const af_pe *pe, int32_t max_iv, int64_t *ivs,
+                        int32_t *n_iv);
 int af_genome_regions(af_ctx *ctx, const af_genome *g, const uint8_t *reads, int64_t n, int32_t stride,
                       const int32_t *lens, const af_params *p, const af_pe *pe, int32_t max_reg, int64_t *regs,
                       int32_t *n_reg);

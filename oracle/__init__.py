@@ -229,6 +229,9 @@ def _glib():
         L.afo_genome_seeds.restype = ctypes.c_int
         L.afo_genome_seeds.argtypes = [vp, vp, i32, ctypes.POINTER(Params), ctypes.POINTER(Pe), ctypes.c_int, vp, vp,
                                        vp, i32]
+        L.afo_genome_intervals.restype = ctypes.c_int
+        L.afo_genome_intervals.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe),
+                                           ctypes.c_int, i32, vp, vp]
         L.afo_genome_regions.restype = ctypes.c_int
         L.afo_genome_regions.argtypes = [vp, vp, i64, i32, vp, ctypes.POINTER(Params), ctypes.POINTER(Pe),
                                          ctypes.c_int, i32, vp, vp]
@@ -292,6 +295,22 @@ class OracleGenome:
         if n < 0:
             raise OverflowError(f"afo_genome_seeds: {n}")
         return rb[:n], qb[:n], ln[:n]
+
+    def intervals(self, reads, lens=None, params=None, pe=None, max_iv=512, threads=0):
+        """mem_collect_intv per read: int64 [n, max_iv, 4] {sa_k, s, qb, qe} in mem_chain's order,
+        counts [n] (-1: past the interval cap)."""
+        reads = np.ascontiguousarray(reads, dtype=np.uint8)
+        n = reads.shape[0]
+        out = np.zeros((n, max_iv, 4), np.int64)
+        niv = np.zeros(n, np.int32)
+        lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.int32)
+        rc = _glib().afo_genome_intervals(self.h, reads.ctypes.data, n, reads.shape[1],
+                                          None if lp is None else lp.ctypes.data,
+                                          ctypes.byref(params or default_params()), ctypes.byref(pe or default_pe()),
+                                          int(threads), max_iv, out.ctypes.data, niv.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"afo_genome_intervals failed: {rc}")
+        return out, niv
 
     def regions(self, reads, lens=None, params=None, pe=None, max_reg=64, threads=0):
         reads = np.ascontiguousarray(reads, dtype=np.uint8)

@@ -105,6 +105,9 @@ const int64_t *afo_genome_sa(const afo_genome *G);     /* suffix array rows 0..2
 int64_t afo_genome_primary(const afo_genome *G);
 int afo_genome_seeds(const afo_genome *G, const uint8_t *read, int32_t l, const afo_params *p, const afo_pe *pe,
                      int memset_mode, int64_t *rbeg, int32_t *qbeg, int32_t *len, int32_t cap);
+int afo_genome_intervals(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                         const afo_params *p, const afo_pe *pe, int n_threads, int32_t max_iv, int64_t *out,
+                         int32_t *n_iv);
 int afo_genome_regions(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
                        const afo_params *p, const afo_pe *pe, int n_threads, int32_t max_reg, afo_reg *regs,
                        int32_t *n_reg);

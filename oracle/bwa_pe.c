@@ -2073,6 +2073,36 @@ int afo_genome_seeds(const afo_genome *G, const uint8_t *read, int32_t l, const 
     return n;
 }
 
+/* mem_collect_intv for each read (FM index): its seed intervals in mem_chain's order, as int64
+ * words {sa_k, s, qb, qe} at out[(r * max_iv + i) * 4]; n_iv[r] the count (-1: past caps.intv) */
+int afo_genome_intervals(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
+                         const afo_params *p, const afo_pe *pe_in, int n_threads, int32_t max_iv, int64_t *out,
+                         int32_t *n_iv) {
+    afo_pe pe;
+    if (pe_in) pe = *pe_in;
+    else afo_pe_default(&pe);
+#ifdef _OPENMP
+    if (n_threads > 0) omp_set_num_threads(n_threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+    for (int64_t r = 0; r < n; ++r) {
+        uint8_t q[AFO_MAX_READ];
+        const int l = read_codes(reads, r, stride, lens, q);
+        rstate_t S;
+        rstate_init(&S, G, p, &pe, q, l);
+        n_iv[r] = 0;
+        if (l < p->min_seed_len) continue;
+        collect_intv(&S);
+        if (S.overflow) { n_iv[r] = -1; continue; }
+        n_iv[r] = S.nsi;
+        for (int i = 0; i < S.nsi && i < max_iv; ++i) {
+            int64_t *o = out + ((size_t)r * max_iv + i) * 4;
+            o[0] = S.si[i].sa_k; o[1] = S.si[i].cnt; o[2] = S.si[i].qb; o[3] = S.si[i].qe;
+        }
+    }
+    return 0;
+}
+
 /* mem_align1_core for each read: its regions in mem_sort_dedup_patch order */
 int afo_genome_regions(const afo_genome *G, const uint8_t *reads, int64_t n, int32_t stride, const int32_t *lens,
                        const afo_params *p, const afo_pe *pe_in, int n_threads, int32_t max_reg, afo_reg *regs,

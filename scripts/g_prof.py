@@ -48,6 +48,8 @@ torch.cuda.synchronize()
 print(f"profiled pass {time.perf_counter() - t0:.3f} s; {disc.summary()}")
 buf = np.zeros((4, CAP, GW), dtype=np.int32)
 ncalls = lib.af_debug_g_prof_read(buf.ctypes.data, buf.size)
+if os.environ.get("GPROF_SAVE"):  # per-read interval counts and region counts of the first call
+    np.save(os.environ["GPROF_SAVE"], buf[0][:, [1, 12, 13]].copy())
 pct = lambda v, q: np.percentile(v, q) if len(v) else 0  # noqa: E731
 for c in range(min(ncalls, 4)):
     B = buf[c]

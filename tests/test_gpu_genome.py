@@ -49,6 +49,28 @@ def _rec_equal(a, b, n):
     return None
 
 
+def _iv_sets_equal(io, no, ig, ng):
+    """Per read: the same count and the same intervals (sorted by qb, qe, SA row, size: equal
+    (qb, qe) keys hold identical intervals, in any order)."""
+    assert np.array_equal(no, ng), np.nonzero(no != ng)[0][:10]
+    for r in range(len(no)):
+        k = min(int(no[r]), io.shape[1])
+        a, b = io[r, :k], ig[r, :k]
+        a = a[np.lexsort((a[:, 1], a[:, 0], a[:, 3], a[:, 2]))]
+        b = b[np.lexsort((b[:, 1], b[:, 0], b[:, 3], b[:, 2]))]
+        assert np.array_equal(a, b), (r, a[:4], b[:4])
+
+
+def test_intervals_equal_oracle(world):
+    """G1 (mem_collect_intv: SMEMs, re-seeding, bwt_seed_strategy1) interval by interval."""
+    contigs, og, gg = world
+    reads, lens = sample_reads(contigs, 800, seed=20, chimeric=0.4)
+    io, no = og.intervals(reads, lens, threads=8)
+    ig, ng = gg.intervals(reads, lens)
+    _iv_sets_equal(io, no, ig, ng)
+    assert no.mean() > 4
+
+
 def test_se_regions_equal_oracle(world):
     contigs, og, gg = world
     reads, lens = sample_reads(contigs, 400, seed=21)
