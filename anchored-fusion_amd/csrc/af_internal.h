@@ -12,6 +12,9 @@
 #ifndef AF_G1_WPS
 #define AF_G1_WPS 4             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish
 #endif
+#ifndef AF_G_HEAVY_CHAINS
+#define AF_G_HEAVY_CHAINS 16    // G2: reads with this many kept chains extend them one job per chain (env AF_G_HEAVY_CHAINS)
+#endif
 #ifndef AF_K2_WPS
 #define AF_K2_WPS 6             // S2 K2 waves per SIMD (launch bound; persistent slots = 4 x this per CU)
 #endif
@@ -207,6 +210,17 @@ struct GReg {                                        // mem_alnreg_t
     int32_t qb, qe, rid, score, truesc, w, seedcov, seedlen0, secondary, sub;
     uint64_t hash;
 };
+// G2's heavy reads (at least min_chains kept chains): the extensions of their chains run as
+// one job per chain (k_g_ext_jobs) before a wave per read finishes it (k_g_heavy)
+struct GHeavy {
+    int64_t *read;                    // [cap_reads] the read (-1: reservation failed)
+    int32_t *nch, *ch_off, *sd_off;   // [cap_reads] its kept chains and seeds in the pools
+    int32_t *ch_read;                 // [cap_ch] each pooled chain's heavy read (-1: unused)
+    void *ch, *sd, *res;              // GChain [cap_ch], GSeed [cap_sd], GReg [cap_sd] (each seed's region)
+    unsigned long long *cnt;          // [0] heavy reads, [1] chains, [2] seeds, [3] job / [4] finish dequeue
+    int64_t cap_reads, cap_ch, cap_sd;
+    int32_t min_chains;               // 0: every read extended by its own wave
+};
 // per-call pools and counters of the genome kernels (per context)
 struct GWork {
     GIv *iv;                    // intervals of every read (G1)
@@ -221,9 +235,12 @@ struct GWork {
     int32_t *heads;             // G2 dequeue heads (8 lines)
     int32_t *stats;             // AF_GSTAT_*
     unsigned long long *g1_next;  // G1: the next read to hand to an idle lane
+    GHeavy hv;
 };
 size_t af_g1_slot_bytes();
 size_t af_g2_slot_bytes();
+size_t af_g_chain_bytes();
+size_t af_g_seed_bytes();
 hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
                                     const int32_t *d_n, int64_t cap, const af_params &p, const GOpt &o, const GWork &w,
                                     uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,

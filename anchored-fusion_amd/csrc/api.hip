@@ -73,6 +73,9 @@ struct af_ctx {
     // per-wave scratch, and the event that orders them after the shared seed / region kernels
     uint8_t *g2_scr_pe = nullptr, *zscratch_pe = nullptr;
     hipEvent_t g_ev = nullptr;
+    // G2's heavy-read pools (GHeavy) and the kept-chain count from which a read is heavy
+    GHeavy g_hv{};
+    int32_t g_heavy_min = AF_G_HEAVY_CHAINS;
     GIv *g_iv = nullptr;
     GReg *g_reg = nullptr;
     int64_t g_iv_cap = 0, g_reg_cap = 0, g_cap_reads = 0;
@@ -413,6 +416,22 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     HIPCHK(c, hipMalloc(&c->g_iv_n, sizeof(int32_t) * cap));
     HIPCHK(c, hipMalloc(&c->g_reg_off, sizeof(int32_t) * cap));
     HIPCHK(c, hipMalloc(&c->g_reg_n, sizeof(int32_t) * cap));
+    // heavy reads: at most every read; 8 pooled chains and 16 seeds per read of the call (a read
+    // that does not fit is extended by its own wave)
+    GHeavy &h = c->g_hv;
+    af_free(h.read); af_free(h.nch); af_free(h.ch_off); af_free(h.sd_off); af_free(h.ch_read);
+    af_free(h.ch); af_free(h.sd); af_free(h.res);
+    h.read = nullptr; h.nch = h.ch_off = h.sd_off = h.ch_read = nullptr; h.ch = h.sd = h.res = nullptr;
+    h.cap_reads = cap; h.cap_ch = std::max<int64_t>(cap * 8, 1 << 16); h.cap_sd = 2 * h.cap_ch;
+    HIPCHK(c, hipMalloc(&h.read, sizeof(int64_t) * h.cap_reads));
+    HIPCHK(c, hipMalloc(&h.nch, sizeof(int32_t) * h.cap_reads));
+    HIPCHK(c, hipMalloc(&h.ch_off, sizeof(int32_t) * h.cap_reads));
+    HIPCHK(c, hipMalloc(&h.sd_off, sizeof(int32_t) * h.cap_reads));
+    HIPCHK(c, hipMalloc(&h.ch_read, sizeof(int32_t) * h.cap_ch));
+    HIPCHK(c, hipMalloc(&h.ch, af_g_chain_bytes() * h.cap_ch));
+    HIPCHK(c, hipMalloc(&h.sd, af_g_seed_bytes() * h.cap_sd));
+    HIPCHK(c, hipMalloc(&h.res, sizeof(GReg) * h.cap_sd));
+    if (!h.cnt) HIPCHK(c, hipMalloc(&h.cnt, 8 * sizeof(unsigned long long)));
     c->g_cap_reads = cap;
     return AF_OK;
 }
@@ -424,6 +443,8 @@ GWork genome_work(af_ctx *c) {
     w.reg_n = c->g_reg_n;
     w.heads = c->ctrl + AF_CTRL_G_HEADS;
     w.g1_next = c->g_iv_fill + 1;
+    w.hv = c->g_hv;
+    w.hv.min_chains = c->g_hv.cnt ? c->g_heavy_min : 0;
     w.stats = c->g_stats;
     return w;
 }
@@ -531,6 +552,7 @@ int af_ctx_create(int device, af_ctx **out) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
+    if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -555,6 +577,8 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->s3_keys); af_free(c->s3_temp); af_free(c->s3_counts);
     af_free(c->g_sel); af_free(c->g_sel_n); af_free(c->g_temp);
     af_free(c->g2_scr_pe); af_free(c->zscratch_pe);
+    af_free(c->g_hv.read); af_free(c->g_hv.nch); af_free(c->g_hv.ch_off); af_free(c->g_hv.sd_off); af_free(c->g_hv.ch_read);
+    af_free(c->g_hv.ch); af_free(c->g_hv.sd); af_free(c->g_hv.res); af_free(c->g_hv.cnt);
     if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
     af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n);

@@ -718,19 +718,14 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     return m;
 }
 
-// mem_chain2aln (oracle mem_chain2aln) for chain ci of S.ch2; regions appended to S.reg.
-// Returns false on a region-cap overflow.
-template <int CPL>
-__device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params &p, int l, int ci, int *nreg_io,
-                            int lane) {
-    DpLds &L = g_dp;
+// mem_chain2aln's extension window of a chain (rmax; clipped to the seed's contig, one strand)
+// into E.rmax (lane 0 computes it)
+__device__ void g_chain_rmax(const DevGenome &G, const af_params &p, int l, const GSeed *sd, int n, int lane) {
     G2Lds &E = g_g2;
     const int64_t l_pac = G.l_pac;
-    const GChain c = S.ch2[ci];
-    const GSeed *sd = S.seed + c.seed0;
     if (lane == 0) {
         int64_t r0 = l_pac << 1, r1 = 0;
-        for (int i = 0; i < c.n; ++i) {
+        for (int i = 0; i < n; ++i) {
             const GSeed t = sd[i];
             const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(p, t.qbeg));
             const int rem = l - t.qbeg - t.len;
@@ -748,6 +743,90 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
         g_fetch_clip(G, &r0, sd[0].rbeg, &r1, &rid);
         E.rmax[0] = r0; E.rmax[1] = r1;
     }
+    wave_sync();
+}
+
+// mem_chain2aln's extension of seed s of a chain (seeds sd[0, n), contig rid): ksw_extend2 to
+// the left and right of the seed inside the window [rmax0, rmax1) and the chain's seed coverage
+// of the region; the read's codes in L.q.  The region on every lane.
+template <int CPL>
+__device__ GReg g_seed_region(const DevGenome &G, const af_params &p, int l, const GSeed *sd, int n, int rid,
+                              const GSeed &s, int64_t rmax0, int64_t rmax1, int lane) {
+    DpLds &L = g_dp;
+    int a_score = -1, a_truesc = -1, a_qb = 0, a_qe = 0;
+    int64_t a_rb = 0, a_re = 0;
+    int aw0 = p.w, aw1 = p.w;
+    if (s.qbeg) {  // left extension
+        const int64_t tmp = s.rbeg - rmax0;
+        const int tl = (int)min(tmp, (int64_t)(s.qbeg + 2 * p.w + 1));
+        for (int x = lane; x < s.qbeg; x += 64) L.qs[x] = L.q[s.qbeg - 1 - x];
+        for (int x = lane; x < tl; x += 64) L.t[x] = G.T[s.rbeg - 1 - x];
+        wave_sync();
+        ExtRes er;
+        for (int it = 0; it < 2; ++it) {
+            const int prev = a_score;
+            aw0 = p.w << it;
+            er = ext_dp<CPL>(s.qbeg, L.qs, tl, L.t, p, aw0, p.pen_clip5, p.zdrop, s.len * p.a, lane);
+            a_score = er.max;
+            if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+        }
+        if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip5) {
+            a_qb = s.qbeg - er.qle; a_rb = s.rbeg - er.tle; a_truesc = a_score;
+        } else {
+            a_qb = 0; a_rb = s.rbeg - er.gtle; a_truesc = er.gscore;
+        }
+        wave_sync();
+    } else {
+        a_score = a_truesc = s.len * p.a; a_qb = 0; a_rb = s.rbeg;
+    }
+    if (s.qbeg + s.len != l) {  // right extension
+        const int qe = s.qbeg + s.len;
+        const int64_t re = s.rbeg + s.len - rmax0;
+        const int sc0 = a_score;
+        const int tl = (int)min(rmax1 - rmax0 - re, (int64_t)((l - qe) + 2 * p.w + 1));
+        for (int x = lane; x < tl; x += 64) L.t[x] = G.T[rmax0 + re + x];
+        wave_sync();
+        ExtRes er;
+        for (int it = 0; it < 2; ++it) {
+            const int prev = a_score;
+            aw1 = p.w << it;
+            er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+            a_score = er.max;
+            if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
+        }
+        if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip3) {
+            a_qe = qe + er.qle; a_re = rmax0 + re + er.tle; a_truesc += a_score - sc0;
+        } else {
+            a_qe = l; a_re = rmax0 + re + er.gtle; a_truesc += er.gscore - sc0;
+        }
+        wave_sync();
+    } else {
+        a_qe = l; a_re = s.rbeg + s.len;
+    }
+    // seedcov: the chain's seeds inside the region
+    int cov = 0;
+    for (int i = lane; i < n; i += 64) {
+        const GSeed t = sd[i];
+        if (t.qbeg >= a_qb && t.qbeg + t.len <= a_qe && t.rbeg >= a_rb && t.rbeg + t.len <= a_re) cov += t.len;
+    }
+    cov = wave_sum(cov);
+    GReg a;
+    a.rb = a_rb; a.re = a_re; a.qb = a_qb; a.qe = a_qe; a.rid = rid; a.score = a_score; a.truesc = a_truesc;
+    a.w = aw0 > aw1 ? aw0 : aw1; a.seedlen0 = s.len; a.seedcov = cov; a.secondary = -1; a.sub = 0; a.hash = 0;
+    return a;
+}
+
+// mem_chain2aln (oracle mem_chain2aln) for chain ci of S.ch2; regions appended to S.reg.  pre
+// (heavy reads): every seed's region already extended (k_g_ext_jobs), pre[seed0 + i] for the
+// chain's seed i -- the walk below only decides which of them bwa keeps.
+// Returns false on a region-cap overflow.
+template <int CPL>
+__device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params &p, int l, int ci, int *nreg_io,
+                            int lane, const GReg *pre = nullptr) {
+    G2Lds &E = g_g2;
+    const GChain c = S.ch2[ci];
+    const GSeed *sd = S.seed + c.seed0;
+    if (!pre) g_chain_rmax(G, p, l, sd, c.n, lane);
     // srt: seed indices by (score << 32 | i) ascending (keys distinct): rank sort on the wave
     for (int i0 = 0; i0 < c.n; i0 += 64) {
         const int i = i0 + lane;
@@ -810,68 +889,8 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
             }
         }
         if (nreg >= AF_G_MAX_REG) return false;
-        int a_score = -1, a_truesc = -1, a_qb = 0, a_qe = 0;
-        int64_t a_rb = 0, a_re = 0;
-        int aw0 = p.w, aw1 = p.w;
-        if (s.qbeg) {  // left extension
-            const int64_t tmp = s.rbeg - rmax0;
-            const int tl = (int)min(tmp, (int64_t)(s.qbeg + 2 * p.w + 1));
-            for (int x = lane; x < s.qbeg; x += 64) L.qs[x] = L.q[s.qbeg - 1 - x];
-            for (int x = lane; x < tl; x += 64) L.t[x] = G.T[s.rbeg - 1 - x];
-            wave_sync();
-            ExtRes er;
-            for (int it = 0; it < 2; ++it) {
-                const int prev = a_score;
-                aw0 = p.w << it;
-                er = ext_dp<CPL>(s.qbeg, L.qs, tl, L.t, p, aw0, p.pen_clip5, p.zdrop, s.len * p.a, lane);
-                a_score = er.max;
-                if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
-            }
-            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip5) {
-                a_qb = s.qbeg - er.qle; a_rb = s.rbeg - er.tle; a_truesc = a_score;
-            } else {
-                a_qb = 0; a_rb = s.rbeg - er.gtle; a_truesc = er.gscore;
-            }
-            wave_sync();
-        } else {
-            a_score = a_truesc = s.len * p.a; a_qb = 0; a_rb = s.rbeg;
-        }
-        if (s.qbeg + s.len != l) {  // right extension
-            const int qe = s.qbeg + s.len;
-            const int64_t re = s.rbeg + s.len - rmax0;
-            const int sc0 = a_score;
-            const int tl = (int)min(rmax1 - rmax0 - re, (int64_t)((l - qe) + 2 * p.w + 1));
-            for (int x = lane; x < tl; x += 64) L.t[x] = G.T[rmax0 + re + x];
-            wave_sync();
-            ExtRes er;
-            for (int it = 0; it < 2; ++it) {
-                const int prev = a_score;
-                aw1 = p.w << it;
-                er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
-                a_score = er.max;
-                if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
-            }
-            if (er.gscore <= 0 || er.gscore <= a_score - p.pen_clip3) {
-                a_qe = qe + er.qle; a_re = rmax0 + re + er.tle; a_truesc += a_score - sc0;
-            } else {
-                a_qe = l; a_re = rmax0 + re + er.gtle; a_truesc += er.gscore - sc0;
-            }
-            wave_sync();
-        } else {
-            a_qe = l; a_re = s.rbeg + s.len;
-        }
-        // seedcov: the chain's seeds inside the region
-        int cov = 0;
-        for (int i = lane; i < c.n; i += 64) {
-            const GSeed t = sd[i];
-            if (t.qbeg >= a_qb && t.qbeg + t.len <= a_qe && t.rbeg >= a_rb && t.rbeg + t.len <= a_re) cov += t.len;
-        }
-        cov = wave_sum(cov);
-        if (lane == 0) {
-            GReg &a = S.reg[nreg];
-            a.rb = a_rb; a.re = a_re; a.qb = a_qb; a.qe = a_qe; a.rid = c.rid; a.score = a_score; a.truesc = a_truesc;
-            a.w = aw0 > aw1 ? aw0 : aw1; a.seedlen0 = s.len; a.seedcov = cov; a.secondary = -1; a.sub = 0; a.hash = 0;
-        }
+        const GReg a = pre ? pre[c.seed0 + (uint32_t)sk] : g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, s, rmax0, rmax1, lane);
+        if (lane == 0) S.reg[nreg] = a;
         *nreg_io = nreg + 1;
         wave_sync();
     }
@@ -999,7 +1018,84 @@ __device__ __forceinline__ int g_next_item(int32_t *heads, int &head, int &heads
     return -1;
 }
 
-// G2: mem_align1_core for every read (one wave per read)
+// the read's regions S.reg[0, nreg) into the call's pool (ovf: the read past a cap)
+__device__ void g_put_regions(const GWork &w, const G2Scr &S, int64_t r, int nreg, bool ovf, int lane) {
+    int off = 0;
+    if (!ovf && nreg > 0) {
+        if (lane == 0) g_g2.misc[4] = atomicAdd(w.reg_fill, nreg);
+        wave_sync();
+        off = g_g2.misc[4];
+        if ((int64_t)off + nreg > w.reg_cap) {
+            if (lane == 0) atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
+            ovf = true;
+        }
+    }
+    if (!ovf)
+        for (int k = lane; k < nreg; k += 64) w.reg[off + k] = S.reg[k];
+    if (lane == 0) {
+        w.reg_off[r] = off;
+        w.reg_n[r] = ovf ? -1 : nreg;
+        if (ovf) atomicAdd(&w.stats[AF_GSTAT_OVERFLOW], 1);
+    }
+    wave_sync();
+}
+
+// a heavy read's kept chains S.ch2[0, nch) and their seeds into the heavy pools (false: a pool is
+// full -- the read is then extended by its own wave)
+__device__ bool g_defer_heavy(const GWork &w, const G2Scr &S, int64_t r, int nch, int lane) {
+    const GHeavy &h = w.hv;
+    G2Lds &E = g_g2;
+    int nsd = 0;
+    for (int i = lane; i < nch; i += 64) nsd += S.ch2[i].n;
+    nsd = wave_sum(nsd);
+    if (lane == 0) {
+        const int64_t hr = (int64_t)atomicAdd(&h.cnt[0], 1ull);
+        const int64_t co = (int64_t)atomicAdd(&h.cnt[1], (unsigned long long)nch);
+        const int64_t so = (int64_t)atomicAdd(&h.cnt[2], (unsigned long long)nsd);
+        const bool ok = hr < h.cap_reads && co + nch <= h.cap_ch && so + nsd <= h.cap_sd;
+        if (hr < h.cap_reads) {
+            h.read[hr] = ok ? r : -1;
+            h.nch[hr] = nch; h.ch_off[hr] = (int32_t)co; h.sd_off[hr] = (int32_t)so;
+        }
+        E.misc[5] = ok ? (int32_t)hr : -1;
+        E.misc[6] = (int32_t)min(co, h.cap_ch);
+        E.misc[7] = (int32_t)so;
+    }
+    wave_sync();
+    const int hr = E.misc[5], co = E.misc[6], so = E.misc[7];
+    if (hr < 0) {  // chain slots of a failed reservation hold no job
+        for (int i = co + lane; i < h.cap_ch && i < co + nch; i += 64) h.ch_read[i] = -1;
+        return false;
+    }
+    GChain *hch = reinterpret_cast<GChain *>(h.ch) + co;
+    GSeed *hsd = reinterpret_cast<GSeed *>(h.sd) + so;
+    int base = 0;  // each chain's seeds contiguous, in chain order
+    for (int i0 = 0; i0 < nch; i0 += 64) {
+        const int i = i0 + lane;
+        GChain c{};
+        int cn = 0;
+        if (i < nch) { c = S.ch2[i]; cn = c.n; }
+        // exclusive prefix of the chain sizes over the 64 lanes
+        int inc = cn;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(inc, d);
+            if (lane >= d) inc += t;
+        }
+        const int s0 = base + inc - cn;
+        if (i < nch) {
+            for (int k = 0; k < cn; ++k) hsd[s0 + k] = S.seed[c.seed0 + k];
+            c.seed0 = s0;
+            hch[i] = c;
+            h.ch_read[co + i] = hr;
+        }
+        base += __shfl(inc, 63);
+    }
+    return true;
+}
+
+// G2: mem_align1_core for every read (one wave per read); a read with at least hv.min_chains
+// kept chains leaves their extensions to k_g_ext_jobs and its finish to k_g_heavy
 template <int CPL>
 __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
                                                      const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
@@ -1019,7 +1115,7 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
         const int l = read_len(lens, r, stride);
         const int niv = w.iv_n[r];
         int nreg = 0;
-        bool ovf = niv < 0;
+        bool ovf = niv < 0, deferred = false;
         GPROF(uint64_t gp_c[5] = {(uint64_t)clock64(), 0, 0, 0, 0}; const uint32_t gp_t0 = gp_rt(); int gp_n[4] = {0, 0, 0, 0};
               int64_t gp_occ = 0; if (niv > 0) for (int i = 0; i < niv; ++i) { const int64_t s_ = w.iv[w.iv_off[r] + i].s;
                   gp_occ += s_ > p.max_occ ? p.max_occ : s_; })
@@ -1031,11 +1127,14 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
             else {
                 const int nch = g_chain_flt(S, nch0, p, o, lane);
                 GPROF(gp_c[2] = clock64(); gp_n[1] = nch;)
-                for (int ci = 0; ci < nch && !ovf; ++ci)
-                    if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane)) ovf = true;
-                GPROF(gp_c[3] = clock64(); gp_n[2] = nreg;)
-                if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
-                GPROF(gp_c[4] = clock64(); gp_n[3] = nreg;)
+                if (w.hv.min_chains > 0 && nch >= w.hv.min_chains) deferred = g_defer_heavy(w, S, r, nch, lane);
+                if (!deferred) {
+                    for (int ci = 0; ci < nch && !ovf; ++ci)
+                        if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane)) ovf = true;
+                    GPROF(gp_c[3] = clock64(); gp_n[2] = nreg;)
+                    if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+                    GPROF(gp_c[4] = clock64(); gp_n[3] = nreg;)
+                }
             }
         }
         GPROF(if (lane == 0) { int32_t *g = gp_row(r); if (g) { const uint64_t ce = clock64();
@@ -1043,25 +1142,91 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
               g[4] = gp_c[1] ? (int32_t)(gp_c[1] - gp_c[0]) : 0; g[5] = gp_c[2] ? (int32_t)(gp_c[2] - gp_c[1]) : 0;
               g[6] = gp_c[3] ? (int32_t)(gp_c[3] - gp_c[2]) : 0; g[7] = gp_c[4] ? (int32_t)(gp_c[4] - gp_c[3]) : 0;
               g[8] = (int32_t)gp_occ; g[10] = gp_n[0]; g[11] = gp_n[1]; g[12] = gp_n[2]; g[13] = gp_n[3];
-              g[14] = (int32_t)blockIdx.x; g[15] = (int32_t)gp_t0; g[16] = (int32_t)gp_rt(); g[2] = l; } })
-        int off = 0;
-        if (!ovf && nreg > 0) {
-            if (lane == 0) g_g2.misc[4] = atomicAdd(w.reg_fill, nreg);
-            wave_sync();
-            off = g_g2.misc[4];
-            if ((int64_t)off + nreg > w.reg_cap) {
-                if (lane == 0) atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
-                ovf = true;
-            }
-        }
-        if (!ovf)
-            for (int k = lane; k < nreg; k += 64) w.reg[off + k] = S.reg[k];
-        if (lane == 0) {
-            w.reg_off[r] = off;
-            w.reg_n[r] = ovf ? -1 : nreg;
-            if (ovf) atomicAdd(&w.stats[AF_GSTAT_OVERFLOW], 1);
+              g[14] = (int32_t)blockIdx.x; g[15] = (int32_t)gp_t0; g[16] = (int32_t)gp_rt(); g[2] = l;
+              g[9] = deferred; } })
+        if (!deferred) g_put_regions(w, S, r, nreg, ovf, lane);
+    }
+}
+
+// G2, heavy reads: one job per pooled chain -- every seed of the chain extended (mem_chain2aln's
+// window and ksw_extend2 both ways), whether or not bwa's walk keeps it; k_g_heavy picks.
+template <int CPL>
+__global__ __launch_bounds__(64, 2) void k_g_ext_jobs(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                      const int32_t *__restrict__ lens, af_params p, GWork w) {
+    const int lane = threadIdx.x;
+    const GHeavy &h = w.hv;
+    const int64_t n_jobs = min((int64_t)*(volatile unsigned long long *)&h.cnt[1], h.cap_ch);
+    const GChain *hch = reinterpret_cast<const GChain *>(h.ch);
+    const GSeed *hsd = reinterpret_cast<const GSeed *>(h.sd);
+    GReg *res = reinterpret_cast<GReg *>(h.res);
+    for (;;) {
+        int64_t j = 0;
+        if (lane == 0) j = (int64_t)atomicAdd(&h.cnt[3], 1ull);
+        j = (int64_t)__builtin_amdgcn_readfirstlane((int)j);
+        if (j >= n_jobs) break;
+        const int hr = h.ch_read[j];
+        if (hr < 0) continue;
+        const int64_t r = h.read[hr];
+        if (r < 0) continue;
+        const GChain c = hch[j];
+        const GSeed *sd = hsd + h.sd_off[hr] + c.seed0;
+        const int l = read_len(lens, r, stride);
+        g_load_read(reads, r, stride, l, lane);
+        g_chain_rmax(G, p, l, sd, c.n, lane);
+        const int64_t rmax0 = g_g2.rmax[0], rmax1 = g_g2.rmax[1];
+        GReg *out = res + h.sd_off[hr] + c.seed0;
+        for (int k = 0; k < c.n; ++k) {
+            const GReg a = g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, sd[k], rmax0, rmax1, lane);
+            if (lane == 0) out[k] = a;
         }
         wave_sync();
+    }
+}
+
+// G2, heavy reads: bwa's walk over the kept chains with the jobs' regions, dedup / patch, the
+// read's regions into the pool
+template <int CPL>
+__global__ __launch_bounds__(64, 2) void k_g_heavy(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                   const int32_t *__restrict__ lens, af_params p, GOpt o, GWork w,
+                                                   uint8_t *__restrict__ scr_base, size_t scr_stride,
+                                                   uint8_t *__restrict__ zscratch, size_t zstride) {
+    const int lane = threadIdx.x;
+    const GHeavy &h = w.hv;
+    const int64_t n_heavy = min((int64_t)*(volatile unsigned long long *)&h.cnt[0], h.cap_reads);
+    const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
+    uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
+    const GChain *hch = reinterpret_cast<const GChain *>(h.ch);
+    const GSeed *hsd = reinterpret_cast<const GSeed *>(h.sd);
+    const GReg *res = reinterpret_cast<const GReg *>(h.res);
+    for (;;) {
+        int64_t hr = 0;
+        if (lane == 0) hr = (int64_t)atomicAdd(&h.cnt[4], 1ull);
+        hr = (int64_t)__builtin_amdgcn_readfirstlane((int)hr);
+        if (hr >= n_heavy) break;
+        const int64_t r = h.read[hr];
+        if (r < 0) continue;
+        GPROF(const uint64_t gp_c0 = clock64();)
+        const int nch = h.nch[hr], co = h.ch_off[hr], so = h.sd_off[hr];
+        int nsd = 0;
+        for (int i = lane; i < nch; i += 64) {
+            const GChain c = hch[co + i];
+            S.ch2[i] = c;
+            nsd = max(nsd, c.seed0 + c.n);
+        }
+        nsd = wave_max(nsd);
+        for (int k = lane; k < nsd; k += 64) S.seed[k] = hsd[so + k];
+        wave_sync();
+        const int l = read_len(lens, r, stride);
+        g_load_read(reads, r, stride, l, lane);
+        int nreg = 0;
+        bool ovf = false;
+        for (int ci = 0; ci < nch && !ovf; ++ci)
+            if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane, res + so)) ovf = true;
+        GPROF(const uint64_t gp_c1 = clock64();)
+        if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+        GPROF(if (lane == 0) { int32_t *g = gp_row(r); if (g) { g[6] = (int32_t)(gp_c1 - gp_c0);
+              g[7] = (int32_t)(clock64() - gp_c1); g[12] = nreg; g[13] = nreg; } })
+        g_put_regions(w, S, r, nreg, ovf, lane);
     }
 }
 
@@ -1626,6 +1791,7 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
+    if (t < 5 && w.hv.cnt) w.hv.cnt[t] = 0;
     if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
     if (t < AF_GSTAT_N) w.stats[t] = 0;
     (void)n_reads;
@@ -1664,6 +1830,8 @@ static void gprof_next(hipStream_t s) {
 }
 #endif
 size_t af_g2_slot_bytes() { return g2_slot_bytes(); }
+size_t af_g_chain_bytes() { return sizeof(GChain); }
+size_t af_g_seed_bytes() { return sizeof(GSeed); }
 
 // S4 / S5 up to the regions: G1 + G2 over reads [0, *d_n) (or cap) of a call
 hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, int32_t stride, const int32_t *lens,
@@ -1678,8 +1846,16 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
-#define AF_GO(C) hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap, \
-                                    (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride)
+#define AF_GO(C)                                                                                                       \
+    do {                                                                                                               \
+        hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,       \
+                           (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride);                       \
+        if (w.hv.min_chains > 0) {                                                                                     \
+            hipLaunchKernelGGL((k_g_ext_jobs<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, w);     \
+            hipLaunchKernelGGL((k_g_heavy<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, o, w,      \
+                               g2_scratch, g2_slot_bytes(), zscratch, zstride);                                        \
+        }                                                                                                              \
+    } while (0)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);

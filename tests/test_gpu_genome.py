@@ -183,3 +183,41 @@ def test_pe_se_one_launch_equals_oracle(world):
     for r in range(se.shape[0]):
         msg = _rec_equal(ro5[r], rg[P + r], min(no5[r], 8))
         assert msg is None, ("S5", r, msg)
+
+
+def test_heavy_path_equals_oracle(world, monkeypatch):
+    """G2's heavy-read path (kept chains extended one job per chain, k_g_ext_jobs, then bwa's walk
+    over the jobs' regions, k_g_heavy) forced for every read (AF_G_HEAVY_CHAINS=1, read when the
+    context is made): regions, S5 records and S4 records equal the oracle's."""
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.genome import GenomeIndex
+    contigs, og, _ = world
+    monkeypatch.setenv("AF_G_HEAVY_CHAINS", "1")
+    gh = GenomeIndex(contigs, device=0)
+    try:
+        reads, lens = sample_reads(contigs, 500, seed=41, chimeric=0.4)
+        ro, no = og.regions(reads, lens, max_reg=64, threads=8)
+        rg, ng = gh.regions(reads, lens, max_reg=64)
+        assert np.array_equal(no, ng), np.nonzero(no != ng)[0][:10]
+        for r in range(len(no)):
+            for k in range(min(no[r], 64)):
+                o = ro[r, k]
+                want = (o["rb"], o["re"], o["qb"], o["qe"], o["rid"], o["score"], o["truesc"], o["w"], o["seedcov"],
+                        o["seedlen0"])
+                assert tuple(int(v) for v in want) == tuple(int(v) for v in rg[r, k][:10]), (r, k)
+        so, sno = og.align_se(reads, lens, id_base=3, threads=8)
+        sg, sng = gh.align_se(reads, lens, id_base=3)
+        assert np.array_equal(sno, sng)
+        for r in range(len(sno)):
+            msg = _rec_equal(so[r], sg[r], min(sno[r], 8))
+            assert msg is None, (r, msg)
+        pairs = sample_pairs(contigs, 600, seed=42)
+        plens = np.full(pairs.shape[0], pairs.shape[1], np.int32)
+        po, pno = og.align_pe(pairs, plens, pe=oracle.default_pe(chunk_bases=200_000, pair_base=1), threads=8)
+        pg, png = gh.align_pe(pairs, plens, pe=_lib.default_pe(chunk_bases=200_000, pair_base=1))
+        assert np.array_equal(pno, png)
+        for r in range(len(pno)):
+            msg = _rec_equal(po[r], pg[r], min(pno[r], 8))
+            assert msg is None, (r, msg)
+    finally:
+        gh.close()
