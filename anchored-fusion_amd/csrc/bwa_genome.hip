@@ -817,8 +817,9 @@ __device__ GReg g_seed_region(const DevGenome &G, const af_params &p, int l, con
 }
 
 // mem_chain2aln (oracle mem_chain2aln) for chain ci of S.ch2; regions appended to S.reg.  pre
-// (heavy reads): every seed's region already extended (k_g_ext_jobs), pre[seed0 + i] for the
-// chain's seed i -- the walk below only decides which of them bwa keeps.
+// (heavy reads): the region of the chain's first seed in bwa's order (its longest) already
+// extended by k_g_ext_jobs, at pre[seed0]; the other seeds the walk keeps (few: most lie inside
+// the first one's region) are extended here.
 // Returns false on a region-cap overflow.
 template <int CPL>
 __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params &p, int l, int ci, int *nreg_io,
@@ -826,7 +827,7 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
     G2Lds &E = g_g2;
     const GChain c = S.ch2[ci];
     const GSeed *sd = S.seed + c.seed0;
-    if (!pre) g_chain_rmax(G, p, l, sd, c.n, lane);
+    g_chain_rmax(G, p, l, sd, c.n, lane);
     // srt: seed indices by (score << 32 | i) ascending (keys distinct): rank sort on the wave
     for (int i0 = 0; i0 < c.n; i0 += 64) {
         const int i = i0 + lane;
@@ -889,7 +890,8 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
             }
         }
         if (nreg >= AF_G_MAX_REG) return false;
-        const GReg a = pre ? pre[c.seed0 + (uint32_t)sk] : g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, s, rmax0, rmax1, lane);
+        const GReg a = pre && k == c.n - 1 ? pre[c.seed0]
+                                           : g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, s, rmax0, rmax1, lane);
         if (lane == 0) S.reg[nreg] = a;
         *nreg_io = nreg + 1;
         wave_sync();
@@ -1148,8 +1150,8 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
     }
 }
 
-// G2, heavy reads: one job per pooled chain -- every seed of the chain extended (mem_chain2aln's
-// window and ksw_extend2 both ways), whether or not bwa's walk keeps it; k_g_heavy picks.
+// G2, heavy reads: one job per pooled chain -- the region of the chain's first seed in bwa's walk
+// (the longest; ties: the last), extended whether or not the walk keeps it; k_g_heavy decides.
 template <int CPL>
 __global__ __launch_bounds__(64, 2) void k_g_ext_jobs(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
                                                       const int32_t *__restrict__ lens, af_params p, GWork w) {
@@ -1174,11 +1176,19 @@ __global__ __launch_bounds__(64, 2) void k_g_ext_jobs(DevGenome G, const uint8_t
         g_load_read(reads, r, stride, l, lane);
         g_chain_rmax(G, p, l, sd, c.n, lane);
         const int64_t rmax0 = g_g2.rmax[0], rmax1 = g_g2.rmax[1];
-        GReg *out = res + h.sd_off[hr] + c.seed0;
-        for (int k = 0; k < c.n; ++k) {
-            const GReg a = g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, sd[k], rmax0, rmax1, lane);
-            if (lane == 0) out[k] = a;
+        uint64_t best = 0;  // max of (len << 32 | i): srt's last entry
+        for (int i = lane; i < c.n; i += 64) {
+            const uint64_t ki = (uint64_t)(uint32_t)sd[i].len << 32 | (uint32_t)i;
+            best = ki > best ? ki : best;
         }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t t = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)best, d) |
+                               (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), d) << 32;
+            best = t > best ? t : best;
+        }
+        const GReg a = g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, sd[(uint32_t)best], rmax0, rmax1, lane);
+        if (lane == 0) res[h.sd_off[hr] + c.seed0] = a;
         wave_sync();
     }
 }

@@ -470,8 +470,10 @@ size_t fastq_sync(const std::vector<char> &D, size_t from) {
 }
 
 // records with a header at [start, lim) of D into b.  1 = done, 0 = a record runs past the end
-// of D (read more), -1 = malformed (err set)
-int parse_mem(const std::vector<char> &D, size_t start, size_t lim, bool at_eof, Batch &b, std::string &err) {
+// of D (read more), -1 = malformed (err set).  *multi_line: a record's sequence or quality spans
+// several lines (kseq accepts it; a part boundary cannot be found by the 4-line rule then)
+int parse_mem(const std::vector<char> &D, size_t start, size_t lim, bool at_eof, Batch &b, std::string &err,
+              bool *multi_line) {
     b.clear();
     MemLines L{D.data(), D.size(), start};
     const char *d = D.data();
@@ -492,13 +494,16 @@ int parse_mem(const std::vector<char> &D, size_t start, size_t lim, bool at_eof,
         b.names.insert(b.names.end(), d + s + 1, d + s + 1 + nl);
         b.names.push_back('\0');
         bool plus = false;
+        int seq_lines = 0, qual_lines = 0;
         while (L.next(s, e)) {
             if (e > s && d[s] == '+') { plus = true; break; }
             b.seqs.insert(b.seqs.end(), d + s, d + e);
+            ++seq_lines;
         }
         const size_t slen = b.seqs.size() - seq0;
         size_t ql = 0;
-        while (plus && ql < slen && L.next(s, e)) ql += e - s;
+        while (plus && ql < slen && L.next(s, e)) { ql += e - s; ++qual_lines; }
+        if (seq_lines > 1 || qual_lines > 1) *multi_line = true;
         if (!plus || ql < slen) {
             if (!at_eof) {  // the record continues in the next blocks
                 b.names.resize(name0);
@@ -548,15 +553,30 @@ static int af_fastq_part_read_impl(const char *path, int part, int parts, int th
     for (size_t i = b0; i < b1; ++i) lim += (size_t)blk[i].isize;
     std::vector<char> D;
     int rc = 1;
+    bool multi_line = false;
     for (size_t ra = 8;; ra *= 2) {
         const size_t be = std::min(blk.size(), b1 + ra);
         if (!bgzf_inflate(fp, blk, b0, be, f->threads, D, f->err)) { rc = -1; break; }
         const size_t start = part == 0 ? 0 : fastq_sync(D, 0);
+        // a 4-line FASTQ reaches its first record start within 4 line ends of any byte; more
+        // means records of several lines, which the part rule cannot split
+        int lines = 0;
+        for (const char *q = D.data(), *qe = D.data() + std::min(start, D.size()); lines <= 4 && q < qe; ++lines) {
+            q = static_cast<const char *>(memchr(q, '\n', (size_t)(qe - q)));
+            if (!q) break;
+            ++q;
+        }
+        if (lines > 4) { multi_line = true; rc = 1; break; }
         if (start >= lim) { f->b.clear(); rc = 1; break; }  // no record starts in this part
-        rc = parse_mem(D, start, lim, be == blk.size(), f->b, f->err);
+        rc = parse_mem(D, start, lim, be == blk.size(), f->b, f->err, &multi_line);
         if (rc != 0) break;
     }
     fclose(fp);
+    if (rc >= 0 && multi_line) {
+        f->b.clear();
+        f->err = std::string(path) + ": FASTQ records span several lines; parts need 4-line records (read the file whole)";
+        return AF_E_UNSUPPORTED;
+    }
     if (rc < 0) {
         f->err = std::string(path) + ": " + f->err;
         return AF_E_INVALID;

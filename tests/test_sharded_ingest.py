@@ -20,7 +20,7 @@ from cells_world import write_bgzf
 CHUNK = 20_000  # bases per bwa chunk: the sample spans many chunks
 
 
-def _write_pair(d, n, seed, bgzf=True, ragged=True):
+def _write_pair(d, n, seed, bgzf=True, ragged=True, wrap=0):
     rng = np.random.default_rng(seed)
     recs = [[], []]
     for i in range(n):
@@ -28,6 +28,9 @@ def _write_pair(d, n, seed, bgzf=True, ragged=True):
             L = int(rng.integers(60, 151)) if ragged else 100
             s = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, L)].tobytes().decode()
             q = "".join(chr(c) for c in rng.integers(33, 74, L))  # includes '@' (64) and '+' (43)
+            if wrap:  # sequence and quality wrapped at `wrap` columns (kseq reads them; parts cannot split them)
+                s = "\n".join(s[k:k + wrap] for k in range(0, len(s), wrap))
+                q = "\n".join(q[k:k + wrap] for k in range(0, len(q), wrap))
             recs[m].append(f"@pair{i:07d}/{m + 1} extra\n{s}\n+\n{q}\n")
     paths = []
     with Pool(4) as pool:
@@ -90,10 +93,19 @@ def test_read_part_rejects_plain_gzip(tmp_path):
         afio.read_part(fq1, 0, 2)
 
 
-@pytest.mark.parametrize("world,bgzf", [(2, True), (3, True), (2, False)])
-def test_read_pairs_sharded_gloo(tmp_path, world, bgzf):
+def test_read_part_rejects_wrapped_records(tmp_path):
+    """Multi-line records: every part refuses (NotBGZF -> the whole-file reader), none drops records."""
+    fq1, _ = _write_pair(str(tmp_path), 3000, seed=4, wrap=60)
+    for parts in (1, 3):
+        for p in range(parts):
+            with pytest.raises(afio.NotBGZF):
+                afio.read_part(fq1, p, parts)
+
+
+@pytest.mark.parametrize("world,bgzf,wrap", [(2, True, 0), (3, True, 0), (2, False, 0), (3, True, 60)])
+def test_read_pairs_sharded_gloo(tmp_path, world, bgzf, wrap):
     d = str(tmp_path)
-    fq1, fq2 = _write_pair(d, 4000, seed=3, bgzf=bgzf)
+    fq1, fq2 = _write_pair(d, 4000, seed=3, bgzf=bgzf, wrap=wrap)
     names, reads, lens = afio.read_pairs(fq1, fq2)
     lens = np.full(reads.shape[0], reads.shape[1], np.int32) if lens is None else lens
     grid = set(chunk_ends(lens.astype(np.int64).reshape(-1, 2).sum(axis=1), CHUNK).tolist()) | {0}
