@@ -1152,11 +1152,13 @@ int64_t af_genome_primary(const af_genome *g) { return g ? g->dev.primary : -1; 
 
 int af_genome_read(af_ctx *c, const af_genome *g, int32_t what, int64_t first, int64_t n, void *out) {
     if (!c || !g || !out || first < 0 || n < 0) return fail(c, AF_E_INVALID, "bad argument");
-    const int64_t rows = what == 0 ? g->dev.N : g->dev.N + 1;
-    if (what < 0 || what > 1 || first + n > rows) return fail(c, AF_E_INVALID, "range outside the text / suffix array");
+    const int64_t rows = what == 0 ? g->dev.N : what == 1 ? g->dev.N + 1 : 8 * g->dev.n_blk;
+    if (what < 0 || what > 2 || first + n > rows)
+        return fail(c, AF_E_INVALID, "range outside the text / suffix array / occurrence table");
     (void)hipSetDevice(c->device);
     if (what == 0) HIPCHK(c, hipMemcpy(out, g->dev.T + first, n, hipMemcpyDeviceToHost));
-    else HIPCHK(c, hipMemcpy(out, g->dev.sa + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    else if (what == 1) HIPCHK(c, hipMemcpy(out, g->dev.sa + first, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    else HIPCHK(c, hipMemcpy(out, g->dev.occ + first, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
     return AF_OK;
 }
 

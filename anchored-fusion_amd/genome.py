@@ -129,6 +129,17 @@ class GenomeIndex:
         _lib.check(self.ctx, _lib.lib().af_genome_read(self.ctx, self.g, 1, first, n, out.ctypes.data), "af_genome_read")
         return out
 
+    def occ(self, first_blk=0, n_blk=None):
+        """Occurrence-table blocks [first_blk, first_blk + n_blk) as uint64 [n, 8]: counts of
+        A/C/G/T before the block, then the block's 128 BWT codes at 2 bits (row k of the block at
+        bits 2 (k & 31) of word 4 + (k >> 5)); the '$' row is stored as A and not counted."""
+        total = (2 * self.l_pac + 1 + 127) // 128 + 1  # fmindex.hip: one block past the last row
+        n_blk = total - first_blk if n_blk is None else n_blk
+        out = np.zeros((n_blk, 8), np.uint64)
+        _lib.check(self.ctx, _lib.lib().af_genome_read(self.ctx, self.g, 2, 8 * first_blk, 8 * n_blk, out.ctypes.data),
+                   "af_genome_read")
+        return out
+
     def primary(self):
         return int(_lib.lib().af_genome_primary(self.g))
 

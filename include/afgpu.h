@@ -298,8 +298,10 @@ int af_genome_build_device(af_ctx *ctx, const char *d_blob, int64_t n_blob, cons
 void af_genome_free(af_genome *g);
 int64_t af_genome_lpac(const af_genome *g);
 int64_t af_genome_primary(const af_genome *g);
-/* copies rows [first, first + n) of the bwa text (what = 0, uint8 codes) or of the suffix array
- * (what = 1, int64, rows 0..2 l_pac) to host memory (tests) */
+/* copies rows [first, first + n) of the bwa text (what = 0, uint8 codes), of the suffix array
+ * (what = 1, int64, rows 0..2 l_pac) or words of the occurrence table (what = 2, uint64: per
+ * 128-row block, the A/C/G/T counts before the block then its four 2-bit BWT words; '$' stored as
+ * A and not counted) to host memory (tests) */
 int af_genome_read(af_ctx *ctx, const af_genome *g, int32_t what, int64_t first, int64_t n, void *out);
 /* S5 (single-end): records of reads [0, n) (`stride` bytes per row, d_lens may be NULL) into
  * d_recs[r * AF_G_MAX_REC + k] for k < d_n_rec[r]; read ids id_base + r (bwa's hash tie-breaks),

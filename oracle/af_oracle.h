@@ -100,6 +100,8 @@ afo_genome *afo_genome_build(const char *blob, const int64_t *ctg_off, const int
                              int memset_too);
 void afo_genome_free(afo_genome *G);
 int64_t afo_genome_lpac(const afo_genome *G);
+/* test hook: the SA-IS suffix array equals the prefix-doubling one on T (0), else first differing row + 1 */
+int64_t afo_suffix_array_check(const uint8_t *T, int64_t N);
 const uint8_t *afo_genome_text(const afo_genome *G);   /* the bwa text T, 2 l_pac codes */
 const int64_t *afo_genome_sa(const afo_genome *G);     /* suffix array rows 0..2 l_pac */
 int64_t afo_genome_primary(const afo_genome *G);

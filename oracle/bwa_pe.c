@@ -113,8 +113,9 @@ static int cmp_u64v(const void *a, const void *b) {
 }
 
 /* Suffix array of T (length N) with '$' smallest, by prefix doubling (Manber-Myers with the
- * bucket trick): sa has N + 1 rows, sa[0] = N.  Ranks are group starts among rows 1..N. */
-static int64_t *suffix_array(const uint8_t *T, int64_t N) {
+ * bucket trick): sa has N + 1 rows, sa[0] = N.  Ranks are group starts among rows 1..N.
+ * Used for texts too long for the int32 SA-IS below, and as its cross-check. */
+static int64_t *suffix_array_doubling(const uint8_t *T, int64_t N) {
     int64_t *sa = (int64_t *)malloc(sizeof(int64_t) * (N + 1));
     int64_t *rk = (int64_t *)malloc(sizeof(int64_t) * (N + 1)), *tmp = (int64_t *)malloc(sizeof(int64_t) * (N + 1));
     int64_t *cur = (int64_t *)malloc(sizeof(int64_t) * (N + 1));
@@ -152,6 +153,109 @@ static int64_t *suffix_array(const uint8_t *T, int64_t N) {
     sa[0] = N;
     free(rk); free(tmp); free(cur);
     return sa;
+}
+
+/* SA-IS (Nong, Zhang & Chan 2009: induced sorting of the LMS substrings, recursion on their
+ * names) over int32 symbols s[0, n) in [0, K) whose last symbol is a unique smallest sentinel.
+ * The suffix array is unique, so this equals the doubling construction (and bwa's is.c) row for
+ * row; it is linear, which lets the oracle index tens of Mbp in seconds. */
+#define SAIS_T(i) ((t[(i) >> 3] >> ((i) & 7)) & 1)
+#define SAIS_LMS(i) ((i) > 0 && SAIS_T(i) && !SAIS_T((i) - 1))
+static void sais_buckets(const int32_t *s, int32_t n, int32_t K, int32_t *bkt, int end) {
+    memset(bkt, 0, sizeof(int32_t) * K);
+    for (int32_t i = 0; i < n; ++i) ++bkt[s[i]];
+    int32_t sum = 0;
+    for (int32_t c = 0; c < K; ++c) { sum += bkt[c]; bkt[c] = end ? sum : sum - bkt[c]; }
+}
+static void sais_induce(const uint8_t *t, int32_t *SA, const int32_t *s, int32_t *bkt, int32_t n, int32_t K) {
+    sais_buckets(s, n, K, bkt, 0);  /* L-type suffixes, left to right from the bucket heads */
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t j = SA[i] - 1;
+        if (SA[i] > 0 && !SAIS_T(j)) SA[bkt[s[j]]++] = j;
+    }
+    sais_buckets(s, n, K, bkt, 1);  /* S-type suffixes, right to left from the bucket tails */
+    for (int32_t i = n - 1; i >= 0; --i) {
+        const int32_t j = SA[i] - 1;
+        if (SA[i] > 0 && SAIS_T(j)) SA[--bkt[s[j]]] = j;
+    }
+}
+static void sais(const int32_t *s, int32_t *SA, int32_t n, int32_t K) {
+    uint8_t *t = (uint8_t *)calloc((size_t)n / 8 + 1, 1);
+    int32_t *bkt = (int32_t *)malloc(sizeof(int32_t) * K);
+    /* types: S if s[i] < s[i + 1], or equal and s[i + 1] is S; the sentinel is S */
+    t[(n - 1) >> 3] |= (uint8_t)(1 << ((n - 1) & 7));
+    for (int32_t i = n - 2; i >= 0; --i)
+        if (s[i] < s[i + 1] || (s[i] == s[i + 1] && SAIS_T(i + 1))) t[i >> 3] |= (uint8_t)(1 << (i & 7));
+    /* stage 1: the LMS substrings sorted by one induction */
+    sais_buckets(s, n, K, bkt, 1);
+    for (int32_t i = 0; i < n; ++i) SA[i] = -1;
+    for (int32_t i = 1; i < n; ++i)
+        if (SAIS_LMS(i)) SA[--bkt[s[i]]] = i;
+    sais_induce(t, SA, s, bkt, n, K);
+    int32_t n1 = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (SAIS_LMS(SA[i])) SA[n1++] = SA[i];
+    /* names of the LMS substrings (equal substrings share a name) at SA[n1 + pos / 2] */
+    for (int32_t i = n1; i < n; ++i) SA[i] = -1;
+    int32_t name = 0, prev = -1;
+    for (int32_t i = 0; i < n1; ++i) {
+        const int32_t pos = SA[i];
+        int diff = 0;
+        for (int32_t d = 0; d < n; ++d) {
+            if (prev == -1 || pos + d == n - 1 || prev + d == n - 1 || s[pos + d] != s[prev + d] ||
+                SAIS_T(pos + d) != SAIS_T(prev + d)) { diff = 1; break; }
+            if (d > 0 && (SAIS_LMS(pos + d) || SAIS_LMS(prev + d))) break;
+        }
+        if (diff) { ++name; prev = pos; }
+        SA[n1 + pos / 2] = name - 1;
+    }
+    for (int32_t i = n - 1, j = n - 1; i >= n1; --i)
+        if (SA[i] >= 0) SA[j--] = SA[i];
+    /* stage 2: the reduced string's suffix array (recursion while names repeat) */
+    int32_t *s1 = SA + n - n1, *SA1 = SA;
+    if (name < n1) sais(s1, SA1, n1, name);
+    else for (int32_t i = 0; i < n1; ++i) SA1[s1[i]] = i;
+    /* stage 3: the LMS suffixes in order at their buckets' tails, then one induction */
+    sais_buckets(s, n, K, bkt, 1);
+    for (int32_t i = 1, j = 0; i < n; ++i)
+        if (SAIS_LMS(i)) s1[j++] = i;
+    for (int32_t i = 0; i < n1; ++i) SA1[i] = s1[SA1[i]];
+    for (int32_t i = n1; i < n; ++i) SA[i] = -1;
+    for (int32_t i = n1 - 1; i >= 0; --i) {
+        const int32_t j = SA[i];
+        SA[i] = -1;
+        SA[--bkt[s[j]]] = j;
+    }
+    sais_induce(t, SA, s, bkt, n, K);
+    free(t);
+    free(bkt);
+}
+#undef SAIS_T
+#undef SAIS_LMS
+
+/* Suffix array of T (codes 0..3, length N) with '$' smallest: rows 0..N, sa[0] = N */
+static int64_t *suffix_array(const uint8_t *T, int64_t N) {
+    if (N + 1 >= INT32_MAX || N < 1) return suffix_array_doubling(T, N);
+    const int32_t n = (int32_t)(N + 1);
+    int32_t *s = (int32_t *)malloc(sizeof(int32_t) * n), *SA = (int32_t *)malloc(sizeof(int32_t) * n);
+    for (int32_t i = 0; i < n - 1; ++i) s[i] = T[i] + 1;
+    s[n - 1] = 0;
+    sais(s, SA, n, 5);
+    free(s);
+    int64_t *sa = (int64_t *)malloc(sizeof(int64_t) * (N + 1));
+    for (int32_t i = 0; i < n; ++i) sa[i] = SA[i];
+    free(SA);
+    return sa;
+}
+
+/* test hook: SA-IS and the doubling construction agree on T (0 = equal, else first differing row + 1) */
+int64_t afo_suffix_array_check(const uint8_t *T, int64_t N) {
+    int64_t *a = suffix_array(T, N), *b = suffix_array_doubling(T, N), r = 0;
+    for (int64_t i = 0; i <= N && !r; ++i)
+        if (a[i] != b[i]) r = i + 1;
+    free(a);
+    free(b);
+    return r;
 }
 
 /* FM mode: the BWT of T$ and its occurrence checkpoints (bwt_t: bwt_occ4, primary, L2) */

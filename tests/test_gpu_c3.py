@@ -1,9 +1,11 @@
 """configs[2] on the GPU: the device-made hg38-scale world (simworld) and the device pipeline
 (discover.CandidateDiscovery: S2 + S3 + the S4/S5/S6 genome searches).
 
-At full size (50 M pairs, 3.09 Gbp) the results are checked through properties; the first
-bwa chunks of the same pairs are checked bit-exactly against the CPU oracle (the GPU aligned them
-in the same place of the same input stream, so read ids and insert-size chunks agree)."""
+At full size (50 M pairs, 3.09 Gbp) the results are checked through properties (the bwa index
+by fm_checks on samples, exact reads beyond 2^31 placed on their bases); the first bwa chunks of
+the same pairs are checked bit-exactly against the CPU oracle (the GPU aligned them in the same
+place of the same input stream, so read ids and insert-size chunks agree).  On the 2 % world
+(62 Mbp) the bwa index and every S4 / S5 record equal the oracle's own index and genome calls."""
 import numpy as np
 import pytest
 
@@ -56,6 +58,13 @@ def test_discovery_matches_oracle_reduced(anchor):
     W = _world(anchor, 0.02)
     ref = W.genome_index()
     tiles = W.tiles()
+    # the oracle's bwa index of the same contigs (62 Mbp): text and suffix array row for row
+    contigs = [(nm, W.blob[o:o + ln].cpu().numpy().tobytes()) for nm, o, ln in zip(W.names, W.offsets, W.lens)]
+    og = oracle.OracleGenome(contigs)
+    assert og.l_pac == ref.l_pac and og.primary() == ref.primary()
+    assert np.array_equal(og.text(), ref.text())
+    bad = np.nonzero(og.sa() != ref.sa())[0]
+    assert bad.size == 0, f"{bad.size} suffix-array rows differ, first {bad[:5]}"
     n = 140_000
     reads_t = W.simulate_pairs(n, read_len=150, seed=9)
     d = discover.CandidateDiscovery(anchor, ref, tiles, n, 150, device=0, inflight=3, batch_chunks=1)
@@ -89,9 +98,9 @@ def test_discovery_matches_oracle_reduced(anchor):
     rows = d.q_rows[:nq].cpu().numpy()
     for k, (r, s) in enumerate(want):
         assert rows[k] == r and q[k].tobytes() == s
-    # S4 / S5 records (af_grec) of the device calls == the same engine's host-buffer calls on the
-    # same queries (the engine itself is pinned bit-exact vs oracle/bwa_pe.c by test_gpu_genome.py)
-    _check_genome_records(d, ref, q, nq, c["s4_pairs"])
+    # S4 / S5 records (af_grec) of the device calls == oracle/bwa_pe.c's genome calls (FM mode) on
+    # the same queries and contigs: S4 with the step's chunk grid, S5 with its read ids
+    _check_genome_records_oracle(d, og, q, nq, c["s4_pairs"])
     # S5's genome check and the S6 queries == the host chain over the same records
     _check_s5_s6(d, ref, reads, got, an, c["s4_pairs"], nq)
     summ = d.summary()
@@ -114,6 +123,27 @@ def _check_genome_records(d, ref, q, nq, npair):
     want_r, want_n = np.concatenate([r4, r5]), np.concatenate([n4, n5])
     assert np.array_equal(nrec, want_n)
     assert (nrec >= 1).all()
+    for r in range(nq):
+        for k in range(min(int(nrec[r]), discover.MAX_REC)):
+            a, b = recs[r, k], want_r[r, k]
+            nc = int(a["n_cigar"])
+            assert all(int(a[f]) == int(b[f]) for f in ("flag", "rid", "mrid", "pos", "mpos", "score", "n_cigar",
+                                                         "seq_b", "seq_e")), (r, k)
+            assert np.array_equal(a["cigar"][:nc], b["cigar"][:nc]), (r, k)
+
+
+def _check_genome_records_oracle(d, og, q, nq, npair):
+    from anchored_fusion_amd import discover, genome
+    recs = d.q_recs[:nq * discover.MAX_REC * genome.REC_DTYPE.itemsize].cpu().numpy().view(genome.REC_DTYPE)
+    recs = recs.reshape(nq, discover.MAX_REC)
+    nrec = d.q_nh[:nq].cpu().numpy()
+    lens = d.q_lens[:nq].cpu().numpy()
+    r4, n4 = og.align_pe(q[:2 * npair], lens[:2 * npair], pe=oracle.default_pe(chunk_bases=d.chunk_bases, pair_base=0),
+                         threads=16)
+    r5, n5 = og.align_se(q[2 * npair:nq], lens[2 * npair:nq], id_base=0, threads=16)
+    want_r, want_n = np.concatenate([r4, r5]), np.concatenate([n4, n5])
+    assert np.array_equal(nrec, want_n), np.nonzero(nrec != want_n)[0][:10]
+    assert (nrec >= 1).all() and 2 * npair > 100 and nq - 2 * npair > 100
     for r in range(nq):
         for k in range(min(int(nrec[r]), discover.MAX_REC)):
             a, b = recs[r, k], want_r[r, k]
@@ -153,6 +183,13 @@ def test_c3_full_size(anchor):
     W = _world(anchor, 1.0)
     ref = W.genome_index()
     tiles = W.tiles()
+    # the 3.09 Gbp index by its defining properties on samples (tests/fm_checks.py): occurrence
+    # totals, BWT blocks vs T[SA - 1], LF steps, suffix order over >= 4 kb
+    from fm_checks import check_index
+    summ_ix = check_index(ref.text, ref.sa, ref.occ, ref.l_pac, ref.primary(), seed=3, n_rows=1500, n_blocks=64)
+    print("index checks", summ_ix)
+    assert summ_ix["rows_above_2_31"] > 500 and summ_ix["undecided"] == 0
+    _check_exact_reads_high(W, ref, L=150)
     N, L = 50_000_000, 150
     reads_t = W.simulate_pairs(N, read_len=L, seed=20251015)
     torch.cuda.synchronize()
@@ -195,6 +232,45 @@ def test_c3_full_size(anchor):
     d.close()
     ref.close()
     tiles.close()
+
+
+def _check_exact_reads_high(W, ref, L, n=3000):
+    """Error-free reads cut from the genome beyond 2^31 (forward pac coordinates; their reverse
+    complements too): every one maps with CIGAR L M and score L (S5's call), at a locus whose bases
+    equal the read (a repeat may place it elsewhere with the same score), and most at their origin."""
+    import torch
+    comp = bytes.maketrans(b"ACGT", b"TGCA")
+    rng = np.random.default_rng(11)
+    offs = np.asarray(W.offsets, np.int64)
+    lens = np.asarray(W.lens, np.int64)
+    reads, origin = [], []
+    while len(reads) < n:
+        g = int(rng.integers(1 << 31, int(offs[-1] + lens[-1]) - L))
+        k = int(np.searchsorted(offs, g, side="right") - 1)
+        if g + L > offs[k] + lens[k]:
+            continue
+        s = W.blob[g:g + L].cpu().numpy().tobytes()
+        if b"N" in s:
+            continue
+        rev = len(reads) % 2 == 1
+        reads.append(s[::-1].translate(comp) if rev else s)
+        origin.append((k, g - int(offs[k]), rev))
+    arr = np.frombuffer(b"".join(reads), np.uint8).reshape(n, L)
+    recs, nrec = ref.align_se(arr, np.full(n, L, np.int32))
+    at_origin = 0
+    for i in range(n):
+        r = recs[i, 0]
+        assert (int(r["flag"]) & 4) == 0 and int(r["score"]) == L and int(r["n_cigar"]) == 1, i
+        assert int(r["cigar"][0]) == (L << 4), i
+        k, p = int(r["rid"]), int(r["pos"])
+        g0 = int(offs[k]) + p
+        locus = W.blob[g0:g0 + L].cpu().numpy().tobytes()
+        rev = bool(int(r["flag"]) & 0x10)
+        assert (locus[::-1].translate(comp) if rev else locus) == reads[i], i
+        at_origin += (k, p, rev) == origin[i]
+    print(f"exact reads beyond 2^31: {n} mapped, {at_origin} at their origin")
+    assert at_origin > 0.8 * n
+    torch.cuda.synchronize()
 
 
 def test_discovery_rank_shard_and_exchange(anchor):
