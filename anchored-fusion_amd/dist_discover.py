@@ -256,11 +256,11 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     if names is not None:
         want = np.concatenate([r1.cpu().numpy(), r5[src].cpu().numpy()]) - g0
         mine = {int(r) + g0: names[int(r) // 2] for r in want}
-        if world > 1:
+        if world > 1:  # only rank 0 renders: the names go there alone
             import torch.distributed as dist
-            parts = [None] * world
-            dist.all_gather_object(parts, mine, group=host_group)
-            named = {k: v for p in parts for k, v in p.items()}
+            parts = [None] * world if rank == 0 else None
+            dist.gather_object(mine, parts, dst=0, group=host_group)
+            named = {k: v for p in parts for k, v in p.items()} if rank == 0 else None
         else:
             named = mine
     if rank != 0:

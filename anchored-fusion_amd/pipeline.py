@@ -429,11 +429,16 @@ def _default_aligner(device, chunk_bases):
 
 def gpu_backend(device, chunk_bases=10_000_000, inflight=4, batch_chunks=240):
     """The default per-rank backend of dist_discover: discover.CandidateDiscovery over the rank's
-    reads uploaded to its GPU, with the rank's genome index and tiles (built once per rank)."""
+    reads uploaded to its GPU (once per rank: the upload is kept for every anchor gene), with the
+    rank's genome index and tiles (built once per rank)."""
+    held = {}
+
     def make(anchor, reads, lens, lo, searches, gene):
         from . import blat
         from .discover import CandidateDiscovery
-        reads_t, lens_t, pair_bases = upload_reads(reads, lens, device)
+        if held.get("src") is not reads:
+            held.update(src=reads, up=upload_reads(reads, lens, device))
+        reads_t, lens_t, pair_bases = held["up"]
         d = CandidateDiscovery(anchor.encode(), searches.genome_index(),
                                searches.place.tiles(searches.genome, blat.params("split_tail").step_size),
                                reads_t.shape[0] // 2, reads_t.shape[1], device=device, inflight=inflight,

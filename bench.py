@@ -85,12 +85,15 @@ def pmc_traffic(pairs, read_len):
     return None
 
 
+PROF = os.path.join("profiles", "r04")  # this round's committed rocprofv3 summaries (scripts/summarize_r04.py)
+
+
 def rocprof_k1(bytes_per_launch, n_launch):
     """K1's roofline fraction from the committed rocprofv3 kernel trace of the same command
-    (profiles/r02/kernel_stats_c3.csv: average k_seed_stream duration over every launch of the
+    (profiles/r04/kernel_stats_c3.csv: average k_seed_stream duration over every launch of the
     traced steps, the same mix of full and remainder batches), beside the live HIP-event figure."""
     import csv
-    path = os.path.join(ROOT, "profiles", "r02", "kernel_stats_c3.csv")
+    path = os.path.join(ROOT, PROF, "kernel_stats_c3.csv")
     try:
         for r in csv.DictReader(open(path)):
             if "k_seed_stream" in r["Name"]:
@@ -98,7 +101,7 @@ def rocprof_k1(bytes_per_launch, n_launch):
                 if calls % max(1, n_launch):
                     return None  # a different batch shape
                 gbs = bytes_per_launch / avg_ns
-                return {"source": "profiles/r02/kernel_stats_c3.csv", "launches": calls,
+                return {"source": f"{PROF}/kernel_stats_c3.csv", "launches": calls,
                         "avg_us": round(avg_ns / 1e3, 1), "achieved": round(gbs, 1),
                         "frac": round(gbs / HBM_PEAK_GBS, 4)}
     except (OSError, KeyError, ValueError):
@@ -107,15 +110,18 @@ def rocprof_k1(bytes_per_launch, n_launch):
 
 
 def issue_roofline():
-    """The compute-bound kernels of the C3 step against their VALU issue roofline, from the
-    committed counter pass (profiles/r02/pmc_valu_c3.json; one batch in flight), or None."""
+    """The step's compute / latency-bound kernels against their VALU issue roofline and HBM
+    traffic, from this round's committed counter passes of the same command (profiles/r04/
+    pmc_c3.json: SQ issue / wait counters and FETCH_SIZE per launch), or None."""
     try:
-        pm = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_valu_c3.json")))
+        pm = json.load(open(os.path.join(ROOT, PROF, "pmc_c3.json")))
     except (OSError, ValueError):
         return None
-    return {"source": "profiles/r02/pmc_valu_c3.json", "model": pm.get("issue_model"),
-            "kernels": {k: {f: e[f] for f in ("avg_duration_us", "unit", "valu_per_unit", "issue_frac", "wait_any_frac")}
-                        for k, e in pm.get("kernels", {}).items()}}
+    keep = ("avg_duration_us", "unit", "valu_issue_frac", "wait_any_frac", "avg_resident_waves_per_simd",
+            "fetch_gbs_x2", "fetch_bytes_per_unit_x2")
+    return {"source": f"{PROF}/pmc_c3.json", "model": pm.get("issue_model"),
+            "kernels": {k: {f: e[f] for f in keep if f in e} for k, e in pm.get("kernels", {}).items()
+                        if any(k.startswith(p) for p in ("k_g_", "k_blat", "k_s2_", "k_s5"))}}
 
 
 def cpu_threads(args):
@@ -443,6 +449,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
             "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
                     "genome_bwa_s4_s5 = S5, its genome check, then S4 on slot 0 beside the S6 BLAT "
                     "of S5's survivors on slot 1's stream, joined at its end"},
+        "genome_phase": None if world > 1 else genome_phase(summ, phase(3, 4)),
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
             "kernel": "k_seed_filter", "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -466,6 +473,25 @@ def bench_c3(args, world, rank, gpu, dev, backend):
     disc.close()
     ref.close()
     tiles.close()
+
+
+def genome_phase(summ, ms):
+    """The genome phase's rates: bwa-mem genome reads (S4's both ends + S5's split reads, one
+    seed / region launch) and BLAT queries (S6) over the phase's wall time, and the HBM bytes per
+    genome read of its kernels from the committed FETCH_SIZE pass (profiles/r04/pmc_c3.json)."""
+    q, n6 = summ.get("queries_s4_s5", 0), summ.get("s6_queries", 0)
+    out = {"ms": round(ms, 3), "bwa_genome_reads": q, "blat_queries": n6,
+           "bwa_genome_reads_per_s": round(q / (ms * 1e-3), 1) if ms else None,
+           "blat_queries_per_s": round(n6 / (ms * 1e-3), 1) if ms else None}
+    try:
+        pm = json.load(open(os.path.join(ROOT, PROF, "pmc_c3.json")))["kernels"]
+        per = {k: e["fetch_bytes_per_unit_x2"] for k, e in pm.items() if "fetch_bytes_per_unit_x2" in e}
+        if per:
+            out["fetch_bytes_per_unit_x2"] = per
+            out["fetch_source"] = f"{PROF}/pmc_c3.json"
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def genome_subset(W, flank=250_000):
@@ -580,8 +606,22 @@ def cpu_baseline_c3(anchor, reads_t, args, subset):
         dt += t6 - t0
         passes += 1
         counts = dict(s4_pairs=len(s4) // 2, s5_split_reads=len(fasta), s6_queries=len(s6q))
+    s2s3 = st["s2_s3"] + st["gather"]
+    gen = st["s4"] + st["s5"] + st["s5_check"] + st["s6"]
     return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
             "host_cpus_visible": os.cpu_count(),
+            "cores_note": f"{threads} OpenMP threads = the GPU's host CPU share (OMP_NUM_THREADS); "
+                          f"host_cpus_visible = the whole machine",
+            "legs": {
+                "s2_s3": {"pairs_per_s": round(n * passes / s2s3, 1), "s_per_pass": round(s2s3 / passes, 3),
+                          "comparable": True,
+                          "note": "S2 + S3 + the query gathers: the same pairs and anchor as the GPU step"},
+                "genome": {"s_per_pass": round(gen / passes, 3), "comparable": False,
+                           "queries_per_s": round(passes * (counts.get("s4_pairs", 0) * 2 + counts.get("s5_split_reads", 0)
+                                                            + counts.get("s6_queries", 0)) / gen, 1) if gen else None,
+                           "note": f"S4/S5 bwa-mem + S5 check + S6 BLAT on the gene loci +- 250 kb only "
+                                   f"({sum(len(q) for _, q in subset) / 1e6:.1f} Mbp, not the GPU's 3.09 Gbp: far "
+                                   f"fewer repeat occurrences per seed, so not a like-for-like rate)"}},
             "stages_s_per_pass": {k: round(v / passes, 3) for k, v in st.items()},
             "queries_per_pass": counts,
             "sample": f"first {n} pairs of the batch x {passes} passes ({dt:.1f} s): S2 + S3 + gathers + S4/S5 "

@@ -1,0 +1,114 @@
+"""Turns a profile_r04.sh output directory (gpurun_out/<tag>: kt/ kernel trace + stats, sq/ and
+fetch/ counter passes of the configs[2] bench) into the committed round-4 profile summaries:
+
+  profiles/r04/kernel_stats_c3.csv   rocprofv3 --stats of the traced bench (3 timed + 1 warm-up steps)
+  profiles/r04/pmc_c3.json           per kernel of the step: launches, average duration (trace),
+                                     VALU issue / wait / active fractions, resident waves, HBM
+                                     FETCH_SIZE per launch (gfx950: x2 for wide reads), per unit
+  profiles/r04/pmc_c3.md             the same as a table
+
+usage: python3 scripts/summarize_r04.py gpurun_out/<tag> profiles/r04 [bench_line.json]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+CLOCK_GHZ = 2.4   # MI355X_MICROARCH.md: peak engine clock
+N_SIMD = 1024     # 256 CUs x 4 SIMDs
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0][:60]
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    os.makedirs(out, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    shutil.copy(stats[0], os.path.join(out, "kernel_stats_c3.csv"))
+    dur = {}
+    for r in csv.DictReader(open(stats[0])):
+        k = short(r["Name"])
+        c, t = dur.get(k, (0, 0.0))
+        dur[k] = (c + int(r["Calls"]), t + float(r["TotalDurationNs"]))
+
+    def counters(sub):
+        acc = collections.defaultdict(float)
+        disp = collections.defaultdict(set)
+        for f in glob.glob(os.path.join(src, sub, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                k = short(r["Kernel_Name"])
+                acc[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+                disp[k].add(r["Dispatch_Id"])
+        return {k: v / len(disp[k[0]]) for k, v in acc.items()}, {k: len(v) for k, v in disp.items()}
+
+    sq, nd = counters("sq")
+    fe, _ = counters("fetch")
+    bench = {}
+    if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):
+        bench = json.load(open(sys.argv[3]))
+    counts = bench.get("counts_per_step", {})
+    units = {  # units per launch of the step's kernels (bench counts per step)
+        "k_g_seeds": ("genome reads (S4 + S5)", counts.get("queries_s4_s5")),
+        "k_g_regions": ("genome reads (S4 + S5)", counts.get("queries_s4_s5")),
+        "k_g_se": ("S5 split reads", counts.get("s5_split_reads")),
+        "k_g_pe": ("S4 pairs", counts.get("s4_pairs")),
+        "k_blat": ("S6 query strands", 2 * counts["s6_queries"] if counts.get("s6_queries") else None),
+    }
+    kern = {}
+    for k in sorted(nd):
+        g = lambda c: sq.get((k, c), 0.0)  # noqa: E731
+        calls, tot = dur.get(k, (0, 0.0))
+        avg_us = tot / calls / 1e3 if calls else None
+        e = {"launches_counted": nd[k], "avg_duration_us": round(avg_us, 1) if avg_us else None}
+        wc = g("SQ_WAVE_CYCLES")
+        if wc:
+            e["wait_any_frac"] = round(g("SQ_WAIT_ANY") / wc, 3)
+            e["wait_inst_any_frac"] = round(g("SQ_WAIT_INST_ANY") / wc, 3)
+            e["active_inst_frac"] = round(g("SQ_ACTIVE_INST_ANY") / wc, 3)
+        if g("SQ_WAVES"):
+            e["waves"] = int(g("SQ_WAVES"))
+        if avg_us and g("SQ_INSTS_VALU"):
+            e["valu_per_launch"] = round(g("SQ_INSTS_VALU"))
+            e["valu_issue_frac"] = round(g("SQ_INSTS_VALU") * 2 / (avg_us * 1e3 * CLOCK_GHZ * N_SIMD), 4)
+        if avg_us and g("SQ_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
+            e["sq_busy_frac"] = round(g("SQ_BUSY_CYCLES") / g("GRBM_GUI_ACTIVE"), 3)
+        if avg_us and wc:
+            # resident waves averaged over the launch: wave-cycles / (duration x clock)
+            e["avg_resident_waves_per_simd"] = round(wc / (avg_us * 1e3 * CLOCK_GHZ) / N_SIMD, 2)
+        fs = fe.get((k, "FETCH_SIZE"))
+        if fs is not None:
+            e["fetch_bytes_per_launch_x2"] = round(fs * 1024 * 2)
+            if avg_us:
+                e["fetch_gbs_x2"] = round(fs * 1024 * 2 / (avg_us * 1e3), 1)
+        for key, (uname, n) in units.items():
+            if k.startswith(key) and n:
+                e["unit"] = uname
+                e["units_per_step"] = n
+                if e.get("fetch_bytes_per_launch_x2") and calls:
+                    e["fetch_bytes_per_unit_x2"] = round(e["fetch_bytes_per_launch_x2"] / n, 1)
+        kern[k] = e
+    res = {"source": f"rocprofv3 --kernel-trace --stats, then --pmc passes (SQ; FETCH_SIZE) of "
+                     f"python3 bench.py --no-cpu (configs[2], one GPU); {src}",
+           "issue_model": "a wave64 VALU instruction issues over 2 cycles on a SIMD (MI355X_MICROARCH.md): "
+                          "valu_issue_frac = SQ_INSTS_VALU x 2 / (avg duration x 2.4 GHz x 1024 SIMDs)",
+           "fetch_note": "FETCH_SIZE (KiB) x 1024 x 2: the gfx950 correction for wide coalesced reads; other "
+                         "access widths are uncalibrated (MI355X_MICROARCH.md, HBM)",
+           "kernels": kern}
+    json.dump(res, open(os.path.join(out, "pmc_c3.json"), "w"), indent=1)
+    cols = ["avg_duration_us", "launches_counted", "valu_issue_frac", "wait_any_frac", "active_inst_frac",
+            "avg_resident_waves_per_simd", "fetch_gbs_x2", "fetch_bytes_per_unit_x2"]
+    lines = ["| kernel | " + " | ".join(cols) + " |", "|---" * (len(cols) + 1) + "|"]
+    for k, e in kern.items():
+        lines.append(f"| {k} | " + " | ".join(str(e.get(c, "")) for c in cols) + " |")
+    open(os.path.join(out, "pmc_c3.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
