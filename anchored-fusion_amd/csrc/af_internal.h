@@ -36,10 +36,13 @@ struct DevIndex {
 };
 
 // BLAT tile index (blat.hip): target codes, every step-th 11-mer's positions grouped by key
-// (start[key] .. start[key + 1]) ascending, N counts before each 4096-base block
+// (start[key] .. start[key + 1]) ascending; the target's N bases as one bit per base (nmask, 64
+// bases per word) and N counts before each 64-base block (ncum): any N count in O(1)
 struct DevTile {
     const uint8_t *T;
     const uint32_t *start, *pos, *ncum;
+    const uint64_t *nmask;
+    const uint32_t *nnext;  // per 64-base block: the first N at or after its start (0xFFFFFFFF: none)
     int64_t n;
     int32_t step;
 };
@@ -307,7 +310,7 @@ hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t 
                             int64_t cap, uint8_t *q, int32_t *q_lens, int32_t *q_rows, int32_t *n_q, int32_t *sel,
                             int64_t *sel_n, void *temp, size_t temp_bytes, hipStream_t s);
 // k_blat's per-wave global scratch (blat.hip layout) and its resident waves on n_cu CUs
-constexpr size_t AF_BLAT_SLOT_BYTES = 704 << 10;
+constexpr size_t AF_BLAT_SLOT_BYTES = 2088 << 10;  // blat.hip SC_END
 int af_blat_slots(int n_cu);
 hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
                           int64_t cap,

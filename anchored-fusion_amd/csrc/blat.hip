@@ -42,11 +42,13 @@ namespace {
 
 constexpr int TILE = AF_TILE;
 constexpr uint32_t NKEYS = 1u << (2 * TILE);
-constexpr int NMAX = 32768, MAXCL = 4096, MAXR = 16, MAXROWS = 4 * MAXR, NBLK_SHIFT = 12;
-// per-slot scratch layout (bytes; the traceback of gen_cigar uses the first 64 KB)
-constexpr size_t SC_KEYS_A = 64 << 10, SC_KEYS_B = SC_KEYS_A + NMAX * 8, SC_CLUMP = SC_KEYS_B + NMAX * 8,
-                 SC_REGS = SC_CLUMP + MAXCL * 24, SC_ROWS = SC_REGS + (8 << 10), SC_END = SC_ROWS + (24 << 10);
-static_assert(SC_END == AF_BLAT_SLOT_BYTES, "BLAT slot layout");
+// parts per query strand: one per clump at most, so MAXP adds no cap of its own (BLAT aligns every
+// clump whose seed lies in no earlier alignment)
+constexpr int NMAX = 32768, MAXCL = 4096, MAXP = MAXCL;
+// stitching work per query strand (predecessor candidates the chain DP rescans after a chain is
+// emitted; the first pass over every part is always made): once past it,
+// no further chain is emitted and the strand is counted in AF_BLAT_CAP_PARTS (oracle/blat.c: the same)
+constexpr int64_t STITCH_WORK = 1 << 24;
 
 struct Clump { int64_t diag, t; int32_t cnt, q; };
 struct Reg {
@@ -55,13 +57,21 @@ struct Reg {
     int32_t bsz[AF_PSL_MAX_BLOCKS], bq[AF_PSL_MAX_BLOCKS];
     int64_t bt[AF_PSL_MAX_BLOCKS];
 };
+static_assert(sizeof(Reg) == 320, "Reg layout");
+// per-slot scratch layout (bytes; the traceback of gen_cigar uses the first 64 KB): hit keys (two
+// buffers), clumps, parts, the chain DP's per-part words (sorted order, best, predecessor, flags,
+// chain), the strand's rows
+constexpr size_t SC_KEYS_A = 64 << 10, SC_KEYS_B = SC_KEYS_A + NMAX * 8, SC_CLUMP = SC_KEYS_B + NMAX * 8,
+                 SC_REGS = SC_CLUMP + MAXCL * 24, SC_DP = SC_REGS + (size_t)MAXP * sizeof(Reg),
+                 SC_ROWS = SC_DP + 8 * 4 * (size_t)MAXP, SC_END = SC_ROWS + (8 << 10);
+static_assert(SC_END == AF_BLAT_SLOT_BYTES, "BLAT slot layout");
+static_assert(AF_BLAT_MAX_ROWS * sizeof(af_psl) <= (8 << 10), "BLAT rows scratch");
 
 struct __attribute__((aligned(16))) BlatLds {
     uint32_t hist[AF_MAX_READ];    // radix digit counts (256) / per offset: first position index - first hit index
     uint8_t q0[AF_MAX_READ + 16];  // the query's codes (strand 0)
     int32_t base[AF_MAX_READ + 1];  // first hit index per query offset (exclusive scan of the counts)
     int32_t nh, ncl, nr, nrow, tmp[8];
-    int32_t order[MAXR], best[MAXR], prev[MAXR], chain[MAXR];
 };
 __shared__ BlatLds g_bl;
 
@@ -205,20 +215,6 @@ __device__ uint64_t *wave_radix_sort(uint64_t *a, uint64_t *b, int n, int lo, in
     return a;
 }
 
-// N bases in T[a, b), on the wave (the oracle's n_in)
-__device__ int64_t n_in(const DevTile &X, int64_t a, int64_t b, int lane) {
-    if (b <= a) return 0;
-    const int64_t ba = a >> NBLK_SHIFT, bb = b >> NBLK_SHIFT;
-    int c = 0;
-    if (ba == bb) {
-        for (int64_t i = a + lane; i < b; i += 64) c += X.T[i] > 3;
-        return wave_sum(c);
-    }
-    for (int64_t i = a + lane; i < ((ba + 1) << NBLK_SHIFT); i += 64) c += X.T[i] > 3;
-    for (int64_t i = (bb << NBLK_SHIFT) + lane; i < b; i += 64) c += X.T[i] > 3;
-    return (int64_t)wave_sum(c) + (int64_t)(X.ncum[bb] - X.ncum[ba + 1]);
-}
-
 // r without its first k aligned bases (lane 0; 0 if k does not fit the first block)
 __device__ bool trim_front(const DevTile &X, const uint8_t *Q, const Reg &r, int k, Reg &o) {
     o = r;
@@ -347,6 +343,82 @@ __device__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, u
     return g_bl.tmp[0] != 0;
 }
 
+// The chain DP's per-part words (parts in (qb, tb, qe) order, position k): ORD[k] = the part's
+// index in RG, BEST / PREV its chain score and predecessor, FL bit 0 = used by an emitted chain,
+// bit 1 = recomputed in this pass, CH the chain being emitted
+struct ChainDp {
+    int32_t *ORD, *BEST, *PREV, *FL, *CH;
+    int32_t *QE;    // the part's qe, -1 once used (one load tells both)
+    uint32_t *TE;   // its te
+    uint32_t *NXT;  // the first N of the target at or after te (no N: 0xFFFFFFFF)
+};
+
+// the first N of the target at or after p (the oracle's n_in(p, b) == 0 <=> first_n(p) >= b)
+__device__ __forceinline__ uint32_t first_n(const DevTile &X, int64_t p) {
+    const int64_t b = p >> 6;
+    const uint64_t m = X.nmask[b] >> (p & 63);
+    return m ? (uint32_t)(p + __builtin_ctzll(m)) : X.nnext[b + 1];
+}
+
+// best[i] / prev[i] over the unused parts j < i (oracle/blat.c chain_node, the literal rule): a
+// predecessor must end before i on both sequences, leave part of i's first block after the
+// overlap trim, lie within max_intron on the target with no N in between; the first j with the
+// highest best[j] + trimmed score - gap flags wins over i alone.  Lanes over j on the parts'
+// sorted per-part words (coalesced; four 64-part chunks per pass); the trimmed score from a
+// prefix sum of i's first block (PRE, LDS), the N test against the part's first N after te.
+__device__ void chain_node(const DevTile &X, const Reg *RG, const ChainDp &C, int i, int64_t max_intron, int lane) {
+    const Reg &ri = RG[C.ORD[i]];
+    const uint8_t *Q = g_dp.q;
+    int32_t *PRE = reinterpret_cast<int32_t *>(g_bl.hist);  // PRE[k] = score of the block's first k bases, k < bsz[0]
+    const int b0 = ri.bsz[0] < AF_MAX_READ ? ri.bsz[0] : AF_MAX_READ;
+    int carry = 0;
+    for (int u0 = 0; u0 < b0; u0 += 64) {
+        const int u = u0 + lane;
+        int m = 0;
+        if (u < b0) {
+            const uint8_t x = Q[ri.bq[0] + u], y = X.T[ri.bt[0] + u];
+            m = (x > 3 || y > 3) ? 0 : (x == y ? 1 : -1);
+        }
+        const int inc = wave_incl_sum(m, lane);
+        if (u < b0) PRE[u] = carry + inc - m;
+        carry += __builtin_amdgcn_readlane(inc, 63);
+    }
+    wave_sync();
+    const int iqb = ri.qb, iqe = ri.qe, isc = ri.score, ib0 = ri.bsz[0];
+    const int64_t itb = ri.tb, ite = ri.te;
+    int best = isc, prev = -1;
+    for (int j0 = 0; j0 < i; j0 += 256) {
+        int sc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = j0 + 64 * c + lane;
+            int v = INT_MIN;
+            if (j < i) {
+                const int aqe = C.QE[j];
+                const int64_t ate = C.TE[j];
+                const int64_t nx = C.NXT[j];
+                const int bj = C.BEST[j];
+                if (aqe >= 0 && iqe > aqe && ite > ate) {
+                    int64_t kk = aqe - iqb;
+                    if (ate - itb > kk) kk = ate - itb;
+                    const int k = kk > 0 ? (int)kk : 0;
+                    const int64_t btb = itb + k;
+                    if (!(k > 0 && k >= ib0) && btb - ate <= max_intron && nx >= btb)
+                        v = bj + (isc - (k > 0 ? PRE[k] : 0)) - (iqb + k > aqe) - (btb > ate);
+                }
+            }
+            sc[c] = v;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int mx = wave_max(sc[c]);
+            if (mx > best) { best = mx; prev = j0 + 64 * c + (int)__builtin_ctzll(__ballot(sc[c] == mx)); }
+        }
+    }
+    if (lane == 0) { C.BEST[i] = best; C.PREV[i] = prev; }
+    wave_sync();
+}
+
 template <int CPL>
 __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
                                                         int32_t stride, const int32_t *__restrict__ lens,
@@ -368,6 +440,9 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
     Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
     Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
     af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
+    int32_t *dpw = reinterpret_cast<int32_t *>(zg + SC_DP);
+    const ChainDp CD{dpw, dpw + MAXP, dpw + 2 * MAXP, dpw + 3 * MAXP, dpw + 4 * MAXP, dpw + 5 * MAXP,
+                     reinterpret_cast<uint32_t *>(dpw + 6 * MAXP), reinterpret_cast<uint32_t *>(dpw + 7 * MAXP)};
     // work items are (query, strand): item 2k + s is strand s of the k-th query (of the cost order
     // when given: heaviest first), so a heavy query's strands run on two waves at once
     const int64_t i0 = 2 * (int64_t)q0, i1 = 2 * (int64_t)nq;
@@ -534,85 +609,106 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             const uint64_t *CO = wave_radix_sort(KA, KB, ncl, 32, 2, lane);
             BPM(2);
             BP(cc_ += ncl;)
-            // ---- parts: one per clump whose seed lies in no earlier part -------------------------
+            // ---- parts: one per clump whose seed lies in no earlier part (lanes over the parts) ----
             int nr = 0, c = 0;
-            for (; c < ncl && nr < MAXR; ++c) {
+            for (; c < ncl && nr < MAXP; ++c) {
                 const Clump cc = CL[(uint32_t)CO[c]];
-                bool skip = false;
-                for (int r = 0; r < nr && !skip; ++r) {
-                    const Reg &g = RG[r];
-                    skip = g.qb <= cc.q && cc.q + TILE <= g.qe && g.tb <= cc.t && cc.t + TILE <= g.te;
+                bool inside = false;
+                for (int r0 = 0; r0 < nr && !inside; r0 += 64) {
+                    const int r = r0 + lane;
+                    bool in = false;
+                    if (r < nr) {
+                        const Reg &g = RG[r];
+                        in = g.qb <= cc.q && cc.q + TILE <= g.qe && g.tb <= cc.t && cc.t + TILE <= g.te;
+                    }
+                    inside = __ballot(in) != 0;
                 }
-                if (skip) continue;
+                if (inside) continue;
                 if (align_clump<CPL>(X, L, cc.q, cc.t, RG[nr], zg, lane)) ++nr;
                 __threadfence_block();
                 wave_sync();
             }
-            if (lane == 0 && caps && nr == MAXR && c < ncl) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
+            if (lane == 0 && caps && nr == MAXP && c < ncl) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
             if (nr == 0) continue;
             BPM(3);
             BP(cr += nr;)
-            // ---- parts in (qb, tb, qe) order, then chains, best first -----------------------------
-            if (lane == 0) {
-                for (int i = 1; i < nr; ++i)
-                    for (int j = i; j > 0; --j) {
-                        const Reg &a = RG[j - 1], &b = RG[j];
-                        const bool gt = a.qb > b.qb || (a.qb == b.qb && (a.tb > b.tb || (a.tb == b.tb && a.qe > b.qe)));
-                        if (!gt) break;
-                        const Reg tmp = RG[j - 1];
-                        RG[j - 1] = RG[j];
-                        RG[j] = tmp;
+            // ---- parts in (qb, tb, qe) order, ties in creation order: ORD ----------------------
+            {
+                const auto key = [&](int r) {
+                    const Reg &g = RG[r];
+                    return ((uint64_t)g.qb << 54) | ((uint64_t)g.tb << 21) | ((uint64_t)g.qe << 12) | (uint64_t)r;
+                };
+                if (nr <= 64) {
+                    if (lane < nr) {
+                        const uint64_t k = key(lane);
+                        int rank = 0;
+                        for (int r = 0; r < nr; ++r) rank += key(r) < k;
+                        CD.ORD[rank] = lane;
                     }
-                for (int i = 0; i < nr; ++i) RG[i].used = 0;
-            }
-            __threadfence_block();
-            wave_sync();
-            for (;;) {
-                int bi = -1;
-                for (int i = 0; i < nr; ++i) {
-                    if (RG[i].used) continue;
-                    int best = RG[i].score, prev = -1;
-                    for (int j = 0; j < i; ++j) {
-                        if (RG[j].used) continue;
-                        const Reg &a = RG[j], &ri = RG[i];
-                        if (ri.qe <= a.qe || ri.te <= a.te) continue;
-                        const int k = chain_trim(a, ri);
-                        if (k > 0 && k >= ri.bsz[0]) continue;
-                        // the trimmed part's start and score (trim_front, uniform on every lane)
-                        int dsc = 0;
-                        for (int u = 0; u < k; ++u) {
-                            const uint8_t x = D.q[ri.bq[0] + u], y = X.T[ri.bt[0] + u];
-                            dsc += (x > 3 || y > 3) ? 0 : (x == y ? 1 : -1);
-                        }
-                        const int bqb = ri.qb + k;
-                        const int64_t btb = ri.tb + k;
-                        if (btb - a.te > bp.max_intron) continue;
-                        if (n_in(X, a.te, btb, lane)) continue;
-                        const int s = B.best[j] + (ri.score - dsc) - (bqb > a.qe) - (btb > a.te);
-                        if (s > best) { best = s; prev = j; }
-                    }
-                    if (lane == 0) { B.best[i] = best; B.prev[i] = prev; }
+                } else {
+                    for (int r = lane; r < nr; r += 64) KA[r] = key(r);
+                    __threadfence_block();
                     wave_sync();
-                    if (bi < 0 || best > B.best[bi]) bi = i;
+                    const uint64_t *SK = wave_radix_sort(KA, KB, nr, 12, 7, lane);
+                    for (int r = lane; r < nr; r += 64) CD.ORD[r] = (int32_t)(SK[r] & 4095u);
+                }
+                __threadfence_block();
+                wave_sync();
+                for (int r = lane; r < nr; r += 64) {
+                    const Reg &g = RG[CD.ORD[r]];
+                    CD.FL[r] = 0;
+                    CD.QE[r] = g.qe;
+                    CD.TE[r] = (uint32_t)g.te;
+                    CD.NXT[r] = first_n(X, g.te);
+                }
+                __threadfence_block();
+                wave_sync();
+            }
+            // ---- chains, best first (oracle/blat.c: each round takes the unused part with the
+            // highest chain score, first in order on ties; only the parts whose predecessor path
+            // met a used part are recomputed, the others keep their exact value) ----------------
+            int64_t work = 0;  // the recomputations' candidates (the first pass is always made)
+            for (int i = 0; i < nr; ++i) {
+                chain_node(X, RG, CD, i, bp.max_intron, lane);
+                __threadfence_block();
+                wave_sync();
+            }
+            for (;;) {
+                if (work > STITCH_WORK) {
+                    if (lane == 0 && caps) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
+                    break;
+                }
+                // the unused part with the highest chain score, the first on ties
+                int bv = INT_MIN, bi = -1;
+                for (int i0 = 0; i0 < nr; i0 += 64) {
+                    const int i = i0 + lane;
+                    const bool free_ = i < nr && !(CD.FL[i] & 1);
+                    if (!__ballot(free_)) continue;
+                    const int v = free_ ? CD.BEST[i] : INT_MIN;
+                    const int mx = wave_max(v);
+                    if (bi < 0 || mx > bv) { bv = mx; bi = i0 + (int)__builtin_ctzll(__ballot(free_ && v == mx)); }
                 }
                 if (bi < 0) break;
+                int first = bi;
                 if (lane == 0) {
                     int m = 0;
-                    for (int i = bi; i >= 0; i = B.prev[i]) B.chain[m++] = i;
+                    for (int i = bi; i >= 0; i = CD.PREV[i]) CD.CH[m++] = i;
+                    first = CD.CH[m - 1];
                     af_psl o{};
                     o.query = (int32_t)qi; o.strand = strand; o.q_size = L;
                     bool ok = true;
-                    Reg part[2];  // the previous part (trimmed) and the current one
-                    Reg first{}, last{};
+                    Reg prevp{}, firstp{}, lastp{};
                     for (int c = m - 1; c >= 0; --c) {
-                        RG[B.chain[c]].used = 1;
+                        const int k = CD.CH[c];
+                        CD.FL[k] |= 1;
+                        CD.QE[k] = -1;
+                        const Reg &src = RG[CD.ORD[k]];
                         Reg cur;
-                        if (c == m - 1) cur = RG[B.chain[c]];
-                        else trim_front(X, D.q, RG[B.chain[c]], chain_trim(part[0], RG[B.chain[c]]), cur);
+                        if (c == m - 1) cur = src;
+                        else trim_front(X, D.q, src, chain_trim(prevp, src), cur);
                         if (c < m - 1) {
-                            const Reg &a = part[0];
-                            if (cur.qb > a.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - a.qe; }
-                            if (cur.tb > a.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - a.te); }
+                            if (cur.qb > prevp.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - prevp.qe; }
+                            if (cur.tb > prevp.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - prevp.te); }
                         }
                         o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
                         o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi;
@@ -622,18 +718,56 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                             o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
                             o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
                         }
-                        if (c == m - 1) first = cur;
-                        if (c == 0) last = cur;
-                        part[0] = cur;
+                        if (c == m - 1) firstp = cur;
+                        if (c == 0) lastp = cur;
+                        prevp = cur;
                     }
-                    o.q_start = strand ? L - last.qe : first.qb;
-                    o.q_end = strand ? L - first.qb : last.qe;
-                    o.t_start = first.tb; o.t_end = last.te;
+                    o.q_start = strand ? L - lastp.qe : firstp.qb;
+                    o.q_end = strand ? L - firstp.qb : lastp.qe;
+                    o.t_start = firstp.tb; o.t_end = lastp.te;
                     o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
-                    if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10 &&
-                        B.nrow < MAXROWS)
-                        RW[B.nrow++] = o;
+                    if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10) {
+                        // the strand's best max_rows rows in psl_before order (stable), all counted
+                        const int n = B.nrow < max_rows ? B.nrow : max_rows;
+                        int at = n;
+                        while (at > 0 && psl_before(o, RW[at - 1])) --at;
+                        if (at < max_rows) {
+                            for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) RW[x] = RW[x - 1];
+                            RW[at] = o;
+                        }
+                        ++B.nrow;
+                    }
                 }
+                first = __builtin_amdgcn_readfirstlane(first);
+                __threadfence_block();
+                wave_sync();
+                // parts after the chain's first whose predecessor path meets a used or recomputed
+                // part: recomputed in order (a recomputed part marks its successors in turn)
+                for (int i0 = first + 1 - ((first + 1) & 63); i0 < nr; i0 += 64) {
+                    const int i = i0 + lane;
+                    bool live = i > first && i < nr && !(CD.FL[i] & 1);
+                    const int pv = live ? CD.PREV[i] : -1;
+                    bool dirty = live && pv >= 0 && pv < i0 && (CD.FL[pv] & 3);
+                    // predecessors inside this chunk: the marks spread lane to lane
+                    uint64_t dm = __ballot(dirty);
+                    for (;;) {
+                        const bool more = !dirty && live && pv >= i0 && ((CD.FL[pv] & 1) || ((dm >> (pv - i0)) & 1));
+                        const uint64_t nm = __ballot(more);
+                        if (!nm) break;
+                        dirty = dirty || more;
+                        dm |= nm;
+                    }
+                    while (dm) {
+                        const int l = (int)__builtin_ctzll(dm);
+                        dm &= dm - 1;
+                        chain_node(X, RG, CD, i0 + l, bp.max_intron, lane);
+                        work += i0 + l;
+                        if (lane == 0) CD.FL[i0 + l] |= 2;
+                        __threadfence_block();
+                        wave_sync();
+                    }
+                }
+                for (int i = lane; i < nr; i += 64) CD.FL[i] &= 1;
                 __threadfence_block();
                 wave_sync();
             }
@@ -641,13 +775,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
         BPM(4);
         // ---- rows of both strands, best first ---------------------------------------------------
         if (lane == 0) {
-            const int n = B.nrow;
-            for (int i = 1; i < n; ++i)
-                for (int j = i; j > 0 && psl_before(RW[j], RW[j - 1]); --j) {
-                    const af_psl tmp = RW[j - 1];
-                    RW[j - 1] = RW[j];
-                    RW[j] = tmp;
-                }
+            const int n = B.nrow;  // RW holds the first max_rows of them in order
             const int m = n < max_rows ? n : max_rows;
             const int64_t sl = 2 * qi + s_item;  // this strand's rows, best first, for k_blat_merge
             for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
@@ -688,20 +816,27 @@ __global__ void k_tile_keys(const uint8_t *__restrict__ T, int64_t n, int32_t st
     if (ok) atomicAdd(&cnt[key], 1u);
 }
 
-__global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, uint32_t *__restrict__ nblk) {
-    const int64_t b = blockIdx.x;  // one workgroup per 4096-base block; nblk[b + 1] = its N count
-    const int64_t a = b << NBLK_SHIFT;
-    int c = 0;
-    for (int64_t i = a + threadIdx.x; i < n && i < a + (1 << NBLK_SHIFT); i += blockDim.x) c += T[i] > 3;
-    __shared__ int part[256];
-    part[threadIdx.x] = c;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) nblk[b + 1] = (uint32_t)part[0];
+// one thread per 64-base block b: its N bits (bit u = base 64 b + u), nblk[b + 1] = their count and
+// rfirst[nb - 1 - b] = its first N (0xFFFFFFFF: none), reversed for the suffix min of k_tile_nnext
+__global__ void k_tile_nblocks(const uint8_t *__restrict__ T, int64_t n, int64_t nb, uint64_t *__restrict__ mask,
+                               uint32_t *__restrict__ nblk, uint32_t *__restrict__ rfirst) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t a = b << 6;
+    uint64_t m = 0;
+    for (int u = 0; u < 64 && a + u < n; ++u) m |= (uint64_t)(T[a + u] > 3) << u;
+    mask[b] = m;
+    nblk[b + 1] = (uint32_t)__builtin_popcountll(m);
+    rfirst[nb - 1 - b] = m ? (uint32_t)(a + __builtin_ctzll(m)) : 0xFFFFFFFFu;
 }
+// nnext[b] = the first N at or after block b (the reversed prefix min back in order)
+__global__ void k_tile_nnext(const uint32_t *__restrict__ rmin, int64_t nb, uint32_t *__restrict__ nnext) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) nnext[b] = rmin[nb - 1 - b];
+}
+struct MinU32 {
+    __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
+};
 
 }  // namespace
 
@@ -841,12 +976,15 @@ hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, De
                                hipStream_t s) {
     hipError_t e;
     const int64_t n_tiles = n >= TILE ? (n - TILE) / step + 1 : 0;
-    const int64_t nb = (n >> NBLK_SHIFT) + 2;
+    const int64_t nb = (n >> 6) + 2;  // N counts before each 64-base block (and one past the last)
     uint8_t *T = nullptr;
-    uint32_t *start = nullptr, *pos = nullptr, *ncum = nullptr;
-    uint32_t *keys = nullptr, *keys2 = nullptr, *pos2 = nullptr, *cnt = nullptr;
+    uint32_t *start = nullptr, *pos = nullptr, *ncum = nullptr, *nnext = nullptr;
+    uint64_t *nmask = nullptr;
+    uint32_t *keys = nullptr, *keys2 = nullptr, *pos2 = nullptr, *cnt = nullptr, *rf = nullptr, *rm = nullptr;
     void *temp = nullptr;
     auto cleanup = [&]() {
+        if (rf) (void)hipFree(rf);
+        if (rm) (void)hipFree(rm);
         if (keys) (void)hipFree(keys);
         if (keys2) (void)hipFree(keys2);
         if (pos2) (void)hipFree(pos2);
@@ -861,10 +999,16 @@ hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, De
     allocs[(*na)++] = pos;
     if ((e = hipMalloc(&ncum, sizeof(uint32_t) * (size_t)nb)) != hipSuccess) return e;
     allocs[(*na)++] = ncum;
+    if ((e = hipMalloc(&nmask, sizeof(uint64_t) * (size_t)nb)) != hipSuccess) return e;
+    allocs[(*na)++] = nmask;
+    if ((e = hipMalloc(&nnext, sizeof(uint32_t) * (size_t)nb)) != hipSuccess) return e;
+    allocs[(*na)++] = nnext;
     if ((e = hipMalloc(&keys, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
         (e = hipMalloc(&keys2, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
         (e = hipMalloc(&pos2, sizeof(uint32_t) * (size_t)(n_tiles > 0 ? n_tiles : 1))) != hipSuccess ||
-        (e = hipMalloc(&cnt, sizeof(uint32_t) * (NKEYS + 1))) != hipSuccess) {
+        (e = hipMalloc(&cnt, sizeof(uint32_t) * (NKEYS + 1))) != hipSuccess ||
+        (e = hipMalloc(&rf, sizeof(uint32_t) * (size_t)nb)) != hipSuccess ||
+        (e = hipMalloc(&rm, sizeof(uint32_t) * (size_t)nb)) != hipSuccess) {
         cleanup();
         return e;
     }
@@ -872,16 +1016,20 @@ hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, De
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb_sort, keys, keys2, pos, pos2, n_tiles, 0, 2 * TILE + 1);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, cnt, start, NKEYS + 1);
     (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb_scan2, ncum, ncum, nb);
-    size_t tb = std::max(tb_sort, std::max(tb_scan, tb_scan2));
+    size_t tb_min = 0;
+    (void)hipcub::DeviceScan::InclusiveScan(nullptr, tb_min, rf, rm, MinU32(), nb - 1);
+    size_t tb = std::max(std::max(tb_sort, tb_min), std::max(tb_scan, tb_scan2));
     if ((e = hipMalloc(&temp, tb > 0 ? tb : 16)) != hipSuccess) { cleanup(); return e; }
     const int bs = 256;
     if ((e = hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (NKEYS + 1), s)) != hipSuccess ||
-        (e = hipMemsetAsync(ncum, 0, sizeof(uint32_t) * (size_t)nb, s)) != hipSuccess) { cleanup(); return e; }
+        (e = hipMemsetAsync(ncum, 0, sizeof(uint32_t) * (size_t)nb, s)) != hipSuccess ||
+        (e = hipMemsetAsync(nnext, 0xFF, sizeof(uint32_t) * (size_t)nb, s)) != hipSuccess) { cleanup(); return e; }
     hipLaunchKernelGGL(k_tile_codes, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, d_seq, n, T);
     if (n_tiles > 0)
         hipLaunchKernelGGL(k_tile_keys, dim3((unsigned)((n_tiles + bs - 1) / bs)), dim3(bs), 0, s, T, n, step, n_tiles,
                            keys, pos2, cnt);
-    hipLaunchKernelGGL(k_tile_nblocks, dim3((unsigned)(nb - 1)), dim3(256), 0, s, T, n, ncum);
+    hipLaunchKernelGGL(k_tile_nblocks, dim3((unsigned)((nb - 1 + bs - 1) / bs)), dim3(bs), 0, s, T, n, nb - 1, nmask,
+                       ncum, rf);
     if ((e = hipGetLastError()) != hipSuccess) { cleanup(); return e; }
     size_t t1 = tb;
     if (n_tiles > 0 &&
@@ -891,8 +1039,13 @@ hipError_t af_build_tile_index(const uint8_t *d_seq, int64_t n, int32_t step, De
     if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t1, cnt, start, NKEYS + 1, s)) != hipSuccess) { cleanup(); return e; }
     t1 = tb;
     if ((e = hipcub::DeviceScan::InclusiveSum(temp, t1, ncum, ncum, nb, s)) != hipSuccess) { cleanup(); return e; }
+    t1 = tb;
+    if ((e = hipcub::DeviceScan::InclusiveScan(temp, t1, rf, rm, MinU32(), nb - 1, s)) != hipSuccess) { cleanup(); return e; }
+    hipLaunchKernelGGL(k_tile_nnext, dim3((unsigned)((nb - 1 + bs - 1) / bs)), dim3(bs), 0, s, rm, nb - 1, nnext);
+    if ((e = hipGetLastError()) != hipSuccess) { cleanup(); return e; }
     if ((e = hipStreamSynchronize(s)) != hipSuccess) { cleanup(); return e; }
     cleanup();
-    X->T = T; X->start = start; X->pos = pos; X->ncum = ncum; X->n = n; X->step = step;
+    X->T = T; X->start = start; X->pos = pos; X->ncum = ncum; X->nmask = nmask; X->nnext = nnext; X->n = n;
+    X->step = step;
     return hipSuccess;
 }

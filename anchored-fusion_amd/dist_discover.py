@@ -31,6 +31,8 @@ same code on CPU tensors.  The per-rank work is done by a backend with three pha
 -- implemented by discover.CandidateDiscovery on the GPU; the tests run the CPU oracle through
 the same driver.  Read names (for `render` only) go over `host_group` as objects.
 """
+import os
+
 import numpy as np
 
 from .genome import sam_lines
@@ -112,12 +114,22 @@ def _block(seq, lens, idx, width):
     return out
 
 
+def _collective(world):
+    """Whether the exchanges go through the process group: always at world > 1; at world 1 only
+    when AF_DIST_COLLECTIVES=1 and a group is initialised (a one-rank RCCL group runs the same
+    all-gathers / all-to-alls on one GPU -- tests/test_gpu_dist.py), else the local shortcut."""
+    if world > 1:
+        return True
+    import torch.distributed as dist
+    return os.environ.get("AF_DIST_COLLECTIVES") == "1" and dist.is_available() and dist.is_initialized()
+
+
 def _allgatherv(t, group, world):
     """All-gatherv of the rows of t (any dtype) over group; world 1: t itself."""
     import torch
 
     from .shard import allgatherv_device
-    if world == 1:
+    if not _collective(world):
         return t
     b = _words(t).view(torch.uint8)
     out = allgatherv_device(b, group)
@@ -131,7 +143,7 @@ def _alltoallv(parts, recv_rows, group, world):
     import torch.distributed as dist
     per = int(parts[0].shape[1])
     inp = torch.cat(parts).contiguous()
-    if world == 1:
+    if not _collective(world):
         return inp
     out = torch.empty((int(sum(recv_rows)), per), dtype=torch.uint8, device=inp.device)
     dist.all_to_all_single(out.view(-1), inp.view(-1), [int(r) * per for r in recv_rows],
@@ -143,7 +155,7 @@ def _gatherv(t, group, world, rank):
     """The rows of t from every rank on rank 0 (rank order), None elsewhere (an all-to-all whose
     only destination is rank 0)."""
     import torch
-    if world == 1:
+    if not _collective(world):
         return t
     b = _words(t).view(torch.uint8)
     n = _allgatherv(torch.tensor([[b.shape[0]]], dtype=torch.int64, device=b.device), group, world)[:, 0].tolist()

@@ -162,6 +162,7 @@ int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int3
 /* afo_blat that also counts how often its caps bound (caps[4] added to, the order of
  * af_blat_caps: hits past MAXH per strand, MAXCL clumps reached, MAXR parts reached with clumps
  * left, per query rows past max_rows) */
+void afo_blat_set_literal(int on);  /* test switch: the chain DP recomputes every part each round */
 int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
                   const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads,
                   int32_t *caps);

@@ -20,8 +20,11 @@
 #define NKEYS (1u << (2 * TILE))
 #define MAXH 32768     /* tile hits per query strand (the first MAXH in query order) */
 #define MAXCL 4096     /* clumps per query strand (the first MAXCL in diagonal order) */
-#define MAXR 16        /* aligned clumps per query strand */
-#define NBLK_SHIFT 12  /* N counts per 4096-base block: stitching never crosses an N */
+#define MAXP MAXCL     /* aligned clumps per query strand: one per clump at most (no cap of its own) */
+/* stitching work per query strand (predecessor candidates the chain DP rescans after a chain is
+ * emitted; the first pass is always made): once past it,
+ * no further chain is emitted and the strand is counted as cap[2] */
+#define STITCH_WORK (1LL << 24)
 
 struct afo_tiles {
     uint8_t *T;        /* codes 0-3, 4 = N */
@@ -29,7 +32,8 @@ struct afo_tiles {
     int32_t step;
     uint32_t *start;   /* NKEYS + 1 */
     uint32_t *pos;     /* tile positions, ascending per key */
-    uint32_t *ncum;    /* N count before each 4096-base block */
+    uint32_t *ncum;    /* N count before each 64-base block: stitching never crosses an N */
+    uint64_t *nmask;   /* N bits, 64 bases per word */
 };
 
 afo_tiles *afo_tiles_build(const char *seq, int64_t n, int32_t step) {
@@ -63,32 +67,27 @@ afo_tiles *afo_tiles_build(const char *seq, int64_t n, int32_t step) {
         if (ok) X->pos[fill[k]++] = (uint32_t)p;
     }
     free(fill);
-    int64_t nb = (n >> NBLK_SHIFT) + 2;
+    int64_t nb = (n >> 6) + 2;
     X->ncum = (uint32_t *)calloc(nb, sizeof(uint32_t));
-    for (int64_t b = 0; b + 1 < nb; ++b) {
-        uint32_t c = 0;
-        for (int64_t i = b << NBLK_SHIFT; i < n && i < (b + 1) << NBLK_SHIFT; ++i) c += X->T[i] > 3;
-        X->ncum[b + 1] = X->ncum[b] + c;
-    }
+    X->nmask = (uint64_t *)calloc(nb, sizeof(uint64_t));
+    for (int64_t i = 0; i < n; ++i)
+        if (X->T[i] > 3) X->nmask[i >> 6] |= 1ull << (i & 63);
+    for (int64_t b = 0; b + 1 < nb; ++b) X->ncum[b + 1] = X->ncum[b] + (uint32_t)__builtin_popcountll(X->nmask[b]);
     return X;
 }
 
 void afo_tiles_free(afo_tiles *X) {
     if (!X) return;
-    free(X->T); free(X->start); free(X->pos); free(X->ncum); free(X);
+    free(X->T); free(X->start); free(X->pos); free(X->ncum); free(X->nmask); free(X);
 }
 
-/* N bases in T[a, b) */
+/* N bases in T[a, b): the 64-base blocks' prefix counts, corrected by the end blocks' masks */
 static int64_t n_in(const afo_tiles *X, int64_t a, int64_t b) {
-    int64_t c = 0;
-    int64_t ba = a >> NBLK_SHIFT, bb = b >> NBLK_SHIFT;
-    if (ba == bb) {
-        for (int64_t i = a; i < b; ++i) c += X->T[i] > 3;
-        return c;
-    }
-    for (int64_t i = a; i < (ba + 1) << NBLK_SHIFT; ++i) c += X->T[i] > 3;
-    c += X->ncum[bb] - X->ncum[ba + 1];
-    for (int64_t i = bb << NBLK_SHIFT; i < b; ++i) c += X->T[i] > 3;
+    if (b <= a) return 0;
+    int64_t ba = a >> 6, bb = b >> 6;
+    int64_t c = (int64_t)X->ncum[bb] - (int64_t)X->ncum[ba];
+    c -= __builtin_popcountll(X->nmask[ba] & ((1ull << (a & 63)) - 1));
+    c += __builtin_popcountll(X->nmask[bb] & ((1ull << (b & 63)) - 1));
     return c;
 }
 
@@ -243,7 +242,57 @@ static int tile_key(const uint8_t *Q, int q, uint32_t *k) {
     return 1;
 }
 
-/* one strand of one query: rows appended to out (n_out in/out) */
+static int cmp_psl(const void *a, const void *b);
+
+/* test switch: 1 = the chain DP recomputes every unused part each round (afo_blat_set_literal) */
+static int g_blat_literal = 0;
+void afo_blat_set_literal(int on) { g_blat_literal = on; }
+
+/* the chain DP of part i (position i of ord) over the unused parts before it: a predecessor a
+ * must end before i on both sequences; i is trimmed by the overlap (chain_trim) and must keep part
+ * of its first block; the target gap must be <= max_intron and hold no N; the score is best[a] +
+ * the trimmed part's score - 1 per query / target gap; the first a with the highest score wins
+ * over i alone */
+static void chain_node(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, const reg_b *regs,
+                       const int *ord, int *best, int *prev, const int *fl, int i) {
+    const reg_b *ri = &regs[ord[i]];
+    best[i] = ri->score; prev[i] = -1;
+    if (g_blat_literal) {  /* the plain statement: trim_front per candidate */
+        for (int j = 0; j < i; ++j) {
+            if (fl[j] & 1) continue;
+            const reg_b *a = &regs[ord[j]];
+            reg_b b;
+            if (ri->qe <= a->qe || ri->te <= a->te) continue;
+            if (!trim_front(X, Q, ri, chain_trim(a, ri), &b)) continue;
+            if (b.tb - a->te > bp->max_intron || n_in(X, a->te, b.tb)) continue;
+            int s = best[j] + b.score - (b.qb > a->qe) - (b.tb > a->te);
+            if (s > best[i]) { best[i] = s; prev[i] = j; }
+        }
+        return;
+    }
+    /* pre[k] = the score of the first block's first k bases (what trim_front removes) */
+    int pre[AFO_MAX_READ + 1];
+    pre[0] = 0;
+    for (int u = 0; u < ri->bsz[0] && u < AFO_MAX_READ; ++u) {
+        uint8_t x = Q[ri->bq[0] + u], y = X->T[ri->bt[0] + u];
+        pre[u + 1] = pre[u] + ((x > 3 || y > 3) ? 0 : (x == y ? 1 : -1));
+    }
+    for (int j = 0; j < i; ++j) {
+        if (fl[j] & 1) continue;
+        const reg_b *a = &regs[ord[j]];
+        if (ri->qe <= a->qe || ri->te <= a->te) continue;
+        const int k = chain_trim(a, ri);
+        if (k > 0 && k >= ri->bsz[0]) continue;
+        const int32_t bqb = ri->qb + k;
+        const int64_t btb = ri->tb + k;
+        if (btb - a->te > bp->max_intron || n_in(X, a->te, btb)) continue;
+        int s = best[j] + (ri->score - pre[k]) - (bqb > a->qe) - (btb > a->te);
+        if (s > best[i]) { best[i] = s; prev[i] = j; }
+    }
+}
+
+/* one strand of one query: its rows, the best cap_out in cmp_psl order, at out; *n_out counts
+ * every row */
 static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, int L, int strand,
                         int32_t qi, afo_psl *out, int *n_out, int cap_out, hit_t *hits, reg_b *regs, int *cap) {
     int nh = 0;
@@ -284,7 +333,7 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
     if (ncl == MAXCL) cap[1] = 1;
     qsort(cl, ncl, sizeof(clump_t), cmp_clump);  /* (hits desc, diagonal): keys are unique */
     int nr = 0, c = 0;
-    for (; c < ncl && nr < MAXR; ++c) {
+    for (; c < ncl && nr < MAXP; ++c) {
         int32_t q = cl[c].q;
         int64_t t = cl[c].t;
         int skip = 0;
@@ -293,68 +342,92 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         if (skip) continue;
         if (align_clump(X, Q, L, q, t, &regs[nr])) ++nr;
     }
-    if (nr == MAXR && c < ncl) cap[2] = 1;
+    if (nr == MAXP && c < ncl) cap[2] = 1;
     free(cl);
-    /* regions in (qb, tb, qe) order for the chain DP */
+    if (nr == 0) return;
+    /* regions in (qb, tb, qe) order for the chain DP (stable: ties keep their creation order) */
+    int *ord = (int *)malloc(sizeof(int) * 5 * nr);
+    int *best = ord + nr, *prev = best + nr, *fl = prev + nr, *chain = fl + nr;
+    for (int i = 0; i < nr; ++i) ord[i] = i;
     for (int i = 1; i < nr; ++i)
         for (int j = i; j > 0; --j) {
-            reg_b *a = &regs[j - 1], *b = &regs[j];
+            const reg_b *a = &regs[ord[j - 1]], *b = &regs[ord[j]];
             int gt = a->qb > b->qb || (a->qb == b->qb && (a->tb > b->tb || (a->tb == b->tb && a->qe > b->qe)));
             if (!gt) break;
-            reg_b tmp = *a; *a = *b; *b = tmp;
+            int tmp = ord[j - 1]; ord[j - 1] = ord[j]; ord[j] = tmp;
         }
-    int best[MAXR], prev[MAXR];
+    for (int i = 0; i < nr; ++i) { regs[i].used = 0; fl[i] = 0; }
+    /* BLAT-style stitching: each round emits the chain with the highest score over the unused
+     * parts (the first in order on ties).  chain_node is the literal DP of one part; after a
+     * chain is emitted only the parts whose predecessor path meets a used (or recomputed) part
+     * are recomputed -- the others' values cannot change, as removing parts only lowers scores
+     * (g_blat_literal = 1 recomputes every part each round, the plain statement of the rule). */
+    int64_t work = 0;  /* the recomputations' candidates (the first pass is always made) */
+    for (int i = 0; i < nr; ++i) chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
     for (;;) {
+        if (work > STITCH_WORK && !g_blat_literal) { cap[2] = 1; break; }
         int bi = -1;
-        for (int i = 0; i < nr; ++i) {
-            if (regs[i].used) continue;
-            best[i] = regs[i].score; prev[i] = -1;
-            for (int j = 0; j < i; ++j) {
-                if (regs[j].used) continue;
-                const reg_b *a = &regs[j];
-                reg_b b;
-                if (regs[i].qe <= a->qe || regs[i].te <= a->te) continue;
-                if (!trim_front(X, Q, &regs[i], chain_trim(a, &regs[i]), &b)) continue;
-                if (b.tb - a->te > bp->max_intron || n_in(X, a->te, b.tb)) continue;
-                int s = best[j] + b.score - (b.qb > a->qe) - (b.tb > a->te);
-                if (s > best[i]) { best[i] = s; prev[i] = j; }
-            }
-            if (bi < 0 || best[i] > best[bi]) bi = i;
-        }
+        for (int i = 0; i < nr; ++i)
+            if (!fl[i] && (bi < 0 || best[i] > best[bi])) bi = i;
         if (bi < 0) break;
-        int chain[MAXR], m = 0;
+        int m = 0;
         for (int i = bi; i >= 0; i = prev[i]) chain[m++] = i;
         afo_psl o;
         memset(&o, 0, sizeof(o));
         o.query = qi; o.strand = strand; o.q_size = L;
         int ok = 1;
-        reg_b part[MAXR];
-        for (int c = m - 1; c >= 0; --c) {
-            regs[chain[c]].used = 1;
-            if (c == m - 1) part[c] = regs[chain[c]];
-            else trim_front(X, Q, &regs[chain[c]], chain_trim(&part[c + 1], &regs[chain[c]]), &part[c]);
-            const reg_b *r = &part[c];
-            if (c < m - 1) {
-                const reg_b *a = &part[c + 1];
-                if (r->qb > a->qe) { ++o.q_num_insert; o.q_base_insert += r->qb - a->qe; }
-                if (r->tb > a->te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(r->tb - a->te); }
+        reg_b pp, first, last, cur;
+        memset(&first, 0, sizeof first); memset(&last, 0, sizeof last); memset(&pp, 0, sizeof pp);
+        for (int k = m - 1; k >= 0; --k) {
+            fl[chain[k]] = 1;
+            const reg_b *src = &regs[ord[chain[k]]];
+            if (k == m - 1) cur = *src;
+            else trim_front(X, Q, src, chain_trim(&pp, src), &cur);
+            if (k < m - 1) {
+                if (cur.qb > pp.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - pp.qe; }
+                if (cur.tb > pp.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - pp.te); }
             }
-            o.matches += r->matches; o.mismatches += r->mismatches; o.n_count += r->ncount;
-            o.q_num_insert += r->qni; o.q_base_insert += r->qbi; o.t_num_insert += r->tni; o.t_base_insert += r->tbi;
-            for (int b = 0; b < r->nb; ++b) {
+            o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
+            o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi; o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
+            for (int b = 0; b < cur.nb; ++b) {
                 if (o.block_count >= AFO_PSL_MAX_BLOCKS) { ok = 0; break; }
-                o.block_sizes[o.block_count] = r->bsz[b]; o.q_starts[o.block_count] = r->bq[b];
-                o.t_starts[o.block_count] = r->bt[b]; ++o.block_count;
+                o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
+                o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
             }
+            if (k == m - 1) first = cur;
+            if (k == 0) last = cur;
+            pp = cur;
         }
-        const reg_b *f = &part[m - 1], *l = &part[0];
-        o.q_start = strand ? L - l->qe : f->qb;
-        o.q_end = strand ? L - f->qb : l->qe;
-        o.t_start = f->tb; o.t_end = l->te;
+        o.q_start = strand ? L - last.qe : first.qb;
+        o.q_end = strand ? L - first.qb : last.qe;
+        o.t_start = first.tb; o.t_end = last.te;
         o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
-        if (!ok || o.score < bp->min_score || psl_millibad(&o) > (100 - bp->min_identity) * 10) continue;
-        if (*n_out < cap_out) out[(*n_out)++] = o;
+        if (ok && o.score >= bp->min_score && psl_millibad(&o) <= (100 - bp->min_identity) * 10) {
+            /* the strand's best cap_out rows in cmp_psl order, stable; every row counted */
+            int n = *n_out < cap_out ? *n_out : cap_out, at = n;
+            while (at > 0 && cmp_psl(&o, &out[at - 1]) < 0) --at;
+            if (at < cap_out) {
+                for (int x = n < cap_out ? n : cap_out - 1; x > at; --x) out[x] = out[x - 1];
+                out[at] = o;
+            }
+            ++*n_out;
+        }
+        if (g_blat_literal) {
+            for (int i = 0; i < nr; ++i)
+                if (!fl[i]) chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
+        } else {
+            for (int i = chain[m - 1] + 1; i < nr; ++i) {
+                if (fl[i] & 1) continue;
+                if (prev[i] >= 0 && fl[prev[i]]) {
+                    chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
+                    work += i;
+                    fl[i] = 2;
+                }
+            }
+            for (int i = 0; i < nr; ++i) fl[i] &= 1;
+        }
     }
+    free(ord);
 }
 
 static int cmp_psl(const void *a, const void *b) {
@@ -389,13 +462,13 @@ int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries,
             Q[1][L - 1 - i] = c > 3 ? 4 : 3 - c;
         }
         hit_t *hits = (hit_t *)malloc(sizeof(hit_t) * MAXH);
-        reg_b regs[MAXR];
-        afo_psl cand[2 * 2 * MAXR];
-        int nc = 0;
+        reg_b *regs = (reg_b *)malloc(sizeof(reg_b) * MAXP);
+        afo_psl cand[2][AFO_BLAT_MAX_ROWS];
+        int nc[2] = {0, 0};
         int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
         for (int s = 0; s < 2; ++s) {
-            memset(regs, 0, sizeof(regs));
-            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand, &nc, 2 * 2 * MAXR, hits, regs, cap[s]);
+            memset(regs, 0, sizeof(reg_b) * MAXP);
+            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand[s], &nc[s], max_rows, hits, regs, cap[s]);
         }
         if (caps) {
             for (int s = 0; s < 2; ++s)
@@ -404,16 +477,22 @@ int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries,
 #pragma omp atomic
                         caps[k] += 1;
                     }
-            if (nc > max_rows) {
+            if (nc[0] + nc[1] > max_rows) {
 #pragma omp atomic
                 caps[3] += 1;
             }
         }
         free(hits);
-        qsort(cand, nc, sizeof(afo_psl), cmp_psl);
-        int m = nc < max_rows ? nc : max_rows;
-        for (int k = 0; k < m; ++k) rows[qi * max_rows + k] = cand[k];
-        n_rows[qi] = m;
+        free(regs);
+        /* the two strands' sorted lists merged (strand 0 first on equal keys: cmp_psl orders by
+         * strand, so never) */
+        int na = nc[0] < max_rows ? nc[0] : max_rows, nb = nc[1] < max_rows ? nc[1] : max_rows;
+        int i = 0, j = 0, k = 0;
+        for (; k < max_rows && (i < na || j < nb); ++k) {
+            int take_b = j < nb && (i >= na || cmp_psl(&cand[1][j], &cand[0][i]) < 0);
+            rows[qi * max_rows + k] = take_b ? cand[1][j++] : cand[0][i++];
+        }
+        n_rows[qi] = k;
     }
     return 0;
 }

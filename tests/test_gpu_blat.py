@@ -96,8 +96,8 @@ def test_blat_parity(preset):
 
 
 def test_blat_caps_match_oracle():
-    """Every cap counter of af_blat_caps (hits, clumps, parts, rows) on a world where each binds
-    (tests/test_blat_caps.py), equal to the oracle's."""
+    """Every cap counter of af_blat_caps (hits, clumps, rows; parts never binds: every clump may
+    become a part) on a world where each binds (tests/test_blat_caps.py), equal to the oracle's."""
     from anchored_fusion_amd import blat
     from test_blat_caps import caps_world
     ctgs, qs = caps_world()
@@ -110,7 +110,32 @@ def test_blat_caps_match_oracle():
         assert np.array_equal(ng, no)
         cg, co = g.caps(), o.caps()
         assert cg == co, (max_rows, cg, co)
-        assert min(cg.values()) > 0 if max_rows == 1 else cg["hits"] > 0
+        assert cg["parts"] == 0 and (min(cg["hits"], cg["clumps"], cg["rows"]) > 0 if max_rows == 1 else cg["hits"] > 0)
+        g.close()
+
+
+def test_blat_many_parts_equal_oracle():
+    """A repeat family of 60 diverged copies and split halves (tests/test_blat_caps.py
+    family_world): dozens of parts per query strand, chains across a 2 kb gap, the row cap bound --
+    every PSL field and every counter equal to the oracle's, for max_rows 16 and 3."""
+    from anchored_fusion_amd import blat
+    from test_blat_caps import family_world
+    ctgs, qs = family_world()
+    rng = np.random.default_rng(4)
+    qs = qs + [q[int(a):int(a) + 120] for q, a in zip(qs * 4, rng.integers(0, 100, 8))]
+    p = blat.params("split_tail")
+    g = _gpu_ref(ctgs, p.step_size)
+    o = OracleTileReference(ctgs, p.step_size)
+    try:
+        for max_rows in (16, 3):
+            rg, ng = g.search(qs, p, max_rows)
+            ro, no = o.search(qs, p, max_rows)
+            assert np.array_equal(ng, no), (max_rows, ng, no)
+            for q in range(len(qs)):
+                assert rg[q, :ng[q]].tobytes() == ro[q, :no[q]].tobytes(), (max_rows, q)
+            cg, co = g.caps(), o.caps()
+            assert cg == co and cg["parts"] == 0 and cg["rows"] > 0, (cg, co)
+    finally:
         g.close()
 
 

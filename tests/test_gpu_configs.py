@@ -4,8 +4,10 @@
   chunk (pair_base) -- through discover.CandidateDiscovery as bench.py's ranks run it: S2
   bit-exact vs the oracle on the shard's first two chunks (the read ids and insert-size chunks of
   the global input), the S4 / S5 records equal to the genome engine's own host-buffer calls,
-  S5's genome check and the S6 queries equal to the host chain, and the candidate exchange over
-  a one-rank RCCL group returning exactly the packed rows with global read rows.  The genome is
+  S5's genome check and the S6 queries equal to the host chain, and the product's multi-GPU step
+  (dist_discover.search on the rank's lo) through a one-rank RCCL group, its all-gathers and
+  all-to-alls on device tensors, giving the same counts, S4 records and survivors with global
+  read rows.  The genome is
   the configs[2] world at 5 % scale (the index build of the full 3.1 Gbp is test_gpu_c3's).
 * configs[4] (1,000 cells x 100 k pairs over 8 GPUs): one rank's 125 cells through
   singlecell.run, the planted fusion merged from the cells, and three sampled cells' tables
@@ -67,25 +69,40 @@ def test_configs3_rank3_shape(anchor):
         nq = int(d.n_q.item())
         _check_genome_records(d, gidx, d.q[:nq].cpu().numpy(), nq, c["s4_pairs"])
         _check_s5_s6(d, gidx, reads, full, an, c["s4_pairs"], nq)
-        # the candidate exchange (one-rank RCCL group): rows with global read rows
+        # the product's multi-GPU step (dist_discover.search) on the rank's lo, its exchanges through a
+        # one-rank RCCL group on device tensors (AF_DIST_COLLECTIVES=1): the same counts, S4 records
+        # and survivors, global read rows inside the shard
+        npair = c["s4_pairs"]
+        rec_bytes = 2 * npair * discover.MAX_REC * discover._genome.REC_DTYPE.itemsize
+        s4_n0, s4_r0 = d.q_nh[:2 * npair].cpu().numpy(), d.q_recs[:rec_bytes].cpu().numpy()
+        from anchored_fusion_amd import dist_discover
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), AF_DIST_COLLECTIVES="1")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         try:
-            packed = d.pack()
-            ex = d.exchange()
+            out, cnt = dist_discover.search(d.attach(reads_t, None), lo, 0, 1, device="cuda:0")
             torch.cuda.synchronize()
         finally:
             dist.destroy_process_group()
-        assert torch.equal(ex.cpu(), packed.cpu()) and ex.shape[0] == nq + summ["s6_queries"]
-        p = packed.cpu().numpy()
-        grow = p[:, 0].view(np.uint32).astype(np.int64) | (p[:, 1].astype(np.int64) << 32)
-        assert np.array_equal(grow[:nq], d.q_rows[:nq].cpu().numpy().astype(np.int64) + 2 * lo)
-        local = grow - 2 * lo
-        assert (local >= 0).all() and (local < 2 * n).all()
-        assert np.array_equal(p[:, 3], full["flag"][local]) and np.array_equal(p[:, 4], full["pos"][local])
+            os.environ.pop("AF_DIST_COLLECTIVES", None)
+        for k in ("tmp1", "tmp2", "s5_split_reads", "s6_queries", "s4_pairs"):
+            assert cnt[k] == summ[k], (k, cnt[k], summ[k])
+        _, _, recs, nrec, g1 = out["s4"]
+        assert np.array_equal(nrec.cpu().numpy(), s4_n0)
+        got_r = recs.cpu().numpy().view(np.uint8).reshape(2 * npair, -1)
+        want_r = s4_r0.reshape(2 * npair, -1)
+        live = np.arange(discover.MAX_REC)[None, :] < s4_n0[:, None]
+        per = want_r.shape[1] // discover.MAX_REC
+        assert np.array_equal(got_r.reshape(2 * npair, discover.MAX_REC, per)[live],
+                              want_r.reshape(2 * npair, discover.MAX_REC, per)[live])
+        surv = out["surv"].cpu().numpy()
+        assert surv.shape[0] == summ["s6_queries"]
+        grow = surv[:, -2].view(np.uint32).astype(np.int64) | (surv[:, -1].astype(np.int64) << 32)
+        assert (grow >= 2 * lo).all() and (grow < 2 * (lo + n)).all()
+        g1 = g1.cpu().numpy()
+        assert (g1 >= 2 * lo).all() and (g1 < 2 * (lo + n)).all()
     finally:
         d.close()
         gidx.close()
