@@ -39,16 +39,18 @@ def main():
 
     def counters(sub):
         acc = collections.defaultdict(float)
-        disp = collections.defaultdict(set)
+        disp = collections.defaultdict(dict)
         for f in glob.glob(os.path.join(src, sub, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 k = short(r["Kernel_Name"])
                 acc[(k, r["Counter_Name"])] += float(r["Counter_Value"])
-                disp[k].add(r["Dispatch_Id"])
-        return {k: v / len(disp[k[0]]) for k, v in acc.items()}, {k: len(v) for k, v in disp.items()}
+                disp[k][r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+        avg = {k: v / len(disp[k[0]]) for k, v in acc.items()}
+        ns = {k: sum(v.values()) / len(v) for k, v in disp.items()}
+        return avg, {k: len(v) for k, v in disp.items()}, ns
 
-    sq, nd = counters("sq")
-    fe, _ = counters("fetch")
+    sq, nd, _ = counters("sq")
+    fe, _, fe_ns = counters("fetch")
     bench = {}
     if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):
         bench = json.load(open(sys.argv[3]))
@@ -73,19 +75,22 @@ def main():
             e["active_inst_frac"] = round(g("SQ_ACTIVE_INST_ANY") / wc, 3)
         if g("SQ_WAVES"):
             e["waves"] = int(g("SQ_WAVES"))
-        if avg_us and g("SQ_INSTS_VALU"):
+        # the counter pass's own duration in cycles: GRBM_GUI_ACTIVE sums the 8 XCDs
+        # (MI355X_MICROARCH.md); SQ_WAVE_CYCLES / WAIT / ACTIVE count quad-cycles
+        cyc = g("GRBM_GUI_ACTIVE") / 8
+        if cyc:
+            e["pmc_pass_cycles"] = round(cyc)
+        if cyc and g("SQ_INSTS_VALU"):
             e["valu_per_launch"] = round(g("SQ_INSTS_VALU"))
-            e["valu_issue_frac"] = round(g("SQ_INSTS_VALU") * 2 / (avg_us * 1e3 * CLOCK_GHZ * N_SIMD), 4)
-        if avg_us and g("SQ_BUSY_CYCLES") and g("GRBM_GUI_ACTIVE"):
-            e["sq_busy_frac"] = round(g("SQ_BUSY_CYCLES") / g("GRBM_GUI_ACTIVE"), 3)
-        if avg_us and wc:
-            # resident waves averaged over the launch: wave-cycles / (duration x clock)
-            e["avg_resident_waves_per_simd"] = round(wc / (avg_us * 1e3 * CLOCK_GHZ) / N_SIMD, 2)
+            e["valu_issue_frac"] = round(g("SQ_INSTS_VALU") * 2 / (cyc * N_SIMD), 4)
+        if cyc and wc:
+            e["avg_resident_waves_per_simd"] = round(4 * wc / cyc / N_SIMD, 2)
         fs = fe.get((k, "FETCH_SIZE"))
         if fs is not None:
             e["fetch_bytes_per_launch_x2"] = round(fs * 1024 * 2)
-            if avg_us:
-                e["fetch_gbs_x2"] = round(fs * 1024 * 2 / (avg_us * 1e3), 1)
+            if fe_ns.get(k):  # over the FETCH pass's own dispatch time (kernels serialised)
+                e["fetch_pass_us"] = round(fe_ns[k] / 1e3, 1)
+                e["fetch_gbs_x2"] = round(fs * 1024 * 2 / fe_ns[k], 1)
         for key, (uname, n) in units.items():
             if k.startswith(key) and n:
                 e["unit"] = uname
@@ -95,13 +100,17 @@ def main():
         kern[k] = e
     res = {"source": f"rocprofv3 --kernel-trace --stats, then --pmc passes (SQ; FETCH_SIZE) of "
                      f"python3 bench.py --no-cpu (configs[2], one GPU); {src}",
-           "issue_model": "a wave64 VALU instruction issues over 2 cycles on a SIMD (MI355X_MICROARCH.md): "
-                          "valu_issue_frac = SQ_INSTS_VALU x 2 / (avg duration x 2.4 GHz x 1024 SIMDs)",
+           "issue_model": "a wave64 VALU instruction issues over 2 cycles on a SIMD: valu_issue_frac = "
+                          "SQ_INSTS_VALU x 2 / (pass cycles x 1024 SIMDs), pass cycles = GRBM_GUI_ACTIVE / 8 (the "
+                          "counter pass's own dispatch, kernels serialised); resident waves = 4 x SQ_WAVE_CYCLES "
+                          "(quad-cycles) / pass cycles / 1024; avg_duration_us is the kernel trace's (the step as "
+                          "run: batches in flight, S4 beside S5 / S6)",
            "fetch_note": "FETCH_SIZE (KiB) x 1024 x 2: the gfx950 correction for wide coalesced reads; other "
-                         "access widths are uncalibrated (MI355X_MICROARCH.md, HBM)",
+                         "access widths are uncalibrated (MI355X_MICROARCH.md, HBM); GB/s over the FETCH pass's own "
+                         "dispatch time",
            "kernels": kern}
     json.dump(res, open(os.path.join(out, "pmc_c3.json"), "w"), indent=1)
-    cols = ["avg_duration_us", "launches_counted", "valu_issue_frac", "wait_any_frac", "active_inst_frac",
+    cols = ["avg_duration_us", "fetch_pass_us", "pmc_pass_cycles", "valu_issue_frac", "wait_any_frac", "active_inst_frac",
             "avg_resident_waves_per_simd", "fetch_gbs_x2", "fetch_bytes_per_unit_x2"]
     lines = ["| kernel | " + " | ".join(cols) + " |", "|---" * (len(cols) + 1) + "|"]
     for k, e in kern.items():
