@@ -41,7 +41,7 @@ EXPORTS = (
     "af_genome_build", "af_genome_build_device", "af_genome_free", "af_genome_lpac",
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
     "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats", "af_s5_filter_device",
-    "af_genome_align_se_ids_device", "af_genome_align_pe_se_device", "af_genome_intervals", "af_s5_rules_host", "af_blat_caps",
+    "af_genome_align_se_ids_device", "af_genome_align_pe_se_device", "af_genome_intervals", "af_s5_rules_host", "af_blat_caps", "af_blat_spill",
 )
 AF_G_MAX_REC = 8
 AF_GSTAT_N = 4
@@ -204,6 +204,8 @@ def lib():
     L.af_s5_rules_host.restype = ctypes.c_int
     L.af_blat_caps.argtypes = [_vp, _vp, ctypes.c_int]
     L.af_blat_caps.restype = ctypes.c_int
+    L.af_blat_spill.argtypes = [_vp, _vp, _vp, _vp, _i64]
+    L.af_blat_spill.restype = ctypes.c_int
     _L = L
     return L
 

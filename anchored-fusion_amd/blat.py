@@ -70,6 +70,7 @@ class TileReference:
                    "af_tile_index_build")
 
     def _open(self, device, ctx):
+        self.device = int(device)
         self._own_ctx = ctx is None
         if ctx is None:
             ctx = ctypes.c_void_p()
@@ -118,6 +119,39 @@ class TileReference:
                                                    nr.ctypes.data), "af_blat")
         return rows, nr
 
+    def search_all(self, seqs, p):
+        """Every row of every query, as BLAT prints them: (rows [n, MAX_ROWS], n_rows [n], {query:
+        [its rows past MAX_ROWS]}) -- af_blat_device with the spill pool on this reference's
+        context (device buffers made here; the rows come back to the host)."""
+        import torch
+        n = len(seqs)
+        if not n:
+            return np.zeros((0, MAX_ROWS), PSL_DTYPE), np.zeros(0, np.int32), {}
+        buf, lens = pack_queries(seqs)
+        dev = torch.device("cuda", self.device)
+        q_t = torch.from_numpy(buf).to(dev)
+        l_t = torch.from_numpy(lens).to(dev)
+        n_t = torch.tensor([n], dtype=torch.int32, device=dev)
+        rows_t = torch.zeros(n * MAX_ROWS * PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        nr_t = torch.zeros(n, dtype=torch.int32, device=dev)
+        cap = max(1024, 4 * n)
+        sp = dict(rows=torch.zeros(cap * PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+                  q=torch.zeros(cap, dtype=torch.int32, device=dev), n=torch.zeros(1, dtype=torch.int32, device=dev))
+        stream = torch.cuda.current_stream(dev)
+        self.spill_to(sp["rows"], sp["q"], sp["n"])
+        try:
+            self.search_device(q_t, n_t, buf.shape[1], rows_t, nr_t, lens_t=l_t, p=p, stream=stream)
+        finally:
+            self.spill_to()
+        torch.cuda.synchronize(dev)
+        ns = int(sp["n"].item())
+        if ns > cap:
+            raise _lib.AFError(f"af_blat spill pool of {cap} rows overflowed ({ns} rows)")
+        rows = rows_t.cpu().numpy().view(PSL_DTYPE).reshape(n, MAX_ROWS)
+        extra = spilled_rows(sp["rows"][:ns * PSL_DTYPE.itemsize].cpu().numpy().view(PSL_DTYPE),
+                             sp["q"][:ns].cpu().numpy())
+        return rows, nr_t.cpu().numpy(), extra
+
     def search_device(self, queries_t, n_queries_t, stride, rows_t, n_rows_t, lens_t=None, p=None, max_rows=MAX_ROWS,
                       stream=None, first_t=None):
         """af_blat_device on device buffers (rows_t: cap * max_rows * 328 bytes); first_t (an int32
@@ -135,6 +169,17 @@ class TileReference:
             n_queries_t.data_ptr(), cap, int(stride), None if lens_t is None else lens_t.data_ptr(),
             ctypes.byref(p or params()), int(max_rows), rows_t.data_ptr(), n_rows_t.data_ptr(),
             _stream_handle(stream)), "af_blat_device_range")
+
+    def spill_to(self, rows_t=None, query_t=None, n_t=None):
+        """af_blat_spill: later device searches on this reference's context append each query's
+        rows past max_rows to rows_t (uint8 [cap * 328]) with their query index in query_t, the
+        count in n_t (int32 device word the caller zeroes); no arguments: unregister."""
+        if rows_t is None:
+            _lib.check(self.ctx, _lib.lib().af_blat_spill(self.ctx, None, None, None, 0), "af_blat_spill")
+            return
+        cap = min(rows_t.numel() * rows_t.element_size() // PSL_DTYPE.itemsize, int(query_t.numel()))
+        _lib.check(self.ctx, _lib.lib().af_blat_spill(self.ctx, rows_t.data_ptr(), query_t.data_ptr(), n_t.data_ptr(),
+                                                      int(cap)), "af_blat_spill")
 
     def caps(self, reset=True):
         """af_blat_caps: query strands / queries at each of the search's caps since the last reset
@@ -154,16 +199,34 @@ class TileReference:
         return k, s, e
 
 
-def psl_lines(ref, queries, rows, nr, offsets=None, full_sizes=None):
+PSL_ORDER = ("score", "strand", "t_start", "q_start", "t_end", "q_end")  # psl_before: score desc, then ascending
+
+
+def spilled_rows(rows, query):
+    """The spill pool's rows (PSL_DTYPE [n], query index [n]) grouped per query in the search's row
+    order (score desc, strand, tStart, qStart, tEnd, qEnd): {query: [row, ...]}.  They follow the
+    query's kept rows."""
+    out = {}
+    if len(rows) == 0:
+        return out
+    order = np.lexsort((rows["q_end"], rows["t_end"], rows["q_start"], rows["t_start"], rows["strand"],
+                        -rows["score"].astype(np.int64), query))
+    for i in order:
+        out.setdefault(int(query[i]), []).append(rows[i])
+    return out
+
+
+def psl_lines(ref, queries, rows, nr, offsets=None, full_sizes=None, extra=None):
     """PSL lines (21 columns, psLayout 3) of the rows of queries [(name, seq)].  offsets /
     full_sizes: a query that is a window of a longer sequence reports the full query's size and
-    coordinates (offset added; '-' strand blocks mapped on the full reverse complement)."""
+    coordinates (offset added; '-' strand blocks mapped on the full reverse complement).  extra:
+    {query index: [rows past the kept ones]} (spilled_rows), printed after them."""
     out = []
     for i, (name, seq) in enumerate(queries):
         off = 0 if offsets is None else int(offsets[i])
         full = len(seq) if full_sizes is None else int(full_sizes[i])
-        for k in range(max(int(nr[i]), 0)):
-            r = rows[i, k]
+        mine = [rows[i, k] for k in range(max(int(nr[i]), 0))] + (extra.get(i, []) if extra else [])
+        for r in mine:
             loc = ref.locate(r["t_start"], r["t_end"])
             if loc is None:
                 continue

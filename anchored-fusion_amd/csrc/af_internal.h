@@ -312,11 +312,18 @@ hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t 
 // k_blat's per-wave global scratch (blat.hip layout) and its resident waves on n_cu CUs
 constexpr size_t AF_BLAT_SLOT_BYTES = 2088 << 10;  // blat.hip SC_END
 int af_blat_slots(int n_cu);
+// the rows past max_rows (af_blat_spill): appended at rows[atomicAdd(n, 1)] with their query
+struct BlatSpill {
+    af_psl *rows = nullptr;
+    int32_t *query = nullptr, *n = nullptr;
+    int64_t cap = 0;
+};
 hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, hipStream_t s);
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, const BlatSpill &spill,
+                          hipStream_t s);
 // k_blat's schedule: the queries by estimated cost, heaviest first (work: af_blat_order_bytes(cap))
 size_t af_blat_order_bytes(int64_t cap);
 hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,

@@ -31,6 +31,7 @@ struct af_ctx {
     int32_t *blat_order = nullptr;
     int64_t blat_ord_cap = 0;
     int32_t *blat_caps = nullptr;   // AF_BLAT_CAP_N counters, cumulative until af_blat_caps resets them
+    BlatSpill blat_spill;           // af_blat_spill's pool (caller-owned device buffers)
     af_psl *blat_stage = nullptr;   // per (query, strand) rows before k_blat_merge
     int32_t *blat_stage_n = nullptr;
     int64_t blat_stage_rows = 0, blat_stage_items = 0;
@@ -1079,7 +1080,7 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
             hipSuccess ||
         (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride, lens ? d_lens : nullptr, *p,
                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows,
-                            c->blat_order, c->blat_stage, c->blat_stage_n, c->blat_caps, s)) !=
+                            c->blat_order, c->blat_stage, c->blat_stage_n, c->blat_caps, BlatSpill{}, s)) !=
             hipSuccess ||
         (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipMemcpyAsync(n_rows, d_nrows, 4 * n_queries, hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -1118,7 +1119,15 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
     }
     HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
                              c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows,
-                             order, c->blat_stage, c->blat_stage_n, c->blat_caps, s));
+                             order, c->blat_stage, c->blat_stage_n, c->blat_caps, c->blat_spill, s));
+    return AF_OK;
+}
+
+int af_blat_spill(af_ctx *c, af_psl *d_rows, int32_t *d_query, int32_t *d_n, int64_t cap) {
+    if (!c) return fail(c, AF_E_INVALID, "null argument");
+    if (!d_rows || cap <= 0) { c->blat_spill = BlatSpill{}; return AF_OK; }
+    if (!d_query || !d_n) return fail(c, AF_E_INVALID, "af_blat_spill: null query / count buffer");
+    c->blat_spill = BlatSpill{d_rows, d_query, d_n, cap};
     return AF_OK;
 }
 

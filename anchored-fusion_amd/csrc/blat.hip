@@ -428,7 +428,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                                                         uint8_t *__restrict__ bscratch, int32_t diag_passes,
                                                         af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
                                                         int32_t max_rows, const int32_t *__restrict__ order,
-                                                        int32_t *__restrict__ caps) {
+                                                        int32_t *__restrict__ caps, BlatSpill spill) {
     DpLds &D = g_dp;
     BlatLds &B = g_bl;
     const int lane = threadIdx.x;
@@ -727,13 +727,22 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                     o.t_start = firstp.tb; o.t_end = lastp.te;
                     o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
                     if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10) {
-                        // the strand's best max_rows rows in psl_before order (stable), all counted
+                        // the strand's best max_rows rows in psl_before order (stable), all counted;
+                        // the row that falls off the list goes to the spill pool
                         const int n = B.nrow < max_rows ? B.nrow : max_rows;
                         int at = n;
                         while (at > 0 && psl_before(o, RW[at - 1])) --at;
-                        if (at < max_rows) {
+                        af_psl out = o;
+                        bool off = at >= max_rows;
+                        if (!off) {
+                            if (n == max_rows) { out = RW[max_rows - 1]; off = true; }
                             for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) RW[x] = RW[x - 1];
                             RW[at] = o;
+                        }
+                        if (off && spill.cap > 0) {
+                            const int k = atomicAdd(spill.n, 1);
+                            if (k < spill.cap) { spill.rows[k] = out; spill.query[k] = (int32_t)qi; }
+                            else if (caps) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
                         }
                         ++B.nrow;
                     }
@@ -845,7 +854,7 @@ struct MinU32 {
 __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__restrict__ stage_n,
                              const int32_t *__restrict__ n_q, const int32_t *__restrict__ q_first, int64_t cap,
                              int32_t max_rows, af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
-                             int32_t *__restrict__ caps) {
+                             int32_t *__restrict__ caps, BlatSpill spill) {
     const int64_t nq = *n_q < cap ? *n_q : cap;
     const int64_t q0 = q_first ? max((int64_t)0, min((int64_t)*q_first, nq)) : 0;
     const int64_t qi = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -853,7 +862,7 @@ __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__
     const af_psl *A = stage + 2 * qi * max_rows, *Bs = A + max_rows;
     const int sa = stage_n[2 * qi], sb = stage_n[2 * qi + 1];
     const int na = sa < max_rows ? sa : max_rows, nb = sb < max_rows ? sb : max_rows;
-    if (caps && sa + sb > max_rows) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
+    if (caps && sa + sb > max_rows && spill.cap <= 0) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
 #ifdef AF_BLAT_CHECK
     if (na < 0 || nb < 0) {
         printf("k_blat_merge: query %ld rows %d %d\n", (long)qi, na, nb);
@@ -866,6 +875,15 @@ __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__
         rows[qi * max_rows + k] = take_b ? Bs[j++] : A[i++];
     }
     n_rows[qi] = k;
+    // the strands' kept rows that the merge leaves out follow the max_rows taken: to the pool
+    if (spill.cap > 0) {
+        for (; i < na || j < nb;) {
+            const af_psl &r = j < nb && (i >= na || psl_before(Bs[j], A[i])) ? Bs[j++] : A[i++];
+            const int x = atomicAdd(spill.n, 1);
+            if (x < spill.cap) { spill.rows[x] = r; spill.query[x] = (int32_t)qi; }
+            else if (caps) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
+        }
+    }
 }
 
 // the queries' forward tile hits (tiles over repMatch excluded): the scheduling key of k_blat,
@@ -925,7 +943,8 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
                           int64_t cap,
                           int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
                           uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, hipStream_t s) {
+                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, const BlatSpill &spill,
+                          hipStream_t s) {
     // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
     int bits = 64 - __builtin_clzll((unsigned long long)(X.n + 1024));
     const int diag_passes = (bits + 7) / 8;
@@ -933,14 +952,14 @@ hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_
     dim3 g(n_slots), b(64);
 #define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, q_first, cap, \
                                     heads, \
-                                    bscratch, diag_passes, stage, stage_n, max_rows, order, caps)
+                                    bscratch, diag_passes, stage, stage_n, max_rows, order, caps, spill)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
     hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, stage, stage_n, n_queries,
-                       q_first, cap, max_rows, rows, n_rows, caps);
+                       q_first, cap, max_rows, rows, n_rows, caps, spill);
     return hipGetLastError();
 }
 

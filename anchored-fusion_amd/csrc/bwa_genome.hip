@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     bool ovf = false, rev = false;
     int64_t rr = -1, min_intv = 1, ik_k = 0, ik_l = 0, ik_s = 0, last_s = 0;
     const uint8_t *rd = nullptr;
-    GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0;)
+    GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0; int gp_fwd = 0, gp_bwd = 0, gp_ss = 0;)
     auto code = [&](int t) -> int { return nt4(rd[t]); };
     auto push_curr = [&](int64_t k, int64_t l, int64_t s, int qb, int qe) { Lc[nc++] = g1_pack(k, l, s, qb, qe); };
     auto smem_start = [&](int x0, int64_t mi, int ps) {
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                     rd = reads + rr * (int64_t)stride;
                     ni = 0; ovf = false; x = 0;
                     st = len >= msl ? G1_P1 : G1_DONE;
-                    GPROF(gp_c0 = clock64(); gp_t0 = gp_rt();)
+                    GPROF(gp_c0 = clock64(); gp_t0 = gp_rt(); gp_fwd = gp_bwd = gp_ss = 0;)
                 }
             }
         }
@@ -310,7 +310,8 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                     }
                 }
                 GPROF({ int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0); g[1] = ovf ? -1 : ni;
-                        g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid; } })
+                        g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid;
+                        g[19] = gp_fwd; g[21] = gp_bwd; g[22] = gp_ss; } })
                 st = G1_IDLE;
             }
         }
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         int64_t rk = 0, rl = 0, rs = 0;
         if (need) fm_ext1(G, ek, el, es, ec, efwd, rk, rl, rs);
         if (!need) continue;
+        GPROF(if (st == G1_FWD) ++gp_fwd; else if (st == G1_BWD) ++gp_bwd; else ++gp_ss;)
         if (st == G1_FWD) {
             if (rs != ik_s) {
                 push_curr(ik_k, ik_l, ik_s, 0, ik_qe);

@@ -105,6 +105,34 @@ class CandidateDiscovery:
                        over=z(1))
         self.t_rows = z(self.qcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
         self.t_nh = z(self.qcap)
+        # S6 rows past MAX_ROWS per query (BLAT prints them all; fn:630-649 reads every one):
+        # af_blat_spill's pool, counted in the summary
+        spill_cap = max(1 << 16, self.qcap // 2)
+        self.t_spill = dict(rows=z(spill_cap * _blat.PSL_DTYPE.itemsize, dt=torch.uint8), q=z(spill_cap), n=z(1))
+
+    def _s6_search(self, stream):
+        """S6 (`blat -minScore=20 genome split.fa`, fn:530) of the survivors' rows: MAX_ROWS per
+        query in t_rows, the rest in the spill pool (registered for this search only: the tile
+        reference may serve other searches)."""
+        import torch
+        with torch.cuda.stream(stream):
+            self.t_spill["n"].zero_()
+        sp = self.t_spill
+        self.tiles_ref.spill_to(sp["rows"], sp["q"], sp["n"])
+        try:
+            self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
+                                         lens_t=self.s6["lens"], p=self.p_tail, stream=stream)
+        finally:
+            self.tiles_ref.spill_to()
+
+    def s6_spilled(self):
+        """{S6 query: [its rows past MAX_ROWS]} of the last search, in row order (synchronises)."""
+        import torch
+        torch.cuda.synchronize(self.dev)
+        sp = self.t_spill
+        n = min(int(sp["n"].item()), int(sp["q"].numel()))
+        rows = sp["rows"][:n * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
+        return _blat.spilled_rows(rows, sp["q"][:n].cpu().numpy())
 
     def close(self):
         self.grp.close()
@@ -172,8 +200,7 @@ class CandidateDiscovery:
                                  stream=s0)
         # S6 (`blat -minScore=20 genome split.fa`, fn:530) beside S4's records
         s6.wait_stream(s0)
-        self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
-                                     lens_t=self.s6["lens"], p=self.p_tail, stream=s6)
+        self._s6_search(s6)
         s0.wait_stream(s6)
         s0.wait_stream(spe)
         if _DEBUG:
@@ -265,14 +292,16 @@ class CandidateDiscovery:
         _genome.s5_filter_device(self.ref.ctx, recs[b * w:], self.q_nh[b:], n5, self.q[b:], self.L, self.q_lens[b:],
                                  self.q_rows[b:], self.out, self.qcap, self.s6["q"], self.s6["lens"], self.s6["src"],
                                  self.s6["n"], self.s6["over"], stream=s0, cont_t=cont_t)
-        self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
-                                     lens_t=self.s6["lens"], p=self.p_tail, stream=s0)
+        self._s6_search(s0)
         s0.synchronize()
         n6 = int(self.s6["n"].item())
         self.counts["s6_queries"] = n6
+        ns = min(int(self.t_spill["n"].item()), int(self.t_spill["q"].numel()))
         return dict(src=self.s6["src"][:n6], s6_seq=self.s6["q"][:n6], s6_len=self.s6["lens"][:n6],
                     psl=self.t_rows[:n6 * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize].view(torch.int32),
-                    n_psl=self.t_nh[:n6])
+                    n_psl=self.t_nh[:n6],
+                    spill_psl=self.t_spill["rows"][:ns * _blat.PSL_DTYPE.itemsize].view(torch.int32),
+                    spill_q=self.t_spill["q"][:ns])
 
     def s4_phase(self, q, ql, pair_base=0):
         """S4 over whole bwa chunks of the globally zipped pairs: reads q uint8 [2P, w] pair-major,
@@ -291,8 +320,8 @@ class CandidateDiscovery:
         s0.synchronize()
         return recs_t, nrec_t
 
-    def psl_lines(self, queries, rows, nrows):
-        return _blat.psl_lines(self.tiles_ref, queries, rows, nrows)
+    def psl_lines(self, queries, rows, nrows, extra=None):
+        return _blat.psl_lines(self.tiles_ref, queries, rows, nrows, extra=extra)
 
     def summary(self):
         """Host-side counts of the last pass (synchronises)."""
@@ -308,6 +337,7 @@ class CandidateDiscovery:
         c.update(queries_s4_s5=nq, queries_placed=int(((first & 4) == 0).sum()) if nq else 0,
                  genome_records=int(self.q_nh[:nq].sum().item()), s6_queries=n6,
                  s6_placed=int((tn > 0).sum()), s6_at_row_cap=int((tn >= _blat.MAX_ROWS).sum()),
+                 s6_rows_spilled=int(self.t_spill["n"].item()),
                  s6_clipped=int(self.s6["over"].item()),
                  mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()),
                  s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))

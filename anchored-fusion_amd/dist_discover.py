@@ -226,8 +226,14 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     P6 = _t(surv["psl"], dev).view(torch.int32).reshape(ns, MAX_ROWS, PSL_WORDS)
     kk, rr = torch.nonzero(torch.arange(P6.shape[1], device=dev)[None, :] < npsl[:, None], as_tuple=True)
     table = torch.cat([_words(ords[kk]), P6[kk, rr]], dim=1)
+    # the rows past MAX_ROWS (the backend's spill pool), tagged with their query's ordinal
+    sq = _t(surv["spill_q"], dev, torch.int64) if "spill_q" in surv else torch.zeros(0, dtype=torch.int64, device=dev)
+    SP = _t(surv["spill_psl"], dev).view(torch.int32).reshape(-1, PSL_WORDS) if "spill_psl" in surv else \
+        torch.zeros((0, PSL_WORDS), dtype=torch.int32, device=dev)
+    sp_table = torch.cat([_words(ords[sq]), SP], dim=1)
     all_rows = _gatherv(rows, group, world, rank)
     all_psl = _gatherv(table, group, world, rank)
+    all_spill = _gatherv(sp_table, group, world, rank)
     # S4's stream: tmp1 / tmp2 of every rank zipped in the global order, from their keys alone
     t1, t2 = L.t1, L.t2
     k1, r1, l1 = _t(t1["key"], dev, torch.int64), _t(t1["row"], dev, torch.int64) + g0, _t(t1["len"], dev, torch.int64)
@@ -280,7 +286,7 @@ def search(backend, lo, rank, world, group=None, device="cpu", names=None, host_
     order = torch.argsort(_i64(all_rows[:, :2]), stable=True)
     porder = torch.argsort(_i64(all_psl[:, :2]), stable=True)
     return dict(s4=(q_all, ql, recs, nrec, g1), surv=all_rows[order], psl=all_psl[porder], w=(w5, w6), names=named,
-                max_rows=MAX_ROWS), counts
+                max_rows=MAX_ROWS, spill=all_spill), counts
 
 
 def _s4_reads(t1, t2, r1, r2, g1, g2, shares, starts, W4, rank, world, group, dev):
@@ -318,7 +324,7 @@ def render(result, backend, gene, genome_names, s4_text=True):
     """What consume_products reads, from search's rank-0 result (searched with names, and with
     s4_reads for s4_text): S4's SAM lines (blocks.S4Records, the fields Find_blocks reads,
     without s4_text), the split_sam lines of the survivors (split.fa order) and S6's PSL."""
-    from .blat import PSL_DTYPE
+    from .blat import PSL_DTYPE, spilled_rows
     from .blocks import S4Records
     from .genome import REC_DTYPE
     q, ql, recs, nrec, g1 = result["s4"]
@@ -363,6 +369,13 @@ def render(result, backend, gene, genome_names, s4_text=True):
             if m:
                 rows[k, :m] = table[r:r + m, 2:].copy().view(PSL_DTYPE).reshape(m)
             r += m
+        extra = {}
+        sp = result.get("spill")
+        if sp is not None and len(sp):
+            sp = sp.cpu().numpy()
+            at = {int(o): k for k, o in enumerate(S[:, :2].copy().view(np.int64).reshape(-1))}
+            qk = np.array([at[int(o)] for o in sp[:, :2].copy().view(np.int64).reshape(-1)], np.int64)
+            extra = spilled_rows(sp[:, 2:].copy().view(PSL_DTYPE).reshape(-1), qk)
         psl = PSL_HEADER + backend.psl_lines([(str(k), s6[k, :l6[k]].tobytes().decode()) for k in range(n)], rows,
-                                             npsl)
+                                             npsl, extra=extra)
     return s4, split_sam, psl

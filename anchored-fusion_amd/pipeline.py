@@ -291,7 +291,7 @@ def device_products(d, gene, names, genome_names, s4_text=False):
         t_rows = d.t_rows[:n6 * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize].cpu().numpy().view(blat.PSL_DTYPE)
         psl = ["psLayout version 3\n", "\n"] + blat.psl_lines(
             d.tiles_ref, [(str(k), s6q[k, :s6l[k]].tobytes().decode()) for k in range(n6)],
-            t_rows.reshape(n6, blat.MAX_ROWS), d.t_nh[:n6].cpu().numpy())
+            t_rows.reshape(n6, blat.MAX_ROWS), d.t_nh[:n6].cpu().numpy(), extra=d.s6_spilled())
     return s4, split_sam, psl
 
 

@@ -77,10 +77,11 @@ class Placer:
         lines = [[] for _ in queries]
         short = [i for i, (_, sq) in enumerate(queries) if len(sq) <= _lib.AF_MAX_READ]
         longs = [i for i, (_, sq) in enumerate(queries) if len(sq) > _lib.AF_MAX_READ]
-        if short:
-            rows, nr = ref.search([queries[i][1] for i in short], p, blat.MAX_ROWS)
+        if short:  # every row of each query (the rows past MAX_ROWS from the search's spill pool)
+            rows, nr, extra = ref.search_all([queries[i][1] for i in short], p)
             for k, i in enumerate(short):
-                lines[i] = blat.psl_lines(ref, [queries[i]], rows[k:k + 1], nr[k:k + 1])
+                lines[i] = blat.psl_lines(ref, [queries[i]], rows[k:k + 1], nr[k:k + 1],
+                                          extra={0: extra[k]} if k in extra else None)
         if longs:
             pw = blat.params(preset, min_score=0, min_identity=0)
             pieces = [stitch.windows(queries[i][1]) for i in longs]

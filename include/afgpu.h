@@ -214,11 +214,22 @@ int af_blat_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, c
 int af_blat_device_range(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_first,
                          const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
                          const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
+/* A device pool for the rows past max_rows (BLAT prints every row; the fixed per-query row slots
+ * keep the first max_rows): once registered on ctx, every later af_blat_device(_range) call on ctx
+ * appends each query's rows past its first max_rows to d_rows[k] with d_query[k] = the query's
+ * index, k from the device counter *d_n (the caller zeroes it; k >= cap: the row is dropped and
+ * counted in AF_BLAT_CAP_ROWS).  Spilled rows come in no particular order; in the search's order
+ * (best score first, the af_blat order) every one of them follows the query's max_rows kept rows.
+ * d_rows == NULL or cap == 0 unregisters.
+ * (BLAT prints all of a query's alignments, which functions.py:630-649 reads one by one.) */
+int af_blat_spill(af_ctx *ctx, af_psl *d_rows, int32_t *d_query, int32_t *d_n, int64_t cap);
 /* How often the search's fixed caps bound (BLAT itself has none), counted per query strand on the
  * context since the last reset: [HITS] tile hits past 32768 (the first 32768 in query order are
- * clumped), [CLUMPS] 4096 clumps reached (the first in diagonal order kept), [PARTS] 16 aligned
- * parts reached with clumps left; per query: [ROWS] rows past max_rows dropped.  Synchronises;
- * reset != 0 zeroes the counters after reading. */
+ * clumped), [CLUMPS] 4096 clumps reached (the first in diagonal order kept), [PARTS] the stitching
+ * work budget reached (the chain DP's rescans after emitted chains; no further chain emitted --
+ * every clump is aligned, parts have no cap of their own); [ROWS] without a spill pool: queries
+ * with rows past max_rows dropped, with one: rows dropped because the pool was full.
+ * Synchronises; reset != 0 zeroes the counters after reading. */
 #define AF_BLAT_CAP_HITS 0
 #define AF_BLAT_CAP_CLUMPS 1
 #define AF_BLAT_CAP_PARTS 2

@@ -448,7 +448,8 @@ int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int3
 int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
                   const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads,
                   int32_t *caps) {
-    if (!X || max_rows < 1 || max_rows > AFO_BLAT_MAX_ROWS || bp->step_size != X->step) return -1;
+    /* max_rows up to MAXP: every row of a query (the GPU's kept rows + its spill pool, tests) */
+    if (!X || max_rows < 1 || max_rows > MAXP || bp->step_size != X->step) return -1;
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads > 0 ? threads : 1)
     for (int64_t qi = 0; qi < n_queries; ++qi) {
         int L = lens ? lens[qi] : stride;
@@ -463,7 +464,9 @@ int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries,
         }
         hit_t *hits = (hit_t *)malloc(sizeof(hit_t) * MAXH);
         reg_b *regs = (reg_b *)malloc(sizeof(reg_b) * MAXP);
-        afo_psl cand[2][AFO_BLAT_MAX_ROWS];
+        afo_psl *cand[2];
+        cand[0] = (afo_psl *)malloc(sizeof(afo_psl) * 2 * (size_t)max_rows);
+        cand[1] = cand[0] + max_rows;
         int nc[2] = {0, 0};
         int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
         for (int s = 0; s < 2; ++s) {
@@ -493,6 +496,7 @@ int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries,
             rows[qi * max_rows + k] = take_b ? cand[1][j++] : cand[0][i++];
         }
         n_rows[qi] = k;
+        free(cand[0]);
     }
     return 0;
 }

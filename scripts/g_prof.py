@@ -64,6 +64,17 @@ for c in range(min(ncalls, 4)):
     g1 = B[:, 0] & 0xFFFFFFFF
     print(f"  G1 cycles/read mean {g1.mean():.0f} p50 {pct(g1, 50):.0f} p90 {pct(g1, 90):.0f} p99 {pct(g1, 99):.0f} "
           f"max {g1.max()}; intervals/read mean {B[:, 1].mean():.1f} max {B[:, 1].max()}")
+    ext = B[:, 19] + B[:, 21] + B[:, 22]
+    print(f"  G1 FM extensions/read mean {ext.mean():.0f} p50 {pct(ext, 50):.0f} p99 {pct(ext, 99):.0f} max {ext.max()}; "
+          f"shares fwd {B[:, 19].sum() / max(ext.sum(), 1):.3f} bwd {B[:, 21].sum() / max(ext.sum(), 1):.3f} "
+          f"seed-strategy {B[:, 22].sum() / max(ext.sum(), 1):.3f}; total {ext.sum()}")
+    s1 = np.argsort(-g1)
+    print("  G1 slowest: cycles wall_us | fwd bwd ss | len intervals")
+    for i in s1[:8]:
+        r = B[i]
+        print(f"   {g1[i]:>11d} {((r[18] - r[17]) & 0xFFFFFFFF) / 100:8.1f} | {r[19]} {r[21]} {r[22]} | {r[2]} {r[1]}")
+    cyc_per_ext = g1 / np.maximum(ext, 1)
+    print(f"  G1 cycles per extension p50 {pct(cyc_per_ext, 50):.0f} p90 {pct(cyc_per_ext, 90):.0f}")
     lanes = B[:, 20]
     lane_sum = np.bincount(lanes, weights=g1)
     print(f"  G1 per-lane cycles: mean {lane_sum[lane_sum > 0].mean():.0f} max {lane_sum.max():.0f}")

@@ -5,6 +5,8 @@ They let the end-to-end pipeline (anchored_fusion_amd.pipeline) run on CPU in th
 """
 import bisect
 
+import numpy as np
+
 import afpkg  # noqa: F401
 import oracle
 from anchored_fusion_amd.align import AlignResult
@@ -26,6 +28,14 @@ class OracleTileReference:
         buf, lens = pack_queries(seqs)
         op = oracle.blat_params(**{f: getattr(p, f) for f, _ in p._fields_})
         return self.tiles.blat(buf, lens, op, max_rows, threads=8)
+
+    def search_all(self, seqs, p, all_rows=256):
+        """TileReference.search_all's contract on the oracle: the first MAX_ROWS rows per query and
+        the rest (up to all_rows) as {query: [rows]}."""
+        from anchored_fusion_amd.blat import MAX_ROWS
+        rows, nr = self.search(seqs, p, all_rows)
+        extra = {k: list(rows[k, MAX_ROWS:int(c)]) for k, c in enumerate(nr) if c > MAX_ROWS}
+        return rows[:, :MAX_ROWS].copy(), np.minimum(nr, MAX_ROWS).astype(np.int32), extra
 
     def caps(self, reset=True):
         from anchored_fusion_amd.blat import CAP_NAMES

@@ -6,6 +6,8 @@ the host restatements the consumer stages use (align.partition, genome_check, bl
 distributed driver can be checked on CPU with gloo against the one-process host path."""
 import numpy as np
 
+ALL_ROWS = 256  # rows per S6 query the oracle backend keeps (the GPU: MAX_ROWS + its spill pool)
+
 import afpkg  # noqa: F401
 import oracle
 from anchored_fusion_amd import blat, blocks, genome, genome_check
@@ -96,12 +98,20 @@ class OracleDiscovery:
         out["s6_seq"] = _rows([np.frombuffer(x.encode(), np.uint8) for x in seqs])
         out["s6_len"] = np.array([len(x) for x in seqs], np.int32)
         if fa:
-            rows, out["n_psl"] = self.tiles.search(seqs, blat.params("split_tail"), blat.MAX_ROWS)
-            out["psl"] = rows.view(np.int32).reshape(len(seqs), blat.MAX_ROWS, -1)
+            # every row (up to ALL_ROWS): the first MAX_ROWS kept, the rest as the GPU's spill pool
+            allr, alln = self.tiles.search(seqs, blat.params("split_tail"), ALL_ROWS)
+            M = blat.MAX_ROWS
+            out["n_psl"] = np.minimum(alln, M).astype(np.int32)
+            out["psl"] = np.ascontiguousarray(allr[:, :M]).view(np.int32).reshape(len(seqs), M, -1)
+            sq = np.concatenate([np.full(max(0, int(c) - M), k, np.int64) for k, c in enumerate(alln)] +
+                                [np.zeros(0, np.int64)])
+            sr = np.concatenate([allr[k, M:int(c)] for k, c in enumerate(alln)] + [allr[:0, 0]])
+            out["spill_q"] = sq
+            out["spill_psl"] = np.ascontiguousarray(sr).view(np.int32).reshape(len(sr), blat.PSL_DTYPE.itemsize // 4)
         return out
 
-    def psl_lines(self, queries, rows, nrows):
-        return blat.psl_lines(self.tiles, queries, np.stack(rows), np.asarray(nrows))
+    def psl_lines(self, queries, rows, nrows, extra=None):
+        return blat.psl_lines(self.tiles, queries, np.stack(rows), np.asarray(nrows), extra=extra)
 
 
 def _np(x):

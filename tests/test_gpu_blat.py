@@ -271,3 +271,30 @@ def test_blat_edge_cases():
         rg, ng = g.search([], p)
         assert len(ng) == 0
         g.close()
+
+
+def test_blat_spill_rows_equal_oracle_all_rows():
+    """Rows past MAX_ROWS (af_blat_spill; TileReference.search_all, every BLAT call of the Placer
+    and S6): the kept rows followed by the spilled ones in row order equal the oracle's full row
+    list (max_rows 256), field by field; nothing is counted as dropped."""
+    from anchored_fusion_amd import blat
+    from test_blat_caps import family_world
+    ctgs, qs = family_world()
+    rng = np.random.default_rng(8)
+    qs = qs + [q[int(a):int(a) + 150] for q, a in zip(qs * 3, rng.integers(0, 80, 6))]
+    p = blat.params("split_tail")
+    g = _gpu_ref(ctgs, p.step_size)
+    o = OracleTileReference(ctgs, p.step_size)
+    try:
+        g.caps()
+        rows, nr, extra = g.search_all(qs, p)
+        ro, no = o.search(qs, p, 256)
+        assert g.caps()["rows"] == 0
+        assert (no > blat.MAX_ROWS).sum() >= 2 and (no < 256).all()
+        for q in range(len(qs)):
+            got = [rows[q, k] for k in range(nr[q])] + extra.get(q, [])
+            assert len(got) == no[q], (q, len(got), no[q])
+            for k, r in enumerate(got):
+                assert r.tobytes() == ro[q, k].tobytes(), (q, k)
+    finally:
+        g.close()
