@@ -12,6 +12,9 @@
 #ifndef AF_G1_WPS
 #define AF_G1_WPS 4             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish
 #endif
+#ifndef AF_G1_HEAVY_EXT
+#define AF_G1_HEAVY_EXT 2048    // G1: a read past this many FM extensions moves to the wave-per-read kernel (env AF_G1_HEAVY_EXT)
+#endif
 #ifndef AF_G_HEAVY_CHAINS
 #define AF_G_HEAVY_CHAINS 16    // G2: reads with this many kept chains extend them one job per chain (env AF_G_HEAVY_CHAINS)
 #endif
@@ -238,6 +241,11 @@ struct GWork {
     int32_t *heads;             // G2 dequeue heads (8 lines)
     int32_t *stats;             // AF_GSTAT_*
     unsigned long long *g1_next;  // G1: the next read to hand to an idle lane
+    // G1's heavy reads: a lane whose read needs more than g1_max_ext FM extensions hands it to
+    // k_g_seeds_wave (one wave per read) through g1_hv[0, *g1_hv_n); 0 = never
+    int64_t *g1_hv = nullptr;
+    unsigned long long *g1_hv_n = nullptr, *g1_hv_next = nullptr;
+    int32_t g1_max_ext = 0;
     GHeavy hv;
 };
 size_t af_g1_slot_bytes();

@@ -77,6 +77,8 @@ struct af_ctx {
     // G2's heavy-read pools (GHeavy) and the kept-chain count from which a read is heavy
     GHeavy g_hv{};
     int32_t g_heavy_min = AF_G_HEAVY_CHAINS;
+    int32_t g1_max_ext = AF_G1_HEAVY_EXT;
+    int64_t *g1_hv = nullptr;       // G1's heavy-read list (ensure_genome_pools)
     GIv *g_iv = nullptr;
     GReg *g_reg = nullptr;
     int64_t g_iv_cap = 0, g_reg_cap = 0, g_cap_reads = 0;
@@ -391,7 +393,7 @@ int ensure_genome_scratch(af_ctx *c) {
     c->g2_waves = std::min(c->n_cu * 8, c->n_slots);
     HIPCHK(c, hipMalloc(&c->g1_scr, af_g1_slot_bytes() * (size_t)c->g1_threads));
     HIPCHK(c, hipMalloc(&c->g2_scr, af_g2_slot_bytes() * (size_t)c->g2_waves));
-    HIPCHK(c, hipMalloc(&c->g_iv_fill, 2 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMalloc(&c->g_iv_fill, 4 * sizeof(unsigned long long)));  // iv fill, G1 next, G1 heavy count / next
     HIPCHK(c, hipMalloc(&c->g_reg_fill, sizeof(int32_t)));
     HIPCHK(c, hipMalloc(&c->g_stats, sizeof(int32_t) * AF_GSTAT_N));
     HIPCHK(c, hipMemset(c->g_stats, 0, sizeof(int32_t) * AF_GSTAT_N));
@@ -405,9 +407,9 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     // the region pool's fill and offsets are int32 (at most 16 regions per read on average)
     if (n_reads > INT32_MAX / 16 - AF_G_MAX_REG) return fail(c, AF_E_INVALID, "too many reads for one genome call");
     af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_off); af_free(c->g_iv_n); af_free(c->g_reg_off);
-    af_free(c->g_reg_n);
+    af_free(c->g_reg_n); af_free(c->g1_hv);
     c->g_iv = nullptr; c->g_reg = nullptr; c->g_iv_off = nullptr; c->g_iv_n = nullptr; c->g_reg_off = nullptr;
-    c->g_reg_n = nullptr; c->g_cap_reads = 0;
+    c->g_reg_n = nullptr; c->g1_hv = nullptr; c->g_cap_reads = 0;
     const int64_t cap = std::max<int64_t>(n_reads, 1 << 14);
     c->g_iv_cap = cap * 96 + AF_G_MAX_INTV;
     c->g_reg_cap = cap * 16 + AF_G_MAX_REG;
@@ -417,6 +419,7 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     HIPCHK(c, hipMalloc(&c->g_iv_n, sizeof(int32_t) * cap));
     HIPCHK(c, hipMalloc(&c->g_reg_off, sizeof(int32_t) * cap));
     HIPCHK(c, hipMalloc(&c->g_reg_n, sizeof(int32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->g1_hv, sizeof(int64_t) * cap));
     // heavy reads: at most every read; 8 pooled chains and 16 seeds per read of the call (a read
     // that does not fit is extended by its own wave)
     GHeavy &h = c->g_hv;
@@ -444,6 +447,8 @@ GWork genome_work(af_ctx *c) {
     w.reg_n = c->g_reg_n;
     w.heads = c->ctrl + AF_CTRL_G_HEADS;
     w.g1_next = c->g_iv_fill + 1;
+    w.g1_hv = c->g1_hv; w.g1_hv_n = c->g_iv_fill + 2; w.g1_hv_next = c->g_iv_fill + 3;
+    w.g1_max_ext = c->g1_hv ? c->g1_max_ext : 0;
     w.hv = c->g_hv;
     w.hv.min_chains = c->g_hv.cnt ? c->g_heavy_min : 0;
     w.stats = c->g_stats;
@@ -554,6 +559,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
+    if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -582,7 +588,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g_hv.ch); af_free(c->g_hv.sd); af_free(c->g_hv.res); af_free(c->g_hv.cnt);
     if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
-    af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n);
+    af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n); af_free(c->g1_hv);
     af_free(c->g_iv_off); af_free(c->g_ghist); af_free(c->g_nchunks); af_free(c->g_cstart); af_free(c->g_scan);
     af_free(c->g_pes); af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens); af_free(c->g_hreads);
     af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_nsel); af_free(c->s5_temp);

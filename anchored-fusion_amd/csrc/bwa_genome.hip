@@ -60,11 +60,16 @@ struct GKb { int16_t n, internal; int16_t key[G_KB_MAXK]; int16_t ptr[G_KB_MAXK 
 // counts and 128 2-bit symbols (symbol t of a 32-bit word at bits 2t, 2t + 1); the symbols
 // below row i are counted for all four bases at once from three popcounts per word (low bits,
 // high bits, both): T = both, G = high - T, C = low - T, A = the rest.
-__device__ __forceinline__ void fm_occ4(const DevGenome &G, int64_t i, int64_t o[4]) {
+struct OccBlk { uint4 c01, c23, w01, w23; };
+__device__ __forceinline__ OccBlk fm_blk(const DevGenome &G, int64_t b) {
+    const uint4 *blk = reinterpret_cast<const uint4 *>(G.occ + b * 8);
+    return OccBlk{blk[0], blk[1], blk[2], blk[3]};
+}
+// occ of row i from its (loaded) block
+__device__ __forceinline__ void fm_occ4b(const DevGenome &G, const OccBlk &B, int64_t i, int64_t o[4]) {
     const int64_t b = i >> 7;
     const int r = (int)(i & 127);
-    const uint4 *blk = reinterpret_cast<const uint4 *>(G.occ + b * 8);
-    const uint4 c01 = blk[0], c23 = blk[1], w01 = blk[2], w23 = blk[3];
+    const uint4 c01 = B.c01, c23 = B.c23, w01 = B.w01, w23 = B.w23;
     const uint32_t wv[8] = {w01.x, w01.y, w01.z, w01.w, w23.x, w23.y, w23.z, w23.w};
     uint32_t nlo = 0, nhi = 0, n11 = 0;
 #pragma unroll
@@ -83,6 +88,9 @@ __device__ __forceinline__ void fm_occ4(const DevGenome &G, int64_t i, int64_t o
     o[3] = (int64_t)((uint64_t)c23.z | (uint64_t)c23.w << 32) + (int)n11;
     if (G.primary >= (b << 7) && G.primary < i) o[0] -= 1;  // the '$' row is stored as A
 }
+__device__ __forceinline__ void fm_occ4(const DevGenome &G, int64_t i, int64_t o[4]) {
+    fm_occ4b(G, fm_blk(G, i >> 7), i, o);
+}
 __device__ __forceinline__ int64_t sel4(const int64_t v[4], int c) {
     return c == 0 ? v[0] : c == 1 ? v[1] : c == 2 ? v[2] : v[3];
 }
@@ -93,8 +101,15 @@ __device__ __forceinline__ void fm_ext1(const DevGenome &G, int64_t k, int64_t l
                                        int64_t &ok, int64_t &ol, int64_t &os) {
     if (fwd) { const int64_t t = k; k = l; l = t; }
     int64_t a[4], b[4];
-    fm_occ4(G, k, a);
-    fm_occ4(G, k + s, b);
+    // rows k and k + s: one 64-B block when both fall in it (a narrow interval), else two
+    if (((k + s) >> 7) == (k >> 7)) {
+        const OccBlk B = fm_blk(G, k >> 7);
+        fm_occ4b(G, B, k, a);
+        fm_occ4b(G, B, k + s, b);
+    } else {
+        fm_occ4(G, k, a);
+        fm_occ4(G, k + s, b);
+    }
     int64_t lo = l + (k <= G.primary && k + s - 1 >= G.primary);
 #pragma unroll
     for (int d = 3; d > 0; --d)
@@ -153,6 +168,9 @@ __device__ __forceinline__ G1Iv g1_unpack(uint4 v) {
     r.qe = (int)(v.w >> 12 & 511);
     return r;
 }
+#ifndef G1_PC
+#define G1_PC 1  // prev entries the backward scan holds in registers
+#endif
 enum : int { G1_IDLE, G1_P1, G1_FWD, G1_BWD, G1_P2, G1_P3, G1_SS, G1_DONE, G1_EXIT };
 
 __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const uint8_t *__restrict__ reads,
@@ -175,6 +193,12 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     bool ovf = false, rev = false;
     int64_t rr = -1, min_intv = 1, ik_k = 0, ik_l = 0, ik_s = 0, last_s = 0;
     const uint8_t *rd = nullptr;
+    // bwt_smem1's backward scan reads prev's entries in order: G1_PC at a time into registers (one
+    // memory wait per G1_PC entries instead of one per entry); pc0 = the first cached entry's
+    // index in scan order, -1 none (prev is swapped at each position: the cache is dropped)
+    uint4 pcache[G1_PC];
+    int pc0 = -1;
+    int ne = 0;  // the read's FM extensions so far (past w.g1_max_ext: handed to k_g_seeds_wave)
     GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0; int gp_fwd = 0, gp_bwd = 0, gp_ss = 0;)
     auto code = [&](int t) -> int { return nt4(rd[t]); };
     auto push_curr = [&](int64_t k, int64_t l, int64_t s, int qb, int qe) { Lc[nc++] = g1_pack(k, l, s, qb, qe); };
@@ -188,7 +212,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     auto fwd_end = [&]() {  // curr holds the forward intervals in push order (bwa reverses them)
         ret = (int)g1_unpack(Lc[nc - 1]).qe;
         uint4 *t = Lp; Lp = Lc; Lc = t;
-        np = nc; nc = 0; rev = true; i = sx - 1; j = 0;
+        np = nc; nc = 0; rev = true; i = sx - 1; j = 0; pc0 = -1;
         st = G1_BWD;
     };
     auto take = [&](const G1Iv &m) -> bool {  // an interval into the read's list
@@ -225,7 +249,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 else {
                     len = read_len(lens, rr, stride);
                     rd = reads + rr * (int64_t)stride;
-                    ni = 0; ovf = false; x = 0;
+                    ni = 0; ovf = false; x = 0; ne = 0;
                     st = len >= msl ? G1_P1 : G1_DONE;
                     GPROF(gp_c0 = clock64(); gp_t0 = gp_rt(); gp_fwd = gp_bwd = gp_ss = 0;)
                 }
@@ -251,10 +275,25 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 if (j == np) {
                     if (nc == 0) { smem_end(); continue; }
                     uint4 *t = Lp; Lp = Lc; Lc = t;
-                    np = nc; nc = 0; rev = false; --i; j = 0;
+                    np = nc; nc = 0; rev = false; --i; j = 0; pc0 = -1;
                     continue;
                 }
-                pv = g1_unpack(Lp[rev ? np - 1 - j : j]);
+                if (pc0 < 0 || j < pc0 || j >= pc0 + G1_PC) {
+                    pc0 = j;
+#pragma unroll
+                    for (int u = 0; u < G1_PC; ++u) {
+                        const int jj = j + u < np ? j + u : np - 1;
+                        pcache[u] = Lp[rev ? np - 1 - jj : jj];
+                    }
+                }
+                {
+                    const int u = j - pc0;
+                    uint4 e = pcache[0];
+#pragma unroll
+                    for (int v = 1; v < G1_PC; ++v)
+                        if (u == v) e = pcache[v];
+                    pv = g1_unpack(e);
+                }
                 const int c = i < 0 ? -1 : code(i);
                 if (c < 0 || c > 3) { mem_push(pv, i + 1); ++j; continue; }
                 need = true; ek = pv.k; el = pv.l; es = pv.s; ec = c; efwd = false; p_qe = pv.qe;
@@ -320,6 +359,11 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         int64_t rk = 0, rl = 0, rs = 0;
         if (need) fm_ext1(G, ek, el, es, ec, efwd, rk, rl, rs);
         if (!need) continue;
+        if (w.g1_max_ext > 0 && ++ne > w.g1_max_ext) {  // a heavy read: restarted by k_g_seeds_wave
+            w.g1_hv[atomicAdd(w.g1_hv_n, 1ull)] = rr;
+            st = G1_IDLE;
+            continue;
+        }
         GPROF(if (st == G1_FWD) ++gp_fwd; else if (st == G1_BWD) ++gp_bwd; else ++gp_ss;)
         if (st == G1_FWD) {
             if (rs != ik_s) {
@@ -337,6 +381,203 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 if (st != G1_DONE) { x = i + 1; st = G1_P3; }
             } else { ik_k = rk; ik_l = rl; ik_s = rs; ++i; }
         }
+    }
+}
+
+// G1 for the reads k_g_seeds handed off (more than w.g1_max_ext FM extensions: repeat-rich reads
+// whose backward scans hold many entries per position): one WAVE per read, restarted from the
+// read's first pass.  Forward scans and the seed strategy run on the whole wave (every lane makes
+// the same lookup); the backward scan extends all of a position's prev entries at once (lanes
+// over entries) and applies bwt_smem1's ordered rules from ballots -- an entry joins curr when its
+// interval survives and its size differs from the previous surviving entry's; only entry 0 can
+// become a mem (no entry before it survived).  Lists in the wave's slot of the G1 scratch (prev,
+// curr, mems, the read's intervals), written by the lanes that own the entries.  The intervals and
+// their pool layout are those of k_g_seeds.
+__device__ __forceinline__ void g1w_sync() {
+    __threadfence_block();
+    wave_sync();
+}
+__device__ __forceinline__ int64_t shfl64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l), hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+struct G1W {
+    uint4 *prev, *curr, *mem, *lst;
+    const uint8_t *q;
+    int len, ni, msl;
+    bool ovf;
+};
+// an interval into the read's list (uniform)
+__device__ __forceinline__ bool g1w_take(G1W &R, const G1Iv &m, int lane) {
+    if (R.ni >= AF_G_MAX_INTV) { R.ovf = true; return false; }
+    if (lane == 0) R.lst[R.ni] = g1_pack(m.k, m.l, m.s, m.qb, m.qe);
+    ++R.ni;
+    return true;
+}
+// bwt_smem1 from x0 with min_intv (oracle fm_smem1), its mems of >= min_seed_len into the list in
+// bwa's (reversed) order; returns the position the pass continues from
+__device__ __forceinline__ int g1w_smem(const DevGenome &G, G1W &R, int x0, int64_t min_intv, int lane) {
+    if (min_intv < 1) min_intv = 1;
+    int64_t ik_k, ik_l, ik_s;
+    fm_set(G, R.q[x0], ik_k, ik_l, ik_s);
+    int ik_qe = x0 + 1, nc = 0, ret = 0;
+    // forward: the wave as one lane
+    for (int i = x0 + 1;; ++i) {
+        bool push = false, stop = false;
+        int64_t rk = 0, rl = 0, rs = 0;
+        if (i == R.len || R.q[i] > 3) push = stop = true;
+        else {
+            fm_ext1(G, ik_k, ik_l, ik_s, 3 - R.q[i], true, rk, rl, rs);
+            if (rs != ik_s) { push = true; stop = rs < min_intv; }
+        }
+        if (push) {
+            if (lane == 0) R.curr[nc] = g1_pack(ik_k, ik_l, ik_s, 0, ik_qe);
+            ++nc;
+            ret = ik_qe;
+        }
+        if (stop) break;
+        ik_k = rk; ik_l = rl; ik_s = rs; ik_qe = i + 1;
+    }
+    g1w_sync();
+    // prev = curr reversed (bwa reverses the forward intervals)
+    int np = nc;
+    for (int j = lane; j < np; j += 64) R.prev[j] = R.curr[np - 1 - j];
+    g1w_sync();
+    int nm = 0, last_mem_qb = 0;
+    for (int i = x0 - 1;; --i) {
+        const int c = i < 0 ? -1 : (R.q[i] > 3 ? -1 : (int)R.q[i]);
+        int ncur = 0;
+        bool any = false;       // a surviving entry in an earlier chunk
+        int64_t carry = 0;      // its size
+        for (int j0 = 0; j0 < np; j0 += 64) {
+            const int j = j0 + lane;
+            const bool live = j < np;
+            G1Iv pv{};
+            if (live) pv = g1_unpack(R.prev[j]);
+            int64_t rk = 0, rl = 0, rs = 0;
+            bool valid = false;
+            if (live && c >= 0) {
+                fm_ext1(G, pv.k, pv.l, pv.s, c, false, rk, rl, rs);
+                valid = rs >= min_intv;
+            }
+            const uint64_t vm = __ballot(valid);
+            if (j0 == 0 && !(vm & 1ull) && (nm == 0 || i + 1 < last_mem_qb)) {  // entry 0 fails: a mem
+                if (lane == 0) R.mem[nm] = g1_pack(pv.k, pv.l, pv.s, i + 1, pv.qe);
+                ++nm;
+                last_mem_qb = i + 1;
+            }
+            const uint64_t below = vm & ((1ull << lane) - 1ull);
+            const int pl = below ? 63 - __builtin_clzll(below) : -1;
+            const int64_t ps = shfl64(rs, pl < 0 ? 0 : pl);
+            const bool push = valid && (pl >= 0 ? rs != ps : (!any || rs != carry));
+            const uint64_t pm = __ballot(push);
+            if (push) R.curr[ncur + __builtin_popcountll(pm & ((1ull << lane) - 1ull))] = g1_pack(rk, rl, rs, 0, pv.qe);
+            ncur += __builtin_popcountll(pm);
+            if (vm) { carry = shfl64(rs, 63 - __builtin_clzll(vm)); any = true; }
+        }
+        g1w_sync();
+        if (ncur == 0) break;
+        uint4 *t = R.prev; R.prev = R.curr; R.curr = t;
+        np = ncur;
+    }
+    // bwa reverses the mems; the caller keeps those of >= min_seed_len
+    for (int t = nm - 1; t >= 0; --t) {
+        const G1Iv m = g1_unpack(R.mem[t]);
+        if (m.qe - m.qb >= R.msl && !g1w_take(R, m, lane)) break;
+    }
+    g1w_sync();
+    return ret;
+}
+
+__global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                     const int32_t *__restrict__ lens, int64_t cap, af_params p,
+                                                     GOpt o, uint4 *__restrict__ scratch, GWork w) {
+    __shared__ uint8_t qs[AF_MAX_READ + 16];
+    const int lane = threadIdx.x;
+    uint4 *const base = scratch + (int64_t)blockIdx.x * G1_SLOT;
+    const int64_t nh = min((int64_t)*(volatile unsigned long long *)w.g1_hv_n, cap);
+    const int msl = p.min_seed_len;
+    const int split_len = (int)((float)msl * 1.5f + .499);
+    for (;;) {
+        int64_t h = 0;
+        if (lane == 0) h = (int64_t)atomicAdd(w.g1_hv_next, 1ull);
+        h = (int64_t)__builtin_amdgcn_readfirstlane((int)h);
+        if (h >= nh) break;
+        const int64_t rr = w.g1_hv[h];
+        G1W R{base, base + G1_LIST, base + 2 * G1_LIST, base + 3 * G1_LIST, qs, read_len(lens, rr, stride), 0, msl, false};
+        const uint8_t *rd = reads + rr * (int64_t)stride;
+        for (int t = lane; t < R.len; t += 64) qs[t] = nt4(rd[t]);
+        wave_sync();
+        // pass 1: SMEMs covering each position
+        for (int x = 0; x < R.len && !R.ovf;) {
+            if (R.q[x] > 3) { ++x; continue; }
+            x = g1w_smem(G, R, x, 1, lane);
+        }
+        // pass 2: re-seeding of long SMEMs with few occurrences
+        const int old_n = R.ni;
+        for (int k2 = 0; k2 < old_n && !R.ovf; ++k2) {
+            const G1Iv pk = g1_unpack(R.lst[k2]);
+            if (pk.qe - pk.qb < split_len || pk.s > o.split_width) continue;
+            const int mid = (pk.qb + pk.qe) >> 1;
+            if (R.q[mid] > 3) continue;
+            g1w_smem(G, R, mid, pk.s + 1, lane);
+        }
+        // pass 3: bwt_seed_strategy1 from each position
+        if (o.max_mem_intv > 0)
+            for (int x = 0; x < R.len && !R.ovf;) {
+                const int c0 = R.q[x];
+                if (c0 > 3) { ++x; continue; }
+                int64_t ik_k, ik_l, ik_s;
+                fm_set(G, c0, ik_k, ik_l, ik_s);
+                const int sx = x;
+                for (int i = x + 1;; ++i) {
+                    if (i >= R.len) { x = R.len; break; }
+                    const int c = R.q[i];
+                    if (c > 3) { x = i + 1; break; }
+                    int64_t rk, rl, rs;
+                    fm_ext1(G, ik_k, ik_l, ik_s, 3 - c, true, rk, rl, rs);
+                    if (rs < o.max_mem_intv && i - sx >= msl) {
+                        if (rs > 0) g1w_take(R, G1Iv{rk, rl, rs, sx, i + 1}, lane);
+                        x = i + 1;
+                        break;
+                    }
+                    ik_k = rk; ik_l = rl; ik_s = rs;
+                }
+            }
+        g1w_sync();
+        // the list sorted by (qb, qe) into the call's pool (k_g_seeds' G1_DONE)
+        if (lane == 0) {
+            const int ni = R.ni;
+            uint4 *Lf = R.lst;
+            if (R.ovf) w.iv_n[rr] = -1;
+            else {
+                for (int a = 1; a < ni; ++a) {
+                    const uint4 t = Lf[a];
+                    const uint32_t kt = (t.w >> 3 & 511) << 9 | (t.w >> 12 & 511);
+                    int b = a;
+                    while (b > 0) {
+                        const uint4 u = Lf[b - 1];
+                        if (((u.w >> 3 & 511) << 9 | (u.w >> 12 & 511)) <= kt) break;
+                        Lf[b] = u;
+                        --b;
+                    }
+                    Lf[b] = t;
+                }
+                const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
+                if (ni && off + ni > w.iv_cap) {
+                    atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
+                    w.iv_n[rr] = -1;
+                } else {
+                    for (int a = 0; a < ni; ++a) {
+                        const G1Iv m = g1_unpack(Lf[a]);
+                        w.iv[off + a] = GIv{m.k, m.s, m.qb, m.qe};
+                    }
+                    w.iv_off[rr] = off;
+                    w.iv_n[rr] = ni;
+                }
+            }
+        }
+        g1w_sync();
     }
 }
 
@@ -1420,7 +1661,11 @@ __global__ __launch_bounds__(64, 2) void k_g_se(DevGenome G, const uint8_t *__re
     if (n > cap) n = cap;
     const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
     uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
-    for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    for (;;) {  // reads dequeued one at a time (their costs vary by orders of magnitude)
+        int64_t r = 0;
+        if (lane == 0) r = (int64_t)atomicAdd(&w.hv.cnt[6], 1ull);
+        r = (int64_t)__builtin_amdgcn_readfirstlane((int)r);
+        if (r >= n) break;
         const int l = read_len(lens, r, stride);
         const int nr = w.reg_n[r];
         const bool ovf = nr < 0;
@@ -1674,7 +1919,11 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
     static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "pool holds a region list");
     static_assert((size_t)AF_G_MAX_CHAIN * sizeof(GChain) >= 2 * (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "ch holds 2 lists");
     static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= 2 * (size_t)(AF_G_MAX_REG + 4) * sizeof(P64g), "seed holds v");
-    for (int64_t pp = blockIdx.x; pp < n; pp += gridDim.x) {
+    for (;;) {  // pairs dequeued one at a time (a pair with many rescue windows costs many others)
+        int64_t pp = 0;
+        if (lane == 0) pp = (int64_t)atomicAdd(&w.hv.cnt[5], 1ull);
+        pp = (int64_t)__builtin_amdgcn_readfirstlane((int)pp);
+        if (pp >= n) break;
         for (int m = 0; m < 2; ++m) {
             const int64_t r = 2 * pp + m;
             const int l = read_len(lens, r, stride);
@@ -1803,7 +2052,8 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
-    if (t < 5 && w.hv.cnt) w.hv.cnt[t] = 0;
+    if (t == 1 && w.g1_hv_n) { *w.g1_hv_n = 0; *w.g1_hv_next = 0; }
+    if (t < 7 && w.hv.cnt) w.hv.cnt[t] = 0;  // [5] k_g_pe's and [6] k_g_se's dequeue counters too
     if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
     if (t < AF_GSTAT_N) w.stats[t] = 0;
     (void)n_reads;
@@ -1856,6 +2106,9 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
+    if (w.g1_max_ext > 0)  // the heavy reads, one wave each, in the lane kernel's (finished) scratch
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
+                           reinterpret_cast<uint4 *>(g1_scratch), w);
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C)                                                                                                       \
@@ -1884,6 +2137,9 @@ hipError_t af_launch_genome_intervals(const DevGenome &G, const uint8_t *reads, 
     const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, nullptr, cap,
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
+    if (w.g1_max_ext > 0)
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
+                           reinterpret_cast<uint4 *>(g1_scratch), w);
     return hipGetLastError();
 }
 

@@ -1,4 +1,5 @@
-"""Per-query phase cycles of k_blat on the configs[2] tails (profiling build libafgpu_prof.so).
+"""Per-query phase cycles of k_blat on the configs[2] S6 queries (S5's survivors; profiling build
+libafgpu_prof.so; one strand's row per query: the strands of a query share it, the last written wins).
 
 python scripts/blat_prof.py [pairs] [out.json]   (GPU; make -C anchored-fusion_amd/csrc prof first)
 """
@@ -16,7 +17,7 @@ import torch  # noqa: E402
 from anchored_fusion_amd import _lib, discover, simworld  # noqa: E402
 from anchored_fusion_amd import io as afio  # noqa: E402
 
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 8_000_160
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
 out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/blat_prof.json"
 anchor = afio.anchor_sequence(os.path.join(ROOT, "tests", "golden", "target_gene.fasta"))
 W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=1.0)
@@ -24,15 +25,16 @@ ref, tiles = W.genome_index(), W.tiles()
 reads = W.simulate_pairs(N, read_len=150, seed=20251015)
 L = _lib.lib()
 assert L.af_debug_blat_prof_enable() == 16
-d = discover.CandidateDiscovery(anchor, ref, tiles, N, 150, device=0)
+W.blob = None
+d = discover.CandidateDiscovery(anchor, ref, tiles, N, 150, device=0, inflight=4, batch_chunks=240)
 d.run(reads)
 torch.cuda.synchronize()
-nt = min(int(d.tails["n"].item()), d.tcap)
+nt = min(int(d.s6["n"].item()), d.qcap)
 P = np.zeros((nt, 16), dtype=np.int32)
 assert L.af_debug_blat_prof_read(P.ctypes.data_as(__import__("ctypes").c_void_p), nt) == 0
 names = ["hits", "sort", "clumps", "align", "chain"]
 tot = P[:, 9].astype(np.int64)
-res = dict(tails=nt, mean_cycles={n: float(P[:, k].mean()) for k, n in enumerate(names)},
+res = dict(queries=nt, mean_cycles={n: float(P[:, k].mean()) for k, n in enumerate(names)},
            mean_total=float(tot.mean()), mean_filter_cycles=float(P[:, 10].mean()), mean_kept=float(P[:, 11].mean()), pct_total={p: float(np.percentile(tot, p)) for p in (50, 90, 99, 99.9)},
            mean_hits=float(P[:, 5].mean()), mean_clumps=float(P[:, 6].mean()), mean_parts=float(P[:, 7].mean()),
            mean_len=float(P[:, 8].mean()),

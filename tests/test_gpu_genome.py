@@ -221,3 +221,36 @@ def test_heavy_path_equals_oracle(world, monkeypatch):
             assert msg is None, (r, msg)
     finally:
         gh.close()
+
+
+@pytest.mark.parametrize("max_ext", [1, 300])
+def test_g1_wave_path_equals_oracle(world, monkeypatch, max_ext):
+    """G1's heavy reads (k_g_seeds_wave: one wave per read, a position's backward-scan entries
+    extended at once) -- every read handed off after its first FM extension (max_ext 1), or the
+    reads past 300 extensions: intervals, S5 records and S4 records equal the oracle's."""
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.genome import GenomeIndex
+    contigs, og, _ = world
+    monkeypatch.setenv("AF_G1_HEAVY_EXT", str(max_ext))
+    gw = GenomeIndex(contigs, device=0)
+    try:
+        reads, lens = sample_reads(contigs, 800, seed=50, chimeric=0.4)
+        io, no = og.intervals(reads, lens, threads=8)
+        ig, ng = gw.intervals(reads, lens)
+        _iv_sets_equal(io, no, ig, ng)
+        so, sno = og.align_se(reads, lens, id_base=5, threads=8)
+        sg, sng = gw.align_se(reads, lens, id_base=5)
+        assert np.array_equal(sno, sng)
+        for r in range(len(sno)):
+            msg = _rec_equal(so[r], sg[r], min(sno[r], 8))
+            assert msg is None, (r, msg)
+        pairs = sample_pairs(contigs, 500, seed=51)
+        plens = np.full(pairs.shape[0], pairs.shape[1], np.int32)
+        po, pno = og.align_pe(pairs, plens, pe=oracle.default_pe(chunk_bases=200_000, pair_base=3), threads=8)
+        pg, png = gw.align_pe(pairs, plens, pe=_lib.default_pe(chunk_bases=200_000, pair_base=3))
+        assert np.array_equal(pno, png)
+        for r in range(len(pno)):
+            msg = _rec_equal(po[r], pg[r], min(pno[r], 8))
+            assert msg is None, (r, msg)
+    finally:
+        gw.close()
