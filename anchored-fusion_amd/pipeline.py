@@ -318,8 +318,9 @@ def run_gene_device(gene, anchor, names, reads_t, lens_t, pair_bases, index, hom
         if c["s2_overflow_reads"]:
             log(f"[{gene}] WARNING: {c['s2_overflow_reads']} reads hit a per-read cap of the S2 restatement and "
                 f"are reported unmapped (AF_FLAG_MEM_OVERFLOW / AF_FLAG_CIGAR_OVERFLOW; bwa has no caps)")
-        caps = {k: v for k, v in c.items() if k.startswith("genome_") or k in ("s6_clipped", "s4_pairs_dropped",
-                                                                                   "s5_dropped")}
+        caps = {k: v for k, v in c.items() if k in ("genome_cap_overflow", "genome_pool_overflow",
+                                                     "genome_record_overflow", "s6_clipped", "s4_pairs_dropped",
+                                                     "s5_dropped") or (k.startswith("blat_cap_") and v)}
         if any(caps.values()):
             log(f"[{gene}] WARNING: caps reached: {caps}")
         s4, split_sam, psl = device_products(d, gene, names, gidx.names)
