@@ -27,6 +27,9 @@ from .align import AlignerGroup, chunk_ends
 from .shard import chunk_pairs
 
 MAX_REC = _genome.MAX_REC
+# S4 and S5 as two concurrent genome calls on two contexts (1) or one call whose seed / region
+# launches cover both (0); bench A/B: AF_S4_SPLIT
+_S4_SPLIT = os.environ.get("AF_S4_SPLIT", "1") == "1"
 EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
 HIT_WORDS = 44      # af_grec as int32 words (176 B)
 PSL_WORDS = 82      # af_psl as int32 words (328 B)
@@ -134,8 +137,20 @@ class CandidateDiscovery:
         rows = sp["rows"][:n * _blat.PSL_DTYPE.itemsize].cpu().numpy().view(_blat.PSL_DTYPE)
         return _blat.spilled_rows(rows, sp["q"][:n].cpu().numpy())
 
+    def _s4_ctx(self):
+        """A second context for S4's genome call (its own pools and scratch; the index is shared)."""
+        if getattr(self, "_ctx4", None) is None:
+            import ctypes
+            c = ctypes.c_void_p()
+            _lib.check(None, _lib.lib().af_ctx_create(int(self.dev.index or 0), ctypes.byref(c)), "af_ctx_create")
+            self._ctx4 = c
+        return self._ctx4
+
     def close(self):
         self.grp.close()
+        if getattr(self, "_ctx4", None) is not None:
+            _lib.lib().af_ctx_destroy(self._ctx4)
+            self._ctx4 = None
 
     def run(self, reads_t, k1_events=None, phase_events=None, lens_t=None):
         """One pass over reads_t (uint8 [2 n_pairs, read_len] on the device; lens_t: int32 [2 n_pairs]
@@ -189,7 +204,18 @@ class CandidateDiscovery:
         # records on s0, S4's on slot 2's stream (idle once S2 is done)
         spe = self.grp.streams[2] if G > 2 else s0
         spe.wait_stream(s0)
-        if npair or n5:
+        if _S4_SPLIT and spe is not s0:
+            # S4's whole call on a second context of the same index, on its own stream, beside
+            # S5's (each has its own seed / region launches, pools and scratch): S4's records
+            # start once its 2 npair reads are seeded instead of after every read of both calls
+            if npair:
+                self.ref.align_pe_device(self.q, npair, self.L, self.q_lens, recs, self.q_nh, params=self.p_genome,
+                                         pe=pe, stream=spe, ctx=self._s4_ctx())
+            if n5:
+                self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
+                                         lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0,
+                                         stream=s0)
+        elif npair or n5:
             self.ref.align_pe_se_device(self.q, npair, n5, self.L, self.q_lens, recs, self.q_nh,
                                         params=self.p_genome, pe_s4=pe, pe_s5=pe, se_id_base=0, stream=s0,
                                         stream_pe=spe)
@@ -342,7 +368,11 @@ class CandidateDiscovery:
                  mapped_reads=int(((self.out["flag"] & 4) == 0).sum().item()),
                  s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))
                                         != 0).sum().item()))
-        c.update({f"genome_{k}": v for k, v in self.ref.stats().items()})
+        gs = self.ref.stats()
+        if getattr(self, "_ctx4", None) is not None:  # S4's call on its own context
+            for k, v in self.ref.stats(ctx=self._ctx4).items():
+                gs[k] += v
+        c.update({f"genome_{k}": v for k, v in gs.items()})
         c.update({f"blat_cap_{k}": v for k, v in self.tiles_ref.caps().items()})
         return c
 

@@ -143,9 +143,10 @@ class GenomeIndex:
     def primary(self):
         return int(_lib.lib().af_genome_primary(self.g))
 
-    def stats(self):
+    def stats(self, ctx=None):
+        c = self.ctx if ctx is None else ctx
         out = np.zeros(_lib.AF_GSTAT_N, np.int32)
-        _lib.check(self.ctx, _lib.lib().af_genome_stats(self.ctx, out.ctypes.data), "af_genome_stats")
+        _lib.check(c, _lib.lib().af_genome_stats(c, out.ctypes.data), "af_genome_stats")
         return dict(zip(STAT_NAMES, (int(v) for v in out)))
 
     # ---- the calls (host buffers) ----------------------------------------------------------
