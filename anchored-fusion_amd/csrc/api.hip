@@ -265,12 +265,24 @@ int ensure_blat_stage(af_ctx *c, int64_t cap, int32_t max_rows) {
     return AF_OK;
 }
 
-int ensure_bscratch(af_ctx *c) {
-    if (c->bscratch) return AF_OK;
-    c->blat_slots = af_blat_slots(c->n_cu);
+// k_blat's per-wave scratch for `items` query strands: one slot per strand up to the resident
+// waves of the chip (a search of a few queries -- the partner stages' targets, each a context of
+// its own -- holds a few slots, not the 2 MB x 6,144 a genome-wide S6 needs)
+int ensure_bscratch(af_ctx *c, int64_t items) {
+    const int max_slots = af_blat_slots(c->n_cu);
+    const int want = (int)std::min<int64_t>(max_slots, std::max<int64_t>(64, (items + 63) / 64 * 64));
+    if (!c->blat_caps) {
+        HIPCHK(c, hipMalloc(&c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N));
+        HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
+    }
+    if (c->bscratch && c->blat_slots >= want) return AF_OK;
+    if (c->bscratch) {
+        HIPCHK(c, hipDeviceSynchronize());  // an earlier search may still use the old slots
+        af_free(c->bscratch);
+        c->bscratch = nullptr;
+    }
+    c->blat_slots = want;
     HIPCHK(c, hipMalloc(&c->bscratch, (size_t)AF_BLAT_SLOT_BYTES * c->blat_slots));
-    HIPCHK(c, hipMalloc(&c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N));
-    HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
     return AF_OK;
 }
 
@@ -1060,7 +1072,7 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         for (int64_t i = 0; i < n_queries; ++i)
             if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
     (void)hipSetDevice(c->device);
-    if ((rc = ensure_bscratch(c)) || (rc = ensure_blat_order(c, n_queries)) ||
+    if ((rc = ensure_bscratch(c, 2 * n_queries)) || (rc = ensure_blat_order(c, n_queries)) ||
         (rc = ensure_blat_stage(c, n_queries, max_rows)))
         return rc;
     const int64_t bytes = n_queries * (int64_t)stride, nr = n_queries * (int64_t)max_rows;
@@ -1112,7 +1124,7 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
     if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
     if (cap_queries == 0) return AF_OK;
     (void)hipSetDevice(c->device);
-    if ((rc = ensure_bscratch(c)) || (rc = ensure_blat_stage(c, cap_queries, max_rows))) return rc;
+    if ((rc = ensure_bscratch(c, 2 * cap_queries)) || (rc = ensure_blat_stage(c, cap_queries, max_rows))) return rc;
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
     HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));

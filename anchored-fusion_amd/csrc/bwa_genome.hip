@@ -623,6 +623,14 @@ struct G2Lds {
     int64_t rmax[2];
 };
 __shared__ G2Lds g_g2;
+// the containment boxes of a read's first regions (mem_chain2aln's "extension made before" test
+// reads them per seed: LDS instead of the region records in global scratch)
+constexpr int G2_BOXES = 512;
+struct G2Box {
+    int64_t rb, re;
+    int32_t qb, qe, w, seedlen0;
+};
+__shared__ G2Box g_box[G2_BOXES];
 
 // ---- bntseq.c on the device
 __device__ __forceinline__ int g_pos2rid(const DevGenome &G, int64_t pos_f) {
@@ -1068,9 +1076,10 @@ template <int CPL>
 __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params &p, int l, int ci, int *nreg_io,
                             int lane, const GReg *pre = nullptr) {
     G2Lds &E = g_g2;
+    G2Box *const box = g_box;
     const GChain c = S.ch2[ci];
     const GSeed *sd = S.seed + c.seed0;
-    g_chain_rmax(G, p, l, sd, c.n, lane);
+    bool have_rmax = false;  // the chain's window, made when a seed is extended here (not for pre's)
     // srt: seed indices by (score << 32 | i) ascending (keys distinct): rank sort on the wave
     for (int i0 = 0; i0 < c.n; i0 += 64) {
         const int i = i0 + lane;
@@ -1082,7 +1091,6 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
         }
     }
     wave_sync();
-    const int64_t rmax0 = E.rmax[0], rmax1 = E.rmax[1];
     for (int k = c.n - 1; k >= 0; --k) {
         const uint64_t sk = S.srt[k];
         const GSeed s = sd[(uint32_t)sk];
@@ -1093,7 +1101,14 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
             const int i = i0 + lane;
             bool h = false;
             if (i < nreg) {
-                const GReg pr = S.reg[i];
+                // the region's box: LDS for the first G2_BOXES regions of the read, else its record
+                GReg pr;
+                if (i < G2_BOXES) {
+                    const G2Box &bx = box[i];
+                    pr.rb = bx.rb; pr.re = bx.re; pr.qb = bx.qb; pr.qe = bx.qe; pr.w = bx.w; pr.seedlen0 = bx.seedlen0;
+                } else {
+                    pr = S.reg[i];
+                }
                 if (!(s.rbeg < pr.rb || s.rbeg + s.len > pr.re || s.qbeg < pr.qb || s.qbeg + s.len > pr.qe) &&
                     !((double)(s.len - pr.seedlen0) > .1 * l)) {
                     int qd = s.qbeg - pr.qb;
@@ -1133,9 +1148,13 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
             }
         }
         if (nreg >= AF_G_MAX_REG) return false;
-        const GReg a = pre && k == c.n - 1 ? pre[c.seed0]
-                                           : g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, s, rmax0, rmax1, lane);
-        if (lane == 0) S.reg[nreg] = a;
+        const bool use_pre = pre && k == c.n - 1;
+        if (!use_pre && !have_rmax) { g_chain_rmax(G, p, l, sd, c.n, lane); have_rmax = true; }
+        const GReg a = use_pre ? pre[c.seed0] : g_seed_region<CPL>(G, p, l, sd, c.n, c.rid, s, E.rmax[0], E.rmax[1], lane);
+        if (lane == 0) {
+            S.reg[nreg] = a;
+            if (nreg < G2_BOXES) box[nreg] = G2Box{a.rb, a.re, a.qb, a.qe, a.w, a.seedlen0};
+        }
         *nreg_io = nreg + 1;
         wave_sync();
     }
