@@ -38,7 +38,7 @@ namespace {
 __device__ int32_t *g_gprof = nullptr;
 __device__ int64_t g_gprof_cap = 0;
 __device__ int32_t g_gprof_call = 0;
-constexpr int GP_W = 24;
+constexpr int GP_W = 32;  // [24, 32): k_g_pe's phases on the pair's first read
 __device__ __forceinline__ int32_t *gp_row(int64_t r) {
     return g_gprof && r < g_gprof_cap ? g_gprof + ((int64_t)g_gprof_call * g_gprof_cap + r) * GP_W : nullptr;
 }
@@ -1161,23 +1161,32 @@ __device__ bool g_chain2aln(const DevGenome &G, const G2Scr &S, const af_params 
     return true;
 }
 
-// mem_patch_reg (oracle mem_patch_reg): the merged score, 0 if not merged; *w_out its band
-template <int CPL>
-__device__ int g_patch_reg(const DevGenome &G, const af_params &p, const GReg &a, const GReg &b, int *w_out,
-                           uint8_t *zg, int lane) {
-    const int64_t l_pac = G.l_pac;
-    if (a.rb < l_pac && b.rb >= l_pac) return 0;
-    if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) return 0;
-    if (b.re - a.rb > AF_S2_MAX_TSPAN) return 0;  // the oracle's AFO_PE_MAX_TSPAN (L.t holds 1 KiB)
+// mem_patch_reg's tests before its alignment (oracle mem_patch_reg): false if a and b cannot
+// merge; else *w_out the band
+__device__ __forceinline__ bool g_patch_pre(int64_t l_pac, const af_params &p, const GReg &a, const GReg &b,
+                                            int *w_out) {
+    if (a.rb < l_pac && b.rb >= l_pac) return false;
+    if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) return false;
+    if (b.re - a.rb > AF_S2_MAX_TSPAN) return false;  // the oracle's AFO_PE_MAX_TSPAN (L.t holds 1 KiB)
     int w = (int)((a.re - b.rb) - (a.qe - b.qb));
     w = w > 0 ? w : -w;
     double r = (double)(a.re - b.rb) / (double)(b.re - a.rb) - (double)(a.qe - b.qb) / (double)(b.qe - a.qb);
     r = r > 0. ? r : -r;
     if (a.re < b.rb || a.qe < b.qb) {
-        if (w > p.w << 1 || r >= (double)0.05f) return 0;
-    } else if (w > p.w << 2 || r >= (double)(0.05f * 2)) return 0;
+        if (w > p.w << 1 || r >= (double)0.05f) return false;
+    } else if (w > p.w << 2 || r >= (double)(0.05f * 2)) return false;
     w += a.w + b.w;
-    w = w < p.w << 2 ? w : p.w << 2;
+    *w_out = w < p.w << 2 ? w : p.w << 2;
+    return true;
+}
+
+// mem_patch_reg (oracle mem_patch_reg): the merged score, 0 if not merged; *w_out its band
+template <int CPL>
+__device__ int g_patch_reg(const DevGenome &G, const af_params &p, const GReg &a, const GReg &b, int *w_out,
+                           uint8_t *zg, int lane) {
+    const int64_t l_pac = G.l_pac;
+    int w;
+    if (!g_patch_pre(l_pac, p, a, b, &w)) return 0;
     const int lq = b.qe - a.qb;
     const int score = gen_cigar_wave<CPL, false>(G.T, l_pac, p, w, lq, a.qb, a.rb, b.re, g_dp, zg, lane);
     const int q_s = (int)((double)(b.qe - a.qb) / (double)((b.qe - b.qb) + (a.qe - a.qb)) * (double)(b.score + a.score) + .499);
@@ -1201,65 +1210,168 @@ struct GLtArsHash {
     }
 };
 
-// mem_sort_dedup_patch (oracle mem_sort_dedup_patch) over a[0, n); patch: merge colinear hits
+// ---- region lists sorted through keys in LDS: lane 0's introsort compares and swaps small keys
+// (each region's index with the fields its comparator reads) in the G2 boxes' space, which is dead
+// once a read's chains are extended; the wave then moves the 64-B regions in key order through tmp.
+// The swaps depend only on the comparator's answers, so the order (ties included) is the one the
+// introsort over the regions themselves gives.
+static_assert(AF_G_MAX_REG <= 1024 && AF_MAX_READ < 32768, "region keys pack a 10-bit index and a 15-bit qb");
+static_assert(sizeof(G2Box) * G2_BOXES >= 16 * AF_G_MAX_REG, "the boxes hold 16 B of key per region");
+static_assert(sizeof(GReg) == 64, "regions move as 4 x 16 B");
+struct GKeyRe {  // re << 10 | index (mem_sort_dedup_patch's sort by re)
+    __device__ bool operator()(uint64_t a, uint64_t b) const { return (a >> 10) < (b >> 10); }
+};
+struct GKey16 { int64_t x; int32_t y; int32_t z; };
+struct GKeyArs {  // x = rb, y = score, z = qb << 16 | index: score desc, rb, qb
+    __device__ bool operator()(const GKey16 &a, const GKey16 &b) const {
+        return a.y > b.y || (a.y == b.y && (a.x < b.x || (a.x == b.x && (a.z >> 16) < (b.z >> 16))));
+    }
+};
+struct GKeyHash {  // x = hash, y = score, z = index: score desc, hash (mark_primary_se)
+    __device__ bool operator()(const GKey16 &a, const GKey16 &b) const {
+        return a.y > b.y || (a.y == b.y && (uint64_t)a.x < (uint64_t)b.x);
+    }
+};
+// a[k] = old a[from(k)] for k < m (wave)
+template <class F>
+__device__ __forceinline__ void g_regs_gather(GReg *a, GReg *tmp, int m, F from, int lane) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a);
+    uint4 *t = reinterpret_cast<uint4 *>(tmp);
+    for (int k = lane; k < 4 * m; k += 64) t[k] = src[4 * from(k >> 2) + (k & 3)];
+    wave_sync();
+    uint4 *dst = reinterpret_cast<uint4 *>(a);
+    for (int k = lane; k < 4 * m; k += 64) dst[k] = t[k];
+    wave_sync();
+}
+
+// mem_sort_dedup_patch's overlap test of q = a[j] against p = a[i] (oracle mem_sort_dedup_patch)
+__device__ __forceinline__ bool g_dd_overlap(const GReg &q, const GReg &pp) {
+    const int64_t or_ = q.re - pp.rb;
+    const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
+    const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
+    const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
+    return (float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq;
+}
+
+// mem_sort_dedup_patch (oracle mem_sort_dedup_patch) over a[0, n); patch: merge colinear hits;
+// tmp: n regions of scratch.  bwa's walk for a[i] visits j = i-1, i-2, ... while a[j] is on a[i]'s
+// contig within max_chain_gap; the wave tests 64 of them at once and stops at the first that
+// changes something (an overlap drop, or a patch candidate passing mem_patch_reg's cheap tests),
+// which lane 0 applies before the walk resumes below it with a[i] as it now is.
 template <int CPL>
 __device__ int g_dedup_patch(const DevGenome &G, const af_params &p, const GOpt &o, GReg *a, int n, bool patch,
-                             uint8_t *zg, int lane) {
+                             uint8_t *zg, int lane, GReg *tmp) {
     G2Lds &E = g_g2;
     if (n <= 1) return n;
-    if (lane == 0) ks_introsort(a, n, GLtArs2());
+    const int64_t l_pac = G.l_pac, gap = o.max_chain_gap;
+    uint64_t *k1 = reinterpret_cast<uint64_t *>(g_box);
+    for (int i = lane; i < n; i += 64) k1[i] = (uint64_t)a[i].re << 10 | (uint64_t)i;
     wave_sync();
-    for (int i = 1; i < n; ++i) {
-        if (a[i].rid != a[i - 1].rid || a[i].rb >= a[i - 1].re + o.max_chain_gap) continue;
-        for (int j = i - 1; j >= 0 && a[i].rid == a[j].rid && a[i].rb < a[j].re + o.max_chain_gap; --j) {
-            const GReg q = a[j], pp = a[i];
-            if (q.qe == q.qb) continue;
-            const int64_t or_ = q.re - pp.rb;
-            const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
-            const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
-            const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
-            if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
-                const bool drop_p = pp.score < q.score;
-                wave_sync();
-                if (lane == 0) {
-                    if (drop_p) a[i].qe = a[i].qb;
-                    else a[j].qe = a[j].qb;
+    if (lane == 0) ks_introsort(k1, n, GKeyRe());
+    wave_sync();
+    g_regs_gather(a, tmp, n, [&](int k) { return (int)(k1[k] & 1023); }, lane);
+    for (int i0 = 1; i0 < n; i0 += 64) {
+        // a[i] is walked unless it starts a new contig or lies past a[i-1] + max_chain_gap (reads of
+        // a[i].rb and a[i-1].re, which no earlier step of the walk changes)
+        bool walk = false;
+        if (i0 + lane < n) {
+            const GReg &x = a[i0 + lane], &y = a[i0 + lane - 1];
+            walk = !(x.rid != y.rid || x.rb >= y.re + gap);
+        }
+        uint64_t wm = __ballot(walk);
+        while (wm) {
+            const int i = i0 + __builtin_ctzll(wm);
+            wm &= wm - 1;
+            GReg pp = a[i];
+            for (int j = i - 1; j >= 0;) {
+                const int jj = j - lane;
+                bool cont = false, ev = false;
+                if (jj >= 0) {
+                    const GReg q = a[jj];
+                    cont = pp.rid == q.rid && pp.rb < q.re + gap;
+                    if (cont && q.qe != q.qb) {
+                        int w_;
+                        ev = g_dd_overlap(q, pp) || (patch && q.rb < pp.rb && g_patch_pre(l_pac, p, q, pp, &w_));
+                    }
                 }
-                wave_sync();
-                if (drop_p) break;
-            } else if (q.rb < pp.rb && patch) {
-                int w = 0;
-                const int score = g_patch_reg<CPL>(G, p, q, pp, &w, zg, lane);
-                if (score > 0) {
-                    wave_sync();
+                const uint64_t stop = __ballot(!cont), em = __ballot(ev);
+                const uint64_t e = em & (stop ? (stop & (0ull - stop)) - 1 : ~0ull);
+                if (!e) {
+                    if (stop) break;
+                    j -= 64;
+                    continue;
+                }
+                const int js = j - __builtin_ctzll(e);
+                const GReg q = a[js];
+                if (g_dd_overlap(q, pp)) {
+                    const bool drop_p = pp.score < q.score;
                     if (lane == 0) {
-                        GReg &P = a[i];
-                        P.seedcov = P.seedcov > q.seedcov ? P.seedcov : q.seedcov;
-                        P.sub = P.sub > q.sub ? P.sub : q.sub;
-                        P.qb = q.qb; P.rb = q.rb;
-                        P.truesc = P.score = score;
-                        P.w = w;
-                        a[j].qb = a[j].qe;
+                        if (drop_p) a[i].qe = a[i].qb;
+                        else a[js].qe = a[js].qb;
                     }
                     wave_sync();
+                    if (drop_p) break;
+                } else {
+                    int w = 0;
+                    const int score = g_patch_reg<CPL>(G, p, q, pp, &w, zg, lane);
+                    if (score > 0) {
+                        wave_sync();
+                        if (lane == 0) {
+                            GReg &P = a[i];
+                            P.seedcov = P.seedcov > q.seedcov ? P.seedcov : q.seedcov;
+                            P.sub = P.sub > q.sub ? P.sub : q.sub;
+                            P.qb = q.qb; P.rb = q.rb;
+                            P.truesc = P.score = score;
+                            P.w = w;
+                            a[js].qb = a[js].qe;
+                        }
+                        wave_sync();
+                        pp = a[i];
+                    }
                 }
+                j = js - 1;
             }
         }
     }
-    if (lane == 0) {
-        int m = 0;
-        for (int i = 0; i < n; ++i)
-            if (a[i].qe > a[i].qb) a[m++] = a[i];
-        ks_introsort(a, m, GLtArs());
-        for (int i = 1; i < m; ++i)
-            if (a[i].score == a[i - 1].score && a[i].rb == a[i - 1].rb && a[i].qb == a[i - 1].qb) a[i].qe = a[i].qb;
-        int mm = m ? 1 : 0;
-        for (int i = 1; i < m; ++i)
-            if (a[i].qe > a[i].qb) a[mm++] = a[i];
-        E.misc[2] = mm;
+    // the live regions (in order) sorted by (score desc, rb, qb); equal neighbours dropped
+    GKey16 *k2 = reinterpret_cast<GKey16 *>(g_box);
+    int m = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        GReg x;
+        const bool live = i < n && ((x = a[i]), x.qe > x.qb);
+        const uint64_t lm = __ballot(live);
+        if (live) k2[m + lanes_below(lm, lane)] = GKey16{x.rb, x.score, x.qb << 16 | i};
+        m += __builtin_popcountll(lm);
     }
     wave_sync();
-    return E.misc[2];
+    if (lane == 0) ks_introsort(k2, m, GKeyArs());
+    wave_sync();
+    // kept keys compacted in order: a kept key's z goes to slot mm + (kept before it) <= its own
+    // slot, so the next chunk's first comparison (with this chunk's last key) still reads that
+    // key's own z
+    int mm = 0;
+    for (int i0 = 0; i0 < m; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = false;
+        GKey16 c{0, 0, 0};
+        if (i < m) {
+            c = k2[i];
+            keep = i == 0;
+            if (i > 0) {
+                const GKey16 d = k2[i - 1];
+                keep = !(c.y == d.y && c.x == d.x && (c.z >> 16) == (d.z >> 16));
+            }
+        }
+        const uint64_t km = __ballot(keep);
+        wave_sync();
+        if (keep) k2[mm + lanes_below(km, lane)].z = c.z;
+        mm += __builtin_popcountll(km);
+        wave_sync();
+    }
+    g_regs_gather(a, tmp, mm, [&](int k) { return k2[k].z & 0xffff; }, lane);
+    (void)E;
+    return mm;
 }
 
 __device__ __forceinline__ void g_load_read(const uint8_t *reads, int64_t r, int32_t stride, int l, int lane) {
@@ -1396,7 +1508,7 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
                     for (int ci = 0; ci < nch && !ovf; ++ci)
                         if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane)) ovf = true;
                     GPROF(gp_c[3] = clock64(); gp_n[2] = nreg;)
-                    if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+                    if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane, reinterpret_cast<GReg *>(S.seed));
                     GPROF(gp_c[4] = clock64(); gp_n[3] = nreg;)
                 }
             }
@@ -1495,7 +1607,7 @@ __global__ __launch_bounds__(64, 2) void k_g_heavy(DevGenome G, const uint8_t *_
         for (int ci = 0; ci < nch && !ovf; ++ci)
             if (!g_chain2aln<CPL>(G, S, p, l, ci, &nreg, lane, res + so)) ovf = true;
         GPROF(const uint64_t gp_c1 = clock64();)
-        if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane);
+        if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane, reinterpret_cast<GReg *>(S.seed));
         GPROF(if (lane == 0) { int32_t *g = gp_row(r); if (g) { g[6] = (int32_t)(gp_c1 - gp_c0);
               g[7] = (int32_t)(clock64() - gp_c1); g[12] = nreg; g[13] = nreg; } })
         g_put_regions(w, S, r, nreg, ovf, lane);
@@ -1528,6 +1640,52 @@ __device__ void g_mark_primary(GReg *a, int n, int64_t id, const af_params &p, i
         if (k == nz) z[nz++] = i;
         else a[i].secondary = z[k];
     }
+}
+
+// mem_mark_primary_se on the wave: the sort through keys in LDS, then lane 0's walk over the
+// regions' query spans, scores and subs in LDS (the boxes' space); tmp: n regions of scratch
+__device__ void g_mark_primary_w(GReg *a, int n, int64_t id, GReg *tmp, int lane) {
+    if (n == 0) return;
+    GKey16 *k = reinterpret_cast<GKey16 *>(g_box);
+    for (int i = lane; i < n; i += 64) {
+        const uint64_t h = hash_64((uint64_t)(id + i));
+        a[i].sub = 0; a[i].secondary = -1; a[i].hash = h;
+        k[i] = GKey16{(int64_t)h, a[i].score, i};
+    }
+    wave_sync();
+    if (lane == 0) ks_introsort(k, n, GKeyHash());
+    wave_sync();
+    g_regs_gather(a, tmp, n, [&](int j) { return k[j].z; }, lane);
+    int32_t *span = reinterpret_cast<int32_t *>(g_box);  // qb << 16 | qe
+    int32_t *score = span + AF_G_MAX_REG, *sub = score + AF_G_MAX_REG, *z = sub + AF_G_MAX_REG;
+    for (int i = lane; i < n; i += 64) { span[i] = a[i].qb << 16 | a[i].qe; score[i] = a[i].score; sub[i] = 0; }
+    wave_sync();
+    if (lane == 0) {
+        int nz = 0;
+        z[nz++] = 0;
+        for (int i = 1; i < n; ++i) {
+            const int qbi = span[i] >> 16, qei = span[i] & 0xffff;
+            int kk;
+            for (kk = 0; kk < nz; ++kk) {
+                const int j = z[kk];
+                const int qbj = span[j] >> 16, qej = span[j] & 0xffff;
+                const int b_max = qbj > qbi ? qbj : qbi;
+                const int e_min = qej < qei ? qej : qei;
+                if (e_min > b_max) {
+                    const int min_l = qei - qbi < qej - qbj ? qei - qbi : qej - qbj;
+                    if ((float)(e_min - b_max) >= (float)min_l * 0.5f) {
+                        if (sub[j] == 0) sub[j] = score[i];
+                        break;
+                    }
+                }
+            }
+            if (kk == nz) z[nz++] = i;
+            else a[i].secondary = z[kk];
+        }
+    }
+    wave_sync();
+    for (int i = lane; i < n; i += 64) a[i].sub = sub[i];
+    wave_sync();
 }
 
 // one mem_aln_t (oracle aln_t)
@@ -1822,6 +1980,7 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
             wave_sync();
             const int P = l_ms * p.a < 250 ? 16 : 8;
             int sc, te, qe, tb, qb;
+            GPROF(if (lane == 0) ++E.misc[5];)
             g_ksw_align2(E.rq, l_ms, staged ? E.tw : G.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb,
                          qb, lane);
             if (sc >= p.min_seed_len && qb >= 0) {
@@ -1853,8 +2012,10 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
             ++n;
         }
         if (n) {
-            const int m = g_dedup_patch<2>(G, p, o, ma, E.na[mi], false, zg, lane);
+            GPROF(const uint64_t gp_d0 = clock64();)
+            const int m = g_dedup_patch<2>(G, p, o, ma, E.na[mi], false, zg, lane, reinterpret_cast<GReg *>(S.seed));
             if (lane == 0) E.na[mi] = m;
+            GPROF(if (lane == 0) E.misc[6] += (int32_t)(clock64() - gp_d0);)
             wave_sync();
         }
     }
@@ -1862,6 +2023,7 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
 }
 
 struct P64g { uint64_t x, y; };
+static_assert(sizeof(G2Box) * G2_BOXES >= sizeof(P64g) * AF_G_MAX_REG, "the boxes hold mem_pair's keys");
 struct GLtP64 {
     __device__ bool operator()(const P64g &a, const P64g &b) const { return a.x < b.x || (a.x == b.x && a.y < b.y); }
 };
@@ -1943,6 +2105,8 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
         if (lane == 0) pp = (int64_t)atomicAdd(&w.hv.cnt[5], 1ull);
         pp = (int64_t)__builtin_amdgcn_readfirstlane((int)pp);
         if (pp >= n) break;
+        GPROF(const uint64_t gp_c0 = clock64(); const uint32_t gp_t0 = gp_rt();
+              if (lane == 0) { E.misc[5] = 0; E.misc[6] = 0; })
         for (int m = 0; m < 2; ++m) {
             const int64_t r = 2 * pp + m;
             const int l = read_len(lens, r, stride);
@@ -1975,14 +2139,17 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
                     wave_sync();
                 }
             }
+        GPROF(const uint64_t gp_c1 = clock64(); const int gp_na0 = E.na[0], gp_na1 = E.na[1];)
         // primary marking, pairing and the record choice (mem_sam_pe)
+        g_mark_primary_w(A[0], E.na[0], (int64_t)((uint64_t)(o.pair_base + pp) << 1 | 0), reinterpret_cast<GReg *>(S.seed), lane);
+        g_mark_primary_w(A[1], E.na[1], (int64_t)((uint64_t)(o.pair_base + pp) << 1 | 1), reinterpret_cast<GReg *>(S.seed), lane);
         if (lane == 0) {
             const uint64_t id = (uint64_t)(o.pair_base + pp);
-            g_mark_primary(A[0], E.na[0], (int64_t)(id << 1 | 0), p, S.kept);
-            g_mark_primary(A[1], E.na[1], (int64_t)(id << 1 | 1), p, S.kept);
             int z[2] = {0, 0}, extra = 1, mode = 0;  // mode 1: paired records
             int o_sc = 0;
-            if (E.na[0] && E.na[1] && (o_sc = g_mem_pair(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)id, z, V)) > 0) {
+            // mem_pair's sort keys in LDS (the boxes' space) when they fit
+            P64g *Vp = E.na[0] + E.na[1] <= AF_G_MAX_REG ? reinterpret_cast<P64g *>(g_box) : V;
+            if (E.na[0] && E.na[1] && (o_sc = g_mem_pair(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)id, z, Vp)) > 0) {
                 int is_multi = 0;
                 for (int i = 0; i < 2; ++i) {
                     int j;
@@ -2007,6 +2174,7 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
             E.misc[1] = mode; E.misc[2] = z[0]; E.misc[3] = z[1]; E.misc[4] = extra;
         }
         wave_sync();
+        GPROF(const uint64_t gp_c2 = clock64();)
         const int mode = E.misc[1];
         int extra = E.misc[4];
         const int zz[2] = {E.misc[2], E.misc[3]};
@@ -2064,6 +2232,10 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
                 }
             }
         }
+        GPROF(if (lane == 0) { int32_t *g = gp_row(2 * pp); if (g) { const uint64_t ce = clock64();
+              g[24] = (int32_t)(gp_c1 - gp_c0); g[25] = (int32_t)(gp_c2 - gp_c1); g[26] = (int32_t)(ce - gp_c2);
+              g[27] = E.misc[5]; g[28] = E.misc[6]; g[29] = gp_na0 << 16 | gp_na1; g[30] = (int32_t)gp_t0;
+              g[31] = (int32_t)gp_rt(); } })
         wave_sync();
     }
 }

@@ -107,4 +107,24 @@ for c in range(min(ncalls, 4)):
     b1 = tg0.min()
     print(f"  G1 makespan {(tg1 - b1).max() / 100:.0f} us; per-read wall p50 {pct(tg1 - tg0, 50) / 100:.1f} us "
           f"p99 {pct(tg1 - tg0, 99) / 100:.1f} us max {(tg1 - tg0).max() / 100:.1f} us")
+    # k_g_pe (rows of the pairs' first reads): rescue (ksw_align2 + dedup), pairing, records
+    P = B[B[:, 30] != 0]
+    if len(P):
+        resc, pair, rec = P[:, 24], P[:, 25], P[:, 26]
+        tot = resc + pair + rec
+        print(f"  PE {len(P)} pairs: cycles/pair mean {tot.mean():.0f} p50 {pct(tot, 50):.0f} p99 {pct(tot, 99):.0f} "
+              f"max {tot.max()}; shares rescue {resc.sum() / tot.sum():.3f} (dedup {P[:, 28].sum() / tot.sum():.3f}) "
+              f"pair {pair.sum() / tot.sum():.3f} records {rec.sum() / tot.sum():.3f}")
+        print(f"  PE ksw_align2 calls/pair mean {P[:, 27].mean():.2f} p99 {pct(P[:, 27], 99):.0f} max {P[:, 27].max()}; "
+              f"pairs with >= 8: {(P[:, 27] >= 8).sum()} holding {resc[P[:, 27] >= 8].sum() / tot.sum():.3f} of the cycles")
+        sp = np.argsort(-tot)
+        print(f"  PE top-100 pairs hold {tot[sp[:100]].sum() / tot.sum():.3f}; top-1000 {tot[sp[:1000]].sum() / tot.sum():.3f}")
+        print("  PE heaviest: cyc rescue dedup pair records | ksw na0 na1")
+        for i in sp[:12]:
+            r = P[i]
+            print(f"   {tot[i]:>11d} {r[24]:>10d} {r[28]:>10d} {r[25]:>9d} {r[26]:>9d} | {r[27]} {r[29] >> 16} {r[29] & 0xFFFF}")
+        t0_, t1_ = P[:, 30] & 0xFFFFFFFF, P[:, 31] & 0xFFFFFFFF
+        base = t0_.min()
+        print(f"  PE makespan {(t1_ - base).max() / 100:.0f} us; last pair starts at {(t0_ - base).max() / 100:.0f} us; "
+              f"per-pair wall p50 {pct(t1_ - t0_, 50) / 100:.1f} us max {(t1_ - t0_).max() / 100:.1f} us")
 disc.close()
