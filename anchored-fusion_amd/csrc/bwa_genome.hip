@@ -635,6 +635,13 @@ __shared__ G2Box g_box[G2_BOXES];
 // ---- bntseq.c on the device
 __device__ __forceinline__ int g_pos2rid(const DevGenome &G, int64_t pos_f) {
     if (pos_f >= G.l_pac) return -1;
+    if (G.ctg_bkt) {  // the bucket's contig; past a boundary inside it, the next ones in turn
+        const int32_t e = G.ctg_bkt[pos_f >> AF_CTG_BKT_SHIFT];
+        int rid = e & 0x7fffffff;
+        if (e < 0)
+            while (rid + 1 < G.n_ctg && pos_f >= G.ctg_off_d[rid + 1]) ++rid;
+        return rid;
+    }
     int left = 0, mid = 0, right = G.n_ctg;
     while (left < right) {
         mid = (left + right) >> 1;
@@ -666,10 +673,34 @@ __device__ __forceinline__ void g_fetch_clip(const DevGenome &G, int64_t *beg, i
     *end = *end < fe ? *end : fe;
 }
 
+// ---- mem_chain's working set in LDS (the G2 boxes' space, free until chain2aln): the kbtree's
+// first G_KB_LDS nodes and the first G_CH_LDS chains' keys and end seeds; the rest stays in the
+// wave's global scratch.  Lane 0's walk then reads LDS for the common short lists instead of
+// chasing scratch lines through L2.
+constexpr int G_KB_LDS = 64, G_CH_LDS = 240;
+struct GChainHot {             // a chain's pos, contig, seed count and first / last seeds
+    int64_t pos, r_first, r_last;
+    int32_t q_first, len_first, q_last, len_last, rid, n, last;
+};
+struct GChainLds {
+    GChainHot ch[G_CH_LDS];
+    GKb node[G_KB_LDS];
+    int32_t rid[64];           // the wave's batch of occurrences: each one's contig (g_intv2rid)
+};
+
+static_assert(sizeof(GChainLds) <= sizeof(G2Box) * G2_BOXES, "mem_chain's LDS set fits the boxes");
+
 // ---- klib kbtree (t = 5) over chain indices keyed by chain pos; lane 0 (oracle kb_*)
-struct GTree { GKb *node; int nn, root; const GChain *ch; };
+struct GTree {
+    GKb *node_l, *node_g;
+    int nn, root;
+    const GChain *ch;
+    const GChainHot *hot;
+    __device__ GKb &nd(int i) const { return i < G_KB_LDS ? node_l[i] : node_g[i]; }
+    __device__ int64_t pos(int x) const { return x < G_CH_LDS ? hot[x].pos : ch[x].pos; }
+};
 __device__ __forceinline__ int gkb_cmp(const GTree &b, int x, int64_t kpos) {
-    const int64_t a = b.ch[x].pos;
+    const int64_t a = b.pos(x);
     return (kpos < a) - (a < kpos);
 }
 __device__ int gkb_getp_aux(const GTree &b, const GKb &x, int64_t kpos, int *r) {
@@ -686,14 +717,14 @@ __device__ int gkb_getp_aux(const GTree &b, const GKb &x, int64_t kpos, int *r) 
     return begin;
 }
 __device__ int gkb_new(GTree &b, int internal) {
-    GKb &z = b.node[b.nn];
+    GKb &z = b.nd(b.nn);
     z.n = 0; z.internal = (int16_t)internal;
     return b.nn++;
 }
 __device__ int gkb_lower(const GTree &b, int64_t kpos) {
     int r = 0, lower = -1, xi = b.root;
     while (xi >= 0) {
-        const GKb &x = b.node[xi];
+        const GKb &x = b.nd(xi);
         const int i = gkb_getp_aux(b, x, kpos, &r);
         if (i >= 0 && r == 0) return x.key[i];
         if (i >= 0) lower = x.key[i];
@@ -703,8 +734,8 @@ __device__ int gkb_lower(const GTree &b, int64_t kpos) {
     return lower;
 }
 __device__ void gkb_split(GTree &b, int xi, int i, int yi) {
-    const int zi = gkb_new(b, b.node[yi].internal);
-    GKb &x = b.node[xi], &y = b.node[yi], &z = b.node[zi];
+    const int zi = gkb_new(b, b.nd(yi).internal);
+    GKb &x = b.nd(xi), &y = b.nd(yi), &z = b.nd(zi);
     z.n = G_KB_T - 1;
     for (int u = 0; u < G_KB_T - 1; ++u) z.key[u] = y.key[G_KB_T + u];
     if (y.internal)
@@ -717,18 +748,18 @@ __device__ void gkb_split(GTree &b, int xi, int i, int yi) {
     ++x.n;
 }
 __device__ bool gkb_putp(GTree &b, int k) {
-    const int64_t kpos = b.ch[k].pos;
+    const int64_t kpos = b.pos(k);
     int xi = b.root;
     if (b.nn + 16 >= G_KB_NODES) return false;  // one insertion adds at most depth + 1 nodes
-    if (b.node[xi].n == G_KB_MAXK) {
+    if (b.nd(xi).n == G_KB_MAXK) {
         const int si = gkb_new(b, 1);
-        b.node[si].ptr[0] = (int16_t)xi;
+        b.nd(si).ptr[0] = (int16_t)xi;
         b.root = si;
         gkb_split(b, si, 0, xi);
         xi = si;
     }
     for (;;) {  // __kb_putp_aux, iteratively
-        GKb &x = b.node[xi];
+        GKb &x = b.nd(xi);
         if (!x.internal) {
             const int i = gkb_getp_aux(b, x, kpos, nullptr);
             for (int u = x.n - 1; u >= i + 1; --u) x.key[u + 1] = x.key[u];
@@ -737,11 +768,11 @@ __device__ bool gkb_putp(GTree &b, int k) {
             return true;
         }
         int i = gkb_getp_aux(b, x, kpos, nullptr) + 1;
-        if (b.node[x.ptr[i]].n == G_KB_MAXK) {
+        if (b.nd(x.ptr[i]).n == G_KB_MAXK) {
             gkb_split(b, xi, i, x.ptr[i]);
-            if (gkb_cmp(b, b.node[xi].key[i], kpos) > 0) ++i;
+            if (gkb_cmp(b, b.nd(xi).key[i], kpos) > 0) ++i;
         }
-        xi = b.node[xi].ptr[i];
+        xi = b.nd(xi).ptr[i];
     }
 }
 // in-order traversal into order[] (iterative; depth <= 8 for 8192 keys at t = 5)
@@ -751,7 +782,7 @@ __device__ int gkb_traverse(const GTree &b, int32_t *order) {
     while (top > 0) {
         const int xi = stk_node[top - 1];
         const int i = stk_i[top - 1];
-        const GKb &x = b.node[xi];
+        const GKb &x = b.nd(xi);
         if (!x.internal) {
             for (int u = 0; u < x.n; ++u) order[n++] = x.key[u];
             --top;
@@ -766,23 +797,33 @@ __device__ int gkb_traverse(const GTree &b, int32_t *order) {
 }
 
 // test_and_merge (oracle test_and_merge), lane 0: 1 merged / contained, 0 not, -1 overflow
-__device__ int g_test_and_merge(const G2Scr &S, int ci, const GSeed &p, int rid, int64_t l_pac, int w,
-                                int max_chain_gap, int *npool) {
-    GChain &c = S.ch[ci];
-    const GSeed first = S.pool[c.seed0], last = S.pool[S.last_of[ci]];
-    const int64_t qend = (int64_t)last.qbeg + last.len, rend = last.rbeg + last.len;
-    if (rid != c.rid) return 0;
-    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend) return 1;
-    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return 0;
-    const int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
-    if (y >= 0 && x - y <= w && y - x <= w && x - last.len < max_chain_gap && y - last.len < max_chain_gap) {
+__device__ int g_test_and_merge(const G2Scr &S, GChainHot *hot, int ci, const GSeed &p, int rid, int64_t l_pac,
+                                int w, int max_chain_gap, int *npool) {
+    GChainHot h;
+    if (ci < G_CH_LDS) h = hot[ci];
+    else {
+        const GChain c = S.ch[ci];
+        const int li = S.last_of[ci];
+        const GSeed first = S.pool[c.seed0], last = S.pool[li];
+        h = GChainHot{c.pos, first.rbeg, last.rbeg, first.qbeg, first.len, last.qbeg, last.len, c.rid, c.n, li};
+    }
+    const int64_t qend = (int64_t)h.q_last + h.len_last, rend = h.r_last + h.len_last;
+    if (rid != h.rid) return 0;
+    if (p.qbeg >= h.q_first && p.qbeg + p.len <= qend && p.rbeg >= h.r_first && p.rbeg + p.len <= rend) return 1;
+    if ((h.r_last < l_pac || h.r_first < l_pac) && p.rbeg >= l_pac) return 0;
+    const int64_t x = p.qbeg - h.q_last, y = p.rbeg - h.r_last;
+    if (y >= 0 && x - y <= w && y - x <= w && x - h.len_last < max_chain_gap && y - h.len_last < max_chain_gap) {
         if (*npool >= AF_G_MAX_OCC) return -1;
         const int k = (*npool)++;
         S.pool[k] = p;
         S.next[k] = -1;
-        S.next[S.last_of[ci]] = k;
+        S.next[h.last] = k;
         S.last_of[ci] = k;
-        ++c.n;
+        S.ch[ci].n = h.n + 1;
+        if (ci < G_CH_LDS) {
+            GChainHot &g = hot[ci];
+            g.r_last = p.rbeg; g.q_last = p.qbeg; g.len_last = p.len; g.n = h.n + 1; g.last = k;
+        }
         return 1;
     }
     return 0;
@@ -794,9 +835,10 @@ __device__ int g_test_and_merge(const G2Scr &S, int ci, const GSeed &p, int rid,
 __device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, int niv, const af_params &p,
                            const GOpt &o, int lane) {
     G2Lds &E = g_g2;
+    GChainLds &C = *reinterpret_cast<GChainLds *>(g_box);
     int nch = 0, npool = 0;
     bool ovf = false;
-    GTree tree{S.kb, 0, 0, S.ch};
+    GTree tree{C.node, S.kb, 0, 0, S.ch, C.ch};
     if (lane == 0) tree.root = gkb_new(tree, 0);
     for (int i = 0; i < niv && !ovf; ++i) {
         const GIv v = iv[i];
@@ -807,7 +849,11 @@ __device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, in
             const int64_t c = c0 + lane;
             const int nb = (int)min((int64_t)64, cnt - c0);
             wave_sync();
-            if (c < cnt) E.occ[lane] = G.sa[v.sa_k + c * step];
+            if (c < cnt) {
+                const int64_t rb = G.sa[v.sa_k + c * step];
+                E.occ[lane] = rb;
+                C.rid[lane] = g_intv2rid(G, rb, rb + slen);
+            }
             wave_sync();
             if (lane == 0) {
                 for (int u = 0; u < nb && !ovf; ++u) {
@@ -815,14 +861,14 @@ __device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, in
                     s.rbeg = E.occ[u];
                     s.qbeg = v.qb;
                     s.len = slen;
-                    const int rid = g_intv2rid(G, s.rbeg, s.rbeg + s.len);
+                    const int rid = C.rid[u];
                     if (rid < 0) continue;
                     bool to_add = false;
                     if (nch) {
                         const int lower = gkb_lower(tree, s.rbeg);
                         if (lower < 0) to_add = true;
                         else {
-                            const int r = g_test_and_merge(S, lower, s, rid, G.l_pac, p.w, o.max_chain_gap, &npool);
+                            const int r = g_test_and_merge(S, C.ch, lower, s, rid, G.l_pac, p.w, o.max_chain_gap, &npool);
                             if (r < 0) ovf = true;
                             else if (!r) to_add = true;
                         }
@@ -834,6 +880,7 @@ __device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, in
                         S.next[kk] = -1;
                         S.ch[nch] = GChain{s.rbeg, 1, -1, rid, 0, 0, kk};
                         S.last_of[nch] = kk;
+                        if (nch < G_CH_LDS) C.ch[nch] = GChainHot{s.rbeg, s.rbeg, s.rbeg, s.qbeg, s.len, s.qbeg, s.len, rid, 1, kk};
                         if (!gkb_putp(tree, nch)) { ovf = true; break; }
                         ++nch;
                     }
