@@ -194,11 +194,15 @@ __device__ __forceinline__ void af_emit_tail(const AfTails &t, const uint8_t *re
 // and the FM occurrence table: per 128 rows, counts of A/C/G/T before the block then the rows'
 // BWT characters at 2 bits (row k of the block at bits 2 (k & 31) of word k >> 5); the '$' row
 // (`primary`) is stored as A and corrected on lookup.
+constexpr int AF_CTG_BKT_SHIFT = 16;
 struct DevGenome {
     const uint8_t *T = nullptr;    // codes 0..3
     int64_t *sa = nullptr;
     uint64_t *occ = nullptr;
     int64_t *ctg_off_d = nullptr, *ctg_len_d = nullptr;  // contigs in pac (bns anns)
+    // contig of each 2^AF_CTG_BKT_SHIFT-base bucket of pac: the rid at its start, bit 31 set when a
+    // contig boundary falls inside (bns_pos2rid then steps from that rid)
+    int32_t *ctg_bkt = nullptr;
     int64_t l_pac = 0, N = 0, primary = -1, n_blk = 0;
     int64_t C[4] = {0, 0, 0, 0};   // first row of the suffixes starting with c
     int64_t base_cnt[4] = {0, 0, 0, 0};

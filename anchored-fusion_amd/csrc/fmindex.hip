@@ -251,6 +251,26 @@ inline dim3 grid_for(int64_t n, int bs = 256) {
 // Builds the index of `n_ctg` contigs of d_blob (device bytes; contig k at blob offset src_off[k],
 // src_len[k] bytes).  Fills *G (device pointers it owns: T, sa, occ, ctg_off, ctg_len) and returns
 // hipSuccess or the first error.  Synchronous on stream s.
+// the contig bucket table (DevGenome::ctg_bkt): one thread per bucket, bns_pos2rid's binary
+// search at the bucket's first and last base
+__device__ int ctg_search(const int64_t *off, int n_ctg, int64_t pos) {
+    int lo = 0, hi = n_ctg;  // the last contig starting at or before pos
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= pos) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__global__ void k_ctg_bkt(const int64_t *__restrict__ off, int n_ctg, int64_t l_pac, int64_t nb, int32_t *__restrict__ bkt) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t p0 = b << AF_CTG_BKT_SHIFT;
+    const int64_t p1 = min(p0 + ((int64_t)1 << AF_CTG_BKT_SHIFT), l_pac) - 1;
+    const int r0 = ctg_search(off, n_ctg, p0), r1 = ctg_search(off, n_ctg, p1);
+    bkt[b] = r0 | (r1 != r0 ? (int32_t)0x80000000 : 0);
+}
+
 hipError_t af_fm_build(const uint8_t *d_blob, const int64_t *src_off, const int64_t *src_len, int n_ctg, DevGenome *G,
                        hipStream_t s) {
     hipError_t ok = hipSuccess;
@@ -281,6 +301,12 @@ hipError_t af_fm_build(const uint8_t *d_blob, const int64_t *src_off, const int6
     FMCHK(hipMalloc(&G->ctg_len_d, sizeof(int64_t) * n_ctg));
     FMCHK(hipMemcpyAsync(G->ctg_off_d, pac_off.data(), sizeof(int64_t) * n_ctg, hipMemcpyHostToDevice, s));
     FMCHK(hipMemcpyAsync(G->ctg_len_d, src_len, sizeof(int64_t) * n_ctg, hipMemcpyHostToDevice, s));
+    {
+        const int64_t nb = ((l_pac - 1) >> AF_CTG_BKT_SHIFT) + 1;
+        FMCHK(hipMalloc(&G->ctg_bkt, sizeof(int32_t) * nb));
+        hipLaunchKernelGGL(k_ctg_bkt, grid_for(nb), dim3(256), 0, s, G->ctg_off_d, n_ctg, l_pac, nb, G->ctg_bkt);
+        FMCHK(hipGetLastError());
+    }
     FMCHK(hipMalloc(&d_src, sizeof(int64_t) * n_ctg));
     FMCHK(hipMemcpyAsync(d_src, src_off, sizeof(int64_t) * n_ctg, hipMemcpyHostToDevice, s));
     // ---- pac and T
@@ -545,6 +571,7 @@ void af_fm_free(DevGenome *G) {
     (void)hipFree(const_cast<uint8_t *>(G->T));
     (void)hipFree(G->sa);
     (void)hipFree(G->occ);
+    (void)hipFree(G->ctg_bkt);
     (void)hipFree(G->ctg_off_d);
     (void)hipFree(G->ctg_len_d);
     *G = DevGenome{};
