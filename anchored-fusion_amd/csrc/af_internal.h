@@ -251,8 +251,15 @@ struct GWork {
     unsigned long long *g1_hv_n = nullptr, *g1_hv_next = nullptr;
     int32_t g1_max_ext = 0;
     GHeavy hv;
+    // G2's dequeue order: the reads by their seed count, largest first (keys / values in, then
+    // sorted; ord_tmp: the radix sort's temporary storage); ord_tmp null = read order
+    uint32_t *ord_key = nullptr, *ord_key_s = nullptr;
+    int32_t *ord_val = nullptr, *ord_val_s = nullptr;
+    void *ord_tmp = nullptr;
+    size_t ord_tmp_bytes = 0;
 };
 size_t af_g1_slot_bytes();
+size_t af_g_order_tmp_bytes(int64_t cap);  // G2 order sort's temporary storage (0: failure)
 size_t af_g2_slot_bytes();
 size_t af_g_chain_bytes();
 size_t af_g_seed_bytes();

@@ -27,6 +27,7 @@
 // rows, query and target windows in LDS (ksw_dp.h g_dp).  Caps equal the oracle's AFO_G_MAX_*;
 // a read past one is reported unmapped with AF_FLAG_MEM_OVERFLOW, counted in the call's stats.
 #include "bwa_dev.h"
+#include <hipcub/hipcub.hpp>
 
 #pragma clang fp contract(off)
 
@@ -1243,20 +1244,6 @@ __device__ int g_patch_reg(const DevGenome &G, const af_params &p, const GReg &a
     return score;
 }
 
-struct GLtArs2 {
-    __device__ bool operator()(const GReg &a, const GReg &b) const { return a.re < b.re; }
-};
-struct GLtArs {
-    __device__ bool operator()(const GReg &a, const GReg &b) const {
-        return a.score > b.score || (a.score == b.score && (a.rb < b.rb || (a.rb == b.rb && a.qb < b.qb)));
-    }
-};
-struct GLtArsHash {
-    __device__ bool operator()(const GReg &a, const GReg &b) const {
-        return a.score > b.score || (a.score == b.score && a.hash < b.hash);
-    }
-};
-
 // ---- region lists sorted through keys in LDS: lane 0's introsort compares and swaps small keys
 // (each region's index with the fields its comparator reads) in the G2 boxes' space, which is dead
 // once a read's chains are extended; the wave then moves the 64-B regions in key order through tmp.
@@ -1524,7 +1511,8 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
                                                      const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
                                                      int64_t cap, int64_t read0, af_params p, GOpt o, GWork w,
                                                      uint8_t *__restrict__ scr_base, size_t scr_stride,
-                                                     uint8_t *__restrict__ zscratch, size_t zstride) {
+                                                     uint8_t *__restrict__ zscratch, size_t zstride,
+                                                     const int32_t *__restrict__ order) {
     const int lane = threadIdx.x;
     int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
     if (n > cap) n = cap;
@@ -1534,7 +1522,7 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
     for (;;) {
         const int it = g_next_item(w.heads, head, heads_left, n - read0, lane);
         if (it < 0) break;
-        const int64_t r = read0 + it;
+        const int64_t r = read0 + (order ? order[it] : it);
         const int l = read_len(lens, r, stride);
         const int niv = w.iv_n[r];
         int nreg = 0;
@@ -1662,34 +1650,7 @@ __global__ __launch_bounds__(64, 2) void k_g_heavy(DevGenome G, const uint8_t *_
 }
 
 // ==================================================================== records
-// mem_mark_primary_se (oracle mark_primary_se), lane 0: a[0, n) sorted by (score desc, hash),
-// secondaries marked; z: scratch
-__device__ void g_mark_primary(GReg *a, int n, int64_t id, const af_params &p, int32_t *z) {
-    if (n == 0) return;
-    for (int i = 0; i < n; ++i) { a[i].sub = 0; a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i)); }
-    ks_introsort(a, n, GLtArsHash());
-    int nz = 0;
-    z[nz++] = 0;
-    for (int i = 1; i < n; ++i) {
-        int k;
-        for (k = 0; k < nz; ++k) {
-            const int j = z[k];
-            const int b_max = a[j].qb > a[i].qb ? a[j].qb : a[i].qb;
-            const int e_min = a[j].qe < a[i].qe ? a[j].qe : a[i].qe;
-            if (e_min > b_max) {
-                const int min_l = a[i].qe - a[i].qb < a[j].qe - a[j].qb ? a[i].qe - a[i].qb : a[j].qe - a[j].qb;
-                if ((float)(e_min - b_max) >= (float)min_l * 0.5f) {
-                    if (a[j].sub == 0) a[j].sub = a[i].score;
-                    break;
-                }
-            }
-        }
-        if (k == nz) z[nz++] = i;
-        else a[i].secondary = z[k];
-    }
-}
-
-// mem_mark_primary_se on the wave: the sort through keys in LDS, then lane 0's walk over the
+// mem_mark_primary_se (oracle mark_primary_se) on the wave: the sort through keys in LDS, then lane 0's walk over the
 // regions' query spans, scores and subs in LDS (the boxes' space); tmp: n regions of scratch
 __device__ void g_mark_primary_w(GReg *a, int n, int64_t id, GReg *tmp, int lane) {
     if (n == 0) return;
@@ -1896,7 +1857,7 @@ __global__ __launch_bounds__(64, 2) void k_g_se(DevGenome G, const uint8_t *__re
         const int na = ovf ? 0 : nr;
         for (int k = lane; k < na; k += 64) S.reg[k] = w.reg[w.reg_off[r] + k];
         wave_sync();
-        if (lane == 0) g_mark_primary(S.reg, na, ids ? ids[r] : id_base + r, p, S.kept);
+        g_mark_primary_w(S.reg, na, ids ? ids[r] : id_base + r, reinterpret_cast<GReg *>(S.seed), lane);
         g_load_read(reads, r, stride, l, lane);
         af_grec *out = recs + r * AF_G_MAX_REC;
         const int nrec = g_reg2sam<CPL>(G, p, l, S.reg, na, 0, nullptr, (int32_t)r, out, zg, lane);
@@ -2287,6 +2248,28 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
     }
 }
 
+// G2's dequeue keys: each read's seed count (bwa's occurrences per interval, at most max_occ)
+// + 1, 0 past the call's reads, so that the sort puts the reads that chain and extend longest
+// first and the makespan is not a heavy read started last
+__global__ void k_g_cost(const int32_t *__restrict__ n_ptr, int64_t cap, int32_t max_occ, GWork w) {
+    int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
+    if (n > cap) n = cap;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < cap; r += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t key = 0;
+        if (r < n) {
+            const int niv = w.iv_n[r];
+            uint64_t c = 0;
+            for (int i = 0; i < niv; ++i) {
+                const int64_t s_ = w.iv[w.iv_off[r] + i].s;
+                c += (uint64_t)(s_ > max_occ ? max_occ : s_);
+            }
+            key = (uint32_t)(c < 0xfffffffeull ? c : 0xfffffffeull) + 1;
+        }
+        w.ord_key[r] = key;
+        w.ord_val[r] = (int32_t)r;
+    }
+}
+
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
@@ -2300,6 +2283,14 @@ __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
 }  // namespace
 
 size_t af_g1_slot_bytes() { return (size_t)G1_SLOT * sizeof(uint4); }
+
+size_t af_g_order_tmp_bytes(int64_t cap) {
+    size_t b = 0;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                      (const int32_t *)nullptr, (int32_t *)nullptr, (int)cap) != hipSuccess)
+        return 0;
+    return b;
+}
 
 #ifdef AF_G_PROF
 static int32_t *h_gprof = nullptr;
@@ -2347,12 +2338,22 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     if (w.g1_max_ext > 0)  // the heavy reads, one wave each, in the lane kernel's (finished) scratch
         hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
                            reinterpret_cast<uint4 *>(g1_scratch), w);
+    const int32_t *order = nullptr;
+    if (w.ord_tmp && cap > 1) {  // G2's reads, most seeds first
+        hipLaunchKernelGGL(k_g_cost, dim3((unsigned)std::min<int64_t>(4096, (cap + 255) / 256)), dim3(256), 0, s, d_n, cap,
+                           p.max_occ, w);
+        size_t tb = w.ord_tmp_bytes;
+        const hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(w.ord_tmp, tb, w.ord_key, w.ord_key_s, w.ord_val,
+                                                                          w.ord_val_s, (int)cap, 0, 32, s);
+        if (e != hipSuccess) return e;
+        order = w.ord_val_s;
+    }
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C)                                                                                                       \
     do {                                                                                                               \
         hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,       \
-                           (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride);                       \
+                           (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride, order);                \
         if (w.hv.min_chains > 0) {                                                                                     \
             hipLaunchKernelGGL((k_g_ext_jobs<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, w);     \
             hipLaunchKernelGGL((k_g_heavy<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, o, w,      \
