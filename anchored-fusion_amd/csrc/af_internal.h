@@ -12,6 +12,9 @@
 #ifndef AF_G1_WPS
 #define AF_G1_WPS 4             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish
 #endif
+#ifndef AF_G2_FIRST_OCC
+#define AF_G2_FIRST_OCC 128     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
+#endif
 #ifndef AF_G1_HEAVY_EXT
 #define AF_G1_HEAVY_EXT 2048    // G1: a read past this many FM extensions moves to the wave-per-read kernel (env AF_G1_HEAVY_EXT)
 #endif
@@ -251,15 +254,15 @@ struct GWork {
     unsigned long long *g1_hv_n = nullptr, *g1_hv_next = nullptr;
     int32_t g1_max_ext = 0;
     GHeavy hv;
-    // G2's dequeue order: the reads by their seed count, largest first (keys / values in, then
-    // sorted; ord_tmp: the radix sort's temporary storage); ord_tmp null = read order
-    uint32_t *ord_key = nullptr, *ord_key_s = nullptr;
-    int32_t *ord_val = nullptr, *ord_val_s = nullptr;
-    void *ord_tmp = nullptr;
-    size_t ord_tmp_bytes = 0;
+    // G2's dequeue order: G1 lists the reads with at least g2_first_occ seeds (bwa's occurrences
+    // per interval, at most max_occ, summed) in g2_list[0, *g2_list_n) and flags them; G2 takes
+    // that list first, then the other reads in order (0 = read order)
+    int32_t *g2_list = nullptr;
+    uint8_t *g2_flag = nullptr;
+    unsigned long long *g2_list_n = nullptr, *g2_list_next = nullptr;
+    int32_t g2_first_occ = 0;
 };
 size_t af_g1_slot_bytes();
-size_t af_g_order_tmp_bytes(int64_t cap);  // G2 order sort's temporary storage (0: failure)
 size_t af_g2_slot_bytes();
 size_t af_g_chain_bytes();
 size_t af_g_seed_bytes();

@@ -78,12 +78,10 @@ struct af_ctx {
     GHeavy g_hv{};
     int32_t g_heavy_min = AF_G_HEAVY_CHAINS;
     int32_t g1_max_ext = AF_G1_HEAVY_EXT;
-    // G2's dequeue order (most seeds first; env AF_G2_ORDER=0: read order)
-    int32_t g2_order = 1;
-    uint32_t *g_ord_key = nullptr, *g_ord_key_s = nullptr;
-    int32_t *g_ord_val = nullptr, *g_ord_val_s = nullptr;
-    void *g_ord_tmp = nullptr;
-    size_t g_ord_tmp_bytes = 0;
+    // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
+    int32_t g2_first_occ = AF_G2_FIRST_OCC;
+    int32_t *g2_list = nullptr;
+    uint8_t *g2_flag = nullptr;
     int64_t *g1_hv = nullptr;       // G1's heavy-read list (ensure_genome_pools)
     GIv *g_iv = nullptr;
     GReg *g_reg = nullptr;
@@ -411,7 +409,8 @@ int ensure_genome_scratch(af_ctx *c) {
     c->g2_waves = std::min(c->n_cu * 8, c->n_slots);
     HIPCHK(c, hipMalloc(&c->g1_scr, af_g1_slot_bytes() * (size_t)c->g1_threads));
     HIPCHK(c, hipMalloc(&c->g2_scr, af_g2_slot_bytes() * (size_t)c->g2_waves));
-    HIPCHK(c, hipMalloc(&c->g_iv_fill, 4 * sizeof(unsigned long long)));  // iv fill, G1 next, G1 heavy count / next
+    // iv fill, G1 next, G1 heavy count / next, G2 first-list count / next
+    HIPCHK(c, hipMalloc(&c->g_iv_fill, 8 * sizeof(unsigned long long)));
     HIPCHK(c, hipMalloc(&c->g_reg_fill, sizeof(int32_t)));
     HIPCHK(c, hipMalloc(&c->g_stats, sizeof(int32_t) * AF_GSTAT_N));
     HIPCHK(c, hipMemset(c->g_stats, 0, sizeof(int32_t) * AF_GSTAT_N));
@@ -454,19 +453,10 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     HIPCHK(c, hipMalloc(&h.sd, af_g_seed_bytes() * h.cap_sd));
     HIPCHK(c, hipMalloc(&h.res, sizeof(GReg) * h.cap_sd));
     if (!h.cnt) HIPCHK(c, hipMalloc(&h.cnt, 8 * sizeof(unsigned long long)));
-    af_free(c->g_ord_key); af_free(c->g_ord_key_s); af_free(c->g_ord_val); af_free(c->g_ord_val_s); af_free(c->g_ord_tmp);
-    c->g_ord_key = c->g_ord_key_s = nullptr; c->g_ord_val = c->g_ord_val_s = nullptr; c->g_ord_tmp = nullptr;
-    c->g_ord_tmp_bytes = 0;
-    if (c->g2_order) {
-        const size_t tb = af_g_order_tmp_bytes(cap);
-        if (!tb) return fail(c, AF_E_HIP, "G2 order sort sizing failed");
-        HIPCHK(c, hipMalloc(&c->g_ord_key, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->g_ord_key_s, sizeof(uint32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->g_ord_val, sizeof(int32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->g_ord_val_s, sizeof(int32_t) * cap));
-        HIPCHK(c, hipMalloc(&c->g_ord_tmp, tb));
-        c->g_ord_tmp_bytes = tb;
-    }
+    af_free(c->g2_list); af_free(c->g2_flag);
+    c->g2_list = nullptr; c->g2_flag = nullptr;
+    HIPCHK(c, hipMalloc(&c->g2_list, sizeof(int32_t) * cap));
+    HIPCHK(c, hipMalloc(&c->g2_flag, cap));
     c->g_cap_reads = cap;
     return AF_OK;
 }
@@ -482,8 +472,8 @@ GWork genome_work(af_ctx *c) {
     w.g1_max_ext = c->g1_hv ? c->g1_max_ext : 0;
     w.hv = c->g_hv;
     w.hv.min_chains = c->g_hv.cnt ? c->g_heavy_min : 0;
-    w.ord_key = c->g_ord_key; w.ord_key_s = c->g_ord_key_s; w.ord_val = c->g_ord_val; w.ord_val_s = c->g_ord_val_s;
-    w.ord_tmp = c->g_ord_tmp; w.ord_tmp_bytes = c->g_ord_tmp_bytes;
+    w.g2_list = c->g2_list; w.g2_flag = c->g2_flag; w.g2_list_n = c->g_iv_fill + 4; w.g2_list_next = c->g_iv_fill + 5;
+    w.g2_first_occ = c->g2_flag ? c->g2_first_occ : 0;
     w.stats = c->g_stats;
     return w;
 }
@@ -592,7 +582,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
-    if (const char *go = getenv("AF_G2_ORDER")) c->g2_order = atoi(go) != 0;
+    if (const char *go = getenv("AF_G2_FIRST_OCC")) c->g2_first_occ = std::max(0, atoi(go));
     if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
@@ -620,7 +610,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g2_scr_pe); af_free(c->zscratch_pe);
     af_free(c->g_hv.read); af_free(c->g_hv.nch); af_free(c->g_hv.ch_off); af_free(c->g_hv.sd_off); af_free(c->g_hv.ch_read);
     af_free(c->g_hv.ch); af_free(c->g_hv.sd); af_free(c->g_hv.res); af_free(c->g_hv.cnt);
-    af_free(c->g_ord_key); af_free(c->g_ord_key_s); af_free(c->g_ord_val); af_free(c->g_ord_val_s); af_free(c->g_ord_tmp);
+    af_free(c->g2_list); af_free(c->g2_flag);
     if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
     af_free(c->g_reg_fill); af_free(c->g_stats); af_free(c->g_iv_n); af_free(c->g_reg_off); af_free(c->g_reg_n); af_free(c->g1_hv);

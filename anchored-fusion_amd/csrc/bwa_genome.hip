@@ -27,7 +27,6 @@
 // rows, query and target windows in LDS (ksw_dp.h g_dp).  Caps equal the oracle's AFO_G_MAX_*;
 // a read past one is reported unmapped with AF_FLAG_MEM_OVERFLOW, counted in the call's stats.
 #include "bwa_dev.h"
-#include <hipcub/hipcub.hpp>
 
 #pragma clang fp contract(off)
 
@@ -322,6 +321,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 if (c > 3) { x = i + 1; st = G1_P3; continue; }
                 need = true; ek = ik_k; el = ik_l; es = ik_s; ec = 3 - c; efwd = true;
             } else {  // G1_DONE: the list sorted by (qb, qe) into the call's pool
+                bool hv = false;  // G2 takes it first
                 if (ovf) w.iv_n[rr] = -1;
                 else {
                     for (int a = 1; a < ni; ++a) {  // equal keys are identical intervals (any order)
@@ -341,13 +341,20 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                         atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
                         w.iv_n[rr] = -1;
                     } else {
+                        int64_t occ = 0;
                         for (int a = 0; a < ni; ++a) {
                             const G1Iv m = g1_unpack(Lf[a]);
                             w.iv[off + a] = GIv{m.k, m.s, m.qb, m.qe};
+                            occ += m.s > p.max_occ ? p.max_occ : m.s;
                         }
                         w.iv_off[rr] = off;
                         w.iv_n[rr] = ni;
+                        hv = w.g2_first_occ > 0 && occ >= w.g2_first_occ;
                     }
+                }
+                if (w.g2_first_occ > 0) {
+                    w.g2_flag[rr] = hv;
+                    if (hv) w.g2_list[atomicAdd(w.g2_list_n, 1ull)] = (int32_t)rr;
                 }
                 GPROF({ int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0); g[1] = ovf ? -1 : ni;
                         g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid;
@@ -550,6 +557,7 @@ __global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t 
         if (lane == 0) {
             const int ni = R.ni;
             uint4 *Lf = R.lst;
+            bool hv = false;  // G2 takes it first
             if (R.ovf) w.iv_n[rr] = -1;
             else {
                 for (int a = 1; a < ni; ++a) {
@@ -569,13 +577,20 @@ __global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t 
                     atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
                     w.iv_n[rr] = -1;
                 } else {
+                    int64_t occ = 0;
                     for (int a = 0; a < ni; ++a) {
                         const G1Iv m = g1_unpack(Lf[a]);
                         w.iv[off + a] = GIv{m.k, m.s, m.qb, m.qe};
+                        occ += m.s > p.max_occ ? p.max_occ : m.s;
                     }
                     w.iv_off[rr] = off;
                     w.iv_n[rr] = ni;
+                    hv = w.g2_first_occ > 0 && occ >= w.g2_first_occ;
                 }
+            }
+            if (w.g2_first_occ > 0) {
+                w.g2_flag[rr] = hv;
+                if (hv) w.g2_list[atomicAdd(w.g2_list_n, 1ull)] = (int32_t)rr;
             }
         }
         g1w_sync();
@@ -1511,18 +1526,30 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
                                                      const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
                                                      int64_t cap, int64_t read0, af_params p, GOpt o, GWork w,
                                                      uint8_t *__restrict__ scr_base, size_t scr_stride,
-                                                     uint8_t *__restrict__ zscratch, size_t zstride,
-                                                     const int32_t *__restrict__ order) {
+                                                     uint8_t *__restrict__ zscratch, size_t zstride) {
     const int lane = threadIdx.x;
     int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
     if (n > cap) n = cap;
     const G2Scr S = g2_scr(scr_base + (size_t)blockIdx.x * scr_stride);
     uint8_t *zg = zscratch + (size_t)blockIdx.x * zstride;
     int head = (int)(blockIdx.x & 7), heads_left = 8;
+    // G1's list of the reads with the most seeds first, then the others in order
+    bool first = w.g2_first_occ > 0;
+    const int64_t n_first = first ? (int64_t)*(volatile unsigned long long *)w.g2_list_n : 0;
     for (;;) {
-        const int it = g_next_item(w.heads, head, heads_left, n - read0, lane);
-        if (it < 0) break;
-        const int64_t r = read0 + (order ? order[it] : it);
+        int64_t r;
+        if (first) {
+            int h = 0;
+            if (lane == 0) h = (int)atomicAdd(w.g2_list_next, 1ull);
+            h = __builtin_amdgcn_readfirstlane(h);
+            if (h >= n_first) { first = false; continue; }
+            r = w.g2_list[h];
+        } else {
+            const int it = g_next_item(w.heads, head, heads_left, n - read0, lane);
+            if (it < 0) break;
+            r = read0 + it;
+            if (w.g2_first_occ > 0 && w.g2_flag[r]) continue;
+        }
         const int l = read_len(lens, r, stride);
         const int niv = w.iv_n[r];
         int nreg = 0;
@@ -2248,32 +2275,11 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
     }
 }
 
-// G2's dequeue keys: each read's seed count (bwa's occurrences per interval, at most max_occ)
-// + 1, 0 past the call's reads, so that the sort puts the reads that chain and extend longest
-// first and the makespan is not a heavy read started last
-__global__ void k_g_cost(const int32_t *__restrict__ n_ptr, int64_t cap, int32_t max_occ, GWork w) {
-    int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
-    if (n > cap) n = cap;
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < cap; r += (int64_t)gridDim.x * blockDim.x) {
-        uint32_t key = 0;
-        if (r < n) {
-            const int niv = w.iv_n[r];
-            uint64_t c = 0;
-            for (int i = 0; i < niv; ++i) {
-                const int64_t s_ = w.iv[w.iv_off[r] + i].s;
-                c += (uint64_t)(s_ > max_occ ? max_occ : s_);
-            }
-            key = (uint32_t)(c < 0xfffffffeull ? c : 0xfffffffeull) + 1;
-        }
-        w.ord_key[r] = key;
-        w.ord_val[r] = (int32_t)r;
-    }
-}
-
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
     if (t == 1 && w.g1_hv_n) { *w.g1_hv_n = 0; *w.g1_hv_next = 0; }
+    if (t == 2 && w.g2_list_n) { *w.g2_list_n = 0; *w.g2_list_next = 0; }
     if (t < 7 && w.hv.cnt) w.hv.cnt[t] = 0;  // [5] k_g_pe's and [6] k_g_se's dequeue counters too
     if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
     if (t < AF_GSTAT_N) w.stats[t] = 0;
@@ -2284,13 +2290,6 @@ __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
 
 size_t af_g1_slot_bytes() { return (size_t)G1_SLOT * sizeof(uint4); }
 
-size_t af_g_order_tmp_bytes(int64_t cap) {
-    size_t b = 0;
-    if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                      (const int32_t *)nullptr, (int32_t *)nullptr, (int)cap) != hipSuccess)
-        return 0;
-    return b;
-}
 
 #ifdef AF_G_PROF
 static int32_t *h_gprof = nullptr;
@@ -2338,22 +2337,12 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     if (w.g1_max_ext > 0)  // the heavy reads, one wave each, in the lane kernel's (finished) scratch
         hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
                            reinterpret_cast<uint4 *>(g1_scratch), w);
-    const int32_t *order = nullptr;
-    if (w.ord_tmp && cap > 1) {  // G2's reads, most seeds first
-        hipLaunchKernelGGL(k_g_cost, dim3((unsigned)std::min<int64_t>(4096, (cap + 255) / 256)), dim3(256), 0, s, d_n, cap,
-                           p.max_occ, w);
-        size_t tb = w.ord_tmp_bytes;
-        const hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(w.ord_tmp, tb, w.ord_key, w.ord_key_s, w.ord_val,
-                                                                          w.ord_val_s, (int)cap, 0, 32, s);
-        if (e != hipSuccess) return e;
-        order = w.ord_val_s;
-    }
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C)                                                                                                       \
     do {                                                                                                               \
         hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,       \
-                           (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride, order);                \
+                           (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride);                       \
         if (w.hv.min_chains > 0) {                                                                                     \
             hipLaunchKernelGGL((k_g_ext_jobs<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, w);     \
             hipLaunchKernelGGL((k_g_heavy<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, o, w,      \
