@@ -8,3 +8,5 @@ python3 scripts/timeline.py $O $ms > $O/timeline.txt; grep -v "rocclr\|rocprim\|
 AF_S4_SPLIT=0 timeout -k 10 300 python3 -u scripts/g_prof.py > $O/gprof.log 2>&1 || { tail -30 $O/gprof.log; exit 1; }
 timeout -k 10 300 python3 -u scripts/blat_prof.py 50000000 $O/blat_phases_c3.json > $O/blat_prof.log 2>&1 || { tail -30 $O/blat_prof.log; exit 1; }
 tail -3 $O/blat_prof.log
+WORLD=c3 PAIRS=8000000 READ_LEN=150 timeout -k 10 300 python3 -u scripts/s2_prof.py > $O/s2_prof.log 2>&1 || { tail -30 $O/s2_prof.log; exit 1; }
+tail -25 $O/s2_prof.log
