@@ -2344,7 +2344,7 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
         hipLaunchKernelGGL((k_g_regions<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,       \
                            (int64_t)0, p, o, w, g2_scratch, g2_slot_bytes(), zscratch, zstride);                       \
         if (w.hv.min_chains > 0) {                                                                                     \
-            hipLaunchKernelGGL((k_g_ext_jobs<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, w);     \
+            hipLaunchKernelGGL((k_g_ext_jobs<C>), dim3(2 * n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, w); \
             hipLaunchKernelGGL((k_g_heavy<C>), dim3(n_g2_waves), dim3(64), 0, s, G, reads, stride, lens, p, o, w,      \
                                g2_scratch, g2_slot_bytes(), zscratch, zstride);                                        \
         }                                                                                                              \
