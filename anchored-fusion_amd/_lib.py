@@ -23,6 +23,7 @@ CSRC = os.path.join(HERE, "csrc")
 
 AF_OK = 0
 AF_E_INVALID, AF_E_HIP, AF_E_CAPACITY, AF_E_NOMEM, AF_E_UNSUPPORTED = -1, -2, -3, -4, -5
+AF_BLAT_LONG_MAX = 131072
 AF_MAX_CIGAR = 32
 AF_MAX_READ = 320
 AF_K = 16
@@ -42,6 +43,8 @@ EXPORTS = (
     "af_genome_primary", "af_genome_read", "af_genome_align_se_device", "af_genome_align_pe_device",
     "af_genome_align_se", "af_genome_align_pe", "af_genome_regions", "af_genome_stats", "af_s5_filter_device",
     "af_genome_align_se_ids_device", "af_genome_align_pe_se_device", "af_genome_intervals", "af_s5_rules_host", "af_blat_caps", "af_blat_spill",
+    "af_blat_query_caps", "af_s6_queries_device", "af_s6_check_device", "af_s6_compact_device",
+    "af_blat_device_begin", "af_blat_device_end", "af_blat_long", "af_blat_heavy_stats",
 )
 AF_G_MAX_REC = 8
 AF_GSTAT_N = 4
@@ -67,6 +70,15 @@ class Pe(ctypes.Structure):
 class AlnOut(ctypes.Structure):
     _fields_ = [("flag", ctypes.c_void_p), ("pos", ctypes.c_void_p), ("score", ctypes.c_void_p),
                 ("n_cigar", ctypes.c_void_p), ("hits", ctypes.c_void_p), ("cigar", ctypes.c_void_p)]
+
+
+class S6Set(ctypes.Structure):
+    """af_s6_set: S6 query rows with their BLAT rows, spill pool and per-query cap counters."""
+    _fields_ = [("q", ctypes.c_void_p), ("stride", ctypes.c_int32), ("pad0", ctypes.c_int32),
+                ("lens", ctypes.c_void_p), ("src", ctypes.c_void_p), ("n", ctypes.c_void_p), ("over", ctypes.c_void_p),
+                ("n_over", ctypes.c_void_p), ("rows", ctypes.c_void_p), ("n_rows", ctypes.c_void_p),
+                ("caps", ctypes.c_void_p), ("spill_rows", ctypes.c_void_p), ("spill_query", ctypes.c_void_p),
+                ("spill_n", ctypes.c_void_p), ("spill_cap", ctypes.c_int64), ("cap", ctypes.c_int64)]
 
 
 def build(force=False):
@@ -206,6 +218,23 @@ def lib():
     L.af_blat_caps.restype = ctypes.c_int
     L.af_blat_spill.argtypes = [_vp, _vp, _vp, _vp, _i64]
     L.af_blat_spill.restype = ctypes.c_int
+    L.af_blat_query_caps.argtypes = [_vp, _vp, _i64]
+    L.af_blat_query_caps.restype = ctypes.c_int
+    _s6 = ctypes.POINTER(S6Set)
+    L.af_s6_queries_device.argtypes = [_vp, _i64, _vp, _i32, _vp, _vp, ctypes.POINTER(AlnOut), _vp, _s6, _vp]
+    L.af_s6_queries_device.restype = ctypes.c_int
+    L.af_s6_check_device.argtypes = [_vp, _vp, _vp, _i64, _vp, ctypes.POINTER(AlnOut), _vp, _s6, _vp, _vp]
+    L.af_s6_check_device.restype = ctypes.c_int
+    L.af_s6_compact_device.argtypes = [_vp, _s6, _vp, _s6, _i32, _vp]
+    L.af_s6_compact_device.restype = ctypes.c_int
+    L.af_blat_device_begin.argtypes = [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _vp, _i32, _vp, _vp, _vp]
+    L.af_blat_device_begin.restype = ctypes.c_int
+    L.af_blat_device_end.argtypes = [_vp, _vp, _vp]
+    L.af_blat_device_end.restype = ctypes.c_int
+    L.af_blat_long.argtypes = [_vp, _vp, ctypes.c_char_p, _i32, _vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp]
+    L.af_blat_long.restype = ctypes.c_int
+    L.af_blat_heavy_stats.argtypes = [_vp, _vp]
+    L.af_blat_heavy_stats.restype = ctypes.c_int
     _L = L
     return L
 

@@ -22,8 +22,11 @@ PSL_DTYPE = np.dtype([(n, "<i4") for n in (
     ("t_start", "<i8"), ("t_end", "<i8"), ("block_sizes", "<i4", (16,)), ("q_starts", "<i4", (16,)),
     ("t_starts", "<i8", (16,))])
 assert PSL_DTYPE.itemsize == 328
+BLOCK_DTYPE = np.dtype([("size", "<i4"), ("q_start", "<i4"), ("t_start", "<i8")])  # af_psl_block
 TILE = 11
 MAX_ROWS = 16
+LONG_MAX = 131072   # AF_BLAT_LONG_MAX: the longest query af_blat_long searches whole
+LONG_ROWS = 4096    # rows a long search returns (every row is counted)
 CAP_NAMES = ("hits", "clumps", "parts", "rows")  # af_blat_caps' counters, in order
 
 # the reference's option sets (functions.py call sites); rep_match None = BLAT's default
@@ -119,7 +122,7 @@ class TileReference:
                                                    nr.ctypes.data), "af_blat")
         return rows, nr
 
-    def search_all(self, seqs, p):
+    def search_all(self, seqs, p, spill_cap=None):
         """Every row of every query, as BLAT prints them: (rows [n, MAX_ROWS], n_rows [n], {query:
         [its rows past MAX_ROWS]}) -- af_blat_device with the spill pool on this reference's
         context (device buffers made here; the rows come back to the host)."""
@@ -134,7 +137,7 @@ class TileReference:
         n_t = torch.tensor([n], dtype=torch.int32, device=dev)
         rows_t = torch.zeros(n * MAX_ROWS * PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         nr_t = torch.zeros(n, dtype=torch.int32, device=dev)
-        cap = max(1024, 4 * n)
+        cap = spill_cap or max(1024, 4 * n)
         sp = dict(rows=torch.zeros(cap * PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev),
                   q=torch.zeros(cap, dtype=torch.int32, device=dev), n=torch.zeros(1, dtype=torch.int32, device=dev))
         stream = torch.cuda.current_stream(dev)
@@ -152,11 +155,61 @@ class TileReference:
                              sp["q"][:ns].cpu().numpy())
         return rows, nr_t.cpu().numpy(), extra
 
+    def search_long(self, seq, p, max_rows=LONG_ROWS):
+        """af_blat_long: one query longer than a read (the anchor transcript, fn:341 / fn:966) searched
+        whole -> (rows [k] PSL_DTYPE best first, n_rows (all rows), blocks BLOCK_DTYPE, block_off
+        [k + 1]): row i's blocks are blocks[block_off[i]:block_off[i + 1]]."""
+        b = seq.encode() if isinstance(seq, str) else bytes(seq)
+        if len(b) > LONG_MAX:
+            raise ValueError(f"query longer than {LONG_MAX}")
+        rows = np.zeros(max_rows, dtype=PSL_DTYPE)
+        nr = np.zeros(1, np.int32)
+        off = np.zeros(max_rows + 1, np.int64)
+        nb = np.zeros(1, np.int64)
+        cap = 1 << 16
+        while True:
+            blocks = np.zeros(cap, dtype=BLOCK_DTYPE)
+            rc = _lib.lib().af_blat_long(self.ctx, self.idx, b, len(b), ctypes.byref(p), int(max_rows), rows.ctypes.data,
+                                         nr.ctypes.data, blocks.ctypes.data, cap, off.ctypes.data, nb.ctypes.data)
+            if rc == _lib.AF_E_CAPACITY and int(nb[0]) > cap:
+                cap = int(nb[0])
+                continue
+            _lib.check(self.ctx, rc, "af_blat_long")
+            k = min(int(nr[0]), int(max_rows))
+            return rows[:k].copy(), int(nr[0]), blocks[:int(off[k])].copy(), off[:k + 1].copy()
+
     def search_device(self, queries_t, n_queries_t, stride, rows_t, n_rows_t, lens_t=None, p=None, max_rows=MAX_ROWS,
                       stream=None, first_t=None):
         """af_blat_device on device buffers (rows_t: cap * max_rows * 328 bytes); first_t (an int32
         device word, optional): search only the queries from *first_t on (af_blat_device_range)."""
         from .align import _stream_handle
+        cap = self._check_device(queries_t, stride, rows_t, n_rows_t, lens_t, max_rows)
+        _lib.check(self.ctx, _lib.lib().af_blat_device_range(
+            self.ctx, self.idx, queries_t.data_ptr(), None if first_t is None else first_t.data_ptr(),
+            n_queries_t.data_ptr(), cap, int(stride), None if lens_t is None else lens_t.data_ptr(),
+            ctypes.byref(p or params()), int(max_rows), rows_t.data_ptr(), n_rows_t.data_ptr(),
+            _stream_handle(stream)), "af_blat_device_range")
+
+    def search_device_begin(self, queries_t, n_queries_t, stride, rows_t, n_rows_t, lens_t=None, p=None,
+                            max_rows=MAX_ROWS, stream=None):
+        """af_blat_device_begin: the per-strand pass of a device search (the heavy strands' clumps
+        left as jobs); search_device_end finishes it for the live queries."""
+        from .align import _stream_handle
+        cap = self._check_device(queries_t, stride, rows_t, n_rows_t, lens_t, max_rows)
+        _lib.check(self.ctx, _lib.lib().af_blat_device_begin(
+            self.ctx, self.idx, queries_t.data_ptr(), n_queries_t.data_ptr(), cap, int(stride),
+            None if lens_t is None else lens_t.data_ptr(), ctypes.byref(p or params()), int(max_rows),
+            rows_t.data_ptr(), n_rows_t.data_ptr(), _stream_handle(stream)), "af_blat_device_begin")
+
+    def search_device_end(self, live_t=None, stream=None):
+        """af_blat_device_end: the deferred strands and the rows of the queries with live_t[q] != 0
+        (uint8 device flags; None: every query)."""
+        from .align import _stream_handle
+        _lib.check(self.ctx, _lib.lib().af_blat_device_end(
+            self.ctx, None if live_t is None else live_t.data_ptr(), _stream_handle(stream)), "af_blat_device_end")
+
+    @staticmethod
+    def _check_device(queries_t, stride, rows_t, n_rows_t, lens_t, max_rows):
         cap = int(queries_t.shape[0])
         if queries_t.dim() != 2 or int(queries_t.shape[1]) < int(stride):
             raise ValueError("queries_t must be [cap, >= stride]")
@@ -164,11 +217,7 @@ class TileReference:
             raise ValueError("rows_t / n_rows_t too small for cap queries")
         if lens_t is not None and lens_t.numel() < cap:
             raise ValueError("lens_t holds fewer than cap entries")
-        _lib.check(self.ctx, _lib.lib().af_blat_device_range(
-            self.ctx, self.idx, queries_t.data_ptr(), None if first_t is None else first_t.data_ptr(),
-            n_queries_t.data_ptr(), cap, int(stride), None if lens_t is None else lens_t.data_ptr(),
-            ctypes.byref(p or params()), int(max_rows), rows_t.data_ptr(), n_rows_t.data_ptr(),
-            _stream_handle(stream)), "af_blat_device_range")
+        return cap
 
     def spill_to(self, rows_t=None, query_t=None, n_t=None):
         """af_blat_spill: later device searches on this reference's context append each query's
@@ -180,6 +229,25 @@ class TileReference:
         cap = min(rows_t.numel() * rows_t.element_size() // PSL_DTYPE.itemsize, int(query_t.numel()))
         _lib.check(self.ctx, _lib.lib().af_blat_spill(self.ctx, rows_t.data_ptr(), query_t.data_ptr(), n_t.data_ptr(),
                                                       int(cap)), "af_blat_spill")
+
+    def query_caps_to(self, counts_t=None, cap=0):
+        """af_blat_query_caps: later device searches on this reference's context count their cap
+        events per query in counts_t (int32 [4 * cap], zeroed by the caller: counter k of query q
+        at k * cap + q); no arguments: unregister."""
+        if counts_t is None:
+            _lib.check(self.ctx, _lib.lib().af_blat_query_caps(self.ctx, None, 0), "af_blat_query_caps")
+            return
+        if counts_t.numel() < len(CAP_NAMES) * int(cap):
+            raise ValueError("counts_t holds fewer than 4 * cap counters")
+        _lib.check(self.ctx, _lib.lib().af_blat_query_caps(self.ctx, counts_t.data_ptr(), int(cap)),
+                   "af_blat_query_caps")
+
+    def heavy_stats(self):
+        """af_blat_heavy_stats of the last device search: strands deferred, their jobs, jobs aligned,
+        strands chained (synchronises)."""
+        out = np.zeros(4, np.int32)
+        _lib.check(self.ctx, _lib.lib().af_blat_heavy_stats(self.ctx, out.ctypes.data), "af_blat_heavy_stats")
+        return dict(zip(("deferred", "jobs", "aligned", "chained"), (int(v) for v in out)))
 
     def caps(self, reset=True):
         """af_blat_caps: query strands / queries at each of the search's caps since the last reset
@@ -204,8 +272,9 @@ PSL_ORDER = ("score", "strand", "t_start", "q_start", "t_end", "q_end")  # psl_b
 
 def spilled_rows(rows, query):
     """The spill pool's rows (PSL_DTYPE [n], query index [n]) grouped per query in the search's row
-    order (score desc, strand, tStart, qStart, tEnd, qEnd): {query: [row, ...]}.  They follow the
-    query's kept rows."""
+    order (score desc, strand, tStart, qStart, tEnd, qEnd; rows equal on all six -- the pool holds
+    them in atomic order -- by their bytes, so the order does not depend on the run): {query: [row,
+    ...]}.  They follow the query's kept rows."""
     out = {}
     if len(rows) == 0:
         return out
@@ -213,6 +282,31 @@ def spilled_rows(rows, query):
                         -rows["score"].astype(np.int64), query))
     for i in order:
         out.setdefault(int(query[i]), []).append(rows[i])
+    for q, rs in out.items():  # exact ties of the six keys: by the row's bytes
+        keys = [tuple(int(r[f]) for f in PSL_ORDER) for r in rs]
+        if len(set(keys)) < len(keys):
+            out[q] = [r for _, _, r in sorted(((-k[0],) + k[1:], r.tobytes(), r) for k, r in zip(keys, rs))]
+    return out
+
+
+def psl_lines_long(ref, name, seq, rows, blocks, block_off):
+    """PSL lines of one long query's rows (search_long): every block of each row."""
+    out = []
+    L = len(seq)
+    for i, r in enumerate(rows):
+        loc = ref.locate(r["t_start"], r["t_end"])
+        if loc is None:
+            continue
+        tk, ts, te = loc
+        base = ref.offsets[tk]
+        bl = blocks[int(block_off[i]):int(block_off[i + 1])]
+        qs = [int(b["q_start"]) for b in bl]  # '-': on the reverse-complemented query, as BLAT prints them
+        f = [int(r["matches"]), int(r["mismatches"]), 0, int(r["n_count"]), int(r["q_num_insert"]),
+             int(r["q_base_insert"]), int(r["t_num_insert"]), int(r["t_base_insert"]), "-" if r["strand"] else "+", name,
+             L, int(r["q_start"]), int(r["q_end"]), ref.names[tk], ref.lens[tk], ts, te, len(bl),
+             ",".join(str(int(b["size"])) for b in bl) + ",", ",".join(map(str, qs)) + ",",
+             ",".join(str(int(b["t_start"]) - base) for b in bl) + ","]
+        out.append("\t".join(map(str, f)) + "\n")
     return out
 
 

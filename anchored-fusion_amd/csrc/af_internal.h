@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <vector>
 #include "../../include/afgpu.h"
 
 #define AF_NEG_INF (-0x40000000)
@@ -340,12 +341,91 @@ struct BlatSpill {
     int32_t *query = nullptr, *n = nullptr;
     int64_t cap = 0;
 };
-hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
-                          int64_t cap,
-                          int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
-                          uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, const BlatSpill &spill,
-                          hipStream_t s);
+// where a search's cap events (AF_BLAT_CAP_*) are counted: per query in q[k * qcap + query] when
+// registered (af_blat_query_caps; queries past qcap and no registration: the context's counters)
+struct BlatCaps {
+    int32_t *ctx = nullptr;
+    int32_t *q = nullptr;
+    int64_t qcap = 0;
+    __device__ void hit(int64_t query, int k) const {
+        if (q && query >= 0 && query < qcap) atomicAdd(&q[k * qcap + query], 1);
+        else if (ctx) atomicAdd(&ctx[k], 1);
+    }
+};
+// A heavy strand (more than min_clumps clumps) is deferred by k_blat: its clumps go to the job pool
+// (aligned one job per wave by k_blat_jobs) and its entry to the strand table (chained by
+// k_blat_heavy).  ctrl: AF_BLAT_HV_CTRL_WORDS words, one 128-B line apart: the pool fills, the first
+// job offset that did not fit, and the two kernels' dequeue heads.
+struct BlatJob {
+    int32_t q, hs;  // the clump's seed (query offset, target position t) and its strand table entry
+    int64_t t;
+};
+#define AF_BLAT_HV_JOBS_N 0
+#define AF_BLAT_HV_JOBS_VALID (1 * AF_HEAD_STRIDE)
+#define AF_BLAT_HV_STRANDS_N (2 * AF_HEAD_STRIDE)
+#define AF_BLAT_HV_JOB_HEADS (3 * AF_HEAD_STRIDE)
+#define AF_BLAT_HV_STRAND_HEADS (11 * AF_HEAD_STRIDE)
+#define AF_BLAT_HV_JOBS_DONE (19 * AF_HEAD_STRIDE)     // jobs aligned (k_blat_jobs)
+#define AF_BLAT_HV_STRANDS_DONE (20 * AF_HEAD_STRIDE)  // deferred strands chained (k_blat_heavy)
+#define AF_BLAT_HV_CTRL_WORDS (21 * AF_HEAD_STRIDE)
+#ifndef AF_BLAT_HEAVY_CLUMPS
+#define AF_BLAT_HEAVY_CLUMPS 32  // default: strands with more clumps are deferred (env AF_BLAT_HEAVY_CLUMPS)
+#endif
+struct BlatHeavy {
+    int32_t min_clumps = 0;   // 0: no strand is deferred
+    BlatJob *jobs = nullptr;
+    int64_t jobs_cap = 0;
+    void *parts = nullptr;    // one blat.hip Reg (af_blat_part_bytes) per job
+    uint8_t *part_ok = nullptr;
+    int4 *strands = nullptr;  // {item, first job, clumps (0: not deferred after all), 0}
+    int64_t strands_cap = 0;
+    int32_t *ctrl = nullptr, *jobs_n = nullptr, *jobs_valid = nullptr, *strands_n = nullptr;
+};
+size_t af_blat_part_bytes();
+// one BLAT search's launch arguments
+struct BlatLaunch {
+    DevTile X;
+    const uint8_t *queries = nullptr;
+    const int32_t *n_queries = nullptr, *q_first = nullptr;
+    int64_t cap = 0;
+    int32_t stride = 0;
+    const int32_t *lens = nullptr;
+    af_blat_params p{};
+    int32_t *heads = nullptr;
+    uint8_t *bscratch = nullptr;
+    int32_t n_slots = 0;
+    af_psl *rows = nullptr;
+    int32_t *n_rows = nullptr;
+    int32_t max_rows = 0;
+    const int32_t *order = nullptr;
+    af_psl *stage = nullptr;
+    int32_t *stage_n = nullptr;
+    BlatCaps caps;
+    BlatSpill spill;
+    BlatHeavy hv;
+};
+// af_launch_blat = _begin (k_blat: every strand with at most hv.min_clumps clumps searched) + _end
+// (the deferred strands' jobs and chains, then the rows of every query: live[q] == 0 -> no rows)
+hipError_t af_launch_blat_begin(const BlatLaunch &B, hipStream_t s);
+hipError_t af_launch_blat_end(const BlatLaunch &B, const uint8_t *live, hipStream_t s);
+hipError_t af_launch_blat(const BlatLaunch &B, hipStream_t s);
+// blat_long.hip: one long query (codes of both strands at d_q2, strand s at d_q2 + s L) -> every
+// row (unsorted), its strand's emission order, its first block in `blocks`; cap events to caps
+hipError_t af_blat_long_run(const DevTile &X, const uint8_t *d_q2, int L, const af_blat_params &bp, int32_t *caps,
+                            std::vector<af_psl> &rows, std::vector<int32_t> &seq, std::vector<int64_t> &boff,
+                            std::vector<af_psl_block> &blocks, int n_cu, hipStream_t s);
+// s5s6.hip: S6 rows of the QNAME-group leaders before the check, and their compaction after it
+hipError_t af_launch_s6_queries(int64_t n, const uint8_t *q, int32_t q_stride, const int32_t *q_lens,
+                                const int32_t *q_rows, const af_aln_out &s2, const uint8_t *cont, const af_s6_set &pre,
+                                uint8_t *keep, int32_t *sel, int64_t *n_sel, void *temp, size_t temp_bytes,
+                                hipStream_t s);
+size_t af_s6_compact_temp_bytes(int64_t n);
+hipError_t af_launch_s6_check(const af_grec *recs, const int32_t *n_rec, int64_t n, const int32_t *q_rows,
+                              const af_aln_out &s2, const uint8_t *cont, const af_s6_set &pre, uint8_t *keep,
+                              uint8_t *live, hipStream_t s);
+hipError_t af_launch_s6_compact(const af_s6_set &pre, const uint8_t *live, const af_s6_set &out, int32_t max_rows,
+                                int32_t *caps, int32_t *flag, int32_t *idx, int32_t *sflag, int32_t *sidx, void *temp,
+                                size_t temp_bytes, hipStream_t s);
 // k_blat's schedule: the queries by estimated cost, heaviest first (work: af_blat_order_bytes(cap))
 size_t af_blat_order_bytes(int64_t cap);
 hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, int64_t cap,

@@ -32,6 +32,12 @@ struct af_ctx {
     int64_t blat_ord_cap = 0;
     int32_t *blat_caps = nullptr;   // AF_BLAT_CAP_N counters, cumulative until af_blat_caps resets them
     BlatSpill blat_spill;           // af_blat_spill's pool (caller-owned device buffers)
+    int32_t *blat_qcaps = nullptr;  // af_blat_query_caps' per-query counters (caller-owned), their query capacity
+    int64_t blat_qcap = 0;
+    BlatHeavy blat_hv;              // the deferred strands' job pool, part pool and strand table
+    int32_t blat_heavy_min = AF_BLAT_HEAVY_CLUMPS;
+    BlatLaunch blat_pending;        // af_blat_device_begin's search, finished by af_blat_device_end
+    bool blat_open = false;
     af_psl *blat_stage = nullptr;   // per (query, strand) rows before k_blat_merge
     int32_t *blat_stage_n = nullptr;
     int64_t blat_stage_rows = 0, blat_stage_items = 0;
@@ -104,6 +110,11 @@ struct af_ctx {
     void *s5_temp = nullptr;
     size_t s5_temp_bytes = 0;
     int64_t s5_cap = 0;
+    // af_s6_compact_device: the pre rows' survivor flags and new indices, the spill pool's, scan scratch
+    int32_t *s6_flag = nullptr, *s6_idx = nullptr, *s6_sflag = nullptr, *s6_sidx = nullptr;
+    void *s6_temp = nullptr;
+    size_t s6_temp_bytes = 0;
+    int64_t s6_cap = 0, s6_spill_cap = 0;
 };
 
 struct af_genome {
@@ -244,6 +255,32 @@ int ensure_zscratch(af_ctx *c) {
     if (c->zscratch) return AF_OK;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     HIPCHK(c, hipMalloc(&c->zscratch, zstride * c->n_slots));
+    return AF_OK;
+}
+
+// the deferred strands' pools for a search of cap queries (grow-only): jobs for 64 clumps per query
+// (at least 16 K, at most 1 M: a strand that does not fit is searched by k_blat itself)
+int ensure_blat_heavy(af_ctx *c, int64_t cap) {
+    BlatHeavy &h = c->blat_hv;
+    h.min_clumps = c->blat_heavy_min;
+    if (h.min_clumps <= 0) return AF_OK;
+    const int64_t jobs = std::min<int64_t>(1 << 20, std::max<int64_t>(1 << 14, 64 * cap));
+    const int64_t strands = std::min<int64_t>(1 << 16, std::max<int64_t>(1024, 2 * cap));
+    if (h.ctrl && h.jobs_cap >= jobs && h.strands_cap >= strands) return AF_OK;
+    if (h.ctrl) HIPCHK(c, hipDeviceSynchronize());  // an earlier search may still use the pools
+    af_free(h.jobs); af_free(h.parts); af_free(h.part_ok); af_free(h.strands); af_free(h.ctrl);
+    h = BlatHeavy{};
+    h.min_clumps = c->blat_heavy_min;
+    HIPCHK(c, hipMalloc(&h.jobs, sizeof(BlatJob) * jobs));
+    HIPCHK(c, hipMalloc(&h.parts, af_blat_part_bytes() * jobs));
+    HIPCHK(c, hipMalloc(&h.part_ok, jobs));
+    HIPCHK(c, hipMalloc(&h.strands, sizeof(int4) * strands));
+    HIPCHK(c, hipMalloc(&h.ctrl, sizeof(int32_t) * AF_BLAT_HV_CTRL_WORDS));
+    h.jobs_cap = jobs;
+    h.strands_cap = strands;
+    h.jobs_n = h.ctrl + AF_BLAT_HV_JOBS_N;
+    h.jobs_valid = h.ctrl + AF_BLAT_HV_JOBS_VALID;
+    h.strands_n = h.ctrl + AF_BLAT_HV_STRANDS_N;
     return AF_OK;
 }
 
@@ -582,6 +619,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
+    if (const char *hv = getenv("AF_BLAT_HEAVY_CLUMPS")) c->blat_heavy_min = std::max(0, atoi(hv));  // 0: none deferred
     if (const char *go = getenv("AF_G2_FIRST_OCC")) c->g2_first_occ = std::max(0, atoi(go));
     if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
@@ -617,6 +655,9 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g_iv_off); af_free(c->g_ghist); af_free(c->g_nchunks); af_free(c->g_cstart); af_free(c->g_scan);
     af_free(c->g_pes); af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens); af_free(c->g_hreads);
     af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_nsel); af_free(c->s5_temp);
+    af_free(c->s6_flag); af_free(c->s6_idx); af_free(c->s6_sflag); af_free(c->s6_sidx); af_free(c->s6_temp);
+    af_free(c->blat_hv.jobs); af_free(c->blat_hv.parts); af_free(c->blat_hv.part_ok); af_free(c->blat_hv.strands);
+    af_free(c->blat_hv.ctrl);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1073,6 +1114,22 @@ static int check_blat(af_ctx *c, const af_index *ix, const af_blat_params *p, in
     return AF_OK;
 }
 
+// a search's launch arguments on c's scratch; defer_heavy: heavy strands become jobs (c->blat_hv)
+static BlatLaunch blat_launch(af_ctx *c, const af_index *ix, const uint8_t *q, const int32_t *n_q, const int32_t *first,
+                              int64_t cap, int32_t stride, const int32_t *lens, const af_blat_params &p, af_psl *rows,
+                              int32_t *n_rows, int32_t max_rows, const int32_t *order, bool with_spill) {
+    BlatLaunch B;
+    B.X = ix->tile;
+    B.queries = q; B.n_queries = n_q; B.q_first = first; B.cap = cap; B.stride = stride; B.lens = lens; B.p = p;
+    B.heads = c->ctrl + AF_CTRL_PLACE_HEADS; B.bscratch = c->bscratch; B.n_slots = c->blat_slots;
+    B.rows = rows; B.n_rows = n_rows; B.max_rows = max_rows; B.order = order;
+    B.stage = c->blat_stage; B.stage_n = c->blat_stage_n;
+    B.caps = BlatCaps{c->blat_caps, with_spill ? c->blat_qcaps : nullptr, with_spill ? c->blat_qcap : 0};
+    if (with_spill) B.spill = c->blat_spill;
+    B.hv = c->blat_hv;
+    return B;
+}
+
 int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_queries, int32_t stride,
             const int32_t *lens, const af_blat_params *p, int32_t max_rows, af_psl *rows, int32_t *n_rows) {
     static_assert(sizeof(af_psl) == 328, "af_psl layout is part of the C-ABI");
@@ -1086,7 +1143,7 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
             if (lens[i] < 0 || lens[i] > stride) return fail(c, AF_E_INVALID, "lens[%lld]=%d outside [0, stride]", (long long)i, lens[i]);
     (void)hipSetDevice(c->device);
     if ((rc = ensure_bscratch(c, 2 * n_queries)) || (rc = ensure_blat_order(c, n_queries)) ||
-        (rc = ensure_blat_stage(c, n_queries, max_rows)))
+        (rc = ensure_blat_stage(c, n_queries, max_rows)) || (rc = ensure_blat_heavy(c, n_queries)))
         return rc;
     const int64_t bytes = n_queries * (int64_t)stride, nr = n_queries * (int64_t)max_rows;
     uint8_t *d_q = nullptr;
@@ -1109,15 +1166,79 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         (e = af_launch_blat_order(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, n_queries, stride,
                                   lens ? d_lens : nullptr, p->rep_match, c->blat_ord_work, c->blat_order, s)) !=
             hipSuccess ||
-        (e = af_launch_blat(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride, lens ? d_lens : nullptr, *p,
-                            c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_nrows, max_rows,
-                            c->blat_order, c->blat_stage, c->blat_stage_n, c->blat_caps, BlatSpill{}, s)) !=
-            hipSuccess ||
+        (e = af_launch_blat(blat_launch(c, ix, d_q, c->ctrl + AF_CTRL_PLACE_N, nullptr, n_queries, stride,
+                                        lens ? d_lens : nullptr, *p, d_rows, d_nrows, max_rows, c->blat_order, false),
+                            s)) != hipSuccess ||
         (e = hipMemcpyAsync(rows, d_rows, sizeof(af_psl) * nr, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipMemcpyAsync(n_rows, d_nrows, 4 * n_queries, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
         return done(fail(c, AF_E_HIP, "af_blat: %s", hipGetErrorString(e)));
     return done(AF_OK);
+}
+
+int af_blat_long(af_ctx *c, const af_index *ix, const uint8_t *query, int32_t len, const af_blat_params *p,
+                 int32_t max_rows, af_psl *rows, int32_t *n_rows, af_psl_block *blocks, int64_t block_cap,
+                 int64_t *block_off, int64_t *n_blocks) {
+    if (!c || !n_rows || !n_blocks || (len > 0 && !query) || (max_rows > 0 && (!rows || !block_off)))
+        return fail(c, AF_E_INVALID, "null argument");
+    int rc = check_blat(c, ix, p, 1, 1);
+    if (rc) return rc;
+    if (len < 0 || len > AF_BLAT_LONG_MAX) return fail(c, AF_E_INVALID, "query length %d outside [0, %d]", len, AF_BLAT_LONG_MAX);
+    if (max_rows < 0 || block_cap < 0) return fail(c, AF_E_INVALID, "max_rows / block_cap out of range");
+    (void)hipSetDevice(c->device);
+    if (!c->blat_caps) {
+        HIPCHK(c, hipMalloc(&c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N));
+        HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
+    }
+    // the codes of both strands (strand 1: the reverse complement)
+    std::vector<uint8_t> q2(2 * (size_t)len + 16, 4);
+    for (int i = 0; i < len; ++i) {
+        const uint8_t ch = query[i];
+        const uint8_t x = (ch == 'A' || ch == 'a') ? 0 : (ch == 'C' || ch == 'c') ? 1 : (ch == 'G' || ch == 'g') ? 2
+                        : (ch == 'T' || ch == 't') ? 3 : 4;
+        q2[i] = x;
+        q2[len + (len - 1 - i)] = x > 3 ? 4 : 3 - x;
+    }
+    uint8_t *d_q2 = nullptr;
+    HIPCHK(c, hipMalloc(&d_q2, q2.size()));
+    std::vector<af_psl> r;
+    std::vector<int32_t> seq;
+    std::vector<int64_t> boff;
+    std::vector<af_psl_block> blk;
+    hipError_t e = hipMemcpyAsync(d_q2, q2.data(), q2.size(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = af_blat_long_run(ix->tile, d_q2, len, *p, c->blat_caps, r, seq, boff, blk, c->n_cu, c->stream);
+    (void)hipFree(d_q2);
+    if (e == hipErrorOutOfMemory) return fail(c, AF_E_CAPACITY, "af_blat_long: the row lists overflowed");
+    if (e != hipSuccess) return fail(c, AF_E_HIP, "af_blat_long: %s", hipGetErrorString(e));
+    // every row best first: score desc, strand, tStart, qStart, tEnd, qEnd, then emission order
+    std::vector<int64_t> ord(r.size());
+    for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int64_t)k;
+    std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+        const af_psl &x = r[a], &y = r[b];
+        if (x.score != y.score) return x.score > y.score;
+        if (x.strand != y.strand) return x.strand < y.strand;
+        if (x.t_start != y.t_start) return x.t_start < y.t_start;
+        if (x.q_start != y.q_start) return x.q_start < y.q_start;
+        if (x.t_end != y.t_end) return x.t_end < y.t_end;
+        if (x.q_end != y.q_end) return x.q_end < y.q_end;
+        return seq[a] < seq[b];
+    });
+    const int64_t m = std::min<int64_t>((int64_t)r.size(), max_rows);
+    int64_t nb = 0;
+    for (int64_t k = 0; k < m; ++k) nb += r[ord[k]].block_count;
+    *n_rows = (int32_t)r.size();
+    *n_blocks = nb;
+    if (nb > block_cap) return fail(c, AF_E_CAPACITY, "af_blat_long: %lld blocks, room for %lld", (long long)nb,
+                                    (long long)block_cap);
+    int64_t off = 0;
+    for (int64_t k = 0; k < m; ++k) {
+        const af_psl &h = r[ord[k]];
+        rows[k] = h;
+        block_off[k] = off;
+        for (int b = 0; b < h.block_count; ++b) blocks[off++] = blk[boff[ord[k]] + b];
+    }
+    if (max_rows > 0) block_off[m] = off;
+    return AF_OK;
 }
 
 int af_blat_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
@@ -1127,18 +1248,22 @@ int af_blat_device(af_ctx *c, const af_index *ix, const uint8_t *d_queries, cons
                                 d_rows, d_n_rows, stream);
 }
 
-int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_first,
-                         const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
-                         const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
+// enqueues the first part of a device search (af_launch_blat_begin) and keeps its arguments on c
+static int blat_device_begin(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_first,
+                             const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
+                             const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows,
+                             hipStream_t s) {
     if (!c || !d_n_queries || (cap_queries > 0 && (!d_queries || !d_rows || !d_n_rows)))
         return fail(c, AF_E_INVALID, "null argument");
     int rc = check_blat(c, ix, p, stride, max_rows);
     if (rc) return rc;
     if (cap_queries < 0 || cap_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "cap_queries out of range");
+    c->blat_open = false;
     if (cap_queries == 0) return AF_OK;
     (void)hipSetDevice(c->device);
-    if ((rc = ensure_bscratch(c, 2 * cap_queries)) || (rc = ensure_blat_stage(c, cap_queries, max_rows))) return rc;
-    hipStream_t s = (hipStream_t)stream;
+    if ((rc = ensure_bscratch(c, 2 * cap_queries)) || (rc = ensure_blat_stage(c, cap_queries, max_rows)) ||
+        (rc = ensure_blat_heavy(c, cap_queries)))
+        return rc;
     HIPCHK(c, hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s));
     HIPCHK(c, af_launch_clamp_count(d_n_queries, cap_queries, c->ctrl + AF_CTRL_PLACE_N, s));
     const int32_t *order = nullptr;  // a subrange keeps query order; the whole set runs heaviest first
@@ -1148,9 +1273,35 @@ int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries
                                        p->rep_match, c->blat_ord_work, c->blat_order, s));
         order = c->blat_order;
     }
-    HIPCHK(c, af_launch_blat(ix->tile, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
-                             c->ctrl + AF_CTRL_PLACE_HEADS, c->bscratch, c->blat_slots, d_rows, d_n_rows, max_rows,
-                             order, c->blat_stage, c->blat_stage_n, c->blat_caps, c->blat_spill, s));
+    c->blat_pending = blat_launch(c, ix, d_queries, c->ctrl + AF_CTRL_PLACE_N, d_first, cap_queries, stride, d_lens, *p,
+                                  d_rows, d_n_rows, max_rows, order, true);
+    HIPCHK(c, af_launch_blat_begin(c->blat_pending, s));
+    c->blat_open = true;
+    return AF_OK;
+}
+
+int af_blat_device_range(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_first,
+                         const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
+                         const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
+    if (int rc = blat_device_begin(c, ix, d_queries, d_first, d_n_queries, cap_queries, stride, d_lens, p, max_rows,
+                                   d_rows, d_n_rows, (hipStream_t)stream))
+        return rc;
+    return af_blat_device_end(c, nullptr, stream);
+}
+
+int af_blat_device_begin(af_ctx *c, const af_index *ix, const uint8_t *d_queries, const int32_t *d_n_queries,
+                         int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
+                         int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream) {
+    return blat_device_begin(c, ix, d_queries, nullptr, d_n_queries, cap_queries, stride, d_lens, p, max_rows, d_rows,
+                             d_n_rows, (hipStream_t)stream);
+}
+
+int af_blat_device_end(af_ctx *c, const uint8_t *d_live, void *stream) {
+    if (!c) return fail(c, AF_E_INVALID, "null argument");
+    if (!c->blat_open) return AF_OK;  // nothing begun (or an empty search)
+    c->blat_open = false;
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, af_launch_blat_end(c->blat_pending, d_live, (hipStream_t)stream));
     return AF_OK;
 }
 
@@ -1159,6 +1310,25 @@ int af_blat_spill(af_ctx *c, af_psl *d_rows, int32_t *d_query, int32_t *d_n, int
     if (!d_rows || cap <= 0) { c->blat_spill = BlatSpill{}; return AF_OK; }
     if (!d_query || !d_n) return fail(c, AF_E_INVALID, "af_blat_spill: null query / count buffer");
     c->blat_spill = BlatSpill{d_rows, d_query, d_n, cap};
+    return AF_OK;
+}
+
+int af_blat_query_caps(af_ctx *c, int32_t *d_counts, int64_t cap) {
+    if (!c) return fail(c, AF_E_INVALID, "null argument");
+    if (!d_counts || cap <= 0) { c->blat_qcaps = nullptr; c->blat_qcap = 0; return AF_OK; }
+    c->blat_qcaps = d_counts;
+    c->blat_qcap = cap;
+    return AF_OK;
+}
+
+int af_blat_heavy_stats(af_ctx *c, int32_t *out) {
+    if (!c || !out) return fail(c, AF_E_INVALID, "null argument");
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    if (!c->blat_hv.ctrl) return AF_OK;
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, hipDeviceSynchronize());
+    const int32_t at[4] = {AF_BLAT_HV_STRANDS_N, AF_BLAT_HV_JOBS_N, AF_BLAT_HV_JOBS_DONE, AF_BLAT_HV_STRANDS_DONE};
+    for (int k = 0; k < 4; ++k) HIPCHK(c, hipMemcpy(out + k, c->blat_hv.ctrl + at[k], 4, hipMemcpyDeviceToHost));
     return AF_OK;
 }
 
@@ -1475,6 +1645,22 @@ int af_genome_stats(af_ctx *c, int32_t *out) {
     return AF_OK;
 }
 
+// the S5 check's per-query flags, selection and select scratch for n queries
+static int ensure_s5(af_ctx *c, int64_t n_queries) {
+    if (n_queries > c->s5_cap) {
+        af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_temp);
+        c->s5_keep = nullptr; c->s5_sel = nullptr; c->s5_temp = nullptr; c->s5_cap = 0;
+        const int64_t n = std::max<int64_t>(n_queries, 1 << 16);
+        c->s5_temp_bytes = af_s5_temp_bytes(n);
+        HIPCHK(c, hipMalloc(&c->s5_keep, n));
+        HIPCHK(c, hipMalloc(&c->s5_sel, sizeof(int32_t) * n));
+        HIPCHK(c, hipMalloc(&c->s5_temp, std::max<size_t>(c->s5_temp_bytes, 16)));
+        c->s5_cap = n;
+    }
+    if (!c->s5_nsel) HIPCHK(c, hipMalloc(&c->s5_nsel, sizeof(int64_t)));
+    return AF_OK;
+}
+
 int af_s5_filter_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
                         const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
                         const af_aln_out *d_s2, const uint8_t *d_cont, int64_t cap, uint8_t *d_s6, int32_t s6_stride,
@@ -1488,20 +1674,92 @@ int af_s5_filter_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec
     if (q_stride <= 0 || q_stride > AF_MAX_READ || s6_stride <= 0 || s6_stride > AF_MAX_READ)
         return fail(c, AF_E_INVALID, "strides must be in [1, %d]", AF_MAX_READ);
     (void)hipSetDevice(c->device);
-    if (n_queries > c->s5_cap) {
-        af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_temp);
-        c->s5_keep = nullptr; c->s5_sel = nullptr; c->s5_temp = nullptr; c->s5_cap = 0;
-        const int64_t n = std::max<int64_t>(n_queries, 1 << 16);
-        c->s5_temp_bytes = af_s5_temp_bytes(n);
-        HIPCHK(c, hipMalloc(&c->s5_keep, n));
-        HIPCHK(c, hipMalloc(&c->s5_sel, sizeof(int32_t) * n));
-        HIPCHK(c, hipMalloc(&c->s5_temp, std::max<size_t>(c->s5_temp_bytes, 16)));
-        c->s5_cap = n;
-    }
-    if (!c->s5_nsel) HIPCHK(c, hipMalloc(&c->s5_nsel, sizeof(int64_t)));
+    if (int rc = ensure_s5(c, n_queries)) return rc;
     HIPCHK(c, af_launch_s5_filter(d_recs, d_n_rec, n_queries, d_q, q_stride, d_q_lens, d_q_rows, *d_s2, d_cont, cap, d_s6,
                                   s6_stride, d_s6_lens, d_s6_src, d_n6, d_n_over, c->s5_keep, c->s5_sel, c->s5_nsel, c->s5_temp,
                                   c->s5_temp_bytes, (hipStream_t)stream));
+    return AF_OK;
+}
+
+static int check_s6_set(af_ctx *c, const af_s6_set *s, bool results, const char *what) {
+    if (!s) return fail(c, AF_E_INVALID, "%s: null set", what);
+    if (s->cap < 0 || s->cap > (1LL << 30) || s->spill_cap < 0 || s->spill_cap > (1LL << 30))
+        return fail(c, AF_E_INVALID, "%s: capacity out of range", what);
+    if (s->stride <= 0 || s->stride > AF_MAX_READ || (s->stride & 3))
+        return fail(c, AF_E_INVALID, "%s: stride must be a multiple of 4 in [4, %d]", what, AF_MAX_READ);
+    if (!s->n || (s->cap > 0 && (!s->q || !s->lens || !s->src)))
+        return fail(c, AF_E_INVALID, "%s: null row buffer", what);
+    if (results && s->cap > 0 && (!s->rows || !s->n_rows)) return fail(c, AF_E_INVALID, "%s: null PSL buffer", what);
+    if (s->spill_cap > 0 && (!s->spill_rows || !s->spill_query || !s->spill_n))
+        return fail(c, AF_E_INVALID, "%s: null spill buffer", what);
+    return AF_OK;
+}
+
+int af_s6_queries_device(af_ctx *c, int64_t n_queries, const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens,
+                         const int32_t *d_q_rows, const af_aln_out *d_s2, const uint8_t *d_cont, const af_s6_set *pre,
+                         void *stream) {
+    if (!c || !d_s2) return fail(c, AF_E_INVALID, "null argument");
+    if (int rc = check_s6_set(c, pre, false, "af_s6_queries_device")) return rc;
+    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
+    if (n_queries > 0 && (!d_q || !d_q_lens || !d_q_rows || !d_s2->flag || !d_s2->pos || !d_s2->n_cigar || !d_s2->cigar))
+        return fail(c, AF_E_INVALID, "null argument");
+    if (q_stride <= 0 || q_stride > AF_MAX_READ) return fail(c, AF_E_INVALID, "q_stride must be in [1, %d]", AF_MAX_READ);
+    (void)hipSetDevice(c->device);
+    if (int rc = ensure_s5(c, n_queries)) return rc;
+    HIPCHK(c, af_launch_s6_queries(n_queries, d_q, q_stride, d_q_lens, d_q_rows, *d_s2, d_cont, *pre, c->s5_keep,
+                                   c->s5_sel, c->s5_nsel, c->s5_temp, c->s5_temp_bytes, (hipStream_t)stream));
+    return AF_OK;
+}
+
+int af_s6_check_device(af_ctx *c, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
+                       const int32_t *d_q_rows, const af_aln_out *d_s2, const uint8_t *d_cont, const af_s6_set *pre,
+                       uint8_t *d_live, void *stream) {
+    if (!c || !d_s2) return fail(c, AF_E_INVALID, "null argument");
+    if (int rc = check_s6_set(c, pre, false, "af_s6_check_device")) return rc;
+    if (pre->cap > 0 && !d_live) return fail(c, AF_E_INVALID, "af_s6_check_device: null live flags");
+    if (n_queries < 0 || n_queries > (1LL << 30)) return fail(c, AF_E_INVALID, "n_queries out of range");
+    if (n_queries > 0 && (!d_recs || !d_n_rec || !d_q_rows || !d_s2->flag || !d_s2->pos || !d_s2->n_cigar ||
+                          !d_s2->cigar))
+        return fail(c, AF_E_INVALID, "null argument");
+    (void)hipSetDevice(c->device);
+    if (int rc = ensure_s5(c, n_queries)) return rc;
+    HIPCHK(c, af_launch_s6_check(d_recs, d_n_rec, n_queries, d_q_rows, *d_s2, d_cont, *pre, c->s5_keep, d_live,
+                                 (hipStream_t)stream));
+    return AF_OK;
+}
+
+int af_s6_compact_device(af_ctx *c, const af_s6_set *pre, const uint8_t *d_live, const af_s6_set *out,
+                         int32_t max_rows, void *stream) {
+    if (!c) return fail(c, AF_E_INVALID, "null argument");
+    if (int rc = check_s6_set(c, pre, true, "af_s6_compact_device (pre)")) return rc;
+    if (int rc = check_s6_set(c, out, true, "af_s6_compact_device (out)")) return rc;
+    if (pre->cap > 0 && !d_live) return fail(c, AF_E_INVALID, "af_s6_compact_device: null live flags");
+    if (pre->stride != out->stride) return fail(c, AF_E_INVALID, "af_s6_compact_device: pre and out strides differ");
+    if (max_rows < 1 || max_rows > AF_BLAT_MAX_ROWS) return fail(c, AF_E_INVALID, "max_rows out of range");
+    if (pre->spill_cap > 0 && out->spill_cap <= 0)
+        return fail(c, AF_E_INVALID, "af_s6_compact_device: pre has a spill pool, out none");
+    (void)hipSetDevice(c->device);
+    if (!c->blat_caps) {
+        HIPCHK(c, hipMalloc(&c->blat_caps, sizeof(int32_t) * AF_BLAT_CAP_N));
+        HIPCHK(c, hipMemset(c->blat_caps, 0, sizeof(int32_t) * AF_BLAT_CAP_N));
+    }
+    if (pre->cap > c->s6_cap || pre->spill_cap > c->s6_spill_cap) {
+        af_free(c->s6_flag); af_free(c->s6_idx); af_free(c->s6_sflag); af_free(c->s6_sidx); af_free(c->s6_temp);
+        c->s6_flag = c->s6_idx = c->s6_sflag = c->s6_sidx = nullptr;
+        c->s6_temp = nullptr;
+        c->s6_cap = c->s6_spill_cap = 0;
+        const int64_t n = std::max<int64_t>(pre->cap, 1 << 16), ns = std::max<int64_t>(pre->spill_cap, 1 << 16);
+        c->s6_temp_bytes = std::max(af_s6_compact_temp_bytes(n), af_s6_compact_temp_bytes(ns));
+        HIPCHK(c, hipMalloc(&c->s6_flag, sizeof(int32_t) * n));
+        HIPCHK(c, hipMalloc(&c->s6_idx, sizeof(int32_t) * n));
+        HIPCHK(c, hipMalloc(&c->s6_sflag, sizeof(int32_t) * ns));
+        HIPCHK(c, hipMalloc(&c->s6_sidx, sizeof(int32_t) * ns));
+        HIPCHK(c, hipMalloc(&c->s6_temp, std::max<size_t>(c->s6_temp_bytes, 16)));
+        c->s6_cap = n;
+        c->s6_spill_cap = ns;
+    }
+    HIPCHK(c, af_launch_s6_compact(*pre, d_live, *out, max_rows, c->blat_caps, c->s6_flag, c->s6_idx, c->s6_sflag,
+                                   c->s6_sidx, c->s6_temp, c->s6_temp_bytes, (hipStream_t)stream));
     return AF_OK;
 }
 

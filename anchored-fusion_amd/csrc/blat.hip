@@ -261,7 +261,7 @@ __device__ __forceinline__ bool psl_before(const af_psl &x, const af_psl &y) {
 
 // one clump seed (q, t) -> Reg r (written by lane 0); false if dropped.  L.q holds the strand.
 template <int CPL>
-__device__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, uint8_t *zg, int lane) {
+__device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, uint8_t *zg, int lane) {
     DpLds &D = g_dp;
     af_params P{};
     P.a = 1; P.b = 1; P.o_del = 3; P.e_del = 1; P.o_ins = 3; P.e_ins = 1; P.w = 16; P.zdrop = 20;
@@ -366,7 +366,7 @@ __device__ __forceinline__ uint32_t first_n(const DevTile &X, int64_t p) {
 // highest best[j] + trimmed score - gap flags wins over i alone.  Lanes over j on the parts'
 // sorted per-part words (coalesced; four 64-part chunks per pass); the trimmed score from a
 // prefix sum of i's first block (PRE, LDS), the N test against the part's first N after te.
-__device__ void chain_node(const DevTile &X, const Reg *RG, const ChainDp &C, int i, int64_t max_intron, int lane) {
+__device__ __forceinline__ void chain_node(const DevTile &X, const Reg *RG, const ChainDp &C, int i, int64_t max_intron, int lane) {
     const Reg &ri = RG[C.ORD[i]];
     const uint8_t *Q = g_dp.q;
     int32_t *PRE = reinterpret_cast<int32_t *>(g_bl.hist);  // PRE[k] = score of the block's first k bases, k < bsz[0]
@@ -419,6 +419,223 @@ __device__ void chain_node(const DevTile &X, const Reg *RG, const ChainDp &C, in
     wave_sync();
 }
 
+// a clump seed (q, t) inside one of the parts RG[0, nr) (lanes over the parts)
+__device__ __forceinline__ bool inside_part(const Reg *RG, int nr, int32_t q, int64_t t, int lane) {
+    bool inside = false;
+    for (int r0 = 0; r0 < nr && !inside; r0 += 64) {
+        const int r = r0 + lane;
+        bool in = false;
+        if (r < nr) {
+            const Reg &g = RG[r];
+            in = g.qb <= q && q + TILE <= g.qe && g.tb <= t && t + TILE <= g.te;
+        }
+        inside = __ballot(in) != 0;
+    }
+    return inside;
+}
+
+// a heavy strand's clumps (in CO order) to the job pool with its entry {2 query + strand, first job,
+// clumps} in the strand table; false (the caller searches it) when either is full
+__device__ __forceinline__ bool defer_strand(const BlatHeavy &hv, const Clump *CL, const uint64_t *CO, int ncl, int64_t item, int lane) {
+    int s = 0, off = 0, ok = 0;
+    if (lane == 0) {
+        s = atomicAdd(hv.strands_n, 1);
+        if (s < hv.strands_cap) {
+            off = atomicAdd(hv.jobs_n, ncl);
+            if ((int64_t)off + ncl <= hv.jobs_cap) ok = 1;
+            else { atomicMin(hv.jobs_valid, off); hv.strands[s] = make_int4((int)item, 0, 0, 0); }
+        }
+    }
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    if (!ok) return false;
+    s = __builtin_amdgcn_readfirstlane(s);
+    off = __builtin_amdgcn_readfirstlane(off);
+#ifdef AF_BLAT_CHECK
+    if (off < 0 || (int64_t)off + ncl > hv.jobs_cap || s < 0 || s >= hv.strands_cap || ncl > MAXCL) {
+        if (lane == 0) printf("defer_strand: off %d ncl %d s %d caps %ld %ld\n", off, ncl, s, (long)hv.jobs_cap, (long)hv.strands_cap);
+        return false;
+    }
+#endif
+    for (int c = lane; c < ncl; c += 64) {
+        const Clump cc = CL[(uint32_t)CO[c]];
+        hv.jobs[off + c] = BlatJob{cc.q, s, cc.t};
+    }
+    if (lane == 0) hv.strands[s] = make_int4((int)item, off, ncl, 0);
+    return true;
+}
+
+// the chains of one strand's parts RG[0, nr) (D.q its codes), best first, into its row list (RW,
+// g_bl.nrow; rows past max_rows to the spill pool)
+__device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_params &bp, Reg *RG, const ChainDp &CD, int nr,
+                              int64_t qi, int strand, int L, uint64_t *KA, uint64_t *KB, af_psl *RW, int32_t max_rows,
+                              const BlatCaps &caps, const BlatSpill &spill, int lane) {
+    DpLds &D = g_dp;
+    BlatLds &B = g_bl;
+    // ---- parts in (qb, tb, qe) order, ties in creation order: ORD ----------------------------
+    // key: qb in bits 54-63, tb in 21-53, qe in 12-20, the part index in 0-11
+    static_assert(AF_MAX_READ < 512, "qb / qe take 9 bits of the ORD key");
+    static_assert(MAXP <= 4096, "the part index takes 12 bits of the ORD key");
+    {
+        const auto key = [&](int r) {
+            const Reg &g = RG[r];
+            return ((uint64_t)g.qb << 54) | ((uint64_t)g.tb << 21) | ((uint64_t)g.qe << 12) | (uint64_t)r;
+        };
+        if (nr <= 64) {
+            if (lane < nr) {
+                const uint64_t k = key(lane);
+                int rank = 0;
+                for (int r = 0; r < nr; ++r) rank += key(r) < k;
+                CD.ORD[rank] = lane;
+            }
+        } else {
+            for (int r = lane; r < nr; r += 64) KA[r] = key(r);
+            __threadfence_block();
+            wave_sync();
+            const uint64_t *SK = wave_radix_sort(KA, KB, nr, 12, 7, lane);
+            for (int r = lane; r < nr; r += 64) CD.ORD[r] = (int32_t)(SK[r] & 4095u);
+        }
+        __threadfence_block();
+        wave_sync();
+        for (int r = lane; r < nr; r += 64) {
+            const Reg &g = RG[CD.ORD[r]];
+            CD.FL[r] = 0;
+            CD.QE[r] = g.qe;
+            CD.TE[r] = (uint32_t)g.te;
+            CD.NXT[r] = first_n(X, g.te);
+        }
+        __threadfence_block();
+        wave_sync();
+    }
+    // ---- chains, best first (oracle/blat.c: each round takes the unused part with the
+    // highest chain score, first in order on ties; only the parts whose predecessor path
+    // met a used part are recomputed, the others keep their exact value) ----------------
+    int64_t work = 0;  // the recomputations' candidates (the first pass is always made)
+    for (int i = 0; i < nr; ++i) {
+        chain_node(X, RG, CD, i, bp.max_intron, lane);
+        __threadfence_block();
+        wave_sync();
+    }
+    for (;;) {
+        if (work > STITCH_WORK) {
+            if (lane == 0) caps.hit(qi, AF_BLAT_CAP_PARTS);
+            break;
+        }
+        // the unused part with the highest chain score, the first on ties
+        int bv = INT_MIN, bi = -1;
+        for (int i0 = 0; i0 < nr; i0 += 64) {
+            const int i = i0 + lane;
+            const bool free_ = i < nr && !(CD.FL[i] & 1);
+            if (!__ballot(free_)) continue;
+            const int v = free_ ? CD.BEST[i] : INT_MIN;
+            const int mx = wave_max(v);
+            if (bi < 0 || mx > bv) { bv = mx; bi = i0 + (int)__builtin_ctzll(__ballot(free_ && v == mx)); }
+        }
+        if (bi < 0) break;
+        int first = bi;
+        if (lane == 0) {
+            int m = 0;
+            for (int i = bi; i >= 0; i = CD.PREV[i]) CD.CH[m++] = i;
+            first = CD.CH[m - 1];
+            af_psl o{};
+            o.query = (int32_t)qi; o.strand = strand; o.q_size = L;
+            bool ok = true;
+            Reg prevp{}, firstp{}, lastp{};
+            for (int c = m - 1; c >= 0; --c) {
+                const int k = CD.CH[c];
+                CD.FL[k] |= 1;
+                CD.QE[k] = -1;
+                const Reg &src = RG[CD.ORD[k]];
+                Reg cur;
+                if (c == m - 1) cur = src;
+                else trim_front(X, D.q, src, chain_trim(prevp, src), cur);
+                if (c < m - 1) {
+                    if (cur.qb > prevp.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - prevp.qe; }
+                    if (cur.tb > prevp.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - prevp.te); }
+                }
+                o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
+                o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi;
+                o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
+                for (int b = 0; b < cur.nb; ++b) {
+                    if (o.block_count >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
+                    o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
+                    o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
+                }
+                if (c == m - 1) firstp = cur;
+                if (c == 0) lastp = cur;
+                prevp = cur;
+            }
+            o.q_start = strand ? L - lastp.qe : firstp.qb;
+            o.q_end = strand ? L - firstp.qb : lastp.qe;
+            o.t_start = firstp.tb; o.t_end = lastp.te;
+            o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
+            if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10) {
+                // the strand's best max_rows rows in psl_before order (stable), all counted;
+                // the row that falls off the list goes to the spill pool
+                const int n = B.nrow < max_rows ? B.nrow : max_rows;
+                int at = n;
+                while (at > 0 && psl_before(o, RW[at - 1])) --at;
+                af_psl out = o;
+                bool off = at >= max_rows;
+                if (!off) {
+                    if (n == max_rows) { out = RW[max_rows - 1]; off = true; }
+                    for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) RW[x] = RW[x - 1];
+                    RW[at] = o;
+                }
+                if (off && spill.cap > 0) {
+                    const int k = atomicAdd(spill.n, 1);
+                    if (k < spill.cap) { spill.rows[k] = out; spill.query[k] = (int32_t)qi; }
+                    else caps.hit(qi, AF_BLAT_CAP_ROWS);
+                }
+                ++B.nrow;
+            }
+        }
+        first = __builtin_amdgcn_readfirstlane(first);
+        __threadfence_block();
+        wave_sync();
+        // parts after the chain's first whose predecessor path meets a used or recomputed
+        // part: recomputed in order (a recomputed part marks its successors in turn)
+        for (int i0 = first + 1 - ((first + 1) & 63); i0 < nr; i0 += 64) {
+            const int i = i0 + lane;
+            bool live = i > first && i < nr && !(CD.FL[i] & 1);
+            const int pv = live ? CD.PREV[i] : -1;
+            bool dirty = live && pv >= 0 && pv < i0 && (CD.FL[pv] & 3);
+            // predecessors inside this chunk: the marks spread lane to lane
+            uint64_t dm = __ballot(dirty);
+            for (;;) {
+                const bool more = !dirty && live && pv >= i0 && ((CD.FL[pv] & 1) || ((dm >> (pv - i0)) & 1));
+                const uint64_t nm = __ballot(more);
+                if (!nm) break;
+                dirty = dirty || more;
+                dm |= nm;
+            }
+            while (dm) {
+                const int l = (int)__builtin_ctzll(dm);
+                dm &= dm - 1;
+                chain_node(X, RG, CD, i0 + l, bp.max_intron, lane);
+                work += i0 + l;
+                if (lane == 0) CD.FL[i0 + l] |= 2;
+                __threadfence_block();
+                wave_sync();
+            }
+        }
+        for (int i = lane; i < nr; i += 64) CD.FL[i] &= 1;
+        __threadfence_block();
+        wave_sync();
+    }
+}
+
+// lane 0: the strand's rows (RW, g_bl.nrow of them) to item (qi, s)'s stage, best first, for k_blat_merge
+__device__ __forceinline__ void strand_stage(af_psl *stage, int32_t *stage_n, int64_t qi, int s, int32_t max_rows, const af_psl *RW,
+                             int lane) {
+    if (lane == 0) {
+        const int n = g_bl.nrow;  // RW holds the first max_rows of them in order
+        const int m = n < max_rows ? n : max_rows;
+        const int64_t sl = 2 * qi + s;
+        for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
+        stage_n[sl] = n;  // all of the strand's rows (k_blat_merge takes the first max_rows)
+    }
+}
+
 template <int CPL>
 __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
                                                         int32_t stride, const int32_t *__restrict__ lens,
@@ -428,7 +645,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                                                         uint8_t *__restrict__ bscratch, int32_t diag_passes,
                                                         af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
                                                         int32_t max_rows, const int32_t *__restrict__ order,
-                                                        int32_t *__restrict__ caps, BlatSpill spill) {
+                                                        BlatCaps caps, BlatSpill spill, BlatHeavy hv) {
     DpLds &D = g_dp;
     BlatLds &B = g_bl;
     const int lane = threadIdx.x;
@@ -478,6 +695,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
         int wsh = 3;  // bucket width 1 << wsh >= 2 * drift: [d - drift, d + drift] meets <= 2 buckets
         while ((1ll << wsh) < 2 * drift) ++wsh;
         BP(int64_t tq0 = clock64(), tq = tq0; int64_t pc[6] = {0, 0, 0, 0, 0, 0}; int ch = 0, cc_ = 0, cr = 0, cs = 0;)
+        bool deferred = false;  // the strand's parts and chains are left to k_blat_jobs / k_blat_heavy
         for (int strand = s_item; strand <= s_item; ++strand) {
             for (int x = lane; x < L; x += 64) {
                 const uint8_t c = B.q0[strand ? L - 1 - x : x];
@@ -506,7 +724,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
             // in flight --------------------------------------------------------------------------
             const int nh_all = min(carry, NMAX);
-            if (lane == 0 && caps && carry > NMAX) atomicAdd(&caps[AF_BLAT_CAP_HITS], 1);
+            if (lane == 0 && carry > NMAX) caps.hit(qi, AF_BLAT_CAP_HITS);
             int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
             for (int h0 = 0; h0 < nh_all; h0 += 256) {
                 int qv[4];
@@ -599,7 +817,7 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             }
             __threadfence_block();
             wave_sync();
-            if (lane == 0 && caps && ncl == MAXCL) atomicAdd(&caps[AF_BLAT_CAP_CLUMPS], 1);
+            if (lane == 0 && ncl == MAXCL) caps.hit(qi, AF_BLAT_CAP_CLUMPS);
             if (ncl == 0) continue;
             // ---- clump order: hits desc, then diagonal (= run order) ------------------------------
             for (int i = lane; i < ncl; i += 64)
@@ -609,194 +827,195 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             const uint64_t *CO = wave_radix_sort(KA, KB, ncl, 32, 2, lane);
             BPM(2);
             BP(cc_ += ncl;)
+            // ---- a heavy strand's clumps are aligned later as grid-wide jobs (k_blat_jobs), its
+            // chains by k_blat_heavy: its serial part loop would set the search's makespan --------
+            if (hv.min_clumps > 0 && ncl > hv.min_clumps && defer_strand(hv, CL, CO, ncl, 2 * qi + s_item, lane)) {
+#ifdef AF_BLAT_CHECK
+                if (lane == 0 && qi < 4) printf("defer: q %ld s %d clumps %d L %d\n", (long)qi, s_item, ncl, L);
+#endif
+                deferred = true;
+                continue;
+            }
             // ---- parts: one per clump whose seed lies in no earlier part (lanes over the parts) ----
             int nr = 0, c = 0;
             for (; c < ncl && nr < MAXP; ++c) {
                 const Clump cc = CL[(uint32_t)CO[c]];
-                bool inside = false;
-                for (int r0 = 0; r0 < nr && !inside; r0 += 64) {
-                    const int r = r0 + lane;
-                    bool in = false;
-                    if (r < nr) {
-                        const Reg &g = RG[r];
-                        in = g.qb <= cc.q && cc.q + TILE <= g.qe && g.tb <= cc.t && cc.t + TILE <= g.te;
-                    }
-                    inside = __ballot(in) != 0;
-                }
-                if (inside) continue;
+                if (inside_part(RG, nr, cc.q, cc.t, lane)) continue;
                 if (align_clump<CPL>(X, L, cc.q, cc.t, RG[nr], zg, lane)) ++nr;
                 __threadfence_block();
                 wave_sync();
             }
-            if (lane == 0 && caps && nr == MAXP && c < ncl) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
+            if (lane == 0 && nr == MAXP && c < ncl) caps.hit(qi, AF_BLAT_CAP_PARTS);
             if (nr == 0) continue;
             BPM(3);
             BP(cr += nr;)
-            // ---- parts in (qb, tb, qe) order, ties in creation order: ORD ----------------------
-            {
-                const auto key = [&](int r) {
-                    const Reg &g = RG[r];
-                    return ((uint64_t)g.qb << 54) | ((uint64_t)g.tb << 21) | ((uint64_t)g.qe << 12) | (uint64_t)r;
-                };
-                if (nr <= 64) {
-                    if (lane < nr) {
-                        const uint64_t k = key(lane);
-                        int rank = 0;
-                        for (int r = 0; r < nr; ++r) rank += key(r) < k;
-                        CD.ORD[rank] = lane;
-                    }
-                } else {
-                    for (int r = lane; r < nr; r += 64) KA[r] = key(r);
-                    __threadfence_block();
-                    wave_sync();
-                    const uint64_t *SK = wave_radix_sort(KA, KB, nr, 12, 7, lane);
-                    for (int r = lane; r < nr; r += 64) CD.ORD[r] = (int32_t)(SK[r] & 4095u);
-                }
-                __threadfence_block();
-                wave_sync();
-                for (int r = lane; r < nr; r += 64) {
-                    const Reg &g = RG[CD.ORD[r]];
-                    CD.FL[r] = 0;
-                    CD.QE[r] = g.qe;
-                    CD.TE[r] = (uint32_t)g.te;
-                    CD.NXT[r] = first_n(X, g.te);
-                }
-                __threadfence_block();
-                wave_sync();
-            }
-            // ---- chains, best first (oracle/blat.c: each round takes the unused part with the
-            // highest chain score, first in order on ties; only the parts whose predecessor path
-            // met a used part are recomputed, the others keep their exact value) ----------------
-            int64_t work = 0;  // the recomputations' candidates (the first pass is always made)
-            for (int i = 0; i < nr; ++i) {
-                chain_node(X, RG, CD, i, bp.max_intron, lane);
-                __threadfence_block();
-                wave_sync();
-            }
-            for (;;) {
-                if (work > STITCH_WORK) {
-                    if (lane == 0 && caps) atomicAdd(&caps[AF_BLAT_CAP_PARTS], 1);
-                    break;
-                }
-                // the unused part with the highest chain score, the first on ties
-                int bv = INT_MIN, bi = -1;
-                for (int i0 = 0; i0 < nr; i0 += 64) {
-                    const int i = i0 + lane;
-                    const bool free_ = i < nr && !(CD.FL[i] & 1);
-                    if (!__ballot(free_)) continue;
-                    const int v = free_ ? CD.BEST[i] : INT_MIN;
-                    const int mx = wave_max(v);
-                    if (bi < 0 || mx > bv) { bv = mx; bi = i0 + (int)__builtin_ctzll(__ballot(free_ && v == mx)); }
-                }
-                if (bi < 0) break;
-                int first = bi;
-                if (lane == 0) {
-                    int m = 0;
-                    for (int i = bi; i >= 0; i = CD.PREV[i]) CD.CH[m++] = i;
-                    first = CD.CH[m - 1];
-                    af_psl o{};
-                    o.query = (int32_t)qi; o.strand = strand; o.q_size = L;
-                    bool ok = true;
-                    Reg prevp{}, firstp{}, lastp{};
-                    for (int c = m - 1; c >= 0; --c) {
-                        const int k = CD.CH[c];
-                        CD.FL[k] |= 1;
-                        CD.QE[k] = -1;
-                        const Reg &src = RG[CD.ORD[k]];
-                        Reg cur;
-                        if (c == m - 1) cur = src;
-                        else trim_front(X, D.q, src, chain_trim(prevp, src), cur);
-                        if (c < m - 1) {
-                            if (cur.qb > prevp.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - prevp.qe; }
-                            if (cur.tb > prevp.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - prevp.te); }
-                        }
-                        o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
-                        o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi;
-                        o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
-                        for (int b = 0; b < cur.nb; ++b) {
-                            if (o.block_count >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
-                            o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
-                            o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
-                        }
-                        if (c == m - 1) firstp = cur;
-                        if (c == 0) lastp = cur;
-                        prevp = cur;
-                    }
-                    o.q_start = strand ? L - lastp.qe : firstp.qb;
-                    o.q_end = strand ? L - firstp.qb : lastp.qe;
-                    o.t_start = firstp.tb; o.t_end = lastp.te;
-                    o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
-                    if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10) {
-                        // the strand's best max_rows rows in psl_before order (stable), all counted;
-                        // the row that falls off the list goes to the spill pool
-                        const int n = B.nrow < max_rows ? B.nrow : max_rows;
-                        int at = n;
-                        while (at > 0 && psl_before(o, RW[at - 1])) --at;
-                        af_psl out = o;
-                        bool off = at >= max_rows;
-                        if (!off) {
-                            if (n == max_rows) { out = RW[max_rows - 1]; off = true; }
-                            for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) RW[x] = RW[x - 1];
-                            RW[at] = o;
-                        }
-                        if (off && spill.cap > 0) {
-                            const int k = atomicAdd(spill.n, 1);
-                            if (k < spill.cap) { spill.rows[k] = out; spill.query[k] = (int32_t)qi; }
-                            else if (caps) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
-                        }
-                        ++B.nrow;
-                    }
-                }
-                first = __builtin_amdgcn_readfirstlane(first);
-                __threadfence_block();
-                wave_sync();
-                // parts after the chain's first whose predecessor path meets a used or recomputed
-                // part: recomputed in order (a recomputed part marks its successors in turn)
-                for (int i0 = first + 1 - ((first + 1) & 63); i0 < nr; i0 += 64) {
-                    const int i = i0 + lane;
-                    bool live = i > first && i < nr && !(CD.FL[i] & 1);
-                    const int pv = live ? CD.PREV[i] : -1;
-                    bool dirty = live && pv >= 0 && pv < i0 && (CD.FL[pv] & 3);
-                    // predecessors inside this chunk: the marks spread lane to lane
-                    uint64_t dm = __ballot(dirty);
-                    for (;;) {
-                        const bool more = !dirty && live && pv >= i0 && ((CD.FL[pv] & 1) || ((dm >> (pv - i0)) & 1));
-                        const uint64_t nm = __ballot(more);
-                        if (!nm) break;
-                        dirty = dirty || more;
-                        dm |= nm;
-                    }
-                    while (dm) {
-                        const int l = (int)__builtin_ctzll(dm);
-                        dm &= dm - 1;
-                        chain_node(X, RG, CD, i0 + l, bp.max_intron, lane);
-                        work += i0 + l;
-                        if (lane == 0) CD.FL[i0 + l] |= 2;
-                        __threadfence_block();
-                        wave_sync();
-                    }
-                }
-                for (int i = lane; i < nr; i += 64) CD.FL[i] &= 1;
-                __threadfence_block();
-                wave_sync();
-            }
+            strand_chains(X, bp, RG, CD, nr, qi, strand, L, KA, KB, RW, max_rows, caps, spill, lane);
         }
         BPM(4);
-        // ---- rows of both strands, best first ---------------------------------------------------
-        if (lane == 0) {
-            const int n = B.nrow;  // RW holds the first max_rows of them in order
-            const int m = n < max_rows ? n : max_rows;
-            const int64_t sl = 2 * qi + s_item;  // this strand's rows, best first, for k_blat_merge
-            for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
-            stage_n[sl] = n;  // all of the strand's rows (k_blat_merge takes the first max_rows)
-            BP(if (g_blprof && qi < (1 << 22)) {
-                int32_t *pf = g_blprof + qi * 16;
-                for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
-                pf[5] = ch; pf[6] = cc_; pf[7] = cr; pf[8] = L;
-                pf[9] = (int32_t)min(clock64() - tq0, (int64_t)0x7fffffff);
-                pf[10] = (int32_t)min(pc[5], (int64_t)0x7fffffff); pf[11] = cs;
-            })
+        if (!deferred) strand_stage(stage, stage_n, qi, s_item, max_rows, RW, lane);
+        BP(if (lane == 0 && g_blprof && qi < (1 << 22)) {
+            int32_t *pf = g_blprof + qi * 16;
+            for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
+            pf[5] = ch; pf[6] = cc_; pf[7] = cr; pf[8] = L;
+            pf[9] = (int32_t)min(clock64() - tq0, (int64_t)0x7fffffff);
+            pf[10] = (int32_t)min(pc[5], (int64_t)0x7fffffff); pf[11] = cs; pf[12] = deferred ? 1 : 0;
+        })
+        __threadfence_block();
+        wave_sync();
+    }
+}
+
+// the query codes of (qi, strand) into D.q (strand 1: the reverse complement); returns its length
+__device__ __forceinline__ int load_strand(const uint8_t *queries, int32_t stride, const int32_t *lens, int64_t qi, int strand,
+                           int lane) {
+    int L = lens ? lens[qi] : stride;
+    if (L > stride) L = stride;
+    if (L > AF_MAX_READ) L = AF_MAX_READ;
+    if (L < 0) L = 0;
+    const uint8_t *row = queries + qi * (int64_t)stride;
+    for (int x = lane; x < L; x += 64) {
+        const uint8_t c = nt4(row[strand ? L - 1 - x : x]);
+        g_dp.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
+    }
+    wave_sync();
+    return L;
+}
+
+// next work item of a persistent grid from 8 per-XCD heads (item = head + 8 * k), or n when drained
+__device__ __forceinline__ int64_t next_item(int32_t *heads, int64_t n, int &head, int &heads_left, int lane) {
+    while (heads_left > 0) {
+        int v = 0;
+        if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
+        v = __builtin_amdgcn_readfirstlane(v);
+        const int64_t it = head + 8 * (int64_t)v;
+        if (it < n) return it;
+        head = (head + 1) & 7;
+        --heads_left;
+    }
+    return n;
+}
+
+// one clump job of a deferred strand per wave: its part (align_clump from the clump's seed tile)
+// into the part pool, ok flag beside it; jobs of queries not live are skipped
+template <int CPL>
+__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat_jobs(DevTile X, const uint8_t *__restrict__ queries,
+                                                             int32_t stride, const int32_t *__restrict__ lens,
+                                                             BlatHeavy hv, const uint8_t *__restrict__ live,
+                                                             int32_t *__restrict__ heads, uint8_t *__restrict__ bscratch) {
+    const int lane = threadIdx.x;
+    uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
+    int64_t n = *hv.jobs_n;
+    if (n > hv.jobs_cap) n = hv.jobs_cap;
+    if (n > *hv.jobs_valid) n = *hv.jobs_valid;
+    Reg *parts = reinterpret_cast<Reg *>(hv.parts);
+#ifdef AF_BLAT_CHECK
+    if (blockIdx.x == 0 && lane == 0)
+        printf("k_blat_jobs: n %ld jobs_n %d valid %d cap %ld strands_n %d heads0 %d\n", (long)n, *hv.jobs_n, *hv.jobs_valid,
+               (long)hv.jobs_cap, *hv.strands_n, heads[0]);
+#endif
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        const int64_t j = next_item(heads, n, head, heads_left, lane);
+        if (j >= n) break;
+        const BlatJob jb = hv.jobs[j];
+#ifdef AF_BLAT_CHECK
+        if (jb.hs < 0 || jb.hs >= hv.strands_cap || jb.hs >= *hv.strands_n) {
+            if (lane == 0) printf("k_blat_jobs: job %ld strand %d outside [0, %d)\n", (long)j, jb.hs, *hv.strands_n);
+            continue;
         }
+#endif
+        const int4 st = hv.strands[jb.hs];
+        const int64_t qi = st.x >> 1;
+#ifdef AF_BLAT_CHECK
+        if (qi < 0 || j < st.y || j >= (int64_t)st.y + st.z || jb.q < 0 || jb.t < 0 || jb.t >= X.n) {
+            if (lane == 0) printf("k_blat_jobs: job %ld (q %d t %ld) strand {%d %d %d}\n", (long)j, jb.q, (long)jb.t, st.x, st.y, st.z);
+            continue;
+        }
+#endif
+        if (live && !live[qi]) continue;
+        const int L = load_strand(queries, stride, lens, qi, st.x & 1, lane);
+        const bool ok = align_clump<CPL>(X, L, jb.q, jb.t, parts[j], zg, lane);
+        if (lane == 0) {
+            hv.part_ok[j] = ok ? 1 : 0;
+            atomicAdd(hv.ctrl + AF_BLAT_HV_JOBS_DONE, 1);
+        }
+#ifdef AF_BLAT_CHECK
+        if (lane == 0 && j % 100 < 2)
+            printf("jobs: q %ld s %d job %ld seed (%d, %ld) L %d ok %d part [%d %d) [%ld %ld) score %d nb %d\n", (long)qi,
+                   st.x & 1, (long)j, jb.q, (long)jb.t, L, ok ? 1 : 0, parts[j].qb, parts[j].qe, (long)parts[j].tb,
+                   (long)parts[j].te, parts[j].score, parts[j].nb);
+#endif
+        __threadfence_block();
+        wave_sync();
+    }
+}
+
+// one deferred strand per wave: its clumps in order, each taking its job's part unless its seed
+// lies in an earlier part (the order k_blat's part loop keeps), then the chains and the rows
+template <int CPL>
+__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat_heavy(DevTile X, const uint8_t *__restrict__ queries,
+                                                              int32_t stride, const int32_t *__restrict__ lens,
+                                                              af_blat_params bp, BlatHeavy hv,
+                                                              const uint8_t *__restrict__ live,
+                                                              int32_t *__restrict__ heads,
+                                                              uint8_t *__restrict__ bscratch,
+                                                              af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
+                                                              int32_t max_rows, BlatCaps caps, BlatSpill spill) {
+    const int lane = threadIdx.x;
+    uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
+    uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
+    Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
+    af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
+    int32_t *dpw = reinterpret_cast<int32_t *>(zg + SC_DP);
+    const ChainDp CD{dpw, dpw + MAXP, dpw + 2 * MAXP, dpw + 3 * MAXP, dpw + 4 * MAXP, dpw + 5 * MAXP,
+                     reinterpret_cast<uint32_t *>(dpw + 6 * MAXP), reinterpret_cast<uint32_t *>(dpw + 7 * MAXP)};
+    const Reg *parts = reinterpret_cast<const Reg *>(hv.parts);
+    int64_t ns = *hv.strands_n;
+    if (ns > hv.strands_cap) ns = hv.strands_cap;
+    int head = (int)(blockIdx.x & 7), heads_left = 8;
+    for (;;) {
+        const int64_t s = next_item(heads, ns, head, heads_left, lane);
+        if (s >= ns) break;
+        const int4 st = hv.strands[s];
+        if (st.z == 0) continue;  // no room in the job pool: k_blat searched the strand itself
+#ifdef AF_BLAT_CHECK
+        if (st.x < 0 || st.y < 0 || (int64_t)st.y + st.z > hv.jobs_cap) {
+            if (lane == 0) printf("k_blat_heavy: strand %ld {%d %d %d} jobs_cap %ld\n", (long)s, st.x, st.y, st.z, (long)hv.jobs_cap);
+            continue;
+        }
+#endif
+        const int64_t qi = st.x >> 1;
+        const int strand = st.x & 1;
+        if (live && !live[qi]) continue;
+        const int L = load_strand(queries, stride, lens, qi, strand, lane);
+        if (lane == 0) g_bl.nrow = 0;
+        wave_sync();
+        int nr = 0, c = 0;
+        for (; c < st.z && nr < MAXP; ++c) {
+            const int64_t j = st.y + (int64_t)c;
+            const BlatJob jb = hv.jobs[j];
+            if (inside_part(RG, nr, jb.q, jb.t, lane)) continue;
+            if (!hv.part_ok[j]) continue;
+            const int32_t *src = reinterpret_cast<const int32_t *>(parts + j);
+            int32_t *dst = reinterpret_cast<int32_t *>(RG + nr);
+            for (int w = lane; w < (int)(sizeof(Reg) / 4); w += 64) dst[w] = src[w];
+#ifdef AF_BLAT_CHECK
+            if (lane == 0 && qi < 2 && nr < 3)
+                printf("heavy part: q %ld s %d job %ld seed (%d, %ld) ok %d part [%d %d) [%ld %ld) score %d m %d nb %d\n",
+                       (long)qi, strand, (long)j, jb.q, (long)jb.t, (int)hv.part_ok[j], parts[j].qb, parts[j].qe,
+                       (long)parts[j].tb, (long)parts[j].te, parts[j].score, parts[j].matches, parts[j].nb);
+#endif
+            ++nr;
+            __threadfence_block();
+            wave_sync();
+        }
+        if (lane == 0 && nr == MAXP && c < st.z) caps.hit(qi, AF_BLAT_CAP_PARTS);
+        if (nr > 0) strand_chains(X, bp, RG, CD, nr, qi, strand, L, KA, KB, RW, max_rows, caps, spill, lane);
+        strand_stage(stage, stage_n, qi, strand, max_rows, RW, lane);
+        if (lane == 0) atomicAdd(hv.ctrl + AF_BLAT_HV_STRANDS_DONE, 1);
+#ifdef AF_BLAT_CHECK
+        if (lane == 0 && qi < 4) printf("heavy: q %ld s %d jobs [%d, +%d) parts %d rows %d\n", (long)qi, strand, st.y, st.z, nr, g_bl.nrow);
+#endif
         __threadfence_block();
         wave_sync();
     }
@@ -854,15 +1073,19 @@ struct MinU32 {
 __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__restrict__ stage_n,
                              const int32_t *__restrict__ n_q, const int32_t *__restrict__ q_first, int64_t cap,
                              int32_t max_rows, af_psl *__restrict__ rows, int32_t *__restrict__ n_rows,
-                             int32_t *__restrict__ caps, BlatSpill spill) {
+                             BlatCaps caps, BlatSpill spill, const uint8_t *__restrict__ live) {
     const int64_t nq = *n_q < cap ? *n_q : cap;
     const int64_t q0 = q_first ? max((int64_t)0, min((int64_t)*q_first, nq)) : 0;
     const int64_t qi = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (qi >= nq) return;
+    if (live && !live[qi]) {  // a query the caller dropped: no rows (its strands may not be searched)
+        n_rows[qi] = 0;
+        return;
+    }
     const af_psl *A = stage + 2 * qi * max_rows, *Bs = A + max_rows;
     const int sa = stage_n[2 * qi], sb = stage_n[2 * qi + 1];
     const int na = sa < max_rows ? sa : max_rows, nb = sb < max_rows ? sb : max_rows;
-    if (caps && sa + sb > max_rows && spill.cap <= 0) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
+    if (sa + sb > max_rows && spill.cap <= 0) caps.hit(qi, AF_BLAT_CAP_ROWS);
 #ifdef AF_BLAT_CHECK
     if (na < 0 || nb < 0) {
         printf("k_blat_merge: query %ld rows %d %d\n", (long)qi, na, nb);
@@ -881,7 +1104,7 @@ __global__ void k_blat_merge(const af_psl *__restrict__ stage, const int32_t *__
             const af_psl &r = j < nb && (i >= na || psl_before(Bs[j], A[i])) ? Bs[j++] : A[i++];
             const int x = atomicAdd(spill.n, 1);
             if (x < spill.cap) { spill.rows[x] = r; spill.query[x] = (int32_t)qi; }
-            else if (caps) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
+            else caps.hit(qi, AF_BLAT_CAP_ROWS);
         }
     }
 }
@@ -939,29 +1162,64 @@ hipError_t af_launch_blat_order(const DevTile &X, const uint8_t *queries, const 
 }
 
 
-hipError_t af_launch_blat(const DevTile &X, const uint8_t *queries, const int32_t *n_queries, const int32_t *q_first,
-                          int64_t cap,
-                          int32_t stride, const int32_t *lens, const af_blat_params &p, int32_t *heads,
-                          uint8_t *bscratch, int32_t n_slots, af_psl *rows, int32_t *n_rows, int32_t max_rows,
-                          const int32_t *order, af_psl *stage, int32_t *stage_n, int32_t *caps, const BlatSpill &spill,
-                          hipStream_t s) {
+hipError_t af_launch_blat_begin(const BlatLaunch &B, hipStream_t s) {
+    hipError_t e;
+    const BlatHeavy &hv = B.hv;
+    if (hv.min_clumps > 0) {
+        // the heavy-strand pool's fills and dequeue heads (jobs_valid: 0x7f7f7f7f, above any pool)
+        if ((e = hipMemsetAsync(hv.ctrl, 0, sizeof(int32_t) * AF_BLAT_HV_CTRL_WORDS, s)) != hipSuccess ||
+            (e = hipMemsetAsync(hv.jobs_valid, 0x7f, sizeof(int32_t), s)) != hipSuccess)
+            return e;
+    }
     // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
-    int bits = 64 - __builtin_clzll((unsigned long long)(X.n + 1024));
+    int bits = 64 - __builtin_clzll((unsigned long long)(B.X.n + 1024));
     const int diag_passes = (bits + 7) / 8;
-    const int cpl = (stride + 1 + 63) / 64;
-    dim3 g(n_slots), b(64);
-#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, X, queries, stride, lens, p, n_queries, q_first, cap, \
-                                    heads, \
-                                    bscratch, diag_passes, stage, stage_n, max_rows, order, caps, spill)
+    const int cpl = (B.stride + 1 + 63) / 64;
+    dim3 g(B.n_slots), b(64);
+#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, B.p, B.n_queries, \
+                                    B.q_first, B.cap, B.heads, B.bscratch, diag_passes, B.stage, B.stage_n, B.max_rows, \
+                                    B.order, B.caps, B.spill, hv)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);
     else AF_GO(AF_CPL);
 #undef AF_GO
-    hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, stage, stage_n, n_queries,
-                       q_first, cap, max_rows, rows, n_rows, caps, spill);
     return hipGetLastError();
 }
+
+hipError_t af_launch_blat_end(const BlatLaunch &B, const uint8_t *live, hipStream_t s) {
+    const BlatHeavy &hv = B.hv;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int cpl = (B.stride + 1 + 63) / 64;
+    dim3 g(B.n_slots), b(64);
+    if (hv.min_clumps > 0) {
+        int32_t *hj = hv.ctrl + AF_BLAT_HV_JOB_HEADS, *hs = hv.ctrl + AF_BLAT_HV_STRAND_HEADS;
+#define AF_GO(C)                                                                                                    \
+    do {                                                                                                            \
+        hipLaunchKernelGGL((k_blat_jobs<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, hv, live, hj, B.bscratch); \
+        if ((e = hipGetLastError()) != hipSuccess) return e;                                                        \
+        hipLaunchKernelGGL((k_blat_heavy<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, B.p, hv, live, hs,        \
+                           B.bscratch, B.stage, B.stage_n, B.max_rows, B.caps, B.spill);                              \
+        if ((e = hipGetLastError()) != hipSuccess) return e;                                                        \
+    } while (0)
+        if (cpl <= 2) AF_GO(2);
+        else if (cpl <= 3) AF_GO(3);
+        else if (cpl <= 4) AF_GO(4);
+        else AF_GO(AF_CPL);
+#undef AF_GO
+    }
+    hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((B.cap + 255) / 256)), dim3(256), 0, s, B.stage, B.stage_n,
+                       B.n_queries, B.q_first, B.cap, B.max_rows, B.rows, B.n_rows, B.caps, B.spill, live);
+    return hipGetLastError();
+}
+
+hipError_t af_launch_blat(const BlatLaunch &B, hipStream_t s) {
+    hipError_t e = af_launch_blat_begin(B, s);
+    return e != hipSuccess ? e : af_launch_blat_end(B, nullptr, s);
+}
+
+size_t af_blat_part_bytes() { return sizeof(Reg); }
 
 int af_blat_slots(int n_cu) {
     if (const char *e = getenv("AF_BLAT_WAVES_PER_CU")) {  // experiment knob: resident BLAT waves per CU

@@ -202,11 +202,12 @@ __host__ __device__ int s6_row(const S5In &in, int32_t qi, const uint8_t *q, int
     return len;
 }
 
-// S6 row k = survivor k (S5 query sel[k]); rows with dropped bytes are counted in *n_over
+// S6 row k = survivor k (S5 query sel[k]); rows with dropped bytes are counted in *n_over and / or
+// flagged in over_rows[k]
 __global__ void k_s6_rows(S5In in, const uint8_t *__restrict__ q, int32_t q_stride, const int32_t *__restrict__ q_lens,
                           const int32_t *__restrict__ sel, const int64_t *__restrict__ n_sel, int64_t cap,
                           uint8_t *__restrict__ out, int32_t out_stride, int32_t *__restrict__ out_lens,
-                          int32_t *__restrict__ out_src, int32_t *__restrict__ n_over) {
+                          int32_t *__restrict__ out_src, int32_t *__restrict__ n_over, uint8_t *__restrict__ over_rows) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n = *n_sel < cap ? *n_sel : cap;
     if (k >= n) return;
@@ -215,6 +216,113 @@ __global__ void k_s6_rows(S5In in, const uint8_t *__restrict__ q, int32_t q_stri
     out_lens[k] = s6_row(in, qi, q, q_stride, q_lens, out + k * (int64_t)out_stride, out_stride, &over);
     out_src[k] = qi;
     if (over && n_over) atomicAdd(n_over, 1);
+    if (over_rows) over_rows[k] = over ? 1 : 0;
+}
+
+// the QNAME-group leaders (fn:718-768 keeps at most a group's first query; no record is read)
+__global__ void k_s5_lead(S5In in, int64_t n, uint8_t *__restrict__ keep) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    keep[q] = (q == 0 || !continues(in, q)) ? 1 : 0;
+}
+
+// ---- the compaction of the leaders' S6 rows and BLAT results to the survivors ----------------------
+// live[p] = pre row p's S5 query survived the check (0 past the row count)
+__global__ void k_s6_live(const int32_t *__restrict__ src, const int32_t *__restrict__ n_pre, int64_t cap,
+                          const uint8_t *__restrict__ keep, uint8_t *__restrict__ live) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= cap) return;
+    const int64_t n = *n_pre < cap ? *n_pre : cap;
+    live[p] = p < n ? keep[src[p]] : 0;
+}
+// the scan input of the live flags (0 past the row count)
+__global__ void k_s6_pre_flags(const uint8_t *__restrict__ live, const int32_t *__restrict__ n_pre, int64_t cap,
+                               int32_t *__restrict__ flag) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= cap) return;
+    const int64_t n = *n_pre < cap ? *n_pre : cap;
+    flag[p] = p < n ? (int32_t)live[p] : 0;
+}
+
+__device__ __forceinline__ void copy_words(int32_t *__restrict__ d, const int32_t *__restrict__ s, int n, int lane, int w) {
+    for (int x = lane; x < n; x += w) d[x] = s[x];
+}
+
+constexpr int PSL_WORDS = (int)(sizeof(af_psl) / 4);
+static_assert(sizeof(af_psl) % 4 == 0 && offsetof(af_psl, query) == 0, "af_psl words");
+
+// one wave per pre row p (grid-stride): survivor k = idx[p] takes p's query row, length, S5 query,
+// PSL rows (query field = k) and row count; its clipped flag and cap events are counted, and its
+// rows the pre spill pool dropped (a full pool: its ROWS events) added to the out pool's count
+__global__ void k_s6_compact(af_s6_set pre, af_s6_set out, const int32_t *__restrict__ flag,
+                             const int32_t *__restrict__ idx, int32_t max_rows, int32_t *__restrict__ caps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t n = *pre.n < pre.cap ? *pre.n : pre.cap;
+    const int qw = pre.stride / 4;
+    for (int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < n; p += waves) {
+        if (!flag[p]) continue;
+        const int64_t k = idx[p];
+        if (k >= out.cap) continue;
+        copy_words(reinterpret_cast<int32_t *>(out.q + k * out.stride), reinterpret_cast<const int32_t *>(pre.q + p * pre.stride),
+                   qw, lane, 64);
+        const int nr = pre.n_rows[p] < max_rows ? pre.n_rows[p] : max_rows;
+        int32_t *dr = reinterpret_cast<int32_t *>(out.rows + k * max_rows);
+        const int32_t *sr = reinterpret_cast<const int32_t *>(pre.rows + p * max_rows);
+        for (int x = lane; x < nr * PSL_WORDS; x += 64) dr[x] = x % PSL_WORDS == 0 ? (int32_t)k : sr[x];  // af_psl.query = k
+        if (lane == 0) {
+            out.lens[k] = pre.lens[p];
+            out.src[k] = pre.src[p];
+            out.n_rows[k] = pre.n_rows[p];
+            if (out.n_over && pre.over && pre.over[p]) atomicAdd(out.n_over, 1);
+        }
+        if (caps && pre.caps && lane < AF_BLAT_CAP_N) {
+            const int32_t v = pre.caps[(int64_t)lane * pre.cap + p];
+            if (v) atomicAdd(&caps[lane], v);
+            if (v && lane == AF_BLAT_CAP_ROWS && out.spill_n && pre.spill_cap > 0) atomicAdd(out.spill_n, v);
+        }
+    }
+}
+
+// sflag[x] = spilled row x belongs to a survivor (0 past the pool's fill)
+__global__ void k_s6_spill_flags(af_s6_set pre, const int32_t *__restrict__ flag, int32_t *__restrict__ sflag) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= pre.spill_cap) return;
+    const int64_t n = *pre.spill_n < pre.spill_cap ? *pre.spill_n : pre.spill_cap;
+    sflag[x] = x < n ? flag[pre.spill_query[x]] : 0;
+}
+
+// the survivors' spilled rows in pool order, their query renumbered; the counts
+__global__ void k_s6_spill_copy(af_s6_set pre, af_s6_set out, const int32_t *__restrict__ flag,
+                                const int32_t *__restrict__ idx, const int32_t *__restrict__ sflag,
+                                const int32_t *__restrict__ sidx, int32_t *__restrict__ caps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t n = *pre.spill_n < pre.spill_cap ? *pre.spill_n : pre.spill_cap;
+    for (int64_t x = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); x < n; x += waves) {
+        if (!sflag[x]) continue;
+        const int64_t j = sidx[x];
+        const int32_t k = idx[pre.spill_query[x]];
+        if (j >= out.spill_cap) {
+            if (lane == 0 && caps) atomicAdd(&caps[AF_BLAT_CAP_ROWS], 1);
+            continue;
+        }
+        int32_t *d = reinterpret_cast<int32_t *>(out.spill_rows + j);
+        const int32_t *sr = reinterpret_cast<const int32_t *>(pre.spill_rows + x);
+        for (int w = lane; w < PSL_WORDS; w += 64) d[w] = w == 0 ? k : sr[w];
+        if (lane == 0) out.spill_query[j] = k;
+    }
+}
+
+// *out.n = min(survivors, out.cap); *out.spill_n = the survivors' spilled rows in the pre pool (k_s6_compact
+// adds those it dropped)
+__global__ void k_s6_compact_counts(af_s6_set pre, af_s6_set out, const int32_t *__restrict__ flag,
+                                    const int32_t *__restrict__ idx, const int32_t *__restrict__ sflag,
+                                    const int32_t *__restrict__ sidx) {
+    if (threadIdx.x != 0) return;
+    const int64_t t = pre.cap > 0 ? (int64_t)idx[pre.cap - 1] + flag[pre.cap - 1] : 0;
+    *out.n = (int32_t)(t < out.cap ? t : out.cap);
+    if (out.spill_n) *out.spill_n = pre.spill_cap > 0 ? sidx[pre.spill_cap - 1] + sflag[pre.spill_cap - 1] : 0;
 }
 
 __global__ void k_s6_count(const int64_t *__restrict__ n_sel, int64_t cap, int32_t *__restrict__ n_out) {
@@ -274,9 +382,87 @@ hipError_t af_launch_s5_filter(const af_grec *recs, const int32_t *n_rec, int64_
                                                s)) != hipSuccess)
             return e;
         hipLaunchKernelGGL(k_s6_rows, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, in, q, q_stride, q_lens, sel,
-                           n_sel, cap, out, out_stride, out_lens, out_src, n_over);
+                           n_sel, cap, out, out_stride, out_lens, out_src, n_over, (uint8_t *)nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_s6_count, dim3(1), dim3(64), 0, s, n_sel, cap, n_out);
+    return hipGetLastError();
+}
+
+hipError_t af_launch_s6_queries(int64_t n, const uint8_t *q, int32_t q_stride, const int32_t *q_lens,
+                                const int32_t *q_rows, const af_aln_out &s2, const uint8_t *cont, const af_s6_set &pre,
+                                uint8_t *keep, int32_t *sel, int64_t *n_sel, void *temp, size_t temp_bytes,
+                                hipStream_t s) {
+    hipError_t e;
+    const S5In in{nullptr, nullptr, q_rows, s2.flag, s2.pos, s2.n_cigar, s2.cigar, cont};
+    if (n <= 0) {
+        if ((e = hipMemsetAsync(n_sel, 0, sizeof(int64_t), s)) != hipSuccess) return e;
+    } else {
+        const int bs = 256;
+        hipLaunchKernelGGL(k_s5_lead, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, in, n, keep);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        size_t tb = temp_bytes;
+        if ((e = hipcub::DeviceSelect::Flagged(temp, tb, hipcub::CountingInputIterator<int32_t>(0), keep, sel, n_sel, n,
+                                               s)) != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(k_s6_rows, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, in, q, q_stride, q_lens, sel,
+                           n_sel, pre.cap, pre.q, pre.stride, pre.lens, pre.src, (int32_t *)nullptr, pre.over);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_s6_count, dim3(1), dim3(64), 0, s, n_sel, pre.cap, pre.n);
+    return hipGetLastError();
+}
+
+size_t af_s6_compact_temp_bytes(int64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t *)nullptr, (int32_t *)nullptr, n);
+    return b;
+}
+
+hipError_t af_launch_s6_check(const af_grec *recs, const int32_t *n_rec, int64_t n, const int32_t *q_rows,
+                              const af_aln_out &s2, const uint8_t *cont, const af_s6_set &pre, uint8_t *keep,
+                              uint8_t *live, hipStream_t s) {
+    const int bs = 256;
+    if (n > 0) {
+        const S5In in{recs, n_rec, q_rows, s2.flag, s2.pos, s2.n_cigar, s2.cigar, cont};
+        hipLaunchKernelGGL(k_s5_check, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), 0, s, in, n, keep);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (pre.cap > 0)
+        hipLaunchKernelGGL(k_s6_live, dim3((unsigned)((pre.cap + bs - 1) / bs)), dim3(bs), 0, s, pre.src, pre.n, pre.cap,
+                           keep, live);
+    return hipGetLastError();
+}
+
+hipError_t af_launch_s6_compact(const af_s6_set &pre, const uint8_t *live, const af_s6_set &out, int32_t max_rows,
+                                int32_t *caps, int32_t *flag, int32_t *idx, int32_t *sflag, int32_t *sidx, void *temp,
+                                size_t temp_bytes, hipStream_t s) {
+    hipError_t e;
+    const int bs = 256;
+    if (out.n_over && (e = hipMemsetAsync(out.n_over, 0, sizeof(int32_t), s)) != hipSuccess) return e;
+    // survivor flags and new indices of the pre rows and of the spilled rows, the counts, then the copies
+    if (pre.cap > 0) {
+        hipLaunchKernelGGL(k_s6_pre_flags, dim3((unsigned)((pre.cap + bs - 1) / bs)), dim3(bs), 0, s, live, pre.n,
+                           pre.cap, flag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        size_t tb = temp_bytes;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(temp, tb, flag, idx, pre.cap, s)) != hipSuccess) return e;
+    }
+    if (pre.spill_cap > 0) {
+        hipLaunchKernelGGL(k_s6_spill_flags, dim3((unsigned)((pre.spill_cap + bs - 1) / bs)), dim3(bs), 0, s, pre, flag,
+                           sflag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        size_t tb = temp_bytes;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(temp, tb, sflag, sidx, pre.spill_cap, s)) != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_s6_compact_counts, dim3(1), dim3(64), 0, s, pre, out, flag, idx, sflag, sidx);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (pre.cap > 0) {
+        hipLaunchKernelGGL(k_s6_compact, dim3(1024), dim3(bs), 0, s, pre, out, flag, idx, max_rows, caps);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (pre.spill_cap > 0)
+        hipLaunchKernelGGL(k_s6_spill_copy, dim3(256), dim3(bs), 0, s, pre, out, flag, idx, sflag, sidx, caps);
     return hipGetLastError();
 }

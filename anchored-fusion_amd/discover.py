@@ -30,6 +30,9 @@ MAX_REC = _genome.MAX_REC
 # S4 and S5 as two concurrent genome calls on two contexts (1) or one call whose seed / region
 # launches cover both (0); bench A/B: AF_S4_SPLIT
 _S4_SPLIT = os.environ.get("AF_S4_SPLIT", "1") == "1"
+# S6 (BLAT) of every S5 query that can be kept, beside S5's genome call, compacted after the check
+# (1), or of the check's survivors after it (0, round 4's order); bench A/B: AF_S6_EARLY
+_S6_EARLY = os.environ.get("AF_S6_EARLY", "1") == "1"
 EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
 HIT_WORDS = 44      # af_grec as int32 words (176 B)
 PSL_WORDS = 82      # af_psl as int32 words (328 B)
@@ -95,8 +98,8 @@ class CandidateDiscovery:
         self._npair = 0
 
     def _alloc_queries(self, cap):
-        """The query buffers (S4 + S5 queries, their records, the S6 queries and their rows) for cap
-        queries; run() grows them when S3's counts need more."""
+        """The query buffers (S4 + S5 queries and their records) for cap queries; run() grows them
+        when S3's counts need more."""
         import torch
         z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
         self.qcap = int(cap)
@@ -104,29 +107,96 @@ class CandidateDiscovery:
         self.q_lens, self.q_rows = z(self.qcap), z(self.qcap)
         self.q_recs = z(self.qcap * MAX_REC * _genome.REC_DTYPE.itemsize, dt=torch.uint8)
         self.q_nh = z(self.qcap)   # SAM records per query
-        self.s6 = dict(q=z(self.qcap, _lib.AF_MAX_READ, dt=torch.uint8), lens=z(self.qcap), src=z(self.qcap), n=z(1),
-                       over=z(1))
-        self.t_rows = z(self.qcap * _blat.MAX_ROWS * _blat.PSL_DTYPE.itemsize, dt=torch.uint8)
-        self.t_nh = z(self.qcap)
-        # S6 rows past MAX_ROWS per query (BLAT prints them all; fn:630-649 reads every one):
-        # af_blat_spill's pool, counted in the summary
-        spill_cap = max(1 << 16, self.qcap // 2)
-        self.t_spill = dict(rows=z(spill_cap * _blat.PSL_DTYPE.itemsize, dt=torch.uint8), q=z(spill_cap), n=z(1))
+        if getattr(self, "s6cap", 0) == 0:
+            self._alloc_s6(4096)
+
+    def _alloc_s6(self, cap):
+        """The S6 rows for cap S5 queries, twice: `s6p` before the genome check (every QNAME-group
+        leader's row, searched beside S5) and the survivors' (`s6`, `t_rows`, `t_nh`, `t_spill`:
+        what the consumers read), each with its PSL rows and a spill pool for the rows past MAX_ROWS
+        (BLAT prints them all; fn:630-649 reads every one); the pre set also counts its cap events
+        per query, so that the summary counts the survivors' only."""
+        import torch
+        z = lambda *shape, dt=torch.int32: torch.zeros(shape, dtype=dt, device=self.dev)  # noqa: E731
+        self.s6cap = int(cap)
+        spill_cap = max(getattr(self, "spill_min", 1 << 16), self.s6cap // 2)
+        psl = _blat.PSL_DTYPE.itemsize
+
+        def rows_set():
+            return dict(q=z(self.s6cap, _lib.AF_MAX_READ, dt=torch.uint8), lens=z(self.s6cap), src=z(self.s6cap), n=z(1),
+                        rows=z(self.s6cap * _blat.MAX_ROWS * psl, dt=torch.uint8), n_rows=z(self.s6cap),
+                        spill_rows=z(spill_cap * psl, dt=torch.uint8), spill_q=z(spill_cap), spill_n=z(1))
+        self.s6p = rows_set()
+        self.s6p.update(over=z(self.s6cap, dt=torch.uint8), caps=z(len(_blat.CAP_NAMES) * self.s6cap),
+                        live=z(self.s6cap, dt=torch.uint8))
+        f = rows_set()
+        f["n_over"] = z(1)
+        self.s6f = f
+        # the survivors' set under the names the consumers read
+        self.s6 = dict(q=f["q"], lens=f["lens"], src=f["src"], n=f["n"], over=f["n_over"])
+        self.t_rows, self.t_nh = f["rows"], f["n_rows"]
+        self.t_spill = dict(rows=f["spill_rows"], q=f["spill_q"], n=f["spill_n"])
+
+    def _s6_pre(self, b, n5, stream, cont_t=None):
+        """The S6 query rows of the S5 queries [b, b + n5) that lead a QNAME group (fn:506-528 on
+        the rows the check can keep), before the check runs."""
+        if n5 > self.s6cap:
+            self._alloc_s6(int(n5 * 1.25) + 1024)
+        _genome.s6_queries_device(self.tiles_ref.ctx, n5, self.q[b:], self.L, self.q_lens[b:], self.q_rows[b:],
+                                  self.out, self.s6p, stream=stream, cont_t=cont_t)
 
     def _s6_search(self, stream):
-        """S6 (`blat -minScore=20 genome split.fa`, fn:530) of the survivors' rows: MAX_ROWS per
-        query in t_rows, the rest in the spill pool (registered for this search only: the tile
-        reference may serve other searches)."""
+        """S6 (`blat -minScore=20 genome split.fa`, fn:530) of the pre-check rows, its first part
+        (af_blat_device_begin: every strand but the heavy ones searched; _s6_finish completes it for
+        the survivors): MAX_ROWS per query in their row slots, the rest in their spill pool, cap
+        events per query (registered for this search only: the tile reference may serve others)."""
         import torch
+        sp = self.s6p
         with torch.cuda.stream(stream):
-            self.t_spill["n"].zero_()
-        sp = self.t_spill
-        self.tiles_ref.spill_to(sp["rows"], sp["q"], sp["n"])
+            sp["spill_n"].zero_()
+            sp["caps"].zero_()
+        self.tiles_ref.spill_to(sp["spill_rows"], sp["spill_q"], sp["spill_n"])
+        self.tiles_ref.query_caps_to(sp["caps"], self.s6cap)
         try:
-            self.tiles_ref.search_device(self.s6["q"], self.s6["n"], _lib.AF_MAX_READ, self.t_rows, self.t_nh,
-                                         lens_t=self.s6["lens"], p=self.p_tail, stream=stream)
+            self.tiles_ref.search_device_begin(sp["q"], sp["n"], _lib.AF_MAX_READ, sp["rows"], sp["n_rows"],
+                                               lens_t=sp["lens"], p=self.p_tail, stream=stream)
         finally:
             self.tiles_ref.spill_to()
+            self.tiles_ref.query_caps_to()
+
+    def _s6_check(self, b, n5, recs, stream, cont_t=None):
+        """S5's genome check (fn:718-768) of the queries [b, b + n5): the pre rows' live flags."""
+        w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+        _genome.s6_check_device(self.tiles_ref.ctx, recs[b * w:], self.q_nh[b:], n5, self.q_rows[b:], self.out,
+                                self.s6p, self.s6p["live"], stream=stream, cont_t=cont_t)
+
+    def _s6_finish(self, stream):
+        """The rest of the S6 search for the survivors (af_blat_device_end), then their S6 rows and
+        BLAT rows compacted and renumbered in query order."""
+        self.tiles_ref.search_device_end(self.s6p["live"], stream=stream)
+        _genome.s6_compact_device(self.tiles_ref.ctx, self.s6p, self.s6p["live"], self.s6f, stream=stream)
+
+    def _s6_late(self, b, n5, recs, s0, s6, cont_t=None):
+        """Round 4's order: S5's genome check and its survivors' S6 rows (af_s5_filter_device), then
+        their BLAT on slot 1's stream."""
+        import torch
+        w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+        if n5 > self.s6cap:
+            self._alloc_s6(int(n5 * 1.25) + 1024)
+        f = self.s6f
+        _genome.s5_filter_device(self.ref.ctx, recs[b * w:], self.q_nh[b:], n5, self.q[b:], self.L, self.q_lens[b:],
+                                 self.q_rows[b:], self.out, self.s6cap, f["q"], f["lens"], f["src"], f["n"],
+                                 f["n_over"], stream=s0, cont_t=cont_t)
+        s6.wait_stream(s0)
+        with torch.cuda.stream(s6):
+            f["spill_n"].zero_()
+        self.tiles_ref.spill_to(f["spill_rows"], f["spill_q"], f["spill_n"])
+        try:
+            self.tiles_ref.search_device(f["q"], f["n"], _lib.AF_MAX_READ, f["rows"], f["n_rows"], lens_t=f["lens"],
+                                         p=self.p_tail, stream=s6)
+        finally:
+            self.tiles_ref.spill_to()
+        s0.wait_stream(s6)
 
     def s6_spilled(self):
         """{S6 query: [its rows past MAX_ROWS]} of the last search, in row order (synchronises)."""
@@ -199,9 +269,18 @@ class CandidateDiscovery:
         pe = _lib.default_pe(chunk_bases=self.chunk_bases, pair_base=0)
         recs = self.q_recs.view(torch.int32)
         w = MAX_REC * _genome.REC_DTYPE.itemsize // 4
+        b = 2 * npair
+        # S6's queries depend only on the S2 records (fn:506-528: deal_cigar's SEQ of the anchored
+        # record); the genome check only decides which are kept.  So the rows of every query that
+        # can be kept are written now and searched (fn:530) on slot 1's stream beside S4 / S5, and
+        # compacted to the survivors once the check has run.
+        if _S6_EARLY:
+            self._s6_pre(b, n5, s0)
+            s6.wait_stream(s0)
+            self._s6_search(s6)
         # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188: bwa's chunks over this input) and S5 (`bwa mem
-        # -M genome split_reads.fa`, fn:716) with one launch of the seed / region kernels; S5's
-        # records on s0, S4's on slot 2's stream (idle once S2 is done)
+        # -M genome split_reads.fa`, fn:716); S5's records on s0, S4's on slot 2's stream (idle
+        # once S2 is done)
         spe = self.grp.streams[2] if G > 2 else s0
         spe.wait_stream(s0)
         if _S4_SPLIT and spe is not s0:
@@ -212,22 +291,21 @@ class CandidateDiscovery:
                 self.ref.align_pe_device(self.q, npair, self.L, self.q_lens, recs, self.q_nh, params=self.p_genome,
                                          pe=pe, stream=spe, ctx=self._s4_ctx())
             if n5:
-                self.ref.align_se_device(self.q[2 * npair:], n5, self.L, recs[2 * npair * w:], self.q_nh[2 * npair:],
-                                         lens_t=self.q_lens[2 * npair:], params=self.p_genome, pe=pe, id_base=0,
+                self.ref.align_se_device(self.q[b:], n5, self.L, recs[b * w:], self.q_nh[b:],
+                                         lens_t=self.q_lens[b:], params=self.p_genome, pe=pe, id_base=0,
                                          stream=s0)
         elif npair or n5:
             self.ref.align_pe_se_device(self.q, npair, n5, self.L, self.q_lens, recs, self.q_nh,
                                         params=self.p_genome, pe_s4=pe, pe_s5=pe, se_id_base=0, stream=s0,
                                         stream_pe=spe)
-        # S5's genome check (fn:718-768) and the S6 queries (fn:506-528)
-        _genome.s5_filter_device(self.ref.ctx, recs[2 * npair * w:], self.q_nh[2 * npair:], n5, self.q[2 * npair:],
-                                 self.L, self.q_lens[2 * npair:], self.q_rows[2 * npair:], self.out, self.qcap,
-                                 self.s6["q"], self.s6["lens"], self.s6["src"], self.s6["n"], self.s6["over"],
-                                 stream=s0)
-        # S6 (`blat -minScore=20 genome split.fa`, fn:530) beside S4's records
-        s6.wait_stream(s0)
-        self._s6_search(s6)
-        s0.wait_stream(s6)
+        # S5's genome check (fn:718-768), then the rest of S6 (the survivors' heavy strands) and the
+        # survivors' rows
+        if _S6_EARLY:
+            self._s6_check(b, n5, recs, s0)
+            s0.wait_stream(s6)
+            self._s6_finish(s0)
+        else:
+            self._s6_late(b, n5, recs, s0, s6)
         s0.wait_stream(spe)
         if _DEBUG:
             s0.synchronize()
@@ -237,6 +315,7 @@ class CandidateDiscovery:
         self.counts = dict(tmp1=n1, tmp2=n2, anchored=na, s4_pairs=npair, s5_split_reads=n5,
                            s4_pairs_dropped=max(0, min(n1, n2) - npair), s5_dropped=max(0, nq_all - nq))
         self._npair = npair
+        self._s4_ctx_used = bool(_S4_SPLIT and spe is not s0 and npair)
         return s0
 
     def _s2(self, reads_t, lens_t=None, k1_events=None):
@@ -312,13 +391,21 @@ class CandidateDiscovery:
         ids_t = ids.to(self.dev, torch.int64).contiguous()
         cont_t = cont.to(self.dev, torch.uint8).contiguous()
         s0.wait_stream(torch.cuda.current_stream(self.dev))  # ids / cont were made on the current stream
+        # S6's rows before the check, searched on slot 1's stream beside S5 (as in run())
+        s6 = self.grp.streams[1] if self.grp.inflight > 1 else s0
+        if _S6_EARLY:
+            self._s6_pre(b, n5, s0, cont_t=cont_t)
+            s6.wait_stream(s0)
+            self._s6_search(s6)
         if n5:
             self.ref.align_se_ids_device(self.q[b:], n5, self.L, ids_t, recs[b * w:], self.q_nh[b:],
                                          lens_t=self.q_lens[b:], params=self.p_genome, pe=pe, stream=s0)
-        _genome.s5_filter_device(self.ref.ctx, recs[b * w:], self.q_nh[b:], n5, self.q[b:], self.L, self.q_lens[b:],
-                                 self.q_rows[b:], self.out, self.qcap, self.s6["q"], self.s6["lens"], self.s6["src"],
-                                 self.s6["n"], self.s6["over"], stream=s0, cont_t=cont_t)
-        self._s6_search(s0)
+        if _S6_EARLY:
+            self._s6_check(b, n5, recs, s0, cont_t=cont_t)
+            s0.wait_stream(s6)
+            self._s6_finish(s0)
+        else:
+            self._s6_late(b, n5, recs, s0, s6, cont_t=cont_t)
         s0.synchronize()
         n6 = int(self.s6["n"].item())
         self.counts["s6_queries"] = n6
@@ -369,7 +456,8 @@ class CandidateDiscovery:
                  s2_overflow_reads=int(((self.out["flag"] & (_lib.AF_FLAG_MEM_OVERFLOW | _lib.AF_FLAG_CIGAR_OVERFLOW))
                                         != 0).sum().item()))
         gs = self.ref.stats()
-        if getattr(self, "_ctx4", None) is not None:  # S4's call on its own context
+        if getattr(self, "_ctx4", None) is not None and getattr(self, "_s4_ctx_used", False):
+            # S4's call on its own context, when this pass made one (its counters are the last call's)
             for k, v in self.ref.stats(ctx=self._ctx4).items():
                 gs[k] += v
         c.update({f"genome_{k}": v for k, v in gs.items()})

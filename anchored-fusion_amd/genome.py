@@ -305,6 +305,84 @@ def s5_filter_device(ctx, recs_t, nrec_t, n, q_t, q_stride, q_lens_t, q_rows_t, 
         _stream_handle(stream)), "af_s5_filter_device")
 
 
+def _s2_aln(s2_out):
+    import torch
+    for k in ("flag", "pos", "n_cigar"):
+        _need(s2_out[k], 4, f"s2_out[{k}]", torch.int32)
+    if s2_out["cigar"].numel() != s2_out["flag"].numel() * _lib.AF_MAX_CIGAR:
+        raise ValueError("s2_out['cigar'] must hold AF_MAX_CIGAR words per record")
+    return _lib.AlnOut(*(s2_out[k].data_ptr() for k in ("flag", "pos", "score", "n_cigar", "hits", "cigar")))
+
+
+_MAX_PSL_ROWS = 16  # blat.MAX_ROWS (af_s6_compact_device's max_rows)
+
+
+def s6_set(d):
+    """af_s6_set of a dict of device tensors (discover.CandidateDiscovery._alloc_s6's layout; absent
+    keys are NULL)."""
+    def ptr(k):
+        t = d.get(k)
+        return None if t is None else t.data_ptr()
+    cap = int(d["q"].shape[0])
+    spill_cap = 0
+    if d.get("spill_rows") is not None:
+        spill_cap = min(d["spill_rows"].numel() // 328, int(d["spill_q"].numel()))
+    if d.get("rows") is not None and d["rows"].numel() < cap * _MAX_PSL_ROWS * 328:
+        raise ValueError("rows hold fewer than cap * max_rows PSL rows")
+    for k in ("lens", "src", "n_rows"):
+        if d.get(k) is not None and d[k].numel() < cap:
+            raise ValueError(f"{k} holds fewer than cap entries")
+    if d.get("caps") is not None and d["caps"].numel() < 4 * cap:
+        raise ValueError("caps holds fewer than 4 * cap counters")
+    return _lib.S6Set(ptr("q"), int(d["q"].shape[1]), 0, ptr("lens"), ptr("src"), ptr("n"), ptr("over"), ptr("n_over"),
+                      ptr("rows"), ptr("n_rows"), ptr("caps"), ptr("spill_rows"), ptr("spill_q"), ptr("spill_n"),
+                      spill_cap, cap)
+
+
+def s6_queries_device(ctx, n, q_t, q_stride, q_lens_t, q_rows_t, s2_out, pre, stream=None, cont_t=None):
+    """af_s6_queries_device: the S6 row of every QNAME-group leader among the n S5 queries (the
+    queries fn:718-768 can keep), before the genome check, into the dict `pre`."""
+    import torch
+    n = int(n)
+    _need(q_t, n * int(q_stride), "q_t")
+    _need(q_lens_t, 4 * n, "q_lens_t")
+    _need(q_rows_t, 4 * n, "q_rows_t", torch.int32)
+    if cont_t is not None:
+        _need(cont_t, n, "cont_t", torch.uint8)
+    o, st = _s2_aln(s2_out), s6_set(pre)
+    _lib.check(ctx, _lib.lib().af_s6_queries_device(
+        ctx, n, q_t.data_ptr(), int(q_stride), q_lens_t.data_ptr(), q_rows_t.data_ptr(), ctypes.byref(o),
+        None if cont_t is None else cont_t.data_ptr(), ctypes.byref(st), _stream_handle(stream)), "af_s6_queries_device")
+
+
+def s6_check_device(ctx, recs_t, nrec_t, n, q_rows_t, s2_out, pre, live_t, stream=None, cont_t=None):
+    """af_s6_check_device: the genome check of the n S5 queries (fn:718-768); live_t[k] (uint8
+    [pre cap]) = 1 when pre row k's query survives."""
+    import torch
+    n = int(n)
+    _need(recs_t, n * MAX_REC * REC_DTYPE.itemsize, "recs_t")
+    _need(nrec_t, 4 * n, "nrec_t")
+    _need(q_rows_t, 4 * n, "q_rows_t", torch.int32)
+    _need(live_t, int(pre["q"].shape[0]), "live_t", torch.uint8)
+    if cont_t is not None:
+        _need(cont_t, n, "cont_t", torch.uint8)
+    o, sp = _s2_aln(s2_out), s6_set(pre)
+    _lib.check(ctx, _lib.lib().af_s6_check_device(
+        ctx, recs_t.data_ptr(), nrec_t.data_ptr(), n, q_rows_t.data_ptr(), ctypes.byref(o),
+        None if cont_t is None else cont_t.data_ptr(), ctypes.byref(sp), live_t.data_ptr(), _stream_handle(stream)),
+        "af_s6_check_device")
+
+
+def s6_compact_device(ctx, pre, live_t, out, stream=None):
+    """af_s6_compact_device: pre's S6 rows and BLAT results of the live rows into `out`,
+    renumbered in order; their cap events go to ctx's af_blat_caps counters."""
+    import torch
+    _need(live_t, int(pre["q"].shape[0]), "live_t", torch.uint8)
+    sp, so = s6_set(pre), s6_set(out)
+    _lib.check(ctx, _lib.lib().af_s6_compact_device(ctx, ctypes.byref(sp), live_t.data_ptr(), ctypes.byref(so),
+                                                    _MAX_PSL_ROWS, _stream_handle(stream)), "af_s6_compact_device")
+
+
 def sam_lines(names, name, seq, recs, n):
     out = []
     rc = None

@@ -147,6 +147,21 @@ class Searches:
         return out
 
 
+def homolog_rows(path, gtf, genome, gene, anchor, place):
+    """<G>_homo_genes.bed (`Find_homo_genes`, fn:336-373), made once: AF:196 searches only when the
+    file is absent, and reads it (column 4, the gene id) either way.  Rows (chrom, start, end,
+    gene_id, gene_name, strand) as strings; the file is written whole or not at all."""
+    if os.path.exists(path):
+        with open(path) as fh:
+            return [ln.rstrip("\n").split("\t") for ln in fh if ln.strip()]
+    rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], place)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as fh:
+        fh.writelines("\t".join(str(v) for v in r) + "\n" for r in rows)
+    os.replace(tmp, path)
+    return rows
+
+
 def align_anchor(anchor, reads, lens, aligner_factory):
     """S1 + S2 for one anchor (AF:167-182): index it and align every pair."""
     aligner = aligner_factory(anchor.encode())
@@ -405,7 +420,8 @@ def run(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gene_names=N
         folder = os.path.join(out_folder, gene + "_fusion")
         os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
         t0 = time.perf_counter()
-        homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+        homo_rows = homolog_rows(os.path.join(folder, "work_dir", gene + "_fusion_homo_genes.bed"), gtf, genome, gene,
+                                 anchor, searches.place)
         log(f"[{gene}] homologs: {len(homo_rows)} gene rows ({time.perf_counter() - t0:.1f} s)")
         prefix = os.path.join(folder, gene + "_fusion")
         if dev_reads is not None:
@@ -491,7 +507,8 @@ def _run_sharded(anchored_cds, fastq1, fastq2, ref_seq, ref_ann, out_folder, gen
         if rank == 0:
             folder = os.path.join(out_folder, gene + "_fusion")
             os.makedirs(os.path.join(folder, "work_dir"), exist_ok=True)
-            homo_rows = partner.homolog_genes(gtf, genome, [(gene, anchor)], searches.place)
+            homo_rows = homolog_rows(os.path.join(folder, "work_dir", gene + "_fusion_homo_genes.bed"), gtf, genome,
+                                     gene, anchor, searches.place)
             results[gene] = consume_products(gene, anchor, index, homo_rows, searches,
                                              os.path.join(folder, gene + "_fusion"), s4, split_sam, psl, log=log,
                                              filt=filt)

@@ -66,31 +66,27 @@ class Placer:
         return ref
 
     def __call__(self, targets, queries, preset):
-        from . import blat, stitch
+        from . import blat
         header = ["psLayout version 3\n", "\n"]
         if not targets or not queries:
             return header
         p = blat.params(preset)
         ref = self.tiles(targets, p.step_size)
-        # queries longer than the kernel's read limit (the anchor transcript itself, fn:341/966)
-        # are searched as windows with no score / identity floor and stitched (stitch.py)
         lines = [[] for _ in queries]
         short = [i for i, (_, sq) in enumerate(queries) if len(sq) <= _lib.AF_MAX_READ]
-        longs = [i for i, (_, sq) in enumerate(queries) if len(sq) > _lib.AF_MAX_READ]
         if short:  # every row of each query (the rows past MAX_ROWS from the search's spill pool)
             rows, nr, extra = ref.search_all([queries[i][1] for i in short], p)
             for k, i in enumerate(short):
                 lines[i] = blat.psl_lines(ref, [queries[i]], rows[k:k + 1], nr[k:k + 1],
                                           extra={0: extra[k]} if k in extra else None)
-        if longs:
-            pw = blat.params(preset, min_score=0, min_identity=0)
-            pieces = [stitch.windows(queries[i][1]) for i in longs]
-            rows, nr = ref.search([w for ps in pieces for _, w in ps], pw, blat.MAX_ROWS)
-            k = 0
-            for i, ps in zip(longs, pieces):
-                nm, sq = queries[i]
-                lines[i] = stitch.stitched_lines(ref, targets, nm, sq, rows[k:k + len(ps)], nr[k:k + len(ps)], ps, p)
-                k += len(ps)
+        # a query longer than a read (the anchor transcript itself, fn:341 / fn:966) is searched
+        # whole, as BLAT takes it (af_blat_long)
+        for i, (nm, sq) in enumerate(queries):
+            if len(sq) > _lib.AF_MAX_READ:
+                rows, n_all, blocks, off = ref.search_long(sq, p)
+                if n_all > len(rows):
+                    raise _lib.AFError(f"af_blat_long: {n_all} rows for {nm}, {len(rows)} returned")
+                lines[i] = blat.psl_lines_long(ref, nm, sq, rows, blocks, off)
         out = list(header)
         for ln in lines:
             out += ln

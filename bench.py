@@ -447,8 +447,10 @@ def bench_c3(args, world, rank, gpu, dev, backend):
             "s2": round(phase(0, 1), 3), "s3_partition": round(phase(1, 2), 3),
             "gather_queries": round(phase(2, 3), 3), "genome_bwa_s4_s5": round(phase(3, 4), 3),
             "note": "HIP events on the first slot's stream; s2 includes every batch's K1 + K2 + K3; "
-                    "genome_bwa_s4_s5 = S5, its genome check, then S4 on slot 0 beside the S6 BLAT "
-                    "of S5's survivors on slot 1's stream, joined at its end"},
+                    "genome_bwa_s4_s5 = the gathers' end to the join of: S4 (bwa PE, its own context, slot 2's "
+                    "stream), S5 (bwa SE, slot 0) then its genome check, and S6 BLAT of every S5 query that can "
+                    "be kept (slot 1, from the gathers on; its heavy strands after the check, survivors only), "
+                    "compacted to the survivors on slot 0"},
         "genome_phase": None if world > 1 else genome_phase(summ, phase(3, 4)),
         "kernels_ms": {"seed_filter_per_launch": round(k1_launch_ms, 5), "seed_filter_per_step": round(k1_ms, 4)},
         "roofline": {
@@ -608,10 +610,18 @@ def cpu_baseline_c3(anchor, reads_t, args, subset):
         counts = dict(s4_pairs=len(s4) // 2, s5_split_reads=len(fasta), s6_queries=len(s6q))
     s2s3 = st["s2_s3"] + st["gather"]
     gen = st["s4"] + st["s5"] + st["s5_check"] + st["s6"]
-    return {"value": round(n * passes / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "host_cpus_visible": os.cpu_count(),
+    rate = n * passes / dt
+    ncpu = os.cpu_count() or threads
+    return {"value": round(rate, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": ncpu,
             "cores_note": f"{threads} OpenMP threads = the GPU's host CPU share (OMP_NUM_THREADS); "
                           f"host_cpus_visible = the whole machine",
+            "per_core": round(rate / threads, 1),
+            "all_cores_extrapolated": {
+                "value": round(rate / threads * ncpu, 1), "cores": ncpu, "measured": False,
+                "note": "per-core rate x host_cpus_visible (linear, an upper bound for the port): the GPU pool "
+                        "shares the machine and caps a one-GPU job's host threads at its CPU share, so the "
+                        "all-core run is not made"},
             "legs": {
                 "s2_s3": {"pairs_per_s": round(n * passes / s2s3, 1), "s_per_pass": round(s2s3 / passes, 3),
                           "comparable": True,

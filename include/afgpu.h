@@ -214,6 +214,37 @@ int af_blat_device(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, c
 int af_blat_device_range(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_first,
                          const int32_t *d_n_queries, int64_t cap_queries, int32_t stride, const int32_t *d_lens,
                          const af_blat_params *p, int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
+/* One long query searched whole (functions.py:341 `Find_homo_genes` and fn:966 hand BLAT the anchor
+ * transcript, kilobases long, as one query): the same search as af_blat with caps sized for it --
+ * AF_BLAT_LONG_HITS tile hits and AF_BLAT_LONG_CLUMPS clumps per strand, AF_BLAT_LONG_PART_BLOCKS
+ * blocks per part -- and rows of any block count.  Host buffers, synchronous.  Every row of both
+ * strands best first (the af_blat order, then emission order); *n_rows = all of them, the first
+ * max_rows written to rows (block_count = all the row's blocks; its first 16 also in the row) with
+ * their blocks at blocks[block_off[k], block_off[k + 1]) (block_off: max_rows + 1 entries);
+ * *n_blocks = the blocks of the rows written -- more than block_cap: AF_E_CAPACITY, no row written.
+ * Cap events are counted on the context (af_blat_caps). */
+#define AF_BLAT_LONG_MAX 131072
+#define AF_BLAT_LONG_HITS (1 << 22)
+#define AF_BLAT_LONG_CLUMPS (1 << 17)
+#define AF_BLAT_LONG_PART_BLOCKS 256
+typedef struct {
+    int32_t size, q_start;  /* q_start on the reverse-complemented query for '-', as af_psl */
+    int64_t t_start;
+} af_psl_block;
+int af_blat_long(af_ctx *ctx, const af_index *idx, const uint8_t *query, int32_t len, const af_blat_params *p,
+                 int32_t max_rows, af_psl *rows, int32_t *n_rows, af_psl_block *blocks, int64_t block_cap,
+                 int64_t *block_off, int64_t *n_blocks);
+/* af_blat_device in two parts, so that a caller can drop queries while the search runs (S6 searched
+ * beside S5's genome check, discover.py): _begin enqueues the per-strand pass -- every query strand
+ * with at most 32 clumps (env AF_BLAT_HEAVY_CLUMPS) searched to its rows; the heavier strands' clumps
+ * left as jobs -- and _end the rest: the jobs' alignments spread over the chip, those strands' chains,
+ * then every query's rows, for the queries with d_live[q] != 0 (NULL: all; a query not live gets 0
+ * rows).  Between the two the context holds the search: no other search may run on it.
+ * af_blat_device = _begin + _end(NULL); the rows of the live queries are the same either way. */
+int af_blat_device_begin(af_ctx *ctx, const af_index *idx, const uint8_t *d_queries, const int32_t *d_n_queries,
+                         int64_t cap_queries, int32_t stride, const int32_t *d_lens, const af_blat_params *p,
+                         int32_t max_rows, af_psl *d_rows, int32_t *d_n_rows, void *stream);
+int af_blat_device_end(af_ctx *ctx, const uint8_t *d_live, void *stream);
 /* A device pool for the rows past max_rows (BLAT prints every row; the fixed per-query row slots
  * keep the first max_rows): once registered on ctx, every later af_blat_device(_range) call on ctx
  * appends each query's rows past its first max_rows to d_rows[k] with d_query[k] = the query's
@@ -236,6 +267,14 @@ int af_blat_spill(af_ctx *ctx, af_psl *d_rows, int32_t *d_query, int32_t *d_n, i
 #define AF_BLAT_CAP_ROWS 3
 #define AF_BLAT_CAP_N 4
 int af_blat_caps(af_ctx *ctx, int32_t *out, int reset);
+/* The last device search's deferred strands (af_blat_device_begin): out[0] strands deferred, [1] their
+ * clump jobs, [2] jobs aligned, [3] strands chained (synchronises) */
+int af_blat_heavy_stats(af_ctx *ctx, int32_t *out);
+/* Per-query cap counters: once registered on ctx, the searches on ctx count each cap event of query q
+ * (q < cap) in d_counts[k * cap + q] (k = AF_BLAT_CAP_*; the caller zeroes them) instead of the
+ * context's counters, so a caller that later drops queries counts its survivors' events only
+ * (af_s6_compact_device).  d_counts == NULL or cap == 0 unregisters. */
+int af_blat_query_caps(af_ctx *ctx, int32_t *d_counts, int64_t cap);
 
 /* S3 on the device (Anchored_Fusion.py:182 `| samtools sort`, then AF:186-194): the records
  * d_flag/d_pos of n_reads reads (pair-major, as written by af_align_pairs*) in samtools'
@@ -387,6 +426,45 @@ int af_s5_filter_device(af_ctx *ctx, const af_grec *d_recs, const int32_t *d_n_r
                         const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens, const int32_t *d_q_rows,
                         const af_aln_out *d_s2, const uint8_t *d_cont, int64_t cap, uint8_t *d_s6, int32_t s6_stride,
                         int32_t *d_s6_lens, int32_t *d_s6_src, int32_t *d_n6, int32_t *d_n_over, void *stream);
+/* The same two steps split so that S6's BLAT runs beside S5's genome call (the S6 queries depend
+ * only on the S2 records; the check only decides which of them are kept):
+ *   af_s6_queries_device   the S6 row of every QNAME-group leader (a query that does not continue
+ *                          the group of the one before it -- the only queries the check can keep),
+ *                          rows as af_s5_filter_device writes them, in query order, into `pre`
+ *                          (q / lens / src / n; over[k] = 1 when row k was clipped);
+ *   af_blat_device_begin   on pre's rows (with af_blat_spill / af_blat_query_caps registered on pre's
+ *                          spill pool and per-query cap counters), beside the S5 genome call;
+ *   af_s6_check_device     the genome check of the n_queries S5 queries (as af_s5_filter_device):
+ *                          d_live[k] = 1 when pre row k's query survives (pre->cap bytes);
+ *   af_blat_device_end     with d_live: the deferred heavy strands of the survivors only;
+ *   af_s6_compact_device   pre's rows of the survivors, renumbered 0.. in query order, to `out` with
+ *                          their PSL rows (query field renumbered), row counts and spilled rows (pool
+ *                          order kept); the survivors' clipped rows are counted in *out->n_over and
+ *                          their cap events added to ctx's af_blat_caps counters.
+ * The result equals af_s5_filter_device followed by af_blat_device on its rows, byte for byte. */
+typedef struct {
+    uint8_t *q;           /* query rows, `stride` bytes each                                  */
+    int32_t stride, pad0;
+    int32_t *lens, *src;  /* row lengths; the S5 query index of each row                     */
+    int32_t *n;           /* row count (device word)                                         */
+    uint8_t *over;        /* pre: per row, 1 when the processed SEQ was clipped to the stride */
+    int32_t *n_over;      /* out: clipped rows (may be NULL)                                 */
+    af_psl *rows;         /* max_rows PSL row slots per query                                */
+    int32_t *n_rows;      /* PSL rows per query                                              */
+    int32_t *caps;        /* pre: the search's per-query cap counters (af_blat_query_caps)   */
+    af_psl *spill_rows;   /* rows past max_rows (af_blat_spill pool), their query, the count */
+    int32_t *spill_query, *spill_n;
+    int64_t spill_cap;
+    int64_t cap;          /* row capacity                                                     */
+} af_s6_set;
+int af_s6_queries_device(af_ctx *ctx, int64_t n_queries, const uint8_t *d_q, int32_t q_stride, const int32_t *d_q_lens,
+                         const int32_t *d_q_rows, const af_aln_out *d_s2, const uint8_t *d_cont, const af_s6_set *pre,
+                         void *stream);
+int af_s6_check_device(af_ctx *ctx, const af_grec *d_recs, const int32_t *d_n_rec, int64_t n_queries,
+                       const int32_t *d_q_rows, const af_aln_out *d_s2, const uint8_t *d_cont, const af_s6_set *pre,
+                       uint8_t *d_live, void *stream);
+int af_s6_compact_device(af_ctx *ctx, const af_s6_set *pre, const uint8_t *d_live, const af_s6_set *out,
+                         int32_t max_rows, void *stream);
 /* Test hook: the same per-query rules (one source, compiled for the host too) over host arrays --
  * the S2 fields indexed by the read rows q_rows (pos, n_cigar, cigar[row * AF_MAX_CIGAR ..]).
  * keep[q] = 1 when af_s5_filter_device keeps query q; rows[q] (out_stride bytes), out_lens[q] and

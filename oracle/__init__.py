@@ -154,6 +154,9 @@ def blat_params(**kw):
     return p
 
 
+BLOCK_DTYPE = np.dtype([("size", "<i4"), ("q_start", "<i4"), ("t_start", "<i8")])  # afo_psl_block
+
+
 class OracleTiles:
     """BLAT restatement (blat.c): the tile index of `seq` and its searches."""
 
@@ -192,6 +195,34 @@ class OracleTiles:
         if rc != 0:
             raise RuntimeError(f"afo_blat failed: {rc}")
         return rows, nr
+
+    def blat_long(self, query, params=None, max_rows=4096):
+        """afo_blat_long: one long query searched whole -> (rows [k] PSL_DTYPE, n_rows (all rows),
+        blocks [m] BLOCK_DTYPE, block_off [k + 1]): row i's blocks are blocks[off[i]:off[i + 1]]."""
+        L = lib()
+        L.afo_blat_long.restype = ctypes.c_int
+        L.afo_blat_long.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32, ctypes.POINTER(BlatParams),
+                                    ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        q = bytes(query)
+        p = params or blat_params(step_size=self.step)
+        rows = np.zeros(max_rows, dtype=PSL_DTYPE)
+        nr = np.zeros(1, np.int32)
+        off = np.zeros(max_rows + 1, np.int64)
+        nb = np.zeros(1, np.int64)
+        cap, caps0 = 1 << 16, self.caps.copy()
+        while True:
+            self.caps[:] = caps0  # a rerun with a larger block arena counts the caps once
+            blocks = np.zeros(cap, dtype=BLOCK_DTYPE)
+            rc = L.afo_blat_long(self.h, q, len(q), ctypes.byref(p), max_rows, rows.ctypes.data, nr.ctypes.data,
+                                 blocks.ctypes.data, cap, off.ctypes.data, nb.ctypes.data, self.caps.ctypes.data)
+            if rc == -3:
+                cap = int(nb[0])
+                continue
+            if rc != 0:
+                raise RuntimeError(f"afo_blat_long failed: {rc}")
+            k = min(int(nr[0]), max_rows)
+            return rows[:k].copy(), int(nr[0]), blocks[:int(off[k])].copy(), off[:k + 1].copy()
 
     def caps_read(self, reset=True):
         out = self.caps.copy()

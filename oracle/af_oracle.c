@@ -183,7 +183,8 @@ int afo_sc(const afo_params *p, uint8_t x, uint8_t y) {
 int afo_ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, const afo_params *p,
                   int w, int end_bonus, int zdrop, int h0, int *_qle, int *_tle, int *_gtle,
                   int *_gscore, int *_max_off) {
-    eh_t eh[AFO_MAX_READ + 2];
+    eh_t eh_stack[AFO_MAX_READ + 2];  /* a longer query (afo_blat_long's parts): a heap row */
+    eh_t *eh = qlen <= AFO_MAX_READ ? eh_stack : (eh_t *)malloc(sizeof(eh_t) * (qlen + 2));
     int oe_del = p->o_del + p->e_del, oe_ins = p->o_ins + p->e_ins;
     int i, j, max, max_i, max_j, max_ie, gscore, max_off, beg, end;
     memset(eh, 0, sizeof(eh_t) * (qlen + 2));
@@ -253,6 +254,7 @@ int afo_ext_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *target, 
     }
     *_qle = max_j + 1; *_tle = max_i + 1; *_gtle = max_ie + 1; *_gscore = gscore;
     *_max_off = max_off;
+    if (eh != eh_stack) free(eh);
     return max;
 }
 
@@ -307,8 +309,9 @@ int afo_global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *targe
     int score = eh[qlen].h;
     /* backtrack from the last cell, then reverse */
     int nc = 0, which = 0;
-    uint32_t tmp[2 * AFO_MAX_READ + 8];
-    int tcap = 2 * AFO_MAX_READ + 8;
+    uint32_t tmp_stack[2 * AFO_MAX_READ + 8];
+    int tcap = qlen + tlen + 8 > 2 * AFO_MAX_READ + 8 ? qlen + tlen + 8 : 2 * AFO_MAX_READ + 8;
+    uint32_t *tmp = tcap > 2 * AFO_MAX_READ + 8 ? (uint32_t *)malloc(sizeof(uint32_t) * tcap) : tmp_stack;
     i = tlen - 1;
     k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
     while (i >= 0 && k >= 0) {
@@ -322,6 +325,7 @@ int afo_global_dp(int qlen, const uint8_t *query, int tlen, const uint8_t *targe
     for (int x = 0; x < nc && x < cap; ++x) cig[x] = tmp[nc - 1 - x];
     *n_cig = nc;
     free(eh); free(z);
+    if (tmp != tmp_stack) free(tmp);
     return score;
 }
 
@@ -343,12 +347,15 @@ int afo_infer_bw(int l1, int l2, int score, int a, int q, int r) {
     return w;
 }
 
-/* bwa_gen_cigar2 restated; query/ref segments in forward-reference orientation */
-int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
-                  int64_t rb, int64_t re, uint32_t *cig, int *n_cig) {
-    uint8_t qq[AFO_MAX_READ], rr[2 * AFO_MAX_READ + 512];
+/* bwa_gen_cigar2 restated; query/ref segments in forward-reference orientation; at most cap ops
+ * written (*n_cig counts them all) */
+int afo_gen_cigar_cap(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
+                      int64_t rb, int64_t re, uint32_t *cig, int cap, int *n_cig) {
     int rlen = (int)(re - rb);
     int score = 0;
+    uint8_t qq_stack[AFO_MAX_READ], rr_stack[2 * AFO_MAX_READ + 512];  /* longer (afo_blat_long): heap */
+    uint8_t *qq = lq <= AFO_MAX_READ ? qq_stack : (uint8_t *)malloc(lq);
+    uint8_t *rr = rlen <= 2 * AFO_MAX_READ + 512 ? rr_stack : (uint8_t *)malloc(rlen);
     for (int i = 0; i < lq; ++i) qq[i] = qseg[i];
     for (int i = 0; i < rlen; ++i) rr[i] = text[rb + i];
     if (rb >= n) { /* reverse both so indels land leftmost in forward coordinates */
@@ -369,8 +376,14 @@ int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, i
         w = w < w_ ? w : w_;
         int min_w = d + 3;
         w = w > min_w ? w : min_w;
-        score = afo_global_dp(lq, qq, rlen, rr, p, w, cig, AFO_MAX_CIGAR, n_cig);
+        score = afo_global_dp(lq, qq, rlen, rr, p, w, cig, cap, n_cig);
     }
+    if (qq != qq_stack) free(qq);
+    if (rr != rr_stack) free(rr);
     return score;
 }
 
+int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
+                  int64_t rb, int64_t re, uint32_t *cig, int *n_cig) {
+    return afo_gen_cigar_cap(text, n, p, w_, lq, qseg, rb, re, cig, AFO_MAX_CIGAR, n_cig);
+}

@@ -163,6 +163,21 @@ int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int3
  * af_blat_caps: hits past MAXH per strand, MAXCL clumps reached, MAXR parts reached with clumps
  * left, per query rows past max_rows) */
 void afo_blat_set_literal(int on);  /* test switch: the chain DP recomputes every part each round */
+/* Long queries (afo_blat_long, af_blat_long): one query of up to AFO_BLAT_LONG_MAX bases searched
+ * whole with the same algorithm -- caps: AFO_BLAT_LONG_HITS tile hits and AFO_BLAT_LONG_CLUMPS
+ * clumps per strand, AFO_BLAT_LONG_PART_BLOCKS blocks per part; rows of any block count.  Every
+ * row of both strands best first; the first max_rows to rows (block_count = all the row's blocks,
+ * the first 16 also in the row), their blocks to blocks[block_off[k], block_off[k + 1]).  *n_rows
+ * = all rows; *n_blocks = the returned rows' blocks (-3 when more than block_cap, nothing
+ * written); caps[0..2] added to as afo_blat_caps counts them per strand. */
+#define AFO_BLAT_LONG_MAX 131072
+#define AFO_BLAT_LONG_HITS (1 << 22)
+#define AFO_BLAT_LONG_CLUMPS (1 << 17)
+#define AFO_BLAT_LONG_PART_BLOCKS 256
+typedef struct { int32_t size, q_start; int64_t t_start; } afo_psl_block;
+int afo_blat_long(const afo_tiles *X, const uint8_t *query, int32_t len, const afo_blat_params *bp, int32_t max_rows,
+                  afo_psl *rows, int32_t *n_rows, afo_psl_block *blocks, int64_t block_cap, int64_t *block_off,
+                  int64_t *n_blocks, int32_t *caps);
 int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int32_t stride, const int32_t *lens,
                   const afo_blat_params *bp, int32_t max_rows, afo_psl *rows, int32_t *n_rows, int threads,
                   int32_t *caps);

@@ -25,6 +25,9 @@ int afo_infer_bw(int l1, int l2, int score, int a, int q, int r);
  * text[rb, re) are reversed together for reverse-strand spans */
 int afo_gen_cigar(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
                   int64_t rb, int64_t re, uint32_t *cig, int *n_cig);
+/* the same writing at most cap ops (*n_cig counts them all); segments of any length */
+int afo_gen_cigar_cap(const uint8_t *text, int64_t n, const afo_params *p, int w_, int lq, const uint8_t *qseg,
+                      int64_t rb, int64_t re, uint32_t *cig, int cap, int *n_cig);
 
 /* the bwa text of the S2 anchor (bwa_pe.c): T = pac ++ revcomp(pac) with bwa's N
  * substitution, suffix ranks, and every 16-mer position of T */

@@ -104,14 +104,42 @@ static void blat_dp_params(afo_params *p) {
 }
 
 typedef struct { int64_t diag, t; int32_t q; } hit_t;
+typedef struct { int32_t sz, q; int64_t t; } blk_t;
+/* a growable list of blocks (the parts' and, in long mode, the rows') */
+typedef struct { blk_t *b; int64_t n, cap; } blk_arena;
+static void arena_push(blk_arena *a, int32_t sz, int32_t q, int64_t t) {
+    if (a->n == a->cap) {
+        a->cap = a->cap ? 2 * a->cap : 1024;
+        a->b = (blk_t *)realloc(a->b, sizeof(blk_t) * a->cap);
+    }
+    a->b[a->n].sz = sz; a->b[a->n].q = q; a->b[a->n].t = t;
+    ++a->n;
+}
+/* one aligned clump ("part"): its blocks are ar[boff, boff + nb); block 0 is (b0sz, b0q, b0t),
+ * which trim_front shortens */
 typedef struct {
     int32_t qb, qe, score, matches, mismatches, ncount, qni, qbi, tni, tbi, nb;
     int64_t tb, te;
-    int32_t bsz[AFO_PSL_MAX_BLOCKS], bq[AFO_PSL_MAX_BLOCKS];
-    int64_t bt[AFO_PSL_MAX_BLOCKS];
+    int32_t b0sz, b0q;
+    int64_t b0t, boff;
     int used;
 } reg_b;
 typedef struct { int32_t cnt, q; int64_t diag, t; } clump_t;
+
+/* The caps of a search mode.  Short queries (afo_blat: reads and tails, <= AFO_MAX_READ bases)
+ * are the GPU kernel k_blat's contract; long queries (afo_blat_long: the anchor transcript of
+ * fn:341 / fn:966, one query of up to AFO_BLAT_LONG_MAX bases) searched whole, as BLAT searches a
+ * query, with larger caps and rows of any block count. */
+typedef struct {
+    int64_t maxh;     /* tile hits per strand (the first maxh in query order) */
+    int maxcl;        /* clumps per strand (the first maxcl in diagonal order) */
+    int part_blocks;  /* blocks per part (a part with more is dropped) */
+    int cig_cap;      /* CIGAR ops per part (more: dropped) */
+    int row_blocks;   /* blocks per row (more: the row is dropped); 0: any */
+} blat_mode;
+static const blat_mode MODE_SHORT = {MAXH, MAXCL, AFO_PSL_MAX_BLOCKS, AFO_MAX_CIGAR, AFO_PSL_MAX_BLOCKS};
+static const blat_mode MODE_LONG = {AFO_BLAT_LONG_HITS, AFO_BLAT_LONG_CLUMPS, AFO_BLAT_LONG_PART_BLOCKS,
+                                    2 * AFO_BLAT_LONG_PART_BLOCKS + 1, 0};
 
 static int cmp_hit(const void *a, const void *b) {
     const hit_t *x = (const hit_t *)a, *y = (const hit_t *)b;
@@ -125,15 +153,20 @@ static int cmp_clump(const void *a, const void *b) {
     return x->q - y->q;
 }
 
-/* one clump's seed tile (q, t) -> an aligned region with blocks; 0 if dropped */
-static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, int64_t t, reg_b *r) {
+static inline blk_t blk_of(const blk_arena *ar, const reg_b *r, int k) {
+    if (k == 0) { blk_t b = {r->b0sz, r->b0q, r->b0t}; return b; }
+    return ar->b[r->boff + k];
+}
+
+/* one clump's seed tile (q, t) -> an aligned region with blocks (appended to ar); 0 if dropped */
+static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, int64_t t, reg_b *r,
+                       const blat_mode *md, blk_arena *ar, uint8_t *qs, uint8_t *ts, uint32_t *cig) {
     afo_params P;
     blat_dp_params(&P);
     int qle, tle, gtle, gscore, max_off;
     int score, truesc, qb, qe;
     int64_t tb, te;
     if (q > 0) {
-        uint8_t qs[AFO_MAX_READ], ts[AFO_MAX_READ + 64];
         int tl = (int)(t < q + P.w ? t : q + P.w);
         for (int i = 0; i < q; ++i) qs[i] = Q[q - 1 - i];
         for (int i = 0; i < tl; ++i) ts[i] = X->T[t - 1 - i];
@@ -162,21 +195,23 @@ static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, i
     int w3 = afo_infer_bw(lq, rl, truesc, P.a, P.o_ins, P.e_ins);
     w2 = w2 > w3 ? w2 : w3;
     w2 = w2 < 64 ? w2 : 64;
-    uint32_t cig[AFO_MAX_CIGAR];
     int nc = 0;
-    afo_gen_cigar(X->T, (int64_t)1 << 62, &P, w2, lq, Q + qb, tb, te, cig, &nc);
-    if (nc > AFO_MAX_CIGAR) return 0;
+    afo_gen_cigar_cap(X->T, (int64_t)1 << 62, &P, w2, lq, Q + qb, tb, te, cig, md->cig_cap, &nc);
+    if (nc > md->cig_cap) return 0;
     int xs = 0, xe = nc;
     if (nc > 0 && (cig[0] & 0xf) == 2) { tb += cig[0] >> 4; xs = 1; }
     else if (nc > 0 && (cig[nc - 1] & 0xf) == 2) { te -= cig[nc - 1] >> 4; xe = nc - 1; }
     memset(r, 0, sizeof(*r));
+    const int64_t a0 = ar->n;
+    r->boff = a0;
     int32_t x = qb;
     int64_t y = tb;
     for (int k = xs; k < xe; ++k) {
         int len = (int)(cig[k] >> 4), op = (int)(cig[k] & 0xf);
         if (op == 0) {
-            if (r->nb >= AFO_PSL_MAX_BLOCKS) return 0;
-            r->bsz[r->nb] = len; r->bq[r->nb] = x; r->bt[r->nb] = y; ++r->nb;
+            if (r->nb >= md->part_blocks) { ar->n = a0; return 0; }
+            arena_push(ar, len, x, y);
+            ++r->nb;
             for (int u = 0; u < len; ++u) {
                 uint8_t a = Q[x + u], b = X->T[y + u];
                 if (a > 3 || b > 3) ++r->ncount;
@@ -190,7 +225,8 @@ static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, i
             ++r->tni; r->tbi += len; y += len;
         }
     }
-    if (r->nb == 0) return 0;
+    if (r->nb == 0) { ar->n = a0; return 0; }
+    r->b0sz = ar->b[a0].sz; r->b0q = ar->b[a0].q; r->b0t = ar->b[a0].t;
     r->qb = qb; r->qe = qe; r->tb = tb; r->te = te;
     r->score = r->matches - r->mismatches - r->qni - r->tni;
     return 1;
@@ -201,15 +237,15 @@ static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, i
 static int trim_front(const afo_tiles *X, const uint8_t *Q, const reg_b *r, int k, reg_b *o) {
     *o = *r;
     if (k <= 0) return 1;
-    if (k >= r->bsz[0]) return 0;
+    if (k >= r->b0sz) return 0;
     for (int u = 0; u < k; ++u) {
-        uint8_t a = Q[r->bq[0] + u], b = X->T[r->bt[0] + u];
+        uint8_t a = Q[r->b0q + u], b = X->T[r->b0t + u];
         if (a > 3 || b > 3) --o->ncount;
         else if (a == b) --o->matches;
         else --o->mismatches;
     }
-    o->bsz[0] -= k; o->bq[0] += k; o->bt[0] += k;
-    o->qb = o->bq[0]; o->tb = o->bt[0];
+    o->b0sz -= k; o->b0q += k; o->b0t += k;
+    o->qb = o->b0q; o->tb = o->b0t;
     o->score = o->matches - o->mismatches - o->qni - o->tni;
     return 1;
 }
@@ -252,9 +288,9 @@ void afo_blat_set_literal(int on) { g_blat_literal = on; }
  * must end before i on both sequences; i is trimmed by the overlap (chain_trim) and must keep part
  * of its first block; the target gap must be <= max_intron and hold no N; the score is best[a] +
  * the trimmed part's score - 1 per query / target gap; the first a with the highest score wins
- * over i alone */
+ * over i alone.  pre: room for the first block's length + 1 */
 static void chain_node(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, const reg_b *regs,
-                       const int *ord, int *best, int *prev, const int *fl, int i) {
+                       const int *ord, int *best, int *prev, const int *fl, int i, int *pre) {
     const reg_b *ri = &regs[ord[i]];
     best[i] = ri->score; prev[i] = -1;
     if (g_blat_literal) {  /* the plain statement: trim_front per candidate */
@@ -271,10 +307,9 @@ static void chain_node(const afo_tiles *X, const afo_blat_params *bp, const uint
         return;
     }
     /* pre[k] = the score of the first block's first k bases (what trim_front removes) */
-    int pre[AFO_MAX_READ + 1];
     pre[0] = 0;
-    for (int u = 0; u < ri->bsz[0] && u < AFO_MAX_READ; ++u) {
-        uint8_t x = Q[ri->bq[0] + u], y = X->T[ri->bt[0] + u];
+    for (int u = 0; u < ri->b0sz; ++u) {
+        uint8_t x = Q[ri->b0q + u], y = X->T[ri->b0t + u];
         pre[u + 1] = pre[u] + ((x > 3 || y > 3) ? 0 : (x == y ? 1 : -1));
     }
     for (int j = 0; j < i; ++j) {
@@ -282,7 +317,7 @@ static void chain_node(const afo_tiles *X, const afo_blat_params *bp, const uint
         const reg_b *a = &regs[ord[j]];
         if (ri->qe <= a->qe || ri->te <= a->te) continue;
         const int k = chain_trim(a, ri);
-        if (k > 0 && k >= ri->bsz[0]) continue;
+        if (k > 0 && k >= ri->b0sz) continue;
         const int32_t bqb = ri->qb + k;
         const int64_t btb = ri->tb + k;
         if (btb - a->te > bp->max_intron || n_in(X, a->te, btb)) continue;
@@ -291,11 +326,52 @@ static void chain_node(const afo_tiles *X, const afo_blat_params *bp, const uint
     }
 }
 
-/* one strand of one query: its rows, the best cap_out in cmp_psl order, at out; *n_out counts
- * every row */
+/* where a strand's rows go: short mode, the best cap_out in cmp_psl order (out; *n_out counts every
+ * row); long mode, every row with all its blocks (rows / rblk, growable) */
+typedef struct { afo_psl h; int64_t boff; int32_t seq; } long_row;  /* seq: the strand's emission order */
+typedef struct {
+    afo_psl *out;
+    int *n_out, cap_out;
+    long_row *rows;
+    int64_t n_rows, cap_rows;
+    int32_t emitted[2];
+    blk_arena rblk;
+} row_sink;
+
+/* per-strand working memory, grown for the query and the mode */
+typedef struct {
+    hit_t *hits;
+    reg_b *regs;
+    clump_t *cl;
+    int *ord, *pre;
+    uint8_t *qs, *ts;
+    uint32_t *cig;
+    blk_arena ar;
+} strand_mem;
+
+static void strand_mem_init(strand_mem *m, const blat_mode *md, int L) {
+    memset(m, 0, sizeof(*m));
+    m->hits = (hit_t *)malloc(sizeof(hit_t) * md->maxh);
+    m->regs = (reg_b *)malloc(sizeof(reg_b) * md->maxcl);
+    m->cl = (clump_t *)malloc(sizeof(clump_t) * md->maxcl);
+    m->ord = (int *)malloc(sizeof(int) * 5 * (size_t)md->maxcl);
+    m->pre = (int *)malloc(sizeof(int) * (L + 2));
+    m->qs = (uint8_t *)malloc(L + 1);
+    m->ts = (uint8_t *)malloc(L + 64);
+    m->cig = (uint32_t *)malloc(sizeof(uint32_t) * (md->cig_cap + 1));
+}
+static void strand_mem_free(strand_mem *m) {
+    free(m->hits); free(m->regs); free(m->cl); free(m->ord); free(m->pre); free(m->qs); free(m->ts); free(m->cig);
+    free(m->ar.b);
+}
+
+/* one strand of one query: its rows to the sink; cap[3]: the hit, clump and stitching caps bound */
 static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uint8_t *Q, int L, int strand,
-                        int32_t qi, afo_psl *out, int *n_out, int cap_out, hit_t *hits, reg_b *regs, int *cap) {
-    int nh = 0;
+                        int32_t qi, const blat_mode *md, row_sink *sink, strand_mem *M, int *cap) {
+    hit_t *hits = M->hits;
+    reg_b *regs = M->regs;
+    M->ar.n = 0;
+    int64_t nh = 0;
     int64_t all = 0;
     for (int q = 0; q + TILE <= L; ++q) {
         uint32_t k;
@@ -303,50 +379,50 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         const int64_t c = (int64_t)X->start[k + 1] - X->start[k];
         if (c <= bp->rep_match) all += c;
     }
-    if (all > MAXH) cap[0] = 1;
-    for (int q = 0; q + TILE <= L && nh < MAXH; ++q) {
+    if (all > md->maxh) cap[0] = 1;
+    for (int q = 0; q + TILE <= L && nh < md->maxh; ++q) {
         uint32_t k;
         if (!tile_key(Q, q, &k)) continue;
         uint32_t lo = X->start[k], hi = X->start[k + 1];
         if (hi == lo || (int64_t)(hi - lo) > bp->rep_match) continue;
-        for (uint32_t i = lo; i < hi && nh < MAXH; ++i) {
+        for (uint32_t i = lo; i < hi && nh < md->maxh; ++i) {
             hits[nh].t = X->pos[i]; hits[nh].q = q; hits[nh].diag = (int64_t)X->pos[i] - q;
             ++nh;
         }
     }
     if (nh == 0) return;
     qsort(hits, nh, sizeof(hit_t), cmp_hit);
-    clump_t *cl = (clump_t *)malloc(sizeof(clump_t) * MAXCL);
+    clump_t *cl = M->cl;
     int ncl = 0;
-    for (int i = 0; i < nh && ncl < MAXCL;) {
-        int j = i, bq = i;
+    for (int64_t i = 0; i < nh && ncl < md->maxcl;) {
+        int64_t j = i, bq = i;
         while (j + 1 < nh && hits[j + 1].diag - hits[j].diag <= bp->max_gap + 2) {
             ++j;
             if (hits[j].q < hits[bq].q || (hits[j].q == hits[bq].q && hits[j].t < hits[bq].t)) bq = j;
         }
         if (j - i + 1 >= bp->min_match) {
-            cl[ncl].cnt = j - i + 1; cl[ncl].q = hits[bq].q; cl[ncl].t = hits[bq].t; cl[ncl].diag = hits[bq].diag;
+            cl[ncl].cnt = (int32_t)(j - i + 1); cl[ncl].q = hits[bq].q; cl[ncl].t = hits[bq].t;
+            cl[ncl].diag = hits[bq].diag;
             ++ncl;
         }
         i = j + 1;
     }
-    if (ncl == MAXCL) cap[1] = 1;
+    if (ncl == md->maxcl) cap[1] = 1;
     qsort(cl, ncl, sizeof(clump_t), cmp_clump);  /* (hits desc, diagonal): keys are unique */
     int nr = 0, c = 0;
-    for (; c < ncl && nr < MAXP; ++c) {
+    for (; c < ncl && nr < md->maxcl; ++c) {
         int32_t q = cl[c].q;
         int64_t t = cl[c].t;
         int skip = 0;
         for (int r = 0; r < nr; ++r)
             if (regs[r].qb <= q && q + TILE <= regs[r].qe && regs[r].tb <= t && t + TILE <= regs[r].te) { skip = 1; break; }
         if (skip) continue;
-        if (align_clump(X, Q, L, q, t, &regs[nr])) ++nr;
+        if (align_clump(X, Q, L, q, t, &regs[nr], md, &M->ar, M->qs, M->ts, M->cig)) ++nr;
     }
-    if (nr == MAXP && c < ncl) cap[2] = 1;
-    free(cl);
+    if (nr == md->maxcl && c < ncl) cap[2] = 1;
     if (nr == 0) return;
     /* regions in (qb, tb, qe) order for the chain DP (stable: ties keep their creation order) */
-    int *ord = (int *)malloc(sizeof(int) * 5 * nr);
+    int *ord = M->ord;
     int *best = ord + nr, *prev = best + nr, *fl = prev + nr, *chain = fl + nr;
     for (int i = 0; i < nr; ++i) ord[i] = i;
     for (int i = 1; i < nr; ++i)
@@ -363,7 +439,7 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
      * are recomputed -- the others' values cannot change, as removing parts only lowers scores
      * (g_blat_literal = 1 recomputes every part each round, the plain statement of the rule). */
     int64_t work = 0;  /* the recomputations' candidates (the first pass is always made) */
-    for (int i = 0; i < nr; ++i) chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
+    for (int i = 0; i < nr; ++i) chain_node(X, bp, Q, regs, ord, best, prev, fl, i, M->pre);
     for (;;) {
         if (work > STITCH_WORK && !g_blat_literal) { cap[2] = 1; break; }
         int bi = -1;
@@ -376,6 +452,7 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         memset(&o, 0, sizeof(o));
         o.query = qi; o.strand = strand; o.q_size = L;
         int ok = 1;
+        const int64_t rb0 = sink->rblk.n;
         reg_b pp, first, last, cur;
         memset(&first, 0, sizeof first); memset(&last, 0, sizeof last); memset(&pp, 0, sizeof pp);
         for (int k = m - 1; k >= 0; --k) {
@@ -389,10 +466,15 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
             }
             o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
             o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi; o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
-            for (int b = 0; b < cur.nb; ++b) {
-                if (o.block_count >= AFO_PSL_MAX_BLOCKS) { ok = 0; break; }
-                o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
-                o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
+            for (int b = 0; b < cur.nb && ok; ++b) {
+                const blk_t bk = blk_of(&M->ar, &cur, b);
+                if (md->row_blocks && o.block_count >= md->row_blocks) { ok = 0; break; }
+                if (o.block_count < AFO_PSL_MAX_BLOCKS) {
+                    o.block_sizes[o.block_count] = bk.sz; o.q_starts[o.block_count] = bk.q;
+                    o.t_starts[o.block_count] = bk.t;
+                }
+                if (!md->row_blocks) arena_push(&sink->rblk, bk.sz, bk.q, bk.t);
+                ++o.block_count;
             }
             if (k == m - 1) first = cur;
             if (k == 0) last = cur;
@@ -403,23 +485,36 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         o.t_start = first.tb; o.t_end = last.te;
         o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
         if (ok && o.score >= bp->min_score && psl_millibad(&o) <= (100 - bp->min_identity) * 10) {
-            /* the strand's best cap_out rows in cmp_psl order, stable; every row counted */
-            int n = *n_out < cap_out ? *n_out : cap_out, at = n;
-            while (at > 0 && cmp_psl(&o, &out[at - 1]) < 0) --at;
-            if (at < cap_out) {
-                for (int x = n < cap_out ? n : cap_out - 1; x > at; --x) out[x] = out[x - 1];
-                out[at] = o;
+            if (sink->out) {
+                /* the strand's best cap_out rows in cmp_psl order, stable; every row counted */
+                int n = *sink->n_out < sink->cap_out ? *sink->n_out : sink->cap_out, at = n;
+                while (at > 0 && cmp_psl(&o, &sink->out[at - 1]) < 0) --at;
+                if (at < sink->cap_out) {
+                    for (int x = n < sink->cap_out ? n : sink->cap_out - 1; x > at; --x) sink->out[x] = sink->out[x - 1];
+                    sink->out[at] = o;
+                }
+                ++*sink->n_out;
+            } else {
+                if (sink->n_rows == sink->cap_rows) {
+                    sink->cap_rows = sink->cap_rows ? 2 * sink->cap_rows : 64;
+                    sink->rows = (long_row *)realloc(sink->rows, sizeof(long_row) * sink->cap_rows);
+                }
+                sink->rows[sink->n_rows].h = o;
+                sink->rows[sink->n_rows].boff = rb0;
+                sink->rows[sink->n_rows].seq = sink->emitted[strand]++;
+                ++sink->n_rows;
             }
-            ++*n_out;
+        } else if (!sink->out) {
+            sink->rblk.n = rb0;  /* the row's blocks, not kept */
         }
         if (g_blat_literal) {
             for (int i = 0; i < nr; ++i)
-                if (!fl[i]) chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
+                if (!fl[i]) chain_node(X, bp, Q, regs, ord, best, prev, fl, i, M->pre);
         } else {
             for (int i = chain[m - 1] + 1; i < nr; ++i) {
                 if (fl[i] & 1) continue;
                 if (prev[i] >= 0 && fl[prev[i]]) {
-                    chain_node(X, bp, Q, regs, ord, best, prev, fl, i);
+                    chain_node(X, bp, Q, regs, ord, best, prev, fl, i, M->pre);
                     work += i;
                     fl[i] = 2;
                 }
@@ -427,7 +522,6 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
             for (int i = 0; i < nr; ++i) fl[i] &= 1;
         }
     }
-    free(ord);
 }
 
 static int cmp_psl(const void *a, const void *b) {
@@ -450,53 +544,115 @@ int afo_blat_caps(const afo_tiles *X, const uint8_t *queries, int64_t n_queries,
                   int32_t *caps) {
     /* max_rows up to MAXP: every row of a query (the GPU's kept rows + its spill pool, tests) */
     if (!X || max_rows < 1 || max_rows > MAXP || bp->step_size != X->step) return -1;
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads > 0 ? threads : 1)
-    for (int64_t qi = 0; qi < n_queries; ++qi) {
-        int L = lens ? lens[qi] : stride;
-        if (L > stride) L = stride;
-        if (L > AFO_MAX_READ) L = AFO_MAX_READ;
-        if (L < 0) L = 0;
-        uint8_t Q[2][AFO_MAX_READ];
-        for (int i = 0; i < L; ++i) {
-            uint8_t c = afo_nt4(queries[qi * stride + i]);
-            Q[0][i] = c;
-            Q[1][L - 1 - i] = c > 3 ? 4 : 3 - c;
-        }
-        hit_t *hits = (hit_t *)malloc(sizeof(hit_t) * MAXH);
-        reg_b *regs = (reg_b *)malloc(sizeof(reg_b) * MAXP);
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+    {
+        strand_mem M;
+        strand_mem_init(&M, &MODE_SHORT, AFO_MAX_READ);
         afo_psl *cand[2];
         cand[0] = (afo_psl *)malloc(sizeof(afo_psl) * 2 * (size_t)max_rows);
         cand[1] = cand[0] + max_rows;
-        int nc[2] = {0, 0};
-        int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
-        for (int s = 0; s < 2; ++s) {
-            memset(regs, 0, sizeof(reg_b) * MAXP);
-            blat_strand(X, bp, Q[s], L, s, (int32_t)qi, cand[s], &nc[s], max_rows, hits, regs, cap[s]);
-        }
-        if (caps) {
-            for (int s = 0; s < 2; ++s)
-                for (int k = 0; k < 3; ++k)
-                    if (cap[s][k]) {
-#pragma omp atomic
-                        caps[k] += 1;
-                    }
-            if (nc[0] + nc[1] > max_rows) {
-#pragma omp atomic
-                caps[3] += 1;
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t qi = 0; qi < n_queries; ++qi) {
+            int L = lens ? lens[qi] : stride;
+            if (L > stride) L = stride;
+            if (L > AFO_MAX_READ) L = AFO_MAX_READ;
+            if (L < 0) L = 0;
+            uint8_t Q[2][AFO_MAX_READ];
+            for (int i = 0; i < L; ++i) {
+                uint8_t c = afo_nt4(queries[qi * stride + i]);
+                Q[0][i] = c;
+                Q[1][L - 1 - i] = c > 3 ? 4 : 3 - c;
             }
+            int nc[2] = {0, 0};
+            int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
+            for (int s = 0; s < 2; ++s) {
+                row_sink sink;
+                memset(&sink, 0, sizeof sink);
+                sink.out = cand[s]; sink.n_out = &nc[s]; sink.cap_out = max_rows;
+                blat_strand(X, bp, Q[s], L, s, (int32_t)qi, &MODE_SHORT, &sink, &M, cap[s]);
+            }
+            if (caps) {
+                for (int s = 0; s < 2; ++s)
+                    for (int k = 0; k < 3; ++k)
+                        if (cap[s][k]) {
+#pragma omp atomic
+                            caps[k] += 1;
+                        }
+                if (nc[0] + nc[1] > max_rows) {
+#pragma omp atomic
+                    caps[3] += 1;
+                }
+            }
+            /* the two strands' sorted lists merged (strand 0 first on equal keys: cmp_psl orders by
+             * strand, so never) */
+            int na = nc[0] < max_rows ? nc[0] : max_rows, nb = nc[1] < max_rows ? nc[1] : max_rows;
+            int i = 0, j = 0, k = 0;
+            for (; k < max_rows && (i < na || j < nb); ++k) {
+                int take_b = j < nb && (i >= na || cmp_psl(&cand[1][j], &cand[0][i]) < 0);
+                rows[qi * max_rows + k] = take_b ? cand[1][j++] : cand[0][i++];
+            }
+            n_rows[qi] = k;
         }
-        free(hits);
-        free(regs);
-        /* the two strands' sorted lists merged (strand 0 first on equal keys: cmp_psl orders by
-         * strand, so never) */
-        int na = nc[0] < max_rows ? nc[0] : max_rows, nb = nc[1] < max_rows ? nc[1] : max_rows;
-        int i = 0, j = 0, k = 0;
-        for (; k < max_rows && (i < na || j < nb); ++k) {
-            int take_b = j < nb && (i >= na || cmp_psl(&cand[1][j], &cand[0][i]) < 0);
-            rows[qi * max_rows + k] = take_b ? cand[1][j++] : cand[0][i++];
-        }
-        n_rows[qi] = k;
         free(cand[0]);
+        strand_mem_free(&M);
     }
     return 0;
+}
+
+/* cmp_psl, then the strand's emission order (a total order: the sort's result is unique) */
+static int cmp_long_row(const void *a, const void *b) {
+    const long_row *x = (const long_row *)a, *y = (const long_row *)b;
+    const int c = cmp_psl(&x->h, &y->h);
+    return c ? c : x->seq - y->seq;
+}
+
+int afo_blat_long(const afo_tiles *X, const uint8_t *query, int32_t len, const afo_blat_params *bp, int32_t max_rows,
+                  afo_psl *rows, int32_t *n_rows, afo_psl_block *blocks, int64_t block_cap, int64_t *block_off,
+                  int64_t *n_blocks, int32_t *caps) {
+    if (!X || len < 0 || len > AFO_BLAT_LONG_MAX || max_rows < 0 || bp->step_size != X->step) return -1;
+    const int L = len;
+    uint8_t *Q[2];
+    Q[0] = (uint8_t *)malloc((size_t)L + 1);
+    Q[1] = (uint8_t *)malloc((size_t)L + 1);
+    for (int i = 0; i < L; ++i) {
+        uint8_t c = afo_nt4(query[i]);
+        Q[0][i] = c;
+        Q[1][L - 1 - i] = c > 3 ? 4 : 3 - c;
+    }
+    strand_mem M;
+    strand_mem_init(&M, &MODE_LONG, L);
+    row_sink sink;
+    memset(&sink, 0, sizeof sink);
+    int cap[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    for (int s = 0; s < 2; ++s) blat_strand(X, bp, Q[s], L, s, 0, &MODE_LONG, &sink, &M, cap[s]);
+    strand_mem_free(&M);
+    free(Q[0]); free(Q[1]);
+    if (caps)
+        for (int s = 0; s < 2; ++s)
+            for (int k = 0; k < 3; ++k) caps[k] += cap[s][k];
+    /* every row of both strands, best first (strand 0's rows before strand 1's: cmp_psl's order) */
+    qsort(sink.rows, sink.n_rows, sizeof(long_row), cmp_long_row);
+    const int64_t m = sink.n_rows < max_rows ? sink.n_rows : max_rows;
+    int64_t nb = 0;
+    for (int64_t k = 0; k < m; ++k) nb += sink.rows[k].h.block_count;
+    *n_rows = (int32_t)sink.n_rows;
+    *n_blocks = nb;
+    int rc = 0;
+    if (nb > block_cap) {
+        rc = -3;
+    } else {
+        int64_t off = 0;
+        for (int64_t k = 0; k < m; ++k) {
+            rows[k] = sink.rows[k].h;
+            block_off[k] = off;
+            for (int b = 0; b < sink.rows[k].h.block_count; ++b, ++off) {
+                const blk_t bk = sink.rblk.b[sink.rows[k].boff + b];
+                blocks[off].size = bk.sz; blocks[off].q_start = bk.q; blocks[off].t_start = bk.t;
+            }
+        }
+        block_off[m] = off;
+    }
+    free(sink.rows);
+    free(sink.rblk.b);
+    return rc;
 }

@@ -1,8 +1,8 @@
-# Round-4 configs[2] profile set (TAG names the output dir): a rocprofv3 kernel trace of the bench
+# configs[2] profile set (TAG names the output dir): a rocprofv3 kernel trace of the bench
 # step, then counter passes (each in a run of its own) on the genome calls and BLAT:
 # SQ occupancy / issue / wait counters, then FETCH_SIZE.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${TAG:-r04p}; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/${TAG:-prof}; mkdir -p $O
 export TMPDIR=/tmp
 K=${KREGEX:-k_g_|k_blat|k_s5_check|k_seed_stream|k_s2_}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu > $O/kt.log 2>&1 && \

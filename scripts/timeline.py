@@ -1,4 +1,4 @@
-"""Timeline of the last bench step from a rocprofv3 kernel trace (profile_r04.sh's kt/ directory):
+"""Timeline of the last bench step from a rocprofv3 kernel trace (profile_step.sh's kt/ directory):
 per kernel name, the first start and last end relative to the step's start (the last trace
 timestamp minus the step time), launches, and the summed busy time; the window's kernels sorted by
 start.

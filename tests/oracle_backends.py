@@ -37,6 +37,12 @@ class OracleTileReference:
         extra = {k: list(rows[k, MAX_ROWS:int(c)]) for k, c in enumerate(nr) if c > MAX_ROWS}
         return rows[:, :MAX_ROWS].copy(), np.minimum(nr, MAX_ROWS).astype(np.int32), extra
 
+    def search_long(self, seq, p, max_rows=4096):
+        """TileReference.search_long's contract on the oracle (afo_blat_long)."""
+        op = oracle.blat_params(**{f: getattr(p, f) for f, _ in p._fields_})
+        b = seq.encode() if isinstance(seq, str) else bytes(seq)
+        return self.tiles.blat_long(b, op, max_rows)
+
     def caps(self, reset=True):
         from anchored_fusion_amd.blat import CAP_NAMES
         return dict(zip(CAP_NAMES, (int(v) for v in self.tiles.caps_read(reset))))

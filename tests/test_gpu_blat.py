@@ -114,6 +114,49 @@ def test_blat_caps_match_oracle():
         g.close()
 
 
+def test_blat_query_caps_sum_to_context_caps():
+    """af_blat_query_caps: with per-query counters registered, a device search counts every cap
+    event per query and none on the context; the per-query counts sum to the context's counts of
+    the same search made without them (caps_world, one row slot per query: hits, clumps and rows
+    bind)."""
+    import torch
+
+    from anchored_fusion_amd import blat
+    from anchored_fusion_amd.place import pack_queries
+    from test_blat_caps import caps_world
+    ctgs, qs = caps_world()
+    p = blat.params("homologs")
+    g = _gpu_ref(ctgs, p.step_size)
+    dev = torch.device("cuda:0")
+    buf, lens = pack_queries(qs)
+    n = len(qs)
+    qt, lt = torch.from_numpy(buf).to(dev), torch.from_numpy(lens).to(dev)
+    nq = torch.tensor([n], dtype=torch.int32, device=dev)
+    try:
+        per = []
+        for registered in (False, True):
+            rows = torch.zeros(n * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            nr = torch.zeros(n, dtype=torch.int32, device=dev)
+            qc = torch.zeros(4 * n, dtype=torch.int32, device=dev)
+            g.caps(reset=True)
+            if registered:
+                g.query_caps_to(qc, n)
+            try:
+                g.search_device(qt, nq, buf.shape[1], rows, nr, lens_t=lt, p=p, max_rows=1,
+                                stream=torch.cuda.current_stream())
+            finally:
+                g.query_caps_to()
+            torch.cuda.synchronize()
+            per.append((g.caps(reset=True), qc.view(4, n).cpu().numpy(), nr.cpu().numpy()))
+        (ctx0, _, nr0), (ctx1, qc1, nr1) = per
+        assert np.array_equal(nr0, nr1)
+        assert all(v == 0 for v in ctx1.values()), ctx1
+        assert dict(zip(blat.CAP_NAMES, (int(v) for v in qc1.sum(axis=1)))) == ctx0
+        assert ctx0["hits"] > 0 and ctx0["rows"] > 0 and (qc1 > 0).any(axis=0).sum() < n
+    finally:
+        g.close()
+
+
 def test_blat_many_parts_equal_oracle():
     """A repeat family of 60 diverged copies and split halves (tests/test_blat_caps.py
     family_world): dozens of parts per query strand, chains across a 2 kb gap, the row cap bound --
@@ -129,8 +172,10 @@ def test_blat_many_parts_equal_oracle():
     try:
         for max_rows in (16, 3):
             rg, ng = g.search(qs, p, max_rows)
+            hs = g.heavy_stats()
+            assert hs["aligned"] == hs["jobs"] and hs["chained"] == hs["deferred"], hs
             ro, no = o.search(qs, p, max_rows)
-            assert np.array_equal(ng, no), (max_rows, ng, no)
+            assert np.array_equal(ng, no), (max_rows, ng, no, hs)
             for q in range(len(qs)):
                 assert rg[q, :ng[q]].tobytes() == ro[q, :no[q]].tobytes(), (max_rows, q)
             cg, co = g.caps(), o.caps()
@@ -296,5 +341,85 @@ def test_blat_spill_rows_equal_oracle_all_rows():
             assert len(got) == no[q], (q, len(got), no[q])
             for k, r in enumerate(got):
                 assert r.tobytes() == ro[q, k].tobytes(), (q, k)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("heavy", ["1", "0"])
+def test_blat_heavy_jobs_equal_oracle(monkeypatch, heavy):
+    """A strand with more than AF_BLAT_HEAVY_CLUMPS clumps is deferred (its clumps aligned as
+    grid-wide jobs by k_blat_jobs, its chains by k_blat_heavy): with every multi-clump strand
+    deferred (1) and with none (0), the device search equals the oracle -- rows, spilled rows, caps
+    (family_world: dozens of parts per strand; _world: the parity queries)."""
+    import torch
+
+    from anchored_fusion_amd import blat
+    from test_blat_caps import family_world
+    monkeypatch.setenv("AF_BLAT_HEAVY_CLUMPS", heavy)
+    for ctgs, qs, preset in ((family_world()[0], family_world()[1], "split_tail"),
+                             (_world(11)[0], _queries(*_world(11), 3, n=60), "anchored_split")):
+        p = blat.params(preset)
+        g = _gpu_ref(ctgs, p.step_size)
+        o = OracleTileReference(ctgs, p.step_size)
+        try:
+            rg, ng, eg = g.search_all(qs, p, spill_cap=1 << 17)
+            ro, no = o.search(qs, p, 4096)  # every row of a query
+            assert (no < 4096).all()
+            assert np.array_equal(no, ng + np.array([len(eg.get(i, [])) for i in range(len(qs))]))
+            for i in range(len(qs)):
+                mine = [r.tobytes() for r in rg[i, :min(int(ng[i]), blat.MAX_ROWS)]] + \
+                       sorted(r.tobytes() for r in eg.get(i, []))
+                theirs = [r.tobytes() for r in ro[i, :min(int(ng[i]), blat.MAX_ROWS)]] + \
+                         sorted(r.tobytes() for r in ro[i, blat.MAX_ROWS:no[i]])
+                assert mine == theirs, (preset, i)
+            cg, co = g.caps(), o.caps()
+            assert cg["hits"] == co["hits"] and cg["clumps"] == co["clumps"] and cg["parts"] == co["parts"]
+        finally:
+            g.close()
+        torch.cuda.synchronize()
+
+
+def test_blat_begin_end_live_mask():
+    """af_blat_device_begin / _end with a live mask (the S6 search beside S5): the live queries'
+    rows equal a whole search's, the others get none -- heavy strands included (every strand with
+    more than one clump deferred)."""
+    import os
+
+    import torch
+
+    from anchored_fusion_amd import blat
+    from anchored_fusion_amd.place import pack_queries
+    from test_blat_caps import family_world
+    os.environ["AF_BLAT_HEAVY_CLUMPS"] = "1"
+    try:
+        ctgs, qs = family_world()
+        p = blat.params("split_tail")
+        g = _gpu_ref(ctgs, p.step_size)
+    finally:
+        del os.environ["AF_BLAT_HEAVY_CLUMPS"]
+    dev = torch.device("cuda:0")
+    buf, lens = pack_queries(qs)
+    n = len(qs)
+    qt, lt = torch.from_numpy(buf).to(dev), torch.from_numpy(lens).to(dev)
+    nq = torch.tensor([n], dtype=torch.int32, device=dev)
+    live = torch.from_numpy((np.arange(n) % 3 != 1).astype(np.uint8)).to(dev)
+    try:
+        rows_a = torch.zeros(n * blat.MAX_ROWS * blat.PSL_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        nr_a = torch.zeros(n, dtype=torch.int32, device=dev)
+        g.search_device(qt, nq, buf.shape[1], rows_a, nr_a, lens_t=lt, p=p, stream=torch.cuda.current_stream())
+        rows_b = torch.zeros_like(rows_a)
+        nr_b = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        g.search_device_begin(qt, nq, buf.shape[1], rows_b, nr_b, lens_t=lt, p=p, stream=torch.cuda.current_stream())
+        g.search_device_end(live, stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        ra = rows_a.cpu().numpy().view(blat.PSL_DTYPE).reshape(n, blat.MAX_ROWS)
+        rb = rows_b.cpu().numpy().view(blat.PSL_DTYPE).reshape(n, blat.MAX_ROWS)
+        na, nb, lv = nr_a.cpu().numpy(), nr_b.cpu().numpy(), live.cpu().numpy()
+        assert na[lv == 1].sum() > 0
+        for i in range(n):
+            if lv[i]:
+                assert nb[i] == na[i] and ra[i, :na[i]].tobytes() == rb[i, :nb[i]].tobytes(), i
+            else:
+                assert nb[i] == 0, i
     finally:
         g.close()

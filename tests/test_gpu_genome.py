@@ -169,6 +169,7 @@ def test_pe_se_one_launch_equals_oracle(world):
     recs = torch.zeros(n * MAX_REC * REC_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     nrec = torch.zeros(n, dtype=torch.int32, device=dev)
     s_a, s_b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s_a.wait_stream(torch.cuda.current_stream(dev))  # the zeroed recs / nrec and the uploads come first
     gg.align_pe_se_device(rt, pairs.shape[0] // 2, se.shape[0], L, lt, recs, nrec,
                           pe_s4=_lib.default_pe(chunk_bases=150_000, pair_base=2), pe_s5=_lib.default_pe(),
                           se_id_base=11, stream=s_a, stream_pe=s_b)

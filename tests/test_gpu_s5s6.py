@@ -136,3 +136,93 @@ def test_s5_check_and_s6_rows_equal_host():
     finally:
         gi.close()
         al.close()
+
+
+def test_s6_before_check_then_compact_equals_sequential():
+    """af_s6_queries_device + af_blat_device_begin + af_s6_check_device + af_blat_device_end +
+    af_s6_compact_device (S6 searched beside S5, discover.run) equals af_s5_filter_device + BLAT of
+    its survivors byte for byte: the S6 rows, their S5 query
+    index, the PSL rows (query field renumbered) and row counts, the spilled rows (max_rows 16:
+    repeat-derived queries pass it), the clipped-row count and the cap counters."""
+    import torch
+
+    from anchored_fusion_amd import _lib, blat, genome
+    from anchored_fusion_amd.align import AnchorAligner
+    from anchored_fusion_amd.discover import CandidateDiscovery
+    contigs, anchor, reads = _world(n_pairs=2000, seed=37)
+    N, L = reads.shape[0] // 2, reads.shape[1]
+    dev = torch.device("cuda:0")
+    al = AnchorAligner(anchor, device=0)
+    gi = genome.GenomeIndex(contigs, device=0)
+    tiles = blat.TileReference([(n, s.decode()) for n, s in contigs], blat.TILE)
+    try:
+        reads_t = torch.from_numpy(reads).to(dev)
+        z = lambda *sh, dt=torch.int32: torch.zeros(sh, dtype=dt, device=dev)  # noqa: E731
+        out = {k: z(2 * N) for k in ("flag", "pos", "score", "n_cigar", "hits")}
+        out["cigar"] = z(2 * N, 32)
+        al.align_pairs_device(reads_t, N, L, out)
+        _, _, an, cnt = al.partition_device(out["flag"], out["pos"])
+        na = int(cnt.cpu()[2])
+        cap = 2 * N
+        q, q_lens, q_rows, n_q = z(cap, L, dt=torch.uint8), z(cap), z(cap), z(1)
+        al.gather_reads_device(reads_t, L, an, na, _lib.AF_GATHER_SPLIT_SAM, q, q_lens, q_rows, n_q, out_t=out)
+        torch.cuda.synchronize()
+        n5 = int(n_q.item())
+        recs = z(cap * genome.MAX_REC * genome.REC_DTYPE.itemsize // 4)
+        nrec = z(cap)
+        gi.align_se_device(q, n5, L, recs, nrec, lens_t=q_lens)
+        torch.cuda.synchronize()
+        p = blat.params("split_tail")
+        psl = blat.PSL_DTYPE.itemsize
+        # sequential: the check, then BLAT of its survivors
+        s6, s6_lens, s6_src, n6, n_over = z(cap, _lib.AF_MAX_READ, dt=torch.uint8), z(cap), z(cap), z(1), z(1)
+        genome.s5_filter_device(gi.ctx, recs, nrec, n5, q, L, q_lens, q_rows, out, cap, s6, s6_lens, s6_src, n6,
+                                n_over_t=n_over)
+        rows_a, nr_a = z(cap * blat.MAX_ROWS * psl, dt=torch.uint8), z(cap)
+        nsp = 1 << 18  # both spill pools hold every row (a full pool drops rows in atomic order)
+        sp_a = dict(rows=z(nsp * psl, dt=torch.uint8), q=z(nsp), n=z(1))
+        tiles.caps(reset=True)
+        tiles.spill_to(sp_a["rows"], sp_a["q"], sp_a["n"])
+        try:
+            tiles.search_device(s6, n6, _lib.AF_MAX_READ, rows_a, nr_a, lens_t=s6_lens, p=p)
+        finally:
+            tiles.spill_to()
+        torch.cuda.synchronize()
+        caps_a = tiles.caps(reset=True)
+        # split: the leaders' rows, BLAT, the check + compaction (CandidateDiscovery's buffers)
+        d = CandidateDiscovery.__new__(CandidateDiscovery)
+        d.dev, d.tiles_ref, d.p_tail, d.L, d.s6cap, d.spill_min = dev, tiles, p, L, 0, nsp
+        d.q, d.q_lens, d.q_rows, d.out, d.q_nh = q, q_lens, q_rows, out, nrec
+        d._alloc_s6(64)  # grown by _s6_pre
+        d._s6_pre(0, n5, torch.cuda.current_stream())
+        d._s6_search(torch.cuda.current_stream())
+        d._s6_check(0, n5, recs, torch.cuda.current_stream())
+        d._s6_finish(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        caps_b = tiles.caps(reset=True)
+        k6 = int(n6.item())
+        assert int(d.s6["n"].item()) == k6 and 20 < k6 < int(d.s6p["n"].item()) <= n5
+        assert torch.equal(d.s6["lens"][:k6], s6_lens[:k6]) and torch.equal(d.s6["src"][:k6], s6_src[:k6])
+        for k in range(k6):
+            ln = int(s6_lens[k])
+            assert torch.equal(d.s6["q"][k, :ln], s6[k, :ln]), k
+        assert torch.equal(d.t_nh[:k6], nr_a[:k6])
+        ra = rows_a.cpu().numpy().view(blat.PSL_DTYPE).reshape(cap, blat.MAX_ROWS)
+        rb = d.t_rows.cpu().numpy().view(blat.PSL_DTYPE).reshape(-1, blat.MAX_ROWS)
+        nh = nr_a[:k6].cpu().numpy()
+        for k in range(k6):
+            m = min(int(nh[k]), blat.MAX_ROWS)
+            assert ra[k, :m].tobytes() == rb[k, :m].tobytes(), k
+        assert nh.sum() > 0
+        ns_a, ns_b = int(sp_a["n"].item()), int(d.t_spill["n"].item())
+        assert ns_a == ns_b and 0 < ns_a <= nsp
+        ea = blat.spilled_rows(sp_a["rows"][:ns_a * psl].cpu().numpy().view(blat.PSL_DTYPE), sp_a["q"][:ns_a].cpu().numpy())
+        eb = blat.spilled_rows(d.t_spill["rows"][:ns_b * psl].cpu().numpy().view(blat.PSL_DTYPE),
+                               d.t_spill["q"][:ns_b].cpu().numpy())
+        assert {k: sorted(r.tobytes() for r in v) for k, v in ea.items()} == {k: sorted(r.tobytes() for r in v) for k, v in eb.items()}
+        assert int(d.s6["over"].item()) == int(n_over.item())
+        assert caps_a == caps_b
+    finally:
+        tiles.close()
+        gi.close()
+        al.close()
