@@ -19,6 +19,9 @@
 #ifndef AF_G1_HEAVY_EXT
 #define AF_G1_HEAVY_EXT 2048    // G1: a read past this many FM extensions moves to the wave-per-read kernel (env AF_G1_HEAVY_EXT)
 #endif
+#ifndef AF_G_PE_SPEC_WINDOWS
+#define AF_G_PE_SPEC_WINDOWS 4  // S4: pairs with this many rescue windows run their SWs as grid jobs (env AF_G_PE_SPEC_WINDOWS)
+#endif
 #ifndef AF_G_HEAVY_CHAINS
 #define AF_G_HEAVY_CHAINS 16    // G2: reads with this many kept chains extend them one job per chain (env AF_G_HEAVY_CHAINS)
 #endif
@@ -235,6 +238,20 @@ struct GHeavy {
     int64_t cap_reads, cap_ch, cap_sd;
     int32_t min_chains;               // 0: every read extended by its own wave
 };
+// S4's heavy pairs (at least min_windows mate-rescue windows, mem_matesw calls): their rescue
+// SWs (ksw_align2 per window and direction) run as grid-wide jobs (k_g_pe_jobs) before a wave per
+// pair finishes it with their results (k_g_pe, pass 2)
+constexpr int AF_G_PE_RES_W = 8;  // ints per (window, direction) result: sc te qe tb qb ran
+struct GPeSpec {
+    int32_t *pair;                    // [cap_pairs] the pair (-1: reservation failed)
+    int32_t *off;                     // [cap_pairs] its first window slot
+    int32_t *nj;                      // [cap_pairs] its windows per end: n0 | n1 << 16
+    int2 *job;                        // [cap_jobs] window slot -> {heavy pair, i << 16 | j} (y -1: none)
+    int32_t *res;                     // [cap_jobs * 4 * AF_G_PE_RES_W] results per slot and direction
+    unsigned long long *cnt;          // [0] heavy pairs, [1] slots, [2] job / [3] finish dequeue, [4] slots written below
+    int64_t cap_pairs = 0, cap_jobs = 0;
+    int32_t min_windows = 0;          // 0: every pair rescued by its own wave
+};
 // per-call pools and counters of the genome kernels (per context)
 struct GWork {
     GIv *iv;                    // intervals of every read (G1)
@@ -255,6 +272,7 @@ struct GWork {
     unsigned long long *g1_hv_n = nullptr, *g1_hv_next = nullptr;
     int32_t g1_max_ext = 0;
     GHeavy hv;
+    GPeSpec pe{};
     // G2's dequeue order: G1 lists the reads with at least g2_first_occ seeds (bwa's occurrences
     // per interval, at most max_occ, summed) in g2_list[0, *g2_list_n) and flags them; G2 takes
     // that list first, then the other reads in order (0 = read order)

@@ -83,6 +83,8 @@ struct af_ctx {
     // G2's heavy-read pools (GHeavy) and the kept-chain count from which a read is heavy
     GHeavy g_hv{};
     int32_t g_heavy_min = AF_G_HEAVY_CHAINS;
+    GPeSpec g_pe{};
+    int32_t g_pe_min = AF_G_PE_SPEC_WINDOWS;
     int32_t g1_max_ext = AF_G1_HEAVY_EXT;
     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
     int32_t g2_first_occ = AF_G2_FIRST_OCC;
@@ -490,6 +492,18 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     HIPCHK(c, hipMalloc(&h.sd, af_g_seed_bytes() * h.cap_sd));
     HIPCHK(c, hipMalloc(&h.res, sizeof(GReg) * h.cap_sd));
     if (!h.cnt) HIPCHK(c, hipMalloc(&h.cnt, 8 * sizeof(unsigned long long)));
+    // S4's heavy pairs: one in 16 pairs of the call, 16 window slots each on average (a pair that
+    // does not fit runs its rescues on its own wave)
+    GPeSpec &e = c->g_pe;
+    af_free(e.pair); af_free(e.off); af_free(e.nj); af_free(e.job); af_free(e.res);
+    e.pair = e.off = e.nj = e.res = nullptr; e.job = nullptr;
+    e.cap_pairs = std::max<int64_t>(cap / 32, 1024); e.cap_jobs = 16 * e.cap_pairs;
+    HIPCHK(c, hipMalloc(&e.pair, sizeof(int32_t) * e.cap_pairs));
+    HIPCHK(c, hipMalloc(&e.off, sizeof(int32_t) * e.cap_pairs));
+    HIPCHK(c, hipMalloc(&e.nj, sizeof(int32_t) * e.cap_pairs));
+    HIPCHK(c, hipMalloc(&e.job, sizeof(int2) * e.cap_jobs));
+    HIPCHK(c, hipMalloc(&e.res, sizeof(int32_t) * 4 * AF_G_PE_RES_W * e.cap_jobs));
+    if (!e.cnt) HIPCHK(c, hipMalloc(&e.cnt, 8 * sizeof(unsigned long long)));
     af_free(c->g2_list); af_free(c->g2_flag);
     c->g2_list = nullptr; c->g2_flag = nullptr;
     HIPCHK(c, hipMalloc(&c->g2_list, sizeof(int32_t) * cap));
@@ -509,6 +523,8 @@ GWork genome_work(af_ctx *c) {
     w.g1_max_ext = c->g1_hv ? c->g1_max_ext : 0;
     w.hv = c->g_hv;
     w.hv.min_chains = c->g_hv.cnt ? c->g_heavy_min : 0;
+    w.pe = c->g_pe;
+    w.pe.min_windows = c->g_pe.cnt ? c->g_pe_min : 0;
     w.g2_list = c->g2_list; w.g2_flag = c->g2_flag; w.g2_list_n = c->g_iv_fill + 4; w.g2_list_next = c->g_iv_fill + 5;
     w.g2_first_occ = c->g2_flag ? c->g2_first_occ : 0;
     w.stats = c->g_stats;
@@ -619,6 +635,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_cu = std::max(1, cus);
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
+    if (const char *pw = getenv("AF_G_PE_SPEC_WINDOWS")) c->g_pe_min = std::max(0, atoi(pw));  // tests: 1 = every rescuing pair
     if (const char *hv = getenv("AF_BLAT_HEAVY_CLUMPS")) c->blat_heavy_min = std::max(0, atoi(hv));  // 0: none deferred
     if (const char *go = getenv("AF_G2_FIRST_OCC")) c->g2_first_occ = std::max(0, atoi(go));
     if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
@@ -648,6 +665,8 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g2_scr_pe); af_free(c->zscratch_pe);
     af_free(c->g_hv.read); af_free(c->g_hv.nch); af_free(c->g_hv.ch_off); af_free(c->g_hv.sd_off); af_free(c->g_hv.ch_read);
     af_free(c->g_hv.ch); af_free(c->g_hv.sd); af_free(c->g_hv.res); af_free(c->g_hv.cnt);
+    af_free(c->g_pe.pair); af_free(c->g_pe.off); af_free(c->g_pe.nj); af_free(c->g_pe.job); af_free(c->g_pe.res);
+    af_free(c->g_pe.cnt);
     af_free(c->g2_list); af_free(c->g2_flag);
     if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);

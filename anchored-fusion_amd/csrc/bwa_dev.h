@@ -95,6 +95,36 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
     }
 }
 
+// a[0, n) sorted on the wave by rank when the comparator orders every pair strictly (no two items
+// equivalent): every correct sort, klib's introsort included, then gives this one order.  Each
+// lane ranks its items against all n (LDS broadcast reads); tmp: n items of scratch.  Returns
+// false, a unchanged, when some pair is equivalent (the caller runs the introsort for bwa's tie
+// order).  Wave-uniform call.
+template <class T, class LT>
+__device__ bool wave_rank_sort(T *a, int n, LT lt, T *tmp, int lane) {
+    bool tie = false;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        if (i < n) {
+            const T x = a[i];
+            int r = 0;
+            for (int j = 0; j < n; ++j) {
+                const T y = a[j];
+                if (lt(y, x)) ++r;
+                else if (j != i && !lt(x, y)) tie = true;
+            }
+            if (!tie) tmp[r] = x;
+        }
+    }
+    if (__ballot(tie)) return false;
+    __threadfence_block();
+    wave_sync();
+    for (int i = lane; i < n; i += 64) a[i] = tmp[i];
+    __threadfence_block();
+    wave_sync();
+    return true;
+}
+
 // utils.h hash_64
 __device__ __forceinline__ uint64_t hash_64(uint64_t key) {
     key += ~(key << 32);

@@ -1267,6 +1267,8 @@ __device__ int g_patch_reg(const DevGenome &G, const af_params &p, const GReg &a
 static_assert(AF_G_MAX_REG <= 1024 && AF_MAX_READ < 32768, "region keys pack a 10-bit index and a 15-bit qb");
 static_assert(sizeof(G2Box) * G2_BOXES >= 16 * AF_G_MAX_REG, "the boxes hold 16 B of key per region");
 static_assert(sizeof(GReg) == 64, "regions move as 4 x 16 B");
+// lists this long or longer are sorted on the wave by rank (wave_rank_sort), shorter by lane 0
+constexpr int G_RANK_MIN = 24;
 struct GKeyRe {  // re << 10 | index (mem_sort_dedup_patch's sort by re)
     __device__ bool operator()(uint64_t a, uint64_t b) const { return (a >> 10) < (b >> 10); }
 };
@@ -1316,8 +1318,10 @@ __device__ int g_dedup_patch(const DevGenome &G, const af_params &p, const GOpt 
     uint64_t *k1 = reinterpret_cast<uint64_t *>(g_box);
     for (int i = lane; i < n; i += 64) k1[i] = (uint64_t)a[i].re << 10 | (uint64_t)i;
     wave_sync();
-    if (lane == 0) ks_introsort(k1, n, GKeyRe());
-    wave_sync();
+    if (n < G_RANK_MIN || !wave_rank_sort(k1, n, GKeyRe(), reinterpret_cast<uint64_t *>(tmp), lane)) {
+        if (lane == 0) ks_introsort(k1, n, GKeyRe());
+        wave_sync();
+    }
     g_regs_gather(a, tmp, n, [&](int k) { return (int)(k1[k] & 1023); }, lane);
     for (int i0 = 1; i0 < n; i0 += 64) {
         // a[i] is walked unless it starts a new contig or lies past a[i-1] + max_chain_gap (reads of
@@ -1394,8 +1398,10 @@ __device__ int g_dedup_patch(const DevGenome &G, const af_params &p, const GOpt 
         m += __builtin_popcountll(lm);
     }
     wave_sync();
-    if (lane == 0) ks_introsort(k2, m, GKeyArs());
-    wave_sync();
+    if (m < G_RANK_MIN || !wave_rank_sort(k2, m, GKeyArs(), reinterpret_cast<GKey16 *>(tmp), lane)) {
+        if (lane == 0) ks_introsort(k2, m, GKeyArs());
+        wave_sync();
+    }
     // kept keys compacted in order: a kept key's z goes to slot mm + (kept before it) <= its own
     // slot, so the next chunk's first comparison (with this chunk's last key) still reads that
     // key's own z
@@ -1688,8 +1694,10 @@ __device__ void g_mark_primary_w(GReg *a, int n, int64_t id, GReg *tmp, int lane
         k[i] = GKey16{(int64_t)h, a[i].score, i};
     }
     wave_sync();
-    if (lane == 0) ks_introsort(k, n, GKeyHash());
-    wave_sync();
+    if (n < G_RANK_MIN || !wave_rank_sort(k, n, GKeyHash(), reinterpret_cast<GKey16 *>(tmp), lane)) {
+        if (lane == 0) ks_introsort(k, n, GKeyHash());
+        wave_sync();
+    }
     g_regs_gather(a, tmp, n, [&](int j) { return k[j].z; }, lane);
     int32_t *span = reinterpret_cast<int32_t *>(g_box);  // qb << 16 | qe
     int32_t *score = span + AF_G_MAX_REG, *sub = score + AF_G_MAX_REG, *z = sub + AF_G_MAX_REG;
@@ -1973,10 +1981,51 @@ __device__ void g_ksw_align2(const uint8_t *q, int qlen, const uint8_t *target, 
     if (r.score == rr.score) { tb = r.te - rr.te; qb = r.qe - rr.qe; }
 }
 
+// mem_matesw's window of direction r for the mate region a (the rescued read l_ms long): [rb, re)
+// clipped to one contig (rid); true when bwa runs its SW there
+__device__ __forceinline__ bool g_mate_window(const DevGenome &G, const af_params &p, const S2Pes &pe, int r,
+                                              const GReg &a, int l_ms, int64_t &rb, int64_t &re, int &rid) {
+    const int64_t l_pac = G.l_pac;
+    const bool is_rev = (r >> 1) != (r & 1);
+    const bool is_larger = !(r >> 1);
+    if (!is_rev) {
+        rb = is_larger ? a.rb + pe.low : a.rb - pe.high;
+        re = (is_larger ? a.rb + pe.high : a.rb - pe.low) + l_ms;
+    } else {
+        rb = (is_larger ? a.rb + pe.low : a.rb - pe.high) - l_ms;
+        re = is_larger ? a.rb + pe.high : a.rb - pe.low;
+    }
+    if (rb < 0) rb = 0;
+    if (re > l_pac << 1) re = l_pac << 1;
+    if (rb < re) g_fetch_clip(G, &rb, (rb + re) >> 1, &re, &rid);
+    // (rb >= re leaves rid from the previous direction, as bwa does; re - rb < min_seed_len then)
+    return a.rid == rid && re - rb >= p.min_seed_len;
+}
+
+// that window's ksw_align2 for the rescued read's codes qc (strand of direction r)
+__device__ __forceinline__ void g_mate_ksw(const DevGenome &G, const af_params &p, const uint8_t *qc, int l_ms, int r,
+                                           int64_t rb, int64_t re, int &sc, int &te, int &qe, int &tb, int &qb,
+                                           int lane) {
+    GPeLds &E = g_gpe;
+    const bool is_rev = (r >> 1) != (r & 1);
+    for (int x = lane; x < l_ms; x += 64) {
+        const int c = qc[is_rev ? l_ms - 1 - x : x];
+        E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
+    }
+    const bool staged = re - rb <= (int64_t)sizeof(E.tw);
+    if (staged)
+        for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = G.T[rb + x];
+    wave_sync();
+    const int P = l_ms * p.a < 250 ? 16 : 8;
+    g_ksw_align2(E.rq, l_ms, staged ? E.tw : G.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb, qb,
+                 lane);
+}
+
 // mem_matesw (oracle mem_matesw): rescue read mi (regions ma[0, *na)) in the insert-size window
-// of its mate's region a.  Returns false on a region-cap overflow.
+// of its mate's region a.  sr: the windows' SW results computed ahead (k_g_pe_jobs; 4 directions
+// x AF_G_PE_RES_W ints) or null.  Returns false on a region-cap overflow.
 __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, const G2Scr &S, int mi, GReg *ma,
-                         const GReg &a, uint8_t *zg, int lane) {
+                         const GReg &a, uint8_t *zg, const int32_t *sr, int lane) {
     GPeLds &E = g_gpe;
     const int64_t l_pac = G.l_pac;
     const int l_ms = E.len[mi];
@@ -1992,32 +2041,16 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
     for (int r = 0; r < 4; ++r) {
         if (skip[r]) continue;
         const bool is_rev = (r >> 1) != (r & 1);
-        const bool is_larger = !(r >> 1);
         int64_t rb, re;
-        if (!is_rev) {
-            rb = is_larger ? a.rb + E.pes[r].low : a.rb - E.pes[r].high;
-            re = (is_larger ? a.rb + E.pes[r].high : a.rb - E.pes[r].low) + l_ms;
-        } else {
-            rb = (is_larger ? a.rb + E.pes[r].low : a.rb - E.pes[r].high) - l_ms;
-            re = is_larger ? a.rb + E.pes[r].high : a.rb - E.pes[r].low;
-        }
-        if (rb < 0) rb = 0;
-        if (re > l_pac << 1) re = l_pac << 1;
-        if (rb < re) g_fetch_clip(G, &rb, (rb + re) >> 1, &re, &rid);
-        if (a.rid == rid && re - rb >= p.min_seed_len) {
-            for (int x = lane; x < l_ms; x += 64) {
-                const int c = E.q[mi][is_rev ? l_ms - 1 - x : x];
-                E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
-            }
-            const bool staged = re - rb <= (int64_t)sizeof(E.tw);
-            if (staged)
-                for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = G.T[rb + x];
-            wave_sync();
-            const int P = l_ms * p.a < 250 ? 16 : 8;
+        if (g_mate_window(G, p, E.pes[r], r, a, l_ms, rb, re, rid)) {
             int sc, te, qe, tb, qb;
-            GPROF(if (lane == 0) ++E.misc[5];)
-            g_ksw_align2(E.rq, l_ms, staged ? E.tw : G.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb,
-                         qb, lane);
+            const int32_t *q = sr ? sr + r * AF_G_PE_RES_W : nullptr;
+            if (q && q[5]) {
+                sc = q[0]; te = q[1]; qe = q[2]; tb = q[3]; qb = q[4];
+            } else {
+                GPROF(if (lane == 0) ++E.misc[5];)
+                g_mate_ksw(G, p, E.q[mi], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
+            }
             if (sc >= p.min_seed_len && qb >= 0) {
                 if (lane == 0) {
                     GReg b{};
@@ -2120,7 +2153,7 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
                                                 int64_t cap, af_params p, GOpt o, GWork w, S2Work sw,
                                                 uint8_t *__restrict__ scr_base, size_t scr_stride,
                                                 uint8_t *__restrict__ zscratch, size_t zstride,
-                                                af_grec *__restrict__ recs, int32_t *__restrict__ n_rec) {
+                                                af_grec *__restrict__ recs, int32_t *__restrict__ n_rec, int mode) {
     GPeLds &E = g_gpe;
     G3Lds &H = g_g3;
     const int lane = threadIdx.x;
@@ -2135,11 +2168,32 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
     static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "pool holds a region list");
     static_assert((size_t)AF_G_MAX_CHAIN * sizeof(GChain) >= 2 * (size_t)(AF_G_MAX_REG + 1) * sizeof(GReg), "ch holds 2 lists");
     static_assert((size_t)AF_G_MAX_OCC * sizeof(GSeed) >= 2 * (size_t)(AF_G_MAX_REG + 4) * sizeof(P64g), "seed holds v");
+    // mode 0: every pair; 1: every pair, those with at least w.pe.min_windows rescue windows left
+    // to k_g_pe_jobs (their SWs) and mode 2 (the rest, with those SWs' results)
+    const GPeSpec &X = w.pe;
+    int64_t nh = 0;
+    if (mode == 2) {
+        nh = (int64_t)X.cnt[0];
+        if (nh > X.cap_pairs) nh = X.cap_pairs;
+    }
     for (;;) {  // pairs dequeued one at a time (a pair with many rescue windows costs many others)
         int64_t pp = 0;
-        if (lane == 0) pp = (int64_t)atomicAdd(&w.hv.cnt[5], 1ull);
-        pp = (int64_t)__builtin_amdgcn_readfirstlane((int)pp);
-        if (pp >= n) break;
+        const int32_t *sres = nullptr;  // mode 2: the pair's precomputed SW results
+        int nj0 = 0;
+        if (mode == 2) {
+            int64_t hp = 0;
+            if (lane == 0) hp = (int64_t)atomicAdd(&X.cnt[3], 1ull);
+            hp = (int64_t)__builtin_amdgcn_readfirstlane((int)hp);
+            if (hp >= nh) break;
+            pp = X.pair[hp];
+            if (pp < 0) continue;  // reservation failed: mode 1 finished the pair
+            sres = X.res + (int64_t)X.off[hp] * 4 * AF_G_PE_RES_W;
+            nj0 = X.nj[hp] & 0xffff;
+        } else {
+            if (lane == 0) pp = (int64_t)atomicAdd(&w.hv.cnt[5], 1ull);
+            pp = (int64_t)__builtin_amdgcn_readfirstlane((int)pp);
+            if (pp >= n) break;
+        }
         GPROF(const uint64_t gp_c0 = clock64(); const uint32_t gp_t0 = gp_rt();
               if (lane == 0) { E.misc[5] = 0; E.misc[6] = 0; })
         for (int m = 0; m < 2; ++m) {
@@ -2164,11 +2218,46 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
             }
         }
         wave_sync();
+        if (mode == 1 && X.min_windows > 0) {
+            // a heavy pair's windows to the job list (slot k: end i, its j-th top hit); the
+            // pair is finished by mode 2
+            const int n0 = E.nb[0] < o.max_matesw ? E.nb[0] : o.max_matesw;
+            const int n1 = E.nb[1] < o.max_matesw ? E.nb[1] : o.max_matesw;
+            const int nwin = (E.ovf[1] ? 0 : n0) + (E.ovf[0] ? 0 : n1);
+            if (nwin >= X.min_windows) {
+                int hp = -1, off = 0;
+                if (lane == 0) {
+                    const int64_t h = (int64_t)atomicAdd(&X.cnt[0], 1ull);
+                    if (h < X.cap_pairs) {
+                        const int64_t o0 = (int64_t)atomicAdd(&X.cnt[1], (unsigned long long)(n0 + n1));
+                        if (o0 + n0 + n1 <= X.cap_jobs) {
+                            hp = (int)h; off = (int)o0;
+                            X.pair[h] = (int32_t)pp; X.off[h] = off; X.nj[h] = n0 | n1 << 16;
+                            atomicAdd(&w.stats[AF_GSTAT_PE_JOBS], 1);
+                        } else {
+                            X.pair[h] = -1;
+                            atomicMin(&X.cnt[4], (unsigned long long)o0);  // slots from o0 on are unwritten
+                        }
+                    }
+                }
+                hp = __builtin_amdgcn_readfirstlane(hp);
+                off = __builtin_amdgcn_readfirstlane(off);
+                if (hp >= 0) {
+                    for (int k = lane; k < n0 + n1; k += 64) {
+                        const int i = k >= n0, j = k - (i ? n0 : 0);
+                        X.job[off + k] = make_int2(hp, E.ovf[!i] ? -1 : (i << 16 | j));
+                    }
+                    wave_sync();
+                    continue;
+                }
+            }
+        }
         for (int i = 0; i < 2; ++i)
             for (int j = 0; j < E.nb[i] && j < o.max_matesw; ++j) {
                 if (E.ovf[!i]) continue;
                 const GReg bj = B[i * (AF_G_MAX_REG + 1) + j];
-                if (!g_matesw(G, p, o, S, !i, A[!i], bj, zg, lane)) {
+                const int32_t *sr = sres ? sres + (int64_t)((i ? nj0 : 0) + j) * 4 * AF_G_PE_RES_W : nullptr;
+                if (!g_matesw(G, p, o, S, !i, A[!i], bj, zg, sr, lane)) {
                     wave_sync();
                     if (lane == 0) { E.ovf[!i] = 1; E.na[!i] = 0; }
                     wave_sync();
@@ -2275,12 +2364,79 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
     }
 }
 
+// one rescue window of a heavy pair per wave (k_g_pe mode 1's job list): for each direction bwa
+// may search, the window and its ksw_align2 as mem_matesw computes them (results ahead of the
+// pair's own walk, which decides per window whether to use them)
+__global__ __launch_bounds__(64, 2) void k_g_pe_jobs(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+                                                     const int32_t *__restrict__ lens, af_params p, GOpt o, GWork w,
+                                                     S2Work sw) {
+    GPeLds &E = g_gpe;
+    const int lane = threadIdx.x;
+    const GPeSpec &X = w.pe;
+    int64_t n = (int64_t)X.cnt[1];
+    if (n > X.cap_jobs) n = X.cap_jobs;
+    if (n > (int64_t)X.cnt[4]) n = (int64_t)X.cnt[4];
+    for (;;) {
+        int64_t k = 0;
+        if (lane == 0) k = (int64_t)atomicAdd(&X.cnt[2], 1ull);
+        k = (int64_t)__builtin_amdgcn_readfirstlane((int)k);
+        if (k >= n) break;
+        const int2 jb = X.job[k];
+        if (jb.y < 0) continue;
+        const int i = jb.y >> 16, j = jb.y & 0xffff;
+        const int64_t pp = X.pair[jb.x];
+        int32_t *out = X.res + k * 4 * AF_G_PE_RES_W;
+        // the rescued read (the other end) and its codes
+        const int64_t rm = 2 * pp + !i;
+        const int l_ms = read_len(lens, rm, stride);
+        for (int x = lane; x < l_ms; x += 64) E.q[0][x] = nt4(reads[rm * (int64_t)stride + x]);
+        if (lane < 4) E.pes[lane] = sw.pes[(int64_t)g_chunk_of(sw, pp) * 4 + lane];
+        // bj: end i's j-th region scoring within pen_unpaired of its best (k_g_pe's copy list)
+        const GReg *ai = w.reg + w.reg_off[2 * pp + i];
+        const int na = w.reg_n[2 * pp + i] > 0 ? w.reg_n[2 * pp + i] : 0;
+        const int top = na ? ai[0].score : 0;
+        int seen = 0, at = -1;
+        for (int c0 = 0; c0 < na && at < 0; c0 += 64) {
+            const bool q = c0 + lane < na && ai[c0 + lane].score >= top - o.pen_unpaired;
+            const uint64_t m = __ballot(q);
+            const int cnt = __builtin_popcountll(m);
+            if (seen + cnt > j) {
+                uint64_t mm = m;
+                for (int t = 0; t < j - seen; ++t) mm &= mm - 1;
+                at = c0 + __builtin_ctzll(mm);
+            }
+            seen += cnt;
+        }
+        wave_sync();
+        if (at < 0) {  // (no such region: never used)
+            if (lane < 4) out[lane * AF_G_PE_RES_W + 5] = 0;
+            continue;
+        }
+        const GReg bj = ai[at];
+        int rid = -1;
+        for (int r = 0; r < 4; ++r) {
+            int64_t rb, re;
+            int ran = 0, sc = 0, te = 0, qe = 0, tb = 0, qb = 0;
+            if (!E.pes[r].failed && g_mate_window(G, p, E.pes[r], r, bj, l_ms, rb, re, rid)) {
+                g_mate_ksw(G, p, E.q[0], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
+                ran = 1;
+            }
+            if (lane == 0) {
+                int32_t *o_ = out + r * AF_G_PE_RES_W;
+                o_[0] = sc; o_[1] = te; o_[2] = qe; o_[3] = tb; o_[4] = qb; o_[5] = ran;
+            }
+            wave_sync();
+        }
+    }
+}
+
 __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t == 0) { *w.iv_fill = 0; *w.reg_fill = 0; *w.g1_next = 0; }
     if (t == 1 && w.g1_hv_n) { *w.g1_hv_n = 0; *w.g1_hv_next = 0; }
     if (t == 2 && w.g2_list_n) { *w.g2_list_n = 0; *w.g2_list_next = 0; }
     if (t < 7 && w.hv.cnt) w.hv.cnt[t] = 0;  // [5] k_g_pe's and [6] k_g_se's dequeue counters too
+    if (t < 5 && w.pe.cnt) w.pe.cnt[t] = t == 4 ? 1ull << 62 : 0;
     if (t < 8) heads[AF_HEAD_STRIDE * t] = 0;
     if (t < AF_GSTAT_N) w.stats[t] = 0;
     (void)n_reads;
@@ -2397,8 +2553,17 @@ hipError_t af_launch_genome_pe(const DevGenome &G, const uint8_t *reads, int32_t
     if (e != hipSuccess) return e;
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
-#define AF_GO(C) hipLaunchKernelGGL((k_g_pe<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_npairs, \
-                                    cap_pairs, p, o, w, sw, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec)
+    const int mode = w.pe.min_windows > 0 ? 1 : 0;
+#define AF_GO(C)                                                                                                      \
+    do {                                                                                                              \
+        hipLaunchKernelGGL((k_g_pe<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_npairs, cap_pairs, p, \
+                           o, w, sw, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec, mode);               \
+        if (mode) {                                                                                                   \
+            hipLaunchKernelGGL(k_g_pe_jobs, dim3(2 * n_waves), dim3(64), 0, s, G, reads, stride, lens, p, o, w, sw);   \
+            hipLaunchKernelGGL((k_g_pe<C>), dim3(n_waves), dim3(64), 0, s, G, reads, stride, lens, d_npairs,          \
+                               cap_pairs, p, o, w, sw, g2_scratch, g2_slot_bytes(), zscratch, zstride, recs, n_rec, 2); \
+        }                                                                                                             \
+    } while (0)
     if (cpl <= 2) AF_GO(2);
     else if (cpl <= 3) AF_GO(3);
     else if (cpl <= 4) AF_GO(4);

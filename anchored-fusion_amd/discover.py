@@ -33,6 +33,11 @@ _S4_SPLIT = os.environ.get("AF_S4_SPLIT", "1") == "1"
 # S6 (BLAT) of every S5 query that can be kept, beside S5's genome call, compacted after the check
 # (1), or of the check's survivors after it (0, round 4's order); bench A/B: AF_S6_EARLY
 _S6_EARLY = os.environ.get("AF_S6_EARLY", "1") == "1"
+# the early S6 search's heavy strands (af_blat_device_end) right behind its first part on slot 1,
+# for every pre-check query (1), or after the check for its survivors only (0, the default: on
+# configs[2] a query the check drops holds a 3,559-part strand whose serial chain DP costs
+# 177 ms of step -- 428.8 vs 252.0 ms per step, profiles/r05/knobs_s6_heavy.txt)
+_S6_HEAVY_EARLY = os.environ.get("AF_S6_HEAVY_EARLY", "0") == "1"
 EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
 HIT_WORDS = 44      # af_grec as int32 words (176 B)
 PSL_WORDS = 82      # af_psl as int32 words (328 B)
@@ -160,6 +165,8 @@ class CandidateDiscovery:
         try:
             self.tiles_ref.search_device_begin(sp["q"], sp["n"], _lib.AF_MAX_READ, sp["rows"], sp["n_rows"],
                                                lens_t=sp["lens"], p=self.p_tail, stream=stream)
+            if _S6_HEAVY_EARLY:
+                self.tiles_ref.search_device_end(None, stream=stream)
         finally:
             self.tiles_ref.spill_to()
             self.tiles_ref.query_caps_to()
@@ -173,7 +180,8 @@ class CandidateDiscovery:
     def _s6_finish(self, stream):
         """The rest of the S6 search for the survivors (af_blat_device_end), then their S6 rows and
         BLAT rows compacted and renumbered in query order."""
-        self.tiles_ref.search_device_end(self.s6p["live"], stream=stream)
+        if not _S6_HEAVY_EARLY:
+            self.tiles_ref.search_device_end(self.s6p["live"], stream=stream)
         _genome.s6_compact_device(self.tiles_ref.ctx, self.s6p, self.s6p["live"], self.s6f, stream=stream)
 
     def _s6_late(self, b, n5, recs, s0, s6, cont_t=None):

@@ -30,7 +30,7 @@ REC_DTYPE = np.dtype([("read", "<i4"), ("flag", "<i4"), ("rid", "<i4"), ("mrid",
 assert REC_DTYPE.itemsize == 176
 _OPS = "MIDNSHP=X"
 _COMP = str.maketrans("ACGTNacgtn", "TGCANtgcan")
-STAT_NAMES = ("cap_overflow", "pool_overflow", "record_overflow")
+STAT_NAMES = ("cap_overflow", "pool_overflow", "record_overflow", "pe_rescue_job_pairs")
 
 
 def _need(t, nbytes, what, dtype=None):

@@ -334,10 +334,11 @@ typedef struct {
 } af_grec;
 /* counters of the last genome call on a context: [0] reads past a per-read cap, [1] reads whose
  * intervals / regions did not fit the call's pools (also flagged), [2] reads with more than
- * AF_G_MAX_REC records */
+ * AF_G_MAX_REC records, [3] S4 pairs whose mate-rescue SWs ran as grid-wide jobs (informational) */
 #define AF_GSTAT_OVERFLOW 0
 #define AF_GSTAT_POOL 1
 #define AF_GSTAT_RECS 2
+#define AF_GSTAT_PE_JOBS 3
 #define AF_GSTAT_N 4
 /* blob: contig k is blob[ctg_off[k], ctg_off[k] + ctg_len[k]) (host arrays; bytes between contigs
  * are ignored, as a FASTA's headers are).  Synchronous; the index stays in HBM. */

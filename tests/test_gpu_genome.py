@@ -255,3 +255,42 @@ def test_g1_wave_path_equals_oracle(world, monkeypatch, max_ext):
             assert msg is None, (r, msg)
     finally:
         gw.close()
+
+
+@pytest.mark.parametrize("windows", [1, 3])
+def test_pe_rescue_jobs_equal_oracle(world, monkeypatch, windows):
+    """S4's heavy pairs (at least AF_G_PE_SPEC_WINDOWS mate-rescue windows, read when the context
+    is made): their rescue SWs computed ahead as grid-wide jobs (k_g_pe_jobs), the pair's own walk
+    taking the results (k_g_pe mode 2) -- every record equal to the oracle's, on sampled pairs and on
+    the crafted rescue pairs of test_genome_rescue_blocks.py."""
+    from anchored_fusion_amd import _lib
+    from anchored_fusion_amd.genome import GenomeIndex
+    from test_genome_rescue_blocks import L, crafted
+    contigs, og, _ = world
+    monkeypatch.setenv("AF_G_PE_SPEC_WINDOWS", str(windows))
+    gj = GenomeIndex(contigs, device=0)
+    try:
+        pairs = sample_pairs(contigs, 800, seed=61)
+        plens = np.full(pairs.shape[0], pairs.shape[1], np.int32)
+        po, pno = og.align_pe(pairs, plens, pe=oracle.default_pe(chunk_bases=200_000, pair_base=5), threads=8)
+        pg, png = gj.align_pe(pairs, plens, pe=_lib.default_pe(chunk_bases=200_000, pair_base=5))
+        assert np.array_equal(pno, png)
+        for r in range(len(pno)):
+            msg = _rec_equal(po[r], pg[r], min(pno[r], 8))
+            assert msg is None, (r, msg)
+        assert gj.stats()["pe_rescue_job_pairs"] > 0
+    finally:
+        gj.close()
+    c2, reads, _ = crafted()
+    og2 = oracle.OracleGenome(c2)
+    g2 = GenomeIndex(c2, device=0)
+    try:
+        lens = np.full(reads.shape[0], L, np.int32)
+        ro, no = og2.align_pe(reads, lens, pe=oracle.default_pe(), pair_base=0, threads=8)
+        rg, ng = g2.align_pe(reads, lens, pe=_lib.default_pe())
+        assert np.array_equal(no, ng)
+        for r in range(len(no)):
+            msg = _rec_equal(ro[r], rg[r], min(no[r], 8))
+            assert msg is None, (r, msg)
+    finally:
+        g2.close()
