@@ -184,7 +184,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     if (n > cap) n = cap;
     uint4 *const base = scratch + tid * G1_SLOT;
     uint4 *Lp = base, *Lc = base + G1_LIST;        // bwt_smem1's prev / curr (swapped by pointer)
-    uint4 *const Lm = base + 2 * G1_LIST, *const Lf = base + 3 * G1_LIST;  // its mems; the read's list
+    uint4 *const Lf = base + 3 * G1_LIST;  // the read's list (base + 2 G1_LIST: k_g_seeds_wave's mems)
     const int msl = p.min_seed_len;
     const int split_len = (int)((float)msl * 1.5f + .499);
     // lane state
@@ -193,15 +193,28 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     bool ovf = false, rev = false;
     int64_t rr = -1, min_intv = 1, ik_k = 0, ik_l = 0, ik_s = 0, last_s = 0;
     const uint8_t *rd = nullptr;
-    // bwt_smem1's backward scan reads prev's entries in order: G1_PC at a time into registers (one
-    // memory wait per G1_PC entries instead of one per entry); pc0 = the first cached entry's
-    // index in scan order, -1 none (prev is swapped at each position: the cache is dropped)
-    uint4 pcache[G1_PC];
-    int pc0 = -1;
+    // bwt_smem1's backward scan reads prev's entries in order: entry pf_j of the scan is in pf,
+    // loaded during the trip that extends entry pf_j - 1 (its wait overlaps that trip's FM
+    // lookup); at a new position prev's first entry is curr's first (or, after the forward scan,
+    // last) push, kept in registers (c_first / c_last): no list load waits on the critical path
+    uint4 pf = make_uint4(0, 0, 0, 0), c_first = pf, c_last = pf;
+    int pf_j = -1;
+    // pass 1's intervals that pass 2 re-seeds (long, few occurrences, a base at the middle), for
+    // the first 64 of the list: pass 2 reads only those
+    uint64_t elig = 0;
     int ne = 0;  // the read's FM extensions so far (past w.g1_max_ext: handed to k_g_seeds_wave)
-    GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0; int gp_fwd = 0, gp_bwd = 0, gp_ss = 0;)
-    auto code = [&](int t) -> int { return nt4(rd[t]); };
-    auto push_curr = [&](int64_t k, int64_t l, int64_t s, int qb, int qe) { Lc[nc++] = g1_pack(k, l, s, qb, qe); };
+    GPROF(uint64_t gp_c0 = 0; uint32_t gp_t0 = 0; int gp_fwd = 0, gp_bwd = 0, gp_ss = 0;
+          uint64_t gp_loop = 0, gp_ext = 0; int gp_trips = 0, gp_iters = 0;)
+    // each lane's read as codes in LDS, two per byte, lane-interleaved (byte (t / 2) * 64 + lane):
+    // the state machine's base reads stay off the memory path that every trip already waits on
+    __shared__ uint8_t g1_rd[(AF_MAX_READ / 2) * 64];
+    auto code = [&](int t) -> int { return (g1_rd[(t >> 1) * 64 + lane] >> ((t & 1) << 2)) & 15; };
+    auto push_curr = [&](int64_t k, int64_t l, int64_t s, int qb, int qe) {
+        const uint4 e = g1_pack(k, l, s, qb, qe);
+        if (nc == 0) c_first = e;
+        c_last = e;
+        Lc[nc++] = e;
+    };
     auto smem_start = [&](int x0, int64_t mi, int ps) {
         const int c = code(x0);
         sx = x0; min_intv = mi < 1 ? 1 : mi; pass = ps;
@@ -210,9 +223,10 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         st = G1_FWD;
     };
     auto fwd_end = [&]() {  // curr holds the forward intervals in push order (bwa reverses them)
-        ret = (int)g1_unpack(Lc[nc - 1]).qe;
+        ret = (int)g1_unpack(c_last).qe;
         uint4 *t = Lp; Lp = Lc; Lc = t;
-        np = nc; nc = 0; rev = true; i = sx - 1; j = 0; pc0 = -1;
+        np = nc; nc = 0; rev = true; i = sx - 1; j = 0;
+        pf = c_last; pf_j = 0;  // prev in reverse push order: entry 0 is the last push
         st = G1_BWD;
     };
     auto take = [&](const G1Iv &m) -> bool {  // an interval into the read's list
@@ -220,18 +234,23 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         Lf[ni++] = g1_pack(m.k, m.l, m.s, m.qb, m.qe);
         return true;
     };
-    auto smem_end = [&]() {  // bwa reverses the mems; the caller keeps those of >= min_seed_len
-        for (int t = nm - 1; t >= 0; --t) {
-            const G1Iv m = g1_unpack(Lm[t]);
-            if (m.qe - m.qb >= msl && !take(m)) return;
-        }
+    auto smem_end = [&]() {
         if (pass == 1) { x = ret; st = G1_P1; }
         else { ++k2; st = G1_P2; }
     };
-    auto mem_push = [&](const G1Iv &pv, int qb) {  // a prev entry that cannot extend becomes a mem
+    // a prev entry that cannot extend becomes a mem; those of >= min_seed_len go straight to the
+    // read's list (bwa collects a smem's mems and appends them reversed: the list's order is
+    // immaterial, k_g_regions sorts it by (qb, qe) and equal keys are identical intervals)
+    auto mem_push = [&](const G1Iv &pv, int qb) {
         if (nc == 0 && (nm == 0 || qb < last_mem_qb)) {
-            Lm[nm++] = g1_pack(pv.k, pv.l, pv.s, qb, pv.qe);
+            ++nm;
             last_mem_qb = qb;
+            if (pv.qe - qb >= msl) {
+                if (pass == 1 && ni < 64 && pv.qe - qb >= split_len && pv.s <= o.split_width &&
+                    code((qb + pv.qe) >> 1) <= 3)
+                    elig |= 1ull << ni;
+                take(G1Iv{pv.k, pv.l, pv.s, qb, pv.qe});
+            }
         }
     };
     G1Iv pv{};
@@ -249,9 +268,12 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 else {
                     len = read_len(lens, rr, stride);
                     rd = reads + rr * (int64_t)stride;
-                    ni = 0; ovf = false; x = 0; ne = 0;
+                    for (int t = 0; t < len; t += 2)
+                        g1_rd[(t >> 1) * 64 + lane] = (uint8_t)(nt4(rd[t]) | (t + 1 < len ? nt4(rd[t + 1]) : 4) << 4);
+                    ni = 0; ovf = false; x = 0; ne = 0; elig = 0;
                     st = len >= msl ? G1_P1 : G1_DONE;
-                    GPROF(gp_c0 = clock64(); gp_t0 = gp_rt(); gp_fwd = gp_bwd = gp_ss = 0;)
+                    GPROF(gp_c0 = clock64(); gp_t0 = gp_rt(); gp_fwd = gp_bwd = gp_ss = 0;
+                          gp_loop = gp_ext = 0; gp_trips = gp_iters = 0;)
                 }
             }
         }
@@ -261,7 +283,9 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         int64_t ek = 0, el = 0, es = 0;
         int ec = 0;
         bool efwd = false;
+        GPROF(const uint64_t gp_l0 = clock64(); ++gp_trips;)
         while (!need && st != G1_IDLE && st != G1_EXIT) {
+            GPROF(++gp_iters;)
             if (st == G1_P1) {  // pass 1: SMEMs covering each position
                 if (x >= len) { old_n = ni; k2 = 0; st = G1_P2; continue; }
                 if (code(x) > 3) { ++x; continue; }
@@ -275,29 +299,28 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 if (j == np) {
                     if (nc == 0) { smem_end(); continue; }
                     uint4 *t = Lp; Lp = Lc; Lc = t;
-                    np = nc; nc = 0; rev = false; --i; j = 0; pc0 = -1;
+                    np = nc; nc = 0; rev = false; --i; j = 0;
+                    pf = c_first; pf_j = 0;  // prev in push order: entry 0 is the first push
                     continue;
                 }
-                if (pc0 < 0 || j < pc0 || j >= pc0 + G1_PC) {
-                    pc0 = j;
-#pragma unroll
-                    for (int u = 0; u < G1_PC; ++u) {
-                        const int jj = j + u < np ? j + u : np - 1;
-                        pcache[u] = Lp[rev ? np - 1 - jj : jj];
-                    }
-                }
-                {
-                    const int u = j - pc0;
-                    uint4 e = pcache[0];
-#pragma unroll
-                    for (int v = 1; v < G1_PC; ++v)
-                        if (u == v) e = pcache[v];
-                    pv = g1_unpack(e);
-                }
+                if (pf_j != j) { pf = Lp[rev ? np - 1 - j : j]; pf_j = j; }
+                pv = g1_unpack(pf);
                 const int c = i < 0 ? -1 : code(i);
-                if (c < 0 || c > 3) { mem_push(pv, i + 1); ++j; continue; }
+                if (c < 0 || c > 3) {
+                    // no entry extends past the read's start or an N: each would become a mem at the
+                    // same qb, and only the first can (mem_push needs qb < last_mem_qb after it, and
+                    // curr stays as it is) -- the rest of prev is skipped unread
+                    mem_push(pv, i + 1);
+                    j = np;
+                    continue;
+                }
                 need = true; ek = pv.k; el = pv.l; es = pv.s; ec = c; efwd = false; p_qe = pv.qe;
+                if (j + 1 < np) { pf = Lp[rev ? np - 2 - j : j + 1]; pf_j = j + 1; }  // next trip's entry
             } else if (st == G1_P2) {  // pass 2: re-seed long SMEMs with few occurrences
+                if (k2 < 64 && k2 < old_n) {  // the next interval pass 2 re-seeds, from the mask
+                    const uint64_t m = elig & (~0ull << k2);
+                    k2 = m ? (int)__builtin_ctzll(m) : (old_n < 64 ? old_n : 64);
+                }
                 if (k2 >= old_n) {
                     if (o.max_mem_intv > 0) { x = 0; st = G1_P3; }
                     else st = G1_DONE;
@@ -320,22 +343,10 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 const int c = code(i);
                 if (c > 3) { x = i + 1; st = G1_P3; continue; }
                 need = true; ek = ik_k; el = ik_l; es = ik_s; ec = 3 - c; efwd = true;
-            } else {  // G1_DONE: the list sorted by (qb, qe) into the call's pool
+            } else {  // G1_DONE: the list into the call's pool (k_g_regions sorts it by (qb, qe))
                 bool hv = false;  // G2 takes it first
                 if (ovf) w.iv_n[rr] = -1;
                 else {
-                    for (int a = 1; a < ni; ++a) {  // equal keys are identical intervals (any order)
-                        const uint4 t = Lf[a];
-                        const uint32_t kt = (t.w >> 3 & 511) << 9 | (t.w >> 12 & 511);
-                        int b = a;
-                        while (b > 0) {
-                            const uint4 u = Lf[b - 1];
-                            if (((u.w >> 3 & 511) << 9 | (u.w >> 12 & 511)) <= kt) break;
-                            Lf[b] = u;
-                            --b;
-                        }
-                        Lf[b] = t;
-                    }
                     const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
                     if (ni && off + ni > w.iv_cap) {  // the pool is sized from the call's read count
                         atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
@@ -358,14 +369,18 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                 }
                 GPROF({ int32_t *g = gp_row(rr); if (g) { g[0] = (int32_t)(clock64() - gp_c0); g[1] = ovf ? -1 : ni;
                         g[17] = (int32_t)gp_t0; g[18] = (int32_t)gp_rt(); g[20] = (int32_t)tid;
-                        g[19] = gp_fwd; g[21] = gp_bwd; g[22] = gp_ss; } })
+                        g[19] = gp_fwd; g[21] = gp_bwd; g[22] = gp_ss;
+                        g[23] = (int32_t)(gp_loop >> 4); g[24] = (int32_t)(gp_ext >> 4); g[25] = gp_trips;
+                        g[26] = gp_iters; } })
                 st = G1_IDLE;
             }
         }
+        GPROF(const uint64_t gp_l1 = clock64(); gp_loop += gp_l1 - gp_l0;)
         if (__ballot(need) == 0) continue;
         // the extensions of this trip: every lane that needs one at once
         int64_t rk = 0, rl = 0, rs = 0;
         if (need) fm_ext1(G, ek, el, es, ec, efwd, rk, rl, rs);
+        GPROF(gp_ext += clock64() - gp_l1;)
         if (!need) continue;
         if (w.g1_max_ext > 0 && ++ne > w.g1_max_ext) {  // a heavy read: restarted by k_g_seeds_wave
             w.g1_hv[atomicAdd(w.g1_hv_n, 1ull)] = rr;
@@ -414,6 +429,7 @@ struct G1W {
     const uint8_t *q;
     int len, ni, msl;
     bool ovf;
+    int gp_f = 0, gp_bp = 0, gp_be = 0;  // profiling build: forward steps, backward positions / entries
 };
 // an interval into the read's list (uniform)
 __device__ __forceinline__ bool g1w_take(G1W &R, const G1Iv &m, int lane) {
@@ -435,6 +451,7 @@ __device__ __forceinline__ int g1w_smem(const DevGenome &G, G1W &R, int x0, int6
         int64_t rk = 0, rl = 0, rs = 0;
         if (i == R.len || R.q[i] > 3) push = stop = true;
         else {
+            GPROF(++R.gp_f;)
             fm_ext1(G, ik_k, ik_l, ik_s, 3 - R.q[i], true, rk, rl, rs);
             if (rs != ik_s) { push = true; stop = rs < min_intv; }
         }
@@ -454,6 +471,7 @@ __device__ __forceinline__ int g1w_smem(const DevGenome &G, G1W &R, int x0, int6
     int nm = 0, last_mem_qb = 0;
     for (int i = x0 - 1;; --i) {
         const int c = i < 0 ? -1 : (R.q[i] > 3 ? -1 : (int)R.q[i]);
+        GPROF(++R.gp_bp; R.gp_be += np;)
         int ncur = 0;
         bool any = false;       // a surviving entry in an earlier chunk
         int64_t carry = 0;      // its size
@@ -513,6 +531,7 @@ __global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t 
         if (h >= nh) break;
         const int64_t rr = w.g1_hv[h];
         G1W R{base, base + G1_LIST, base + 2 * G1_LIST, base + 3 * G1_LIST, qs, read_len(lens, rr, stride), 0, msl, false};
+        GPROF(const uint64_t gp_w0 = clock64(); int gp_ssn = 0;)
         const uint8_t *rd = reads + rr * (int64_t)stride;
         for (int t = lane; t < R.len; t += 64) qs[t] = nt4(rd[t]);
         wave_sync();
@@ -543,6 +562,7 @@ __global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t 
                     const int c = R.q[i];
                     if (c > 3) { x = i + 1; break; }
                     int64_t rk, rl, rs;
+                    GPROF(++gp_ssn;)
                     fm_ext1(G, ik_k, ik_l, ik_s, 3 - c, true, rk, rl, rs);
                     if (rs < o.max_mem_intv && i - sx >= msl) {
                         if (rs > 0) g1w_take(R, G1Iv{rk, rl, rs, sx, i + 1}, lane);
@@ -553,25 +573,15 @@ __global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t 
                 }
             }
         g1w_sync();
-        // the list sorted by (qb, qe) into the call's pool (k_g_seeds' G1_DONE)
+        GPROF(if (lane == 0) { int32_t *g = gp_row(rr); if (g) { g[27] = -(int32_t)((clock64() - gp_w0) >> 4) - 1;
+              g[28] = R.gp_f; g[29] = R.gp_bp; g[30] = R.gp_be; g[31] = gp_ssn; } })
+        // the list into the call's pool (k_g_seeds' G1_DONE; k_g_regions sorts it)
         if (lane == 0) {
             const int ni = R.ni;
             uint4 *Lf = R.lst;
             bool hv = false;  // G2 takes it first
             if (R.ovf) w.iv_n[rr] = -1;
             else {
-                for (int a = 1; a < ni; ++a) {
-                    const uint4 t = Lf[a];
-                    const uint32_t kt = (t.w >> 3 & 511) << 9 | (t.w >> 12 & 511);
-                    int b = a;
-                    while (b > 0) {
-                        const uint4 u = Lf[b - 1];
-                        if (((u.w >> 3 & 511) << 9 | (u.w >> 12 & 511)) <= kt) break;
-                        Lf[b] = u;
-                        --b;
-                    }
-                    Lf[b] = t;
-                }
                 const int64_t off = ni ? (int64_t)atomicAdd(w.iv_fill, (unsigned long long)ni) : 0;
                 if (ni && off + ni > w.iv_cap) {
                     atomicAdd(&w.stats[AF_GSTAT_POOL], 1);
@@ -1527,6 +1537,30 @@ __device__ bool g_defer_heavy(const GWork &w, const G2Scr &S, int64_t r, int nch
 
 // G2: mem_align1_core for every read (one wave per read); a read with at least hv.min_chains
 // kept chains leaves their extensions to k_g_ext_jobs and its finish to k_g_heavy
+// a read's intervals iv[0, n) into (qb, qe) order, as mem_collect_intv's ks_introsort leaves them
+// (equal keys are identical intervals: any order among them is bwa's); G1 pools them in collection
+// order.  Lanes rank the keys in LDS (the G2 boxes, free until mem_chain); the entries move
+// through tmp (n of them).
+static_assert(AF_G_MAX_INTV <= 1024 && AF_MAX_READ < 512, "interval keys pack qb, qe and a 10-bit index");
+__device__ void g_iv_sort(GIv *iv, int n, GIv *tmp, int lane) {
+    if (n <= 1) return;
+    uint32_t *key = reinterpret_cast<uint32_t *>(g_box);
+    for (int i = lane; i < n; i += 64) key[i] = (uint32_t)iv[i].qb << 19 | (uint32_t)iv[i].qe << 10 | (uint32_t)i;
+    __threadfence_block();
+    wave_sync();
+    for (int i = lane; i < n; i += 64) {
+        const uint32_t x = key[i];
+        int r = 0;
+        for (int j = 0; j < n; ++j) r += key[j] < x;
+        tmp[r] = iv[i];
+    }
+    __threadfence_block();
+    wave_sync();
+    for (int i = lane; i < n; i += 64) iv[i] = tmp[i];
+    __threadfence_block();
+    wave_sync();
+}
+
 template <int CPL>
 __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
                                                      const int32_t *__restrict__ lens, const int32_t *__restrict__ n_ptr,
@@ -1565,6 +1599,7 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
                   gp_occ += s_ > p.max_occ ? p.max_occ : s_; })
         if (!ovf && l >= p.min_seed_len && niv > 0) {
             g_load_read(reads, r, stride, l, lane);
+            g_iv_sort(w.iv + w.iv_off[r], niv, reinterpret_cast<GIv *>(S.seed), lane);
             const int nch0 = g_mem_chain(G, S, w.iv + w.iv_off[r], niv, p, o, lane);
             GPROF(gp_c[1] = clock64(); gp_n[0] = nch0;)
             if (nch0 < 0) ovf = true;
@@ -2490,9 +2525,12 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, d_n, cap,
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
-    if (w.g1_max_ext > 0)  // the heavy reads, one wave each, in the lane kernel's (finished) scratch
-        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
-                           reinterpret_cast<uint4 *>(g1_scratch), w);
+    // the heavy reads, one wave each, in the lane kernel's (finished) scratch: as many waves as the
+    // scratch holds lanes' slots (their count is known on the device only; a call of few reads can
+    // hand off thousands of repeat-rich ones, each 600+ dependent lookups long)
+    if (w.g1_max_ext > 0)
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64)), dim3(64), 0, s, G,
+                           reads, stride, lens, cap, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
 #define AF_GO(C)                                                                                                       \
@@ -2522,8 +2560,8 @@ hipError_t af_launch_genome_intervals(const DevGenome &G, const uint8_t *reads, 
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, nullptr, cap,
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     if (w.g1_max_ext > 0)
-        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, cap, p, o,
-                           reinterpret_cast<uint4 *>(g1_scratch), w);
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64)), dim3(64), 0, s, G,
+                           reads, stride, lens, cap, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     return hipGetLastError();
 }
 

@@ -75,6 +75,20 @@ for c in range(min(ncalls, 4)):
         print(f"   {g1[i]:>11d} {((r[18] - r[17]) & 0xFFFFFFFF) / 100:8.1f} | {r[19]} {r[21]} {r[22]} | {r[2]} {r[1]}")
     cyc_per_ext = g1 / np.maximum(ext, 1)
     print(f"  G1 cycles per extension p50 {pct(cyc_per_ext, 50):.0f} p90 {pct(cyc_per_ext, 90):.0f}")
+    if True:  # [23, 27) hold G1's trip split (k_g_pe overwrites them on S4 pairs' first reads)
+        loop, extc, trips, iters = (B[:, 23].astype(np.int64) << 4, B[:, 24].astype(np.int64) << 4, B[:, 25], B[:, 26])
+        ok = trips > 0
+        print(f"  G1 per trip (wave time, S5 reads): bookkeeping loop {(loop[ok] / trips[ok]).mean():.0f} cycles, "
+              f"FM extension {(extc[ok] / trips[ok]).mean():.0f} cycles, rest "
+              f"{((g1[ok] - loop[ok] - extc[ok]) / trips[ok]).mean():.0f}; lane's loop iterations per trip "
+              f"{(iters[ok] / trips[ok]).mean():.2f}")
+    hw = B[:, 27] < 0  # G1's wave path (k_g_seeds_wave: -(cycles >> 4) - 1); S4 pairs' first reads carry PE data there
+    if hw.any():
+        wc = (-B[hw, 27] - 1) << 4
+        print(f"  G1 wave path: {int(hw.sum())} reads seen; cycles/read mean {wc.mean():.0f} p50 {pct(wc, 50):.0f} "
+              f"max {wc.max()}; fwd steps mean {B[hw, 28].mean():.0f}, bwd positions mean {B[hw, 29].mean():.0f} "
+              f"(entries {B[hw, 30].mean():.0f}), seed-strategy steps mean {B[hw, 31].mean():.0f}; "
+              f"cycles per sequential step {(wc / np.maximum(B[hw, 28] + B[hw, 29] + B[hw, 31], 1)).mean():.0f}")
     lanes = B[:, 20]
     lane_sum = np.bincount(lanes, weights=g1)
     print(f"  G1 per-lane cycles: mean {lane_sum[lane_sum > 0].mean():.0f} max {lane_sum.max():.0f}")
