@@ -38,10 +38,6 @@ _S6_EARLY = os.environ.get("AF_S6_EARLY", "1") == "1"
 # configs[2] a query the check drops holds a 3,559-part strand whose serial chain DP costs
 # 177 ms of step -- 428.8 vs 252.0 ms per step, profiles/r05/knobs_s6_heavy.txt)
 _S6_HEAVY_EARLY = os.environ.get("AF_S6_HEAVY_EARLY", "0") == "1"
-EX_HITS = 4         # SAM records (genome calls) / PSL rows (S6) per query carried by exchange()
-HIT_WORDS = 44      # af_grec as int32 words (176 B)
-PSL_WORDS = 82      # af_psl as int32 words (328 B)
-EX_WORDS = 39 + EX_HITS * HIT_WORDS
 _DEBUG = os.environ.get("AF_DEBUG_DISCOVER") == "1"
 
 
@@ -482,50 +478,3 @@ class CandidateDiscovery:
         read = self.q_rows[self._npair * 2:][src] if n6 else self.s6["src"][:0]
         return (read.cpu().numpy(), self.t_nh[:n6].cpu().numpy(),
                 rows.reshape(n6, _blat.MAX_ROWS)[:, 0] if n6 else rows)
-
-    def pack(self):
-        """The breakpoint candidates of the last pass as int32 rows [k, EX_WORDS] on the device:
-        every S4 / S5 query and every S6 query -- the read's global row (2 words), kind (0 genome
-        query, 1 S6 query), its S2 FLAG / POS / n_cigar / 32 CIGAR words, the record / row count and the first
-        EX_HITS of them (af_grec SAM records of the genome bwa calls, af_psl rows for BLAT).  These
-        are the only records the stages after S6 read (SURVEY §8 e)."""
-        import torch
-        torch.cuda.synchronize(self.dev)
-        nq = min(int(self.n_q.item()), self.qcap)
-        n6 = int(self.s6["n"].item())
-        s6_rows = self.q_rows[2 * self._npair:][self.s6["src"][:n6].long()] if n6 else self.q_rows[:0]
-        parts = []
-        for kind, n, rows, nh, hits, width, per in (
-                (0, nq, self.q_rows, self.q_nh, self.q_recs, HIT_WORDS, MAX_REC),
-                (1, n6, s6_rows, self.t_nh, self.t_rows, PSL_WORDS, _blat.MAX_ROWS)):
-            if n == 0:
-                continue
-            r = rows[:n].long()
-            p = torch.zeros((n, EX_WORDS), dtype=torch.int32, device=self.dev)
-            g = r + 2 * self.pair_base
-            p[:, 0] = (g & 0xFFFFFFFF).to(torch.int32)
-            p[:, 1] = (g >> 32).to(torch.int32)
-            p[:, 2] = kind
-            p[:, 3] = self.out["flag"][r]
-            p[:, 4] = self.out["pos"][r]
-            p[:, 5] = self.out["n_cigar"][r]
-            p[:, 6:38] = self.out["cigar"][r]
-            p[:, 38] = nh[:n]
-            h = hits[:n * per * width * 4].view(torch.int32).view(n, per, width)
-            k = min(EX_HITS * HIT_WORDS // width, per)
-            p[:, 39:39 + k * width] = h[:, :k].reshape(n, k * width)
-            parts.append(p)
-        if not parts:
-            return torch.zeros((0, EX_WORDS), dtype=torch.int32, device=self.dev)
-        return torch.cat(parts) if len(parts) > 1 else parts[0]
-
-    def exchange(self, group=None):
-        """All-gatherv of pack() across the ranks (shard.allgatherv_device: counts all-gather, then
-        one max-padded all_gather; RCCL has no v-variant).  Returns the gathered rows on the
-        device, rank order.  A gloo group (CPU tests) gathers host copies."""
-        import torch.distributed as dist
-        from .shard import allgatherv_device
-        rows = self.pack()
-        if dist.get_backend(group) == "nccl":
-            return allgatherv_device(rows, group)
-        return allgatherv_device(rows.cpu(), group).to(self.dev)

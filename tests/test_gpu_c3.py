@@ -273,17 +273,20 @@ def _check_exact_reads_high(W, ref, L, n=3000):
     torch.cuda.synchronize()
 
 
-def test_discovery_rank_shard_and_exchange(anchor):
+def test_discovery_rank_shard_and_search(anchor, monkeypatch):
     """A rank's shard (pair_base on the bwa chunk grid, as bench.py's ranks run it): records
-    bit-exact vs the oracle with the same read ids, and the candidate exchange over a one-rank
-    RCCL group returns exactly the packed rows, with global read rows."""
+    bit-exact vs the oracle with the same read ids; then the product's multi-GPU step
+    (dist_discover.search) over a one-rank RCCL group (AF_DIST_COLLECTIVES=1: every all-gather /
+    all-to-all through RCCL on device tensors) gives the single-process pass's counts, S4 records
+    and survivors, with global read rows."""
     import os
     import socket
 
     import torch
     import torch.distributed as dist
 
-    from anchored_fusion_amd import discover
+    from anchored_fusion_amd import discover, dist_discover
+    from anchored_fusion_amd.genome import MAX_REC, REC_DTYPE
     from anchored_fusion_amd.shard import chunk_pairs
     W = _world(anchor, 0.02)
     ref = W.genome_index()
@@ -297,27 +300,39 @@ def test_discovery_rank_shard_and_exchange(anchor):
     got = {k: v.cpu().numpy() for k, v in d.out.items()}
     got["cigar"] = got["cigar"].view(np.uint32)
     assert_records_equal(got, oracle.OracleIndex(anchor).align_pairs(reads, threads=8, pair_base=pb), reads)
+    q = d.q[:int(d.n_q.item())].cpu().numpy()
+    _check_genome_records(d, ref, q, q.shape[0], d.counts["s4_pairs"])
+    # the single-process pass's products
+    counts1 = dict(d.counts)
+    npair = counts1["s4_pairs"]
+    words = REC_DTYPE.itemsize // 4
+    recs1 = d.q_recs.view(torch.int32)[:2 * npair * MAX_REC * words].reshape(2 * npair, MAX_REC, words).clone()
+    nrec1 = d.q_nh[:2 * npair].clone()
+    n6 = int(d.s6["n"].item())
+    surv_rows1 = (d.q_rows[2 * npair:][d.s6["src"][:n6].long()].long() + 2 * pb).cpu()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    monkeypatch.setenv("AF_DIST_COLLECTIVES", "1")
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        packed = d.pack()
-        ex = d.exchange()
+        res, counts = dist_discover.search(d.attach(reads_t), pb, 0, 1, device="cuda:0")
         torch.cuda.synchronize()
     finally:
         dist.destroy_process_group()
-    assert ex.shape == packed.shape and torch.equal(ex.cpu(), packed.cpu()) and ex.shape[0] > 0
-    q = d.q[:int(d.n_q.item())].cpu().numpy()
-    _check_genome_records(d, ref, q, q.shape[0], d.counts["s4_pairs"])
-    p = packed.cpu().numpy()
-    grow = p[:, 0].view(np.uint32).astype(np.int64) | (p[:, 1].astype(np.int64) << 32)
-    nq = int(d.n_q.item())
-    assert np.array_equal(grow[:nq], d.q_rows[:nq].cpu().numpy().astype(np.int64) + 2 * pb)
-    assert (p[:nq, 2] == 0).all() and (p[nq:, 2] == 1).all()
-    local = grow - 2 * pb
-    assert np.array_equal(p[:, 3], got["flag"][local]) and np.array_equal(p[:, 4], got["pos"][local])
+    for k in ("tmp1", "tmp2", "s5_split_reads", "s4_pairs"):
+        assert counts[k] == counts1[k], k
+    assert counts["s6_queries"] == n6 > 0
+    _, _, recs, nrec, _ = res["s4"]
+    assert torch.equal(nrec.cpu(), nrec1.cpu().to(nrec.dtype))
+    live = torch.arange(MAX_REC)[None, :] < nrec1.cpu().clamp(max=MAX_REC).long()[:, None]
+    assert torch.equal(recs.cpu()[live], recs1.cpu()[live])
+    # the survivors in ordinal order with their global read rows (the last two words of a row)
+    grow = dist_discover._i64(res["surv"][:, -2:]).cpu()
+    assert torch.equal(torch.sort(grow).values, torch.sort(surv_rows1).values)
+    assert (grow >= 2 * pb).all() and (grow < 2 * (pb + n)).all()
     d.close()
     ref.close()
     tiles.close()

@@ -8,7 +8,7 @@
   (dist_discover.search on the rank's lo) through a one-rank RCCL group, its all-gathers and
   all-to-alls on device tensors, giving the same counts, S4 records and survivors with global
   read rows.  The genome is
-  the configs[2] world at 5 % scale (the index build of the full 3.1 Gbp is test_gpu_c3's).
+  the configs[2] world at full size (3.09 Gbp: the index and tiles the bench's ranks build).
 * configs[4] (1,000 cells x 100 k pairs over 8 GPUs): one rank's 125 cells through
   singlecell.run, the planted fusion merged from the cells, and three sampled cells' tables
   byte-identical to the CPU-oracle backends on the same cells (SC:205-287)."""
@@ -37,7 +37,7 @@ def test_configs3_rank3_shape(anchor):
     lo, hi = shard_range(N, rank, world, L)
     n = hi - lo
     assert lo % chunk_pairs(L) == 0 and 6_000_000 < n < 6_500_000
-    W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=0.05)
+    W = simworld.GenomeWorld(anchor, device=0, seed=20251015, scale=1.0)
     gidx, tiles = W.genome_index(), W.tiles()
     reads_t = W.simulate_pairs(n, read_len=L, seed=20251015, pair_base=lo)
     torch.cuda.synchronize()
