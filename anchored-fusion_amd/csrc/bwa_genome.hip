@@ -1351,7 +1351,10 @@ __device__ int g_dedup_patch(const DevGenome &G, const af_params &p, const GOpt 
                 bool cont = false, ev = false;
                 if (jj >= 0) {
                     const GReg q = a[jj];
-                    cont = pp.rid == q.rid && pp.rb < q.re + gap;
+                    // without patching only an overlap changes something, and it needs q.re > pp.rb:
+                    // re ascends along the list, so the walk may stop at the first q ending at or
+                    // before pp's start (the regions below it cannot overlap pp either)
+                    cont = pp.rid == q.rid && pp.rb < q.re + gap && (patch || q.re > pp.rb);
                     if (cont && q.qe != q.qb) {
                         int w_;
                         ev = g_dd_overlap(q, pp) || (patch && q.rb < pp.rb && g_patch_pre(l_pac, p, q, pp, &w_));
@@ -2180,6 +2183,99 @@ __device__ int g_mem_pair(const DevGenome &G, const af_params &p, const S2Pes *p
     return (int)(best.x >> 32);
 }
 
+// mem_pair on the wave for long region lists (the same result as g_mem_pair: its keys are unique,
+// so the rank sort gives klib's order, and the best pair is the maximum of keys that name their two
+// entries, so it does not depend on the scan order).  Lanes build the keys; the scan keeps bwa's
+// order over i, with lanes over the earlier entries k of the wanted kind, 64 at a time from y[which]
+// down, stopping at the first (highest) k past the insert-size window as bwa's break does.  Every
+// lane returns the score (0: none) and z.
+__device__ int g_mem_pair_w(const DevGenome &G, const af_params &p, const S2Pes *pes, const GReg *a0, int n0,
+                            const GReg *a1, int n1, int id, int z[2], P64g *v, P64g *tmp, int lane) {
+    const int64_t l_pac = G.l_pac;
+    const int nv = n0 + n1;
+    for (int t = lane; t < nv; t += 64) {
+        const int r = t >= n0, i = t - (r ? n0 : 0);
+        const GReg &e = r ? a1[i] : a0[i];
+        const int64_t x = e.rb < l_pac ? e.rb : (l_pac << 1) - 1 - e.rb;
+        P64g key;
+        key.x = (uint64_t)e.rid << 32 | (uint64_t)(x - G.ctg_off_d[e.rid]);
+        key.y = (uint64_t)(uint32_t)e.score << 32 | (uint64_t)i << 2 | (uint64_t)(e.rb >= l_pac) << 1 | (uint64_t)r;
+        v[t] = key;
+    }
+    __threadfence_block();
+    wave_sync();
+    if (!wave_rank_sort(v, nv, GLtP64(), tmp, lane)) {  // (keys name their entry: never taken)
+        if (lane == 0) ks_introsort(v, nv, GLtP64());
+        __threadfence_block();
+        wave_sync();
+    }
+    int y[4] = {-1, -1, -1, -1};
+    bool have = false;
+    P64g best{0, 0};
+    for (int i = 0; i < nv; ++i) {
+        const P64g vi = v[i];
+        for (int r = 0; r < 2; ++r) {
+            const int dir = r << 1 | (int)(vi.y >> 1 & 1);
+            if (pes[dir].failed) continue;
+            const int which = r << 1 | (int)((vi.y & 1) ^ 1);
+            if (y[which] < 0) continue;
+            const int64_t lo = pes[dir].low, hi = pes[dir].high;
+            for (int k0 = y[which]; k0 >= 0; k0 -= 64) {
+                const int k = k0 - lane;
+                bool valid = false, brk = false;
+                int64_t dist = 0;
+                P64g vk{0, 0};
+                if (k >= 0) {
+                    vk = v[k];
+                    valid = (int)(vk.y & 3) == which;
+                    dist = (int64_t)vi.x - (int64_t)vk.x;
+                    brk = valid && dist > hi;
+                }
+                const uint64_t bm = __ballot(brk);
+                const int first = bm ? (int)__builtin_ctzll(bm) : 64;  // lanes below it precede bwa's break
+                if (valid && lane < first && dist >= lo) {
+                    const double ns = ((double)dist - pes[dir].avg) / pes[dir].std;
+                    int q = (int)((double)((vi.y >> 32) + (vk.y >> 32)) + .721 * log(2. * erfc(fabs(ns) * 0.70710678118654752440)) * p.a + .499);
+                    if (q < 0) q = 0;
+                    P64g u;
+                    u.y = (uint64_t)k << 32 | (uint64_t)i;
+                    u.x = (uint64_t)q << 32 | (hash_64(u.y ^ (uint64_t)(int64_t)(int32_t)((uint32_t)id << 8)) & 0xffffffffU);
+                    if (!have || GLtP64()(best, u)) { best = u; have = true; }
+                }
+                if (bm) break;
+            }
+        }
+        y[vi.y & 3] = i;
+    }
+    // the lanes' best to lane 0 through tmp (its sort copy is dead)
+    tmp[lane] = have ? best : P64g{0, 0};
+    reinterpret_cast<uint8_t *>(tmp + 64)[lane] = have ? 1 : 0;
+    __threadfence_block();
+    wave_sync();
+    int res = 0;
+    if (lane == 0) {
+        bool any = false;
+        P64g b{0, 0};
+        for (int l = 0; l < 64; ++l)
+            if (reinterpret_cast<const uint8_t *>(tmp + 64)[l] && (!any || GLtP64()(b, tmp[l]))) { b = tmp[l]; any = true; }
+        if (any) {
+            const int i = (int)(b.y >> 32), k = (int)(b.y << 32 >> 32);
+            z[v[i].y & 1] = (int)(v[i].y << 32 >> 34);
+            z[v[k].y & 1] = (int)(v[k].y << 32 >> 34);
+            res = (int)(b.x >> 32);
+        }
+        tmp[0].x = (uint64_t)(uint32_t)res | (uint64_t)(uint32_t)z[0] << 32;
+        tmp[0].y = (uint64_t)(uint32_t)z[1];
+    }
+    __threadfence_block();
+    wave_sync();
+    const P64g o = tmp[0];
+    z[0] = (int)(o.x >> 32); z[1] = (int)(uint32_t)o.y;
+    res = (int)(uint32_t)o.x;
+    wave_sync();
+    return res;
+}
+
 // G4: mem_sam_pe for every pair (one wave per pair); records of read 2pp + m at
 // recs[(2 pp + m) * AF_G_MAX_REC ..], counts n_rec[2 pp + m]
 template <int CPL>
@@ -2302,13 +2398,21 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
         // primary marking, pairing and the record choice (mem_sam_pe)
         g_mark_primary_w(A[0], E.na[0], (int64_t)((uint64_t)(o.pair_base + pp) << 1 | 0), reinterpret_cast<GReg *>(S.seed), lane);
         g_mark_primary_w(A[1], E.na[1], (int64_t)((uint64_t)(o.pair_base + pp) << 1 | 1), reinterpret_cast<GReg *>(S.seed), lane);
+        // mem_pair of long region lists on the wave (lane 0's g_mem_pair below otherwise)
+        int zw[2] = {0, 0}, o_sc_w = 0;
+        const int npr = E.na[0] + E.na[1];
+        const bool pair_w = E.na[0] && E.na[1] && npr >= G_RANK_MIN && npr <= AF_G_MAX_REG;
+        if (pair_w)
+            o_sc_w = g_mem_pair_w(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)(o.pair_base + pp), zw,
+                                  reinterpret_cast<P64g *>(g_box), V, lane);
         if (lane == 0) {
             const uint64_t id = (uint64_t)(o.pair_base + pp);
-            int z[2] = {0, 0}, extra = 1, mode = 0;  // mode 1: paired records
+            int z[2] = {zw[0], zw[1]}, extra = 1, mode = 0;  // mode 1: paired records
             int o_sc = 0;
             // mem_pair's sort keys in LDS (the boxes' space) when they fit
             P64g *Vp = E.na[0] + E.na[1] <= AF_G_MAX_REG ? reinterpret_cast<P64g *>(g_box) : V;
-            if (E.na[0] && E.na[1] && (o_sc = g_mem_pair(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)id, z, Vp)) > 0) {
+            if (E.na[0] && E.na[1] &&
+                (o_sc = pair_w ? o_sc_w : g_mem_pair(G, p, E.pes, A[0], E.na[0], A[1], E.na[1], (int)(uint32_t)id, z, Vp)) > 0) {
                 int is_multi = 0;
                 for (int i = 0; i < 2; ++i) {
                     int j;
