@@ -142,9 +142,19 @@ __device__ __forceinline__ void drift_mark(uint64_t key, int wsh, int round) {
         atomicOr(&twice[g >> 5], 1u << (g & 31));
     }
 }
+// whether key k (marked for this round) may have another key within drift of its diagonal
+__device__ __forceinline__ bool drift_kept(uint64_t k, int64_t drift, int wsh, int round) {
+    const uint32_t *once = reinterpret_cast<const uint32_t *>(g_z), *twice = reinterpret_cast<const uint32_t *>(g_dp.t);
+    const int64_t d = (int64_t)(k >> 9);
+    const uint64_t b = (uint64_t)d >> wsh, b0 = (uint64_t)(d - drift) >> wsh, b1 = (uint64_t)(d + drift) >> wsh;
+    const uint32_t h = bucket_hash(b, round, 14), g = h & 8191;
+    bool keep = (twice[g >> 5] >> (g & 31)) & 1u;
+    const uint64_t bn = b0 != b ? b0 : b1;  // the bucket width is >= 2 drift: one neighbour at most
+    if (bn != b) { const uint32_t hn = bucket_hash(bn, round, 14); keep = keep || ((once[hn >> 5] >> (hn & 31)) & 1u); }
+    return keep;
+}
 // src[0, n) (marked for this round) -> dst: the keys kept, in order; returns their count
 __device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh, int round, int lane) {
-    const uint32_t *once = reinterpret_cast<const uint32_t *>(g_z), *twice = reinterpret_cast<const uint32_t *>(g_dp.t);
     int nk = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -152,12 +162,7 @@ __device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t dri
         uint64_t k = 0;
         if (i < n) {
             k = src[i];
-            const int64_t d = (int64_t)(k >> 9);
-            const uint64_t b = (uint64_t)d >> wsh, b0 = (uint64_t)(d - drift) >> wsh, b1 = (uint64_t)(d + drift) >> wsh;
-            const uint32_t h = bucket_hash(b, round, 14), g = h & 8191;
-            keep = (twice[g >> 5] >> (g & 31)) & 1u;
-            const uint64_t bn = b0 != b ? b0 : b1;  // the bucket width is >= 2 drift: one neighbour at most
-            if (bn != b) { const uint32_t hn = bucket_hash(bn, round, 14); keep = keep || ((once[hn >> 5] >> (hn & 31)) & 1u); }
+            keep = drift_kept(k, drift, wsh, round);
         }
         const uint64_t m = __ballot(keep);
         if (keep) dst[nk + lanes_below_blat(m, lane)] = k;
@@ -722,13 +727,12 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             }
             wave_sync();
             // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
-            // in flight --------------------------------------------------------------------------
+            // in flight.  With the drift filter (min_match >= 2) the hits are gathered twice: the
+            // first pass only marks their buckets (LDS), the second keeps round 0's survivors --
+            // the one list written to scratch is theirs (125 of 7,633 hits per strand at configs[2])
             const int nh_all = min(carry, NMAX);
             if (lane == 0 && carry > NMAX) caps.hit(qi, AF_BLAT_CAP_HITS);
-            int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
-            for (int h0 = 0; h0 < nh_all; h0 += 256) {
-                int qv[4];
-                uint32_t pv[4];
+            auto gather = [&](int h0, int &qc, int (&qv)[4], uint32_t (&pv)[4]) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int h = h0 + 64 * j + lane;
@@ -743,13 +747,19 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
                     const int h = h0 + 64 * j + lane;
                     pv[j] = h < nh_all ? X.pos[DEL[qv[j]] + (uint32_t)h] : 0u;
                 }
+            };
+            int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
+            for (int h0 = 0; h0 < nh_all; h0 += 256) {
+                int qv[4];
+                uint32_t pv[4];
+                gather(h0, qc, qv, pv);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int h = h0 + 64 * j + lane;
                     if (h < nh_all) {
                         const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
-                        KA[h] = key;
                         if (filt) drift_mark(key, wsh, 0);
+                        else KA[h] = key;
                     }
                 }
             }
@@ -763,15 +773,35 @@ __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8
             // min_match >= 2 hits, and removing them changes no other run): hashed bucket bitmaps,
             // false keeps only, a few rounds while they pay ---------------------------------------
             uint64_t *H0 = KA, *H1 = KB;
-            if (filt)
-                for (int round = 0; round < AF_BLAT_ROUNDS && (round == 0 || nh > AF_BLAT_FILTER_MIN); ++round) {
-                    const int nk = round == 0 ? drift_keep(H0, H1, nh, drift, wsh, 0, lane)
-                                              : drift_filter(H0, H1, nh, drift, wsh, round, lane);
-                    uint64_t *t = H0; H0 = H1; H1 = t;
-                    const bool stop = nk * 8 > nh * 7;
-                    nh = nk;
-                    if (stop) break;
+            if (filt) {
+                // round 0 on the second gathering pass, its survivors in order into H0
+                int nk = 0;
+                qc = 0;
+                for (int h0 = 0; h0 < nh_all; h0 += 256) {
+                    int qv[4];
+                    uint32_t pv[4];
+                    gather(h0, qc, qv, pv);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int h = h0 + 64 * j + lane;
+                        const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
+                        const bool keep = h < nh_all && drift_kept(key, drift, wsh, 0);
+                        const uint64_t m = __ballot(keep);
+                        if (keep) H0[nk + lanes_below_blat(m, lane)] = key;
+                        nk += (int)__builtin_popcountll(m);
+                    }
                 }
+                __threadfence_block();
+                wave_sync();
+                bool stop = nk * 8 > nh * 7;
+                nh = nk;
+                for (int round = 1; !stop && round < AF_BLAT_ROUNDS && nh > AF_BLAT_FILTER_MIN; ++round) {
+                    const int nk2 = drift_filter(H0, H1, nh, drift, wsh, round, lane);
+                    uint64_t *t = H0; H0 = H1; H1 = t;
+                    stop = nk2 * 8 > nh * 7;
+                    nh = nk2;
+                }
+            }
             BPM(5);
             BP(cs += nh;)
             if (nh == 0) continue;

@@ -353,10 +353,18 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
                         w.iv_n[rr] = -1;
                     } else {
                         int64_t occ = 0;
-                        for (int a = 0; a < ni; ++a) {
-                            const G1Iv m = g1_unpack(Lf[a]);
-                            w.iv[off + a] = GIv{m.k, m.s, m.qb, m.qe};
-                            occ += m.s > p.max_occ ? p.max_occ : m.s;
+                        // four list entries loaded before any store: one memory wait per four
+                        for (int a0 = 0; a0 < ni; a0 += 4) {
+                            uint4 e4[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) e4[u] = Lf[a0 + u < ni ? a0 + u : a0];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (a0 + u < ni) {
+                                    const G1Iv m = g1_unpack(e4[u]);
+                                    w.iv[off + a0 + u] = GIv{m.k, m.s, m.qb, m.qe};
+                                    occ += m.s > p.max_occ ? p.max_occ : m.s;
+                                }
                         }
                         w.iv_off[rr] = off;
                         w.iv_n[rr] = ni;

@@ -85,12 +85,12 @@ def pmc_traffic(pairs, read_len):
     return None
 
 
-PROF = os.path.join("profiles", "r04")  # this round's committed rocprofv3 summaries (scripts/summarize_r04.py)
+PROF = os.path.join("profiles", "r05")  # this round's committed rocprofv3 summaries (scripts/summarize_prof.py)
 
 
 def rocprof_k1(bytes_per_launch, n_launch):
     """K1's roofline fraction from the committed rocprofv3 kernel trace of the same command
-    (profiles/r04/kernel_stats_c3.csv: average k_seed_stream duration over every launch of the
+    (profiles/r05/kernel_stats_c3.csv: average k_seed_stream duration over every launch of the
     traced steps, the same mix of full and remainder batches), beside the live HIP-event figure."""
     import csv
     path = os.path.join(ROOT, PROF, "kernel_stats_c3.csv")
@@ -111,7 +111,7 @@ def rocprof_k1(bytes_per_launch, n_launch):
 
 def issue_roofline():
     """The step's compute / latency-bound kernels against their VALU issue roofline and HBM
-    traffic, from this round's committed counter passes of the same command (profiles/r04/
+    traffic, from this round's committed counter passes of the same command (profiles/r05/
     pmc_c3.json: SQ issue / wait counters and FETCH_SIZE per launch), or None."""
     try:
         pm = json.load(open(os.path.join(ROOT, PROF, "pmc_c3.json")))
@@ -480,7 +480,7 @@ def bench_c3(args, world, rank, gpu, dev, backend):
 def genome_phase(summ, ms):
     """The genome phase's rates: bwa-mem genome reads (S4's both ends + S5's split reads, one
     seed / region launch) and BLAT queries (S6) over the phase's wall time, and the HBM bytes per
-    genome read of its kernels from the committed FETCH_SIZE pass (profiles/r04/pmc_c3.json)."""
+    genome read of its kernels from the committed FETCH_SIZE pass (profiles/r05/pmc_c3.json)."""
     q, n6 = summ.get("queries_s4_s5", 0), summ.get("s6_queries", 0)
     out = {"ms": round(ms, 3), "bwa_genome_reads": q, "blat_queries": n6,
            "bwa_genome_reads_per_s": round(q / (ms * 1e-3), 1) if ms else None,
