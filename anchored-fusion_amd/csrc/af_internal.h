@@ -19,8 +19,11 @@
 #ifndef AF_G1_HEAVY_EXT
 #define AF_G1_HEAVY_EXT 2048    // G1: a read past this many FM extensions moves to the wave-per-read kernel (env AF_G1_HEAVY_EXT)
 #endif
+#ifndef AF_S2_SPEC_WINDOWS
+#define AF_S2_SPEC_WINDOWS 4    // S2 K3c: pairs with this many rescue windows run their SWs as grid jobs (env AF_S2_SPEC_WINDOWS)
+#endif
 #ifndef AF_G_PE_SPEC_WINDOWS
-#define AF_G_PE_SPEC_WINDOWS 4  // S4: pairs with this many rescue windows run their SWs as grid jobs (env AF_G_PE_SPEC_WINDOWS)
+#define AF_G_PE_SPEC_WINDOWS 2  // S4: pairs with this many rescue windows run their SWs as grid jobs (env AF_G_PE_SPEC_WINDOWS)
 #endif
 #ifndef AF_G_HEAVY_CHAINS
 #define AF_G_HEAVY_CHAINS 16    // G2: reads with this many kept chains extend them one job per chain (env AF_G_HEAVY_CHAINS)
@@ -132,6 +135,20 @@ struct S2Pes {
     int32_t low, high, failed, pad;
     double avg, std;
 };
+// Heavy pairs of S2 / S4 (at least min_windows mate-rescue windows, mem_matesw calls): their
+// rescue SWs (ksw_align2 per window and direction) run as grid-wide jobs (k_s2_pe_jobs /
+// k_g_pe_jobs) before a wave per pair finishes it with their results (k_s2_pairs / k_g_pe, mode 2)
+constexpr int AF_G_PE_RES_W = 8;  // ints per (window, direction) result: sc te qe tb qb ran
+struct GPeSpec {
+    int32_t *pair;                    // [cap_pairs] the pair (S2: its pair-list item; -1: reservation failed)
+    int32_t *off;                     // [cap_pairs] its first window slot
+    int32_t *nj;                      // [cap_pairs] its windows per end: n0 | n1 << 16
+    int2 *job;                        // [cap_jobs] window slot -> {heavy pair, i << 16 | j} (y -1: none)
+    int32_t *res;                     // [cap_jobs * 4 * AF_G_PE_RES_W] results per slot and direction
+    unsigned long long *cnt;          // [0] heavy pairs, [1] slots, [2] job / [3] finish dequeue, [4] slots written below
+    int64_t cap_pairs = 0, cap_jobs = 0;
+    int32_t min_windows = 0;          // 0: every pair rescued by its own wave
+};
 // bwa options of the paired-end path that af_params does not carry (af_pe)
 struct S2Opt {
     int32_t pen_unpaired, max_ins, max_matesw, split_width, max_mem_intv, max_chain_gap;
@@ -154,6 +171,7 @@ struct S2Work {
     int32_t max_chunks;
     int32_t *heads_k2, *heads_k3;  // per-XCD dequeue heads (8 lines each)
     void *plan;         // per listed pair: the record choice of K3c for K3d (s2.hip S2Plan)
+    GPeSpec sp{};       // K3c's heavy pairs (rescue SWs as jobs)
 };
 
 // split-read tails output (af_split_tails_device / af_align_candidates_tails_device)
@@ -237,20 +255,6 @@ struct GHeavy {
     unsigned long long *cnt;          // [0] heavy reads, [1] chains, [2] seeds, [3] job / [4] finish dequeue
     int64_t cap_reads, cap_ch, cap_sd;
     int32_t min_chains;               // 0: every read extended by its own wave
-};
-// S4's heavy pairs (at least min_windows mate-rescue windows, mem_matesw calls): their rescue
-// SWs (ksw_align2 per window and direction) run as grid-wide jobs (k_g_pe_jobs) before a wave per
-// pair finishes it with their results (k_g_pe, pass 2)
-constexpr int AF_G_PE_RES_W = 8;  // ints per (window, direction) result: sc te qe tb qb ran
-struct GPeSpec {
-    int32_t *pair;                    // [cap_pairs] the pair (-1: reservation failed)
-    int32_t *off;                     // [cap_pairs] its first window slot
-    int32_t *nj;                      // [cap_pairs] its windows per end: n0 | n1 << 16
-    int2 *job;                        // [cap_jobs] window slot -> {heavy pair, i << 16 | j} (y -1: none)
-    int32_t *res;                     // [cap_jobs * 4 * AF_G_PE_RES_W] results per slot and direction
-    unsigned long long *cnt;          // [0] heavy pairs, [1] slots, [2] job / [3] finish dequeue, [4] slots written below
-    int64_t cap_pairs = 0, cap_jobs = 0;
-    int32_t min_windows = 0;          // 0: every pair rescued by its own wave
 };
 // per-call pools and counters of the genome kernels (per context)
 struct GWork {

@@ -85,6 +85,8 @@ struct af_ctx {
     int32_t g_heavy_min = AF_G_HEAVY_CHAINS;
     GPeSpec g_pe{};
     int32_t g_pe_min = AF_G_PE_SPEC_WINDOWS;
+    GPeSpec s2_sp{};
+    int32_t s2_sp_min = AF_S2_SPEC_WINDOWS;
     int32_t g1_max_ext = AF_G1_HEAVY_EXT;
     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
     int32_t g2_first_occ = AF_G2_FIRST_OCC;
@@ -396,6 +398,17 @@ int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bas
         HIPCHK(c, hipMalloc(&c->s2_plist, sizeof(int32_t) * cap));
         HIPCHK(c, hipMalloc(&c->s2_scan, sizeof(int64_t) * cap));
         HIPCHK(c, hipMalloc(&c->s2_plan, af_s2_plan_bytes() * cap));
+        // K3c's heavy pairs: one in 32 listed pairs, 16 window slots each on average
+        GPeSpec &e = c->s2_sp;
+        af_free(e.pair); af_free(e.off); af_free(e.nj); af_free(e.job); af_free(e.res);
+        e.pair = e.off = e.nj = e.res = nullptr; e.job = nullptr;
+        e.cap_pairs = std::max<int64_t>(cap / 32, 1024); e.cap_jobs = 16 * e.cap_pairs;
+        HIPCHK(c, hipMalloc(&e.pair, sizeof(int32_t) * e.cap_pairs));
+        HIPCHK(c, hipMalloc(&e.off, sizeof(int32_t) * e.cap_pairs));
+        HIPCHK(c, hipMalloc(&e.nj, sizeof(int32_t) * e.cap_pairs));
+        HIPCHK(c, hipMalloc(&e.job, sizeof(int2) * e.cap_jobs));
+        HIPCHK(c, hipMalloc(&e.res, sizeof(int32_t) * 4 * AF_G_PE_RES_W * e.cap_jobs));
+        if (!e.cnt) HIPCHK(c, hipMalloc(&e.cnt, 8 * sizeof(unsigned long long)));
         c->s2_cap_pairs = cap;
     }
     const int64_t mc = std::min<int64_t>(n_pairs, 2 * n_pairs * (int64_t)stride / std::max<int64_t>(chunk_bases, 1) + 2) + 1;
@@ -636,6 +649,7 @@ int af_ctx_create(int device, af_ctx **out) {
     c->n_slots = c->n_cu * 4 * AF_K2_WPS;  // k_align: AF_K2_WPS waves per SIMD (VGPR and LDS budget)
     if (const char *hv = getenv("AF_G_HEAVY_CHAINS")) c->g_heavy_min = std::max(0, atoi(hv));  // tests: 1 = every read
     if (const char *pw = getenv("AF_G_PE_SPEC_WINDOWS")) c->g_pe_min = std::max(0, atoi(pw));  // tests: 1 = every rescuing pair
+    if (const char *sw = getenv("AF_S2_SPEC_WINDOWS")) c->s2_sp_min = std::max(0, atoi(sw));
     if (const char *hv = getenv("AF_BLAT_HEAVY_CLUMPS")) c->blat_heavy_min = std::max(0, atoi(hv));  // 0: none deferred
     if (const char *go = getenv("AF_G2_FIRST_OCC")) c->g2_first_occ = std::max(0, atoi(go));
     if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
@@ -667,6 +681,8 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g_hv.ch); af_free(c->g_hv.sd); af_free(c->g_hv.res); af_free(c->g_hv.cnt);
     af_free(c->g_pe.pair); af_free(c->g_pe.off); af_free(c->g_pe.nj); af_free(c->g_pe.job); af_free(c->g_pe.res);
     af_free(c->g_pe.cnt);
+    af_free(c->s2_sp.pair); af_free(c->s2_sp.off); af_free(c->s2_sp.nj); af_free(c->s2_sp.job); af_free(c->s2_sp.res);
+    af_free(c->s2_sp.cnt);
     af_free(c->g2_list); af_free(c->g2_flag);
     if (c->g_ev) (void)hipEventDestroy(c->g_ev);
     af_free(c->g1_scr); af_free(c->g2_scr); af_free(c->g_iv); af_free(c->g_reg); af_free(c->g_iv_fill);
@@ -907,6 +923,8 @@ static int align_candidates(af_ctx *c, af_index *ix, const uint8_t *d_reads, int
     }
     w.heads_k2 = c->ctrl + AF_CTRL_HEADS2; w.heads_k3 = c->ctrl + AF_CTRL_S2_HEADS3;
     w.plan = c->s2_plan;
+    w.sp = c->s2_sp;
+    w.sp.min_windows = c->s2_sp.cnt ? c->s2_sp_min : 0;
     S2Opt opt{pe.pen_unpaired, pe.max_ins, pe.max_matesw, pe.split_width, pe.max_mem_intv, pe.max_chain_gap, pe.pair_base};
     if (d_lens)
         HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, pe.chunk_bases, c->s2_cstart, c->s2_scan,

@@ -1085,6 +1085,7 @@ __global__ __launch_bounds__(CLS_THREADS) void k_s2_classify(int64_t n_pairs, in
     if (blockIdx.x == 0 && tid < 8) {  // K2 ran; the previous call's K3c ran
         w.heads_k2[AF_HEAD_STRIDE * tid] = 0;
         w.heads_k3[AF_HEAD_STRIDE * tid] = 0;
+        if (tid < 5 && w.sp.cnt) w.sp.cnt[tid] = tid == 4 ? 1ull << 62 : 0;  // K3c's heavy-pair counters
     }
     if (tid == 0) nl = 0;
     __syncthreads();
@@ -1293,9 +1294,58 @@ __device__ int s2_dedup_nopatch(PeReg *a, int n, int max_chain_gap) {
     return n ? mm : 0;
 }
 
+// mem_matesw's window of direction r for a mate region starting at a_rb (the rescued read l_ms
+// long): [rb, re) clipped to the strand's half of the doubled text; true when bwa runs its SW there
+__device__ __forceinline__ bool s2_mate_window(int64_t l_pac, const af_params &p, const S2Pes &pe, int r,
+                                               int64_t a_rb, int l_ms, int64_t &rb, int64_t &re, int &rid) {
+    const bool is_rev = (r >> 1) != (r & 1);
+    const bool is_larger = !(r >> 1);
+    if (!is_rev) {
+        rb = is_larger ? a_rb + pe.low : a_rb - pe.high;
+        re = (is_larger ? a_rb + pe.high : a_rb - pe.low) + l_ms;
+    } else {
+        rb = (is_larger ? a_rb + pe.low : a_rb - pe.high) - l_ms;
+        re = is_larger ? a_rb + pe.high : a_rb - pe.low;
+    }
+    if (rb < 0) rb = 0;
+    if (re > l_pac << 1) re = l_pac << 1;
+    if (rb < re) {
+        const int64_t mid = (rb + re) >> 1;
+        const int64_t fb = mid < l_pac ? 0 : l_pac, fe = mid < l_pac ? l_pac : l_pac << 1;
+        rb = rb > fb ? rb : fb;
+        re = re < fe ? re : fe;
+        rid = 0;
+    }
+    // (rb >= re keeps rid from an earlier direction, as bwa does; re - rb < min_seed_len then)
+    return rid == 0 && re - rb >= p.min_seed_len;
+}
+
+// that window's ksw_align2 for the rescued read's codes qc (strand of direction r)
+__device__ __forceinline__ void s2_mate_ksw(const DevText &X, const af_params &p, const uint8_t *qc, int l_ms, int r,
+                                            int64_t rb, int64_t re, int &sc, int &te, int &qe, int &tb, int &qb,
+                                            int lane) {
+    PeLds &E = g_pe;
+    const bool is_rev = (r >> 1) != (r & 1);
+    for (int x = lane; x < l_ms; x += 64) {
+        const int c = qc[is_rev ? l_ms - 1 - x : x];
+        E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
+    }
+    const bool staged = re - rb <= PE_TW;
+    if (staged)
+        for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = X.T[rb + x];
+    wave_sync();
+    const int P = l_ms * p.a < 250 ? 16 : 8;
+    SPROF(if (lane == 0) E.misc[7] += (int)(re - rb);)
+    s2_ksw_align2(E.rq, l_ms, staged ? E.tw : X.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe, tb, qb,
+                  lane);
+}
+
 // mem_matesw (oracle mem_matesw): rescue read mi in the insert-size window of a region at a_rb
-// of its mate.  Returns false on a region-cap overflow of read mi.
-__device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, int mi, int64_t a_rb, int lane) {
+// of its mate.  sr: the windows' SW results computed ahead (k_s2_pe_jobs; 4 directions x
+// AF_G_PE_RES_W ints) or null.  Returns false on a region-cap overflow of read mi.
+template <bool SPEC>
+__device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, int mi, int64_t a_rb,
+                          const int32_t *sr, int lane) {
     PeLds &E = g_pe;
     const int64_t l_pac = X.n;
     const int l_ms = E.len[mi];
@@ -1311,38 +1361,15 @@ __device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, 
     for (int r = 0; r < 4; ++r) {
         if (skip[r]) continue;
         const bool is_rev = (r >> 1) != (r & 1);
-        const bool is_larger = !(r >> 1);
         int64_t rb, re;
-        if (!is_rev) {
-            rb = is_larger ? a_rb + E.pes[r].low : a_rb - E.pes[r].high;
-            re = (is_larger ? a_rb + E.pes[r].high : a_rb - E.pes[r].low) + l_ms;
-        } else {
-            rb = (is_larger ? a_rb + E.pes[r].low : a_rb - E.pes[r].high) - l_ms;
-            re = is_larger ? a_rb + E.pes[r].high : a_rb - E.pes[r].low;
-        }
-        if (rb < 0) rb = 0;
-        if (re > l_pac << 1) re = l_pac << 1;
-        if (rb < re) {
-            const int64_t mid = (rb + re) >> 1;
-            const int64_t fb = mid < l_pac ? 0 : l_pac, fe = mid < l_pac ? l_pac : l_pac << 1;
-            rb = rb > fb ? rb : fb;
-            re = re < fe ? re : fe;
-            rid = 0;
-        }
-        if (rid == 0 && re - rb >= p.min_seed_len) {
-            for (int x = lane; x < l_ms; x += 64) {
-                const int c = E.q[mi][is_rev ? l_ms - 1 - x : x];
-                E.rq[x] = (uint8_t)(is_rev ? (c < 4 ? 3 - c : 4) : c);
-            }
-            const bool staged = re - rb <= PE_TW;
-            if (staged)
-                for (int x = lane; x < (int)(re - rb); x += 64) E.tw[x] = X.T[rb + x];
-            wave_sync();
-            const int P = l_ms * p.a < 250 ? 16 : 8;
-            SPROF(if (lane == 0) E.misc[7] += (int)(re - rb);)
+        if (s2_mate_window(l_pac, p, E.pes[r], r, a_rb, l_ms, rb, re, rid)) {
             int sc, te, qe, tb, qb;
-            s2_ksw_align2(E.rq, l_ms, staged ? E.tw : X.T + rb, (int)(re - rb), P, p.min_seed_len * p.a, p, sc, te, qe,
-                          tb, qb, lane);
+            const int32_t *res = SPEC && sr ? sr + r * AF_G_PE_RES_W : nullptr;
+            if (SPEC && res && res[5]) {
+                sc = res[0]; te = res[1]; qe = res[2]; tb = res[3]; qb = res[4];
+            } else {
+                s2_mate_ksw(X, p, E.q[mi], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
+            }
             if (sc >= p.min_seed_len && qb >= 0) {
                 bool ok = true;
                 if (lane == 0) {
@@ -1456,6 +1483,9 @@ __device__ int s2_mem_pair(int64_t l_pac, const af_params &p, const S2Pes *pes, 
 
 // K3c: mem_sam_pe up to the record choice for every listed pair (one wave per pair): mate
 // rescue, primary marking, pairing; the choice (S2Plan) goes to K3d
+// mode 0: every listed pair; 1: every listed pair, those with at least w.sp.min_windows rescue
+// windows left to k_s2_pe_jobs (their SWs) and mode 2 (the rest, with those SWs' results)
+template <int mode>
 __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
                                                  const int32_t *__restrict__ lens, af_params p, S2Opt o,
                                                  const int32_t *__restrict__ hits, S2Work w,
@@ -1464,19 +1494,38 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
     const int lane = threadIdx.x;
     const int64_t l_pac = X.n;
     const int npl = *w.n_plist;
+    const GPeSpec &Y = w.sp;
+    int64_t nh = 0;
+    if constexpr (mode == 2) {
+        nh = (int64_t)Y.cnt[0];
+        if (nh > Y.cap_pairs) nh = Y.cap_pairs;
+    }
     int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
         int item = npl;
-        while (heads_left > 0) {
-            int v = 0;
-            if (lane == 0) v = atomicAdd(&w.heads_k3[AF_HEAD_STRIDE * head], 1);
-            v = __builtin_amdgcn_readfirstlane(v);
-            const int64_t it = head + 8 * (int64_t)v;
-            if (it < npl) { item = (int)it; break; }
-            head = (head + 1) & 7;
-            --heads_left;
+        const int32_t *sres = nullptr;  // mode 2: the pair's precomputed SW results
+        int nj0 = 0;
+        if constexpr (mode == 2) {
+            int64_t hp = 0;
+            if (lane == 0) hp = (int64_t)atomicAdd(&Y.cnt[3], 1ull);
+            hp = (int64_t)__builtin_amdgcn_readfirstlane((int)hp);
+            if (hp >= nh) break;
+            item = Y.pair[hp];
+            if (item < 0) continue;  // reservation failed: mode 1 finished the pair
+            sres = Y.res + (int64_t)Y.off[hp] * 4 * AF_G_PE_RES_W;
+            nj0 = Y.nj[hp] & 0xffff;
+        } else {
+            while (heads_left > 0) {
+                int v = 0;
+                if (lane == 0) v = atomicAdd(&w.heads_k3[AF_HEAD_STRIDE * head], 1);
+                v = __builtin_amdgcn_readfirstlane(v);
+                const int64_t it = head + 8 * (int64_t)v;
+                if (it < npl) { item = (int)it; break; }
+                head = (head + 1) & 7;
+                --heads_left;
+            }
+            if (item >= npl) break;
         }
-        if (item >= npl) break;
         const int64_t pp = w.plist[item];
         S2DBG("k3c pair %d start\n", (int)pp);
         SPROF(const int64_t c0 = clock64(); int64_t c1 = c0, c2 = c0, c3 = c0; int nsw = 0;)
@@ -1518,11 +1567,45 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
             }
         }
         wave_sync();
+        if constexpr (mode == 1) {
+            // a heavy pair's windows to the job list (slot k: end i, its j-th top region); the pair
+            // is finished by mode 2
+            const int n0 = E.nb[0] < o.max_matesw ? E.nb[0] : o.max_matesw;
+            const int n1 = E.nb[1] < o.max_matesw ? E.nb[1] : o.max_matesw;
+            const int nwin = (E.ovf[1] ? 0 : n0) + (E.ovf[0] ? 0 : n1);
+            if (nwin >= Y.min_windows) {
+                int hp = -1, off = 0;
+                if (lane == 0) {
+                    const int64_t h = (int64_t)atomicAdd(&Y.cnt[0], 1ull);
+                    if (h < Y.cap_pairs) {
+                        const int64_t o0 = (int64_t)atomicAdd(&Y.cnt[1], (unsigned long long)(n0 + n1));
+                        if (o0 + n0 + n1 <= Y.cap_jobs) {
+                            hp = (int)h; off = (int)o0;
+                            Y.pair[h] = item; Y.off[h] = off; Y.nj[h] = n0 | n1 << 16;
+                        } else {
+                            Y.pair[h] = -1;
+                            atomicMin(&Y.cnt[4], (unsigned long long)o0);  // slots from o0 on are unwritten
+                        }
+                    }
+                }
+                hp = __builtin_amdgcn_readfirstlane(hp);
+                off = __builtin_amdgcn_readfirstlane(off);
+                if (hp >= 0) {
+                    for (int k = lane; k < n0 + n1; k += 64) {
+                        const int i = k >= n0, j = k - (i ? n0 : 0);
+                        Y.job[off + k] = make_int2(hp, E.ovf[!i] ? -1 : (i << 16 | j));
+                    }
+                    wave_sync();
+                    continue;
+                }
+            }
+        }
         SPROF(c1 = clock64(); if (lane == 0) E.misc[7] = 0;)
         for (int i = 0; i < 2; ++i)
             for (int j = 0; j < E.nb[i] && j < o.max_matesw; ++j) {
                 if (E.ovf[!i]) continue;
-                if (!s2_matesw(X, p, o, !i, E.brb[i][j], lane)) {
+                const int32_t *sr = sres ? sres + (int64_t)((i ? nj0 : 0) + j) * 4 * AF_G_PE_RES_W : nullptr;
+                if (!s2_matesw<mode == 2>(X, p, o, !i, E.brb[i][j], sr, lane)) {
                     wave_sync();
                     if (lane == 0) { E.ovf[!i] = 1; E.na[!i] = 0; }
                     wave_sync();
@@ -1589,6 +1672,82 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
             pf[4] = (int32_t)(c3 - c2); pf[6] = nsw; pf[7] = E.na[0]; pf[8] = E.na[1];
         })
         wave_sync();
+    }
+}
+
+// one rescue window of a heavy pair per wave (k_s2_pairs mode 1's job list): for each direction
+// bwa may search, the window and its ksw_align2 as mem_matesw computes them (results ahead of the
+// pair's own walk, which decides per window whether to use them)
+__global__ __launch_bounds__(64, 4) void k_s2_pe_jobs(DevText X, const uint8_t *__restrict__ reads, int32_t stride,
+                                                    const int32_t *__restrict__ lens, af_params p, S2Opt o,
+                                                    const int32_t *__restrict__ hits, S2Work w) {
+    PeLds &E = g_pe;
+    const int lane = threadIdx.x;
+    const GPeSpec &Y = w.sp;
+    int64_t n = (int64_t)Y.cnt[1];
+    if (n > Y.cap_jobs) n = Y.cap_jobs;
+    if (n > (int64_t)Y.cnt[4]) n = (int64_t)Y.cnt[4];
+    for (;;) {
+        int64_t k = 0;
+        if (lane == 0) k = (int64_t)atomicAdd(&Y.cnt[2], 1ull);
+        k = (int64_t)__builtin_amdgcn_readfirstlane((int)k);
+        if (k >= n) break;
+        const int2 jb = Y.job[k];
+        if (jb.y < 0) continue;
+        const int i = jb.y >> 16, j = jb.y & 0xffff;
+        const int64_t pp = w.plist[Y.pair[jb.x]];
+        int32_t *out = Y.res + k * 4 * AF_G_PE_RES_W;
+        // the rescued read (the other end) and its codes
+        const int64_t rm = 2 * pp + !i;
+        int l_ms = lens ? lens[rm] : stride;
+        if (l_ms > stride) l_ms = stride;
+        if (l_ms > AF_MAX_READ) l_ms = AF_MAX_READ;
+        if (l_ms < 0) l_ms = 0;
+        for (int x = lane; x < l_ms; x += 64) {
+            const uint8_t ch = reads[rm * (int64_t)stride + x];
+            E.q[0][x] = ch == 'A' || ch == 'a' ? 0 : ch == 'C' || ch == 'c' ? 1 : ch == 'G' || ch == 'g' ? 2
+                      : ch == 'T' || ch == 't' ? 3 : 4;
+        }
+        if (lane < 4) E.pes[lane] = w.pes[(int64_t)s2_chunk_of(w, pp) * 4 + lane];
+        // a_rb: end i's j-th region scoring within pen_unpaired of its best (K3c's list)
+        const int64_t ri = 2 * pp + i;
+        const int h = hits[ri];
+        const int2 mp = h > 0 ? w.rmap[ri] : int2{0, 0};
+        const int na = mp.y > 0 ? mp.y : 0;
+        const S2Reg *ai = w.pool + mp.x;
+        const int top = na ? ai[0].score : 0;
+        int seen = 0, at = -1;
+        for (int c0 = 0; c0 < na && at < 0; c0 += 64) {
+            const bool q = c0 + lane < na && ai[c0 + lane].score >= top - o.pen_unpaired;
+            const uint64_t m = __ballot(q);
+            const int cnt = __builtin_popcountll(m);
+            if (seen + cnt > j) {
+                uint64_t mm = m;
+                for (int t = 0; t < j - seen; ++t) mm &= mm - 1;
+                at = c0 + __builtin_ctzll(mm);
+            }
+            seen += cnt;
+        }
+        wave_sync();
+        if (at < 0) {  // (no such region: never used)
+            if (lane < 4) out[lane * AF_G_PE_RES_W + 5] = 0;
+            continue;
+        }
+        const int64_t a_rb = ai[at].rb;
+        int rid = -1;
+        for (int r = 0; r < 4; ++r) {
+            int64_t rb, re;
+            int ran = 0, sc = 0, te = 0, qe = 0, tb = 0, qb = 0;
+            if (!E.pes[r].failed && s2_mate_window(X.n, p, E.pes[r], r, a_rb, l_ms, rb, re, rid)) {
+                s2_mate_ksw(X, p, E.q[0], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
+                ran = 1;
+            }
+            if (lane == 0) {
+                int32_t *o_ = out + r * AF_G_PE_RES_W;
+                o_[0] = sc; o_[1] = te; o_[2] = qe; o_[3] = tb; o_[4] = qb; o_[5] = ran;
+            }
+            wave_sync();
+        }
     }
 }
 
@@ -1825,7 +1984,13 @@ hipError_t af_launch_s2(const DevText &X, const uint8_t *reads, int64_t n_pairs,
                        o.max_ins);
     const AfTails t = tails ? *tails : AfTails{};
     S2Plan *plan = static_cast<S2Plan *>(w.plan);
-    hipLaunchKernelGGL(k_s2_pairs, g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, plan);
+    if (w.sp.min_windows > 0) {
+        hipLaunchKernelGGL(k_s2_pairs<1>, g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, plan);
+        hipLaunchKernelGGL(k_s2_pe_jobs, dim3(2 * g3.x), b, 0, s, X, reads, stride, lens, p, o, hits, w);
+        hipLaunchKernelGGL(k_s2_pairs<2>, g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, plan);
+    } else {
+        hipLaunchKernelGGL(k_s2_pairs<0>, g3, b, 0, s, X, reads, stride, lens, p, o, hits, w, plan);
+    }
 #define AF_GO(C) hipLaunchKernelGGL((k_s2_records<C>), g4, b, 0, s, X, reads, stride, lens, p, w, plan, out, zscratch, \
                                     zstride, t, tails ? 1 : 0)
     if (cpl <= 2) AF_GO(2);

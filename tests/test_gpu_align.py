@@ -326,3 +326,19 @@ def test_partition_device_on_s2_records(aligner, anchor):
     assert c[2] > 1000
     for g, k, w in zip((t1, t2, an), c, want):
         assert np.array_equal(g[:k].cpu().numpy(), w)
+
+
+@pytest.mark.parametrize("windows", ["1", "3"])
+def test_k3c_rescue_jobs_parity(anchor, oidx, monkeypatch, windows):
+    """K3c's heavy pairs (at least AF_S2_SPEC_WINDOWS mate-rescue windows, read when the context
+    is made): their rescue SWs computed ahead as grid-wide jobs (k_s2_pe_jobs), the pair's walk
+    taking the results (k_s2_pairs mode 2) -- every record equal to the oracle's, on the rescue,
+    tandem-repeat and fusion-rich cases."""
+    from anchored_fusion_amd.align import AnchorAligner
+    from cases import rescue_pairs, tandem_pairs
+    monkeypatch.setenv("AF_S2_SPEC_WINDOWS", windows)
+    sets = [rescue_pairs(anchor)[0], tandem_pairs(anchor), synthetic_pairs(anchor, 3000, 150, seed=71, fusion_frac=0.9)[0]]
+    with AnchorAligner(anchor, device=0) as a:
+        for reads in sets:
+            g, r = _both(a, oidx, reads)
+            assert_records_equal(g, r, reads)
