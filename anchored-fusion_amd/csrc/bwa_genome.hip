@@ -965,6 +965,9 @@ __device__ int g_chain_weight(const G2Scr &S, const GChain &c) {
 struct GLtFlt {
     __device__ bool operator()(const GChain &a, const GChain &b) const { return a.w > b.w; }
 };
+struct GKeyFlt {  // w << 32 | index: GLtFlt on the keys
+    __device__ bool operator()(uint64_t a, uint64_t b) const { return (a >> 32) > (b >> 32); }
+};
 
 // mem_chain_flt (oracle mem_chain_flt) over S.ch2 on the wave: returns the kept count.  The
 // chains' weights, query spans and the overlap scan against the kept list are lane-parallel (the
@@ -980,7 +983,26 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
         a[i] = c;
     }
     wave_sync();
-    if (lane == 0) ks_introsort(a, n_chn, GLtFlt());
+    if (n_chn <= (int)(sizeof(G2Box) * G2_BOXES / sizeof(uint64_t))) {
+        // lane 0's introsort over (w, index) keys in LDS (the boxes, free until chain2aln) instead
+        // of 32-B chains in scratch: the swaps depend only on the comparator's answers, so the
+        // order, ties included, is the one the introsort over the chains gives; the wave then
+        // moves the chains in key order through S.ch (free after mem_chain)
+        uint64_t *key = reinterpret_cast<uint64_t *>(g_box);
+        for (int i = lane; i < n_chn; i += 64) key[i] = (uint64_t)(uint32_t)a[i].w << 32 | (uint32_t)i;
+        __threadfence_block();
+        wave_sync();
+        if (lane == 0) ks_introsort(key, n_chn, GKeyFlt());
+        __threadfence_block();
+        wave_sync();
+        for (int i = lane; i < n_chn; i += 64) S.ch[i] = a[(uint32_t)key[i]];
+        __threadfence_block();
+        wave_sync();
+        for (int i = lane; i < n_chn; i += 64) a[i] = S.ch[i];
+    } else if (lane == 0) {
+        ks_introsort(a, n_chn, GLtFlt());
+    }
+    __threadfence_block();
     wave_sync();
     int32_t *cb = S.last_of, *ce = S.order, *cw = S.next;  // free after mem_chain
     for (int i = lane; i < n_chn; i += 64) {
