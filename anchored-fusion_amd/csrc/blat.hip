@@ -309,35 +309,46 @@ __device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int6
     gen_cigar_wave<CPL>(X.T, (int64_t)1 << 62, P, w2, lq, qb, tb, te, D, zg, lane);
     const int nc = D.misc[2];
     if (nc > AF_MAX_CIGAR) return false;
+    // the blocks from the CIGAR (the ring holds the ops in reverse order: forward op x is
+    // ring[(nc - 1 - x) & 63]), walked by the whole wave; each block's bases counted lane-parallel
+    // from the LDS copies gen_cigar_wave staged (D.t[i] = T[tb + i], D.q the strand's codes)
+    const int64_t tb0 = tb;
+    int xs = 0, xe = nc;
+    const uint32_t f0 = nc > 0 ? D.ring[(nc - 1) & 63] : 0u, fl = nc > 0 ? D.ring[0] : 0u;
+    if (nc > 0 && (f0 & 0xf) == 2) { tb += f0 >> 4; xs = 1; }
+    else if (nc > 0 && (fl & 0xf) == 2) { te -= fl >> 4; xe = nc - 1; }
+    Reg o{};  // lane 63's (the one writing r)
     bool ok = true;
-    if (lane == 0) {
-        // ring holds the ops in reverse order: forward op x is ring[(nc - 1 - x) & 63]
-        int xs = 0, xe = nc;
-        const uint32_t f0 = nc > 0 ? D.ring[(nc - 1) & 63] : 0u, fl = nc > 0 ? D.ring[0] : 0u;
-        if (nc > 0 && (f0 & 0xf) == 2) { tb += f0 >> 4; xs = 1; }
-        else if (nc > 0 && (fl & 0xf) == 2) { te -= fl >> 4; xe = nc - 1; }
-        Reg o{};
+    int nmat = 0, nmis = 0, nn = 0, nb = 0, qni = 0, qbi = 0, tni = 0, tbi = 0;
+    {
         int32_t x = qb;
         int64_t y = tb;
-        for (int k = xs; k < xe && ok; ++k) {
+        for (int k = xs; k < xe; ++k) {
             const uint32_t op4 = D.ring[(nc - 1 - k) & 63];
             const int len = (int)(op4 >> 4), op = (int)(op4 & 0xf);
             if (op == 0) {
-                if (o.nb >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
-                o.bsz[o.nb] = len; o.bq[o.nb] = x; o.bt[o.nb] = y; ++o.nb;
-                for (int u = 0; u < len; ++u) {
-                    const uint8_t a = D.q[x + u], b = X.T[y + u];
-                    if (a > 3 || b > 3) ++o.ncount;
-                    else if (a == b) ++o.matches;
-                    else ++o.mismatches;
+                if (nb >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
+                if (lane == 63) { o.bsz[nb] = len; o.bq[nb] = x; o.bt[nb] = y; }
+                ++nb;
+                const uint8_t *tq = D.q + x, *tt = D.t + (y - tb0);
+                for (int u = lane; u < len; u += 64) {
+                    const uint8_t a = tq[u], b = tt[u];
+                    if (a > 3 || b > 3) ++nn;
+                    else if (a == b) ++nmat;
+                    else ++nmis;
                 }
                 x += len; y += len;
             } else if (op == 1) {
-                ++o.qni; o.qbi += len; x += len;
+                ++qni; qbi += len; x += len;
             } else {
-                ++o.tni; o.tbi += len; y += len;
+                ++tni; tbi += len; y += len;
             }
         }
+    }
+    nmat = wave_incl_sum(nmat, lane); nmis = wave_incl_sum(nmis, lane); nn = wave_incl_sum(nn, lane);
+    if (lane == 63) {
+        o.nb = nb; o.qni = qni; o.qbi = qbi; o.tni = tni; o.tbi = tbi;
+        o.matches = nmat; o.mismatches = nmis; o.ncount = nn;
         if (o.nb == 0) ok = false;
         o.qb = qb; o.qe = qe; o.tb = tb; o.te = te;
         o.score = o.matches - o.mismatches - o.qni - o.tni;
