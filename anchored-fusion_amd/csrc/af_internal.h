@@ -23,7 +23,7 @@
 #define AF_S2_SPEC_WINDOWS 4    // S2 K3c: pairs with this many rescue windows run their SWs as grid jobs (env AF_S2_SPEC_WINDOWS)
 #endif
 #ifndef AF_G_PE_SPEC_WINDOWS
-#define AF_G_PE_SPEC_WINDOWS 2  // S4: pairs with this many rescue windows run their SWs as grid jobs (env AF_G_PE_SPEC_WINDOWS)
+#define AF_G_PE_SPEC_WINDOWS 4  // S4: pairs with this many rescue windows run their SWs as grid jobs (env AF_G_PE_SPEC_WINDOWS)
 #endif
 #ifndef AF_G_HEAVY_CHAINS
 #define AF_G_HEAVY_CHAINS 16    // G2: reads with this many kept chains extend them one job per chain (env AF_G_HEAVY_CHAINS)

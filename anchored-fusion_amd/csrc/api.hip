@@ -398,11 +398,11 @@ int ensure_s2_work(af_ctx *c, int64_t n_pairs, int32_t stride, int64_t chunk_bas
         HIPCHK(c, hipMalloc(&c->s2_plist, sizeof(int32_t) * cap));
         HIPCHK(c, hipMalloc(&c->s2_scan, sizeof(int64_t) * cap));
         HIPCHK(c, hipMalloc(&c->s2_plan, af_s2_plan_bytes() * cap));
-        // K3c's heavy pairs: one in 32 listed pairs, 16 window slots each on average
+        // K3c's heavy pairs: one in 8 of the batch's pairs, 16 window slots each on average
         GPeSpec &e = c->s2_sp;
         af_free(e.pair); af_free(e.off); af_free(e.nj); af_free(e.job); af_free(e.res);
         e.pair = e.off = e.nj = e.res = nullptr; e.job = nullptr;
-        e.cap_pairs = std::max<int64_t>(cap / 32, 1024); e.cap_jobs = 16 * e.cap_pairs;
+        e.cap_pairs = std::max<int64_t>(cap / 8, 1024); e.cap_jobs = 16 * e.cap_pairs;
         HIPCHK(c, hipMalloc(&e.pair, sizeof(int32_t) * e.cap_pairs));
         HIPCHK(c, hipMalloc(&e.off, sizeof(int32_t) * e.cap_pairs));
         HIPCHK(c, hipMalloc(&e.nj, sizeof(int32_t) * e.cap_pairs));
@@ -505,12 +505,13 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     HIPCHK(c, hipMalloc(&h.sd, af_g_seed_bytes() * h.cap_sd));
     HIPCHK(c, hipMalloc(&h.res, sizeof(GReg) * h.cap_sd));
     if (!h.cnt) HIPCHK(c, hipMalloc(&h.cnt, 8 * sizeof(unsigned long long)));
-    // S4's heavy pairs: one in 16 pairs of the call, 16 window slots each on average (a pair that
-    // does not fit runs its rescues on its own wave)
+    // S4's heavy pairs: up to half the call's pairs (cap counts reads), 8 window slots each on
+    // average (a pair that does not fit runs its rescues on its own wave; counted by
+    // AF_GSTAT_PE_JOBS: 1,628 of the configs[2] step's 26 k pairs hit the round's first cap of 1/32)
     GPeSpec &e = c->g_pe;
     af_free(e.pair); af_free(e.off); af_free(e.nj); af_free(e.job); af_free(e.res);
     e.pair = e.off = e.nj = e.res = nullptr; e.job = nullptr;
-    e.cap_pairs = std::max<int64_t>(cap / 32, 1024); e.cap_jobs = 16 * e.cap_pairs;
+    e.cap_pairs = std::max<int64_t>(cap / 4, 1024); e.cap_jobs = 8 * e.cap_pairs;
     HIPCHK(c, hipMalloc(&e.pair, sizeof(int32_t) * e.cap_pairs));
     HIPCHK(c, hipMalloc(&e.off, sizeof(int32_t) * e.cap_pairs));
     HIPCHK(c, hipMalloc(&e.nj, sizeof(int32_t) * e.cap_pairs));
