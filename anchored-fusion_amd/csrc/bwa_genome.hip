@@ -2106,6 +2106,10 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
     }
     if (skip[0] + skip[1] + skip[2] + skip[3] == 4) return true;
     int n = 0, rid = -1;
+    // bwa sorts and dedups the list after every searched direction once one has been searched;
+    // the dedup is idempotent on its own output (its walk drops nothing more, its final order is by
+    // unique keys), so it runs only when a rescued region went in since the last one
+    bool deduped = false, dirty = false;
     for (int r = 0; r < 4; ++r) {
         if (skip[r]) continue;
         const bool is_rev = (r >> 1) != (r & 1);
@@ -2144,10 +2148,13 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
                 }
                 wave_sync();
                 if (!E.misc[0]) return false;
+                dirty = true;
             }
             ++n;
         }
-        if (n) {
+        if (n && (!deduped || dirty)) {
+            deduped = true;
+            dirty = false;
             GPROF(const uint64_t gp_d0 = clock64();)
             const int m = g_dedup_patch<2>(G, p, o, ma, E.na[mi], false, zg, lane, reinterpret_cast<GReg *>(S.seed));
             if (lane == 0) E.na[mi] = m;

@@ -1248,50 +1248,112 @@ __device__ void s2_ksw_align2(const uint8_t *q, int qlen, const uint8_t *target,
     if (r.score == rr.score) { tb = r.te - rr.te; qb = r.qe - rr.qe; }
 }
 
-struct LtArsR {
-    __device__ bool operator()(const PeReg &a, const PeReg &b) const { return LtArs()(a.r, b.r); }
+// mem_sort_dedup_patch without patching (mate-SW context) on the wave.  The two sorts run over
+// keys (re | index; rb, score, qb | index): by rank on the wave when no two keys tie, else klib's
+// introsort on lane 0 -- its swaps depend only on the comparator's answers, so the order, ties
+// included, is the one the introsort over the regions gives.  Without patching, a[i]'s walk only
+// drops, and a[i] itself does not change along it: every overlapping q below a[i] (all of them
+// fit one wave, n <= 32) is known at once; they drop in walk order until one outscores a[i],
+// which drops a[i] instead and ends its walk.
+constexpr int PE_W8 = (int)(sizeof(PeReg) / 8);  // a region moves as this many 8-byte words
+static_assert(AF_S2_MAX_REG <= 32 && sizeof(PeReg) % 8 == 0 && sizeof(P64) * 2 * AF_S2_MAX_REG >= 32 * AF_S2_MAX_REG,
+              "the dedup moves <= 32 regions through registers; its keys fit E.v");
+struct S2KeyRe {  // re << 6 | index
+    __device__ bool operator()(uint64_t a, uint64_t b) const { return (a >> 6) < (b >> 6); }
 };
-struct LtArs2R {
-    __device__ bool operator()(const PeReg &a, const PeReg &b) const { return a.r.re < b.r.re; }
-};
-struct LtArsHash {
-    __device__ bool operator()(const PeReg &a, const PeReg &b) const {
-        return a.r.score > b.r.score || (a.r.score == b.r.score && a.hash < b.hash);
+struct S2Key16 { int64_t x; int32_t y; int32_t z; };
+struct S2KeyArs {  // x = rb, y = score, z = qb << 8 | index: score desc, rb, qb (LtArs)
+    __device__ bool operator()(const S2Key16 &a, const S2Key16 &b) const {
+        return a.y > b.y || (a.y == b.y && (a.x < b.x || (a.x == b.x && (a.z >> 8) < (b.z >> 8))));
     }
 };
+// a[k] = old a[from(k)] for k < m <= 64 (wave; through registers)
+template <class F>
+__device__ __forceinline__ void s2_regs_gather(PeReg *a, int m, F from, int lane) {
+    uint2 t[PE_W8];
+    const int f = lane < m ? from(lane) : 0;
+    if (lane < m)
+        for (int c = 0; c < PE_W8; ++c) t[c] = reinterpret_cast<const uint2 *>(a + f)[c];
+    __threadfence_block();
+    wave_sync();
+    if (lane < m)
+        for (int c = 0; c < PE_W8; ++c) reinterpret_cast<uint2 *>(a + lane)[c] = t[c];
+    __threadfence_block();
+    wave_sync();
+}
 
-// mem_sort_dedup_patch without patching (mate-SW context), lane 0
-__device__ int s2_dedup_nopatch(PeReg *a, int n, int max_chain_gap) {
+__device__ int s2_dedup_nopatch(PeReg *a, int n, int max_chain_gap, int lane) {
     if (n <= 1) return n;
-    ks_introsort(a, n, LtArs2R());
+    PeLds &E = g_pe;
+    uint64_t *k1 = reinterpret_cast<uint64_t *>(E.v), *t1 = k1 + AF_S2_MAX_REG;
+    if (lane < n) k1[lane] = (uint64_t)a[lane].r.re << 6 | (uint64_t)lane;
+    wave_sync();
+    if (!wave_rank_sort(k1, n, S2KeyRe(), t1, lane)) {
+        if (lane == 0) ks_introsort(k1, n, S2KeyRe());
+        wave_sync();
+    }
+    s2_regs_gather(a, n, [&](int k) { return (int)(k1[k] & 63); }, lane);
     for (int i = 1; i < n; ++i) {
-        PeReg &pp = a[i];
-        if (pp.r.rb >= a[i - 1].r.re + max_chain_gap) continue;
-        for (int j = i - 1; j >= 0 && pp.r.rb < a[j].r.re + max_chain_gap; --j) {
-            PeReg &q = a[j];
-            if (q.r.qe == q.r.qb) continue;
-            const int64_t or_ = q.r.re - pp.r.rb;
-            const int64_t oq = q.r.qb < pp.r.qb ? q.r.qe - pp.r.qb : pp.r.qe - q.r.qb;
-            const int64_t mr = q.r.re - q.r.rb < pp.r.re - pp.r.rb ? q.r.re - q.r.rb : pp.r.re - pp.r.rb;
-            const int64_t mq = q.r.qe - q.r.qb < pp.r.qe - pp.r.qb ? q.r.qe - q.r.qb : pp.r.qe - pp.r.qb;
-            if ((float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq) {
-                if (pp.r.score < q.r.score) { pp.r.qe = pp.r.qb; break; }
-                else q.r.qe = q.r.qb;
+        const S2Reg pp = a[i].r;
+        const int jj = i - 1 - lane;
+        bool cont = false, ev = false, win = false;
+        if (jj >= 0) {
+            const S2Reg q = a[jj].r;
+            cont = pp.rb < q.re + max_chain_gap;
+            if (cont && q.qe != q.qb) {
+                const int64_t or_ = q.re - pp.rb;
+                const int64_t oq = q.qb < pp.qb ? q.qe - pp.qb : pp.qe - q.qb;
+                const int64_t mr = q.re - q.rb < pp.re - pp.rb ? q.re - q.rb : pp.re - pp.rb;
+                const int64_t mq = q.qe - q.qb < pp.qe - pp.qb ? q.qe - q.qb : pp.qe - pp.qb;
+                ev = (float)or_ > 0.95f * (float)mr && (float)oq > 0.95f * (float)mq;
+                win = ev && pp.score < q.score;
             }
         }
+        // the walk reaches lanes below the first that leaves the window
+        const uint64_t stop = __ballot(!cont);
+        const uint64_t reach = stop ? (stop & (0ull - stop)) - 1 : ~0ull;
+        const uint64_t wm = __ballot(win) & reach;
+        // events before the first q that outscores a[i] drop their q; that q drops a[i]
+        const uint64_t before = wm ? (wm & (0ull - wm)) - 1 : reach;
+        if (ev && ((1ull << lane) & before)) a[jj].r.qe = a[jj].r.qb;
+        if (wm && lane == 0) a[i].r.qe = a[i].r.qb;
+        __threadfence_block();
+        wave_sync();
     }
-    int m = 0;
-    for (int i = 0; i < n; ++i)
-        if (a[i].r.qe > a[i].r.qb) a[m++] = a[i];
-    n = m;
-    ks_introsort(a, n, LtArsR());
-    for (int i = 1; i < n; ++i)
-        if (a[i].r.score == a[i - 1].r.score && a[i].r.rb == a[i - 1].r.rb && a[i].r.qb == a[i - 1].r.qb)
-            a[i].r.qe = a[i].r.qb;
-    int mm = 1;
-    for (int i = 1; i < n; ++i)
-        if (a[i].r.qe > a[i].r.qb) a[mm++] = a[i];
-    return n ? mm : 0;
+    // the live regions (in order) sorted by LtArs; equal neighbours dropped
+    const bool live = lane < n && a[lane].r.qe > a[lane].r.qb;
+    const uint64_t lm = __ballot(live);
+    const int m = __popcll(lm);
+    S2Key16 *k2 = reinterpret_cast<S2Key16 *>(E.v), *t2 = k2 + AF_S2_MAX_REG;
+    if (live) {
+        const int pos = __popcll(lm & ((1ull << lane) - 1));
+        const S2Reg &r = a[lane].r;
+        k2[pos] = S2Key16{r.rb, r.score, r.qb << 8 | lane};
+    }
+    wave_sync();
+    if (m == 0) return 0;
+    if (!wave_rank_sort(k2, m, S2KeyArs(), t2, lane)) {
+        if (lane == 0) ks_introsort(k2, m, S2KeyArs());
+        wave_sync();
+    }
+    bool keep = false;
+    if (lane < m) {
+        const S2Key16 x = k2[lane];
+        keep = lane == 0;
+        if (lane > 0) {
+            const S2Key16 y = k2[lane - 1];
+            keep = !(x.y == y.y && x.x == y.x && (x.z >> 8) == (y.z >> 8));
+        }
+    }
+    const uint64_t km = __ballot(keep);
+    const int mm = __popcll(km);
+    // surviving key k goes to slot popc(km below k); gather by the inverse map
+    int *src = reinterpret_cast<int *>(t2);
+    if (keep) src[__popcll(km & ((1ull << lane) - 1))] = k2[lane].z & 255;
+    __threadfence_block();
+    wave_sync();
+    s2_regs_gather(a, mm, [&](int k) { return src[k]; }, lane);
+    return mm;
 }
 
 // mem_matesw's window of direction r for a mate region starting at a_rb (the rescued read l_ms
@@ -1358,6 +1420,10 @@ __device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, 
     }
     if (skip[0] + skip[1] + skip[2] + skip[3] == 4) return true;
     int n = 0, rid = -1;
+    // bwa sorts and dedups the list after every searched direction once one has been searched;
+    // the dedup is idempotent on its own output (its walk drops nothing more, its final order is by
+    // unique keys), so it runs only when a rescued region went in since the last one
+    bool deduped = false, dirty = false;
     for (int r = 0; r < 4; ++r) {
         if (skip[r]) continue;
         const bool is_rev = (r >> 1) != (r & 1);
@@ -1371,7 +1437,20 @@ __device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, 
                 s2_mate_ksw(X, p, E.q[mi], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
             }
             if (sc >= p.min_seed_len && qb >= 0) {
-                bool ok = true;
+                // into the list before the first region scoring less (regions move up on the wave)
+                const int na = E.na[mi];
+                if (na >= AF_S2_MAX_REG) return false;
+                PeReg *ma = E.a[mi];
+                const uint64_t lt = __ballot(lane < na && ma[lane].r.score < sc);
+                const int i = lt ? __builtin_ctzll(lt) : na;
+                uint2 t[PE_W8];
+                const bool mv = lane >= i && lane < na;
+                if (mv)
+                    for (int c = 0; c < PE_W8; ++c) t[c] = reinterpret_cast<const uint2 *>(ma + lane)[c];
+                __threadfence_block();
+                wave_sync();
+                if (mv)
+                    for (int c = 0; c < PE_W8; ++c) reinterpret_cast<uint2 *>(ma + lane + 1)[c] = t[c];
                 if (lane == 0) {
                     PeReg b{};
                     b.r.qb = is_rev ? l_ms - (qe + 1) : qb;
@@ -1381,54 +1460,74 @@ __device__ bool s2_matesw(const DevText &X, const af_params &p, const S2Opt &o, 
                     b.r.score = sc;
                     b.r.truesc = 0; b.r.w = 0; b.r.seedlen0 = 0;
                     b.secondary = -1;
-                    const int na = E.na[mi];
-                    if (na >= AF_S2_MAX_REG) ok = false;
-                    else {
-                        PeReg *ma = E.a[mi];
-                        int i;
-                        for (i = 0; i < na; ++i)
-                            if (ma[i].r.score < b.r.score) break;
-                        for (int u = na; u > i; --u) ma[u] = ma[u - 1];
-                        ma[i] = b;
-                        E.na[mi] = na + 1;
-                    }
-                    E.misc[0] = ok;
+                    ma[i] = b;
+                    E.na[mi] = na + 1;
                 }
+                __threadfence_block();
                 wave_sync();
-                if (!E.misc[0]) return false;
+                dirty = true;
             }
             ++n;
         }
-        if (n) {
-            if (lane == 0) E.na[mi] = s2_dedup_nopatch(E.a[mi], E.na[mi], o.max_chain_gap);
+        if (n && (!deduped || dirty)) {
+            {
+                const int m = s2_dedup_nopatch(E.a[mi], E.na[mi], o.max_chain_gap, lane);
+                if (lane == 0) E.na[mi] = m;
+            }
             wave_sync();
+            deduped = true;
+            dirty = false;
         }
     }
     return true;
 }
 
-// mem_mark_primary_se (no ALT contigs), lane 0
-__device__ void s2_mark_primary(PeReg *a, int n, int64_t id, const af_params &p) {
-    if (n == 0) return;
-    for (int i = 0; i < n; ++i) { a[i].secondary = -1; a[i].hash = hash_64((uint64_t)(id + i)); }
-    ks_introsort(a, n, LtArsHash());
-    int32_t *z = g_pe.zz;
-    int nz = 0;
-    z[nz++] = 0;
-    for (int i = 1; i < n; ++i) {
-        int k;
-        for (k = 0; k < nz; ++k) {
-            const int j = z[k];
-            const int b_max = a[j].r.qb > a[i].r.qb ? a[j].r.qb : a[i].r.qb;
-            const int e_min = a[j].r.qe < a[i].r.qe ? a[j].r.qe : a[i].r.qe;
-            if (e_min > b_max) {
-                const int min_l = a[i].r.qe - a[i].r.qb < a[j].r.qe - a[j].r.qb ? a[i].r.qe - a[i].r.qb : a[j].r.qe - a[j].r.qb;
-                if ((float)(e_min - b_max) >= (float)min_l * 0.5f) break;
-            }
-        }
-        if (k == nz) z[nz++] = i;
-        else a[i].secondary = z[k];
+// mem_mark_primary_se (no ALT contigs) on the wave: the sort by (score desc, hash) over keys as in
+// s2_dedup_nopatch, the kept-hit walk on lane 0
+struct S2KeyHash {  // x = hash, y = score, z = index
+    __device__ bool operator()(const S2Key16 &a, const S2Key16 &b) const {
+        return a.y > b.y || (a.y == b.y && (uint64_t)a.x < (uint64_t)b.x);
     }
+};
+__device__ void s2_mark_primary(PeReg *a, int n, int64_t id, const af_params &p, int lane) {
+    if (n == 0) return;
+    PeLds &E = g_pe;
+    S2Key16 *k = reinterpret_cast<S2Key16 *>(E.v), *t = k + AF_S2_MAX_REG;
+    if (lane < n) {
+        a[lane].secondary = -1;
+        a[lane].hash = hash_64((uint64_t)(id + lane));
+        k[lane] = S2Key16{(int64_t)a[lane].hash, a[lane].r.score, lane};
+    }
+    __threadfence_block();
+    wave_sync();
+    if (n > 1) {
+        if (!wave_rank_sort(k, n, S2KeyHash(), t, lane)) {
+            if (lane == 0) ks_introsort(k, n, S2KeyHash());
+            wave_sync();
+        }
+        s2_regs_gather(a, n, [&](int x) { return k[x].z; }, lane);
+    }
+    if (lane == 0) {
+        int32_t *z = E.zz;
+        int nz = 0;
+        z[nz++] = 0;
+        for (int i = 1; i < n; ++i) {
+            int kk;
+            for (kk = 0; kk < nz; ++kk) {
+                const int j = z[kk];
+                const int b_max = a[j].r.qb > a[i].r.qb ? a[j].r.qb : a[i].r.qb;
+                const int e_min = a[j].r.qe < a[i].r.qe ? a[j].r.qe : a[i].r.qe;
+                if (e_min > b_max) {
+                    const int min_l = a[i].r.qe - a[i].r.qb < a[j].r.qe - a[j].r.qb ? a[i].r.qe - a[i].r.qb : a[j].r.qe - a[j].r.qb;
+                    if ((float)(e_min - b_max) >= (float)min_l * 0.5f) break;
+                }
+            }
+            if (kk == nz) z[nz++] = i;
+            else a[i].secondary = z[kk];
+        }
+    }
+    __threadfence_block();
+    wave_sync();
 }
 
 struct LtP64 {
@@ -1613,10 +1712,10 @@ __global__ __launch_bounds__(64, 4) void k_s2_pairs(DevText X, const uint8_t *__
             }
         SPROF(c2 = clock64(); nsw = E.misc[7];)
         // primary marking, pairing and the record choice (mem_sam_pe)
+        const uint64_t id = (uint64_t)(o.pair_base + pp);
+        s2_mark_primary(E.a[0], E.na[0], (int64_t)(id << 1 | 0), p, lane);
+        s2_mark_primary(E.a[1], E.na[1], (int64_t)(id << 1 | 1), p, lane);
         if (lane == 0) {
-            const uint64_t id = (uint64_t)(o.pair_base + pp);
-            s2_mark_primary(E.a[0], E.na[0], (int64_t)(id << 1 | 0), p);
-            s2_mark_primary(E.a[1], E.na[1], (int64_t)(id << 1 | 1), p);
             int z[2] = {0, 0}, extra = 1, which[2] = {-1, -1};
             bool paired = false;
             int o_sc = 0;
