@@ -1201,6 +1201,8 @@ int af_blat(af_ctx *c, const af_index *ix, const uint8_t *queries, int64_t n_que
         (lens && (e = hipMemcpyAsync(d_lens, lens, 4 * n_queries, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemsetAsync(c->ctrl + AF_CTRL_PLACE_HEADS, 0, 4 * AF_HEAD_STRIDE * 8, s)) != hipSuccess ||
         (e = hipMemcpyAsync(c->ctrl + AF_CTRL_PLACE_N, &nq, 4, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        // rows past a query's n_rows come back zeroed, not as stale device memory
+        (e = hipMemsetAsync(d_rows, 0, sizeof(af_psl) * nr, s)) != hipSuccess ||
         (e = af_launch_blat_order(ix->tile, d_q, c->ctrl + AF_CTRL_PLACE_N, n_queries, stride,
                                   lens ? d_lens : nullptr, p->rep_match, c->blat_ord_work, c->blat_order, s)) !=
             hipSuccess ||

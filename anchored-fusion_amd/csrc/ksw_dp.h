@@ -550,6 +550,136 @@ __device__ __noinline__ ExtRes ext_dp_w2(int qlen_, int qsel_, int qoff_, int tl
     return r;
 }
 
+// ksw_extend2 when the band fits the wave (w <= 31 after the max_ins / max_del clamp): lane k
+// holds column j = i - w + k of row i, one cell per lane whatever qlen is (BLAT's band-16
+// extensions of 150-bp queries).  bwa's eh[j].h (H(i-1, j-1), the diagonal predecessor) of a
+// column the row rewrites is the h this lane just computed; eh[j].e and the entries the row
+// leaves alone move down one lane per row; lanes 2w+1.. hold the initial eh of their (untouched)
+// columns.  Same recurrences, tie-breaks, band trimming and bookkeeping split as ext_dp_w1; the
+// exact early exit bounds the columns later rows can read (>= i + 1 - w).
+__device__ __noinline__ ExtRes ext_dp_band(int qlen_, int qsel_, int qoff_, int tlen_, Sc p_, int w_, int end_bonus_,
+                                           int zdrop_, int h0_) {
+#define AF_U(x) __builtin_amdgcn_readfirstlane(x)
+    const int qlen = AF_U(qlen_), tlen = AF_U(tlen_), end_bonus = AF_U(end_bonus_), zdrop = AF_U(zdrop_),
+              h0 = AF_U(h0_), qoff = AF_U(qoff_);
+    int w = AF_U(w_);
+    const Sc p{AF_U(p_.a), AF_U(p_.b), AF_U(p_.o_del), AF_U(p_.e_del), AF_U(p_.o_ins), AF_U(p_.e_ins)};
+    const uint8_t *q = (AF_U(qsel_) ? g_dp.q : g_dp.qs) + qoff;
+    const uint8_t *t = g_dp.t;
+#undef AF_U
+    const int lane = threadIdx.x;
+    const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+    {
+        int max_ins = div_plus(qlen * p.a + end_bonus - p.o_ins, p.e_ins, 1);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = div_plus(qlen * p.a + end_bonus - p.o_del, p.e_del, 1);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    const int v1 = h0 > oe_ins ? h0 - oe_ins : 0;
+    int j = lane - w;  // this lane's column in row i
+    int H = j < 0 || j > qlen ? 0 : (j == 0 ? h0 : max(v1 - (j - 1) * p.e_ins, 0));
+    int E = 0;
+    const bool tail = lane >= 2 * w + 1;  // lanes past the band: untouched columns
+    const int vz = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);
+    int mx = h0 + vz, max_i = vz - 1, max_j = vz - 1, max_ie = vz - 1, gscore = vz - 1, max_off = vz;
+    int beg = 0, end = qlen, rows = 0;
+    int ti_next = tlen > 0 ? t[0] : 4;
+    int qv = q[min(max(j, 0), qlen - 1)];
+    for (int i = 0; i < tlen; ++i, ++j) {
+        const int ti = ti_next;
+        if (i + 1 < tlen) ti_next = t[i + 1];
+        const int qc = (unsigned)j < (unsigned)qlen ? qv : 4;
+        qv = q[min(max(j + 1, 0), qlen - 1)];  // the next row's base of this lane
+        ++rows;
+        beg = max(beg, i - w);
+        end = min(min(end, i + w + 1), qlen);
+        int h1s = 0;
+        if (beg == 0) h1s = max(h0 - (p.o_del + p.e_del * (i + 1)), 0);
+        if (beg >= end) {
+            if (beg == qlen) {
+                max_ie = gscore > h1s ? max_ie : i + vz;
+                gscore = gscore > h1s ? gscore : h1s;
+            }
+            break;
+        }
+        const bool in = (unsigned)(j - beg) < (unsigned)(end - beg);
+        const int tiu = __builtin_amdgcn_readfirstlane(ti);
+        const int s_eq = tiu > 3 ? -1 : p.a, s_ne = tiu > 3 ? -1 : -p.b;
+        const int sc = qc == tiu ? s_eq : (qc > 3 ? -1 : s_ne);
+        int M = H != 0 ? H + sc : 0;
+        M = in ? M : 0;
+        // f as in ext_dp_w1: lanes left of the band carry jE (M = 0), column 0 gets -2^30
+        const int jE = j * p.e_ins, jEo = jE - oe_ins, jE1 = j <= 0 ? (1 << 30) : jE - p.e_ins;
+        const int P = __builtin_amdgcn_mov_dpp(span_incl_max<64>(max(M + jEo, jE)), 0x138, 0xf, 0xf, true);
+        const int f = P - jE1;
+        const int h = max(max(M, E), f);
+        const int key = in ? ((h << 10) | j) : -1;
+        const int kmax = span_max<64>(key) + vz;
+        const int m = max(kmax, 0) >> 10;
+        const int mj = kmax < 0 ? -1 : (kmax & 1023);
+        const int hq = bcast(h, min(max(qlen - 1 - i + w, 0), 63)) + vz;
+        const int Eu = max(max(E - p.e_del, M - oe_del), 0);
+        // the row's eh: E of column j (this layout), then both moved to the next row's layout
+        // (lane k <- column j + 1)
+        const int En = j < end ? Eu : (j == end ? 0 : E);
+        const int e_beg = __builtin_amdgcn_readlane(En, 0);  // column i - w
+        const int Hs = __builtin_amdgcn_mov_dpp(H, 0x130, 0xf, 0xf, true);  // wave_shl:1
+        const int Es = __builtin_amdgcn_mov_dpp(En, 0x130, 0xf, 0xf, true);
+        const int jn = j + 1;
+        H = jn == beg ? h1s : (jn <= end ? h : Hs);
+        E = Es;
+        if (tail) { H = jn > qlen ? 0 : max(v1 - (jn - 1) * p.e_ins, 0); E = 0; }
+        if (end == qlen) {
+            max_ie = gscore > hq ? max_ie : i + vz;
+            gscore = max(gscore, hq);
+        }
+        const bool better = m > mx;
+        const int di = i - max_i, dj = mj - max_j;
+        const int zgap = di > dj ? mx - m - __mul24(di - dj, p.e_del) : mx - m - __mul24(dj - di, p.e_ins);
+        const int zt = better ? INT_MIN : zgap;
+        const int off = mj - i < 0 ? i - mj : mj - i;
+        max_off = better ? max(max_off, off) : max_off;
+        max_i = better ? i + vz : max_i;
+        max_j = better ? mj : max_j;
+        mx = better ? m : mx;
+        const int stop = m == 0 ? 1 : (zt > zdrop ? zdrop : 0);
+        if (__builtin_amdgcn_readfirstlane(stop) > 0) break;
+        // band trimming: first non-zero eh in [beg, end), last in [beg, end]; column i - w (no
+        // lane in the next row's layout) is column beg when beg == i - w: eh = (h1s, e_beg)
+        const int x = (H | E) != 0 ? jn - beg : 1 << 20;
+        const uint64_t f_m = __ballot((unsigned)x < (unsigned)(end - beg));
+        const uint64_t l_m = __ballot((unsigned)x <= (unsigned)(end - beg));
+        const bool edge = beg == i - w && (h1s | e_beg) != 0;
+        const int c0 = i + 1 - w;  // column of lane 0 in the next row
+        const int beg_new = edge ? beg : (f_m ? c0 + (int)__builtin_ctzll(f_m) : end);
+        const int lnz = l_m ? c0 + 63 - (int)__builtin_clzll(l_m) : (edge ? beg : -1);
+        const int jstar = lnz >= beg_new ? lnz : beg_new - 1;
+        beg = beg_new;
+        end = jstar + 2 < qlen ? jstar + 2 : qlen;
+        if ((i & AF_EXIT_MASK) == AF_EXIT_MASK) {
+            const int u = (unsigned)(jn - beg) <= (unsigned)(qlen - beg) ? max(H, E) + (qlen - jn) * p.a : 0;
+            const int U = span_max<64>(u) + vz;
+            const int g = U <= mx ? (U < gscore ? gscore : 0) : 0;
+            if (__builtin_amdgcn_readfirstlane(g) > 0) break;
+        }
+    }
+    ExtRes r;
+    r.max = mx; r.qle = max_j + 1; r.tle = max_i + 1; r.gtle = max_ie + 1; r.gscore = gscore; r.max_off = max_off;
+    r.rows = rows;
+    return r;
+}
+
+// the w ksw_extend2 uses for qlen (ext_dp_w1's clamp)
+__device__ __forceinline__ int ext_band_w(int qlen, const af_params &p, int w, int end_bonus) {
+    int max_ins = div_plus(qlen * p.a + end_bonus - p.o_ins, p.e_ins, 1);
+    max_ins = max_ins > 1 ? max_ins : 1;
+    int max_del = div_plus(qlen * p.a + end_bonus - p.o_del, p.e_del, 1);
+    max_del = max_del > 1 ? max_del : 1;
+    return min(w, min(max_ins, max_del));
+}
+
 // ext_dp_w1 at the narrowest scan span that covers the query (qlen + 1 <= 64)
 __device__ __forceinline__ ExtRes ext_dp_w1s(int qlen, const uint8_t *q, int tlen, const af_params &p, int w,
                                              int end_bonus, int zdrop, int h0) {
@@ -571,6 +701,9 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
     const bool one = CPL == 1 || qlen + 1 <= 64;
     if (one)
         r = ext_dp_w1s(qlen, q, tlen, p, w, end_bonus, zdrop, h0);
+    else if (ext_band_w(qlen, p, w, end_bonus) <= 31)
+        r = ext_dp_band(qlen, q == g_dp.qs ? 0 : 1, (int)(q - (q == g_dp.qs ? g_dp.qs : g_dp.q)), tlen,
+                        Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
     else if (qlen + 1 <= 128)
         r = ext_dp_w2(qlen, q == g_dp.qs ? 0 : 1, (int)(q - (q == g_dp.qs ? g_dp.qs : g_dp.q)), tlen,
                       Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
@@ -582,6 +715,9 @@ __device__ __forceinline__ ExtRes ext_dp(int qlen, const uint8_t *q, int tlen, c
 #endif
     if (CPL == 1 || qlen + 1 <= 64)
         return ext_dp_w1s(qlen, q, tlen, p, w, end_bonus, zdrop, h0);
+    if (ext_band_w(qlen, p, w, end_bonus) <= 31)  // the band fits the wave: one cell per lane
+        return ext_dp_band(qlen, q == g_dp.qs ? 0 : 1, (int)(q - (q == g_dp.qs ? g_dp.qs : g_dp.q)), tlen,
+                           Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
     if (qlen + 1 <= 128)
         return ext_dp_w2(qlen, q == g_dp.qs ? 0 : 1, (int)(q - (q == g_dp.qs ? g_dp.qs : g_dp.q)), tlen,
                          Sc{p.a, p.b, p.o_del, p.e_del, p.o_ins, p.e_ins}, w, end_bonus, zdrop, h0);
