@@ -317,7 +317,8 @@ __device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int6
     const uint32_t f0 = nc > 0 ? D.ring[(nc - 1) & 63] : 0u, fl = nc > 0 ? D.ring[0] : 0u;
     if (nc > 0 && (f0 & 0xf) == 2) { tb += f0 >> 4; xs = 1; }
     else if (nc > 0 && (fl & 0xf) == 2) { te -= fl >> 4; xe = nc - 1; }
-    Reg o{};  // lane 63's (the one writing r)
+    // lane 63 writes the part straight into r (a part that is not ok is never read: the caller's
+    // count or ok flag leaves it out), so no lane holds a Reg of its own
     bool ok = true;
     int nmat = 0, nmis = 0, nn = 0, nb = 0, qni = 0, qbi = 0, tni = 0, tbi = 0;
     {
@@ -328,7 +329,7 @@ __device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int6
             const int len = (int)(op4 >> 4), op = (int)(op4 & 0xf);
             if (op == 0) {
                 if (nb >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
-                if (lane == 63) { o.bsz[nb] = len; o.bq[nb] = x; o.bt[nb] = y; }
+                if (lane == 63) { r.bsz[nb] = len; r.bq[nb] = x; r.bt[nb] = y; }
                 ++nb;
                 const uint8_t *tq = D.q + x, *tt = D.t + (y - tb0);
                 for (int u = lane; u < len; u += 64) {
@@ -347,12 +348,14 @@ __device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int6
     }
     nmat = wave_incl_sum(nmat, lane); nmis = wave_incl_sum(nmis, lane); nn = wave_incl_sum(nn, lane);
     if (lane == 63) {
-        o.nb = nb; o.qni = qni; o.qbi = qbi; o.tni = tni; o.tbi = tbi;
-        o.matches = nmat; o.mismatches = nmis; o.ncount = nn;
-        if (o.nb == 0) ok = false;
-        o.qb = qb; o.qe = qe; o.tb = tb; o.te = te;
-        o.score = o.matches - o.mismatches - o.qni - o.tni;
-        if (ok) r = o;
+        if (nb == 0) ok = false;
+        if (ok) {
+            r.nb = nb; r.qni = qni; r.qbi = qbi; r.tni = tni; r.tbi = tbi;
+            r.matches = nmat; r.mismatches = nmis; r.ncount = nn;
+            r.qb = qb; r.qe = qe; r.tb = tb; r.te = te;
+            r.score = nmat - nmis - qni - tni;
+            r.used = 0;
+        }
         g_bl.tmp[0] = ok ? 1 : 0;
     }
     wave_sync();
