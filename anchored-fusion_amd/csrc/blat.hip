@@ -1277,6 +1277,62 @@ int af_blat_slots(int n_cu) {
     return n_cu * occ;
 }
 
+// Test hook (tests/test_gpu_ext_dp.py; not part of afgpu.h): ksw_extend2 through ext_dp, the
+// dispatch k_blat's clump extensions take (ext_dp_w1 / ext_dp_band / ext_dp_w2 / ext_dp_wave by
+// qlen and the clamped band), on n independent cases, one wave each.  Case k: query codes
+// q[k * stride, + qlen[k]), target codes t[k * stride, + tlen[k]), par[10 k ..] = a, b, o_del,
+// e_del, o_ins, e_ins, w, end_bonus, zdrop, h0; out[7 k ..] = max, qle, tle, gtle, gscore,
+// max_off, rows.
+__global__ __launch_bounds__(64) void k_debug_ext_dp(const uint8_t *__restrict__ q, const uint8_t *__restrict__ t,
+                                                     int32_t stride, const int32_t *__restrict__ qlen,
+                                                     const int32_t *__restrict__ tlen, const int32_t *__restrict__ par,
+                                                     int32_t n, int32_t *__restrict__ out) {
+    const int k = blockIdx.x, lane = threadIdx.x;
+    if (k >= n) return;
+    DpLds &D = g_dp;
+    const int ql = qlen[k], tl = tlen[k];
+    for (int x = lane; x < ql; x += 64) D.qs[x] = q[(int64_t)k * stride + x];
+    for (int x = lane; x < tl; x += 64) D.t[x] = t[(int64_t)k * stride + x];
+    wave_sync();
+    const int32_t *c = par + 10 * (int64_t)k;
+    af_params P{};
+    P.a = c[0]; P.b = c[1]; P.o_del = c[2]; P.e_del = c[3]; P.o_ins = c[4]; P.e_ins = c[5];
+    const ExtRes r = ext_dp<6>(ql, D.qs, tl, D.t, P, c[6], c[7], c[8], c[9], lane);
+    if (lane == 0) {
+        int32_t *o = out + 7 * (int64_t)k;
+        o[0] = r.max; o[1] = r.qle; o[2] = r.tle; o[3] = r.gtle; o[4] = r.gscore; o[5] = r.max_off; o[6] = r.rows;
+    }
+}
+static_assert(AF_MAX_READ + 1 <= 6 * 64, "k_debug_ext_dp's ext_dp<6> covers every query length");
+
+extern "C" int af_debug_ext_dp(const uint8_t *q, const uint8_t *t, int32_t stride, const int32_t *qlen,
+                               const int32_t *tlen, const int32_t *par, int32_t n, int32_t *out) {
+    if (n <= 0) return 0;
+    if (!q || !t || !qlen || !tlen || !par || !out || stride <= 0) return -1;
+    for (int32_t k = 0; k < n; ++k)
+        if (qlen[k] < 1 || qlen[k] > AF_MAX_READ || qlen[k] > stride || tlen[k] < 0 || tlen[k] > 1024 ||
+            tlen[k] > stride)
+            return -1;
+    uint8_t *dq = nullptr, *dt = nullptr;
+    int32_t *dql = nullptr, *dtl = nullptr, *dp = nullptr, *dout = nullptr;
+    const size_t nb = (size_t)n * stride;
+    int rc = -1;
+    if (hipMalloc(&dq, nb) == hipSuccess && hipMalloc(&dt, nb) == hipSuccess && hipMalloc(&dql, 4 * n) == hipSuccess &&
+        hipMalloc(&dtl, 4 * n) == hipSuccess && hipMalloc(&dp, 40 * (size_t)n) == hipSuccess &&
+        hipMalloc(&dout, 28 * (size_t)n) == hipSuccess && hipMemcpy(dq, q, nb, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dt, t, nb, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dql, qlen, 4 * n, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dtl, tlen, 4 * n, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(dp, par, 40 * (size_t)n, hipMemcpyHostToDevice) == hipSuccess) {
+        hipLaunchKernelGGL(k_debug_ext_dp, dim3(n), dim3(64), 0, 0, dq, dt, stride, dql, dtl, dp, n, dout);
+        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(out, dout, 28 * (size_t)n, hipMemcpyDeviceToHost) == hipSuccess)
+            rc = 0;
+    }
+    (void)hipFree(dq); (void)hipFree(dt); (void)hipFree(dql); (void)hipFree(dtl); (void)hipFree(dp); (void)hipFree(dout);
+    return rc;
+}
+
 #ifdef AF_K2_PROF
 extern "C" int af_debug_blat_prof_enable() {
     int32_t *d = nullptr;
