@@ -125,7 +125,7 @@ def _oracle(q, t, a, b, od, ed, oi, ei, w, end_bonus, zdrop, h0):
 def test_band_layout_model_equals_oracle():
     rnd = random.Random(7)
     n = 0
-    for _ in range(160):
+    for _ in range(800):
         qlen = rnd.randint(64, 200)
         q = [rnd.randrange(4) for _ in range(qlen)]
         if rnd.random() < 0.1:
@@ -152,4 +152,4 @@ def test_band_layout_model_equals_oracle():
         want = _oracle(q, t, a, b, od, ed, oi, ei, w, 0, zd, h0)
         assert got == want, (qlen, tlen, w, h0, zd, got, want)
         n += 1
-    assert n == 160
+    assert n == 800
