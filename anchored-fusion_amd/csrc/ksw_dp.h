@@ -879,9 +879,12 @@ __device__ int global_dp_wave(int qlen, const uint8_t *q, int tlen, const uint8_
 // in the lane, E(i, j) arrives from lane k + 1 (wave_shl:1) and the query base moves down one
 // lane per row.  Lanes outside [beg, end) carry -inf, except the H(i, -1) boundary of rows with
 // beg == 0.  Same recurrences, tie-breaks and direction codes as global_dp_wave.
-template <bool TB = true>
+// ZL: the traceback nibbles ((w + 1) * tlen bytes <= ZLDS) go to the wave's LDS slot g_z instead
+// of its global scratch zg
+template <bool TB = true, bool ZL = false>
 __device__ int global_dp_band(int qlen, const uint8_t *q, int tlen, const uint8_t *t, const af_params &p, int w,
-                              uint8_t *__restrict__ zg, DpLds &L, int lane) {
+                              uint8_t *__restrict__ zg_, DpLds &L, int lane) {
+    uint8_t *__restrict__ zg = ZL ? g_z : zg_;
     const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
     const int k = lane;  // qlen >= 64 > 2w + 1: every band lane exists
     const bool band = k <= 2 * w;
@@ -978,7 +981,10 @@ __device__ __forceinline__ int gen_cigar_wave(const uint8_t *text, int64_t n, co
         const int n_col = lq < 2 * w + 1 ? lq : 2 * w + 1;
         uint8_t *z = (TB && (size_t)n_col * rlen <= ZLDS) ? g_z : zg;
         if (lq + 1 <= 64) score = global_dp_wave<1, TB>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
-        else if (w <= 31) score = global_dp_band<TB>(lq, L.qs, rlen, L.t, p, w, zg, L, lane);
+        else if (w <= 31) {
+            if (TB && (size_t)(w + 1) * rlen <= ZLDS) score = global_dp_band<TB, true>(lq, L.qs, rlen, L.t, p, w, zg, L, lane);
+            else score = global_dp_band<TB, false>(lq, L.qs, rlen, L.t, p, w, zg, L, lane);
+        }
         else score = global_dp_wave<CPL, TB>(lq, L.qs, rlen, L.t, p, w, z, L, lane);
     }
     return score;
