@@ -1,8 +1,9 @@
 // ksw_dp.h -- wave-level primitives and the ksw DP restatements shared by the alignment kernels
 // (align.hip: placement; s2.hip: the bwa-mem paired-end S2 path).  Every function restates one
 // bwa routine (ksw_extend2, ksw_global2, bwa_gen_cigar2) with the same recurrences and
-// tie-breaks as oracle/af_oracle.c; lanes hold query columns and DPP scans carry the
-// horizontal gap chain.  Header-only, anonymous namespace: each translation unit gets its own
+// tie-breaks as oracle/af_oracle.c; lanes hold query columns (or, for bands that fit the wave,
+// the band's diagonals: ext_dp_band, global_dp_band) and DPP scans carry the horizontal gap
+// chain.  Header-only, anonymous namespace: each translation unit gets its own
 // LDS slot (g_dp, g_z), referenced only by the kernels that use it.
 #pragma once
 #include "af_internal.h"
