@@ -355,7 +355,7 @@ hipError_t af_launch_gather(const uint8_t *reads, int32_t stride, const int32_t 
                             int64_t cap, uint8_t *q, int32_t *q_lens, int32_t *q_rows, int32_t *n_q, int32_t *sel,
                             int64_t *sel_n, void *temp, size_t temp_bytes, hipStream_t s);
 // k_blat's per-wave global scratch (blat.hip layout) and its resident waves on n_cu CUs
-constexpr size_t AF_BLAT_SLOT_BYTES = 2088 << 10;  // blat.hip SC_END
+constexpr size_t AF_BLAT_SLOT_BYTES = 872 << 10;  // blat.hip SC_END
 int af_blat_slots(int n_cu);
 // the rows past max_rows (af_blat_spill): appended at rows[atomicAdd(n, 1)] with their query
 struct BlatSpill {
@@ -374,36 +374,26 @@ struct BlatCaps {
         else if (ctx) atomicAdd(&ctx[k], 1);
     }
 };
-// A heavy strand (more than min_clumps clumps) is deferred by k_blat: its clumps go to the job pool
-// (aligned one job per wave by k_blat_jobs) and its entry to the strand table (chained by
-// k_blat_heavy).  ctrl: AF_BLAT_HV_CTRL_WORDS words, one 128-B line apart: the pool fills, the first
-// job offset that did not fit, and the two kernels' dequeue heads.
-struct BlatJob {
-    int32_t q, hs;  // the clump's seed (query offset, target position t) and its strand table entry
-    int64_t t;
-};
-#define AF_BLAT_HV_JOBS_N 0
-#define AF_BLAT_HV_JOBS_VALID (1 * AF_HEAD_STRIDE)
+// A heavy strand (more than min_clumps clumps) is deferred by k_blat: its entry {2 query + strand, 0,
+// clumps, 0} goes to the strand table and k_blat_heavy searches it, for the live queries only, once
+// the caller's live flags exist (S6: after S5's check).  ctrl: AF_BLAT_HV_CTRL_WORDS words, one 128-B
+// line apart: the table's fill, the deferred strands' clumps, k_blat_heavy's dequeue heads and
+// counters.
+#define AF_BLAT_HV_JOBS_N 0                            // clumps of the deferred strands
 #define AF_BLAT_HV_STRANDS_N (2 * AF_HEAD_STRIDE)
-#define AF_BLAT_HV_JOB_HEADS (3 * AF_HEAD_STRIDE)
 #define AF_BLAT_HV_STRAND_HEADS (11 * AF_HEAD_STRIDE)
-#define AF_BLAT_HV_JOBS_DONE (19 * AF_HEAD_STRIDE)     // jobs aligned (k_blat_jobs)
-#define AF_BLAT_HV_STRANDS_DONE (20 * AF_HEAD_STRIDE)  // deferred strands chained (k_blat_heavy)
+#define AF_BLAT_HV_JOBS_DONE (19 * AF_HEAD_STRIDE)     // clumps of the strands k_blat_heavy searched
+#define AF_BLAT_HV_STRANDS_DONE (20 * AF_HEAD_STRIDE)  // deferred strands searched (k_blat_heavy)
 #define AF_BLAT_HV_CTRL_WORDS (21 * AF_HEAD_STRIDE)
 #ifndef AF_BLAT_HEAVY_CLUMPS
 #define AF_BLAT_HEAVY_CLUMPS 32  // default: strands with more clumps are deferred (env AF_BLAT_HEAVY_CLUMPS)
 #endif
 struct BlatHeavy {
     int32_t min_clumps = 0;   // 0: no strand is deferred
-    BlatJob *jobs = nullptr;
-    int64_t jobs_cap = 0;
-    void *parts = nullptr;    // one blat.hip Reg (af_blat_part_bytes) per job
-    uint8_t *part_ok = nullptr;
-    int4 *strands = nullptr;  // {item, first job, clumps (0: not deferred after all), 0}
+    int4 *strands = nullptr;  // {item, 0, clumps, 0}
     int64_t strands_cap = 0;
-    int32_t *ctrl = nullptr, *jobs_n = nullptr, *jobs_valid = nullptr, *strands_n = nullptr;
+    int32_t *ctrl = nullptr, *jobs_n = nullptr, *strands_n = nullptr;
 };
-size_t af_blat_part_bytes();
 // one BLAT search's launch arguments
 struct BlatLaunch {
     DevTile X;
@@ -432,10 +422,11 @@ hipError_t af_launch_blat_begin(const BlatLaunch &B, hipStream_t s);
 hipError_t af_launch_blat_end(const BlatLaunch &B, const uint8_t *live, hipStream_t s);
 hipError_t af_launch_blat(const BlatLaunch &B, hipStream_t s);
 // blat_long.hip: one long query (codes of both strands at d_q2, strand s at d_q2 + s L) -> every
-// row (unsorted), its strand's emission order, its first block in `blocks`; cap events to caps
+// row (unsorted), its strand's emission order, its first block in `blocks`; cap events to caps;
+// *overflow = 1 (and no rows) when the device row list or block arena overflowed
 hipError_t af_blat_long_run(const DevTile &X, const uint8_t *d_q2, int L, const af_blat_params &bp, int32_t *caps,
                             std::vector<af_psl> &rows, std::vector<int32_t> &seq, std::vector<int64_t> &boff,
-                            std::vector<af_psl_block> &blocks, int n_cu, hipStream_t s);
+                            std::vector<af_psl_block> &blocks, int n_cu, hipStream_t s, int *overflow);
 // s5s6.hip: S6 rows of the QNAME-group leaders before the check, and their compaction after it
 hipError_t af_launch_s6_queries(int64_t n, const uint8_t *q, int32_t q_stride, const int32_t *q_lens,
                                 const int32_t *q_rows, const af_aln_out &s2, const uint8_t *cont, const af_s6_set &pre,

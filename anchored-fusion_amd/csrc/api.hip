@@ -34,7 +34,7 @@ struct af_ctx {
     BlatSpill blat_spill;           // af_blat_spill's pool (caller-owned device buffers)
     int32_t *blat_qcaps = nullptr;  // af_blat_query_caps' per-query counters (caller-owned), their query capacity
     int64_t blat_qcap = 0;
-    BlatHeavy blat_hv;              // the deferred strands' job pool, part pool and strand table
+    BlatHeavy blat_hv;              // the deferred strands' table
     int32_t blat_heavy_min = AF_BLAT_HEAVY_CLUMPS;
     BlatLaunch blat_pending;        // af_blat_device_begin's search, finished by af_blat_device_end
     bool blat_open = false;
@@ -262,28 +262,22 @@ int ensure_zscratch(af_ctx *c) {
     return AF_OK;
 }
 
-// the deferred strands' pools for a search of cap queries (grow-only): jobs for 64 clumps per query
-// (at least 16 K, at most 1 M: a strand that does not fit is searched by k_blat itself)
+// the deferred strands' table for a search of cap queries (grow-only; a strand that does not fit
+// is searched by k_blat itself)
 int ensure_blat_heavy(af_ctx *c, int64_t cap) {
     BlatHeavy &h = c->blat_hv;
     h.min_clumps = c->blat_heavy_min;
     if (h.min_clumps <= 0) return AF_OK;
-    const int64_t jobs = std::min<int64_t>(1 << 20, std::max<int64_t>(1 << 14, 64 * cap));
     const int64_t strands = std::min<int64_t>(1 << 16, std::max<int64_t>(1024, 2 * cap));
-    if (h.ctrl && h.jobs_cap >= jobs && h.strands_cap >= strands) return AF_OK;
-    if (h.ctrl) HIPCHK(c, hipDeviceSynchronize());  // an earlier search may still use the pools
-    af_free(h.jobs); af_free(h.parts); af_free(h.part_ok); af_free(h.strands); af_free(h.ctrl);
+    if (h.ctrl && h.strands_cap >= strands) return AF_OK;
+    if (h.ctrl) HIPCHK(c, hipDeviceSynchronize());  // an earlier search may still use the table
+    af_free(h.strands); af_free(h.ctrl);
     h = BlatHeavy{};
     h.min_clumps = c->blat_heavy_min;
-    HIPCHK(c, hipMalloc(&h.jobs, sizeof(BlatJob) * jobs));
-    HIPCHK(c, hipMalloc(&h.parts, af_blat_part_bytes() * jobs));
-    HIPCHK(c, hipMalloc(&h.part_ok, jobs));
     HIPCHK(c, hipMalloc(&h.strands, sizeof(int4) * strands));
     HIPCHK(c, hipMalloc(&h.ctrl, sizeof(int32_t) * AF_BLAT_HV_CTRL_WORDS));
-    h.jobs_cap = jobs;
     h.strands_cap = strands;
     h.jobs_n = h.ctrl + AF_BLAT_HV_JOBS_N;
-    h.jobs_valid = h.ctrl + AF_BLAT_HV_JOBS_VALID;
     h.strands_n = h.ctrl + AF_BLAT_HV_STRANDS_N;
     return AF_OK;
 }
@@ -692,7 +686,7 @@ void af_ctx_destroy(af_ctx *c) {
     af_free(c->g_pes); af_free(c->g_recs); af_free(c->g_nrec); af_free(c->g_hlens); af_free(c->g_hreads);
     af_free(c->s5_keep); af_free(c->s5_sel); af_free(c->s5_nsel); af_free(c->s5_temp);
     af_free(c->s6_flag); af_free(c->s6_idx); af_free(c->s6_sflag); af_free(c->s6_sidx); af_free(c->s6_temp);
-    af_free(c->blat_hv.jobs); af_free(c->blat_hv.parts); af_free(c->blat_hv.part_ok); af_free(c->blat_hv.strands);
+    af_free(c->blat_hv.strands);
     af_free(c->blat_hv.ctrl);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1152,7 +1146,7 @@ static int check_blat(af_ctx *c, const af_index *ix, const af_blat_params *p, in
     return AF_OK;
 }
 
-// a search's launch arguments on c's scratch; defer_heavy: heavy strands become jobs (c->blat_hv)
+// a search's launch arguments on c's scratch; heavy strands are deferred to c->blat_hv's table
 static BlatLaunch blat_launch(af_ctx *c, const af_index *ix, const uint8_t *q, const int32_t *n_q, const int32_t *first,
                               int64_t cap, int32_t stride, const int32_t *lens, const af_blat_params &p, af_psl *rows,
                               int32_t *n_rows, int32_t max_rows, const int32_t *order, bool with_spill) {
@@ -1246,10 +1240,13 @@ int af_blat_long(af_ctx *c, const af_index *ix, const uint8_t *query, int32_t le
     std::vector<int64_t> boff;
     std::vector<af_psl_block> blk;
     hipError_t e = hipMemcpyAsync(d_q2, q2.data(), q2.size(), hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = af_blat_long_run(ix->tile, d_q2, len, *p, c->blat_caps, r, seq, boff, blk, c->n_cu, c->stream);
+    int overflow = 0;
+    if (e == hipSuccess)
+        e = af_blat_long_run(ix->tile, d_q2, len, *p, c->blat_caps, r, seq, boff, blk, c->n_cu, c->stream, &overflow);
     (void)hipFree(d_q2);
-    if (e == hipErrorOutOfMemory) return fail(c, AF_E_CAPACITY, "af_blat_long: the row lists overflowed");
+    if (e == hipErrorOutOfMemory) return fail(c, AF_E_NOMEM, "af_blat_long: device memory");
     if (e != hipSuccess) return fail(c, AF_E_HIP, "af_blat_long: %s", hipGetErrorString(e));
+    if (overflow) return fail(c, AF_E_CAPACITY, "af_blat_long: the device row list / block arena overflowed");
     // every row best first: score desc, strand, tStart, qStart, tEnd, qEnd, then emission order
     std::vector<int64_t> ord(r.size());
     for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int64_t)k;

@@ -1,27 +1,32 @@
 // blat.hip -- the BLAT searches of the partner stages on the GPU (functions.py:341, 530, 966, 1007,
-// 1071, 1122, 1244): the tile index and k_blat, one wave per query.  oracle/blat.c is the
-// bit-exact contract; the restated algorithm and its choices are in afgpu.h (af_blat_params).
+// 1071, 1122, 1244): the tile index and k_blat, one wave per query strand.  oracle/blat.c is the
+// bit-exact contract; the restated algorithm and its choices are in afgpu.h (af_blat_params) and
+// DESIGN.md §2.
 //
 // Tile index (af_tile_index_build*): codes of the target (1 B/base), every step_size-th 11-mer
 // without N as (key, position) pairs radix-sorted by key (stable: positions ascending within a
-// key), key starts by a count + scan over all 4^11 keys, and N counts per 4096-base block (the
-// stitcher never joins parts across an N run, i.e. across contigs).
+// key), key starts by a count + scan over all 4^11 keys, per 64-base block an N bitmask, the N
+// count before it and the first N at or after it (the stitcher never joins parts across an N).
 //
-// k_blat per query and strand (strand 1 = the reverse-complemented query):
-//   hits     the query's 11-mer keys (lanes over offsets); then, offset by offset, the wave reads a
-//            key's positions coalesced and stores every hit, the first NMAX in (offset, position)
-//            order, as a 64-bit key (diagonal + 1024) << 9 | offset in the slot's scratch
-//   sort     stable LSD radix sort of the keys by diagonal (8-bit digits over the diagonal bits
-//            the target needs; LDS histogram, wave scan, ballot-ranked scatter), so the hits of
-//            a diagonal stay in offset order
-//   clumps   run starts (diagonal step > max_gap + 2) compacted by ballots; lanes over runs keep
-//            the runs of min_match hits (the first MAXCL, diagonal order), seed = least (offset,
-//            position); a 2-pass radix sort orders them (hits desc, diagonal)
-//   align    per clump, unless its seed tile lies in an earlier part: ksw_extend2 both ways and
-//            bwa_gen_cigar2 (ksw_dp.h, the wave DP of the placement kernel) with BLAT-like scores
-//   stitch   chain DP over the parts (<= 16) with overlap trimming; N checks over the gaps on
-//            the wave; every chain passing minScore / minIdentity becomes a PSL row
-//   output   rows of both strands ordered (score desc, strand, tStart, qStart), max_rows kept
+// k_blat per query strand (strand 1 = the reverse-complemented query):
+//   hits     the query's 11-mer keys (lanes over offsets); every hit, the first NMAX in (offset,
+//            position) order, as a 64-bit key (diagonal + 1024) << 9 | offset; hits with no other
+//            hit within the drift are dropped on the way (hashed diagonal-bucket bitmaps in LDS)
+//   sort     stable LSD radix sort of the keys by diagonal (offsets ascending within a diagonal)
+//   clumps   runs of diagonals (a step > max_gap + 2 starts one) with >= min_match hits, the first
+//            MAXCL in diagonal order, ordered (hits desc, diagonal); each knows its hits S[h0, h1)
+//   HSPs     Kent 2002: a clump's hits of one diagonal whose tiles touch form a range (an exact
+//            match); per range in order, unless it lies inside an HSP made before, a gapless
+//            extension both ways (+1 / -1, an end stops XDOWN positions after its last new best),
+//            the walks as wave scans over 64 positions at a time
+//   stitch   chain DP over the HSPs in (qb, tb, qe) order with overlap trimming (the only place a
+//            gap enters an alignment); every chain passing minScore / minIdentity is a PSL row
+//   output   rows of both strands ordered (score desc, strand, tStart, qStart, tEnd, qEnd)
+//
+// LDS: one BlatLds per wave, declared in each kernel and handed down by reference to helpers that
+// are all force-inlined, so every LDS access is a ds_* instruction on the kernel's own layout and
+// no helper reaches LDS through the LDS lowering's per-kernel offset table (the
+// round-5 fault).
 #include <cstdlib>
 
 #include <hipcub/hipcub.hpp>
@@ -29,7 +34,7 @@
 #include "ksw_dp.h"
 
 #ifndef AF_BLAT_ROUNDS
-#define AF_BLAT_ROUNDS 6  // drift-filter rounds at most (round 0 is marked while the hits are collected; 1 / 2 / 3 / 4 / 6: 160 / 147 / 145 / 144 / 144 ms per C3 step)
+#define AF_BLAT_ROUNDS 6  // drift-filter rounds at most (round 0 is marked while the hits are collected)
 #endif
 #ifndef AF_BLAT_FILTER_MIN
 #define AF_BLAT_FILTER_MIN 256  // hits below which another drift-filter round is not worth its passes
@@ -42,42 +47,48 @@ namespace {
 
 constexpr int TILE = AF_TILE;
 constexpr uint32_t NKEYS = 1u << (2 * TILE);
-// parts per query strand: one per clump at most, so MAXP adds no cap of its own (BLAT aligns every
-// clump whose seed lies in no earlier alignment)
-constexpr int NMAX = 32768, MAXCL = 4096, MAXP = MAXCL;
+// HSPs per query strand: the first MAXP in range order (AF_BLAT_CAP_PARTS when more ranges remain)
+constexpr int NMAX = 32768, MAXCL = 4096, MAXP = 4096;
 // stitching work per query strand (predecessor candidates the chain DP rescans after a chain is
-// emitted; the first pass over every part is always made): once past it,
-// no further chain is emitted and the strand is counted in AF_BLAT_CAP_PARTS (oracle/blat.c: the same)
+// emitted; the first pass over every part is always made): once past it, no further chain is
+// emitted and the strand is counted in AF_BLAT_CAP_PARTS (oracle/blat.c: the same)
 constexpr int64_t STITCH_WORK = 1 << 24;
+constexpr int XDOWN = 10;  // oracle/blat.c XDOWN: an HSP end stops 10 positions after its last new best
 
-struct Clump { int64_t diag, t; int32_t cnt, q; };
+struct Clump { int32_t cnt, h0, h1, pad; };  // hit count, its hits S[h0, h1) in diagonal order
+// one HSP (= one block): query [qb, qe) against target [tb, te), te - tb = qe - qb
 struct Reg {
-    int32_t qb, qe, score, matches, mismatches, ncount, qni, qbi, tni, tbi, nb, used;
+    int32_t qb, qe, score, matches, mismatches, ncount;
     int64_t tb, te;
-    int32_t bsz[AF_PSL_MAX_BLOCKS], bq[AF_PSL_MAX_BLOCKS];
-    int64_t bt[AF_PSL_MAX_BLOCKS];
 };
-static_assert(sizeof(Reg) == 320, "Reg layout");
-// per-slot scratch layout (bytes; the traceback of gen_cigar uses the first 64 KB): hit keys (two
-// buffers), clumps, parts, the chain DP's per-part words (sorted order, best, predecessor, flags,
-// chain), the strand's rows
-constexpr size_t SC_KEYS_A = 64 << 10, SC_KEYS_B = SC_KEYS_A + NMAX * 8, SC_CLUMP = SC_KEYS_B + NMAX * 8,
-                 SC_REGS = SC_CLUMP + MAXCL * 24, SC_DP = SC_REGS + (size_t)MAXP * sizeof(Reg),
+static_assert(sizeof(Reg) == 40, "Reg layout");
+// per-slot scratch layout (bytes): hit keys (two buffers; the one not holding the sorted hits
+// later holds the range starts at +64 KB and the clump order in its first 64 KB), clumps, HSPs,
+// the chain DP's per-part words (sorted order, best, predecessor, flags, chain, qe, te, first N),
+// the strand's rows
+constexpr size_t SC_KEYS_A = 0, SC_KEYS_B = SC_KEYS_A + NMAX * 8, SC_CLUMP = SC_KEYS_B + NMAX * 8,
+                 SC_REGS = SC_CLUMP + MAXCL * sizeof(Clump), SC_DP = SC_REGS + (size_t)MAXP * sizeof(Reg),
                  SC_ROWS = SC_DP + 8 * 4 * (size_t)MAXP, SC_END = SC_ROWS + (8 << 10);
+constexpr size_t SC_RANGES = 64 << 10;  // offset of the range starts inside the spare key buffer
 static_assert(SC_END == AF_BLAT_SLOT_BYTES, "BLAT slot layout");
 static_assert(AF_BLAT_MAX_ROWS * sizeof(af_psl) <= (8 << 10), "BLAT rows scratch");
+static_assert(SC_RANGES + 4 * (size_t)NMAX <= (size_t)NMAX * 8, "range starts fit the spare key buffer");
+static_assert(2 * 8 * (size_t)MAXCL <= SC_RANGES, "clump order fits below the range starts");
 
+// one wave's LDS (declared in each kernel, passed down by reference)
 struct __attribute__((aligned(16))) BlatLds {
-    uint32_t hist[AF_MAX_READ];    // radix digit counts (256) / per offset: first position index - first hit index
-    uint8_t q0[AF_MAX_READ + 16];  // the query's codes (strand 0)
+    uint32_t hist[AF_MAX_READ];     // radix digit counts (256) / per offset: first position index - first hit index / PRE
     int32_t base[AF_MAX_READ + 1];  // first hit index per query offset (exclusive scan of the counts)
-    int32_t nh, ncl, nr, nrow, tmp[8];
+    uint32_t once[512];             // drift filter: 16K-bit "seen" map
+    uint32_t twice[256];            // drift filter: 8K-bit "seen twice" map
+    uint8_t q[AF_MAX_READ + 16];    // the strand's codes
+    int32_t nrow, tmp[7];
 };
-__shared__ BlatLds g_bl;
 
 #ifdef AF_K2_PROF
-// profiling build only: per query [0..4] cycles in hits / sort / clumps / align / chain, [5] hits,
-// [6] clumps, [7] parts, [8] length, [9] total cycles, [10] drift-filter cycles, [11] hits kept
+// profiling build only: per query [0..4] cycles in hits / sort / clumps / HSPs / chain, [5] hits,
+// [6] clumps, [7] HSPs, [8] length, [9] total cycles, [10] drift-filter cycles, [11] hits kept,
+// [12] deferred, [13] ranges
 __device__ int32_t *g_blprof = nullptr;
 #define BP(...) __VA_ARGS__
 #define BPM(k) BP({ const int64_t _n = clock64(); pc[k] += _n - tq; tq = _n; })
@@ -126,35 +137,36 @@ __device__ __forceinline__ uint32_t bucket_hash(uint64_t b, int round, int bits)
 }
 
 // The drift filter: a key (diagonal = key >> 9) is kept when another key may lie within drift of
-// its diagonal.  Buckets of 1 << wsh diagonals hashed into a 16K-bit "seen" map (g_z) and an
-// 8K-bit "seen twice" map (g_dp.t); a hash collision only keeps a key.
-__device__ __forceinline__ void drift_clear(int lane) {
-    static_assert(ZLDS >= 2048, "the drift filter needs 2 KB of g_z");
-    uint32_t *once = reinterpret_cast<uint32_t *>(g_z), *twice = reinterpret_cast<uint32_t *>(g_dp.t);
-    for (int x = lane; x < 512; x += 64) once[x] = 0;
-    for (int x = lane; x < 256; x += 64) twice[x] = 0;
+// its diagonal.  Buckets of 1 << wsh diagonals hashed into a 16K-bit "seen" map and an 8K-bit
+// "seen twice" map; a hash collision only keeps a key.
+__device__ __forceinline__ void drift_clear(BlatLds &B, int lane) {
+    for (int x = lane; x < 512; x += 64) B.once[x] = 0;
+    for (int x = lane; x < 256; x += 64) B.twice[x] = 0;
 }
-__device__ __forceinline__ void drift_mark(uint64_t key, int wsh, int round) {
-    uint32_t *once = reinterpret_cast<uint32_t *>(g_z), *twice = reinterpret_cast<uint32_t *>(g_dp.t);
+__device__ __forceinline__ void drift_mark(BlatLds &B, uint64_t key, int wsh, int round) {
     const uint32_t h = bucket_hash(key >> (9 + wsh), round, 14), bit = 1u << (h & 31);
-    if (atomicOr(&once[h >> 5], bit) & bit) {
+    if (atomicOr(&B.once[h >> 5], bit) & bit) {
         const uint32_t g = h & 8191;
-        atomicOr(&twice[g >> 5], 1u << (g & 31));
+        atomicOr(&B.twice[g >> 5], 1u << (g & 31));
     }
 }
 // whether key k (marked for this round) may have another key within drift of its diagonal
-__device__ __forceinline__ bool drift_kept(uint64_t k, int64_t drift, int wsh, int round) {
-    const uint32_t *once = reinterpret_cast<const uint32_t *>(g_z), *twice = reinterpret_cast<const uint32_t *>(g_dp.t);
+__device__ __forceinline__ bool drift_kept(const BlatLds &B, uint64_t k, int64_t drift, int wsh, int round) {
     const int64_t d = (int64_t)(k >> 9);
     const uint64_t b = (uint64_t)d >> wsh, b0 = (uint64_t)(d - drift) >> wsh, b1 = (uint64_t)(d + drift) >> wsh;
     const uint32_t h = bucket_hash(b, round, 14), g = h & 8191;
-    bool keep = (twice[g >> 5] >> (g & 31)) & 1u;
+    bool keep = (B.twice[g >> 5] >> (g & 31)) & 1u;
     const uint64_t bn = b0 != b ? b0 : b1;  // the bucket width is >= 2 drift: one neighbour at most
-    if (bn != b) { const uint32_t hn = bucket_hash(bn, round, 14); keep = keep || ((once[hn >> 5] >> (hn & 31)) & 1u); }
+    if (bn != b) { const uint32_t hn = bucket_hash(bn, round, 14); keep = keep || ((B.once[hn >> 5] >> (hn & 31)) & 1u); }
     return keep;
 }
-// src[0, n) (marked for this round) -> dst: the keys kept, in order; returns their count
-__device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh, int round, int lane) {
+// src[0, n) -> dst: the keys this round keeps, in order; returns their count
+__device__ __forceinline__ int drift_filter(BlatLds &B, const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh,
+                                            int round, int lane) {
+    drift_clear(B, lane);
+    wave_sync();
+    for (int i = lane; i < n; i += 64) drift_mark(B, src[i], wsh, round);
+    wave_sync();
     int nk = 0;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -162,7 +174,7 @@ __device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t dri
         uint64_t k = 0;
         if (i < n) {
             k = src[i];
-            keep = drift_kept(k, drift, wsh, round);
+            keep = drift_kept(B, k, drift, wsh, round);
         }
         const uint64_t m = __ballot(keep);
         if (keep) dst[nk + lanes_below_blat(m, lane)] = k;
@@ -172,18 +184,12 @@ __device__ int drift_keep(const uint64_t *src, uint64_t *dst, int n, int64_t dri
     wave_sync();
     return nk;
 }
-__device__ int drift_filter(const uint64_t *src, uint64_t *dst, int n, int64_t drift, int wsh, int round, int lane) {
-    drift_clear(lane);
-    wave_sync();
-    for (int i = lane; i < n; i += 64) drift_mark(src[i], wsh, round);
-    wave_sync();
-    return drift_keep(src, dst, n, drift, wsh, round, lane);
-}
 
 // stable LSD radix sort of a[0, n) by bits [lo, lo + 8 * passes) on the wave, ping-ponging with
 // b; returns the buffer holding the result
-__device__ uint64_t *wave_radix_sort(uint64_t *a, uint64_t *b, int n, int lo, int passes, int lane) {
-    uint32_t *H = g_bl.hist;
+__device__ __forceinline__ uint64_t *wave_radix_sort(BlatLds &B, uint64_t *a, uint64_t *b, int n, int lo, int passes,
+                                                     int lane) {
+    uint32_t *H = B.hist;
     for (int p = 0; p < passes; ++p) {
         const int sh = lo + 8 * p;
         for (int x = lane; x < 256; x += 64) H[x] = 0;
@@ -220,30 +226,64 @@ __device__ uint64_t *wave_radix_sort(uint64_t *a, uint64_t *b, int n, int lo, in
     return a;
 }
 
-// r without its first k aligned bases (lane 0; 0 if k does not fit the first block)
-__device__ bool trim_front(const DevTile &X, const uint8_t *Q, const Reg &r, int k, Reg &o) {
-    o = r;
-    if (k <= 0) return true;
-    if (k >= r.bsz[0]) return false;
-    for (int u = 0; u < k; ++u) {
-        const uint8_t a = Q[r.bq[0] + u], b = X.T[r.bt[0] + u];
-        if (a > 3 || b > 3) --o.ncount;
-        else if (a == b) --o.matches;
-        else --o.mismatches;
+// Bases one end of an HSP takes: the walk from query offset qa / target position ta outwards
+// (dir +1: qa, qa + 1, ...; dir -1: qa, qa - 1, ...) over at most n pairs, +1 per match, -1 per
+// mismatch or N; the walk stops at the first step more than XDOWN after its last new best (a
+// strictly higher running score) and takes the bases up to that best (oracle hsp_range).  Lanes
+// over 64 steps at a time: prefix sums, the running best before each step as an exclusive prefix
+// max, the last new-best step as a prefix max of step indices.
+__device__ __forceinline__ int hsp_walk(const uint8_t *Q, const uint8_t *T, int qa, int64_t ta, int dir, int n,
+                                        int lane) {
+    int carry = 0, best = 0, nb = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane + 1;  // this lane's step (1-based)
+        const bool v = i <= n;
+        int sc = 0;
+        if (v) {
+            const uint8_t a = Q[qa + dir * (i - 1)], b = T[ta + dir * (int64_t)(i - 1)];
+            sc = (a > 3 || b > 3 || a != b) ? -1 : 1;
+        }
+        const int s = carry + wave_incl_sum(sc, lane);
+        const int sv = v ? s : kMaxId;
+        const int mincl = wave_incl_max(sv);
+        const int mprev = max(best, wave_shr1(kMaxId, mincl));  // the best before this step
+        const bool f = v && s > mprev;
+        const int nbi = max(nb, wave_incl_max(f ? i : 0));      // the last new best up to this step
+        const uint64_t stop = __ballot(v && !f && i - nbi > XDOWN);
+        if (stop) return __builtin_amdgcn_readlane(nbi, (int)__builtin_ctzll(stop));
+        const uint64_t vm = __ballot(v);
+        const int last = 63 - (int)__builtin_clzll(vm);
+        carry = __builtin_amdgcn_readlane(s, last);
+        best = max(best, __builtin_amdgcn_readlane(mincl, last));
+        nb = __builtin_amdgcn_readlane(nbi, last);
     }
-    o.bsz[0] -= k; o.bq[0] += k; o.bt[0] += k;
-    o.qb = o.bq[0]; o.tb = o.bt[0];
-    o.score = o.matches - o.mismatches - o.qni - o.tni;
-    return true;
+    return nb;
 }
 
-__device__ __forceinline__ int chain_trim(const Reg &a, const Reg &b) {
-    int64_t k = a.qe - b.qb;
-    if (a.te - b.tb > k) k = a.te - b.tb;
-    return k > 0 ? (int)k : 0;
+// the range [q0, q1) on diagonal t0 - q0 (an exact match) -> its HSP (oracle hsp_range); every
+// lane returns it
+__device__ __forceinline__ Reg hsp_range(const DevTile &X, const uint8_t *Q, int L, int q0, int q1, int64_t t0, int lane) {
+    const int64_t t1 = t0 + (q1 - q0);
+    const int nl = (int)min((int64_t)q0, t0);
+    const int left = nl > 0 ? hsp_walk(Q, X.T, q0 - 1, t0 - 1, -1, nl, lane) : 0;
+    const int nr = (int)min((int64_t)(L - q1), X.n - t1);
+    const int right = nr > 0 ? hsp_walk(Q, X.T, q1, t1, 1, nr, lane) : 0;
+    Reg r;
+    r.qb = q0 - left; r.qe = q1 + right;
+    r.tb = t0 - left; r.te = t1 + right;
+    int mt = 0, mm = 0, nn = 0;
+    for (int x = r.qb + lane; x < r.qe; x += 64) {
+        const uint8_t a = Q[x], b = X.T[r.tb + (x - r.qb)];
+        if (a > 3 || b > 3) ++nn;
+        else if (a == b) ++mt;
+        else ++mm;
+    }
+    r.matches = wave_sum(mt); r.mismatches = wave_sum(mm); r.ncount = wave_sum(nn);
+    r.score = r.matches - r.mismatches;
+    return r;
 }
 
-__device__ int psl_millibad(const af_psl &o) {
+__device__ __forceinline__ int psl_millibad(const af_psl &o) {
     const int q_ali = o.q_end - o.q_start;
     const int64_t t_ali = o.t_end - o.t_start;
     const int64_t ali = q_ali < t_ali ? q_ali : t_ali;
@@ -264,104 +304,6 @@ __device__ __forceinline__ bool psl_before(const af_psl &x, const af_psl &y) {
     return x.q_end < y.q_end;
 }
 
-// one clump seed (q, t) -> Reg r (written by lane 0); false if dropped.  L.q holds the strand.
-template <int CPL>
-__device__ __forceinline__ bool align_clump(const DevTile &X, int L, int q, int64_t t, Reg &r, uint8_t *zg, int lane) {
-    DpLds &D = g_dp;
-    af_params P{};
-    P.a = 1; P.b = 1; P.o_del = 3; P.e_del = 1; P.o_ins = 3; P.e_ins = 1; P.w = 16; P.zdrop = 20;
-    int score, truesc, qb, qe;
-    int64_t tb, te;
-    if (q > 0) {
-        const int tl = (int)(t < q + P.w ? t : q + P.w);
-        for (int x = lane; x < q; x += 64) D.qs[x] = D.q[q - 1 - x];
-        for (int x = lane; x < tl; x += 64) D.t[x] = X.T[t - 1 - x];
-        wave_sync();
-        const ExtRes er = ext_dp<CPL>(q, D.qs, tl, D.t, P, P.w, 0, P.zdrop, TILE * P.a, lane);
-        score = er.max;
-        if (er.gscore <= 0 || er.gscore <= score) { qb = q - er.qle; tb = t - er.tle; truesc = score; }
-        else { qb = 0; tb = t - er.gtle; truesc = er.gscore; }
-        wave_sync();
-    } else {
-        score = truesc = TILE * P.a; qb = 0; tb = t;
-    }
-    if (q + TILE < L) {
-        const int qs0 = q + TILE;
-        const int64_t t0 = t + TILE, room = X.n - t0;
-        const int tl = (int)(room < (L - qs0) + P.w ? room : (int64_t)(L - qs0) + P.w);
-        const int sc0 = score;
-        for (int x = lane; x < tl; x += 64) D.t[x] = X.T[t0 + x];
-        wave_sync();
-        const ExtRes er = ext_dp<CPL>(L - qs0, D.q + qs0, tl, D.t, P, P.w, 0, P.zdrop, sc0, lane);
-        score = er.max;
-        if (er.gscore <= 0 || er.gscore <= score) { qe = qs0 + er.qle; te = t0 + er.tle; truesc += score - sc0; }
-        else { qe = L; te = t0 + er.gtle; truesc += er.gscore - sc0; }
-        wave_sync();
-    } else {
-        qe = L; te = t + TILE;
-    }
-    const int lq = qe - qb, rl = (int)(te - tb);
-    if (lq <= 0 || rl <= 0) return false;
-    int w2 = infer_bw(lq, rl, truesc, P.a, P.o_del, P.e_del);
-    const int w3 = infer_bw(lq, rl, truesc, P.a, P.o_ins, P.e_ins);
-    w2 = w2 > w3 ? w2 : w3;
-    w2 = w2 < 64 ? w2 : 64;
-    gen_cigar_wave<CPL>(X.T, (int64_t)1 << 62, P, w2, lq, qb, tb, te, D, zg, lane);
-    const int nc = D.misc[2];
-    if (nc > AF_MAX_CIGAR) return false;
-    // the blocks from the CIGAR (the ring holds the ops in reverse order: forward op x is
-    // ring[(nc - 1 - x) & 63]), walked by the whole wave; each block's bases counted lane-parallel
-    // from the LDS copies gen_cigar_wave staged (D.t[i] = T[tb + i], D.q the strand's codes)
-    const int64_t tb0 = tb;
-    int xs = 0, xe = nc;
-    const uint32_t f0 = nc > 0 ? D.ring[(nc - 1) & 63] : 0u, fl = nc > 0 ? D.ring[0] : 0u;
-    if (nc > 0 && (f0 & 0xf) == 2) { tb += f0 >> 4; xs = 1; }
-    else if (nc > 0 && (fl & 0xf) == 2) { te -= fl >> 4; xe = nc - 1; }
-    // lane 63 writes the part straight into r (a part that is not ok is never read: the caller's
-    // count or ok flag leaves it out), so no lane holds a Reg of its own
-    bool ok = true;
-    int nmat = 0, nmis = 0, nn = 0, nb = 0, qni = 0, qbi = 0, tni = 0, tbi = 0;
-    {
-        int32_t x = qb;
-        int64_t y = tb;
-        for (int k = xs; k < xe; ++k) {
-            const uint32_t op4 = D.ring[(nc - 1 - k) & 63];
-            const int len = (int)(op4 >> 4), op = (int)(op4 & 0xf);
-            if (op == 0) {
-                if (nb >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
-                if (lane == 63) { r.bsz[nb] = len; r.bq[nb] = x; r.bt[nb] = y; }
-                ++nb;
-                const uint8_t *tq = D.q + x, *tt = D.t + (y - tb0);
-                for (int u = lane; u < len; u += 64) {
-                    const uint8_t a = tq[u], b = tt[u];
-                    if (a > 3 || b > 3) ++nn;
-                    else if (a == b) ++nmat;
-                    else ++nmis;
-                }
-                x += len; y += len;
-            } else if (op == 1) {
-                ++qni; qbi += len; x += len;
-            } else {
-                ++tni; tbi += len; y += len;
-            }
-        }
-    }
-    nmat = wave_incl_sum(nmat, lane); nmis = wave_incl_sum(nmis, lane); nn = wave_incl_sum(nn, lane);
-    if (lane == 63) {
-        if (nb == 0) ok = false;
-        if (ok) {
-            r.nb = nb; r.qni = qni; r.qbi = qbi; r.tni = tni; r.tbi = tbi;
-            r.matches = nmat; r.mismatches = nmis; r.ncount = nn;
-            r.qb = qb; r.qe = qe; r.tb = tb; r.te = te;
-            r.score = nmat - nmis - qni - tni;
-            r.used = 0;
-        }
-        g_bl.tmp[0] = ok ? 1 : 0;
-    }
-    wave_sync();
-    return g_bl.tmp[0] != 0;
-}
-
 // The chain DP's per-part words (parts in (qb, tb, qe) order, position k): ORD[k] = the part's
 // index in RG, BEST / PREV its chain score and predecessor, FL bit 0 = used by an emitted chain,
 // bit 1 = recomputed in this pass, CH the chain being emitted
@@ -380,22 +322,25 @@ __device__ __forceinline__ uint32_t first_n(const DevTile &X, int64_t p) {
 }
 
 // best[i] / prev[i] over the unused parts j < i (oracle/blat.c chain_node, the literal rule): a
-// predecessor must end before i on both sequences, leave part of i's first block after the
-// overlap trim, lie within max_intron on the target with no N in between; the first j with the
-// highest best[j] + trimmed score - gap flags wins over i alone.  Lanes over j on the parts'
-// sorted per-part words (coalesced; four 64-part chunks per pass); the trimmed score from a
-// prefix sum of i's first block (PRE, LDS), the N test against the part's first N after te.
-__device__ __forceinline__ void chain_node(const DevTile &X, const Reg *RG, const ChainDp &C, int i, int64_t max_intron, int lane) {
+// predecessor must end before i on both sequences, leave part of i after the overlap trim, lie
+// within max_intron on the target with no N in between; the first j with the highest best[j] +
+// trimmed score - gap flags wins over i alone.  Lanes over j on the parts' sorted per-part words
+// (coalesced; four 64-part chunks per pass); the trimmed score from a prefix sum of i's bases
+// (PRE, LDS), the N test against the part's first N after te.
+__device__ __forceinline__ void chain_node(BlatLds &B, const DevTile &X, const Reg *RG, const ChainDp &C, int i,
+                                           int64_t max_intron, int lane) {
     const Reg &ri = RG[C.ORD[i]];
-    const uint8_t *Q = g_dp.q;
-    int32_t *PRE = reinterpret_cast<int32_t *>(g_bl.hist);  // PRE[k] = score of the block's first k bases, k < bsz[0]
-    const int b0 = ri.bsz[0] < AF_MAX_READ ? ri.bsz[0] : AF_MAX_READ;
+    const uint8_t *Q = B.q;
+    int32_t *PRE = reinterpret_cast<int32_t *>(B.hist);  // PRE[k] = score of the part's first k bases
+    const int iqb = ri.qb, iqe = ri.qe, isc = ri.score, ilen = ri.qe - ri.qb;
+    const int64_t itb = ri.tb, ite = ri.te;
+    const int b0 = ilen < AF_MAX_READ ? ilen : AF_MAX_READ;
     int carry = 0;
     for (int u0 = 0; u0 < b0; u0 += 64) {
         const int u = u0 + lane;
         int m = 0;
         if (u < b0) {
-            const uint8_t x = Q[ri.bq[0] + u], y = X.T[ri.bt[0] + u];
+            const uint8_t x = Q[iqb + u], y = X.T[itb + u];
             m = (x > 3 || y > 3) ? 0 : (x == y ? 1 : -1);
         }
         const int inc = wave_incl_sum(m, lane);
@@ -403,8 +348,6 @@ __device__ __forceinline__ void chain_node(const DevTile &X, const Reg *RG, cons
         carry += __builtin_amdgcn_readlane(inc, 63);
     }
     wave_sync();
-    const int iqb = ri.qb, iqe = ri.qe, isc = ri.score, ib0 = ri.bsz[0];
-    const int64_t itb = ri.tb, ite = ri.te;
     int best = isc, prev = -1;
     for (int j0 = 0; j0 < i; j0 += 256) {
         int sc[4];
@@ -422,7 +365,7 @@ __device__ __forceinline__ void chain_node(const DevTile &X, const Reg *RG, cons
                     if (ate - itb > kk) kk = ate - itb;
                     const int k = kk > 0 ? (int)kk : 0;
                     const int64_t btb = itb + k;
-                    if (!(k > 0 && k >= ib0) && btb - ate <= max_intron && nx >= btb)
+                    if (!(k > 0 && k >= ilen) && btb - ate <= max_intron && nx >= btb)
                         v = bj + (isc - (k > 0 ? PRE[k] : 0)) - (iqb + k > aqe) - (btb > ate);
                 }
             }
@@ -438,58 +381,28 @@ __device__ __forceinline__ void chain_node(const DevTile &X, const Reg *RG, cons
     wave_sync();
 }
 
-// a clump seed (q, t) inside one of the parts RG[0, nr) (lanes over the parts)
-__device__ __forceinline__ bool inside_part(const Reg *RG, int nr, int32_t q, int64_t t, int lane) {
+// the box [q0, q1) x [t0, t1) inside one of the parts RG[0, nr) (lanes over the parts)
+__device__ __forceinline__ bool inside_part(const Reg *RG, int nr, int q0, int q1, int64_t t0, int64_t t1, int lane) {
     bool inside = false;
     for (int r0 = 0; r0 < nr && !inside; r0 += 64) {
         const int r = r0 + lane;
         bool in = false;
         if (r < nr) {
             const Reg &g = RG[r];
-            in = g.qb <= q && q + TILE <= g.qe && g.tb <= t && t + TILE <= g.te;
+            in = g.qb <= q0 && q1 <= g.qe && g.tb <= t0 && t1 <= g.te;
         }
         inside = __ballot(in) != 0;
     }
     return inside;
 }
 
-// a heavy strand's clumps (in CO order) to the job pool with its entry {2 query + strand, first job,
-// clumps} in the strand table; false (the caller searches it) when either is full
-__device__ __forceinline__ bool defer_strand(const BlatHeavy &hv, const Clump *CL, const uint64_t *CO, int ncl, int64_t item, int lane) {
-    int s = 0, off = 0, ok = 0;
-    if (lane == 0) {
-        s = atomicAdd(hv.strands_n, 1);
-        if (s < hv.strands_cap) {
-            off = atomicAdd(hv.jobs_n, ncl);
-            if ((int64_t)off + ncl <= hv.jobs_cap) ok = 1;
-            else { atomicMin(hv.jobs_valid, off); hv.strands[s] = make_int4((int)item, 0, 0, 0); }
-        }
-    }
-    ok = __builtin_amdgcn_readfirstlane(ok);
-    if (!ok) return false;
-    s = __builtin_amdgcn_readfirstlane(s);
-    off = __builtin_amdgcn_readfirstlane(off);
-#ifdef AF_BLAT_CHECK
-    if (off < 0 || (int64_t)off + ncl > hv.jobs_cap || s < 0 || s >= hv.strands_cap || ncl > MAXCL) {
-        if (lane == 0) printf("defer_strand: off %d ncl %d s %d caps %ld %ld\n", off, ncl, s, (long)hv.jobs_cap, (long)hv.strands_cap);
-        return false;
-    }
-#endif
-    for (int c = lane; c < ncl; c += 64) {
-        const Clump cc = CL[(uint32_t)CO[c]];
-        hv.jobs[off + c] = BlatJob{cc.q, s, cc.t};
-    }
-    if (lane == 0) hv.strands[s] = make_int4((int)item, off, ncl, 0);
-    return true;
-}
-
-// the chains of one strand's parts RG[0, nr) (D.q its codes), best first, into its row list (RW,
-// g_bl.nrow; rows past max_rows to the spill pool)
-__device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_params &bp, Reg *RG, const ChainDp &CD, int nr,
-                              int64_t qi, int strand, int L, uint64_t *KA, uint64_t *KB, af_psl *RW, int32_t max_rows,
-                              const BlatCaps &caps, const BlatSpill &spill, int lane) {
-    DpLds &D = g_dp;
-    BlatLds &B = g_bl;
+// the chains of one strand's parts RG[0, nr) (B.q its codes), best first, into its row list (RW,
+// B.nrow; rows past max_rows to the spill pool).  parts_capped: AF_BLAT_CAP_PARTS already counted
+// for the strand (a strand counts each cap once, as the oracle's per-strand flags)
+__device__ __forceinline__ void strand_chains(BlatLds &B, const DevTile &X, const af_blat_params &bp, Reg *RG,
+                                              const ChainDp &CD, int nr, int64_t qi, int strand, int L, uint64_t *KA,
+                                              uint64_t *KB, af_psl *RW, int32_t max_rows, const BlatCaps &caps,
+                                              const BlatSpill &spill, bool parts_capped, int lane) {
     // ---- parts in (qb, tb, qe) order, ties in creation order: ORD ----------------------------
     // key: qb in bits 54-63, tb in 21-53, qe in 12-20, the part index in 0-11
     static_assert(AF_MAX_READ < 512, "qb / qe take 9 bits of the ORD key");
@@ -510,7 +423,7 @@ __device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_pa
             for (int r = lane; r < nr; r += 64) KA[r] = key(r);
             __threadfence_block();
             wave_sync();
-            const uint64_t *SK = wave_radix_sort(KA, KB, nr, 12, 7, lane);
+            const uint64_t *SK = wave_radix_sort(B, KA, KB, nr, 12, 7, lane);
             for (int r = lane; r < nr; r += 64) CD.ORD[r] = (int32_t)(SK[r] & 4095u);
         }
         __threadfence_block();
@@ -530,13 +443,14 @@ __device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_pa
     // met a used part are recomputed, the others keep their exact value) ----------------
     int64_t work = 0;  // the recomputations' candidates (the first pass is always made)
     for (int i = 0; i < nr; ++i) {
-        chain_node(X, RG, CD, i, bp.max_intron, lane);
+        chain_node(B, X, RG, CD, i, bp.max_intron, lane);
         __threadfence_block();
         wave_sync();
     }
+    const uint8_t *Q = B.q;
     for (;;) {
         if (work > STITCH_WORK) {
-            if (lane == 0) caps.hit(qi, AF_BLAT_CAP_PARTS);
+            if (lane == 0 && !parts_capped) caps.hit(qi, AF_BLAT_CAP_PARTS);
             break;
         }
         // the unused part with the highest chain score, the first on ties
@@ -550,65 +464,120 @@ __device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_pa
             if (bi < 0 || mx > bv) { bv = mx; bi = i0 + (int)__builtin_ctzll(__ballot(free_ && v == mx)); }
         }
         if (bi < 0) break;
-        int first = bi;
+        // the chain (lane 0 follows the predecessors), its parts marked used
+        int m = 0;
         if (lane == 0) {
-            int m = 0;
             for (int i = bi; i >= 0; i = CD.PREV[i]) CD.CH[m++] = i;
-            first = CD.CH[m - 1];
-            af_psl o{};
-            o.query = (int32_t)qi; o.strand = strand; o.q_size = L;
-            bool ok = true;
-            Reg prevp{}, firstp{}, lastp{};
-            for (int c = m - 1; c >= 0; --c) {
-                const int k = CD.CH[c];
-                CD.FL[k] |= 1;
-                CD.QE[k] = -1;
-                const Reg &src = RG[CD.ORD[k]];
-                Reg cur;
-                if (c == m - 1) cur = src;
-                else trim_front(X, D.q, src, chain_trim(prevp, src), cur);
-                if (c < m - 1) {
-                    if (cur.qb > prevp.qe) { ++o.q_num_insert; o.q_base_insert += cur.qb - prevp.qe; }
-                    if (cur.tb > prevp.te) { ++o.t_num_insert; o.t_base_insert += (int32_t)(cur.tb - prevp.te); }
+        }
+        m = __builtin_amdgcn_readfirstlane(m);
+        __threadfence_block();
+        wave_sync();
+        const int first = CD.CH[m - 1];
+        for (int c = lane; c < m; c += 64) { CD.FL[CD.CH[c]] |= 1; CD.QE[CD.CH[c]] = -1; }
+        if (m <= AF_PSL_MAX_BLOCKS) {  // a chain of more HSPs than a row holds blocks: no row
+            // lane b: block b, the chain's b-th part (CH[m - 1 - b]), its front trimmed by the
+            // overlap with part b - 1 (trim_front; the oracle's literal accounting)
+            const int b = lane;
+            int32_t qb = 0, qe = 0, blen = 0;
+            int64_t tb = 0, te = 0;
+            int mt = 0, mm = 0, nn = 0, qni = 0, qbi = 0, tni = 0, tbi = 0;
+            if (b < m) {
+                const Reg &src = RG[CD.ORD[CD.CH[m - 1 - b]]];
+                qb = src.qb; qe = src.qe; tb = src.tb; te = src.te;
+                mt = src.matches; mm = src.mismatches; nn = src.ncount;
+                if (b > 0) {
+                    const Reg &prv = RG[CD.ORD[CD.CH[m - b]]];
+                    int64_t kk = prv.qe - qb;
+                    if (prv.te - tb > kk) kk = prv.te - tb;
+                    const int trim = kk > 0 && kk < src.qe - src.qb ? (int)kk : 0;
+                    for (int u = 0; u < trim; ++u) {
+                        const uint8_t x = Q[qb + u], y = X.T[tb + u];
+                        if (x > 3 || y > 3) --nn;
+                        else if (x == y) --mt;
+                        else --mm;
+                    }
+                    qb += trim; tb += trim;
+                    if (qb > prv.qe) { qni = 1; qbi = qb - prv.qe; }
+                    if (tb > prv.te) { tni = 1; tbi = (int)(tb - prv.te); }
                 }
-                o.matches += cur.matches; o.mismatches += cur.mismatches; o.n_count += cur.ncount;
-                o.q_num_insert += cur.qni; o.q_base_insert += cur.qbi;
-                o.t_num_insert += cur.tni; o.t_base_insert += cur.tbi;
-                for (int b = 0; b < cur.nb; ++b) {
-                    if (o.block_count >= AF_PSL_MAX_BLOCKS) { ok = false; break; }
-                    o.block_sizes[o.block_count] = cur.bsz[b]; o.q_starts[o.block_count] = cur.bq[b];
-                    o.t_starts[o.block_count] = cur.bt[b]; ++o.block_count;
-                }
-                if (c == m - 1) firstp = cur;
-                if (c == 0) lastp = cur;
-                prevp = cur;
+                blen = qe - qb;
             }
-            o.q_start = strand ? L - lastp.qe : firstp.qb;
-            o.q_end = strand ? L - firstp.qb : lastp.qe;
-            o.t_start = firstp.tb; o.t_end = lastp.te;
-            o.score = o.matches - o.mismatches - o.q_num_insert - o.t_num_insert;
-            if (ok && o.score >= bp.min_score && psl_millibad(o) <= (100 - bp.min_identity) * 10) {
-                // the strand's best max_rows rows in psl_before order (stable), all counted;
-                // the row that falls off the list goes to the spill pool
+            const int s_mt = wave_sum(mt), s_mm = wave_sum(mm), s_nn = wave_sum(nn);
+            const int s_qni = wave_sum(qni), s_qbi = wave_sum(qbi), s_tni = wave_sum(tni), s_tbi = wave_sum(tbi);
+            const int fqb = __builtin_amdgcn_readlane(qb, 0);
+            const int64_t ftb = ((int64_t)__builtin_amdgcn_readlane((int)(tb >> 32), 0) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tb, 0);
+            const int lqe = __builtin_amdgcn_readlane(qe, m - 1);
+            const int64_t lte = ((int64_t)__builtin_amdgcn_readlane((int)(te >> 32), m - 1) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)te, m - 1);
+            af_psl h;  // the header fields (lane-uniform); the block arrays are written lane by lane
+            h.query = (int32_t)qi; h.strand = strand; h.q_size = L;
+            h.matches = s_mt; h.mismatches = s_mm; h.n_count = s_nn;
+            h.q_num_insert = s_qni; h.q_base_insert = s_qbi; h.t_num_insert = s_tni; h.t_base_insert = s_tbi;
+            h.q_start = strand ? L - lqe : fqb;
+            h.q_end = strand ? L - fqb : lqe;
+            h.t_start = ftb; h.t_end = lte;
+            h.block_count = m;
+            h.score = h.matches - h.mismatches - h.q_num_insert - h.t_num_insert;
+            if (h.score >= bp.min_score && psl_millibad(h) <= (100 - bp.min_identity) * 10) {
+                // the strand's best max_rows rows in psl_before order (stable), all counted; the
+                // row that falls off the list goes to the spill pool
                 const int n = B.nrow < max_rows ? B.nrow : max_rows;
-                int at = n;
-                while (at > 0 && psl_before(o, RW[at - 1])) --at;
-                af_psl out = o;
-                bool off = at >= max_rows;
-                if (!off) {
-                    if (n == max_rows) { out = RW[max_rows - 1]; off = true; }
-                    for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) RW[x] = RW[x - 1];
-                    RW[at] = o;
+                const bool after = lane < n && !psl_before(h, RW[lane]);  // RW sorted: a prefix
+                const int at = (int)__builtin_popcountll(__ballot(after));
+                af_psl *dst = nullptr;  // where the new row goes
+                if (at < max_rows) {
+                    if (n == max_rows && spill.cap > 0) {  // the last kept row falls off
+                        int k = 0;
+                        if (lane == 0) k = atomicAdd(spill.n, 1);
+                        k = __builtin_amdgcn_readfirstlane(k);
+                        if (k < spill.cap) {
+                            const int32_t *src = reinterpret_cast<const int32_t *>(RW + max_rows - 1);
+                            int32_t *d = reinterpret_cast<int32_t *>(spill.rows + k);
+                            for (int w = lane; w < (int)(sizeof(af_psl) / 4); w += 64) d[w] = src[w];
+                            if (lane == 0) spill.query[k] = (int32_t)qi;
+                        } else if (lane == 0) {
+                            caps.hit(qi, AF_BLAT_CAP_ROWS);
+                        }
+                    }
+                    for (int x = (n < max_rows ? n : max_rows - 1); x > at; --x) {
+                        const int32_t *src = reinterpret_cast<const int32_t *>(RW + x - 1);
+                        int32_t *d = reinterpret_cast<int32_t *>(RW + x);
+                        for (int w = lane; w < (int)(sizeof(af_psl) / 4); w += 64) d[w] = src[w];
+                        __threadfence_block();
+                        wave_sync();
+                    }
+                    dst = RW + at;
+                } else if (spill.cap > 0) {
+                    int k = 0;
+                    if (lane == 0) k = atomicAdd(spill.n, 1);
+                    k = __builtin_amdgcn_readfirstlane(k);
+                    if (k < spill.cap) {
+                        dst = spill.rows + k;
+                        if (lane == 0) spill.query[k] = (int32_t)qi;
+                    } else if (lane == 0) {
+                        caps.hit(qi, AF_BLAT_CAP_ROWS);
+                    }
                 }
-                if (off && spill.cap > 0) {
-                    const int k = atomicAdd(spill.n, 1);
-                    if (k < spill.cap) { spill.rows[k] = out; spill.query[k] = (int32_t)qi; }
-                    else caps.hit(qi, AF_BLAT_CAP_ROWS);
+                if (dst) {
+                    if (lane == 0) {
+                        dst->query = h.query; dst->strand = h.strand; dst->score = h.score;
+                        dst->matches = h.matches; dst->mismatches = h.mismatches; dst->n_count = h.n_count;
+                        dst->q_num_insert = h.q_num_insert; dst->q_base_insert = h.q_base_insert;
+                        dst->t_num_insert = h.t_num_insert; dst->t_base_insert = h.t_base_insert;
+                        dst->q_start = h.q_start; dst->q_end = h.q_end; dst->q_size = h.q_size;
+                        dst->block_count = h.block_count; dst->t_start = h.t_start; dst->t_end = h.t_end;
+                    }
+                    if (lane < AF_PSL_MAX_BLOCKS) {
+                        const bool v = lane < m;
+                        dst->block_sizes[lane] = v ? blen : 0;
+                        dst->q_starts[lane] = v ? qb : 0;
+                        dst->t_starts[lane] = v ? tb : 0;
+                    }
                 }
-                ++B.nrow;
+                if (lane == 0) ++B.nrow;
             }
         }
-        first = __builtin_amdgcn_readfirstlane(first);
         __threadfence_block();
         wave_sync();
         // parts after the chain's first whose predecessor path meets a used or recomputed
@@ -630,7 +599,7 @@ __device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_pa
             while (dm) {
                 const int l = (int)__builtin_ctzll(dm);
                 dm &= dm - 1;
-                chain_node(X, RG, CD, i0 + l, bp.max_intron, lane);
+                chain_node(B, X, RG, CD, i0 + l, bp.max_intron, lane);
                 work += i0 + l;
                 if (lane == 0) CD.FL[i0 + l] |= 2;
                 __threadfence_block();
@@ -643,275 +612,19 @@ __device__ __forceinline__ void strand_chains(const DevTile &X, const af_blat_pa
     }
 }
 
-// lane 0: the strand's rows (RW, g_bl.nrow of them) to item (qi, s)'s stage, best first, for k_blat_merge
-__device__ __forceinline__ void strand_stage(af_psl *stage, int32_t *stage_n, int64_t qi, int s, int32_t max_rows, const af_psl *RW,
-                             int lane) {
-    if (lane == 0) {
-        const int n = g_bl.nrow;  // RW holds the first max_rows of them in order
-        const int m = n < max_rows ? n : max_rows;
-        const int64_t sl = 2 * qi + s;
-        for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
-        stage_n[sl] = n;  // all of the strand's rows (k_blat_merge takes the first max_rows)
+// the first index in A[0, n) holding a value >= v (A ascending; every lane the same answer)
+__device__ __forceinline__ int lower_bound_u32(const uint32_t *A, int n, uint32_t v) {
+    int a = 0, b = n;
+    while (a < b) {
+        const int m = (a + b) >> 1;
+        if (A[m] < v) a = m + 1; else b = m;
     }
+    return a;
 }
 
-template <int CPL>
-__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries,
-                                                        int32_t stride, const int32_t *__restrict__ lens,
-                                                        af_blat_params bp, const int32_t *__restrict__ n_q,
-                                                        const int32_t *__restrict__ q_first, int64_t cap,
-                                                        int32_t *__restrict__ heads,
-                                                        uint8_t *__restrict__ bscratch, int32_t diag_passes,
-                                                        af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
-                                                        int32_t max_rows, const int32_t *__restrict__ order,
-                                                        BlatCaps caps, BlatSpill spill, BlatHeavy hv) {
-    DpLds &D = g_dp;
-    BlatLds &B = g_bl;
-    const int lane = threadIdx.x;
-    const int64_t nq64 = *n_q < cap ? *n_q : cap;
-    const int nq = (int)(nq64 < 0 ? 0 : nq64);
-    const int q0 = q_first ? max(0, min(*q_first, nq)) : 0;  // queries [q0, nq)
-    uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
-    uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
-    Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
-    Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
-    af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
-    int32_t *dpw = reinterpret_cast<int32_t *>(zg + SC_DP);
-    const ChainDp CD{dpw, dpw + MAXP, dpw + 2 * MAXP, dpw + 3 * MAXP, dpw + 4 * MAXP, dpw + 5 * MAXP,
-                     reinterpret_cast<uint32_t *>(dpw + 6 * MAXP), reinterpret_cast<uint32_t *>(dpw + 7 * MAXP)};
-    // work items are (query, strand): item 2k + s is strand s of the k-th query (of the cost order
-    // when given: heaviest first), so a heavy query's strands run on two waves at once
-    const int64_t i0 = 2 * (int64_t)q0, i1 = 2 * (int64_t)nq;
-    int head = (int)(blockIdx.x & 7), heads_left = 8;
-    for (;;) {
-        int64_t item = i1;
-        while (heads_left > 0) {
-            int v = 0;
-            if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
-            v = __builtin_amdgcn_readfirstlane(v);
-            const int64_t it = i0 + head + 8 * (int64_t)v;
-            if (it < i1) { item = it; break; }
-            head = (head + 1) & 7;
-            --heads_left;
-        }
-        if (item >= i1) break;
-        const int s_item = (int)(item & 1);
-        const int64_t qi = order ? order[item >> 1] : (item >> 1);
-#ifdef AF_BLAT_CHECK
-        if (qi < 0 || qi >= cap) {
-            if (lane == 0) printf("k_blat: item %ld -> query %ld outside [0, %ld)\n", (long)item, (long)qi, (long)cap);
-            continue;
-        }
-#endif
-        int L = lens ? lens[qi] : stride;
-        if (L > stride) L = stride;
-        if (L > AF_MAX_READ) L = AF_MAX_READ;
-        if (L < 0) L = 0;
-        for (int x = lane; x < L; x += 64) B.q0[x] = nt4(queries[qi * (int64_t)stride + x]);
-        if (lane == 0) B.nrow = 0;
-        wave_sync();
-        const int64_t drift = (int64_t)bp.max_gap + 2;
-        int wsh = 3;  // bucket width 1 << wsh >= 2 * drift: [d - drift, d + drift] meets <= 2 buckets
-        while ((1ll << wsh) < 2 * drift) ++wsh;
-        BP(int64_t tq0 = clock64(), tq = tq0; int64_t pc[6] = {0, 0, 0, 0, 0, 0}; int ch = 0, cc_ = 0, cr = 0, cs = 0;)
-        bool deferred = false;  // the strand's parts and chains are left to k_blat_jobs / k_blat_heavy
-        for (int strand = s_item; strand <= s_item; ++strand) {
-            for (int x = lane; x < L; x += 64) {
-                const uint8_t c = B.q0[strand ? L - 1 - x : x];
-                D.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
-            }
-            wave_sync();
-            // ---- per offset: its tile's position range (count 0: N inside, absent or over rep_match) --
-            const bool filt = bp.min_match >= 2;
-            if (filt) drift_clear(lane);  // round 0 of the drift filter is marked while collecting
-            uint32_t *DEL = B.hist;       // first position index - first hit index, per offset
-            int carry = 0;
-            for (int q0 = 0; q0 < L; q0 += 64) {
-                const int q = q0 + lane;
-                uint32_t k, c = 0, lo = 0;
-                if (q + TILE <= L && tile_key(D.q, q, k)) {
-                    lo = X.start[k];
-                    c = X.start[k + 1] - lo;
-                    if ((int64_t)c > bp.rep_match) c = 0;
-                }
-                const int inc = wave_incl_sum((int)c, lane);
-                const int bq = carry + inc - (int)c;
-                if (q < L) { DEL[q] = lo - (uint32_t)bq; B.base[q] = bq; }
-                carry += __builtin_amdgcn_readlane(inc, 63);
-            }
-            wave_sync();
-            // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
-            // in flight.  With the drift filter (min_match >= 2) the hits are gathered twice: the
-            // first pass only marks their buckets (LDS), the second keeps round 0's survivors --
-            // the one list written to scratch is theirs (125 of 7,633 hits per strand at configs[2])
-            const int nh_all = min(carry, NMAX);
-            if (lane == 0 && carry > NMAX) caps.hit(qi, AF_BLAT_CAP_HITS);
-            auto gather = [&](int h0, int &qc, int (&qv)[4], uint32_t (&pv)[4]) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int h = h0 + 64 * j + lane;
-                    int q = qc;  // the last offset whose first hit index is <= h
-                    if (h < nh_all)
-                        while (q + 1 < L && B.base[q + 1] <= h) ++q;
-                    qv[j] = q;
-                }
-                qc = __builtin_amdgcn_readlane(qv[3], 63);  // (a full group: lane 63 of chunk 3 is a hit)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int h = h0 + 64 * j + lane;
-                    pv[j] = h < nh_all ? X.pos[DEL[qv[j]] + (uint32_t)h] : 0u;
-                }
-            };
-            int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
-            for (int h0 = 0; h0 < nh_all; h0 += 256) {
-                int qv[4];
-                uint32_t pv[4];
-                gather(h0, qc, qv, pv);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int h = h0 + 64 * j + lane;
-                    if (h < nh_all) {
-                        const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
-                        if (filt) drift_mark(key, wsh, 0);
-                        else KA[h] = key;
-                    }
-                }
-            }
-            int nh = nh_all;
-            __threadfence_block();
-            wave_sync();
-            if (nh == 0) continue;
-            BPM(0);
-            BP(ch += nh;)
-            // ---- drop hits with no other hit within the drift (they cannot join a clump of
-            // min_match >= 2 hits, and removing them changes no other run): hashed bucket bitmaps,
-            // false keeps only, a few rounds while they pay ---------------------------------------
-            uint64_t *H0 = KA, *H1 = KB;
-            if (filt) {
-                // round 0 on the second gathering pass, its survivors in order into H0
-                int nk = 0;
-                qc = 0;
-                for (int h0 = 0; h0 < nh_all; h0 += 256) {
-                    int qv[4];
-                    uint32_t pv[4];
-                    gather(h0, qc, qv, pv);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int h = h0 + 64 * j + lane;
-                        const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
-                        const bool keep = h < nh_all && drift_kept(key, drift, wsh, 0);
-                        const uint64_t m = __ballot(keep);
-                        if (keep) H0[nk + lanes_below_blat(m, lane)] = key;
-                        nk += (int)__builtin_popcountll(m);
-                    }
-                }
-                __threadfence_block();
-                wave_sync();
-                bool stop = nk * 8 > nh * 7;
-                nh = nk;
-                for (int round = 1; !stop && round < AF_BLAT_ROUNDS && nh > AF_BLAT_FILTER_MIN; ++round) {
-                    const int nk2 = drift_filter(H0, H1, nh, drift, wsh, round, lane);
-                    uint64_t *t = H0; H0 = H1; H1 = t;
-                    stop = nk2 * 8 > nh * 7;
-                    nh = nk2;
-                }
-            }
-            BPM(5);
-            BP(cs += nh;)
-            if (nh == 0) continue;
-            // ---- sort by diagonal (stable: offsets ascending within a diagonal) ------------------
-            const uint64_t *S = wave_radix_sort(H0, H1, nh, 9, diag_passes, lane);
-            uint32_t *ST = reinterpret_cast<uint32_t *>(S == H0 ? H1 : H0);
-            BPM(1);
-            // ---- run starts, then the clumps (runs of min_match hits) in diagonal order -----------
-            int nrun = 0;
-            for (int i0 = 0; i0 < nh; i0 += 64) {
-                const int i = i0 + lane;
-                bool st = false;
-                if (i < nh) st = i == 0 || (int64_t)(S[i] >> 9) - (int64_t)(S[i - 1] >> 9) > drift;
-                const uint64_t m = __ballot(st);
-                if (st) ST[nrun + lanes_below_blat(m, lane)] = (uint32_t)i;
-                nrun += (int)__builtin_popcountll(m);
-            }
-            __threadfence_block();
-            wave_sync();
-            int ncl = 0;
-            for (int r0 = 0; r0 < nrun && ncl < MAXCL; r0 += 64) {
-                const int r = r0 + lane;
-                bool keep = false;
-                Clump cc{};
-                if (r < nrun) {
-                    const int s0 = (int)ST[r], e0 = r + 1 < nrun ? (int)ST[r + 1] : nh;
-                    if (e0 - s0 >= bp.min_match) {
-                        keep = true;
-                        int bq = 1 << 30;
-                        int64_t bt = 0;
-                        for (int i = s0; i < e0; ++i) {
-                            const int qq = (int)(S[i] & 511u);
-                            const int64_t tt = (int64_t)(S[i] >> 9) - 1024 + qq;
-                            if (qq < bq || (qq == bq && tt < bt)) { bq = qq; bt = tt; }
-                        }
-                        cc.cnt = e0 - s0; cc.q = bq; cc.t = bt; cc.diag = bt - bq;
-                    }
-                }
-                const uint64_t m = __ballot(keep);
-                const int slot = ncl + lanes_below_blat(m, lane);
-                if (keep && slot < MAXCL) CL[slot] = cc;
-                ncl = min(MAXCL, ncl + (int)__builtin_popcountll(m));
-            }
-            __threadfence_block();
-            wave_sync();
-            if (lane == 0 && ncl == MAXCL) caps.hit(qi, AF_BLAT_CAP_CLUMPS);
-            if (ncl == 0) continue;
-            // ---- clump order: hits desc, then diagonal (= run order) ------------------------------
-            for (int i = lane; i < ncl; i += 64)
-                KA[i] = ((uint64_t)(65535 - CL[i].cnt) << 32) | (uint32_t)i;
-            __threadfence_block();
-            wave_sync();
-            const uint64_t *CO = wave_radix_sort(KA, KB, ncl, 32, 2, lane);
-            BPM(2);
-            BP(cc_ += ncl;)
-            // ---- a heavy strand's clumps are aligned later as grid-wide jobs (k_blat_jobs), its
-            // chains by k_blat_heavy: its serial part loop would set the search's makespan --------
-            if (hv.min_clumps > 0 && ncl > hv.min_clumps && defer_strand(hv, CL, CO, ncl, 2 * qi + s_item, lane)) {
-#ifdef AF_BLAT_CHECK
-                if (lane == 0 && qi < 4) printf("defer: q %ld s %d clumps %d L %d\n", (long)qi, s_item, ncl, L);
-#endif
-                deferred = true;
-                continue;
-            }
-            // ---- parts: one per clump whose seed lies in no earlier part (lanes over the parts) ----
-            int nr = 0, c = 0;
-            for (; c < ncl && nr < MAXP; ++c) {
-                const Clump cc = CL[(uint32_t)CO[c]];
-                if (inside_part(RG, nr, cc.q, cc.t, lane)) continue;
-                if (align_clump<CPL>(X, L, cc.q, cc.t, RG[nr], zg, lane)) ++nr;
-                __threadfence_block();
-                wave_sync();
-            }
-            if (lane == 0 && nr == MAXP && c < ncl) caps.hit(qi, AF_BLAT_CAP_PARTS);
-            if (nr == 0) continue;
-            BPM(3);
-            BP(cr += nr;)
-            strand_chains(X, bp, RG, CD, nr, qi, strand, L, KA, KB, RW, max_rows, caps, spill, lane);
-        }
-        BPM(4);
-        if (!deferred) strand_stage(stage, stage_n, qi, s_item, max_rows, RW, lane);
-        BP(if (lane == 0 && g_blprof && qi < (1 << 22)) {
-            int32_t *pf = g_blprof + qi * 16;
-            for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
-            pf[5] = ch; pf[6] = cc_; pf[7] = cr; pf[8] = L;
-            pf[9] = (int32_t)min(clock64() - tq0, (int64_t)0x7fffffff);
-            pf[10] = (int32_t)min(pc[5], (int64_t)0x7fffffff); pf[11] = cs; pf[12] = deferred ? 1 : 0;
-        })
-        __threadfence_block();
-        wave_sync();
-    }
-}
-
-// the query codes of (qi, strand) into D.q (strand 1: the reverse complement); returns its length
-__device__ __forceinline__ int load_strand(const uint8_t *queries, int32_t stride, const int32_t *lens, int64_t qi, int strand,
-                           int lane) {
+// the query codes of (qi, strand) into B.q (strand 1: the reverse complement); returns its length
+__device__ __forceinline__ int load_strand(BlatLds &B, const uint8_t *queries, int32_t stride, const int32_t *lens, int64_t qi,
+                                           int strand, int lane) {
     int L = lens ? lens[qi] : stride;
     if (L > stride) L = stride;
     if (L > AF_MAX_READ) L = AF_MAX_READ;
@@ -919,19 +632,266 @@ __device__ __forceinline__ int load_strand(const uint8_t *queries, int32_t strid
     const uint8_t *row = queries + qi * (int64_t)stride;
     for (int x = lane; x < L; x += 64) {
         const uint8_t c = nt4(row[strand ? L - 1 - x : x]);
-        g_dp.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
+        B.q[x] = strand ? (c > 3 ? 4 : 3 - c) : c;
     }
     wave_sync();
     return L;
 }
 
-// next work item of a persistent grid from 8 per-XCD heads (item = head + 8 * k), or n when drained
-__device__ __forceinline__ int64_t next_item(int32_t *heads, int64_t n, int &head, int &heads_left, int lane) {
+// One query strand (item 2 qi + strand) on the wave, with the slot's scratch zg: its rows to the
+// item's stage; true when it was left to k_blat_heavy instead (allow_defer, a strand table with
+// room, more than hv.min_clumps clumps).
+__device__ __forceinline__ bool search_strand(BlatLds &B, const DevTile &X, const uint8_t *queries, int32_t stride,
+                                              const int32_t *lens, const af_blat_params &bp, int64_t qi, int strand,
+                                              uint8_t *zg, int32_t diag_passes, af_psl *stage, int32_t *stage_n,
+                                              int32_t max_rows, const BlatCaps &caps, const BlatSpill &spill,
+                                              const BlatHeavy &hv, bool allow_defer, int lane) {
+    uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
+    Clump *CL = reinterpret_cast<Clump *>(zg + SC_CLUMP);
+    Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
+    af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
+    int32_t *dpw = reinterpret_cast<int32_t *>(zg + SC_DP);
+    const ChainDp CD{dpw, dpw + MAXP, dpw + 2 * MAXP, dpw + 3 * MAXP, dpw + 4 * MAXP, dpw + 5 * MAXP,
+                     reinterpret_cast<uint32_t *>(dpw + 6 * MAXP), reinterpret_cast<uint32_t *>(dpw + 7 * MAXP)};
+    const int L = load_strand(B, queries, stride, lens, qi, strand, lane);
+    if (lane == 0) B.nrow = 0;
+    wave_sync();
+    const int64_t drift = (int64_t)bp.max_gap + 2;
+    int wsh = 3;  // bucket width 1 << wsh >= 2 * drift: [d - drift, d + drift] meets <= 2 buckets
+    while ((1ll << wsh) < 2 * drift) ++wsh;
+    BP(int64_t tq0 = clock64(), tq = tq0; int64_t pc[6] = {0, 0, 0, 0, 0, 0}; int ch = 0, cc_ = 0, cr = 0, cs = 0, crg = 0;)
+    bool deferred = false;
+    do {
+        // ---- per offset: its tile's position range (count 0: N inside, absent or over rep_match) --
+        const bool filt = bp.min_match >= 2;
+        if (filt) drift_clear(B, lane);  // round 0 of the drift filter is marked while collecting
+        uint32_t *DEL = B.hist;          // first position index - first hit index, per offset
+        int carry = 0;
+        for (int q0 = 0; q0 < L; q0 += 64) {
+            const int q = q0 + lane;
+            uint32_t k, c = 0, lo = 0;
+            if (q + TILE <= L && tile_key(B.q, q, k)) {
+                lo = X.start[k];
+                c = X.start[k + 1] - lo;
+                if ((int64_t)c > bp.rep_match) c = 0;
+            }
+            const int inc = wave_incl_sum((int)c, lane);
+            const int bq = carry + inc - (int)c;
+            if (q < L) { DEL[q] = lo - (uint32_t)bq; B.base[q] = bq; }
+            carry += __builtin_amdgcn_readlane(inc, 63);
+        }
+        wave_sync();
+        // ---- every hit, the first NMAX in (offset, position) order: lanes over hits, 4 chunks
+        // in flight.  With the drift filter (min_match >= 2) the hits are gathered twice: the
+        // first pass only marks their buckets (LDS), the second keeps round 0's survivors
+        const int nh_all = min(carry, NMAX);
+        // (a deferred strand's hit and clump caps were counted by k_blat: not again here)
+        if (lane == 0 && carry > NMAX && allow_defer) caps.hit(qi, AF_BLAT_CAP_HITS);
+        auto gather = [&](int h0, int &qc, int (&qv)[4], uint32_t (&pv)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int h = h0 + 64 * j + lane;
+                int q = qc;  // the last offset whose first hit index is <= h
+                if (h < nh_all)
+                    while (q + 1 < L && B.base[q + 1] <= h) ++q;
+                qv[j] = q;
+            }
+            qc = __builtin_amdgcn_readlane(qv[3], 63);  // (a full group: lane 63 of chunk 3 is a hit)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int h = h0 + 64 * j + lane;
+                pv[j] = h < nh_all ? X.pos[DEL[qv[j]] + (uint32_t)h] : 0u;
+            }
+        };
+        int qc = 0;  // offset of the group's first hit (hit offsets are nondecreasing)
+        for (int h0 = 0; h0 < nh_all; h0 += 256) {
+            int qv[4];
+            uint32_t pv[4];
+            gather(h0, qc, qv, pv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int h = h0 + 64 * j + lane;
+                if (h < nh_all) {
+                    const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
+                    if (filt) drift_mark(B, key, wsh, 0);
+                    else KA[h] = key;
+                }
+            }
+        }
+        int nh = nh_all;
+        __threadfence_block();
+        wave_sync();
+        if (nh == 0) break;
+        BPM(0);
+        BP(ch += nh;)
+        // ---- drop hits with no other hit within the drift (they cannot join a clump of
+        // min_match >= 2 hits, and removing them changes no other run) ----------------------
+        uint64_t *H0 = KA, *H1 = KB;
+        if (filt) {
+            int nk = 0;
+            qc = 0;
+            for (int h0 = 0; h0 < nh_all; h0 += 256) {
+                int qv[4];
+                uint32_t pv[4];
+                gather(h0, qc, qv, pv);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int h = h0 + 64 * j + lane;
+                    const uint64_t key = ((uint64_t)((int64_t)pv[j] - qv[j] + 1024) << 9) | (uint32_t)qv[j];
+                    const bool keep = h < nh_all && drift_kept(B, key, drift, wsh, 0);
+                    const uint64_t m = __ballot(keep);
+                    if (keep) H0[nk + lanes_below_blat(m, lane)] = key;
+                    nk += (int)__builtin_popcountll(m);
+                }
+            }
+            __threadfence_block();
+            wave_sync();
+            bool stop = nk * 8 > nh * 7;
+            nh = nk;
+            for (int round = 1; !stop && round < AF_BLAT_ROUNDS && nh > AF_BLAT_FILTER_MIN; ++round) {
+                const int nk2 = drift_filter(B, H0, H1, nh, drift, wsh, round, lane);
+                uint64_t *t = H0; H0 = H1; H1 = t;
+                stop = nk2 * 8 > nh * 7;
+                nh = nk2;
+            }
+        }
+        BPM(5);
+        BP(cs += nh;)
+        if (nh == 0) break;
+        // ---- sort by diagonal (stable: offsets ascending within a diagonal) ------------------
+        const uint64_t *S = wave_radix_sort(B, H0, H1, nh, 9, diag_passes, lane);
+        uint8_t *SO = reinterpret_cast<uint8_t *>(S == H0 ? H1 : H0);  // the spare key buffer
+        uint32_t *ST = reinterpret_cast<uint32_t *>(SO);
+        BPM(1);
+        // ---- run starts, then the clumps (runs of min_match hits) in diagonal order -----------
+        int nrun = 0;
+        for (int i0 = 0; i0 < nh; i0 += 64) {
+            const int i = i0 + lane;
+            bool st = false;
+            if (i < nh) st = i == 0 || (int64_t)(S[i] >> 9) - (int64_t)(S[i - 1] >> 9) > drift;
+            const uint64_t m = __ballot(st);
+            if (st) ST[nrun + lanes_below_blat(m, lane)] = (uint32_t)i;
+            nrun += (int)__builtin_popcountll(m);
+        }
+        __threadfence_block();
+        wave_sync();
+        int ncl = 0;
+        for (int r0 = 0; r0 < nrun && ncl < MAXCL; r0 += 64) {
+            const int r = r0 + lane;
+            bool keep = false;
+            Clump cc{};
+            if (r < nrun) {
+                const int s0 = (int)ST[r], e0 = r + 1 < nrun ? (int)ST[r + 1] : nh;
+                if (e0 - s0 >= bp.min_match) {
+                    keep = true;
+                    cc.cnt = e0 - s0; cc.h0 = s0; cc.h1 = e0;
+                }
+            }
+            const uint64_t m = __ballot(keep);
+            const int slot = ncl + lanes_below_blat(m, lane);
+            if (keep && slot < MAXCL) CL[slot] = cc;
+            ncl = min(MAXCL, ncl + (int)__builtin_popcountll(m));
+        }
+        __threadfence_block();
+        wave_sync();
+        if (lane == 0 && ncl == MAXCL && allow_defer) caps.hit(qi, AF_BLAT_CAP_CLUMPS);
+        if (ncl == 0) break;
+        // ---- range starts over the sorted hits (ranges never cross a run): a hit starts one
+        // when its diagonal differs from the previous hit's or its tile starts past that one's end
+        uint32_t *RS = reinterpret_cast<uint32_t *>(SO + SC_RANGES);
+        int nrs = 0;
+        for (int i0 = 0; i0 < nh; i0 += 64) {
+            const int i = i0 + lane;
+            bool st = false;
+            if (i < nh) {
+                const uint64_t k = S[i];
+                if (i == 0) st = true;
+                else {
+                    const uint64_t kp = S[i - 1];
+                    st = (k >> 9) != (kp >> 9) || (int)(k & 511u) > (int)(kp & 511u) + TILE;
+                }
+            }
+            const uint64_t m = __ballot(st);
+            if (st) RS[nrs + lanes_below_blat(m, lane)] = (uint32_t)i;
+            nrs += (int)__builtin_popcountll(m);
+        }
+        // ---- clump order: hits desc, then diagonal (= run order) ------------------------------
+        uint64_t *OA = reinterpret_cast<uint64_t *>(SO), *OB = OA + MAXCL;
+        for (int i = lane; i < ncl; i += 64) OA[i] = ((uint64_t)(65535 - CL[i].cnt) << 32) | (uint32_t)i;
+        __threadfence_block();
+        wave_sync();
+        const uint64_t *CO = wave_radix_sort(B, OA, OB, ncl, 32, 2, lane);
+        BPM(2);
+        BP(cc_ += ncl;)
+        // ---- a heavy strand is left to k_blat_heavy, which searches it after the caller's
+        // live flags are known (S6: after S5's check) ------------------------------------------
+        if (allow_defer && hv.min_clumps > 0 && ncl > hv.min_clumps) {
+            int ok = 0;
+            if (lane == 0) {
+                const int s = atomicAdd(hv.strands_n, 1);
+                if (s < hv.strands_cap) {
+                    hv.strands[s] = make_int4((int)(2 * qi + strand), 0, ncl, 0);
+                    atomicAdd(hv.jobs_n, ncl);
+                    ok = 1;
+                }
+            }
+            if (__builtin_amdgcn_readfirstlane(ok)) { deferred = true; break; }
+        }
+        // ---- HSPs: per clump in order, its ranges in order; a range inside an HSP made before
+        // makes none ---------------------------------------------------------------------------
+        int nr = 0;
+        bool capped = false;
+        for (int c = 0; c < ncl && !capped; ++c) {
+            const Clump cc = CL[(uint32_t)CO[c]];
+            const int k0 = lower_bound_u32(RS, nrs, (uint32_t)cc.h0), k1 = lower_bound_u32(RS, nrs, (uint32_t)cc.h1);
+            for (int k = k0; k < k1; ++k) {
+                const int hs = (int)RS[k], he = (k + 1 < nrs ? (int)RS[k + 1] : nh) - 1;
+                const uint64_t ks = S[hs], ke = S[he];
+                const int q0 = (int)(ks & 511u), q1 = (int)(ke & 511u) + TILE;
+                const int64_t t0 = (int64_t)(ks >> 9) - 1024 + q0, t1 = t0 + (q1 - q0);
+                BP(++crg;)
+                if (inside_part(RG, nr, q0, q1, t0, t1, lane)) continue;
+                if (nr == MAXP) { capped = true; break; }
+                const Reg r = hsp_range(X, B.q, L, q0, q1, t0, lane);
+                if (lane == 0) RG[nr] = r;
+                ++nr;
+                __threadfence_block();
+                wave_sync();
+            }
+        }
+        if (lane == 0 && capped) caps.hit(qi, AF_BLAT_CAP_PARTS);
+        BPM(3);
+        BP(cr += nr;)
+        if (nr > 0) strand_chains(B, X, bp, RG, CD, nr, qi, strand, L, KA, KB, RW, max_rows, caps, spill, capped, lane);
+    } while (false);
+    BPM(4);
+    if (!deferred && lane == 0) {  // the strand's rows (RW holds the first max_rows of B.nrow in order)
+        const int n = B.nrow;
+        const int m = n < max_rows ? n : max_rows;
+        const int64_t sl = 2 * qi + strand;
+        for (int k = 0; k < m; ++k) stage[sl * max_rows + k] = RW[k];
+        stage_n[sl] = n;  // all of the strand's rows (k_blat_merge takes the first max_rows)
+    }
+    BP(if (lane == 0 && g_blprof && qi < (1 << 22)) {
+        int32_t *pf = g_blprof + qi * 16;
+        for (int k = 0; k < 5; ++k) pf[k] = (int32_t)min(pc[k], (int64_t)0x7fffffff);
+        pf[5] = ch; pf[6] = cc_; pf[7] = cr; pf[8] = L;
+        pf[9] = (int32_t)min(clock64() - tq0, (int64_t)0x7fffffff);
+        pf[10] = (int32_t)min(pc[5], (int64_t)0x7fffffff); pf[11] = cs; pf[12] = deferred ? 1 : 0; pf[13] = crg;
+    })
+    __threadfence_block();
+    wave_sync();
+    return deferred;
+}
+
+// next work item of a persistent grid from 8 per-XCD heads (item = first + head + 8 * k), or n
+// when drained
+__device__ __forceinline__ int64_t next_item(int32_t *heads, int64_t first, int64_t n, int &head, int &heads_left, int lane) {
     while (heads_left > 0) {
         int v = 0;
         if (lane == 0) v = atomicAdd(&heads[AF_HEAD_STRIDE * head], 1);
         v = __builtin_amdgcn_readfirstlane(v);
-        const int64_t it = head + 8 * (int64_t)v;
+        const int64_t it = first + head + 8 * (int64_t)v;
         if (it < n) return it;
         head = (head + 1) & 7;
         --heads_left;
@@ -939,129 +899,59 @@ __device__ __forceinline__ int64_t next_item(int32_t *heads, int64_t n, int &hea
     return n;
 }
 
-// one clump job of a deferred strand per wave: its part (align_clump from the clump's seed tile)
-// into the part pool, ok flag beside it; jobs of queries not live are skipped
-template <int CPL>
-__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat_jobs(DevTile X, const uint8_t *__restrict__ queries,
-                                                             int32_t stride, const int32_t *__restrict__ lens,
-                                                             BlatHeavy hv, const uint8_t *__restrict__ live,
-                                                             int32_t *__restrict__ heads, uint8_t *__restrict__ bscratch) {
+// every query strand of [q_first, n_q), heaviest queries first (order): items 2k + s = strand s of
+// the k-th query, so a heavy query's strands run on two waves at once
+__global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat(DevTile X, const uint8_t *__restrict__ queries, int32_t stride,
+                                                        const int32_t *__restrict__ lens, af_blat_params bp,
+                                                        const int32_t *__restrict__ n_q, const int32_t *__restrict__ q_first,
+                                                        int64_t cap, int32_t *__restrict__ heads,
+                                                        uint8_t *__restrict__ bscratch, int32_t diag_passes,
+                                                        af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
+                                                        int32_t max_rows, const int32_t *__restrict__ order, BlatCaps caps,
+                                                        BlatSpill spill, BlatHeavy hv) {
+    __shared__ BlatLds B;
     const int lane = threadIdx.x;
+    const int64_t nq64 = *n_q < cap ? *n_q : cap;
+    const int nq = (int)(nq64 < 0 ? 0 : nq64);
+    const int q0 = q_first ? max(0, min(*q_first, nq)) : 0;  // queries [q0, nq)
     uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
-    int64_t n = *hv.jobs_n;
-    if (n > hv.jobs_cap) n = hv.jobs_cap;
-    if (n > *hv.jobs_valid) n = *hv.jobs_valid;
-    Reg *parts = reinterpret_cast<Reg *>(hv.parts);
-#ifdef AF_BLAT_CHECK
-    if (blockIdx.x == 0 && lane == 0)
-        printf("k_blat_jobs: n %ld jobs_n %d valid %d cap %ld strands_n %d heads0 %d\n", (long)n, *hv.jobs_n, *hv.jobs_valid,
-               (long)hv.jobs_cap, *hv.strands_n, heads[0]);
-#endif
     int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
-        const int64_t j = next_item(heads, n, head, heads_left, lane);
-        if (j >= n) break;
-        const BlatJob jb = hv.jobs[j];
-#ifdef AF_BLAT_CHECK
-        if (jb.hs < 0 || jb.hs >= hv.strands_cap || jb.hs >= *hv.strands_n) {
-            if (lane == 0) printf("k_blat_jobs: job %ld strand %d outside [0, %d)\n", (long)j, jb.hs, *hv.strands_n);
-            continue;
-        }
-#endif
-        const int4 st = hv.strands[jb.hs];
-        const int64_t qi = st.x >> 1;
-#ifdef AF_BLAT_CHECK
-        if (qi < 0 || j < st.y || j >= (int64_t)st.y + st.z || jb.q < 0 || jb.t < 0 || jb.t >= X.n) {
-            if (lane == 0) printf("k_blat_jobs: job %ld (q %d t %ld) strand {%d %d %d}\n", (long)j, jb.q, (long)jb.t, st.x, st.y, st.z);
-            continue;
-        }
-#endif
-        if (live && !live[qi]) continue;
-        const int L = load_strand(queries, stride, lens, qi, st.x & 1, lane);
-        const bool ok = align_clump<CPL>(X, L, jb.q, jb.t, parts[j], zg, lane);
-        if (lane == 0) {
-            hv.part_ok[j] = ok ? 1 : 0;
-            atomicAdd(hv.ctrl + AF_BLAT_HV_JOBS_DONE, 1);
-        }
-#ifdef AF_BLAT_CHECK
-        if (lane == 0 && j % 100 < 2)
-            printf("jobs: q %ld s %d job %ld seed (%d, %ld) L %d ok %d part [%d %d) [%ld %ld) score %d nb %d\n", (long)qi,
-                   st.x & 1, (long)j, jb.q, (long)jb.t, L, ok ? 1 : 0, parts[j].qb, parts[j].qe, (long)parts[j].tb,
-                   (long)parts[j].te, parts[j].score, parts[j].nb);
-#endif
-        __threadfence_block();
-        wave_sync();
+        const int64_t item = next_item(heads, 2 * (int64_t)q0, 2 * (int64_t)nq, head, heads_left, lane);
+        if (item >= 2 * (int64_t)nq) break;
+        const int64_t qi = order ? order[item >> 1] : (item >> 1);
+        search_strand(B, X, queries, stride, lens, bp, qi, (int)(item & 1), zg, diag_passes, stage, stage_n, max_rows,
+                      caps, spill, hv, true, lane);
     }
 }
 
-// one deferred strand per wave: its clumps in order, each taking its job's part unless its seed
-// lies in an earlier part (the order k_blat's part loop keeps), then the chains and the rows
-template <int CPL>
+// the deferred strands of the live queries, one per wave, searched in full
 __global__ __launch_bounds__(64, AF_BLAT_WPS) void k_blat_heavy(DevTile X, const uint8_t *__restrict__ queries,
                                                               int32_t stride, const int32_t *__restrict__ lens,
                                                               af_blat_params bp, BlatHeavy hv,
                                                               const uint8_t *__restrict__ live,
-                                                              int32_t *__restrict__ heads,
-                                                              uint8_t *__restrict__ bscratch,
-                                                              af_psl *__restrict__ stage, int32_t *__restrict__ stage_n,
-                                                              int32_t max_rows, BlatCaps caps, BlatSpill spill) {
+                                                              int32_t *__restrict__ heads, uint8_t *__restrict__ bscratch,
+                                                              int32_t diag_passes, af_psl *__restrict__ stage,
+                                                              int32_t *__restrict__ stage_n, int32_t max_rows,
+                                                              BlatCaps caps, BlatSpill spill) {
+    __shared__ BlatLds B;
     const int lane = threadIdx.x;
     uint8_t *zg = bscratch + (size_t)blockIdx.x * SC_END;
-    uint64_t *KA = reinterpret_cast<uint64_t *>(zg + SC_KEYS_A), *KB = reinterpret_cast<uint64_t *>(zg + SC_KEYS_B);
-    Reg *RG = reinterpret_cast<Reg *>(zg + SC_REGS);
-    af_psl *RW = reinterpret_cast<af_psl *>(zg + SC_ROWS);
-    int32_t *dpw = reinterpret_cast<int32_t *>(zg + SC_DP);
-    const ChainDp CD{dpw, dpw + MAXP, dpw + 2 * MAXP, dpw + 3 * MAXP, dpw + 4 * MAXP, dpw + 5 * MAXP,
-                     reinterpret_cast<uint32_t *>(dpw + 6 * MAXP), reinterpret_cast<uint32_t *>(dpw + 7 * MAXP)};
-    const Reg *parts = reinterpret_cast<const Reg *>(hv.parts);
     int64_t ns = *hv.strands_n;
     if (ns > hv.strands_cap) ns = hv.strands_cap;
     int head = (int)(blockIdx.x & 7), heads_left = 8;
     for (;;) {
-        const int64_t s = next_item(heads, ns, head, heads_left, lane);
+        const int64_t s = next_item(heads, 0, ns, head, heads_left, lane);
         if (s >= ns) break;
         const int4 st = hv.strands[s];
-        if (st.z == 0) continue;  // no room in the job pool: k_blat searched the strand itself
-#ifdef AF_BLAT_CHECK
-        if (st.x < 0 || st.y < 0 || (int64_t)st.y + st.z > hv.jobs_cap) {
-            if (lane == 0) printf("k_blat_heavy: strand %ld {%d %d %d} jobs_cap %ld\n", (long)s, st.x, st.y, st.z, (long)hv.jobs_cap);
-            continue;
-        }
-#endif
         const int64_t qi = st.x >> 1;
-        const int strand = st.x & 1;
         if (live && !live[qi]) continue;
-        const int L = load_strand(queries, stride, lens, qi, strand, lane);
-        if (lane == 0) g_bl.nrow = 0;
-        wave_sync();
-        int nr = 0, c = 0;
-        for (; c < st.z && nr < MAXP; ++c) {
-            const int64_t j = st.y + (int64_t)c;
-            const BlatJob jb = hv.jobs[j];
-            if (inside_part(RG, nr, jb.q, jb.t, lane)) continue;
-            if (!hv.part_ok[j]) continue;
-            const int32_t *src = reinterpret_cast<const int32_t *>(parts + j);
-            int32_t *dst = reinterpret_cast<int32_t *>(RG + nr);
-            for (int w = lane; w < (int)(sizeof(Reg) / 4); w += 64) dst[w] = src[w];
-#ifdef AF_BLAT_CHECK
-            if (lane == 0 && qi < 2 && nr < 3)
-                printf("heavy part: q %ld s %d job %ld seed (%d, %ld) ok %d part [%d %d) [%ld %ld) score %d m %d nb %d\n",
-                       (long)qi, strand, (long)j, jb.q, (long)jb.t, (int)hv.part_ok[j], parts[j].qb, parts[j].qe,
-                       (long)parts[j].tb, (long)parts[j].te, parts[j].score, parts[j].matches, parts[j].nb);
-#endif
-            ++nr;
-            __threadfence_block();
-            wave_sync();
+        search_strand(B, X, queries, stride, lens, bp, qi, st.x & 1, zg, diag_passes, stage, stage_n, max_rows, caps,
+                      spill, hv, false, lane);
+        if (lane == 0) {
+            atomicAdd(hv.ctrl + AF_BLAT_HV_JOBS_DONE, st.z);
+            atomicAdd(hv.ctrl + AF_BLAT_HV_STRANDS_DONE, 1);
         }
-        if (lane == 0 && nr == MAXP && c < st.z) caps.hit(qi, AF_BLAT_CAP_PARTS);
-        if (nr > 0) strand_chains(X, bp, RG, CD, nr, qi, strand, L, KA, KB, RW, max_rows, caps, spill, lane);
-        strand_stage(stage, stage_n, qi, strand, max_rows, RW, lane);
-        if (lane == 0) atomicAdd(hv.ctrl + AF_BLAT_HV_STRANDS_DONE, 1);
-#ifdef AF_BLAT_CHECK
-        if (lane == 0 && qi < 4) printf("heavy: q %ld s %d jobs [%d, +%d) parts %d rows %d\n", (long)qi, strand, st.y, st.z, nr, g_bl.nrow);
-#endif
-        __threadfence_block();
-        wave_sync();
     }
 }
 
@@ -1210,24 +1100,15 @@ hipError_t af_launch_blat_begin(const BlatLaunch &B, hipStream_t s) {
     hipError_t e;
     const BlatHeavy &hv = B.hv;
     if (hv.min_clumps > 0) {
-        // the heavy-strand pool's fills and dequeue heads (jobs_valid: 0x7f7f7f7f, above any pool)
-        if ((e = hipMemsetAsync(hv.ctrl, 0, sizeof(int32_t) * AF_BLAT_HV_CTRL_WORDS, s)) != hipSuccess ||
-            (e = hipMemsetAsync(hv.jobs_valid, 0x7f, sizeof(int32_t), s)) != hipSuccess)
-            return e;
+        // the strand table's fill, its counters and dequeue heads
+        if ((e = hipMemsetAsync(hv.ctrl, 0, sizeof(int32_t) * AF_BLAT_HV_CTRL_WORDS, s)) != hipSuccess) return e;
     }
     // radix passes over the diagonal bits: (diagonal + 1024) < n + 1024
     int bits = 64 - __builtin_clzll((unsigned long long)(B.X.n + 1024));
     const int diag_passes = (bits + 7) / 8;
-    const int cpl = (B.stride + 1 + 63) / 64;
-    dim3 g(B.n_slots), b(64);
-#define AF_GO(C) hipLaunchKernelGGL((k_blat<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, B.p, B.n_queries, \
-                                    B.q_first, B.cap, B.heads, B.bscratch, diag_passes, B.stage, B.stage_n, B.max_rows, \
-                                    B.order, B.caps, B.spill, hv)
-    if (cpl <= 2) AF_GO(2);
-    else if (cpl <= 3) AF_GO(3);
-    else if (cpl <= 4) AF_GO(4);
-    else AF_GO(AF_CPL);
-#undef AF_GO
+    hipLaunchKernelGGL(k_blat, dim3(B.n_slots), dim3(64), 0, s, B.X, B.queries, B.stride, B.lens, B.p, B.n_queries,
+                       B.q_first, B.cap, B.heads, B.bscratch, diag_passes, B.stage, B.stage_n, B.max_rows, B.order,
+                       B.caps, B.spill, hv);
     return hipGetLastError();
 }
 
@@ -1235,23 +1116,13 @@ hipError_t af_launch_blat_end(const BlatLaunch &B, const uint8_t *live, hipStrea
     const BlatHeavy &hv = B.hv;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int cpl = (B.stride + 1 + 63) / 64;
-    dim3 g(B.n_slots), b(64);
     if (hv.min_clumps > 0) {
-        int32_t *hj = hv.ctrl + AF_BLAT_HV_JOB_HEADS, *hs = hv.ctrl + AF_BLAT_HV_STRAND_HEADS;
-#define AF_GO(C)                                                                                                    \
-    do {                                                                                                            \
-        hipLaunchKernelGGL((k_blat_jobs<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, hv, live, hj, B.bscratch); \
-        if ((e = hipGetLastError()) != hipSuccess) return e;                                                        \
-        hipLaunchKernelGGL((k_blat_heavy<C>), g, b, 0, s, B.X, B.queries, B.stride, B.lens, B.p, hv, live, hs,        \
-                           B.bscratch, B.stage, B.stage_n, B.max_rows, B.caps, B.spill);                              \
-        if ((e = hipGetLastError()) != hipSuccess) return e;                                                        \
-    } while (0)
-        if (cpl <= 2) AF_GO(2);
-        else if (cpl <= 3) AF_GO(3);
-        else if (cpl <= 4) AF_GO(4);
-        else AF_GO(AF_CPL);
-#undef AF_GO
+        int bits = 64 - __builtin_clzll((unsigned long long)(B.X.n + 1024));
+        const int diag_passes = (bits + 7) / 8;
+        hipLaunchKernelGGL(k_blat_heavy, dim3(B.n_slots), dim3(64), 0, s, B.X, B.queries, B.stride, B.lens, B.p, hv, live,
+                           hv.ctrl + AF_BLAT_HV_STRAND_HEADS, B.bscratch, diag_passes, B.stage, B.stage_n, B.max_rows,
+                           B.caps, B.spill);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k_blat_merge, dim3((unsigned)((B.cap + 255) / 256)), dim3(256), 0, s, B.stage, B.stage_n,
                        B.n_queries, B.q_first, B.cap, B.max_rows, B.rows, B.n_rows, B.caps, B.spill, live);
@@ -1263,15 +1134,13 @@ hipError_t af_launch_blat(const BlatLaunch &B, hipStream_t s) {
     return e != hipSuccess ? e : af_launch_blat_end(B, nullptr, s);
 }
 
-size_t af_blat_part_bytes() { return sizeof(Reg); }
-
 int af_blat_slots(int n_cu) {
     if (const char *e = getenv("AF_BLAT_WAVES_PER_CU")) {  // experiment knob: resident BLAT waves per CU
         const int w = atoi(e);
         if (w > 0) return n_cu * w;
     }
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(k_blat<AF_CPL>), 64, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(k_blat), 64, 0) !=
             hipSuccess || occ < 1)
         occ = 8;
     return n_cu * occ;

@@ -163,6 +163,8 @@ int afo_blat(const afo_tiles *X, const uint8_t *queries, int64_t n_queries, int3
  * af_blat_caps: hits past MAXH per strand, MAXCL clumps reached, MAXR parts reached with clumps
  * left, per query rows past max_rows) */
 void afo_blat_set_literal(int on);  /* test switch: the chain DP recomputes every part each round */
+/* comparison switch: 1 = the round-5 gapped parts (ksw_extend2 per clump), 0 = gapless HSPs (default) */
+void afo_blat_set_gapped(int on);
 /* Long queries (afo_blat_long, af_blat_long): one query of up to AFO_BLAT_LONG_MAX bases searched
  * whole with the same algorithm -- caps: AFO_BLAT_LONG_HITS tile hits and AFO_BLAT_LONG_CLUMPS
  * clumps per strand, AFO_BLAT_LONG_PART_BLOCKS blocks per part; rows of any block count.  Every

@@ -8,6 +8,14 @@
  * options the reference passes (-stepSize, -minMatch, -repMatch, -minScore, -minIdentity,
  * defaults otherwise); the steps and the choices this restatement makes are in afgpu.h
  * (af_blat_params) and DESIGN.md §2.  Parity with the BLAT binary is unpinned.
+ *
+ * Alignment as the paper publishes it for nucleotides: the hits of a clump that lie on one
+ * diagonal with touching tiles form a range (an exact match), each range is extended WITHOUT gaps
+ * into a high-scoring segment pair (HSP: +1 per match, -1 per mismatch, an end stops XDOWN
+ * positions after its last new best -- blat's extendHitLeft / extendHitRight), and gaps appear
+ * only where HSPs are stitched into one alignment (the chain DP below).  The round-5 contract --
+ * one part per clump from a banded ksw_extend2 + global alignment, gaps inside parts -- is kept
+ * behind afo_blat_set_gapped(1) so that the two can be compared (tests, scripts/blat_modes.py).
  */
 #include <math.h>
 #include <stdlib.h>
@@ -25,6 +33,8 @@
  * emitted; the first pass is always made): once past it,
  * no further chain is emitted and the strand is counted as cap[2] */
 #define STITCH_WORK (1LL << 24)
+/* an HSP end stops this many positions after its running score last reached a new best */
+#define XDOWN 10
 
 struct afo_tiles {
     uint8_t *T;        /* codes 0-3, 4 = N */
@@ -124,7 +134,7 @@ typedef struct {
     int64_t b0t, boff;
     int used;
 } reg_b;
-typedef struct { int32_t cnt, q; int64_t diag, t; } clump_t;
+typedef struct { int32_t cnt, q; int64_t diag, t, h0, h1; } clump_t;  /* h0, h1: its hits in diagonal order */
 
 /* The caps of a search mode.  Short queries (afo_blat: reads and tails, <= AFO_MAX_READ bases)
  * are the GPU kernel k_blat's contract; long queries (afo_blat_long: the anchor transcript of
@@ -232,6 +242,43 @@ static int align_clump(const afo_tiles *X, const uint8_t *Q, int L, int32_t q, i
     return 1;
 }
 
+/* +1 / -1 per aligned base pair (an N on either side mismatches): the HSP extension's score */
+static inline int hsp_sc(uint8_t a, uint8_t b) { return (a > 3 || b > 3 || a != b) ? -1 : 1; }
+
+/* a range (the exact match [q0, q1) on diagonal t0 - q0) -> its HSP: extended without gaps to the
+ * left of q0 and the right of q1, each end at the first best running score, the walk stopped XDOWN
+ * positions after its last new best (blat's extendHitLeft / extendHitRight); one block */
+static void hsp_range(const afo_tiles *X, const uint8_t *Q, int L, int32_t q0, int32_t q1, int64_t t0, reg_b *r,
+                      blk_arena *ar) {
+    int s = 0, best = 0, nb = 0;
+    for (int i = 1; q0 - i >= 0 && t0 - i >= 0; ++i) {
+        s += hsp_sc(Q[q0 - i], X->T[t0 - i]);
+        if (s > best) { best = s; nb = i; }
+        else if (i - nb > XDOWN) break;
+    }
+    const int32_t qb = q0 - nb;
+    const int64_t tb = t0 - nb, t1 = t0 + (q1 - q0);
+    s = best = nb = 0;
+    for (int i = 1; q1 + i - 1 < L && t1 + i - 1 < X->n; ++i) {
+        s += hsp_sc(Q[q1 + i - 1], X->T[t1 + i - 1]);
+        if (s > best) { best = s; nb = i; }
+        else if (i - nb > XDOWN) break;
+    }
+    memset(r, 0, sizeof(*r));
+    r->qb = qb; r->qe = q1 + nb; r->tb = tb; r->te = t1 + nb;
+    for (int32_t x = r->qb; x < r->qe; ++x) {
+        const uint8_t a = Q[x], b = X->T[tb + (x - qb)];
+        if (a > 3 || b > 3) ++r->ncount;
+        else if (a == b) ++r->matches;
+        else ++r->mismatches;
+    }
+    r->score = r->matches - r->mismatches;
+    r->boff = ar->n;
+    arena_push(ar, r->qe - r->qb, r->qb, r->tb);
+    r->nb = 1;
+    r->b0sz = r->qe - r->qb; r->b0q = r->qb; r->b0t = r->tb;
+}
+
 /* r without its first k aligned bases (k inside the first block): the chain's query / target
  * overlap with the previous part is given to that part; 0 if k does not fit */
 static int trim_front(const afo_tiles *X, const uint8_t *Q, const reg_b *r, int k, reg_b *o) {
@@ -283,6 +330,9 @@ static int cmp_psl(const void *a, const void *b);
 /* test switch: 1 = the chain DP recomputes every unused part each round (afo_blat_set_literal) */
 static int g_blat_literal = 0;
 void afo_blat_set_literal(int on) { g_blat_literal = on; }
+/* comparison switch: 1 = the round-5 parts (one gapped ksw extension per clump), 0 = HSPs */
+static int g_blat_gapped = 0;
+void afo_blat_set_gapped(int on) { g_blat_gapped = on; }
 
 /* the chain DP of part i (position i of ord) over the unused parts before it: a predecessor a
  * must end before i on both sequences; i is trimmed by the overlap (chain_trim) and must keep part
@@ -402,7 +452,7 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
         }
         if (j - i + 1 >= bp->min_match) {
             cl[ncl].cnt = (int32_t)(j - i + 1); cl[ncl].q = hits[bq].q; cl[ncl].t = hits[bq].t;
-            cl[ncl].diag = hits[bq].diag;
+            cl[ncl].diag = hits[bq].diag; cl[ncl].h0 = i; cl[ncl].h1 = j + 1;
             ++ncl;
         }
         i = j + 1;
@@ -410,16 +460,41 @@ static void blat_strand(const afo_tiles *X, const afo_blat_params *bp, const uin
     if (ncl == md->maxcl) cap[1] = 1;
     qsort(cl, ncl, sizeof(clump_t), cmp_clump);  /* (hits desc, diagonal): keys are unique */
     int nr = 0, c = 0;
-    for (; c < ncl && nr < md->maxcl; ++c) {
-        int32_t q = cl[c].q;
-        int64_t t = cl[c].t;
-        int skip = 0;
-        for (int r = 0; r < nr; ++r)
-            if (regs[r].qb <= q && q + TILE <= regs[r].qe && regs[r].tb <= t && t + TILE <= regs[r].te) { skip = 1; break; }
-        if (skip) continue;
-        if (align_clump(X, Q, L, q, t, &regs[nr], md, &M->ar, M->qs, M->ts, M->cig)) ++nr;
+    if (g_blat_gapped) {
+        for (; c < ncl && nr < md->maxcl; ++c) {
+            int32_t q = cl[c].q;
+            int64_t t = cl[c].t;
+            int skip = 0;
+            for (int r = 0; r < nr; ++r)
+                if (regs[r].qb <= q && q + TILE <= regs[r].qe && regs[r].tb <= t && t + TILE <= regs[r].te) { skip = 1; break; }
+            if (skip) continue;
+            if (align_clump(X, Q, L, q, t, &regs[nr], md, &M->ar, M->qs, M->ts, M->cig)) ++nr;
+        }
+        if (nr == md->maxcl && c < ncl) cap[2] = 1;
+    } else {
+        /* HSPs: per clump in order, its hits in (diagonal, offset) order; a range = hits of one
+         * diagonal whose tiles touch (the next tile starts at or before the range's end); a range
+         * inside (as a box) an HSP made before makes none; the first maxcl HSPs are kept (cap[2]) */
+        for (; c < ncl; ++c) {
+            for (int64_t h = cl[c].h0; h < cl[c].h1;) {
+                const int64_t r0 = h;
+                int32_t q1 = hits[h].q + TILE;
+                while (h + 1 < cl[c].h1 && hits[h + 1].diag == hits[r0].diag && hits[h + 1].q <= q1) {
+                    ++h;
+                    q1 = hits[h].q + TILE;
+                }
+                ++h;
+                const int32_t q0 = hits[r0].q;
+                const int64_t t0 = hits[r0].t, t1 = t0 + (q1 - q0);
+                int skip = 0;
+                for (int r = 0; r < nr && !skip; ++r)
+                    skip = regs[r].qb <= q0 && q1 <= regs[r].qe && regs[r].tb <= t0 && t1 <= regs[r].te;
+                if (skip) continue;
+                if (nr == md->maxcl) { cap[2] = 1; c = ncl; break; }
+                hsp_range(X, Q, L, q0, q1, t0, &regs[nr++], &M->ar);
+            }
+        }
     }
-    if (nr == md->maxcl && c < ncl) cap[2] = 1;
     if (nr == 0) return;
     /* regions in (qb, tb, qe) order for the chain DP (stable: ties keep their creation order) */
     int *ord = M->ord;
