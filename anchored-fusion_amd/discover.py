@@ -37,6 +37,9 @@ _S6_EARLY = os.environ.get("AF_S6_EARLY", "1") == "1"
 # for every pre-check query (1), or after the check for its survivors only (0, the default: on
 # configs[2] a query the check drops holds a 3,559-part strand whose serial chain DP costs
 # 177 ms of step -- 428.8 vs 252.0 ms per step, profiles/r05/knobs_s6_heavy.txt)
+# (experiment knob only: with it, the heavy strands of queries the check drops also spill their
+# rows past MAX_ROWS into the shared pre-check pool, so a full pool can drop survivors' rows in
+# atomic order -- afgpu.h's byte-for-byte equality holds for the default, end(live), only)
 _S6_HEAVY_EARLY = os.environ.get("AF_S6_HEAVY_EARLY", "0") == "1"
 _DEBUG = os.environ.get("AF_DEBUG_DISCOVER") == "1"
 

@@ -84,8 +84,8 @@ class Placer:
         for i, (nm, sq) in enumerate(queries):
             if len(sq) > _lib.AF_MAX_READ:
                 rows, n_all, blocks, off = ref.search_long(sq, p)
-                if n_all > len(rows):
-                    raise _lib.AFError(f"af_blat_long: {n_all} rows for {nm}, {len(rows)} returned")
+                if n_all > len(rows):  # more rows than the first call returned: all of them
+                    rows, n_all, blocks, off = ref.search_long(sq, p, max_rows=n_all)
                 lines[i] = blat.psl_lines_long(ref, nm, sq, rows, blocks, off)
         out = list(header)
         for ln in lines:
