@@ -38,7 +38,9 @@ namespace {
 __device__ int32_t *g_gprof = nullptr;
 __device__ int64_t g_gprof_cap = 0;
 __device__ int32_t g_gprof_call = 0;
-constexpr int GP_W = 32;  // [24, 32): k_g_pe's phases on the pair's first read
+// [0, 27) G1 (lane path) and G2, [27, 32) G1's wave path, [32, 40) k_g_pe's phases on the pair's
+// first read: disjoint, so a read of both paths (or an S4 pair's first read) keeps every field
+constexpr int GP_W = 40;
 __device__ __forceinline__ int32_t *gp_row(int64_t r) {
     return g_gprof && r < g_gprof_cap ? g_gprof + ((int64_t)g_gprof_call * g_gprof_cap + r) * GP_W : nullptr;
 }
@@ -2533,9 +2535,9 @@ __global__ __launch_bounds__(64, 2) void k_g_pe(DevGenome G, const uint8_t *__re
             }
         }
         GPROF(if (lane == 0) { int32_t *g = gp_row(2 * pp); if (g) { const uint64_t ce = clock64();
-              g[24] = (int32_t)(gp_c1 - gp_c0); g[25] = (int32_t)(gp_c2 - gp_c1); g[26] = (int32_t)(ce - gp_c2);
-              g[27] = E.misc[5]; g[28] = E.misc[6]; g[29] = gp_na0 << 16 | gp_na1; g[30] = (int32_t)gp_t0;
-              g[31] = (int32_t)gp_rt(); } })
+              g[32] = (int32_t)(gp_c1 - gp_c0); g[33] = (int32_t)(gp_c2 - gp_c1); g[34] = (int32_t)(ce - gp_c2);
+              g[35] = E.misc[5]; g[36] = E.misc[6]; g[37] = gp_na0 << 16 | gp_na1; g[38] = (int32_t)gp_t0;
+              g[39] = (int32_t)gp_rt(); } })
         wave_sync();
     }
 }

@@ -7,14 +7,17 @@ partner stages, all on the device with no host round trip for the data (SURVEY.m
 | AF:182 `\\| samtools sort`, AF:186-194 filters | `af_partition_device` over every record of the set |
 | AF:186-188 `samtools fastq` + `bwa mem -M genome tmp1 tmp2` (S4) | `af_gather_reads_device` (SEQUENCED) + `af_genome_align_pe_device` |
 | fn:705-716 split reads + `bwa mem -M genome` (S5) | `af_gather_reads_device` (SPLIT_SAM) + `af_genome_align_se_device` |
-| fn:718-768 genome check of the split reads, fn:506-528 S6 FASTA | `af_s5_filter_device` (survivors' processed SEQ) |
-| fn:530 `blat -minScore=20 genome split.fa` (S6) | `af_blat_device` (BLAT restatement) on the survivors |
+| fn:506-528 S6 FASTA (of every S5 query that can be kept) | `af_s6_queries_device` right after the gathers |
+| fn:530 `blat -minScore=20 genome split.fa` (S6) | `af_blat_device_begin` on slot 1 beside S4 / S5, `_end` after the check |
+| fn:718-768 genome check of the split reads | `af_s6_check_device` (live flags), `af_s6_compact_device` (survivors' rows) |
 
 `run()` enqueues one pass; S3 synchronises twice (its select count sizes the sort; the partition
 counts size the gathers) and the gathers once (the split-read count sizes S5).  Everything else
 stays on the device: the records, the row lists, the queries, the genome calls' SAM records
-(af_grec), the S6 queries and their PSL rows, which `exchange()` all-gathers between ranks (one
-process per GPU, RCCL).  S6 follows S5 (its queries are S5's survivors); S4's records are made beside S6.
+(af_grec), the S6 queries and their PSL rows (dist_discover exchanges them between ranks over
+RCCL, one process per GPU).  S6 runs beside S5: its queries depend only on the S2 records, so every
+S5 query that can be kept is searched while S4 / S5 align, and S5's check then keeps the
+survivors' rows (the heavy BLAT strands wait for the check: survivors only).
 Per-call caps (query buffers, the genome calls' per-read caps) are counted in `summary()`.
 """
 import os
@@ -281,13 +284,17 @@ class CandidateDiscovery:
         # record); the genome check only decides which are kept.  So the rows of every query that
         # can be kept are written now and searched (fn:530) on slot 1's stream beside S4 / S5, and
         # compacted to the survivors once the check has run.
+        pre_done = None
         if _S6_EARLY:
             self._s6_pre(b, n5, s0)
-            s6.wait_stream(s0)
-            self._s6_search(s6)
+            pre_done = torch.cuda.Event()
+            pre_done.record(s0)
         # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188: bwa's chunks over this input) and S5 (`bwa mem
         # -M genome split_reads.fa`, fn:716); S5's records on s0, S4's on slot 2's stream (idle
-        # once S2 is done)
+        # once S2 is done).  They are enqueued before S6's BLAT, so that their seed kernels (G1,
+        # one lane per read, 3 waves per SIMD) are dispatched onto the chip first: k_blat's
+        # persistent grid fills every wave slot it finds, and launched first it kept S5's G1 from
+        # becoming resident until it drained (47 ms of G1 instead of ~21)
         spe = self.grp.streams[2] if G > 2 else s0
         spe.wait_stream(s0)
         if _S4_SPLIT and spe is not s0:
@@ -305,6 +312,9 @@ class CandidateDiscovery:
             self.ref.align_pe_se_device(self.q, npair, n5, self.L, self.q_lens, recs, self.q_nh,
                                         params=self.p_genome, pe_s4=pe, pe_s5=pe, se_id_base=0, stream=s0,
                                         stream_pe=spe)
+        if _S6_EARLY:
+            s6.wait_event(pre_done)
+            self._s6_search(s6)
         # S5's genome check (fn:718-768), then the rest of S6 (the survivors' heavy strands) and the
         # survivors' rows
         if _S6_EARLY:

@@ -36,11 +36,12 @@ pre_src = d.s6p["src"][:nt].cpu().numpy()
 kept = np.isin(pre_src, d.s6["src"][:n6].cpu().numpy())
 P = np.zeros((nt, 16), dtype=np.int32)
 assert L.af_debug_blat_prof_read(P.ctypes.data_as(__import__("ctypes").c_void_p), nt) == 0
-names = ["hits", "sort", "clumps", "align", "chain"]
+names = ["hits", "sort", "clumps", "hsp", "chain"]
 tot = P[:, 9].astype(np.int64)
 res = dict(queries=nt, mean_cycles={n: float(P[:, k].mean()) for k, n in enumerate(names)},
            mean_total=float(tot.mean()), mean_filter_cycles=float(P[:, 10].mean()), mean_kept=float(P[:, 11].mean()), pct_total={p: float(np.percentile(tot, p)) for p in (50, 90, 99, 99.9)},
            mean_hits=float(P[:, 5].mean()), mean_clumps=float(P[:, 6].mean()), mean_parts=float(P[:, 7].mean()),
+           mean_ranges=float(P[:, 13].mean()), mean_deferred=float(P[:, 12].mean()),
            mean_len=float(P[:, 8].mean()),
            kept=int(kept.sum()), dropped=int((~kept).sum()),
            cycles_kept=int(tot[kept].sum()), cycles_dropped=int(tot[~kept].sum()),

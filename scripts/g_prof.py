@@ -75,14 +75,14 @@ for c in range(min(ncalls, 4)):
         print(f"   {g1[i]:>11d} {((r[18] - r[17]) & 0xFFFFFFFF) / 100:8.1f} | {r[19]} {r[21]} {r[22]} | {r[2]} {r[1]}")
     cyc_per_ext = g1 / np.maximum(ext, 1)
     print(f"  G1 cycles per extension p50 {pct(cyc_per_ext, 50):.0f} p90 {pct(cyc_per_ext, 90):.0f}")
-    if True:  # [23, 27) hold G1's trip split (k_g_pe overwrites them on S4 pairs' first reads)
+    if True:  # [23, 27) hold G1's trip split
         loop, extc, trips, iters = (B[:, 23].astype(np.int64) << 4, B[:, 24].astype(np.int64) << 4, B[:, 25], B[:, 26])
         ok = trips > 0
         print(f"  G1 per trip (wave time, S5 reads): bookkeeping loop {(loop[ok] / trips[ok]).mean():.0f} cycles, "
               f"FM extension {(extc[ok] / trips[ok]).mean():.0f} cycles, rest "
               f"{((g1[ok] - loop[ok] - extc[ok]) / trips[ok]).mean():.0f}; lane's loop iterations per trip "
               f"{(iters[ok] / trips[ok]).mean():.2f}")
-    hw = B[:, 27] < 0  # G1's wave path (k_g_seeds_wave: -(cycles >> 4) - 1); S4 pairs' first reads carry PE data there
+    hw = B[:, 27] < 0  # G1's wave path (k_g_seeds_wave: -(cycles >> 4) - 1)
     if hw.any():
         wc = (-B[hw, 27] - 1) << 4
         print(f"  G1 wave path: {int(hw.sum())} reads seen; cycles/read mean {wc.mean():.0f} p50 {pct(wc, 50):.0f} "
@@ -109,36 +109,44 @@ for c in range(min(ncalls, 4)):
     for k, nm in ((8, "occ"), (10, "chains"), (11, "kept"), (12, "regions")):
         v = B[:, k]
         print(f"  {nm:8s} mean {v.mean():.1f} p90 {pct(v, 90):.0f} p99 {pct(v, 99):.0f} max {v.max()}")
-    # schedule (s_memrealtime, 100 MHz)
-    t0_, t1_ = B[:, 15] & 0xFFFFFFFF, B[:, 16] & 0xFFFFFFFF
-    base = t0_.min()
-    t0_, t1_ = t0_ - base, t1_ - base
-    span = t1_.max()
-    busy = np.bincount(B[:, 14], weights=(t1_ - t0_))
-    print(f"  G2 makespan {span / 100:.0f} us; per-wave busy mean {busy.mean() / 100:.0f} us max {busy.max() / 100:.0f} us "
-          f"over {len(busy)} waves; last read starts at {t0_.max() / 100:.0f} us")
-    tg0, tg1 = B[:, 17] & 0xFFFFFFFF, B[:, 18] & 0xFFFFFFFF
-    b1 = tg0.min()
-    print(f"  G1 makespan {(tg1 - b1).max() / 100:.0f} us; per-read wall p50 {pct(tg1 - tg0, 50) / 100:.1f} us "
-          f"p99 {pct(tg1 - tg0, 99) / 100:.1f} us max {(tg1 - tg0).max() / 100:.1f} us")
-    # k_g_pe (rows of the pairs' first reads): rescue (ksw_align2 + dedup), pairing, records
-    P = B[B[:, 30] != 0]
+    # schedule (s_memrealtime, 100 MHz, the low 32 bits: times as signed offsets from one stamp,
+    # wrap-safe; rows a kernel did not stamp left out)
+    def rel(t0, t1):
+        ok = (t0 != 0) | (t1 != 0)
+        base = int(t0[ok][0]) if ok.any() else 0
+        d0 = ((t0 - base + (1 << 31)) % (1 << 32)) - (1 << 31)
+        d1 = ((t1 - base + (1 << 31)) % (1 << 32)) - (1 << 31)
+        return ok, d0, d1
+    ok2, t0_, t1_ = rel(B[:, 15] & 0xFFFFFFFF, B[:, 16] & 0xFFFFFFFF)
+    if ok2.any():
+        lo = t0_[ok2].min()
+        busy = np.bincount(B[ok2, 14], weights=(t1_[ok2] - t0_[ok2]))
+        print(f"  G2 makespan {(t1_[ok2].max() - lo) / 100:.0f} us; per-wave busy mean {busy[busy > 0].mean() / 100:.0f} us "
+              f"max {busy.max() / 100:.0f} us over {int((busy > 0).sum())} waves; last read starts at "
+              f"{(t0_[ok2].max() - lo) / 100:.0f} us")
+    ok1, tg0, tg1 = rel(B[:, 17] & 0xFFFFFFFF, B[:, 18] & 0xFFFFFFFF)
+    if ok1.any():
+        w1 = tg1[ok1] - tg0[ok1]
+        print(f"  G1 (lane path) makespan {(tg1[ok1].max() - tg0[ok1].min()) / 100:.0f} us over {int(ok1.sum())} reads; "
+              f"per-read wall p50 {pct(w1, 50) / 100:.1f} us p99 {pct(w1, 99) / 100:.1f} us max {w1.max() / 100:.1f} us")
+    # k_g_pe (rows of the pairs' first reads, fields [32, 40)): rescue (ksw_align2 + dedup), pairing, records
+    P = B[(B[:, 38] != 0) | (B[:, 39] != 0)]
     if len(P):
-        resc, pair, rec = P[:, 24], P[:, 25], P[:, 26]
+        resc, pair, rec = P[:, 32], P[:, 33], P[:, 34]
         tot = resc + pair + rec
         print(f"  PE {len(P)} pairs: cycles/pair mean {tot.mean():.0f} p50 {pct(tot, 50):.0f} p99 {pct(tot, 99):.0f} "
-              f"max {tot.max()}; shares rescue {resc.sum() / tot.sum():.3f} (dedup {P[:, 28].sum() / tot.sum():.3f}) "
+              f"max {tot.max()}; shares rescue {resc.sum() / tot.sum():.3f} (dedup {P[:, 36].sum() / tot.sum():.3f}) "
               f"pair {pair.sum() / tot.sum():.3f} records {rec.sum() / tot.sum():.3f}")
-        print(f"  PE ksw_align2 calls/pair mean {P[:, 27].mean():.2f} p99 {pct(P[:, 27], 99):.0f} max {P[:, 27].max()}; "
-              f"pairs with >= 8: {(P[:, 27] >= 8).sum()} holding {resc[P[:, 27] >= 8].sum() / tot.sum():.3f} of the cycles")
+        print(f"  PE ksw_align2 calls/pair mean {P[:, 35].mean():.2f} p99 {pct(P[:, 35], 99):.0f} max {P[:, 35].max()}; "
+              f"pairs with >= 8: {(P[:, 35] >= 8).sum()} holding {resc[P[:, 35] >= 8].sum() / tot.sum():.3f} of the cycles")
         sp = np.argsort(-tot)
         print(f"  PE top-100 pairs hold {tot[sp[:100]].sum() / tot.sum():.3f}; top-1000 {tot[sp[:1000]].sum() / tot.sum():.3f}")
         print("  PE heaviest: cyc rescue dedup pair records | ksw na0 na1")
         for i in sp[:12]:
             r = P[i]
-            print(f"   {tot[i]:>11d} {r[24]:>10d} {r[28]:>10d} {r[25]:>9d} {r[26]:>9d} | {r[27]} {r[29] >> 16} {r[29] & 0xFFFF}")
-        t0_, t1_ = P[:, 30] & 0xFFFFFFFF, P[:, 31] & 0xFFFFFFFF
-        base = t0_.min()
-        print(f"  PE makespan {(t1_ - base).max() / 100:.0f} us; last pair starts at {(t0_ - base).max() / 100:.0f} us; "
-              f"per-pair wall p50 {pct(t1_ - t0_, 50) / 100:.1f} us max {(t1_ - t0_).max() / 100:.1f} us")
+            print(f"   {tot[i]:>11d} {r[32]:>10d} {r[36]:>10d} {r[33]:>9d} {r[34]:>9d} | {r[35]} {r[37] >> 16} {r[37] & 0xFFFF}")
+        okp, t0_, t1_ = rel(P[:, 38] & 0xFFFFFFFF, P[:, 39] & 0xFFFFFFFF)
+        lo = t0_[okp].min()
+        print(f"  PE makespan {(t1_[okp].max() - lo) / 100:.0f} us; last pair starts at {(t0_[okp].max() - lo) / 100:.0f} us; "
+              f"per-pair wall p50 {pct(t1_[okp] - t0_[okp], 50) / 100:.1f} us max {(t1_[okp] - t0_[okp]).max() / 100:.1f} us")
 disc.close()
