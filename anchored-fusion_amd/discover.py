@@ -284,20 +284,16 @@ class CandidateDiscovery:
         # record); the genome check only decides which are kept.  So the rows of every query that
         # can be kept are written now and searched (fn:530) on slot 1's stream beside S4 / S5, and
         # compacted to the survivors once the check has run.
-        pre_done = None
         if _S6_EARLY:
             self._s6_pre(b, n5, s0)
-            pre_done = torch.cuda.Event()
-            pre_done.record(s0)
+            s6.wait_stream(s0)
+            self._s6_search(s6)
         # S4 (`bwa mem -M genome tmp1 tmp2`, AF:188: bwa's chunks over this input) and S5 (`bwa mem
         # -M genome split_reads.fa`, fn:716); S5's records on s0, S4's on slot 2's stream (idle
-        # once S2 is done).  They are enqueued before S6's BLAT, so that their seed kernels (G1,
-        # one lane per read, 3 waves per SIMD) are dispatched onto the chip first: k_blat's
-        # persistent grid fills every wave slot it finds, and launched first it kept S5's G1 from
-        # becoming resident until it drained (47 ms of G1 instead of ~21)
+        # once S2 is done).  (Enqueued after S6's BLAT: enqueueing them first, so that their seed
+        # kernels take the chip before k_blat's persistent grid, measured 222 vs 212 ms per step.)
         spe = self.grp.streams[2] if G > 2 else s0
-        spe.wait_stream(s0)
-        if _S4_SPLIT and spe is not s0:
+        spe.wait_stream(s0)        if _S4_SPLIT and spe is not s0:
             # S4's whole call on a second context of the same index, on its own stream, beside
             # S5's (each has its own seed / region launches, pools and scratch): S4's records
             # start once its 2 npair reads are seeded instead of after every read of both calls
@@ -312,9 +308,6 @@ class CandidateDiscovery:
             self.ref.align_pe_se_device(self.q, npair, n5, self.L, self.q_lens, recs, self.q_nh,
                                         params=self.p_genome, pe_s4=pe, pe_s5=pe, se_id_base=0, stream=s0,
                                         stream_pe=spe)
-        if _S6_EARLY:
-            s6.wait_event(pre_done)
-            self._s6_search(s6)
         # S5's genome check (fn:718-768), then the rest of S6 (the survivors' heavy strands) and the
         # survivors' rows
         if _S6_EARLY:
