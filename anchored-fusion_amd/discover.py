@@ -293,7 +293,8 @@ class CandidateDiscovery:
         # once S2 is done).  (Enqueued after S6's BLAT: enqueueing them first, so that their seed
         # kernels take the chip before k_blat's persistent grid, measured 222 vs 212 ms per step.)
         spe = self.grp.streams[2] if G > 2 else s0
-        spe.wait_stream(s0)        if _S4_SPLIT and spe is not s0:
+        spe.wait_stream(s0)
+        if _S4_SPLIT and spe is not s0:
             # S4's whole call on a second context of the same index, on its own stream, beside
             # S5's (each has its own seed / region launches, pools and scratch): S4's records
             # start once its 2 npair reads are seeded instead of after every read of both calls

@@ -14,6 +14,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("AF_GPU_LIB", "libafgpu_gprof.so")
+# one genome call for S4 and S5 (their split into two concurrent calls would share the profile slot)
+os.environ.setdefault("AF_S4_SPLIT", "0")
 import afpkg  # noqa: E402,F401
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -83,6 +85,14 @@ for c in range(min(ncalls, 4)):
               f"{((g1[ok] - loop[ok] - extc[ok]) / trips[ok]).mean():.0f}; lane's loop iterations per trip "
               f"{(iters[ok] / trips[ok]).mean():.2f}")
     hw = B[:, 27] < 0  # G1's wave path (k_g_seeds_wave: -(cycles >> 4) - 1)
+    n4 = 2 * int(disc.counts.get("s4_pairs", 0))  # the call's first 2 npair reads are S4's
+    rid = np.nonzero(live)[0]
+    for nm_, sel in (("S4", rid < n4), ("S5", rid >= n4)):
+        h = hw & sel
+        if h.any():
+            wc_ = (-B[h, 27] - 1) << 4
+            print(f"  G1 wave path, {nm_} reads: {int(h.sum())} of {int(sel.sum())}; cycles/read mean {wc_.mean():.0f} "
+                  f"p99 {pct(wc_, 99):.0f} max {wc_.max()}; summed {wc_.sum() / 2.4e9 * 1e3:.1f} ms of one wave at 2.4 GHz")
     if hw.any():
         wc = (-B[hw, 27] - 1) << 4
         print(f"  G1 wave path: {int(hw.sum())} reads seen; cycles/read mean {wc.mean():.0f} p50 {pct(wc, 50):.0f} "
