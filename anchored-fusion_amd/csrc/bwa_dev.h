@@ -100,8 +100,45 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
 // lane ranks its items against all n (LDS broadcast reads); tmp: n items of scratch.  Returns
 // false, a unchanged, when some pair is equivalent (the caller runs the introsort for bwa's tie
 // order).  Wave-uniform call.
+// Long lists (the region lists of repeat-rich reads and pairs: hundreds of entries) take a bitonic
+// network instead of the n^2 / 64 ranking: the variant whose comparators all put the lesser item at
+// the lower index (each merge opens with i against its mirror i ^ (k - 1), then half-cleaners i ^
+// j), so the missing items past n act as +inf and their comparators are skipped.  The original is
+// kept in tmp; an equivalent adjacent pair after the sort means a tie: a is restored, false.
+constexpr int WAVE_BITONIC_MIN = 96;
+template <class T, class LT>
+__device__ bool wave_bitonic_sort(T *a, int n, LT lt, T *tmp, int lane) {
+    for (int i = lane; i < n; i += 64) tmp[i] = a[i];
+    __threadfence_block();
+    wave_sync();
+    int N = 1;
+    while (N < n) N <<= 1;
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i0 = 0; i0 < N; i0 += 64) {
+                const int i = i0 + lane;
+                const int l = j == (k >> 1) ? (i ^ (k - 1)) : (i ^ j);
+                if (l > i && l < n) {
+                    const T x = a[i], y = a[l];
+                    if (lt(y, x)) { a[i] = y; a[l] = x; }
+                }
+            }
+            __threadfence_block();
+            wave_sync();
+        }
+    }
+    bool tie = false;
+    for (int i = lane; i + 1 < n; i += 64) tie = tie || !lt(a[i], a[i + 1]);
+    if (!__ballot(tie)) return true;
+    for (int i = lane; i < n; i += 64) a[i] = tmp[i];
+    __threadfence_block();
+    wave_sync();
+    return false;
+}
+
 template <class T, class LT>
 __device__ bool wave_rank_sort(T *a, int n, LT lt, T *tmp, int lane) {
+    if (n >= WAVE_BITONIC_MIN) return wave_bitonic_sort(a, n, lt, tmp, lane);
     bool tie = false;
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
