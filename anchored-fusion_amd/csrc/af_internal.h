@@ -11,7 +11,7 @@
 #define AF_SEED_WAVES 16        // waves per seed-filter workgroup (1024 threads)
 #define AF_SEED_GROUPS (AF_SEED_BTILE / 64)  // 64-read ballot groups per tile
 #ifndef AF_G1_WPS
-#define AF_G1_WPS 3             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish
+#define AF_G1_WPS 4             // genome G1 (k_g_seeds) waves per SIMD: one read per lane, refilled as lanes finish (126 VGPRs)
 #endif
 #ifndef AF_G2_FIRST_OCC
 #define AF_G2_FIRST_OCC 128     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)

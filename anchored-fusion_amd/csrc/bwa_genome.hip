@@ -40,7 +40,7 @@ __device__ int64_t g_gprof_cap = 0;
 __device__ int32_t g_gprof_call = 0;
 // [0, 27) G1 (lane path) and G2, [27, 32) G1's wave path, [32, 40) k_g_pe's phases on the pair's
 // first read: disjoint, so a read of both paths (or an S4 pair's first read) keeps every field
-constexpr int GP_W = 40;
+constexpr int GP_W = 44;
 __device__ __forceinline__ int32_t *gp_row(int64_t r) {
     return g_gprof && r < g_gprof_cap ? g_gprof + ((int64_t)g_gprof_call * g_gprof_cap + r) * GP_W : nullptr;
 }
@@ -185,7 +185,9 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     int64_t n = n_ptr ? (int64_t)*n_ptr : cap;
     if (n > cap) n = cap;
     uint4 *const base = scratch + tid * G1_SLOT;
-    uint4 *Lp = base, *Lc = base + G1_LIST;        // bwt_smem1's prev / curr (swapped by pointer)
+    int lsel = 0;  // bwt_smem1's prev / curr: base + lsel G1_LIST / the other (swapped by the bit)
+#define Lp (base + lsel * G1_LIST)
+#define Lc (base + (lsel ^ 1) * G1_LIST)
     uint4 *const Lf = base + 3 * G1_LIST;  // the read's list (base + 2 G1_LIST: k_g_seeds_wave's mems)
     const int msl = p.min_seed_len;
     const int split_len = (int)((float)msl * 1.5f + .499);
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
     };
     auto fwd_end = [&]() {  // curr holds the forward intervals in push order (bwa reverses them)
         ret = (int)g1_unpack(c_last).qe;
-        uint4 *t = Lp; Lp = Lc; Lc = t;
+        lsel ^= 1;
         np = nc; nc = 0; rev = true; i = sx - 1; j = 0;
         pf = c_last; pf_j = 0;  // prev in reverse push order: entry 0 is the last push
         st = G1_BWD;
@@ -255,7 +257,6 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
             }
         }
     };
-    G1Iv pv{};
     for (;;) {
         // idle lanes take the next reads (one atomic per wave)
         const uint64_t im = __ballot(st == G1_IDLE);
@@ -300,13 +301,13 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
             } else if (st == G1_BWD) {  // backward search for MEMs: entry j of prev at position i
                 if (j == np) {
                     if (nc == 0) { smem_end(); continue; }
-                    uint4 *t = Lp; Lp = Lc; Lc = t;
+                    lsel ^= 1;
                     np = nc; nc = 0; rev = false; --i; j = 0;
                     pf = c_first; pf_j = 0;  // prev in push order: entry 0 is the first push
                     continue;
                 }
                 if (pf_j != j) { pf = Lp[rev ? np - 1 - j : j]; pf_j = j; }
-                pv = g1_unpack(pf);
+                const G1Iv pv = g1_unpack(pf);
                 const int c = i < 0 ? -1 : code(i);
                 if (c < 0 || c > 3) {
                     // no entry extends past the read's start or an N: each would become a mem at the
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
             }
             ik_k = rk; ik_l = rl; ik_s = rs; ik_qe = i + 1; ++i;
         } else if (st == G1_BWD) {
-            if (rs < min_intv) mem_push(pv, i + 1);
+            if (rs < min_intv) mem_push(G1Iv{ek, el, es, 0, p_qe}, i + 1);
             else if (nc == 0 || rs != last_s) { push_curr(rk, rl, rs, 0, p_qe); last_s = rs; }
             ++j;
         } else {  // G1_SS
@@ -416,6 +417,9 @@ __global__ __launch_bounds__(64, AF_G1_WPS) void k_g_seeds(DevGenome G, const ui
         }
     }
 }
+
+#undef Lp
+#undef Lc
 
 // G1 for the reads k_g_seeds handed off (more than w.g1_max_ext FM extensions: repeat-rich reads
 // whose backward scans hold many entries per position): one WAVE per read, restarted from the
@@ -709,16 +713,20 @@ __device__ __forceinline__ void g_fetch_clip(const DevGenome &G, int64_t *beg, i
     *end = *end < fe ? *end : fe;
 }
 
-// ---- mem_chain's working set in LDS (the G2 boxes' space, free until chain2aln): the kbtree's
-// first G_KB_LDS nodes and the first G_CH_LDS chains' keys and end seeds; the rest stays in the
-// wave's global scratch.  Lane 0's walk then reads LDS for the common short lists instead of
-// chasing scratch lines through L2.
-constexpr int G_KB_LDS = 64, G_CH_LDS = 240;
-struct GChainHot {             // a chain's pos, contig, seed count and first / last seeds
-    int64_t pos, r_first, r_last;
-    int32_t q_first, len_first, q_last, len_last, rid, n, last;
+// ---- mem_chain's working set in LDS (the G2 boxes' space, free until chain2aln): the first
+// G_POS_LDS chains' keys (the kbtree's comparisons read only these), its first G_KB_LDS nodes and
+// the first G_CH_LDS chains' end seeds (test_and_merge's one read per seed); the rest stays in the
+// wave's global scratch.  Lane 0's walk then reads LDS for the lists of up to ~a thousand chains
+// instead of chasing scratch lines through L2.
+constexpr int G_POS_LDS = 1024, G_KB_LDS = 96, G_CH_LDS = 120;
+struct GChainHot {             // a chain's last seed, contig, seed count and first seed's query span
+    int64_t r_last;
+    int32_t rid, n;
+    int16_t q_first, len_first, q_last, len_last, last, pad;
 };
+static_assert(AF_MAX_READ < 32768 && AF_G_MAX_OCC <= 32768, "16-bit query spans and pool indices");
 struct GChainLds {
+    int64_t pos[G_POS_LDS];
     GChainHot ch[G_CH_LDS];
     GKb node[G_KB_LDS];
     int32_t rid[64];           // the wave's batch of occurrences: each one's contig (g_intv2rid)
@@ -731,9 +739,9 @@ struct GTree {
     GKb *node_l, *node_g;
     int nn, root;
     const GChain *ch;
-    const GChainHot *hot;
+    const int64_t *pos_l;
     __device__ GKb &nd(int i) const { return i < G_KB_LDS ? node_l[i] : node_g[i]; }
-    __device__ int64_t pos(int x) const { return x < G_CH_LDS ? hot[x].pos : ch[x].pos; }
+    __device__ int64_t pos(int x) const { return x < G_POS_LDS ? pos_l[x] : ch[x].pos; }
 };
 __device__ __forceinline__ int gkb_cmp(const GTree &b, int x, int64_t kpos) {
     const int64_t a = b.pos(x);
@@ -806,7 +814,7 @@ __device__ bool gkb_putp(GTree &b, int k) {
         int i = gkb_getp_aux(b, x, kpos, nullptr) + 1;
         if (b.nd(x.ptr[i]).n == G_KB_MAXK) {
             gkb_split(b, xi, i, x.ptr[i]);
-            if (gkb_cmp(b, b.nd(xi).key[i], kpos) > 0) ++i;
+            if (gkb_cmp(b, b.nd(xi).key[i], kpos) < 0) ++i;  // klib: cmp(*k, key[i]) > 0, k past the promoted key
         }
         xi = b.nd(xi).ptr[i];
     }
@@ -833,103 +841,213 @@ __device__ int gkb_traverse(const GTree &b, int32_t *order) {
 }
 
 // test_and_merge (oracle test_and_merge), lane 0: 1 merged / contained, 0 not, -1 overflow
-__device__ int g_test_and_merge(const G2Scr &S, GChainHot *hot, int ci, const GSeed &p, int rid, int64_t l_pac,
-                                int w, int max_chain_gap, int *npool) {
-    GChainHot h;
-    if (ci < G_CH_LDS) h = hot[ci];
-    else {
+// (hot: the first nhot chains' end seeds in LDS; r_first: chain ci's pos, its first seed's rbeg)
+__device__ int g_test_and_merge(const G2Scr &S, GChainHot *hot, int nhot, int ci, int64_t r_first, const GSeed &p,
+                                int rid, int64_t l_pac, int w, int max_chain_gap, int *npool) {
+    int64_t r_last;
+    int q_first, len_first, q_last, len_last, crid, cn, clast;
+    if (ci < nhot) {
+        const GChainHot h = hot[ci];
+        r_last = h.r_last;
+        q_first = h.q_first; len_first = h.len_first; q_last = h.q_last; len_last = h.len_last;
+        crid = h.rid; cn = h.n; clast = h.last;
+    } else {
         const GChain c = S.ch[ci];
-        const int li = S.last_of[ci];
-        const GSeed first = S.pool[c.seed0], last = S.pool[li];
-        h = GChainHot{c.pos, first.rbeg, last.rbeg, first.qbeg, first.len, last.qbeg, last.len, c.rid, c.n, li};
+        clast = S.last_of[ci];
+        const GSeed first = S.pool[c.seed0], last = S.pool[clast];
+        r_last = last.rbeg;
+        q_first = first.qbeg; len_first = first.len; q_last = last.qbeg; len_last = last.len;
+        crid = c.rid; cn = c.n;
     }
-    const int64_t qend = (int64_t)h.q_last + h.len_last, rend = h.r_last + h.len_last;
-    if (rid != h.rid) return 0;
-    if (p.qbeg >= h.q_first && p.qbeg + p.len <= qend && p.rbeg >= h.r_first && p.rbeg + p.len <= rend) return 1;
-    if ((h.r_last < l_pac || h.r_first < l_pac) && p.rbeg >= l_pac) return 0;
-    const int64_t x = p.qbeg - h.q_last, y = p.rbeg - h.r_last;
-    if (y >= 0 && x - y <= w && y - x <= w && x - h.len_last < max_chain_gap && y - h.len_last < max_chain_gap) {
+    (void)len_first;
+    const int64_t qend = (int64_t)q_last + len_last, rend = r_last + len_last;
+    if (rid != crid) return 0;
+    if (p.qbeg >= q_first && p.qbeg + p.len <= qend && p.rbeg >= r_first && p.rbeg + p.len <= rend) return 1;
+    if ((r_last < l_pac || r_first < l_pac) && p.rbeg >= l_pac) return 0;
+    const int64_t x = p.qbeg - q_last, y = p.rbeg - r_last;
+    if (y >= 0 && x - y <= w && y - x <= w && x - len_last < max_chain_gap && y - len_last < max_chain_gap) {
         if (*npool >= AF_G_MAX_OCC) return -1;
         const int k = (*npool)++;
         S.pool[k] = p;
         S.next[k] = -1;
-        S.next[h.last] = k;
+        S.next[clast] = k;
         S.last_of[ci] = k;
-        S.ch[ci].n = h.n + 1;
-        if (ci < G_CH_LDS) {
+        S.ch[ci].n = cn + 1;
+        if (ci < nhot) {
             GChainHot &g = hot[ci];
-            g.r_last = p.rbeg; g.q_last = p.qbeg; g.len_last = p.len; g.n = h.n + 1; g.last = k;
+            g.r_last = p.rbeg; g.q_last = (int16_t)p.qbeg; g.len_last = (int16_t)p.len; g.n = cn + 1; g.last = (int16_t)k;
         }
         return 1;
     }
     return 0;
 }
 
+// ---- mem_chain's chains as a sorted array in LDS (the same space): while no two chains share a
+// pos and there are at most G_ARR of them, the kbtree holds distinct keys, so its lookups (the
+// largest key <= the seed's rbeg) and its in-order traversal are those of a sorted array -- the
+// wave searches it (two ballots) and shifts it open for an insertion, instead of lane 0 walking
+// tree nodes.  A second chain at an existing pos (whose place among the equal keys depends on the
+// tree's shape) or chain G_ARR + 1 restarts the read on the kbtree.
+constexpr int G_ARR = 1024, G_CH_ARR = 180;
+// the array mode's chain limit (tests: env AF_G_CHAIN_ARR -- 0 every read on the kbtree, a small
+// count most reads restarted there)
+__device__ int g_chain_arr = G_ARR;
+struct GChainArr {
+    int64_t key[G_ARR];
+    int16_t id[G_ARR];
+    GChainHot ch[G_CH_ARR];
+    int32_t rid[64];
+};
+static_assert(sizeof(GChainArr) <= sizeof(G2Box) * G2_BOXES, "the array mode's LDS set fits the boxes");
+static_assert(G_ARR <= 64 * 16, "g_arr_rank covers 64 strides of 16 keys");
+// the number of keys <= kpos among key[0, n) (ascending, n <= 1024): a ballot over the 64
+// strides of 16, then one over the stride
+__device__ __forceinline__ int g_arr_rank(const int64_t *key, int n, int64_t kpos, int lane) {
+    const int i1 = lane << 4;
+    const uint64_t m1 = __ballot(i1 < n && key[i1] <= kpos);
+    if (!m1) return 0;
+    const int b = __builtin_popcountll(m1) - 1;
+    const int i2 = (b << 4) + (lane & 15);
+    const uint64_t m2 = __ballot(lane < 16 && i2 < n && key[i2] <= kpos);
+    return (b << 4) + __builtin_popcountll(m2);
+}
+
 // mem_chain over the read's intervals (oracle mem_chain): returns the chain count (tree order,
-// seeds compacted in S.seed), -1 on overflow.  The wave gathers 64 SA rows at a time; lane 0
-// walks them in order.
+// seeds compacted in S.seed), -1 on overflow.  The wave gathers 64 SA rows at a time; the array
+// mode takes each seed on the whole wave, the kbtree mode on lane 0.
 __device__ int g_mem_chain(const DevGenome &G, const G2Scr &S, const GIv *iv, int niv, const af_params &p,
                            const GOpt &o, int lane) {
     G2Lds &E = g_g2;
     GChainLds &C = *reinterpret_cast<GChainLds *>(g_box);
+    GChainArr &A = *reinterpret_cast<GChainArr *>(g_box);
     int nch = 0, npool = 0;
     bool ovf = false;
-    GTree tree{C.node, S.kb, 0, 0, S.ch, C.ch};
-    if (lane == 0) tree.root = gkb_new(tree, 0);
-    for (int i = 0; i < niv && !ovf; ++i) {
-        const GIv v = iv[i];
-        const int slen = v.qe - v.qb;
-        const int64_t step = v.s > p.max_occ ? v.s / p.max_occ : 1;
-        const int64_t cnt = v.s > p.max_occ ? (int64_t)p.max_occ : v.s;  // k < s && count < max_occ
-        for (int64_t c0 = 0; c0 < cnt && !ovf; c0 += 64) {
-            const int64_t c = c0 + lane;
-            const int nb = (int)min((int64_t)64, cnt - c0);
-            wave_sync();
-            if (c < cnt) {
-                const int64_t rb = G.sa[v.sa_k + c * step];
-                E.occ[lane] = rb;
-                C.rid[lane] = g_intv2rid(G, rb, rb + slen);
-            }
-            wave_sync();
-            if (lane == 0) {
-                for (int u = 0; u < nb && !ovf; ++u) {
-                    GSeed s;
-                    s.rbeg = E.occ[u];
-                    s.qbeg = v.qb;
-                    s.len = slen;
-                    const int rid = C.rid[u];
-                    if (rid < 0) continue;
-                    bool to_add = false;
-                    if (nch) {
-                        const int lower = gkb_lower(tree, s.rbeg);
-                        if (lower < 0) to_add = true;
-                        else {
-                            const int r = g_test_and_merge(S, C.ch, lower, s, rid, G.l_pac, p.w, o.max_chain_gap, &npool);
-                            if (r < 0) ovf = true;
-                            else if (!r) to_add = true;
-                        }
-                    } else to_add = true;
-                    if (to_add && !ovf) {
-                        if (nch >= AF_G_MAX_CHAIN || npool >= AF_G_MAX_OCC) { ovf = true; break; }
-                        const int kk = npool++;
-                        S.pool[kk] = s;
-                        S.next[kk] = -1;
-                        S.ch[nch] = GChain{s.rbeg, 1, -1, rid, 0, 0, kk};
-                        S.last_of[nch] = kk;
-                        if (nch < G_CH_LDS) C.ch[nch] = GChainHot{s.rbeg, s.rbeg, s.rbeg, s.qbeg, s.len, s.qbeg, s.len, rid, 1, kk};
-                        if (!gkb_putp(tree, nch)) { ovf = true; break; }
-                        ++nch;
-                    }
+    GTree tree{C.node, S.kb, 0, 0, S.ch, C.pos};
+    bool by_arr = true;
+    for (int arr = 1; arr >= 0; --arr) {
+        by_arr = arr;
+        nch = 0; npool = 0; ovf = false;
+        bool restart = false;
+        tree.nn = 0; tree.root = 0;
+        if (!arr && lane == 0) tree.root = gkb_new(tree, 0);
+        int32_t *const ridv = arr ? A.rid : C.rid;
+        for (int i = 0; i < niv && !ovf && !restart; ++i) {
+            const GIv v = iv[i];
+            const int slen = v.qe - v.qb;
+            const int64_t step = v.s > p.max_occ ? v.s / p.max_occ : 1;
+            const int64_t cnt = v.s > p.max_occ ? (int64_t)p.max_occ : v.s;  // k < s && count < max_occ
+            for (int64_t c0 = 0; c0 < cnt && !ovf && !restart; c0 += 64) {
+                const int64_t c = c0 + lane;
+                const int nb = (int)min((int64_t)64, cnt - c0);
+                wave_sync();
+                if (c < cnt) {
+                    const int64_t rb = G.sa[v.sa_k + c * step];
+                    E.occ[lane] = rb;
+                    ridv[lane] = g_intv2rid(G, rb, rb + slen);
                 }
-                E.misc[0] = ovf;
+                wave_sync();
+                if (arr) {
+                    for (int u = 0; u < nb; ++u) {
+                        GSeed s;
+                        s.rbeg = E.occ[u];
+                        s.qbeg = v.qb;
+                        s.len = slen;
+                        const int rid = A.rid[u];
+                        if (rid < 0) continue;
+                        const int at = g_arr_rank(A.key, nch, s.rbeg, lane);  // lower: entry at - 1
+                        int r = 0;
+                        if (at > 0) {
+                            const int64_t kl = A.key[at - 1];
+                            if (lane == 0)
+                                r = g_test_and_merge(S, A.ch, G_CH_ARR, A.id[at - 1], kl, s, rid, G.l_pac, p.w,
+                                                     o.max_chain_gap, &npool);
+                            r = __builtin_amdgcn_readfirstlane(r);
+                            npool = __builtin_amdgcn_readfirstlane(npool);
+                            if (r < 0) { ovf = true; break; }
+                            if (r == 0 && kl == s.rbeg) { restart = true; break; }  // a second chain at this pos
+                        }
+                        if (r) continue;
+                        if (nch >= g_chain_arr) { restart = true; break; }
+                        if (nch >= AF_G_MAX_CHAIN || npool >= AF_G_MAX_OCC) { ovf = true; break; }
+                        // open entry `at`: move [at, nch) up by one, the top 64 first
+                        for (int top = nch - 1; top >= at; top -= 64) {
+                            const int e = top - lane;
+                            int64_t kv = 0;
+                            int16_t iv_ = 0;
+                            if (e >= at) { kv = A.key[e]; iv_ = A.id[e]; }
+                            wave_sync();
+                            if (e >= at) { A.key[e + 1] = kv; A.id[e + 1] = iv_; }
+                            wave_sync();
+                        }
+                        if (lane == 0) {
+                            const int kk = npool;
+                            S.pool[kk] = s;
+                            S.next[kk] = -1;
+                            S.ch[nch] = GChain{s.rbeg, 1, -1, rid, 0, 0, kk};
+                            S.last_of[nch] = kk;
+                            if (nch < G_CH_ARR)
+                                A.ch[nch] = GChainHot{s.rbeg, rid, 1, (int16_t)s.qbeg, (int16_t)s.len, (int16_t)s.qbeg,
+                                                      (int16_t)s.len, (int16_t)kk, 0};
+                            A.key[at] = s.rbeg;
+                            A.id[at] = (int16_t)nch;
+                        }
+                        ++npool;
+                        ++nch;
+                        wave_sync();
+                    }
+                } else if (lane == 0) {
+                    for (int u = 0; u < nb && !ovf; ++u) {
+                        GSeed s;
+                        s.rbeg = E.occ[u];
+                        s.qbeg = v.qb;
+                        s.len = slen;
+                        const int rid = C.rid[u];
+                        if (rid < 0) continue;
+                        bool to_add = false;
+                        if (nch) {
+                            const int lower = gkb_lower(tree, s.rbeg);
+                            if (lower < 0) to_add = true;
+                            else {
+                                const int r = g_test_and_merge(S, C.ch, G_CH_LDS, lower, tree.pos(lower), s, rid, G.l_pac,
+                                                               p.w, o.max_chain_gap, &npool);
+                                if (r < 0) ovf = true;
+                                else if (!r) to_add = true;
+                            }
+                        } else to_add = true;
+                        if (to_add && !ovf) {
+                            if (nch >= AF_G_MAX_CHAIN || npool >= AF_G_MAX_OCC) { ovf = true; break; }
+                            const int kk = npool++;
+                            S.pool[kk] = s;
+                            S.next[kk] = -1;
+                            S.ch[nch] = GChain{s.rbeg, 1, -1, rid, 0, 0, kk};
+                            S.last_of[nch] = kk;
+                            if (nch < G_POS_LDS) C.pos[nch] = s.rbeg;
+                            if (nch < G_CH_LDS)
+                                C.ch[nch] = GChainHot{s.rbeg, rid, 1, (int16_t)s.qbeg, (int16_t)s.len, (int16_t)s.qbeg,
+                                                      (int16_t)s.len, (int16_t)kk, 0};
+                            if (!gkb_putp(tree, nch)) { ovf = true; break; }
+                            ++nch;
+                        }
+                    }
+                    E.misc[0] = ovf;
+                }
+                wave_sync();
+                if (!arr) ovf = E.misc[0] != 0;
             }
-            wave_sync();
-            ovf = E.misc[0] != 0;
         }
+        if (!restart) break;
     }
     int no = 0;
+    if (!ovf) {
+        // the chains in key order: the array's ids, or the tree's in-order traversal
+        if (by_arr) {
+            for (int a = lane; a < nch; a += 64) S.order[a] = A.id[a];
+            no = nch;
+            __threadfence_block();
+            wave_sync();
+        } else if (lane == 0) no = gkb_traverse(tree, S.order);
+    }
     if (lane == 0 && !ovf) {
-        no = gkb_traverse(tree, S.order);
         int ns = 0;
         for (int a = 0; a < no; ++a) {
             GChain c = S.ch[S.order[a]];
@@ -1006,16 +1124,31 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     }
     __threadfence_block();
     wave_sync();
-    int32_t *cb = S.last_of, *ce = S.order, *cw = S.next;  // free after mem_chain
+    // the overlap scan: the kept chains in kept order, each packed in one word (query begin / end
+    // and weight, 9 bits each, and bit 31 once its `first` is set) with its `first` beside it, so a
+    // lane tests one kept chain per LDS read; LDS (the boxes, free again after the sort) when the
+    // lists fit, else the scratch free after mem_chain
+    static_assert(AF_MAX_READ < 512 && AF_G_MAX_CHAIN < 32768, "9-bit spans and weights, 16-bit chain indices");
+    constexpr int NL = (int)(sizeof(G2Box) * G2_BOXES / (3 * sizeof(int16_t) + sizeof(uint32_t) + sizeof(int16_t)));
+    const bool lds = n_chn <= NL;
+    uint8_t *const lb = reinterpret_cast<uint8_t *>(g_box);
+    uint32_t *kp = lds ? reinterpret_cast<uint32_t *>(lb) : reinterpret_cast<uint32_t *>(S.last_of);
+    int16_t *kf = lds ? reinterpret_cast<int16_t *>(lb + 4 * NL) : reinterpret_cast<int16_t *>(S.order);
+    static_assert(AF_G_MAX_OCC >= AF_G_MAX_CHAIN, "S.next holds two 16-bit lists of the chains");
+    int16_t *cb = lds ? reinterpret_cast<int16_t *>(lb + 6 * NL) : reinterpret_cast<int16_t *>(S.next);
+    int16_t *ce = lds ? cb + NL : cb + AF_G_MAX_CHAIN;
+    int16_t *cw = lds ? ce + NL : reinterpret_cast<int16_t *>(S.kept);
     for (int i = lane; i < n_chn; i += 64) {
         const GChain c = a[i];
         const GSeed t = S.seed[c.seed0 + c.n - 1];
-        cb[i] = S.seed[c.seed0].qbeg;
-        ce[i] = t.qbeg + t.len;
-        cw[i] = c.w;
+        cb[i] = (int16_t)S.seed[c.seed0].qbeg;
+        ce[i] = (int16_t)(t.qbeg + t.len);
+        cw[i] = (int16_t)(c.w < 511 ? c.w : 511);
     }
-    int32_t *chains = S.kept;
-    if (lane == 0) { a[0].kept = 3; chains[0] = 0; }
+    __threadfence_block();
+    wave_sync();
+    auto pack = [&](int i) -> uint32_t { return (uint32_t)cb[i] | (uint32_t)ce[i] << 9 | (uint32_t)cw[i] << 18; };
+    if (lane == 0) { a[0].kept = 3; kp[0] = pack(0); kf[0] = -1; }
     wave_sync();
     int nc = 1;
     for (int i = 1; i < n_chn; ++i) {
@@ -1024,16 +1157,16 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
         for (int k0 = 0; k0 < nc && !brk; k0 += 64) {
             const int k = k0 + lane;
             bool ov = false, bk = false;
-            int j = 0;
+            uint32_t x = 0;
             if (k < nc) {
-                j = chains[k];
-                const int bj = cb[j], ej = ce[j];
+                x = kp[k];
+                const int bj = (int)(x & 511), ej = (int)(x >> 9 & 511);
                 const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
                 if (e_min > b_max) {
                     const int lj = ej - bj, min_l = li < lj ? li : lj;
                     if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
                         ov = true;
-                        const int wj = cw[j];
+                        const int wj = (int)(x >> 18 & 511);
                         bk = (float)wi < (float)wj * 0.5f && wj - wi >= p.min_seed_len << 1;
                     }
                 }
@@ -1046,19 +1179,20 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
                 brk = true;
             }
             if (om) large_ovlp = true;
-            if ((om >> lane) & 1ull)
-                if (a[j].first < 0) a[j].first = i;
+            if (((om >> lane) & 1ull) && !(x >> 31)) { kp[k] = x | 1u << 31; kf[k] = (int16_t)i; }
         }
         if (!brk) {
-            if (lane == 0) { chains[nc] = i; a[i].kept = large_ovlp ? 2 : 3; }
+            if (lane == 0) { kp[nc] = pack(i); kf[nc] = -1; a[i].kept = large_ovlp ? 2 : 3; }
             ++nc;
         }
+        __threadfence_block();
         wave_sync();
     }
     for (int k = lane; k < nc; k += 64) {
-        const int f = a[chains[k]].first;
+        const int f = kf[k];
         if (f >= 0) a[f].kept = 1;
     }
+    __threadfence_block();
     wave_sync();
     int m = 0;
     for (int i0 = 0; i0 < n_chn; i0 += 64) {
@@ -1727,7 +1861,7 @@ __global__ __launch_bounds__(64, 2) void k_g_heavy(DevGenome G, const uint8_t *_
         if (hr >= n_heavy) break;
         const int64_t r = h.read[hr];
         if (r < 0) continue;
-        GPROF(const uint64_t gp_c0 = clock64();)
+        GPROF(const uint64_t gp_c0 = clock64(); const uint32_t gp_t0 = gp_rt();)
         const int nch = h.nch[hr], co = h.ch_off[hr], so = h.sd_off[hr];
         int nsd = 0;
         for (int i = lane; i < nch; i += 64) {
@@ -1747,7 +1881,8 @@ __global__ __launch_bounds__(64, 2) void k_g_heavy(DevGenome G, const uint8_t *_
         GPROF(const uint64_t gp_c1 = clock64();)
         if (!ovf) nreg = g_dedup_patch<CPL>(G, p, o, S.reg, nreg, true, zg, lane, reinterpret_cast<GReg *>(S.seed));
         GPROF(if (lane == 0) { int32_t *g = gp_row(r); if (g) { g[6] = (int32_t)(gp_c1 - gp_c0);
-              g[7] = (int32_t)(clock64() - gp_c1); g[12] = nreg; g[13] = nreg; } })
+              g[7] = (int32_t)(clock64() - gp_c1); g[12] = nreg; g[13] = nreg;
+              g[40] = (int32_t)gp_t0; g[41] = (int32_t)gp_rt(); g[42] = (int32_t)blockIdx.x; } })
         g_put_regions(w, S, r, nreg, ovf, lane);
     }
 }
@@ -2663,6 +2798,15 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
                                     uint8_t *g1_scratch, int n_g1_threads, uint8_t *g2_scratch, int n_g2_waves,
                                     uint8_t *zscratch, hipStream_t s) {
     GPROF(gprof_next(s);)
+    {
+        static int chain_arr = G_ARR;  // the value the symbol holds (read by the kernel at its launch)
+        const char *e = getenv("AF_G_CHAIN_ARR");
+        const int want = e ? std::max(0, std::min(G_ARR, atoi(e))) : G_ARR;
+        if (want != chain_arr) {
+            chain_arr = want;
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chain_arr), &chain_arr, sizeof(int));
+        }
+    }
     hipLaunchKernelGGL(k_g_zero, dim3(1), dim3(64), 0, s, w, cap, w.heads);
     // one lane per read, at most the scratch's lanes (idle lanes refill from w.g1_next)
     const int64_t g1_waves = std::max<int64_t>(1, std::min<int64_t>(n_g1_threads / 64, (cap + 63) / 64));

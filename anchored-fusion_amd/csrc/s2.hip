@@ -480,7 +480,7 @@ __device__ void kb_putp(int k) {
         int i = kb_getp_aux(x, kpos, nullptr) + 1;
         if (S.x.kb[x.ptr[i]].n == KB_MAXK) {
             kb_split(xi, i, x.ptr[i]);
-            if (kb_cmp(S.x.kb[xi].key[i], kpos) > 0) ++i;
+            if (kb_cmp(S.x.kb[xi].key[i], kpos) < 0) ++i;  // klib: cmp(*k, key[i]) > 0, k past the promoted key
         }
         xi = S.x.kb[xi].ptr[i];
     }

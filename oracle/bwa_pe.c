@@ -1015,7 +1015,7 @@ static void kb_putp_aux(kbtree_t *b, int xi, int k) {
         if (b->node[x->ptr[i]].n == KB_MAXK) {
             kb_split(b, xi, i, x->ptr[i]);
             x = &b->node[xi];
-            if (kb_cmp(b, x->key[i], kpos) > 0) ++i;  /* b->cmp(*k, key[i]) > 0 */
+            if (kb_cmp(b, x->key[i], kpos) < 0) ++i;  /* b->cmp(*k, key[i]) > 0: k past the promoted key */
         }
         kb_putp_aux(b, x->ptr[i], k);
     }

@@ -139,6 +139,17 @@ for c in range(min(ncalls, 4)):
         w1 = tg1[ok1] - tg0[ok1]
         print(f"  G1 (lane path) makespan {(tg1[ok1].max() - tg0[ok1].min()) / 100:.0f} us over {int(ok1.sum())} reads; "
               f"per-read wall p50 {pct(w1, 50) / 100:.1f} us p99 {pct(w1, 99) / 100:.1f} us max {w1.max() / 100:.1f} us")
+    # k_g_heavy (fields [40, 43): its start / end stamps and wave): the reads G2 deferred
+    H = B[(B[:, 40] != 0) | (B[:, 41] != 0)]
+    if len(H):
+        hc = (H[:, 6] & 0xFFFFFFFF) + (H[:, 7] & 0xFFFFFFFF)
+        okh, t0_, t1_ = rel(H[:, 40] & 0xFFFFFFFF, H[:, 41] & 0xFFFFFFFF)
+        lo = t0_[okh].min()
+        busy = np.bincount(H[okh, 42], weights=(t1_[okh] - t0_[okh]))
+        print(f"  heavy reads (k_g_heavy) {len(H)}: cycles/read mean {hc.mean():.0f} p99 {pct(hc, 99):.0f} max {hc.max()}; "
+              f"summed {hc.sum() / 2.4e9 * 1e3:.1f} ms of one wave at 2.4 GHz; makespan {(t1_[okh].max() - lo) / 100:.0f} us "
+              f"over {int((busy > 0).sum())} waves (busy mean {busy[busy > 0].mean() / 100:.0f} us max {busy.max() / 100:.0f} us); "
+              f"last read starts at {(t0_[okh].max() - lo) / 100:.0f} us; per-read wall max {(t1_[okh] - t0_[okh]).max() / 100:.0f} us")
     # k_g_pe (rows of the pairs' first reads, fields [32, 40)): rescue (ksw_align2 + dedup), pairing, records
     P = B[(B[:, 38] != 0) | (B[:, 39] != 0)]
     if len(P):

@@ -86,6 +86,32 @@ def test_se_regions_equal_oracle(world):
             assert tuple(int(v) for v in want) == tuple(int(v) for v in g[:10]), (r, k)
 
 
+@pytest.mark.parametrize("arr", ["0", "3"])
+def test_chain_modes_equal_oracle(world, monkeypatch, arr):
+    """mem_chain's two modes (bwa_genome.hip g_mem_chain): the sorted chain array in LDS (default)
+    and the kbtree, which a read restarts on at a second chain with an existing pos or past the
+    array's limit -- forced here for every read (AF_G_CHAIN_ARR=0) or past 3 chains (most
+    multi-chain reads restart).  Regions and records equal the oracle's either way."""
+    monkeypatch.setenv("AF_G_CHAIN_ARR", arr)
+    contigs, og, gg = world
+    reads, lens = sample_reads(contigs, 400, seed=31, chimeric=0.4)
+    ro, no = og.regions(reads, lens, max_reg=64, threads=8)
+    rg, ng = gg.regions(reads, lens, max_reg=64)
+    assert np.array_equal(no, ng), np.nonzero(no != ng)[0][:10]
+    for r in range(len(no)):
+        for k in range(min(no[r], 64)):
+            o = ro[r, k]
+            want = (o["rb"], o["re"], o["qb"], o["qe"], o["rid"], o["score"], o["truesc"], o["w"], o["seedcov"],
+                    o["seedlen0"])
+            assert tuple(int(v) for v in want) == tuple(int(v) for v in rg[r, k][:10]), (r, k)
+    so, sn = og.align_se(reads, lens, id_base=7, threads=8)
+    sg, sgn = gg.align_se(reads, lens, id_base=7)
+    assert np.array_equal(sn, sgn)
+    for r in range(len(sn)):
+        msg = _rec_equal(so[r], sg[r], min(sn[r], 8))
+        assert msg is None, (r, msg)
+
+
 def test_se_records_equal_oracle(world):
     contigs, og, gg = world
     reads, lens = sample_reads(contigs, 600, seed=22, chimeric=0.4)
