@@ -88,6 +88,7 @@ struct af_ctx {
     GPeSpec s2_sp{};
     int32_t s2_sp_min = AF_S2_SPEC_WINDOWS;
     int32_t g1_max_ext = AF_G1_HEAVY_EXT;
+    bool g1_ext_env = false;        // AF_G1_HEAVY_EXT given: the hand-off threshold is fixed
     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
     int32_t g2_first_occ = AF_G2_FIRST_OCC;
     int32_t *g2_list = nullptr;
@@ -520,7 +521,12 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
     return AF_OK;
 }
 
-GWork genome_work(af_ctx *c) {
+// n_reads: the call's reads.  G1's hand-off threshold follows the load: a lane-path read's time is
+// its chain of extensions, each a trip of the whole wave, while the wave path's reads share the
+// CUs -- with few reads per CU (a rank's share at N = 8: ~70 S5 reads per CU) the CUs are idle
+// and long reads finish sooner on waves (512: 39.7 vs 42.1 ms per rank step), with hundreds per
+// CU (one GPU's 50 M pairs: ~580) the waves' work would queue (1,024: 238 vs 203 ms)
+GWork genome_work(af_ctx *c, int64_t n_reads) {
     GWork w;
     w.iv = c->g_iv; w.iv_cap = c->g_iv_cap; w.iv_fill = c->g_iv_fill; w.iv_off = c->g_iv_off; w.iv_n = c->g_iv_n;
     w.reg = c->g_reg; w.reg_cap = c->g_reg_cap; w.reg_fill = c->g_reg_fill; w.reg_off = c->g_reg_off;
@@ -528,7 +534,12 @@ GWork genome_work(af_ctx *c) {
     w.heads = c->ctrl + AF_CTRL_G_HEADS;
     w.g1_next = c->g_iv_fill + 1;
     w.g1_hv = c->g1_hv; w.g1_hv_n = c->g_iv_fill + 2; w.g1_hv_next = c->g_iv_fill + 3;
-    w.g1_max_ext = c->g1_hv ? c->g1_max_ext : 0;
+    int32_t mx = c->g1_max_ext;
+    if (!c->g1_ext_env && n_reads > 0) {
+        const int64_t per_cu = n_reads / std::max(1, c->n_cu);
+        mx = per_cu >= 160 ? mx : per_cu >= 96 ? std::min(mx, 1024) : std::min(mx, 512);
+    }
+    w.g1_max_ext = c->g1_hv ? mx : 0;
     w.hv = c->g_hv;
     w.hv.min_chains = c->g_hv.cnt ? c->g_heavy_min : 0;
     w.pe = c->g_pe;
@@ -647,7 +658,10 @@ int af_ctx_create(int device, af_ctx **out) {
     if (const char *sw = getenv("AF_S2_SPEC_WINDOWS")) c->s2_sp_min = std::max(0, atoi(sw));
     if (const char *hv = getenv("AF_BLAT_HEAVY_CLUMPS")) c->blat_heavy_min = std::max(0, atoi(hv));  // 0: none deferred
     if (const char *go = getenv("AF_G2_FIRST_OCC")) c->g2_first_occ = std::max(0, atoi(go));
-    if (const char *hv = getenv("AF_G1_HEAVY_EXT")) c->g1_max_ext = std::max(0, atoi(hv));     // tests: 1 = every read
+    if (const char *hv = getenv("AF_G1_HEAVY_EXT")) {  // tests: 1 = every read
+        c->g1_max_ext = std::max(0, atoi(hv));
+        c->g1_ext_env = true;
+    }
     if (hipMalloc(&c->ctrl, AF_CTRL_BYTES) != hipSuccess) { delete c; return AF_E_HIP; }
     if (hipMemset(c->ctrl, 0, AF_CTRL_BYTES) != hipSuccess) { af_free(c->ctrl); delete c; return AF_E_HIP; }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1427,7 +1441,7 @@ static int genome_se_device(af_ctx *c, const af_genome *g, const uint8_t *d_read
     if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
     hipStream_t s = (hipStream_t)stream;
     const GOpt o = genome_opt(pe);
-    const GWork w = genome_work(c);
+    const GWork w = genome_work(c, n);
     HIPCHK(c, af_launch_genome_regions(g->dev, d_reads, stride, d_lens, nullptr, n, *p, o, w, c->g1_scr, c->g1_threads,
                                        c->g2_scr, c->g2_waves, c->zscratch, s));
     HIPCHK(c, af_launch_genome_se(g->dev, d_reads, stride, d_lens, nullptr, n, *p, id_base, d_ids, w, c->g2_scr,
@@ -1465,7 +1479,7 @@ int af_genome_align_pe_device(af_ctx *c, const af_genome *g, const uint8_t *d_re
         return rc;
     hipStream_t s = (hipStream_t)stream;
     const GOpt o = genome_opt(&e);
-    const GWork w = genome_work(c);
+    const GWork w = genome_work(c, 2 * n_pairs);
     S2Work sw{};
     sw.ghist = c->g_ghist; sw.pes = c->g_pes; sw.ppc = 0; sw.cstart = c->g_cstart; sw.n_chunks = c->g_nchunks;
     sw.max_chunks = c->g_max_chunks;
@@ -1508,7 +1522,7 @@ int af_genome_align_pe_se_device(af_ctx *c, const af_genome *g, const uint8_t *d
     }
     if (!c->g_ev) HIPCHK(c, hipEventCreateWithFlags(&c->g_ev, hipEventDisableTiming));
     const GOpt o = genome_opt(&e4);
-    const GWork w = genome_work(c);
+    const GWork w = genome_work(c, n);
     if (n_pairs)
         HIPCHK(c, af_launch_s2_chunks(n_pairs, stride, d_lens, e4.chunk_bases, c->g_cstart, c->g_scan, c->g_max_chunks,
                                       c->g_nchunks, s));
@@ -1618,7 +1632,7 @@ int af_genome_regions(af_ctx *c, const af_genome *g, const uint8_t *reads, int64
     const int32_t *d_lens = nullptr;
     if ((rc = genome_stage(c, reads, n, stride, lens, false, &d_lens))) return rc;
     if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
-    const GWork w = genome_work(c);
+    const GWork w = genome_work(c, n);
     HIPCHK(c, af_launch_genome_regions(g->dev, c->g_hreads, stride, d_lens, nullptr, n, *p, genome_opt(pe), w, c->g1_scr,
                                        c->g1_threads, c->g2_scr, c->g2_waves, c->zscratch, c->stream));
     std::vector<int32_t> off((size_t)n);
@@ -1652,7 +1666,7 @@ int af_genome_intervals(af_ctx *c, const af_genome *g, const uint8_t *reads, int
     const int32_t *d_lens = nullptr;
     if ((rc = genome_stage(c, reads, n, stride, lens, false, &d_lens))) return rc;
     if ((rc = ensure_genome_scratch(c)) || (rc = ensure_genome_pools(c, n))) return rc;
-    const GWork w = genome_work(c);
+    const GWork w = genome_work(c, n);
     HIPCHK(c, af_launch_genome_intervals(g->dev, c->g_hreads, stride, d_lens, n, *p, genome_opt(pe), w, c->g1_scr,
                                          c->g1_threads, c->stream));
     std::vector<int64_t> off((size_t)n);

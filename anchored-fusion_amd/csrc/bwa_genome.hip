@@ -888,7 +888,7 @@ __device__ int g_test_and_merge(const G2Scr &S, GChainHot *hot, int nhot, int ci
 // wave searches it (two ballots) and shifts it open for an insertion, instead of lane 0 walking
 // tree nodes.  A second chain at an existing pos (whose place among the equal keys depends on the
 // tree's shape) or chain G_ARR + 1 restarts the read on the kbtree.
-constexpr int G_ARR = 1024, G_CH_ARR = 180;
+constexpr int G_ARR = 1392, G_CH_ARR = 64;
 // the array mode's chain limit (tests: env AF_G_CHAIN_ARR -- 0 every read on the kbtree, a small
 // count most reads restarted there)
 __device__ int g_chain_arr = G_ARR;
@@ -899,17 +899,17 @@ struct GChainArr {
     int32_t rid[64];
 };
 static_assert(sizeof(GChainArr) <= sizeof(G2Box) * G2_BOXES, "the array mode's LDS set fits the boxes");
-static_assert(G_ARR <= 64 * 16, "g_arr_rank covers 64 strides of 16 keys");
-// the number of keys <= kpos among key[0, n) (ascending, n <= 1024): a ballot over the 64
-// strides of 16, then one over the stride
+static_assert(G_ARR <= 64 * 32, "g_arr_rank covers 64 strides of 32 keys");
+// the number of keys <= kpos among key[0, n) (ascending, n <= 2048): a ballot over the 64
+// strides of 32, then one over the stride
 __device__ __forceinline__ int g_arr_rank(const int64_t *key, int n, int64_t kpos, int lane) {
-    const int i1 = lane << 4;
+    const int i1 = lane << 5;
     const uint64_t m1 = __ballot(i1 < n && key[i1] <= kpos);
     if (!m1) return 0;
     const int b = __builtin_popcountll(m1) - 1;
-    const int i2 = (b << 4) + (lane & 15);
-    const uint64_t m2 = __ballot(lane < 16 && i2 < n && key[i2] <= kpos);
-    return (b << 4) + __builtin_popcountll(m2);
+    const int i2 = (b << 5) + (lane & 31);
+    const uint64_t m2 = __ballot(lane < 32 && i2 < n && key[i2] <= kpos);
+    return (b << 5) + __builtin_popcountll(m2);
 }
 
 // mem_chain over the read's intervals (oracle mem_chain): returns the chain count (tree order,
@@ -1154,32 +1154,48 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     for (int i = 1; i < n_chn; ++i) {
         const int bi = cb[i], ei = ce[i], wi = cw[i], li = ei - bi;
         bool large_ovlp = false, brk = false;
-        for (int k0 = 0; k0 < nc && !brk; k0 += 64) {
-            const int k = k0 + lane;
-            bool ov = false, bk = false;
-            uint32_t x = 0;
-            if (k < nc) {
-                x = kp[k];
-                const int bj = (int)(x & 511), ej = (int)(x >> 9 & 511);
-                const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
-                if (e_min > b_max) {
-                    const int lj = ej - bj, min_l = li < lj ? li : lj;
-                    if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
-                        ov = true;
-                        const int wj = (int)(x >> 18 & 511);
-                        bk = (float)wi < (float)wj * 0.5f && wj - wi >= p.min_seed_len << 1;
+        // four chunks of 64 kept chains per round: their loads issued together, then taken in
+        // kept order up to the first breaking chain
+        for (int k0 = 0; k0 < nc && !brk; k0 += 256) {
+            uint32_t x[4];
+            uint64_t om[4], bm[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + 64 * u + lane;
+                x[u] = k < nc ? kp[k] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + 64 * u + lane;
+                bool ov = false, bk = false;
+                if (k < nc) {
+                    const int bj = (int)(x[u] & 511), ej = (int)(x[u] >> 9 & 511);
+                    const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
+                    if (e_min > b_max) {
+                        const int lj = ej - bj, min_l = li < lj ? li : lj;
+                        if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
+                            ov = true;
+                            const int wj = (int)(x[u] >> 18 & 511);
+                            bk = (float)wi < (float)wj * 0.5f && wj - wi >= p.min_seed_len << 1;
+                        }
                     }
                 }
+                bm[u] = __ballot(bk);
+                om[u] = __ballot(ov);
             }
-            const uint64_t bm = __ballot(bk);
-            uint64_t om = __ballot(ov);
-            if (bm) {
-                const int f = __builtin_ctzll(bm);
-                if (f < 63) om &= (2ull << f) - 1ull;
-                brk = true;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (brk) break;
+                uint64_t m = om[u];
+                if (bm[u]) {
+                    const int f = __builtin_ctzll(bm[u]);
+                    if (f < 63) m &= (2ull << f) - 1ull;
+                    brk = true;
+                }
+                if (m) large_ovlp = true;
+                const int k = k0 + 64 * u + lane;
+                if (((m >> lane) & 1ull) && !(x[u] >> 31)) { kp[k] = x[u] | 1u << 31; kf[k] = (int16_t)i; }
             }
-            if (om) large_ovlp = true;
-            if (((om >> lane) & 1ull) && !(x >> 31)) { kp[k] = x | 1u << 31; kf[k] = (int16_t)i; }
         }
         if (!brk) {
             if (lane == 0) { kp[nc] = pack(i); kf[nc] = -1; a[i].kept = large_ovlp ? 2 : 3; }
