@@ -65,6 +65,7 @@ __device__ int32_t *g_s2prof = nullptr;  // K2 items at [item * 16], K3c items a
 constexpr int64_t S2PROF_K3 = (int64_t)1 << 24;
 #define SPROF(...) __VA_ARGS__
 __shared__ int64_t g_sub[5];  // K2 seeding sub-phase marks (pmems, pass 1, pass 2, pass 3)
+__shared__ int32_t g_ext[2];  // K2 extension rows and ksw_extend2 calls of the read
 #else
 #define SPROF(...)
 #endif
@@ -773,6 +774,7 @@ __device__ void s2_chain2aln(const DevText &X, const af_params &p, int l, int ci
                 const int prev = a_score;
                 aw0 = p.w << it;
                 er = ext_dp<CPL>(s.qbeg, L.qs, tl, L.t, p, aw0, p.pen_clip5, p.zdrop, s.len * p.a, lane);
+                SPROF(if (lane == 0) { g_ext[0] += er.rows; g_ext[1] += 1; })
                 a_score = er.max;
                 if (a_score == prev || er.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
             }
@@ -797,6 +799,7 @@ __device__ void s2_chain2aln(const DevText &X, const af_params &p, int l, int ci
                 const int prev = a_score;
                 aw1 = p.w << it;
                 er = ext_dp<CPL>(l - qe, L.q + qe, tl, L.t, p, aw1, p.pen_clip3, p.zdrop, sc0, lane);
+                SPROF(if (lane == 0) { g_ext[0] += er.rows; g_ext[1] += 1; })
                 a_score = er.max;
                 if (a_score == prev || er.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
             }
@@ -948,7 +951,8 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
         }
         if (item >= ncand) break;
         const int64_t r = cand[item];
-        SPROF(const int64_t t0 = clock64(); int64_t t1 = t0, t2 = t0, t3 = t0, t4 = t0;)
+        SPROF(const int64_t t0 = clock64(); int64_t t1 = t0, t2 = t0, t3 = t0, t4 = t0;
+              if (lane == 0) g_ext[0] = g_ext[1] = 0;)
         int l = lens ? lens[r] : stride;
         if (l > stride) l = stride;
         if (l > AF_MAX_READ) l = AF_MAX_READ;
@@ -1029,7 +1033,7 @@ __global__ __launch_bounds__(64, AF_S2_WPS) void k_s2_regions(DevText X, const u
             const int64_t t5 = clock64();
             pf[0] = (int32_t)r; pf[1] = (int32_t)(t5 - t0); pf[2] = (int32_t)(t1 - t0); pf[3] = (int32_t)(t2 - t1);
             pf[4] = (int32_t)(t3 - t2); pf[5] = (int32_t)(t4 - t3); pf[6] = pr_npm; pf[7] = pr_nsi; pf[8] = pr_nch;
-            pf[9] = pr_nreg0; pf[10] = n_reg; pf[11] = l;
+            pf[9] = pr_nreg0; pf[10] = n_reg; pf[11] = g_ext[0] << 8 | min(g_ext[1], 255);
             pf[12] = (int32_t)(g_sub[0] - t0); pf[13] = (int32_t)(g_sub[1] - g_sub[0]);
             pf[14] = (int32_t)(g_sub[2] - g_sub[1]); pf[15] = (int32_t)(g_sub[3] - g_sub[2]);
             pf[6] |= (int32_t)min(g_sub[4] - g_sub[3], (int64_t)0x7FFFFF) << 8;

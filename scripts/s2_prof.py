@@ -56,6 +56,10 @@ sub = k2[:, 6] >> 8
 k2[:, 6] &= 0xFF
 print(f"    seeding: read load {k2[:, 12].mean():.0f}, MEMs {k2[:, 13].mean():.0f}, pass 1 {k2[:, 14].mean():.0f}, "
       f"pass 2 {k2[:, 15].mean():.0f}, pass 3 {sub.mean():.0f}")
+rows, calls = k2[:, 11] >> 8, k2[:, 11] & 0xFF
+print(f"    extension: ksw_extend2 calls/read {calls.mean():.2f}, rows/read {rows.mean():.1f}, rows/call "
+      f"{rows.sum() / max(calls.sum(), 1):.1f}, cycles/row {k2[:, 4].sum() / max(rows.sum(), 1):.0f}; reads with no "
+      f"extension {(calls == 0).mean():.3f}")
 print(f"    MEMs {k2[:, 6].mean():.2f}, intervals {k2[:, 7].mean():.2f}, chains {k2[:, 8].mean():.2f}, "
       f"regions {k2[:, 9].mean():.2f} -> {k2[:, 10].mean():.2f}")
 resc = k3[:, 6] > 0
