@@ -164,10 +164,12 @@ int af_split_tails_device(af_ctx *ctx, const uint8_t *d_reads, int64_t n_reads, 
  *   hits    every 11-mer of the query and of its reverse complement looked up;
  *   clumps  hits sorted by diagonal, split where successive diagonals drift by > max_gap + 2;
  *           a clump needs >= min_match hits (-minMatch);
- *   align   each clump's first tile extended both ways by banded DP (match +1, mismatch -1,
- *           gap 3 + 1 per base, band 16, z-drop 20) and aligned globally for its blocks;
- *   stitch  colinear alignments of one strand and target up to max_intron apart joined into one
- *           multi-block hit (each joint one q / t insert), best chain first;
+ *   HSPs    within a clump, hits of one diagonal whose tiles touch form a range; a range not
+ *           inside an HSP made before is extended without gaps both ways (+1 match, -1 mismatch
+ *           or N, each end stopping XDOWN = 10 positions past its last new best, at its first best);
+ *   stitch  HSPs of one strand and target that advance on both sequences, up to max_intron apart,
+ *           joined into one multi-block hit (overlaps trimmed from the later HSP; each joint one
+ *           q / t insert: the only gaps), best chain first;
  *   filter  PSL score = matches + repMatches/2 - misMatches - qNumInsert - tNumInsert >= min_score
  *           and identity 100 - milliBad / 10 >= min_identity (pslCalcMilliBad, mRNA mode).
  * One row per hit, the PSL columns (qStarts on the reverse-complemented query for '-'). */
