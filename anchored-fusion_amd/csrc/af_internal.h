@@ -386,7 +386,7 @@ struct BlatCaps {
 #define AF_BLAT_HV_STRANDS_DONE (20 * AF_HEAD_STRIDE)  // deferred strands searched (k_blat_heavy)
 #define AF_BLAT_HV_CTRL_WORDS (21 * AF_HEAD_STRIDE)
 #ifndef AF_BLAT_HEAVY_CLUMPS
-#define AF_BLAT_HEAVY_CLUMPS 32  // default: strands with more clumps are deferred (env AF_BLAT_HEAVY_CLUMPS)
+#define AF_BLAT_HEAVY_CLUMPS 512  // default: strands with more clumps are deferred (env AF_BLAT_HEAVY_CLUMPS)
 #endif
 struct BlatHeavy {
     int32_t min_clumps = 0;   // 0: no strand is deferred
