@@ -671,6 +671,7 @@ struct G2Box {
     int32_t qb, qe, w, seedlen0;
 };
 __shared__ G2Box g_box[G2_BOXES];
+GPROF(__shared__ int64_t g_gp_flt;)  // mem_chain_flt's sort cycles of the current read (profiling build)
 
 // ---- bntseq.c on the device
 __device__ __forceinline__ int g_pos2rid(const DevGenome &G, int64_t pos_f) {
@@ -1103,6 +1104,7 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
         a[i] = c;
     }
     wave_sync();
+    GPROF(const int64_t gp_s0 = clock64();)
     if (n_chn <= (int)(sizeof(G2Box) * G2_BOXES / sizeof(uint64_t))) {
         // lane 0's introsort over (w, index) keys in LDS (the boxes, free until chain2aln) instead
         // of 32-B chains in scratch: the swaps depend only on the comparator's answers, so the
@@ -1124,6 +1126,7 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     }
     __threadfence_block();
     wave_sync();
+    GPROF(if (lane == 0) g_gp_flt = clock64() - gp_s0;)
     // the overlap scan: the kept chains in kept order, each packed in one word (query begin / end
     // and weight, 9 bits each, and bit 31 once its `first` is set) with its `first` beside it, so a
     // lane tests one kept chain per LDS read; LDS (the boxes, free again after the sort) when the
@@ -1807,7 +1810,7 @@ __global__ __launch_bounds__(64, 2) void k_g_regions(DevGenome G, const uint8_t 
               g[6] = gp_c[3] ? (int32_t)(gp_c[3] - gp_c[2]) : 0; g[7] = gp_c[4] ? (int32_t)(gp_c[4] - gp_c[3]) : 0;
               g[8] = (int32_t)gp_occ; g[10] = gp_n[0]; g[11] = gp_n[1]; g[12] = gp_n[2]; g[13] = gp_n[3];
               g[14] = (int32_t)blockIdx.x; g[15] = (int32_t)gp_t0; g[16] = (int32_t)gp_rt(); g[2] = l;
-              g[9] = deferred; } })
+              g[9] = deferred; g[43] = gp_c[2] ? (int32_t)g_gp_flt : 0; } })
         if (!deferred) g_put_regions(w, S, r, nreg, ovf, lane);
     }
 }

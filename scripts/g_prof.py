@@ -111,11 +111,11 @@ for c in range(min(ncalls, 4)):
     srt = np.argsort(-g2)
     top = g2[srt[:100]].sum() / tot
     print(f"  top-100 reads hold {top:.3f} of G2 cycles; top-1000 {g2[srt[:1000]].sum() / tot:.3f}")
-    print("  heaviest: cyc chain flt ext dedup | len niv occ nch kept nreg nreg2")
+    print("  heaviest: cyc chain flt (its sort) ext dedup | len niv occ nch kept nreg nreg2")
     for i in srt[:12]:
         r = B[i]
-        print(f"   {g2[i]:>11d} {ph[0][i]:>10d} {ph[1][i]:>9d} {ph[2][i]:>10d} {ph[3][i]:>9d} | {r[2]} {r[1]} {r[8]} "
-              f"{r[10]} {r[11]} {r[12]} {r[13]}")
+        print(f"   {g2[i]:>11d} {ph[0][i]:>10d} {ph[1][i]:>9d} ({r[43]:>8d}) {ph[2][i]:>10d} {ph[3][i]:>9d} | {r[2]} {r[1]} "
+              f"{r[8]} {r[10]} {r[11]} {r[12]} {r[13]}")
     for k, nm in ((8, "occ"), (10, "chains"), (11, "kept"), (12, "regions")):
         v = B[:, k]
         print(f"  {nm:8s} mean {v.mean():.1f} p90 {pct(v, 90):.0f} p99 {pct(v, 99):.0f} max {v.max()}")
