@@ -1131,8 +1131,15 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     // and weight, 9 bits each, and bit 31 once its `first` is set) with its `first` beside it, so a
     // lane tests one kept chain per LDS read; LDS (the boxes, free again after the sort) when the
     // lists fit, else the scratch free after mem_chain
+    // In LDS the kept chains are also grouped by their packed word (a repeat-rich read's chains
+    // come from a few intervals: hundreds of chains, a handful of distinct spans and weights), so a
+    // chain is tested against the groups (a lane each) instead of every kept chain: members of a
+    // group answer alike, the scan's first breaking chain is the first member of the earliest
+    // breaking group, and the members whose `first` is still unset form a suffix of the group's
+    // list (each member is set once).  Past NG groups the chunk scan takes over.
     static_assert(AF_MAX_READ < 512 && AF_G_MAX_CHAIN < 32768, "9-bit spans and weights, 16-bit chain indices");
-    constexpr int NL = (int)(sizeof(G2Box) * G2_BOXES / (3 * sizeof(int16_t) + sizeof(uint32_t) + sizeof(int16_t)));
+    constexpr int NG = 64;
+    constexpr int NL = (int)((sizeof(G2Box) * G2_BOXES - NG * 10) / 14) & ~1;
     const bool lds = n_chn <= NL;
     uint8_t *const lb = reinterpret_cast<uint8_t *>(g_box);
     uint32_t *kp = lds ? reinterpret_cast<uint32_t *>(lb) : reinterpret_cast<uint32_t *>(S.last_of);
@@ -1141,6 +1148,9 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     int16_t *cb = lds ? reinterpret_cast<int16_t *>(lb + 6 * NL) : reinterpret_cast<int16_t *>(S.next);
     int16_t *ce = lds ? cb + NL : cb + AF_G_MAX_CHAIN;
     int16_t *cw = lds ? ce + NL : reinterpret_cast<int16_t *>(S.kept);
+    int16_t *nx = reinterpret_cast<int16_t *>(lb + 12 * NL);  // the next member of a kept chain's group
+    uint32_t *gkey = reinterpret_cast<uint32_t *>(lb + 14 * NL);
+    int16_t *gfirst = reinterpret_cast<int16_t *>(gkey + NG), *gpend = gfirst + NG, *gtail = gpend + NG;
     for (int i = lane; i < n_chn; i += 64) {
         const GChain c = a[i];
         const GSeed t = S.seed[c.seed0 + c.n - 1];
@@ -1151,12 +1161,79 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     __threadfence_block();
     wave_sync();
     auto pack = [&](int i) -> uint32_t { return (uint32_t)cb[i] | (uint32_t)ce[i] << 9 | (uint32_t)cw[i] << 18; };
-    if (lane == 0) { a[0].kept = 3; kp[0] = pack(0); kf[0] = -1; }
+    bool grp = lds && g_chain_arr > 0;  // (AF_G_CHAIN_ARR=0, a test mode: the kbtree and the chunk scan)
+    int ng = 1;
+    if (lane == 0) {
+        a[0].kept = 3; kp[0] = pack(0); kf[0] = -1;
+        if (grp) { nx[0] = -1; gkey[0] = kp[0]; gfirst[0] = 0; gpend[0] = 0; gtail[0] = 0; }
+    }
     wave_sync();
     int nc = 1;
+    // a chain whose span and weight equal the previous chain's, when that one broke off, breaks at
+    // the same kept chain and finds every `first` up to it set: nothing to do
+    uint32_t prev_key = 0xFFFFFFFFu;
+    bool prev_brk = false;
     for (int i = 1; i < n_chn; ++i) {
         const int bi = cb[i], ei = ce[i], wi = cw[i], li = ei - bi;
+        const uint32_t key_i = pack(i);
+        if (prev_brk && key_i == prev_key) continue;
+        prev_key = key_i;
         bool large_ovlp = false, brk = false;
+        if (grp) {
+            const uint32_t x = lane < ng ? gkey[lane] : 0u;
+            const int gf = lane < ng ? gfirst[lane] : INT_MAX;
+            bool ov = false, bk = false;
+            if (lane < ng) {
+                const int bj = (int)(x & 511), ej = (int)(x >> 9 & 511);
+                const int b_max = bj > bi ? bj : bi, e_min = ej < ei ? ej : ei;
+                if (e_min > b_max) {
+                    const int lj = ej - bj, min_l = li < lj ? li : lj;
+                    if ((float)(e_min - b_max) >= (float)min_l * 0.5f && min_l < o.max_chain_gap) {
+                        ov = true;
+                        const int wj = (int)(x >> 18 & 511);
+                        bk = (float)wi < (float)wj * 0.5f && wj - wi >= p.min_seed_len << 1;
+                    }
+                }
+            }
+            int bp = bk ? gf : INT_MAX;  // the first breaking kept chain
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) bp = min(bp, __shfl_xor(bp, d));
+            brk = bp != INT_MAX;
+            large_ovlp = __ballot(ov && gf <= bp) != 0;
+            if (ov) {  // the group's members up to bp whose `first` is unset
+                int pos = gpend[lane];
+                while (pos >= 0 && pos <= bp) {
+                    kp[pos] |= 1u << 31;
+                    kf[pos] = (int16_t)i;
+                    pos = nx[pos];
+                }
+                gpend[lane] = (int16_t)pos;
+            }
+            prev_brk = brk;
+            if (!brk) {
+                const uint32_t key = key_i;
+                const uint64_t gm = __ballot(lane < ng && x == key);
+                if (lane == 0) {
+                    kp[nc] = key; kf[nc] = -1; nx[nc] = -1; a[i].kept = large_ovlp ? 2 : 3;
+                    if (gm) {
+                        const int g = __builtin_ctzll(gm);
+                        nx[gtail[g]] = (int16_t)nc;
+                        gtail[g] = (int16_t)nc;
+                        if (gpend[g] < 0) gpend[g] = (int16_t)nc;
+                    } else if (ng < NG) {
+                        gkey[ng] = key; gfirst[ng] = (int16_t)nc; gpend[ng] = (int16_t)nc; gtail[ng] = (int16_t)nc;
+                    }
+                }
+                if (!gm) {
+                    if (ng < NG) ++ng;
+                    else grp = false;  // past NG groups: the chunk scan (kp / kf hold every kept chain)
+                }
+                ++nc;
+            }
+            __threadfence_block();
+            wave_sync();
+            continue;
+        }
         // four chunks of 64 kept chains per round: their loads issued together, then taken in
         // kept order up to the first breaking chain
         for (int k0 = 0; k0 < nc && !brk; k0 += 256) {
@@ -1200,8 +1277,9 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
                 if (((m >> lane) & 1ull) && !(x[u] >> 31)) { kp[k] = x[u] | 1u << 31; kf[k] = (int16_t)i; }
             }
         }
+        prev_brk = brk;
         if (!brk) {
-            if (lane == 0) { kp[nc] = pack(i); kf[nc] = -1; a[i].kept = large_ovlp ? 2 : 3; }
+            if (lane == 0) { kp[nc] = key_i; kf[nc] = -1; a[i].kept = large_ovlp ? 2 : 3; }
             ++nc;
         }
         __threadfence_block();
