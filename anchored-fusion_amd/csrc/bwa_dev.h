@@ -95,6 +95,128 @@ __device__ void ks_introsort(T *a, int n, LT lt) {
     }
 }
 
+// klib's introsort with its exact output (ties included), partitions on the wave.  A Hoare
+// partition's swaps are fixed by two lists of the ORIGINAL segment: the left stoppers L (indices in
+// (s, t] holding no key below the pivot, t -- the pivot's slot -- last) and the right stoppers R
+// (indices in [s, t) holding no key above it, descending).  Swap k exchanges L[k] and R[k] for
+// every k before the first K with R[k] <= L[k] (R[k] = -1 past R's end); the i scan of round K then
+// stops at L[K] or, when the swapped-in key at R[K - 1] comes first, there: the pivot lands at
+// min(L[K], R[K - 1]).  Segments are independent (their order of processing does not matter),
+// each child of more than 16 keys is partitioned with its parent's depth (at depth 0 klib's comb
+// sort on lane 0).  klib's closing insertion sort is stable (strict comparisons), so its output is
+// the stable sort of the partitioned array: a bitonic network over (key, position) pairs.
+// scr: 5 n ints of scratch (L, R, the segment queue; then the positions).  Wave-uniform call.
+template <class T, class LT>
+__device__ void wave_introsort(T *a, int n, LT lt, int32_t *scr, int lane) {
+    if (n < 3) {
+        if (n == 2 && lane == 0 && lt(a[1], a[0])) { T sw = a[0]; a[0] = a[1]; a[1] = sw; }
+        __threadfence_block();
+        wave_sync();
+        return;
+    }
+    int d = 2;
+    while ((1 << d) < n) ++d;
+    d <<= 1;
+    int32_t *const Lp = scr, *const Rp = scr + n, *const Q = scr + 2 * n;
+    int qh = 0, qt = 1;
+    if (lane == 0) { Q[0] = 0; Q[1] = n - 1; Q[2] = d; }
+    __threadfence_block();
+    wave_sync();
+    while (qh < qt) {
+        const int s = Q[3 * qh], t = Q[3 * qh + 1];
+        int dd = Q[3 * qh + 2];
+        ++qh;
+        if (s >= t) continue;
+        if (--dd == 0) {
+            if (lane == 0) ks_comb(a + s, t - s + 1, lt);
+            __threadfence_block();
+            wave_sync();
+            continue;
+        }
+        if (lane == 0) {
+            const int i = s, j = t;
+            int k = i + ((j - i) >> 1) + 1;
+            if (lt(a[k], a[i])) {
+                if (lt(a[k], a[j])) k = j;
+            } else k = lt(a[j], a[i]) ? i : j;
+            if (k != t) { T sw = a[k]; a[k] = a[t]; a[t] = sw; }
+        }
+        __threadfence_block();
+        wave_sync();
+        const T rp = a[t];
+        int nl = 0, nr = 0;
+        for (int x0 = s + 1; x0 <= t; x0 += 64) {
+            const int x = x0 + lane;
+            const bool st = x <= t && !lt(a[x], rp);
+            const uint64_t m = __ballot(st);
+            if (st) Lp[nl + lanes_below(m, lane)] = x;
+            nl += __builtin_popcountll(m);
+        }
+        for (int x0 = t - 1; x0 >= s; x0 -= 64) {
+            const int x = x0 - lane;
+            const bool st = x >= s && !lt(rp, a[x]);
+            const uint64_t m = __ballot(st);
+            if (st) Rp[nr + lanes_below(m, lane)] = x;
+            nr += __builtin_popcountll(m);
+        }
+        __threadfence_block();
+        wave_sync();
+        int K = -1;
+        for (int k0 = 0; K < 0 && k0 < nl; k0 += 64) {
+            const int k = k0 + lane;
+            bool c = false;
+            if (k < nl) c = (k < nr ? Rp[k] : -1) <= Lp[k];
+            const uint64_t m = __ballot(c);
+            if (m) K = k0 + (int)__builtin_ctzll(m);
+        }
+        const int fi = K == 0 ? Lp[0] : min(Lp[K], Rp[K - 1]);
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            const int k = k0 + lane;
+            if (k < K) {
+                const int li = Lp[k], ri = Rp[k];
+                const T x = a[li];
+                a[li] = a[ri];
+                a[ri] = x;
+            }
+        }
+        __threadfence_block();
+        wave_sync();
+        if (lane == 0) {
+            T sw = a[fi]; a[fi] = a[t]; a[t] = sw;
+            int q = qt;
+            if (fi - s > 16) { Q[3 * q] = s; Q[3 * q + 1] = fi - 1; Q[3 * q + 2] = dd; ++q; }
+            if (t - fi > 16) { Q[3 * q] = fi + 1; Q[3 * q + 1] = t; Q[3 * q + 2] = dd; ++q; }
+        }
+        if (fi - s > 16) ++qt;
+        if (t - fi > 16) ++qt;
+        __threadfence_block();
+        wave_sync();
+    }
+    // the closing insertion sort: (key, position) ascending, the network whose comparators all put
+    // the lesser pair low (missing pairs past n act as +inf)
+    int32_t *const P = scr;
+    for (int i = lane; i < n; i += 64) P[i] = i;
+    __threadfence_block();
+    wave_sync();
+    int N = 1;
+    while (N < n) N <<= 1;
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i0 = 0; i0 < N; i0 += 64) {
+                const int i = i0 + lane;
+                const int l = j == (k >> 1) ? (i ^ (k - 1)) : (i ^ j);
+                if (l > i && l < n) {
+                    const T x = a[i], y = a[l];
+                    const int px = P[i], py = P[l];
+                    if (lt(y, x) || (!lt(x, y) && py < px)) { a[i] = y; a[l] = x; P[i] = py; P[l] = px; }
+                }
+            }
+            __threadfence_block();
+            wave_sync();
+        }
+    }
+}
+
 // a[0, n) sorted on the wave by rank when the comparator orders every pair strictly (no two items
 // equivalent): every correct sort, klib's introsort included, then gives this one order.  Each
 // lane ranks its items against all n (LDS broadcast reads); tmp: n items of scratch.  Returns

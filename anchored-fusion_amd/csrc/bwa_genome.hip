@@ -1105,6 +1105,8 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
     }
     wave_sync();
     GPROF(const int64_t gp_s0 = clock64();)
+    static_assert(3 * AF_G_MAX_CHAIN >= 5 * (int)(sizeof(G2Box) * G2_BOXES / sizeof(uint64_t)),
+                  "wave_introsort's scratch: S.last_of, S.order and S.kept (consecutive in g2_scr)");
     if (n_chn <= (int)(sizeof(G2Box) * G2_BOXES / sizeof(uint64_t))) {
         // lane 0's introsort over (w, index) keys in LDS (the boxes, free until chain2aln) instead
         // of 32-B chains in scratch: the swaps depend only on the comparator's answers, so the
@@ -1114,7 +1116,10 @@ __device__ int g_chain_flt(const G2Scr &S, int n_chn, const af_params &p, const 
         for (int i = lane; i < n_chn; i += 64) key[i] = (uint64_t)(uint32_t)a[i].w << 32 | (uint32_t)i;
         __threadfence_block();
         wave_sync();
-        if (lane == 0) ks_introsort(key, n_chn, GKeyFlt());
+        // (weights tie, so the order is klib's introsort's: lane 0 for short lists, its exact wave
+        // form past 64 keys, with the scratch free after mem_chain)
+        if (n_chn >= 64) wave_introsort(key, n_chn, GKeyFlt(), S.last_of, lane);
+        else if (lane == 0) ks_introsort(key, n_chn, GKeyFlt());
         __threadfence_block();
         wave_sync();
         for (int i = lane; i < n_chn; i += 64) S.ch[i] = a[(uint32_t)key[i]];
@@ -2856,6 +2861,39 @@ __global__ void k_g_zero(GWork w, int64_t n_reads, int32_t *heads) {
 
 size_t af_g1_slot_bytes() { return (size_t)G1_SLOT * sizeof(uint4); }
 
+
+// ---- test hook: wave_introsort (mem_chain_flt's sort, weights << 32 | index keys compared by
+// weight only, descending) against klib's introsort on lane 0, on the same keys.  One wave per
+// list; scratch 5 n ints.  tests/test_gpu_genome.py::test_wave_introsort_equals_klib.
+__global__ __launch_bounds__(64) void k_debug_isort(uint64_t *__restrict__ a, uint64_t *__restrict__ b, int n,
+                                                    int32_t *__restrict__ scr) {
+    const int lane = threadIdx.x;
+    if (blockIdx.x == 0) {
+        if (lane == 0) ks_introsort(a, n, GKeyFlt());
+    } else {
+        wave_introsort(b, n, GKeyFlt(), scr, lane);
+    }
+}
+extern "C" int af_debug_wave_introsort(const uint64_t *keys, int32_t n, uint64_t *out_klib, uint64_t *out_wave) {
+    if (n < 0 || n > (1 << 16) || (n > 0 && (!keys || !out_klib || !out_wave))) return -1;
+    if (n == 0) return 0;
+    uint64_t *da = nullptr, *db = nullptr;
+    int32_t *ds = nullptr;
+    int rc = -1;
+    const size_t nb = sizeof(uint64_t) * (size_t)n;
+    if (hipMalloc(&da, nb) == hipSuccess && hipMalloc(&db, nb) == hipSuccess &&
+        hipMalloc(&ds, sizeof(int32_t) * 5 * (size_t)n) == hipSuccess &&
+        hipMemcpy(da, keys, nb, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(db, keys, nb, hipMemcpyHostToDevice) == hipSuccess) {
+        hipLaunchKernelGGL(k_debug_isort, dim3(2), dim3(64), 0, 0, da, db, n, ds);
+        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(out_klib, da, nb, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(out_wave, db, nb, hipMemcpyDeviceToHost) == hipSuccess)
+            rc = 0;
+    }
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(ds);
+    return rc;
+}
 
 #ifdef AF_G_PROF
 static int32_t *h_gprof = nullptr;

@@ -90,8 +90,9 @@ def test_se_regions_equal_oracle(world):
 def test_chain_modes_equal_oracle(world, monkeypatch, arr):
     """mem_chain's two modes (bwa_genome.hip g_mem_chain): the sorted chain array in LDS (default)
     and the kbtree, which a read restarts on at a second chain with an existing pos or past the
-    array's limit -- forced here for every read (AF_G_CHAIN_ARR=0) or past 3 chains (most
-    multi-chain reads restart).  Regions and records equal the oracle's either way."""
+    array's limit -- forced here for every read (AF_G_CHAIN_ARR=0, which also runs mem_chain_flt's
+    chunk scan instead of its grouped scan) or past 3 chains (most multi-chain reads restart).
+    Regions and records equal the oracle's either way."""
     monkeypatch.setenv("AF_G_CHAIN_ARR", arr)
     contigs, og, gg = world
     reads, lens = sample_reads(contigs, 400, seed=31, chimeric=0.4)
@@ -110,6 +111,27 @@ def test_chain_modes_equal_oracle(world, monkeypatch, arr):
     for r in range(len(sn)):
         msg = _rec_equal(so[r], sg[r], min(sn[r], 8))
         assert msg is None, (r, msg)
+
+
+def test_wave_introsort_equals_klib():
+    """bwa_dev.h wave_introsort (mem_chain_flt's sort of (weight << 32 | index) keys by weight,
+    descending: ties everywhere) returns klib's introsort's exact order, through the test hook
+    af_debug_wave_introsort; lists of 3..2,048 keys with 1..1,000 distinct weights."""
+    import ctypes
+    from anchored_fusion_amd import _lib
+    L = _lib.lib()
+    L.af_debug_wave_introsort.restype = ctypes.c_int
+    L.af_debug_wave_introsort.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(41)
+    for n in (3, 17, 64, 65, 100, 257, 600, 1024, 1106, 2048):
+        for nw in (1, 2, 5, 40, 1000):
+            w = rng.integers(0, nw, n).astype(np.uint64)
+            keys = (w << np.uint64(32)) | np.arange(n, dtype=np.uint64)
+            a = np.zeros(n, np.uint64)
+            b = np.zeros(n, np.uint64)
+            assert L.af_debug_wave_introsort(keys.ctypes.data, n, a.ctypes.data, b.ctypes.data) == 0
+            assert np.array_equal(a, b), (n, nw, np.nonzero(a != b)[0][:5])
+            assert np.all(np.diff((a >> np.uint64(32)).astype(np.int64)) <= 0)
 
 
 def test_se_records_equal_oracle(world):
