@@ -2338,10 +2338,16 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
     const int l_ms = E.len[mi];
     int skip[4];
     for (int r = 0; r < 4; ++r) skip[r] = E.pes[r].failed ? 1 : 0;
-    for (int i = 0; i < E.na[mi]; ++i) {
-        int64_t dist;
-        const int r = g_infer_dir(l_pac, a.rb, ma[i].rb, &dist);
-        if (dist >= E.pes[r].low && dist <= E.pes[r].high) skip[r] = 1;
+    {  // a direction is skipped when some region already pairs with a in it: lanes over the regions
+        int bits = 0;
+        const int na0 = E.na[mi];
+        for (int i = lane; i < na0; i += 64) {
+            int64_t dist;
+            const int r = g_infer_dir(l_pac, a.rb, ma[i].rb, &dist);
+            if (dist >= E.pes[r].low && dist <= E.pes[r].high) bits |= 1 << r;
+        }
+        for (int r = 0; r < 4; ++r)
+            if (__ballot((bits >> r) & 1)) skip[r] = 1;
     }
     if (skip[0] + skip[1] + skip[2] + skip[3] == 4) return true;
     int n = 0, rid = -1;
@@ -2363,6 +2369,26 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
                 g_mate_ksw(G, p, E.q[mi], l_ms, r, rb, re, sc, te, qe, tb, qb, lane);
             }
             if (sc >= p.min_seed_len && qb >= 0) {
+                // the rescued region into the list, before the first region of a lower score (found
+                // by ballots; the tail moves up one slot a lane per region, top chunk first)
+                const int na = E.na[mi];
+                if (na >= AF_G_MAX_REG) return false;
+                int at = na;
+                for (int i0 = 0; i0 < na; i0 += 64) {
+                    const int i = i0 + lane;
+                    const uint64_t m = __ballot(i < na && ma[i].score < sc);
+                    if (m) { at = i0 + (int)__builtin_ctzll(m); break; }
+                }
+                for (int top = na - 1; top >= at; top -= 64) {
+                    const int e = top - lane;
+                    GReg x;
+                    if (e >= at) x = ma[e];
+                    __threadfence_block();
+                    wave_sync();
+                    if (e >= at) ma[e + 1] = x;
+                    __threadfence_block();
+                    wave_sync();
+                }
                 if (lane == 0) {
                     GReg b{};
                     b.rid = a.rid;
@@ -2373,20 +2399,11 @@ __device__ bool g_matesw(const DevGenome &G, const af_params &p, const GOpt &o, 
                     b.score = sc;
                     b.secondary = -1;
                     b.seedcov = (int)((b.re - b.rb < b.qe - b.qb ? b.re - b.rb : b.qe - b.qb) >> 1);
-                    const int na = E.na[mi];
-                    bool ok = na < AF_G_MAX_REG;
-                    if (ok) {
-                        int i;
-                        for (i = 0; i < na; ++i)
-                            if (ma[i].score < b.score) break;
-                        for (int u = na; u > i; --u) ma[u] = ma[u - 1];
-                        ma[i] = b;
-                        E.na[mi] = na + 1;
-                    }
-                    E.misc[0] = ok;
+                    ma[at] = b;
+                    E.na[mi] = na + 1;
                 }
+                __threadfence_block();
                 wave_sync();
-                if (!E.misc[0]) return false;
                 dirty = true;
             }
             ++n;
