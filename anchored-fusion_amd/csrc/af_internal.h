@@ -16,6 +16,9 @@
 #ifndef AF_G2_FIRST_OCC
 #define AF_G2_FIRST_OCC 128     // G2 takes the reads with at least this many seeds first (env AF_G2_FIRST_OCC; 0: read order)
 #endif
+#ifndef AF_G1W_WPS
+#define AF_G1W_WPS 6            // G1's wave path (k_g_seeds_wave): waves per SIMD, one read per wave (80 VGPRs)
+#endif
 #ifndef AF_G1_HEAVY_EXT
 #define AF_G1_HEAVY_EXT 2048    // G1: a read past this many FM extensions moves to the wave-per-read kernel (env AF_G1_HEAVY_EXT)
 #endif

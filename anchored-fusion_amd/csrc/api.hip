@@ -524,8 +524,10 @@ int ensure_genome_pools(af_ctx *c, int64_t n_reads) {
 // n_reads: the call's reads.  G1's hand-off threshold follows the load: a lane-path read's time is
 // its chain of extensions, each a trip of the whole wave, while the wave path's reads share the
 // CUs -- with few reads per CU (a rank's share at N = 8: ~70 S5 reads per CU) the CUs are idle
-// and long reads finish sooner on waves (512: 39.7 vs 42.1 ms per rank step), with hundreds per
-// CU (one GPU's 50 M pairs: ~580) the waves' work would queue (1,024: 238 vs 203 ms)
+// and every read finishes sooner on a wave of its own (threshold 1, each read handed off after its
+// first extension: the rank-share step 37.1 -> 35.3 ms with the wave path at 6 waves per SIMD),
+// with hundreds per CU (one GPU's 50 M pairs: ~580) the waves' work would queue (1,024: 238 vs
+// 203 ms)
 GWork genome_work(af_ctx *c, int64_t n_reads) {
     GWork w;
     w.iv = c->g_iv; w.iv_cap = c->g_iv_cap; w.iv_fill = c->g_iv_fill; w.iv_off = c->g_iv_off; w.iv_n = c->g_iv_n;
@@ -537,7 +539,7 @@ GWork genome_work(af_ctx *c, int64_t n_reads) {
     int32_t mx = c->g1_max_ext;
     if (!c->g1_ext_env && n_reads > 0) {
         const int64_t per_cu = n_reads / std::max(1, c->n_cu);
-        mx = per_cu >= 160 ? mx : per_cu >= 96 ? std::min(mx, 1024) : std::min(mx, 512);
+        mx = per_cu >= 160 ? mx : per_cu >= 96 ? std::min(mx, 1024) : 1;
     }
     w.g1_max_ext = c->g1_hv ? mx : 0;
     w.hv = c->g_hv;

@@ -529,7 +529,7 @@ __device__ __forceinline__ int g1w_smem(const DevGenome &G, G1W &R, int x0, int6
     return ret;
 }
 
-__global__ __launch_bounds__(64) void k_g_seeds_wave(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
+__global__ __launch_bounds__(64, AF_G1W_WPS) void k_g_seeds_wave(DevGenome G, const uint8_t *__restrict__ reads, int32_t stride,
                                                      const int32_t *__restrict__ lens, int64_t cap, af_params p,
                                                      GOpt o, uint4 *__restrict__ scratch, GWork w) {
     __shared__ uint8_t qs[AF_MAX_READ + 16];
@@ -2968,7 +2968,8 @@ hipError_t af_launch_genome_regions(const DevGenome &G, const uint8_t *reads, in
     // scratch holds lanes' slots (their count is known on the device only; a call of few reads can
     // hand off thousands of repeat-rich ones, each 600+ dependent lookups long)
     if (w.g1_max_ext > 0)
-        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64)), dim3(64), 0, s, G,
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64 * AF_G1W_WPS / AF_G1_WPS)),
+                           dim3(64), 0, s, G,
                            reads, stride, lens, cap, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     const size_t zstride = (size_t)(AF_MAX_READ + 1) * 1024;
     const int cpl = (stride + 1 + 63) / 64;
@@ -2999,7 +3000,8 @@ hipError_t af_launch_genome_intervals(const DevGenome &G, const uint8_t *reads, 
     hipLaunchKernelGGL(k_g_seeds, dim3((unsigned)g1_waves), dim3(64), 0, s, G, reads, stride, lens, nullptr, cap,
                        (int64_t)0, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     if (w.g1_max_ext > 0)
-        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64)), dim3(64), 0, s, G,
+        hipLaunchKernelGGL(k_g_seeds_wave, dim3((unsigned)std::max<int64_t>(1, n_g1_threads / 64 * AF_G1W_WPS / AF_G1_WPS)),
+                           dim3(64), 0, s, G,
                            reads, stride, lens, cap, p, o, reinterpret_cast<uint4 *>(g1_scratch), w);
     return hipGetLastError();
 }

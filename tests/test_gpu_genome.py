@@ -272,11 +272,12 @@ def test_heavy_path_equals_oracle(world, monkeypatch):
         gh.close()
 
 
-@pytest.mark.parametrize("max_ext", [1, 300])
+@pytest.mark.parametrize("max_ext", [0, 1, 300])
 def test_g1_wave_path_equals_oracle(world, monkeypatch, max_ext):
     """G1's heavy reads (k_g_seeds_wave: one wave per read, a position's backward-scan entries
-    extended at once) -- every read handed off after its first FM extension (max_ext 1), or the
-    reads past 300 extensions: intervals, S5 records and S4 records equal the oracle's."""
+    extended at once) -- every read handed off after its first FM extension (max_ext 1; the
+    default for calls of few reads per CU), the reads past 300 extensions, or none (0: the lane
+    path alone): intervals, S5 records and S4 records equal the oracle's."""
     from anchored_fusion_amd import _lib
     from anchored_fusion_amd.genome import GenomeIndex
     contigs, og, _ = world
