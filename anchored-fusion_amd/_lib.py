@@ -17,7 +17,7 @@ except Exception:  # pragma: no cover - torch is optional for the host-buffer AP
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# AF_GPU_LIB selects an in-tree build variant (e.g. libafgpu_prof.so for scripts/k2_prof.py)
+# AF_GPU_LIB selects an in-tree build variant (e.g. libafgpu_prof.so for scripts/s2_prof.py)
 LIB_PATH = os.path.join(HERE, os.environ.get("AF_GPU_LIB", "libafgpu.so"))
 CSRC = os.path.join(HERE, "csrc")
 
